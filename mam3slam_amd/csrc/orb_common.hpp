@@ -1,0 +1,73 @@
+// orb_common.hpp — geometry shared by the host orchestration and the gfx950 kernels of the ORB path.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/mam_orb.h"
+
+namespace mam {
+
+constexpr int EDGE_THRESHOLD = 19;
+constexpr int PATCH_SIZE = 31;
+constexpr int HALF_PATCH_SIZE = 15;
+constexpr int BLUR_TILE_W = 64;
+constexpr int BLUR_TILE_H = 16;
+
+// One pyramid level of the current frame size (all frames in a batch share it).
+struct LevelGeom {
+    int w, h;               // level size: cvRound(W * invScale[l]) (ORBextractor.cc:1175)
+    int pitch;              // row pitch of this level in the pyramid and blur buffers (bytes)
+    int pad0;
+    long long frame_bytes;  // h * pitch
+    long long pyr_off;      // byte offset of frame 0 of this level in the pyramid buffer (l >= 1)
+    long long blur_off;     // byte offset of frame 0 of this level in the blurred buffer
+    // FAST cell grid (ORBextractor.cc:785-803)
+    int minBX, minBY, maxBX, maxBY;
+    int nCols, nRows, wCell, hCell;
+    int cell_base;          // first entry of this level in the per-frame cell table
+    int ncells;             // active cells of this level
+    int cellcap;            // candidate slots per cell (bound on NMS survivors in a band)
+    int cand_base;          // u32 offset of this level's candidate slots within a frame
+    int cand_cap;           // ncells * cellcap
+    int nfeat;              // mnFeaturesPerLevel[l]
+    int nini;               // initial DistributeOctTree nodes round(W/H) (ORBextractor.cc:559)
+    int kp_base;            // first keypoint slot of this level within a frame
+    int kp_cap;             // keypoint slots for this level
+    float scale;            // mvScaleFactor[l]
+    float hX;               // (float)(maxX-minX)/nIni
+    int psize;              // (int)(PATCH_SIZE * scale) (ORBextractor.cc:877)
+    // bilinear resize tables from level l-1 (l >= 1), built exactly as OpenCV's hal::resize does
+    const int* xofs;
+    const short* ialpha;    // 2 per dx
+    const int* yofs;
+    const short* ibeta;     // 2 per dy
+    int xmax;               // first dx using the right-edge replicate formula
+    int xvec;               // first column using the scalar (>>22) vertical formula
+    int tile_base;          // first blur tile of this level within a frame
+    int tiles_x, tiles_y;
+    int pad1;
+};
+
+struct Geom {
+    int nlevels;
+    int cells_per_frame;    // active FAST cells over all levels
+    int cand_per_frame;     // u32 candidate slots per frame
+    int kp_slots;           // keypoint slots per frame (sum of kp_cap)
+    int tiles_per_frame;    // blur tiles per frame
+    int node_cap;           // DistributeOctTree node capacity (LDS)
+    int max_level_cells;
+    int roi_max_rows, roi_max_cols;
+    int umax[16];
+    LevelGeom L[MAM_MAX_LEVELS];
+};
+
+// FAST cell descriptor (one workgroup each): ROI rows [y0,y1) cols [x0,x1) of level `level`.
+struct CellDesc {
+    int level;
+    int ci, cj;             // cell row / column index
+    int x0, y0, x1, y1;
+    int slot;               // index of this cell within its level (candidate slot block)
+};
+
+}  // namespace mam

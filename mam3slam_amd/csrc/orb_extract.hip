@@ -1,0 +1,608 @@
+// orb_extract.hip — host orchestration + C-ABI of the ORB extractor (include/mam_orb.h).
+//
+// Mirrors MAM3SLAM::ORBextractor (reference include/ORBextractor.h:43-100, src/ORBextractor.cc:409-469,
+// 1086-1195): the constructor tables are computed on the host exactly as the reference does; the per-frame
+// work runs as five kernel stages on the context's HIP stream (orb_kernels.hip). The same pipeline serves
+// a single host frame (mam_orb_extract, synchronous, reference semantics) and device-resident batches of
+// frames (mam_orb_extract_batch_device, asynchronous; used by multi-agent harnesses and bench.py).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "orb_common.hpp"
+#include "orb_kernels.hip"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+#define MAM_HIP(call)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (call);                                                                  \
+        if (e_ != hipSuccess) {                                                                  \
+            g_last_error = std::string(#call) + ": " + hipGetErrorString(e_);                    \
+            return MAM_ERR_DEVICE;                                                               \
+        }                                                                                        \
+    } while (0)
+
+inline int cvRoundF(float v) { return (int)lrintf(v); }
+inline int cvRoundD(double v) { return (int)lrint(v); }
+inline int cvFloorF(float v) { int i = (int)v; return i - (i > v); }
+inline int cvCeilF(float v) { int i = (int)v; return i + (i < v); }
+inline short satShortF(float v) {
+    int iv = cvRoundF(v);
+    return (short)(iv < -32768 ? -32768 : iv > 32767 ? 32767 : iv);
+}
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int alloc(size_t count) {
+        if (count <= n && p) return MAM_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (count == 0) return MAM_OK;
+        MAM_HIP(hipMalloc(&p, count * sizeof(T)));
+        n = count;
+        return MAM_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct StageEvent {
+    int stage;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct mam_orb_ctx {
+    mam_orb_params prm{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // constructor tables (ORBextractor.cc:409-469)
+    std::vector<float> scale, invScale, sigma2, invSigma2;
+    std::vector<int> nPerLevel, umax;
+    // geometry for the current frame size
+    int W = 0, H = 0, Fcap = 0;
+    mam::Geom geom{};
+    std::vector<mam::CellDesc> cells;
+    DevBuf<mam::Geom> d_geom;
+    DevBuf<mam::CellDesc> d_cells;
+    DevBuf<int> d_tabs_i;
+    DevBuf<short> d_tabs_s;
+    // per-batch device scratch
+    DevBuf<uint8_t> d_pyr, d_blur, d_input;
+    DevBuf<uint32_t> d_cand, d_keys, d_okey, d_orank;
+    DevBuf<uint16_t> d_knode;
+    DevBuf<int> d_cellcnt, d_lvlcnt;
+    DevBuf<mam_keypoint> d_kps;
+    DevBuf<uint8_t> d_desc;
+    DevBuf<int32_t> d_counts;
+    size_t fast_lds = 0, dist_lds = 0;
+    // last-call bookkeeping for debug taps
+    const uint8_t* last_in0 = nullptr;
+    size_t last_stride = 0, last_fstride = 0;
+    int last_nframes = 0;
+    // profiling
+    bool profiling = false;
+    std::vector<StageEvent> pending;
+    std::vector<hipEvent_t> event_pool;
+    double stage_ms[MAM_STAGE_COUNT] = {0};
+    int64_t stage_n[MAM_STAGE_COUNT] = {0};
+};
+
+namespace {
+
+int build_tables(mam_orb_ctx* c) {
+    const mam_orb_params& p = c->prm;
+    const int L = p.nlevels;
+    const double scaleFactor = (double)p.scale_factor;   // member is double (ORBextractor.h:72)
+    c->scale.assign(L, 0.f); c->sigma2.assign(L, 0.f); c->invScale.assign(L, 0.f); c->invSigma2.assign(L, 0.f);
+    c->scale[0] = 1.0f; c->sigma2[0] = 1.0f;
+    for (int i = 1; i < L; i++) {
+        c->scale[i] = (float)((double)c->scale[i - 1] * scaleFactor);
+        c->sigma2[i] = c->scale[i] * c->scale[i];
+    }
+    for (int i = 0; i < L; i++) { c->invScale[i] = 1.0f / c->scale[i]; c->invSigma2[i] = 1.0f / c->sigma2[i]; }
+    c->nPerLevel.assign(L, 0);
+    float factor = (float)(1.0f / scaleFactor);
+    float nDesired = p.nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; l++) {
+        c->nPerLevel[l] = cvRoundF(nDesired);
+        sum += c->nPerLevel[l];
+        nDesired *= factor;
+    }
+    c->nPerLevel[L - 1] = std::max(p.nfeatures - sum, 0);
+    c->umax.assign(16, 0);
+    int v, v0, vmax = cvFloorF(15 * sqrtf(2.f) / 2 + 1);
+    int vmin = cvCeilF(15 * sqrtf(2.f) / 2);
+    const double hp2 = 15 * 15;
+    for (v = 0; v <= vmax; ++v) c->umax[v] = cvRoundD(sqrt(hp2 - v * v));
+    for (v = 15, v0 = 0; v >= vmin; --v) {
+        while (c->umax[v0] == c->umax[v0 + 1]) ++v0;
+        c->umax[v] = v0;
+        ++v0;
+    }
+    return MAM_OK;
+}
+
+// OpenCV hal::resize INTER_LINEAR coefficient tables (see orb_kernels.hip k_pyr_down).
+void resize_tables(int sw, int sh, int dw, int dh, std::vector<int>& xofs, std::vector<short>& ialpha,
+                   std::vector<int>& yofs, std::vector<short>& ibeta, int* xmax_out, int* xvec_out) {
+    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    xofs.resize(dw); ialpha.resize(2 * dw); yofs.resize(dh); ibeta.resize(2 * dh);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cvFloorF(fx);
+        fx -= sx;
+        if (sx < 0) fx = 0, sx = 0;
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) fx = 0, sx = sw - 1;
+        }
+        xofs[dx] = sx;
+        ialpha[2 * dx] = satShortF((1.f - fx) * 2048);
+        ialpha[2 * dx + 1] = satShortF(fx * 2048);
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cvFloorF(fy);
+        fy -= sy;
+        yofs[dy] = sy;
+        ibeta[2 * dy] = satShortF((1.f - fy) * 2048);
+        ibeta[2 * dy + 1] = satShortF(fy * 2048);
+    }
+    int xvec = 0;
+    while (xvec <= dw - 16) xvec += 16;
+    while (xvec < dw - 8) xvec += 8;
+    *xmax_out = xmax;
+    *xvec_out = xvec;
+}
+
+size_t distribute_lds_bytes(int NC, int max_cells) {
+    auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    size_t s = 0;
+    for (int b = 0; b < 2; b++) s += 4 * a16(NC * 2) + a16(NC * 4);
+    s += a16((size_t)NC * 16) + 3 * a16(NC * 4) + a16(NC * 8) + a16((max_cells + 1) * 4) + 64 + 64;
+    return s;
+}
+
+// Geometry for a W x H frame and capacity F (reallocates device scratch when either grows/changes).
+int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
+    if (W == c->W && H == c->H && F <= c->Fcap) return MAM_OK;
+    const bool geom_changed = (W != c->W || H != c->H);
+    const int Fcap = std::max(F, geom_changed ? F : c->Fcap);
+    const int L = c->prm.nlevels;
+    mam::Geom& g = c->geom;
+    if (geom_changed) {
+        g = mam::Geom{};
+        g.nlevels = L;
+        for (int v = 0; v < 16; v++) g.umax[v] = c->umax[v];
+        c->cells.clear();
+        int cand = 0, kp = 0, tiles = 0, node_cap = 0, maxcells = 0, rmax = 0, cmax = 0;
+        std::vector<int> ti;
+        std::vector<short> ts;
+        std::vector<size_t> tab_off(L, 0);
+        for (int l = 0; l < L; l++) {
+            mam::LevelGeom& lv = g.L[l];
+            lv.w = cvRoundF((float)W * c->invScale[l]);
+            lv.h = cvRoundF((float)H * c->invScale[l]);
+            if (lv.w < 2 * mam::EDGE_THRESHOLD + 8 || lv.h < 2 * mam::EDGE_THRESHOLD + 8 || lv.w > 4095 || lv.h > 4095) {
+                g_last_error = "frame size out of range for the level pyramid";
+                return MAM_ERR_ARG;
+            }
+            lv.pitch = (lv.w + 63) & ~63;
+            lv.frame_bytes = (long long)lv.h * lv.pitch;
+            lv.scale = c->scale[l];
+            lv.psize = (int)(mam::PATCH_SIZE * c->scale[l]);
+            lv.nfeat = c->nPerLevel[l];
+            // FAST cell grid, ComputeKeyPointsOctTree (ORBextractor.cc:785-823)
+            lv.minBX = mam::EDGE_THRESHOLD - 3;
+            lv.minBY = lv.minBX;
+            lv.maxBX = lv.w - mam::EDGE_THRESHOLD + 3;
+            lv.maxBY = lv.h - mam::EDGE_THRESHOLD + 3;
+            const float width = (float)(lv.maxBX - lv.minBX), height = (float)(lv.maxBY - lv.minBY);
+            lv.nCols = (int)(width / 35.f);
+            lv.nRows = (int)(height / 35.f);
+            if (lv.nCols < 1 || lv.nRows < 1) { g_last_error = "level too small for a FAST cell"; return MAM_ERR_ARG; }
+            lv.wCell = (int)ceil(width / lv.nCols);
+            lv.hCell = (int)ceil(height / lv.nRows);
+            lv.cell_base = (int)c->cells.size();
+            int cap = 0, slot = 0;
+            for (int i = 0; i < lv.nRows; i++) {
+                const float iniY = (float)(lv.minBY + i * lv.hCell);
+                float maxY = iniY + lv.hCell + 6;
+                if (iniY >= lv.maxBY - 3) continue;
+                if (maxY > lv.maxBY) maxY = (float)lv.maxBY;
+                for (int j = 0; j < lv.nCols; j++) {
+                    const float iniX = (float)(lv.minBX + j * lv.wCell);
+                    float maxX = iniX + lv.wCell + 6;
+                    if (iniX >= lv.maxBX - 6) continue;
+                    if (maxX > lv.maxBX) maxX = (float)lv.maxBX;
+                    mam::CellDesc cd;
+                    cd.level = l; cd.ci = i; cd.cj = j;
+                    cd.x0 = (int)iniX; cd.y0 = (int)iniY; cd.x1 = (int)maxX; cd.y1 = (int)maxY;
+                    cd.slot = slot++;
+                    const int bh = cd.y1 - cd.y0 - 6, bw = cd.x1 - cd.x0 - 6;
+                    if (bh > 0 && bw > 0) cap = std::max(cap, ((bh + 1) / 2) * ((bw + 1) / 2));
+                    rmax = std::max(rmax, cd.y1 - cd.y0);
+                    cmax = std::max(cmax, cd.x1 - cd.x0);
+                    c->cells.push_back(cd);
+                }
+            }
+            lv.ncells = slot;
+            lv.cellcap = std::max(cap, 1);
+            lv.cand_base = cand;
+            lv.cand_cap = lv.ncells * lv.cellcap;
+            cand += lv.cand_cap;
+            maxcells = std::max(maxcells, lv.ncells);
+            // DistributeOctTree initial nodes (ORBextractor.cc:559-560)
+            lv.nini = (int)roundf((float)(lv.maxBX - lv.minBX) / (lv.maxBY - lv.minBY));
+            if (lv.nini < 1) { g_last_error = "frame aspect gives zero initial octree nodes"; return MAM_ERR_ARG; }
+            lv.hX = (float)(lv.maxBX - lv.minBX) / lv.nini;
+            lv.kp_base = kp;
+            lv.kp_cap = std::max(lv.nfeat + 3, 4 * lv.nini);
+            kp += lv.kp_cap;
+            node_cap = std::max(node_cap, std::max(lv.kp_cap, lv.nini) + 8);
+            // blur tiles
+            lv.tiles_x = (lv.w + mam::BLUR_TILE_W - 1) / mam::BLUR_TILE_W;
+            lv.tiles_y = (lv.h + mam::BLUR_TILE_H - 1) / mam::BLUR_TILE_H;
+            lv.tile_base = tiles;
+            tiles += lv.tiles_x * lv.tiles_y;
+        }
+        if (cand >= (1 << 24)) { g_last_error = "too many FAST candidate slots"; return MAM_ERR_ARG; }
+        g.cells_per_frame = (int)c->cells.size();
+        g.cand_per_frame = cand;
+        g.kp_slots = kp;
+        g.tiles_per_frame = tiles;
+        g.node_cap = (node_cap + 3) & ~3;
+        g.max_level_cells = maxcells;
+        g.roi_max_rows = rmax;
+        g.roi_max_cols = cmax;
+        // resize tables for levels >= 1
+        std::vector<int> xo, yo;
+        std::vector<short> al, be;
+        std::vector<size_t> ioff(L, 0), soff(L, 0);
+        std::vector<int> xmaxv(L, 0), xvecv(L, 0);
+        for (int l = 1; l < L; l++) {
+            int xmax, xvec;
+            resize_tables(g.L[l - 1].w, g.L[l - 1].h, g.L[l].w, g.L[l].h, xo, al, yo, be, &xmax, &xvec);
+            ioff[l] = ti.size();
+            ti.insert(ti.end(), xo.begin(), xo.end());
+            ti.insert(ti.end(), yo.begin(), yo.end());
+            soff[l] = ts.size();
+            ts.insert(ts.end(), al.begin(), al.end());
+            ts.insert(ts.end(), be.begin(), be.end());
+            xmaxv[l] = xmax;
+            xvecv[l] = xvec;
+        }
+        if (int rc = c->d_tabs_i.alloc(std::max<size_t>(ti.size(), 1))) return rc;
+        if (int rc = c->d_tabs_s.alloc(std::max<size_t>(ts.size(), 1))) return rc;
+        if (!ti.empty()) MAM_HIP(hipMemcpy(c->d_tabs_i.p, ti.data(), ti.size() * sizeof(int), hipMemcpyHostToDevice));
+        if (!ts.empty()) MAM_HIP(hipMemcpy(c->d_tabs_s.p, ts.data(), ts.size() * sizeof(short), hipMemcpyHostToDevice));
+        for (int l = 1; l < L; l++) {
+            mam::LevelGeom& lv = g.L[l];
+            lv.xofs = c->d_tabs_i.p + ioff[l];
+            lv.yofs = c->d_tabs_i.p + ioff[l] + lv.w;
+            lv.ialpha = c->d_tabs_s.p + soff[l];
+            lv.ibeta = c->d_tabs_s.p + soff[l] + 2 * lv.w;
+            lv.xmax = xmaxv[l];
+            lv.xvec = xvecv[l];
+        }
+        if (int rc = c->d_cells.alloc(c->cells.size())) return rc;
+        MAM_HIP(hipMemcpy(c->d_cells.p, c->cells.data(), c->cells.size() * sizeof(mam::CellDesc), hipMemcpyHostToDevice));
+        c->fast_lds = 2 * (((size_t)rmax * cmax + 15) & ~(size_t)15) + 64;
+        c->dist_lds = distribute_lds_bytes(g.node_cap, maxcells);
+        if (c->fast_lds > 160 * 1024 || c->dist_lds > 160 * 1024) {
+            g_last_error = "LDS budget exceeded (nfeatures or cell size too large)";
+            return MAM_ERR_ARG;
+        }
+        c->W = W;
+        c->H = H;
+    }
+    // per-frame buffer offsets for capacity Fcap
+    long long pyr = 0, blur = 0;
+    for (int l = 0; l < L; l++) {
+        mam::LevelGeom& lv = g.L[l];
+        lv.pyr_off = l == 0 ? 0 : pyr;
+        if (l > 0) pyr += (long long)Fcap * lv.frame_bytes;
+        lv.blur_off = blur;
+        blur += (long long)Fcap * lv.frame_bytes;
+    }
+    const size_t cand = (size_t)Fcap * g.cand_per_frame;
+    if (int rc = c->d_pyr.alloc(std::max<long long>(pyr, 64))) return rc;
+    if (int rc = c->d_blur.alloc(blur)) return rc;
+    if (int rc = c->d_cand.alloc(cand)) return rc;
+    if (int rc = c->d_keys.alloc(cand)) return rc;
+    if (int rc = c->d_knode.alloc(cand)) return rc;
+    if (int rc = c->d_cellcnt.alloc((size_t)Fcap * g.cells_per_frame)) return rc;
+    if (int rc = c->d_lvlcnt.alloc((size_t)Fcap * L * 2)) return rc;
+    if (int rc = c->d_okey.alloc((size_t)Fcap * g.kp_slots)) return rc;
+    if (int rc = c->d_orank.alloc((size_t)Fcap * g.kp_slots)) return rc;
+    if (int rc = c->d_geom.alloc(1)) return rc;
+    MAM_HIP(hipMemcpy(c->d_geom.p, &g, sizeof(mam::Geom), hipMemcpyHostToDevice));
+    c->Fcap = Fcap;
+    return MAM_OK;
+}
+
+hipEvent_t take_event(mam_orb_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct StageScope {
+    mam_orb_ctx* c;
+    hipStream_t s;
+    int stage;
+    hipEvent_t a = nullptr;
+    StageScope(mam_orb_ctx* c_, hipStream_t s_, int st) : c(c_), s(s_), stage(st) {
+        if (c->profiling) {
+            a = take_event(c);
+            (void)hipEventRecord(a, s);
+        }
+    }
+    ~StageScope() {
+        if (c->profiling) {
+            hipEvent_t b = take_event(c);
+            (void)hipEventRecord(b, s);
+            c->pending.push_back({stage, a, b});
+        }
+    }
+};
+
+int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size_t fstride, int lap0, int lap1,
+                 mam_keypoint* d_kps, uint8_t* d_desc, int capacity, int32_t* d_counts, hipStream_t s) {
+    const mam::Geom& g = c->geom;
+    const int L = g.nlevels;
+    mam::LevelSrc src{d_in, stride, fstride, c->d_pyr.p};
+    {
+        StageScope sc(c, s, MAM_STAGE_PYRAMID);
+        for (int l = 1; l < L; l++) {
+            const mam::LevelGeom& lv = g.L[l];
+            dim3 grid((lv.w + 255) / 256, (lv.h + 3) / 4, F);
+            hipLaunchKernelGGL(mam::k_pyr_down, grid, dim3(256), 0, s, c->d_geom.p, l, src, c->d_pyr.p);
+        }
+    }
+    {
+        StageScope sc(c, s, MAM_STAGE_FAST);
+        hipLaunchKernelGGL(mam::k_fast_cells, dim3(g.cells_per_frame, F), dim3(256), c->fast_lds, s, c->d_geom.p,
+                           c->d_cells.p, src, c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast);
+    }
+    {
+        StageScope sc(c, s, MAM_STAGE_BLUR);
+        hipLaunchKernelGGL(mam::k_blur7, dim3(g.tiles_per_frame, F), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p);
+    }
+    {
+        StageScope sc(c, s, MAM_STAGE_DISTRIBUTE);
+        hipLaunchKernelGGL(mam::k_distribute, dim3(L, F), dim3(256), c->dist_lds, s, c->d_geom.p, c->d_cellcnt.p,
+                           c->d_cand.p, c->d_keys.p, c->d_knode.p, c->d_okey.p, c->d_orank.p, c->d_lvlcnt.p, lap0,
+                           lap1);
+    }
+    {
+        StageScope sc(c, s, MAM_STAGE_DESCRIBE);
+        const long long waves = (long long)F * g.kp_slots;
+        const int blocks = (int)((waves + 3) / 4);
+        hipLaunchKernelGGL(mam::k_describe, dim3(blocks), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p,
+                           c->d_okey.p, c->d_orank.p, c->d_lvlcnt.p, F, d_kps, d_desc, capacity, d_counts,
+                           c->prm.desc_fma);
+    }
+    MAM_HIP(hipGetLastError());
+    c->last_in0 = d_in;
+    c->last_stride = stride;
+    c->last_fstride = fstride;
+    c->last_nframes = F;
+    return MAM_OK;
+}
+
+bool valid_params(const mam_orb_params* p) {
+    return p && p->nlevels >= 1 && p->nlevels <= MAM_MAX_LEVELS && p->nfeatures >= 0 && p->scale_factor > 1.0f &&
+           p->ini_th_fast >= 0 && p->ini_th_fast <= 255 && p->min_th_fast >= 0 && p->min_th_fast <= 255;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mam_last_error(void) { return g_last_error.c_str(); }
+
+int mam_orb_create(const mam_orb_params* params, int device, mam_orb_ctx** out) {
+    if (!out || !valid_params(params)) return MAM_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    MAM_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) { g_last_error = "no such HIP device"; return MAM_ERR_ARG; }
+    MAM_HIP(hipSetDevice(device));
+    mam_orb_ctx* c = new mam_orb_ctx();
+    c->prm = *params;
+    c->device = device;
+    build_tables(c);
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        g_last_error = hipGetErrorString(e);
+        delete c;
+        return MAM_ERR_DEVICE;
+    }
+    *out = c;
+    return MAM_OK;
+}
+
+void mam_orb_destroy(mam_orb_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& pe : c->pending) { (void)hipEventDestroy(pe.a); (void)hipEventDestroy(pe.b); }
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    c->d_geom.release(); c->d_cells.release(); c->d_tabs_i.release(); c->d_tabs_s.release();
+    c->d_pyr.release(); c->d_blur.release(); c->d_input.release();
+    c->d_cand.release(); c->d_keys.release(); c->d_okey.release(); c->d_orank.release(); c->d_knode.release();
+    c->d_cellcnt.release(); c->d_lvlcnt.release(); c->d_kps.release(); c->d_desc.release(); c->d_counts.release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int mam_orb_levels(const mam_orb_ctx* c) { return c ? c->prm.nlevels : MAM_ERR_ARG; }
+
+int mam_orb_scales(const mam_orb_ctx* c, float* out) {
+    if (!c || !out) return MAM_ERR_ARG;
+    const int L = c->prm.nlevels;
+    for (int l = 0; l < L; l++) {
+        out[l] = c->scale[l]; out[L + l] = c->invScale[l];
+        out[2 * L + l] = c->sigma2[l]; out[3 * L + l] = c->invSigma2[l];
+    }
+    return MAM_OK;
+}
+
+int mam_orb_features_per_level(const mam_orb_ctx* c, int32_t* out) {
+    if (!c || !out) return MAM_ERR_ARG;
+    for (int l = 0; l < c->prm.nlevels; l++) out[l] = c->nPerLevel[l];
+    return MAM_OK;
+}
+
+int mam_orb_max_keypoints(const mam_orb_ctx* c) {
+    if (!c) return MAM_ERR_ARG;
+    int s = 0;
+    for (int l = 0; l < c->prm.nlevels; l++) s += c->nPerLevel[l] + 3;
+    return s;
+}
+
+int mam_orb_extract_batch_device(mam_orb_ctx* c, const uint8_t* d_imgs, int nframes, int w, int h, size_t stride,
+                                 size_t frame_stride, int lap0, int lap1, mam_keypoint* d_kps, uint8_t* d_desc,
+                                 int capacity, int32_t* d_counts, void* stream) {
+    if (!c || !d_imgs || nframes <= 0 || w <= 0 || h <= 0 || stride < (size_t)w || !d_kps || !d_desc || !d_counts ||
+        capacity < 0)
+        return MAM_ERR_ARG;
+    if (nframes > 1 && frame_stride < stride * h) return MAM_ERR_ARG;
+    MAM_HIP(hipSetDevice(c->device));
+    if (int rc = ensure_geometry(c, w, h, nframes)) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return run_pipeline(c, d_imgs, nframes, stride, frame_stride, lap0, lap1, d_kps, d_desc, capacity, d_counts, s);
+}
+
+int mam_orb_extract(mam_orb_ctx* c, const uint8_t* img, int w, int h, size_t stride, int lap0, int lap1,
+                    mam_keypoint* kps, uint8_t* desc, int capacity, int* n_out, int* mono_out) {
+    if (!c || !n_out || !mono_out) return MAM_ERR_ARG;
+    *n_out = 0;
+    *mono_out = 0;
+    if (!img || w <= 0 || h <= 0) return MAM_ERR_EMPTY;
+    if (stride < (size_t)w || capacity < 0) return MAM_ERR_ARG;
+    MAM_HIP(hipSetDevice(c->device));
+    if (int rc = ensure_geometry(c, w, h, 1)) return rc;
+    const int kcap = c->geom.kp_slots;
+    if (int rc = c->d_input.alloc((size_t)w * h)) return rc;
+    if (int rc = c->d_kps.alloc(kcap)) return rc;
+    if (int rc = c->d_desc.alloc((size_t)kcap * 32)) return rc;
+    if (int rc = c->d_counts.alloc(2)) return rc;
+    MAM_HIP(hipMemcpy2DAsync(c->d_input.p, w, img, stride, w, h, hipMemcpyHostToDevice, c->stream));
+    if (int rc = run_pipeline(c, c->d_input.p, 1, w, (size_t)w * h, lap0, lap1, c->d_kps.p, c->d_desc.p, kcap,
+                              c->d_counts.p, c->stream))
+        return rc;
+    int32_t cnt[2];
+    MAM_HIP(hipMemcpyAsync(cnt, c->d_counts.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipStreamSynchronize(c->stream));
+    if (cnt[0] < 0) { g_last_error = "internal keypoint slot overflow"; return MAM_ERR_DEVICE; }
+    *n_out = cnt[0];
+    if (cnt[0] > capacity || (cnt[0] > 0 && (!kps || !desc))) return MAM_ERR_CAPACITY;
+    *mono_out = cnt[1];
+    if (cnt[0] > 0) {
+        MAM_HIP(hipMemcpyAsync(kps, c->d_kps.p, sizeof(mam_keypoint) * cnt[0], hipMemcpyDeviceToHost, c->stream));
+        MAM_HIP(hipMemcpyAsync(desc, c->d_desc.p, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost, c->stream));
+        MAM_HIP(hipStreamSynchronize(c->stream));
+    }
+    return MAM_OK;
+}
+
+int mam_orb_get_level(mam_orb_ctx* c, int frame, int level, uint8_t* out, int* w_out, int* h_out) {
+    if (!c || level < 0 || level >= c->prm.nlevels || frame < 0 || frame >= c->last_nframes || !c->last_in0)
+        return MAM_ERR_ARG;
+    const mam::LevelGeom& lv = c->geom.L[level];
+    if (w_out) *w_out = lv.w;
+    if (h_out) *h_out = lv.h;
+    if (!out) return MAM_OK;
+    MAM_HIP(hipStreamSynchronize(c->stream));
+    const uint8_t* src;
+    size_t pitch;
+    if (level == 0) { src = c->last_in0 + (size_t)frame * c->last_fstride; pitch = c->last_stride; }
+    else { src = c->d_pyr.p + lv.pyr_off + (size_t)frame * lv.frame_bytes; pitch = lv.pitch; }
+    MAM_HIP(hipMemcpy2D(out, lv.w, src, pitch, lv.w, lv.h, hipMemcpyDeviceToHost));
+    return MAM_OK;
+}
+
+int mam_orb_debug_blurred(mam_orb_ctx* c, int frame, int level, uint8_t* out) {
+    if (!c || !out || level < 0 || level >= c->prm.nlevels || frame < 0 || frame >= c->last_nframes)
+        return MAM_ERR_ARG;
+    const mam::LevelGeom& lv = c->geom.L[level];
+    MAM_HIP(hipStreamSynchronize(c->stream));
+    MAM_HIP(hipMemcpy2D(out, lv.w, c->d_blur.p + lv.blur_off + (size_t)frame * lv.frame_bytes, lv.pitch, lv.w, lv.h,
+                        hipMemcpyDeviceToHost));
+    return lv.w * lv.h;
+}
+
+int mam_orb_debug_candidates(mam_orb_ctx* c, int frame, int level, uint32_t* out, int capacity) {
+    if (!c || level < 0 || level >= c->prm.nlevels || frame < 0 || frame >= c->last_nframes) return MAM_ERR_ARG;
+    MAM_HIP(hipStreamSynchronize(c->stream));
+    const mam::LevelGeom& lv = c->geom.L[level];
+    std::vector<int> cnt(lv.ncells);
+    MAM_HIP(hipMemcpy(cnt.data(), c->d_cellcnt.p + (size_t)frame * c->geom.cells_per_frame + lv.cell_base,
+                      sizeof(int) * lv.ncells, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> slots((size_t)lv.cand_cap);
+    MAM_HIP(hipMemcpy(slots.data(), c->d_cand.p + (size_t)frame * c->geom.cand_per_frame + lv.cand_base,
+                      sizeof(uint32_t) * lv.cand_cap, hipMemcpyDeviceToHost));
+    int n = 0;
+    for (int i = 0; i < lv.ncells; i++)
+        for (int k = 0; k < cnt[i]; k++) {
+            if (out && n < capacity) out[n] = slots[(size_t)i * lv.cellcap + k];
+            n++;
+        }
+    return n;
+}
+
+int mam_orb_set_profiling(mam_orb_ctx* c, int enable) {
+    if (!c) return MAM_ERR_ARG;
+    c->profiling = enable != 0;
+    for (int i = 0; i < MAM_STAGE_COUNT; i++) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
+    for (auto& pe : c->pending) { c->event_pool.push_back(pe.a); c->event_pool.push_back(pe.b); }
+    c->pending.clear();
+    return MAM_OK;
+}
+
+int mam_orb_stage_times(mam_orb_ctx* c, double* ms_out, int64_t* launches_out) {
+    if (!c) return MAM_ERR_ARG;
+    for (auto& pe : c->pending) {
+        (void)hipEventSynchronize(pe.b);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, pe.a, pe.b);
+        c->stage_ms[pe.stage] += ms;
+        c->stage_n[pe.stage] += 1;
+        c->event_pool.push_back(pe.a);
+        c->event_pool.push_back(pe.b);
+    }
+    c->pending.clear();
+    for (int i = 0; i < MAM_STAGE_COUNT; i++) {
+        if (ms_out) ms_out[i] = c->stage_ms[i];
+        if (launches_out) launches_out[i] = c->stage_n[i];
+    }
+    return MAM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,786 @@
+// orb_kernels.hip — gfx950 kernels of the ORB extraction hot path (MI355X, wave64).
+//
+// Stage map (reference call stack SURVEY.md §3.A):
+//   k_pyr_down      ComputePyramid: cv::resize INTER_LINEAR 8U, level l from level l-1
+//                   (src/ORBextractor.cc:1170-1195); one launch per level, batched over frames.
+//   k_fast_cells    ComputeKeyPointsOctTree's per-cell FAST (src/ORBextractor.cc:805-872): one workgroup per
+//                   35-px cell of every level of every frame; ROI staged in LDS, FAST-9 "strength" per
+//                   pixel, in-cell 3x3 NMS at iniThFAST, retry at minThFAST only if the cell came out empty,
+//                   ordered compaction (wave ballots + LDS scan) into per-cell candidate slots.
+//   k_blur7         GaussianBlur(7x7, sigma 2, REFLECT_101) fixed-point (src/ORBextractor.cc:1132-1133): LDS
+//                   tiles, separable integer passes, all levels in one launch.
+//   k_distribute    DistributeOctTree (src/ORBextractor.cc:555-779): one workgroup per (frame, level); the
+//                   quadtree rounds are rebuilt in parallel (list order reconstructed by scans), the
+//                   final-phase std::sort replayed by mam::stl_sort; retain-best per node; lapping ranks.
+//   k_describe      IC_Angle + computeOrbDescriptor + lapping placement (src/ORBextractor.cc:76-146,
+//                   1122-1165): one wave per keypoint; rBRIEF bits built by __ballot.
+//
+// Integer/byte work throughout: HBM- and latency-bound, no MFMA.
+#include <hip/hip_runtime.h>
+
+#include "det_math.hpp"
+#include "introsort.hpp"
+#include "orb_common.hpp"
+
+namespace mam {
+
+__constant__ int8_t c_pattern[1024] = {
+#include "orb_pattern.inc"
+};
+
+// Gaussian taps of cv::GaussianBlur(7x7, sigma=2) on 8U in fixed point (getGaussianKernelBitExact +
+// getGaussianKernelFixedPoint_ED, 8 fractional bits).
+#define GT0 18
+#define GT1 34
+#define GT2 48
+#define GT3 56
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Exclusive scan over a 256-thread block. scr: >= 4 ints of LDS. All threads must call.
+__device__ __forceinline__ int block_excl_scan(int v, int* scr, int* total) {
+    const int incl = wave_incl_scan(v);
+    const int w = wave_id();
+    if (lane_id() == 63) scr[w] = incl;
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int s = scr[i];
+        if (i < w) pre += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return incl - v + pre;
+}
+
+__device__ __forceinline__ int block_sum(int v, int* scr) {
+    int t;
+    block_excl_scan(v, scr, &t);
+    return t;
+}
+
+__device__ __forceinline__ int block_min(int v, int* scr) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    if (lane_id() == 0) scr[wave_id()] = v;
+    __syncthreads();
+    int r = min(min(scr[0], scr[1]), min(scr[2], scr[3]));
+    __syncthreads();
+    return r;
+}
+
+struct LevelSrc {
+    const uint8_t* in0;
+    size_t in_stride;
+    size_t in_fstride;
+    const uint8_t* pyr;
+};
+
+__device__ __forceinline__ const uint8_t* level_ptr(const Geom* g, const LevelSrc& s, int f, int l, int* pitch) {
+    if (l == 0) {
+        *pitch = (int)s.in_stride;
+        return s.in0 + (size_t)f * s.in_fstride;
+    }
+    const LevelGeom& L = g->L[l];
+    *pitch = L.pitch;
+    return s.pyr + L.pyr_off + (size_t)f * L.frame_bytes;
+}
+
+// ------------------------------------------------------------------------------------------------ pyramid
+// OpenCV hal::resize INTER_LINEAR, CV_8UC1: exact-int horizontal pass
+// (HResizeLinear), vertical pass with VResizeLinearVec_32s8u's mulhi formula for x < xvec and
+// FixedPtCast<int,uchar,22> beyond. 4 output pixels per thread, one u32 store.
+__global__ __launch_bounds__(256) void k_pyr_down(const Geom* __restrict__ g, int l, LevelSrc s, uint8_t* pyr) {
+    const LevelGeom& L = g->L[l];
+    const LevelGeom& P = g->L[l - 1];
+    const int f = blockIdx.z;
+    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int dx0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+    if (dy >= L.h || dx0 >= L.w) return;
+    int spitch;
+    const uint8_t* src = level_ptr(g, s, f, l - 1, &spitch);
+    uint8_t* dst = pyr + L.pyr_off + (size_t)f * L.frame_bytes;
+    const int sy = L.yofs[dy];
+    const int sh = P.h;
+    const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
+    const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
+    const uint8_t* S0 = src + (size_t)ry0 * spitch;
+    const uint8_t* S1 = src + (size_t)ry1 * spitch;
+    const int b0 = L.ibeta[2 * dy], b1 = L.ibeta[2 * dy + 1];
+    uint32_t packed = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int dx = dx0 + i;
+        if (dx < L.w) {
+            const int sx = L.xofs[dx];
+            int h0, h1;
+            if (dx < L.xmax) {
+                const int a0 = L.ialpha[2 * dx], a1 = L.ialpha[2 * dx + 1];
+                h0 = S0[sx] * a0 + S0[sx + 1] * a1;
+                h1 = S1[sx] * a0 + S1[sx + 1] * a1;
+            } else {
+                h0 = S0[sx] * 2048;
+                h1 = S1[sx] * 2048;
+            }
+            int v;
+            if (dx < L.xvec) {
+                const int t0 = min(max(h0 >> 4, -32768), 32767);
+                const int t1 = min(max(h1 >> 4, -32768), 32767);
+                const int m0 = (t0 * b0) >> 16, m1 = (t1 * b1) >> 16;
+                int sum = min(max(m0 + m1, -32768), 32767);
+                sum = min(max(sum + 2, -32768), 32767);
+                v = sum >> 2;
+            } else {
+                v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+            }
+            v = min(max(v, 0), 255);
+            packed |= (uint32_t)v << (8 * i);
+        }
+    }
+    uint8_t* o = dst + (size_t)dy * L.pitch + dx0;
+    if (dx0 + 4 <= L.w) {
+        *reinterpret_cast<uint32_t*>(o) = packed;
+    } else {
+        for (int i = 0; i < 4 && dx0 + i < L.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ FAST cells
+// FAST-9/16 "strength" S = max over the 16 arcs of 9 contiguous circle pixels of min(v-p) (dark) or
+// min(p-v) (bright). Pixel is a FAST corner at threshold t iff S > t and OpenCV's cornerScore is then S-1
+// (fast_score.cpp: max(t, A, B) - 1), so one S map serves both thresholds.
+__device__ __forceinline__ int fast_strength(const uint8_t* im, int cols, int r, int c) {
+    const uint8_t* p = im + r * cols + c;
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * cols];
+    d[1] = v - p[3 * cols + 1];
+    d[2] = v - p[2 * cols + 2];
+    d[3] = v - p[cols + 3];
+    d[4] = v - p[3];
+    d[5] = v - p[-cols + 3];
+    d[6] = v - p[-2 * cols + 2];
+    d[7] = v - p[-3 * cols + 1];
+    d[8] = v - p[-3 * cols];
+    d[9] = v - p[-3 * cols - 1];
+    d[10] = v - p[-2 * cols - 2];
+    d[11] = v - p[-cols - 3];
+    d[12] = v - p[-3];
+    d[13] = v - p[cols - 3];
+    d[14] = v - p[2 * cols - 2];
+    d[15] = v - p[3 * cols - 1];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    }
+    int A = -1024, Bm = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int mn8 = min(mn4[k], mn4[(k + 4) & 15]);
+        const int mx8 = max(mx4[k], mx4[(k + 4) & 15]);
+        A = max(A, min(mn8, d[(k + 8) & 15]));
+        Bm = min(Bm, max(mx8, d[(k + 8) & 15]));
+    }
+    const int S = max(A, -Bm);
+    return S < 0 ? 0 : S;
+}
+
+__device__ __forceinline__ bool fast_is_kp(const uint8_t* S, int cols, int idx, int t) {
+    const int s = S[idx];
+    if (s <= t) return false;
+    const int sc = s - 1;
+    const int nb[8] = {-cols - 1, -cols, -cols + 1, -1, 1, cols - 1, cols, cols + 1};
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int q = S[idx + nb[i]];
+        const int scq = q > t ? q - 1 : 0;
+        if (!(sc > scq)) return false;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_fast_cells(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
+                                                    LevelSrc s, uint32_t* __restrict__ cand,
+                                                    int* __restrict__ cell_counts, int iniTh, int minTh) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const CellDesc c = cells[blockIdx.x];
+    const int f = blockIdx.y;
+    const LevelGeom& L = g->L[c.level];
+    const int roi_cap = ((g->roi_max_rows * g->roi_max_cols) + 15) & ~15;
+    uint8_t* im = smem;
+    uint8_t* S = smem + roi_cap;
+    int* scr = reinterpret_cast<int*>(smem + 2 * roi_cap);
+    const int tid = threadIdx.x;
+    int pitch;
+    const uint8_t* lev = level_ptr(g, s, f, c.level, &pitch);
+    const int rows = c.y1 - c.y0, cols = c.x1 - c.x0;
+    const int npx = rows * cols;
+    for (int i = tid; i < npx; i += 256) {
+        const int r = i / cols, cc = i - r * cols;
+        im[i] = lev[(size_t)(c.y0 + r) * pitch + c.x0 + cc];
+        S[i] = 0;
+    }
+    __syncthreads();
+    const int bh = rows - 6, bw = cols - 6;
+    const int nb = (bh > 0 && bw > 0) ? bh * bw : 0;
+    for (int i = tid; i < nb; i += 256) {
+        const int r = 3 + i / bw, cc = 3 + i % bw;
+        S[r * cols + cc] = (uint8_t)fast_strength(im, cols, r, cc);
+    }
+    __syncthreads();
+    int cnt = 0;
+    for (int i = tid; i < nb; i += 256) {
+        const int r = 3 + i / bw, cc = 3 + i % bw;
+        cnt += fast_is_kp(S, cols, r * cols + cc, iniTh) ? 1 : 0;
+    }
+    const int total = block_sum(cnt, scr);
+    const int th = total > 0 ? iniTh : minTh;
+    uint32_t* out = cand + (size_t)f * g->cand_per_frame + L.cand_base + (size_t)c.slot * L.cellcap;
+    int base = 0;
+    for (int chunk = 0; chunk < nb; chunk += 256) {
+        const int i = chunk + tid;
+        bool flag = false;
+        int r = 0, cc = 0;
+        if (i < nb) {
+            r = 3 + i / bw;
+            cc = 3 + i % bw;
+            flag = fast_is_kp(S, cols, r * cols + cc, th);
+        }
+        int tot;
+        const int pos = block_excl_scan(flag ? 1 : 0, scr, &tot);
+        if (flag) {
+            const uint32_t x = (uint32_t)(cc + c.cj * L.wCell);
+            const uint32_t y = (uint32_t)(r + c.ci * L.hCell);
+            const uint32_t sc = (uint32_t)(S[r * cols + cc] - 1);
+            out[base + pos] = x | (y << 12) | (sc << 24);
+        }
+        base += tot;
+    }
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = base;
+}
+
+// ------------------------------------------------------------------------------------------------ blur
+__device__ __forceinline__ int refl101(int p, int n) {
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
+__global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ blur) {
+    __shared__ uint8_t tin[BLUR_TILE_H + 6][BLUR_TILE_W + 8];
+    __shared__ uint32_t th_[BLUR_TILE_H + 6][BLUR_TILE_W];
+    const int f = blockIdx.y;
+    int tile = blockIdx.x;
+    int l = 0;
+    for (int i = 1; i < g->nlevels; i++)
+        if (tile >= g->L[i].tile_base) l = i;
+    const LevelGeom& L = g->L[l];
+    tile -= L.tile_base;
+    const int x0 = (tile % L.tiles_x) * BLUR_TILE_W;
+    const int y0 = (tile / L.tiles_x) * BLUR_TILE_H;
+    int pitch;
+    const uint8_t* lev = level_ptr(g, s, f, l, &pitch);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < (BLUR_TILE_H + 6) * (BLUR_TILE_W + 6); i += 256) {
+        const int r = i / (BLUR_TILE_W + 6), c = i % (BLUR_TILE_W + 6);
+        const int gy = refl101(y0 - 3 + r, L.h), gx = refl101(x0 - 3 + c, L.w);
+        tin[r][c] = lev[(size_t)gy * pitch + gx];
+    }
+    __syncthreads();
+    for (int i = tid; i < (BLUR_TILE_H + 6) * BLUR_TILE_W; i += 256) {
+        const int r = i / BLUR_TILE_W, c = i % BLUR_TILE_W;
+        const uint8_t* p = &tin[r][c];
+        th_[r][c] = GT0 * (p[0] + p[6]) + GT1 * (p[1] + p[5]) + GT2 * (p[2] + p[4]) + GT3 * p[3];
+    }
+    __syncthreads();
+    uint8_t* out = blur + L.blur_off + (size_t)f * L.frame_bytes;
+    for (int i = tid; i < BLUR_TILE_H * BLUR_TILE_W; i += 256) {
+        const int r = i / BLUR_TILE_W, c = i % BLUR_TILE_W;
+        const int y = y0 + r, x = x0 + c;
+        if (y < L.h && x < L.w) {
+            const uint32_t sum = GT0 * (th_[r][c] + th_[r + 6][c]) + GT1 * (th_[r + 1][c] + th_[r + 5][c]) +
+                                 GT2 * (th_[r + 2][c] + th_[r + 4][c]) + GT3 * th_[r + 3][c];
+            const uint32_t v = (sum + 32768u) >> 16;
+            out[(size_t)y * L.pitch + x] = (uint8_t)(v > 255u ? 255u : v);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ distribute
+// LDS-resident node table in LIST ORDER (node id == list position). Each round rebuilds the list:
+// reference semantics (ORBextractor.cc:605-748): children are push_front'ed in creation order and the
+// parent erased, so the new list = reverse(creation sequence) ++ (unexpanded nodes in order).
+struct NodeBuf {
+    uint16_t* x0;
+    uint16_t* y0;
+    uint16_t* x1;
+    uint16_t* y1;
+    uint32_t* cnt;
+};
+
+__device__ __forceinline__ int quad_of(const NodeBuf& A, int p, uint32_t key) {
+    const int x = key & 0xFFF, y = (key >> 12) & 0xFFF;
+    const int hx = (A.x1[p] - A.x0[p] + 1) >> 1;  // ceil((UR.x-UL.x)/2.f)
+    const int hy = (A.y1[p] - A.y0[p] + 1) >> 1;
+    const bool left = x < A.x0[p] + hx, top = y < A.y0[p] + hy;
+    return left ? (top ? 0 : 2) : (top ? 1 : 3);
+}
+
+__device__ __forceinline__ void child_rect(const NodeBuf& A, int p, int q, int* x0, int* y0, int* x1, int* y1) {
+    const int ax0 = A.x0[p], ay0 = A.y0[p], ax1 = A.x1[p], ay1 = A.y1[p];
+    const int hx = (ax1 - ax0 + 1) >> 1, hy = (ay1 - ay0 + 1) >> 1;
+    *x0 = (q & 1) ? ax0 + hx : ax0;
+    *x1 = (q & 1) ? ax1 : ax0 + hx;
+    *y0 = (q & 2) ? ay0 + hy : ay0;
+    *y1 = (q & 2) ? ay1 : ay0 + hy;
+}
+
+__global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, const int* __restrict__ cell_counts,
+                                                    const uint32_t* __restrict__ cand, uint32_t* __restrict__ keys,
+                                                    uint16_t* __restrict__ knode, uint32_t* __restrict__ out_key,
+                                                    uint32_t* __restrict__ out_rank, int* __restrict__ lvl_counts,
+                                                    int lap0, int lap1) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom& L = g->L[l];
+    const int NC = g->node_cap;
+    // ---- LDS carve (all offsets multiples of 16 B)
+    uint8_t* p8 = smem;
+    auto take = [&](size_t bytes) { uint8_t* r = p8; p8 += (bytes + 15) & ~(size_t)15; return r; };
+    NodeBuf nb[2];
+    for (int b = 0; b < 2; b++) {
+        nb[b].x0 = (uint16_t*)take(NC * 2);
+        nb[b].y0 = (uint16_t*)take(NC * 2);
+        nb[b].x1 = (uint16_t*)take(NC * 2);
+        nb[b].y1 = (uint16_t*)take(NC * 2);
+        nb[b].cnt = (uint32_t*)take(NC * 4);
+    }
+    uint32_t* ch = (uint32_t*)take((size_t)NC * 16);
+    int* xr = (int*)take(NC * 4);
+    int* aux = (int*)take(NC * 4);       // E[r] then CB[r]
+    int* candl = (int*)take(NC * 4);
+    SortEl* arr = (SortEl*)take(NC * 8);
+    int* cellOff = (int*)take((g->max_level_cells + 1) * 4);
+    int* scr = (int*)take(64);
+    int* sh = (int*)take(64);           // block-uniform scalars
+
+    // ---- 0. gather this level's candidates in reference order (cells row-major, FAST order inside)
+    const int* cc = cell_counts + (size_t)f * g->cells_per_frame + L.cell_base;
+    int carry = 0;
+    for (int c0 = 0; c0 < L.ncells; c0 += 256) {
+        const int c = c0 + tid;
+        const int v = c < L.ncells ? cc[c] : 0;
+        int tot;
+        const int pre = block_excl_scan(v, scr, &tot);
+        if (c < L.ncells) cellOff[c] = carry + pre;
+        carry += tot;
+    }
+    const int n = carry;
+    const uint32_t* cbase = cand + (size_t)f * g->cand_per_frame + L.cand_base;
+    uint32_t* K = keys + (size_t)f * g->cand_per_frame + L.cand_base;
+    uint16_t* KN = knode + (size_t)f * g->cand_per_frame + L.cand_base;
+    for (int c = wave_id(); c < L.ncells; c += 4) {
+        const int cnt = cc[c], off = cellOff[c];
+        for (int i = lane_id(); i < cnt; i += 64) K[off + i] = cbase[(size_t)c * L.cellcap + i];
+    }
+    __syncthreads();
+    int* lc = lvl_counts + ((size_t)f * g->nlevels + l) * 2;
+    if (n == 0) {
+        if (tid == 0) { lc[0] = 0; lc[1] = 0; }
+        return;
+    }
+    const int N = L.nfeat;
+    const int H = L.maxBY - L.minBY;
+    // ---- 1. initial nodes (ORBextractor.cc:559-598)
+    int cur = 0;
+    {
+        NodeBuf& A = nb[0];
+        for (int i = tid; i < L.nini; i += 256) {
+            A.x0[i] = (uint16_t)(int)(L.hX * (float)i);
+            A.x1[i] = (uint16_t)(int)(L.hX * (float)(i + 1));
+            A.y0[i] = 0;
+            A.y1[i] = (uint16_t)H;
+            A.cnt[i] = 0;
+        }
+        __syncthreads();
+        for (int k = tid; k < n; k += 256) {
+            const float x = (float)(K[k] & 0xFFF);
+            const int i = (int)(x / L.hX);
+            KN[k] = (uint16_t)i;
+            atomicAdd(&A.cnt[i], 1u);
+        }
+        __syncthreads();
+        // erase empty initial nodes, keep order
+        NodeBuf& B = nb[1];
+        int keep_carry = 0;
+        for (int i0 = 0; i0 < L.nini; i0 += 256) {
+            const int i = i0 + tid;
+            const bool ne = i < L.nini && A.cnt[i] > 0;
+            int tot;
+            const int pos = block_excl_scan(ne ? 1 : 0, scr, &tot);
+            if (ne) {
+                const int np = keep_carry + pos;
+                B.x0[np] = A.x0[i]; B.y0[np] = A.y0[i]; B.x1[np] = A.x1[i]; B.y1[np] = A.y1[i];
+                B.cnt[np] = A.cnt[i];
+                ch[4 * i] = np;
+            }
+            keep_carry += tot;
+        }
+        __syncthreads();
+        for (int k = tid; k < n; k += 256) KN[k] = (uint16_t)ch[4 * KN[k]];
+        if (tid == 0) sh[0] = keep_carry;
+        __syncthreads();
+        cur = 1;
+    }
+    int S = sh[0];
+
+    // Rebuild the list given xr[p] (expansion rank, -1 = unexpanded) for p < S, NX expanded nodes whose
+    // children were already counted into ch[4p..4p+3]; aux[r] = #non-empty children of rank r.
+    // Produces the new list in the other buffer, remaps keys, builds candl (children with >1 keys in
+    // creation order) and returns (via sh) the new size and #candidates.
+    auto rebuild = [&](int NX) {
+        NodeBuf& A = nb[cur];
+        NodeBuf& B = nb[cur ^ 1];
+        // exclusive scan of aux over ranks -> creation base (in place)
+        int cb_carry = 0;
+        for (int r0 = 0; r0 < NX; r0 += 256) {
+            const int r = r0 + tid;
+            const int v = r < NX ? aux[r] : 0;
+            int tot;
+            const int pre = block_excl_scan(v, scr, &tot);
+            if (r < NX) aux[r] = cb_carry + pre;
+            cb_carry += tot;
+        }
+        const int C = cb_carry;
+        __syncthreads();
+        int k_carry = 0;
+        for (int p0 = 0; p0 < S; p0 += 256) {
+            const int p = p0 + tid;
+            const bool kept = p < S && xr[p] < 0;
+            int tot;
+            const int kr = block_excl_scan(kept ? 1 : 0, scr, &tot);
+            if (p < S) {
+                if (kept) {
+                    const int np = C + k_carry + kr;
+                    B.x0[np] = A.x0[p]; B.y0[np] = A.y0[p]; B.x1[np] = A.x1[p]; B.y1[np] = A.y1[p];
+                    B.cnt[np] = A.cnt[p];
+                    ch[4 * p] = np;
+                } else {
+                    int c = aux[xr[p]];
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t cq = ch[4 * p + q];
+                        if (cq > 0) {
+                            const int np = C - 1 - c;
+                            int cx0, cy0, cx1, cy1;
+                            child_rect(A, p, q, &cx0, &cy0, &cx1, &cy1);
+                            B.x0[np] = (uint16_t)cx0; B.y0[np] = (uint16_t)cy0;
+                            B.x1[np] = (uint16_t)cx1; B.y1[np] = (uint16_t)cy1;
+                            B.cnt[np] = cq;
+                            ch[4 * p + q] = np;
+                            c++;
+                        }
+                    }
+                }
+            }
+            k_carry += tot;
+        }
+        __syncthreads();
+        for (int k = tid; k < n; k += 256) {
+            const int p = KN[k];
+            if (xr[p] < 0) KN[k] = (uint16_t)ch[4 * p];
+            else KN[k] = (uint16_t)ch[4 * p + quad_of(A, p, K[k])];
+        }
+        // candidates for the next step: children with >1 keys, creation order = descending position
+        int m_carry = 0;
+        for (int c0 = 0; c0 < C; c0 += 256) {
+            const int c = c0 + tid;
+            const bool big = c < C && B.cnt[C - 1 - c] > 1;
+            int tot;
+            const int pos = block_excl_scan(big ? 1 : 0, scr, &tot);
+            if (big) candl[m_carry + pos] = C - 1 - c;
+            m_carry += tot;
+        }
+        if (tid == 0) { sh[0] = C + k_carry; sh[1] = m_carry; }
+        __syncthreads();
+        cur ^= 1;
+    };
+
+    bool finish = false;
+    bool final_phase = false;
+    int m = 0;
+    int guard = 0;
+    while (!finish) {
+        if (++guard > 4096) {  // unreachable for a correct rebuild (S grows or the loop ends); never hang
+            if (tid == 0) { lc[0] = -1; lc[1] = 0; }
+            return;
+        }
+        const int prevSize = S;
+        if (!final_phase) {
+            // ---- phase-1 round: every node with >1 keys divides (ORBextractor.cc:605-677)
+            NodeBuf& A = nb[cur];
+            int x_carry = 0;
+            for (int p0 = 0; p0 < S; p0 += 256) {
+                const int p = p0 + tid;
+                const bool ex = p < S && A.cnt[p] > 1;
+                int tot;
+                const int pos = block_excl_scan(ex ? 1 : 0, scr, &tot);
+                if (p < S) {
+                    xr[p] = ex ? x_carry + pos : -1;
+                    if (ex) { ch[4 * p] = 0; ch[4 * p + 1] = 0; ch[4 * p + 2] = 0; ch[4 * p + 3] = 0; }
+                }
+                x_carry += tot;
+            }
+            const int NX = x_carry;
+            __syncthreads();
+            for (int k = tid; k < n; k += 256) {
+                const int p = KN[k];
+                if (xr[p] >= 0) atomicAdd(&ch[4 * p + quad_of(A, p, K[k])], 1u);
+            }
+            __syncthreads();
+            for (int p = tid; p < S; p += 256) {
+                if (xr[p] >= 0)
+                    aux[xr[p]] = (ch[4 * p] > 0) + (ch[4 * p + 1] > 0) + (ch[4 * p + 2] > 0) + (ch[4 * p + 3] > 0);
+            }
+            __syncthreads();
+            rebuild(NX);
+            S = sh[0];
+            m = sh[1];
+            if (S >= N || S == prevSize) finish = true;
+            else if (S + m * 3 > N) final_phase = true;
+        } else {
+            // ---- final phase (ORBextractor.cc:680-748): sort last round's >1-key children by
+            // (size, UL.x) with libstdc++'s introsort, expand from the largest until size >= N.
+            if (m == 0) break;
+            NodeBuf& A = nb[cur];
+            for (int i = tid; i < m; i += 256) {
+                const int p = candl[i];
+                arr[i].key = (A.cnt[p] << 12) | A.x0[p];
+                arr[i].val = (uint32_t)p;
+            }
+            __syncthreads();
+            if (tid == 0) stl_sort(arr, arr + m);
+            __syncthreads();
+            for (int p = tid; p < S; p += 256) xr[p] = -1;
+            __syncthreads();
+            for (int i = tid; i < m; i += 256) {
+                const int p = arr[i].val;
+                xr[p] = i;  // sorted index for now
+                ch[4 * p] = 0; ch[4 * p + 1] = 0; ch[4 * p + 2] = 0; ch[4 * p + 3] = 0;
+            }
+            __syncthreads();
+            for (int k = tid; k < n; k += 256) {
+                const int p = KN[k];
+                if (xr[p] >= 0) atomicAdd(&ch[4 * p + quad_of(A, p, K[k])], 1u);
+            }
+            __syncthreads();
+            // expansion rank r = m-1-i; grow(r) = sum_{r'<=r} (e(r')-1); stop at the first r with S+grow >= N
+            int g_carry = 0;
+            int rstop_local = m - 1;
+            for (int r0 = 0; r0 < m; r0 += 256) {
+                const int r = r0 + tid;
+                int e = 0;
+                if (r < m) {
+                    const int p = arr[m - 1 - r].val;
+                    e = (ch[4 * p] > 0) + (ch[4 * p + 1] > 0) + (ch[4 * p + 2] > 0) + (ch[4 * p + 3] > 0);
+                    aux[r] = e;
+                }
+                int tot;
+                const int pre = block_excl_scan(r < m ? e - 1 : 0, scr, &tot);
+                if (r < m && S + g_carry + pre + (e - 1) >= N) rstop_local = min(rstop_local, r);
+                g_carry += tot;
+            }
+            const int rstop = block_min(rstop_local, scr);
+            const int NX = rstop + 1;
+            for (int p = tid; p < S; p += 256) {
+                const int i = xr[p];
+                if (i >= 0) {
+                    const int r = m - 1 - i;
+                    xr[p] = r <= rstop ? r : -1;
+                }
+            }
+            __syncthreads();
+            rebuild(NX);
+            S = sh[0];
+            m = sh[1];
+            if (S >= N || S == prevSize) finish = true;
+        }
+    }
+
+    // ---- retain the best key per node (first max response in candidate order, ORBextractor.cc:758-776)
+    NodeBuf& A = nb[cur];
+    (void)A;
+    for (int p = tid; p < S; p += 256) ch[p] = 0;
+    __syncthreads();
+    for (int k = tid; k < n; k += 256) {
+        const uint32_t v = ((K[k] >> 24) << 24) | (0xFFFFFFu - (uint32_t)k);
+        atomicMax(&ch[KN[k]], v);
+    }
+    __syncthreads();
+    // ---- outputs in list order + lapping ranks (ORBextractor.cc:1141-1162)
+    uint32_t* ok = out_key + (size_t)f * g->kp_slots + L.kp_base;
+    uint32_t* orr = out_rank + (size_t)f * g->kp_slots + L.kp_base;
+    if (S > L.kp_cap) {
+        if (tid == 0) { lc[0] = -1; lc[1] = 0; }
+        return;
+    }
+    int st_carry = 0;
+    for (int p0 = 0; p0 < S; p0 += 256) {
+        const int p = p0 + tid;
+        bool st = false;
+        uint32_t kv = 0;
+        if (p < S) {
+            const uint32_t k = 0xFFFFFFu - (ch[p] & 0xFFFFFFu);
+            kv = K[k];
+            float xs = (float)((int)(kv & 0xFFF) + L.minBX);
+            if (l != 0) xs = xs * L.scale;
+            st = xs >= (float)lap0 && xs <= (float)lap1;
+        }
+        int tot;
+        const int rk = block_excl_scan(st ? 1 : 0, scr, &tot);
+        if (p < S) {
+            ok[p] = kv;
+            orr[p] = st ? (0x80000000u | (uint32_t)(st_carry + rk)) : (uint32_t)(p - (st_carry + rk));
+        }
+        st_carry += tot;
+    }
+    if (tid == 0) { lc[0] = S; lc[1] = st_carry; }
+}
+
+// ------------------------------------------------------------------------------------------------ describe
+__global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, LevelSrc s,
+                                                  const uint8_t* __restrict__ blur,
+                                                  const uint32_t* __restrict__ out_key,
+                                                  const uint32_t* __restrict__ out_rank,
+                                                  const int* __restrict__ lvl_counts, int nframes,
+                                                  mam_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                  int capacity, int32_t* __restrict__ counts, int desc_fma) {
+    const int gw = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = lane_id();
+    const int f = gw / g->kp_slots;
+    const int r = gw - f * g->kp_slots;
+    if (f >= nframes) return;
+    const int nl = g->nlevels;
+    const int* lc = lvl_counts + (size_t)f * nl * 2;
+    int l = 0;
+    for (int i = 1; i < nl; i++)
+        if (r >= g->L[i].kp_base) l = i;
+    int ntot = 0, mono_before = 0, st_before = 0, mono_tot = 0;
+    bool bad = false;
+    for (int i = 0; i < nl; i++) {
+        const int cnt = lc[2 * i], st = lc[2 * i + 1];
+        if (cnt < 0) bad = true;
+        ntot += cnt;
+        mono_tot += cnt - st;
+        if (i < l) { mono_before += cnt - st; st_before += st; }
+    }
+    const bool overflow = bad || ntot > capacity;
+    if (r == 0 && lane == 0) {
+        counts[2 * f] = overflow ? -2 : ntot;
+        counts[2 * f + 1] = overflow ? 0 : mono_tot;
+    }
+    const LevelGeom& L = g->L[l];
+    const int idx = r - L.kp_base;
+    if (overflow || idx >= lc[2 * l]) return;
+    const uint32_t kv = out_key[(size_t)f * g->kp_slots + r];
+    const uint32_t rk = out_rank[(size_t)f * g->kp_slots + r];
+    const int x = (int)(kv & 0xFFF) + L.minBX;
+    const int y = (int)((kv >> 12) & 0xFFF) + L.minBY;
+    const int score = (int)(kv >> 24);
+    // IC_Angle on the unblurred level (ORBextractor.cc:76-103): integer moments over the radius-15 disk
+    int pitch;
+    const uint8_t* lev = level_ptr(g, s, f, l, &pitch);
+    const uint8_t* center = lev + (size_t)y * pitch + x;
+    int m10 = 0, m01 = 0;
+    if (lane < 31) {
+        const int u = lane - 15;
+        const int au = u < 0 ? -u : u;
+        for (int v = -15; v <= 15; v++) {
+            const int av = v < 0 ? -v : v;
+            if (au <= g->umax[av]) {
+                const int val = center[v * pitch + u];
+                m10 += u * val;
+                m01 += v * val;
+            }
+        }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // rBRIEF on the blurred level (ORBextractor.cc:107-146): lane owns pairs lane, lane+64, ...
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    float a, b;
+    det_sincos(angle * factorPI, &b, &a);
+    const uint8_t* bl = blur + L.blur_off + (size_t)f * L.frame_bytes;
+    const int bpitch = L.pitch;
+    const uint8_t* bc = bl + (size_t)y * bpitch + x;
+    uint64_t words[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int pr = lane + 64 * k;
+        int val[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const float px = (float)c_pattern[4 * pr + 2 * e];
+            const float py = (float)c_pattern[4 * pr + 2 * e + 1];
+            float fy, fx;
+            if (desc_fma) {
+                fy = __builtin_fmaf(px, b, py * a);
+                fx = __builtin_fmaf(px, a, -(py * b));
+            } else {
+                const float t0 = px * b, t1 = py * a;
+                fy = t0 + t1;
+                const float t2 = px * a, t3 = py * b;
+                fx = t2 - t3;
+            }
+            val[e] = bc[__float2int_rn(fy) * bpitch + __float2int_rn(fx)];
+        }
+        words[k] = __ballot(val[0] < val[1]);
+    }
+    // placement (ORBextractor.cc:1141-1162)
+    int o;
+    if (rk & 0x80000000u) o = ntot - 1 - (st_before + (int)(rk & 0x7FFFFFFFu));
+    else o = mono_before + (int)rk;
+    uint8_t* dd = desc + ((size_t)f * capacity + o) * 32;
+    const uint64_t mine = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+    if (lane < 4) reinterpret_cast<uint64_t*>(dd)[lane] = mine;
+    if (lane == 0) {
+        mam_keypoint kp;
+        float xs = (float)x, ys = (float)y;
+        if (l != 0) { xs = xs * L.scale; ys = ys * L.scale; }
+        kp.x = xs; kp.y = ys;
+        kp.size = (float)L.psize;
+        kp.angle = angle;
+        kp.response = (float)score;
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[(size_t)f * capacity + o] = kp;
+    }
+}
+
+}  // namespace mam

@@ -1,0 +1,88 @@
+"""Deterministic synthetic mono frames (SURVEY.md §8(d) "Synthetic inputs").
+
+There is no dataset in this environment: every benchmark and parity case runs on seeded textured
+frames. Scene = random axis-aligned and rotated rectangles (grey levels U[20,235]) plus Gaussian-smoothed
+noise, clamped to u8. Frame k of agent a is a crop of a larger canvas translated 2 px/frame with a
+0.2 deg/frame roll, so consecutive frames share structure (useful for matching).
+
+seed = 0x4D414D33 ^ (agent << 16) ^ frame  (the survey's convention).
+"""
+from __future__ import annotations
+
+import functools
+
+import numpy as np
+
+_SEED_BASE = 0x4D414D33
+
+
+def frame_seed(agent: int, frame: int) -> int:
+    return (_SEED_BASE ^ (agent << 16) ^ frame) & 0xFFFFFFFF
+
+
+def _smooth_noise(rng: np.random.Generator, h: int, w: int, sigma: float = 8.0) -> np.ndarray:
+    from scipy.ndimage import gaussian_filter
+
+    n = rng.normal(0.0, 1.0, size=(h, w)).astype(np.float32)
+    n = gaussian_filter(n, 1.2)
+    n *= sigma / max(float(n.std()), 1e-6)
+    return n
+
+
+@functools.lru_cache(maxsize=16)
+def make_canvas(h: int, w: int, seed: int, n_rects: int | None = None) -> np.ndarray:
+    """A textured float32 canvas of size h x w (cached; treat as read-only)."""
+    rng = np.random.default_rng(seed)
+    img = np.full((h, w), float(rng.uniform(60, 190)), np.float32)
+    if n_rects is None:
+        n_rects = max(40, (h * w) // 2500)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    for _ in range(n_rects):
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        rw, rh = rng.uniform(6, max(8, w / 8)), rng.uniform(6, max(8, h / 8))
+        val = float(rng.uniform(20, 235))
+        if rng.random() < 0.5:
+            x0, x1 = int(cx - rw / 2), int(cx + rw / 2)
+            y0, y1 = int(cy - rh / 2), int(cy + rh / 2)
+            img[max(0, y0):max(0, y1), max(0, x0):max(0, x1)] = val
+        else:
+            th = rng.uniform(0, np.pi)
+            c, s = np.cos(th), np.sin(th)
+            x0, x1 = int(max(0, cx - rw - rh)), int(min(w, cx + rw + rh + 1))
+            y0, y1 = int(max(0, cy - rw - rh)), int(min(h, cy + rw + rh + 1))
+            if x1 <= x0 or y1 <= y0:
+                continue
+            dx = xx[y0:y1, x0:x1] - cx
+            dy = yy[y0:y1, x0:x1] - cy
+            u = dx * c + dy * s
+            v = -dx * s + dy * c
+            m = (np.abs(u) < rw / 2) & (np.abs(v) < rh / 2)
+            img[y0:y1, x0:x1][m] = val
+    img += _smooth_noise(rng, h, w)
+    return img
+
+
+def make_frame(w: int, h: int, agent: int = 0, frame: int = 0, motion: bool = True) -> np.ndarray:
+    """u8 h x w frame; consecutive `frame` indices of one agent view one moving scene."""
+    canvas_seed = frame_seed(agent, 0)
+    margin = 64
+    ch, cw = h + 2 * margin, w + 2 * margin + 4 * 256
+    canvas = make_canvas(ch, cw, canvas_seed)
+    tx = 2.0 * frame if motion else 0.0
+    ang = 0.2 * frame if motion else 0.0
+    if ang != 0.0:
+        from scipy.ndimage import rotate
+
+        sub = canvas[:, int(tx): int(tx) + w + 2 * margin]
+        sub = rotate(sub, ang, reshape=False, order=1, mode="reflect")
+        out = sub[margin:margin + h, margin:margin + w]
+    else:
+        out = canvas[margin:margin + h, margin + int(tx): margin + int(tx) + w]
+    # per-frame sensor noise keeps frames distinct even without motion
+    rng = np.random.default_rng(frame_seed(agent, frame) ^ 0x5A5A)
+    out = out + rng.normal(0.0, 1.5, size=out.shape).astype(np.float32)
+    return np.ascontiguousarray(np.clip(np.rint(out), 0, 255).astype(np.uint8))
+
+
+def make_batch(w: int, h: int, n: int, agent: int = 0, start: int = 0) -> np.ndarray:
+    return np.stack([make_frame(w, h, agent, start + i) for i in range(n)])

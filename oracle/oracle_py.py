@@ -1,0 +1,178 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle (oracle/liboracle.so).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker.
+The product package (mam3slam_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+class KeyPoint(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("desc_fma", C.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                     ("octave", "<i4"), ("class_id", "<i4")])
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.oracle_fast_atan2.restype = C.c_float
+        _lib.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
+    return _lib
+
+
+def params(nfeatures=1000, scale_factor=1.2, nlevels=8, ini=20, mn=7, desc_fma=0) -> OrbParams:
+    return OrbParams(nfeatures, scale_factor, nlevels, ini, mn, desc_fma)
+
+
+def _u8p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def extract(img: np.ndarray, p: OrbParams | None = None, lap=(0, 1000)):
+    """ORBextractor::operator() on the oracle. Returns (keypoints structured array, desc (N,32) u8, mono)."""
+    p = p or params()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = p.nfeatures + 3 * p.nlevels + 64
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(0)
+    mono = C.c_int(0)
+    rc = lib().oracle_orb_extract(C.byref(p), _u8p(img), w, h, C.c_size_t(w), int(lap[0]), int(lap[1]),
+                                  kps.ctypes.data_as(C.c_void_p), _u8p(desc), cap, C.byref(n), C.byref(mono))
+    if rc != 0:
+        raise RuntimeError(f"oracle_orb_extract rc={rc}")
+    return kps[:n.value].copy(), desc[:n.value].copy(), mono.value
+
+
+def tables(p: OrbParams | None = None):
+    p = p or params()
+    L = p.nlevels
+    scales = np.zeros(4 * L, np.float32)
+    nfeat = np.zeros(L, np.int32)
+    umax = np.zeros(16, np.int32)
+    rc = lib().oracle_orb_tables(C.byref(p), scales.ctypes.data_as(C.c_void_p), nfeat.ctypes.data_as(C.c_void_p),
+                                 umax.ctypes.data_as(C.c_void_p))
+    assert rc == 0
+    return scales.reshape(4, L), nfeat, umax
+
+
+def pyramid(img: np.ndarray, p: OrbParams | None = None):
+    p = p or params()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    sizes = np.zeros(2 * p.nlevels, np.int32)
+    cap = w * h * 4
+    out = np.zeros(cap, np.uint8)
+    rc = lib().oracle_orb_pyramid(C.byref(p), _u8p(img), w, h, C.c_size_t(w), sizes.ctypes.data_as(C.c_void_p),
+                                  _u8p(out), C.c_size_t(cap))
+    assert rc == 0
+    levels, off = [], 0
+    for l in range(p.nlevels):
+        lw, lh = int(sizes[2 * l]), int(sizes[2 * l + 1])
+        levels.append(out[off:off + lw * lh].reshape(lh, lw).copy())
+        off += lw * lh
+    return levels
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    sh, sw = src.shape
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_linear(_u8p(src), sw, sh, C.c_size_t(sw), _u8p(dst), dw, dh)
+    return dst
+
+
+def fast(roi: np.ndarray, threshold: int) -> np.ndarray:
+    roi = np.ascontiguousarray(roi, dtype=np.uint8)
+    rows, cols = roi.shape
+    cap = rows * cols
+    out = np.zeros(max(cap, 1), np.uint32)
+    n = lib().oracle_fast(_u8p(roi), cols, rows, C.c_size_t(cols), threshold, out.ctypes.data_as(C.c_void_p), cap)
+    return out[:n].copy()
+
+
+def gaussian7(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape
+    dst = np.zeros_like(src)
+    lib().oracle_gaussian7(_u8p(src), w, h, _u8p(dst))
+    return dst
+
+
+def gaussian_taps():
+    t = np.zeros(7, np.int32)
+    lib().oracle_gaussian7_taps(t.ctypes.data_as(C.c_void_p))
+    return t
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return float(lib().oracle_fast_atan2(y, x))
+
+
+def sincos(a: float):
+    s, c = C.c_float(), C.c_float()
+    lib().oracle_sincos(C.c_float(a), C.byref(s), C.byref(c))
+    return s.value, c.value
+
+
+def level_stage(img: np.ndarray, level: int, p: OrbParams | None = None):
+    p = p or params()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = w * h
+    cand = np.zeros(cap, np.uint32)
+    kept = np.zeros(cap, np.uint32)
+    nc, nk = C.c_int(), C.c_int()
+    rc = lib().oracle_level_stage(C.byref(p), _u8p(img), w, h, C.c_size_t(w), level,
+                                  cand.ctypes.data_as(C.c_void_p), cap, C.byref(nc),
+                                  kept.ctypes.data_as(C.c_void_p), cap, C.byref(nk))
+    assert rc == 0
+    return cand[:nc.value].copy(), kept[:nk.value].copy()
+
+
+def distribute(cand: np.ndarray, minx, maxx, miny, maxy, n_keep) -> np.ndarray:
+    cand = np.ascontiguousarray(cand, dtype=np.uint32)
+    cap = max(len(cand), 1) + 8
+    out = np.zeros(cap, np.uint32)
+    m = lib().oracle_distribute(cand.ctypes.data_as(C.c_void_p), len(cand), minx, maxx, miny, maxy, n_keep,
+                                out.ctypes.data_as(C.c_void_p), cap)
+    return out[:m].copy()
+
+
+def std_sort_pairs(keys: np.ndarray, payload: np.ndarray):
+    k = np.ascontiguousarray(keys, dtype=np.uint32).copy()
+    v = np.ascontiguousarray(payload, dtype=np.uint32).copy()
+    lib().oracle_std_sort_pairs(k.ctypes.data_as(C.c_void_p), v.ctypes.data_as(C.c_void_p), len(k))
+    return k, v
+
+
+def unpack(packed: np.ndarray):
+    packed = np.asarray(packed, dtype=np.uint32)
+    return packed & 0xFFF, (packed >> 12) & 0xFFF, packed >> 24

@@ -1,0 +1,182 @@
+"""CPU: pin the oracle (oracle/orb_oracle.cpp) with hand-derived known answers.
+
+The reference ships no golden vectors for this path and cannot be built here, so the
+OpenCV-4.5.4 primitives are pinned by values derivable by hand from the reference source and the published
+algorithms; everything else is "parity unpinned" (DESIGN.md §Oracle).
+"""
+import ctypes
+import ctypes.util
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_constructor_tables(oracle):
+    scales, nfeat, umax = oracle.tables(oracle.params(1000))
+    # mnFeaturesPerLevel (ORBextractor.cc:434-445) — SURVEY.md §8 table
+    assert nfeat.tolist() == [217, 181, 151, 126, 105, 87, 73, 60]
+    assert oracle.tables(oracle.params(2000))[1].tolist() == [434, 362, 302, 251, 209, 175, 145, 122]
+    assert oracle.tables(oracle.params(700))[1].tolist() == [152, 127, 106, 88, 73, 61, 51, 42]
+    assert oracle.tables(oracle.params(1500))[1].tolist() == [326, 271, 226, 189, 157, 131, 109, 91]
+    assert oracle.tables(oracle.params(5000))[1].tolist() == [1086, 905, 754, 628, 524, 436, 364, 303]
+    # umax (ORBextractor.cc:453-468)
+    assert umax.tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+    # scale chain float(prev * (double)1.2f)
+    s = [1.0]
+    for _ in range(7):
+        s.append(float(np.float32(np.float64(np.float32(s[-1])) * np.float64(np.float32(1.2)))))
+    assert np.array_equal(scales[0], np.array(s, np.float32))
+    assert np.array_equal(scales[1], np.float32(1.0) / scales[0])
+
+
+def test_pyramid_sizes(oracle):
+    img = np.zeros((480, 640), np.uint8)
+    levels = oracle.pyramid(img)
+    assert [l.shape[::-1] for l in levels] == [(640, 480), (533, 400), (444, 333), (370, 278), (309, 231),
+                                               (257, 193), (214, 161), (179, 134)]
+    assert sum(l.size for l in levels) == 950532
+    img = np.zeros((720, 1280), np.uint8)
+    assert sum(l.size for l in oracle.pyramid(img)) == 2853088
+
+
+def test_gaussian_taps_and_impulse(oracle):
+    taps = oracle.gaussian_taps()
+    assert taps.tolist() == [18, 34, 48, 56, 48, 34, 18] and taps.sum() == 256
+    # error-diffusion construction of getGaussianKernelFixedPoint_ED, recomputed here
+    k = [math.exp(x * x * (-0.125 / 4.0)) for x in (-6, -4, -2)]
+    s = 2 * sum(k) + 1
+    err, ed = 0.0, []
+    for v in k:
+        adj = v / s * 256 + err
+        r = round(adj)
+        err = adj - r
+        ed.append(r)
+    assert ed == [18, 34, 48] and 256 - 2 * sum(ed) == 56
+    img = np.zeros((15, 15), np.uint8)
+    img[7, 7] = 255
+    out = oracle.gaussian7(img)
+    for y in range(15):
+        for x in range(15):
+            ky = taps[y - 4] if 4 <= y <= 10 else 0
+            kx = taps[x - 4] if 4 <= x <= 10 else 0
+            assert out[y, x] == (int(ky) * int(kx) * 255 + 32768) >> 16
+    const = np.full((20, 30), 77, np.uint8)
+    assert np.all(oracle.gaussian7(const) == 77)
+
+
+def test_fast_atan2(oracle):
+    assert oracle.fast_atan2(0.0, 1.0) == 0.0
+    assert oracle.fast_atan2(1.0, 0.0) == 90.0
+    assert oracle.fast_atan2(0.0, -1.0) == 180.0
+    assert oracle.fast_atan2(-1.0, 0.0) == 270.0
+    rng = np.random.default_rng(0)
+    for _ in range(2000):
+        y, x = rng.integers(-400000, 400000, 2)
+        if x == 0 and y == 0:
+            continue
+        ref = math.degrees(math.atan2(y, x)) % 360.0
+        got = oracle.fast_atan2(float(y), float(x))
+        d = abs(got - ref)
+        assert min(d, 360 - d) < 0.01, (y, x, got, ref)
+
+
+def _fast_bruteforce(roi, t):
+    """Textbook FAST-9/16 (segment test, cornerScore = max(t, best arc margin) - 1, strict 3x3 NMS inside the
+    detection band) — an independent statement of App. A.1 used to pin the oracle's OpenCV restatement."""
+    rows, cols = roi.shape
+    circ = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2),
+            (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+    score = np.zeros((rows, cols), np.int32)
+    corner = np.zeros((rows, cols), bool)
+    for i in range(3, rows - 3):
+        for j in range(3, cols - 3):
+            v = int(roi[i, j])
+            d = [v - int(roi[i + dy, j + dx]) for dx, dy in circ]
+            A = max(min(d[(s + k) % 16] for k in range(9)) for s in range(16))
+            B = max(min(-d[(s + k) % 16] for k in range(9)) for s in range(16))
+            if max(A, B) > t:
+                corner[i, j] = True
+                score[i, j] = max(t, A, B) - 1
+    out = []
+    for i in range(3, rows - 3):
+        for j in range(3, cols - 3):
+            if corner[i, j]:
+                s = score[i, j]
+                nb = score[i - 1:i + 2, j - 1:j + 2].copy()
+                nb[1, 1] = -1
+                if (s > nb).all():
+                    out.append(j | (i << 12) | (int(s) << 24))
+    return np.array(out, np.uint32)
+
+
+def test_fast_isolated_peak(oracle):
+    roi = np.zeros((9, 9), np.uint8)
+    roi[4, 4] = 100
+    got = oracle.fast(roi, 20)
+    assert got.tolist() == [4 | (4 << 12) | (99 << 24)]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fast_matches_definition(oracle, seed):
+    rng = np.random.default_rng(seed)
+    roi = rng.integers(0, 256, size=(24, 29)).astype(np.uint8)
+    if seed % 2:
+        from scipy.ndimage import uniform_filter
+
+        roi = uniform_filter(roi.astype(np.float32), 2).astype(np.uint8)
+    for t in (7, 20, 40):
+        assert np.array_equal(oracle.fast(roi, t), _fast_bruteforce(roi, t)), (seed, t)
+
+
+def test_distribute_reversed_list_order(oracle):
+    # one initial node over [0,100]^2 split once into 4 single-key children: push_front n1..n4 leaves the
+    # list [n4, n3, n2, n1] (ORBextractor.cc:626-671)
+    def pk(x, y, s):
+        return x | (y << 12) | (s << 24)
+
+    cand = np.array([pk(10, 10, 5), pk(60, 10, 7), pk(10, 60, 9), pk(60, 60, 1)], np.uint32)
+    out = oracle.distribute(cand, 0, 100, 0, 100, 4)
+    assert out.tolist() == [pk(60, 60, 1), pk(10, 60, 9), pk(60, 10, 7), pk(10, 10, 5)]
+    # retain best: two keys sharing the upper-left quadrant at N=1 -> the root split already gives
+    # size >= N, nodes keep their max-response key (first max wins)
+    cand = np.array([pk(10, 10, 5), pk(12, 11, 8), pk(13, 12, 8), pk(80, 80, 3)], np.uint32)
+    out = oracle.distribute(cand, 0, 100, 0, 100, 1)
+    assert out.tolist() == [pk(80, 80, 3), pk(12, 11, 8)]
+
+
+def test_device_introsort_matches_libstdcxx(tmp_path):
+    exe = tmp_path / "t"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), os.path.join(ROOT, "tests/cpp/test_introsort.cpp")],
+                   check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
+def test_det_sincos_correctly_rounded(oracle):
+    """det_sincos = (float)cos/sin of the float argument evaluated in double; compare with Python's libm
+    double cos/sin rounded once to float over the rBRIEF argument range [0, 2*pi)."""
+    rng = np.random.default_rng(1)
+    xs = np.float32(rng.uniform(0, 2 * np.pi, 20000))
+    bad = 0
+    for x in xs:
+        s, c = oracle.sincos(float(x))
+        if s != float(np.float32(math.sin(float(x)))) or c != float(np.float32(math.cos(float(x)))):
+            bad += 1
+    assert bad == 0
+
+
+def test_glibc_cosf_residual_is_small(oracle):
+    """Records the residual the trig policy leaves vs the reference's literal glibc cosf/sinf (informative;
+    DESIGN.md §Parity policy quotes the rate)."""
+    libm = ctypes.CDLL(ctypes.util.find_library("m"))
+    libm.cosf.restype = ctypes.c_float
+    libm.cosf.argtypes = [ctypes.c_float]
+    rng = np.random.default_rng(2)
+    xs = np.float32(rng.uniform(0, 2 * np.pi, 20000))
+    diff = sum(1 for x in xs if libm.cosf(float(x)) != oracle.sincos(float(x))[1])
+    assert diff / len(xs) < 0.05

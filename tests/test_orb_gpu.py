@@ -1,0 +1,126 @@
+"""GPU parity: the HIP ORB extractor (through the C-ABI) vs the CPU oracle, bit-exact.
+
+Stages are compared separately (pyramid, blurred levels, per-level FAST candidates) so a failure points at
+one kernel; the end-to-end check compares every keypoint field and every descriptor byte, in output order,
+plus the returned monoIndex (reference semantics: src/ORBextractor.cc:1086-1168).
+"""
+import numpy as np
+import pytest
+
+from mam3slam_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+# (w, h, nfeatures) — BASELINE.json configs (640x480/1000, 1280x720/2000), the testMultiAgentSystem YAML
+# (960x960, 700 features, test/settingsForTest_00.yaml:37) and the 5x init extractor (Tracking.cc:606).
+CASES = [(640, 480, 1000), (1280, 720, 2000), (960, 960, 700), (640, 480, 5000)]
+
+
+def _extractor(nfeat, desc_fma=False):
+    from mam3slam_amd import ORBextractor
+
+    return ORBextractor(nfeat, 1.2, 8, 20, 7, desc_fma=desc_fma)
+
+
+def _first_diff(a, b):
+    idx = np.nonzero(a != b)
+    return tuple(int(i[0]) for i in idx) if len(idx[0]) else None
+
+
+def _assert_kps_equal(kg, dg, mg, ko, do, mo, tag):
+    assert len(kg) == len(ko), f"{tag}: n {len(kg)} vs oracle {len(ko)}"
+    assert mg == mo, f"{tag}: monoIndex {mg} vs {mo}"
+    for f in ("x", "y", "size", "angle", "response", "octave", "class_id"):
+        a, b = kg[f], ko[f]
+        if f in ("x", "y", "size", "angle", "response"):
+            a, b = a.view(np.uint32), b.view(np.uint32)   # bit-exact floats
+        d = _first_diff(a, b)
+        assert d is None, f"{tag}: field {f} differs first at {d}: gpu={kg[d[0]]} oracle={ko[d[0]]}"
+    d = _first_diff(dg, do)
+    assert d is None, f"{tag}: descriptor differs first at {d}: gpu={dg[d[0]]} oracle={do[d[0]]} kp={ko[d[0]]}"
+
+
+@pytest.mark.parametrize("w,h,nfeat", CASES[:3])
+def test_pyramid_blur_candidates(gpu_lib, oracle, w, h, nfeat):
+    ext = _extractor(nfeat)
+    img = synth.make_frame(w, h, agent=1, frame=3)
+    ext(img)
+    p = oracle.params(nfeat)
+    levels = oracle.pyramid(img, p)
+    for l, lev in enumerate(levels):
+        g = ext.level(l)
+        d = _first_diff(g, lev)
+        assert d is None, f"level {l} pixel {d}: gpu={g[d]} oracle={lev[d]}"
+        gb = ext.debug_blurred(l)
+        ob = oracle.gaussian7(lev)
+        d = _first_diff(gb, ob)
+        assert d is None, f"blurred level {l} pixel {d}: gpu={gb[d]} oracle={ob[d]}"
+        cand_o, _ = oracle.level_stage(img, l, p)
+        cand_g = ext.debug_candidates(l)
+        assert len(cand_g) == len(cand_o), f"level {l}: {len(cand_g)} candidates vs oracle {len(cand_o)}"
+        d = _first_diff(cand_g, cand_o)
+        assert d is None, f"level {l} candidate {d}: gpu={oracle.unpack(cand_g[d])} oracle={oracle.unpack(cand_o[d])}"
+
+
+@pytest.mark.parametrize("w,h,nfeat", CASES)
+def test_extract_bit_exact(gpu_lib, oracle, w, h, nfeat):
+    ext = _extractor(nfeat)
+    p = oracle.params(nfeat)
+    for fr in range(2):
+        img = synth.make_frame(w, h, agent=0, frame=fr)
+        kg, dg, mg = ext(img)
+        ko, do, mo = oracle.extract(img, p)
+        _assert_kps_equal(kg, dg, mg, ko, do, mo, f"{w}x{h}/{nfeat} frame {fr}")
+
+
+def test_extract_desc_fma_policy(gpu_lib, oracle):
+    ext = _extractor(1000, desc_fma=True)
+    img = synth.make_frame(640, 480, agent=2, frame=5)
+    kg, dg, mg = ext(img)
+    ko, do, mo = oracle.extract(img, oracle.params(1000, desc_fma=1))
+    _assert_kps_equal(kg, dg, mg, ko, do, mo, "desc_fma=1")
+
+
+def test_lapping_area_placement(gpu_lib, oracle):
+    ext = _extractor(1000)
+    img = synth.make_frame(640, 480, agent=3, frame=1)
+    for lap in [(0, 1000), (200, 400), (700, 900), (0, 0)]:
+        kg, dg, mg = ext(img, None, lap)
+        ko, do, mo = oracle.extract(img, oracle.params(1000), lap)
+        _assert_kps_equal(kg, dg, mg, ko, do, mo, f"lap {lap}")
+
+
+def test_batch_device_matches_single(gpu_lib, oracle):
+    import torch
+
+    from mam3slam_amd.orb import KP_DTYPE
+
+    w, h, F = 640, 480, 6
+    ext = _extractor(1000)
+    imgs = np.stack([synth.make_frame(w, h, agent=4, frame=i) for i in range(F)])
+    cap = ext.max_keypoints()
+    d_img = torch.from_numpy(imgs).cuda()
+    d_kps = torch.zeros((F, cap * 28), dtype=torch.uint8, device="cuda")
+    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.zeros((F, 2), dtype=torch.int32, device="cuda")
+    ext.extract_batch_device(d_img.data_ptr(), F, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                             d_cnt.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    cnt = d_cnt.cpu().numpy()
+    kps = d_kps.cpu().numpy().view(KP_DTYPE).reshape(F, cap)
+    desc = d_desc.cpu().numpy()
+    for i in range(F):
+        ko, do, mo = oracle.extract(imgs[i], oracle.params(1000))
+        n = int(cnt[i, 0])
+        _assert_kps_equal(kps[i, :n], desc[i, :n], int(cnt[i, 1]), ko, do, mo, f"batch frame {i}")
+
+
+def test_error_contract(gpu_lib):
+    from mam3slam_amd._lib import MAM_ERR_EMPTY
+
+    ext = _extractor(1000)
+    k, d, m = ext(np.zeros((0, 0), np.uint8))
+    assert m == MAM_ERR_EMPTY and len(k) == 0
+    # flat image: no corners at all -> zero keypoints, monoIndex 0
+    k, d, m = ext(np.full((480, 640), 128, np.uint8))
+    assert len(k) == 0 and m == 0
