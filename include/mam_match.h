@@ -1,0 +1,163 @@
+/*
+ * mam_match.h — C-ABI drop-in boundary for MAM3SLAM's ORBmatcher hot-path searches (gfx950 / MI355X).
+ *
+ * Replaces (mono agents, Pinhole camera):
+ *   ORBmatcher::DescriptorDistance(a, b)                          reference: src/ORBmatcher.cc:2058-2074
+ *   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
+ *                                                                 reference: src/ORBmatcher.cc:43-213, 215-221
+ *   ORBmatcher::SearchByProjection(Frame& Cur, const Frame& Last, th, bMono)
+ *                                                                 reference: src/ORBmatcher.cc:1676-1887, 2012-2053
+ *   ORBmatcher::SearchForTriangulation(KF1, KF2, vMatchedPairs, bOnlyStereo=false, bCoarse)
+ *                                                                 reference: src/ORBmatcher.cc:907-1146
+ *   with Frame::GetFeaturesInArea / PosInGrid / AssignFeaturesToGrid (src/Frame.cc:385-416, 657-735) built
+ *   on the device, and Pinhole::project / epipolarConstrain (src/CameraModels/Pinhole.cpp:35-41, 107-129).
+ *
+ * Pointers/objects of the reference become indices: a Frame's mvpMapPoints is passed as `taken` flags
+ * (1 = slot holds a MapPoint with Observations() > 0, the only property the searches read) and results come
+ * back as per-keypoint indices of the matched MapPoint / last-frame keypoint (-1 = untouched). The
+ * ORBmatcher wrapper (mam3slam_amd/match.py) maps indices back to objects.
+ *
+ * Every search exists in two forms: a synchronous host-pointer call with the reference's one-frame
+ * semantics, and a batched device-pointer call (many frames / keyframe pairs per launch, asynchronous on a
+ * stream) used by the multi-agent harness and bench.py.
+ */
+#ifndef MAM_MATCH_H
+#define MAM_MATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mam_orb.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAM_GRID_COLS 64 /* FRAME_GRID_COLS, include/Frame.h */
+#define MAM_GRID_ROWS 48 /* FRAME_GRID_ROWS */
+#define MAM_TH_HIGH 100
+#define MAM_TH_LOW 50
+#define MAM_HISTO_LENGTH 30
+
+/* Frame-level geometry shared by every frame of a call (one agent = one camera). */
+typedef struct mam_frame_geom {
+    float min_x, max_x, min_y, max_y;   /* mnMinX.. (Frame.cc:782-809) */
+    float grid_inv_w, grid_inv_h;       /* mfGridElementWidthInv / HeightInv (Frame.cc:341-342) */
+    int32_t nlevels;
+    float scale_factors[MAM_MAX_LEVELS];/* mvScaleFactors */
+    float level_sigma2[MAM_MAX_LEVELS]; /* mvLevelSigma2 */
+} mam_frame_geom;
+
+/* MapPoint fields SearchByProjection(F, vpMapPoints) reads (ORBmatcher.cc:49-90), filled by
+ * Frame::isInFrustum (Frame.cc:512-586). 64 bytes. */
+typedef struct mam_mp_track {
+    float proj_x, proj_y;     /* mTrackProjX / mTrackProjY */
+    float view_cos;           /* mTrackViewCos */
+    float track_depth;        /* mTrackDepth */
+    int32_t track_in_view;    /* mbTrackInView */
+    int32_t scale_level;      /* mnTrackScaleLevel */
+    int32_t is_bad;           /* isBad() */
+    int32_t nobs;             /* Observations() */
+    uint8_t desc[32];         /* GetDescriptor() */
+} mam_mp_track;
+
+/* Sophus::SE3f as stored: unit quaternion (x, y, z, w) + translation. */
+typedef struct mam_pose {
+    float q[4];
+    float t[3];
+} mam_pose;
+
+/* Pinhole intrinsics (GeometricCamera::mvParameters, float). */
+typedef struct mam_pinhole {
+    float fx, fy, cx, cy;
+} mam_pinhole;
+
+/* Last-frame entry for SearchByProjection(Cur, Last) (ORBmatcher.cc:1695-1712). 48 bytes. */
+typedef struct mam_last_entry {
+    float pos[3];             /* pMP->GetWorldPos() */
+    float angle;              /* LastFrame.mvKeysUn[i].angle */
+    int32_t octave;           /* LastFrame.mvKeys[i].octave */
+    int32_t valid;            /* mvpMapPoints[i] != NULL && !mvbOutlier[i] */
+    int32_t nobs;             /* pMP->Observations() */
+    int32_t pad;
+    uint8_t desc[32];         /* pMP->GetDescriptor() */
+} mam_last_entry;
+
+/* DBoW2::FeatureVector flattened: node ids ascending, node_off[n_nodes+1] into feats (feature indices). */
+typedef struct mam_featvec {
+    int32_t n_nodes;
+    const uint32_t* node_ids;
+    const int32_t* node_off;
+    const uint32_t* feats;
+} mam_featvec;
+
+typedef struct mam_match_ctx mam_match_ctx;
+
+int mam_match_create(int device, mam_match_ctx** out);
+void mam_match_destroy(mam_match_ctx* ctx);
+
+/* DescriptorDistance over n pairs (rows of a and b, 32 B each). Host pointers. */
+int mam_descriptor_distance(mam_match_ctx* ctx, const uint8_t* a, const uint8_t* b, int n, int32_t* out);
+
+/* SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints) with ORBmatcher(nnratio).
+ * F: n keypoints (mvKeysUn), descriptors n x 32, taken[n] (may be NULL).
+ * out_kp_to_mp[n]: index of the MapPoint assigned to keypoint i in this call, else -1.
+ * Returns nmatches (>= 0) or a negative MAM_ERR_*. */
+int mam_search_by_projection(mam_match_ctx* ctx, const mam_frame_geom* geom, int n, const mam_keypoint* keys,
+                             const uint8_t* desc, const uint8_t* taken, int n_mps, const mam_mp_track* mps,
+                             float th, int far_points, float th_far_points, float nnratio, int32_t* out_kp_to_mp);
+
+/* SearchByProjection(CurrentFrame, LastFrame, th, bMono) with ORBmatcher(nnratio, checkOri).
+ * out_kp_to_last[n_cur]: index i of the last-frame entry whose MapPoint was assigned, else -1 (after the
+ * rotation-consistency pass). tlw/mb are only read when !mono (bForward/bBackward, ORBmatcher.cc:1688-1692). */
+int mam_search_by_projection_motion(mam_match_ctx* ctx, const mam_frame_geom* geom, int n_cur,
+                                    const mam_keypoint* keys, const uint8_t* desc, const uint8_t* taken,
+                                    const mam_pose* tcw, const mam_pose* tlw, float mb, const mam_pinhole* cam,
+                                    int n_last, const mam_last_entry* last, float th, int mono, int check_ori,
+                                    int32_t* out_kp_to_last);
+
+/* SearchForTriangulation(KF1, KF2, pairs, bOnlyStereo=false, bCoarse) with ORBmatcher(nnratio, checkOri)
+ * for mono Pinhole keyframes. F12 (row-major 3x3, float) is the epipolarConstrain fundamental matrix
+ * K1^-T [t12]x R12 K2^-1 and ep the epipole of KF1's centre in KF2 — both per pair, computed by the
+ * wrapper. has_mp1/has_mp2: GetMapPoint(idx) != NULL. out_match12[n1]: idx2 or -1; returns nmatches. */
+int mam_search_for_triangulation(mam_match_ctx* ctx, const mam_frame_geom* geom, int n1, const mam_keypoint* keys1,
+                                 const uint8_t* desc1, const uint8_t* has_mp1, const mam_featvec* fv1, int n2,
+                                 const mam_keypoint* keys2, const uint8_t* desc2, const uint8_t* has_mp2,
+                                 const mam_featvec* fv2, const float* F12, const float* ep, int check_ori,
+                                 int coarse, int32_t* out_match12);
+
+/* ---- batched device-resident forms (asynchronous on `stream`; NULL = the context's stream) ---------- */
+
+/* A batch of frames laid out as the extractor's batched output: frame f's keypoints at
+ * keys + f*kp_stride, descriptors at desc + f*kp_stride*32, count counts[2f]. */
+typedef struct mam_frames_dev {
+    int32_t nframes;
+    int32_t kp_stride;
+    const mam_keypoint* keys;
+    const uint8_t* desc;
+    const int32_t* counts;
+    const uint8_t* taken;     /* [nframes][kp_stride] or NULL */
+} mam_frames_dev;
+
+/* Frame f matches n_mps[f] MapPoints at mps + f*mp_stride. Outputs at out_kp_to_mp + f*kp_stride and
+ * out_nmatches[f]. */
+int mam_search_by_projection_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_frames_dev* frames,
+                                          const mam_mp_track* mps, int mp_stride, const int32_t* n_mps, float th,
+                                          int far_points, float th_far_points, float nnratio,
+                                          int32_t* out_kp_to_mp, int32_t* out_nmatches, void* stream);
+
+/* Frame f (current) matches n_last[f] last-frame entries at last + f*last_stride with pose tcw[f]. */
+int mam_search_by_projection_motion_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom,
+                                                 const mam_frames_dev* frames, const mam_pose* tcw,
+                                                 const mam_pinhole* cam, const mam_last_entry* last, int last_stride,
+                                                 const int32_t* n_last, float th, int check_ori,
+                                                 int32_t* out_kp_to_last, int32_t* out_nmatches, void* stream);
+
+int mam_match_set_profiling(mam_match_ctx* ctx, int enable);
+/* ms_out/launches_out: [0] grid build, [1] candidate gather, [2] greedy resolve, [3] triangulation. */
+int mam_match_stage_times(mam_match_ctx* ctx, double* ms_out, int64_t* launches_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAM_MATCH_H */

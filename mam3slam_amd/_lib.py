@@ -53,6 +53,12 @@ SIGNATURES = {
 }
 
 
+def _match_sigs():
+    from .match import _SIGS
+
+    return _SIGS
+
+
 def lib() -> C.CDLL:
     """Load libmam_gpu.so (building it first if a hipcc is present and the .so is stale/missing)."""
     global _lib
@@ -65,7 +71,7 @@ def lib() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise MamError(f"HIP library {LIB_PATH} missing: run `python -m mam3slam_amd.build`")
     L = C.CDLL(LIB_PATH)
-    for name, (res, args) in SIGNATURES.items():
+    for name, (res, args) in all_signatures().items():
         fn = getattr(L, name, None)
         if fn is None:
             continue
@@ -73,6 +79,12 @@ def lib() -> C.CDLL:
         fn.argtypes = args
     _lib = L
     return L
+
+
+def all_signatures() -> dict:
+    d = dict(SIGNATURES)
+    d.update(_match_sigs())
+    return d
 
 
 def check(rc: int, what: str) -> int:

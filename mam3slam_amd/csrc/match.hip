@@ -1,0 +1,979 @@
+// match.hip — gfx950 ORBmatcher hot-path searches + C-ABI (include/mam_match.h).
+//
+// Reference semantics (mono, Pinhole):
+//   SearchByProjection(F, vpMapPoints)   src/ORBmatcher.cc:43-213   (greedy: a keypoint taken by an earlier
+//                                        MapPoint of the same call is skipped by later ones, :88-90)
+//   SearchByProjection(Cur, Last)        src/ORBmatcher.cc:1676-1887 + rotation histogram :1855-1884
+//   SearchForTriangulation               src/ORBmatcher.cc:907-1146 (per idx1 independent; last equal wins)
+//   Frame grid / GetFeaturesInArea       src/Frame.cc:385-416, 657-735
+//
+// Stages (one launch each, batched over frames):
+//   k_grid     per frame: PosInGrid for every keypoint, LDS bitonic sort of (cell, idx) -> cell-major index
+//              list with ascending idx per cell = AssignFeaturesToGrid's cell vectors.
+//   k_gather   one wave per search unit (MapPoint / last-frame entry): window cells enumerated ix -> iy -> cell
+//              order exactly as GetFeaturesInArea, level + radius filters, Hamming distance (4x popcount64);
+//              COUNT pass, per-frame scan, FILL pass into a per-frame candidate pool (entry = idx | dist<<16 |
+//              level<<25, in enumeration order).
+//   k_resolve  per frame, one wave: the reference's sequential greedy loop replayed exactly but 64 units at a
+//              time — each lane resolves one unit against the taken-set at chunk start; lanes whose candidate
+//              set contains a keypoint picked by an earlier lane of the chunk are re-run after the earlier
+//              lanes commit (progress: the first open lane never conflicts). Then the rotation-histogram pass.
+//   k_tri      SearchForTriangulation: one wave per idx1 of each shared vocabulary node; wave argmin on
+//              (dist, -position) implements "dist <= bestDist, last equal wins".
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/mam_match.h"
+#include "runtime.hpp"
+
+namespace mam {
+
+constexpr int NCELLS = MAM_GRID_COLS * MAM_GRID_ROWS;
+constexpr int GRID_SORT_MAX = 8192;   // keypoints per frame the grid sort handles (LDS 32 KB)
+
+struct ProjArgs {
+    mam_frame_geom g;
+    mam_frames_dev fr;
+    int mode;                 // 0: local MapPoints, 1: last frame (motion model)
+    int unit_stride;          // mp_stride / last_stride
+    const int32_t* n_units;   // per frame
+    // mode 0
+    const mam_mp_track* mps;
+    float th, th_far, nnratio;
+    int far_points;
+    // mode 1
+    const mam_pose* tcw;
+    mam_pinhole cam;
+    const mam_last_entry* last;
+    int check_ori;
+    // scratch
+    uint16_t* grid_idx;       // [F][kp_stride]
+    int32_t* grid_start;      // [F][NCELLS+1]
+    int32_t* cand_cnt;        // [F][unit_stride]
+    int32_t* cand_off;        // [F][unit_stride]
+    uint32_t* pool;           // [F][pool_per_frame]
+    int32_t* pool_total;      // [F]
+    int pool_per_frame;
+    uint32_t* events;         // [F][unit_stride]
+    int32_t* out;             // [F][kp_stride]
+    int32_t* out_n;           // [F]
+};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ int desc_dist(const uint8_t* a, const uint8_t* b) {
+    const uint4 a0 = reinterpret_cast<const uint4*>(a)[0], a1 = reinterpret_cast<const uint4*>(a)[1];
+    const uint4 b0 = reinterpret_cast<const uint4*>(b)[0], b1 = reinterpret_cast<const uint4*>(b)[1];
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+__device__ __forceinline__ int frame_n(const mam_frames_dev& fr, int f) {
+    int n = fr.counts[2 * f];
+    return n < 0 ? 0 : (n > fr.kp_stride ? fr.kp_stride : n);
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ unsigned wave_minu(unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------ grid
+__global__ __launch_bounds__(256) void k_grid(ProjArgs p) {
+    __shared__ uint32_t keys[GRID_SORT_MAX];
+    __shared__ int32_t start[NCELLS + 1];
+    __shared__ int red[4];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = frame_n(p.fr, f);
+    if (n > GRID_SORT_MAX) {
+        if (tid == 0) p.out_n[f] = MAM_ERR_CAPACITY;
+        return;
+    }
+    int P = 2;
+    while (P < n) P <<= 1;
+    const mam_keypoint* K = p.fr.keys + (size_t)f * p.fr.kp_stride;
+    int nvalid = 0;
+    for (int i = tid; i < P; i += 256) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (i < n) {
+            // PosInGrid (Frame.cc:725-735): std::round (half away from zero)
+            const int posX = (int)roundf((K[i].x - p.g.min_x) * p.g.grid_inv_w);
+            const int posY = (int)roundf((K[i].y - p.g.min_y) * p.g.grid_inv_h);
+            if (!(posX < 0 || posX >= MAM_GRID_COLS || posY < 0 || posY >= MAM_GRID_ROWS)) {
+                key = ((uint32_t)(posX * MAM_GRID_ROWS + posY) << 16) | (uint32_t)i;
+                nvalid++;
+            }
+        }
+        keys[i] = key;
+    }
+    nvalid = wave_sum(nvalid);
+    if (lane_id() == 0) red[tid >> 6] = nvalid;
+    __syncthreads();
+    const int nv = red[0] + red[1] + red[2] + red[3];
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < P; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t a = keys[i], b = keys[ixj];
+                    const bool asc = (i & k) == 0;
+                    if ((a > b) == asc) { keys[i] = b; keys[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int c = tid; c <= NCELLS; c += 256) start[c] = nv;
+    __syncthreads();
+    for (int i = tid; i < nv; i += 256) {
+        const int cell = (int)(keys[i] >> 16);
+        const int prev = i ? (int)(keys[i - 1] >> 16) : -1;
+        for (int c = prev + 1; c <= cell; c++) start[c] = i;
+    }
+    __syncthreads();
+    int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
+    for (int c = tid; c <= NCELLS; c += 256) gs[c] = start[c];
+    uint16_t* gi = p.grid_idx + (size_t)f * p.fr.kp_stride;
+    for (int i = tid; i < nv; i += 256) gi[i] = (uint16_t)(keys[i] & 0xFFFFu);
+}
+
+// ------------------------------------------------------------------------------------------------ gather
+struct Window {
+    float x, y, r;
+    int minL, maxL;
+    bool checkL;
+    int cx0, cx1, cy0, cy1;
+    const uint8_t* desc;
+};
+
+// Search window of unit j of frame f; false = the reference `continue`s before or inside GetFeaturesInArea.
+__device__ bool unit_window(const ProjArgs& p, int f, int j, Window* w) {
+    if (j >= p.n_units[f]) return false;
+    if (p.mode == 0) {
+        const mam_mp_track& mp = p.mps[(size_t)f * p.unit_stride + j];
+        if (!mp.track_in_view) return false;
+        if (p.far_points && mp.track_depth > p.th_far) return false;
+        if (mp.is_bad) return false;
+        const int lvl = mp.scale_level;
+        float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos (ORBmatcher.cc:215-221)
+        if (p.th != 1.0f) r *= p.th;
+        w->x = mp.proj_x;
+        w->y = mp.proj_y;
+        w->r = r * p.g.scale_factors[lvl];
+        w->minL = lvl - 1;
+        w->maxL = lvl;
+        w->desc = mp.desc;
+    } else {
+        const mam_last_entry& L = p.last[(size_t)f * p.unit_stride + j];
+        if (!L.valid) return false;
+        const mam_pose& T = p.tcw[f];
+        // Sophus SE3f action (so3.hpp:358-367, se3.hpp:321-324), evaluated as written
+        const float qx = T.q[0], qy = T.q[1], qz = T.q[2], qw = T.q[3];
+        const float px = L.pos[0], py = L.pos[1], pz = L.pos[2];
+        float u0 = qy * pz - qz * py, u1 = qz * px - qx * pz, u2 = qx * py - qy * px;
+        u0 += u0; u1 += u1; u2 += u2;
+        const float c0 = qy * u2 - qz * u1, c1 = qz * u0 - qx * u2, c2 = qx * u1 - qy * u0;
+        const float xc = ((px + qw * u0) + c0) + T.t[0];
+        const float yc = ((py + qw * u1) + c1) + T.t[1];
+        const float zc = ((pz + qw * u2) + c2) + T.t[2];
+        const float invzc = (float)(1.0 / (double)zc);
+        if (invzc < 0) return false;
+        const float u = p.cam.fx * xc / zc + p.cam.cx;   // Pinhole::project (Pinhole.cpp:35-41)
+        const float v = p.cam.fy * yc / zc + p.cam.cy;
+        if (u < p.g.min_x || u > p.g.max_x) return false;
+        if (v < p.g.min_y || v > p.g.max_y) return false;
+        w->x = u;
+        w->y = v;
+        w->r = p.th * p.g.scale_factors[L.octave];
+        w->minL = L.octave - 1;
+        w->maxL = L.octave + 1;
+        w->desc = L.desc;
+    }
+    // GetFeaturesInArea cell range (Frame.cc:657-683)
+    const float r = w->r;
+    w->cx0 = max(0, (int)floorf((w->x - p.g.min_x - r) * p.g.grid_inv_w));
+    if (w->cx0 >= MAM_GRID_COLS) return false;
+    w->cx1 = min(MAM_GRID_COLS - 1, (int)ceilf((w->x - p.g.min_x + r) * p.g.grid_inv_w));
+    if (w->cx1 < 0) return false;
+    w->cy0 = max(0, (int)floorf((w->y - p.g.min_y - r) * p.g.grid_inv_h));
+    if (w->cy0 >= MAM_GRID_ROWS) return false;
+    w->cy1 = min(MAM_GRID_ROWS - 1, (int)ceilf((w->y - p.g.min_y + r) * p.g.grid_inv_h));
+    if (w->cy1 < 0) return false;
+    w->checkL = (w->minL > 0) || (w->maxL >= 0);
+    return true;
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
+    const long long gw = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int f = (int)(gw / p.unit_stride);
+    const int j = (int)(gw - (long long)f * p.unit_stride);
+    if (f >= nframes) return;
+    const int lane = lane_id();
+    Window w;
+    const bool ok = unit_window(p, f, j, &w);
+    if (!ok) {
+        if (!FILL && lane == 0) p.cand_cnt[(size_t)f * p.unit_stride + j] = 0;
+        return;
+    }
+    if (FILL && p.pool_total[f] > p.pool_per_frame) return;
+    const int ny = w.cy1 - w.cy0 + 1;
+    const int ncell = (w.cx1 - w.cx0 + 1) * ny;
+    const int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
+    const uint16_t* gi = p.grid_idx + (size_t)f * p.fr.kp_stride;
+    const mam_keypoint* K = p.fr.keys + (size_t)f * p.fr.kp_stride;
+    const uint8_t* D = p.fr.desc + (size_t)f * p.fr.kp_stride * 32;
+    uint32_t* pool = p.pool + (size_t)f * p.pool_per_frame;
+    int base = FILL ? p.cand_off[(size_t)f * p.unit_stride + j] : 0;
+    int total = 0;
+    for (int e0 = 0; e0 < ncell; e0 += 64) {
+        const int e = e0 + lane;
+        int cnt = 0, k0 = 0, k1 = 0;
+        if (e < ncell) {
+            const int ix = w.cx0 + e / ny, iy = w.cy0 + e % ny;
+            const int cell = ix * MAM_GRID_ROWS + iy;
+            k0 = gs[cell];
+            k1 = gs[cell + 1];
+            for (int k = k0; k < k1; k++) {
+                const int idx = gi[k];
+                const mam_keypoint& kp = K[idx];
+                if (w.checkL) {
+                    if (kp.octave < w.minL) continue;
+                    if (w.maxL >= 0 && kp.octave > w.maxL) continue;
+                }
+                const float dx = kp.x - w.x, dy = kp.y - w.y;
+                if (fabsf(dx) < w.r && fabsf(dy) < w.r) cnt++;
+            }
+        }
+        if (FILL) {
+            const int incl = wave_incl_scan(cnt);
+            int o = base + incl - cnt;
+            if (cnt > 0) {
+                for (int k = k0; k < k1; k++) {
+                    const int idx = gi[k];
+                    const mam_keypoint& kp = K[idx];
+                    if (w.checkL) {
+                        if (kp.octave < w.minL) continue;
+                        if (w.maxL >= 0 && kp.octave > w.maxL) continue;
+                    }
+                    const float dx = kp.x - w.x, dy = kp.y - w.y;
+                    if (fabsf(dx) < w.r && fabsf(dy) < w.r) {
+                        const int dist = desc_dist(w.desc, D + (size_t)idx * 32);
+                        pool[o++] = (uint32_t)idx | ((uint32_t)dist << 16) | ((uint32_t)kp.octave << 25);
+                    }
+                }
+            }
+            base += __shfl(incl, 63, 64);
+        } else {
+            total += wave_sum(cnt);
+        }
+    }
+    if (!FILL && lane == 0) p.cand_cnt[(size_t)f * p.unit_stride + j] = total;
+}
+
+__global__ __launch_bounds__(256) void k_scan(ProjArgs p) {
+    __shared__ int scr[4];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int nu = p.n_units[f];
+    const int32_t* cc = p.cand_cnt + (size_t)f * p.unit_stride;
+    int32_t* co = p.cand_off + (size_t)f * p.unit_stride;
+    int carry = 0;
+    for (int j0 = 0; j0 < nu; j0 += 256) {
+        const int j = j0 + tid;
+        const int v = j < nu ? cc[j] : 0;
+        const int incl = wave_incl_scan(v);
+        if (lane_id() == 63) scr[tid >> 6] = incl;
+        __syncthreads();
+        int pre = 0, tot = 0;
+        for (int i = 0; i < 4; i++) {
+            if (i < (tid >> 6)) pre += scr[i];
+            tot += scr[i];
+        }
+        __syncthreads();
+        if (j < nu) co[j] = carry + pre + incl - v;
+        carry += tot;
+    }
+    if (tid == 0) p.pool_total[f] = carry;
+}
+
+// ------------------------------------------------------------------------------------------------ resolve
+__device__ __forceinline__ int rot_bin(float rot) {
+    const float factor = 1.0f / MAM_HISTO_LENGTH;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == MAM_HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+__global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int S = p.fr.kp_stride;
+    const int nwords = (S + 31) / 32;
+    uint32_t* takenb = reinterpret_cast<uint32_t*>(smem);              // S bits
+    int* picked = reinterpret_cast<int*>(smem + ((nwords * 4 + 15) & ~15));  // lowest open lane taking idx (64 = none)
+    int* writer = picked + ((S + 3) & ~3);                                // highest committing lane writing idx
+    __shared__ int hist[MAM_HISTO_LENGTH];
+    __shared__ int top[3];
+    const int n = frame_n(p.fr, f);
+    int32_t* out = p.out + (size_t)f * S;
+    if (p.out_n[f] < 0) return;   // grid stage flagged this frame
+    if (p.pool_total[f] > p.pool_per_frame) {
+        if (lane == 0) p.out_n[f] = MAM_ERR_CAPACITY;
+        return;
+    }
+    for (int i = lane; i < n; i += 64) out[i] = -1;
+    for (int w = lane; w < nwords; w += 64) {
+        uint32_t bits = 0;
+        if (p.fr.taken)
+            for (int b = 0; b < 32; b++) {
+                const int i = w * 32 + b;
+                if (i < n && p.fr.taken[(size_t)f * S + i]) bits |= 1u << b;
+            }
+        takenb[w] = bits;
+    }
+    for (int i = lane; i < S; i += 64) { picked[i] = 64; writer[i] = -1; }
+    if (lane < MAM_HISTO_LENGTH) hist[lane] = 0;
+    __syncthreads();
+    const int nu = p.n_units[f];
+    const uint32_t* pool = p.pool + (size_t)f * p.pool_per_frame;
+    const int32_t* cc = p.cand_cnt + (size_t)f * p.unit_stride;
+    const int32_t* co = p.cand_off + (size_t)f * p.unit_stride;
+    uint32_t* ev = p.events + (size_t)f * p.unit_stride;
+    const mam_keypoint* K = p.fr.keys + (size_t)f * S;
+    int nm = 0, nev = 0;
+    for (int j0 = 0; j0 < nu; j0 += 64) {
+        const int j = j0 + lane;
+        const bool active = j < nu;
+        const int cnt = active ? cc[j] : 0;
+        const int off = active ? co[j] : 0;
+        int nobs = 0;
+        float lang = 0.f;
+        if (active) {
+            if (p.mode == 0) {
+                nobs = p.mps[(size_t)f * p.unit_stride + j].nobs;
+            } else {
+                nobs = p.last[(size_t)f * p.unit_stride + j].nobs;
+                lang = p.last[(size_t)f * p.unit_stride + j].angle;
+            }
+        }
+        bool done = !active || cnt == 0;
+        while (__any(!done)) {
+            // (1) each open lane replays the reference's candidate loop against the taken-set
+            //     (ORBmatcher.cc:84-128 for mode 0, :1745-1772 for mode 1)
+            bool assign = false;
+            int bestIdx = -1;
+            if (!done) {
+                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1;
+                for (int t = 0; t < cnt; t++) {
+                    const uint32_t e = pool[off + t];
+                    const int idx = (int)(e & 0xFFFFu);
+                    if ((takenb[idx >> 5] >> (idx & 31)) & 1u) continue;
+                    const int dist = (int)((e >> 16) & 0x1FFu);
+                    const int lvl = (int)(e >> 25);
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist; bestDist = dist;
+                        bestLevel2 = bestLevel; bestLevel = lvl;
+                        bestIdx = idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = lvl;
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist <= MAM_TH_HIGH) {
+                    assign = true;
+                    if (p.mode == 0 && bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) assign = false;
+                }
+            }
+            // (2) picks that grow the taken-set; the first open lane whose candidate list holds a keypoint
+            //     picked by an EARLIER open lane is stale, lanes before it are final
+            const bool takes = !done && assign && nobs > 0;
+            if (takes) atomicMin(&picked[bestIdx], lane);
+            __syncthreads();
+            bool stale = false;
+            if (!done) {
+                for (int t = 0; t < cnt && !stale; t++) {
+                    const int idx = (int)(pool[off + t] & 0xFFFFu);
+                    if (picked[idx] < lane) stale = true;
+                }
+            }
+            const int jstar = wave_min(stale ? lane : 64);
+            __syncthreads();
+            if (takes) picked[bestIdx] = 64;
+            // (3) commit lanes < jstar in lane order: out[] last writer wins, taken bits, counts, events
+            const bool commit = !done && lane < jstar;
+            const bool cassign = commit && assign;
+            if (cassign) atomicMax(&writer[bestIdx], lane);
+            __syncthreads();
+            if (cassign) {
+                if (writer[bestIdx] == lane) out[bestIdx] = j;
+                if (nobs > 0) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
+            }
+            nm += wave_sum(cassign ? 1 : 0);
+            if (p.mode == 1 && p.check_ori) {
+                const int incl = wave_incl_scan(cassign ? 1 : 0);
+                if (cassign) {
+                    const int bin = rot_bin(lang - K[bestIdx].angle);
+                    ev[nev + incl - 1] = (uint32_t)bestIdx | ((uint32_t)bin << 16);
+                }
+                nev += __shfl(incl, 63, 64);
+            }
+            __syncthreads();
+            if (cassign) writer[bestIdx] = -1;
+            done = done || commit;
+            __syncthreads();
+        }
+    }
+    // (4) rotation consistency (ORBmatcher.cc:1855-1884, ComputeThreeMaxima :2012-2053)
+    if (p.mode == 1 && p.check_ori) {
+        for (int e = lane; e < nev; e += 64) atomicAdd(&hist[ev[e] >> 16], 1);
+        __syncthreads();
+        if (lane == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < MAM_HISTO_LENGTH; i++) {
+                const int s = hist[i];
+                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+                else if (s > max3) { max3 = s; ind3 = i; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            top[0] = ind1; top[1] = ind2; top[2] = ind3;
+        }
+        __syncthreads();
+        int removed = 0;
+        for (int e = lane; e < nev; e += 64) {
+            const int bin = (int)(ev[e] >> 16);
+            if (bin != top[0] && bin != top[1] && bin != top[2]) {
+                out[ev[e] & 0xFFFFu] = -1;
+                removed++;
+            }
+        }
+        nm -= wave_sum(removed);
+    }
+    if (lane == 0) p.out_n[f] = nm;
+}
+
+// ------------------------------------------------------------------------------------------------ triangulation
+struct TriArgs {
+    mam_frame_geom g;
+    const mam_keypoint* keys1;
+    const uint8_t* desc1;
+    const uint8_t* has1;
+    const mam_keypoint* keys2;
+    const uint8_t* desc2;
+    const uint8_t* has2;
+    const uint32_t* feats1;
+    const uint32_t* feats2;
+    const int32_t* work;      // per work item: position in feats1
+    const int32_t* work_n2;   // per work item: [begin, end) in feats2 (2 ints)
+    int nwork;
+    float F[9];
+    float ep[2];
+    int coarse;
+    int32_t* out;             // [n1]
+};
+
+__global__ __launch_bounds__(256) void k_tri(TriArgs a) {
+    const int gw = (int)(((long long)blockIdx.x * 256 + threadIdx.x) >> 6);
+    if (gw >= a.nwork) return;
+    const int lane = lane_id();
+    const uint32_t idx1 = a.feats1[a.work[gw]];
+    if (a.has1[idx1]) return;
+    const mam_keypoint kp1 = a.keys1[idx1];
+    const uint8_t* d1 = a.desc1 + (size_t)idx1 * 32;
+    const int b = a.work_n2[2 * gw], e = a.work_n2[2 * gw + 1];
+    // epipolar line of kp1 in image 2 (Pinhole::epipolarConstrain, Pinhole.cpp:114-117)
+    const float la = kp1.x * a.F[0] + kp1.y * a.F[3] + a.F[6];
+    const float lb = kp1.x * a.F[1] + kp1.y * a.F[4] + a.F[7];
+    const float lc = kp1.x * a.F[2] + kp1.y * a.F[5] + a.F[8];
+    unsigned best = 0xFFFFFFFFu;   // (dist << 16) | (0xFFFF - position): min = smallest dist, LAST position
+    for (int i0 = b; i0 < e; i0 += 64) {
+        const int i2 = i0 + lane;
+        if (i2 < e) {
+            const uint32_t idx2 = a.feats2[i2];
+            if (!a.has2[idx2]) {
+                const int dist = desc_dist(d1, a.desc2 + (size_t)idx2 * 32);
+                if (dist <= MAM_TH_LOW) {
+                    const mam_keypoint kp2 = a.keys2[idx2];
+                    const float distex = a.ep[0] - kp2.x;
+                    const float distey = a.ep[1] - kp2.y;
+                    if (!(distex * distex + distey * distey < 100 * a.g.scale_factors[kp2.octave])) {
+                        bool ok = a.coarse != 0;
+                        if (!ok) {
+                            const float num = la * kp2.x + lb * kp2.y + lc;
+                            const float den = la * la + lb * lb;
+                            if (den != 0) {
+                                const float dsqr = num * num / den;
+                                ok = dsqr < 3.84 * a.g.level_sigma2[kp2.octave];
+                            }
+                        }
+                        if (ok) best = min(best, ((unsigned)dist << 16) | (0xFFFFu - (unsigned)(i2 - b)));
+                    }
+                }
+            }
+        }
+    }
+    best = wave_minu(best);
+    if (lane == 0 && best != 0xFFFFFFFFu) a.out[idx1] = (int32_t)a.feats2[b + (int)(0xFFFFu - (best & 0xFFFFu))];
+}
+
+__global__ __launch_bounds__(256) void k_tri_rot(const mam_keypoint* keys1, const mam_keypoint* keys2, int n1,
+                                                  int check_ori, int32_t* out, int32_t* nmatch) {
+    __shared__ int hist[MAM_HISTO_LENGTH];
+    __shared__ int top[3];
+    __shared__ int red[4];
+    const int tid = threadIdx.x;
+    if (tid < MAM_HISTO_LENGTH) hist[tid] = 0;
+    __syncthreads();
+    int cnt = 0;
+    for (int i = tid; i < n1; i += 256) {
+        if (out[i] >= 0) {
+            cnt++;
+            if (check_ori) atomicAdd(&hist[rot_bin(keys1[i].angle - keys2[out[i]].angle)], 1);
+        }
+    }
+    __syncthreads();
+    if (check_ori) {
+        if (tid == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < MAM_HISTO_LENGTH; i++) {
+                const int s = hist[i];
+                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+                else if (s > max3) { max3 = s; ind3 = i; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            top[0] = ind1; top[1] = ind2; top[2] = ind3;
+        }
+        __syncthreads();
+        for (int i = tid; i < n1; i += 256) {
+            if (out[i] >= 0) {
+                const int bin = rot_bin(keys1[i].angle - keys2[out[i]].angle);
+                if (bin != top[0] && bin != top[1] && bin != top[2]) { out[i] = -1; cnt--; }
+            }
+        }
+    }
+    cnt = wave_sum(cnt);
+    if (lane_id() == 0) red[tid >> 6] = cnt;
+    __syncthreads();
+    if (tid == 0) *nmatch = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = desc_dist(a + (size_t)i * 32, b + (size_t)i * 32);
+}
+
+}  // namespace mam
+
+// ==================================================================================================== host
+using mam::DevBuf;
+
+struct mam_match_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    mam::StageTimer timer{4};
+    int pool_per_unit = 96;
+    // scratch
+    DevBuf<uint16_t> grid_idx;
+    DevBuf<int32_t> grid_start, cand_cnt, cand_off, pool_total, out_n_tmp;
+    DevBuf<uint32_t> pool, events;
+    // host-API staging
+    DevBuf<uint8_t> stage;
+};
+
+namespace {
+
+template <typename T>
+T* carve(uint8_t*& p, size_t count) {
+    T* r = reinterpret_cast<T*>(p);
+    p += (count * sizeof(T) + 255) & ~(size_t)255;
+    return r;
+}
+
+size_t carve_bytes(size_t count, size_t elem) { return (count * elem + 255) & ~(size_t)255; }
+
+int ensure_scratch(mam_match_ctx* c, int F, int kp_stride, int unit_stride, int pool_per_frame) {
+    if (int rc = c->grid_idx.alloc((size_t)F * kp_stride)) return rc;
+    if (int rc = c->grid_start.alloc((size_t)F * (mam::NCELLS + 1))) return rc;
+    if (int rc = c->cand_cnt.alloc((size_t)F * unit_stride)) return rc;
+    if (int rc = c->cand_off.alloc((size_t)F * unit_stride)) return rc;
+    if (int rc = c->pool_total.alloc(F)) return rc;
+    if (int rc = c->pool.alloc((size_t)F * pool_per_frame)) return rc;
+    if (int rc = c->events.alloc((size_t)F * unit_stride)) return rc;
+    return MAM_OK;
+}
+
+// Shared launcher for both projection searches.
+int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) {
+    if (F <= 0) return MAM_OK;
+    if (a.fr.kp_stride > mam::GRID_SORT_MAX || a.fr.kp_stride <= 0 || a.unit_stride <= 0) return MAM_ERR_ARG;
+    if (int rc = ensure_scratch(c, F, a.fr.kp_stride, a.unit_stride, a.pool_per_frame)) return rc;
+    a.grid_idx = c->grid_idx.p;
+    a.grid_start = c->grid_start.p;
+    a.cand_cnt = c->cand_cnt.p;
+    a.cand_off = c->cand_off.p;
+    a.pool = c->pool.p;
+    a.pool_total = c->pool_total.p;
+    a.events = c->events.p;
+    MAM_HIP(hipMemsetAsync(a.out_n, 0, sizeof(int32_t) * F, s));
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 0);
+        hipLaunchKernelGGL(mam::k_grid, dim3(F), dim3(256), 0, s, a);
+    }
+    const long long waves = (long long)F * a.unit_stride;
+    const int blocks = (int)((waves + 3) / 4);
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 1);
+        hipLaunchKernelGGL(mam::k_gather<false>, dim3(blocks), dim3(256), 0, s, a, F);
+        hipLaunchKernelGGL(mam::k_scan, dim3(F), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(mam::k_gather<true>, dim3(blocks), dim3(256), 0, s, a, F);
+    }
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 2);
+        const int S = a.fr.kp_stride;
+        const size_t lds = ((((S + 31) / 32) * 4 + 15) & ~15) + 2 * 4 * ((S + 3) & ~3);
+        hipLaunchKernelGGL(mam::k_resolve, dim3(F), dim3(64), lds, s, a);
+    }
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
+
+bool geom_ok(const mam_frame_geom* g) { return g && g->nlevels >= 1 && g->nlevels <= MAM_MAX_LEVELS; }
+
+}  // namespace
+
+extern "C" {
+
+int mam_match_create(int device, mam_match_ctx** out) {
+    if (!out) return MAM_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    MAM_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) { mam::set_last_error("no such HIP device"); return MAM_ERR_ARG; }
+    MAM_HIP(hipSetDevice(device));
+    mam_match_ctx* c = new mam_match_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        mam::set_last_error("hipStreamCreate failed");
+        return MAM_ERR_DEVICE;
+    }
+    *out = c;
+    return MAM_OK;
+}
+
+void mam_match_destroy(mam_match_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int mam_descriptor_distance(mam_match_ctx* c, const uint8_t* a, const uint8_t* b, int n, int32_t* out) {
+    if (!c || n < 0 || (n > 0 && (!a || !b || !out))) return MAM_ERR_ARG;
+    if (n == 0) return MAM_OK;
+    MAM_HIP(hipSetDevice(c->device));
+    const size_t bytes = carve_bytes((size_t)n * 32, 1) * 2 + carve_bytes(n, 4);
+    if (int rc = c->stage.alloc(bytes)) return rc;
+    uint8_t* p = c->stage.p;
+    uint8_t* da = carve<uint8_t>(p, (size_t)n * 32);
+    uint8_t* db = carve<uint8_t>(p, (size_t)n * 32);
+    int32_t* dout = carve<int32_t>(p, n);
+    MAM_HIP(hipMemcpyAsync(da, a, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    MAM_HIP(hipMemcpyAsync(db, b, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(mam::k_hamming, dim3((n + 255) / 256), dim3(256), 0, c->stream, da, db, n, dout);
+    MAM_HIP(hipMemcpyAsync(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipStreamSynchronize(c->stream));
+    return MAM_OK;
+}
+
+int mam_search_by_projection_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_frames_dev* fr,
+                                          const mam_mp_track* mps, int mp_stride, const int32_t* n_mps, float th,
+                                          int far_points, float th_far_points, float nnratio, int32_t* out,
+                                          int32_t* out_n, void* stream) {
+    if (!c || !geom_ok(g) || !fr || !mps || !n_mps || !out || !out_n || mp_stride <= 0) return MAM_ERR_ARG;
+    MAM_HIP(hipSetDevice(c->device));
+    mam::ProjArgs a{};
+    a.g = *g;
+    a.fr = *fr;
+    a.mode = 0;
+    a.unit_stride = mp_stride;
+    a.n_units = n_mps;
+    a.mps = mps;
+    a.th = th;
+    a.th_far = th_far_points;
+    a.nnratio = nnratio;
+    a.far_points = far_points;
+    a.pool_per_frame = std::max(mp_stride * c->pool_per_unit, 1 << 16);
+    a.out = out;
+    a.out_n = out_n;
+    return launch_projection(c, a, fr->nframes, stream ? (hipStream_t)stream : c->stream);
+}
+
+int mam_search_by_projection_motion_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_frames_dev* fr,
+                                                 const mam_pose* tcw, const mam_pinhole* cam,
+                                                 const mam_last_entry* last, int last_stride, const int32_t* n_last,
+                                                 float th, int check_ori, int32_t* out, int32_t* out_n, void* stream) {
+    if (!c || !geom_ok(g) || !fr || !tcw || !cam || !last || !n_last || !out || !out_n || last_stride <= 0)
+        return MAM_ERR_ARG;
+    MAM_HIP(hipSetDevice(c->device));
+    mam::ProjArgs a{};
+    a.g = *g;
+    a.fr = *fr;
+    a.mode = 1;
+    a.unit_stride = last_stride;
+    a.n_units = n_last;
+    a.tcw = tcw;
+    a.cam = *cam;
+    a.last = last;
+    a.th = th;
+    a.check_ori = check_ori;
+    a.pool_per_frame = std::max(last_stride * c->pool_per_unit, 1 << 16);
+    a.out = out;
+    a.out_n = out_n;
+    return launch_projection(c, a, fr->nframes, stream ? (hipStream_t)stream : c->stream);
+}
+
+// ---- synchronous single-frame forms over host buffers (reference semantics)
+static int stage_frame(mam_match_ctx* c, int n, const mam_keypoint* keys, const uint8_t* desc, const uint8_t* taken,
+                       size_t extra_bytes, uint8_t** extra, mam_frames_dev* fr, int32_t** dout, int32_t** dcount,
+                       int32_t** dn) {
+    const int S = std::max(n, 1);
+    const size_t bytes = carve_bytes(S, sizeof(mam_keypoint)) + carve_bytes((size_t)S * 32, 1) + carve_bytes(S, 1) +
+                         carve_bytes(S, 4) + carve_bytes(2, 4) + carve_bytes(4, 4) + extra_bytes + 256;
+    if (int rc = c->stage.alloc(bytes)) return rc;
+    uint8_t* p = c->stage.p;
+    mam_keypoint* dk = carve<mam_keypoint>(p, S);
+    uint8_t* dd = carve<uint8_t>(p, (size_t)S * 32);
+    uint8_t* dt = carve<uint8_t>(p, S);
+    *dout = carve<int32_t>(p, S);
+    *dcount = carve<int32_t>(p, 2);
+    *dn = carve<int32_t>(p, 4);
+    *extra = p;
+    if (n > 0) {
+        MAM_HIP(hipMemcpyAsync(dk, keys, sizeof(mam_keypoint) * n, hipMemcpyHostToDevice, c->stream));
+        MAM_HIP(hipMemcpyAsync(dd, desc, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+        if (taken) MAM_HIP(hipMemcpyAsync(dt, taken, n, hipMemcpyHostToDevice, c->stream));
+    }
+    const int32_t cnt[2] = {n, 0};
+    MAM_HIP(hipMemcpyAsync(*dcount, cnt, sizeof(cnt), hipMemcpyHostToDevice, c->stream));
+    fr->nframes = 1;
+    fr->kp_stride = S;
+    fr->keys = dk;
+    fr->desc = dd;
+    fr->counts = *dcount;
+    fr->taken = taken ? dt : nullptr;
+    return MAM_OK;
+}
+
+int mam_search_by_projection(mam_match_ctx* c, const mam_frame_geom* g, int n, const mam_keypoint* keys,
+                             const uint8_t* desc, const uint8_t* taken, int n_mps, const mam_mp_track* mps, float th,
+                             int far_points, float th_far_points, float nnratio, int32_t* out) {
+    if (!c || !geom_ok(g) || n < 0 || n_mps < 0 || (n > 0 && (!keys || !desc || !out)) || (n_mps > 0 && !mps))
+        return MAM_ERR_ARG;
+    if (n > mam::GRID_SORT_MAX) return MAM_ERR_CAPACITY;
+    MAM_HIP(hipSetDevice(c->device));
+    for (int attempt = 0; attempt < 6; attempt++) {
+        mam_frames_dev fr;
+        uint8_t* extra;
+        int32_t *dout, *dcount, *dn;
+        const int U = std::max(n_mps, 1);
+        if (int rc = stage_frame(c, n, keys, desc, taken, carve_bytes(U, sizeof(mam_mp_track)) + carve_bytes(1, 4),
+                                 &extra, &fr, &dout, &dcount, &dn))
+            return rc;
+        mam_mp_track* dm = carve<mam_mp_track>(extra, U);
+        int32_t* dnu = carve<int32_t>(extra, 1);
+        if (n_mps > 0) MAM_HIP(hipMemcpyAsync(dm, mps, sizeof(mam_mp_track) * n_mps, hipMemcpyHostToDevice, c->stream));
+        MAM_HIP(hipMemcpyAsync(dnu, &n_mps, 4, hipMemcpyHostToDevice, c->stream));
+        if (int rc = mam_search_by_projection_batch_device(c, g, &fr, dm, U, dnu, th, far_points, th_far_points,
+                                                           nnratio, dout, dn, c->stream))
+            return rc;
+        int32_t nm = 0;
+        MAM_HIP(hipMemcpyAsync(&nm, dn, 4, hipMemcpyDeviceToHost, c->stream));
+        if (n > 0) MAM_HIP(hipMemcpyAsync(out, dout, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+        MAM_HIP(hipStreamSynchronize(c->stream));
+        if (nm == MAM_ERR_CAPACITY && c->pool_per_unit < (1 << 14)) { c->pool_per_unit *= 4; continue; }
+        return nm;
+    }
+    return MAM_ERR_CAPACITY;
+}
+
+int mam_search_by_projection_motion(mam_match_ctx* c, const mam_frame_geom* g, int n, const mam_keypoint* keys,
+                                    const uint8_t* desc, const uint8_t* taken, const mam_pose* tcw,
+                                    const mam_pose* tlw, float mb, const mam_pinhole* cam, int n_last,
+                                    const mam_last_entry* last, float th, int mono, int check_ori, int32_t* out) {
+    (void)tlw; (void)mb;
+    if (!c || !geom_ok(g) || !tcw || !cam || n < 0 || n_last < 0 || (n > 0 && (!keys || !desc || !out)) ||
+        (n_last > 0 && !last))
+        return MAM_ERR_ARG;
+    if (!mono) { mam::set_last_error("stereo motion search is out of scope (mono agents only)"); return MAM_ERR_ARG; }
+    if (n > mam::GRID_SORT_MAX) return MAM_ERR_CAPACITY;
+    MAM_HIP(hipSetDevice(c->device));
+    for (int attempt = 0; attempt < 6; attempt++) {
+        mam_frames_dev fr;
+        uint8_t* extra;
+        int32_t *dout, *dcount, *dn;
+        const int U = std::max(n_last, 1);
+        if (int rc = stage_frame(c, n, keys, desc, taken,
+                                 carve_bytes(U, sizeof(mam_last_entry)) + carve_bytes(1, 4) + carve_bytes(1, sizeof(mam_pose)),
+                                 &extra, &fr, &dout, &dcount, &dn))
+            return rc;
+        mam_last_entry* dl = carve<mam_last_entry>(extra, U);
+        int32_t* dnu = carve<int32_t>(extra, 1);
+        mam_pose* dp = carve<mam_pose>(extra, 1);
+        if (n_last > 0)
+            MAM_HIP(hipMemcpyAsync(dl, last, sizeof(mam_last_entry) * n_last, hipMemcpyHostToDevice, c->stream));
+        MAM_HIP(hipMemcpyAsync(dnu, &n_last, 4, hipMemcpyHostToDevice, c->stream));
+        MAM_HIP(hipMemcpyAsync(dp, tcw, sizeof(mam_pose), hipMemcpyHostToDevice, c->stream));
+        if (int rc = mam_search_by_projection_motion_batch_device(c, g, &fr, dp, cam, dl, U, dnu, th, check_ori, dout,
+                                                                  dn, c->stream))
+            return rc;
+        int32_t nm = 0;
+        MAM_HIP(hipMemcpyAsync(&nm, dn, 4, hipMemcpyDeviceToHost, c->stream));
+        if (n > 0) MAM_HIP(hipMemcpyAsync(out, dout, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+        MAM_HIP(hipStreamSynchronize(c->stream));
+        if (nm == MAM_ERR_CAPACITY && c->pool_per_unit < (1 << 14)) { c->pool_per_unit *= 4; continue; }
+        return nm;
+    }
+    return MAM_ERR_CAPACITY;
+}
+
+int mam_search_for_triangulation(mam_match_ctx* c, const mam_frame_geom* g, int n1, const mam_keypoint* keys1,
+                                 const uint8_t* desc1, const uint8_t* has1, const mam_featvec* fv1, int n2,
+                                 const mam_keypoint* keys2, const uint8_t* desc2, const uint8_t* has2,
+                                 const mam_featvec* fv2, const float* F12, const float* ep, int check_ori, int coarse,
+                                 int32_t* out) {
+    if (!c || !geom_ok(g) || !fv1 || !fv2 || !F12 || !ep || n1 < 0 || n2 < 0 || (n1 > 0 && (!keys1 || !desc1 || !has1 || !out)) ||
+        (n2 > 0 && (!keys2 || !desc2 || !has2)))
+        return MAM_ERR_ARG;
+    MAM_HIP(hipSetDevice(c->device));
+    for (int i = 0; i < n1; i++) out[i] = -1;
+    if (n1 == 0) return 0;
+    // shared vocabulary nodes: the reference's merge walk visits exactly the node ids present in both
+    // FeatureVectors (ORBmatcher.cc:958-1108); flatten to one work item per idx1 entry.
+    std::vector<int32_t> work, work_n2;
+    int a1 = 0, a2 = 0;
+    while (a1 < fv1->n_nodes && a2 < fv2->n_nodes) {
+        const uint32_t id1 = fv1->node_ids[a1], id2 = fv2->node_ids[a2];
+        if (id1 == id2) {
+            for (int i1 = fv1->node_off[a1]; i1 < fv1->node_off[a1 + 1]; i1++) {
+                work.push_back(i1);
+                work_n2.push_back(fv2->node_off[a2]);
+                work_n2.push_back(fv2->node_off[a2 + 1]);
+            }
+            a1++;
+            a2++;
+        } else if (id1 < id2) {
+            a1++;
+        } else {
+            a2++;
+        }
+    }
+    const int nw = (int)work.size();
+    const int nf1 = fv1->node_off[fv1->n_nodes], nf2 = fv2->node_off[fv2->n_nodes];
+    const size_t bytes = carve_bytes(n1, sizeof(mam_keypoint)) + carve_bytes((size_t)n1 * 32, 1) + carve_bytes(n1, 1) +
+                         carve_bytes(std::max(n2, 1), sizeof(mam_keypoint)) + carve_bytes((size_t)std::max(n2, 1) * 32, 1) +
+                         carve_bytes(std::max(n2, 1), 1) + carve_bytes(std::max(nf1, 1), 4) +
+                         carve_bytes(std::max(nf2, 1), 4) + carve_bytes(std::max(nw, 1), 4) +
+                         carve_bytes(2 * std::max(nw, 1), 4) + carve_bytes(n1, 4) + carve_bytes(1, 4);
+    if (int rc = c->stage.alloc(bytes)) return rc;
+    uint8_t* p = c->stage.p;
+    mam::TriArgs a{};
+    a.g = *g;
+    mam_keypoint* dk1 = carve<mam_keypoint>(p, n1);
+    uint8_t* dd1 = carve<uint8_t>(p, (size_t)n1 * 32);
+    uint8_t* dh1 = carve<uint8_t>(p, n1);
+    mam_keypoint* dk2 = carve<mam_keypoint>(p, std::max(n2, 1));
+    uint8_t* dd2 = carve<uint8_t>(p, (size_t)std::max(n2, 1) * 32);
+    uint8_t* dh2 = carve<uint8_t>(p, std::max(n2, 1));
+    uint32_t* df1 = carve<uint32_t>(p, std::max(nf1, 1));
+    uint32_t* df2 = carve<uint32_t>(p, std::max(nf2, 1));
+    int32_t* dw = carve<int32_t>(p, std::max(nw, 1));
+    int32_t* dw2 = carve<int32_t>(p, 2 * std::max(nw, 1));
+    int32_t* dout = carve<int32_t>(p, n1);
+    int32_t* dn = carve<int32_t>(p, 1);
+    hipStream_t s = c->stream;
+    MAM_HIP(hipMemcpyAsync(dk1, keys1, sizeof(mam_keypoint) * n1, hipMemcpyHostToDevice, s));
+    MAM_HIP(hipMemcpyAsync(dd1, desc1, (size_t)n1 * 32, hipMemcpyHostToDevice, s));
+    MAM_HIP(hipMemcpyAsync(dh1, has1, n1, hipMemcpyHostToDevice, s));
+    if (n2 > 0) {
+        MAM_HIP(hipMemcpyAsync(dk2, keys2, sizeof(mam_keypoint) * n2, hipMemcpyHostToDevice, s));
+        MAM_HIP(hipMemcpyAsync(dd2, desc2, (size_t)n2 * 32, hipMemcpyHostToDevice, s));
+        MAM_HIP(hipMemcpyAsync(dh2, has2, n2, hipMemcpyHostToDevice, s));
+    }
+    if (nf1 > 0) MAM_HIP(hipMemcpyAsync(df1, fv1->feats, 4 * (size_t)nf1, hipMemcpyHostToDevice, s));
+    if (nf2 > 0) MAM_HIP(hipMemcpyAsync(df2, fv2->feats, 4 * (size_t)nf2, hipMemcpyHostToDevice, s));
+    if (nw > 0) {
+        MAM_HIP(hipMemcpyAsync(dw, work.data(), 4 * (size_t)nw, hipMemcpyHostToDevice, s));
+        MAM_HIP(hipMemcpyAsync(dw2, work_n2.data(), 8 * (size_t)nw, hipMemcpyHostToDevice, s));
+    }
+    MAM_HIP(hipMemsetAsync(dout, 0xFF, 4 * (size_t)n1, s));
+    a.keys1 = dk1; a.desc1 = dd1; a.has1 = dh1;
+    a.keys2 = dk2; a.desc2 = dd2; a.has2 = dh2;
+    a.feats1 = df1; a.feats2 = df2;
+    a.work = dw; a.work_n2 = dw2; a.nwork = nw;
+    for (int i = 0; i < 9; i++) a.F[i] = F12[i];
+    a.ep[0] = ep[0]; a.ep[1] = ep[1];
+    a.coarse = coarse;
+    a.out = dout;
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 3);
+        if (nw > 0) hipLaunchKernelGGL(mam::k_tri, dim3((nw + 3) / 4), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(mam::k_tri_rot, dim3(1), dim3(256), 0, s, dk1, dk2, n1, check_ori, dout, dn);
+    }
+    MAM_HIP(hipGetLastError());
+    int32_t nm = 0;
+    MAM_HIP(hipMemcpyAsync(out, dout, 4 * (size_t)n1, hipMemcpyDeviceToHost, s));
+    MAM_HIP(hipMemcpyAsync(&nm, dn, 4, hipMemcpyDeviceToHost, s));
+    MAM_HIP(hipStreamSynchronize(s));
+    return nm;
+}
+
+int mam_match_set_profiling(mam_match_ctx* c, int enable) {
+    if (!c) return MAM_ERR_ARG;
+    c->timer.reset(enable != 0);
+    return MAM_OK;
+}
+
+int mam_match_stage_times(mam_match_ctx* c, double* ms_out, int64_t* launches_out) {
+    if (!c) return MAM_ERR_ARG;
+    c->timer.collect();
+    for (int i = 0; i < 4; i++) {
+        if (ms_out) ms_out[i] = c->timer.ms[i];
+        if (launches_out) launches_out[i] = c->timer.n[i];
+    }
+    return MAM_OK;
+}
+
+}  // extern "C"

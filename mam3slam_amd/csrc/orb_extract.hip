@@ -17,19 +17,11 @@
 
 #include "orb_common.hpp"
 #include "orb_kernels.hip"
+#include "runtime.hpp"
 
 namespace {
 
 thread_local std::string g_last_error;
-
-#define MAM_HIP(call)                                                                            \
-    do {                                                                                         \
-        hipError_t e_ = (call);                                                                  \
-        if (e_ != hipSuccess) {                                                                  \
-            g_last_error = std::string(#call) + ": " + hipGetErrorString(e_);                    \
-            return MAM_ERR_DEVICE;                                                               \
-        }                                                                                        \
-    } while (0)
 
 inline int cvRoundF(float v) { return (int)lrintf(v); }
 inline int cvRoundD(double v) { return (int)lrint(v); }
@@ -40,33 +32,11 @@ inline short satShortF(float v) {
     return (short)(iv < -32768 ? -32768 : iv > 32767 ? 32767 : iv);
 }
 
-template <typename T>
-struct DevBuf {
-    T* p = nullptr;
-    size_t n = 0;
-    int alloc(size_t count) {
-        if (count <= n && p) return MAM_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-        if (count == 0) return MAM_OK;
-        MAM_HIP(hipMalloc(&p, count * sizeof(T)));
-        n = count;
-        return MAM_OK;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-    }
-};
-
-struct StageEvent {
-    int stage;
-    hipEvent_t a, b;
-};
+using mam::DevBuf;
 
 }  // namespace
+
+void mam::set_last_error(const std::string& s) { g_last_error = s; }
 
 struct mam_orb_ctx {
     mam_orb_params prm{};
@@ -97,11 +67,7 @@ struct mam_orb_ctx {
     size_t last_stride = 0, last_fstride = 0;
     int last_nframes = 0;
     // profiling
-    bool profiling = false;
-    std::vector<StageEvent> pending;
-    std::vector<hipEvent_t> event_pool;
-    double stage_ms[MAM_STAGE_COUNT] = {0};
-    int64_t stage_n[MAM_STAGE_COUNT] = {0};
+    mam::StageTimer timer{MAM_STAGE_COUNT};
 };
 
 namespace {
@@ -340,36 +306,7 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
     return MAM_OK;
 }
 
-hipEvent_t take_event(mam_orb_ctx* c) {
-    if (!c->event_pool.empty()) {
-        hipEvent_t e = c->event_pool.back();
-        c->event_pool.pop_back();
-        return e;
-    }
-    hipEvent_t e = nullptr;
-    (void)hipEventCreate(&e);
-    return e;
-}
-
-struct StageScope {
-    mam_orb_ctx* c;
-    hipStream_t s;
-    int stage;
-    hipEvent_t a = nullptr;
-    StageScope(mam_orb_ctx* c_, hipStream_t s_, int st) : c(c_), s(s_), stage(st) {
-        if (c->profiling) {
-            a = take_event(c);
-            (void)hipEventRecord(a, s);
-        }
-    }
-    ~StageScope() {
-        if (c->profiling) {
-            hipEvent_t b = take_event(c);
-            (void)hipEventRecord(b, s);
-            c->pending.push_back({stage, a, b});
-        }
-    }
-};
+using StageScope = mam::StageTimer::Scope;
 
 int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size_t fstride, int lap0, int lap1,
                  mam_keypoint* d_kps, uint8_t* d_desc, int capacity, int32_t* d_counts, hipStream_t s) {
@@ -377,7 +314,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
     const int L = g.nlevels;
     mam::LevelSrc src{d_in, stride, fstride, c->d_pyr.p};
     {
-        StageScope sc(c, s, MAM_STAGE_PYRAMID);
+        StageScope sc(&c->timer, s, MAM_STAGE_PYRAMID);
         for (int l = 1; l < L; l++) {
             const mam::LevelGeom& lv = g.L[l];
             dim3 grid((lv.w + 255) / 256, (lv.h + 3) / 4, F);
@@ -385,22 +322,22 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
         }
     }
     {
-        StageScope sc(c, s, MAM_STAGE_FAST);
+        StageScope sc(&c->timer, s, MAM_STAGE_FAST);
         hipLaunchKernelGGL(mam::k_fast_cells, dim3(g.cells_per_frame, F), dim3(256), c->fast_lds, s, c->d_geom.p,
                            c->d_cells.p, src, c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast);
     }
     {
-        StageScope sc(c, s, MAM_STAGE_BLUR);
+        StageScope sc(&c->timer, s, MAM_STAGE_BLUR);
         hipLaunchKernelGGL(mam::k_blur7, dim3(g.tiles_per_frame, F), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p);
     }
     {
-        StageScope sc(c, s, MAM_STAGE_DISTRIBUTE);
+        StageScope sc(&c->timer, s, MAM_STAGE_DISTRIBUTE);
         hipLaunchKernelGGL(mam::k_distribute, dim3(L, F), dim3(256), c->dist_lds, s, c->d_geom.p, c->d_cellcnt.p,
                            c->d_cand.p, c->d_keys.p, c->d_knode.p, c->d_okey.p, c->d_orank.p, c->d_lvlcnt.p, lap0,
                            lap1);
     }
     {
-        StageScope sc(c, s, MAM_STAGE_DESCRIBE);
+        StageScope sc(&c->timer, s, MAM_STAGE_DESCRIBE);
         const long long waves = (long long)F * g.kp_slots;
         const int blocks = (int)((waves + 3) / 4);
         hipLaunchKernelGGL(mam::k_describe, dim3(blocks), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p,
@@ -451,8 +388,6 @@ void mam_orb_destroy(mam_orb_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto& pe : c->pending) { (void)hipEventDestroy(pe.a); (void)hipEventDestroy(pe.b); }
-    for (auto e : c->event_pool) (void)hipEventDestroy(e);
     c->d_geom.release(); c->d_cells.release(); c->d_tabs_i.release(); c->d_tabs_s.release();
     c->d_pyr.release(); c->d_blur.release(); c->d_input.release();
     c->d_cand.release(); c->d_keys.release(); c->d_okey.release(); c->d_orank.release(); c->d_knode.release();
@@ -579,28 +514,16 @@ int mam_orb_debug_candidates(mam_orb_ctx* c, int frame, int level, uint32_t* out
 
 int mam_orb_set_profiling(mam_orb_ctx* c, int enable) {
     if (!c) return MAM_ERR_ARG;
-    c->profiling = enable != 0;
-    for (int i = 0; i < MAM_STAGE_COUNT; i++) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
-    for (auto& pe : c->pending) { c->event_pool.push_back(pe.a); c->event_pool.push_back(pe.b); }
-    c->pending.clear();
+    c->timer.reset(enable != 0);
     return MAM_OK;
 }
 
 int mam_orb_stage_times(mam_orb_ctx* c, double* ms_out, int64_t* launches_out) {
     if (!c) return MAM_ERR_ARG;
-    for (auto& pe : c->pending) {
-        (void)hipEventSynchronize(pe.b);
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, pe.a, pe.b);
-        c->stage_ms[pe.stage] += ms;
-        c->stage_n[pe.stage] += 1;
-        c->event_pool.push_back(pe.a);
-        c->event_pool.push_back(pe.b);
-    }
-    c->pending.clear();
+    c->timer.collect();
     for (int i = 0; i < MAM_STAGE_COUNT; i++) {
-        if (ms_out) ms_out[i] = c->stage_ms[i];
-        if (launches_out) launches_out[i] = c->stage_n[i];
+        if (ms_out) ms_out[i] = c->timer.ms[i];
+        if (launches_out) launches_out[i] = c->timer.n[i];
     }
     return MAM_OK;
 }

@@ -1,0 +1,290 @@
+"""ORBmatcher — Python mirror of MAM3SLAM::ORBmatcher's hot-path searches over the C-ABI (include/mam_match.h).
+
+Reference interface (include/ORBmatcher.h:40-93, src/ORBmatcher.cc):
+    ORBmatcher(float nnratio=0.6, bool checkOri=true)
+    static int DescriptorDistance(const cv::Mat& a, const cv::Mat& b)
+    int SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, float th=3, bool bFarPoints=false,
+                           float thFarPoints=50)
+    int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, float th, bool bMono)
+    int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pair<size_t,size_t>>& vMatchedPairs,
+                               bool bOnlyStereo, bool bCoarse=false)
+    TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30
+
+Frames/KeyFrames are passed as FrameData (numpy views of the fields the searches read). Object pointers are
+replaced by indices: the search results are per-keypoint indices into the MapPoint list / last frame
+(-1 = untouched), exactly what the reference writes into Frame::mvpMapPoints.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ._lib import MamError, check, lib
+from .orb import KP_DTYPE
+
+TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
+GRID_COLS, GRID_ROWS = 64, 48
+MAX_LEVELS = 16
+
+
+class FrameGeom(C.Structure):
+    _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float),
+                ("grid_inv_w", C.c_float), ("grid_inv_h", C.c_float), ("nlevels", C.c_int32),
+                ("scale_factors", C.c_float * MAX_LEVELS), ("level_sigma2", C.c_float * MAX_LEVELS)]
+
+
+class Pose(C.Structure):
+    _fields_ = [("q", C.c_float * 4), ("t", C.c_float * 3)]
+
+
+class Pinhole(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float)]
+
+
+class FeatVec(C.Structure):
+    _fields_ = [("n_nodes", C.c_int32), ("node_ids", C.c_void_p), ("node_off", C.c_void_p), ("feats", C.c_void_p)]
+
+
+class FramesDev(C.Structure):
+    _fields_ = [("nframes", C.c_int32), ("kp_stride", C.c_int32), ("keys", C.c_void_p), ("desc", C.c_void_p),
+                ("counts", C.c_void_p), ("taken", C.c_void_p)]
+
+
+MP_TRACK_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("view_cos", "<f4"), ("track_depth", "<f4"),
+                           ("track_in_view", "<i4"), ("scale_level", "<i4"), ("is_bad", "<i4"), ("nobs", "<i4"),
+                           ("desc", "u1", (32,))])
+LAST_ENTRY_DTYPE = np.dtype([("pos", "<f4", (3,)), ("angle", "<f4"), ("octave", "<i4"), ("valid", "<i4"),
+                             ("nobs", "<i4"), ("pad", "<i4"), ("desc", "u1", (32,))])
+assert MP_TRACK_DTYPE.itemsize == 64 and LAST_ENTRY_DTYPE.itemsize == 64
+
+_SIGS = {
+    "mam_match_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "mam_match_destroy": (None, [C.c_void_p]),
+    "mam_descriptor_distance": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    "mam_search_by_projection": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_int, C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_float,
+                                           C.c_void_p]),
+    "mam_search_by_projection_motion": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p,
+                                                  C.c_int, C.c_void_p, C.c_float, C.c_int, C.c_int, C.c_void_p]),
+    "mam_search_for_triangulation": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                               C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "mam_search_by_projection_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                                        C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_float,
+                                                        C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mam_search_by_projection_motion_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                               C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                                               C.c_float, C.c_int, C.c_void_p, C.c_void_p,
+                                                               C.c_void_p]),
+    "mam_match_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "mam_match_stage_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+}
+
+
+def _bind():
+    L = lib()
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    return L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+@dataclass
+class FrameData:
+    """The Frame / KeyFrame fields the searches read. keys = mvKeysUn (KP_DTYPE), desc = mDescriptors."""
+
+    keys: np.ndarray
+    desc: np.ndarray
+    width: int
+    height: int
+    scale_factors: np.ndarray
+    level_sigma2: np.ndarray
+    taken: np.ndarray | None = None          # mvpMapPoints[i] && Observations() > 0  (Frame)
+    has_mp: np.ndarray | None = None         # GetMapPoint(i) != NULL                   (KeyFrame)
+    featvec: dict | None = None              # DBoW2::FeatureVector: node id -> list of feature indices
+    pose: tuple | None = None                # (q xyzw float32[4], t float32[3]) = Tcw
+    extra: dict = field(default_factory=dict)
+
+    def geom(self) -> FrameGeom:
+        g = FrameGeom()
+        # ComputeImageBounds without distortion (Frame.cc:801-807) and the grid inverses (Frame.cc:341-342)
+        g.min_x, g.max_x, g.min_y, g.max_y = 0.0, float(self.width), 0.0, float(self.height)
+        g.grid_inv_w = float(np.float32(GRID_COLS) / np.float32(self.width))
+        g.grid_inv_h = float(np.float32(GRID_ROWS) / np.float32(self.height))
+        g.nlevels = len(self.scale_factors)
+        for i, v in enumerate(self.scale_factors):
+            g.scale_factors[i] = float(v)
+        for i, v in enumerate(self.level_sigma2):
+            g.level_sigma2[i] = float(v)
+        return g
+
+
+def flatten_featvec(fv: dict):
+    ids = np.array(sorted(fv), dtype=np.uint32)
+    off = np.zeros(len(ids) + 1, np.int32)
+    feats = []
+    for i, k in enumerate(ids):
+        lst = sorted(fv[int(k)])
+        feats.extend(lst)
+        off[i + 1] = off[i] + len(lst)
+    return ids, off, np.array(feats if feats else [0], dtype=np.uint32)
+
+
+def quat_to_rot(q):
+    x, y, z, w = [np.float32(v) for v in q]
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]], np.float32)
+
+
+def fundamental_12(pose1, pose2, K1, K2):
+    """F12 = K1^-T [t12]x R12 K2^-1 with T12 = T1w * T2w^-1 (ORBmatcher.cc:926-930, Pinhole.cpp:109-112)."""
+    R1, t1 = quat_to_rot(pose1[0]), np.asarray(pose1[1], np.float32)
+    R2, t2 = quat_to_rot(pose2[0]), np.asarray(pose2[1], np.float32)
+    R12 = (R1 @ R2.T).astype(np.float32)
+    t12 = (t1 - R12 @ t2).astype(np.float32)
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]], np.float32)
+    F = np.linalg.inv(K1.T.astype(np.float64)).astype(np.float32) @ tx @ R12 @ np.linalg.inv(
+        K2.astype(np.float64)).astype(np.float32)
+    return F.astype(np.float32)
+
+
+def epipole_12(pose1, pose2, cam2: Pinhole):
+    """ep = KF2 camera projection of KF1's centre (ORBmatcher.cc:913-919)."""
+    R1, t1 = quat_to_rot(pose1[0]), np.asarray(pose1[1], np.float32)
+    R2, t2 = quat_to_rot(pose2[0]), np.asarray(pose2[1], np.float32)
+    Cw = (-R1.T @ t1).astype(np.float32)
+    C2 = (R2 @ Cw + t2).astype(np.float32)
+    return np.array([cam2.fx * C2[0] / C2[2] + cam2.cx, cam2.fy * C2[1] / C2[2] + cam2.cy], np.float32)
+
+
+class ORBmatcher:
+    TH_HIGH, TH_LOW, HISTO_LENGTH = TH_HIGH, TH_LOW, HISTO_LENGTH
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        self._L = _bind()
+        self._ctx = C.c_void_p()
+        check(self._L.mam_match_create(int(device), C.byref(self._ctx)), "mam_match_create")
+
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self._L.mam_match_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def DescriptorDistance(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a, np.uint8).reshape(-1, 32)
+        b = np.ascontiguousarray(b, np.uint8).reshape(-1, 32)
+        out = np.zeros(len(a), np.int32)
+        check(self._L.mam_descriptor_distance(self._ctx, _p(a), _p(b), len(a), _p(out)), "descriptor_distance")
+        return out
+
+    def SearchByProjection(self, F: FrameData, mps: np.ndarray, th: float = 3, bFarPoints: bool = False,
+                           thFarPoints: float = 50):
+        """Local-map search (ORBmatcher.cc:43-213). Returns (nmatches, kp_to_mp)."""
+        keys = np.ascontiguousarray(F.keys, KP_DTYPE)
+        desc = np.ascontiguousarray(F.desc, np.uint8)
+        taken = None if F.taken is None else np.ascontiguousarray(F.taken, np.uint8)
+        mps = np.ascontiguousarray(mps, MP_TRACK_DTYPE)
+        out = np.full(max(len(keys), 1), -1, np.int32)
+        g = F.geom()
+        n = self._L.mam_search_by_projection(self._ctx, C.byref(g), len(keys), _p(keys), _p(desc), _p(taken),
+                                             len(mps), _p(mps), float(th), int(bFarPoints), float(thFarPoints),
+                                             self.mfNNratio, _p(out))
+        check(n, "SearchByProjection")
+        return n, out[:len(keys)]
+
+    def SearchByProjectionMotion(self, Cur: FrameData, last: np.ndarray, cam: Pinhole, th: float, bMono: bool = True):
+        """Motion-model search SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1676-1887).
+        `last` holds LastFrame's entries (LAST_ENTRY_DTYPE); Cur.pose = CurrentFrame Tcw."""
+        if not bMono:
+            raise MamError("stereo motion search is out of scope (mono agents only)")
+        keys = np.ascontiguousarray(Cur.keys, KP_DTYPE)
+        desc = np.ascontiguousarray(Cur.desc, np.uint8)
+        taken = None if Cur.taken is None else np.ascontiguousarray(Cur.taken, np.uint8)
+        last = np.ascontiguousarray(last, LAST_ENTRY_DTYPE)
+        pose = Pose()
+        for i in range(4):
+            pose.q[i] = float(Cur.pose[0][i])
+        for i in range(3):
+            pose.t[i] = float(Cur.pose[1][i])
+        out = np.full(max(len(keys), 1), -1, np.int32)
+        g = Cur.geom()
+        n = self._L.mam_search_by_projection_motion(self._ctx, C.byref(g), len(keys), _p(keys), _p(desc), _p(taken),
+                                                    C.byref(pose), None, 0.0, C.byref(cam), len(last), _p(last),
+                                                    float(th), 1, int(self.mbCheckOrientation), _p(out))
+        check(n, "SearchByProjection(motion)")
+        return n, out[:len(keys)]
+
+    def SearchForTriangulation(self, KF1: FrameData, KF2: FrameData, F12: np.ndarray, ep: np.ndarray,
+                               bOnlyStereo: bool = False, bCoarse: bool = False):
+        """ORBmatcher.cc:907-1146 (mono Pinhole). Returns (nmatches, vMatchedPairs as (k,2) int array)."""
+        if bOnlyStereo:
+            return 0, np.zeros((0, 2), np.int64)
+        k1 = np.ascontiguousarray(KF1.keys, KP_DTYPE)
+        k2 = np.ascontiguousarray(KF2.keys, KP_DTYPE)
+        d1 = np.ascontiguousarray(KF1.desc, np.uint8)
+        d2 = np.ascontiguousarray(KF2.desc, np.uint8)
+        h1 = np.ascontiguousarray(KF1.has_mp if KF1.has_mp is not None else np.zeros(len(k1)), np.uint8)
+        h2 = np.ascontiguousarray(KF2.has_mp if KF2.has_mp is not None else np.zeros(len(k2)), np.uint8)
+        i1, o1, f1 = flatten_featvec(KF1.featvec)
+        i2, o2, f2 = flatten_featvec(KF2.featvec)
+        fv1 = FeatVec(len(i1), i1.ctypes.data, o1.ctypes.data, f1.ctypes.data)
+        fv2 = FeatVec(len(i2), i2.ctypes.data, o2.ctypes.data, f2.ctypes.data)
+        F12 = np.ascontiguousarray(F12, np.float32).reshape(9)
+        ep = np.ascontiguousarray(ep, np.float32).reshape(2)
+        out = np.full(max(len(k1), 1), -1, np.int32)
+        g = KF2.geom()
+        n = self._L.mam_search_for_triangulation(self._ctx, C.byref(g), len(k1), _p(k1), _p(d1), _p(h1),
+                                                 C.byref(fv1), len(k2), _p(k2), _p(d2), _p(h2), C.byref(fv2),
+                                                 _p(F12), _p(ep), int(self.mbCheckOrientation), int(bCoarse), _p(out))
+        check(n, "SearchForTriangulation")
+        out = out[:len(k1)]
+        idx = np.nonzero(out >= 0)[0]
+        return n, np.stack([idx, out[idx]], 1).astype(np.int64)
+
+    # ---- batched device-resident (bench / multi-agent harness)
+    def search_by_projection_batch_device(self, F: FrameData, frames: FramesDev, d_mps: int, mp_stride: int,
+                                          d_nmps: int, th: float, d_out: int, d_nmatch: int, stream: int = 0,
+                                          far=False, th_far=50.0):
+        g = F.geom()
+        return check(self._L.mam_search_by_projection_batch_device(
+            self._ctx, C.byref(g), C.byref(frames), C.c_void_p(d_mps), mp_stride, C.c_void_p(d_nmps), float(th),
+            int(far), float(th_far), self.mfNNratio, C.c_void_p(d_out), C.c_void_p(d_nmatch), C.c_void_p(stream)),
+            "search_by_projection_batch_device")
+
+    def search_motion_batch_device(self, F: FrameData, frames: FramesDev, d_tcw: int, cam: Pinhole, d_last: int,
+                                   last_stride: int, d_nlast: int, th: float, d_out: int, d_nmatch: int,
+                                   stream: int = 0):
+        g = F.geom()
+        return check(self._L.mam_search_by_projection_motion_batch_device(
+            self._ctx, C.byref(g), C.byref(frames), C.c_void_p(d_tcw), C.byref(cam), C.c_void_p(d_last),
+            last_stride, C.c_void_p(d_nlast), float(th), int(self.mbCheckOrientation), C.c_void_p(d_out),
+            C.c_void_p(d_nmatch), C.c_void_p(stream)), "search_motion_batch_device")
+
+    def set_profiling(self, enable: bool):
+        check(self._L.mam_match_set_profiling(self._ctx, 1 if enable else 0), "match_set_profiling")
+
+    def stage_times(self):
+        ms = np.zeros(4, np.float64)
+        n = np.zeros(4, np.int64)
+        check(self._L.mam_match_stage_times(self._ctx, _p(ms), _p(n)), "match_stage_times")
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(["grid", "gather", "resolve", "triangulation"])}

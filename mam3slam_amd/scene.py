@@ -1,0 +1,177 @@
+"""Synthetic matching / mapping inputs built around real extracted ORB features.
+
+There is no dataset, vocabulary or map: the searches are fed structures generated from a frame's own
+keypoints so that real matches exist, plus the adversarial cases the reference's control flow has
+(duplicate MapPoints competing for one keypoint, pre-taken keypoints, bad / not-in-view points, wrong-level
+predictions, Hamming ties, outliers behind the camera, empty windows).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .match import LAST_ENTRY_DTYPE, MP_TRACK_DTYPE, FrameData, Pinhole, epipole_12, fundamental_12
+from .orb import KP_DTYPE
+
+
+def scale_tables(nlevels=8, scale=1.2):
+    s = [np.float32(1.0)]
+    for _ in range(nlevels - 1):
+        s.append(np.float32(np.float64(s[-1]) * np.float64(np.float32(scale))))
+    s = np.array(s, np.float32)
+    return s, (s * s).astype(np.float32)
+
+
+def flip_bits(desc: np.ndarray, rng: np.random.Generator, kmax: int) -> np.ndarray:
+    d = desc.copy()
+    for i in range(len(d)):
+        k = int(rng.integers(0, kmax + 1))
+        for b in rng.choice(256, size=k, replace=False):
+            d[i, b >> 3] ^= np.uint8(1 << (b & 7))
+    return d
+
+
+def make_frame_data(keys, desc, w, h, rng=None, taken_frac=0.0) -> FrameData:
+    sf, s2 = scale_tables()
+    taken = None
+    if rng is not None and taken_frac > 0:
+        taken = (rng.random(len(keys)) < taken_frac).astype(np.uint8)
+    return FrameData(keys=np.ascontiguousarray(keys, KP_DTYPE), desc=np.ascontiguousarray(desc, np.uint8), width=w,
+                     height=h, scale_factors=sf, level_sigma2=s2, taken=taken)
+
+
+def local_mappoints(F: FrameData, rng: np.random.Generator, frac=0.8, dup_frac=0.15, n_random=60, kflip=14):
+    """MapPoint track records around F's keypoints (what Frame::isInFrustum leaves in each MapPoint)."""
+    n = len(F.keys)
+    sel = rng.choice(n, size=int(n * frac), replace=False)
+    m = len(sel)
+    mps = np.zeros(m, MP_TRACK_DTYPE)
+    k = F.keys[sel]
+    mps["proj_x"] = k["x"] + rng.normal(0, 0.8, m).astype(np.float32)
+    mps["proj_y"] = k["y"] + rng.normal(0, 0.8, m).astype(np.float32)
+    mps["view_cos"] = rng.uniform(0.99, 1.0, m).astype(np.float32)
+    mps["track_depth"] = rng.uniform(0.5, 60, m).astype(np.float32)
+    mps["track_in_view"] = (rng.random(m) < 0.95).astype(np.int32)
+    mps["scale_level"] = np.clip(k["octave"] + rng.integers(0, 2, m), 0, 7)
+    mps["is_bad"] = (rng.random(m) < 0.02).astype(np.int32)
+    mps["nobs"] = rng.integers(0, 6, m) * (rng.random(m) < 0.97) + (rng.random(m) < 0.97)
+    mps["desc"] = flip_bits(F.desc[sel], rng, kflip)
+    # duplicates: near-identical MapPoints competing for the same keypoint (greedy conflicts)
+    nd = int(m * dup_frac)
+    dup = mps[rng.choice(m, size=nd, replace=False)].copy()
+    dup["proj_x"] += rng.normal(0, 0.5, nd).astype(np.float32)
+    dup["desc"] = flip_bits(dup["desc"], rng, 3)
+    # random points: mostly empty windows / no good match
+    rnd = np.zeros(n_random, MP_TRACK_DTYPE)
+    rnd["proj_x"] = rng.uniform(-20, F.width + 20, n_random)
+    rnd["proj_y"] = rng.uniform(-20, F.height + 20, n_random)
+    rnd["view_cos"] = rng.uniform(0.9, 1.0, n_random)
+    rnd["track_in_view"] = 1
+    rnd["scale_level"] = rng.integers(0, 8, n_random)
+    rnd["nobs"] = 1
+    rnd["desc"] = rng.integers(0, 256, (n_random, 32), dtype=np.uint8)
+    allm = np.concatenate([mps, dup, rnd])
+    return allm[rng.permutation(len(allm))]
+
+
+def pinhole(w, h, f=500.0) -> Pinhole:
+    return Pinhole(np.float32(f), np.float32(f), np.float32(w / 2), np.float32(h / 2))
+
+
+def small_pose(rng, rot=0.01, trans=0.05):
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = rng.uniform(-rot, rot)
+    q = np.append(axis * np.sin(ang / 2), np.cos(ang / 2)).astype(np.float32)
+    q /= np.float32(np.linalg.norm(q))
+    t = rng.uniform(-trans, trans, 3).astype(np.float32)
+    return q.astype(np.float32), t
+
+
+def motion_last_frame(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.75, n_out=80, kflip=12):
+    """LastFrame entries whose MapPoints re-project near F's keypoints under F.pose (Tcw)."""
+    from .match import quat_to_rot
+
+    q, t = F.pose
+    R = quat_to_rot(q)
+    n = len(F.keys)
+    sel = rng.choice(n, size=int(n * frac), replace=False)
+    m = len(sel)
+    k = F.keys[sel]
+    z = rng.uniform(2.0, 12.0, m)
+    u = k["x"] + rng.normal(0, 0.7, m)
+    v = k["y"] + rng.normal(0, 0.7, m)
+    Xc = np.stack([(u - cam.cx) / cam.fx * z, (v - cam.cy) / cam.fy * z, z], 1)
+    Xw = (Xc - t[None, :].astype(np.float64)) @ R.astype(np.float64)   # R^T (Xc - t)
+    last = np.zeros(m, LAST_ENTRY_DTYPE)
+    last["pos"] = Xw.astype(np.float32)
+    last["angle"] = ((k["angle"] + rng.normal(0, 4.0, m)) % 360).astype(np.float32)
+    last["octave"] = np.clip(k["octave"] + rng.integers(-1, 2, m), 0, 7)
+    last["valid"] = (rng.random(m) < 0.95).astype(np.int32)
+    last["nobs"] = rng.integers(1, 8, m) * (rng.random(m) < 0.98)
+    last["desc"] = flip_bits(F.desc[sel], rng, kflip)
+    # a block with a consistent large rotation (a minority histogram bin) and pure outliers
+    rot = rng.random(m) < 0.08
+    last["angle"][rot] = (last["angle"][rot] + 90.0) % 360
+    out = np.zeros(n_out, LAST_ENTRY_DTYPE)
+    out["pos"] = rng.uniform(-8, 8, (n_out, 3)).astype(np.float32)
+    out["angle"] = rng.uniform(0, 360, n_out)
+    out["octave"] = rng.integers(0, 8, n_out)
+    out["valid"] = 1
+    out["nobs"] = 1
+    out["desc"] = rng.integers(0, 256, (n_out, 32), dtype=np.uint8)
+    allm = np.concatenate([last, out])
+    return allm[rng.permutation(len(allm))]
+
+
+def quantize(desc: np.ndarray, centroids: np.ndarray, node_ids: np.ndarray):
+    """Nearest-centroid Hamming quantizer (a one-level stand-in for DBoW2's transform at levelsup=4)."""
+    x = np.unpackbits(desc, axis=1).astype(np.int16)
+    c = np.unpackbits(centroids, axis=1).astype(np.int16)
+    d = (x[:, None, :] != c[None, :, :]).sum(-1)
+    lab = d.argmin(1)
+    fv = {}
+    for i, l in enumerate(lab):
+        fv.setdefault(int(node_ids[l]), []).append(i)
+    return fv
+
+
+def keyframe_pair(F: FrameData, cam: Pinhole, rng: np.random.Generator, n_nodes=24, kflip=10, baseline=0.3):
+    """(KF1, KF2, F12, ep): KF2 sees KF1's features shifted by a horizontal disparity (x-translation rig), so
+    the epipolar lines are near-horizontal and many pairs satisfy the constraint; plus extra features."""
+    n = len(F.keys)
+    k1 = F.keys.copy()
+    sel = rng.choice(n, size=int(n * 0.8), replace=False)
+    k2 = F.keys[sel].copy()
+    disp = rng.uniform(3, 40, len(sel)).astype(np.float32)
+    k2["x"] = np.clip(k2["x"] - disp, 0, F.width - 1)
+    k2["y"] = k2["y"] + rng.normal(0, 0.8, len(sel)).astype(np.float32)
+    k2["octave"] = np.clip(k2["octave"] + rng.integers(-1, 2, len(sel)), 0, 7)
+    k2["angle"] = ((k2["angle"] + rng.normal(0, 5, len(sel))) % 360).astype(np.float32)
+    d2 = flip_bits(F.desc[sel], rng, kflip)
+    ne = n // 5
+    ke = np.zeros(ne, KP_DTYPE)
+    ke["x"] = rng.uniform(0, F.width - 1, ne)
+    ke["y"] = rng.uniform(0, F.height - 1, ne)
+    ke["octave"] = rng.integers(0, 8, ne)
+    ke["angle"] = rng.uniform(0, 360, ne)
+    ke["size"] = 31
+    de = rng.integers(0, 256, (ne, 32), dtype=np.uint8)
+    k2 = np.concatenate([k2, ke])
+    d2 = np.concatenate([d2, de])
+    perm = rng.permutation(len(k2))
+    k2, d2 = k2[perm], d2[perm]
+    centroids = rng.integers(0, 256, (n_nodes, 32), dtype=np.uint8)
+    node_ids = np.sort(rng.choice(1_000_000, size=n_nodes, replace=False)).astype(np.uint32)
+    KF1 = make_frame_data(k1, F.desc, F.width, F.height)
+    KF2 = make_frame_data(k2, d2, F.width, F.height)
+    KF1.has_mp = (rng.random(len(k1)) < 0.2).astype(np.uint8)
+    KF2.has_mp = (rng.random(len(k2)) < 0.2).astype(np.uint8)
+    KF1.featvec = quantize(KF1.desc, centroids, node_ids)
+    KF2.featvec = quantize(KF2.desc, centroids, node_ids)
+    q0 = np.array([0, 0, 0, 1], np.float32)
+    KF1.pose = (q0, np.zeros(3, np.float32))
+    KF2.pose = (q0, np.array([-baseline, 0.0, -0.05], np.float32))
+    K = np.array([[cam.fx, 0, cam.cx], [0, cam.fy, cam.cy], [0, 0, 1]], np.float32)
+    F12 = fundamental_12(KF1.pose, KF2.pose, K, K)
+    ep = epipole_12(KF1.pose, KF2.pose, cam)
+    return KF1, KF2, F12, ep

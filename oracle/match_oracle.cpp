@@ -1,0 +1,299 @@
+// match_oracle.cpp — TEST INFRASTRUCTURE ONLY (see orb_oracle.h header note).
+//
+// Single-threaded CPU restatement of the ORBmatcher searches on the hot path, following the reference:
+//   src/Frame.cc:385-416        AssignFeaturesToGrid      src/Frame.cc:725-735   PosInGrid
+//   src/Frame.cc:657-723        GetFeaturesInArea (enumeration order ix -> iy -> cell vector)
+//   src/ORBmatcher.cc:43-213    SearchByProjection(Frame&, vector<MapPoint*>) (mono branch), :215-221 radius
+//   src/ORBmatcher.cc:1676-1887 SearchByProjection(Frame&, const Frame&) (mono branch)
+//   src/ORBmatcher.cc:907-1146  SearchForTriangulation (mono, Pinhole), :2012-2053 ComputeThreeMaxima
+//   src/ORBmatcher.cc:2058-2074 DescriptorDistance
+//   src/CameraModels/Pinhole.cpp:35-41 project, :107-129 epipolarConstrain (F12 supplied by the caller)
+//   Thirdparty/Sophus/sophus/so3.hpp:358-367, se3.hpp:321-324 point action
+// Float expressions are evaluated as written, left to right, without contraction.
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../include/mam_match.h"
+
+namespace {
+
+int descDist(const uint8_t* a, const uint8_t* b) {
+    const uint32_t* pa = reinterpret_cast<const uint32_t*>(a);
+    const uint32_t* pb = reinterpret_cast<const uint32_t*>(b);
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        unsigned int v = pa[i] ^ pb[i];
+        v = v - ((v >> 1) & 0x55555555);
+        v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+        dist += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+    }
+    return dist;
+}
+
+struct FrameO {
+    const mam_frame_geom* g;
+    int N;
+    const mam_keypoint* keys;
+    std::vector<size_t> grid[MAM_GRID_COLS][MAM_GRID_ROWS];
+
+    FrameO(const mam_frame_geom* g_, int n, const mam_keypoint* k) : g(g_), N(n), keys(k) {
+        for (int i = 0; i < N; i++) {
+            int posX, posY;
+            if (PosInGrid(keys[i], posX, posY)) grid[posX][posY].push_back(i);
+        }
+    }
+    bool PosInGrid(const mam_keypoint& kp, int& posX, int& posY) const {
+        posX = (int)roundf((kp.x - g->min_x) * g->grid_inv_w);
+        posY = (int)roundf((kp.y - g->min_y) * g->grid_inv_h);
+        if (posX < 0 || posX >= MAM_GRID_COLS || posY < 0 || posY >= MAM_GRID_ROWS) return false;
+        return true;
+    }
+    std::vector<size_t> GetFeaturesInArea(float x, float y, float r, int minLevel, int maxLevel) const {
+        std::vector<size_t> vIndices;
+        const float factorX = r, factorY = r;
+        const int nMinCellX = std::max(0, (int)floorf((x - g->min_x - factorX) * g->grid_inv_w));
+        if (nMinCellX >= MAM_GRID_COLS) return vIndices;
+        const int nMaxCellX = std::min(MAM_GRID_COLS - 1, (int)ceilf((x - g->min_x + factorX) * g->grid_inv_w));
+        if (nMaxCellX < 0) return vIndices;
+        const int nMinCellY = std::max(0, (int)floorf((y - g->min_y - factorY) * g->grid_inv_h));
+        if (nMinCellY >= MAM_GRID_ROWS) return vIndices;
+        const int nMaxCellY = std::min(MAM_GRID_ROWS - 1, (int)ceilf((y - g->min_y + factorY) * g->grid_inv_h));
+        if (nMaxCellY < 0) return vIndices;
+        const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+                const std::vector<size_t>& vCell = grid[ix][iy];
+                for (size_t j = 0; j < vCell.size(); j++) {
+                    const mam_keypoint& kpUn = keys[vCell[j]];
+                    if (bCheckLevels) {
+                        if (kpUn.octave < minLevel) continue;
+                        if (maxLevel >= 0 && kpUn.octave > maxLevel) continue;
+                    }
+                    const float distx = kpUn.x - x;
+                    const float disty = kpUn.y - y;
+                    if (fabsf(distx) < factorX && fabsf(disty) < factorY) vIndices.push_back(vCell[j]);
+                }
+            }
+        }
+        return vIndices;
+    }
+};
+
+void ComputeThreeMaxima(const std::vector<int>* histo, const int L, int& ind1, int& ind2, int& ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < L; i++) {
+        const int s = (int)histo[i].size();
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+// Sophus SE3f point action: so3() * p + translation(), so3()*p = p + w*uv + q.vec() x uv, uv = 2 q.vec() x p
+void se3Apply(const mam_pose* T, const float p[3], float out[3]) {
+    const float qx = T->q[0], qy = T->q[1], qz = T->q[2], qw = T->q[3];
+    float uv[3] = {qy * p[2] - qz * p[1], qz * p[0] - qx * p[2], qx * p[1] - qy * p[0]};
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    const float cx = qy * uv[2] - qz * uv[1], cy = qz * uv[0] - qx * uv[2], cz = qx * uv[1] - qy * uv[0];
+    out[0] = ((p[0] + qw * uv[0]) + cx) + T->t[0];
+    out[1] = ((p[1] + qw * uv[1]) + cy) + T->t[1];
+    out[2] = ((p[2] + qw * uv[2]) + cz) + T->t[2];
+}
+
+int roundBin(float rot) {
+    const float factor = 1.0f / MAM_HISTO_LENGTH;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == MAM_HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descDist(a, b); }
+
+int oracle_search_by_projection(const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc,
+                                const uint8_t* taken_in, int n_mps, const mam_mp_track* mps, float th,
+                                int far_points, float th_far_points, float nnratio, int32_t* out) {
+    FrameO F(g, n, keys);
+    std::vector<uint8_t> taken(n, 0);
+    if (taken_in) memcpy(taken.data(), taken_in, n);
+    for (int i = 0; i < n; i++) out[i] = -1;
+    int nmatches = 0;
+    const bool bFactor = th != 1.0;
+    for (int iMP = 0; iMP < n_mps; iMP++) {
+        const mam_mp_track& mp = mps[iMP];
+        if (!mp.track_in_view) continue;   // mbTrackInViewR is false for mono frames
+        if (far_points && mp.track_depth > th_far_points) continue;
+        if (mp.is_bad) continue;
+        const int nPredictedLevel = mp.scale_level;
+        float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos
+        if (bFactor) r *= th;
+        const std::vector<size_t> vIndices =
+            F.GetFeaturesInArea(mp.proj_x, mp.proj_y, r * g->scale_factors[nPredictedLevel], nPredictedLevel - 1,
+                                nPredictedLevel);
+        if (vIndices.empty()) continue;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (size_t idx : vIndices) {
+            if (taken[idx]) continue;          // mvpMapPoints[idx] && Observations() > 0
+            const int dist = descDist(mp.desc, desc + idx * 32);
+            if (dist < bestDist) {
+                bestDist2 = bestDist; bestDist = dist;
+                bestLevel2 = bestLevel; bestLevel = keys[idx].octave;
+                bestIdx = (int)idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = keys[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= MAM_TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            out[bestIdx] = iMP;
+            if (mp.nobs > 0) taken[bestIdx] = 1;
+            nmatches++;
+        }
+    }
+    return nmatches;
+}
+
+int oracle_search_by_projection_motion(const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc,
+                                       const uint8_t* taken_in, const mam_pose* tcw, const mam_pinhole* cam,
+                                       int n_last, const mam_last_entry* last, float th, int check_ori,
+                                       int32_t* out) {
+    FrameO F(g, n, keys);
+    std::vector<uint8_t> taken(n, 0);
+    if (taken_in) memcpy(taken.data(), taken_in, n);
+    for (int i = 0; i < n; i++) out[i] = -1;
+    std::vector<int> rotHist[MAM_HISTO_LENGTH];
+    int nmatches = 0;
+    for (int i = 0; i < n_last; i++) {
+        const mam_last_entry& L = last[i];
+        if (!L.valid) continue;
+        float x3Dc[3];
+        se3Apply(tcw, L.pos, x3Dc);
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        if (invzc < 0) continue;
+        const float u = cam->fx * x3Dc[0] / x3Dc[2] + cam->cx;
+        const float v = cam->fy * x3Dc[1] / x3Dc[2] + cam->cy;
+        if (u < g->min_x || u > g->max_x) continue;
+        if (v < g->min_y || v > g->max_y) continue;
+        const int nLastOctave = L.octave;
+        const float radius = th * g->scale_factors[nLastOctave];
+        const std::vector<size_t> vIndices2 = F.GetFeaturesInArea(u, v, radius, nLastOctave - 1, nLastOctave + 1);
+        if (vIndices2.empty()) continue;
+        int bestDist = 256, bestIdx2 = -1;
+        for (size_t i2 : vIndices2) {
+            if (taken[i2]) continue;
+            const int dist = descDist(L.desc, desc + i2 * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = (int)i2; }
+        }
+        if (bestDist <= MAM_TH_HIGH) {
+            out[bestIdx2] = i;
+            if (L.nobs > 0) taken[bestIdx2] = 1;
+            nmatches++;
+            if (check_ori) rotHist[roundBin(L.angle - keys[bestIdx2].angle)].push_back(bestIdx2);
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ComputeThreeMaxima(rotHist, MAM_HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < MAM_HISTO_LENGTH; i++) {
+            if (i != ind1 && i != ind2 && i != ind3) {
+                for (size_t j = 0; j < rotHist[i].size(); j++) {
+                    out[rotHist[i][j]] = -1;
+                    nmatches--;
+                }
+            }
+        }
+    }
+    return nmatches;
+}
+
+int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_keypoint* keys1, const uint8_t* desc1,
+                                    const uint8_t* has_mp1, const mam_featvec* fv1, int n2,
+                                    const mam_keypoint* keys2, const uint8_t* desc2, const uint8_t* has_mp2,
+                                    const mam_featvec* fv2, const float* F12, const float* ep, int check_ori,
+                                    int coarse, int32_t* out) {
+    (void)n2;
+    std::vector<int> rotHist[MAM_HISTO_LENGTH];
+    for (int i = 0; i < n1; i++) out[i] = -1;
+    int nmatches = 0;
+    int a1 = 0, a2 = 0;
+    // F12 row-major: F(r,c) = F12[3r+c]
+    auto F = [&](int r, int c) { return F12[3 * r + c]; };
+    while (a1 < fv1->n_nodes && a2 < fv2->n_nodes) {
+        const uint32_t id1 = fv1->node_ids[a1], id2 = fv2->node_ids[a2];
+        if (id1 == id2) {
+            for (int i1 = fv1->node_off[a1]; i1 < fv1->node_off[a1 + 1]; i1++) {
+                const uint32_t idx1 = fv1->feats[i1];
+                if (has_mp1[idx1]) continue;
+                const mam_keypoint& kp1 = keys1[idx1];
+                int bestDist = MAM_TH_LOW, bestIdx2 = -1;
+                for (int i2 = fv2->node_off[a2]; i2 < fv2->node_off[a2 + 1]; i2++) {
+                    const uint32_t idx2 = fv2->feats[i2];
+                    if (has_mp2[idx2]) continue;
+                    const int dist = descDist(desc1 + (size_t)idx1 * 32, desc2 + (size_t)idx2 * 32);
+                    if (dist > MAM_TH_LOW || dist > bestDist) continue;
+                    const mam_keypoint& kp2 = keys2[idx2];
+                    const float distex = ep[0] - kp2.x;
+                    const float distey = ep[1] - kp2.y;
+                    if (distex * distex + distey * distey < 100 * g->scale_factors[kp2.octave]) continue;
+                    bool ok = coarse != 0;
+                    if (!ok) {
+                        const float a = kp1.x * F(0, 0) + kp1.y * F(1, 0) + F(2, 0);
+                        const float b = kp1.x * F(0, 1) + kp1.y * F(1, 1) + F(2, 1);
+                        const float c = kp1.x * F(0, 2) + kp1.y * F(1, 2) + F(2, 2);
+                        const float num = a * kp2.x + b * kp2.y + c;
+                        const float den = a * a + b * b;
+                        if (den == 0) ok = false;
+                        else {
+                            const float dsqr = num * num / den;
+                            ok = dsqr < 3.84 * g->level_sigma2[kp2.octave];
+                        }
+                    }
+                    if (ok) { bestIdx2 = (int)idx2; bestDist = dist; }
+                }
+                if (bestIdx2 >= 0) {
+                    out[idx1] = bestIdx2;
+                    nmatches++;
+                    if (check_ori) rotHist[roundBin(kp1.angle - keys2[bestIdx2].angle)].push_back((int)idx1);
+                }
+            }
+            a1++;
+            a2++;
+        } else if (id1 < id2) {
+            while (a1 < fv1->n_nodes && fv1->node_ids[a1] < id2) a1++;   // lower_bound
+        } else {
+            while (a2 < fv2->n_nodes && fv2->node_ids[a2] < id1) a2++;
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ComputeThreeMaxima(rotHist, MAM_HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < MAM_HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (size_t j = 0; j < rotHist[i].size(); j++) {
+                out[rotHist[i][j]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    return nmatches;
+}
+
+}  // extern "C"

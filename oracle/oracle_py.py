@@ -176,3 +176,85 @@ def std_sort_pairs(keys: np.ndarray, payload: np.ndarray):
 def unpack(packed: np.ndarray):
     packed = np.asarray(packed, dtype=np.uint32)
     return packed & 0xFFF, (packed >> 12) & 0xFFF, packed >> 24
+
+
+# ---------------------------------------------------------------- matcher oracle (oracle/match_oracle.cpp)
+def _vp(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def descriptor_distance(a, b) -> int:
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return int(lib().oracle_descriptor_distance(_vp(a), _vp(b)))
+
+
+def search_by_projection(F, mps, th, far_points=False, th_far=50.0, nnratio=0.8):
+    """F: mam3slam_amd.match.FrameData; mps: MP_TRACK_DTYPE array. Returns (nmatches, kp_to_mp)."""
+    from mam3slam_amd.match import KP_DTYPE, MP_TRACK_DTYPE
+
+    L = lib()
+    L.oracle_search_by_projection.restype = C.c_int
+    L.oracle_search_by_projection.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                              C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_float, C.c_void_p]
+    keys = np.ascontiguousarray(F.keys, KP_DTYPE)
+    desc = np.ascontiguousarray(F.desc, np.uint8)
+    taken = None if F.taken is None else np.ascontiguousarray(F.taken, np.uint8)
+    mps = np.ascontiguousarray(mps, MP_TRACK_DTYPE)
+    out = np.full(max(len(keys), 1), -1, np.int32)
+    g = F.geom()
+    n = L.oracle_search_by_projection(C.byref(g), len(keys), _vp(keys), _vp(desc), _vp(taken), len(mps), _vp(mps),
+                                      float(th), int(far_points), float(th_far), float(nnratio), _vp(out))
+    return n, out[:len(keys)]
+
+
+def search_by_projection_motion(F, last, cam, th, check_ori=True):
+    from mam3slam_amd.match import KP_DTYPE, LAST_ENTRY_DTYPE, Pose
+
+    L = lib()
+    L.oracle_search_by_projection_motion.restype = C.c_int
+    L.oracle_search_by_projection_motion.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                     C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_float, C.c_int,
+                                                     C.c_void_p]
+    keys = np.ascontiguousarray(F.keys, KP_DTYPE)
+    desc = np.ascontiguousarray(F.desc, np.uint8)
+    taken = None if F.taken is None else np.ascontiguousarray(F.taken, np.uint8)
+    last = np.ascontiguousarray(last, LAST_ENTRY_DTYPE)
+    pose = Pose()
+    for i in range(4):
+        pose.q[i] = float(F.pose[0][i])
+    for i in range(3):
+        pose.t[i] = float(F.pose[1][i])
+    out = np.full(max(len(keys), 1), -1, np.int32)
+    g = F.geom()
+    n = L.oracle_search_by_projection_motion(C.byref(g), len(keys), _vp(keys), _vp(desc), _vp(taken), C.byref(pose),
+                                             C.byref(cam), len(last), _vp(last), float(th), int(check_ori), _vp(out))
+    return n, out[:len(keys)]
+
+
+def search_for_triangulation(KF1, KF2, F12, ep, check_ori=False, coarse=False):
+    from mam3slam_amd.match import KP_DTYPE, FeatVec, flatten_featvec
+
+    L = lib()
+    L.oracle_search_for_triangulation.restype = C.c_int
+    L.oracle_search_for_triangulation.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                  C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                  C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    k1 = np.ascontiguousarray(KF1.keys, KP_DTYPE)
+    k2 = np.ascontiguousarray(KF2.keys, KP_DTYPE)
+    d1 = np.ascontiguousarray(KF1.desc, np.uint8)
+    d2 = np.ascontiguousarray(KF2.desc, np.uint8)
+    h1 = np.ascontiguousarray(KF1.has_mp, np.uint8)
+    h2 = np.ascontiguousarray(KF2.has_mp, np.uint8)
+    i1, o1, f1 = flatten_featvec(KF1.featvec)
+    i2, o2, f2 = flatten_featvec(KF2.featvec)
+    fv1 = FeatVec(len(i1), i1.ctypes.data, o1.ctypes.data, f1.ctypes.data)
+    fv2 = FeatVec(len(i2), i2.ctypes.data, o2.ctypes.data, f2.ctypes.data)
+    F12 = np.ascontiguousarray(F12, np.float32).reshape(9)
+    ep = np.ascontiguousarray(ep, np.float32).reshape(2)
+    out = np.full(max(len(k1), 1), -1, np.int32)
+    g = KF2.geom()
+    n = L.oracle_search_for_triangulation(C.byref(g), len(k1), _vp(k1), _vp(d1), _vp(h1), C.byref(fv1), len(k2),
+                                          _vp(k2), _vp(d2), _vp(h2), C.byref(fv2), _vp(F12), _vp(ep), int(check_ori),
+                                          int(coarse), _vp(out))
+    return n, out[:len(k1)]

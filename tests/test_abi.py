@@ -24,10 +24,10 @@ def test_library_exports_every_declared_symbol():
 
     L = _lib.lib()  # builds with hipcc if missing; loads without a GPU
     declared = _declared()
-    assert len(declared) >= 14
+    assert len(declared) >= 24
     missing = [n for n in declared if not hasattr(L, n)]
     assert not missing, f"declared but not exported: {missing}"
-    unbound = [n for n in declared if n not in _lib.SIGNATURES]
+    unbound = [n for n in declared if n not in _lib.all_signatures()]
     assert not unbound, f"declared but no ctypes signature in mam3slam_amd/_lib.py: {unbound}"
 
 

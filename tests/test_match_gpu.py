@@ -1,0 +1,160 @@
+"""GPU parity: ORBmatcher hot-path searches (HIP via the C-ABI) vs the CPU oracle — index-exact.
+
+Inputs are real ORB features (oracle extraction of seeded synthetic frames) wrapped in synthetic map
+structures (mam3slam_amd/scene.py) that exercise the reference's control flow: greedy keypoint taking
+(ORBmatcher.cc:88-90, 1747-1749), duplicate MapPoints, pre-taken keypoints, ratio test, rotation histogram
+(:1855-1884), "last equal wins" in SearchForTriangulation (:1017).
+"""
+import numpy as np
+import pytest
+
+from mam3slam_amd import scene, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def frames(oracle):
+    out = []
+    for (w, h, nf, fr) in [(640, 480, 1000, 0), (640, 480, 1000, 7), (1280, 720, 2000, 3)]:
+        img = synth.make_frame(w, h, agent=5, frame=fr)
+        k, d, _ = oracle.extract(img, oracle.params(nf))
+        out.append((w, h, k, d))
+    return out
+
+
+def _matcher(nnratio=0.8, ori=True):
+    from mam3slam_amd.match import ORBmatcher
+
+    return ORBmatcher(nnratio, ori)
+
+
+def test_descriptor_distance(gpu_lib, oracle):
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, (4096, 32), dtype=np.uint8)
+    b = rng.integers(0, 256, (4096, 32), dtype=np.uint8)
+    b[:10] = a[:10]
+    b[10:20] = ~a[10:20]
+    got = _matcher().DescriptorDistance(a, b)
+    ref = np.array([oracle.descriptor_distance(a[i], b[i]) for i in range(len(a))])
+    assert np.array_equal(got, ref)
+    assert (got[:10] == 0).all() and (got[10:20] == 256).all()
+
+
+@pytest.mark.parametrize("fi", [0, 1, 2])
+@pytest.mark.parametrize("th", [1, 3, 15])
+def test_search_by_projection_local(gpu_lib, oracle, frames, fi, th):
+    w, h, k, d = frames[fi]
+    M = _matcher(0.8)
+    for seed in range(3):
+        rng = np.random.default_rng(100 * fi + seed)
+        F = scene.make_frame_data(k, d, w, h, rng, taken_frac=0.1 * seed)
+        mps = scene.local_mappoints(F, rng)
+        far = seed == 2
+        ng, og = M.SearchByProjection(F, mps, th, far, 30.0)
+        no, oo = oracle.search_by_projection(F, mps, th, far, 30.0, 0.8)
+        assert ng == no, (seed, ng, no)
+        diff = np.nonzero(og != oo)[0]
+        assert len(diff) == 0, f"seed {seed}: {len(diff)} keypoints differ, first {diff[:5]} gpu={og[diff[:5]]} " \
+                               f"oracle={oo[diff[:5]]}"
+
+
+def test_search_by_projection_nnratio_and_edges(gpu_lib, oracle, frames):
+    w, h, k, d = frames[0]
+    rng = np.random.default_rng(9)
+    F = scene.make_frame_data(k, d, w, h, rng)
+    mps = scene.local_mappoints(F, rng, kflip=40)
+    for nn in (0.6, 0.9, 1.0):
+        M = _matcher(nn)
+        ng, og = M.SearchByProjection(F, mps, 5)
+        no, oo = oracle.search_by_projection(F, mps, 5, nnratio=nn)
+        assert ng == no and np.array_equal(og, oo), nn
+    M = _matcher(0.8)
+    # every keypoint already taken -> no match; no MapPoints -> 0
+    F.taken = np.ones(len(k), np.uint8)
+    ng, og = M.SearchByProjection(F, mps, 3)
+    assert ng == 0 and (og == -1).all()
+    F.taken = None
+    ng, og = M.SearchByProjection(F, mps[:0], 3)
+    assert ng == 0 and (og == -1).all()
+
+
+@pytest.mark.parametrize("fi", [0, 2])
+@pytest.mark.parametrize("th,ori", [(7, True), (15, True), (15, False), (30, True)])
+def test_search_by_projection_motion(gpu_lib, oracle, frames, fi, th, ori):
+    w, h, k, d = frames[fi]
+    cam = scene.pinhole(w, h)
+    M = _matcher(0.9, ori)
+    for seed in range(3):
+        rng = np.random.default_rng(1000 + seed)
+        F = scene.make_frame_data(k, d, w, h, rng, taken_frac=0.05 * seed)
+        F.pose = scene.small_pose(rng)
+        last = scene.motion_last_frame(F, cam, rng)
+        ng, og = M.SearchByProjectionMotion(F, last, cam, th, True)
+        no, oo = oracle.search_by_projection_motion(F, last, cam, th, ori)
+        assert ng == no, (seed, ng, no)
+        diff = np.nonzero(og != oo)[0]
+        assert len(diff) == 0, f"seed {seed}: {len(diff)} differ, first {diff[:5]} gpu={og[diff[:5]]} oracle={oo[diff[:5]]}"
+
+
+@pytest.mark.parametrize("fi", [0, 1, 2])
+@pytest.mark.parametrize("ori,coarse", [(False, False), (True, False), (False, True)])
+def test_search_for_triangulation(gpu_lib, oracle, frames, fi, ori, coarse):
+    w, h, k, d = frames[fi]
+    cam = scene.pinhole(w, h)
+    M = _matcher(0.6, ori)
+    for seed in range(2):
+        rng = np.random.default_rng(2000 + seed)
+        F = scene.make_frame_data(k, d, w, h)
+        KF1, KF2, F12, ep = scene.keyframe_pair(F, cam, rng)
+        ng, pairs = M.SearchForTriangulation(KF1, KF2, F12, ep, False, coarse)
+        no, oo = oracle.search_for_triangulation(KF1, KF2, F12, ep, ori, coarse)
+        ref_pairs = np.stack([np.nonzero(oo >= 0)[0], oo[oo >= 0]], 1)
+        assert ng == no
+        assert np.array_equal(pairs, ref_pairs)
+
+
+def test_projection_batch_device(gpu_lib, oracle, frames):
+    import torch
+
+    from mam3slam_amd.match import MP_TRACK_DTYPE, FramesDev
+
+    w, h, k, d = frames[0]
+    Fn = 5
+    M = _matcher(0.8)
+    S = 1100
+    keys = np.zeros((Fn, S), k.dtype)
+    desc = np.zeros((Fn, S, 32), np.uint8)
+    counts = np.zeros((Fn, 2), np.int32)
+    mp_list, FD = [], []
+    for f in range(Fn):
+        rng = np.random.default_rng(50 + f)
+        sel = np.sort(rng.choice(len(k), size=len(k) - 7 * f, replace=False))
+        F = scene.make_frame_data(k[sel], d[sel], w, h)
+        keys[f, :len(sel)] = F.keys
+        desc[f, :len(sel)] = F.desc
+        counts[f, 0] = len(sel)
+        mp_list.append(scene.local_mappoints(F, rng))
+        FD.append(F)
+    ms = max(len(m) for m in mp_list)
+    mps = np.zeros((Fn, ms), MP_TRACK_DTYPE)
+    nmps = np.array([len(m) for m in mp_list], np.int32)
+    for f in range(Fn):
+        mps[f, :nmps[f]] = mp_list[f]
+    dev = torch.device("cuda")
+    t_keys = torch.from_numpy(keys.view(np.uint8).reshape(Fn, -1)).to(dev)
+    t_desc = torch.from_numpy(desc).to(dev)
+    t_cnt = torch.from_numpy(counts).to(dev)
+    t_mps = torch.from_numpy(mps.view(np.uint8).reshape(Fn, -1)).to(dev)
+    t_nmps = torch.from_numpy(nmps).to(dev)
+    t_out = torch.zeros((Fn, S), dtype=torch.int32, device=dev)
+    t_nm = torch.zeros(Fn, dtype=torch.int32, device=dev)
+    fr = FramesDev(Fn, S, t_keys.data_ptr(), t_desc.data_ptr(), t_cnt.data_ptr(), None)
+    M.search_by_projection_batch_device(FD[0], fr, t_mps.data_ptr(), ms, t_nmps.data_ptr(), 3.0, t_out.data_ptr(),
+                                        t_nm.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out, nm = t_out.cpu().numpy(), t_nm.cpu().numpy()
+    for f in range(Fn):
+        no, oo = oracle.search_by_projection(FD[f], mp_list[f], 3.0, nnratio=0.8)
+        assert nm[f] == no
+        assert np.array_equal(out[f, :counts[f, 0]], oo)
