@@ -1,0 +1,84 @@
+/*
+ * mam_lba.h — C-ABI drop-in boundary for Optimizer::LocalBundleAdjustment's solve (gfx950 / MI355X).
+ *
+ * Replaces the g2o section of the reference call (src/Optimizer.cc:1188-1410):
+ *   g2o::SparseOptimizer + BlockSolver_6_3 + LinearSolverEigen + OptimizationAlgorithmLevenberg,
+ *   VertexSE3Expmap / VertexSBAPointXYZ vertices, EdgeSE3ProjectXYZ mono edges with RobustKernelHuber,
+ *   optimizer.initializeOptimization(); optimizer.optimize(10); and the per-edge chi2()/isDepthPositive()
+ *   read-back used for outlier rejection (:1413-1460).
+ * g2o sources followed: core/optimization_algorithm_levenberg.cpp:61-194, core/block_solver.hpp:353-604,
+ *   core/base_binary_edge.hpp:54-120, core/robust_kernel_impl.cpp:76-91, core/sparse_optimizer.cpp:166-190,
+ *   355-436, types/se3quat.h, types/types_six_dof_expmap.h:73-76, src/OptimizableTypes.cpp:139-160,
+ *   src/CameraModels/Pinhole.cpp:35-81.
+ *
+ * The window construction (local / fixed keyframes, local MapPoints), the outlier erase and the write-back
+ * under Map::mMutexMapUpdate stay in the host wrapper (mam3slam_amd/lba.py, the analogue of Optimizer.cc:1118-
+ * 1186 and :1463-1497), exactly as SURVEY.md §8(b) assigns them.
+ */
+#ifndef MAM_LBA_H
+#define MAM_LBA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The g2o graph in reference order. Poses: every KeyFrame vertex (local then fixed, any order); the Hessian
+ * column order (g2o _ivMap) is recovered from pose_id / point_id (vertices sorted by id, non-fixed poses
+ * first, then points), so callers pass ids exactly as the reference assigns them (KF mnId; MapPoint
+ * mnId+maxKFid+1). Edges: insertion order (Optimizer.cc:1252-1331). Doubles are the float map values cast
+ * to double, as the reference does (Optimizer.cc:1218, 1235, 1286). */
+typedef struct mam_lba_problem {
+    int32_t n_poses;
+    const int64_t* pose_id;        /* vertex id */
+    const uint8_t* pose_fixed;     /* setFixed: init KF / fixed cameras */
+    const double* pose_q;          /* [n_poses][4] unit quaternion x, y, z, w (Tcw) */
+    const double* pose_t;          /* [n_poses][3] */
+    const int32_t* pose_cam;       /* [n_poses] index into cams (NULL = camera 0) */
+    int32_t n_points;
+    const int64_t* point_id;
+    const double* point_xyz;       /* [n_points][3] */
+    int32_t n_edges;
+    const int32_t* edge_point;     /* vertex 0 (index into points) */
+    const int32_t* edge_pose;      /* vertex 1 (index into poses) */
+    const double* edge_obs;        /* [n_edges][2] keypoint (mvKeysUn) */
+    const double* edge_inv_sigma2; /* information = invSigma2 * I2 */
+    int32_t n_cams;
+    const float* cams;             /* [n_cams][4] Pinhole fx, fy, cx, cy (mvParameters, float) */
+    double huber_delta;            /* (double)(float)sqrt(5.991) */
+    int32_t iterations;            /* optimize(10) */
+} mam_lba_problem;
+
+typedef struct mam_lba_result {
+    double* pose_q;                /* [n_poses][4] (fixed poses copied through) */
+    double* pose_t;                /* [n_poses][3] */
+    double* point_xyz;             /* [n_points][3] */
+    double* edge_chi2;             /* [n_edges] chi2() after optimisation (may be NULL) */
+    uint8_t* edge_depth_ok;        /* [n_edges] isDepthPositive() (may be NULL) */
+    int32_t iterations;            /* optimize() return: iterations run */
+    int32_t lm_trials;             /* total Levenberg trials */
+    double initial_chi2;           /* activeRobustChi2 before the first step */
+    double final_chi2;             /* activeRobustChi2 at the end */
+    int32_t status;                /* 0 ok, 1 aborted by stop flag, <0 MAM_ERR_* */
+} mam_lba_result;
+
+typedef struct mam_lba_ctx mam_lba_ctx;
+
+int mam_lba_create(int device, mam_lba_ctx** out);
+void mam_lba_destroy(mam_lba_ctx* ctx);
+
+/* Host buffers in, host buffers out; synchronous. stop_flag (may be NULL) is polled between iterations and
+ * Levenberg trials like g2o's force-stop flag (sparse_optimizer.cpp:377, levenberg.cpp:149). */
+int mam_lba_solve(mam_lba_ctx* ctx, const mam_lba_problem* problem, const volatile int32_t* stop_flag,
+                  mam_lba_result* result);
+
+int mam_lba_set_profiling(mam_lba_ctx* ctx, int enable);
+/* [0] linearize+blocks, [1] Schur, [2] dense solve, [3] back-substitution+update+chi2 */
+int mam_lba_stage_times(mam_lba_ctx* ctx, double* ms_out, int64_t* launches_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAM_LBA_H */

@@ -54,9 +54,10 @@ SIGNATURES = {
 
 
 def _match_sigs():
+    from .lba import _SIGS as lba_sigs
     from .match import _SIGS
 
-    return _SIGS
+    return {**_SIGS, **lba_sigs}
 
 
 def lib() -> C.CDLL:

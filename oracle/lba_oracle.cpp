@@ -1,0 +1,497 @@
+// lba_oracle.cpp — TEST INFRASTRUCTURE ONLY (see orb_oracle.h header note).
+//
+// Single-threaded FP64 CPU restatement of the g2o solve inside Optimizer::LocalBundleAdjustment
+// (reference src/Optimizer.cc:1188-1410) with the vendored g2o it drives, step by step:
+//   core/sparse_optimizer.cpp:166-190  buildIndexMapping (non-fixed poses by id, then points by id)
+//   core/sparse_optimizer.cpp:355-436  optimize / update (oplus in _ivMap order)
+//   core/sparse_optimizer.cpp:61-114   computeActiveErrors / activeRobustChi2 (edge insertion order)
+//   core/optimization_algorithm_levenberg.cpp:61-194  LM trials, lambda init/update, scale, termination
+//   core/block_solver.hpp:353-604      Schur complement, back-substitution, setLambda / restoreDiagonal
+//   core/base_binary_edge.hpp:54-120   constructQuadraticForm (robust branch)
+//   core/robust_kernel_impl.cpp:76-91  Huber
+//   types/se3quat.h                    SE3Quat exp / map / product / normalizeRotation
+//   src/OptimizableTypes.{h:99-110, cpp:139-160}  EdgeSE3ProjectXYZ error / Jacobians
+//   src/CameraModels/Pinhole.cpp:35-41, 71-81      project / projectJac (float parameters)
+// Eigen's SimplicialLDLT with AMD ordering is replaced by a dense LDL^T of the reduced camera system with the
+// same failure rule (exact zero pivot); the difference is summation order only.
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <vector>
+
+#include "../include/mam_lba.h"
+#include "../include/mam_orb.h"
+
+namespace {
+
+struct Quat { double x, y, z, w; };
+struct SE3 { Quat r; double t[3]; };
+
+void normalizeRotation(SE3& T) {
+    if (T.r.w < 0) { T.r.x = -T.r.x; T.r.y = -T.r.y; T.r.z = -T.r.z; T.r.w = -T.r.w; }
+    const double n = std::sqrt(T.r.x * T.r.x + T.r.y * T.r.y + T.r.z * T.r.z + T.r.w * T.r.w);
+    T.r.x /= n; T.r.y /= n; T.r.z /= n; T.r.w /= n;
+}
+
+void cross(const double a[3], const double b[3], double o[3]) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Eigen QuaternionBase::_transformVector
+void quatRotate(const Quat& q, const double v[3], double o[3]) {
+    const double qv[3] = {q.x, q.y, q.z};
+    double uv[3];
+    cross(qv, v, uv);
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    double c[3];
+    cross(qv, uv, c);
+    for (int i = 0; i < 3; i++) o[i] = v[i] + q.w * uv[i] + c[i];
+}
+
+Quat quatMul(const Quat& a, const Quat& b) {
+    Quat r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    return r;
+}
+
+void toRotationMatrix(const Quat& q, double R[9]) {
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+// Eigen quaternion_assign_impl<Matrix3>
+Quat fromRotationMatrix(const double m[9]) {
+    Quat q;
+    const double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        double s = std::sqrt(t + 1.0);
+        q.w = 0.5 * s;
+        s = 0.5 / s;
+        q.x = (m[7] - m[5]) * s;
+        q.y = (m[2] - m[6]) * s;
+        q.z = (m[3] - m[1]) * s;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[3 * i + i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = std::sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
+        double c[3];
+        c[i] = 0.5 * s;
+        s = 0.5 / s;
+        q.w = (m[3 * k + j] - m[3 * j + k]) * s;
+        c[j] = (m[3 * j + i] + m[3 * i + j]) * s;
+        c[k] = (m[3 * k + i] + m[3 * i + k]) * s;
+        q.x = c[0]; q.y = c[1]; q.z = c[2];
+    }
+    return q;
+}
+
+void mat3mul(const double A[9], const double B[9], double C[9]) {
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+// SE3Quat::exp (se3quat.h)
+SE3 se3Exp(const double u[6]) {
+    const double omega[3] = {u[0], u[1], u[2]};
+    const double upsilon[3] = {u[3], u[4], u[5]};
+    const double theta = std::sqrt(omega[0] * omega[0] + omega[1] * omega[1] + omega[2] * omega[2]);
+    const double Om[9] = {0, -omega[2], omega[1], omega[2], 0, -omega[0], -omega[1], omega[0], 0};
+    double Om2[9];
+    mat3mul(Om, Om, Om2);
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = ((i % 4 == 0) ? 1.0 : 0.0) + Om[i] + Om2[i];
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        const double a = std::sin(theta) / theta;
+        const double b = (1 - std::cos(theta)) / (theta * theta);
+        const double c = (theta - std::sin(theta)) / std::pow(theta, 3);
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4 == 0) ? 1.0 : 0.0;
+            R[i] = I + a * Om[i] + b * Om2[i];
+            V[i] = I + b * Om[i] + c * Om2[i];
+        }
+    }
+    SE3 T;
+    T.r = fromRotationMatrix(R);
+    for (int i = 0; i < 3; i++) T.t[i] = V[3 * i] * upsilon[0] + V[3 * i + 1] * upsilon[1] + V[3 * i + 2] * upsilon[2];
+    normalizeRotation(T);
+    return T;
+}
+
+// SE3Quat::operator*
+SE3 se3Mul(const SE3& a, const SE3& b) {
+    SE3 r = a;
+    double rt[3];
+    quatRotate(a.r, b.t, rt);
+    for (int i = 0; i < 3; i++) r.t[i] += rt[i];
+    r.r = quatMul(a.r, b.r);
+    normalizeRotation(r);
+    return r;
+}
+
+void se3Map(const SE3& T, const double X[3], double o[3]) {
+    quatRotate(T.r, X, o);
+    for (int i = 0; i < 3; i++) o[i] += T.t[i];
+}
+
+struct Graph {
+    const mam_lba_problem* p;
+    std::vector<SE3> pose;
+    std::vector<double> pt;                // 3 per point
+    std::vector<int> pose_h;               // Hessian block of pose (-1 fixed)
+    std::vector<int> point_h;              // Hessian block of point
+    std::vector<int> hpose;                // inverse: Hessian pose block -> pose index
+    std::vector<int> hpoint;
+    int Np = 0, Nl = 0;
+    // per-edge state
+    std::vector<double> err;               // 2 per edge (last computeActiveErrors)
+    // system
+    std::vector<double> Hpp;               // 36 per Hessian pose
+    std::vector<double> Hll;               // 9 per point
+    std::vector<double> Hpl;               // 18 per edge: pose x landmark (6x3), row-major
+    std::vector<double> b;                 // 6 Np + 3 Nl
+    std::vector<double> x;
+
+    const float* cam(int pose_idx) const {
+        const int c = p->pose_cam ? p->pose_cam[pose_idx] : 0;
+        return p->cams + 4 * c;
+    }
+
+    void computeActiveErrors() {
+        for (int e = 0; e < p->n_edges; e++) {
+            const int ip = p->edge_pose[e], il = p->edge_point[e];
+            double Xc[3];
+            se3Map(pose[ip], &pt[3 * il], Xc);
+            const float* c = cam(ip);
+            const double u = c[0] * Xc[0] / Xc[2] + c[2];
+            const double v = c[1] * Xc[1] / Xc[2] + c[3];
+            err[2 * e] = p->edge_obs[2 * e] - u;
+            err[2 * e + 1] = p->edge_obs[2 * e + 1] - v;
+        }
+    }
+    double chi2(int e) const {
+        const double w = p->edge_inv_sigma2[e];
+        const double e0 = err[2 * e], e1 = err[2 * e + 1];
+        return e0 * (w * e0) + e1 * (w * e1);
+    }
+    void robustify(double e, double rho[3]) const {
+        const double delta = p->huber_delta, dsqr = delta * delta;
+        if (e <= dsqr) { rho[0] = e; rho[1] = 1.; rho[2] = 0.; }
+        else {
+            const double sqrte = std::sqrt(e);
+            rho[0] = 2 * sqrte * delta - dsqr;
+            rho[1] = delta / sqrte;
+            rho[2] = -0.5 * rho[1] / e;
+        }
+    }
+    double activeRobustChi2() const {
+        double chi = 0.0, rho[3];
+        for (int e = 0; e < p->n_edges; e++) {
+            robustify(chi2(e), rho);
+            chi += rho[0];
+        }
+        return chi;
+    }
+
+    void buildSystem() {
+        std::fill(Hpp.begin(), Hpp.end(), 0.0);
+        std::fill(Hll.begin(), Hll.end(), 0.0);
+        std::fill(Hpl.begin(), Hpl.end(), 0.0);
+        std::fill(b.begin(), b.end(), 0.0);
+        for (int e = 0; e < p->n_edges; e++) {
+            const int ip = p->edge_pose[e], il = p->edge_point[e];
+            const SE3& T = pose[ip];
+            double Xc[3];
+            se3Map(T, &pt[3 * il], Xc);
+            const double x = Xc[0], y = Xc[1], z = Xc[2];
+            const float* c = cam(ip);
+            // -projectJac (Pinhole.cpp:71-81)
+            const double J[6] = {-(c[0] / z), -0.0, -(-c[0] * x / (z * z)), -0.0, -(c[1] / z), -(-c[1] * y / (z * z))};
+            double R[9];
+            toRotationMatrix(T.r, R);
+            double A[6];   // 2x3 jacobianOplusXi = J R
+            for (int r = 0; r < 2; r++)
+                for (int k = 0; k < 3; k++)
+                    A[3 * r + k] = J[3 * r] * R[k] + J[3 * r + 1] * R[3 + k] + J[3 * r + 2] * R[6 + k];
+            const double D[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
+            double B[12];  // 2x6 jacobianOplusXj = J * SE3deriv
+            for (int r = 0; r < 2; r++)
+                for (int k = 0; k < 6; k++)
+                    B[6 * r + k] = J[3 * r] * D[k] + J[3 * r + 1] * D[6 + k] + J[3 * r + 2] * D[12 + k];
+            // robust branch of constructQuadraticForm
+            const double w = p->edge_inv_sigma2[e];
+            double rho[3];
+            robustify(chi2(e), rho);
+            const double orr[2] = {-(w * err[2 * e]) * rho[1], -(w * err[2 * e + 1]) * rho[1]};
+            const double wo = rho[1] * w;   // weightedOmega = rho1 * invSigma2 * I
+            const int hl = point_h[il];
+            double* bl = &b[6 * Np + 3 * hl];
+            double* Hl = &Hll[9 * hl];
+            for (int i = 0; i < 3; i++) {
+                bl[i] += A[i] * orr[0] + A[3 + i] * orr[1];
+                for (int j = 0; j < 3; j++) Hl[3 * i + j] += A[i] * wo * A[j] + A[3 + i] * wo * A[3 + j];
+            }
+            const int hp = pose_h[ip];
+            if (hp >= 0) {
+                double* He = &Hpl[18 * e];   // pose x landmark = B^T W A
+                for (int i = 0; i < 6; i++)
+                    for (int j = 0; j < 3; j++) He[3 * i + j] += B[i] * wo * A[j] + B[6 + i] * wo * A[3 + j];
+                double* bp = &b[6 * hp];
+                double* Hp = &Hpp[36 * hp];
+                for (int i = 0; i < 6; i++) {
+                    bp[i] += B[i] * orr[0] + B[6 + i] * orr[1];
+                    for (int j = 0; j < 6; j++) Hp[6 * i + j] += B[i] * wo * B[j] + B[6 + i] * wo * B[6 + j];
+                }
+            }
+        }
+    }
+
+    double computeLambdaInit() const {
+        double maxDiagonal = 0.;
+        for (int h = 0; h < Np; h++)
+            for (int j = 0; j < 6; j++) maxDiagonal = std::max(std::fabs(Hpp[36 * h + 7 * j]), maxDiagonal);
+        for (int h = 0; h < Nl; h++)
+            for (int j = 0; j < 3; j++) maxDiagonal = std::max(std::fabs(Hll[9 * h + 4 * j]), maxDiagonal);
+        return 1e-5 * maxDiagonal;
+    }
+
+    static bool inv3(const double m[9], double o[9]) {
+        const double c00 = m[4] * m[8] - m[5] * m[7], c01 = m[5] * m[6] - m[3] * m[8], c02 = m[3] * m[7] - m[4] * m[6];
+        const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
+        o[0] = c00 / det; o[3] = c01 / det; o[6] = c02 / det;
+        o[1] = (m[2] * m[7] - m[1] * m[8]) / det; o[4] = (m[0] * m[8] - m[2] * m[6]) / det;
+        o[7] = (m[1] * m[6] - m[0] * m[7]) / det;
+        o[2] = (m[1] * m[5] - m[2] * m[4]) / det; o[5] = (m[2] * m[3] - m[0] * m[5]) / det;
+        o[8] = (m[0] * m[4] - m[1] * m[3]) / det;
+        return true;
+    }
+
+    // BlockSolver::setLambda + solve (Schur) + restoreDiagonal
+    bool solve(double lambda, const std::vector<std::vector<int>>& point_edges) {
+        const int n = 6 * Np;
+        std::vector<double> S((size_t)n * n, 0.0), bs(n);
+        for (int h = 0; h < Np; h++)
+            for (int i = 0; i < 6; i++)
+                for (int j = 0; j < 6; j++) S[(size_t)(6 * h + i) * n + 6 * h + j] = Hpp[36 * h + 6 * i + j] + (i == j ? lambda : 0.0);
+        std::vector<double> coeff(n, 0.0), Dinv(9 * (size_t)Nl);
+        for (int hl = 0; hl < Nl; hl++) {
+            const int il = hpoint[hl];
+            double D[9];
+            for (int k = 0; k < 9; k++) D[k] = Hll[9 * hl + k] + ((k % 4 == 0) ? lambda : 0.0);
+            double* Di = &Dinv[9 * (size_t)hl];
+            inv3(D, Di);
+            const double* bl = &b[n + 3 * hl];
+            double db[3];
+            for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
+            const std::vector<int>& E = point_edges[il];
+            for (size_t a = 0; a < E.size(); a++) {
+                const int ea = E[a], ha = pose_h[p->edge_pose[ea]];
+                if (ha < 0) continue;
+                const double* Ba = &Hpl[18 * (size_t)ea];
+                double BDinv[18];
+                for (int i = 0; i < 6; i++)
+                    for (int j = 0; j < 3; j++)
+                        BDinv[3 * i + j] = Ba[3 * i] * Di[j] + Ba[3 * i + 1] * Di[3 + j] + Ba[3 * i + 2] * Di[6 + j];
+                for (int i = 0; i < 6; i++) coeff[6 * ha + i] += Ba[3 * i] * db[0] + Ba[3 * i + 1] * db[1] + Ba[3 * i + 2] * db[2];
+                for (size_t c = 0; c < E.size(); c++) {
+                    const int ec = E[c], hc = pose_h[p->edge_pose[ec]];
+                    if (hc < 0 || hc < ha) continue;   // upper blocks (i2 >= i1)
+                    const double* Bc = &Hpl[18 * (size_t)ec];
+                    for (int i = 0; i < 6; i++)
+                        for (int j = 0; j < 6; j++)
+                            S[(size_t)(6 * ha + i) * n + 6 * hc + j] -=
+                                BDinv[3 * i] * Bc[3 * j] + BDinv[3 * i + 1] * Bc[3 * j + 1] + BDinv[3 * i + 2] * Bc[3 * j + 2];
+                }
+            }
+        }
+        for (int i = 0; i < n; i++) bs[i] = b[i] - coeff[i];
+        // dense LDL^T of the symmetric reduced system from its upper triangle
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < i; j++) S[(size_t)i * n + j] = S[(size_t)j * n + i];
+        std::vector<double> L((size_t)n * n, 0.0), d(n);
+        for (int j = 0; j < n; j++) {
+            double s = S[(size_t)j * n + j];
+            for (int k = 0; k < j; k++) s -= L[(size_t)j * n + k] * L[(size_t)j * n + k] * d[k];
+            if (s == 0.0) return false;
+            d[j] = s;
+            for (int i = j + 1; i < n; i++) {
+                double t = S[(size_t)i * n + j];
+                for (int k = 0; k < j; k++) t -= L[(size_t)i * n + k] * L[(size_t)j * n + k] * d[k];
+                L[(size_t)i * n + j] = t / s;
+            }
+        }
+        std::vector<double> yv(n);
+        for (int i = 0; i < n; i++) {
+            double t = bs[i];
+            for (int k = 0; k < i; k++) t -= L[(size_t)i * n + k] * yv[k];
+            yv[i] = t;
+        }
+        for (int i = 0; i < n; i++) yv[i] /= d[i];
+        for (int i = n - 1; i >= 0; i--) {
+            double t = yv[i];
+            for (int k = i + 1; k < n; k++) t -= L[(size_t)k * n + i] * x[k];
+            x[i] = t;
+        }
+        // landmarks: xl = Dinv (bl - Hpl^T xp)
+        for (int hl = 0; hl < Nl; hl++) {
+            const int il = hpoint[hl];
+            double cl[3] = {b[n + 3 * hl], b[n + 3 * hl + 1], b[n + 3 * hl + 2]};
+            for (int e : point_edges[il]) {
+                const int h = pose_h[p->edge_pose[e]];
+                if (h < 0) continue;
+                const double* Be = &Hpl[18 * (size_t)e];
+                for (int j = 0; j < 3; j++)
+                    for (int i = 0; i < 6; i++) cl[j] -= Be[3 * i + j] * x[6 * h + i];
+            }
+            const double* Di = &Dinv[9 * (size_t)hl];
+            for (int i = 0; i < 3; i++) x[n + 3 * hl + i] = Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1] + Di[3 * i + 2] * cl[2];
+        }
+        return true;
+    }
+
+    void update() {
+        for (int h = 0; h < Np; h++) {
+            const int ip = hpose[h];
+            pose[ip] = se3Mul(se3Exp(&x[6 * h]), pose[ip]);
+        }
+        for (int hl = 0; hl < Nl; hl++) {
+            const int il = hpoint[hl];
+            for (int i = 0; i < 3; i++) pt[3 * il + i] += x[6 * Np + 3 * hl + i];
+        }
+    }
+
+    double computeScale(double lambda) const {
+        double scale = 0.;
+        for (size_t j = 0; j < x.size(); j++) scale += x[j] * (lambda * x[j] + b[j]);
+        return scale;
+    }
+};
+
+}  // namespace
+
+extern "C" int oracle_lba_solve(const mam_lba_problem* p, const int32_t* stop_flag, mam_lba_result* r) {
+    if (!p || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return MAM_ERR_ARG;
+    Graph g;
+    g.p = p;
+    g.pose.resize(p->n_poses);
+    for (int i = 0; i < p->n_poses; i++) {
+        g.pose[i].r = {p->pose_q[4 * i], p->pose_q[4 * i + 1], p->pose_q[4 * i + 2], p->pose_q[4 * i + 3]};
+        for (int k = 0; k < 3; k++) g.pose[i].t[k] = p->pose_t[3 * i + k];
+        normalizeRotation(g.pose[i]);   // SE3Quat(q, t) constructor
+    }
+    g.pt.assign(p->point_xyz, p->point_xyz + 3 * (size_t)p->n_points);
+    // _ivMap (sparse_optimizer.cpp:166-190): vertices sorted by id; non-fixed poses, then points
+    std::vector<int> po(p->n_poses), pl(p->n_points);
+    std::iota(po.begin(), po.end(), 0);
+    std::iota(pl.begin(), pl.end(), 0);
+    std::stable_sort(po.begin(), po.end(), [&](int a, int b) { return p->pose_id[a] < p->pose_id[b]; });
+    std::stable_sort(pl.begin(), pl.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
+    g.pose_h.assign(p->n_poses, -1);
+    for (int i : po)
+        if (!p->pose_fixed[i]) { g.pose_h[i] = g.Np++; g.hpose.push_back(i); }
+    g.point_h.assign(p->n_points, -1);
+    for (int i : pl) { g.point_h[i] = g.Nl++; g.hpoint.push_back(i); }
+    std::vector<std::vector<int>> point_edges(p->n_points);
+    for (int e = 0; e < p->n_edges; e++) point_edges[p->edge_point[e]].push_back(e);
+    g.err.assign(2 * (size_t)p->n_edges, 0.0);
+    g.Hpp.assign(36 * (size_t)g.Np, 0.0);
+    g.Hll.assign(9 * (size_t)g.Nl, 0.0);
+    g.Hpl.assign(18 * (size_t)p->n_edges, 0.0);
+    g.b.assign(6 * (size_t)g.Np + 3 * (size_t)g.Nl, 0.0);
+    g.x.assign(g.b.size(), 0.0);
+
+    auto terminate = [&]() { return stop_flag && *stop_flag; };
+    double currentLambda = -1.0, ni = 2.0;
+    int nBad = 0, trials = 0, its = 0;
+    int status = 0;
+    g.computeActiveErrors();
+    r->initial_chi2 = g.activeRobustChi2();
+    bool ok = g.Np + g.Nl > 0;
+    for (int it = 0; it < p->iterations && !terminate() && ok; it++) {
+        g.computeActiveErrors();
+        double currentChi = g.activeRobustChi2();
+        const double iniChi = currentChi;
+        g.buildSystem();
+        if (it == 0) { currentLambda = g.computeLambdaInit(); ni = 2; nBad = 0; }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            std::vector<SE3> bp = g.pose;   // push
+            std::vector<double> bpt = g.pt;
+            const bool ok2 = g.solve(currentLambda, point_edges);
+            g.update();
+            g.computeActiveErrors();
+            double tempChi = g.activeRobustChi2();
+            if (!ok2) tempChi = std::numeric_limits<double>::max();
+            rho = currentChi - tempChi;
+            double scale = g.computeScale(currentLambda);
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                const double scaleFactor = std::max(1. / 3., alpha);
+                currentLambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                currentLambda *= ni;
+                ni *= 2;
+                g.pose = bp;   // pop
+                g.pt = bpt;
+            }
+            qmax++;
+            trials++;
+        } while (rho < 0 && qmax < 10 && !terminate());
+        its++;
+        bool term = false;
+        if (qmax == 10 || rho == 0) term = true;
+        else {
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+            else nBad = 0;
+            if (nBad >= 3) term = true;
+        }
+        ok = !term;
+    }
+    if (terminate()) status = 1;
+    for (int i = 0; i < p->n_poses; i++) {
+        r->pose_q[4 * i] = g.pose[i].r.x; r->pose_q[4 * i + 1] = g.pose[i].r.y;
+        r->pose_q[4 * i + 2] = g.pose[i].r.z; r->pose_q[4 * i + 3] = g.pose[i].r.w;
+        for (int k = 0; k < 3; k++) r->pose_t[3 * i + k] = g.pose[i].t[k];
+    }
+    memcpy(r->point_xyz, g.pt.data(), sizeof(double) * 3 * (size_t)p->n_points);
+    // chi2() reads the error of the LAST computeActiveErrors (a rejected trial's, if the run ended on one);
+    // isDepthPositive() recomputes from the current estimates (OptimizableTypes.h:99-110)
+    for (int e = 0; e < p->n_edges; e++) {
+        if (r->edge_chi2) r->edge_chi2[e] = g.chi2(e);
+        if (r->edge_depth_ok) {
+            double Xc[3];
+            se3Map(g.pose[p->edge_pose[e]], &g.pt[3 * p->edge_point[e]], Xc);
+            r->edge_depth_ok[e] = Xc[2] > 0.0;
+        }
+    }
+    g.computeActiveErrors();
+    r->final_chi2 = g.activeRobustChi2();
+    r->iterations = its;
+    r->lm_trials = trials;
+    r->status = status;
+    return MAM_OK;
+}

@@ -258,3 +258,19 @@ def search_for_triangulation(KF1, KF2, F12, ep, check_ori=False, coarse=False):
                                           _vp(k2), _vp(d2), _vp(h2), C.byref(fv2), _vp(F12), _vp(ep), int(check_ori),
                                           int(coarse), _vp(out))
     return n, out[:len(k1)]
+
+
+# ---------------------------------------------------------------- LBA oracle (oracle/lba_oracle.cpp)
+def lba_solve(prob, stop=None):
+    """g2o LocalBundleAdjustment solve restatement. prob: mam3slam_amd.lba.LBAProblem."""
+    from mam3slam_amd.lba import alloc_result, wrap_result
+
+    L = lib()
+    L.oracle_lba_solve.restype = C.c_int
+    L.oracle_lba_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    P = prob.as_c()
+    R, arrs = alloc_result(prob)
+    sf = None if stop is None else stop.ctypes.data_as(C.c_void_p)
+    rc = L.oracle_lba_solve(C.byref(P), sf, C.byref(R))
+    assert rc == 0, rc
+    return wrap_result(R, arrs)
