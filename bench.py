@@ -1,10 +1,16 @@
 #!/usr/bin/env python3
-"""bench.py — tracked frames/s of the MI355X ORB hot path (BASELINE.json metric), one JSON line on rank 0.
+"""bench.py — tracked frames/s of the MI355X ORB + local-BA hot path (BASELINE.json metric); one JSON line.
 
-Step = one pass of the hot path over one batch of synthetic frames resident in HBM: ORB extraction of B
-frames (pyramid -> FAST cells -> blur -> DistributeOctTree -> orientation + rBRIEF + lapping placement) and
-the per-frame matching stage that follows it in Tracking (when built). N GPUs = N agents, one process per
-GPU, each with its own frame stream (independent units: weak scaling, no data-path collective).
+Step = one pass of the hot path over one batch of B synthetic frames resident in HBM, i.e. what Tracking does
+per frame, batched:
+  1. ORB extraction (pyramid, per-cell FAST, DistributeOctTree, orientation, rBRIEF, lapping placement)
+  2. SearchByProjection(CurrentFrame, LastFrame, th=15)     (TrackWithMotionModel, Tracking.cc:2810)
+  3. SearchByProjection(F, localMapPoints, th=1), nnratio 0.8 (SearchLocalPoints, Tracking.cc:3146-3156),
+     with the keypoints matched in (2) taken
+and for --config c2 additionally one LocalBundleAdjustment (50 KF / 3000 MP, BASELINE configs[2]) per step,
+solved concurrently on its own HIP stream (the LocalMapping thread's work, Optimizer.cc:1116).
+N GPUs = N agents, one process per GPU, each with its own frame stream: independent units, weak scaling,
+no data-path collective.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c1|c2]
 """
@@ -14,6 +20,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -23,54 +30,84 @@ sys.path.insert(0, ROOT)
 
 CONFIGS = {
     # BASELINE.json configs[1]: single-agent mono 640x480, 1000 features, 8 levels, extract + match
-    "c1": dict(width=640, height=480, nfeatures=1000),
-    # configs[2] frame geometry: 1280x720, 2000 features
-    "c2": dict(width=1280, height=720, nfeatures=2000),
+    "c1": dict(width=640, height=480, nfeatures=1000, lba=False),
+    # BASELINE.json configs[2]: 1280x720, 2000 features + LocalBundleAdjustment (50 KF / 3000 MapPoints)
+    "c2": dict(width=1280, height=720, nfeatures=2000, lba=True),
 }
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFS = 78.6    # MI355X FP64 vector (spec)
 
 
 def level_sizes(w, h, nlevels=8, scale=1.2):
-    s = [1.0]
+    s = [np.float32(1.0)]
     for _ in range(nlevels - 1):
-        s.append(float(np.float32(np.float64(np.float32(s[-1])) * np.float64(np.float32(scale)))))
-    return [(int(np.rint(np.float32(w) * (np.float32(1.0) / np.float32(x)))),
-             int(np.rint(np.float32(h) * (np.float32(1.0) / np.float32(x))))) for x in s]
+        s.append(np.float32(np.float64(s[-1]) * np.float64(np.float32(scale))))
+    return [(int(np.rint(np.float32(w) * (np.float32(1.0) / x))), int(np.rint(np.float32(h) * (np.float32(1.0) / x))))
+            for x in s]
 
 
-def stage_bytes(w, h, n_kp, n_cand):
-    """Algorithmic HBM bytes per frame for each stage."""
+def stage_bytes(w, h, n_kp, n_cand, n_last, n_mps, cand_motion, cand_local):
+    """Algorithmic HBM bytes per frame for each kernel stage."""
     lv = level_sizes(w, h)
     P = sum(a * b for a, b in lv)
     P_ge1 = P - w * h
     P_le6 = P - lv[-1][0] * lv[-1][1]
     return {
-        "pyramid": P_le6 + P_ge1,                 # read levels 0..6, write levels 1..7
-        "fast": P + 4 * n_cand,                   # read every level once, write packed candidates
-        "blur": 2 * P,                            # read + write every level
-        "distribute": 4 * n_cand + 8 * n_kp,      # read candidates, write kept keypoints + ranks
-        "describe": n_kp * (961 + 37 * 37 + 60),  # 31x31 moment patch + 37x37 blurred patch + 60 B out
+        "pyramid": P_le6 + P_ge1,                  # read levels 0..6, write levels 1..7
+        "fast": P + 4 * n_cand,                    # read every level once, write packed candidates
+        "blur": 2 * P,                             # read + write every level
+        "distribute": 4 * n_cand + 8 * n_kp,       # read candidates, write kept keypoints + ranks
+        "describe": n_kp * (961 + 37 * 37 + 60),   # 31x31 moment disk + 37x37 blurred patch + 60 B out
+        "grid": 2 * n_kp * (28 + 2),               # both searches: read keypoints, write cell-sorted index
+        "gather": n_last * 64 + n_mps * 64 + (cand_motion + cand_local) * (2 + 28 + 32 + 4),
+        "resolve": (cand_motion + cand_local) * 4 + (n_last + n_mps) * 8 + 2 * n_kp * 4,
     }
 
 
 def cpu_baseline(cfg, seconds=10.0):
-    """Oracle (single-thread C++ restatement of the reference path) on a bounded sample of the workload."""
-    from mam3slam_amd import synth
+    """The oracle (single-thread C++ restatement of the reference path) on a bounded sample of the same
+    step workload: extraction + motion search + local-map search per frame."""
+    from mam3slam_amd import scene, synth
     from oracle import oracle_py
 
     p = oracle_py.params(cfg["nfeatures"])
-    frames = [synth.make_frame(cfg["width"], cfg["height"], agent=0, frame=i) for i in range(8)]
-    oracle_py.extract(frames[0], p)  # warm
+    W, H = cfg["width"], cfg["height"]
+    items = []
+    for i in range(4):
+        img = synth.make_frame(W, H, agent=0, frame=i)
+        k, d, _ = oracle_py.extract(img, p)
+        rng = np.random.default_rng(i)
+        F = scene.make_frame_data(k, d, W, H)
+        F.pose = scene.small_pose(rng)
+        cam = scene.pinhole(W, H)
+        items.append((img, scene.motion_last_frame(F, cam, rng), scene.local_mappoints(F, rng), F.pose, cam))
     n, t0 = 0, time.perf_counter()
     while True:
-        oracle_py.extract(frames[n % len(frames)], p)
+        img, last, mps, pose, cam = items[n % len(items)]
+        k, d, _ = oracle_py.extract(img, p)
+        F = scene.make_frame_data(k, d, W, H)
+        F.pose = pose
+        _, out = oracle_py.search_by_projection_motion(F, last, cam, 15.0, True)
+        F.taken = (out >= 0).astype(np.uint8)
+        oracle_py.search_by_projection(F, mps, 1.0, nnratio=0.8)
         n += 1
         el = time.perf_counter() - t0
-        if (el >= seconds and n >= 10) or n >= 2000:
+        if (el >= seconds and n >= 5) or n >= 2000:
             break
-    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} frames {cfg['width']}x{cfg['height']}/{cfg['nfeatures']} ORB extract, oracle C++ "
-                      f"restatement single-threaded, {el:.1f}s"}
+    res = {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
+           "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15) + "
+                     f"SearchByProjection(local map, th 1) on the oracle C++ restatement, single thread, {el:.1f}s"}
+    if cfg["lba"]:
+        from mam3slam_amd.lba import synthetic_problem
+
+        prob = synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, seed=1)
+        t1 = time.perf_counter()
+        r = oracle_py.lba_solve(prob)
+        lba_ms = (time.perf_counter() - t1) * 1e3
+        res["lba_ms"] = lba_ms
+        res["sample"] += f"; LocalBundleAdjustment 50 KF/3000 MP ({len(prob.edge_point)} edges, {r.iterations} it) " \
+                         f"{lba_ms:.1f} ms"
+    return res
 
 
 def main():
@@ -95,7 +132,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from mam3slam_amd import ORBextractor, synth
+    from mam3slam_amd import ORBextractor, scene, synth
+    from mam3slam_amd.match import LAST_ENTRY_DTYPE, MP_TRACK_DTYPE, FramesDev, ORBmatcher, Pose
     from mam3slam_amd.orb import KP_DTYPE
 
     cfg = CONFIGS[args.config]
@@ -107,20 +145,107 @@ def main():
     d_kps = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)
     d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
     d_cnt = torch.zeros((B, 2), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # one explicit stream orders extraction -> motion search -> local search (NULL would mean each library
+    # context's own stream: unordered with each other)
+    tstream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(tstream)
+    stream = tstream.cuda_stream
 
-    def step():
+    def extract():
         ext.extract_batch_device(d_img.data_ptr(), B, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap,
                                  d_cnt.data_ptr(), stream=stream)
+
+    # ---- per-frame map structures around the frame's own features (built once; resident in HBM)
+    extract()
+    torch.cuda.synchronize(dev)
+    kps_h = d_kps.cpu().numpy().view(KP_DTYPE).reshape(B, cap)
+    desc_h = d_desc.cpu().numpy()
+    cnt_h = d_cnt.cpu().numpy()
+    cam = scene.pinhole(W, H)
+    lasts, mpss, poses = [], [], []
+    F0 = None
+    for f in range(B):
+        rng = np.random.default_rng(1000 * rank + f)
+        F = scene.make_frame_data(kps_h[f, :cnt_h[f, 0]], desc_h[f, :cnt_h[f, 0]], W, H)
+        F.pose = scene.small_pose(rng)
+        F0 = F0 or F
+        lasts.append(scene.motion_last_frame(F, cam, rng))
+        mpss.append(scene.local_mappoints(F, rng))
+        poses.append(F.pose)
+    Ls, Ms = max(len(x) for x in lasts), max(len(x) for x in mpss)
+    last = np.zeros((B, Ls), LAST_ENTRY_DTYPE)
+    mps = np.zeros((B, Ms), MP_TRACK_DTYPE)
+    tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+    for f in range(B):
+        last[f, :len(lasts[f])] = lasts[f]
+        mps[f, :len(mpss[f])] = mpss[f]
+        tcw[f]["q"], tcw[f]["t"] = poses[f]
+    d_last = torch.from_numpy(last.view(np.uint8).reshape(B, -1).copy()).to(dev)
+    d_mps = torch.from_numpy(mps.view(np.uint8).reshape(B, -1).copy()).to(dev)
+    d_tcw = torch.from_numpy(tcw.view(np.uint8).copy()).to(dev)
+    d_nlast = torch.tensor([len(x) for x in lasts], dtype=torch.int32, device=dev)
+    d_nmps = torch.tensor([len(x) for x in mpss], dtype=torch.int32, device=dev)
+    d_out1 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    d_out2 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    d_nm1 = torch.zeros(B, dtype=torch.int32, device=dev)
+    d_nm2 = torch.zeros(B, dtype=torch.int32, device=dev)
+    d_taken = torch.zeros((B, cap), dtype=torch.uint8, device=dev)
+    m_motion = ORBmatcher(0.9, True, device=local)
+    m_local = ORBmatcher(0.8, True, device=local)
+    fr1 = FramesDev(B, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), None)
+    fr2 = FramesDev(B, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), d_taken.data_ptr())
+
+    def match():
+        m_motion.search_motion_batch_device(F0, fr1, d_tcw.data_ptr(), cam, d_last.data_ptr(), Ls,
+                                            d_nlast.data_ptr(), 15.0, d_out1.data_ptr(), d_nm1.data_ptr(),
+                                            stream=stream)
+        torch.ge(d_out1, 0, out=d_taken.view(torch.bool))
+        m_local.search_by_projection_batch_device(F0, fr2, d_mps.data_ptr(), Ms, d_nmps.data_ptr(), 1.0,
+                                                  d_out2.data_ptr(), d_nm2.data_ptr(), stream=stream)
+
+    lba_solver, lba_prob = None, None
+    if cfg["lba"]:
+        from mam3slam_amd.lba import LBASolver, synthetic_problem
+
+        lba_solver = LBASolver(device=local)
+        lba_prob = synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, seed=1 + rank)
+
+    lba_stats = {"n": 0, "ms": 0.0, "its": 0}
+
+    def lba_worker():
+        t = time.perf_counter()
+        r = lba_solver.solve(lba_prob)
+        lba_stats["ms"] += (time.perf_counter() - t) * 1e3
+        lba_stats["n"] += 1
+        lba_stats["its"] = r.iterations
+
+    def step():
+        th = None
+        if lba_solver is not None:
+            th = threading.Thread(target=lba_worker)
+            th.start()
+        extract()
+        match()
+        if th is not None:
+            th.join()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     cnt = d_cnt.cpu().numpy()
     n_kp = float(cnt[:, 0].mean())
-    n_cand = float(sum(len(ext.debug_candidates(l, f)) for l in range(8) for f in range(min(B, 4)))) / min(B, 4)
+    nf_probe = min(B, 4)
+    n_cand = float(sum(len(ext.debug_candidates(l, f)) for l in range(8) for f in range(nf_probe))) / nf_probe
+    nm1, nm2 = d_nm1.cpu().numpy(), d_nm2.cpu().numpy()
+    if (nm1 < 0).any() or (nm2 < 0).any() or (cnt[:, 0] < 0).any():
+        raise RuntimeError(f"device error codes in outputs: {nm1.min()} {nm2.min()} {cnt[:, 0].min()}")
 
     ext.set_profiling(True)
+    m_motion.set_profiling(True)
+    m_local.set_profiling(True)
+    lba_stats.update(n=0, ms=0.0)
+    if lba_solver is not None:
+        lba_solver.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -131,20 +256,30 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    stages = ext.stage_times()
-    ext.set_profiling(False)
+    stages = dict(ext.stage_times())
+    sm1, sm2 = m_motion.stage_times(), m_local.stage_times()
+    for k in ("grid", "gather", "resolve"):
+        stages[k] = (sm1[k][0] + sm2[k][0], sm1[k][1] + sm2[k][1])
+    for o in (ext, m_motion, m_local):
+        o.set_profiling(False)
+    lba_stage = lba_solver.stage_times() if lba_solver is not None else None
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     T = float(t.item())
     frames_total = world * B * args.steps
 
-    # roofline of the dominant stage: algorithmic bytes per launch / average launch duration (HIP events)
-    sb = stage_bytes(W, H, n_kp, n_cand)
+    # roofline of the dominant kernel stage: algorithmic bytes per launch / mean launch duration (HIP events
+    # recorded around each launch on the stream it runs on)
+    mean_last = float(np.mean([len(x) for x in lasts]))
+    mean_mps = float(np.mean([len(x) for x in mpss]))
+    sb = stage_bytes(W, H, n_kp, n_cand, mean_last, mean_mps, cand_motion=mean_last * 6.0, cand_local=mean_mps * 3.0)
+    per_step_ms = {k: v[0] / args.steps for k, v in stages.items()}
     dom = max(stages, key=lambda k: stages[k][0])
     ms_tot, launches = stages[dom]
     avg_ms = ms_tot / max(launches, 1)
-    bytes_per_launch = sb[dom] * B
+    launches_per_step = launches / args.steps
+    bytes_per_launch = sb[dom] * B / launches_per_step
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
@@ -155,6 +290,10 @@ def main():
             traffic = None
 
     if rank == 0:
+        workload = (f"{args.config}: mono {W}x{H}, {NF} features, 8 levels; step = {B} frames x (ORB extract + "
+                    f"SearchByProjection motion th15 + SearchByProjection local map th1)")
+        if cfg["lba"]:
+            workload += " + 1 LocalBundleAdjustment 50KF/3000MP per step (concurrent stream)"
         out = {
             "metric": "tracked frames/sec (ORB extract+match+localBA) at 1/2/4/8 GPUs vs CPU ref",
             "value": frames_total / T,
@@ -168,16 +307,20 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": f"{args.config}: mono {W}x{H}, {NF} features, 8 levels, ORB extract "
-                                   f"(match stage not yet in step)",
-                       "frames_per_step_per_gpu": B, "width": W, "height": H, "nfeatures": NF,
-                       "keypoints_per_frame": n_kp, "candidates_per_frame": n_cand,
-                       "parallelism": f"agents{world} (one agent per GPU)"},
-            "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in stages.items()},
+            "config": {"workload": workload, "frames_per_step_per_gpu": B, "width": W, "height": H,
+                       "nfeatures": NF, "keypoints_per_frame": n_kp, "fast_candidates_per_frame": n_cand,
+                       "last_frame_points": mean_last, "local_map_points": mean_mps,
+                       "matches_motion_per_frame": float(nm1.mean()), "matches_local_per_frame": float(nm2.mean()),
+                       "parallelism": f"agents{world} (one agent per GPU, independent)"},
+            "stage_ms_per_step": per_step_ms,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
+                         "avg_launch_ms": avg_ms},
         }
+        if cfg["lba"]:
+            out["lba"] = {"solves": lba_stats["n"], "ms_per_solve_wall": lba_stats["ms"] / max(lba_stats["n"], 1),
+                          "iterations": lba_stats["its"], "edges": int(len(lba_prob.edge_point)),
+                          "stage_ms_total": {k: v[0] for k, v in lba_stage.items()}}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         print(json.dumps(out), flush=True)

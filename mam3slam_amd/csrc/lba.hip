@@ -170,19 +170,43 @@ __global__ __launch_bounds__(256) void k_point_sys(Dev d) {
     for (int k = 0; k < 3; k++) d.b[6 * (size_t)d.Np + 3 * (size_t)h + k] = bl[k];
 }
 
-// ---- one wave per non-fixed pose: H_pp (36 lanes) and b_p (6 lanes)
+// fixed-order (butterfly) wave sum: every lane ends with the same value, deterministic run to run
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---- one wave per non-fixed pose: lanes stride over the pose's edges, accumulate the 21 upper entries of
+// H_pp and the 6 of b_p in registers, then a fixed-order wave reduction
 __global__ __launch_bounds__(64) void k_pose_sys(Dev d) {
     const int h = blockIdx.x, lane = threadIdx.x;
-    if (lane >= 42) return;
-    double acc = 0.0;
-    const int a = lane < 36 ? lane / 6 : lane - 36, c = lane < 36 ? lane % 6 : 0;
-    for (int s = d.qe_off[h]; s < d.qe_off[h + 1]; s++) {
+    double acc[27];
+#pragma unroll
+    for (int k = 0; k < 27; k++) acc[k] = 0.0;
+    for (int s = d.qe_off[h] + lane; s < d.qe_off[h + 1]; s += 64) {
         const double* j = d.jac + 21 * (size_t)d.qe_idx[s];
-        if (lane < 36) acc += j[6 + a] * j[20] * j[6 + c] + j[12 + a] * j[20] * j[12 + c];
-        else acc += j[6 + a] * j[18] + j[12 + a] * j[19];
+        double B0[6], B1[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) { B0[k] = j[6 + k]; B1[k] = j[12 + k]; }
+        const double wo = j[20], o0 = j[18], o1 = j[19];
+        int q = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int c = a; c < 6; c++) acc[q++] += B0[a] * wo * B0[c] + B1[a] * wo * B1[c];
+#pragma unroll
+        for (int a = 0; a < 6; a++) acc[21 + a] += B0[a] * o0 + B1[a] * o1;
     }
-    if (lane < 36) d.Hpp[36 * (size_t)h + lane] = acc;
-    else d.b[6 * (size_t)h + a] = acc;
+#pragma unroll
+    for (int k = 0; k < 27; k++) acc[k] = wave_sum_d(acc[k]);
+    if (lane == 0) {
+        int q = 0;
+        double* H = d.Hpp + 36 * (size_t)h;
+        for (int a = 0; a < 6; a++)
+            for (int c = a; c < 6; c++) { H[6 * a + c] = acc[q]; H[6 * c + a] = acc[q]; q++; }
+        for (int a = 0; a < 6; a++) d.b[6 * (size_t)h + a] = acc[21 + a];
+    }
 }
 
 // ---- fixed-order sum of rho0 (and max diag) in one workgroup
@@ -248,19 +272,34 @@ __global__ __launch_bounds__(256) void k_schur_prep(Dev d, double lambda) {
 
 __global__ __launch_bounds__(64) void k_schur_blk(Dev d, double lambda) {
     const int bp = blockIdx.x, lane = threadIdx.x;
-    if (lane >= 36) return;
     const int i1 = d.bp_ij[2 * bp], i2 = d.bp_ij[2 * bp + 1];
-    const int r = lane / 6, c = lane % 6;
-    double acc = 0.0;
-    if (i1 == i2) acc = d.Hpp[36 * (size_t)i1 + lane] + (r == c ? lambda : 0.0);
-    for (int s = d.bp_off[bp]; s < d.bp_off[bp + 1]; s++) {
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; k++) acc[k] = 0.0;
+    for (int s = d.bp_off[bp] + lane; s < d.bp_off[bp + 1]; s += 64) {
         const double* W = d.bdinv + 18 * (size_t)d.bp_ea[s];
         const double* B = d.hpl + 18 * (size_t)d.bp_ec[s];
-        acc -= W[3 * r] * B[3 * c] + W[3 * r + 1] * B[3 * c + 1] + W[3 * r + 2] * B[3 * c + 2];
+        double w[18], b[18];
+#pragma unroll
+        for (int k = 0; k < 18; k++) { w[k] = W[k]; b[k] = B[k]; }
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c < 6; c++) acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
     }
-    const int n = 6 * d.Np;
-    d.S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
-    d.S[(size_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;
+#pragma unroll
+    for (int k = 0; k < 36; k++) acc[k] = wave_sum_d(acc[k]);
+    if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < 36; k++) v = (k == lane) ? acc[k] : v;
+        double out = -v;
+        if (i1 == i2) out = (d.Hpp[36 * (size_t)i1 + lane] + (r == c ? lambda : 0.0)) - v;
+        const int n = 6 * d.Np;
+        d.S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = out;
+        d.S[(size_t)(6 * i2 + c) * n + 6 * i1 + r] = out;
+    }
 }
 
 __global__ __launch_bounds__(64) void k_schur_rhs(Dev d) {
@@ -271,95 +310,173 @@ __global__ __launch_bounds__(64) void k_schur_rhs(Dev d) {
     d.bs[6 * (size_t)h + lane] = acc;
 }
 
-// ---- dense LDL^T solve of S x = bs, one workgroup, blocked right-looking (panel NB columns).
-// S holds the full symmetric matrix; the lower triangle is overwritten by L (unit diagonal implicit),
-// the diagonal by D. flag[0] = 1 on an exact zero pivot (Eigen SimplicialLDLT's failure rule).
+// ---- dense LDL^T solve of S x = bs, one workgroup, blocked right-looking with NB = 16 column panels.
+// S holds the full symmetric matrix. Per panel: (1) wave 0 factors the 16x16 diagonal block in registers
+// (lane i owns row i, columns broadcast by shuffles); (2) every thread forward-solves panel rows
+// L21 = A21 L11^-T D^-1 and keeps W = L21 D in the (dead) upper triangle; (3) the trailing lower triangle
+// is updated A22 -= L21 W^T in 4x4 register tiles. flag[0] = 1 on an exact zero pivot (the failure rule of
+// Eigen's SimplicialLDLT). Then blocked forward / diagonal / backward substitution.
 constexpr int NB = 16;
 
 __global__ __launch_bounds__(1024) void k_ldlt(Dev d) {
     const int n = 6 * d.Np;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     double* A = d.S;
-    __shared__ double diag[NB * NB];
+    __shared__ double Ld[NB * NB];
     __shared__ double dk[NB];
     __shared__ int fail;
     if (t == 0) fail = 0;
-    __syncthreads();
     for (int kb = 0; kb < n; kb += NB) {
         const int nb = min(NB, n - kb);
-        // 1. factor the diagonal block in LDS (unblocked LDL^T, column by column)
-        for (int i = t; i < nb * nb; i += 1024) diag[i] = A[(size_t)(kb + i / nb) * n + kb + i % nb];
-        __syncthreads();
-        for (int j = 0; j < nb; j++) {
-            if (t == 0) {
-                double sj = diag[j * nb + j];
-                for (int k = 0; k < j; k++) sj -= diag[j * nb + k] * diag[j * nb + k] * dk[k];
-                if (sj == 0.0) fail = 1;
-                dk[j] = sj;
+        // (1) diagonal block
+        if (wid == 0) {
+            double row[NB];
+#pragma unroll
+            for (int c = 0; c < NB; c++) row[c] = (lane < nb && c < nb) ? A[(size_t)(kb + lane) * n + kb + c] : 0.0;
+            double dloc[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                if (j < nb) {
+                    // d_j = a_jj - sum_k L_jk^2 d_k  (lane j holds row j)
+                    double s = row[j];
+#pragma unroll
+                    for (int k = 0; k < NB; k++)
+                        if (k < j) s -= row[k] * row[k] * dloc[k];
+                    const double dj = __shfl(s, j, 64);
+                    dloc[j] = dj;
+                    // L_ij = (a_ij - sum_k L_ik L_jk d_k) / d_j for i > j
+                    double lj[NB];
+#pragma unroll
+                    for (int k = 0; k < NB; k++) lj[k] = __shfl(row[k], j, 64);
+                    if (lane > j && lane < nb) {
+                        double v = row[j];
+#pragma unroll
+                        for (int k = 0; k < NB; k++)
+                            if (k < j) v -= row[k] * lj[k] * dloc[k];
+                        row[j] = dj != 0.0 ? v / dj : 0.0;
+                    }
+                } else {
+                    dloc[j] = 1.0;
+                }
             }
-            __syncthreads();
-            const int i = j + 1 + t;
-            if (i < nb) {
-                double si = diag[i * nb + j];
-                for (int k = 0; k < j; k++) si -= diag[i * nb + k] * diag[j * nb + k] * dk[k];
-                diag[i * nb + j] = dk[j] != 0.0 ? si / dk[j] : 0.0;
+            if (lane < nb) {
+#pragma unroll
+                for (int c = 0; c < NB; c++) Ld[lane * NB + c] = row[c];
+                dk[lane] = dloc[lane < NB ? lane : 0];
+                if (dloc[lane] == 0.0) fail = 1;
             }
-            __syncthreads();
         }
-        // write back the factored diagonal block: L below diagonal, D on diagonal
+        __syncthreads();
         for (int i = t; i < nb * nb; i += 1024) {
             const int r = i / nb, c = i % nb;
-            if (r > c) A[(size_t)(kb + r) * n + kb + c] = diag[r * nb + c];
+            if (r > c) A[(size_t)(kb + r) * n + kb + c] = Ld[r * NB + c];
             else if (r == c) A[(size_t)(kb + r) * n + kb + c] = dk[r];
         }
-        // 2. panel rows below: L21 = A21 L11^-T D^-1 (row-wise forward substitution); keep W = L21 D in the
-        //    strictly-upper mirror position (free after the mirror is no longer needed) -> use row storage
+        // (2) panel rows
         for (int i = kb + nb + t; i < n; i += 1024) {
             double w[NB];
-            for (int j = 0; j < nb; j++) {
-                double s = A[(size_t)i * n + kb + j];
-                for (int k = 0; k < j; k++) s -= w[k] * diag[j * nb + k];
-                w[j] = s;   // w_j = (L21 D)_ij
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                if (j < nb) {
+                    double s = A[(size_t)i * n + kb + j];
+#pragma unroll
+                    for (int k = 0; k < NB; k++)
+                        if (k < j) s -= w[k] * Ld[j * NB + k];
+                    w[j] = s;
+                }
             }
-            for (int j = 0; j < nb; j++) {
-                A[(size_t)i * n + kb + j] = dk[j] != 0.0 ? w[j] / dk[j] : 0.0;   // L21
-                A[(size_t)(kb + j) * n + i] = w[j];                               // W^T in the upper part
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                if (j < nb) {
+                    A[(size_t)i * n + kb + j] = dk[j] != 0.0 ? w[j] / dk[j] : 0.0;   // L21
+                    A[(size_t)(kb + j) * n + i] = w[j];                               // W^T (upper, dead)
+                }
             }
         }
         __syncthreads();
-        // 3. trailing update of the lower triangle: A22 -= L21 W^T
+        // (3) trailing update, 4x4 register tiles over the lower triangle of the m x m trailing block
         const int m = n - kb - nb;
-        const long long cnt = (long long)m * (m + 1) / 2;
-        for (long long q = t; q < cnt; q += 1024) {
-            // map q -> (r, c) with c <= r over the m x m trailing lower triangle
-            int r = (int)((sqrt(8.0 * (double)q + 1.0) - 1.0) * 0.5);
-            while ((long long)r * (r + 1) / 2 > q) r--;
-            while ((long long)(r + 1) * (r + 2) / 2 <= q) r++;
-            const int c = (int)(q - (long long)r * (r + 1) / 2);
-            const int gi = kb + nb + r, gj = kb + nb + c;
-            double s = A[(size_t)gi * n + gj];
-            for (int k = 0; k < nb; k++) s -= A[(size_t)gi * n + kb + k] * A[(size_t)(kb + k) * n + gj];
-            A[(size_t)gi * n + gj] = s;
+        const int T = (m + 3) / 4;
+        const int ntile = T * (T + 1) / 2;
+        for (int q = t; q < ntile; q += 1024) {
+            int tr = (int)((sqrt(8.0 * (double)q + 1.0) - 1.0) * 0.5);
+            while (tr * (tr + 1) / 2 > q) tr--;
+            while ((tr + 1) * (tr + 2) / 2 <= q) tr++;
+            const int tc = q - tr * (tr + 1) / 2;
+            const int r0 = kb + nb + 4 * tr, c0 = kb + nb + 4 * tc;
+            double acc[4][4];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
+            for (int k = 0; k < nb; k++) {
+                double lr[4], wc[4];
+#pragma unroll
+                for (int a = 0; a < 4; a++) {
+                    lr[a] = (r0 + a < n) ? A[(size_t)(r0 + a) * n + kb + k] : 0.0;
+                    wc[a] = (c0 + a < n) ? A[(size_t)(kb + k) * n + c0 + a] : 0.0;
+                }
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int b = 0; b < 4; b++) acc[a][b] += lr[a] * wc[b];
+            }
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int gi = r0 + a, gj = c0 + b;
+                    if (gi < n && gj < n && gj <= gi) A[(size_t)gi * n + gj] -= acc[a][b];
+                }
         }
         __syncthreads();
     }
     if (t == 0) d.flag[0] = fail;
     __syncthreads();
     if (fail) return;
-    // forward: L y = bs (column-oriented), then y /= D, then L^T x = y
+    // blocked substitution: L y = bs; y /= D; L^T x = y
     double* y = d.x;
     for (int i = t; i < n; i += 1024) y[i] = d.bs[i];
     __syncthreads();
-    for (int j = 0; j < n; j++) {
-        const double yj = y[j];
-        for (int i = j + 1 + t; i < n; i += 1024) y[i] -= A[(size_t)i * n + j] * yj;
+    for (int kb = 0; kb < n; kb += NB) {
+        const int nb = min(NB, n - kb);
+        if (wid == 0) {
+            // unit-lower triangular solve of the 16-row block in one wave
+            double v = lane < nb ? y[kb + lane] : 0.0;
+            for (int j = 0; j < nb; j++) {
+                const double yj = __shfl(v, j, 64);
+                if (lane > j && lane < nb) v -= A[(size_t)(kb + lane) * n + kb + j] * yj;
+            }
+            if (lane < nb) y[kb + lane] = v;
+        }
+        __syncthreads();
+        for (int i = kb + nb + t; i < n; i += 1024) {
+            double s = y[i];
+            for (int j = 0; j < nb; j++) s -= A[(size_t)i * n + kb + j] * y[kb + j];
+            y[i] = s;
+        }
         __syncthreads();
     }
     for (int i = t; i < n; i += 1024) y[i] /= A[(size_t)i * n + i];
     __syncthreads();
-    for (int j = n - 1; j >= 0; j--) {
-        const double xj = y[j];
-        for (int i = t; i < j; i += 1024) y[i] -= A[(size_t)j * n + i] * xj;
+    const int nblk = (n + NB - 1) / NB;
+    for (int bi = nblk - 1; bi >= 0; bi--) {
+        const int kb = bi * NB, nb = min(NB, n - kb);
+        if (wid == 0) {
+            // unit-upper (L^T) solve of the block: x_i = y_i - sum_{j>i} L_ji x_j
+            double v = lane < nb ? y[kb + lane] : 0.0;
+            for (int j = nb - 1; j >= 0; j--) {
+                const double xj = __shfl(v, j, 64);
+                if (lane < j) v -= A[(size_t)(kb + j) * n + kb + lane] * xj;
+            }
+            if (lane < nb) y[kb + lane] = v;
+        }
+        __syncthreads();
+        for (int i = t; i < kb; i += 1024) {
+            double s = y[i];
+            for (int j = 0; j < nb; j++) s -= A[(size_t)(kb + j) * n + i] * y[kb + j];
+            y[i] = s;
+        }
         __syncthreads();
     }
 }

@@ -8,8 +8,9 @@
 //   Frame grid / GetFeaturesInArea       src/Frame.cc:385-416, 657-735
 //
 // Stages (one launch each, batched over frames):
-//   k_grid     per frame: PosInGrid for every keypoint, LDS bitonic sort of (cell, idx) -> cell-major index
-//              list with ascending idx per cell = AssignFeaturesToGrid's cell vectors.
+//   k_grid     per frame: PosInGrid for every keypoint, LDS counting sort by cell (atomics) + per-cell insertion
+//              sort by index -> cell-major index list with ascending idx per cell = AssignFeaturesToGrid's cell
+//              vectors, plus the (x, y, octave) of each entry in that order for coalesced window scans.
 //   k_gather   one wave per search unit (MapPoint / last-frame entry): window cells enumerated ix -> iy -> cell
 //              order exactly as GetFeaturesInArea, level + radius filters, Hamming distance (4x popcount64);
 //              COUNT pass, per-frame scan, FILL pass into a per-frame candidate pool (entry = idx | dist<<16 |
@@ -51,7 +52,9 @@ struct ProjArgs {
     const mam_last_entry* last;
     int check_ori;
     // scratch
-    uint16_t* grid_idx;       // [F][kp_stride]
+    uint16_t* grid_idx;       // [F][kp_stride] keypoint index, cell-major (cell vectors of AssignFeaturesToGrid)
+    float2* grid_xy;          // [F][kp_stride] keypoint (x, y) in the same order
+    uint8_t* grid_oct;        // [F][kp_stride] keypoint octave in the same order
     int32_t* grid_start;      // [F][NCELLS+1]
     int32_t* cand_cnt;        // [F][unit_stride]
     int32_t* cand_off;        // [F][unit_stride]
@@ -106,62 +109,78 @@ __device__ __forceinline__ unsigned wave_minu(unsigned v) {
 }
 
 // ------------------------------------------------------------------------------------------------ grid
-__global__ __launch_bounds__(256) void k_grid(ProjArgs p) {
-    __shared__ uint32_t keys[GRID_SORT_MAX];
-    __shared__ int32_t start[NCELLS + 1];
-    __shared__ int red[4];
-    const int f = blockIdx.x, tid = threadIdx.x;
+__global__ __launch_bounds__(1024) void k_grid(ProjArgs p) {
+    __shared__ int cnt[NCELLS + 1];
+    __shared__ int start[NCELLS + 1];
+    __shared__ uint16_t cellOf[GRID_SORT_MAX];
+    __shared__ uint16_t sorted[GRID_SORT_MAX];
+    __shared__ int wsum[16];
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int n = frame_n(p.fr, f);
     if (n > GRID_SORT_MAX) {
         if (tid == 0) p.out_n[f] = MAM_ERR_CAPACITY;
         return;
     }
-    int P = 2;
-    while (P < n) P <<= 1;
     const mam_keypoint* K = p.fr.keys + (size_t)f * p.fr.kp_stride;
-    int nvalid = 0;
-    for (int i = tid; i < P; i += 256) {
-        uint32_t key = 0xFFFFFFFFu;
-        if (i < n) {
-            // PosInGrid (Frame.cc:725-735): std::round (half away from zero)
-            const int posX = (int)roundf((K[i].x - p.g.min_x) * p.g.grid_inv_w);
-            const int posY = (int)roundf((K[i].y - p.g.min_y) * p.g.grid_inv_h);
-            if (!(posX < 0 || posX >= MAM_GRID_COLS || posY < 0 || posY >= MAM_GRID_ROWS)) {
-                key = ((uint32_t)(posX * MAM_GRID_ROWS + posY) << 16) | (uint32_t)i;
-                nvalid++;
-            }
-        }
-        keys[i] = key;
-    }
-    nvalid = wave_sum(nvalid);
-    if (lane_id() == 0) red[tid >> 6] = nvalid;
+    for (int c = tid; c <= NCELLS; c += 1024) cnt[c] = 0;
     __syncthreads();
-    const int nv = red[0] + red[1] + red[2] + red[3];
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < P; i += 256) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint32_t a = keys[i], b = keys[ixj];
-                    const bool asc = (i & k) == 0;
-                    if ((a > b) == asc) { keys[i] = b; keys[ixj] = a; }
-                }
-            }
-            __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        // PosInGrid (Frame.cc:725-735): std::round (half away from zero)
+        const int posX = (int)roundf((K[i].x - p.g.min_x) * p.g.grid_inv_w);
+        const int posY = (int)roundf((K[i].y - p.g.min_y) * p.g.grid_inv_h);
+        uint16_t cell = 0xFFFF;
+        if (!(posX < 0 || posX >= MAM_GRID_COLS || posY < 0 || posY >= MAM_GRID_ROWS)) {
+            cell = (uint16_t)(posX * MAM_GRID_ROWS + posY);   // ix-major, then iy: GetFeaturesInArea's order
+            atomicAdd(&cnt[cell], 1);
         }
+        cellOf[i] = cell;
     }
-    for (int c = tid; c <= NCELLS; c += 256) start[c] = nv;
     __syncthreads();
-    for (int i = tid; i < nv; i += 256) {
-        const int cell = (int)(keys[i] >> 16);
-        const int prev = i ? (int)(keys[i - 1] >> 16) : -1;
-        for (int c = prev + 1; c <= cell; c++) start[c] = i;
+    // exclusive scan of the 3072 cell counts: 3 cells per thread
+    const int c0 = 3 * tid;
+    const int a0 = cnt[c0], a1 = cnt[c0 + 1], a2 = cnt[c0 + 2];
+    const int v = a0 + a1 + a2;
+    const int incl = wave_incl_scan(v);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int pre = 0, tot = 0;
+    for (int w = 0; w < 16; w++) {
+        if (w < wid) pre += wsum[w];
+        tot += wsum[w];
+    }
+    const int base = pre + incl - v;
+    start[c0] = base;
+    start[c0 + 1] = base + a0;
+    start[c0 + 2] = base + a0 + a1;
+    if (tid == 0) start[NCELLS] = tot;
+    __syncthreads();
+    for (int c = tid; c < NCELLS; c += 1024) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const int cell = cellOf[i];
+        if (cell != 0xFFFF) sorted[start[cell] + atomicAdd(&cnt[cell], 1)] = (uint16_t)i;
+    }
+    __syncthreads();
+    // atomics placed each cell's entries in arbitrary order: restore ascending keypoint index
+    for (int c = tid; c < NCELLS; c += 1024) {
+        const int b0 = start[c], b1 = start[c + 1];
+        for (int k = b0 + 1; k < b1; k++) {
+            const uint16_t val = sorted[k];
+            int m = k - 1;
+            while (m >= b0 && sorted[m] > val) { sorted[m + 1] = sorted[m]; m--; }
+            sorted[m + 1] = val;
+        }
     }
     __syncthreads();
     int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
-    for (int c = tid; c <= NCELLS; c += 256) gs[c] = start[c];
-    uint16_t* gi = p.grid_idx + (size_t)f * p.fr.kp_stride;
-    for (int i = tid; i < nv; i += 256) gi[i] = (uint16_t)(keys[i] & 0xFFFFu);
+    for (int c = tid; c <= NCELLS; c += 1024) gs[c] = start[c];
+    const size_t off = (size_t)f * p.fr.kp_stride;
+    for (int k = tid; k < tot; k += 1024) {
+        const int i = sorted[k];
+        p.grid_idx[off + k] = (uint16_t)i;
+        p.grid_xy[off + k] = make_float2(K[i].x, K[i].y);
+        p.grid_oct[off + k] = (uint8_t)K[i].octave;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------ gather
@@ -248,7 +267,8 @@ __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
     const int ncell = (w.cx1 - w.cx0 + 1) * ny;
     const int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
     const uint16_t* gi = p.grid_idx + (size_t)f * p.fr.kp_stride;
-    const mam_keypoint* K = p.fr.keys + (size_t)f * p.fr.kp_stride;
+    const float2* gxy = p.grid_xy + (size_t)f * p.fr.kp_stride;
+    const uint8_t* gct = p.grid_oct + (size_t)f * p.fr.kp_stride;
     const uint8_t* D = p.fr.desc + (size_t)f * p.fr.kp_stride * 32;
     uint32_t* pool = p.pool + (size_t)f * p.pool_per_frame;
     int base = FILL ? p.cand_off[(size_t)f * p.unit_stride + j] : 0;
@@ -262,13 +282,13 @@ __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
             k0 = gs[cell];
             k1 = gs[cell + 1];
             for (int k = k0; k < k1; k++) {
-                const int idx = gi[k];
-                const mam_keypoint& kp = K[idx];
+                const int oct = gct[k];
                 if (w.checkL) {
-                    if (kp.octave < w.minL) continue;
-                    if (w.maxL >= 0 && kp.octave > w.maxL) continue;
+                    if (oct < w.minL) continue;
+                    if (w.maxL >= 0 && oct > w.maxL) continue;
                 }
-                const float dx = kp.x - w.x, dy = kp.y - w.y;
+                const float2 xy = gxy[k];
+                const float dx = xy.x - w.x, dy = xy.y - w.y;
                 if (fabsf(dx) < w.r && fabsf(dy) < w.r) cnt++;
             }
         }
@@ -277,16 +297,17 @@ __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
             int o = base + incl - cnt;
             if (cnt > 0) {
                 for (int k = k0; k < k1; k++) {
-                    const int idx = gi[k];
-                    const mam_keypoint& kp = K[idx];
+                    const int oct = gct[k];
                     if (w.checkL) {
-                        if (kp.octave < w.minL) continue;
-                        if (w.maxL >= 0 && kp.octave > w.maxL) continue;
+                        if (oct < w.minL) continue;
+                        if (w.maxL >= 0 && oct > w.maxL) continue;
                     }
-                    const float dx = kp.x - w.x, dy = kp.y - w.y;
+                    const float2 xy = gxy[k];
+                    const float dx = xy.x - w.x, dy = xy.y - w.y;
                     if (fabsf(dx) < w.r && fabsf(dy) < w.r) {
+                        const int idx = gi[k];
                         const int dist = desc_dist(w.desc, D + (size_t)idx * 32);
-                        pool[o++] = (uint32_t)idx | ((uint32_t)dist << 16) | ((uint32_t)kp.octave << 25);
+                        pool[o++] = (uint32_t)idx | ((uint32_t)dist << 16) | ((uint32_t)oct << 25);
                     }
                 }
             }
@@ -332,14 +353,16 @@ __device__ __forceinline__ int rot_bin(float rot) {
     return bin;
 }
 
+constexpr int CAND_LDS = 4096;    // candidate entries of one 64-unit chunk staged in LDS (16 KB)
+
 __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int f = blockIdx.x, lane = threadIdx.x;
     const int S = p.fr.kp_stride;
     const int nwords = (S + 31) / 32;
-    uint32_t* takenb = reinterpret_cast<uint32_t*>(smem);              // S bits
-    int* picked = reinterpret_cast<int*>(smem + ((nwords * 4 + 15) & ~15));  // lowest open lane taking idx (64 = none)
-    int* writer = picked + ((S + 3) & ~3);                                // highest committing lane writing idx
+    uint32_t* takenb = reinterpret_cast<uint32_t*>(smem);                       // S bits
+    int* mark = reinterpret_cast<int*>(smem + ((nwords * 4 + 15) & ~15));       // per keypoint, 64 = none
+    uint32_t* cbuf = reinterpret_cast<uint32_t*>(mark + ((S + 3) & ~3));        // chunk candidates
     __shared__ int hist[MAM_HISTO_LENGTH];
     __shared__ int top[3];
     const int n = frame_n(p.fr, f);
@@ -359,7 +382,7 @@ __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
             }
         takenb[w] = bits;
     }
-    for (int i = lane; i < S; i += 64) { picked[i] = 64; writer[i] = -1; }
+    for (int i = lane; i < S; i += 64) mark[i] = 64;
     if (lane < MAM_HISTO_LENGTH) hist[lane] = 0;
     __syncthreads();
     const int nu = p.n_units[f];
@@ -374,6 +397,15 @@ __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
         const bool active = j < nu;
         const int cnt = active ? cc[j] : 0;
         const int off = active ? co[j] : 0;
+        // the chunk's lists are contiguous in the pool (offsets are an exclusive scan in unit order):
+        // stage them in LDS with coalesced loads, then every lane walks its list from LDS
+        const int cbase = co[j0];
+        const int ctot = wave_sum(cnt);
+        const bool staged = ctot <= CAND_LDS;
+        if (staged)
+            for (int k = lane; k < ctot; k += 64) cbuf[k] = pool[cbase + k];
+        __syncthreads();
+        const uint32_t* lst = staged ? cbuf + (off - cbase) : pool + off;
         int nobs = 0;
         float lang = 0.f;
         if (active) {
@@ -393,7 +425,7 @@ __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
             if (!done) {
                 int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1;
                 for (int t = 0; t < cnt; t++) {
-                    const uint32_t e = pool[off + t];
+                    const uint32_t e = lst[t];
                     const int idx = (int)(e & 0xFFFFu);
                     if ((takenb[idx >> 5] >> (idx & 31)) & 1u) continue;
                     const int dist = (int)((e >> 16) & 0x1FFu);
@@ -415,25 +447,26 @@ __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
             // (2) picks that grow the taken-set; the first open lane whose candidate list holds a keypoint
             //     picked by an EARLIER open lane is stale, lanes before it are final
             const bool takes = !done && assign && nobs > 0;
-            if (takes) atomicMin(&picked[bestIdx], lane);
+            if (takes) atomicMin(&mark[bestIdx], lane);
             __syncthreads();
             bool stale = false;
             if (!done) {
                 for (int t = 0; t < cnt && !stale; t++) {
-                    const int idx = (int)(pool[off + t] & 0xFFFFu);
-                    if (picked[idx] < lane) stale = true;
+                    if (mark[lst[t] & 0xFFFFu] < lane) stale = true;
                 }
             }
             const int jstar = wave_min(stale ? lane : 64);
             __syncthreads();
-            if (takes) picked[bestIdx] = 64;
-            // (3) commit lanes < jstar in lane order: out[] last writer wins, taken bits, counts, events
+            if (takes) mark[bestIdx] = 64;
+            __syncthreads();
+            // (3) commit lanes < jstar in lane order: out[] last writer wins (min of 63-lane = max lane),
+            //     taken bits, counts, events
             const bool commit = !done && lane < jstar;
             const bool cassign = commit && assign;
-            if (cassign) atomicMax(&writer[bestIdx], lane);
+            if (cassign) atomicMin(&mark[bestIdx], 63 - lane);
             __syncthreads();
             if (cassign) {
-                if (writer[bestIdx] == lane) out[bestIdx] = j;
+                if (mark[bestIdx] == 63 - lane) out[bestIdx] = j;
                 if (nobs > 0) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
             }
             nm += wave_sum(cassign ? 1 : 0);
@@ -446,7 +479,7 @@ __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
                 nev += __shfl(incl, 63, 64);
             }
             __syncthreads();
-            if (cassign) writer[bestIdx] = -1;
+            if (cassign) mark[bestIdx] = 64;
             done = done || commit;
             __syncthreads();
         }
@@ -605,6 +638,8 @@ struct mam_match_ctx {
     int pool_per_unit = 96;
     // scratch
     DevBuf<uint16_t> grid_idx;
+    DevBuf<float2> grid_xy;
+    DevBuf<uint8_t> grid_oct;
     DevBuf<int32_t> grid_start, cand_cnt, cand_off, pool_total, out_n_tmp;
     DevBuf<uint32_t> pool, events;
     // host-API staging
@@ -624,6 +659,8 @@ size_t carve_bytes(size_t count, size_t elem) { return (count * elem + 255) & ~(
 
 int ensure_scratch(mam_match_ctx* c, int F, int kp_stride, int unit_stride, int pool_per_frame) {
     if (int rc = c->grid_idx.alloc((size_t)F * kp_stride)) return rc;
+    if (int rc = c->grid_xy.alloc((size_t)F * kp_stride)) return rc;
+    if (int rc = c->grid_oct.alloc((size_t)F * kp_stride)) return rc;
     if (int rc = c->grid_start.alloc((size_t)F * (mam::NCELLS + 1))) return rc;
     if (int rc = c->cand_cnt.alloc((size_t)F * unit_stride)) return rc;
     if (int rc = c->cand_off.alloc((size_t)F * unit_stride)) return rc;
@@ -639,6 +676,8 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     if (a.fr.kp_stride > mam::GRID_SORT_MAX || a.fr.kp_stride <= 0 || a.unit_stride <= 0) return MAM_ERR_ARG;
     if (int rc = ensure_scratch(c, F, a.fr.kp_stride, a.unit_stride, a.pool_per_frame)) return rc;
     a.grid_idx = c->grid_idx.p;
+    a.grid_xy = c->grid_xy.p;
+    a.grid_oct = c->grid_oct.p;
     a.grid_start = c->grid_start.p;
     a.cand_cnt = c->cand_cnt.p;
     a.cand_off = c->cand_off.p;
@@ -648,7 +687,7 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     MAM_HIP(hipMemsetAsync(a.out_n, 0, sizeof(int32_t) * F, s));
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
-        hipLaunchKernelGGL(mam::k_grid, dim3(F), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(mam::k_grid, dim3(F), dim3(1024), 0, s, a);
     }
     const long long waves = (long long)F * a.unit_stride;
     const int blocks = (int)((waves + 3) / 4);
@@ -661,7 +700,7 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     {
         mam::StageTimer::Scope sc(&c->timer, s, 2);
         const int S = a.fr.kp_stride;
-        const size_t lds = ((((S + 31) / 32) * 4 + 15) & ~15) + 2 * 4 * ((S + 3) & ~3);
+        const size_t lds = ((((S + 31) / 32) * 4 + 15) & ~15) + 4 * ((S + 3) & ~3) + 4 * (size_t)mam::CAND_LDS;
         hipLaunchKernelGGL(mam::k_resolve, dim3(F), dim3(64), lds, s, a);
     }
     MAM_HIP(hipGetLastError());

@@ -150,8 +150,10 @@ def test_projection_batch_device(gpu_lib, oracle, frames):
     t_out = torch.zeros((Fn, S), dtype=torch.int32, device=dev)
     t_nm = torch.zeros(Fn, dtype=torch.int32, device=dev)
     fr = FramesDev(Fn, S, t_keys.data_ptr(), t_desc.data_ptr(), t_cnt.data_ptr(), None)
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
     M.search_by_projection_batch_device(FD[0], fr, t_mps.data_ptr(), ms, t_nmps.data_ptr(), 3.0, t_out.data_ptr(),
-                                        t_nm.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+                                        t_nm.data_ptr(), stream=st.cuda_stream)
     torch.cuda.synchronize()
     out, nm = t_out.cpu().numpy(), t_nm.cpu().numpy()
     for f in range(Fn):

@@ -103,8 +103,10 @@ def test_batch_device_matches_single(gpu_lib, oracle):
     d_kps = torch.zeros((F, cap * 28), dtype=torch.uint8, device="cuda")
     d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device="cuda")
     d_cnt = torch.zeros((F, 2), dtype=torch.int32, device="cuda")
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
     ext.extract_batch_device(d_img.data_ptr(), F, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(), cap,
-                             d_cnt.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+                             d_cnt.data_ptr(), stream=st.cuda_stream)
     torch.cuda.synchronize()
     cnt = d_cnt.cpu().numpy()
     kps = d_kps.cpu().numpy().view(KP_DTYPE).reshape(F, cap)
