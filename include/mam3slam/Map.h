@@ -1,0 +1,171 @@
+/*
+ * Minimal map model: the fields and methods of the reference's Frame, KeyFrame, MapPoint and Map that the hot
+ * path reads or writes, with the reference's names, so the ORBmatcher / LocalBundleAdjustment wrappers keep
+ * the reference signatures. In the reference these are the real classes (src/Frame.cc, src/KeyFrame.cc,
+ * src/MapPoint.cc, src/Map.cc); INTEGRATION.md shows the wrappers compiled against them instead.
+ *
+ * Scope: mono agents (mvuRight = -1, no second camera), Pinhole camera, no IMU. Mutex discipline follows the
+ * reference where the hot path takes locks (observations, pose, Map::mMutexMapUpdate).
+ */
+#ifndef MAM3SLAM_MAP_H
+#define MAM3SLAM_MAP_H
+
+#include <map>
+#include <mutex>
+#include <set>
+#include <tuple>
+#include <vector>
+
+#include "Types.h"
+
+namespace MAM3SLAM {
+
+class ORBextractor;
+class KeyFrame;
+class MapPoint;
+class Map;
+
+/* Frame (src/Frame.cc:289-382, mono constructor without BoW / IMU). */
+class Frame {
+public:
+    Frame() = default;
+    Frame(const ImageView& imGray, ORBextractor* extractor, const Pinhole* pCamera, unsigned long id = 0);
+
+    void SetPose(const SE3f& Tcw) { mTcw = Tcw; mbHasPose = true; }
+    const SE3f& GetPose() const { return mTcw; }
+
+    /* mam_frame_geom view of the static image bounds / grid / scale tables (Frame.cc:341-342, 782-809). */
+    mam_frame_geom Geom() const;
+
+    unsigned long mnId = 0;
+    int N = 0;
+    std::vector<KeyPoint> mvKeys, mvKeysUn;
+    Mat8U mDescriptors;
+    std::vector<MapPoint*> mvpMapPoints;
+    std::vector<bool> mvbOutlier;
+    int monoLeft = -1;
+
+    int mnScaleLevels = 0;
+    float mfScaleFactor = 0.f;
+    std::vector<float> mvScaleFactors, mvInvScaleFactors, mvLevelSigma2, mvInvLevelSigma2;
+
+    float mnMinX = 0.f, mnMaxX = 0.f, mnMinY = 0.f, mnMaxY = 0.f;
+    float mfGridElementWidthInv = 0.f, mfGridElementHeightInv = 0.f;
+
+    const Pinhole* mpCamera = nullptr;
+    SE3f mTcw;
+    bool mbHasPose = false;
+};
+
+/* KeyFrame (src/KeyFrame.cc): the copy of a Frame plus covisibility, BA bookkeeping and the BoW feature
+ * vector SearchForTriangulation walks. */
+class KeyFrame {
+public:
+    KeyFrame(const Frame& F, Map* pMap, unsigned long id);
+
+    SE3f GetPose();
+    SE3f GetPoseInverse();
+    void SetPose(const SE3f& Tcw);
+    void GetCameraCenter(float Ow[3]);
+
+    std::vector<MapPoint*> GetMapPointMatches();
+    MapPoint* GetMapPoint(size_t idx);
+    void AddMapPoint(MapPoint* pMP, size_t idx);
+    void EraseMapPointMatch(int idx);
+    void EraseMapPointMatch(MapPoint* pMP);
+
+    /* mvpOrderedConnectedKeyFrames (set by the caller's covisibility graph; KeyFrame.cc:237-241). */
+    void SetVectorCovisibleKeyFrames(const std::vector<KeyFrame*>& v) { mvpOrderedConnectedKeyFrames = v; }
+    std::vector<KeyFrame*> GetVectorCovisibleKeyFrames() { return mvpOrderedConnectedKeyFrames; }
+
+    bool isBad() const { return mbBad; }
+    void SetBadFlag() { mbBad = true; }
+    Map* GetMap() const { return mpMap; }
+    mam_frame_geom Geom() const;
+
+    unsigned long mnId;
+    unsigned long mnBALocalForKF = 0, mnBAFixedForKF = 0;
+    const int N;
+    std::vector<KeyPoint> mvKeys, mvKeysUn;
+    std::vector<float> mvuRight;
+    Mat8U mDescriptors;
+    int mnScaleLevels;
+    std::vector<float> mvScaleFactors, mvLevelSigma2, mvInvLevelSigma2;
+    float mnMinX, mnMaxX, mnMinY, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv;
+    const Pinhole* mpCamera;
+    /* DBoW2::FeatureVector: node id -> feature indices (ascending node ids). */
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+
+private:
+    std::mutex mMutexPose, mMutexFeatures;
+    SE3f mTcw, mTwc;
+    std::vector<MapPoint*> mvpMapPoints;
+    std::vector<KeyFrame*> mvpOrderedConnectedKeyFrames;
+    bool mbBad = false;
+    Map* mpMap;
+};
+
+/* MapPoint (src/MapPoint.cc). Observations keyed by KeyFrame* exactly like the reference (std::map order). */
+class MapPoint {
+public:
+    MapPoint(const float Pos[3], KeyFrame* pRefKF, Map* pMap, unsigned long id);
+
+    void GetWorldPos(float Pos[3]);
+    void SetWorldPos(const float Pos[3]);
+    std::map<KeyFrame*, std::tuple<int, int>> GetObservations();
+    int Observations();
+    void AddObservation(KeyFrame* pKF, int idx);          /* MapPoint.cc:133-166, mono */
+    void EraseObservation(KeyFrame* pKF);                 /* MapPoint.cc:168-201 */
+    std::tuple<int, int> GetIndexInKeyFrame(KeyFrame* pKF);
+    void SetBadFlag();                                    /* MapPoint.cc:216-239 */
+    bool isBad();
+    void UpdateNormalAndDepth();                          /* MapPoint.cc:426-493 */
+    void SetDescriptor(const uint8_t d[32]);
+    void GetDescriptor(uint8_t d[32]);
+    Map* GetMap() const { return mpMap; }
+    void GetNormal(float n[3]);
+    float GetMinDistanceInvariance() { return 0.8f * mfMinDistance; }
+    float GetMaxDistanceInvariance() { return 1.2f * mfMaxDistance; }
+
+    unsigned long mnId;
+    unsigned long mnBALocalForKF = 0;
+    /* Tracking fields written by Frame::isInFrustum (Frame.cc:512-586), read by SearchByProjection. */
+    bool mbTrackInView = false;
+    float mTrackProjX = 0.f, mTrackProjY = 0.f, mTrackDepth = 0.f, mTrackViewCos = 0.f;
+    int mnTrackScaleLevel = 0;
+
+private:
+    std::mutex mMutexPos, mMutexFeatures;
+    float mWorldPos[3];
+    float mNormalVector[3] = {0.f, 0.f, 0.f};
+    float mfMinDistance = 0.f, mfMaxDistance = 0.f;
+    uint8_t mDescriptor[32] = {0};
+    std::map<KeyFrame*, std::tuple<int, int>> mObservations;
+    int nObs = 0;
+    bool mbBad = false;
+    KeyFrame* mpRefKF;
+    Map* mpMap;
+};
+
+/* Map (src/Map.cc): init keyframe id, the map-update mutex, change counter. */
+class Map {
+public:
+    explicit Map(unsigned long initKFid = 0) : mnInitKFid(initKFid) {}
+    unsigned long GetInitKFid() const { return mnInitKFid; }
+    bool IsInertial() const { return false; }
+    void EraseMapPoint(MapPoint* pMP) { std::lock_guard<std::mutex> l(mMutexMap); mspMapPoints.erase(pMP); }
+    void AddMapPoint(MapPoint* pMP) { std::lock_guard<std::mutex> l(mMutexMap); mspMapPoints.insert(pMP); }
+    void IncreaseChangeIndex() { std::lock_guard<std::mutex> l(mMutexMap); mnMapChange++; }
+    int GetMapChangeIndex() { std::lock_guard<std::mutex> l(mMutexMap); return mnMapChange; }
+
+    std::mutex mMutexMapUpdate;
+
+private:
+    unsigned long mnInitKFid;
+    std::mutex mMutexMap;
+    std::set<MapPoint*> mspMapPoints;
+    int mnMapChange = 0;
+};
+
+}  // namespace MAM3SLAM
+#endif

@@ -1,0 +1,48 @@
+/*
+ * MAM3SLAM::Optimizer::LocalBundleAdjustment — the reference entry point (include/Optimizer.h:57,
+ * src/Optimizer.cc:1116-1498) with the g2o solve replaced by the gfx950 solver (include/mam_lba.h).
+ * The window build (local keyframes by covisibility, local MapPoints, fixed keyframes), the early returns
+ * (no fixed keyframe, stop flag), the outlier erase (chi2 > 5.991 || depth <= 0) and the write-back under
+ * Map::mMutexMapUpdate follow the reference line by line; only `optimizer.optimize(10)` runs on the GPU.
+ */
+#ifndef MAM3SLAM_OPTIMIZER_H
+#define MAM3SLAM_OPTIMIZER_H
+
+#include <list>
+#include <vector>
+
+#include "../mam_lba.h"
+#include "Map.h"
+
+namespace MAM3SLAM {
+
+/* The g2o graph LocalBundleAdjustment builds, in the reference's insertion order (Optimizer.cc:1212-1394). */
+struct LocalBAWindow {
+    std::list<KeyFrame*> lLocalKeyFrames, lFixedCameras;
+    std::list<MapPoint*> lLocalMapPoints;
+    int num_fixedKF = 0;
+    unsigned long maxKFid = 0;
+    /* flattened problem (owned storage for mam_lba_problem) */
+    std::vector<KeyFrame*> vpKF;                 /* pose vertices: local then fixed */
+    std::vector<MapPoint*> vpMP;
+    std::vector<int64_t> pose_id, point_id;
+    std::vector<uint8_t> pose_fixed;
+    std::vector<double> pose_q, pose_t, point_xyz, edge_obs, edge_inv_sigma2;
+    std::vector<int32_t> pose_cam, edge_point, edge_pose;
+    std::vector<float> cams;
+    std::vector<const Pinhole*> camera_list;
+    mam_lba_problem Problem(int iterations = 10) const;
+};
+
+class Optimizer {
+public:
+    static void LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& num_fixedKF,
+                                      int& num_OptKF, int& num_MPs, int& num_edges);
+
+    /* Optimizer.cc:1118-1180 + vertex/edge setup :1212-1394. Returns false where the reference returns before
+     * optimizing because no keyframe is fixed (:1182-1186). */
+    static bool BuildLocalBAWindow(KeyFrame* pKF, Map* pMap, LocalBAWindow& w);
+};
+
+}  // namespace MAM3SLAM
+#endif

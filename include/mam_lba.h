@@ -69,9 +69,10 @@ typedef struct mam_lba_ctx mam_lba_ctx;
 int mam_lba_create(int device, mam_lba_ctx** out);
 void mam_lba_destroy(mam_lba_ctx* ctx);
 
-/* Host buffers in, host buffers out; synchronous. stop_flag (may be NULL) is polled between iterations and
- * Levenberg trials like g2o's force-stop flag (sparse_optimizer.cpp:377, levenberg.cpp:149). */
-int mam_lba_solve(mam_lba_ctx* ctx, const mam_lba_problem* problem, const volatile int32_t* stop_flag,
+/* Host buffers in, host buffers out; synchronous. stop_flag (may be NULL) is the caller's `bool* pbStopFlag`
+ * (one byte, written by another thread), polled between iterations and Levenberg trials like g2o's force-stop
+ * flag (sparse_optimizer.cpp:377, levenberg.cpp:149). */
+int mam_lba_solve(mam_lba_ctx* ctx, const mam_lba_problem* problem, const volatile uint8_t* stop_flag,
                   mam_lba_result* result);
 
 int mam_lba_set_profiling(mam_lba_ctx* ctx, int enable);

@@ -38,6 +38,9 @@ extern "C" {
 #define MAM_TH_HIGH 100
 #define MAM_TH_LOW 50
 #define MAM_HISTO_LENGTH 30
+/* out_kp_to_last value for a keypoint the rotation check un-assigned: the reference sets
+ * CurrentFrame.mvpMapPoints[i] = NULL there (ORBmatcher.cc:1876-1881), clearing whatever it held. */
+#define MAM_MATCH_CLEARED (-2)
 
 /* Frame-level geometry shared by every frame of a call (one agent = one camera). */
 typedef struct mam_frame_geom {
@@ -108,8 +111,8 @@ int mam_search_by_projection(mam_match_ctx* ctx, const mam_frame_geom* geom, int
                              float th, int far_points, float th_far_points, float nnratio, int32_t* out_kp_to_mp);
 
 /* SearchByProjection(CurrentFrame, LastFrame, th, bMono) with ORBmatcher(nnratio, checkOri).
- * out_kp_to_last[n_cur]: index i of the last-frame entry whose MapPoint was assigned, else -1 (after the
- * rotation-consistency pass). tlw/mb are only read when !mono (bForward/bBackward, ORBmatcher.cc:1688-1692). */
+ * out_kp_to_last[n_cur]: index i of the last-frame entry whose MapPoint was assigned, MAM_MATCH_CLEARED (-2)
+ * if the assignment was removed by the rotation-consistency pass (slot must become NULL), else -1 (untouched). tlw/mb are only read when !mono (bForward/bBackward, ORBmatcher.cc:1688-1692). */
 int mam_search_by_projection_motion(mam_match_ctx* ctx, const mam_frame_geom* geom, int n_cur,
                                     const mam_keypoint* keys, const uint8_t* desc, const uint8_t* taken,
                                     const mam_pose* tcw, const mam_pose* tlw, float mb, const mam_pinhole* cam,

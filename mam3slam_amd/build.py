@@ -1,4 +1,5 @@
-"""Build the gfx950 shared library (libmam_gpu.so) in-tree with hipcc.
+"""Build the gfx950 shared library (libmam_gpu.so) in-tree with hipcc, and the C++ host API library
+(libmam3slam.so: MAM3SLAM::ORBextractor / ORBmatcher / Optimizer over the C-ABI) with g++.
 
 Invoked by __graft_entry__.build() and by the tests. The library is the product: HIP kernels + host
 orchestration + C-ABI (include/mam_orb.h). No torch extension, no JIT cache: the .so sits next to this file
@@ -32,16 +33,51 @@ FLAGS = [
 ]
 
 
+HOST = os.path.join(HERE, "host")
+HOST_LIB = os.path.join(HERE, "libmam3slam.so")
+INCLUDE = os.path.join(HERE, "..", "include")
+CXX = os.environ.get("CXX", "g++")
+HOST_FLAGS = ["-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-Wall", "-Wextra", "-Wno-unused-parameter"]
+
+
 def _sources():
     return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
 
 
 def _deps():
     out = []
-    for root in (CSRC, os.path.join(HERE, "..", "include")):
-        for f in os.listdir(root):
-            out.append(os.path.join(root, f))
+    for root, _, files in os.walk(CSRC):
+        out += [os.path.join(root, f) for f in files]
+    for root, _, files in os.walk(INCLUDE):
+        out += [os.path.join(root, f) for f in files]
     return out
+
+
+def _host_sources():
+    return sorted(os.path.join(HOST, f) for f in os.listdir(HOST) if f.endswith(".cpp"))
+
+
+def host_needs_build() -> bool:
+    if not os.path.exists(HOST_LIB):
+        return True
+    t = os.path.getmtime(HOST_LIB)
+    deps = _host_sources() + [os.path.join(r, f) for r, _, fs in os.walk(INCLUDE) for f in fs] + [LIB]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """libmam3slam.so links libmam_gpu.so from the same directory (rpath $ORIGIN)."""
+    if not force and not host_needs_build():
+        return HOST_LIB
+    cmd = [CXX, *HOST_FLAGS, "-I", INCLUDE, "-o", HOST_LIB + ".tmp", *_host_sources(), "-L", HERE, "-l:libmam_gpu.so",
+           "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"host build failed ({r.returncode}):\n{r.stderr[-8000:]}")
+    os.replace(HOST_LIB + ".tmp", HOST_LIB)
+    return HOST_LIB
 
 
 def needs_build() -> bool:
@@ -52,8 +88,13 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
-        return LIB
+    if force or needs_build():
+        _build_gpu(verbose)
+    build_host(force=force, verbose=verbose)
+    return LIB
+
+
+def _build_gpu(verbose: bool) -> None:
     cmd = [HIPCC, *FLAGS, "-o", LIB + ".tmp", *_sources()]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -61,7 +102,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-8000:]}")
     os.replace(LIB + ".tmp", LIB)
-    return LIB
 
 
 if __name__ == "__main__":

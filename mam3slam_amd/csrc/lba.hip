@@ -680,7 +680,7 @@ int mam_lba_stage_times(mam_lba_ctx* c, double* ms_out, int64_t* launches_out) {
     return MAM_OK;
 }
 
-int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile int32_t* stop_flag, mam_lba_result* r) {
+int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8_t* stop_flag, mam_lba_result* r) {
     if (!c || !p || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || !p->cams || p->n_cams < 1)
         return MAM_ERR_ARG;
     if ((p->n_poses > 0 && (!p->pose_id || !p->pose_fixed || !p->pose_q || !p->pose_t)) ||

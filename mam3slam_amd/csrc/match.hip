@@ -505,7 +505,7 @@ __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
         for (int e = lane; e < nev; e += 64) {
             const int bin = (int)(ev[e] >> 16);
             if (bin != top[0] && bin != top[1] && bin != top[2]) {
-                out[ev[e] & 0xFFFFu] = -1;
+                out[ev[e] & 0xFFFFu] = MAM_MATCH_CLEARED;
                 removed++;
             }
         }

@@ -1,0 +1,205 @@
+// MAM3SLAM::Optimizer::LocalBundleAdjustment (include/mam3slam/Optimizer.h).
+// Window build, outlier erase and write-back follow src/Optimizer.cc:1116-1498 line by line (mono agents); the
+// g2o `optimizer.optimize(10)` is mam_lba_solve on the GPU (include/mam_lba.h).
+#include <cmath>
+#include <stdexcept>
+#include <string>
+
+#include "mam3slam/Optimizer.h"
+
+namespace MAM3SLAM {
+
+namespace {
+
+struct ThreadLBA {
+    mam_lba_ctx* ctx = nullptr;
+    ~ThreadLBA() {
+        if (ctx) mam_lba_destroy(ctx);
+    }
+};
+thread_local ThreadLBA t_lba;
+
+mam_lba_ctx* lbaCtx() {
+    if (!t_lba.ctx) {
+        const int rc = mam_lba_create(0, &t_lba.ctx);
+        if (rc < 0) throw std::runtime_error(std::string("mam_lba_create failed: ") + mam_last_error());
+    }
+    return t_lba.ctx;
+}
+
+}  // namespace
+
+mam_lba_problem LocalBAWindow::Problem(int iterations) const {
+    mam_lba_problem p;
+    p.n_poses = (int32_t)vpKF.size();
+    p.pose_id = pose_id.data();
+    p.pose_fixed = pose_fixed.data();
+    p.pose_q = pose_q.data();
+    p.pose_t = pose_t.data();
+    p.pose_cam = pose_cam.data();
+    p.n_points = (int32_t)vpMP.size();
+    p.point_id = point_id.data();
+    p.point_xyz = point_xyz.data();
+    p.n_edges = (int32_t)edge_point.size();
+    p.edge_point = edge_point.data();
+    p.edge_pose = edge_pose.data();
+    p.edge_obs = edge_obs.data();
+    p.edge_inv_sigma2 = edge_inv_sigma2.data();
+    p.n_cams = (int32_t)camera_list.size();
+    p.cams = cams.data();
+    p.huber_delta = (double)(float)std::sqrt(5.991);   // const float thHuberMono = sqrt(5.991) (:1275)
+    p.iterations = iterations;
+    return p;
+}
+
+bool Optimizer::BuildLocalBAWindow(KeyFrame* pKF, Map* pMap, LocalBAWindow& w) {
+    w = LocalBAWindow();
+    // Local KeyFrames: first breadth search from the current keyframe (:1118-1132)
+    w.lLocalKeyFrames.push_back(pKF);
+    pKF->mnBALocalForKF = pKF->mnId;
+    Map* pCurrentMap = pKF->GetMap();
+    const std::vector<KeyFrame*> vNeighKFs = pKF->GetVectorCovisibleKeyFrames();
+    for (KeyFrame* pKFi : vNeighKFs) {
+        pKFi->mnBALocalForKF = pKF->mnId;
+        if (!pKFi->isBad() && pKFi->GetMap() == pCurrentMap) w.lLocalKeyFrames.push_back(pKFi);
+    }
+    // Local MapPoints seen in local KeyFrames (:1134-1160)
+    w.num_fixedKF = 0;
+    for (KeyFrame* pKFi : w.lLocalKeyFrames) {
+        if (pKFi->mnId == pMap->GetInitKFid()) w.num_fixedKF = 1;
+        const std::vector<MapPoint*> vpMPs = pKFi->GetMapPointMatches();
+        for (MapPoint* pMP : vpMPs) {
+            if (pMP && !pMP->isBad() && pMP->GetMap() == pCurrentMap && pMP->mnBALocalForKF != pKF->mnId) {
+                w.lLocalMapPoints.push_back(pMP);
+                pMP->mnBALocalForKF = pKF->mnId;
+            }
+        }
+    }
+    // Fixed KeyFrames: observers of local MapPoints that are not local (:1162-1178)
+    for (MapPoint* pMP : w.lLocalMapPoints) {
+        const auto observations = pMP->GetObservations();
+        for (const auto& obs : observations) {
+            KeyFrame* pKFi = obs.first;
+            if (pKFi->mnBALocalForKF != pKF->mnId && pKFi->mnBAFixedForKF != pKF->mnId) {
+                pKFi->mnBAFixedForKF = pKF->mnId;
+                if (!pKFi->isBad() && pKFi->GetMap() == pCurrentMap) w.lFixedCameras.push_back(pKFi);
+            }
+        }
+    }
+    w.num_fixedKF = (int)w.lFixedCameras.size() + w.num_fixedKF;
+    if (w.num_fixedKF == 0) return false;   // :1182-1186
+
+    // Vertices (:1212-1243): local keyframes (init KF fixed), then fixed cameras
+    auto camIndex = [&](const Pinhole* c) {
+        for (size_t i = 0; i < w.camera_list.size(); i++)
+            if (w.camera_list[i] == c) return (int32_t)i;
+        w.camera_list.push_back(c);
+        for (int k = 0; k < 4; k++) w.cams.push_back(c->mvParameters[k]);
+        return (int32_t)(w.camera_list.size() - 1);
+    };
+    std::map<KeyFrame*, int32_t> kfIndex;
+    auto addPose = [&](KeyFrame* pKFi, bool fixed) {
+        const SE3f Tcw = pKFi->GetPose();
+        kfIndex[pKFi] = (int32_t)w.vpKF.size();
+        w.vpKF.push_back(pKFi);
+        w.pose_id.push_back((int64_t)pKFi->mnId);
+        w.pose_fixed.push_back(fixed ? 1 : 0);
+        for (int k = 0; k < 4; k++) w.pose_q.push_back((double)Tcw.q[k]);   // unit_quaternion().cast<double>()
+        for (int k = 0; k < 3; k++) w.pose_t.push_back((double)Tcw.t[k]);
+        w.pose_cam.push_back(camIndex(pKFi->mpCamera));
+        if (pKFi->mnId > w.maxKFid) w.maxKFid = pKFi->mnId;
+    };
+    for (KeyFrame* pKFi : w.lLocalKeyFrames) addPose(pKFi, pKFi->mnId == pMap->GetInitKFid());
+    for (KeyFrame* pKFi : w.lFixedCameras) addPose(pKFi, true);
+
+    // MapPoint vertices and mono edges (:1245-1394), edge insertion order = point order x observation order
+    for (MapPoint* pMP : w.lLocalMapPoints) {
+        float pos[3];
+        pMP->GetWorldPos(pos);
+        const int32_t pi = (int32_t)w.vpMP.size();
+        w.vpMP.push_back(pMP);
+        w.point_id.push_back((int64_t)(pMP->mnId + w.maxKFid + 1));
+        for (int k = 0; k < 3; k++) w.point_xyz.push_back((double)pos[k]);
+        const auto observations = pMP->GetObservations();
+        for (const auto& obs : observations) {
+            KeyFrame* pKFi = obs.first;
+            if (pKFi->isBad() || pKFi->GetMap() != pCurrentMap) continue;
+            const int leftIndex = std::get<0>(obs.second);
+            if (leftIndex == -1) continue;
+            if (pKFi->mvuRight[leftIndex] >= 0)
+                throw std::invalid_argument("LocalBundleAdjustment: stereo observations are out of scope");
+            auto it = kfIndex.find(pKFi);
+            if (it == kfIndex.end()) continue;   // unreachable: every observer is local or fixed
+            const KeyPoint& kpUn = pKFi->mvKeysUn[leftIndex];
+            w.edge_point.push_back(pi);
+            w.edge_pose.push_back(it->second);
+            w.edge_obs.push_back((double)kpUn.pt.x);
+            w.edge_obs.push_back((double)kpUn.pt.y);
+            w.edge_inv_sigma2.push_back((double)pKFi->mvInvLevelSigma2[kpUn.octave]);
+        }
+    }
+    return true;
+}
+
+void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& num_fixedKF,
+                                      int& num_OptKF, int& num_MPs, int& num_edges) {
+    LocalBAWindow w;
+    const bool ok = BuildLocalBAWindow(pKF, pMap, w);
+    num_fixedKF = w.num_fixedKF;
+    if (!ok) return;
+    num_OptKF = (int)w.lLocalKeyFrames.size();
+    (void)num_MPs;                             // never written by the reference either
+    num_edges = (int)w.edge_point.size();
+    if (pbStopFlag && *pbStopFlag) return;     // :1406-1408
+
+    const mam_lba_problem prob = w.Problem(10);
+    std::vector<double> q(w.pose_q.size()), t(w.pose_t.size()), x(w.point_xyz.size()), chi2(w.edge_point.size());
+    std::vector<uint8_t> depth(w.edge_point.size());
+    mam_lba_result res;
+    res.pose_q = q.data();
+    res.pose_t = t.data();
+    res.point_xyz = x.data();
+    res.edge_chi2 = chi2.data();
+    res.edge_depth_ok = depth.data();
+    // g2o polls the force-stop flag between iterations (setForceStopFlag, :1203-1204); so does the solver
+    static_assert(sizeof(bool) == 1, "pbStopFlag is read as one byte");
+    const int rc = mam_lba_solve(lbaCtx(), &prob, reinterpret_cast<const volatile uint8_t*>(pbStopFlag), &res);
+    if (rc < 0) throw std::runtime_error(std::string("mam_lba_solve failed: ") + mam_last_error());
+
+    // Check inlier observations (:1413-1430)
+    std::vector<std::pair<KeyFrame*, MapPoint*>> vToErase;
+    vToErase.reserve(w.edge_point.size());
+    for (size_t i = 0; i < w.edge_point.size(); i++) {
+        MapPoint* pMP = w.vpMP[w.edge_point[i]];
+        if (pMP->isBad()) continue;
+        if (chi2[i] > 5.991 || !depth[i]) vToErase.push_back(std::make_pair(w.vpKF[w.edge_pose[i]], pMP));
+    }
+
+    std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);   // :1463
+    for (auto& e : vToErase) {                                   // :1465-1474
+        e.first->EraseMapPointMatch(e.second);
+        e.second->EraseObservation(e.first);
+    }
+    // Recover optimized data (:1478-1494): local keyframes, then points
+    size_t k = 0;
+    for (KeyFrame* pKFi : w.lLocalKeyFrames) {
+        SE3f Tiw;
+        for (int j = 0; j < 4; j++) Tiw.q[j] = (float)q[4 * k + j];
+        for (int j = 0; j < 3; j++) Tiw.t[j] = (float)t[3 * k + j];
+        // Sophus::SE3f(Quaternionf, t) normalises the quaternion (so3.hpp:481-487)
+        const float n = std::sqrt(Tiw.q[0] * Tiw.q[0] + Tiw.q[1] * Tiw.q[1] + Tiw.q[2] * Tiw.q[2] + Tiw.q[3] * Tiw.q[3]);
+        for (int j = 0; j < 4; j++) Tiw.q[j] /= n;
+        pKFi->SetPose(Tiw);
+        k++;
+    }
+    size_t p = 0;
+    for (MapPoint* pMP : w.lLocalMapPoints) {
+        const float pos[3] = {(float)x[3 * p], (float)x[3 * p + 1], (float)x[3 * p + 2]};
+        pMP->SetWorldPos(pos);
+        pMP->UpdateNormalAndDepth();
+        p++;
+    }
+    pMap->IncreaseChangeIndex();
+}
+
+}  // namespace MAM3SLAM

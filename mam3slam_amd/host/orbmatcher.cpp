@@ -1,0 +1,215 @@
+// MAM3SLAM::ORBmatcher over the gfx950 searches (include/mam3slam/ORBmatcher.h, include/mam_match.h).
+// The wrapper only marshals: object pointers -> indices and flags going in, indices -> pointers coming out, with
+// the reference's side effects on Frame::mvpMapPoints (src/ORBmatcher.cc:43-213, 907-1146, 1676-1887).
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "mam3slam/ORBmatcher.h"
+
+namespace MAM3SLAM {
+
+const int ORBmatcher::TH_HIGH = MAM_TH_HIGH;
+const int ORBmatcher::TH_LOW = MAM_TH_LOW;
+const int ORBmatcher::HISTO_LENGTH = MAM_HISTO_LENGTH;
+
+namespace {
+
+void throwOn(int rc, const char* what) {
+    if (rc < 0) throw std::runtime_error(std::string(what) + " failed (" + std::to_string(rc) + "): " + mam_last_error());
+}
+
+// One device context per thread (the reference builds a matcher on the stack at every call site; device
+// state must outlive it). The device is the calling thread's current HIP device (0 unless set).
+struct ThreadCtx {
+    mam_match_ctx* ctx = nullptr;
+    ~ThreadCtx() {
+        if (ctx) mam_match_destroy(ctx);
+    }
+};
+thread_local ThreadCtx t_ctx;
+thread_local int t_device = 0;
+
+mam_match_ctx* ctx() {
+    if (!t_ctx.ctx) throwOn(mam_match_create(t_device, &t_ctx.ctx), "mam_match_create");
+    return t_ctx.ctx;
+}
+
+// Eigen's 3x3 inverse (cofactors, Eigen/src/LU/InverseImpl.h compute_inverse<3x3>), row-major arrays.
+void inverse3(const float m[9], float r[9]) {
+    auto M = [&](int i, int j) { return m[3 * i + j]; };
+    auto cof = [&](int i, int j) {
+        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+        return M(i1, j1) * M(i2, j2) - M(i1, j2) * M(i2, j1);
+    };
+    const float c0[3] = {cof(0, 0), cof(1, 0), cof(2, 0)};
+    const float det = (c0[0] * M(0, 0) + c0[1] * M(1, 0)) + c0[2] * M(2, 0);
+    const float invdet = 1.0f / det;
+    r[1 * 3 + 0] = cof(0, 1) * invdet;
+    r[1 * 3 + 1] = cof(1, 1) * invdet;
+    r[2 * 3 + 0] = cof(0, 2) * invdet;
+    r[1 * 3 + 2] = cof(2, 1) * invdet;
+    r[2 * 3 + 1] = cof(1, 2) * invdet;
+    r[2 * 3 + 2] = cof(2, 2) * invdet;
+    r[0] = c0[0] * invdet;
+    r[1] = c0[1] * invdet;
+    r[2] = c0[2] * invdet;
+}
+
+void mul3(const float a[9], const float b[9], float c[9]) {
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) c[3 * i + j] = (a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j]) + a[3 * i + 2] * b[6 + j];
+}
+
+}  // namespace
+
+ORBmatcher::ORBmatcher(float nnratio, bool checkOri) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
+
+int ORBmatcher::DescriptorDistance(const uint8_t* a, const uint8_t* b) {
+    int d = 0;
+    DescriptorDistances(a, b, 1, &d);
+    return d;
+}
+
+void ORBmatcher::DescriptorDistances(const uint8_t* a, const uint8_t* b, int n, int* out) {
+    static_assert(sizeof(int) == sizeof(int32_t), "int32 output");
+    throwOn(mam_descriptor_distance(ctx(), a, b, n, reinterpret_cast<int32_t*>(out)), "mam_descriptor_distance");
+}
+
+int ORBmatcher::SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th,
+                                   const bool bFarPoints, const float thFarPoints) {
+    const int n = F.N;
+    std::vector<mam_mp_track> mps(vpMapPoints.size());
+    for (size_t i = 0; i < vpMapPoints.size(); i++) {
+        MapPoint* pMP = vpMapPoints[i];
+        mam_mp_track& t = mps[i];
+        std::memset(&t, 0, sizeof(t));
+        if (!pMP) { t.is_bad = 1; continue; }
+        t.track_in_view = pMP->mbTrackInView ? 1 : 0;
+        t.proj_x = pMP->mTrackProjX;
+        t.proj_y = pMP->mTrackProjY;
+        t.view_cos = pMP->mTrackViewCos;
+        t.track_depth = pMP->mTrackDepth;
+        t.scale_level = pMP->mnTrackScaleLevel;
+        t.is_bad = pMP->isBad() ? 1 : 0;
+        t.nobs = pMP->Observations();
+        pMP->GetDescriptor(t.desc);
+    }
+    // the keypoint-taken test of ORBmatcher.cc:88-90
+    std::vector<uint8_t> taken(n > 0 ? n : 1, 0);
+    for (int i = 0; i < n; i++) taken[i] = (F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0) ? 1 : 0;
+    std::vector<int32_t> out(n > 0 ? n : 1, -1);
+    const mam_frame_geom g = F.Geom();
+    const int nm = mam_search_by_projection(ctx(), &g, n, reinterpret_cast<const mam_keypoint*>(F.mvKeysUn.data()),
+                                            F.mDescriptors.data.data(), taken.data(), (int)mps.size(), mps.data(), th,
+                                            bFarPoints ? 1 : 0, thFarPoints, mfNNratio, out.data());
+    throwOn(nm, "mam_search_by_projection");
+    for (int i = 0; i < n; i++)
+        if (out[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[out[i]];
+    return nm;
+}
+
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
+    if (!bMono) throw std::invalid_argument("SearchByProjection(Frame, Frame): stereo is out of scope (mono agents)");
+    const int n = CurrentFrame.N;
+    std::vector<mam_last_entry> last(LastFrame.N);
+    for (int i = 0; i < LastFrame.N; i++) {
+        mam_last_entry& e = last[i];
+        std::memset(&e, 0, sizeof(e));
+        MapPoint* pMP = LastFrame.mvpMapPoints[i];
+        if (!pMP || LastFrame.mvbOutlier[i]) continue;   // ORBmatcher.cc:1697-1701
+        e.valid = 1;
+        pMP->GetWorldPos(e.pos);
+        e.angle = LastFrame.mvKeysUn[i].angle;
+        e.octave = LastFrame.mvKeys[i].octave;
+        e.nobs = pMP->Observations();
+        pMP->GetDescriptor(e.desc);
+    }
+    std::vector<uint8_t> taken(n > 0 ? n : 1, 0);
+    for (int i = 0; i < n; i++)
+        taken[i] = (CurrentFrame.mvpMapPoints[i] && CurrentFrame.mvpMapPoints[i]->Observations() > 0) ? 1 : 0;
+    std::vector<int32_t> out(n > 0 ? n : 1, -1);
+    const mam_frame_geom g = CurrentFrame.Geom();
+    const mam_pose tcw = CurrentFrame.GetPose().toC();
+    const mam_pinhole cam = CurrentFrame.mpCamera->toC();
+    const int nm = mam_search_by_projection_motion(
+        ctx(), &g, n, reinterpret_cast<const mam_keypoint*>(CurrentFrame.mvKeysUn.data()),
+        CurrentFrame.mDescriptors.data.data(), taken.data(), &tcw, nullptr, 0.f, &cam, (int)last.size(), last.data(),
+        th, 1, mbCheckOrientation ? 1 : 0, out.data());
+    throwOn(nm, "mam_search_by_projection_motion");
+    for (int i = 0; i < n; i++) {
+        if (out[i] >= 0) CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[out[i]];
+        else if (out[i] == MAM_MATCH_CLEARED) CurrentFrame.mvpMapPoints[i] = nullptr;
+    }
+    return nm;
+}
+
+void ORBmatcher::ComputeF12(KeyFrame* pKF1, KeyFrame* pKF2, float F12[9], float ep[2]) {
+    // ORBmatcher.cc:913-930: epipole and relative pose; Pinhole.cpp:107-112: F12 = K1^-T [t12]x R12 K2^-1
+    const SE3f T1w = pKF1->GetPose(), T2w = pKF2->GetPose(), Tw2 = pKF2->GetPoseInverse();
+    float Cw[3], C2[3];
+    pKF1->GetCameraCenter(Cw);
+    T2w.map(Cw, C2);
+    pKF2->mpCamera->project(C2, ep);
+    const SE3f T12 = T1w * Tw2;
+    float R12[9];
+    T12.rotationMatrix(R12);
+    const float* t = T12.t;
+    const float tx[9] = {0.f, -t[2], t[1], t[2], 0.f, -t[0], -t[1], t[0], 0.f};
+    float K1[9], K2[9], K1t[9], K1ti[9], K2i[9], A[9], B[9];
+    pKF1->mpCamera->toK(K1);
+    pKF2->mpCamera->toK(K2);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) K1t[3 * i + j] = K1[3 * j + i];
+    inverse3(K1t, K1ti);
+    inverse3(K2, K2i);
+    mul3(K1ti, tx, A);
+    mul3(A, R12, B);
+    mul3(B, K2i, F12);
+}
+
+int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2,
+                                       std::vector<std::pair<size_t, size_t>>& vMatchedPairs, const bool bOnlyStereo,
+                                       const bool bCoarse) {
+    vMatchedPairs.clear();
+    if (bOnlyStereo) return 0;   // mono keyframes: every candidate fails the stereo test (ORBmatcher.cc:1000-1002)
+    float F12[9], ep[2];
+    ComputeF12(pKF1, pKF2, F12, ep);
+    const int n1 = pKF1->N, n2 = pKF2->N;
+    std::vector<uint8_t> has1(n1 > 0 ? n1 : 1, 0), has2(n2 > 0 ? n2 : 1, 0);
+    for (int i = 0; i < n1; i++) has1[i] = pKF1->GetMapPoint(i) ? 1 : 0;
+    for (int i = 0; i < n2; i++) has2[i] = pKF2->GetMapPoint(i) ? 1 : 0;
+    auto flatten = [](const std::map<unsigned int, std::vector<unsigned int>>& fv, std::vector<uint32_t>& ids,
+                      std::vector<int32_t>& off, std::vector<uint32_t>& feats) {
+        ids.clear();
+        off.assign(1, 0);
+        feats.clear();
+        for (const auto& node : fv) {
+            ids.push_back(node.first);
+            feats.insert(feats.end(), node.second.begin(), node.second.end());
+            off.push_back((int32_t)feats.size());
+        }
+        if (feats.empty()) feats.push_back(0);
+        if (ids.empty()) ids.push_back(0);
+    };
+    std::vector<uint32_t> i1, f1, i2, f2;
+    std::vector<int32_t> o1, o2;
+    flatten(pKF1->mFeatVec, i1, o1, f1);
+    flatten(pKF2->mFeatVec, i2, o2, f2);
+    const mam_featvec fv1{(int32_t)pKF1->mFeatVec.size(), i1.data(), o1.data(), f1.data()};
+    const mam_featvec fv2{(int32_t)pKF2->mFeatVec.size(), i2.data(), o2.data(), f2.data()};
+    std::vector<int32_t> out(n1 > 0 ? n1 : 1, -1);
+    const mam_frame_geom g = pKF2->Geom();
+    const int nm = mam_search_for_triangulation(
+        ctx(), &g, n1, reinterpret_cast<const mam_keypoint*>(pKF1->mvKeysUn.data()), pKF1->mDescriptors.data.data(),
+        has1.data(), &fv1, n2, reinterpret_cast<const mam_keypoint*>(pKF2->mvKeysUn.data()),
+        pKF2->mDescriptors.data.data(), has2.data(), &fv2, F12, ep, mbCheckOrientation ? 1 : 0, bCoarse ? 1 : 0,
+        out.data());
+    throwOn(nm, "mam_search_for_triangulation");
+    vMatchedPairs.reserve(nm);
+    for (int i = 0; i < n1; i++)   // ORBmatcher.cc:1135-1143: ascending idx1
+        if (out[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)out[i]));
+    return nm;
+}
+
+}  // namespace MAM3SLAM

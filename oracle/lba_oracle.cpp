@@ -387,7 +387,7 @@ struct Graph {
 
 }  // namespace
 
-extern "C" int oracle_lba_solve(const mam_lba_problem* p, const int32_t* stop_flag, mam_lba_result* r) {
+extern "C" int oracle_lba_solve(const mam_lba_problem* p, const volatile uint8_t* stop_flag, mam_lba_result* r) {
     if (!p || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return MAM_ERR_ARG;
     Graph g;
     g.p = p;

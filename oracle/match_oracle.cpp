@@ -215,7 +215,7 @@ int oracle_search_by_projection_motion(const mam_frame_geom* g, int n, const mam
         for (int i = 0; i < MAM_HISTO_LENGTH; i++) {
             if (i != ind1 && i != ind2 && i != ind3) {
                 for (size_t j = 0; j < rotHist[i].size(); j++) {
-                    out[rotHist[i][j]] = -1;
+                    out[rotHist[i][j]] = MAM_MATCH_CLEARED;
                     nmatches--;
                 }
             }

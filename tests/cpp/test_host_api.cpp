@@ -1,0 +1,526 @@
+// Tests of the C++ host API (include/mam3slam/*.h): the reference-signature wrappers over the C-ABI.
+//
+//   test_host_api cpu   host logic only (no device calls): Sophus-equivalent algebra, MapPoint observation
+//                       bookkeeping, the LocalBundleAdjustment window build (Optimizer.cc:1118-1394).
+//   test_host_api gpu   the wrappers end to end on the GPU vs the CPU oracle (liboracle.so, test
+//                       infrastructure): ORBextractor bit-exact, both SearchByProjection and
+//                       SearchForTriangulation index-exact with the reference's side effects on mvpMapPoints,
+//                       LocalBundleAdjustment write-back / outlier erase vs the oracle solve.
+//
+// Prints "OK <n> checks" and exits 0, or prints the first failure and exits 1.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "mam3slam/ORBextractor.h"
+#include "mam3slam/ORBmatcher.h"
+#include "mam3slam/Optimizer.h"
+
+extern "C" {
+int oracle_orb_extract(const mam_orb_params* p, const uint8_t* img, int w, int h, size_t stride, int lap0, int lap1,
+                       mam_keypoint* kps, uint8_t* desc, int capacity, int* n_out, int* mono_out);
+int oracle_search_by_projection(const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc,
+                                const uint8_t* taken, int n_mps, const mam_mp_track* mps, float th, int far_points,
+                                float th_far_points, float nnratio, int32_t* out);
+int oracle_search_by_projection_motion(const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc,
+                                       const uint8_t* taken, const mam_pose* tcw, const mam_pinhole* cam, int n_last,
+                                       const mam_last_entry* last, float th, int check_ori, int32_t* out);
+int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_keypoint* keys1, const uint8_t* desc1,
+                                    const uint8_t* has_mp1, const mam_featvec* fv1, int n2,
+                                    const mam_keypoint* keys2, const uint8_t* desc2, const uint8_t* has_mp2,
+                                    const mam_featvec* fv2, const float* F12, const float* ep, int check_ori,
+                                    int coarse, int32_t* out);
+int oracle_lba_solve(const mam_lba_problem* p, const volatile uint8_t* stop_flag, mam_lba_result* r);
+}
+
+using namespace MAM3SLAM;
+
+static int g_checks = 0;
+#define CHECK(cond, ...)                                                           \
+    do {                                                                           \
+        g_checks++;                                                                \
+        if (!(cond)) {                                                             \
+            std::fprintf(stderr, "FAIL %s:%d: %s: ", __FILE__, __LINE__, #cond);   \
+            std::fprintf(stderr, __VA_ARGS__);                                     \
+            std::fprintf(stderr, "\n");                                            \
+            std::exit(1);                                                          \
+        }                                                                          \
+    } while (0)
+
+// ---- synthetic inputs ---------------------------------------------------------------------------------------
+
+static std::vector<uint8_t> makeImage(int w, int h, uint32_t seed) {
+    std::mt19937 rng(seed);
+    std::vector<uint8_t> img((size_t)w * h);
+    std::uniform_int_distribution<int> val(20, 235);
+    for (auto& p : img) p = (uint8_t)val(rng);   // start from noise, then paint rectangles
+    std::vector<float> acc((size_t)w * h, 128.f);
+    for (int r = 0; r < 160; r++) {
+        const int x0 = rng() % w, y0 = rng() % h, rw = 8 + rng() % 80, rh = 8 + rng() % 80, v = val(rng);
+        for (int y = y0; y < std::min(h, y0 + rh); y++)
+            for (int x = x0; x < std::min(w, x0 + rw); x++) acc[(size_t)y * w + x] = (float)v;
+    }
+    std::normal_distribution<float> noise(0.f, 6.f);
+    for (size_t i = 0; i < img.size(); i++) {
+        const float v = acc[i] + noise(rng);
+        img[i] = (uint8_t)std::min(255.f, std::max(0.f, v));
+    }
+    return img;
+}
+
+static SE3f poseAround(float angle, float radius) {
+    // camera on a circle looking at the origin (yaw about the y axis)
+    SE3f Twc;
+    const float h = 0.5f * (angle + 3.14159265f);
+    Twc.q[0] = 0.f; Twc.q[1] = std::sin(h); Twc.q[2] = 0.f; Twc.q[3] = std::cos(h);
+    Twc.t[0] = radius * std::sin(angle); Twc.t[1] = 0.f; Twc.t[2] = radius * std::cos(angle);
+    return Twc.inverse();
+}
+
+static Frame emptyFrame(int n, int w, int h, const std::vector<float>& scales, const std::vector<float>& sig2,
+                        const Pinhole* cam) {
+    Frame F;
+    F.N = n;
+    F.mvKeys.resize(n);
+    F.mvKeysUn.resize(n);
+    F.mDescriptors.create(n, 32);
+    F.mvpMapPoints.assign(n, nullptr);
+    F.mvbOutlier.assign(n, false);
+    F.mnScaleLevels = (int)scales.size();
+    F.mvScaleFactors = scales;
+    F.mvLevelSigma2 = sig2;
+    for (float s : sig2) F.mvInvLevelSigma2.push_back(1.0f / s);
+    F.mnMaxX = (float)w;
+    F.mnMaxY = (float)h;
+    F.mfGridElementWidthInv = 64.f / (float)w;
+    F.mfGridElementHeightInv = 48.f / (float)h;
+    F.mpCamera = cam;
+    return F;
+}
+
+// A small map: nkf keyframes on a circle observing npts points (each seen by `obs` consecutive keyframes).
+struct Scene {
+    Pinhole cam{500.f, 500.f, 320.f, 240.f};
+    std::vector<float> scales, sig2;
+    Map map{0};
+    std::vector<std::unique_ptr<KeyFrame>> kfs;
+    std::vector<std::unique_ptr<MapPoint>> mps;
+
+    Scene(int nkf, int npts, int obs, uint32_t seed, float outlier_frac = 0.05f) {
+        float s = 1.f;
+        for (int l = 0; l < 8; l++) {
+            scales.push_back(s);
+            sig2.push_back(s * s);
+            s = (float)((double)s * (double)1.2f);
+        }
+        std::mt19937 rng(seed);
+        std::uniform_real_distribution<float> U(-1.5f, 1.5f), U01(0.f, 1.f);
+        std::normal_distribution<float> N01(0.f, 1.f);
+        const int kp_per_kf = npts;   // upper bound on the observations one keyframe receives
+        for (int k = 0; k < nkf; k++) {
+            Frame F = emptyFrame(kp_per_kf, 640, 480, scales, sig2, &cam);
+            F.SetPose(poseAround(0.08f * (float)k, 6.f));
+            kfs.emplace_back(new KeyFrame(F, &map, (unsigned long)k));
+        }
+        std::vector<int> used(nkf, 0);
+        for (int i = 0; i < npts; i++) {
+            const float X[3] = {U(rng), U(rng), U(rng)};
+            const int k0 = (int)(rng() % (unsigned)(nkf - obs + 1));
+            mps.emplace_back(new MapPoint(X, kfs[k0].get(), &map, (unsigned long)i));
+            MapPoint* pMP = mps.back().get();
+            map.AddMapPoint(pMP);
+            uint8_t d[32];
+            for (auto& b : d) b = (uint8_t)rng();
+            pMP->SetDescriptor(d);
+            for (int k = k0; k < k0 + obs; k++) {
+                KeyFrame* pKF = kfs[k].get();
+                const int idx = used[k]++;
+                float Xc[3], uv[2];
+                pKF->GetPose().map(X, Xc);
+                cam.project(Xc, uv);
+                const int oct = (int)(rng() % 8u);
+                const bool out = U01(rng) < outlier_frac;
+                KeyPoint& kp = pKF->mvKeysUn[idx];
+                kp.pt.x = uv[0] + N01(rng) * scales[oct] + (out ? 25.f : 0.f);
+                kp.pt.y = uv[1] + N01(rng) * scales[oct];
+                kp.octave = oct;
+                pKF->mvKeys[idx] = kp;
+                pKF->AddMapPoint(pMP, idx);
+                pMP->AddObservation(pKF, idx);
+            }
+            // perturb the initial estimate
+            const float Xp[3] = {X[0] + 0.03f * N01(rng), X[1] + 0.03f * N01(rng), X[2] + 0.03f * N01(rng)};
+            pMP->SetWorldPos(Xp);
+        }
+        for (int k = 1; k < nkf; k++) {   // perturb poses (not the init keyframe)
+            SE3f T = kfs[k]->GetPose();
+            T.t[0] += 0.02f * N01(rng);
+            T.t[1] += 0.02f * N01(rng);
+            kfs[k]->SetPose(T);
+        }
+    }
+    void resetMarks() {
+        for (auto& k : kfs) k->mnBALocalForKF = k->mnBAFixedForKF = 0;
+        for (auto& p : mps) p->mnBALocalForKF = 0;
+    }
+};
+
+// ---- CPU tests ----------------------------------------------------------------------------------------------
+
+static void testAlgebra() {
+    SE3f T = poseAround(0.7f, 4.f);
+    const SE3f I = T * T.inverse();
+    CHECK(std::fabs(I.q[3]) > 0.99999f && std::fabs(I.t[0]) < 1e-5f && std::fabs(I.t[2]) < 1e-5f, "T*T^-1 != I");
+    float R[9];
+    T.rotationMatrix(R);
+    const float p[3] = {0.3f, -0.2f, 1.1f};
+    float a[3], b[3];
+    T.map(p, a);
+    for (int i = 0; i < 3; i++) b[i] = R[3 * i] * p[0] + R[3 * i + 1] * p[1] + R[3 * i + 2] * p[2] + T.t[i];
+    for (int i = 0; i < 3; i++) CHECK(std::fabs(a[i] - b[i]) < 1e-5f, "quaternion action vs matrix: %d", i);
+}
+
+static void testObservations() {
+    Scene S(4, 10, 3, 1, 0.f);
+    MapPoint* pMP = S.mps[0].get();
+    auto obs = pMP->GetObservations();
+    CHECK(pMP->Observations() == 3 && obs.size() == 3, "nObs %d", pMP->Observations());
+    KeyFrame* first = obs.begin()->first;
+    const int idx = std::get<0>(obs.begin()->second);
+    first->EraseMapPointMatch(pMP);
+    pMP->EraseObservation(first);
+    CHECK(first->GetMapPoint(idx) == nullptr, "EraseMapPointMatch(pMP)");
+    // nObs 2 <= 2 -> SetBadFlag erases the remaining matches (MapPoint.cc:193-200, 216-239)
+    CHECK(pMP->isBad(), "point with 2 observations must be bad");
+    for (auto& o : obs) CHECK(o.first->GetMapPoint(std::get<0>(o.second)) == nullptr, "bad point still matched");
+}
+
+static void testWindow() {
+    Scene S(12, 300, 4, 7);
+    KeyFrame* pKF = S.kfs[6].get();
+    // covisibility: keyframes 3..9 except 6; 0 is the init keyframe (not covisible here)
+    std::vector<KeyFrame*> cov;
+    for (int k : {5, 7, 4, 8, 3, 9}) cov.push_back(S.kfs[k].get());
+    pKF->SetVectorCovisibleKeyFrames(cov);
+    LocalBAWindow w;
+    CHECK(Optimizer::BuildLocalBAWindow(pKF, &S.map, w), "window must have fixed keyframes");
+    std::vector<unsigned long> local, fixed;
+    for (auto* k : w.lLocalKeyFrames) local.push_back(k->mnId);
+    for (auto* k : w.lFixedCameras) fixed.push_back(k->mnId);
+    CHECK((local == std::vector<unsigned long>{6, 5, 7, 4, 8, 3, 9}), "local keyframe order");
+    // fixed = observers of local points outside the local set, in first-seen order (std::map by pointer order
+    // within a point); the set must be exactly {0,1,2,10,11} minus keyframes sharing no local point
+    for (auto id : fixed) CHECK(id < 3 || id > 9, "fixed keyframe %lu is local", id);
+    CHECK(w.num_fixedKF == (int)fixed.size(), "num_fixedKF %d (init KF 0 not local)", w.num_fixedKF);
+    // local points: every point observed by a local keyframe, once, in discovery order
+    size_t expect = 0;
+    for (auto& mp : S.mps) {
+        bool seen = false;
+        for (auto& o : mp->GetObservations())
+            if (o.first->mnId >= 3 && o.first->mnId <= 9) seen = true;
+        expect += seen;
+    }
+    CHECK(w.lLocalMapPoints.size() == expect, "local points %zu vs %zu", w.lLocalMapPoints.size(), expect);
+    size_t edges = 0;
+    for (auto* mp : w.lLocalMapPoints) edges += mp->GetObservations().size();
+    CHECK(w.edge_point.size() == edges, "edges %zu vs %zu", w.edge_point.size(), edges);
+    // ids: poses = mnId, points = mnId + maxKFid + 1; only fixed cameras (and the init KF) are fixed
+    CHECK(w.maxKFid == 11 || w.maxKFid == 10 || w.maxKFid == 9, "maxKFid %lu", w.maxKFid);
+    for (size_t i = 0; i < w.vpKF.size(); i++)
+        CHECK(w.pose_fixed[i] == (i >= local.size() ? 1 : 0), "pose %zu fixed flag", i);
+    for (size_t i = 0; i < w.vpMP.size(); i++)
+        CHECK(w.point_id[i] == (int64_t)(w.vpMP[i]->mnId + w.maxKFid + 1), "point id");
+    // edges reference the observing keyframe with its keypoint measurement and invSigma2
+    for (size_t e = 0; e < w.edge_point.size(); e++) {
+        MapPoint* mp = w.vpMP[w.edge_point[e]];
+        KeyFrame* kf = w.vpKF[w.edge_pose[e]];
+        const int idx = std::get<0>(mp->GetIndexInKeyFrame(kf));
+        CHECK(idx >= 0 && w.edge_obs[2 * e] == (double)kf->mvKeysUn[idx].pt.x, "edge %zu measurement", e);
+        CHECK(w.edge_inv_sigma2[e] == (double)kf->mvInvLevelSigma2[kf->mvKeysUn[idx].octave], "edge invSigma2");
+    }
+    // a second window for the same keyframe finds no new points (the reference's visit stamps)
+    LocalBAWindow w2;
+    Optimizer::BuildLocalBAWindow(pKF, &S.map, w2);
+    CHECK(w2.lLocalMapPoints.empty(), "visit stamps must suppress re-adding points");
+    // no fixed keyframe -> the reference returns before optimizing
+    Scene S2(5, 40, 5, 3);   // every point seen by every keyframe
+    std::vector<KeyFrame*> all;
+    for (int k = 0; k < 5; k++)
+        if (k != 2) all.push_back(S2.kfs[k].get());
+    KeyFrame* p2 = S2.kfs[2].get();
+    p2->SetVectorCovisibleKeyFrames(all);
+    Map other(99);   // init keyframe id not in the window
+    int nf = -1, no = -1, nm = -7, ne = -1;
+    // same keyframes but a map whose init id is absent: num_fixedKF must be 0
+    LocalBAWindow w3;
+    CHECK(!Optimizer::BuildLocalBAWindow(p2, &other, w3) && w3.num_fixedKF == 0, "no fixed KF");
+    S2.resetMarks();
+    Optimizer::LocalBundleAdjustment(p2, nullptr, &other, nf, no, nm, ne);
+    CHECK(nf == 0 && no == -1 && nm == -7 && ne == -1, "early return leaves outputs: %d %d %d %d", nf, no, nm, ne);
+}
+
+// ---- GPU tests ----------------------------------------------------------------------------------------------
+
+static void testExtractor() {
+    const int w = 640, h = 480;
+    ORBextractor ext(1000, 1.2f, 8, 20, 7);
+    mam_orb_params p{1000, 1.2f, 8, 20, 7, 0};
+    for (uint32_t seed : {1u, 2u}) {
+        auto img = makeImage(w, h, seed);
+        std::vector<KeyPoint> kps;
+        Mat8U desc;
+        std::vector<int> lap = {0, 1000};
+        const int mono = ext(ImageView(img.data(), w, h), ImageView(), kps, desc, lap);
+        std::vector<mam_keypoint> ko(2000);
+        std::vector<uint8_t> dco(2000 * 32);
+        int n = 0, mo = 0;
+        oracle_orb_extract(&p, img.data(), w, h, w, 0, 1000, ko.data(), dco.data(), 2000, &n, &mo);
+        CHECK((int)kps.size() == n && mono == mo, "extract n %zu vs %d", kps.size(), n);
+        CHECK(std::memcmp(kps.data(), ko.data(), sizeof(KeyPoint) * n) == 0, "keypoints differ");
+        CHECK(std::memcmp(desc.data.data(), dco.data(), 32 * (size_t)n) == 0, "descriptors differ");
+        CHECK(desc.rows == n && desc.cols == 32, "descriptor matrix shape");
+    }
+    std::vector<KeyPoint> kps;
+    Mat8U desc;
+    std::vector<int> lap = {0, 1000};
+    CHECK(ext(ImageView(), ImageView(), kps, desc, lap) == -1, "empty image must return -1");
+    auto pyr = ext.GetImagePyramid();
+    CHECK(pyr.size() == 8 && pyr[1].cols == 533 && pyr[1].rows == 400, "pyramid level 1 %dx%d", pyr[1].cols, pyr[1].rows);
+}
+
+static void testMatcher() {
+    const int w = 640, h = 480;
+    Pinhole cam(500.f, 500.f, 320.f, 240.f);
+    ORBextractor ext(1000, 1.2f, 8, 20, 7);
+    auto img = makeImage(w, h, 5);
+    Frame F(ImageView(img.data(), w, h), &ext, &cam, 1);
+    CHECK(F.N > 500, "frame has %d keypoints", F.N);
+    std::mt19937 rng(11);
+    Map map(0);
+    // local MapPoints around the keypoints, some duplicated, some pre-assigned to the frame
+    std::vector<std::unique_ptr<MapPoint>> owned;
+    std::vector<MapPoint*> vp;
+    for (int i = 0; i < F.N; i++) {
+        if (rng() % 5 == 0) continue;
+        for (int dup = 0; dup < (rng() % 7 == 0 ? 2 : 1); dup++) {
+            const float X[3] = {0.f, 0.f, 1.f};
+            owned.emplace_back(new MapPoint(X, nullptr, &map, owned.size()));
+            MapPoint* pMP = owned.back().get();
+            uint8_t d[32];
+            std::memcpy(d, F.mDescriptors.ptr(i), 32);
+            for (int f = 0; f < (int)(rng() % 14); f++) d[rng() % 32] ^= (uint8_t)(1u << (rng() % 8));
+            pMP->SetDescriptor(d);
+            pMP->mbTrackInView = rng() % 20 != 0;
+            pMP->mTrackProjX = F.mvKeysUn[i].pt.x + 0.7f * ((float)(rng() % 100) / 50.f - 1.f);
+            pMP->mTrackProjY = F.mvKeysUn[i].pt.y + 0.7f * ((float)(rng() % 100) / 50.f - 1.f);
+            pMP->mTrackViewCos = 0.99f + 0.01f * (float)(rng() % 100) / 100.f;
+            pMP->mTrackDepth = 1.f + (float)(rng() % 50);
+            pMP->mnTrackScaleLevel = std::min(7, F.mvKeysUn[i].octave + (int)(rng() % 2));
+            vp.push_back(pMP);
+        }
+    }
+    // observations: most points have some (so a match takes the keypoint), some have none
+    KeyFrame dummy(F, &map, 100);
+    for (size_t j = 0; j < vp.size(); j++)
+        if (rng() % 10) vp[j]->AddObservation(&dummy, (int)(j % (size_t)F.N));
+    // a few keypoints already hold a MapPoint with observations (skipped), some hold one without (overwritten)
+    std::vector<MapPoint*> before(F.N, nullptr);
+    for (int i = 0; i < F.N; i += 13) before[i] = vp[(size_t)i % vp.size()];
+    F.mvpMapPoints = before;
+
+    // expected: the oracle on the same marshalled inputs
+    std::vector<mam_mp_track> tr(vp.size());
+    for (size_t j = 0; j < vp.size(); j++) {
+        std::memset(&tr[j], 0, sizeof(tr[j]));
+        tr[j].proj_x = vp[j]->mTrackProjX; tr[j].proj_y = vp[j]->mTrackProjY;
+        tr[j].view_cos = vp[j]->mTrackViewCos; tr[j].track_depth = vp[j]->mTrackDepth;
+        tr[j].track_in_view = vp[j]->mbTrackInView; tr[j].scale_level = vp[j]->mnTrackScaleLevel;
+        tr[j].nobs = vp[j]->Observations();
+        vp[j]->GetDescriptor(tr[j].desc);
+    }
+    std::vector<uint8_t> taken(F.N);
+    for (int i = 0; i < F.N; i++) taken[i] = before[i] && before[i]->Observations() > 0;
+    std::vector<int32_t> oo(F.N);
+    const mam_frame_geom g = F.Geom();
+    const int no = oracle_search_by_projection(&g, F.N, reinterpret_cast<const mam_keypoint*>(F.mvKeysUn.data()),
+                                               F.mDescriptors.data.data(), taken.data(), (int)tr.size(), tr.data(),
+                                               1.f, 0, 50.f, 0.8f, oo.data());
+    ORBmatcher matcher(0.8f, true);
+    const int ng = matcher.SearchByProjection(F, vp, 1.f);
+    CHECK(ng == no && ng > 100, "SearchByProjection nmatches %d vs oracle %d", ng, no);
+    for (int i = 0; i < F.N; i++) {
+        MapPoint* expect = oo[i] >= 0 ? vp[oo[i]] : before[i];
+        CHECK(F.mvpMapPoints[i] == expect, "keypoint %d assignment", i);
+    }
+
+    // motion model: LastFrame = F with its assignments and a pose, current = a second extraction of the
+    // same image with a small pose change (the projections land near the same keypoints)
+    Frame Last = F;
+    Last.SetPose(SE3f());
+    for (int i = 0; i < Last.N; i++) {
+        if (!Last.mvpMapPoints[i]) continue;
+        MapPoint* pMP = Last.mvpMapPoints[i];
+        const float z = 2.f + (float)(i % 7);
+        const float X[3] = {(Last.mvKeysUn[i].pt.x - 320.f) * z / 500.f, (Last.mvKeysUn[i].pt.y - 240.f) * z / 500.f, z};
+        pMP->SetWorldPos(X);
+        Last.mvbOutlier[i] = (i % 17 == 0);
+    }
+    Frame Cur(ImageView(img.data(), w, h), &ext, &cam, 2);
+    SE3f Tc;
+    Tc.t[0] = 0.004f;
+    Cur.SetPose(Tc);
+    for (int i = 0; i < Cur.N; i += 29) Cur.mvpMapPoints[i] = vp[(size_t)(i * 3) % vp.size()];
+    std::vector<MapPoint*> cbefore = Cur.mvpMapPoints;
+    std::vector<mam_last_entry> le(Last.N);
+    for (int i = 0; i < Last.N; i++) {
+        std::memset(&le[i], 0, sizeof(le[i]));
+        MapPoint* pMP = Last.mvpMapPoints[i];
+        if (!pMP || Last.mvbOutlier[i]) continue;
+        le[i].valid = 1;
+        pMP->GetWorldPos(le[i].pos);
+        le[i].angle = Last.mvKeysUn[i].angle;
+        le[i].octave = Last.mvKeys[i].octave;
+        le[i].nobs = pMP->Observations();
+        pMP->GetDescriptor(le[i].desc);
+    }
+    std::vector<uint8_t> ctaken(Cur.N);
+    for (int i = 0; i < Cur.N; i++) ctaken[i] = cbefore[i] && cbefore[i]->Observations() > 0;
+    std::vector<int32_t> mo(Cur.N);
+    const mam_frame_geom cg = Cur.Geom();
+    const mam_pose tcw = Tc.toC();
+    const mam_pinhole pc = cam.toC();
+    const int nmo = oracle_search_by_projection_motion(&cg, Cur.N, reinterpret_cast<const mam_keypoint*>(Cur.mvKeysUn.data()),
+                                                       Cur.mDescriptors.data.data(), ctaken.data(), &tcw, &pc, Last.N,
+                                                       le.data(), 15.f, 1, mo.data());
+    ORBmatcher m2(0.9f, true);
+    const int nmg = m2.SearchByProjection(Cur, Last, 15.f, true);
+    CHECK(nmg == nmo && nmg > 100, "motion nmatches %d vs oracle %d", nmg, nmo);
+    for (int i = 0; i < Cur.N; i++) {
+        MapPoint* expect = mo[i] >= 0 ? Last.mvpMapPoints[mo[i]] : (mo[i] == MAM_MATCH_CLEARED ? nullptr : cbefore[i]);
+        CHECK(Cur.mvpMapPoints[i] == expect, "motion keypoint %d", i);
+    }
+
+    // triangulation between two keyframes of the same image with a baseline; BoW nodes = hash of the descriptor
+    KeyFrame K1(F, &map, 10), K2(Cur, &map, 11);
+    SE3f T2;
+    T2.t[0] = -0.1f;
+    K2.SetPose(T2);
+    for (int i = 0; i < K1.N; i++) K1.mFeatVec[K1.mDescriptors.ptr(i)[0] % 40].push_back(i);
+    for (int i = 0; i < K2.N; i++) K2.mFeatVec[K2.mDescriptors.ptr(i)[0] % 40].push_back(i);
+    for (int i = 0; i < K2.N; i += 9) K2.AddMapPoint(vp[(size_t)i % vp.size()], i);
+    float F12[9], ep[2];
+    ORBmatcher::ComputeF12(&K1, &K2, F12, ep);
+    auto flat = [](KeyFrame& K, std::vector<uint32_t>& ids, std::vector<int32_t>& off, std::vector<uint32_t>& ft) {
+        off.assign(1, 0);
+        for (auto& n : K.mFeatVec) {
+            ids.push_back(n.first);
+            ft.insert(ft.end(), n.second.begin(), n.second.end());
+            off.push_back((int32_t)ft.size());
+        }
+    };
+    std::vector<uint32_t> i1, f1, i2, f2;
+    std::vector<int32_t> o1, o2;
+    flat(K1, i1, o1, f1);
+    flat(K2, i2, o2, f2);
+    mam_featvec fv1{(int32_t)i1.size(), i1.data(), o1.data(), f1.data()}, fv2{(int32_t)i2.size(), i2.data(), o2.data(), f2.data()};
+    std::vector<uint8_t> h1(K1.N), h2(K2.N);
+    for (int i = 0; i < K1.N; i++) h1[i] = K1.GetMapPoint(i) != nullptr;
+    for (int i = 0; i < K2.N; i++) h2[i] = K2.GetMapPoint(i) != nullptr;
+    std::vector<int32_t> to(K1.N);
+    const mam_frame_geom g2 = K2.Geom();
+    const int nto = oracle_search_for_triangulation(&g2, K1.N, reinterpret_cast<const mam_keypoint*>(K1.mvKeysUn.data()),
+                                                    K1.mDescriptors.data.data(), h1.data(), &fv1, K2.N,
+                                                    reinterpret_cast<const mam_keypoint*>(K2.mvKeysUn.data()),
+                                                    K2.mDescriptors.data.data(), h2.data(), &fv2, F12, ep, 0, 0,
+                                                    to.data());
+    ORBmatcher m3(0.6f, false);
+    std::vector<std::pair<size_t, size_t>> pairs;
+    const int ntg = m3.SearchForTriangulation(&K1, &K2, pairs, false, false);
+    CHECK(ntg == nto && ntg > 50, "triangulation %d vs oracle %d", ntg, nto);
+    size_t j = 0;
+    for (int i = 0; i < K1.N; i++)
+        if (to[i] >= 0) {
+            CHECK(j < pairs.size() && pairs[j].first == (size_t)i && pairs[j].second == (size_t)to[i], "pair %zu", j);
+            j++;
+        }
+    CHECK(j == pairs.size(), "pair count");
+    CHECK(ORBmatcher::DescriptorDistance(F.mDescriptors.ptr(0), F.mDescriptors.ptr(0)) == 0, "self distance");
+}
+
+static void testLocalBA() {
+    Scene S(16, 600, 5, 21, 0.08f);
+    KeyFrame* pKF = S.kfs[8].get();
+    std::vector<KeyFrame*> cov;
+    for (int k = 2; k < 14; k++)
+        if (k != 8) cov.push_back(S.kfs[k].get());
+    pKF->SetVectorCovisibleKeyFrames(cov);
+    // expected: oracle solve of the same window
+    LocalBAWindow w;
+    CHECK(Optimizer::BuildLocalBAWindow(pKF, &S.map, w), "window");
+    const mam_lba_problem prob = w.Problem(10);
+    std::vector<double> q(w.pose_q.size()), t(w.pose_t.size()), x(w.point_xyz.size()), chi2(w.edge_point.size());
+    std::vector<uint8_t> depth(w.edge_point.size());
+    mam_lba_result r{q.data(), t.data(), x.data(), chi2.data(), depth.data(), 0, 0, 0, 0, 0};
+    CHECK(oracle_lba_solve(&prob, nullptr, &r) == 0 && r.status == 0, "oracle solve");
+    CHECK(r.final_chi2 < r.initial_chi2, "oracle made progress");
+    std::vector<std::pair<KeyFrame*, MapPoint*>> erase;
+    for (size_t e = 0; e < w.edge_point.size(); e++)
+        if (chi2[e] > 5.991 || !depth[e]) erase.push_back({w.vpKF[w.edge_pose[e]], w.vpMP[w.edge_point[e]]});
+    CHECK(!erase.empty(), "scene must produce outliers");
+
+    S.resetMarks();
+    int nf = 0, no = 0, nm = 0, ne = 0;
+    bool stop = false;
+    Optimizer::LocalBundleAdjustment(pKF, &stop, &S.map, nf, no, nm, ne);
+    CHECK(nf == w.num_fixedKF && no == (int)w.lLocalKeyFrames.size() && ne == (int)w.edge_point.size(),
+          "counters %d %d %d", nf, no, ne);
+    CHECK(S.map.GetMapChangeIndex() == 1, "IncreaseChangeIndex");
+    size_t k = 0;
+    double worst = 0.0;
+    for (KeyFrame* kf : w.lLocalKeyFrames) {
+        const SE3f T = kf->GetPose();
+        for (int j = 0; j < 3; j++) worst = std::max(worst, std::fabs((double)T.t[j] - t[3 * k + j]) / (1e-9 + std::fabs(t[3 * k + j]) + 1.0));
+        for (int j = 0; j < 4; j++) worst = std::max(worst, std::fabs((double)T.q[j] - q[4 * k + j]));
+        k++;
+    }
+    size_t pi = 0;
+    for (MapPoint* mp : w.lLocalMapPoints) {
+        float X[3];
+        mp->GetWorldPos(X);
+        const double n = std::sqrt(x[3 * pi] * x[3 * pi] + x[3 * pi + 1] * x[3 * pi + 1] + x[3 * pi + 2] * x[3 * pi + 2]);
+        for (int j = 0; j < 3; j++) worst = std::max(worst, std::fabs((double)X[j] - x[3 * pi + j]) / std::max(n, 1e-9));
+        pi++;
+    }
+    CHECK(worst <= 1e-4, "write-back vs oracle: worst rel %.3g", worst);
+    for (auto& e : erase) {
+        CHECK(std::get<0>(e.second->GetIndexInKeyFrame(e.first)) == -1, "outlier observation not erased");
+    }
+    // the stop flag set before the solve: no update, like the reference (:1406-1408)
+    Scene S2(8, 100, 4, 5);
+    KeyFrame* p2 = S2.kfs[4].get();
+    p2->SetVectorCovisibleKeyFrames({S2.kfs[3].get(), S2.kfs[5].get()});
+    const SE3f before = p2->GetPose();
+    stop = true;
+    Optimizer::LocalBundleAdjustment(p2, &stop, &S2.map, nf, no, nm, ne);
+    const SE3f after = p2->GetPose();
+    CHECK(std::memcmp(&before, &after, sizeof(SE3f)) == 0 && S2.map.GetMapChangeIndex() == 0, "stop flag");
+}
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "cpu";
+    testAlgebra();
+    testObservations();
+    testWindow();
+    if (mode == "gpu") {
+        testExtractor();
+        testMatcher();
+        testLocalBA();
+    }
+    std::printf("OK %d checks (%s)\n", g_checks, mode.c_str());
+    return 0;
+}

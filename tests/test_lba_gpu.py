@@ -63,7 +63,7 @@ def test_lba_fixed_only_points(solver, oracle):
 
 def test_lba_stop_flag(solver, oracle):
     prob = synthetic_problem(n_opt=8, n_fixed=2, n_points=200, seed=9)
-    stop = np.ones(1, np.int32)
+    stop = np.ones(1, np.uint8)   # bool pbStopFlag
     rg = solver.solve(prob, stop)
     ro = oracle.lba_solve(prob, stop)
     assert rg.iterations == ro.iterations == 0 and rg.status == ro.status == 1
