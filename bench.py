@@ -8,9 +8,11 @@ per frame, batched:
   3. SearchByProjection(F, localMapPoints, th=1), nnratio 0.8 (SearchLocalPoints, Tracking.cc:3146-3156),
      with the keypoints matched in (2) taken
 and for --config c2 additionally one LocalBundleAdjustment (50 KF / 3000 MP, BASELINE configs[2]) per step,
-solved concurrently on its own HIP stream (the LocalMapping thread's work, Optimizer.cc:1116).
-N GPUs = N agents, one process per GPU, each with its own frame stream: independent units, weak scaling,
-no data-path collective.
+solved concurrently on its own HIP stream (the LocalMapping thread's work, Optimizer.cc:1116), followed by the
+shared-map exchange: the LBA write-back packed into fixed-size records, all-gathered over RCCL, applied in agent
+order.
+N GPUs = N agents, one process per GPU, each with its own frame stream: independent units, weak scaling; the only
+collective is that exchange (c2).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c1|c2]
 """
@@ -207,10 +209,22 @@ def main():
     if cfg["lba"]:
         from mam3slam_amd.lba import LBASolver, synthetic_problem
 
+        from mam3slam_amd.exchange import MapUpdateExchange
+
         lba_solver = LBASolver(device=local)
         lba_prob = synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, seed=1 + rank)
+        # shared-map exchange after every LBA: the agents' windows overlap in id space (a merged
+        # map), so replicas see conflicting writes resolved in agent order
+        exch = MapUpdateExchange(capacity=4096, device=dev)
+        d_pose_id = torch.from_numpy(lba_prob.pose_id).to(dev)
+        d_pose_fixed = torch.from_numpy(lba_prob.pose_fixed).to(dev)
+        d_point_id = torch.from_numpy(lba_prob.point_id - (int(lba_prob.pose_id.max()) + 1)).to(dev)
+        kf_cap, mp_cap = 1024, 1 << 16
+        d_kf_table = torch.zeros((kf_cap, 8), dtype=torch.float32, device=dev)
+        d_mp_table = torch.zeros((mp_cap, 4), dtype=torch.float32, device=dev)
+        d_xstatus = torch.zeros(1, dtype=torch.int32, device=dev)
 
-    lba_stats = {"n": 0, "ms": 0.0, "its": 0}
+    lba_stats = {"n": 0, "ms": 0.0, "its": 0, "res": None}
 
     def lba_worker():
         t = time.perf_counter()
@@ -218,6 +232,18 @@ def main():
         lba_stats["ms"] += (time.perf_counter() - t) * 1e3
         lba_stats["n"] += 1
         lba_stats["its"] = r.iterations
+        lba_stats["res"] = r
+
+    def exchange_updates():
+        r = lba_stats["res"]
+        bad = None   # bad flags come from the host-side erase (nObs <= 2); the synthetic window tracks no counts
+        d_q = torch.from_numpy(r.pose_q).to(dev)
+        d_t = torch.from_numpy(r.pose_t).to(dev)
+        d_x = torch.from_numpy(r.point_xyz).to(dev)
+        exch.pack_lba(d_q.data_ptr(), d_t.data_ptr(), d_pose_id.data_ptr(), d_pose_fixed.data_ptr(), len(r.pose_q),
+                      d_x.data_ptr(), d_point_id.data_ptr(), bad, len(r.point_xyz), stream=stream)
+        exch.gather()
+        exch.apply(d_kf_table.data_ptr(), kf_cap, d_mp_table.data_ptr(), mp_cap, d_xstatus.data_ptr(), stream=stream)
 
     def step():
         th = None
@@ -228,6 +254,7 @@ def main():
         match()
         if th is not None:
             th.join()
+            exchange_updates()
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,63 @@
+/*
+ * mam_exchange.h — shared-map update exchange between agents (one agent per GPU), SURVEY.md §8(e).
+ *
+ * In the reference every agent's LocalMapping thread writes KeyFrame poses and MapPoint positions of a merged
+ * Atlas map under Map::mMutexMapUpdate (src/Optimizer.cc:1463-1497: KeyFrame::SetPose, MapPoint::SetWorldPos,
+ * erase of outlier observations -> MapPoint::SetBadFlag), and the other agents read them through shared
+ * pointers. With one process per GPU there is no shared memory: after each LocalBundleAdjustment an agent packs
+ * its write-back as fixed-size records, the records of all agents are all-gathered over RCCL (xGMI), and every
+ * agent applies them to its device-resident copy of the shared tables in agent-id order. The reference's
+ * interleaving is racy (last writer under the mutex wins); here the order is fixed (agent 0 first, highest
+ * agent last), so every replica ends with identical bytes.
+ *
+ * Buffer layout for one agent (one all-gather block): record 0 is a header (kind MAM_UPDATE_HEADER, id = number
+ * of records that follow, agent = producer), records 1..capacity the updates. The gathered buffer is
+ * n_agents such blocks back to back (torch.distributed.all_gather_into_tensor order = rank order).
+ */
+#ifndef MAM_EXCHANGE_H
+#define MAM_EXCHANGE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { MAM_UPDATE_HEADER = 0, MAM_UPDATE_KF = 1, MAM_UPDATE_MP = 2 };
+
+/* 64 bytes. KF: v = Tcw unit quaternion x, y, z, w then translation (what KeyFrame::SetPose receives,
+ * Optimizer.cc:1478-1486). MP: v[0..2] = world position (MapPoint::SetWorldPos, :1489-1494), bad = the point
+ * was marked bad by the outlier erase. */
+typedef struct mam_map_update {
+    int64_t id;
+    int32_t kind;
+    int32_t agent;
+    float v[7];
+    int32_t bad;
+    float reserved[4];
+} mam_map_update;
+
+/* Pack one LocalBundleAdjustment write-back (DEVICE pointers, asynchronous on `stream`):
+ *   poses: n_poses entries, pose_q [n][4] / pose_t [n][3] f64 (mam_lba_result order), pose_id, pose_fixed — only
+ *          non-fixed poses are written back by the reference, so only those are packed;
+ *   points: n_points entries, point_xyz [n][3] f64, point_id, point_bad (may be NULL).
+ * Values are converted exactly like the write-back: quaternion and translation cast to float and the quaternion
+ * renormalised in float (Sophus::SE3f constructor), positions cast to float.
+ * out: capacity+1 records (header + updates). Returns MAM_ERR_CAPACITY if the update does not fit. */
+int mam_exchange_pack_lba(const double* pose_q, const double* pose_t, const int64_t* pose_id,
+                          const uint8_t* pose_fixed, int n_poses, const double* point_xyz, const int64_t* point_id,
+                          const uint8_t* point_bad, int n_points, int agent, mam_map_update* out, int capacity,
+                          void* stream);
+
+/* Apply gathered blocks (n_agents x (capacity+1) records, DEVICE) to device tables, agent 0 first:
+ *   kf_table [kf_cap][8] floats (q xyzw, t, 1.0 = written), mp_table [mp_cap][4] floats (xyz, bad flag).
+ * Records with an id outside the table or a malformed header set *status (device int32) to MAM_ERR_ARG and are
+ * skipped. Asynchronous on `stream`. */
+int mam_exchange_apply(const mam_map_update* gathered, int n_agents, int capacity, float* kf_table, int64_t kf_cap,
+                       float* mp_table, int64_t mp_cap, int32_t* status, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAM_EXCHANGE_H */

@@ -54,10 +54,11 @@ SIGNATURES = {
 
 
 def _match_sigs():
+    from .exchange import _SIGS as ex_sigs
     from .lba import _SIGS as lba_sigs
     from .match import _SIGS
 
-    return {**_SIGS, **lba_sigs}
+    return {**_SIGS, **lba_sigs, **ex_sigs}
 
 
 def lib() -> C.CDLL:

@@ -1,0 +1,95 @@
+"""Shared-map update exchange between agents, one agent per GPU (include/mam_exchange.h).
+
+After each LocalBundleAdjustment an agent packs its write-back (optimised KeyFrame poses, MapPoint positions, bad
+flags — what src/Optimizer.cc:1463-1497 writes into the shared Atlas under mMutexMapUpdate) into one fixed-size
+block of 64-byte records on the GPU (`pack_lba`), the blocks of all agents are all-gathered
+(`torch.distributed.all_gather_into_tensor`: RCCL over xGMI on MI355X, gloo on CPU), and every agent applies the
+gathered blocks to its device-resident shared tables in agent-id order (`apply`), so all replicas hold identical
+bytes. One collective per LBA, fixed size: no all-gatherv, no count exchange.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import check, lib
+
+UPDATE_HEADER, UPDATE_KF, UPDATE_MP = 0, 1, 2
+UPDATE_DTYPE = np.dtype([("id", "<i8"), ("kind", "<i4"), ("agent", "<i4"), ("v", "<f4", (7,)), ("bad", "<i4"),
+                         ("reserved", "<f4", (4,))])
+assert UPDATE_DTYPE.itemsize == 64
+RECORD_BYTES = 64
+
+_SIGS = {
+    "mam_exchange_pack_lba": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p]),
+    "mam_exchange_apply": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                                     C.c_void_p, C.c_void_p]),
+}
+
+
+def _bind():
+    L = lib()
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    return L
+
+
+class MapUpdateExchange:
+    """Fixed-capacity all-gather of update blocks. `device` is where the send/receive buffers live (a CUDA device
+    for the product path; "cpu" with the gloo backend for host-side tests of the collective)."""
+
+    def __init__(self, capacity: int = 4096, device="cuda", group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.capacity = int(capacity)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        nbytes = (self.capacity + 1) * RECORD_BYTES
+        self.send = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        self.recv = torch.zeros(self.world * nbytes, dtype=torch.uint8, device=device)
+        self._L = None
+
+    @property
+    def block_bytes(self) -> int:
+        return (self.capacity + 1) * RECORD_BYTES
+
+    def gather(self):
+        """All-gather every agent's block into `recv` (rank order). Returns `recv`."""
+        import torch.distributed as dist
+
+        if self.world == 1:
+            self.recv.copy_(self.send)
+        elif dist.get_backend(self.group) == "gloo":
+            dist.all_gather(list(self.recv.view(self.world, -1).unbind(0)), self.send, group=self.group)
+        else:
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        return self.recv
+
+    # ---- device kernels (product path)
+    def _lib(self):
+        if self._L is None:
+            self._L = _bind()
+        return self._L
+
+    def pack_lba(self, d_pose_q: int, d_pose_t: int, d_pose_id: int, d_pose_fixed: int, n_poses: int,
+                 d_point_xyz: int, d_point_id: int, d_point_bad: int | None, n_points: int, stream: int = 0,
+                 agent: int | None = None):
+        """Pack one LBA write-back (device pointers) into the send block on `stream`."""
+        a = self.rank if agent is None else int(agent)
+        check(self._lib().mam_exchange_pack_lba(
+            C.c_void_p(d_pose_q), C.c_void_p(d_pose_t), C.c_void_p(d_pose_id), C.c_void_p(d_pose_fixed), n_poses,
+            C.c_void_p(d_point_xyz), C.c_void_p(d_point_id), C.c_void_p(d_point_bad or 0), n_points, a,
+            C.c_void_p(self.send.data_ptr()), self.capacity, C.c_void_p(stream)), "mam_exchange_pack_lba")
+
+    def apply(self, d_kf_table: int, kf_cap: int, d_mp_table: int, mp_cap: int, d_status: int, stream: int = 0,
+              gathered: int | None = None, n_agents: int | None = None):
+        """Apply the gathered blocks (default: `recv`) to the device tables, agent 0 first."""
+        check(self._lib().mam_exchange_apply(
+            C.c_void_p(gathered or self.recv.data_ptr()), n_agents or self.world, self.capacity,
+            C.c_void_p(d_kf_table), int(kf_cap), C.c_void_p(d_mp_table), int(mp_cap), C.c_void_p(d_status),
+            C.c_void_p(stream)), "mam_exchange_apply")

@@ -4,9 +4,10 @@ Reference: static void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbS
            int& num_fixedKF, int& num_OptKF, int& num_MPs, int& num_edges)   (src/Optimizer.cc:1116-1498)
 
 `LBAProblem` is the g2o graph the reference builds (vertices, mono edges, Huber delta, 10 iterations);
-`solve()` runs the Levenberg-Marquardt / Schur solve on the GPU; `local_bundle_adjustment()` (below) is the
-full call: window construction from a `MapModel` (Optimizer.cc:1118-1186), solve, outlier erase
-(chi2 > 5.991 or depth <= 0, :1413-1460) and write-back as float (:1463-1497).
+`solve()` runs the Levenberg-Marquardt / Schur solve on the GPU (`stop_flag`: a one-byte array, the reference's
+`bool* pbStopFlag`). The full call with the reference signature — window construction (Optimizer.cc:1118-1186),
+solve, outlier erase (chi2 > 5.991 or depth <= 0, :1413-1460) and write-back as float (:1463-1497) — is the C++
+host API `MAM3SLAM::Optimizer::LocalBundleAdjustment` (include/mam3slam/Optimizer.h).
 """
 from __future__ import annotations
 

@@ -1,0 +1,136 @@
+"""Shared-map update exchange (include/mam_exchange.h).
+
+CPU: the collective itself — MapUpdateExchange.gather() at world_size 2 over gloo — with blocks packed and applied
+by the numpy restatement (oracle/exchange_oracle.py): both ranks receive identical bytes in rank order and end with
+identical tables where the higher agent wins a conflict. GPU: the pack / apply kernels byte-exact vs the
+restatement, including conflicts, bad flags, out-of-range ids and capacity overflow.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from mam3slam_amd.exchange import MapUpdateExchange
+from oracle import exchange_oracle as xo
+
+
+def _agent_update(agent, n_poses=12, n_points=300, shared=200, seed=0):
+    """An agent's LBA write-back: poses ids 10*agent.., points drawn from a shared id pool (merged map)."""
+    rng = np.random.default_rng(seed + 17 * agent)
+    q = rng.normal(size=(n_poses, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    t = rng.normal(size=(n_poses, 3))
+    pid = np.arange(n_poses, dtype=np.int64) + 5 * agent          # overlapping keyframe ids
+    fixed = (rng.random(n_poses) < 0.3).astype(np.uint8)
+    mid = np.sort(rng.choice(shared + n_points, size=n_points, replace=False)).astype(np.int64)
+    xyz = rng.normal(size=(n_points, 3)) * 3
+    bad = (rng.random(n_points) < 0.05).astype(np.uint8)
+    return q, t, pid, fixed, xyz, mid, bad
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, cap, outdir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ex = MapUpdateExchange(capacity=cap, device="cpu")
+    q, t, pid, fixed, xyz, mid, bad = _agent_update(rank)
+    blk = xo.pack_lba(q, t, pid, fixed, xyz, mid, bad, rank, cap)
+    ex.send.numpy()[:] = blk.view(np.uint8)
+    got = ex.gather().numpy().copy()
+    kf = np.zeros((64, 8), np.float32)
+    mp = np.zeros((1024, 4), np.float32)
+    st = xo.apply(got.view(xo.UPDATE_DTYPE), world, cap, kf, mp)
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), got=got, kf=kf, mp=mp, st=st)
+    dist.destroy_process_group()
+
+
+def test_gather_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+
+    cap, world = 512, 2
+    mp.start_processes(_rank_main, args=(world, _free_port(), cap, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r0, r1 = (np.load(tmp_path / f"r{r}.npz") for r in range(world))
+    assert np.array_equal(r0["got"], r1["got"])
+    assert np.array_equal(r0["kf"], r1["kf"]) and np.array_equal(r0["mp"], r1["mp"])
+    assert int(r0["st"]) == 0
+    blocks = r0["got"].view(xo.UPDATE_DTYPE).reshape(world, cap + 1)
+    for a in range(world):
+        exp = xo.pack_lba(*_agent_update(a), a, cap)
+        assert np.array_equal(blocks[a].view(np.uint8), exp.view(np.uint8)), f"block {a} not in rank order"
+    # conflicts: ids written by both agents hold agent 1's values (applied last)
+    q1, t1, pid1, fx1, xyz1, mid1, bad1 = _agent_update(1)
+    for i, m in enumerate(mid1):
+        assert np.array_equal(r0["mp"][m, :3], xyz1[i].astype(np.float32))
+    b1 = xo.pack_lba(q1, t1, pid1, fx1, xyz1, mid1, bad1, 1, cap)
+    for u in b1[1:1 + int(b1[0]["id"])]:
+        if u["kind"] == xo.UPDATE_KF:
+            assert np.array_equal(r0["kf"][u["id"], :7], u["v"]) and r0["kf"][u["id"], 7] == 1.0
+
+
+def test_pack_capacity_and_header():
+    q, t, pid, fixed, xyz, mid, bad = _agent_update(0)
+    n_opt = int((fixed == 0).sum())
+    blk = xo.pack_lba(q, t, pid, fixed, xyz, mid, bad, 3, n_opt + len(mid))
+    assert blk[0]["id"] == n_opt + len(mid) and blk[0]["agent"] == 3
+    assert (blk["kind"][1:1 + n_opt] == xo.UPDATE_KF).all() and (blk["kind"][1 + n_opt:] == xo.UPDATE_MP).all()
+    small = xo.pack_lba(q, t, pid, fixed, xyz, mid, bad, 3, n_opt + len(mid) - 1)
+    assert small[0]["id"] == xo.ERR_CAPACITY
+    kf, mpt = np.zeros((64, 8), np.float32), np.zeros((1024, 4), np.float32)
+    assert xo.apply(small, 1, n_opt + len(mid) - 1, kf, mpt) == xo.ERR_ARG and not kf.any()
+
+
+@pytest.mark.gpu
+def test_pack_apply_kernels(gpu_lib):
+    import torch
+
+    dev = torch.device("cuda")
+    cap, agents = 600, 3
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    ex = MapUpdateExchange(capacity=cap, device=dev)
+    blocks = []
+    for a in range(agents):
+        q, t, pid, fixed, xyz, mid, bad = _agent_update(a, seed=5)
+        T = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (q, t, pid, fixed, xyz, mid, bad)]
+        ex.send.fill_(0xAB)
+        torch.cuda.synchronize()
+        ex.pack_lba(T[0].data_ptr(), T[1].data_ptr(), T[2].data_ptr(), T[3].data_ptr(), len(pid), T[4].data_ptr(),
+                    T[5].data_ptr(), T[6].data_ptr(), len(mid), stream=st.cuda_stream, agent=a)
+        torch.cuda.synchronize()
+        got = ex.send.cpu().numpy().view(xo.UPDATE_DTYPE)
+        exp = xo.pack_lba(q, t, pid, fixed, xyz, mid, bad, a, cap)
+        n = int(exp[0]["id"])
+        assert np.array_equal(got[:1 + n].view(np.uint8), exp[:1 + n].view(np.uint8)), f"agent {a} pack"
+        blocks.append(exp)
+    # an out-of-range id in agent 2's block -> status ERR_ARG, the record skipped
+    blocks[2][5]["id"] = 10 ** 6
+    gathered = np.concatenate(blocks)
+    d_g = torch.from_numpy(gathered.view(np.uint8).copy()).to(dev)
+    kf = torch.zeros((64, 8), dtype=torch.float32, device=dev)
+    mpt = torch.zeros((1024, 4), dtype=torch.float32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ex.apply(kf.data_ptr(), 64, mpt.data_ptr(), 1024, status.data_ptr(), stream=st.cuda_stream,
+             gathered=d_g.data_ptr(), n_agents=agents)
+    torch.cuda.synchronize()
+    kf_o, mp_o = np.zeros((64, 8), np.float32), np.zeros((1024, 4), np.float32)
+    st_o = xo.apply(gathered, agents, cap, kf_o, mp_o)
+    assert int(status.item()) == st_o == xo.ERR_ARG
+    assert np.array_equal(kf.cpu().numpy(), kf_o) and np.array_equal(mpt.cpu().numpy(), mp_o)
+    # capacity overflow is reported in the header
+    q, t, pid, fixed, xyz, mid, bad = _agent_update(0, n_points=cap)
+    T = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (q, t, pid, fixed, xyz, mid, bad)]
+    ex.pack_lba(T[0].data_ptr(), T[1].data_ptr(), T[2].data_ptr(), T[3].data_ptr(), len(pid), T[4].data_ptr(),
+                T[5].data_ptr(), T[6].data_ptr(), len(mid), stream=st.cuda_stream, agent=0)
+    torch.cuda.synchronize()
+    assert int(ex.send.cpu().numpy().view(xo.UPDATE_DTYPE)[0]["id"]) == xo.ERR_CAPACITY
