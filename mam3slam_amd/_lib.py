@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmam_gpu.so")
+# MAM3SLAM_GPU_LIB: load an alternative build (kernel-variant experiments); default the in-tree product
+LIB_PATH = os.environ.get("MAM3SLAM_GPU_LIB") or os.path.join(HERE, "libmam_gpu.so")
 
 
 class MamError(RuntimeError):

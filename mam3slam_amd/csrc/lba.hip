@@ -19,7 +19,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <type_traits>
 #include <limits>
 #include <numeric>
 #include <string>
@@ -42,7 +46,7 @@ struct Dev {
     const int32_t* pose_cam;
     const int32_t* pose_h;       // Hessian pose block of pose (-1 fixed)
     const int32_t* hpose;        // Hessian pose block -> pose
-    const int32_t* point_h;      // unused on device (points are indexed by Hessian order directly)
+    const int32_t* point_h;      // Hessian point of point
     const int32_t* hpoint;       // Hessian point -> point
     const int32_t* pe_off;       // per Hessian point: edge segment [pe_off[h], pe_off[h+1]) into pe_idx
     const int32_t* pe_idx;
@@ -53,6 +57,8 @@ struct Dev {
     const int32_t* bp_ec;
     const int32_t* bp_ij;        // (i1, i2) per block pair
     int nbp;
+    int npad;                    // padded dimension of S (ldlt_pad(6 Np))
+    double* ws;                  // global LDL^T workspace when it does not fit in LDS
     double delta;
     // state
     const double* pose;          // [P][7] q(xyzw) t
@@ -145,11 +151,18 @@ __global__ __launch_bounds__(256) void k_linearize(Dev d, int want_jac) {
     o[18] = -(w * e0) * r1;
     o[19] = -(w * e1) * r1;
     o[20] = r1 * w;
+    // H_pl = B^T (rho' Omega) A for edges whose pose is optimised (base_binary_edge.hpp:54-120)
+    if (d.pose_h[ipose] >= 0) {
+        const double wo = r1 * w;
+        double* hp = d.hpl + 18 * (size_t)e;
+        for (int a = 0; a < 6; a++)
+            for (int c = 0; c < 3; c++) hp[3 * a + c] = o[6 + a] * wo * o[c] + o[12 + a] * wo * o[3 + c];
+    }
 }
 
-// ---- per point: H_ll, b_l, per-edge H_pl
-__global__ __launch_bounds__(256) void k_point_sys(Dev d) {
-    const int h = blockIdx.x * 256 + threadIdx.x;
+// ---- per point: H_ll, b_l (edge order, as constructQuadraticForm runs edge by edge)
+__global__ __launch_bounds__(64) void k_point_sys(Dev d) {
+    const int h = blockIdx.x * 64 + threadIdx.x;
     if (h >= d.L) return;
     double H[9] = {0}, bl[3] = {0};
     for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
@@ -159,11 +172,6 @@ __global__ __launch_bounds__(256) void k_point_sys(Dev d) {
         for (int a = 0; a < 3; a++) {
             bl[a] += j[a] * j[18] + j[3 + a] * j[19];
             for (int c = 0; c < 3; c++) H[3 * a + c] += j[a] * wo * j[c] + j[3 + a] * wo * j[3 + c];
-        }
-        if (d.pose_h[d.edge_pose[e]] >= 0) {
-            double* hp = d.hpl + 18 * (size_t)e;
-            for (int a = 0; a < 6; a++)
-                for (int c = 0; c < 3; c++) hp[3 * a + c] = j[6 + a] * wo * j[c] + j[12 + a] * wo * j[3 + c];
         }
     }
     for (int k = 0; k < 9; k++) d.Hll[9 * (size_t)h + k] = H[k];
@@ -240,8 +248,8 @@ __global__ __launch_bounds__(1024) void k_max_diag(Dev d) {
 }
 
 // ---- Schur
-__global__ __launch_bounds__(256) void k_schur_prep(Dev d, double lambda) {
-    const int h = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(64) void k_schur_prep(Dev d, double lambda) {
+    const int h = blockIdx.x * 64 + threadIdx.x;
     if (h >= d.L) return;
     double D[9];
     for (int k = 0; k < 9; k++) D[k] = d.Hll[9 * (size_t)h + k] + ((k % 4 == 0) ? lambda : 0.0);
@@ -254,19 +262,23 @@ __global__ __launch_bounds__(256) void k_schur_prep(Dev d, double lambda) {
     Di[2] = (D[1] * D[5] - D[2] * D[4]) / det; Di[5] = (D[2] * D[3] - D[0] * D[5]) / det;
     Di[8] = (D[0] * D[4] - D[1] * D[3]) / det;
     for (int k = 0; k < 9; k++) d.Dinv[9 * (size_t)h + k] = Di[k];
+}
+
+// per edge (optimised pose): H_pl D^-1 and the coefficient H_pl D^-1 b_l (block_solver.hpp:405-427)
+__global__ __launch_bounds__(256) void k_schur_edge(Dev d) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= d.E || d.pose_h[d.edge_pose[e]] < 0) return;
+    const int h = d.point_h[d.edge_point[e]];
+    const double* Di = d.Dinv + 9 * (size_t)h;
     const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)h;
     double db[3];
     for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
-    for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
-        const int e = d.pe_idx[s];
-        if (d.pose_h[d.edge_pose[e]] < 0) continue;
-        const double* B = d.hpl + 18 * (size_t)e;
-        double* o = d.bdinv + 18 * (size_t)e;
-        double* cf = d.coef + 6 * (size_t)e;
-        for (int i = 0; i < 6; i++) {
-            for (int j = 0; j < 3; j++) o[3 * i + j] = B[3 * i] * Di[j] + B[3 * i + 1] * Di[3 + j] + B[3 * i + 2] * Di[6 + j];
-            cf[i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
-        }
+    const double* B = d.hpl + 18 * (size_t)e;
+    double* o = d.bdinv + 18 * (size_t)e;
+    double* cf = d.coef + 6 * (size_t)e;
+    for (int i = 0; i < 6; i++) {
+        for (int j = 0; j < 3; j++) o[3 * i + j] = B[3 * i] * Di[j] + B[3 * i + 1] * Di[3 + j] + B[3 * i + 2] * Di[6 + j];
+        cf[i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
     }
 }
 
@@ -296,189 +308,250 @@ __global__ __launch_bounds__(64) void k_schur_blk(Dev d, double lambda) {
         for (int k = 0; k < 36; k++) v = (k == lane) ? acc[k] : v;
         double out = -v;
         if (i1 == i2) out = (d.Hpp[36 * (size_t)i1 + lane] + (r == c ? lambda : 0.0)) - v;
-        const int n = 6 * d.Np;
-        d.S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = out;
-        d.S[(size_t)(6 * i2 + c) * n + 6 * i1 + r] = out;
+        const int N = d.npad;
+        d.S[(size_t)(6 * i1 + r) * N + 6 * i2 + c] = out;
+        d.S[(size_t)(6 * i2 + c) * N + 6 * i1 + r] = out;
     }
 }
 
+// b_s = b_p - sum of the pose's coefficients: lanes stride the pose's edges, fixed-order wave reduction
 __global__ __launch_bounds__(64) void k_schur_rhs(Dev d) {
     const int h = blockIdx.x, lane = threadIdx.x;
-    if (lane >= 6) return;
-    double acc = d.b[6 * (size_t)h + lane];
-    for (int s = d.qe_off[h]; s < d.qe_off[h + 1]; s++) acc -= d.coef[6 * (size_t)d.qe_idx[s] + lane];
-    d.bs[6 * (size_t)h + lane] = acc;
+    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int s = d.qe_off[h] + lane; s < d.qe_off[h + 1]; s += 64) {
+        const double* c = d.coef + 6 * (size_t)d.qe_idx[s];
+#pragma unroll
+        for (int k = 0; k < 6; k++) acc[k] += c[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) acc[k] = wave_sum_d(acc[k]);
+    if (lane < 6) {
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) v = (k == lane) ? acc[k] : v;
+        d.bs[6 * (size_t)h + lane] = d.b[6 * (size_t)h + lane] - v;
+    }
 }
 
-// ---- dense LDL^T solve of S x = bs, one workgroup, blocked right-looking with NB = 16 column panels.
-// S holds the full symmetric matrix. Per panel: (1) wave 0 factors the 16x16 diagonal block in registers
-// (lane i owns row i, columns broadcast by shuffles); (2) every thread forward-solves panel rows
-// L21 = A21 L11^-T D^-1 and keeps W = L21 D in the (dead) upper triangle; (3) the trailing lower triangle
-// is updated A22 -= L21 W^T in 4x4 register tiles. flag[0] = 1 on an exact zero pivot (the failure rule of
-// Eigen's SimplicialLDLT). Then blocked forward / diagonal / backward substitution.
+// ---- dense LDL^T solve of S x = bs: one workgroup of 1024 threads, blocked right-looking, NB = 16 panels.
+// S is npad x npad (npad = 6 Np rounded up to 16; the padding is an identity block after the real unknowns, so it
+// changes nothing and every panel is full). Per panel:
+//   (1) wave 0 factors the 16x16 diagonal block in registers: lane i owns row i, the pivot row is read with
+//       v_readlane (uniform), and solves the block of the forward substitution L11 y1 = y1;
+//   (2) every thread takes one panel row: L21 = A21 L11^-T D^-1, W21 = L21 D (staged transposed in the panel
+//       workspace for the trailing update) and the fused forward-substitution update y2 -= L21 y1;
+//   (3) the trailing lower triangle A22 -= L21 W21^T in 4x4 register tiles, both operands from the workspace.
+// An exact zero pivot sets flag[0] (the failure rule of Eigen's SimplicialLDLT) and skips the solve.
+// Then y /= D and the backward substitution L^T x = y, block by block, each thread updating its own y_i.
+// The workspace (panel + y) is LDS when it fits (use_lds), else a global scratch buffer.
 constexpr int NB = 16;
+#ifndef MAM_LDLT_THREADS
+#define MAM_LDLT_THREADS 512
+#endif
+constexpr int LDLT_THREADS = MAM_LDLT_THREADS;   // 512: 2 waves per SIMD, 256 registers per lane
 
-__global__ __launch_bounds__(1024) void k_ldlt(Dev d) {
-    const int n = 6 * d.Np;
+__host__ __device__ inline int ldlt_pad(int n) { return (n + NB - 1) / NB * NB; }
+
+// workspace doubles: PL and PW (NB x (npad - NB) each) + y (npad)
+__host__ __device__ inline size_t ldlt_ws_doubles(int npad) {
+    const int m = npad > NB ? npad - NB : 0;
+    return (size_t)2 * NB * (size_t)m + (size_t)npad;
+}
+__host__ __device__ inline size_t ldlt_lds_bytes(int npad) { return ldlt_ws_doubles(npad) * sizeof(double); }
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), l);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+template <bool use_lds>
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
+    extern __shared__ __attribute__((aligned(16))) double lds_ws[];
+    const int n = 6 * d.Np, N = d.npad;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     double* A = d.S;
+    double* ws = use_lds ? lds_ws : d.ws;
+    double* Y = ws + (size_t)2 * NB * (N - NB);
     __shared__ double Ld[NB * NB];
     __shared__ double dk[NB];
+    __shared__ double invdk[NB];
+    __shared__ double colb[64];
     __shared__ int fail;
     if (t == 0) fail = 0;
-    for (int kb = 0; kb < n; kb += NB) {
-        const int nb = min(NB, n - kb);
-        // (1) diagonal block
+    for (int i = t; i < N; i += LDLT_THREADS) {
+        Y[i] = d.bs[i];
+        if (i >= n) A[(size_t)i * N + i] = 1.0;
+    }
+    __syncthreads();
+#ifdef MAM_LDLT_PROFILE
+    long long tp0 = clock64(), tacc[4] = {0, 0, 0, 0};
+#define LDLT_PHASE(k) do { const long long tn = clock64(); tacc[k] += tn - tp0; tp0 = tn; } while (0)
+#else
+#define LDLT_PHASE(k) do {} while (0)
+#endif
+    for (int kb = 0; kb < N; kb += NB) {
+        // (1) diagonal block + forward block solve (wave 0). Right-looking inside the block: at step j the pivot
+        // d_j is lane j's current diagonal, column j is scaled (l_ij = a_ij / d_j) and broadcast through LDS, and
+        // every lane i > j updates its row: a_ik -= l_ij d_j l_kj for j < k <= i.
         if (wid == 0) {
             double row[NB];
 #pragma unroll
-            for (int c = 0; c < NB; c++) row[c] = (lane < nb && c < nb) ? A[(size_t)(kb + lane) * n + kb + c] : 0.0;
-            double dloc[NB];
+            for (int c = 0; c < NB; c++) row[c] = lane < NB ? A[(size_t)(kb + lane) * N + kb + c] : 0.0;
+            double dmine = 1.0;
 #pragma unroll
             for (int j = 0; j < NB; j++) {
-                if (j < nb) {
-                    // d_j = a_jj - sum_k L_jk^2 d_k  (lane j holds row j)
-                    double s = row[j];
+                const double dj = readlane_d(row[j], j);
+                if (lane == j) dmine = dj;
+                const double inv = dj != 0.0 ? 1.0 / dj : 0.0;
+                const double l = row[j] * inv;
+                if (lane > j) row[j] = l;
+                colb[lane] = l;   // lanes <= j write values nobody reads
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const double ldj = l * dj;
 #pragma unroll
-                    for (int k = 0; k < NB; k++)
-                        if (k < j) s -= row[k] * row[k] * dloc[k];
-                    const double dj = __shfl(s, j, 64);
-                    dloc[j] = dj;
-                    // L_ij = (a_ij - sum_k L_ik L_jk d_k) / d_j for i > j
-                    double lj[NB];
-#pragma unroll
-                    for (int k = 0; k < NB; k++) lj[k] = __shfl(row[k], j, 64);
-                    if (lane > j && lane < nb) {
-                        double v = row[j];
-#pragma unroll
-                        for (int k = 0; k < NB; k++)
-                            if (k < j) v -= row[k] * lj[k] * dloc[k];
-                        row[j] = dj != 0.0 ? v / dj : 0.0;
-                    }
-                } else {
-                    dloc[j] = 1.0;
-                }
+                for (int k = j + 1; k < NB; k++)
+                    if (k <= lane) row[k] -= ldj * colb[k];
+                __builtin_amdgcn_wave_barrier();
             }
-            if (lane < nb) {
+            // forward block solve (unit lower) on y1
+            double yv = lane < NB ? Y[kb + lane] : 0.0;
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const double yj = readlane_d(yv, j);
+                if (lane > j) yv -= row[j] * yj;
+            }
+            if (lane < NB) {
 #pragma unroll
                 for (int c = 0; c < NB; c++) Ld[lane * NB + c] = row[c];
-                dk[lane] = dloc[lane < NB ? lane : 0];
-                if (dloc[lane] == 0.0) fail = 1;
+                dk[lane] = dmine;
+                invdk[lane] = dmine != 0.0 ? 1.0 / dmine : 0.0;
+                Y[kb + lane] = yv;
+                if (dmine == 0.0) fail = 1;
             }
         }
         __syncthreads();
-        for (int i = t; i < nb * nb; i += 1024) {
-            const int r = i / nb, c = i % nb;
-            if (r > c) A[(size_t)(kb + r) * n + kb + c] = Ld[r * NB + c];
-            else if (r == c) A[(size_t)(kb + r) * n + kb + c] = dk[r];
+        LDLT_PHASE(0);
+        for (int i = t; i < NB * NB; i += LDLT_THREADS) {
+            const int r = i / NB, c = i % NB;
+            if (r > c) A[(size_t)(kb + r) * N + kb + c] = Ld[r * NB + c];
+            else if (r == c) A[(size_t)(kb + r) * N + kb + c] = dk[r];
         }
-        // (2) panel rows
-        for (int i = kb + nb + t; i < n; i += 1024) {
+        // (2) panel rows (+ forward-substitution update)
+        const int m = N - kb - NB;
+        double* PL = ws;
+        double* PW = ws + (size_t)NB * m;
+        for (int i = kb + NB + t; i < N; i += LDLT_THREADS) {
+            // keep the L11 factors in LDS (reading them per row): hoisting all 120 into registers spills
+            asm volatile("" ::: "memory");
             double w[NB];
 #pragma unroll
-            for (int j = 0; j < NB; j++) {
-                if (j < nb) {
-                    double s = A[(size_t)i * n + kb + j];
+            for (int j = 0; j < NB; j++) w[j] = A[(size_t)i * N + kb + j];
 #pragma unroll
-                    for (int k = 0; k < NB; k++)
-                        if (k < j) s -= w[k] * Ld[j * NB + k];
-                    w[j] = s;
-                }
+            for (int j = 1; j < NB; j++) {
+#pragma unroll
+                for (int k = 0; k < j; k++) w[j] -= w[k] * Ld[j * NB + k];
             }
+            double yi = Y[i];
 #pragma unroll
             for (int j = 0; j < NB; j++) {
-                if (j < nb) {
-                    A[(size_t)i * n + kb + j] = dk[j] != 0.0 ? w[j] / dk[j] : 0.0;   // L21
-                    A[(size_t)(kb + j) * n + i] = w[j];                               // W^T (upper, dead)
-                }
+                const double lij = w[j] * invdk[j];
+                A[(size_t)i * N + kb + j] = lij;
+                PL[(size_t)j * m + (i - kb - NB)] = lij;
+                PW[(size_t)j * m + (i - kb - NB)] = w[j];
+                yi -= lij * Y[kb + j];
             }
+            Y[i] = yi;
         }
         __syncthreads();
-        // (3) trailing update, 4x4 register tiles over the lower triangle of the m x m trailing block
-        const int m = n - kb - nb;
-        const int T = (m + 3) / 4;
+        LDLT_PHASE(1);
+        // (3) trailing update over the lower triangle of the m x m trailing block
+        const int T = m / 4;
         const int ntile = T * (T + 1) / 2;
-        for (int q = t; q < ntile; q += 1024) {
-            int tr = (int)((sqrt(8.0 * (double)q + 1.0) - 1.0) * 0.5);
+        for (int q = t; q < ntile; q += LDLT_THREADS) {
+            int tr = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
             while (tr * (tr + 1) / 2 > q) tr--;
             while ((tr + 1) * (tr + 2) / 2 <= q) tr++;
             const int tc = q - tr * (tr + 1) / 2;
-            const int r0 = kb + nb + 4 * tr, c0 = kb + nb + 4 * tc;
+            const int r0 = kb + NB + 4 * tr, c0 = kb + NB + 4 * tc;
+            double a4[4][4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                const double2* ap = reinterpret_cast<const double2*>(A + (size_t)(r0 + a) * N + c0);
+                const double2 x01 = ap[0], x23 = ap[1];
+                a4[a][0] = x01.x; a4[a][1] = x01.y; a4[a][2] = x23.x; a4[a][3] = x23.y;
+            }
             double acc[4][4];
 #pragma unroll
             for (int a = 0; a < 4; a++)
 #pragma unroll
                 for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
-            for (int k = 0; k < nb; k++) {
-                double lr[4], wc[4];
-#pragma unroll
-                for (int a = 0; a < 4; a++) {
-                    lr[a] = (r0 + a < n) ? A[(size_t)(r0 + a) * n + kb + k] : 0.0;
-                    wc[a] = (c0 + a < n) ? A[(size_t)(kb + k) * n + c0 + a] : 0.0;
-                }
+#pragma unroll 4
+            for (int k = 0; k < NB; k++) {
+                const double2* pl = reinterpret_cast<const double2*>(PL + (size_t)k * m + 4 * tr);
+                const double2* pw = reinterpret_cast<const double2*>(PW + (size_t)k * m + 4 * tc);
+                const double2 l01 = pl[0], l23 = pl[1], w01 = pw[0], w23 = pw[1];
+                const double lr[4] = {l01.x, l01.y, l23.x, l23.y}, wc[4] = {w01.x, w01.y, w23.x, w23.y};
 #pragma unroll
                 for (int a = 0; a < 4; a++)
 #pragma unroll
                     for (int b = 0; b < 4; b++) acc[a][b] += lr[a] * wc[b];
             }
 #pragma unroll
-            for (int a = 0; a < 4; a++)
+            for (int a = 0; a < 4; a++) {
+                double2* ap = reinterpret_cast<double2*>(A + (size_t)(r0 + a) * N + c0);
+                if (tr != tc) {
+                    ap[0] = make_double2(a4[a][0] - acc[a][0], a4[a][1] - acc[a][1]);
+                    ap[1] = make_double2(a4[a][2] - acc[a][2], a4[a][3] - acc[a][3]);
+                } else {
 #pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int gi = r0 + a, gj = c0 + b;
-                    if (gi < n && gj < n && gj <= gi) A[(size_t)gi * n + gj] -= acc[a][b];
+                    for (int b = 0; b < 4; b++)
+                        if (b <= a) A[(size_t)(r0 + a) * N + c0 + b] = a4[a][b] - acc[a][b];
                 }
+            }
         }
         __syncthreads();
+        LDLT_PHASE(2);
     }
+#ifdef MAM_LDLT_PROFILE
+    if (t == 0) for (int k = 0; k < 3; k++) d.red[4 + k] += (double)tacc[k];
+#endif
     if (t == 0) d.flag[0] = fail;
+    if (fail) return;   // uniform (LDS flag after the last barrier)
+    // y /= D
+    for (int i = t; i < N; i += LDLT_THREADS) Y[i] /= A[(size_t)i * N + i];
     __syncthreads();
-    if (fail) return;
-    // blocked substitution: L y = bs; y /= D; L^T x = y
-    double* y = d.x;
-    for (int i = t; i < n; i += 1024) y[i] = d.bs[i];
-    __syncthreads();
-    for (int kb = 0; kb < n; kb += NB) {
-        const int nb = min(NB, n - kb);
+    // backward substitution L^T x = y: block solve by wave 0, then each thread i < kb updates its own y_i
+    for (int kb = N - NB; kb >= 0; kb -= NB) {
         if (wid == 0) {
-            // unit-lower triangular solve of the 16-row block in one wave
-            double v = lane < nb ? y[kb + lane] : 0.0;
-            for (int j = 0; j < nb; j++) {
-                const double yj = __shfl(v, j, 64);
-                if (lane > j && lane < nb) v -= A[(size_t)(kb + lane) * n + kb + j] * yj;
+            double col[NB];   // lane c holds L(kb + j, kb + c) for j > c
+#pragma unroll
+            for (int j = 0; j < NB; j++) col[j] = lane < NB ? A[(size_t)(kb + j) * N + kb + lane] : 0.0;
+            double v = lane < NB ? Y[kb + lane] : 0.0;
+#pragma unroll
+            for (int j = NB - 1; j >= 0; j--) {
+                const double xj = readlane_d(v, j);
+                if (lane < j) v -= col[j] * xj;
             }
-            if (lane < nb) y[kb + lane] = v;
+            if (lane < NB) Y[kb + lane] = v;
         }
         __syncthreads();
-        for (int i = kb + nb + t; i < n; i += 1024) {
-            double s = y[i];
-            for (int j = 0; j < nb; j++) s -= A[(size_t)i * n + kb + j] * y[kb + j];
-            y[i] = s;
+        for (int i = t; i < kb; i += LDLT_THREADS) {
+            double sy = Y[i];
+#pragma unroll
+            for (int j = 0; j < NB; j++) sy -= A[(size_t)(kb + j) * N + i] * Y[kb + j];
+            Y[i] = sy;
         }
         __syncthreads();
     }
-    for (int i = t; i < n; i += 1024) y[i] /= A[(size_t)i * n + i];
+    for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+#ifdef MAM_LDLT_PROFILE
     __syncthreads();
-    const int nblk = (n + NB - 1) / NB;
-    for (int bi = nblk - 1; bi >= 0; bi--) {
-        const int kb = bi * NB, nb = min(NB, n - kb);
-        if (wid == 0) {
-            // unit-upper (L^T) solve of the block: x_i = y_i - sum_{j>i} L_ji x_j
-            double v = lane < nb ? y[kb + lane] : 0.0;
-            for (int j = nb - 1; j >= 0; j--) {
-                const double xj = __shfl(v, j, 64);
-                if (lane < j) v -= A[(size_t)(kb + j) * n + kb + lane] * xj;
-            }
-            if (lane < nb) y[kb + lane] = v;
-        }
-        __syncthreads();
-        for (int i = t; i < kb; i += 1024) {
-            double s = y[i];
-            for (int j = 0; j < nb; j++) s -= A[(size_t)(kb + j) * n + i] * y[kb + j];
-            y[i] = s;
-        }
-        __syncthreads();
-    }
+    if (t == 0) d.red[7] += (double)(clock64() - tp0);
+#endif
 }
 
 __global__ __launch_bounds__(256) void k_backsub(Dev d) {
@@ -615,6 +688,8 @@ using mam::DevBuf;
 struct mam_lba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    size_t ldlt_lds_budget = 0;   // dynamic LDS the factorization may use (panel staging)
+    mam::PinnedBuf staging;       // host mirror of the uploaded part of the arena (one copy per solve)
     mam::StageTimer timer{4};
     DevBuf<uint8_t> arena;
 };
@@ -648,6 +723,16 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
     MAM_HIP(hipSetDevice(device));
     mam_lba_ctx* c = new mam_lba_ctx();
     c->device = device;
+    // gfx950: 160 KB of LDS per workgroup; fall back to the 64 KB default if the opt-in is refused
+    c->ldlt_lds_budget = 0;
+    for (size_t budget : {(size_t)160 * 1024 - 4096, (size_t)64 * 1024 - 4096}) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess) {
+            c->ldlt_lds_budget = budget;
+            break;
+        }
+        (void)hipGetLastError();
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return MAM_ERR_DEVICE;
@@ -693,6 +778,9 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         if (p->edge_point[e] < 0 || p->edge_point[e] >= L || p->edge_pose[e] < 0 || p->edge_pose[e] >= P)
             return MAM_ERR_ARG;
     MAM_HIP(hipSetDevice(c->device));
+#ifdef MAM_LDLT_PROFILE
+    const auto h_t0 = std::chrono::steady_clock::now();
+#endif
     // ---- structure (sparse_optimizer.cpp:166-190): Hessian order = vertices sorted by id
     std::vector<int> po(P), pl(L);
     std::iota(po.begin(), po.end(), 0);
@@ -700,83 +788,129 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     std::stable_sort(po.begin(), po.end(), [&](int a, int b) { return p->pose_id[a] < p->pose_id[b]; });
     std::stable_sort(pl.begin(), pl.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
     std::vector<int32_t> pose_h(P, -1), hpose, point_h(L, -1), hpoint;
+    hpose.reserve(P);
+    hpoint.reserve(L);
     for (int i : po)
         if (!p->pose_fixed[i]) { pose_h[i] = (int)hpose.size(); hpose.push_back(i); }
     for (int i : pl) { point_h[i] = (int)hpoint.size(); hpoint.push_back(i); }
     const int Np = (int)hpose.size();
-    std::vector<std::vector<int>> pe(L);
-    for (int e = 0; e < E; e++) pe[point_h[p->edge_point[e]]].push_back(e);
-    std::vector<int32_t> pe_off(L + 1, 0), pe_idx;
-    for (int h = 0; h < L; h++) { pe_idx.insert(pe_idx.end(), pe[h].begin(), pe[h].end()); pe_off[h + 1] = (int)pe_idx.size(); }
-    std::vector<std::vector<int>> qe(Np);
+    // per Hessian point / pose edge lists (counting sorts, edge order kept)
+    std::vector<int32_t> pe_off(L + 1, 0), pe_idx(E), qe_off(Np + 1, 0), qe_idx;
     for (int e = 0; e < E; e++) {
+        pe_off[point_h[p->edge_point[e]] + 1]++;
         const int h = pose_h[p->edge_pose[e]];
-        if (h >= 0) qe[h].push_back(e);
+        if (h >= 0) qe_off[h + 1]++;
     }
-    std::vector<int32_t> qe_off(Np + 1, 0), qe_idx;
-    for (int h = 0; h < Np; h++) { qe_idx.insert(qe_idx.end(), qe[h].begin(), qe[h].end()); qe_off[h + 1] = (int)qe_idx.size(); }
-    // S block pairs (i1 <= i2) with their contributions in landmark (Hessian point) order
-    std::vector<std::vector<std::pair<int, int>>> blk((size_t)Np * Np);
-    for (int h = 0; h < L; h++) {
-        const std::vector<int>& Es = pe[h];
-        for (int ea : Es) {
-            const int ha = pose_h[p->edge_pose[ea]];
-            if (ha < 0) continue;
-            for (int ec : Es) {
-                const int hc = pose_h[p->edge_pose[ec]];
-                if (hc < 0 || hc < ha) continue;
-                blk[(size_t)ha * Np + hc].push_back({ea, ec});
-            }
+    for (int h = 0; h < L; h++) pe_off[h + 1] += pe_off[h];
+    for (int h = 0; h < Np; h++) qe_off[h + 1] += qe_off[h];
+    qe_idx.resize(qe_off[Np]);
+    {
+        std::vector<int32_t> cp(pe_off.begin(), pe_off.end() - 1), cq(qe_off.begin(), qe_off.end() - 1);
+        for (int e = 0; e < E; e++) {
+            pe_idx[cp[point_h[p->edge_point[e]]]++] = e;
+            const int h = pose_h[p->edge_pose[e]];
+            if (h >= 0) qe_idx[cq[h]++] = e;
         }
     }
-    std::vector<int32_t> bp_off(1, 0), bp_ea, bp_ec, bp_ij;
+    // S block pairs (i1 <= i2, row-major; diagonal blocks always present) with their contributions in landmark
+    // (Hessian point) order, then edge order within the landmark
+    // per landmark, its optimised-pose edges as (pose block, edge) in edge order: the pair loops below then run
+    // over small contiguous arrays
+    std::vector<int32_t> le_off(L + 1, 0), le_h, le_e;
+    le_h.reserve(E);
+    le_e.reserve(E);
+    for (int h = 0; h < L; h++) {
+        for (int sa = pe_off[h]; sa < pe_off[h + 1]; sa++) {
+            const int e = pe_idx[sa], hp = pose_h[p->edge_pose[e]];
+            if (hp < 0) continue;
+            le_h.push_back(hp);
+            le_e.push_back(e);
+        }
+        le_off[h + 1] = (int32_t)le_h.size();
+    }
+    std::vector<int32_t> bcnt((size_t)Np * Np, 0);
+    for (int h = 0; h < L; h++) {
+        const int32_t* hs = le_h.data() + le_off[h];
+        const int cnt = le_off[h + 1] - le_off[h];
+        for (int a = 0; a < cnt; a++) {
+            int32_t* rowc = bcnt.data() + (size_t)hs[a] * Np;
+            for (int c = 0; c < cnt; c++)
+                if (hs[c] >= hs[a]) rowc[hs[c]]++;
+        }
+    }
+    std::vector<int32_t> bslot((size_t)Np * Np, -1), bp_off(1, 0), bp_ij;
     for (int a = 0; a < Np; a++)
         for (int b = a; b < Np; b++) {
-            const auto& v = blk[(size_t)a * Np + b];
-            if (v.empty() && a != b) continue;
-            for (auto& pr : v) { bp_ea.push_back(pr.first); bp_ec.push_back(pr.second); }
-            bp_off.push_back((int)bp_ea.size());
+            const int32_t cnt = bcnt[(size_t)a * Np + b];
+            if (cnt == 0 && a != b) continue;
+            bslot[(size_t)a * Np + b] = bp_off.back();
+            bp_off.push_back(bp_off.back() + cnt);
             bp_ij.push_back(a);
             bp_ij.push_back(b);
         }
     const int nbp = (int)bp_ij.size() / 2;
-    const int n = 6 * Np, nx = 6 * Np + 3 * L;
-    // ---- device arena
+    std::vector<int32_t> bp_ea(bp_off.back()), bp_ec(bp_off.back());
+    for (int h = 0; h < L; h++) {
+        const int32_t* hs = le_h.data() + le_off[h];
+        const int32_t* es = le_e.data() + le_off[h];
+        const int cnt = le_off[h + 1] - le_off[h];
+        for (int a = 0; a < cnt; a++) {
+            int32_t* rows = bslot.data() + (size_t)hs[a] * Np;
+            for (int c = 0; c < cnt; c++) {
+                if (hs[c] < hs[a]) continue;
+                const int32_t pos = rows[hs[c]]++;
+                bp_ea[pos] = es[a];
+                bp_ec[pos] = es[c];
+            }
+        }
+    }
+    const int n = 6 * Np, nx = 6 * Np + 3 * L, npad = mam::lba::ldlt_pad(n);
+    const size_t nbpc = bp_ea.size();
+    // ---- device arena: the uploaded inputs first (mirrored in pinned host memory, one copy), scratch after
     size_t bytes = sz<int32_t>(E) * 2 + sz<double>(2 * (size_t)E) + sz<double>(E) + sz<float>(4 * (size_t)p->n_cams) +
-                   sz<int32_t>(P) * 2 + sz<int32_t>(Np) + sz<int32_t>(L) + sz<int32_t>(L + 1) + sz<int32_t>(E) +
-                   sz<int32_t>(Np + 1) + sz<int32_t>(E) + sz<int32_t>(nbp + 1) + sz<int32_t>(bp_ea.size()) * 2 +
+                   sz<int32_t>(P) * 2 + sz<int32_t>(Np) + sz<int32_t>(L) * 2 + sz<int32_t>(L + 1) + sz<int32_t>(E) +
+                   sz<int32_t>(Np + 1) + sz<int32_t>(E) + sz<int32_t>(nbp + 1) + sz<int32_t>(nbpc) * 2 +
                    sz<int32_t>(2 * (size_t)nbp) + 2 * sz<double>(7 * (size_t)P) + 2 * sz<double>(3 * (size_t)L) +
-                   sz<double>(2 * (size_t)E) + sz<double>(21 * (size_t)E) + sz<double>(E) + 2 * sz<double>(18 * (size_t)E) +
+                   sz<double>(2 * (size_t)E) + sz<double>(21 * (size_t)E) + sz<double>(E) + sz<double>(18 * (size_t)E) * 2 +
                    sz<double>(6 * (size_t)E) + sz<double>(36 * (size_t)Np) + sz<double>(9 * (size_t)L) + sz<double>(nx) +
-                   sz<double>(9 * (size_t)L) + sz<double>((size_t)n * n) + sz<double>(nx) + sz<double>(n) + sz<double>(8) +
+                   sz<double>(9 * (size_t)L) + sz<double>((size_t)npad * npad) + sz<double>(nx) + sz<double>(npad) + sz<double>(8) +
+                   sz<double>(mam::lba::ldlt_ws_doubles(npad)) +
                    sz<int>(4) + sz<uint8_t>(E) + 4096;
     if (int rc = c->arena.alloc(bytes)) return rc;
+    if (int rc = c->staging.alloc(bytes)) return rc;
     Carver cv{c->arena.p};
+    uint8_t* const host_base = c->staging.p;
     mam::lba::Dev d{};
-    d.P = P; d.L = L; d.E = E; d.Np = Np; d.nbp = nbp; d.delta = p->huber_delta;
+    d.P = P; d.L = L; d.E = E; d.Np = Np; d.nbp = nbp; d.npad = npad; d.delta = p->huber_delta;
     hipStream_t s = c->stream;
-    auto up = [&](auto* dst, const auto* src, size_t count) -> int {
-        if (count) MAM_HIP(hipMemcpyAsync((void*)dst, (const void*)src, count * sizeof(*src), hipMemcpyHostToDevice, s));
-        return MAM_OK;
+    // carve a device array and fill its pinned mirror
+    auto put = [&](auto* src, size_t count) {
+        using T = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
+        T* dst = cv.take<T>(count);
+        if (count) std::memcpy(host_base + (reinterpret_cast<uint8_t*>(dst) - c->arena.p), src, count * sizeof(T));
+        return dst;
     };
-    int32_t* ep = cv.take<int32_t>(E); if (int rc = up(ep, p->edge_point, E)) return rc; d.edge_point = ep;
-    int32_t* eq = cv.take<int32_t>(E); if (int rc = up(eq, p->edge_pose, E)) return rc; d.edge_pose = eq;
-    double* eo = cv.take<double>(2 * (size_t)E); if (int rc = up(eo, p->edge_obs, 2 * (size_t)E)) return rc; d.edge_obs = eo;
-    double* ew = cv.take<double>(E); if (int rc = up(ew, p->edge_inv_sigma2, E)) return rc; d.edge_w = ew;
-    float* cams = cv.take<float>(4 * (size_t)p->n_cams); if (int rc = up(cams, p->cams, 4 * (size_t)p->n_cams)) return rc; d.cams = cams;
-    int32_t* pc = cv.take<int32_t>(P);
-    if (p->pose_cam) { if (int rc = up(pc, p->pose_cam, P)) return rc; d.pose_cam = pc; } else d.pose_cam = nullptr;
-    int32_t* ph = cv.take<int32_t>(P); if (int rc = up(ph, pose_h.data(), P)) return rc; d.pose_h = ph;
-    int32_t* hp = cv.take<int32_t>(Np); if (int rc = up(hp, hpose.data(), Np)) return rc; d.hpose = hp;
-    int32_t* hl = cv.take<int32_t>(L); if (int rc = up(hl, hpoint.data(), L)) return rc; d.hpoint = hl;
-    int32_t* peo = cv.take<int32_t>(L + 1); if (int rc = up(peo, pe_off.data(), L + 1)) return rc; d.pe_off = peo;
-    int32_t* pei = cv.take<int32_t>(E); if (int rc = up(pei, pe_idx.data(), pe_idx.size())) return rc; d.pe_idx = pei;
-    int32_t* qeo = cv.take<int32_t>(Np + 1); if (int rc = up(qeo, qe_off.data(), Np + 1)) return rc; d.qe_off = qeo;
-    int32_t* qei = cv.take<int32_t>(E); if (int rc = up(qei, qe_idx.data(), qe_idx.size())) return rc; d.qe_idx = qei;
-    int32_t* bpo = cv.take<int32_t>(nbp + 1); if (int rc = up(bpo, bp_off.data(), nbp + 1)) return rc; d.bp_off = bpo;
-    int32_t* bpa = cv.take<int32_t>(bp_ea.size()); if (int rc = up(bpa, bp_ea.data(), bp_ea.size())) return rc; d.bp_ea = bpa;
-    int32_t* bpc = cv.take<int32_t>(bp_ec.size()); if (int rc = up(bpc, bp_ec.data(), bp_ec.size())) return rc; d.bp_ec = bpc;
-    int32_t* bij = cv.take<int32_t>(2 * (size_t)nbp); if (int rc = up(bij, bp_ij.data(), bp_ij.size())) return rc; d.bp_ij = bij;
+    d.edge_point = put(p->edge_point, E);
+    d.edge_pose = put(p->edge_pose, E);
+    d.edge_obs = put(p->edge_obs, 2 * (size_t)E);
+    d.edge_w = put(p->edge_inv_sigma2, E);
+    d.cams = put(p->cams, 4 * (size_t)p->n_cams);
+    {
+        const int32_t* pcm = put(p->pose_cam ? p->pose_cam : pose_h.data(), P);
+        d.pose_cam = p->pose_cam ? pcm : nullptr;
+    }
+    d.pose_h = put(pose_h.data(), P);
+    d.hpose = put(hpose.data(), Np);
+    d.hpoint = put(hpoint.data(), L);
+    d.point_h = put(point_h.data(), L);
+    d.pe_off = put(pe_off.data(), L + 1);
+    d.pe_idx = put(pe_idx.data(), E);
+    d.qe_off = put(qe_off.data(), Np + 1);
+    d.qe_idx = put(qe_idx.data(), qe_idx.size());
+    d.bp_off = put(bp_off.data(), nbp + 1);
+    d.bp_ea = put(bp_ea.data(), nbpc);
+    d.bp_ec = put(bp_ec.data(), nbpc);
+    d.bp_ij = put(bp_ij.data(), 2 * (size_t)nbp);
     // state: poses packed [q t], SE3Quat(q, t) normalises on construction
     std::vector<double> pose0(7 * (size_t)P);
     for (int i = 0; i < P; i++) {
@@ -786,12 +920,15 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         for (int k = 0; k < 4; k++) pose0[7 * i + k] = q[k] / nq;
         for (int k = 0; k < 3; k++) pose0[7 * i + 4 + k] = p->pose_t[3 * i + k];
     }
-    double* poseA = cv.take<double>(7 * (size_t)P);
+    double* poseA = put(pose0.data(), 7 * (size_t)P);
+    double* ptA = put(p->point_xyz, 3 * (size_t)L);
+    const size_t upload = cv.off;
+#ifdef MAM_LDLT_PROFILE
+    const auto h_t1 = std::chrono::steady_clock::now();
+#endif
+    MAM_HIP(hipMemcpyAsync(c->arena.p, host_base, upload, hipMemcpyHostToDevice, s));
     double* poseB = cv.take<double>(7 * (size_t)P);
-    double* ptA = cv.take<double>(3 * (size_t)L);
     double* ptB = cv.take<double>(3 * (size_t)L);
-    if (int rc = up(poseA, pose0.data(), pose0.size())) return rc;
-    if (int rc = up(ptA, p->point_xyz, 3 * (size_t)L)) return rc;
     d.err = cv.take<double>(2 * (size_t)E);
     d.jac = cv.take<double>(21 * (size_t)E);
     d.rho0 = cv.take<double>(E);
@@ -802,14 +939,16 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     d.Hll = cv.take<double>(9 * (size_t)L);
     d.b = cv.take<double>(nx);
     d.Dinv = cv.take<double>(9 * (size_t)L);
-    d.S = cv.take<double>((size_t)n * n);
+    d.S = cv.take<double>((size_t)npad * npad);
     d.x = cv.take<double>(nx);
-    d.bs = cv.take<double>(n);
+    d.bs = cv.take<double>(npad);
+    d.ws = cv.take<double>(mam::lba::ldlt_ws_doubles(npad));
     d.red = cv.take<double>(8);
+    MAM_HIP(hipMemsetAsync(d.red, 0, sizeof(double) * 8, s));
     d.flag = cv.take<int>(4);
     uint8_t* depth = cv.take<uint8_t>(E);
-    if (n > 0) MAM_HIP(hipMemsetAsync(d.S, 0, sizeof(double) * (size_t)n * n, s));
     MAM_HIP(hipMemsetAsync(d.x, 0, sizeof(double) * nx, s));
+    if (npad > 0) MAM_HIP(hipMemsetAsync(d.bs, 0, sizeof(double) * npad, s));
 
     const int gE = (E + 255) / 256, gL = (L + 255) / 256, gPL = (std::max(P, L) + 255) / 256;
     double* cur_pose = poseA; double* cur_pt = ptA;
@@ -832,7 +971,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     double chi0 = 0;
     if (int rc = chi_of(cur_pose, cur_pt, false, &chi0)) return rc;
     r->initial_chi2 = chi0;
-    double currentLambda = -1.0, ni = 2.0;
+    double currentLambda = -1.0, ni = 2.0, acceptedChi = chi0;
     int nBad = 0, trials = 0, its = 0;
     bool ok = Np + L > 0;
     for (int it = 0; it < p->iterations && !stopped() && ok; it++) {
@@ -842,30 +981,45 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
             state(cur_pose, cur_pt, tr_pose, tr_pt);
             if (E > 0) hipLaunchKernelGGL(mam::lba::k_linearize, dim3(gE), dim3(256), 0, s, d, 1);
             hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(1024), 0, s, d, 0);
-            if (L > 0) hipLaunchKernelGGL(mam::lba::k_point_sys, dim3(gL), dim3(256), 0, s, d);
+            if (L > 0) hipLaunchKernelGGL(mam::lba::k_point_sys, dim3((L + 63) / 64), dim3(64), 0, s, d);
             if (Np > 0) hipLaunchKernelGGL(mam::lba::k_pose_sys, dim3(Np), dim3(64), 0, s, d);
             hipLaunchKernelGGL(mam::lba::k_max_diag, dim3(1), dim3(1024), 0, s, d);
         }
-        MAM_HIP(hipMemcpyAsync(h_red, d.red, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
-        MAM_HIP(hipStreamSynchronize(s));
-        currentChi = h_red[0];
+        if (it == 0) {
+            // lambda init needs max diag(H); afterwards the iteration-start chi2 is, bit for bit, the chi2 of the
+            // trial that was just accepted (same kernels on the same state), so no round trip is needed
+            MAM_HIP(hipMemcpyAsync(h_red, d.red, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+            MAM_HIP(hipStreamSynchronize(s));
+            currentChi = h_red[0];
+            currentLambda = 1e-5 * h_red[2];
+            ni = 2;
+            nBad = 0;
+        } else {
+            currentChi = acceptedChi;
+        }
         const double iniChi = currentChi;
-        if (it == 0) { currentLambda = 1e-5 * h_red[2]; ni = 2; nBad = 0; }
         double rho = 0;
         int qmax = 0;
         do {
             {
                 mam::StageTimer::Scope sc(&c->timer, s, 1);
-                if (L > 0) hipLaunchKernelGGL(mam::lba::k_schur_prep, dim3(gL), dim3(256), 0, s, d, currentLambda);
+                if (L > 0) hipLaunchKernelGGL(mam::lba::k_schur_prep, dim3((L + 63) / 64), dim3(64), 0, s, d, currentLambda);
+                if (E > 0) hipLaunchKernelGGL(mam::lba::k_schur_edge, dim3(gE), dim3(256), 0, s, d);
                 // the factorization leaves fill-in in S: clear the whole matrix before the blocks are rewritten
-                if (n > 0) MAM_HIP(hipMemsetAsync(d.S, 0, sizeof(double) * (size_t)n * n, s));
+                if (npad > 0) MAM_HIP(hipMemsetAsync(d.S, 0, sizeof(double) * (size_t)npad * npad, s));
                 if (nbp > 0) hipLaunchKernelGGL(mam::lba::k_schur_blk, dim3(nbp), dim3(64), 0, s, d, currentLambda);
                 if (Np > 0) hipLaunchKernelGGL(mam::lba::k_schur_rhs, dim3(Np), dim3(64), 0, s, d);
             }
             {
                 mam::StageTimer::Scope sc(&c->timer, s, 2);
                 MAM_HIP(hipMemsetAsync(d.flag, 0, sizeof(int), s));
-                if (Np > 0) hipLaunchKernelGGL(mam::lba::k_ldlt, dim3(1), dim3(1024), 0, s, d);
+                if (Np > 0) {
+                    const size_t lds = mam::lba::ldlt_lds_bytes(npad);
+                    if (lds <= c->ldlt_lds_budget)
+                        hipLaunchKernelGGL(mam::lba::k_ldlt<true>, dim3(1), dim3(mam::lba::LDLT_THREADS), lds, s, d);
+                    else
+                        hipLaunchKernelGGL(mam::lba::k_ldlt<false>, dim3(1), dim3(mam::lba::LDLT_THREADS), 0, s, d);
+                }
             }
             {
                 mam::StageTimer::Scope sc(&c->timer, s, 3);
@@ -894,6 +1048,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
                 currentLambda *= scaleFactor;
                 ni = 2;
                 currentChi = tempChi;
+                acceptedChi = tempChi;
                 std::swap(cur_pose, tr_pose);   // accept: discardTop
                 std::swap(cur_pt, tr_pt);
             } else {
@@ -914,6 +1069,17 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         ok = !term;
     }
     MAM_HIP(hipGetLastError());
+#ifdef MAM_LDLT_PROFILE
+    {
+        double ph[4];
+        MAM_HIP(hipMemcpy(ph, d.red + 4, sizeof(ph), hipMemcpyDeviceToHost));
+        const auto h_t2 = std::chrono::steady_clock::now();
+        fprintf(stderr, "ldlt cycles: diag %.0f panel %.0f trailing %.0f subst %.0f (trials %d); host setup %.3f ms, "
+                "loop %.3f ms\n", ph[0], ph[1], ph[2], ph[3], trials,
+                std::chrono::duration<double, std::milli>(h_t1 - h_t0).count(),
+                std::chrono::duration<double, std::milli>(h_t2 - h_t1).count());
+    }
+#endif
     // ---- results
     std::vector<double> pose_h_out(7 * (size_t)P);
     if (P) MAM_HIP(hipMemcpyAsync(pose_h_out.data(), cur_pose, sizeof(double) * 7 * P, hipMemcpyDeviceToHost, s));
@@ -938,9 +1104,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         for (int k = 0; k < 4; k++) r->pose_q[4 * i + k] = pose_h_out[7 * i + k];
         for (int k = 0; k < 3; k++) r->pose_t[3 * i + k] = pose_h_out[7 * i + 4 + k];
     }
-    double fchi = 0;
-    if (int rc = chi_of(cur_pose, cur_pt, false, &fchi)) return rc;
-    r->final_chi2 = fchi;
+    r->final_chi2 = acceptedChi;   // activeRobustChi2 of the final state: the last accepted trial's (or initial) chi2
     r->iterations = its;
     r->lm_trials = trials;
     r->status = stopped() ? 1 : 0;

@@ -44,6 +44,25 @@ struct DevBuf {
     ~DevBuf() { release(); }
 };
 
+// Pinned host staging buffer (grows, never shrinks): lets a solve upload all its inputs with one copy.
+struct PinnedBuf {
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    int alloc(size_t bytes) {
+        if (bytes <= n && p) return MAM_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        if (bytes == 0) return MAM_OK;
+        MAM_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), bytes, hipHostMallocDefault));
+        n = bytes;
+        return MAM_OK;
+    }
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
 // Accumulates per-stage kernel time with HIP event pairs recorded on the launch stream.
 struct StageTimer {
     struct Ev {
