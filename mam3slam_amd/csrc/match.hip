@@ -15,10 +15,9 @@
 //              order exactly as GetFeaturesInArea, level + radius filters, Hamming distance (4x popcount64);
 //              COUNT pass, per-frame scan, FILL pass into a per-frame candidate pool (entry = idx | dist<<16 |
 //              level<<25, in enumeration order).
-//   k_resolve  per frame, one wave: the reference's sequential greedy loop replayed exactly but 64 units at a
-//              time — each lane resolves one unit against the taken-set at chunk start; lanes whose candidate
-//              set contains a keypoint picked by an earlier lane of the chunk are re-run after the earlier
-//              lanes commit (progress: the first open lane never conflicts). Then the rotation-histogram pass.
+//   k_resolve  per frame, one workgroup: the reference's sequential greedy loop replayed exactly as dependency
+//              rounds — a unit resolves once every earlier unit sharing a candidate keypoint has; units ready in
+//              the same round have disjoint candidates and commit in parallel. Then the rotation-histogram pass.
 //   k_tri      SearchForTriangulation: one wave per idx1 of each shared vocabulary node; wave argmin on
 //              (dist, -position) implements "dist <= bestDist, last equal wins".
 #include <hip/hip_runtime.h>
@@ -62,6 +61,7 @@ struct ProjArgs {
     int32_t* pool_total;      // [F]
     int pool_per_frame;
     uint32_t* events;         // [F][unit_stride]
+    int pool_lds;             // candidate entries the resolve stage stages in LDS
     int32_t* out;             // [F][kp_stride]
     int32_t* out_n;           // [F]
 };
@@ -355,25 +355,39 @@ __device__ __forceinline__ int rot_bin(float rot) {
 
 constexpr int CAND_LDS = 4096;    // candidate entries of one 64-unit chunk staged in LDS (16 KB)
 
-__global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
+// Greedy resolve as dependency rounds. Unit u's outcome depends only on the taken-state of its candidate
+// keypoints, which only earlier units sharing a candidate can change. Each round: every open unit writes its index
+// into minU[k] (atomicMin) for each candidate k; a unit is READY when it is the minimum on all its candidates
+// (every earlier unit sharing one is already final). Ready units have pairwise disjoint candidate sets, so they
+// resolve and commit in parallel with exactly the sequential loop's result (ORBmatcher.cc:84-128 / :1745-1772):
+// taken bits, out[] (a later round = a later unit overwrites: last writer wins), match counts, rotation events.
+constexpr int RESOLVE_THREADS = 1024;
+constexpr int RESOLVE_POOL_LDS = 24576;   // candidate entries staged in LDS per frame (up to 96 KB)
+
+__global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int f = blockIdx.x, lane = threadIdx.x;
+    const int f = blockIdx.x, t = threadIdx.x;
     const int S = p.fr.kp_stride;
     const int nwords = (S + 31) / 32;
-    uint32_t* takenb = reinterpret_cast<uint32_t*>(smem);                       // S bits
-    int* mark = reinterpret_cast<int*>(smem + ((nwords * 4 + 15) & ~15));       // per keypoint, 64 = none
-    uint32_t* cbuf = reinterpret_cast<uint32_t*>(mark + ((S + 3) & ~3));        // chunk candidates
+    uint32_t* takenb = reinterpret_cast<uint32_t*>(smem);                              // S bits
+    int* minU = reinterpret_cast<int*>(smem + ((nwords * 4 + 15) & ~15));             // per keypoint
+    int* minA = minU + ((S + 3) & ~3);                                                 // per keypoint
+    int* outU = minA + ((S + 3) & ~3);                                                 // last assigner
+    uint32_t* cpool = reinterpret_cast<uint32_t*>(outU + ((S + 3) & ~3));              // staged candidates
     __shared__ int hist[MAM_HISTO_LENGTH];
     __shared__ int top[3];
+    __shared__ int s_nm, s_nev;
     const int n = frame_n(p.fr, f);
     int32_t* out = p.out + (size_t)f * S;
     if (p.out_n[f] < 0) return;   // grid stage flagged this frame
     if (p.pool_total[f] > p.pool_per_frame) {
-        if (lane == 0) p.out_n[f] = MAM_ERR_CAPACITY;
+        if (t == 0) p.out_n[f] = MAM_ERR_CAPACITY;
         return;
     }
-    for (int i = lane; i < n; i += 64) out[i] = -1;
-    for (int w = lane; w < nwords; w += 64) {
+    const int nu = p.n_units[f];
+    const uint32_t* gpool = p.pool + (size_t)f * p.pool_per_frame;
+    for (int i = t; i < n; i += RESOLVE_THREADS) out[i] = -1;
+    for (int w = t; w < nwords; w += RESOLVE_THREADS) {
         uint32_t bits = 0;
         if (p.fr.taken)
             for (int b = 0; b < 32; b++) {
@@ -382,119 +396,183 @@ __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
             }
         takenb[w] = bits;
     }
-    for (int i = lane; i < S; i += 64) mark[i] = 64;
-    if (lane < MAM_HISTO_LENGTH) hist[lane] = 0;
-    __syncthreads();
-    const int nu = p.n_units[f];
-    const uint32_t* pool = p.pool + (size_t)f * p.pool_per_frame;
+    for (int i = t; i < S; i += RESOLVE_THREADS) { minU[i] = 0x7FFFFFFF; minA[i] = 0x7FFFFFFF; outU[i] = -1; }
+    if (t < MAM_HISTO_LENGTH) hist[t] = 0;
+    if (t == 0) { s_nm = 0; s_nev = 0; }
     const int32_t* cc = p.cand_cnt + (size_t)f * p.unit_stride;
     const int32_t* co = p.cand_off + (size_t)f * p.unit_stride;
     uint32_t* ev = p.events + (size_t)f * p.unit_stride;
     const mam_keypoint* K = p.fr.keys + (size_t)f * S;
-    int nm = 0, nev = 0;
-    for (int j0 = 0; j0 < nu; j0 += 64) {
-        const int j = j0 + lane;
-        const bool active = j < nu;
-        const int cnt = active ? cc[j] : 0;
-        const int off = active ? co[j] : 0;
-        // the chunk's lists are contiguous in the pool (offsets are an exclusive scan in unit order):
-        // stage them in LDS with coalesced loads, then every lane walks its list from LDS
-        const int cbase = co[j0];
-        const int ctot = wave_sum(cnt);
-        const bool staged = ctot <= CAND_LDS;
-        if (staged)
-            for (int k = lane; k < ctot; k += 64) cbuf[k] = pool[cbase + k];
-        __syncthreads();
-        const uint32_t* lst = staged ? cbuf + (off - cbase) : pool + off;
-        int nobs = 0;
-        float lang = 0.f;
-        if (active) {
-            if (p.mode == 0) {
-                nobs = p.mps[(size_t)f * p.unit_stride + j].nobs;
-            } else {
-                nobs = p.last[(size_t)f * p.unit_stride + j].nobs;
-                lang = p.last[(size_t)f * p.unit_stride + j].angle;
-            }
+    // A candidate is RELEVANT to its unit if its taken state can change the unit's result: dist <= TH_HIGH (it
+    // could be the pick) or, in the ratio-tested local search, dist <= TH_HIGH / nnratio (it could be the second
+    // best that fails the test). Irrelevant candidates never change a result, so the lists are filtered to the
+    // relevant ones while they are staged in LDS.
+    const int rel = p.mode == 1 ? MAM_TH_HIGH
+                                : (p.nnratio > 0.f ? min(256, (int)ceilf((float)MAM_TH_HIGH / p.nnratio) + 1) : 256);
+    // each thread owns units t, t + 1024, ... (at most UPT)
+    constexpr int UPT = 4;
+    if (nu > UPT * RESOLVE_THREADS) {
+        if (t == 0) p.out_n[f] = MAM_ERR_CAPACITY;
+        return;
+    }
+    int ucnt[UPT], uoff[UPT];
+    int mysum = 0;
+#pragma unroll
+    for (int k = 0; k < UPT; k++) {
+        const int u = t + k * RESOLVE_THREADS;
+        int c = 0;
+        if (u < nu) {
+            const uint32_t* lst = gpool + co[u];
+            const int cnt = cc[u];
+            for (int q = 0; q < cnt; q++) c += (int)((lst[q] >> 16) & 0x1FFu) <= rel ? 1 : 0;
         }
-        bool done = !active || cnt == 0;
-        while (__any(!done)) {
-            // (1) each open lane replays the reference's candidate loop against the taken-set
-            //     (ORBmatcher.cc:84-128 for mode 0, :1745-1772 for mode 1)
-            bool assign = false;
-            int bestIdx = -1;
-            if (!done) {
-                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1;
-                for (int t = 0; t < cnt; t++) {
-                    const uint32_t e = lst[t];
-                    const int idx = (int)(e & 0xFFFFu);
-                    if ((takenb[idx >> 5] >> (idx & 31)) & 1u) continue;
-                    const int dist = (int)((e >> 16) & 0x1FFu);
-                    const int lvl = (int)(e >> 25);
-                    if (dist < bestDist) {
-                        bestDist2 = bestDist; bestDist = dist;
-                        bestLevel2 = bestLevel; bestLevel = lvl;
-                        bestIdx = idx;
-                    } else if (dist < bestDist2) {
-                        bestLevel2 = lvl;
-                        bestDist2 = dist;
-                    }
-                }
-                if (bestDist <= MAM_TH_HIGH) {
-                    assign = true;
-                    if (p.mode == 0 && bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) assign = false;
-                }
+        ucnt[k] = c;
+        mysum += c;
+    }
+    // block exclusive scan of the per-thread relevant counts
+    __shared__ int wtot[RESOLVE_THREADS / 64];
+    const int incl = wave_incl_scan(mysum);
+    if ((t & 63) == 63) wtot[t >> 6] = incl;
+    __syncthreads();
+    int base = incl - mysum, total = 0;
+    for (int w = 0; w < RESOLVE_THREADS / 64; w++) {
+        if (w < (t >> 6)) base += wtot[w];
+        total += wtot[w];
+    }
+    const bool staged = total <= p.pool_lds;
+#pragma unroll
+    for (int k = 0; k < UPT; k++) {
+        const int u = t + k * RESOLVE_THREADS;
+        if (u >= nu) { uoff[k] = 0; continue; }
+        if (staged) {
+            uoff[k] = base;
+            const uint32_t* lst = gpool + co[u];
+            const int cnt = cc[u];
+            for (int q = 0; q < cnt; q++) {
+                const uint32_t e = lst[q];
+                if ((int)((e >> 16) & 0x1FFu) <= rel) cpool[base++] = e;
             }
-            // (2) picks that grow the taken-set; the first open lane whose candidate list holds a keypoint
-            //     picked by an EARLIER open lane is stale, lanes before it are final
-            const bool takes = !done && assign && nobs > 0;
-            if (takes) atomicMin(&mark[bestIdx], lane);
-            __syncthreads();
-            bool stale = false;
-            if (!done) {
-                for (int t = 0; t < cnt && !stale; t++) {
-                    if (mark[lst[t] & 0xFFFFu] < lane) stale = true;
-                }
-            }
-            const int jstar = wave_min(stale ? lane : 64);
-            __syncthreads();
-            if (takes) mark[bestIdx] = 64;
-            __syncthreads();
-            // (3) commit lanes < jstar in lane order: out[] last writer wins (min of 63-lane = max lane),
-            //     taken bits, counts, events
-            const bool commit = !done && lane < jstar;
-            const bool cassign = commit && assign;
-            if (cassign) atomicMin(&mark[bestIdx], 63 - lane);
-            __syncthreads();
-            if (cassign) {
-                if (mark[bestIdx] == 63 - lane) out[bestIdx] = j;
-                if (nobs > 0) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
-            }
-            nm += wave_sum(cassign ? 1 : 0);
-            if (p.mode == 1 && p.check_ori) {
-                const int incl = wave_incl_scan(cassign ? 1 : 0);
-                if (cassign) {
-                    const int bin = rot_bin(lang - K[bestIdx].angle);
-                    ev[nev + incl - 1] = (uint32_t)bestIdx | ((uint32_t)bin << 16);
-                }
-                nev += __shfl(incl, 63, 64);
-            }
-            __syncthreads();
-            if (cassign) mark[bestIdx] = 64;
-            done = done || commit;
-            __syncthreads();
+        } else {
+            uoff[k] = co[u];     // unfiltered global list (same results, more work)
+            ucnt[k] = cc[u];
         }
     }
+    const uint32_t* pool = staged ? cpool : gpool;
+    unsigned open = 0, taker = 0;
+#pragma unroll
+    for (int k = 0; k < UPT; k++) {
+        const int u = t + k * RESOLVE_THREADS;
+        if (u < nu && ucnt[k] > 0) {
+            open |= 1u << k;
+            const int nobs = p.mode == 0 ? p.mps[(size_t)f * p.unit_stride + u].nobs
+                                         : p.last[(size_t)f * p.unit_stride + u].nobs;
+            if (nobs > 0) taker |= 1u << k;
+        }
+    }
+    int nm = 0;
+    __syncthreads();
+    while (__syncthreads_or(open != 0)) {
+        // (1) claims. A candidate k is RELEVANT to unit v if k's taken state can change v's result: dist <= TH_HIGH
+        //     (it could be the pick), or in the ratio-tested local search dist <= TH_HIGH / nnratio (it could be the
+        //     second best that fails the test). minU[k]: earliest open unit that could TAKE k (nobs > 0 and
+        //     dist <= TH_HIGH); minA[k]: earliest open unit to which k is relevant.
+        for (int k = 0; k < UPT; k++) {
+            if (!((open >> k) & 1u)) continue;
+            const int u = t + k * RESOLVE_THREADS;
+            const uint32_t* lst = pool + uoff[k];
+            const int cnt = ucnt[k];
+            const bool tk = (taker >> k) & 1u;
+            for (int q = 0; q < cnt; q++) {
+                const uint32_t e = lst[q];
+                const int dist = (int)((e >> 16) & 0x1FFu);
+                if (dist <= rel) atomicMin(&minA[e & 0xFFFFu], u);
+                if (tk && dist <= MAM_TH_HIGH) atomicMin(&minU[e & 0xFFFFu], u);
+            }
+        }
+        __syncthreads();
+        // (2) ready units resolve and commit
+        unsigned was_open = open;
+        for (int k = 0; k < UPT; k++) {
+            if (!((open >> k) & 1u)) continue;
+            const int u = t + k * RESOLVE_THREADS;
+            const uint32_t* lst = pool + uoff[k];
+            const int cnt = ucnt[k];
+            // ready: no earlier open unit can take one of u's candidates, and (if u takes) no earlier open unit
+            // looks at a keypoint u could take
+            const bool tk = (taker >> k) & 1u;
+            bool ready = true;
+            for (int q = 0; q < cnt && ready; q++) {
+                const uint32_t e = lst[q];
+                const int dist = (int)((e >> 16) & 0x1FFu);
+                ready = (dist > rel || minU[e & 0xFFFFu] >= u) &&
+                        (!tk || dist > MAM_TH_HIGH || minA[e & 0xFFFFu] >= u);
+            }
+            if (!ready) continue;
+            open &= ~(1u << k);
+            int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+            for (int q = 0; q < cnt; q++) {
+                const uint32_t e = lst[q];
+                const int idx = (int)(e & 0xFFFFu);
+                if ((takenb[idx >> 5] >> (idx & 31)) & 1u) continue;
+                const int dist = (int)((e >> 16) & 0x1FFu);
+                const int lvl = (int)(e >> 25);
+                if (dist < bestDist) {
+                    bestDist2 = bestDist; bestDist = dist;
+                    bestLevel2 = bestLevel; bestLevel = lvl;
+                    bestIdx = idx;
+                } else if (dist < bestDist2) {
+                    bestLevel2 = lvl;
+                    bestDist2 = dist;
+                }
+            }
+            bool assign = bestDist <= MAM_TH_HIGH;
+            if (assign && p.mode == 0 && bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) assign = false;
+            if (!assign) continue;
+            int nobs;
+            float lang = 0.f;
+            if (p.mode == 0) {
+                nobs = p.mps[(size_t)f * p.unit_stride + u].nobs;
+            } else {
+                nobs = p.last[(size_t)f * p.unit_stride + u].nobs;
+                lang = p.last[(size_t)f * p.unit_stride + u].angle;
+            }
+            atomicMax(&outU[bestIdx], u);   // units that do not take may assign the same keypoint: last wins
+            if (nobs > 0) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
+            nm++;
+            if (p.mode == 1 && p.check_ori) {
+                const int bin = rot_bin(lang - K[bestIdx].angle);
+                ev[atomicAdd(&s_nev, 1)] = (uint32_t)bestIdx | ((uint32_t)bin << 16);
+            }
+        }
+        __syncthreads();
+        // (3) release the claims of every unit that was open this round
+        for (int k = 0; k < UPT; k++) {
+            if (!((was_open >> k) & 1u)) continue;
+            const int u = t + k * RESOLVE_THREADS;
+            const uint32_t* lst = pool + uoff[k];
+            const int cnt = ucnt[k];
+            for (int q = 0; q < cnt; q++) {
+                minU[lst[q] & 0xFFFFu] = 0x7FFFFFFF;
+                minA[lst[q] & 0xFFFFu] = 0x7FFFFFFF;
+            }
+        }
+    }
+    atomicAdd(&s_nm, nm);
+    __syncthreads();
+    for (int i = t; i < n; i += RESOLVE_THREADS) out[i] = outU[i];
+    __syncthreads();
+    const int nev = s_nev;
     // (4) rotation consistency (ORBmatcher.cc:1855-1884, ComputeThreeMaxima :2012-2053)
     if (p.mode == 1 && p.check_ori) {
-        for (int e = lane; e < nev; e += 64) atomicAdd(&hist[ev[e] >> 16], 1);
+        for (int e = t; e < nev; e += RESOLVE_THREADS) atomicAdd(&hist[ev[e] >> 16], 1);
         __syncthreads();
-        if (lane == 0) {
+        if (t == 0) {
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < MAM_HISTO_LENGTH; i++) {
-                const int s = hist[i];
-                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-                else if (s > max3) { max3 = s; ind3 = i; }
+                const int sh = hist[i];
+                if (sh > max1) { max3 = max2; max2 = max1; max1 = sh; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (sh > max2) { max3 = max2; max2 = sh; ind3 = ind2; ind2 = i; }
+                else if (sh > max3) { max3 = sh; ind3 = i; }
             }
             if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
             else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
@@ -502,16 +580,17 @@ __global__ __launch_bounds__(64) void k_resolve(ProjArgs p) {
         }
         __syncthreads();
         int removed = 0;
-        for (int e = lane; e < nev; e += 64) {
+        for (int e = t; e < nev; e += RESOLVE_THREADS) {
             const int bin = (int)(ev[e] >> 16);
             if (bin != top[0] && bin != top[1] && bin != top[2]) {
                 out[ev[e] & 0xFFFFu] = MAM_MATCH_CLEARED;
                 removed++;
             }
         }
-        nm -= wave_sum(removed);
+        if (removed) atomicAdd(&s_nm, -removed);
+        __syncthreads();
     }
-    if (lane == 0) p.out_n[f] = nm;
+    if (t == 0) p.out_n[f] = s_nm;
 }
 
 // ------------------------------------------------------------------------------------------------ triangulation
@@ -636,6 +715,7 @@ struct mam_match_ctx {
     hipStream_t stream = nullptr;
     mam::StageTimer timer{4};
     int pool_per_unit = 96;
+    size_t resolve_lds_max = 64 * 1024;
     // scratch
     DevBuf<uint16_t> grid_idx;
     DevBuf<float2> grid_xy;
@@ -700,8 +780,13 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     {
         mam::StageTimer::Scope sc(&c->timer, s, 2);
         const int S = a.fr.kp_stride;
-        const size_t lds = ((((S + 31) / 32) * 4 + 15) & ~15) + 4 * ((S + 3) & ~3) + 4 * (size_t)mam::CAND_LDS;
-        hipLaunchKernelGGL(mam::k_resolve, dim3(F), dim3(64), lds, s, a);
+        const size_t fixed = ((((S + 31) / 32) * 4 + 15) & ~15) + 12 * ((S + 3) & ~3);
+        if (fixed + 4096 > c->resolve_lds_max) {
+            mam::set_last_error("keypoint capacity too large for the resolve stage");
+            return MAM_ERR_CAPACITY;
+        }
+        a.pool_lds = (int)std::min<size_t>((size_t)mam::RESOLVE_POOL_LDS, (c->resolve_lds_max - fixed) / 4);
+        hipLaunchKernelGGL(mam::k_resolve, dim3(F), dim3(mam::RESOLVE_THREADS), fixed + 4 * (size_t)a.pool_lds, s, a);
     }
     MAM_HIP(hipGetLastError());
     return MAM_OK;
@@ -722,6 +807,13 @@ int mam_match_create(int device, mam_match_ctx** out) {
     MAM_HIP(hipSetDevice(device));
     mam_match_ctx* c = new mam_match_ctx();
     c->device = device;
+    // the resolve stage may stage up to ~110 KB in LDS (gfx950: 160 KB per workgroup)
+    c->resolve_lds_max = 64 * 1024;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_resolve), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024 - 1024) == hipSuccess)
+        c->resolve_lds_max = 160 * 1024 - 1024;
+    else
+        (void)hipGetLastError();
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         mam::set_last_error("hipStreamCreate failed");

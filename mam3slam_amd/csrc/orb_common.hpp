@@ -11,8 +11,8 @@ namespace mam {
 constexpr int EDGE_THRESHOLD = 19;
 constexpr int PATCH_SIZE = 31;
 constexpr int HALF_PATCH_SIZE = 15;
-constexpr int BLUR_TILE_W = 64;
-constexpr int BLUR_TILE_H = 16;
+constexpr int BLUR_TILE_W = 128;   // k_blur7 output tile: 4 px per thread-quad
+constexpr int BLUR_TILE_H = 32;
 
 // One pyramid level of the current frame size (all frames in a batch share it).
 struct LevelGeom {

@@ -165,9 +165,13 @@ __global__ __launch_bounds__(256) void k_pyr_down(const Geom* __restrict__ g, in
 }
 
 // ------------------------------------------------------------------------------------------------ FAST cells
-// FAST-9/16 "strength" S = max over the 16 arcs of 9 contiguous circle pixels of min(v-p) (dark) or
-// min(p-v) (bright). Pixel is a FAST corner at threshold t iff S > t and OpenCV's cornerScore is then S-1
-// (fast_score.cpp: max(t, A, B) - 1), so one S map serves both thresholds.
+// FAST-9/16 "strength" S = max over the 16 arcs of 9 contiguous circle pixels of min(v-p) (dark circle) or
+// min(p-v) (bright circle). A pixel is a FAST corner at threshold t iff S > t, and OpenCV's cornerScore is then
+// S-1 (fast_score.cpp: max(t, A, B) - 1), so one S map serves both thresholds. Arc minima by 3-input min/max:
+// m3[k] = min(d[k..k+2]), arc[k] = min(m3[k], m3[k+3], m3[k+6]).
+__device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
+__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
+
 __device__ __forceinline__ int fast_strength(const uint8_t* im, int cols, int r, int c) {
     const uint8_t* p = im + r * cols + c;
     const int v = p[0];
@@ -188,44 +192,35 @@ __device__ __forceinline__ int fast_strength(const uint8_t* im, int cols, int r,
     d[13] = v - p[cols - 3];
     d[14] = v - p[2 * cols - 2];
     d[15] = v - p[3 * cols - 1];
-    int mn2[16], mx2[16];
+    int mn3[16], mx3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
+        mn3[k] = min3i(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+        mx3[k] = max3i(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
     }
-    int mn4[16], mx4[16];
+    int arcmin[16], arcmax[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+        arcmin[k] = min3i(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]);
+        arcmax[k] = max3i(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]);
     }
-    int A = -1024, Bm = 1024;
+    int A = max3i(arcmin[0], arcmin[1], arcmin[2]), Bm = min3i(arcmax[0], arcmax[1], arcmax[2]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int mn8 = min(mn4[k], mn4[(k + 4) & 15]);
-        const int mx8 = max(mx4[k], mx4[(k + 4) & 15]);
-        A = max(A, min(mn8, d[(k + 8) & 15]));
-        Bm = min(Bm, max(mx8, d[(k + 8) & 15]));
+    for (int k = 3; k < 15; k += 2) {
+        A = max3i(A, arcmin[k], arcmin[k + 1]);
+        Bm = min3i(Bm, arcmax[k], arcmax[k + 1]);
     }
+    A = max(A, arcmin[15]);
+    Bm = min(Bm, arcmax[15]);
     const int S = max(A, -Bm);
     return S < 0 ? 0 : S;
 }
 
-__device__ __forceinline__ bool fast_is_kp(const uint8_t* S, int cols, int idx, int t) {
-    const int s = S[idx];
-    if (s <= t) return false;
-    const int sc = s - 1;
-    const int nb[8] = {-cols - 1, -cols, -cols + 1, -1, 1, cols - 1, cols, cols + 1};
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int q = S[idx + nb[i]];
-        const int scq = q > t ? q - 1 : 0;
-        if (!(sc > scq)) return false;
-    }
-    return true;
-}
-
+// One workgroup per cell. (a) ROI -> LDS; (b) S for the inner pixels (the 3-pixel ring stays 0: cv::FAST on the
+// cell ROI never scores it); (c) each thread takes a contiguous run of inner pixels in row-major order and
+// computes the NMS peak P = S if S > max of its 8 neighbours (else 0): with t >= 1 OpenCV's test
+// "score > every neighbour's score-or-0" is exactly S > t && S > max8(S) && S >= 2, for both thresholds;
+// (d) iniThFAST if any P > iniTh else minThFAST; (e) one block scan places the run's corners in order.
 __global__ __launch_bounds__(256) void k_fast_cells(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
                                                     LevelSrc s, uint32_t* __restrict__ cand,
                                                     int* __restrict__ cell_counts, int iniTh, int minTh) {
@@ -242,48 +237,72 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geom* __restrict__ g, 
     const uint8_t* lev = level_ptr(g, s, f, c.level, &pitch);
     const int rows = c.y1 - c.y0, cols = c.x1 - c.x0;
     const int npx = rows * cols;
-    for (int i = tid; i < npx; i += 256) {
-        const int r = i / cols, cc = i - r * cols;
-        im[i] = lev[(size_t)(c.y0 + r) * pitch + c.x0 + cc];
-        S[i] = 0;
+    // linear index walks with incremental (row, col): one integer division per thread, not per pixel
+    {
+        const int dq = 256 / cols, dr = 256 - dq * cols;
+        int r = tid / cols, cc = tid - r * cols;
+        const uint8_t* src = lev + (size_t)c.y0 * pitch + c.x0;
+        for (int i = tid; i < npx; i += 256) {
+            im[i] = src[(size_t)r * pitch + cc];
+            S[i] = 0;
+            r += dq;
+            cc += dr;
+            if (cc >= cols) { cc -= cols; r++; }
+        }
     }
     __syncthreads();
     const int bh = rows - 6, bw = cols - 6;
     const int nb = (bh > 0 && bw > 0) ? bh * bw : 0;
-    for (int i = tid; i < nb; i += 256) {
-        const int r = 3 + i / bw, cc = 3 + i % bw;
-        S[r * cols + cc] = (uint8_t)fast_strength(im, cols, r, cc);
+    if (nb > 0) {
+        const int dq = 256 / bw, dr = 256 - dq * bw;
+        int r = 3 + tid / bw, cc = 3 + tid % bw;
+        for (int i = tid; i < nb; i += 256) {
+            S[r * cols + cc] = (uint8_t)fast_strength(im, cols, r, cc);
+            r += dq;
+            cc += dr;
+            if (cc >= bw + 3) { cc -= bw; r++; }
+        }
     }
     __syncthreads();
+    // (c) NMS peaks over this thread's run [i0, i1), stored in place of the (no longer needed) ROI pixels
+    const int per = (nb + 255) / 256;
+    const int i0 = min(tid * per, nb), i1 = min(i0 + per, nb);
+    const int tlo = max(iniTh, 1), thi = max(minTh, 1);
+    int cnt_ini = 0;
+    const int r0 = nb > 0 ? 3 + i0 / bw : 0, c0 = nb > 0 ? 3 + i0 % bw : 0;
+    int rr = r0, ccol = c0;
+    for (int i = i0; i < i1; i++) {
+        const int q = rr * cols + ccol;
+        if (++ccol == bw + 3) { ccol = 3; rr++; }
+        const int sv = S[q];
+        int pk = 0;
+        if (sv > min(tlo, thi)) {
+            const int m8 = max(max(max3i(S[q - cols - 1], S[q - cols], S[q - cols + 1]), max3i(S[q - 1], S[q + 1], S[q + cols - 1])),
+                               max(S[q + cols], S[q + cols + 1]));
+            pk = (sv > m8 && sv >= 2) ? sv : 0;
+        }
+        im[i] = (uint8_t)pk;
+        cnt_ini += pk > tlo ? 1 : 0;
+    }
+    const int total = block_sum(cnt_ini, scr);
+    const int th = total > 0 ? tlo : thi;
     int cnt = 0;
-    for (int i = tid; i < nb; i += 256) {
-        const int r = 3 + i / bw, cc = 3 + i % bw;
-        cnt += fast_is_kp(S, cols, r * cols + cc, iniTh) ? 1 : 0;
-    }
-    const int total = block_sum(cnt, scr);
-    const int th = total > 0 ? iniTh : minTh;
+    for (int i = i0; i < i1; i++) cnt += im[i] > th ? 1 : 0;
+    int tot;
+    int pos = block_excl_scan(cnt, scr, &tot);
     uint32_t* out = cand + (size_t)f * g->cand_per_frame + L.cand_base + (size_t)c.slot * L.cellcap;
-    int base = 0;
-    for (int chunk = 0; chunk < nb; chunk += 256) {
-        const int i = chunk + tid;
-        bool flag = false;
-        int r = 0, cc = 0;
-        if (i < nb) {
-            r = 3 + i / bw;
-            cc = 3 + i % bw;
-            flag = fast_is_kp(S, cols, r * cols + cc, th);
+    rr = r0;
+    ccol = c0;
+    for (int i = i0; i < i1; i++) {
+        const int pk = im[i];
+        if (pk > th) {
+            const uint32_t x = (uint32_t)(ccol + c.cj * L.wCell);
+            const uint32_t y = (uint32_t)(rr + c.ci * L.hCell);
+            out[pos++] = x | (y << 12) | ((uint32_t)(pk - 1) << 24);
         }
-        int tot;
-        const int pos = block_excl_scan(flag ? 1 : 0, scr, &tot);
-        if (flag) {
-            const uint32_t x = (uint32_t)(cc + c.cj * L.wCell);
-            const uint32_t y = (uint32_t)(r + c.ci * L.hCell);
-            const uint32_t sc = (uint32_t)(S[r * cols + cc] - 1);
-            out[base + pos] = x | (y << 12) | (sc << 24);
-        }
-        base += tot;
+        if (++ccol == bw + 3) { ccol = 3; rr++; }
     }
-    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = base;
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = tot;
 }
 
 // ------------------------------------------------------------------------------------------------ blur
@@ -292,9 +311,16 @@ __device__ __forceinline__ int refl101(int p, int n) {
     return p;
 }
 
+// Tile of BLUR_TILE_W x BLUR_TILE_H outputs. Input staged in LDS as bytes (rows y0-3 .. y0+H+2, cols x0-4 ..
+// x0+W+3); interior tiles load aligned 32-bit words, border tiles reflect per byte (BORDER_REFLECT_101).
+// Horizontal pass: 4 outputs per thread from 12 staged bytes -> u16 sums in LDS; vertical pass: 4 outputs per
+// thread from 7 x 4 u16 -> one 32-bit store. Integer arithmetic exactly as the fixed-point separable filter.
+constexpr int BLUR_IN_W = BLUR_TILE_W + 8;   // staged columns (x0-4 .. x0+W+3), multiple of 4
+constexpr int BLUR_IN_H = BLUR_TILE_H + 6;
+
 __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ blur) {
-    __shared__ uint8_t tin[BLUR_TILE_H + 6][BLUR_TILE_W + 8];
-    __shared__ uint32_t th_[BLUR_TILE_H + 6][BLUR_TILE_W];
+    __shared__ __attribute__((aligned(16))) uint8_t tin[BLUR_IN_H][BLUR_IN_W];
+    __shared__ __attribute__((aligned(16))) uint16_t th_[BLUR_IN_H][BLUR_TILE_W];
     const int f = blockIdx.y;
     int tile = blockIdx.x;
     int l = 0;
@@ -307,28 +333,74 @@ __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, Level
     int pitch;
     const uint8_t* lev = level_ptr(g, s, f, l, &pitch);
     const int tid = threadIdx.x;
-    for (int i = tid; i < (BLUR_TILE_H + 6) * (BLUR_TILE_W + 6); i += 256) {
-        const int r = i / (BLUR_TILE_W + 6), c = i % (BLUR_TILE_W + 6);
-        const int gy = refl101(y0 - 3 + r, L.h), gx = refl101(x0 - 3 + c, L.w);
-        tin[r][c] = lev[(size_t)gy * pitch + gx];
+    const int w = L.w, h = L.h;
+    const bool words = x0 >= 4 && x0 + BLUR_TILE_W + 4 <= w && ((pitch | (int)((uintptr_t)lev & 3)) & 3) == 0;
+    if (words) {
+        constexpr int WPR = BLUR_IN_W / 4;
+        for (int i = tid; i < BLUR_IN_H * WPR; i += 256) {
+            const int r = i / WPR, c = i - r * WPR;
+            const int gy = refl101(y0 - 3 + r, h);
+            *reinterpret_cast<uint32_t*>(&tin[r][4 * c]) =
+                *reinterpret_cast<const uint32_t*>(lev + (size_t)gy * pitch + x0 - 4 + 4 * c);
+        }
+    } else {
+        for (int i = tid; i < BLUR_IN_H * BLUR_IN_W; i += 256) {
+            const int r = i / BLUR_IN_W, c = i - r * BLUR_IN_W;
+            const int gy = refl101(y0 - 3 + r, h);
+            const int gx = refl101(min(x0 - 4 + c, 2 * w - 2), w);
+            tin[r][c] = lev[(size_t)gy * pitch + gx];
+        }
     }
     __syncthreads();
-    for (int i = tid; i < (BLUR_TILE_H + 6) * BLUR_TILE_W; i += 256) {
-        const int r = i / BLUR_TILE_W, c = i % BLUR_TILE_W;
-        const uint8_t* p = &tin[r][c];
-        th_[r][c] = GT0 * (p[0] + p[6]) + GT1 * (p[1] + p[5]) + GT2 * (p[2] + p[4]) + GT3 * p[3];
+    // horizontal: output column x0+4q+k uses staged columns 4q+k+1 .. 4q+k+7
+    constexpr int QPR = BLUR_TILE_W / 4;
+    for (int i = tid; i < BLUR_IN_H * QPR; i += 256) {
+        const int r = i / QPR, q = i - r * QPR;
+        const uint32_t wa = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q]);
+        const uint32_t wb = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 4]);
+        const uint32_t wc = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 8]);
+        int p[12];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            p[k] = (wa >> (8 * k)) & 0xFF;
+            p[4 + k] = (wb >> (8 * k)) & 0xFF;
+            p[8 + k] = (wc >> (8 * k)) & 0xFF;
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int* pp = p + k + 1;
+            o[k] = GT0 * (pp[0] + pp[6]) + GT1 * (pp[1] + pp[5]) + GT2 * (pp[2] + pp[4]) + GT3 * pp[3];
+        }
+        uint2 packed;
+        packed.x = o[0] | (o[1] << 16);
+        packed.y = o[2] | (o[3] << 16);
+        *reinterpret_cast<uint2*>(&th_[r][4 * q]) = packed;
     }
     __syncthreads();
     uint8_t* out = blur + L.blur_off + (size_t)f * L.frame_bytes;
-    for (int i = tid; i < BLUR_TILE_H * BLUR_TILE_W; i += 256) {
-        const int r = i / BLUR_TILE_W, c = i % BLUR_TILE_W;
-        const int y = y0 + r, x = x0 + c;
-        if (y < L.h && x < L.w) {
-            const uint32_t sum = GT0 * (th_[r][c] + th_[r + 6][c]) + GT1 * (th_[r + 1][c] + th_[r + 5][c]) +
-                                 GT2 * (th_[r + 2][c] + th_[r + 4][c]) + GT3 * th_[r + 3][c];
-            const uint32_t v = (sum + 32768u) >> 16;
-            out[(size_t)y * L.pitch + x] = (uint8_t)(v > 255u ? 255u : v);
+    for (int i = tid; i < BLUR_TILE_H * QPR; i += 256) {
+        const int r = i / QPR, q = i - r * QPR;
+        const int y = y0 + r, x = x0 + 4 * q;
+        if (y >= h || x >= w) continue;
+        uint32_t col[7][4];
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const uint2 v = *reinterpret_cast<const uint2*>(&th_[r + k][4 * q]);
+            col[k][0] = v.x & 0xFFFF; col[k][1] = v.x >> 16; col[k][2] = v.y & 0xFFFF; col[k][3] = v.y >> 16;
         }
+        uint32_t packed = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t sum = GT0 * (col[0][c] + col[6][c]) + GT1 * (col[1][c] + col[5][c]) +
+                                 GT2 * (col[2][c] + col[4][c]) + GT3 * col[3][c];
+            const uint32_t v = (sum + 32768u) >> 16;
+            packed |= (v > 255u ? 255u : v) << (8 * c);
+        }
+        uint8_t* o = out + (size_t)y * L.pitch + x;
+        if (x + 4 <= w) *reinterpret_cast<uint32_t*>(o) = packed;
+        else
+            for (int c = 0; c < 4 && x + c < w; c++) o[c] = (uint8_t)(packed >> (8 * c));
     }
 }
 
