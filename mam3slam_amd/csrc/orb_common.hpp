@@ -11,6 +11,8 @@ namespace mam {
 constexpr int EDGE_THRESHOLD = 19;
 constexpr int PATCH_SIZE = 31;
 constexpr int HALF_PATCH_SIZE = 15;
+constexpr int PYR_XB = 1024;        // k_pyr_down output columns per workgroup (4 per thread)
+constexpr int PYR_RB = 8;           // k_pyr_down output rows per workgroup
 constexpr int BLUR_TILE_W = 128;   // k_blur7 output tile: 4 px per thread-quad
 constexpr int BLUR_TILE_H = 32;
 
@@ -58,6 +60,7 @@ struct Geom {
     int node_cap;           // DistributeOctTree node capacity (LDS)
     int max_level_cells;
     int roi_max_rows, roi_max_cols;
+    int pyr_seg_w, pyr_rows;   // k_pyr_down LDS staging: source bytes per row / source rows per block (max)
     int umax[16];
     LevelGeom L[MAM_MAX_LEVELS];
 };

@@ -256,6 +256,17 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
             ts.insert(ts.end(), be.begin(), be.end());
             xmaxv[l] = xmax;
             xvecv[l] = xvec;
+            // LDS staging bounds of k_pyr_down: source columns / rows one (PYR_XB x PYR_RB) output block reads
+            const int sw = g.L[l - 1].w, sh = g.L[l - 1].h, dw = g.L[l].w, dh = g.L[l].h;
+            for (int dx0 = 0; dx0 < dw; dx0 += mam::PYR_XB) {
+                const int a = xo[dx0] & ~3, b = std::min(xo[std::min(dx0 + mam::PYR_XB, dw) - 1] + 1, sw - 1);
+                g.pyr_seg_w = std::max(g.pyr_seg_w, ((b - a + 1) + 3) & ~3);
+            }
+            for (int dy0 = 0; dy0 < dh; dy0 += mam::PYR_RB) {
+                const int a = std::min(std::max(yo[dy0], 0), sh - 1);
+                const int b = std::min(std::max(yo[std::min(dy0 + mam::PYR_RB, dh) - 1] + 1, 0), sh - 1);
+                g.pyr_rows = std::max(g.pyr_rows, b - a + 1);
+            }
         }
         if (int rc = c->d_tabs_i.alloc(std::max<size_t>(ti.size(), 1))) return rc;
         if (int rc = c->d_tabs_s.alloc(std::max<size_t>(ts.size(), 1))) return rc;
@@ -272,7 +283,8 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         }
         if (int rc = c->d_cells.alloc(c->cells.size())) return rc;
         MAM_HIP(hipMemcpy(c->d_cells.p, c->cells.data(), c->cells.size() * sizeof(mam::CellDesc), hipMemcpyHostToDevice));
-        c->fast_lds = 2 * (((size_t)rmax * cmax + 15) & ~(size_t)15) + 64;
+        // k_fast_cells LDS: P bytes | S bytes | f16 pixel pairs (4 B per ROI position) | scan scratch
+        c->fast_lds = 2 * (((size_t)rmax * cmax + 15) & ~(size_t)15) + 4 * (size_t)rmax * cmax + 64;
         c->dist_lds = distribute_lds_bytes(g.node_cap, maxcells);
         if (c->fast_lds > 160 * 1024 || c->dist_lds > 160 * 1024) {
             g_last_error = "LDS budget exceeded (nfeatures or cell size too large)";
@@ -315,20 +327,23 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
     mam::LevelSrc src{d_in, stride, fstride, c->d_pyr.p};
     {
         StageScope sc(&c->timer, s, MAM_STAGE_PYRAMID);
+        const size_t lds = (size_t)g.pyr_seg_w * g.pyr_rows;
         for (int l = 1; l < L; l++) {
             const mam::LevelGeom& lv = g.L[l];
-            dim3 grid((lv.w + 255) / 256, (lv.h + 3) / 4, F);
-            hipLaunchKernelGGL(mam::k_pyr_down, grid, dim3(256), 0, s, c->d_geom.p, l, src, c->d_pyr.p);
+            dim3 grid((lv.w + mam::PYR_XB - 1) / mam::PYR_XB, (lv.h + mam::PYR_RB - 1) / mam::PYR_RB, F);
+            hipLaunchKernelGGL(mam::k_pyr_down, grid, dim3(256), lds, s, c->d_geom.p, l, src, c->d_pyr.p);
         }
+    }
+    // (blur and FAST are both VALU-bound: running the blur on a second stream beside FAST + DistributeOctTree
+    // measured no gain, so the stages stay in order on one stream)
+    {
+        StageScope sc(&c->timer, s, MAM_STAGE_BLUR);
+        hipLaunchKernelGGL(mam::k_blur7, dim3(g.tiles_per_frame, F), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p);
     }
     {
         StageScope sc(&c->timer, s, MAM_STAGE_FAST);
         hipLaunchKernelGGL(mam::k_fast_cells, dim3(g.cells_per_frame, F), dim3(256), c->fast_lds, s, c->d_geom.p,
                            c->d_cells.p, src, c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast);
-    }
-    {
-        StageScope sc(&c->timer, s, MAM_STAGE_BLUR);
-        hipLaunchKernelGGL(mam::k_blur7, dim3(g.tiles_per_frame, F), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p);
     }
     {
         StageScope sc(&c->timer, s, MAM_STAGE_DISTRIBUTE);

@@ -109,37 +109,70 @@ __device__ __forceinline__ const uint8_t* level_ptr(const Geom* g, const LevelSr
 // OpenCV hal::resize INTER_LINEAR, CV_8UC1: exact-int horizontal pass
 // (HResizeLinear), vertical pass with VResizeLinearVec_32s8u's mulhi formula for x < xvec and
 // FixedPtCast<int,uchar,22> beyond. 4 output pixels per thread, one u32 store.
+// One workgroup per PYR_XB x PYR_RB output block: the source rows/columns the block reads are staged in LDS
+// (32-bit loads where aligned), each thread owns one 4-pixel column quad for the block's rows and keeps its
+// xofs/alpha coefficients in registers.
 __global__ __launch_bounds__(256) void k_pyr_down(const Geom* __restrict__ g, int l, LevelSrc s, uint8_t* pyr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t rbuf[];
     const LevelGeom& L = g->L[l];
     const LevelGeom& P = g->L[l - 1];
     const int f = blockIdx.z;
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int dx0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
-    if (dy >= L.h || dx0 >= L.w) return;
+    const int dx0 = blockIdx.x * PYR_XB, dy0 = blockIdx.y * PYR_RB;
+    const int nx = min(PYR_XB, L.w - dx0), ny = min(PYR_RB, L.h - dy0);
+    const int SW = g->pyr_seg_w;
     int spitch;
     const uint8_t* src = level_ptr(g, s, f, l - 1, &spitch);
     uint8_t* dst = pyr + L.pyr_off + (size_t)f * L.frame_bytes;
-    const int sy = L.yofs[dy];
     const int sh = P.h;
-    const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
-    const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
-    const uint8_t* S0 = src + (size_t)ry0 * spitch;
-    const uint8_t* S1 = src + (size_t)ry1 * spitch;
-    const int b0 = L.ibeta[2 * dy], b1 = L.ibeta[2 * dy + 1];
-    uint32_t packed = 0;
+    const int sxa = L.xofs[dx0] & ~3;
+    const int sxb = min(L.xofs[dx0 + nx - 1] + 1, P.w - 1);
+    const int segw = sxb - sxa + 1;
+    const int ry_lo = min(max(L.yofs[dy0], 0), sh - 1);
+    const int ry_hi = min(max(L.yofs[dy0 + ny - 1] + 1, 0), sh - 1);
+    const int nrows = ry_hi - ry_lo + 1;
+    const int tid = threadIdx.x;
+    const bool aligned = ((spitch | (int)((uintptr_t)src & 3)) & 3) == 0;
+    const int nw = aligned ? segw >> 2 : 0;   // whole words inside the segment
+    for (int i = tid; i < nrows * nw; i += 256) {
+        const int r = i / nw, c = i - r * nw;
+        *reinterpret_cast<uint32_t*>(rbuf + r * SW + 4 * c) =
+            *reinterpret_cast<const uint32_t*>(src + (size_t)(ry_lo + r) * spitch + sxa + 4 * c);
+    }
+    const int tail = segw - 4 * nw;
+    for (int i = tid; i < nrows * tail; i += 256) {
+        const int r = i / tail, c = 4 * nw + (i - r * tail);
+        rbuf[r * SW + c] = src[(size_t)(ry_lo + r) * spitch + sxa + c];
+    }
+    __syncthreads();
+    const int q = tid;   // PYR_XB / 4 == 256 quads
+    if (4 * q >= nx) return;
+    int sx[4], a0[4], a1[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const int dx = dx0 + i;
-        if (dx < L.w) {
-            const int sx = L.xofs[dx];
+        const int dx = min(dx0 + 4 * q + i, L.w - 1);
+        sx[i] = L.xofs[dx] - sxa;
+        a0[i] = L.ialpha[2 * dx];
+        a1[i] = L.ialpha[2 * dx + 1];
+    }
+    for (int rr = 0; rr < ny; rr++) {
+        const int dy = dy0 + rr;
+        const int sy = L.yofs[dy];
+        const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
+        const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
+        const uint8_t* S0 = rbuf + (ry0 - ry_lo) * SW;
+        const uint8_t* S1 = rbuf + (ry1 - ry_lo) * SW;
+        const int b0 = L.ibeta[2 * dy], b1 = L.ibeta[2 * dy + 1];
+        uint32_t packed = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int dx = dx0 + 4 * q + i;
             int h0, h1;
             if (dx < L.xmax) {
-                const int a0 = L.ialpha[2 * dx], a1 = L.ialpha[2 * dx + 1];
-                h0 = S0[sx] * a0 + S0[sx + 1] * a1;
-                h1 = S1[sx] * a0 + S1[sx + 1] * a1;
+                h0 = S0[sx[i]] * a0[i] + S0[sx[i] + 1] * a1[i];
+                h1 = S1[sx[i]] * a0[i] + S1[sx[i] + 1] * a1[i];
             } else {
-                h0 = S0[sx] * 2048;
-                h1 = S1[sx] * 2048;
+                h0 = S0[sx[i]] * 2048;
+                h1 = S1[sx[i]] * 2048;
             }
             int v;
             if (dx < L.xvec) {
@@ -155,27 +188,39 @@ __global__ __launch_bounds__(256) void k_pyr_down(const Geom* __restrict__ g, in
             v = min(max(v, 0), 255);
             packed |= (uint32_t)v << (8 * i);
         }
-    }
-    uint8_t* o = dst + (size_t)dy * L.pitch + dx0;
-    if (dx0 + 4 <= L.w) {
-        *reinterpret_cast<uint32_t*>(o) = packed;
-    } else {
-        for (int i = 0; i < 4 && dx0 + i < L.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+        uint8_t* o = dst + (size_t)dy * L.pitch + dx0 + 4 * q;
+        if (dx0 + 4 * q + 4 <= L.w) {
+            *reinterpret_cast<uint32_t*>(o) = packed;
+        } else {
+            for (int i = 0; i < 4 && dx0 + 4 * q + i < L.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------------------ FAST cells
 // FAST-9/16 "strength" S = max over the 16 arcs of 9 contiguous circle pixels of min(v-p) (dark circle) or
 // min(p-v) (bright circle). A pixel is a FAST corner at threshold t iff S > t, and OpenCV's cornerScore is then
-// S-1 (fast_score.cpp: max(t, A, B) - 1), so one S map serves both thresholds. Arc minima by 3-input min/max:
+// S-1 (fast_score.cpp: max(t, A, B) - 1), so one S map serves both thresholds.
+// Two horizontally adjacent pixels per lane in packed fp16 (every difference of two bytes, -255..255, is exact in
+// fp16): the ROI is staged as pixel pairs (p[c], p[c+1]), so one 32-bit LDS read gives a circle sample for both
+// pixels, and the arc minima / maxima use gfx950's 3-input packed v_pk_minimum3_f16 / v_pk_maximum3_f16:
 // m3[k] = min(d[k..k+2]), arc[k] = min(m3[k], m3[k+3], m3[k+6]).
-__device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
-__device__ __forceinline__ int fast_strength(const uint8_t* im, int cols, int r, int c) {
-    const uint8_t* p = im + r * cols + c;
-    const int v = p[0];
-    int d[16];
+__device__ __forceinline__ half2_t hmin3(half2_t a, half2_t b, half2_t c) {
+    return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ __forceinline__ half2_t hmax3(half2_t a, half2_t b, half2_t c) {
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+
+// S of the pixel pair at (r, c), (r, c + 1); hp: ROI pixel pairs, row pitch `cols` (in pairs)
+__device__ __forceinline__ void fast_strength2(const half2_t* hp, int cols, int r, int c, int* s0, int* s1) {
+    const half2_t* p = hp + r * cols + c;
+    const half2_t v = p[0];
+    half2_t d[16];
     d[0] = v - p[3 * cols];
     d[1] = v - p[3 * cols + 1];
     d[2] = v - p[2 * cols + 2];
@@ -192,28 +237,30 @@ __device__ __forceinline__ int fast_strength(const uint8_t* im, int cols, int r,
     d[13] = v - p[cols - 3];
     d[14] = v - p[2 * cols - 2];
     d[15] = v - p[3 * cols - 1];
-    int mn3[16], mx3[16];
+    half2_t mn3[16], mx3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        mn3[k] = min3i(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
-        mx3[k] = max3i(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+        mn3[k] = hmin3(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+        mx3[k] = hmax3(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
     }
-    int arcmin[16], arcmax[16];
+    half2_t arcmin[16], arcmax[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        arcmin[k] = min3i(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]);
-        arcmax[k] = max3i(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]);
+        arcmin[k] = hmin3(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]);
+        arcmax[k] = hmax3(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]);
     }
-    int A = max3i(arcmin[0], arcmin[1], arcmin[2]), Bm = min3i(arcmax[0], arcmax[1], arcmax[2]);
+    half2_t A = hmax3(arcmin[0], arcmin[1], arcmin[2]), Bm = hmin3(arcmax[0], arcmax[1], arcmax[2]);
 #pragma unroll
     for (int k = 3; k < 15; k += 2) {
-        A = max3i(A, arcmin[k], arcmin[k + 1]);
-        Bm = min3i(Bm, arcmax[k], arcmax[k + 1]);
+        A = hmax3(A, arcmin[k], arcmin[k + 1]);
+        Bm = hmin3(Bm, arcmax[k], arcmax[k + 1]);
     }
-    A = max(A, arcmin[15]);
-    Bm = min(Bm, arcmax[15]);
-    const int S = max(A, -Bm);
-    return S < 0 ? 0 : S;
+    A = __builtin_elementwise_maximum(A, arcmin[15]);
+    Bm = __builtin_elementwise_minimum(Bm, arcmax[15]);
+    const half2_t S = __builtin_elementwise_maximum(A, -Bm);
+    const int a0 = (int)S.x, a1 = (int)S.y;
+    *s0 = a0 < 0 ? 0 : a0;
+    *s1 = a1 < 0 ? 0 : a1;
 }
 
 // One workgroup per cell. (a) ROI -> LDS; (b) S for the inner pixels (the 3-pixel ring stays 0: cv::FAST on the
@@ -229,9 +276,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geom* __restrict__ g, 
     const int f = blockIdx.y;
     const LevelGeom& L = g->L[c.level];
     const int roi_cap = ((g->roi_max_rows * g->roi_max_cols) + 15) & ~15;
-    uint8_t* im = smem;
+    uint8_t* im = smem;                                                        // NMS peaks (phase c)
     uint8_t* S = smem + roi_cap;
-    int* scr = reinterpret_cast<int*>(smem + 2 * roi_cap);
+    half2_t* hp = reinterpret_cast<half2_t*>(smem + 2 * roi_cap);                // pixel pairs
+    int* scr = reinterpret_cast<int*>(smem + 2 * roi_cap + 4 * (size_t)g->roi_max_rows * g->roi_max_cols);
     const int tid = threadIdx.x;
     int pitch;
     const uint8_t* lev = level_ptr(g, s, f, c.level, &pitch);
@@ -243,7 +291,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geom* __restrict__ g, 
         int r = tid / cols, cc = tid - r * cols;
         const uint8_t* src = lev + (size_t)c.y0 * pitch + c.x0;
         for (int i = tid; i < npx; i += 256) {
-            im[i] = src[(size_t)r * pitch + cc];
+            const uint8_t* q = src + (size_t)r * pitch + cc;
+            half2_t h;
+            h.x = (_Float16)(int)q[0];
+            h.y = cc + 1 < cols ? (_Float16)(int)q[1] : (_Float16)0;
+            hp[i] = h;
             S[i] = 0;
             r += dq;
             cc += dr;
@@ -253,14 +305,20 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geom* __restrict__ g, 
     __syncthreads();
     const int bh = rows - 6, bw = cols - 6;
     const int nb = (bh > 0 && bw > 0) ? bh * bw : 0;
+    const int pw = (bw + 1) >> 1;   // pixel pairs per inner row
     if (nb > 0) {
-        const int dq = 256 / bw, dr = 256 - dq * bw;
-        int r = 3 + tid / bw, cc = 3 + tid % bw;
-        for (int i = tid; i < nb; i += 256) {
-            S[r * cols + cc] = (uint8_t)fast_strength(im, cols, r, cc);
+        const int np = bh * pw;
+        const int dq = 256 / pw, dr = 256 - dq * pw;
+        int r = 3 + tid / pw, pc = tid % pw;
+        for (int i = tid; i < np; i += 256) {
+            const int cc = 3 + 2 * pc;
+            int s0, s1;
+            fast_strength2(hp, cols, r, cc, &s0, &s1);
+            S[r * cols + cc] = (uint8_t)s0;
+            if (2 * pc + 1 < bw) S[r * cols + cc + 1] = (uint8_t)s1;
             r += dq;
-            cc += dr;
-            if (cc >= bw + 3) { cc -= bw; r++; }
+            pc += dr;
+            if (pc >= pw) { pc -= pw; r++; }
         }
     }
     __syncthreads();
