@@ -12,9 +12,10 @@
 //              sort by index -> cell-major index list with ascending idx per cell = AssignFeaturesToGrid's cell
 //              vectors, plus the (x, y, octave) of each entry in that order for coalesced window scans.
 //   k_gather   one wave per search unit (MapPoint / last-frame entry): window cells enumerated ix -> iy -> cell
-//              order exactly as GetFeaturesInArea, level + radius filters, Hamming distance (4x popcount64);
-//              COUNT pass, per-frame scan, FILL pass into a per-frame candidate pool (entry = idx | dist<<16 |
-//              level<<25, in enumeration order).
+//              order exactly as GetFeaturesInArea, level + radius filters, Hamming distance (4x popcount64),
+//              only the candidates that can change a result kept (dist <= TH_HIGH, or <= TH_HIGH / nnratio for the
+//              ratio test), written in enumeration order to a per-unit slot (entry = idx | dist<<16 | level<<25),
+//              longer lists to a per-frame overflow area.
 //   k_resolve  per frame, one workgroup: the reference's sequential greedy loop replayed exactly as dependency
 //              rounds — a unit resolves once every earlier unit sharing a candidate keypoint has; units ready in
 //              the same round have disjoint candidates and commit in parallel. Then the rotation-histogram pass.
@@ -59,7 +60,9 @@ struct ProjArgs {
     int32_t* cand_off;        // [F][unit_stride]
     uint32_t* pool;           // [F][pool_per_frame]
     int32_t* pool_total;      // [F]
-    int pool_per_frame;
+    int pool_per_frame;       // unit_stride * slot_cap + ovf_cap
+    int slot_cap;             // candidate slots per unit
+    int ovf_cap;              // per-frame overflow area for longer lists (pool_total = used)
     uint32_t* events;         // [F][unit_stride]
     int pool_lds;             // candidate entries the resolve stage stages in LDS
     int32_t* out;             // [F][kp_stride]
@@ -249,20 +252,19 @@ __device__ bool unit_window(const ProjArgs& p, int f, int j, Window* w) {
     return true;
 }
 
-template <bool FILL>
-__global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
-    const long long gw = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
-    const int f = (int)(gw / p.unit_stride);
-    const int j = (int)(gw - (long long)f * p.unit_stride);
-    if (f >= nframes) return;
+// A candidate is RELEVANT to its unit if its taken state can change the unit's result: dist <= TH_HIGH (it could
+// be the pick) or, in the ratio-tested local search, dist <= TH_HIGH / nnratio (it could be the second best that
+// fails the test). Irrelevant candidates never change a result (nor any other unit's), so only relevant ones are
+// kept, in GetFeaturesInArea enumeration order.
+__device__ __forceinline__ int rel_threshold(const ProjArgs& p) {
+    return p.mode == 1 ? MAM_TH_HIGH
+                       : (p.nnratio > 0.f ? min(256, (int)ceilf((float)MAM_TH_HIGH / p.nnratio) + 1) : 256);
+}
+
+// One pass over a unit's window: lanes own window cells (ix -> iy order), count their relevant candidates, a wave
+// scan places them; entries at positions < lim are written to dst. Returns the relevant count.
+__device__ int gather_pass(const ProjArgs& p, int f, const Window& w, int rel, uint32_t* dst, int lim) {
     const int lane = lane_id();
-    Window w;
-    const bool ok = unit_window(p, f, j, &w);
-    if (!ok) {
-        if (!FILL && lane == 0) p.cand_cnt[(size_t)f * p.unit_stride + j] = 0;
-        return;
-    }
-    if (FILL && p.pool_total[f] > p.pool_per_frame) return;
     const int ny = w.cy1 - w.cy0 + 1;
     const int ncell = (w.cx1 - w.cx0 + 1) * ny;
     const int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
@@ -270,9 +272,7 @@ __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
     const float2* gxy = p.grid_xy + (size_t)f * p.fr.kp_stride;
     const uint8_t* gct = p.grid_oct + (size_t)f * p.fr.kp_stride;
     const uint8_t* D = p.fr.desc + (size_t)f * p.fr.kp_stride * 32;
-    uint32_t* pool = p.pool + (size_t)f * p.pool_per_frame;
-    int base = FILL ? p.cand_off[(size_t)f * p.unit_stride + j] : 0;
-    int total = 0;
+    int base = 0;
     for (int e0 = 0; e0 < ncell; e0 += 64) {
         const int e = e0 + lane;
         int cnt = 0, k0 = 0, k1 = 0;
@@ -289,59 +289,64 @@ __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
                 }
                 const float2 xy = gxy[k];
                 const float dx = xy.x - w.x, dy = xy.y - w.y;
-                if (fabsf(dx) < w.r && fabsf(dy) < w.r) cnt++;
+                if (fabsf(dx) < w.r && fabsf(dy) < w.r && desc_dist(w.desc, D + (size_t)gi[k] * 32) <= rel) cnt++;
             }
         }
-        if (FILL) {
-            const int incl = wave_incl_scan(cnt);
-            int o = base + incl - cnt;
-            if (cnt > 0) {
-                for (int k = k0; k < k1; k++) {
-                    const int oct = gct[k];
-                    if (w.checkL) {
-                        if (oct < w.minL) continue;
-                        if (w.maxL >= 0 && oct > w.maxL) continue;
-                    }
-                    const float2 xy = gxy[k];
-                    const float dx = xy.x - w.x, dy = xy.y - w.y;
-                    if (fabsf(dx) < w.r && fabsf(dy) < w.r) {
-                        const int idx = gi[k];
-                        const int dist = desc_dist(w.desc, D + (size_t)idx * 32);
-                        pool[o++] = (uint32_t)idx | ((uint32_t)dist << 16) | ((uint32_t)oct << 25);
-                    }
+        const int incl = wave_incl_scan(cnt);
+        int o = base + incl - cnt;
+        if (cnt > 0 && o < lim) {
+            for (int k = k0; k < k1 && o < lim; k++) {
+                const int oct = gct[k];
+                if (w.checkL) {
+                    if (oct < w.minL) continue;
+                    if (w.maxL >= 0 && oct > w.maxL) continue;
+                }
+                const float2 xy = gxy[k];
+                const float dx = xy.x - w.x, dy = xy.y - w.y;
+                if (fabsf(dx) < w.r && fabsf(dy) < w.r) {
+                    const int idx = gi[k];
+                    const int dist = desc_dist(w.desc, D + (size_t)idx * 32);
+                    if (dist <= rel) dst[o++] = (uint32_t)idx | ((uint32_t)dist << 16) | ((uint32_t)oct << 25);
                 }
             }
-            base += __shfl(incl, 63, 64);
-        } else {
-            total += wave_sum(cnt);
         }
+        base += __shfl(incl, 63, 64);
     }
-    if (!FILL && lane == 0) p.cand_cnt[(size_t)f * p.unit_stride + j] = total;
+    return base;
 }
 
-__global__ __launch_bounds__(256) void k_scan(ProjArgs p) {
-    __shared__ int scr[4];
-    const int f = blockIdx.x, tid = threadIdx.x;
-    const int nu = p.n_units[f];
-    const int32_t* cc = p.cand_cnt + (size_t)f * p.unit_stride;
-    int32_t* co = p.cand_off + (size_t)f * p.unit_stride;
-    int carry = 0;
-    for (int j0 = 0; j0 < nu; j0 += 256) {
-        const int j = j0 + tid;
-        const int v = j < nu ? cc[j] : 0;
-        const int incl = wave_incl_scan(v);
-        if (lane_id() == 63) scr[tid >> 6] = incl;
-        __syncthreads();
-        int pre = 0, tot = 0;
-        for (int i = 0; i < 4; i++) {
-            if (i < (tid >> 6)) pre += scr[i];
-            tot += scr[i];
-        }
-        __syncthreads();
-        if (j < nu) co[j] = carry + pre + incl - v;
-        carry += tot;
+// One wave per unit. Lists go to a fixed slot of slot_cap entries per unit; a longer list is written again into
+// the frame's overflow area (atomic allocation; the list stays contiguous and in order).
+__global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
+    const long long gw = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int f = (int)(gw / p.unit_stride);
+    const int j = (int)(gw - (long long)f * p.unit_stride);
+    if (f >= nframes) return;
+    const int lane = lane_id();
+    int32_t* cntp = p.cand_cnt + (size_t)f * p.unit_stride + j;
+    int32_t* offp = p.cand_off + (size_t)f * p.unit_stride + j;
+    Window w;
+    if (!unit_window(p, f, j, &w)) {
+        if (lane == 0) { *cntp = 0; *offp = 0; }
+        return;
     }
-    if (tid == 0) p.pool_total[f] = carry;
+    uint32_t* fpool = p.pool + (size_t)f * p.pool_per_frame;
+    const int rel = rel_threshold(p);
+    const int CAP = p.slot_cap;
+    int total = gather_pass(p, f, w, rel, fpool + (size_t)j * CAP, CAP);
+    int off = j * CAP;
+    if (total > CAP) {
+        int o2 = 0;
+        if (lane == 0) o2 = atomicAdd(&p.pool_total[f], total);
+        o2 = __shfl(o2, 0, 64);
+        if (o2 + total <= p.ovf_cap) {
+            off = p.unit_stride * CAP + o2;
+            gather_pass(p, f, w, rel, fpool + off, total);
+        } else {
+            total = 0;   // capacity: pool_total > ovf_cap makes the resolve stage report the frame
+        }
+    }
+    if (lane == 0) { *cntp = total; *offp = off; }
 }
 
 // ------------------------------------------------------------------------------------------------ resolve
@@ -380,7 +385,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
     const int n = frame_n(p.fr, f);
     int32_t* out = p.out + (size_t)f * S;
     if (p.out_n[f] < 0) return;   // grid stage flagged this frame
-    if (p.pool_total[f] > p.pool_per_frame) {
+    if (p.pool_total[f] > p.ovf_cap) {   // a list did not fit its slot nor the overflow area
         if (t == 0) p.out_n[f] = MAM_ERR_CAPACITY;
         return;
     }
@@ -714,7 +719,7 @@ struct mam_match_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     mam::StageTimer timer{4};
-    int pool_per_unit = 96;
+    int slot_cap = 32;        // candidate slots per unit (grows x4 when a host call overflows)
     size_t resolve_lds_max = 64 * 1024;
     // scratch
     DevBuf<uint16_t> grid_idx;
@@ -733,6 +738,12 @@ T* carve(uint8_t*& p, size_t count) {
     T* r = reinterpret_cast<T*>(p);
     p += (count * sizeof(T) + 255) & ~(size_t)255;
     return r;
+}
+
+void set_pool(mam_match_ctx* c, mam::ProjArgs& a, int unit_stride) {
+    a.slot_cap = c->slot_cap;
+    a.ovf_cap = std::max(unit_stride * c->slot_cap / 2, 1 << 16);
+    a.pool_per_frame = unit_stride * a.slot_cap + a.ovf_cap;
 }
 
 size_t carve_bytes(size_t count, size_t elem) { return (count * elem + 255) & ~(size_t)255; }
@@ -773,9 +784,8 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     const int blocks = (int)((waves + 3) / 4);
     {
         mam::StageTimer::Scope sc(&c->timer, s, 1);
-        hipLaunchKernelGGL(mam::k_gather<false>, dim3(blocks), dim3(256), 0, s, a, F);
-        hipLaunchKernelGGL(mam::k_scan, dim3(F), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(mam::k_gather<true>, dim3(blocks), dim3(256), 0, s, a, F);
+        MAM_HIP(hipMemsetAsync(a.pool_total, 0, sizeof(int32_t) * F, s));
+        hipLaunchKernelGGL(mam::k_gather, dim3(blocks), dim3(256), 0, s, a, F);
     }
     {
         mam::StageTimer::Scope sc(&c->timer, s, 2);
@@ -866,7 +876,7 @@ int mam_search_by_projection_batch_device(mam_match_ctx* c, const mam_frame_geom
     a.th_far = th_far_points;
     a.nnratio = nnratio;
     a.far_points = far_points;
-    a.pool_per_frame = std::max(mp_stride * c->pool_per_unit, 1 << 16);
+    set_pool(c, a, mp_stride);
     a.out = out;
     a.out_n = out_n;
     return launch_projection(c, a, fr->nframes, stream ? (hipStream_t)stream : c->stream);
@@ -890,7 +900,7 @@ int mam_search_by_projection_motion_batch_device(mam_match_ctx* c, const mam_fra
     a.last = last;
     a.th = th;
     a.check_ori = check_ori;
-    a.pool_per_frame = std::max(last_stride * c->pool_per_unit, 1 << 16);
+    set_pool(c, a, last_stride);
     a.out = out;
     a.out_n = out_n;
     return launch_projection(c, a, fr->nframes, stream ? (hipStream_t)stream : c->stream);
@@ -954,7 +964,7 @@ int mam_search_by_projection(mam_match_ctx* c, const mam_frame_geom* g, int n, c
         MAM_HIP(hipMemcpyAsync(&nm, dn, 4, hipMemcpyDeviceToHost, c->stream));
         if (n > 0) MAM_HIP(hipMemcpyAsync(out, dout, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
         MAM_HIP(hipStreamSynchronize(c->stream));
-        if (nm == MAM_ERR_CAPACITY && c->pool_per_unit < (1 << 14)) { c->pool_per_unit *= 4; continue; }
+        if (nm == MAM_ERR_CAPACITY && c->slot_cap < (1 << 12)) { c->slot_cap *= 4; continue; }
         return nm;
     }
     return MAM_ERR_CAPACITY;
@@ -994,7 +1004,7 @@ int mam_search_by_projection_motion(mam_match_ctx* c, const mam_frame_geom* g, i
         MAM_HIP(hipMemcpyAsync(&nm, dn, 4, hipMemcpyDeviceToHost, c->stream));
         if (n > 0) MAM_HIP(hipMemcpyAsync(out, dout, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
         MAM_HIP(hipStreamSynchronize(c->stream));
-        if (nm == MAM_ERR_CAPACITY && c->pool_per_unit < (1 << 14)) { c->pool_per_unit *= 4; continue; }
+        if (nm == MAM_ERR_CAPACITY && c->slot_cap < (1 << 12)) { c->slot_cap *= 4; continue; }
         return nm;
     }
     return MAM_ERR_CAPACITY;
