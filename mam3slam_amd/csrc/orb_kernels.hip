@@ -846,17 +846,24 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, Le
     int pitch;
     const uint8_t* lev = level_ptr(g, s, f, l, &pitch);
     const uint8_t* center = lev + (size_t)y * pitch + x;
+    // lane = (column u, half): the disk column u spans |v| <= vmax(u) (umax decreases with |v|), lanes 0..30 take
+    // v in [-vmax, 0], lanes 32..62 take v in [1, vmax]; integer sums are order-independent
     int m10 = 0, m01 = 0;
-    if (lane < 31) {
-        const int u = lane - 15;
-        const int au = u < 0 ? -u : u;
-        for (int v = -15; v <= 15; v++) {
-            const int av = v < 0 ? -v : v;
-            if (au <= g->umax[av]) {
-                const int val = center[v * pitch + u];
-                m10 += u * val;
+    {
+        const int col = lane & 31;
+        if (col < 31) {
+            const int u = col - 15;
+            const int au = u < 0 ? -u : u;
+            int vmax = 0;
+            while (vmax < 15 && au <= g->umax[vmax + 1]) vmax++;
+            const int v0 = lane < 32 ? -vmax : 1, v1 = lane < 32 ? 0 : vmax;
+            const uint8_t* cp = center + u;
+            for (int v = v0; v <= v1; v++) {
+                const int val = cp[v * pitch];
+                m10 += val;
                 m01 += v * val;
             }
+            m10 *= u;
         }
     }
     m10 = wave_sum(m10);
