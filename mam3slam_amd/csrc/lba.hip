@@ -52,11 +52,9 @@ struct Dev {
     const int32_t* pe_idx;
     const int32_t* qe_off;       // per Hessian pose: edges
     const int32_t* qe_idx;
-    const int32_t* bp_off;       // per S block pair: contributions
-    const int32_t* bp_ea;
-    const int32_t* bp_ec;
-    const int32_t* bp_ij;        // (i1, i2) per block pair
+    const int32_t* bp_ij;        // (i1 <= i2) per block of the upper triangle of S, row-major
     int nbp;
+    int32_t* eidx;               // [Np][L] edge of (pose block, Hessian point), -1 if none
     int npad;                    // padded dimension of S (ldlt_pad(6 Np))
     double* ws;                  // global LDL^T workspace when it does not fit in LDS
     double delta;
@@ -282,15 +280,27 @@ __global__ __launch_bounds__(256) void k_schur_edge(Dev d) {
     }
 }
 
+__global__ __launch_bounds__(256) void k_eidx(Dev d) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= d.E) return;
+    const int hp = d.pose_h[d.edge_pose[e]];
+    if (hp >= 0) d.eidx[(size_t)hp * d.L + d.point_h[d.edge_point[e]]] = e;
+}
+
 __global__ __launch_bounds__(64) void k_schur_blk(Dev d, double lambda) {
     const int bp = blockIdx.x, lane = threadIdx.x;
     const int i1 = d.bp_ij[2 * bp], i2 = d.bp_ij[2 * bp + 1];
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
-    for (int s = d.bp_off[bp] + lane; s < d.bp_off[bp + 1]; s += 64) {
-        const double* W = d.bdinv + 18 * (size_t)d.bp_ea[s];
-        const double* B = d.hpl + 18 * (size_t)d.bp_ec[s];
+    // landmarks seen by both poses: walk pose i2's edges, look up pose i1's edge of the same landmark
+    const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
+    for (int s = d.qe_off[i2] + lane; s < d.qe_off[i2 + 1]; s += 64) {
+        const int ec = d.qe_idx[s];
+        const int ea = ei1[d.point_h[d.edge_point[ec]]];
+        if (ea < 0) continue;
+        const double* W = d.bdinv + 18 * (size_t)ea;
+        const double* B = d.hpl + 18 * (size_t)ec;
         double w[18], b[18];
 #pragma unroll
         for (int k = 0; k < 18; k++) { w[k] = W[k]; b[k] = B[k]; }
@@ -814,62 +824,17 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     }
     // S block pairs (i1 <= i2, row-major; diagonal blocks always present) with their contributions in landmark
     // (Hessian point) order, then edge order within the landmark
-    // per landmark, its optimised-pose edges as (pose block, edge) in edge order: the pair loops below then run
-    // over small contiguous arrays
-    std::vector<int32_t> le_off(L + 1, 0), le_h, le_e;
-    le_h.reserve(E);
-    le_e.reserve(E);
-    for (int h = 0; h < L; h++) {
-        for (int sa = pe_off[h]; sa < pe_off[h + 1]; sa++) {
-            const int e = pe_idx[sa], hp = pose_h[p->edge_pose[e]];
-            if (hp < 0) continue;
-            le_h.push_back(hp);
-            le_e.push_back(e);
-        }
-        le_off[h + 1] = (int32_t)le_h.size();
-    }
-    std::vector<int32_t> bcnt((size_t)Np * Np, 0);
-    for (int h = 0; h < L; h++) {
-        const int32_t* hs = le_h.data() + le_off[h];
-        const int cnt = le_off[h + 1] - le_off[h];
-        for (int a = 0; a < cnt; a++) {
-            int32_t* rowc = bcnt.data() + (size_t)hs[a] * Np;
-            for (int c = 0; c < cnt; c++)
-                if (hs[c] >= hs[a]) rowc[hs[c]]++;
-        }
-    }
-    std::vector<int32_t> bslot((size_t)Np * Np, -1), bp_off(1, 0), bp_ij;
+    // every block of the upper triangle of S (g2o keeps only the non-empty ones; the empty ones are zero here)
+    std::vector<int32_t> bp_ij;
+    bp_ij.reserve((size_t)Np * (Np + 1));
     for (int a = 0; a < Np; a++)
-        for (int b = a; b < Np; b++) {
-            const int32_t cnt = bcnt[(size_t)a * Np + b];
-            if (cnt == 0 && a != b) continue;
-            bslot[(size_t)a * Np + b] = bp_off.back();
-            bp_off.push_back(bp_off.back() + cnt);
-            bp_ij.push_back(a);
-            bp_ij.push_back(b);
-        }
+        for (int b = a; b < Np; b++) { bp_ij.push_back(a); bp_ij.push_back(b); }
     const int nbp = (int)bp_ij.size() / 2;
-    std::vector<int32_t> bp_ea(bp_off.back()), bp_ec(bp_off.back());
-    for (int h = 0; h < L; h++) {
-        const int32_t* hs = le_h.data() + le_off[h];
-        const int32_t* es = le_e.data() + le_off[h];
-        const int cnt = le_off[h + 1] - le_off[h];
-        for (int a = 0; a < cnt; a++) {
-            int32_t* rows = bslot.data() + (size_t)hs[a] * Np;
-            for (int c = 0; c < cnt; c++) {
-                if (hs[c] < hs[a]) continue;
-                const int32_t pos = rows[hs[c]]++;
-                bp_ea[pos] = es[a];
-                bp_ec[pos] = es[c];
-            }
-        }
-    }
     const int n = 6 * Np, nx = 6 * Np + 3 * L, npad = mam::lba::ldlt_pad(n);
-    const size_t nbpc = bp_ea.size();
     // ---- device arena: the uploaded inputs first (mirrored in pinned host memory, one copy), scratch after
     size_t bytes = sz<int32_t>(E) * 2 + sz<double>(2 * (size_t)E) + sz<double>(E) + sz<float>(4 * (size_t)p->n_cams) +
                    sz<int32_t>(P) * 2 + sz<int32_t>(Np) + sz<int32_t>(L) * 2 + sz<int32_t>(L + 1) + sz<int32_t>(E) +
-                   sz<int32_t>(Np + 1) + sz<int32_t>(E) + sz<int32_t>(nbp + 1) + sz<int32_t>(nbpc) * 2 +
+                   sz<int32_t>(Np + 1) + sz<int32_t>(E) + sz<int32_t>((size_t)Np * L) +
                    sz<int32_t>(2 * (size_t)nbp) + 2 * sz<double>(7 * (size_t)P) + 2 * sz<double>(3 * (size_t)L) +
                    sz<double>(2 * (size_t)E) + sz<double>(21 * (size_t)E) + sz<double>(E) + sz<double>(18 * (size_t)E) * 2 +
                    sz<double>(6 * (size_t)E) + sz<double>(36 * (size_t)Np) + sz<double>(9 * (size_t)L) + sz<double>(nx) +
@@ -907,9 +872,6 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     d.pe_idx = put(pe_idx.data(), E);
     d.qe_off = put(qe_off.data(), Np + 1);
     d.qe_idx = put(qe_idx.data(), qe_idx.size());
-    d.bp_off = put(bp_off.data(), nbp + 1);
-    d.bp_ea = put(bp_ea.data(), nbpc);
-    d.bp_ec = put(bp_ec.data(), nbpc);
     d.bp_ij = put(bp_ij.data(), 2 * (size_t)nbp);
     // state: poses packed [q t], SE3Quat(q, t) normalises on construction
     std::vector<double> pose0(7 * (size_t)P);
@@ -927,6 +889,11 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     const auto h_t1 = std::chrono::steady_clock::now();
 #endif
     MAM_HIP(hipMemcpyAsync(c->arena.p, host_base, upload, hipMemcpyHostToDevice, s));
+    d.eidx = cv.take<int32_t>((size_t)Np * L);
+    if ((size_t)Np * L > 0) {
+        MAM_HIP(hipMemsetAsync(d.eidx, 0xFF, sizeof(int32_t) * (size_t)Np * L, s));
+        if (E > 0) hipLaunchKernelGGL(mam::lba::k_eidx, dim3((E + 255) / 256), dim3(256), 0, s, d);
+    }
     double* poseB = cv.take<double>(7 * (size_t)P);
     double* ptB = cv.take<double>(3 * (size_t)L);
     d.err = cv.take<double>(2 * (size_t)E);
