@@ -376,6 +376,102 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
+// wave 0: LDL^T of the 16x16 diagonal block at kb (final on entry), written back to A (L below, D on the diagonal),
+// plus Ld (L11, row-major), dk / invdk (D and 1/D) for the panel rows, and the forward block solve of y.
+// Right-looking inside the block: at step j the pivot d_j is lane j's current diagonal, column j is scaled
+// (l_ij = a_ij / d_j) and broadcast by v_readlane, and every lane i > j updates a_ik -= l_ij d_j l_kj, j < k <= i.
+__device__ __forceinline__ void ldlt_diag(double* A, int N, int kb, double* Y, double* Ld, double* dk, double* invdk,
+                                          int* fail, int lane) {
+    double row[NB];
+#pragma unroll
+    for (int c = 0; c < NB; c++) row[c] = lane < NB ? A[(size_t)(kb + lane) * N + kb + c] : 0.0;
+    double dmine = 1.0;
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        const double dj = readlane_d(row[j], j);
+        if (lane == j) dmine = dj;
+        const double inv = dj != 0.0 ? 1.0 / dj : 0.0;
+        const double l = row[j] * inv;
+        if (lane > j) row[j] = l;
+        const double ldj = l * dj;
+#pragma unroll
+        for (int k = j + 1; k < NB; k++) {
+            const double lk = readlane_d(l, k);
+            if (k <= lane) row[k] -= ldj * lk;
+        }
+    }
+    double yv = lane < NB ? Y[kb + lane] : 0.0;
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        const double yj = readlane_d(yv, j);
+        if (lane > j) yv -= row[j] * yj;
+    }
+    if (lane < NB) {
+#pragma unroll
+        for (int c = 0; c < NB; c++) {
+            Ld[lane * NB + c] = row[c];
+            if (c < lane) A[(size_t)(kb + lane) * N + kb + c] = row[c];
+        }
+        A[(size_t)(kb + lane) * N + kb + lane] = dmine;
+        dk[lane] = dmine;
+        invdk[lane] = dmine != 0.0 ? 1.0 / dmine : 0.0;
+        Y[kb + lane] = yv;
+        if (dmine == 0.0) *fail = 1;
+    }
+}
+
+// A22 tile (tr, tc) (4x4, relative to row/col kb + NB) -= L21 W21^T over the panel staged in PL / PW
+__device__ __forceinline__ void ldlt_tile(double* A, int N, int kb, const double* PL, const double* PW, int m, int tr,
+                                          int tc) {
+    const int r0 = kb + NB + 4 * tr, c0 = kb + NB + 4 * tc;
+    double a4[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        const double2* ap = reinterpret_cast<const double2*>(A + (size_t)(r0 + a) * N + c0);
+        const double2 x01 = ap[0], x23 = ap[1];
+        a4[a][0] = x01.x; a4[a][1] = x01.y; a4[a][2] = x23.x; a4[a][3] = x23.y;
+    }
+    double acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < NB; k++) {
+        const double2* pl = reinterpret_cast<const double2*>(PL + (size_t)k * m + 4 * tr);
+        const double2* pw = reinterpret_cast<const double2*>(PW + (size_t)k * m + 4 * tc);
+        const double2 l01 = pl[0], l23 = pl[1], w01 = pw[0], w23 = pw[1];
+        const double lr[4] = {l01.x, l01.y, l23.x, l23.y}, wc[4] = {w01.x, w01.y, w23.x, w23.y};
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[a][b] += lr[a] * wc[b];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        double2* ap = reinterpret_cast<double2*>(A + (size_t)(r0 + a) * N + c0);
+        if (tr != tc) {
+            ap[0] = make_double2(a4[a][0] - acc[a][0], a4[a][1] - acc[a][1]);
+            ap[1] = make_double2(a4[a][2] - acc[a][2], a4[a][3] - acc[a][3]);
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if (b <= a) A[(size_t)(r0 + a) * N + c0 + b] = a4[a][b] - acc[a][b];
+        }
+    }
+}
+
+// triangle index q -> (tr, tc), tc <= tr
+__device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
+    int r = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+    while (r * (r + 1) / 2 > q) r--;
+    while ((r + 1) * (r + 2) / 2 <= q) r++;
+    *tr = r;
+    *tc = q - r * (r + 1) / 2;
+}
+
+// With lookahead: after a panel's rows (B), the next block column is updated first (C1); then wave 0 factors the
+// next diagonal block while the other waves update the rest of the trailing matrix (C2).
 template <bool use_lds>
 __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
     extern __shared__ __attribute__((aligned(16))) double lds_ws[];
@@ -387,7 +483,6 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
     __shared__ double Ld[NB * NB];
     __shared__ double dk[NB];
     __shared__ double invdk[NB];
-    __shared__ double colb[64];
     __shared__ int fail;
     if (t == 0) fail = 0;
     for (int i = t; i < N; i += LDLT_THREADS) {
@@ -401,56 +496,11 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
 #else
 #define LDLT_PHASE(k) do {} while (0)
 #endif
+    if (wid == 0) ldlt_diag(A, N, 0, Y, Ld, dk, invdk, &fail, lane);
+    __syncthreads();
+    LDLT_PHASE(0);
     for (int kb = 0; kb < N; kb += NB) {
-        // (1) diagonal block + forward block solve (wave 0). Right-looking inside the block: at step j the pivot
-        // d_j is lane j's current diagonal, column j is scaled (l_ij = a_ij / d_j) and broadcast through LDS, and
-        // every lane i > j updates its row: a_ik -= l_ij d_j l_kj for j < k <= i.
-        if (wid == 0) {
-            double row[NB];
-#pragma unroll
-            for (int c = 0; c < NB; c++) row[c] = lane < NB ? A[(size_t)(kb + lane) * N + kb + c] : 0.0;
-            double dmine = 1.0;
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const double dj = readlane_d(row[j], j);
-                if (lane == j) dmine = dj;
-                const double inv = dj != 0.0 ? 1.0 / dj : 0.0;
-                const double l = row[j] * inv;
-                if (lane > j) row[j] = l;
-                colb[lane] = l;   // lanes <= j write values nobody reads
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const double ldj = l * dj;
-#pragma unroll
-                for (int k = j + 1; k < NB; k++)
-                    if (k <= lane) row[k] -= ldj * colb[k];
-                __builtin_amdgcn_wave_barrier();
-            }
-            // forward block solve (unit lower) on y1
-            double yv = lane < NB ? Y[kb + lane] : 0.0;
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const double yj = readlane_d(yv, j);
-                if (lane > j) yv -= row[j] * yj;
-            }
-            if (lane < NB) {
-#pragma unroll
-                for (int c = 0; c < NB; c++) Ld[lane * NB + c] = row[c];
-                dk[lane] = dmine;
-                invdk[lane] = dmine != 0.0 ? 1.0 / dmine : 0.0;
-                Y[kb + lane] = yv;
-                if (dmine == 0.0) fail = 1;
-            }
-        }
-        __syncthreads();
-        LDLT_PHASE(0);
-        for (int i = t; i < NB * NB; i += LDLT_THREADS) {
-            const int r = i / NB, c = i % NB;
-            if (r > c) A[(size_t)(kb + r) * N + kb + c] = Ld[r * NB + c];
-            else if (r == c) A[(size_t)(kb + r) * N + kb + c] = dk[r];
-        }
-        // (2) panel rows (+ forward-substitution update)
+        // (B) panel rows: L21 = A21 L11^-T D^-1, W21 = L21 D (staged transposed), y2 -= L21 y1
         const int m = N - kb - NB;
         double* PL = ws;
         double* PW = ws + (size_t)NB * m;
@@ -478,53 +528,31 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
         }
         __syncthreads();
         LDLT_PHASE(1);
-        // (3) trailing update over the lower triangle of the m x m trailing block
+        if (m == 0) break;
         const int T = m / 4;
-        const int ntile = T * (T + 1) / 2;
-        for (int q = t; q < ntile; q += LDLT_THREADS) {
-            int tr = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
-            while (tr * (tr + 1) / 2 > q) tr--;
-            while ((tr + 1) * (tr + 2) / 2 <= q) tr++;
-            const int tc = q - tr * (tr + 1) / 2;
-            const int r0 = kb + NB + 4 * tr, c0 = kb + NB + 4 * tc;
-            double a4[4][4];
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const double2* ap = reinterpret_cast<const double2*>(A + (size_t)(r0 + a) * N + c0);
-                const double2 x01 = ap[0], x23 = ap[1];
-                a4[a][0] = x01.x; a4[a][1] = x01.y; a4[a][2] = x23.x; a4[a][3] = x23.y;
-            }
-            double acc[4][4];
-#pragma unroll
-            for (int a = 0; a < 4; a++)
-#pragma unroll
-                for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
-#pragma unroll 4
-            for (int k = 0; k < NB; k++) {
-                const double2* pl = reinterpret_cast<const double2*>(PL + (size_t)k * m + 4 * tr);
-                const double2* pw = reinterpret_cast<const double2*>(PW + (size_t)k * m + 4 * tc);
-                const double2 l01 = pl[0], l23 = pl[1], w01 = pw[0], w23 = pw[1];
-                const double lr[4] = {l01.x, l01.y, l23.x, l23.y}, wc[4] = {w01.x, w01.y, w23.x, w23.y};
-#pragma unroll
-                for (int a = 0; a < 4; a++)
-#pragma unroll
-                    for (int b = 0; b < 4; b++) acc[a][b] += lr[a] * wc[b];
-            }
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                double2* ap = reinterpret_cast<double2*>(A + (size_t)(r0 + a) * N + c0);
-                if (tr != tc) {
-                    ap[0] = make_double2(a4[a][0] - acc[a][0], a4[a][1] - acc[a][1]);
-                    ap[1] = make_double2(a4[a][2] - acc[a][2], a4[a][3] - acc[a][3]);
-                } else {
-#pragma unroll
-                    for (int b = 0; b < 4; b++)
-                        if (b <= a) A[(size_t)(r0 + a) * N + c0 + b] = a4[a][b] - acc[a][b];
-                }
-            }
+        // (C1) the next block column: tiles with tc < 4, enumerated column by column
+        const int n1 = 4 * T - 6;
+        for (int q = t; q < n1; q += LDLT_THREADS) {
+            int tc = 0, qq = q;
+            while (qq >= T - tc) { qq -= T - tc; tc++; }
+            ldlt_tile(A, N, kb, PL, PW, m, tc + qq, tc);
         }
         __syncthreads();
         LDLT_PHASE(2);
+        // (C2) wave 0 factors the next diagonal block; the other waves update the tiles with tc >= 4
+        if (wid == 0) {
+            ldlt_diag(A, N, kb + NB, Y, Ld, dk, invdk, &fail, lane);
+        } else {
+            const int T2 = T - 4;
+            const int n2 = T2 * (T2 + 1) / 2;
+            for (int q = t - 64; q < n2; q += LDLT_THREADS - 64) {
+                int tr, tc;
+                tri_index(q, &tr, &tc);
+                ldlt_tile(A, N, kb, PL, PW, m, tr + 4, tc + 4);
+            }
+        }
+        __syncthreads();
+        LDLT_PHASE(0);
     }
 #ifdef MAM_LDLT_PROFILE
     if (t == 0) for (int k = 0; k < 3; k++) d.red[4 + k] += (double)tacc[k];
@@ -1041,7 +1069,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         double ph[4];
         MAM_HIP(hipMemcpy(ph, d.red + 4, sizeof(ph), hipMemcpyDeviceToHost));
         const auto h_t2 = std::chrono::steady_clock::now();
-        fprintf(stderr, "ldlt cycles: diag %.0f panel %.0f trailing %.0f subst %.0f (trials %d); host setup %.3f ms, "
+        fprintf(stderr, "ldlt cycles: diag+trailing-rest %.0f panel %.0f next-column %.0f subst %.0f (trials %d); host setup %.3f ms, "
                 "loop %.3f ms\n", ph[0], ph[1], ph[2], ph[3], trials,
                 std::chrono::duration<double, std::milli>(h_t1 - h_t0).count(),
                 std::chrono::duration<double, std::milli>(h_t2 - h_t1).count());
