@@ -350,15 +350,16 @@ __global__ __launch_bounds__(64) void k_schur_rhs(Dev d) {
 //       v_readlane (uniform), and solves the block of the forward substitution L11 y1 = y1;
 //   (2) every thread takes one panel row: L21 = A21 L11^-T D^-1, W21 = L21 D (staged transposed in the panel
 //       workspace for the trailing update) and the fused forward-substitution update y2 -= L21 y1;
-//   (3) the trailing lower triangle A22 -= L21 W21^T in 4x4 register tiles, both operands from the workspace.
+//   (3) the trailing lower triangle A22 -= L21 W21^T in 16x16 blocks, one wave each, as f64 MFMAs
+//       (v_mfma_f64_16x16x4_f64) with both operands from the workspace.
 // An exact zero pivot sets flag[0] (the failure rule of Eigen's SimplicialLDLT) and skips the solve.
 // Then y /= D and the backward substitution L^T x = y, block by block, each thread updating its own y_i.
 // The workspace (panel + y) is LDS when it fits (use_lds), else a global scratch buffer.
 constexpr int NB = 16;
 #ifndef MAM_LDLT_THREADS
-#define MAM_LDLT_THREADS 512
+#define MAM_LDLT_THREADS 1024
 #endif
-constexpr int LDLT_THREADS = MAM_LDLT_THREADS;   // 512: 2 waves per SIMD, 256 registers per lane
+constexpr int LDLT_THREADS = MAM_LDLT_THREADS;   // 16 waves: 4 per SIMD hide the MFMA / memory latency
 
 __host__ __device__ inline int ldlt_pad(int n) { return (n + NB - 1) / NB * NB; }
 
@@ -420,45 +421,27 @@ __device__ __forceinline__ void ldlt_diag(double* A, int N, int kb, double* Y, d
     }
 }
 
-// A22 tile (tr, tc) (4x4, relative to row/col kb + NB) -= L21 W21^T over the panel staged in PL / PW
-__device__ __forceinline__ void ldlt_tile(double* A, int N, int kb, const double* PL, const double* PW, int m, int tr,
-                                          int tc) {
-    const int r0 = kb + NB + 4 * tr, c0 = kb + NB + 4 * tc;
-    double a4[4][4];
+// One wave: the 16x16 block (br, bc) of A22 (block indices relative to row/col kb + NB) -= L21 W21^T as four
+// chained v_mfma_f64_16x16x4_f64 (K = 16), accumulator initialised with the A block. Lane maps (gfx950, f64):
+// A operand L[R0 + (lane&15)][k0 + (lane>>4)], B operand W[C0 + (lane&15)][k0 + (lane>>4)],
+// C/D col = lane&15, row = (lane>>4) + 4 reg.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ldlt_tile16(double* A, int N, int kb, const double* PL, const double* PW, int m, int br,
+                                            int bc, int lane) {
+    const int R0 = kb + NB + 16 * br, C0 = kb + NB + 16 * bc;
+    const int col = lane & 15, rq = lane >> 4;
+    dbl4 c;
 #pragma unroll
-    for (int a = 0; a < 4; a++) {
-        const double2* ap = reinterpret_cast<const double2*>(A + (size_t)(r0 + a) * N + c0);
-        const double2 x01 = ap[0], x23 = ap[1];
-        a4[a][0] = x01.x; a4[a][1] = x01.y; a4[a][2] = x23.x; a4[a][3] = x23.y;
-    }
-    double acc[4][4];
+    for (int r = 0; r < 4; r++) c[r] = A[(size_t)(R0 + rq + 4 * r) * N + C0 + col];
 #pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < NB; k++) {
-        const double2* pl = reinterpret_cast<const double2*>(PL + (size_t)k * m + 4 * tr);
-        const double2* pw = reinterpret_cast<const double2*>(PW + (size_t)k * m + 4 * tc);
-        const double2 l01 = pl[0], l23 = pl[1], w01 = pw[0], w23 = pw[1];
-        const double lr[4] = {l01.x, l01.y, l23.x, l23.y}, wc[4] = {w01.x, w01.y, w23.x, w23.y};
-#pragma unroll
-        for (int a = 0; a < 4; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc[a][b] += lr[a] * wc[b];
+    for (int k0 = 0; k0 < NB; k0 += 4) {
+        const int k = k0 + rq;
+        const double av = -PL[(size_t)k * m + 16 * br + col];
+        const double bv = PW[(size_t)k * m + 16 * bc + col];
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c, 0, 0, 0);
     }
 #pragma unroll
-    for (int a = 0; a < 4; a++) {
-        double2* ap = reinterpret_cast<double2*>(A + (size_t)(r0 + a) * N + c0);
-        if (tr != tc) {
-            ap[0] = make_double2(a4[a][0] - acc[a][0], a4[a][1] - acc[a][1]);
-            ap[1] = make_double2(a4[a][2] - acc[a][2], a4[a][3] - acc[a][3]);
-        } else {
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-                if (b <= a) A[(size_t)(r0 + a) * N + c0 + b] = a4[a][b] - acc[a][b];
-        }
-    }
+    for (int r = 0; r < 4; r++) A[(size_t)(R0 + rq + 4 * r) * N + C0 + col] = c[r];
 }
 
 // triangle index q -> (tr, tc), tc <= tr
@@ -529,26 +512,21 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
         __syncthreads();
         LDLT_PHASE(1);
         if (m == 0) break;
-        const int T = m / 4;
-        // (C1) the next block column: tiles with tc < 4, enumerated column by column
-        const int n1 = 4 * T - 6;
-        for (int q = t; q < n1; q += LDLT_THREADS) {
-            int tc = 0, qq = q;
-            while (qq >= T - tc) { qq -= T - tc; tc++; }
-            ldlt_tile(A, N, kb, PL, PW, m, tc + qq, tc);
-        }
+        const int T16 = m / 16;
+        // (C1) the next block column: blocks (br, 0), one wave each
+        for (int br = wid; br < T16; br += LDLT_THREADS / 64) ldlt_tile16(A, N, kb, PL, PW, m, br, 0, lane);
         __syncthreads();
         LDLT_PHASE(2);
-        // (C2) wave 0 factors the next diagonal block; the other waves update the tiles with tc >= 4
+        // (C2) wave 0 factors the next diagonal block; the other waves update the blocks with bc >= 1
         if (wid == 0) {
             ldlt_diag(A, N, kb + NB, Y, Ld, dk, invdk, &fail, lane);
         } else {
-            const int T2 = T - 4;
+            const int T2 = T16 - 1;
             const int n2 = T2 * (T2 + 1) / 2;
-            for (int q = t - 64; q < n2; q += LDLT_THREADS - 64) {
+            for (int q = wid - 1; q < n2; q += LDLT_THREADS / 64 - 1) {
                 int tr, tc;
                 tri_index(q, &tr, &tc);
-                ldlt_tile(A, N, kb, PL, PW, m, tr + 4, tc + 4);
+                ldlt_tile16(A, N, kb, PL, PW, m, tr + 1, tc + 1, lane);
             }
         }
         __syncthreads();
