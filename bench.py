@@ -310,12 +310,54 @@ def main():
         match()
     torch.cuda.synchronize(dev)
     stages = dict(ext.stage_times())
+
     sm1, sm2 = m_motion.stage_times(), m_local.stage_times()
     for k in ("grid", "gather", "resolve"):
         stages[k] = (sm1[k][0] + sm2[k][0], sm1[k][1] + sm2[k][1])
     for o in (ext, m_motion, m_local):
         o.set_profiling(False)
     lba_stage = lba_solver.stage_times() if lba_solver is not None else None
+    # single-frame latency (B = 1, one HIP graph, synchronised per frame): the per-frame view of the north-star target
+    ext.set_profiling(False)
+    m_motion.set_profiling(False)
+    m_local.set_profiling(False)
+    fr1_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), None)
+    fr2_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), d_taken.data_ptr())
+
+    def one_frame_launch():
+        ext.extract_batch_device(d_img.data_ptr(), 1, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                                 d_cnt.data_ptr(), stream=stream)
+        m_motion.search_motion_batch_device(F0, fr1_1, d_tcw.data_ptr(), cam, d_last.data_ptr(), Ls,
+                                            d_nlast.data_ptr(), 15.0, d_out1.data_ptr(), d_nm1.data_ptr(),
+                                            stream=stream)
+        torch.ge(d_out1[:1], 0, out=d_taken[:1].view(torch.bool))
+        m_local.search_by_projection_batch_device(F0, fr2_1, d_mps.data_ptr(), Ms, d_nmps.data_ptr(), 1.0,
+                                                  d_out2.data_ptr(), d_nm2.data_ptr(), stream=stream)
+
+    one_frame_launch()
+    torch.cuda.synchronize(dev)
+    g1 = None
+    if not args.no_graph:
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, stream=tstream):
+            one_frame_launch()
+        torch.cuda.synchronize(dev)
+
+    def one_frame():
+        if g1 is not None:
+            g1.replay()
+        else:
+            one_frame_launch()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(5):
+        one_frame()
+    lat = []
+    for _ in range(50):
+        t1 = time.perf_counter()
+        one_frame()
+        lat.append((time.perf_counter() - t1) * 1e3)
+    latency_ms = float(np.median(lat))
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -367,6 +409,7 @@ def main():
                        "parallelism": f"agents{world} (one agent per GPU, independent)",
                        "launch": "hip graph per tracking step" if graph is not None else "eager"},
             "stage_ms_per_step": per_step_ms,
+            "latency_ms_per_frame_b1": latency_ms,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": avg_ms},
@@ -377,6 +420,8 @@ def main():
                           "stage_ms_total": {k: v[0] for k, v in lba_stage.items()}}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+            out["cpu_baseline"]["latency_ms_per_frame"] = 1e3 / out["cpu_baseline"]["value"]
+            out["speedup_latency_b1"] = out["cpu_baseline"]["latency_ms_per_frame"] / latency_ms
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
