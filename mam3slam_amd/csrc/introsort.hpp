@@ -199,4 +199,227 @@ MAM_HD void stl_sort(SortEl* first, SortEl* last) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Data-parallel formulation of the same algorithm (used by one wave on the device for n <= 64).
+//
+// __unguarded_partition(first+1, last, pivot at *first) as stoppers: L_k = k-th position from the left in
+// [first+1, last) with !(a < pivot), R_k = k-th position from the right in [first, last) with !(pivot < a)
+// (*first, the pivot itself, is the sentinel). Every swap exchanges L_k and R_k of the ORIGINAL values as long
+// as L_k < R_k; with K the first k where L_k >= R_k, the returned cut is L_0 when K = 0, else
+// min(L_K, R_{K-1}) (after swap K-1 the left scan meets the swapped value at R_{K-1}, which stops it).
+// Ranges at most 16 long are left for the final insertion sort, which is stable, so it equals a stable sort
+// of the post-partition array by key. These are exactly the operations the sequential code performs.
+MAM_HD int sl_partition_model(SortEl* a, int first, int last) {
+    const int mid = first + (last - first) / 2;
+    sl_move_median_to_first(a + first, a + first + 1, a + mid, a + last - 1);
+    const SortEl pv = a[first];
+    int Lp[1024], Rp[1024];
+    int nl = 0, nr = 0;
+    for (int p = first + 1; p < last; p++)
+        if (!sl_less(a[p], pv)) Lp[nl++] = p;
+    for (int p = last - 1; p >= first; p--)
+        if (!sl_less(pv, a[p])) Rp[nr++] = p;
+    int K = 0;
+    while (K < nl && K < nr && Lp[K] < Rp[K]) K++;
+    for (int k = 0; k < K; k++) sl_swap(a + Lp[k], a + Rp[k]);
+    if (K == 0) return Lp[0];
+    return K < nl ? (Lp[K] < Rp[K - 1] ? Lp[K] : Rp[K - 1]) : Rp[K - 1];
+}
+
+// Host model of the whole data-parallel sort (n <= 1024): same result as stl_sort.
+inline void stl_sort_model(SortEl* a, int n) {
+    if (n == 0) return;
+    int sf[64], sl[64], sd[64], sp = 0;
+    sf[sp] = 0; sl[sp] = n; sd[sp] = sl_lg(n) * 2; ++sp;
+    while (sp > 0) {
+        --sp;
+        int f = sf[sp], l = sl[sp], d = sd[sp];
+        while (l - f > 16) {
+            if (d == 0) { sl_heap_sort(a + f, a + l); break; }
+            --d;
+            const int cut = sl_partition_model(a, f, l);
+            sf[sp] = cut; sl[sp] = l; sd[sp] = d; ++sp;
+            l = cut;
+        }
+    }
+    // final insertion sort == stable sort by key
+    SortEl tmp[1024];
+    for (int i = 0; i < n; i++) {
+        int r = 0;
+        for (int q = 0; q < n; q++) r += sl_less(a[q], a[i]) || (a[q].key == a[i].key && q < i);
+        tmp[r] = a[i];
+    }
+    for (int i = 0; i < n; i++) a[i] = tmp[i];
+}
+
+#if defined(__HIPCC__)
+// One full wave sorts arr[0, n) (n <= 64 * E, in LDS) exactly like stl_sort: E elements per lane in registers
+// (position e * 64 + lane), the stoppers of each partition found by ballot and paired through LDS by rank. Ranges
+// whose depth budget runs out fall back to lane 0's sequential heapsort on LDS (the same operations as stl_sort).
+// scratch: LDS, >= MAM_SORT_WAVE_SCRATCH(E) ints, private to this wave.
+#define MAM_SORT_WAVE_SCRATCH(E) (3 * 24 + 2 * 64 * (E))
+template <int E>
+__device__ __forceinline__ void stl_sort_wave(SortEl* arr, int n, int* scratch) {
+    const int lane = threadIdx.x & 63;
+    if (n <= 1) return;
+    int* const stack = scratch;
+    int* const Lpos = scratch + 72;
+    int* const Rpos = scratch + 72 + 64 * E;
+    uint32_t key[E], val[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int p = e * 64 + lane;
+        key[e] = p < n ? arr[p].key : 0xFFFFFFFFu;
+        val[e] = p < n ? arr[p].val : 0u;
+    }
+    auto get_key = [&](int p) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const uint32_t v = __shfl(key[e], p & 63, 64);
+            if ((p >> 6) == e) r = v;
+        }
+        return r;
+    };
+    auto get_val = [&](int p) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const uint32_t v = __shfl(val[e], p & 63, 64);
+            if ((p >> 6) == e) r = v;
+        }
+        return r;
+    };
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint64_t above = ~(below | (1ull << lane));
+    int sp = 0;
+    int cf = 0, cl = n, cd = sl_lg(n) * 2;
+    while (true) {
+        while (cl - cf > 16) {
+            if (cd == 0) {
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int p = e * 64 + lane;
+                    if (p < n) { arr[p].key = key[e]; arr[p].val = val[e]; }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) sl_heap_sort(arr + cf, arr + cl);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int p = e * 64 + lane;
+                    if (p < n) { key[e] = arr[p].key; val[e] = arr[p].val; }
+                }
+                break;
+            }
+            --cd;
+            // __move_median_to_first(first, first + 1, mid, last - 1)
+            const int mid = cf + (cl - cf) / 2;
+            const uint32_t ka = get_key(cf + 1), kb = get_key(mid), kc = get_key(cl - 1);
+            int sw;
+            if (ka < kb) sw = kb < kc ? mid : (ka < kc ? cl - 1 : cf + 1);
+            else sw = ka < kc ? cf + 1 : (kb < kc ? cl - 1 : mid);
+            {
+                const uint32_t kf = get_key(cf), vf = get_val(cf), ks = get_key(sw), vs = get_val(sw);
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int p = e * 64 + lane;
+                    if (p == cf) { key[e] = ks; val[e] = vs; }
+                    else if (p == sw) { key[e] = kf; val[e] = vf; }
+                }
+            }
+            const uint32_t pv = get_key(cf);
+            uint64_t mL[E], mR[E];
+            bool isL[E], isR[E];
+            int nl = 0, nr = 0;
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int p = e * 64 + lane;
+                const bool inr = p > cf && p < cl;
+                isL[e] = inr && !(key[e] < pv);                    // left scan stops here
+                isR[e] = (inr && !(pv < key[e])) || p == cf;       // right scan stops here (pivot = sentinel)
+                mL[e] = __ballot(isL[e]);
+                mR[e] = __ballot(isR[e]);
+                nl += __popcll(mL[e]);
+                nr += __popcll(mR[e]);
+            }
+            int rankL[E], rankR[E];
+            {
+                int lo = 0;
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    rankL[e] = lo + __popcll(mL[e] & below);        // k-th from the left
+                    lo += __popcll(mL[e]);
+                }
+                int hi = 0;
+#pragma unroll
+                for (int e = E - 1; e >= 0; e--) {
+                    rankR[e] = hi + __popcll(mR[e] & above);        // k-th from the right
+                    hi += __popcll(mR[e]);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                if (isL[e]) Lpos[rankL[e]] = e * 64 + lane;
+                if (isR[e]) Rpos[rankR[e]] = e * 64 + lane;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            int src[E];
+            int K = 0;
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int partnerL = (isL[e] && rankL[e] < nr) ? Rpos[rankL[e]] : -1;
+                const bool swapL = partnerL > e * 64 + lane;        // swap k happens iff L_k < R_k (monotone in k)
+                src[e] = swapL ? partnerL : -1;
+                K += __popcll(__ballot(swapL));
+            }
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                if (src[e] < 0) src[e] = (isR[e] && rankR[e] < K) ? Lpos[rankR[e]] : e * 64 + lane;
+            }
+            uint32_t nk[E], nv[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) { nk[e] = get_key(src[e]); nv[e] = get_val(src[e]); }
+#pragma unroll
+            for (int e = 0; e < E; e++) { key[e] = nk[e]; val[e] = nv[e]; }
+            // returned cut: L_0 if no swap, else min(L_K, R_{K-1}) (L_K absent -> R_{K-1})
+            int cut;
+            if (K == 0) cut = Lpos[0];
+            else {
+                const int rk = Rpos[K - 1];
+                cut = (K < nl && Lpos[K] < rk) ? Lpos[K] : rk;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) { stack[3 * sp] = cut; stack[3 * sp + 1] = cl; stack[3 * sp + 2] = cd; }
+            ++sp;
+            cl = cut;
+        }
+        if (sp == 0) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        --sp;
+        cf = stack[3 * sp];
+        cl = stack[3 * sp + 1];
+        cd = stack[3 * sp + 2];
+    }
+    // final insertion sort == stable sort by key of the partitioned array: rank by (key, position)
+    int r[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) r[e] = 0;
+    for (int q = 0; q < n; q++) {
+        const uint32_t kq = get_key(q);
+#pragma unroll
+        for (int e = 0; e < E; e++) r[e] += (kq < key[e]) || (kq == key[e] && q < e * 64 + lane);
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        if (e * 64 + lane < n) { arr[r[e]].key = key[e]; arr[r[e]].val = val[e]; }
+    }
+}
+#endif
+
 }  // namespace mam

@@ -236,6 +236,7 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         g.cand_per_frame = cand;
         g.kp_slots = kp;
         g.tiles_per_frame = tiles;
+        node_cap = std::max(node_cap, MAM_SORT_WAVE_SCRATCH(4));  // aux doubles as the wave sort's scratch
         g.node_cap = (node_cap + 3) & ~3;
         g.max_level_cells = maxcells;
         g.roi_max_rows = rmax;
@@ -360,6 +361,19 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
                            c->prm.desc_fma);
     }
     MAM_HIP(hipGetLastError());
+#ifdef MAM_DIST_PROFILE
+    {
+        static int calls = 0;
+        if (++calls % 20 == 0) {
+            unsigned long long h[8];
+            MAM_HIP(hipStreamSynchronize(s));
+            MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::g_dprof), sizeof(h)));
+            fprintf(stderr, "distribute cycles (sum over WGs): init %llu rounds %llu pre-sort %llu sort %llu final %llu "
+                    "out %llu; sorts %llu mean m %.1f\n", h[0], h[1], h[2], h[3], h[4], h[5], h[7],
+                    h[7] ? (double)h[6] / h[7] : 0.0);
+        }
+    }
+#endif
     c->last_in0 = d_in;
     c->last_stride = stride;
     c->last_fstride = fstride;

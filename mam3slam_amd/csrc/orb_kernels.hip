@@ -491,6 +491,13 @@ __device__ __forceinline__ void child_rect(const NodeBuf& A, int p, int q, int* 
     *y1 = (q & 2) ? ay1 : ay0 + hy;
 }
 
+#ifdef MAM_DIST_PROFILE
+__device__ unsigned long long g_dprof[8];
+#define DPROF(k) do { __syncthreads(); if (tid == 0) { const long long tn = clock64(); atomicAdd(&g_dprof[k], (unsigned long long)(tn - dp0)); dp0 = tn; } } while (0)
+#else
+#define DPROF(k) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, const int* __restrict__ cell_counts,
                                                     const uint32_t* __restrict__ cand, uint32_t* __restrict__ keys,
                                                     uint16_t* __restrict__ knode, uint32_t* __restrict__ out_key,
@@ -520,6 +527,9 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
     int* scr = (int*)take(64);
     int* sh = (int*)take(64);           // block-uniform scalars
 
+#ifdef MAM_DIST_PROFILE
+    long long dp0 = clock64();
+#endif
     // ---- 0. gather this level's candidates in reference order (cells row-major, FAST order inside)
     const int* cc = cell_counts + (size_t)f * g->cells_per_frame + L.cell_base;
     int carry = 0;
@@ -589,6 +599,7 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
         cur = 1;
     }
     int S = sh[0];
+    DPROF(0);
 
     // Rebuild the list given xr[p] (expansion rank, -1 = unexpanded) for p < S, NX expanded nodes whose
     // children were already counted into ch[4p..4p+3]; aux[r] = #non-empty children of rank r.
@@ -703,6 +714,7 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
             m = sh[1];
             if (S >= N || S == prevSize) finish = true;
             else if (S + m * 3 > N) final_phase = true;
+            DPROF(1);
         } else {
             // ---- final phase (ORBextractor.cc:680-748): sort last round's >1-key children by
             // (size, UL.x) with libstdc++'s introsort, expand from the largest until size >= N.
@@ -714,8 +726,20 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
                 arr[i].val = (uint32_t)p;
             }
             __syncthreads();
-            if (tid == 0) stl_sort(arr, arr + m);
+            DPROF(2);
+            if (m <= 64) {
+                // one wave replays libstdc++'s introsort (ties included) in registers; aux is dead here
+                if (tid < 64) stl_sort_wave<1>(arr, m, aux);
+            } else if (m <= 256) {
+                if (tid < 64) stl_sort_wave<4>(arr, m, aux);
+            } else if (tid == 0) {
+                stl_sort(arr, arr + m);
+            }
             __syncthreads();
+            DPROF(3);
+#ifdef MAM_DIST_PROFILE
+            if (tid == 0) { atomicAdd(&g_dprof[6], (unsigned long long)m); atomicAdd(&g_dprof[7], 1ull); }
+#endif
             for (int p = tid; p < S; p += 256) xr[p] = -1;
             __syncthreads();
             for (int i = tid; i < m; i += 256) {
@@ -759,6 +783,7 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
             S = sh[0];
             m = sh[1];
             if (S >= N || S == prevSize) finish = true;
+            DPROF(4);
         }
     }
 
@@ -800,6 +825,7 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
         st_carry += tot;
     }
     if (tid == 0) { lc[0] = S; lc[1] = st_carry; }
+    DPROF(5);
 }
 
 // ------------------------------------------------------------------------------------------------ describe

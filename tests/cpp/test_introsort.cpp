@@ -1,5 +1,5 @@
 // Host check: the device introsort emulation (mam3slam_amd/csrc/introsort.hpp) reproduces libstdc++
-// std::sort's output order, ties included, on tie-heavy random inputs of every size 0..600.
+// std::sort's output order, ties included, and so does its data-parallel formulation (stl_sort_model), on tie-heavy random inputs of every size 0..600.
 #include <algorithm>
 #include <cstdio>
 #include <random>
@@ -25,10 +25,16 @@ int main() {
                       [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
                           return a.first < b.first;
                       });
+            std::vector<mam::SortEl> par(emu);
             mam::stl_sort(emu.data(), emu.data() + n);
+            mam::stl_sort_model(par.data(), n);   // data-parallel formulation (device wave sort)
             for (int i = 0; i < n; i++) {
                 if (ref[i].first != emu[i].key || ref[i].second != emu[i].val) {
                     printf("MISMATCH trial=%d n=%d i=%d\n", trial, n, i);
+                    return 1;
+                }
+                if (ref[i].first != par[i].key || ref[i].second != par[i].val) {
+                    printf("MODEL MISMATCH trial=%d n=%d i=%d\n", trial, n, i);
                     return 1;
                 }
             }
