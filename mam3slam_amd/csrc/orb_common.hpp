@@ -65,7 +65,26 @@ struct Geom {
     LevelGeom L[MAM_MAX_LEVELS];
 };
 
-// FAST cell descriptor (one workgroup each): ROI rows [y0,y1) cols [x0,x1) of level `level`.
+// k_fast_cells: workgroup size and LDS carve for ROIs up to rmax x cmax (two pixel-pair planes | S map | peaks |
+// packed count entries). The host rejects geometries beyond FAST_MAX_ENTRIES.
+#ifndef MAM_FAST_THREADS
+#define MAM_FAST_THREADS 256
+#endif
+constexpr int FAST_THREADS = MAM_FAST_THREADS;
+constexpr int FAST_MAX_ENTRIES = 64;   // (iteration, wave) count entries: ceil(pairs / threads) * waves
+__host__ __device__ inline size_t fast_align16(size_t b) { return (b + 15) & ~(size_t)15; }
+// plane pitch CW (pairs per parity plane row = S map pitch): one of FAST_CW_CHOICES, >= (cols + 1) / 2 + 2
+__host__ __device__ inline int fast_min_cw(int cols) { return ((cols + 1) >> 1) + 2; }
+__host__ __device__ inline size_t fast_off_s(int rmax, int cw) { return fast_align16((size_t)rmax * 2 * cw * 4); }
+__host__ __device__ inline size_t fast_off_pk(int rmax, int cw) {
+    return fast_off_s(rmax, cw) + fast_align16((size_t)(rmax - 4) * cw * 4);
+}
+__host__ __device__ inline size_t fast_off_cnt(int rmax, int cw) {
+    return fast_off_pk(rmax, cw) + fast_align16((size_t)(rmax - 6) * cw * 2);
+}
+__host__ __device__ inline size_t fast_lds_bytes(int rmax, int cw) { return fast_off_cnt(rmax, cw) + FAST_MAX_ENTRIES * 4; }
+
+// FAST cell descriptor: ROI rows [y0,y1) cols [x0,x1) of level `level`.
 struct CellDesc {
     int level;
     int ci, cj;             // cell row / column index

@@ -62,6 +62,7 @@ struct mam_orb_ctx {
     DevBuf<uint8_t> d_desc;
     DevBuf<int32_t> d_counts;
     size_t fast_lds = 0, dist_lds = 0;
+    int fast_cw = 0;   // k_fast_cells plane pitch instance
     // last-call bookkeeping for debug taps
     const uint8_t* last_in0 = nullptr;
     size_t last_stride = 0, last_fstride = 0;
@@ -284,8 +285,19 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         }
         if (int rc = c->d_cells.alloc(c->cells.size())) return rc;
         MAM_HIP(hipMemcpy(c->d_cells.p, c->cells.data(), c->cells.size() * sizeof(mam::CellDesc), hipMemcpyHostToDevice));
-        // k_fast_cells LDS: P bytes | S bytes | f16 pixel pairs (4 B per ROI position) | scan scratch
-        c->fast_lds = 2 * (((size_t)rmax * cmax + 15) & ~(size_t)15) + 4 * (size_t)rmax * cmax + 64;
+        c->fast_cw = 0;
+        for (int cw : {24, 32, 40, 48})
+            if (cw >= mam::fast_min_cw(cmax)) { c->fast_cw = cw; break; }
+        if (c->fast_cw == 0) { g_last_error = "FAST cell too wide"; return MAM_ERR_ARG; }
+        c->fast_lds = mam::fast_lds_bytes(rmax, c->fast_cw);
+        {
+            const int max_pairs = std::max(rmax - 6, 0) * ((std::max(cmax - 6, 0) + 1) / 2);
+            if ((max_pairs + mam::FAST_THREADS - 1) / mam::FAST_THREADS * (mam::FAST_THREADS / 64) >
+                mam::FAST_MAX_ENTRIES) {
+                g_last_error = "FAST cell too large";
+                return MAM_ERR_ARG;
+            }
+        }
         c->dist_lds = distribute_lds_bytes(g.node_cap, maxcells);
         if (c->fast_lds > 160 * 1024 || c->dist_lds > 160 * 1024) {
             g_last_error = "LDS budget exceeded (nfeatures or cell size too large)";
@@ -343,8 +355,17 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
     }
     {
         StageScope sc(&c->timer, s, MAM_STAGE_FAST);
-        hipLaunchKernelGGL(mam::k_fast_cells, dim3(g.cells_per_frame, F), dim3(256), c->fast_lds, s, c->d_geom.p,
-                           c->d_cells.p, src, c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast);
+        const dim3 fg(g.cells_per_frame, F), fb(mam::FAST_THREADS);
+        switch (c->fast_cw) {
+            case 24: hipLaunchKernelGGL(mam::k_fast_cells<24>, fg, fb, c->fast_lds, s, c->d_geom.p, c->d_cells.p, src,
+                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast); break;
+            case 32: hipLaunchKernelGGL(mam::k_fast_cells<32>, fg, fb, c->fast_lds, s, c->d_geom.p, c->d_cells.p, src,
+                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast); break;
+            case 40: hipLaunchKernelGGL(mam::k_fast_cells<40>, fg, fb, c->fast_lds, s, c->d_geom.p, c->d_cells.p, src,
+                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast); break;
+            default: hipLaunchKernelGGL(mam::k_fast_cells<48>, fg, fb, c->fast_lds, s, c->d_geom.p, c->d_cells.p, src,
+                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast); break;
+        }
     }
     {
         StageScope sc(&c->timer, s, MAM_STAGE_DISTRIBUTE);

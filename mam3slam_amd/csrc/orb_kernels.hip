@@ -216,27 +216,37 @@ __device__ __forceinline__ half2_t hmax3(half2_t a, half2_t b, half2_t c) {
     return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 
-// S of the pixel pair at (r, c), (r, c + 1); hp: ROI pixel pairs, row pitch `cols` (in pairs)
-__device__ __forceinline__ void fast_strength2(const half2_t* hp, int cols, int r, int c, int* s0, int* s1) {
-    const half2_t* p = hp + r * cols + c;
-    const half2_t v = p[0];
+// S of the pixel pair at inner pair column pc of ROI row r, i.e. pixels (r, 3 + 2pc) and (r, 4 + 2pc)
+// (negative = 0). The ROI pixel pairs are split by column parity into planes E (pair at even column 2k) and O
+// (odd column 2k + 1), interleaved per row (row = CW pairs of E then CW of O, compile-time pitch: every circle
+// sample is one base address + an immediate offset), and consecutive lanes read consecutive words. Column
+// 3 + 2pc + dx is E[pc + (3 + dx) / 2] for odd dx, O[pc + (2 + dx) / 2] for even dx.
+template <int CW, int DY, int DX>
+__device__ __forceinline__ half2_t fast_px(const half2_t* E) {
+    if constexpr ((DX & 1) != 0) return E[DY * 2 * CW + (3 + DX) / 2];
+    else return E[DY * 2 * CW + CW + (2 + DX) / 2];
+}
+template <int CW>
+__device__ __forceinline__ half2_t fast_strength_h2(const half2_t* hp, int r, int pc) {
+    const half2_t* E = hp + r * 2 * CW + pc;
+    const half2_t v = fast_px<CW, 0, 0>(E);
     half2_t d[16];
-    d[0] = v - p[3 * cols];
-    d[1] = v - p[3 * cols + 1];
-    d[2] = v - p[2 * cols + 2];
-    d[3] = v - p[cols + 3];
-    d[4] = v - p[3];
-    d[5] = v - p[-cols + 3];
-    d[6] = v - p[-2 * cols + 2];
-    d[7] = v - p[-3 * cols + 1];
-    d[8] = v - p[-3 * cols];
-    d[9] = v - p[-3 * cols - 1];
-    d[10] = v - p[-2 * cols - 2];
-    d[11] = v - p[-cols - 3];
-    d[12] = v - p[-3];
-    d[13] = v - p[cols - 3];
-    d[14] = v - p[2 * cols - 2];
-    d[15] = v - p[3 * cols - 1];
+    d[0] = v - fast_px<CW, 3, 0>(E);
+    d[1] = v - fast_px<CW, 3, 1>(E);
+    d[2] = v - fast_px<CW, 2, 2>(E);
+    d[3] = v - fast_px<CW, 1, 3>(E);
+    d[4] = v - fast_px<CW, 0, 3>(E);
+    d[5] = v - fast_px<CW, -1, 3>(E);
+    d[6] = v - fast_px<CW, -2, 2>(E);
+    d[7] = v - fast_px<CW, -3, 1>(E);
+    d[8] = v - fast_px<CW, -3, 0>(E);
+    d[9] = v - fast_px<CW, -3, -1>(E);
+    d[10] = v - fast_px<CW, -2, -2>(E);
+    d[11] = v - fast_px<CW, -1, -3>(E);
+    d[12] = v - fast_px<CW, 0, -3>(E);
+    d[13] = v - fast_px<CW, 1, -3>(E);
+    d[14] = v - fast_px<CW, 2, -2>(E);
+    d[15] = v - fast_px<CW, 3, -1>(E);
     half2_t mn3[16], mx3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -257,110 +267,185 @@ __device__ __forceinline__ void fast_strength2(const half2_t* hp, int cols, int 
     }
     A = __builtin_elementwise_maximum(A, arcmin[15]);
     Bm = __builtin_elementwise_minimum(Bm, arcmax[15]);
-    const half2_t S = __builtin_elementwise_maximum(A, -Bm);
-    const int a0 = (int)S.x, a1 = (int)S.y;
-    *s0 = a0 < 0 ? 0 : a0;
-    *s1 = a1 < 0 ? 0 : a1;
+    return __builtin_elementwise_maximum(A, -Bm);
 }
 
-// One workgroup per cell. (a) ROI -> LDS; (b) S for the inner pixels (the 3-pixel ring stays 0: cv::FAST on the
-// cell ROI never scores it); (c) each thread takes a contiguous run of inner pixels in row-major order and
-// computes the NMS peak P = S if S > max of its 8 neighbours (else 0): with t >= 1 OpenCV's test
-// "score > every neighbour's score-or-0" is exactly S > t && S > max8(S) && S >= 2, for both thresholds;
-// (d) iniThFAST if any P > iniTh else minThFAST; (e) one block scan places the run's corners in order.
-__global__ __launch_bounds__(256) void k_fast_cells(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
-                                                    LevelSrc s, uint32_t* __restrict__ cand,
-                                                    int* __restrict__ cell_counts, int iniTh, int minTh) {
+// One workgroup (FAST_THREADS) per cell, everything on pixel pairs (two horizontally adjacent pixels per lane):
+// (a) ROI -> LDS as f16 pixel pairs in two column-parity planes (compile-time pitch CW), 4 pairs per thread;
+// (b) S of every inner pair into a half2 map with a zero guard ring (the 3-pixel ROI ring is never scored by
+//     cv::FAST on the cell ROI, so it reads as 0);
+// (c) NMS peak P = S if S > max of its 8 neighbours and S >= 2 (with t >= 1 OpenCV's "score > every neighbour's
+//     score-or-0" is exactly S > t && S > max8(S) && S >= 2, for both thresholds), counted per (iteration, wave)
+//     at both thresholds by ballot;
+// (d) iniThFAST if any P > iniTh, else minThFAST; every wave reads all count entries with broadcast LDS reads;
+// (e) corners written in row-major order (pair order = pixel order) at ballot prefix positions.
+// The whole kernel is VALU-bound (S is ~100 packed f16 ops per pixel pair); see DESIGN.md.
+template <int CW>
+__global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restrict__ g,
+                                                             const CellDesc* __restrict__ cells, LevelSrc s,
+                                                             uint32_t* __restrict__ cand,
+                                                             int* __restrict__ cell_counts, int iniTh, int minTh) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int T = FAST_THREADS, NW = FAST_THREADS / 64;
     const CellDesc c = cells[blockIdx.x];
     const int f = blockIdx.y;
     const LevelGeom& L = g->L[c.level];
-    const int roi_cap = ((g->roi_max_rows * g->roi_max_cols) + 15) & ~15;
-    uint8_t* im = smem;                                                        // NMS peaks (phase c)
-    uint8_t* S = smem + roi_cap;
-    half2_t* hp = reinterpret_cast<half2_t*>(smem + 2 * roi_cap);                // pixel pairs
-    int* scr = reinterpret_cast<int*>(smem + 2 * roi_cap + 4 * (size_t)g->roi_max_rows * g->roi_max_cols);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+#if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 4)
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = 0;   // timing experiment only
+    return;
+#endif
     int pitch;
     const uint8_t* lev = level_ptr(g, s, f, c.level, &pitch);
     const int rows = c.y1 - c.y0, cols = c.x1 - c.x0;
-    const int npx = rows * cols;
-    // linear index walks with incremental (row, col): one integer division per thread, not per pixel
+    const int bh = rows - 6, bw = cols - 6;
+    const int pw = bw > 0 ? (bw + 1) >> 1 : 0;  // pixel pairs per inner row
+    const int np = bh > 0 ? bh * pw : 0;
+    constexpr int SC = CW;                      // S map pitch (pairs): pw + 2 <= CW (host-checked)
+    // ---- LDS carve (fast_lds_bytes() on the host mirrors it)
+    half2_t* hp = reinterpret_cast<half2_t*>(smem);                                // [rows][E: CW | O: CW]
+    const int rmax = g->roi_max_rows;
+    half2_t* Sh = reinterpret_cast<half2_t*>(smem + fast_off_s(rmax, CW));          // [bh+2][SC]
+    uint16_t* pkm = reinterpret_cast<uint16_t*>(smem + fast_off_pk(rmax, CW));      // [np]
+    int* cnt = reinterpret_cast<int*>(smem + fast_off_cnt(rmax, CW));               // [it*NW] packed
+    const half2_t z = {(_Float16)0, (_Float16)0};
+    // (a) stage 4 pairs per thread: bytes c0 .. c0+4 of one ROI row
     {
-        const int dq = 256 / cols, dr = 256 - dq * cols;
-        int r = tid / cols, cc = tid - r * cols;
+        const int qc = (cols + 3) >> 2, nq = rows * qc;
+        const int dq = T / qc, dr = T - dq * qc;
+        int r = tid / qc, q = tid - r * qc;
         const uint8_t* src = lev + (size_t)c.y0 * pitch + c.x0;
-        for (int i = tid; i < npx; i += 256) {
-            const uint8_t* q = src + (size_t)r * pitch + cc;
-            half2_t h;
-            h.x = (_Float16)(int)q[0];
-            h.y = cc + 1 < cols ? (_Float16)(int)q[1] : (_Float16)0;
-            hp[i] = h;
-            S[i] = 0;
+#pragma unroll 2
+        for (int i = tid; i < nq; i += T) {
+            // columns up to 4q + 4 <= cols + 3 stay inside the level row (cells end >= EDGE_THRESHOLD - 3 before
+            // its right edge); values past the ROI only reach the discarded ring pixel of odd-width cells.
+            // Unconditional loads: all in flight before the first use.
+            const uint8_t* pr = src + (size_t)r * pitch + 4 * q;
+            uint32_t w4;
+            __builtin_memcpy(&w4, pr, 4);
+            const uint32_t b4 = pr[4];
+            _Float16 v[5];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = (_Float16)(int)((w4 >> (8 * k)) & 0xFF);
+            v[4] = (_Float16)(int)b4;
+            half2_t* dE = hp + r * 2 * CW + 2 * q;
+            half2_t* dO = dE + CW;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                half2_t h;
+                h.x = v[k];
+                h.y = v[k + 1];
+                ((k & 1) ? dO : dE)[k >> 1] = h;
+            }
             r += dq;
-            cc += dr;
-            if (cc >= cols) { cc -= cols; r++; }
+            q += dr;
+            if (q >= qc) { q -= qc; r++; }
+        }
+        if (np > 0) {
+            for (int i = tid; i < SC; i += T) { Sh[i] = z; Sh[(bh + 1) * SC + i] = z; }
+            for (int i = tid; i < bh; i += T) { Sh[(i + 1) * SC] = z; Sh[(i + 1) * SC + pw + 1] = z; }
         }
     }
     __syncthreads();
-    const int bh = rows - 6, bw = cols - 6;
-    const int nb = (bh > 0 && bw > 0) ? bh * bw : 0;
-    const int pw = (bw + 1) >> 1;   // pixel pairs per inner row
-    if (nb > 0) {
-        const int np = bh * pw;
-        const int dq = 256 / pw, dr = 256 - dq * pw;
-        int r = 3 + tid / pw, pc = tid % pw;
-        for (int i = tid; i < np; i += 256) {
-            const int cc = 3 + 2 * pc;
-            int s0, s1;
-            fast_strength2(hp, cols, r, cc, &s0, &s1);
-            S[r * cols + cc] = (uint8_t)s0;
-            if (2 * pc + 1 < bw) S[r * cols + cc + 1] = (uint8_t)s1;
+#if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 2)
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = (int)hp[tid].x;   // timing only
+    return;
+#endif
+    const int pwm = max(pw, 1);
+    const int dq = T / pwm, dr = T - dq * pwm;
+    const int r_start = tid / pwm, p_start = tid - r_start * pwm;
+    // (b) strength of every inner pair
+    {
+        int r = r_start, pc = p_start;
+        for (int i = tid; i < np; i += T) {
+#if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 1)
+            half2_t S2 = hp[(r + 3) * 2 * CW + pc] - hp[(r + 3) * 2 * CW + CW + pc + 1];   // timing experiment only
+#else
+            half2_t S2 = fast_strength_h2<CW>(hp, r + 3, pc);
+#endif
+            S2 = __builtin_elementwise_maximum(S2, z);
+            if (2 * pc + 1 >= bw) S2.y = (_Float16)0;   // odd width: the pair's second pixel is ring
+            Sh[(r + 1) * SC + pc + 1] = S2;
             r += dq;
             pc += dr;
             if (pc >= pw) { pc -= pw; r++; }
         }
     }
     __syncthreads();
-    // (c) NMS peaks over this thread's run [i0, i1), stored in place of the (no longer needed) ROI pixels
-    const int per = (nb + 255) / 256;
-    const int i0 = min(tid * per, nb), i1 = min(i0 + per, nb);
     const int tlo = max(iniTh, 1), thi = max(minTh, 1);
-    int cnt_ini = 0;
-    const int r0 = nb > 0 ? 3 + i0 / bw : 0, c0 = nb > 0 ? 3 + i0 % bw : 0;
-    int rr = r0, ccol = c0;
-    for (int i = i0; i < i1; i++) {
-        const int q = rr * cols + ccol;
-        if (++ccol == bw + 3) { ccol = 3; rr++; }
-        const int sv = S[q];
-        int pk = 0;
-        if (sv > min(tlo, thi)) {
-            const int m8 = max(max(max3i(S[q - cols - 1], S[q - cols], S[q - cols + 1]), max3i(S[q - 1], S[q + 1], S[q + cols - 1])),
-                               max(S[q + cols], S[q + cols + 1]));
-            pk = (sv > m8 && sv >= 2) ? sv : 0;
+    const int iters = (np + T - 1) / T;
+    // (c) NMS peaks + per-(iteration, wave) counts at both thresholds, packed (hi << 16) | lo
+    {
+        int r = r_start, pc = p_start;
+        for (int j = 0; j < iters; j++) {
+            const int i = j * T + tid;
+            int pk0 = 0, pk1 = 0;
+            if (i < np) {
+                const half2_t* q = Sh + (r + 1) * SC + pc + 1;
+                const half2_t UL = q[-SC - 1], U = q[-SC], UR = q[-SC + 1];
+                const half2_t ML = q[-1], M = q[0], MR = q[1];
+                const half2_t DL = q[SC - 1], D = q[SC], DR = q[SC + 1];
+                const half2_t up = hmax3(__builtin_shufflevector(UL, U, 1, 2), U, __builtin_shufflevector(U, UR, 1, 2));
+                const half2_t dn = hmax3(__builtin_shufflevector(DL, D, 1, 2), D, __builtin_shufflevector(D, DR, 1, 2));
+                const half2_t md = __builtin_elementwise_maximum(__builtin_shufflevector(ML, M, 1, 2),
+                                                                 __builtin_shufflevector(M, MR, 1, 2));
+                const half2_t m8 = hmax3(up, dn, md);
+                pk0 = (M.x > m8.x && M.x >= (_Float16)2) ? (int)M.x : 0;
+                pk1 = (M.y > m8.y && M.y >= (_Float16)2) ? (int)M.y : 0;
+                pkm[i] = (uint16_t)(pk0 | (pk1 << 8));
+                r += dq;
+                pc += dr;
+                if (pc >= pw) { pc -= pw; r++; }
+            }
+            const int chi = __popcll(__ballot(pk0 > tlo)) + __popcll(__ballot(pk1 > tlo));
+            const int clo = __popcll(__ballot(pk0 > thi)) + __popcll(__ballot(pk1 > thi));
+            if (lane == 0) cnt[j * NW + w] = (chi << 16) | clo;
         }
-        im[i] = (uint8_t)pk;
-        cnt_ini += pk > tlo ? 1 : 0;
     }
-    const int total = block_sum(cnt_ini, scr);
-    const int th = total > 0 ? tlo : thi;
-    int cnt = 0;
-    for (int i = i0; i < i1; i++) cnt += im[i] > th ? 1 : 0;
-    int tot;
-    int pos = block_excl_scan(cnt, scr, &tot);
+    __syncthreads();
+    // (d) cell totals and this wave's bases: every lane reads the entries (same address: LDS broadcast)
+    int tot = 0, mybase_first = 0;
+    const int nent = iters * NW;
+    for (int e = 0; e < nent; e++) {
+        const int v = cnt[e];
+        if (e == w) mybase_first = tot;
+        tot += v;
+    }
+    const int tot_hi = tot >> 16, tot_lo = tot & 0xFFFF;
+    const bool use_hi = tot_hi > 0;
+    const int th = use_hi ? tlo : thi;
+    // (e) ordered emit; the base of entry (j, w) = base(j-1, w) + entries (j-1, w+1 .. NW-1) + (j, 0 .. w-1)
     uint32_t* out = cand + (size_t)f * g->cand_per_frame + L.cand_base + (size_t)c.slot * L.cellcap;
-    rr = r0;
-    ccol = c0;
-    for (int i = i0; i < i1; i++) {
-        const int pk = im[i];
-        if (pk > th) {
-            const uint32_t x = (uint32_t)(ccol + c.cj * L.wCell);
-            const uint32_t y = (uint32_t)(rr + c.ci * L.hCell);
-            out[pos++] = x | (y << 12) | ((uint32_t)(pk - 1) << 24);
+    {
+        int r = r_start, pc = p_start;
+        const uint64_t below = (1ull << lane) - 1ull;
+        int basep = mybase_first;
+        for (int j = 0; j < iters; j++) {
+            if (j > 0) {
+                for (int e = (j - 1) * NW + w; e < j * NW + w; e++) basep += cnt[e];
+            }
+            const int i = j * T + tid;
+            int pk0 = 0, pk1 = 0;
+            if (i < np) {
+                const int v = pkm[i];
+                pk0 = v & 0xFF;
+                pk1 = v >> 8;
+            }
+            const bool f0 = pk0 > th, f1 = pk1 > th;
+            const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+            int pos = (use_hi ? basep >> 16 : basep & 0xFFFF) + __popcll(m0 & below) + __popcll(m1 & below);
+            if (i < np) {
+                const uint32_t x = (uint32_t)(3 + 2 * pc + c.cj * L.wCell);
+                const uint32_t y = (uint32_t)(r + 3 + c.ci * L.hCell);
+                if (f0) out[pos++] = x | (y << 12) | ((uint32_t)(pk0 - 1) << 24);
+                if (f1) out[pos] = (x + 1) | (y << 12) | ((uint32_t)(pk1 - 1) << 24);
+                r += dq;
+                pc += dr;
+                if (pc >= pw) { pc -= pw; r++; }
+            }
         }
-        if (++ccol == bw + 3) { ccol = 3; rr++; }
     }
-    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = tot;
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = use_hi ? tot_hi : tot_lo;
 }
 
 // ------------------------------------------------------------------------------------------------ blur
