@@ -9,13 +9,13 @@
 //
 // Stages (one launch each, batched over frames):
 //   k_grid     per frame: PosInGrid for every keypoint, LDS counting sort by cell (atomics) + per-cell insertion
-//              sort by index -> cell-major index list with ascending idx per cell = AssignFeaturesToGrid's cell
-//              vectors, plus the (x, y, octave) of each entry in that order for coalesced window scans.
-//   k_gather   one wave per search unit (MapPoint / last-frame entry): window cells enumerated ix -> iy -> cell
-//              order exactly as GetFeaturesInArea, level + radius filters, Hamming distance (4x popcount64),
-//              only the candidates that can change a result kept (dist <= TH_HIGH, or <= TH_HIGH / nnratio for the
-//              ratio test), written in enumeration order to a per-unit slot (entry = idx | dist<<16 | level<<25),
-//              longer lists to a per-frame overflow area.
+//              sort by index -> cell-major list with ascending idx per cell = AssignFeaturesToGrid's cell vectors,
+//              stored as 48-byte records (x, y, idx | octave, descriptor) for one-load candidate tests.
+//   k_gather   one wave per search unit (MapPoint / last-frame entry): the window's candidates flattened in
+//              GetFeaturesInArea's order (cells ix -> iy, index order inside) and dealt to the lanes; level +
+//              radius filters, Hamming distance; only the candidates that can change a result kept (dist <=
+//              TH_HIGH, or <= TH_HIGH / nnratio for the ratio test), placed in enumeration order by ballot into a
+//              per-unit slot (entry = idx | dist<<16 | level<<25), longer lists into a per-frame overflow area.
 //   k_resolve  per frame, one workgroup: the reference's sequential greedy loop replayed exactly as dependency
 //              rounds — a unit resolves once every earlier unit sharing a candidate keypoint has; units ready in
 //              the same round have disjoint candidates and commit in parallel. Then the rotation-histogram pass.
@@ -36,6 +36,15 @@ namespace mam {
 constexpr int NCELLS = MAM_GRID_COLS * MAM_GRID_ROWS;
 constexpr int GRID_SORT_MAX = 8192;   // keypoints per frame the grid sort handles (LDS 32 KB)
 
+// One keypoint in grid (cell-major) order: position, index | octave << 16, and its descriptor, so a window scan
+// reads one 48-byte record per candidate (no dependent index -> descriptor load).
+struct __attribute__((aligned(16))) GridEnt {
+    float x, y;
+    uint32_t io;              // keypoint index | octave << 16
+    uint32_t pad;
+    uint4 d0, d1;             // descriptor
+};
+
 struct ProjArgs {
     mam_frame_geom g;
     mam_frames_dev fr;
@@ -52,9 +61,7 @@ struct ProjArgs {
     const mam_last_entry* last;
     int check_ori;
     // scratch
-    uint16_t* grid_idx;       // [F][kp_stride] keypoint index, cell-major (cell vectors of AssignFeaturesToGrid)
-    float2* grid_xy;          // [F][kp_stride] keypoint (x, y) in the same order
-    uint8_t* grid_oct;        // [F][kp_stride] keypoint octave in the same order
+    struct GridEnt* grid_ent; // [F][kp_stride] cell-major keypoint records (cell vectors of AssignFeaturesToGrid)
     int32_t* grid_start;      // [F][NCELLS+1]
     int32_t* cand_cnt;        // [F][unit_stride]
     int32_t* cand_off;        // [F][unit_stride]
@@ -178,11 +185,17 @@ __global__ __launch_bounds__(1024) void k_grid(ProjArgs p) {
     int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
     for (int c = tid; c <= NCELLS; c += 1024) gs[c] = start[c];
     const size_t off = (size_t)f * p.fr.kp_stride;
+    const uint4* D = reinterpret_cast<const uint4*>(p.fr.desc + (size_t)f * p.fr.kp_stride * 32);
     for (int k = tid; k < tot; k += 1024) {
         const int i = sorted[k];
-        p.grid_idx[off + k] = (uint16_t)i;
-        p.grid_xy[off + k] = make_float2(K[i].x, K[i].y);
-        p.grid_oct[off + k] = (uint8_t)K[i].octave;
+        GridEnt e;
+        e.x = K[i].x;
+        e.y = K[i].y;
+        e.io = (uint32_t)i | ((uint32_t)(uint8_t)K[i].octave << 16);
+        e.pad = 0;
+        e.d0 = D[2 * i];
+        e.d1 = D[2 * i + 1];
+        p.grid_ent[off + k] = e;
     }
 }
 
@@ -261,56 +274,60 @@ __device__ __forceinline__ int rel_threshold(const ProjArgs& p) {
                        : (p.nnratio > 0.f ? min(256, (int)ceilf((float)MAM_TH_HIGH / p.nnratio) + 1) : 256);
 }
 
-// One pass over a unit's window: lanes own window cells (ix -> iy order), count their relevant candidates, a wave
-// scan places them; entries at positions < lim are written to dst. Returns the relevant count.
-__device__ int gather_pass(const ProjArgs& p, int f, const Window& w, int rel, uint32_t* dst, int lim) {
+// One pass over a unit's window: the window's candidates (cells in ix -> iy order, each cell's keypoints in index
+// order: GetFeaturesInArea's enumeration) are flattened and dealt to the lanes 64 at a time; each lane finds its
+// cell by a binary search over the cell-count scan, tests level / radius / distance, and a ballot places the
+// relevant ones in order. Entries at positions < lim are written to dst. Returns the relevant count.
+__device__ int gather_pass(const ProjArgs& p, int f, const Window& w, int rel, const uint4 u0, const uint4 u1,
+                           uint32_t* dst, int lim) {
     const int lane = lane_id();
     const int ny = w.cy1 - w.cy0 + 1;
     const int ncell = (w.cx1 - w.cx0 + 1) * ny;
     const int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
-    const uint16_t* gi = p.grid_idx + (size_t)f * p.fr.kp_stride;
-    const float2* gxy = p.grid_xy + (size_t)f * p.fr.kp_stride;
-    const uint8_t* gct = p.grid_oct + (size_t)f * p.fr.kp_stride;
-    const uint8_t* D = p.fr.desc + (size_t)f * p.fr.kp_stride * 32;
+    const GridEnt* G = p.grid_ent + (size_t)f * p.fr.kp_stride;
+    const uint64_t below = (1ull << lane) - 1ull;
     int base = 0;
     for (int e0 = 0; e0 < ncell; e0 += 64) {
         const int e = e0 + lane;
-        int cnt = 0, k0 = 0, k1 = 0;
+        int k0 = 0, c = 0;
         if (e < ncell) {
             const int ix = w.cx0 + e / ny, iy = w.cy0 + e % ny;
             const int cell = ix * MAM_GRID_ROWS + iy;
             k0 = gs[cell];
-            k1 = gs[cell + 1];
-            for (int k = k0; k < k1; k++) {
-                const int oct = gct[k];
-                if (w.checkL) {
-                    if (oct < w.minL) continue;
-                    if (w.maxL >= 0 && oct > w.maxL) continue;
-                }
-                const float2 xy = gxy[k];
-                const float dx = xy.x - w.x, dy = xy.y - w.y;
-                if (fabsf(dx) < w.r && fabsf(dy) < w.r && desc_dist(w.desc, D + (size_t)gi[k] * 32) <= rel) cnt++;
-            }
+            c = gs[cell + 1] - k0;
         }
-        const int incl = wave_incl_scan(cnt);
-        int o = base + incl - cnt;
-        if (cnt > 0 && o < lim) {
-            for (int k = k0; k < k1 && o < lim; k++) {
-                const int oct = gct[k];
-                if (w.checkL) {
-                    if (oct < w.minL) continue;
-                    if (w.maxL >= 0 && oct > w.maxL) continue;
-                }
-                const float2 xy = gxy[k];
-                const float dx = xy.x - w.x, dy = xy.y - w.y;
-                if (fabsf(dx) < w.r && fabsf(dy) < w.r) {
-                    const int idx = gi[k];
-                    const int dist = desc_dist(w.desc, D + (size_t)idx * 32);
-                    if (dist <= rel) dst[o++] = (uint32_t)idx | ((uint32_t)dist << 16) | ((uint32_t)oct << 25);
+        const int incl = wave_incl_scan(c);
+        const int tot = __shfl(incl, 63, 64);
+        const int kb = k0 - (incl - c);   // record index of candidate t in this lane's cell = kb + t
+        for (int t0 = 0; t0 < tot; t0 += 64) {
+            const int t = t0 + lane;
+            int m = 0;   // owner cell: first m with incl[m] > t
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (__shfl(incl, m + step - 1, 64) <= t) m += step;
+            const int k = __shfl(kb, m, 64) + t;
+            bool ok = false;
+            uint32_t ent = 0;
+            if (t < tot) {
+                const GridEnt ge = G[k];
+                const int oct = (int)(ge.io >> 16);
+                const bool lvl_ok = !w.checkL || (oct >= w.minL && (w.maxL < 0 || oct <= w.maxL));
+                const float dx = ge.x - w.x, dy = ge.y - w.y;
+                if (lvl_ok && fabsf(dx) < w.r && fabsf(dy) < w.r) {
+                    const int dist = __popc(u0.x ^ ge.d0.x) + __popc(u0.y ^ ge.d0.y) + __popc(u0.z ^ ge.d0.z) +
+                                     __popc(u0.w ^ ge.d0.w) + __popc(u1.x ^ ge.d1.x) + __popc(u1.y ^ ge.d1.y) +
+                                     __popc(u1.z ^ ge.d1.z) + __popc(u1.w ^ ge.d1.w);
+                    if (dist <= rel) {
+                        ok = true;
+                        ent = (ge.io & 0xFFFFu) | ((uint32_t)dist << 16) | ((uint32_t)oct << 25);
+                    }
                 }
             }
+            const uint64_t b = __ballot(ok);
+            const int o = base + __popcll(b & below);
+            if (ok && o < lim) dst[o] = ent;
+            base += __popcll(b);
         }
-        base += __shfl(incl, 63, 64);
     }
     return base;
 }
@@ -333,7 +350,8 @@ __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
     uint32_t* fpool = p.pool + (size_t)f * p.pool_per_frame;
     const int rel = rel_threshold(p);
     const int CAP = p.slot_cap;
-    int total = gather_pass(p, f, w, rel, fpool + (size_t)j * CAP, CAP);
+    const uint4 u0 = reinterpret_cast<const uint4*>(w.desc)[0], u1 = reinterpret_cast<const uint4*>(w.desc)[1];
+    int total = gather_pass(p, f, w, rel, u0, u1, fpool + (size_t)j * CAP, CAP);
     int off = j * CAP;
     if (total > CAP) {
         int o2 = 0;
@@ -341,7 +359,7 @@ __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
         o2 = __shfl(o2, 0, 64);
         if (o2 + total <= p.ovf_cap) {
             off = p.unit_stride * CAP + o2;
-            gather_pass(p, f, w, rel, fpool + off, total);
+            gather_pass(p, f, w, rel, u0, u1, fpool + off, total);
         } else {
             total = 0;   // capacity: pool_total > ovf_cap makes the resolve stage report the frame
         }
@@ -722,9 +740,7 @@ struct mam_match_ctx {
     int slot_cap = 32;        // candidate slots per unit (grows x4 when a host call overflows)
     size_t resolve_lds_max = 64 * 1024;
     // scratch
-    DevBuf<uint16_t> grid_idx;
-    DevBuf<float2> grid_xy;
-    DevBuf<uint8_t> grid_oct;
+    DevBuf<mam::GridEnt> grid_ent;
     DevBuf<int32_t> grid_start, cand_cnt, cand_off, pool_total, out_n_tmp;
     DevBuf<uint32_t> pool, events;
     // host-API staging
@@ -749,9 +765,7 @@ void set_pool(mam_match_ctx* c, mam::ProjArgs& a, int unit_stride) {
 size_t carve_bytes(size_t count, size_t elem) { return (count * elem + 255) & ~(size_t)255; }
 
 int ensure_scratch(mam_match_ctx* c, int F, int kp_stride, int unit_stride, int pool_per_frame) {
-    if (int rc = c->grid_idx.alloc((size_t)F * kp_stride)) return rc;
-    if (int rc = c->grid_xy.alloc((size_t)F * kp_stride)) return rc;
-    if (int rc = c->grid_oct.alloc((size_t)F * kp_stride)) return rc;
+    if (int rc = c->grid_ent.alloc((size_t)F * kp_stride)) return rc;
     if (int rc = c->grid_start.alloc((size_t)F * (mam::NCELLS + 1))) return rc;
     if (int rc = c->cand_cnt.alloc((size_t)F * unit_stride)) return rc;
     if (int rc = c->cand_off.alloc((size_t)F * unit_stride)) return rc;
@@ -766,9 +780,7 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     if (F <= 0) return MAM_OK;
     if (a.fr.kp_stride > mam::GRID_SORT_MAX || a.fr.kp_stride <= 0 || a.unit_stride <= 0) return MAM_ERR_ARG;
     if (int rc = ensure_scratch(c, F, a.fr.kp_stride, a.unit_stride, a.pool_per_frame)) return rc;
-    a.grid_idx = c->grid_idx.p;
-    a.grid_xy = c->grid_xy.p;
-    a.grid_oct = c->grid_oct.p;
+    a.grid_ent = c->grid_ent.p;
     a.grid_start = c->grid_start.p;
     a.cand_cnt = c->cand_cnt.p;
     a.cand_off = c->cand_off.p;
