@@ -37,6 +37,14 @@ CONFIGS = {
     "c2": dict(width=1280, height=720, nfeatures=2000, lba=True),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+# what actually limits each stage: the byte/integer path has no MFMA work and most stages issue far
+# more VALU work per byte than the HBM roofline can see
+ROOFLINE_NOTES = {
+    "fast": "VALU issue: FAST-9 strength is ~100 packed-f16 min3/max3/sub ops per pixel pair (DESIGN.md §3)",
+    "pyramid": "LDS-staged bilinear resize, latency-bound at 8 small launches",
+    "describe": "one wave per keypoint: LDS-free gathers from the blurred level (latency)",
+    "resolve": "one workgroup per frame, greedy dependency rounds (latency, LDS atomics)",
+}
 FP64_PEAK_TFS = 78.6    # MI355X FP64 vector (spec)
 
 
@@ -117,11 +125,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU (independent frame streams)")
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-graph", action="store_true", help="launch the tracking step eagerly instead of a HIP graph")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the B=1 latency section (profiling runs: every launch then covers one lane's batch)")
+    ap.add_argument("--lanes", type=int, default=4,
+                    help="independent sub-batches (agent groups) per GPU, each with its own contexts and HIP stream, "
+                         "so one group's latency-bound stages overlap another's compute")
     args = ap.parse_args()
 
     import torch
@@ -141,6 +154,10 @@ def main():
 
     cfg = CONFIGS[args.config]
     W, H, NF, B = cfg["width"], cfg["height"], cfg["nfeatures"], args.batch
+    NL = max(1, args.lanes)
+    if B % NL:
+        raise SystemExit(f"--batch {B} is not a multiple of --lanes {NL}")
+    BL = B // NL
     ext = ORBextractor(NF, 1.2, 8, 20, 7, device=local)
     cap = ext.max_keypoints()
     frames = np.stack([synth.make_frame(W, H, agent=rank, frame=i) for i in range(B)])
@@ -154,12 +171,33 @@ def main():
     torch.cuda.set_stream(tstream)
     stream = tstream.cuda_stream
 
+    # lanes: frames [l * BL, (l + 1) * BL) run on lane l's stream with lane l's contexts
+    lanes = []
+    for l in range(NL):
+        lanes.append({"lo": l * BL, "ext": ext if l == 0 else ORBextractor(NF, 1.2, 8, 20, 7, device=local),
+                      "stream": tstream if l == 0 else torch.cuda.Stream(dev)})
+
+    def extract_lane(ln):
+        lo = ln["lo"]
+        ln["ext"].extract_batch_device(d_img[lo].data_ptr(), BL, W, H, W, W * H, d_kps[lo].data_ptr(),
+                                       d_desc[lo].data_ptr(), cap, d_cnt[lo].data_ptr(), stream=ln["stream"].cuda_stream)
+
     def extract():
-        ext.extract_batch_device(d_img.data_ptr(), B, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap,
-                                 d_cnt.data_ptr(), stream=stream)
+        for ln in lanes:
+            extract_lane(ln)
+
+    def fork():
+        for ln in lanes[1:]:
+            ln["stream"].wait_stream(tstream)
+
+    def join():
+        for ln in lanes[1:]:
+            tstream.wait_stream(ln["stream"])
 
     # ---- per-frame map structures around the frame's own features (built once; resident in HBM)
+    fork()
     extract()
+    join()
     torch.cuda.synchronize(dev)
     kps_h = d_kps.cpu().numpy().view(KP_DTYPE).reshape(B, cap)
     desc_h = d_desc.cpu().numpy()
@@ -193,18 +231,36 @@ def main():
     d_nm1 = torch.zeros(B, dtype=torch.int32, device=dev)
     d_nm2 = torch.zeros(B, dtype=torch.int32, device=dev)
     d_taken = torch.zeros((B, cap), dtype=torch.uint8, device=dev)
-    m_motion = ORBmatcher(0.9, True, device=local)
-    m_local = ORBmatcher(0.8, True, device=local)
-    fr1 = FramesDev(B, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), None)
-    fr2 = FramesDev(B, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), d_taken.data_ptr())
+    tcw_bytes = tcw.dtype.itemsize
+    for ln in lanes:
+        lo = ln["lo"]
+        ln["mm"] = ORBmatcher(0.9, True, device=local)
+        ln["ml"] = ORBmatcher(0.8, True, device=local)
+        ln["fr1"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(), None)
+        ln["fr2"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(),
+                              d_taken[lo].data_ptr())
+    m_motion, m_local = lanes[0]["mm"], lanes[0]["ml"]
+
+    def match_lane(ln):
+        lo, st = ln["lo"], ln["stream"]
+        ln["mm"].search_motion_batch_device(F0, ln["fr1"], d_tcw.data_ptr() + lo * tcw_bytes, cam,
+                                            d_last[lo].data_ptr(), Ls, d_nlast[lo:].data_ptr(), 15.0,
+                                            d_out1[lo].data_ptr(), d_nm1[lo:].data_ptr(), stream=st.cuda_stream)
+        with torch.cuda.stream(st):
+            torch.ge(d_out1[lo:lo + BL], 0, out=d_taken[lo:lo + BL].view(torch.bool))
+        ln["ml"].search_by_projection_batch_device(F0, ln["fr2"], d_mps[lo].data_ptr(), Ms, d_nmps[lo:].data_ptr(),
+                                                   1.0, d_out2[lo].data_ptr(), d_nm2[lo:].data_ptr(),
+                                                   stream=st.cuda_stream)
 
     def match():
-        m_motion.search_motion_batch_device(F0, fr1, d_tcw.data_ptr(), cam, d_last.data_ptr(), Ls,
-                                            d_nlast.data_ptr(), 15.0, d_out1.data_ptr(), d_nm1.data_ptr(),
-                                            stream=stream)
-        torch.ge(d_out1, 0, out=d_taken.view(torch.bool))
-        m_local.search_by_projection_batch_device(F0, fr2, d_mps.data_ptr(), Ms, d_nmps.data_ptr(), 1.0,
-                                                  d_out2.data_ptr(), d_nm2.data_ptr(), stream=stream)
+        for ln in lanes:
+            match_lane(ln)
+
+    def track_launch():
+        fork()
+        extract()
+        match()
+        join()
 
     lba_solver, lba_prob = None, None
     if cfg["lba"]:
@@ -252,8 +308,7 @@ def main():
         if graph is not None:
             graph.replay()
         else:
-            extract()
-            match()
+            track_launch()
 
     def step():
         th = None
@@ -272,8 +327,7 @@ def main():
         # the tracking step (~30 launches) replayed as one HIP graph: no per-launch host gaps
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=tstream):
-            extract()
-            match()
+            track_launch()
         torch.cuda.synchronize(dev)
         for _ in range(2):
             step()
@@ -301,20 +355,29 @@ def main():
     el = time.perf_counter() - t0
     # per-stage kernel times (HIP events around every launch, on the stream it runs on) from the same number of
     # eager tracking steps after the timed region: events cannot sit inside the replayed graph
-    ext.set_profiling(True)
-    m_motion.set_profiling(True)
-    m_local.set_profiling(True)
+    # The lanes run one after another here (synchronised in between), so every launch is timed standalone, as
+    # in a --lanes 1 rocprofv3 kernel trace; stage_ms_per_step sums the lanes (work per step, not wall time).
+    objs = [o for ln in lanes for o in (ln["ext"], ln["mm"], ln["ml"])]
+    for o in objs:
+        o.set_profiling(True)
     torch.cuda.synchronize(dev)
     for _ in range(args.steps):
-        extract()
-        match()
-    torch.cuda.synchronize(dev)
-    stages = dict(ext.stage_times())
-
-    sm1, sm2 = m_motion.stage_times(), m_local.stage_times()
-    for k in ("grid", "gather", "resolve"):
-        stages[k] = (sm1[k][0] + sm2[k][0], sm1[k][1] + sm2[k][1])
-    for o in (ext, m_motion, m_local):
+        for ln in lanes:
+            ln["stream"].wait_stream(tstream)
+            extract_lane(ln)
+            match_lane(ln)
+            tstream.wait_stream(ln["stream"])
+            torch.cuda.synchronize(dev)
+    stages = {}
+    for ln in lanes:
+        for k, v in ln["ext"].stage_times().items():
+            a = stages.get(k, (0.0, 0))
+            stages[k] = (a[0] + v[0], a[1] + v[1])
+        sm1, sm2 = ln["mm"].stage_times(), ln["ml"].stage_times()
+        for k in ("grid", "gather", "resolve"):
+            a = stages.get(k, (0.0, 0))
+            stages[k] = (a[0] + sm1[k][0] + sm2[k][0], a[1] + sm1[k][1] + sm2[k][1])
+    for o in objs:
         o.set_profiling(False)
     lba_stage = lba_solver.stage_times() if lba_solver is not None else None
     # single-frame latency (B = 1, one HIP graph, synchronised per frame): the per-frame view of the north-star target
@@ -334,30 +397,33 @@ def main():
         m_local.search_by_projection_batch_device(F0, fr2_1, d_mps.data_ptr(), Ms, d_nmps.data_ptr(), 1.0,
                                                   d_out2.data_ptr(), d_nm2.data_ptr(), stream=stream)
 
-    one_frame_launch()
-    torch.cuda.synchronize(dev)
-    g1 = None
-    if not args.no_graph:
-        g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, stream=tstream):
-            one_frame_launch()
+    def measure_latency():
+        one_frame_launch()
         torch.cuda.synchronize(dev)
+        g1 = None
+        if not args.no_graph:
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1, stream=tstream):
+                one_frame_launch()
+            torch.cuda.synchronize(dev)
 
-    def one_frame():
-        if g1 is not None:
-            g1.replay()
-        else:
-            one_frame_launch()
-        torch.cuda.synchronize(dev)
+        def one_frame():
+            if g1 is not None:
+                g1.replay()
+            else:
+                one_frame_launch()
+            torch.cuda.synchronize(dev)
 
-    for _ in range(5):
-        one_frame()
-    lat = []
-    for _ in range(50):
-        t1 = time.perf_counter()
-        one_frame()
-        lat.append((time.perf_counter() - t1) * 1e3)
-    latency_ms = float(np.median(lat))
+        for _ in range(5):
+            one_frame()
+        lat = []
+        for _ in range(50):
+            t1 = time.perf_counter()
+            one_frame()
+            lat.append((time.perf_counter() - t1) * 1e3)
+        return float(np.median(lat))
+
+    latency_ms = None if args.no_latency else measure_latency()
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -407,10 +473,11 @@ def main():
                        "last_frame_points": mean_last, "local_map_points": mean_mps,
                        "matches_motion_per_frame": float(nm1.mean()), "matches_local_per_frame": float(nm2.mean()),
                        "parallelism": f"agents{world} (one agent per GPU, independent)",
+                       "lanes": NL,
                        "launch": "hip graph per tracking step" if graph is not None else "eager"},
             "stage_ms_per_step": per_step_ms,
             "latency_ms_per_frame_b1": latency_ms,
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "hbm", "kernel": dom, "limiter": ROOFLINE_NOTES.get(dom), "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": avg_ms},
         }
@@ -421,7 +488,8 @@ def main():
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
             out["cpu_baseline"]["latency_ms_per_frame"] = 1e3 / out["cpu_baseline"]["value"]
-            out["speedup_latency_b1"] = out["cpu_baseline"]["latency_ms_per_frame"] / latency_ms
+            if latency_ms:
+                out["speedup_latency_b1"] = out["cpu_baseline"]["latency_ms_per_frame"] / latency_ms
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -70,7 +70,8 @@ def traffic(fetch_db: str, write_db: str, out: str) -> None:
                     "for wide coalesced reads; Infinity-Cache hits are counted (MI355X_MICROARCH.md HBM section)",
            "kernels": kernels}
     for stage, prefix in STAGE_KERNELS.items():
-        hits = [v["bytes_per_launch"] for k, v in kernels.items() if k.startswith(prefix + "(") or k.startswith(prefix + "<")]
+        hits = [v["bytes_per_launch"] for k, v in kernels.items()
+                if k.removeprefix("void ").startswith(prefix + "(") or k.removeprefix("void ").startswith(prefix + "<")]
         if hits:
             res[stage] = sum(hits) / len(hits)
     json.dump(res, open(out, "w"), indent=1)
