@@ -31,6 +31,8 @@
 #include "../../include/mam_match.h"
 #include "runtime.hpp"
 
+#include <cstdio>
+
 namespace mam {
 
 constexpr int NCELLS = MAM_GRID_COLS * MAM_GRID_ROWS;
@@ -384,6 +386,12 @@ constexpr int CAND_LDS = 4096;    // candidate entries of one 64-unit chunk stag
 // (every earlier unit sharing one is already final). Ready units have pairwise disjoint candidate sets, so they
 // resolve and commit in parallel with exactly the sequential loop's result (ORBmatcher.cc:84-128 / :1745-1772):
 // taken bits, out[] (a later round = a later unit overwrites: last writer wins), match counts, rotation events.
+#ifdef MAM_RESOLVE_PROFILE
+__device__ unsigned long long g_rprof[2][8];
+#define RPROF(k) do { __syncthreads(); if (t == 0) { const long long tn = clock64(); atomicAdd(&g_rprof[p.mode][k], (unsigned long long)(tn - rp0)); rp0 = tn; } } while (0)
+#else
+#define RPROF(k) do {} while (0)
+#endif
 constexpr int RESOLVE_THREADS = 1024;
 constexpr int RESOLVE_POOL_LDS = 24576;   // candidate entries staged in LDS per frame (up to 96 KB)
 
@@ -402,57 +410,68 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
     __shared__ int s_nm, s_nev;
     const int n = frame_n(p.fr, f);
     int32_t* out = p.out + (size_t)f * S;
+#ifdef MAM_RESOLVE_PROFILE
+    long long rp0 = clock64();
+#endif
     if (p.out_n[f] < 0) return;   // grid stage flagged this frame
     if (p.pool_total[f] > p.ovf_cap) {   // a list did not fit its slot nor the overflow area
         if (t == 0) p.out_n[f] = MAM_ERR_CAPACITY;
         return;
     }
     const int nu = p.n_units[f];
-    const uint32_t* gpool = p.pool + (size_t)f * p.pool_per_frame;
-    for (int i = t; i < n; i += RESOLVE_THREADS) out[i] = -1;
-    for (int w = t; w < nwords; w += RESOLVE_THREADS) {
-        uint32_t bits = 0;
-        if (p.fr.taken)
-            for (int b = 0; b < 32; b++) {
-                const int i = w * 32 + b;
-                if (i < n && p.fr.taken[(size_t)f * S + i]) bits |= 1u << b;
-            }
-        takenb[w] = bits;
-    }
-    for (int i = t; i < S; i += RESOLVE_THREADS) { minU[i] = 0x7FFFFFFF; minA[i] = 0x7FFFFFFF; outU[i] = -1; }
-    if (t < MAM_HISTO_LENGTH) hist[t] = 0;
-    if (t == 0) { s_nm = 0; s_nev = 0; }
-    const int32_t* cc = p.cand_cnt + (size_t)f * p.unit_stride;
-    const int32_t* co = p.cand_off + (size_t)f * p.unit_stride;
-    uint32_t* ev = p.events + (size_t)f * p.unit_stride;
-    const mam_keypoint* K = p.fr.keys + (size_t)f * S;
-    // A candidate is RELEVANT to its unit if its taken state can change the unit's result: dist <= TH_HIGH (it
-    // could be the pick) or, in the ratio-tested local search, dist <= TH_HIGH / nnratio (it could be the second
-    // best that fails the test). Irrelevant candidates never change a result, so the lists are filtered to the
-    // relevant ones while they are staged in LDS.
-    const int rel = p.mode == 1 ? MAM_TH_HIGH
-                                : (p.nnratio > 0.f ? min(256, (int)ceilf((float)MAM_TH_HIGH / p.nnratio) + 1) : 256);
     // each thread owns units t, t + 1024, ... (at most UPT)
     constexpr int UPT = 4;
     if (nu > UPT * RESOLVE_THREADS) {
         if (t == 0) p.out_n[f] = MAM_ERR_CAPACITY;
         return;
     }
-    int ucnt[UPT], uoff[UPT];
-    int mysum = 0;
+    const uint32_t* gpool = p.pool + (size_t)f * p.pool_per_frame;
+    const int32_t* cc = p.cand_cnt + (size_t)f * p.unit_stride;
+    const int32_t* co = p.cand_off + (size_t)f * p.unit_stride;
+    uint32_t* ev = p.events + (size_t)f * p.unit_stride;
+    const mam_keypoint* K = p.fr.keys + (size_t)f * S;
+    // per-unit scalars first (global loads in flight together): list count / offset, nObs
+    int ucnt[UPT], uoff[UPT], unobs[UPT];
 #pragma unroll
     for (int k = 0; k < UPT; k++) {
         const int u = t + k * RESOLVE_THREADS;
-        int c = 0;
+        ucnt[k] = 0;
+        uoff[k] = 0;
+        unobs[k] = 0;
         if (u < nu) {
-            const uint32_t* lst = gpool + co[u];
-            const int cnt = cc[u];
-            for (int q = 0; q < cnt; q++) c += (int)((lst[q] >> 16) & 0x1FFu) <= rel ? 1 : 0;
+            ucnt[k] = cc[u];
+            uoff[k] = co[u];
+            unobs[k] = p.mode == 0 ? p.mps[(size_t)f * p.unit_stride + u].nobs
+                                   : p.last[(size_t)f * p.unit_stride + u].nobs;
         }
-        ucnt[k] = c;
-        mysum += c;
     }
-    // block exclusive scan of the per-thread relevant counts
+    for (int i = t; i < n; i += RESOLVE_THREADS) out[i] = -1;
+    if (p.fr.taken) {
+        const uint8_t* tk = p.fr.taken + (size_t)f * S;
+        for (int w = t; w < nwords; w += RESOLVE_THREADS) {
+            uint8_t v[32];
+#pragma unroll
+            for (int b = 0; b < 32; b++) v[b] = w * 32 + b < n ? tk[w * 32 + b] : 0;
+            uint32_t bits = 0;
+#pragma unroll
+            for (int b = 0; b < 32; b++) bits |= (v[b] ? 1u : 0u) << b;
+            takenb[w] = bits;
+        }
+    } else {
+        for (int w = t; w < nwords; w += RESOLVE_THREADS) takenb[w] = 0;
+    }
+    for (int i = t; i < S; i += RESOLVE_THREADS) { minU[i] = 0x7FFFFFFF; minA[i] = 0x7FFFFFFF; outU[i] = -1; }
+    if (t < MAM_HISTO_LENGTH) hist[t] = 0;
+    if (t == 0) { s_nm = 0; s_nev = 0; }
+    // A candidate is RELEVANT to its unit if its taken state can change the unit's result: dist <= TH_HIGH (it
+    // could be the pick) or, in the ratio-tested local search, dist <= TH_HIGH / nnratio (it could be the second
+    // best that fails the test). k_gather keeps only relevant candidates (same rel_threshold), so the lists are
+    // staged as they are.
+    const int rel = rel_threshold(p);
+    int mysum = 0;
+#pragma unroll
+    for (int k = 0; k < UPT; k++) mysum += ucnt[k];
+    // block exclusive scan of the per-thread counts
     __shared__ int wtot[RESOLVE_THREADS / 64];
     const int incl = wave_incl_scan(mysum);
     if ((t & 63) == 63) wtot[t >> 6] = incl;
@@ -463,72 +482,78 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
         total += wtot[w];
     }
     const bool staged = total <= p.pool_lds;
+    if (staged) {
 #pragma unroll
-    for (int k = 0; k < UPT; k++) {
-        const int u = t + k * RESOLVE_THREADS;
-        if (u >= nu) { uoff[k] = 0; continue; }
-        if (staged) {
-            uoff[k] = base;
-            const uint32_t* lst = gpool + co[u];
-            const int cnt = cc[u];
-            for (int q = 0; q < cnt; q++) {
-                const uint32_t e = lst[q];
-                if ((int)((e >> 16) & 0x1FFu) <= rel) cpool[base++] = e;
+        for (int k = 0; k < UPT; k++) {
+            const uint32_t* lst = gpool + uoff[k];
+            const int cnt = ucnt[k];
+            int q = 0;
+            for (; q + 4 <= cnt; q += 4) {   // four loads in flight per step
+                const uint32_t e0 = lst[q], e1 = lst[q + 1], e2 = lst[q + 2], e3 = lst[q + 3];
+                cpool[base + q] = e0;
+                cpool[base + q + 1] = e1;
+                cpool[base + q + 2] = e2;
+                cpool[base + q + 3] = e3;
             }
-        } else {
-            uoff[k] = co[u];     // unfiltered global list (same results, more work)
-            ucnt[k] = cc[u];
+            for (; q < cnt; q++) cpool[base + q] = lst[q];
+            uoff[k] = base;
+            base += cnt;
         }
     }
     const uint32_t* pool = staged ? cpool : gpool;
     unsigned open = 0, taker = 0;
 #pragma unroll
     for (int k = 0; k < UPT; k++) {
-        const int u = t + k * RESOLVE_THREADS;
-        if (u < nu && ucnt[k] > 0) {
+        if (ucnt[k] > 0) {
             open |= 1u << k;
-            const int nobs = p.mode == 0 ? p.mps[(size_t)f * p.unit_stride + u].nobs
-                                         : p.last[(size_t)f * p.unit_stride + u].nobs;
-            if (nobs > 0) taker |= 1u << k;
+            if (unobs[k] > 0) taker |= 1u << k;
         }
     }
     int nm = 0;
     __syncthreads();
+    RPROF(0);
+    // Claims carry the round in their high bits, (0xFFF - round) << 12 | unit, so a later round's claim is always
+    // smaller than any earlier one and claims never need releasing: a value from an older round reads as "none".
+    int round = 0;
     while (__syncthreads_or(open != 0)) {
-        // (1) claims. A candidate k is RELEVANT to unit v if k's taken state can change v's result: dist <= TH_HIGH
-        //     (it could be the pick), or in the ratio-tested local search dist <= TH_HIGH / nnratio (it could be the
-        //     second best that fails the test). minU[k]: earliest open unit that could TAKE k (nobs > 0 and
-        //     dist <= TH_HIGH); minA[k]: earliest open unit to which k is relevant.
+#ifdef MAM_RESOLVE_PROFILE
+        if (t == 0) atomicAdd(&g_rprof[p.mode][6], 1ull);
+#endif
+        const int stamp = (0xFFF - round) << 12;
+        // (1) claims. minU[k]: earliest open unit that could TAKE k (nObs > 0 and dist <= TH_HIGH); minA[k]: earliest
+        //     open unit to which k is relevant.
         for (int k = 0; k < UPT; k++) {
             if (!((open >> k) & 1u)) continue;
-            const int u = t + k * RESOLVE_THREADS;
+            const int key = stamp | (t + k * RESOLVE_THREADS);
             const uint32_t* lst = pool + uoff[k];
             const int cnt = ucnt[k];
             const bool tk = (taker >> k) & 1u;
             for (int q = 0; q < cnt; q++) {
                 const uint32_t e = lst[q];
                 const int dist = (int)((e >> 16) & 0x1FFu);
-                if (dist <= rel) atomicMin(&minA[e & 0xFFFFu], u);
-                if (tk && dist <= MAM_TH_HIGH) atomicMin(&minU[e & 0xFFFFu], u);
+                atomicMin(&minA[e & 0xFFFFu], key);
+                if (tk && dist <= MAM_TH_HIGH) atomicMin(&minU[e & 0xFFFFu], key);
             }
         }
         __syncthreads();
+        RPROF(3);
         // (2) ready units resolve and commit
-        unsigned was_open = open;
         for (int k = 0; k < UPT; k++) {
             if (!((open >> k) & 1u)) continue;
             const int u = t + k * RESOLVE_THREADS;
+            const int key = stamp | u;
             const uint32_t* lst = pool + uoff[k];
             const int cnt = ucnt[k];
             // ready: no earlier open unit can take one of u's candidates, and (if u takes) no earlier open unit
-            // looks at a keypoint u could take
+            // looks at a keypoint u could take (a claim left from an older round is larger than any of this round's,
+            // so it never blocks)
             const bool tk = (taker >> k) & 1u;
             bool ready = true;
             for (int q = 0; q < cnt && ready; q++) {
                 const uint32_t e = lst[q];
                 const int dist = (int)((e >> 16) & 0x1FFu);
-                ready = (dist > rel || minU[e & 0xFFFFu] >= u) &&
-                        (!tk || dist > MAM_TH_HIGH || minA[e & 0xFFFFu] >= u);
+                const int mu = minU[e & 0xFFFFu], ma = minA[e & 0xFFFFu];
+                ready = mu >= key && (!tk || dist > MAM_TH_HIGH || ma >= key);
             }
             if (!ready) continue;
             open &= ~(1u << k);
@@ -551,43 +576,30 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
             bool assign = bestDist <= MAM_TH_HIGH;
             if (assign && p.mode == 0 && bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) assign = false;
             if (!assign) continue;
-            int nobs;
-            float lang = 0.f;
-            if (p.mode == 0) {
-                nobs = p.mps[(size_t)f * p.unit_stride + u].nobs;
-            } else {
-                nobs = p.last[(size_t)f * p.unit_stride + u].nobs;
-                lang = p.last[(size_t)f * p.unit_stride + u].angle;
-            }
             atomicMax(&outU[bestIdx], u);   // units that do not take may assign the same keypoint: last wins
-            if (nobs > 0) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
+            if (tk) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
             nm++;
-            if (p.mode == 1 && p.check_ori) {
-                const int bin = rot_bin(lang - K[bestIdx].angle);
-                ev[atomicAdd(&s_nev, 1)] = (uint32_t)bestIdx | ((uint32_t)bin << 16);
-            }
+            if (p.mode == 1 && p.check_ori) ev[atomicAdd(&s_nev, 1)] = (uint32_t)bestIdx | ((uint32_t)u << 16);
         }
-        __syncthreads();
-        // (3) release the claims of every unit that was open this round
-        for (int k = 0; k < UPT; k++) {
-            if (!((was_open >> k) & 1u)) continue;
-            const int u = t + k * RESOLVE_THREADS;
-            const uint32_t* lst = pool + uoff[k];
-            const int cnt = ucnt[k];
-            for (int q = 0; q < cnt; q++) {
-                minU[lst[q] & 0xFFFFu] = 0x7FFFFFFF;
-                minA[lst[q] & 0xFFFFu] = 0x7FFFFFFF;
-            }
-        }
+        round++;
+        RPROF(5);
     }
+    RPROF(1);
     atomicAdd(&s_nm, nm);
     __syncthreads();
     for (int i = t; i < n; i += RESOLVE_THREADS) out[i] = outU[i];
     __syncthreads();
     const int nev = s_nev;
-    // (4) rotation consistency (ORBmatcher.cc:1855-1884, ComputeThreeMaxima :2012-2053)
+    // (4) rotation consistency (ORBmatcher.cc:1855-1884, ComputeThreeMaxima :2012-2053); the bins of the
+    //     committed matches are computed here, all in parallel
     if (p.mode == 1 && p.check_ori) {
-        for (int e = t; e < nev; e += RESOLVE_THREADS) atomicAdd(&hist[ev[e] >> 16], 1);
+        for (int e = t; e < nev; e += RESOLVE_THREADS) {
+            const uint32_t v = ev[e];
+            const int idx = (int)(v & 0xFFFFu), u = (int)(v >> 16);
+            const int bin = rot_bin(p.last[(size_t)f * p.unit_stride + u].angle - K[idx].angle);
+            ev[e] = (uint32_t)idx | ((uint32_t)bin << 16);
+            atomicAdd(&hist[bin], 1);
+        }
         __syncthreads();
         if (t == 0) {
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
@@ -613,6 +625,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
         if (removed) atomicAdd(&s_nm, -removed);
         __syncthreads();
     }
+    RPROF(2);
+#ifdef MAM_RESOLVE_PROFILE
+    if (t == 0) atomicAdd(&g_rprof[p.mode][7], 1ull);
+#endif
     if (t == 0) p.out_n[f] = s_nm;
 }
 
@@ -811,6 +827,23 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
         hipLaunchKernelGGL(mam::k_resolve, dim3(F), dim3(mam::RESOLVE_THREADS), fixed + 4 * (size_t)a.pool_lds, s, a);
     }
     MAM_HIP(hipGetLastError());
+#ifdef MAM_RESOLVE_PROFILE
+    {
+        static int calls = 0;
+        if (++calls % 40 == 0) {
+            unsigned long long h[2][8];
+            MAM_HIP(hipStreamSynchronize(s));
+            MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::g_rprof), sizeof(h)));
+            for (int m = 0; m < 2; m++)
+                fprintf(stderr, "resolve mode %d cycles per WG: setup %.0f claims %.0f resolve %.0f release %.0f loopexit %.0f "
+                        "final %.0f; rounds/WG %.1f\n", m,
+                        (double)h[m][0] / std::max(1ull, h[m][7]), (double)h[m][3] / std::max(1ull, h[m][7]),
+                        (double)h[m][4] / std::max(1ull, h[m][7]), (double)h[m][5] / std::max(1ull, h[m][7]),
+                        (double)h[m][1] / std::max(1ull, h[m][7]),
+                        (double)h[m][2] / std::max(1ull, h[m][7]), (double)h[m][6] / std::max(1ull, h[m][7]));
+        }
+    }
+#endif
     return MAM_OK;
 }
 
