@@ -236,7 +236,9 @@ def main():
         lo = ln["lo"]
         ln["mm"] = ORBmatcher(0.9, True, device=local)
         ln["ml"] = ORBmatcher(0.8, True, device=local)
-        ln["fr1"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(), None)
+        # the motion search leaves the frame's slot state in d_taken (taken_out): the local search's `taken` input
+        ln["fr1"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(), None,
+                              d_taken[lo].data_ptr())
         ln["fr2"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(),
                               d_taken[lo].data_ptr())
     m_motion, m_local = lanes[0]["mm"], lanes[0]["ml"]
@@ -246,8 +248,6 @@ def main():
         ln["mm"].search_motion_batch_device(F0, ln["fr1"], d_tcw.data_ptr() + lo * tcw_bytes, cam,
                                             d_last[lo].data_ptr(), Ls, d_nlast[lo:].data_ptr(), 15.0,
                                             d_out1[lo].data_ptr(), d_nm1[lo:].data_ptr(), stream=st.cuda_stream)
-        with torch.cuda.stream(st):
-            torch.ge(d_out1[lo:lo + BL], 0, out=d_taken[lo:lo + BL].view(torch.bool))
         ln["ml"].search_by_projection_batch_device(F0, ln["fr2"], d_mps[lo].data_ptr(), Ms, d_nmps[lo:].data_ptr(),
                                                    1.0, d_out2[lo].data_ptr(), d_nm2[lo:].data_ptr(),
                                                    stream=st.cuda_stream)
@@ -384,7 +384,7 @@ def main():
     ext.set_profiling(False)
     m_motion.set_profiling(False)
     m_local.set_profiling(False)
-    fr1_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), None)
+    fr1_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), None, d_taken.data_ptr())
     fr2_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), d_taken.data_ptr())
 
     def one_frame_launch():
@@ -393,7 +393,6 @@ def main():
         m_motion.search_motion_batch_device(F0, fr1_1, d_tcw.data_ptr(), cam, d_last.data_ptr(), Ls,
                                             d_nlast.data_ptr(), 15.0, d_out1.data_ptr(), d_nm1.data_ptr(),
                                             stream=stream)
-        torch.ge(d_out1[:1], 0, out=d_taken[:1].view(torch.bool))
         m_local.search_by_projection_batch_device(F0, fr2_1, d_mps.data_ptr(), Ms, d_nmps.data_ptr(), 1.0,
                                                   d_out2.data_ptr(), d_nm2.data_ptr(), stream=stream)
 

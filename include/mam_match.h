@@ -140,6 +140,9 @@ typedef struct mam_frames_dev {
     const uint8_t* desc;
     const int32_t* counts;
     const uint8_t* taken;     /* [nframes][kp_stride] or NULL */
+    uint8_t* taken_out;       /* [nframes][kp_stride] or NULL: the slot state after a projection search (1 =
+                                 mvpMapPoints[i] holds a MapPoint with Observations() > 0, rotation-cleared
+                                 slots 0), i.e. the `taken` input of the frame's next search */
 } mam_frames_dev;
 
 /* Frame f matches n_mps[f] MapPoints at mps + f*mp_stride. Outputs at out_kp_to_mp + f*kp_stride and

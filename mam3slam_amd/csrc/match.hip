@@ -74,6 +74,7 @@ struct ProjArgs {
     int ovf_cap;              // per-frame overflow area for longer lists (pool_total = used)
     uint32_t* events;         // [F][unit_stride]
     int pool_lds;             // candidate entries the resolve stage stages in LDS
+    int flat_lds;             // LDS bytes after the per-keypoint arrays (the flat resolve's unit + entry arrays)
     int32_t* out;             // [F][kp_stride]
     int32_t* out_n;           // [F]
 };
@@ -129,10 +130,11 @@ __global__ __launch_bounds__(1024) void k_grid(ProjArgs p) {
     __shared__ int wsum[16];
     const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int n = frame_n(p.fr, f);
-    if (n > GRID_SORT_MAX) {
-        if (tid == 0) p.out_n[f] = MAM_ERR_CAPACITY;
-        return;
+    if (tid == 0) {   // per-call state of frame f (k_gather and k_resolve run after this kernel on the stream)
+        p.out_n[f] = n > GRID_SORT_MAX ? MAM_ERR_CAPACITY : 0;
+        p.pool_total[f] = 0;
     }
+    if (n > GRID_SORT_MAX) return;
     const mam_keypoint* K = p.fr.keys + (size_t)f * p.fr.kp_stride;
     for (int c = tid; c <= NCELLS; c += 1024) cnt[c] = 0;
     __syncthreads();
@@ -393,6 +395,14 @@ __device__ unsigned long long g_rprof[2][8];
 #define RPROF(k) do {} while (0)
 #endif
 constexpr int RESOLVE_THREADS = 1024;
+
+__host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~(size_t)15; }
+// flat resolve carve after the per-keypoint arrays: ebase, best, second (u32 per unit), flags, notready (u8 per
+// unit), entries (u32) and their units (u16)
+__host__ __device__ inline size_t flat_carve_bytes(int nu, int ne) {
+    return a16((size_t)(nu + 1) * 4) + 2 * a16((size_t)nu * 4) + 2 * a16((size_t)nu) + a16((size_t)ne * 4) +
+           a16((size_t)ne * 2);
+}
 constexpr int RESOLVE_POOL_LDS = 24576;   // candidate entries staged in LDS per frame (up to 96 KB)
 
 __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
@@ -467,122 +477,296 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
     // could be the pick) or, in the ratio-tested local search, dist <= TH_HIGH / nnratio (it could be the second
     // best that fails the test). k_gather keeps only relevant candidates (same rel_threshold), so the lists are
     // staged as they are.
-    const int rel = rel_threshold(p);
-    int mysum = 0;
-#pragma unroll
-    for (int k = 0; k < UPT; k++) mysum += ucnt[k];
-    // block exclusive scan of the per-thread counts
-    __shared__ int wtot[RESOLVE_THREADS / 64];
-    const int incl = wave_incl_scan(mysum);
-    if ((t & 63) == 63) wtot[t >> 6] = incl;
-    __syncthreads();
-    int base = incl - mysum, total = 0;
-    for (int w = 0; w < RESOLVE_THREADS / 64; w++) {
-        if (w < (t >> 6)) base += wtot[w];
-        total += wtot[w];
-    }
-    const bool staged = total <= p.pool_lds;
-    if (staged) {
-#pragma unroll
-        for (int k = 0; k < UPT; k++) {
-            const uint32_t* lst = gpool + uoff[k];
-            const int cnt = ucnt[k];
-            int q = 0;
-            for (; q + 4 <= cnt; q += 4) {   // four loads in flight per step
-                const uint32_t e0 = lst[q], e1 = lst[q + 1], e2 = lst[q + 2], e3 = lst[q + 3];
-                cpool[base + q] = e0;
-                cpool[base + q + 1] = e1;
-                cpool[base + q + 2] = e2;
-                cpool[base + q + 3] = e3;
-            }
-            for (; q < cnt; q++) cpool[base + q] = lst[q];
-            uoff[k] = base;
-            base += cnt;
-        }
-    }
-    const uint32_t* pool = staged ? cpool : gpool;
-    unsigned open = 0, taker = 0;
-#pragma unroll
-    for (int k = 0; k < UPT; k++) {
-        if (ucnt[k] > 0) {
-            open |= 1u << k;
-            if (unobs[k] > 0) taker |= 1u << k;
-        }
-    }
     int nm = 0;
-    __syncthreads();
-    RPROF(0);
-    // Claims carry the round in their high bits, (0xFFF - round) << 12 | unit, so a later round's claim is always
-    // smaller than any earlier one and claims never need releasing: a value from an older round reads as "none".
-    int round = 0;
-    while (__syncthreads_or(open != 0)) {
-#ifdef MAM_RESOLVE_PROFILE
-        if (t == 0) atomicAdd(&g_rprof[p.mode][6], 1ull);
-#endif
-        const int stamp = (0xFFF - round) << 12;
-        // (1) claims. minU[k]: earliest open unit that could TAKE k (nObs > 0 and dist <= TH_HIGH); minA[k]: earliest
-        //     open unit to which k is relevant.
+    // ---- flat path: the candidate lists as one entry array (entry -> unit), every round a few passes over the
+    //      entries dealt evenly to all threads; per-unit best / second best by LDS atomicMin on (dist << 16 | entry)
+    //      (the first minimum in list order is the sequential loop's best, the first minimum of the rest its second
+    //      best, ORBmatcher.cc:94-112). Falls back to the per-unit loop below when the entries do not fit in LDS.
+    __shared__ int wtot4[UPT][RESOLVE_THREADS / 64];
+    {
+#pragma unroll
         for (int k = 0; k < UPT; k++) {
-            if (!((open >> k) & 1u)) continue;
-            const int key = stamp | (t + k * RESOLVE_THREADS);
-            const uint32_t* lst = pool + uoff[k];
-            const int cnt = ucnt[k];
-            const bool tk = (taker >> k) & 1u;
-            for (int q = 0; q < cnt; q++) {
-                const uint32_t e = lst[q];
-                const int dist = (int)((e >> 16) & 0x1FFu);
-                atomicMin(&minA[e & 0xFFFFu], key);
-                if (tk && dist <= MAM_TH_HIGH) atomicMin(&minU[e & 0xFFFFu], key);
+            const int incl = wave_incl_scan(ucnt[k]);
+            if ((t & 63) == 63) wtot4[k][t >> 6] = incl;
+        }
+    }
+    __syncthreads();
+    int ebase_k[UPT], etotal = 0;
+    {
+        int carry = 0;
+#pragma unroll
+        for (int k = 0; k < UPT; k++) {
+            int pre = 0, tot = 0;
+            for (int w = 0; w < RESOLVE_THREADS / 64; w++) {
+                const int v = wtot4[k][w];
+                if (w < (t >> 6)) pre += v;
+                tot += v;
+            }
+            ebase_k[k] = carry + pre + wave_incl_scan(ucnt[k]) - ucnt[k];
+            carry += tot;
+        }
+        etotal = carry;
+    }
+    const size_t flat_bytes = flat_carve_bytes(nu, etotal);
+    if (etotal <= 0xFFFF && flat_bytes <= (size_t)p.flat_lds) {
+        uint8_t* fp = reinterpret_cast<uint8_t*>(cpool);
+        int* ebase = reinterpret_cast<int*>(fp);                         fp += a16((size_t)(nu + 1) * 4);
+        uint32_t* best = reinterpret_cast<uint32_t*>(fp);                 fp += a16((size_t)nu * 4);   // list offset first
+        uint32_t* second = reinterpret_cast<uint32_t*>(fp);               fp += a16((size_t)nu * 4);
+        uint8_t* flags = fp;                                              fp += a16((size_t)nu);       // 1 open, 2 taker
+        uint8_t* notready = fp;                                           fp += a16((size_t)nu);
+        uint32_t* epool = reinterpret_cast<uint32_t*>(fp);                fp += a16((size_t)etotal * 4);
+        uint16_t* eunit = reinterpret_cast<uint16_t*>(fp);
+        unsigned open = 0;
+#pragma unroll
+        for (int k = 0; k < UPT; k++) {
+            const int u = t + k * RESOLVE_THREADS;
+            if (u < nu) {
+                const bool op = ucnt[k] > 0;
+                ebase[u] = ebase_k[k];
+                best[u] = (uint32_t)uoff[k];
+                second[u] = 0xFFFFFFFFu;
+                flags[u] = (op ? 1 : 0) | (unobs[k] > 0 ? 2 : 0);
+                notready[u] = 0;
+                if (op) open |= 1u << k;
+            }
+        }
+        if (t == 0) ebase[nu] = etotal;
+        __syncthreads();
+        // entries in unit order: entry i belongs to the last unit with ebase <= i; all global loads of a pass in
+        // flight together
+        for (int i0 = 0; i0 < etotal; i0 += 4 * RESOLVE_THREADS) {
+            uint32_t v[4];
+            int uu[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int i = i0 + q * RESOLVE_THREADS + t;
+                v[q] = 0;
+                uu[q] = 0;
+                if (i < etotal) {
+                    int lo = 0, hi = nu;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (ebase[mid] <= i) lo = mid;
+                        else hi = mid;
+                    }
+                    uu[q] = lo;
+                    v[q] = gpool[best[lo] + (i - ebase[lo])];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int i = i0 + q * RESOLVE_THREADS + t;
+                if (i < etotal) { epool[i] = v[q]; eunit[i] = (uint16_t)uu[q]; }
             }
         }
         __syncthreads();
-        RPROF(3);
-        // (2) ready units resolve and commit
-        for (int k = 0; k < UPT; k++) {
-            if (!((open >> k) & 1u)) continue;
-            const int u = t + k * RESOLVE_THREADS;
-            const int key = stamp | u;
-            const uint32_t* lst = pool + uoff[k];
-            const int cnt = ucnt[k];
-            // ready: no earlier open unit can take one of u's candidates, and (if u takes) no earlier open unit
-            // looks at a keypoint u could take (a claim left from an older round is larger than any of this round's,
-            // so it never blocks)
-            const bool tk = (taker >> k) & 1u;
-            bool ready = true;
-            for (int q = 0; q < cnt && ready; q++) {
-                const uint32_t e = lst[q];
-                const int dist = (int)((e >> 16) & 0x1FFu);
-                const int mu = minU[e & 0xFFFFu], ma = minA[e & 0xFFFFu];
-                ready = mu >= key && (!tk || dist > MAM_TH_HIGH || ma >= key);
+        for (int u = t; u < nu; u += RESOLVE_THREADS) best[u] = 0xFFFFFFFFu;
+        RPROF(0);
+        int round = 0;
+        while (__syncthreads_or(open != 0)) {
+#ifdef MAM_RESOLVE_PROFILE
+            if (t == 0) atomicAdd(&g_rprof[p.mode][6], 1ull);
+#endif
+            const int stamp = (0xFFF - round) << 12;
+            // (1) claims (see the per-unit loop below for minU / minA)
+            for (int i = t; i < etotal; i += RESOLVE_THREADS) {
+                const int u = eunit[i];
+                const int fl = flags[u];
+                if (!(fl & 1)) continue;
+                const uint32_t e = epool[i];
+                const int key = stamp | u;
+                atomicMin(&minA[e & 0xFFFFu], key);
+                if ((fl & 2) && (int)((e >> 16) & 0x1FFu) <= MAM_TH_HIGH) atomicMin(&minU[e & 0xFFFFu], key);
             }
-            if (!ready) continue;
-            open &= ~(1u << k);
-            int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
-            for (int q = 0; q < cnt; q++) {
-                const uint32_t e = lst[q];
+            __syncthreads();
+            RPROF(3);
+            // (2) readiness: one failing candidate makes its unit wait a round
+            for (int i = t; i < etotal; i += RESOLVE_THREADS) {
+                const int u = eunit[i];
+                const int fl = flags[u];
+                if (!(fl & 1)) continue;
+                const uint32_t e = epool[i];
+                const int key = stamp | u;
+                const int dist = (int)((e >> 16) & 0x1FFu);
+                const bool ok = minU[e & 0xFFFFu] >= key && (!(fl & 2) || dist > MAM_TH_HIGH || minA[e & 0xFFFFu] >= key);
+                if (!ok) notready[u] = 1;
+            }
+            __syncthreads();
+            // (3) best untaken candidate of every ready unit
+            for (int i = t; i < etotal; i += RESOLVE_THREADS) {
+                const int u = eunit[i];
+                if (!(flags[u] & 1) || notready[u]) continue;
+                const uint32_t e = epool[i];
                 const int idx = (int)(e & 0xFFFFu);
                 if ((takenb[idx >> 5] >> (idx & 31)) & 1u) continue;
-                const int dist = (int)((e >> 16) & 0x1FFu);
-                const int lvl = (int)(e >> 25);
-                if (dist < bestDist) {
-                    bestDist2 = bestDist; bestDist = dist;
-                    bestLevel2 = bestLevel; bestLevel = lvl;
-                    bestIdx = idx;
-                } else if (dist < bestDist2) {
-                    bestLevel2 = lvl;
-                    bestDist2 = dist;
+                atomicMin(&best[u], (((e >> 16) & 0x1FFu) << 16) | (uint32_t)i);
+            }
+            __syncthreads();
+            // (4) second best (the ratio test of the local-map search)
+            if (p.mode == 0) {
+                for (int i = t; i < etotal; i += RESOLVE_THREADS) {
+                    const int u = eunit[i];
+                    if (!(flags[u] & 1) || notready[u]) continue;
+                    const uint32_t b = best[u];
+                    if (b == 0xFFFFFFFFu || (int)(b & 0xFFFFu) == i) continue;
+                    const uint32_t e = epool[i];
+                    const int idx = (int)(e & 0xFFFFu);
+                    if ((takenb[idx >> 5] >> (idx & 31)) & 1u) continue;
+                    atomicMin(&second[u], (((e >> 16) & 0x1FFu) << 16) | (uint32_t)i);
+                }
+                __syncthreads();
+            }
+            // (5) ready units commit (each thread its own units)
+#pragma unroll
+            for (int k = 0; k < UPT; k++) {
+                if (!((open >> k) & 1u)) continue;
+                const int u = t + k * RESOLVE_THREADS;
+                if (notready[u]) {
+                    notready[u] = 0;
+                    best[u] = 0xFFFFFFFFu;
+                    second[u] = 0xFFFFFFFFu;
+                    continue;
+                }
+                open &= ~(1u << k);
+                flags[u] = 0;
+                const uint32_t b = best[u];
+                if (b == 0xFFFFFFFFu) continue;
+                const uint32_t eb = epool[b & 0xFFFFu];
+                const int bestDist = (int)(b >> 16), bestLevel = (int)(eb >> 25), bestIdx = (int)(eb & 0xFFFFu);
+                bool assign = bestDist <= MAM_TH_HIGH;
+                if (assign && p.mode == 0) {
+                    const uint32_t s2 = second[u];
+                    const int bestDist2 = s2 == 0xFFFFFFFFu ? 256 : (int)(s2 >> 16);
+                    const int bestLevel2 = s2 == 0xFFFFFFFFu ? -1 : (int)(epool[s2 & 0xFFFFu] >> 25);
+                    if (bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) assign = false;
+                }
+                if (!assign) continue;
+                atomicMax(&outU[bestIdx], u);
+                if ((unobs[k] > 0)) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
+                nm++;
+                if (p.mode == 1 && p.check_ori) ev[atomicAdd(&s_nev, 1)] = (uint32_t)bestIdx | ((uint32_t)u << 16);
+            }
+            round++;
+            RPROF(5);
+        }
+    } else {
+        const int rel = rel_threshold(p);
+        int mysum = 0;
+    #pragma unroll
+        for (int k = 0; k < UPT; k++) mysum += ucnt[k];
+        // block exclusive scan of the per-thread counts
+        __shared__ int wtot[RESOLVE_THREADS / 64];
+        const int incl = wave_incl_scan(mysum);
+        if ((t & 63) == 63) wtot[t >> 6] = incl;
+        __syncthreads();
+        int base = incl - mysum, total = 0;
+        for (int w = 0; w < RESOLVE_THREADS / 64; w++) {
+            if (w < (t >> 6)) base += wtot[w];
+            total += wtot[w];
+        }
+        const bool staged = total <= p.pool_lds;
+        if (staged) {
+    #pragma unroll
+            for (int k = 0; k < UPT; k++) {
+                const uint32_t* lst = gpool + uoff[k];
+                const int cnt = ucnt[k];
+                int q = 0;
+                for (; q + 4 <= cnt; q += 4) {   // four loads in flight per step
+                    const uint32_t e0 = lst[q], e1 = lst[q + 1], e2 = lst[q + 2], e3 = lst[q + 3];
+                    cpool[base + q] = e0;
+                    cpool[base + q + 1] = e1;
+                    cpool[base + q + 2] = e2;
+                    cpool[base + q + 3] = e3;
+                }
+                for (; q < cnt; q++) cpool[base + q] = lst[q];
+                uoff[k] = base;
+                base += cnt;
+            }
+        }
+        const uint32_t* pool = staged ? cpool : gpool;
+        unsigned open = 0, taker = 0;
+    #pragma unroll
+        for (int k = 0; k < UPT; k++) {
+            if (ucnt[k] > 0) {
+                open |= 1u << k;
+                if (unobs[k] > 0) taker |= 1u << k;
+            }
+        }
+        __syncthreads();
+        RPROF(0);
+        // Claims carry the round in their high bits, (0xFFF - round) << 12 | unit, so a later round's claim is always
+        // smaller than any earlier one and claims never need releasing: a value from an older round reads as "none".
+        int round = 0;
+        while (__syncthreads_or(open != 0)) {
+    #ifdef MAM_RESOLVE_PROFILE
+            if (t == 0) atomicAdd(&g_rprof[p.mode][6], 1ull);
+    #endif
+            const int stamp = (0xFFF - round) << 12;
+            // (1) claims. minU[k]: earliest open unit that could TAKE k (nObs > 0 and dist <= TH_HIGH); minA[k]: earliest
+            //     open unit to which k is relevant.
+            for (int k = 0; k < UPT; k++) {
+                if (!((open >> k) & 1u)) continue;
+                const int key = stamp | (t + k * RESOLVE_THREADS);
+                const uint32_t* lst = pool + uoff[k];
+                const int cnt = ucnt[k];
+                const bool tk = (taker >> k) & 1u;
+                for (int q = 0; q < cnt; q++) {
+                    const uint32_t e = lst[q];
+                    const int dist = (int)((e >> 16) & 0x1FFu);
+                    atomicMin(&minA[e & 0xFFFFu], key);
+                    if (tk && dist <= MAM_TH_HIGH) atomicMin(&minU[e & 0xFFFFu], key);
                 }
             }
-            bool assign = bestDist <= MAM_TH_HIGH;
-            if (assign && p.mode == 0 && bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) assign = false;
-            if (!assign) continue;
-            atomicMax(&outU[bestIdx], u);   // units that do not take may assign the same keypoint: last wins
-            if (tk) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
-            nm++;
-            if (p.mode == 1 && p.check_ori) ev[atomicAdd(&s_nev, 1)] = (uint32_t)bestIdx | ((uint32_t)u << 16);
+            __syncthreads();
+            RPROF(3);
+            // (2) ready units resolve and commit
+            for (int k = 0; k < UPT; k++) {
+                if (!((open >> k) & 1u)) continue;
+                const int u = t + k * RESOLVE_THREADS;
+                const int key = stamp | u;
+                const uint32_t* lst = pool + uoff[k];
+                const int cnt = ucnt[k];
+                // ready: no earlier open unit can take one of u's candidates, and (if u takes) no earlier open unit
+                // looks at a keypoint u could take (a claim left from an older round is larger than any of this round's,
+                // so it never blocks)
+                const bool tk = (taker >> k) & 1u;
+                bool ready = true;
+                for (int q = 0; q < cnt && ready; q++) {
+                    const uint32_t e = lst[q];
+                    const int dist = (int)((e >> 16) & 0x1FFu);
+                    const int mu = minU[e & 0xFFFFu], ma = minA[e & 0xFFFFu];
+                    ready = mu >= key && (!tk || dist > MAM_TH_HIGH || ma >= key);
+                }
+                if (!ready) continue;
+                open &= ~(1u << k);
+                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                for (int q = 0; q < cnt; q++) {
+                    const uint32_t e = lst[q];
+                    const int idx = (int)(e & 0xFFFFu);
+                    if ((takenb[idx >> 5] >> (idx & 31)) & 1u) continue;
+                    const int dist = (int)((e >> 16) & 0x1FFu);
+                    const int lvl = (int)(e >> 25);
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist; bestDist = dist;
+                        bestLevel2 = bestLevel; bestLevel = lvl;
+                        bestIdx = idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = lvl;
+                        bestDist2 = dist;
+                    }
+                }
+                bool assign = bestDist <= MAM_TH_HIGH;
+                if (assign && p.mode == 0 && bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) assign = false;
+                if (!assign) continue;
+                atomicMax(&outU[bestIdx], u);   // units that do not take may assign the same keypoint: last wins
+                if (tk) atomicOr(&takenb[bestIdx >> 5], 1u << (bestIdx & 31));
+                nm++;
+                if (p.mode == 1 && p.check_ori) ev[atomicAdd(&s_nev, 1)] = (uint32_t)bestIdx | ((uint32_t)u << 16);
+            }
+            round++;
+            RPROF(5);
         }
-        round++;
-        RPROF(5);
     }
     RPROF(1);
     atomicAdd(&s_nm, nm);
@@ -618,7 +802,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
         for (int e = t; e < nev; e += RESOLVE_THREADS) {
             const int bin = (int)(ev[e] >> 16);
             if (bin != top[0] && bin != top[1] && bin != top[2]) {
-                out[ev[e] & 0xFFFFu] = MAM_MATCH_CLEARED;
+                const uint32_t idx = ev[e] & 0xFFFFu;
+                out[idx] = MAM_MATCH_CLEARED;
+                atomicAnd(&takenb[idx >> 5], ~(1u << (idx & 31)));   // the slot becomes NULL
                 removed++;
             }
         }
@@ -629,6 +815,13 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
 #ifdef MAM_RESOLVE_PROFILE
     if (t == 0) atomicAdd(&g_rprof[p.mode][7], 1ull);
 #endif
+    if (p.fr.taken_out) {
+        // the frame's slot state after the call (mvpMapPoints[i] != NULL && Observations() > 0): what the next
+        // search of the same frame reads as `taken`
+        __syncthreads();
+        uint8_t* to = p.fr.taken_out + (size_t)f * S;
+        for (int i = t; i < S; i += RESOLVE_THREADS) to[i] = i < n ? (uint8_t)((takenb[i >> 5] >> (i & 31)) & 1u) : 0;
+    }
     if (t == 0) p.out_n[f] = s_nm;
 }
 
@@ -803,7 +996,6 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     a.pool = c->pool.p;
     a.pool_total = c->pool_total.p;
     a.events = c->events.p;
-    MAM_HIP(hipMemsetAsync(a.out_n, 0, sizeof(int32_t) * F, s));
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
         hipLaunchKernelGGL(mam::k_grid, dim3(F), dim3(1024), 0, s, a);
@@ -812,7 +1004,6 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     const int blocks = (int)((waves + 3) / 4);
     {
         mam::StageTimer::Scope sc(&c->timer, s, 1);
-        MAM_HIP(hipMemsetAsync(a.pool_total, 0, sizeof(int32_t) * F, s));
         hipLaunchKernelGGL(mam::k_gather, dim3(blocks), dim3(256), 0, s, a, F);
     }
     {
@@ -824,7 +1015,8 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
             return MAM_ERR_CAPACITY;
         }
         a.pool_lds = (int)std::min<size_t>((size_t)mam::RESOLVE_POOL_LDS, (c->resolve_lds_max - fixed) / 4);
-        hipLaunchKernelGGL(mam::k_resolve, dim3(F), dim3(mam::RESOLVE_THREADS), fixed + 4 * (size_t)a.pool_lds, s, a);
+        a.flat_lds = (int)(c->resolve_lds_max - fixed);
+        hipLaunchKernelGGL(mam::k_resolve, dim3(F), dim3(mam::RESOLVE_THREADS), c->resolve_lds_max, s, a);
     }
     MAM_HIP(hipGetLastError());
 #ifdef MAM_RESOLVE_PROFILE
@@ -980,6 +1172,7 @@ static int stage_frame(mam_match_ctx* c, int n, const mam_keypoint* keys, const 
     fr->desc = dd;
     fr->counts = *dcount;
     fr->taken = taken ? dt : nullptr;
+    fr->taken_out = nullptr;
     return MAM_OK;
 }
 

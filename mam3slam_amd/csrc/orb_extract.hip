@@ -13,6 +13,8 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <map>
+#include <memory>
 #include <vector>
 
 #include "orb_common.hpp"
@@ -62,7 +64,17 @@ struct mam_orb_ctx {
     DevBuf<uint8_t> d_desc;
     DevBuf<int32_t> d_counts;
     size_t fast_lds = 0, dist_lds = 0;
+    int dist_kcap = 0;   // candidates per level k_distribute keeps in LDS (more: global scratch)
     int fast_cw = 0;   // k_fast_cells plane pitch instance
+    // single-launch pyramid (k_pyr_bands): per band count, the band table and its LDS carve
+    struct PyrPlan {
+        int nb = 0;
+        size_t lds = 0;
+        int buf1_off = 0, rc_off = 0;
+        DevBuf<int4> bands;
+    };
+    std::vector<std::vector<int>> h_yofs;       // resize row tables per level (host copy, l >= 1)
+    std::map<int, std::unique_ptr<PyrPlan>> pyr_plans;
     // last-call bookkeeping for debug taps
     const uint8_t* last_in0 = nullptr;
     size_t last_stride = 0, last_fstride = 0;
@@ -148,6 +160,9 @@ size_t distribute_lds_bytes(int NC, int max_cells) {
     s += a16((size_t)NC * 16) + 3 * a16(NC * 4) + a16(NC * 8) + a16((max_cells + 1) * 4) + 64 + 64;
     return s;
 }
+
+int build_pyr_plan(mam_orb_ctx* c, int nb);
+int pyr_forced_bands();
 
 // Geometry for a W x H frame and capacity F (reallocates device scratch when either grows/changes).
 int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
@@ -247,9 +262,12 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         std::vector<short> al, be;
         std::vector<size_t> ioff(L, 0), soff(L, 0);
         std::vector<int> xmaxv(L, 0), xvecv(L, 0);
+        c->h_yofs.assign(L, {});
+        c->pyr_plans.clear();
         for (int l = 1; l < L; l++) {
             int xmax, xvec;
             resize_tables(g.L[l - 1].w, g.L[l - 1].h, g.L[l].w, g.L[l].h, xo, al, yo, be, &xmax, &xvec);
+            c->h_yofs[l] = yo;
             ioff[l] = ti.size();
             ti.insert(ti.end(), xo.begin(), xo.end());
             ti.insert(ti.end(), yo.begin(), yo.end());
@@ -258,6 +276,13 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
             ts.insert(ts.end(), be.begin(), be.end());
             xmaxv[l] = xmax;
             xvecv[l] = xvec;
+            // pyr_quad reads three source words per row: the four source columns of an output quad (and the +1 tap)
+            // must lie within 12 bytes of the quad's word-aligned first column (scale factors up to ~2.6)
+            for (int dx = 0; dx < g.L[l].w; dx += 4)
+                if (xo[std::min(dx + 3, g.L[l].w - 1)] - (xo[dx] & ~3) > 10) {
+                    g_last_error = "pyramid scale factor too large for the resize kernel";
+                    return MAM_ERR_ARG;
+                }
             // LDS staging bounds of k_pyr_down: source columns / rows one (PYR_XB x PYR_RB) output block reads
             const int sw = g.L[l - 1].w, sh = g.L[l - 1].h, dw = g.L[l].w, dh = g.L[l].h;
             for (int dx0 = 0; dx0 < dw; dx0 += mam::PYR_XB) {
@@ -299,10 +324,17 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
             }
         }
         c->dist_lds = distribute_lds_bytes(g.node_cap, maxcells);
+        // candidate keys + node ids in LDS (6 B each) up to a 64 KB workgroup (two per CU)
+        c->dist_kcap = (int)std::min<size_t>(16384, c->dist_lds < 60 * 1024 ? (64 * 1024 - c->dist_lds) / 6 : 0) & ~63;
+        c->dist_lds += (size_t)c->dist_kcap * 6 + 32;
         if (c->fast_lds > 160 * 1024 || c->dist_lds > 160 * 1024) {
             g_last_error = "LDS budget exceeded (nfeatures or cell size too large)";
             return MAM_ERR_ARG;
         }
+        for (int nb = 8; nb <= 64; nb += 8)
+            if (int rc = build_pyr_plan(c, nb)) return rc;
+        if (pyr_forced_bands() > 0 && pyr_forced_bands() % 8)
+            if (int rc = build_pyr_plan(c, pyr_forced_bands())) return rc;
         c->W = W;
         c->H = H;
     }
@@ -333,6 +365,79 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
 
 using StageScope = mam::StageTimer::Scope;
 
+// k_pyr_bands plan for nb bands: band j owns rows [h*j/nb, h*(j+1)/nb) of every level >= 1 and needs, per level, the
+// hull of its owned rows and the source rows (yofs of the level above, both taps, clamped) of the rows it needs one
+// level up. Returns nullptr when a band would own no row of the top level or the LDS carve exceeds `lds_max`.
+// Built for every candidate band count when the geometry is set up (no allocation or copy at launch time, so a
+// launch can be captured into a HIP graph).
+int build_pyr_plan(mam_orb_ctx* c, int nb) {
+    const mam::Geom& g = c->geom;
+    const int L = g.nlevels;
+    if (L < 2 || nb < 1 || nb > g.L[L - 1].h) return MAM_OK;
+    std::vector<int4> tab((size_t)nb * L);
+    size_t buf[2] = {0, 0}, rows_max = 0;
+    for (int j = 0; j < nb; j++) {
+        int4* B = &tab[(size_t)j * L];
+        for (int l = 0; l < L; l++) {
+            const long long h = g.L[l].h;
+            B[l].z = (int)(h * j / nb);
+            B[l].w = (int)(h * (j + 1) / nb);
+        }
+        B[L - 1].x = B[L - 1].z;
+        B[L - 1].y = B[L - 1].w;
+        for (int l = L - 2; l >= 0; l--) {
+            const std::vector<int>& yo = c->h_yofs[l + 1];
+            const int sh = g.L[l].h;
+            const int a = std::min(std::max(yo[B[l + 1].x], 0), sh - 1);
+            const int b = std::min(std::max(yo[B[l + 1].y - 1] + 1, 0), sh - 1) + 1;
+            B[l].x = l == 0 ? a : std::min(a, B[l].z);
+            B[l].y = l == 0 ? b : std::max(b, B[l].w);
+        }
+        size_t rows = 0;
+        for (int l = 0; l + 1 < L; l++)
+            buf[l & 1] = std::max(buf[l & 1], (size_t)(B[l].y - B[l].x) * ((g.L[l].w + 3) & ~3));
+        for (int l = 1; l < L; l++) rows += B[l].y - B[l].x;
+        rows_max = std::max(rows_max, rows);
+    }
+    auto plan = std::make_unique<mam_orb_ctx::PyrPlan>();
+    plan->nb = nb;
+    plan->buf1_off = (int)((buf[0] + 15) & ~(size_t)15);
+    plan->rc_off = (int)((plan->buf1_off + buf[1] + 15) & ~(size_t)15);
+    plan->lds = plan->rc_off + rows_max * 8 + 16;   // +16: pyr_quad's 12-byte window may run past the last row
+    if (plan->lds > 160 * 1024) return MAM_OK;
+    if (int rc = plan->bands.alloc(tab.size())) return rc;
+    MAM_HIP(hipMemcpy(plan->bands.p, tab.data(), tab.size() * sizeof(int4), hipMemcpyHostToDevice));
+    c->pyr_plans[nb] = std::move(plan);
+    return MAM_OK;
+}
+
+int pyr_forced_bands() {
+    static const int forced = [] {
+        const char* e = getenv("MAM_PYR_BANDS");
+        return e ? atoi(e) : -1;
+    }();
+    return forced;
+}
+
+mam_orb_ctx::PyrPlan* pyr_plan(mam_orb_ctx* c, int nb, size_t lds_max) {
+    auto it = c->pyr_plans.find(nb);
+    return it != c->pyr_plans.end() && it->second->lds <= lds_max ? it->second.get() : nullptr;
+}
+
+// The single-launch pyramid pays ~1.2-2x the arithmetic for one launch instead of nlevels-1: it wins for a few frames
+// (latency-bound launches), the per-level launches win for batches (MI355X, c1: 1 frame 34 vs 54 us; 64 frames
+// 0.67 vs 0.52 ms per 256). Few frames: as many bands as fit (shortest chain per workgroup).
+// MAM_PYR_BANDS=n forces n bands (0: per-level k_pyr_down launches).
+mam_orb_ctx::PyrPlan* choose_pyr_plan(mam_orb_ctx* c, int F) {
+    const int forced = pyr_forced_bands();
+    if (forced == 0) return nullptr;
+    if (forced > 0) return pyr_plan(c, forced, 160 * 1024);
+    if (F > 4) return nullptr;
+    for (int nb = 64; nb >= 8; nb -= 8)
+        if (mam_orb_ctx::PyrPlan* p = pyr_plan(c, nb, 96 * 1024)) return p;
+    return nullptr;
+}
+
 int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size_t fstride, int lap0, int lap1,
                  mam_keypoint* d_kps, uint8_t* d_desc, int capacity, int32_t* d_counts, hipStream_t s) {
     const mam::Geom& g = c->geom;
@@ -340,11 +445,16 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
     mam::LevelSrc src{d_in, stride, fstride, c->d_pyr.p};
     {
         StageScope sc(&c->timer, s, MAM_STAGE_PYRAMID);
-        const size_t lds = (size_t)g.pyr_seg_w * g.pyr_rows;
-        for (int l = 1; l < L; l++) {
-            const mam::LevelGeom& lv = g.L[l];
-            dim3 grid((lv.w + mam::PYR_XB - 1) / mam::PYR_XB, (lv.h + mam::PYR_RB - 1) / mam::PYR_RB, F);
-            hipLaunchKernelGGL(mam::k_pyr_down, grid, dim3(256), lds, s, c->d_geom.p, l, src, c->d_pyr.p);
+        if (mam_orb_ctx::PyrPlan* pp = choose_pyr_plan(c, F)) {
+            hipLaunchKernelGGL(mam::k_pyr_bands, dim3(pp->nb, F), dim3(256), pp->lds, s, c->d_geom.p, src, c->d_pyr.p,
+                               pp->bands.p, pp->buf1_off, pp->rc_off);
+        } else {
+            const size_t lds = (size_t)g.pyr_seg_w * g.pyr_rows + 16;   // pyr_quad's window past the last row
+            for (int l = 1; l < L; l++) {
+                const mam::LevelGeom& lv = g.L[l];
+                dim3 grid((lv.w + mam::PYR_XB - 1) / mam::PYR_XB, (lv.h + mam::PYR_RB - 1) / mam::PYR_RB, F);
+                hipLaunchKernelGGL(mam::k_pyr_down, grid, dim3(256), lds, s, c->d_geom.p, l, src, c->d_pyr.p);
+            }
         }
     }
     // (blur and FAST are both VALU-bound: running the blur on a second stream beside FAST + DistributeOctTree
@@ -371,7 +481,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
         StageScope sc(&c->timer, s, MAM_STAGE_DISTRIBUTE);
         hipLaunchKernelGGL(mam::k_distribute, dim3(L, F), dim3(256), c->dist_lds, s, c->d_geom.p, c->d_cellcnt.p,
                            c->d_cand.p, c->d_keys.p, c->d_knode.p, c->d_okey.p, c->d_orank.p, c->d_lvlcnt.p, lap0,
-                           lap1);
+                           lap1, c->dist_kcap);
     }
     {
         StageScope sc(&c->timer, s, MAM_STAGE_DESCRIBE);

@@ -106,9 +106,71 @@ __device__ __forceinline__ const uint8_t* level_ptr(const Geom* g, const LevelSr
 }
 
 // ------------------------------------------------------------------------------------------------ pyramid
-// OpenCV hal::resize INTER_LINEAR, CV_8UC1: exact-int horizontal pass
-// (HResizeLinear), vertical pass with VResizeLinearVec_32s8u's mulhi formula for x < xvec and
-// FixedPtCast<int,uchar,22> beyond. 4 output pixels per thread, one u32 store.
+// Column setup of one output quad dx..dx+3: its source columns sx[i] (and sx[i]+1) as byte offsets o[i] from the
+// word-aligned column `base`, horizontal weights (right-edge replicate columns dx >= xmax folded in as a0 = 2048,
+// a1 = 0: S[sx]*2048 + S[sx+1]*0 is the reference's S[sx]*2048) and which columns take the SIMD vertical formula
+// (dx < xvec). The host guarantees o[i] + 1 <= 11 (three source words per row).
+struct PyrQuad {
+    int base;
+    int o[4], a0[4], a1[4];
+    bool vec[4];
+};
+
+__device__ __forceinline__ void pyr_quad_setup(const LevelGeom& L, int dx, int sx_shift, PyrQuad& c) {
+    int sx[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int x = min(dx + i, L.w - 1);
+        sx[i] = L.xofs[x] - sx_shift;
+        const bool edge = dx + i >= L.xmax;
+        c.a0[i] = edge ? 2048 : L.ialpha[2 * x];
+        c.a1[i] = edge ? 0 : L.ialpha[2 * x + 1];
+        c.vec[i] = dx + i < L.xvec;
+    }
+    c.base = sx[0] & ~3;
+#pragma unroll
+    for (int i = 0; i < 4; i++) c.o[i] = sx[i] - c.base;
+}
+
+// bytes o and o+1 of the 12-byte window w0:w1:w2 (o <= 10), as (b0, b1)
+__device__ __forceinline__ void pyr_pair(uint32_t w0, uint32_t w1, uint32_t w2, int o, int& b0, int& b1) {
+    const uint32_t lo = o < 4 ? w0 : (o < 8 ? w1 : w2);
+    const uint32_t hi = o < 4 ? w1 : w2;
+    const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3));
+    b0 = (int)(v & 0xFFu);
+    b1 = (int)((v >> 8) & 0xFFu);
+}
+
+// Four output pixels of one output row from source rows S0 (ry0) and S1 (ry1) (word-aligned row starts): exact-int
+// horizontal pass (HResizeLinear), vertical pass with VResizeLinearVec_32s8u's mulhi formula for x < xvec and
+// FixedPtCast<int,uchar,22> beyond. Three word loads per source row.
+__device__ __forceinline__ uint32_t pyr_quad(const uint8_t* S0, const uint8_t* S1, const PyrQuad& c, int b0,
+                                             int b1) {
+    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(S0 + c.base);
+    const uint32_t* r1 = reinterpret_cast<const uint32_t*>(S1 + c.base);
+    const uint32_t x0 = r0[0], x1 = r0[1], x2 = r0[2];
+    const uint32_t y0 = r1[0], y1 = r1[1], y2 = r1[2];
+    uint32_t packed = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int p0, p1, q0, q1;
+        pyr_pair(x0, x1, x2, c.o[i], p0, p1);
+        pyr_pair(y0, y1, y2, c.o[i], q0, q1);
+        const int h0 = p0 * c.a0[i] + p1 * c.a1[i];
+        const int h1 = q0 * c.a0[i] + q1 * c.a1[i];
+        const int t0 = min(max(h0 >> 4, -32768), 32767);
+        const int t1 = min(max(h1 >> 4, -32768), 32767);
+        const int m0 = (t0 * b0) >> 16, m1 = (t1 * b1) >> 16;
+        int sum = min(max(m0 + m1, -32768), 32767);
+        sum = min(max(sum + 2, -32768), 32767);
+        const int vs = sum >> 2;
+        const int vf = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+        const int v = min(max(c.vec[i] ? vs : vf, 0), 255);
+        packed |= (uint32_t)v << (8 * i);
+    }
+    return packed;
+}
+
 // One workgroup per PYR_XB x PYR_RB output block: the source rows/columns the block reads are staged in LDS
 // (32-bit loads where aligned), each thread owns one 4-pixel column quad for the block's rows and keeps its
 // xofs/alpha coefficients in registers.
@@ -133,10 +195,21 @@ __global__ __launch_bounds__(256) void k_pyr_down(const Geom* __restrict__ g, in
     const int tid = threadIdx.x;
     const bool aligned = ((spitch | (int)((uintptr_t)src & 3)) & 3) == 0;
     const int nw = aligned ? segw >> 2 : 0;   // whole words inside the segment
-    for (int i = tid; i < nrows * nw; i += 256) {
-        const int r = i / nw, c = i - r * nw;
-        *reinterpret_cast<uint32_t*>(rbuf + r * SW + 4 * c) =
-            *reinterpret_cast<const uint32_t*>(src + (size_t)(ry_lo + r) * spitch + sxa + 4 * c);
+    for (int i0 = 0; i0 < nrows * nw; i0 += 8 * 256) {   // 8 global loads in flight per thread, then the stores
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int i = i0 + k * 256 + tid;
+            const int r = i / max(nw, 1), c = i - r * nw;
+            v[k] = i < nrows * nw ? *reinterpret_cast<const uint32_t*>(src + (size_t)(ry_lo + r) * spitch + sxa + 4 * c)
+                                  : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int i = i0 + k * 256 + tid;
+            const int r = i / max(nw, 1), c = i - r * nw;
+            if (i < nrows * nw) *reinterpret_cast<uint32_t*>(rbuf + r * SW + 4 * c) = v[k];
+        }
     }
     const int tail = segw - 4 * nw;
     for (int i = tid; i < nrows * tail; i += 256) {
@@ -146,54 +219,135 @@ __global__ __launch_bounds__(256) void k_pyr_down(const Geom* __restrict__ g, in
     __syncthreads();
     const int q = tid;   // PYR_XB / 4 == 256 quads
     if (4 * q >= nx) return;
-    int sx[4], a0[4], a1[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int dx = min(dx0 + 4 * q + i, L.w - 1);
-        sx[i] = L.xofs[dx] - sxa;
-        a0[i] = L.ialpha[2 * dx];
-        a1[i] = L.ialpha[2 * dx + 1];
-    }
+    PyrQuad cq;
+    pyr_quad_setup(L, dx0 + 4 * q, sxa, cq);
     for (int rr = 0; rr < ny; rr++) {
         const int dy = dy0 + rr;
         const int sy = L.yofs[dy];
         const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
         const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
-        const uint8_t* S0 = rbuf + (ry0 - ry_lo) * SW;
-        const uint8_t* S1 = rbuf + (ry1 - ry_lo) * SW;
-        const int b0 = L.ibeta[2 * dy], b1 = L.ibeta[2 * dy + 1];
-        uint32_t packed = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int dx = dx0 + 4 * q + i;
-            int h0, h1;
-            if (dx < L.xmax) {
-                h0 = S0[sx[i]] * a0[i] + S0[sx[i] + 1] * a1[i];
-                h1 = S1[sx[i]] * a0[i] + S1[sx[i] + 1] * a1[i];
-            } else {
-                h0 = S0[sx[i]] * 2048;
-                h1 = S1[sx[i]] * 2048;
-            }
-            int v;
-            if (dx < L.xvec) {
-                const int t0 = min(max(h0 >> 4, -32768), 32767);
-                const int t1 = min(max(h1 >> 4, -32768), 32767);
-                const int m0 = (t0 * b0) >> 16, m1 = (t1 * b1) >> 16;
-                int sum = min(max(m0 + m1, -32768), 32767);
-                sum = min(max(sum + 2, -32768), 32767);
-                v = sum >> 2;
-            } else {
-                v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-            }
-            v = min(max(v, 0), 255);
-            packed |= (uint32_t)v << (8 * i);
-        }
+        const uint32_t packed = pyr_quad(rbuf + (ry0 - ry_lo) * SW, rbuf + (ry1 - ry_lo) * SW, cq, L.ibeta[2 * dy],
+                                         L.ibeta[2 * dy + 1]);
         uint8_t* o = dst + (size_t)dy * L.pitch + dx0 + 4 * q;
         if (dx0 + 4 * q + 4 <= L.w) {
             *reinterpret_cast<uint32_t*>(o) = packed;
         } else {
             for (int i = 0; i < 4 && dx0 + 4 * q + i < L.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
         }
+    }
+}
+
+// Whole pyramid of one frame in ONE launch: workgroup (band j, frame f) owns rows [own_lo, own_hi) of every level
+// l >= 1 (an even split of each level's rows) and computes, in LDS, the rows [need_lo, need_hi) of every level that
+// its owned rows of the higher levels depend on (host-derived from yofs, PyrBand). Level l is computed from level
+// l-1's LDS rows (level 1 from the input frame in global memory), owned rows are stored to the pyramid buffer.
+// Rows shared by two bands are computed by both: ~1.1-1.5x the arithmetic of the per-level launches, 7 dependent
+// launches (and their per-launch latency, ~10 us each at one frame) become one. Arithmetic identical to
+// k_pyr_down (pyr_quad). Thread t works on quad column q = t % nq for rows t / nq, t / nq + RG, ... so its
+// column coefficients stay in registers for the whole level.
+// One level of k_pyr_bands: rows [bl.x, bl.y) of level l from the LDS rows of level l-1 (first row r0, pitch sp);
+// rc = this level's row coefficients {yofs, ibeta0 | ibeta1 << 16} for rows bl.x.. (LDS).
+__device__ __forceinline__ void pyr_band_level(const LevelGeom& L, int sh, const uint8_t* src, int sp, int r0,
+                                               int4 bl, const int2* rc, uint8_t* lds_dst, bool keep, uint8_t* gdst,
+                                               int tid, const PyrQuad& pre) {
+    const int dp = (L.w + 3) & ~3;
+    const int nq = (L.w + 3) >> 2;
+    const int RG = max(1, 256 / nq);
+    const int nrows = bl.y - bl.x;
+    for (int t = tid; t < nq * RG; t += 256) {
+        const int q = t % nq, rg = t / nq;
+        PyrQuad c;
+        if (t == tid) c = pre;
+        else pyr_quad_setup(L, 4 * q, 0, c);
+#pragma unroll 2
+        for (int r = rg; r < nrows; r += RG) {
+            const int dy = bl.x + r;
+            const int2 yc = rc[r];
+            const int sy = yc.x;
+            const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
+            const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
+            const uint32_t packed = pyr_quad(src + (ry0 - r0) * sp, src + (ry1 - r0) * sp, c,
+                                             (int)(short)(yc.y & 0xFFFF), yc.y >> 16);
+            if (keep) *reinterpret_cast<uint32_t*>(lds_dst + r * dp + 4 * q) = packed;
+            if (dy >= bl.z && dy < bl.w) {
+                uint8_t* o = gdst + (size_t)dy * L.pitch + 4 * q;
+                if (4 * q + 4 <= L.w) {
+                    *reinterpret_cast<uint32_t*>(o) = packed;
+                } else {
+                    for (int i = 0; i < 4 && 4 * q + i < L.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+                }
+            }
+        }
+    }
+}
+
+// LDS: [even levels' rows (level 0 staged from the frame)] [odd levels' rows] [row coefficients of every level].
+// The prologue puts everything with a global-memory latency in flight at once (level-0 rows, all row coefficients);
+// each level's column coefficients are fetched into registers while the previous level computes.
+__global__ __launch_bounds__(256) void k_pyr_bands(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ pyr,
+                                                   const int4* __restrict__ bands, int buf1_off, int rc_off) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t pbuf[];
+    const int j = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, NL = g->nlevels;
+    const int4* B = bands + (size_t)j * NL;
+    int2* rcoef = reinterpret_cast<int2*>(pbuf + rc_off);
+    // ---- prologue: level-0 rows [B[0].x, B[0].y) and the row coefficients of every level
+    {
+        const int4 b0 = B[0];
+        const int w0 = g->L[0].w, p0 = (w0 + 3) & ~3;
+        const uint8_t* in = s.in0 + (size_t)f * s.in_fstride;
+        const int nr = b0.y - b0.x;
+        if (((s.in_stride | (size_t)in | (size_t)w0) & 3) == 0) {
+            // 8 loads in flight per thread before the LDS stores (a load-store loop would wait out one global
+            // latency per word)
+            const int wpr = w0 >> 2, nw = nr * wpr;
+            for (int i0 = 0; i0 < nw; i0 += 8 * 256) {
+                uint32_t v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int i = i0 + k * 256 + tid;
+                    const int r = i / wpr, c = i - r * wpr;
+                    v[k] = i < nw ? *reinterpret_cast<const uint32_t*>(in + (size_t)(b0.x + r) * s.in_stride + 4 * c)
+                                  : 0u;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int i = i0 + k * 256 + tid;
+                    const int r = i / wpr, c = i - r * wpr;
+                    if (i < nw) *reinterpret_cast<uint32_t*>(pbuf + r * p0 + 4 * c) = v[k];
+                }
+            }
+        } else {
+            for (int i = tid; i < nr * w0; i += 256) {
+                const int r = i / w0, c = i - r * w0;
+                pbuf[r * p0 + c] = in[(size_t)(b0.x + r) * s.in_stride + c];
+            }
+        }
+        int off = 0;
+        for (int l = 1; l < NL; l++) {
+            const LevelGeom& L = g->L[l];
+            const int4 bl = B[l];
+            for (int r = tid; r < bl.y - bl.x; r += 256) {
+                const int dy = bl.x + r;
+                rcoef[off + r] = make_int2(L.yofs[dy], (L.ibeta[2 * dy] & 0xFFFF) | ((int)L.ibeta[2 * dy + 1] << 16));
+            }
+            off += bl.y - bl.x;
+        }
+    }
+    PyrQuad pre;
+    pyr_quad_setup(g->L[1], 4 * (tid % ((g->L[1].w + 3) >> 2)), 0, pre);
+    __syncthreads();
+    int off = 0;
+    for (int l = 1; l < NL; l++) {
+        const LevelGeom& L = g->L[l];
+        const int4 bl = B[l];
+        const PyrQuad cur = pre;
+        if (l + 1 < NL) pyr_quad_setup(g->L[l + 1], 4 * (tid % ((g->L[l + 1].w + 3) >> 2)), 0, pre);
+        const uint8_t* src = pbuf + ((l - 1) & 1 ? buf1_off : 0);
+        pyr_band_level(L, g->L[l - 1].h, src, (g->L[l - 1].w + 3) & ~3, B[l - 1].x, bl, rcoef + off,
+                       pbuf + (l & 1 ? buf1_off : 0), l + 1 < NL, pyr + L.pyr_off + (size_t)f * L.frame_bytes, tid,
+                       cur);
+        off += bl.y - bl.x;
+        __syncthreads();
     }
 }
 
@@ -480,11 +634,21 @@ __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, Level
     const bool words = x0 >= 4 && x0 + BLUR_TILE_W + 4 <= w && ((pitch | (int)((uintptr_t)lev & 3)) & 3) == 0;
     if (words) {
         constexpr int WPR = BLUR_IN_W / 4;
-        for (int i = tid; i < BLUR_IN_H * WPR; i += 256) {
+        constexpr int NWORDS = BLUR_IN_H * WPR, NIT = (NWORDS + 255) / 256;
+        uint32_t v[NIT];   // every load in flight before the LDS stores
+#pragma unroll
+        for (int k = 0; k < NIT; k++) {
+            const int i = k * 256 + tid;
             const int r = i / WPR, c = i - r * WPR;
-            const int gy = refl101(y0 - 3 + r, h);
-            *reinterpret_cast<uint32_t*>(&tin[r][4 * c]) =
-                *reinterpret_cast<const uint32_t*>(lev + (size_t)gy * pitch + x0 - 4 + 4 * c);
+            v[k] = i < NWORDS ? *reinterpret_cast<const uint32_t*>(lev + (size_t)refl101(y0 - 3 + r, h) * pitch + x0 -
+                                                                    4 + 4 * c)
+                              : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < NIT; k++) {
+            const int i = k * 256 + tid;
+            const int r = i / WPR, c = i - r * WPR;
+            if (i < NWORDS) *reinterpret_cast<uint32_t*>(&tin[r][4 * c]) = v[k];
         }
     } else {
         for (int i = tid; i < BLUR_IN_H * BLUR_IN_W; i += 256) {
@@ -583,12 +747,16 @@ __device__ unsigned long long g_dprof[8];
 #define DPROF(k) do {} while (0)
 #endif
 
-__global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, const int* __restrict__ cell_counts,
-                                                    const uint32_t* __restrict__ cand, uint32_t* __restrict__ keys,
-                                                    uint16_t* __restrict__ knode, uint32_t* __restrict__ out_key,
-                                                    uint32_t* __restrict__ out_rank, int* __restrict__ lvl_counts,
-                                                    int lap0, int lap1) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+// LDSK: the level's candidate keys (K) and their node ids (KN) live in LDS (kcap entries); every pass over the
+// candidates is then an LDS pass instead of a chain of global-memory round trips. Returns false (before any side
+// effect) when the level has more than kcap candidates: the caller reruns it with K/KN in global scratch.
+template <bool LDSK>
+__device__ __forceinline__ bool distribute_impl(uint8_t* smem, const Geom* __restrict__ g,
+                                                const int* __restrict__ cell_counts,
+                                                const uint32_t* __restrict__ cand, uint32_t* __restrict__ keys,
+                                                uint16_t* __restrict__ knode, uint32_t* __restrict__ out_key,
+                                                uint32_t* __restrict__ out_rank, int* __restrict__ lvl_counts,
+                                                int lap0, int lap1, int kcap) {
     const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
     const LevelGeom& L = g->L[l];
     const int NC = g->node_cap;
@@ -611,6 +779,8 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
     int* cellOff = (int*)take((g->max_level_cells + 1) * 4);
     int* scr = (int*)take(64);
     int* sh = (int*)take(64);           // block-uniform scalars
+    uint32_t* Kl = LDSK ? (uint32_t*)take((size_t)kcap * 4) : nullptr;
+    uint16_t* KNl = LDSK ? (uint16_t*)take((size_t)kcap * 2) : nullptr;
 
 #ifdef MAM_DIST_PROFILE
     long long dp0 = clock64();
@@ -627,18 +797,41 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
         carry += tot;
     }
     const int n = carry;
+    if (LDSK && n > kcap) return false;
     const uint32_t* cbase = cand + (size_t)f * g->cand_per_frame + L.cand_base;
-    uint32_t* K = keys + (size_t)f * g->cand_per_frame + L.cand_base;
-    uint16_t* KN = knode + (size_t)f * g->cand_per_frame + L.cand_base;
-    for (int c = wave_id(); c < L.ncells; c += 4) {
-        const int cnt = cc[c], off = cellOff[c];
-        for (int i = lane_id(); i < cnt; i += 64) K[off + i] = cbase[(size_t)c * L.cellcap + i];
+    uint32_t* K = LDSK ? Kl : keys + (size_t)f * g->cand_per_frame + L.cand_base;
+    uint16_t* KN = LDSK ? KNl : knode + (size_t)f * g->cand_per_frame + L.cand_base;
+    // candidate k -> its cell by binary search over the cell offsets; 4 independent global loads in flight per
+    // thread (a cell-per-wave walk is a chain of ~ncells/4 dependent global round trips)
+    if (tid == 0) cellOff[L.ncells] = n;
+    __syncthreads();
+    for (int k0 = 0; k0 < n; k0 += 4 * 256) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * 256 + tid;
+            v[u] = 0;
+            if (k < n) {
+                int lo = 0, hi = L.ncells;   // last cell with cellOff[c] <= k
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (cellOff[mid] <= k) lo = mid;
+                    else hi = mid;
+                }
+                v[u] = cbase[(size_t)lo * L.cellcap + (k - cellOff[lo])];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * 256 + tid;
+            if (k < n) K[k] = v[u];
+        }
     }
     __syncthreads();
     int* lc = lvl_counts + ((size_t)f * g->nlevels + l) * 2;
     if (n == 0) {
         if (tid == 0) { lc[0] = 0; lc[1] = 0; }
-        return;
+        return true;
     }
     const int N = L.nfeat;
     const int H = L.maxBY - L.minBY;
@@ -764,7 +957,7 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
     while (!finish) {
         if (++guard > 4096) {  // unreachable for a correct rebuild (S grows or the loop ends); never hang
             if (tid == 0) { lc[0] = -1; lc[1] = 0; }
-            return;
+            return true;
         }
         const int prevSize = S;
         if (!final_phase) {
@@ -887,7 +1080,7 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
     uint32_t* orr = out_rank + (size_t)f * g->kp_slots + L.kp_base;
     if (S > L.kp_cap) {
         if (tid == 0) { lc[0] = -1; lc[1] = 0; }
-        return;
+        return true;
     }
     int st_carry = 0;
     for (int p0 = 0; p0 < S; p0 += 256) {
@@ -911,6 +1104,17 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
     }
     if (tid == 0) { lc[0] = S; lc[1] = st_carry; }
     DPROF(5);
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, const int* __restrict__ cell_counts,
+                                                    const uint32_t* __restrict__ cand, uint32_t* __restrict__ keys,
+                                                    uint16_t* __restrict__ knode, uint32_t* __restrict__ out_key,
+                                                    uint32_t* __restrict__ out_rank, int* __restrict__ lvl_counts,
+                                                    int lap0, int lap1, int kcap) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (!distribute_impl<true>(smem, g, cell_counts, cand, keys, knode, out_key, out_rank, lvl_counts, lap0, lap1, kcap))
+        distribute_impl<false>(smem, g, cell_counts, cand, keys, knode, out_key, out_rank, lvl_counts, lap0, lap1, 0);
 }
 
 // ------------------------------------------------------------------------------------------------ describe

@@ -49,7 +49,7 @@ class FeatVec(C.Structure):
 
 class FramesDev(C.Structure):
     _fields_ = [("nframes", C.c_int32), ("kp_stride", C.c_int32), ("keys", C.c_void_p), ("desc", C.c_void_p),
-                ("counts", C.c_void_p), ("taken", C.c_void_p)]
+                ("counts", C.c_void_p), ("taken", C.c_void_p), ("taken_out", C.c_void_p)]
 
 
 MP_TRACK_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("view_cos", "<f4"), ("track_depth", "<f4"),

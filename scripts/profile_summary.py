@@ -6,6 +6,8 @@
         per-kernel HBM bytes per launch from the FETCH_SIZE and WRITE_SIZE passes (kilobytes in rocprofv3), with the
         gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md §HBM (FETCH_SIZE counts half the bytes of wide
         coalesced reads: x2), keyed by bench.py stage name for the single-kernel stages.
+    python scripts/profile_summary.py gaps <run_results.db> [first_kernel]
+        per-frame kernel timeline of a B=1 latency run (durations and inter-kernel gaps)
 """
 from __future__ import annotations
 
@@ -79,10 +81,46 @@ def traffic(fetch_db: str, write_db: str, out: str) -> None:
         print(f"{v['bytes_per_launch'] / 1e6:10.2f} MB/launch  fetch {v['fetch_kb_raw']:10.0f} KB  write {v['write_kb']:10.0f} KB  {k[:70]}")
 
 
+def gaps(db: str, first_kernel: str = "k_pyr_down", frames: int = 40) -> None:
+    """Per-frame timeline of a B=1 latency run: the kernels of the last `frames` frames (a frame starts at each
+    launch of `first_kernel` that follows a launch of another kernel), their mean durations in launch order, and the
+    mean span first start -> last end vs the sum of kernel durations (the rest is inter-kernel gaps)."""
+    if db.endswith(".csv"):   # rocprofv3 -f csv kernel trace
+        with open(db) as f:
+            rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                           for r in csv.DictReader(f)), key=lambda r: r[1])
+    else:
+        c = sqlite3.connect(db)
+        cols = [r[1] for r in c.execute("pragma table_info(kernels)").fetchall()]
+        st = "start" if "start" in cols else "start_timestamp"
+        en = "end" if "end" in cols else "end_timestamp"
+        rows = c.execute(f"select name, {st}, {en} from kernels order by {st}").fetchall()
+    starts = [i for i, r in enumerate(rows) if first_kernel in r[0] and (i == 0 or first_kernel not in rows[i - 1][0])]
+    groups = [rows[a:b] for a, b in zip(starts, starts[1:] + [len(rows)])][-frames - 1:-1]
+    sig = defaultdict(int)
+    for g in groups:
+        sig[tuple(r[0] for r in g)] += 1
+    key = max(sig, key=sig.get)
+    groups = [g for g in groups if tuple(r[0] for r in g) == key]
+    n = len(groups)
+    print(f"{n} frames with the modal launch sequence ({len(key)} kernels)")
+    tot_k = 0.0
+    for j, name in enumerate(key):
+        d = sum(g[j][2] - g[j][1] for g in groups) / n / 1e3
+        gap = sum(g[j][1] - g[j - 1][2] for g in groups) / n / 1e3 if j else 0.0
+        tot_k += d
+        print(f"  {j:2d} gap {gap:6.2f} us  dur {d:7.2f} us  {name[:80]}")
+    span = sum(g[-1][2] - g[0][1] for g in groups) / n / 1e3
+    print(f"span {span:.1f} us, kernels {tot_k:.1f} us, gaps {span - tot_k:.1f} us")
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "stats":
+    mode = sys.argv[1]
+    if mode == "stats":
         stats(sys.argv[2], sys.argv[3])
-    elif sys.argv[1] == "traffic":
+    elif mode == "traffic":
         traffic(sys.argv[2], sys.argv[3], sys.argv[4])
+    elif mode == "gaps":
+        gaps(sys.argv[2], *(sys.argv[3:4]))
     else:
         raise SystemExit(__doc__)

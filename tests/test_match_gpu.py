@@ -160,3 +160,60 @@ def test_projection_batch_device(gpu_lib, oracle, frames):
         no, oo = oracle.search_by_projection(FD[f], mp_list[f], 3.0, nnratio=0.8)
         assert nm[f] == no
         assert np.array_equal(out[f, :counts[f, 0]], oo)
+
+
+def test_motion_batch_device_taken_out(gpu_lib, oracle, frames):
+    """Batched motion search with `taken` in and `taken_out`: matches index-exact per frame, and taken_out is the
+    slot state the reference leaves in CurrentFrame.mvpMapPoints (ORBmatcher.cc:1768-1771 assign, :1876-1881
+    rotation clear), read as `taken` (slot set and Observations() > 0) by the next search."""
+    import torch
+
+    from mam3slam_amd.match import LAST_ENTRY_DTYPE, FramesDev
+
+    w, h, k, d = frames[0]
+    cam = scene.pinhole(w, h)
+    Fn, S = 4, 1100
+    M = _matcher(0.9, True)
+    keys = np.zeros((Fn, S), k.dtype)
+    desc = np.zeros((Fn, S, 32), np.uint8)
+    counts = np.zeros((Fn, 2), np.int32)
+    taken = np.zeros((Fn, S), np.uint8)
+    FD, lasts = [], []
+    tcw = np.zeros(Fn, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+    for f in range(Fn):
+        rng = np.random.default_rng(70 + f)
+        sel = np.sort(rng.choice(len(k), size=len(k) - 5 * f, replace=False))
+        F = scene.make_frame_data(k[sel], d[sel], w, h, rng, taken_frac=0.04 * f)
+        F.pose = scene.small_pose(rng)
+        keys[f, :len(sel)], desc[f, :len(sel)], counts[f, 0] = F.keys, F.desc, len(sel)
+        if F.taken is not None:
+            taken[f, :len(sel)] = F.taken
+        tcw[f]["q"], tcw[f]["t"] = F.pose
+        FD.append(F)
+        lasts.append(scene.motion_last_frame(F, cam, rng))
+    ls = max(len(x) for x in lasts)
+    last = np.zeros((Fn, ls), LAST_ENTRY_DTYPE)
+    for f in range(Fn):
+        last[f, :len(lasts[f])] = lasts[f]
+    dev = torch.device("cuda")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    t_keys, t_desc, t_cnt = T(keys.view(np.uint8).reshape(Fn, -1)), T(desc), T(counts)
+    t_taken, t_last, t_tcw = T(taken), T(last.view(np.uint8).reshape(Fn, -1)), T(tcw.view(np.uint8))
+    t_nlast = T(np.array([len(x) for x in lasts], np.int32))
+    t_out = torch.zeros((Fn, S), dtype=torch.int32, device=dev)
+    t_nm = torch.zeros(Fn, dtype=torch.int32, device=dev)
+    t_tout = torch.full((Fn, S), 7, dtype=torch.uint8, device=dev)
+    fr = FramesDev(Fn, S, t_keys.data_ptr(), t_desc.data_ptr(), t_cnt.data_ptr(), t_taken.data_ptr(),
+                   t_tout.data_ptr())
+    M.search_motion_batch_device(FD[0], fr, t_tcw.data_ptr(), cam, t_last.data_ptr(), ls, t_nlast.data_ptr(), 15.0,
+                                 t_out.data_ptr(), t_nm.data_ptr())
+    torch.cuda.synchronize()
+    out, nm, tout = t_out.cpu().numpy(), t_nm.cpu().numpy(), t_tout.cpu().numpy()
+    for f in range(Fn):
+        n = counts[f, 0]
+        no, oo = oracle.search_by_projection_motion(FD[f], lasts[f], cam, 15.0, True)
+        assert nm[f] == no
+        assert np.array_equal(out[f, :n], oo)
+        exp = np.where(oo >= 0, lasts[f]["nobs"][np.maximum(oo, 0)] > 0, (oo == -1) & (taken[f, :n] > 0))
+        assert np.array_equal(tout[f, :n], exp.astype(np.uint8)), f
+        assert not tout[f, n:].any()
