@@ -290,6 +290,21 @@ __device__ __forceinline__ void stl_sort_wave(SortEl* arr, int n, int* scratch) 
         }
         return r;
     };
+    // wave-uniform positions: v_readlane (scalar result), no LDS round trip
+    auto key_at = [&](int p) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            if ((p >> 6) == e) r = (uint32_t)__builtin_amdgcn_readlane((int)key[e], p & 63);
+        return r;
+    };
+    auto val_at = [&](int p) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            if ((p >> 6) == e) r = (uint32_t)__builtin_amdgcn_readlane((int)val[e], p & 63);
+        return r;
+    };
     const uint64_t below = (1ull << lane) - 1ull;
     const uint64_t above = ~(below | (1ull << lane));
     int sp = 0;
@@ -317,12 +332,12 @@ __device__ __forceinline__ void stl_sort_wave(SortEl* arr, int n, int* scratch) 
             --cd;
             // __move_median_to_first(first, first + 1, mid, last - 1)
             const int mid = cf + (cl - cf) / 2;
-            const uint32_t ka = get_key(cf + 1), kb = get_key(mid), kc = get_key(cl - 1);
+            const uint32_t ka = key_at(cf + 1), kb = key_at(mid), kc = key_at(cl - 1);
             int sw;
             if (ka < kb) sw = kb < kc ? mid : (ka < kc ? cl - 1 : cf + 1);
             else sw = ka < kc ? cf + 1 : (kb < kc ? cl - 1 : mid);
             {
-                const uint32_t kf = get_key(cf), vf = get_val(cf), ks = get_key(sw), vs = get_val(sw);
+                const uint32_t kf = key_at(cf), vf = val_at(cf), ks = key_at(sw), vs = val_at(sw);
 #pragma unroll
                 for (int e = 0; e < E; e++) {
                     const int p = e * 64 + lane;
@@ -330,7 +345,7 @@ __device__ __forceinline__ void stl_sort_wave(SortEl* arr, int n, int* scratch) 
                     else if (p == sw) { key[e] = kf; val[e] = vf; }
                 }
             }
-            const uint32_t pv = get_key(cf);
+            const uint32_t pv = key_at(cf);
             uint64_t mL[E], mR[E];
             bool isL[E], isR[E];
             int nl = 0, nr = 0;
@@ -411,7 +426,7 @@ __device__ __forceinline__ void stl_sort_wave(SortEl* arr, int n, int* scratch) 
 #pragma unroll
     for (int e = 0; e < E; e++) r[e] = 0;
     for (int q = 0; q < n; q++) {
-        const uint32_t kq = get_key(q);
+        const uint32_t kq = key_at(q);
 #pragma unroll
         for (int e = 0; e < E; e++) r[e] += (kq < key[e]) || (kq == key[e] && q < e * 64 + lane);
     }

@@ -401,7 +401,7 @@ __host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~(size_t)15;
 // unit), entries (u32) and their units (u16)
 __host__ __device__ inline size_t flat_carve_bytes(int nu, int ne) {
     return a16((size_t)(nu + 1) * 4) + 2 * a16((size_t)nu * 4) + 2 * a16((size_t)nu) + a16((size_t)ne * 4) +
-           a16((size_t)ne * 2);
+           3 * a16((size_t)ne * 2);
 }
 constexpr int RESOLVE_POOL_LDS = 24576;   // candidate entries staged in LDS per frame (up to 96 KB)
 
@@ -516,7 +516,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
         uint8_t* flags = fp;                                              fp += a16((size_t)nu);       // 1 open, 2 taker
         uint8_t* notready = fp;                                           fp += a16((size_t)nu);
         uint32_t* epool = reinterpret_cast<uint32_t*>(fp);                fp += a16((size_t)etotal * 4);
-        uint16_t* eunit = reinterpret_cast<uint16_t*>(fp);
+        uint16_t* eunit = reinterpret_cast<uint16_t*>(fp);                fp += a16((size_t)etotal * 2);   // | taker << 15
+        uint16_t* act0 = reinterpret_cast<uint16_t*>(fp);                 fp += a16((size_t)etotal * 2);   // active entries
+        uint16_t* act1 = reinterpret_cast<uint16_t*>(fp);
         unsigned open = 0;
 #pragma unroll
         for (int k = 0; k < UPT; k++) {
@@ -557,57 +559,58 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int i = i0 + q * RESOLVE_THREADS + t;
-                if (i < etotal) { epool[i] = v[q]; eunit[i] = (uint16_t)uu[q]; }
+                if (i < etotal) {
+                    epool[i] = v[q];
+                    eunit[i] = (uint16_t)(uu[q] | ((flags[uu[q]] & 2) << 14));
+                    act0[i] = (uint16_t)i;
+                }
             }
         }
         __syncthreads();
         for (int u = t; u < nu; u += RESOLVE_THREADS) best[u] = 0xFFFFFFFFu;
         RPROF(0);
         int round = 0;
-        while (__syncthreads_or(open != 0)) {
+        __shared__ int s_acnt;
+        if (t == 0) s_acnt = 0;
+        int acnt = etotal;   // entries of open units (every unit with entries is open in round 0)
+        uint16_t* act = act0;
+        uint16_t* nxt = act1;
+        while (acnt > 0) {
 #ifdef MAM_RESOLVE_PROFILE
             if (t == 0) atomicAdd(&g_rprof[p.mode][6], 1ull);
 #endif
             const int stamp = (0xFFF - round) << 12;
             // (1) claims (see the per-unit loop below for minU / minA)
-            for (int i = t; i < etotal; i += RESOLVE_THREADS) {
-                const int u = eunit[i];
-                const int fl = flags[u];
-                if (!(fl & 1)) continue;
+            for (int j = t; j < acnt; j += RESOLVE_THREADS) {
+                const int i = act[j];
+                const int ut = eunit[i], u = ut & 0x7FFF;
                 const uint32_t e = epool[i];
                 const int key = stamp | u;
                 atomicMin(&minA[e & 0xFFFFu], key);
-                if ((fl & 2) && (int)((e >> 16) & 0x1FFu) <= MAM_TH_HIGH) atomicMin(&minU[e & 0xFFFFu], key);
+                if ((ut & 0x8000) && (int)((e >> 16) & 0x1FFu) <= MAM_TH_HIGH) atomicMin(&minU[e & 0xFFFFu], key);
             }
             __syncthreads();
             RPROF(3);
-            // (2) readiness: one failing candidate makes its unit wait a round
-            for (int i = t; i < etotal; i += RESOLVE_THREADS) {
-                const int u = eunit[i];
-                const int fl = flags[u];
-                if (!(fl & 1)) continue;
+            // (2) readiness (one failing candidate makes its unit wait a round) and, speculatively for every open
+            //     unit, its best untaken candidate (taken bits only change in the commit below)
+            for (int j = t; j < acnt; j += RESOLVE_THREADS) {
+                const int i = act[j];
+                const int ut = eunit[i], u = ut & 0x7FFF;
                 const uint32_t e = epool[i];
                 const int key = stamp | u;
                 const int dist = (int)((e >> 16) & 0x1FFu);
-                const bool ok = minU[e & 0xFFFFu] >= key && (!(fl & 2) || dist > MAM_TH_HIGH || minA[e & 0xFFFFu] >= key);
-                if (!ok) notready[u] = 1;
-            }
-            __syncthreads();
-            // (3) best untaken candidate of every ready unit
-            for (int i = t; i < etotal; i += RESOLVE_THREADS) {
-                const int u = eunit[i];
-                if (!(flags[u] & 1) || notready[u]) continue;
-                const uint32_t e = epool[i];
                 const int idx = (int)(e & 0xFFFFu);
-                if ((takenb[idx >> 5] >> (idx & 31)) & 1u) continue;
-                atomicMin(&best[u], (((e >> 16) & 0x1FFu) << 16) | (uint32_t)i);
+                const bool ok = minU[idx] >= key && (!(ut & 0x8000) || dist > MAM_TH_HIGH || minA[idx] >= key);
+                if (!ok) notready[u] = 1;
+                if (!((takenb[idx >> 5] >> (idx & 31)) & 1u)) atomicMin(&best[u], ((uint32_t)dist << 16) | (uint32_t)i);
             }
             __syncthreads();
-            // (4) second best (the ratio test of the local-map search)
+            // (3) second best of the ready units (the ratio test of the local-map search)
             if (p.mode == 0) {
-                for (int i = t; i < etotal; i += RESOLVE_THREADS) {
-                    const int u = eunit[i];
-                    if (!(flags[u] & 1) || notready[u]) continue;
+                for (int j = t; j < acnt; j += RESOLVE_THREADS) {
+                    const int i = act[j];
+                    const int u = eunit[i] & 0x7FFF;
+                    if (notready[u]) continue;
                     const uint32_t b = best[u];
                     if (b == 0xFFFFFFFFu || (int)(b & 0xFFFFu) == i) continue;
                     const uint32_t e = epool[i];
@@ -617,7 +620,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
                 }
                 __syncthreads();
             }
-            // (5) ready units commit (each thread its own units)
+            // (4) ready units commit (each thread its own units)
 #pragma unroll
             for (int k = 0; k < UPT; k++) {
                 if (!((open >> k) & 1u)) continue;
@@ -647,6 +650,30 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
                 nm++;
                 if (p.mode == 1 && p.check_ori) ev[atomicAdd(&s_nev, 1)] = (uint32_t)bestIdx | ((uint32_t)u << 16);
             }
+            __syncthreads();
+            // (5) the entries of the units still open, in any order (positions carry no meaning; the entry
+            //     index does): one LDS atomic per wave and pass
+            for (int j0 = 0; j0 < acnt; j0 += RESOLVE_THREADS) {
+                const int j = j0 + t;
+                int i = 0;
+                bool keep = false;
+                if (j < acnt) {
+                    i = act[j];
+                    keep = flags[eunit[i] & 0x7FFF] & 1;
+                }
+                const uint64_t m = __ballot(keep);
+                int base = 0;
+                if ((t & 63) == 0 && m) base = atomicAdd(&s_acnt, __popcll(m));
+                base = __shfl(base, 0, 64);
+                if (keep) nxt[base + __popcll(m & ((1ull << (t & 63)) - 1ull))] = (uint16_t)i;
+            }
+            __syncthreads();
+            acnt = s_acnt;
+            __syncthreads();
+            if (t == 0) s_acnt = 0;
+            uint16_t* tmp = act;
+            act = nxt;
+            nxt = tmp;
             round++;
             RPROF(5);
         }

@@ -763,14 +763,18 @@ __device__ __forceinline__ bool distribute_impl(uint8_t* smem, const Geom* __res
     // ---- LDS carve (all offsets multiples of 16 B)
     uint8_t* p8 = smem;
     auto take = [&](size_t bytes) { uint8_t* r = p8; p8 += (bytes + 15) & ~(size_t)15; return r; };
-    NodeBuf nb[2];
+    // the two node tables as two named structs selected by value (a dynamically indexed array of pointer structs
+    // would live in scratch memory: a global-memory round trip per access)
+    NodeBuf nb0, nb1;
     for (int b = 0; b < 2; b++) {
-        nb[b].x0 = (uint16_t*)take(NC * 2);
-        nb[b].y0 = (uint16_t*)take(NC * 2);
-        nb[b].x1 = (uint16_t*)take(NC * 2);
-        nb[b].y1 = (uint16_t*)take(NC * 2);
-        nb[b].cnt = (uint32_t*)take(NC * 4);
+        NodeBuf& t = b ? nb1 : nb0;
+        t.x0 = (uint16_t*)take(NC * 2);
+        t.y0 = (uint16_t*)take(NC * 2);
+        t.x1 = (uint16_t*)take(NC * 2);
+        t.y1 = (uint16_t*)take(NC * 2);
+        t.cnt = (uint32_t*)take(NC * 4);
     }
+    auto NBsel = [&](int b) -> NodeBuf { return b ? nb1 : nb0; };
     uint32_t* ch = (uint32_t*)take((size_t)NC * 16);
     int* xr = (int*)take(NC * 4);
     int* aux = (int*)take(NC * 4);       // E[r] then CB[r]
@@ -838,7 +842,7 @@ __device__ __forceinline__ bool distribute_impl(uint8_t* smem, const Geom* __res
     // ---- 1. initial nodes (ORBextractor.cc:559-598)
     int cur = 0;
     {
-        NodeBuf& A = nb[0];
+        const NodeBuf A = nb0;
         for (int i = tid; i < L.nini; i += 256) {
             A.x0[i] = (uint16_t)(int)(L.hX * (float)i);
             A.x1[i] = (uint16_t)(int)(L.hX * (float)(i + 1));
@@ -855,7 +859,7 @@ __device__ __forceinline__ bool distribute_impl(uint8_t* smem, const Geom* __res
         }
         __syncthreads();
         // erase empty initial nodes, keep order
-        NodeBuf& B = nb[1];
+        const NodeBuf B = nb1;
         int keep_carry = 0;
         for (int i0 = 0; i0 < L.nini; i0 += 256) {
             const int i = i0 + tid;
@@ -884,8 +888,8 @@ __device__ __forceinline__ bool distribute_impl(uint8_t* smem, const Geom* __res
     // Produces the new list in the other buffer, remaps keys, builds candl (children with >1 keys in
     // creation order) and returns (via sh) the new size and #candidates.
     auto rebuild = [&](int NX) {
-        NodeBuf& A = nb[cur];
-        NodeBuf& B = nb[cur ^ 1];
+        const NodeBuf A = NBsel(cur);
+        const NodeBuf B = NBsel(cur ^ 1);
         // exclusive scan of aux over ranks -> creation base (in place)
         int cb_carry = 0;
         for (int r0 = 0; r0 < NX; r0 += 256) {
@@ -962,7 +966,7 @@ __device__ __forceinline__ bool distribute_impl(uint8_t* smem, const Geom* __res
         const int prevSize = S;
         if (!final_phase) {
             // ---- phase-1 round: every node with >1 keys divides (ORBextractor.cc:605-677)
-            NodeBuf& A = nb[cur];
+            const NodeBuf A = NBsel(cur);
             int x_carry = 0;
             for (int p0 = 0; p0 < S; p0 += 256) {
                 const int p = p0 + tid;
@@ -997,7 +1001,7 @@ __device__ __forceinline__ bool distribute_impl(uint8_t* smem, const Geom* __res
             // ---- final phase (ORBextractor.cc:680-748): sort last round's >1-key children by
             // (size, UL.x) with libstdc++'s introsort, expand from the largest until size >= N.
             if (m == 0) break;
-            NodeBuf& A = nb[cur];
+            const NodeBuf A = NBsel(cur);
             for (int i = tid; i < m; i += 256) {
                 const int p = candl[i];
                 arr[i].key = (A.cnt[p] << 12) | A.x0[p];
@@ -1066,7 +1070,7 @@ __device__ __forceinline__ bool distribute_impl(uint8_t* smem, const Geom* __res
     }
 
     // ---- retain the best key per node (first max response in candidate order, ORBextractor.cc:758-776)
-    NodeBuf& A = nb[cur];
+    const NodeBuf A = NBsel(cur);
     (void)A;
     for (int p = tid; p < S; p += 256) ch[p] = 0;
     __syncthreads();

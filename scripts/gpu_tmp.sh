@@ -5,3 +5,7 @@ timeout -k 10 200 python bench.py --batch 1 --lanes 1 --steps 5 --warmup 2 --no-
 python3 -c "import json;d=json.load(open('$O/b1.json'));print('B1 lat', round(d['latency_ms_per_frame_b1'],4), {k:round(v,4) for k,v in d['stage_ms_per_step'].items()})"
 timeout -k 10 200 python bench.py --no-cpu-baseline --no-latency > $O/b256.json 2>$O/b256.err || exit $?
 python3 -c "import json;d=json.load(open('$O/b256.json'));print('B256', round(d['value']), {k:round(v,4) for k,v in d['stage_ms_per_step'].items()})"
+MAM3SLAM_GPU_LIB=$R/build/libmam_gpu_distprof.so timeout -k 10 200 python bench.py --batch 1 --lanes 1 --steps 40 --warmup 2 --no-cpu-baseline --no-latency > $O/b1_distprof.json 2>$O/b1_distprof.err || exit $?
+tail -1 $O/b1_distprof.err
+MAM3SLAM_GPU_LIB=$R/build/libmam_gpu_resprof.so timeout -k 10 200 python bench.py --batch 1 --lanes 1 --steps 40 --warmup 2 --no-cpu-baseline --no-latency > $O/b1_resprof.json 2>$O/b1_resprof.err || exit $?
+tail -2 $O/b1_resprof.err
