@@ -120,6 +120,77 @@ def cpu_baseline(cfg, seconds=10.0):
     return res
 
 
+def pose_section(args, B, W, H, NF, cam, kps_h, cnt_h, d_out1, lasts, dev, stream):
+    """Optimizer::PoseOptimization after the motion-model search (Tracking.cc:2836), measured beside the step (it is
+    not part of the headline metric): every frame's edges are its motion-search matches (keypoint, last-frame
+    MapPoint position), one workgroup per frame, B frames per launch; plus the single-frame launch and the oracle
+    on one host core (same edges)."""
+    import torch
+
+    from mam3slam_amd import pose, scene
+    from mam3slam_amd.orb import KP_DTYPE
+
+    out1 = d_out1.cpu().numpy()
+    sf, s2 = scene.scale_tables()
+    inv_s2 = (np.float32(1.0) / s2).astype(np.float32)
+    edges_l = []
+    for f in range(B):
+        n = int(cnt_h[f, 0])
+        o = out1[f, :n]
+        idx = np.nonzero(o >= 0)[0]
+        edges_l.append(pose.make_edges(kps_h[f, :n].view(KP_DTYPE), inv_s2, idx, lasts[f]["pos"][o[idx]]))
+    S = max(len(e) for e in edges_l)
+    E = np.zeros((B, S), pose.POSE_EDGE_DTYPE)
+    for f, e in enumerate(edges_l):
+        E[f, :len(e)] = e
+    P = pose.PoseOptimizer(device=dev.index or 0)
+    t_e = torch.from_numpy(E.view(np.uint8).reshape(B, -1)).to(dev)
+    t_n = torch.tensor([len(e) for e in edges_l], dtype=torch.int32, device=dev)
+    tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+    rng = np.random.default_rng(7)
+    for f in range(B):
+        tcw[f]["q"], tcw[f]["t"] = scene.small_pose(rng)   # the motion model's guess around the frame's pose
+    t_p = torch.from_numpy(tcw.view(np.uint8)).to(dev)
+    t_o = torch.zeros((B, S), dtype=torch.uint8, device=dev)
+    t_r = torch.zeros((B, pose.POSE_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+
+    def run(nf):
+        P.optimize_batch_device(nf, t_p.data_ptr(), cam, t_e.data_ptr(), S, t_n.data_ptr(), t_o.data_ptr(),
+                                t_r.data_ptr(), stream=stream.cuda_stream)
+
+    run(B)
+    run(1)
+    torch.cuda.synchronize(dev)
+    reps = max(args.steps, 5)
+    P.set_profiling(True)
+    for _ in range(reps):
+        run(B)
+    torch.cuda.synchronize(dev)
+    ms_b = P.stage_times()["pose"][0] / reps
+    P.set_profiling(True)
+    for _ in range(reps):
+        run(1)
+    torch.cuda.synchronize(dev)
+    ms_1 = P.stage_times()["pose"][0] / reps
+    P.set_profiling(False)
+    res = t_r.cpu().numpy().view(pose.POSE_RESULT_DTYPE).reshape(B)
+    info = {"frames_per_launch": B, "edges_per_frame": float(np.mean([len(e) for e in edges_l])),
+            "ms_per_launch": ms_b, "frames_per_s": B / (ms_b * 1e-3), "ms_single_frame_launch": ms_1,
+            "iterations_per_frame": float(res["iterations"].mean()),
+            "lm_trials_per_frame": float(res["lm_trials"].mean()),
+            "inliers_per_frame": float(res["n_inliers"].mean())}
+    if not args.no_cpu_baseline and int(os.environ.get("RANK", "0")) == 0:
+        from oracle import oracle_py
+
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 2.0 and n < B:
+            oracle_py.pose_optimization_edges((tcw[n]["q"], tcw[n]["t"]), cam, edges_l[n])
+            n += 1
+        info["cpu_ms_per_frame"] = (time.perf_counter() - t0) * 1e3 / n
+        info["cpu_sample"] = f"{n} frames, oracle C++ restatement, 1 thread"
+    return info
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -132,6 +203,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch the tracking step eagerly instead of a HIP graph")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the B=1 latency section (profiling runs: every launch then covers one lane's batch)")
+    ap.add_argument("--no-pose", action="store_true", help="skip the PoseOptimization section")
     ap.add_argument("--lanes", type=int, default=4,
                     help="independent sub-batches (agent groups) per GPU, each with its own contexts and HIP stream, "
                          "so one group's latency-bound stages overlap another's compute")
@@ -423,6 +495,8 @@ def main():
         return float(np.median(lat))
 
     latency_ms = None if args.no_latency else measure_latency()
+    pose_info = None if args.no_pose else pose_section(args, B, W, H, NF, cam, kps_h, cnt_h, d_out1, lasts, dev,
+                                                       tstream)
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -480,6 +554,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": avg_ms},
         }
+        if pose_info is not None:
+            out["pose_optimization"] = pose_info
         if cfg["lba"]:
             out["lba"] = {"solves": lba_stats["n"], "ms_per_solve_wall": lba_stats["ms"] / max(lba_stats["n"], 1),
                           "iterations": lba_stats["its"], "edges": int(len(lba_prob.edge_point)),

@@ -4,6 +4,7 @@
  * The window build (local keyframes by covisibility, local MapPoints, fixed keyframes), the early returns
  * (no fixed keyframe, stop flag), the outlier erase (chi2 > 5.991 || depth <= 0) and the write-back under
  * Map::mMutexMapUpdate follow the reference line by line; only `optimizer.optimize(10)` runs on the GPU.
+ * PoseOptimization: the edge setup and write-back of src/Optimizer.cc:814-1115 around the GPU solve.
  */
 #ifndef MAM3SLAM_OPTIMIZER_H
 #define MAM3SLAM_OPTIMIZER_H
@@ -12,6 +13,7 @@
 #include <vector>
 
 #include "../mam_lba.h"
+#include "../mam_pose.h"
 #include "Map.h"
 
 namespace MAM3SLAM {
@@ -36,6 +38,11 @@ struct LocalBAWindow {
 
 class Optimizer {
 public:
+    /* Optimizer::PoseOptimization(Frame*) (include/Optimizer.h, src/Optimizer.cc:814-1115), mono Pinhole frames: one
+     * edge per keypoint with a MapPoint (in keypoint order), the 4-round g2o solve on the GPU (include/mam_pose.h),
+     * pFrame->mvbOutlier and the pose written back. Returns nInitialCorrespondences - nBad (0 below 3). */
+    static int PoseOptimization(Frame* pFrame);
+
     static void LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& num_fixedKF,
                                       int& num_OptKF, int& num_MPs, int& num_edges);
 

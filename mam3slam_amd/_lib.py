@@ -58,8 +58,9 @@ def _match_sigs():
     from .exchange import _SIGS as ex_sigs
     from .lba import _SIGS as lba_sigs
     from .match import _SIGS
+    from .pose import _SIGS as pose_sigs
 
-    return {**_SIGS, **lba_sigs, **ex_sigs}
+    return {**_SIGS, **lba_sigs, **ex_sigs, **pose_sigs}
 
 
 def lib() -> C.CDLL:

@@ -1,0 +1,566 @@
+// pose.hip — gfx950 Optimizer::PoseOptimization (include/mam_pose.h): the whole 4-round Levenberg-Marquardt of one
+// frame's pose in ONE workgroup, batched over frames (one workgroup per frame), FP64 throughout.
+//
+// Reference: src/Optimizer.cc:814-1115 with g2o's Levenberg (core/optimization_algorithm_levenberg.cpp:61-169),
+// BlockSolver_6_3 + LinearSolverDense (Eigen LDLT, solvers/linear_solver_dense.h:65-118), EdgeSE3ProjectXYZOnlyPose
+// (src/OptimizableTypes.cpp:49-63) and RobustKernelHuber (core/robust_kernel_impl.cpp:76-91).
+//
+// Layout: the frame's edges are staged in LDS as float SoA (obs x/y, Xw, invSigma2; the reference's float inputs,
+// widened to double where used) next to each edge's last error (2 doubles, the stale-after-rejected-trial value
+// g2o's chi2() reads) and its level (0 active, 1 outlier). Every pass deals the edges to the 256 threads; the
+// per-thread partial sums (robust chi2, or the 21 upper entries of H plus b) are reduced by a fixed DPP pattern
+// per wave and a fixed wave order, so every thread ends with the same bits and runs the LM control flow, the 6x6
+// pivoted LDL^T and the SE3 update redundantly: no host round trip, no broadcast, block-uniform branches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <string>
+
+#include "../../include/mam_pose.h"
+#include "runtime.hpp"
+#include "se3.hpp"
+
+namespace mam {
+namespace pose {
+
+constexpr int PT = 256;        // threads per frame
+constexpr int NW = PT / 64;
+constexpr int NRED = 27;       // 21 upper entries of H + 6 of b
+
+struct Args {
+    int nframes;
+    const mam_pose* tcw;
+    mam_pinhole cam;
+    const mam_pose_edge* edges;
+    int stride;
+    const int32_t* n_edges;
+    uint8_t* outlier;
+    mam_pose_result* res;
+    int cap;                   // edges the LDS carve holds
+};
+
+__host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~(size_t)15; }
+// floats: 6 per edge (SoA), errors: 2 doubles per edge, level: 1 byte per edge
+__host__ __device__ inline size_t lds_bytes(int cap) {
+    return a16((size_t)cap * 16) + 6 * a16((size_t)cap * 4) + a16((size_t)cap);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false));
+}
+
+// Wave sum with a fixed DPP pattern (quad perms, row shifts, row broadcasts); the total lands in lane 63.
+__device__ __forceinline__ double wave_sum63(double v) {
+    v += dpp_d<0xb1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_d<0x4e>(v);    // quad_perm [2,3,0,1]
+    v += dpp_d<0x114>(v);   // row_shr:4
+    v += dpp_d<0x118>(v);   // row_shr:8
+    v += dpp_d<0x142>(v);   // row_bcast:15
+    v += dpp_d<0x143>(v);   // row_bcast:31
+    return v;
+}
+
+__device__ __forceinline__ double lane63(double v) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                            __builtin_amdgcn_readlane(__double2loint(v), 63));
+}
+
+// Block sum of N per-thread values into out[0..N) (LDS; waves summed in order 0..NW-1, fixed DPP pattern inside a
+// wave, so the bits do not depend on timing). Ends with a barrier: out[] is readable by every thread.
+template <int N>
+__device__ __forceinline__ void block_sum(const double (&v)[N], double* scr, double* out) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const double s = lane63(wave_sum63(v[k]));
+        if ((threadIdx.x & 63) == 0) scr[w * N + k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < N) {
+        double s = scr[threadIdx.x];
+#pragma unroll
+        for (int q = 1; q < NW; q++) s += scr[q * N + threadIdx.x];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+struct Edges {
+    const float *ox, *oy, *X, *Y, *Z, *w;
+    double* err;
+    uint8_t* level;
+    int n;
+};
+
+// EdgeSE3ProjectXYZOnlyPose::computeError: obs - Pinhole::project(T.map(Xw)); returns chi2 = e^T (w I) e
+__device__ __forceinline__ double edge_error(const Edges& E, int i, const double T[7], const mam_pinhole& c,
+                                             double* e0o, double* e1o) {
+    const double Xw[3] = {(double)E.X[i], (double)E.Y[i], (double)E.Z[i]};
+    double Xc[3];
+    se3::map_point(T, Xw, Xc);
+    const double u = (double)c.fx * Xc[0] / Xc[2] + (double)c.cx;
+    const double v = (double)c.fy * Xc[1] / Xc[2] + (double)c.cy;
+    const double e0 = (double)E.ox[i] - u, e1 = (double)E.oy[i] - v;
+    *e0o = e0;
+    *e1o = e1;
+    const double w = (double)E.w[i];
+    return e0 * (w * e0) + e1 * (w * e1);
+}
+
+__device__ __forceinline__ void rho_of(double chi, bool robust, double delta, double* r0, double* r1) {
+    if (robust) se3::huber(chi, delta, r0, r1);
+    else { *r0 = chi; *r1 = 1.0; }
+}
+
+// computeActiveErrors at T (errors stored) + activeRobustChi2
+__device__ double active_chi(const Edges& E, const double T[7], const mam_pinhole& c, bool robust, double delta,
+                             double* scr) {
+    double acc[1] = {0.0};
+    for (int i = threadIdx.x; i < E.n; i += PT) {
+        if (E.level[i]) continue;
+        double e0, e1;
+        const double chi = edge_error(E, i, T, c, &e0, &e1);
+        E.err[2 * i] = e0;
+        E.err[2 * i + 1] = e1;
+        double r0, r1;
+        rho_of(chi, robust, delta, &r0, &r1);
+        acc[0] += r0;
+    }
+    block_sum<1>(acc, scr, scr + NW * (NRED + 1));
+    return scr[NW * (NRED + 1)];
+}
+
+// One pass: computeActiveErrors + activeRobustChi2 + buildSystem (BaseUnaryEdge::constructQuadraticForm,
+// base_unary_edge.hpp:43-71). H upper (row-major i <= j, 21) then b (6) in red[0..26]; returns the chi.
+__device__ double build_system(const Edges& E, const double T[7], const mam_pinhole& c, bool robust, double delta,
+                               double* scr, double* red) {
+    double acc[NRED + 1];
+#pragma unroll
+    for (int k = 0; k <= NRED; k++) acc[k] = 0.0;
+    for (int i = threadIdx.x; i < E.n; i += PT) {
+        if (E.level[i]) continue;
+        const double Xw[3] = {(double)E.X[i], (double)E.Y[i], (double)E.Z[i]};
+        double Xc[3];
+        se3::map_point(T, Xw, Xc);
+        const double x = Xc[0], y = Xc[1], z = Xc[2];
+        const double u = (double)c.fx * x / z + (double)c.cx;
+        const double v = (double)c.fy * y / z + (double)c.cy;
+        const double e0 = (double)E.ox[i] - u, e1 = (double)E.oy[i] - v;
+        E.err[2 * i] = e0;
+        E.err[2 * i + 1] = e1;
+        const double w = (double)E.w[i];
+        const double chi = e0 * (w * e0) + e1 * (w * e1);
+        double r0, r1;
+        rho_of(chi, robust, delta, &r0, &r1);
+        acc[NRED] += r0;
+        // _jacobianOplusXi = -projectJac(Xc) * SE3deriv (OptimizableTypes.cpp:49-63)
+        const double fx = c.fx, fy = c.fy;
+        const double J[6] = {-(fx / z), -0.0, -(-fx * x / (z * z)), -0.0, -(fy / z), -(-fy * y / (z * z))};
+        const double D[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
+        double A[12];
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int k = 0; k < 6; k++) A[6 * r + k] = J[3 * r] * D[k] + J[3 * r + 1] * D[6 + k] + J[3 * r + 2] * D[12 + k];
+        const double o0 = -(w * e0) * r1, o1 = -(w * e1) * r1;
+        const double wo = r1 * w;
+        int q = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int b = a; b < 6; b++) acc[q++] += A[a] * wo * A[b] + A[6 + a] * wo * A[6 + b];
+#pragma unroll
+        for (int a = 0; a < 6; a++) acc[21 + a] += A[a] * o0 + A[6 + a] * o1;
+    }
+    block_sum<NRED + 1>(acc, scr, red);
+    return red[NRED];
+}
+
+// Eigen 3.4.0 LDLT<MatrixXd, Lower> compute + solve of (H + lambda I) x = b, 6x6, diagonal pivoting; returns
+// isPositive(). Same operation order as the oracle (oracle/pose_oracle.cpp eigen_ldlt_solve). Fully unrolled: the
+// pivot row/column exchanges are predicated swaps over the candidate indices, so the matrix stays in registers
+// (a runtime-indexed private array would live in scratch memory).
+__device__ __forceinline__ void cswap(bool c, double& a, double& b) {
+    const double ta = a, tb = b;
+    a = c ? tb : ta;
+    b = c ? ta : tb;
+}
+
+__device__ bool ldlt6(const double* red, double lambda, double x[6]) {
+    double m[36];
+    {
+        int q = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int b = a; b < 6; b++) { m[6 * a + b] = red[q]; m[6 * b + a] = red[q]; q++; }
+#pragma unroll
+        for (int j = 0; j < 6; j++) m[7 * j] += lambda;
+    }
+    int tr[6];
+    int sign = 0;   // 0 zero, 1 positive semidef, 2 negative semidef, 3 indefinite
+    bool done = false;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        if (done) continue;
+        int big = k;
+        double bv = fabs(m[7 * k]);
+#pragma unroll
+        for (int i = k + 1; i < 6; i++)
+            if (fabs(m[7 * i]) > bv) { bv = fabs(m[7 * i]); big = i; }
+        tr[k] = big;
+#pragma unroll
+        for (int b = k + 1; b < 6; b++) {
+            const bool c = big == b;
+#pragma unroll
+            for (int j = 0; j < k; j++) cswap(c, m[6 * k + j], m[6 * b + j]);
+#pragma unroll
+            for (int i = b + 1; i < 6; i++) cswap(c, m[6 * i + k], m[6 * i + b]);
+            cswap(c, m[7 * k], m[7 * b]);
+#pragma unroll
+            for (int i = k + 1; i < b; i++) cswap(c, m[6 * i + k], m[6 * b + i]);
+        }
+        if (k > 0) {
+            double temp[6];
+#pragma unroll
+            for (int j = 0; j < k; j++) temp[j] = m[7 * j] * m[6 * k + j];
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < k; j++) s += m[6 * k + j] * temp[j];
+            m[7 * k] -= s;
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) {
+                double t = 0.0;
+#pragma unroll
+                for (int j = 0; j < k; j++) t += m[6 * i + j] * temp[j];
+                m[6 * i + k] -= t;
+            }
+        }
+        const double akk = m[7 * k];
+        const bool valid = fabs(akk) > 0.0;
+        if (k == 0 && !valid) {   // the whole diagonal is zero
+            sign = 0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) tr[j] = j;
+            done = true;
+            continue;
+        }
+        if (valid)
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) m[6 * i + k] /= akk;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    double d[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) d[j] = red[21 + j];
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+#pragma unroll
+        for (int i = k + 1; i < 6; i++) cswap(tr[k] == i, d[k], d[i]);
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+#pragma unroll
+        for (int i = k + 1; i < 6; i++) d[i] -= m[6 * i + k] * d[k];
+    const double tol = 2.2250738585072014e-308;   // numeric_limits<double>::min()
+#pragma unroll
+    for (int i = 0; i < 6; i++) d[i] = fabs(m[7 * i]) > tol ? d[i] / m[7 * i] : 0.0;
+#pragma unroll
+    for (int k = 5; k >= 0; k--)
+#pragma unroll
+        for (int i = 0; i < k; i++) d[i] -= m[6 * k + i] * d[k];
+#pragma unroll
+    for (int k = 5; k >= 0; k--)
+#pragma unroll
+        for (int i = k + 1; i < 6; i++) cswap(tr[k] == i, d[k], d[i]);
+#pragma unroll
+    for (int j = 0; j < 6; j++) x[j] = d[j];
+    return sign == 1 || sign == 0;
+}
+
+// SparseOptimizer::optimize(10) on the single pose vertex; T is updated in place. Returns the iterations run.
+__device__ int optimize(const Edges& E, double T[7], const mam_pinhole& c, bool robust, double delta, double* scr,
+                        int* trials) {
+    // initializeOptimization(0): no level-0 edge -> optimize() returns -1 before the loop
+    __shared__ int s_any;
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < E.n; i += PT)
+        if (!E.level[i]) { s_any = 1; break; }
+    __syncthreads();
+    const bool any = s_any != 0;
+    __syncthreads();
+    if (!any) return 0;
+    double lambda = 0.0, ni = 2.0;
+    int nBad = 0, its = 0;
+    bool ok = true;
+    for (int it = 0; it < 10 && ok; it++) {
+        double* red = scr + NW * (NRED + 1) + 8;   // H upper, b, chi (LDS)
+        double currentChi = build_system(E, T, c, robust, delta, scr, red);
+        const double iniChi = currentChi;
+        if (it == 0) {
+            double md = 0.0;
+            md = fmax(fabs(red[0]), md);    // H(0,0)
+            md = fmax(fabs(red[6]), md);    // H(1,1)
+            md = fmax(fabs(red[11]), md);   // H(2,2)
+            md = fmax(fabs(red[15]), md);   // H(3,3)
+            md = fmax(fabs(red[18]), md);   // H(4,4)
+            md = fmax(fabs(red[20]), md);   // H(5,5)
+            lambda = 1e-5 * md;
+            ni = 2;
+            nBad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            double x[6];
+            const bool ok2 = ldlt6(red, lambda, x);
+            double Tn[7];
+            se3::exp_mul(x, T, Tn);
+            double tempChi = active_chi(E, Tn, c, robust, delta, scr);
+            if (!ok2) tempChi = 1.7976931348623157e308;
+            rho = currentChi - tempChi;
+            double scale = 0.0;
+            for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + red[21 + j]);
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && isfinite(tempChi)) {
+                double alpha = 1. - pow((2 * rho - 1), 3);
+                alpha = fmin(alpha, 2. / 3.);
+                lambda *= fmax(1. / 3., alpha);
+                ni = 2;
+                currentChi = tempChi;
+                for (int k = 0; k < 7; k++) T[k] = Tn[k];
+            } else {
+                lambda *= ni;
+                ni *= 2;
+            }
+            qmax++;
+            (*trials)++;
+        } while (rho < 0 && qmax < 10);
+        its++;
+        if (qmax == 10 || rho == 0) ok = false;
+        else {
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+            else nBad = 0;
+            if (nBad >= 3) ok = false;
+        }
+    }
+    return its;
+}
+
+__global__ __launch_bounds__(PT) void k_pose_opt(Args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ double scr[NW * (NRED + 1) + 8 + NRED + 1];   // wave partials | chi sum | H, b, chi sums
+    __shared__ int s_nbad;
+    const int f = blockIdx.x, t = threadIdx.x;
+    const int n = a.n_edges[f];
+    mam_pose_result* R = a.res + f;
+    if (n < 0 || n > a.cap) {
+        if (t == 0) { R->n_inliers = MAM_ERR_CAPACITY; R->rounds = 0; R->iterations = 0; R->lm_trials = 0; }
+        return;
+    }
+    uint8_t* p = smem;
+    Edges E;
+    E.err = reinterpret_cast<double*>(p);      p += a16((size_t)a.cap * 16);
+    float* ox = reinterpret_cast<float*>(p);   p += a16((size_t)a.cap * 4);
+    float* oy = reinterpret_cast<float*>(p);   p += a16((size_t)a.cap * 4);
+    float* X = reinterpret_cast<float*>(p);    p += a16((size_t)a.cap * 4);
+    float* Y = reinterpret_cast<float*>(p);    p += a16((size_t)a.cap * 4);
+    float* Z = reinterpret_cast<float*>(p);    p += a16((size_t)a.cap * 4);
+    float* W = reinterpret_cast<float*>(p);    p += a16((size_t)a.cap * 4);
+    E.level = p;
+    E.ox = ox; E.oy = oy; E.X = X; E.Y = Y; E.Z = Z; E.w = W;
+    E.n = n;
+    const mam_pose_edge* ge = a.edges + (size_t)f * a.stride;
+    uint8_t* out = a.outlier + (size_t)f * a.stride;
+    for (int i = t; i < n; i += PT) {
+        const mam_pose_edge e = ge[i];
+        ox[i] = e.obs[0]; oy[i] = e.obs[1]; X[i] = e.xw[0]; Y[i] = e.xw[1]; Z[i] = e.xw[2]; W[i] = e.inv_sigma2;
+        E.level[i] = 0;
+    }
+    // SE3Quat(Tcw.unit_quaternion().cast<double>(), translation) (normalised)
+    const mam_pose P0 = a.tcw[f];
+    double T0[7] = {(double)P0.q[0], (double)P0.q[1], (double)P0.q[2], (double)P0.q[3],
+                    (double)P0.t[0], (double)P0.t[1], (double)P0.t[2]};
+    se3::normalize_q(T0);
+    double T[7];
+    for (int k = 0; k < 7; k++) T[k] = T0[k];
+    int rounds = 0, its = 0, trials = 0, nBad = 0;
+    __syncthreads();
+    if (n >= 3) {
+        const double delta = (double)(float)sqrt(5.991);   // const float deltaMono = sqrt(5.991) (Optimizer.cc:850)
+        bool robust = true;
+        for (int it = 0; it < 4; it++) {
+            for (int k = 0; k < 7; k++) T[k] = T0[k];   // vSE3->setEstimate(pFrame->GetPose())
+            its += optimize(E, T, a.cam, robust, delta, scr, &trials);
+            rounds++;
+            if (t == 0) s_nbad = 0;
+            __syncthreads();
+            int bad = 0;
+            for (int i = t; i < n; i += PT) {
+                if (E.level[i]) {   // outliers of the last classification: computeError() at the new pose
+                    double e0, e1;
+                    edge_error(E, i, T, a.cam, &e0, &e1);
+                    E.err[2 * i] = e0;
+                    E.err[2 * i + 1] = e1;
+                }
+                const double e0 = E.err[2 * i], e1 = E.err[2 * i + 1], w = (double)E.w[i];
+                const float chi2 = (float)(e0 * (w * e0) + e1 * (w * e1));   // const float chi2 = e->chi2()
+                const bool o = chi2 > 5.991f;
+                E.level[i] = o ? 1 : 0;
+                bad += o ? 1 : 0;
+            }
+            if (bad) atomicAdd(&s_nbad, bad);
+            __syncthreads();
+            nBad = s_nbad;
+            __syncthreads();
+            if (it == 2) robust = false;
+            if (n < 10) break;
+        }
+    }
+    for (int i = t; i < n; i += PT) out[i] = E.level[i];
+    if (t == 0) {
+        R->q[0] = T[0]; R->q[1] = T[1]; R->q[2] = T[2]; R->q[3] = T[3];
+        R->t[0] = T[4]; R->t[1] = T[5]; R->t[2] = T[6];
+        R->n_inliers = n >= 3 ? n - nBad : 0;
+        R->rounds = rounds;
+        R->iterations = its;
+        R->lm_trials = trials;
+    }
+}
+
+}  // namespace pose
+}  // namespace mam
+
+// ==================================================================================================== host
+struct mam_pose_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int cap = 0;
+    size_t lds = 0;
+    mam::StageTimer timer{1};
+    mam::DevBuf<uint8_t> stage;
+};
+
+extern "C" {
+
+int mam_pose_create(int device, mam_pose_ctx** out) {
+    if (!out) return MAM_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    MAM_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) { mam::set_last_error("no such HIP device"); return MAM_ERR_ARG; }
+    MAM_HIP(hipSetDevice(device));
+    mam_pose_ctx* c = new mam_pose_ctx();
+    c->device = device;
+    // LDS carve: as many edges as fit in 160 KB next to the kernel's static scratch
+    size_t lim = 64 * 1024;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::pose::k_pose_opt),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess)
+        lim = 150 * 1024;
+    else
+        (void)hipGetLastError();
+    int cap = 64;
+    while (mam::pose::lds_bytes(cap + 64) <= lim) cap += 64;
+    c->cap = cap;
+    c->lds = mam::pose::lds_bytes(cap);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        mam::set_last_error("hipStreamCreate failed");
+        return MAM_ERR_DEVICE;
+    }
+    *out = c;
+    return MAM_OK;
+}
+
+void mam_pose_destroy(mam_pose_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int mam_pose_max_edges(mam_pose_ctx* c) { return c ? c->cap : MAM_ERR_ARG; }
+
+int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_pose* tcw, const mam_pinhole* cam,
+                                       const mam_pose_edge* edges, int edge_stride, const int32_t* n_edges,
+                                       uint8_t* outlier, mam_pose_result* results, void* stream) {
+    if (!c || nframes < 0 || !cam || edge_stride < 0) return MAM_ERR_ARG;
+    if (nframes == 0) return MAM_OK;
+    if (!tcw || !n_edges || !results || (edge_stride > 0 && (!edges || !outlier))) return MAM_ERR_ARG;
+    if (edge_stride > c->cap) {
+        mam::set_last_error("edge_stride exceeds mam_pose_max_edges()");
+        return MAM_ERR_CAPACITY;
+    }
+    MAM_HIP(hipSetDevice(c->device));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    mam::pose::Args a;
+    a.nframes = nframes;
+    a.tcw = tcw;
+    a.cam = *cam;
+    a.edges = edges;
+    a.stride = edge_stride;
+    a.n_edges = n_edges;
+    a.outlier = outlier;
+    a.res = results;
+    a.cap = c->cap;
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 0);
+        hipLaunchKernelGGL(mam::pose::k_pose_opt, dim3(nframes), dim3(mam::pose::PT), c->lds, s, a);
+    }
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
+
+int mam_pose_optimization(mam_pose_ctx* c, const mam_pose* tcw, const mam_pinhole* cam, int n,
+                          const mam_pose_edge* edges, uint8_t* outlier, mam_pose_result* result) {
+    if (!c || !tcw || !cam || n < 0 || (n > 0 && (!edges || !outlier)) || !result) return MAM_ERR_ARG;
+    if (n > c->cap) {
+        mam::set_last_error("more edges than mam_pose_max_edges()");
+        return MAM_ERR_CAPACITY;
+    }
+    MAM_HIP(hipSetDevice(c->device));
+    const size_t S = std::max(n, 1);
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t bytes = al(S * sizeof(mam_pose_edge)) + al(S) + al(sizeof(mam_pose_result)) + al(sizeof(mam_pose)) + al(4);
+    if (int rc = c->stage.alloc(bytes)) return rc;
+    uint8_t* p = c->stage.p;
+    mam_pose_edge* de = reinterpret_cast<mam_pose_edge*>(p); p += al(S * sizeof(mam_pose_edge));
+    uint8_t* dout = p;                                       p += al(S);
+    mam_pose_result* dres = reinterpret_cast<mam_pose_result*>(p); p += al(sizeof(mam_pose_result));
+    mam_pose* dp = reinterpret_cast<mam_pose*>(p);           p += al(sizeof(mam_pose));
+    int32_t* dn = reinterpret_cast<int32_t*>(p);
+    if (n > 0) MAM_HIP(hipMemcpyAsync(de, edges, sizeof(mam_pose_edge) * n, hipMemcpyHostToDevice, c->stream));
+    MAM_HIP(hipMemcpyAsync(dp, tcw, sizeof(mam_pose), hipMemcpyHostToDevice, c->stream));
+    MAM_HIP(hipMemcpyAsync(dn, &n, 4, hipMemcpyHostToDevice, c->stream));
+    if (int rc = mam_pose_optimization_batch_device(c, 1, dp, cam, de, (int)S, dn, dout, dres, c->stream)) return rc;
+    if (n > 0) MAM_HIP(hipMemcpyAsync(outlier, dout, n, hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipMemcpyAsync(result, dres, sizeof(mam_pose_result), hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipStreamSynchronize(c->stream));
+    return result->n_inliers;
+}
+
+int mam_pose_set_profiling(mam_pose_ctx* c, int enable) {
+    if (!c) return MAM_ERR_ARG;
+    c->timer.collect();
+    c->timer.reset(enable != 0);
+    return MAM_OK;
+}
+
+int mam_pose_stage_times(mam_pose_ctx* c, double* ms_out, int64_t* launches_out) {
+    if (!c || !ms_out || !launches_out) return MAM_ERR_ARG;
+    c->timer.collect();
+    ms_out[0] = c->timer.ms[0];
+    launches_out[0] = c->timer.n[0];
+    return MAM_OK;
+}
+
+}  // extern "C"

@@ -1,6 +1,7 @@
 // MAM3SLAM::Optimizer::LocalBundleAdjustment (include/mam3slam/Optimizer.h).
 // Window build, outlier erase and write-back follow src/Optimizer.cc:1116-1498 line by line (mono agents); the
 // g2o `optimizer.optimize(10)` is mam_lba_solve on the GPU (include/mam_lba.h).
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -19,6 +20,22 @@ struct ThreadLBA {
 };
 thread_local ThreadLBA t_lba;
 
+struct ThreadPose {
+    mam_pose_ctx* ctx = nullptr;
+    ~ThreadPose() {
+        if (ctx) mam_pose_destroy(ctx);
+    }
+};
+thread_local ThreadPose t_pose;
+
+mam_pose_ctx* poseCtx() {
+    if (!t_pose.ctx) {
+        const int rc = mam_pose_create(0, &t_pose.ctx);
+        if (rc < 0) throw std::runtime_error(std::string("mam_pose_create failed: ") + mam_last_error());
+    }
+    return t_pose.ctx;
+}
+
 mam_lba_ctx* lbaCtx() {
     if (!t_lba.ctx) {
         const int rc = mam_lba_create(0, &t_lba.ctx);
@@ -28,6 +45,45 @@ mam_lba_ctx* lbaCtx() {
 }
 
 }  // namespace
+
+int Optimizer::PoseOptimization(Frame* pFrame) {
+    // Set MapPoint vertices (Optimizer.cc:845-895, mono branch): one edge per keypoint with a MapPoint, in order
+    const int N = pFrame->N;
+    std::vector<mam_pose_edge> edges;
+    std::vector<int> idx;
+    edges.reserve(N);
+    idx.reserve(N);
+    if ((int)pFrame->mvbOutlier.size() != N) pFrame->mvbOutlier.assign(N, false);
+    for (int i = 0; i < N; i++) {
+        MapPoint* pMP = pFrame->mvpMapPoints[i];
+        if (!pMP) continue;
+        pFrame->mvbOutlier[i] = false;
+        const KeyPoint& kpUn = pFrame->mvKeysUn[i];
+        mam_pose_edge e;
+        e.obs[0] = kpUn.pt.x;
+        e.obs[1] = kpUn.pt.y;
+        pMP->GetWorldPos(e.xw);
+        e.inv_sigma2 = pFrame->mvInvLevelSigma2[kpUn.octave];
+        edges.push_back(e);
+        idx.push_back(i);
+    }
+    const mam_pose tcw = pFrame->GetPose().toC();
+    const mam_pinhole cam = pFrame->mpCamera->toC();
+    std::vector<uint8_t> outlier(std::max<size_t>(edges.size(), 1));
+    mam_pose_result res;
+    const int n = mam_pose_optimization(poseCtx(), &tcw, &cam, (int)edges.size(), edges.data(), outlier.data(), &res);
+    if (n < 0) throw std::runtime_error(std::string("mam_pose_optimization failed: ") + mam_last_error());
+    if (edges.size() < 3) return 0;   // :997-998 (pose untouched)
+    for (size_t e = 0; e < idx.size(); e++) pFrame->mvbOutlier[idx[e]] = outlier[e] != 0;
+    // Recover optimized pose (:1103-1107): SE3<float>(Quaterniond.cast<float>(), t.cast<float>())
+    SE3f pose;
+    for (int j = 0; j < 4; j++) pose.q[j] = (float)res.q[j];
+    for (int j = 0; j < 3; j++) pose.t[j] = (float)res.t[j];
+    const float qn = std::sqrt(pose.q[0] * pose.q[0] + pose.q[1] * pose.q[1] + pose.q[2] * pose.q[2] + pose.q[3] * pose.q[3]);
+    for (int j = 0; j < 4; j++) pose.q[j] /= qn;
+    pFrame->SetPose(pose);
+    return n;
+}
 
 mam_lba_problem LocalBAWindow::Problem(int iterations) const {
     mam_lba_problem p;

@@ -110,6 +110,8 @@ class FrameData:
     has_mp: np.ndarray | None = None         # GetMapPoint(i) != NULL                   (KeyFrame)
     featvec: dict | None = None              # DBoW2::FeatureVector: node id -> list of feature indices
     pose: tuple | None = None                # (q xyzw float32[4], t float32[3]) = Tcw
+    map_point: np.ndarray | None = None      # mvpMapPoints[i] as an index into a MapPoint table (-1 = NULL)
+    outlier: np.ndarray | None = None        # mvbOutlier
     extra: dict = field(default_factory=dict)
 
     def geom(self) -> FrameGeom:

@@ -175,3 +175,47 @@ def keyframe_pair(F: FrameData, cam: Pinhole, rng: np.random.Generator, n_nodes=
     F12 = fundamental_12(KF1.pose, KF2.pose, K, K)
     ep = epipole_12(KF1.pose, KF2.pose, cam)
     return KF1, KF2, F12, ep
+
+
+def pose_problem(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.7, outlier_frac=0.08, noise=1.0,
+                 rot=0.02, trans=0.06):
+    """Inputs of Optimizer::PoseOptimization around F's keypoints: a true pose, matched MapPoints (world positions)
+    that re-project onto their keypoints with pixel noise (scaled by the keypoint's level), a fraction of gross
+    outliers (points displaced so they re-project 15-60 px away) and an initial pose (F.pose) perturbed from the
+    true one, as the motion model leaves it. Returns (mps_xyz float32[M,3], true pose); sets F.pose and
+    F.map_point."""
+    from .match import quat_to_rot
+
+    qt, tt = small_pose(rng, rot=0.05, trans=0.3)
+    Rt = quat_to_rot(qt).astype(np.float64)
+    n = len(F.keys)
+    sel = np.sort(rng.choice(n, size=int(n * frac), replace=False))
+    m = len(sel)
+    k = F.keys[sel]
+    s = F.scale_factors[k["octave"]].astype(np.float64)
+    z = rng.uniform(2.0, 20.0, m)
+    u = k["x"] + rng.normal(0, noise, m) * s
+    v = k["y"] + rng.normal(0, noise, m) * s
+    bad = rng.random(m) < outlier_frac
+    ang = rng.uniform(0, 2 * np.pi, m)
+    r = rng.uniform(15.0, 60.0, m)
+    u = np.where(bad, u + r * np.cos(ang), u)
+    v = np.where(bad, v + r * np.sin(ang), v)
+    Xc = np.stack([(u - cam.cx) / cam.fx * z, (v - cam.cy) / cam.fy * z, z], 1)
+    Xw = (Xc - tt[None, :].astype(np.float64)) @ Rt   # Rt^T (Xc - t)
+    mp = np.full(n, -1, np.int32)
+    perm = rng.permutation(m)   # MapPoint table order unrelated to keypoint order
+    mp[sel] = perm
+    xyz = np.zeros((m, 3), np.float32)
+    xyz[perm] = Xw.astype(np.float32)
+    dq, dt = small_pose(rng, rot=rot, trans=trans)   # initial = (dq, dt) * true
+    ax, ay, az, aw = [float(x) for x in dq]
+    bx, by, bz, bw = [float(x) for x in qt]
+    q0 = np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by + ay * bw + az * bx - ax * bz,
+                   aw * bz + az * bw + ax * by - ay * bx, aw * bw - ax * bx - ay * by - az * bz])
+    q0 = (q0 / np.linalg.norm(q0)).astype(np.float32)
+    t0 = (quat_to_rot(dq).astype(np.float64) @ tt.astype(np.float64) + dt).astype(np.float32)
+    F.pose = (q0, t0)
+    F.map_point = mp
+    F.outlier = None
+    return xyz, (qt, tt)

@@ -274,3 +274,37 @@ def lba_solve(prob, stop=None):
     rc = L.oracle_lba_solve(C.byref(P), sf, C.byref(R))
     assert rc == 0, rc
     return wrap_result(R, arrs)
+
+
+# ---------------------------------------------------------------- PoseOptimization oracle (oracle/pose_oracle.cpp)
+def pose_optimization_edges(pose, cam, edges):
+    """g2o PoseOptimization restatement on explicit edges (mam3slam_amd.pose.POSE_EDGE_DTYPE).
+    Returns (n_inliers, outlier uint8[n], (q float64[4], t float64[3]), stats)."""
+    from mam3slam_amd.pose import POSE_EDGE_DTYPE, PoseResult, pose_struct
+
+    L = lib()
+    L.oracle_pose_optimization.restype = C.c_int
+    L.oracle_pose_optimization.argtypes = [C.c_void_p] * 2 + [C.c_int] + [C.c_void_p] * 3
+    e = np.ascontiguousarray(edges, POSE_EDGE_DTYPE)
+    n = len(e)
+    out = np.zeros(max(n, 1), np.uint8)
+    res = PoseResult()
+    p = pose_struct(pose)
+    rc = L.oracle_pose_optimization(C.byref(p), C.byref(cam), n, e.ctypes.data if n else None, out.ctypes.data,
+                                    C.byref(res))
+    assert rc >= 0, rc
+    stats = {"rounds": res.rounds, "iterations": res.iterations, "lm_trials": res.lm_trials}
+    return rc, out[:n].copy(), (np.array(res.q[:]), np.array(res.t[:])), stats
+
+
+def pose_optimization(F, mps_xyz, cam):
+    """Optimizer::PoseOptimization(pFrame) on a FrameData (same conventions as mam3slam_amd.pose.pose_optimization):
+    returns (n_inliers, outlier per keypoint, (q, t))."""
+    from mam3slam_amd.pose import make_edges
+
+    idx = np.nonzero(F.map_point >= 0)[0]
+    edges = make_edges(F.keys, 1.0 / F.level_sigma2, idx, mps_xyz[F.map_point[idx]])
+    n, out, qt, _ = pose_optimization_edges(F.pose, cam, edges)
+    outl = np.zeros(len(F.keys), np.uint8)
+    outl[idx] = out
+    return n, outl, qt

@@ -1,6 +1,5 @@
 set -u
 R=${GRAFT_REPO_ROOT:-/root/repo}; O=$R/gpurun_out; mkdir -p $O; cd $R
-for V in distprof resprof; do
-MAM3SLAM_GPU_LIB=$R/build/libmam_gpu_$V.so timeout -k 10 200 python bench.py --batch 1 --lanes 1 --steps 40 --warmup 2 --no-cpu-baseline --no-latency > $O/b1_$V.json 2>$O/b1_$V.err || exit $?
-tail -4 $O/b1_$V.err
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pt_all.log 2>&1; st=$?; tail -5 $O/pt_all.log; [ $st -ne 0 ] && exit $st
+timeout -k 10 400 python bench.py > $O/bench_c1.json 2>$O/bench_c1.err || { tail -5 $O/bench_c1.err; exit 1; }
+cat $O/bench_c1.json

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""PoseOptimization on the GPU (one workgroup per frame) vs the oracle on one host core, c1 / c2 frame shapes.
+
+    python scripts/pose_bench.py [--config c1|c2] [--batch 256] [--reps 20] [--oracle]
+
+Prints one JSON line: ms per batch launch (HIP events on the launch stream), frames/s, single-frame latency,
+LM iterations / trials per frame, and (--oracle) the oracle's ms per frame and the parity of the batch.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c1", choices=["c1", "c2"])
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--oracle", action="store_true")
+    args = ap.parse_args()
+    import torch
+
+    from mam3slam_amd import ORBextractor, pose, scene, synth
+
+    W, H, NF = (640, 480, 1000) if args.config == "c1" else (1280, 720, 2000)
+    ext = ORBextractor(NF, 1.2, 8, 20, 7)
+    cam = scene.pinhole(W, H)
+    B = args.batch
+    kinds = []
+    for i in range(4):
+        k, d, _ = ext(synth.make_frame(W, H, agent=0, frame=i))
+        kinds.append((k, d))
+    edges_l, poses = [], []
+    for f in range(B):
+        k, d = kinds[f % 4]
+        F = scene.make_frame_data(k, d, W, H)
+        xyz, _ = scene.pose_problem(F, cam, np.random.default_rng(f))
+        idx = np.nonzero(F.map_point >= 0)[0]
+        edges_l.append(pose.make_edges(F.keys, 1.0 / F.level_sigma2, idx, xyz[F.map_point[idx]]))
+        poses.append(F.pose)
+    S = max(len(e) for e in edges_l)
+    E = np.zeros((B, S), pose.POSE_EDGE_DTYPE)
+    for f, e in enumerate(edges_l):
+        E[f, :len(e)] = e
+    tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+    for f, (q, t) in enumerate(poses):
+        tcw[f]["q"], tcw[f]["t"] = q, t
+    dev = torch.device("cuda")
+    t_e = torch.from_numpy(E.view(np.uint8).reshape(B, -1)).to(dev)
+    t_n = torch.tensor([len(e) for e in edges_l], dtype=torch.int32, device=dev)
+    t_p = torch.from_numpy(tcw.view(np.uint8)).to(dev)
+    t_o = torch.zeros((B, S), dtype=torch.uint8, device=dev)
+    t_r = torch.zeros((B, pose.POSE_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    P = pose.PoseOptimizer()
+    st = torch.cuda.Stream()
+
+    def run(nf):
+        P.optimize_batch_device(nf, t_p.data_ptr(), cam, t_e.data_ptr(), S, t_n.data_ptr(), t_o.data_ptr(),
+                                t_r.data_ptr(), stream=st.cuda_stream)
+
+    for _ in range(3):
+        run(B)
+        run(1)
+    torch.cuda.synchronize()
+    P.set_profiling(True)
+    for _ in range(args.reps):
+        run(B)
+    torch.cuda.synchronize()
+    ms_b = P.stage_times()["pose"][0] / args.reps
+    P.set_profiling(True)
+    for _ in range(args.reps):
+        run(1)
+    torch.cuda.synchronize()
+    ms_1 = P.stage_times()["pose"][0] / args.reps
+    P.set_profiling(False)
+    lat = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        run(1)
+        st.synchronize()
+        lat.append((time.perf_counter() - t0) * 1e3)
+    res = t_r.cpu().numpy().view(pose.POSE_RESULT_DTYPE).reshape(B)
+    out = {"config": args.config, "batch": B, "edges_per_frame": float(np.mean([len(e) for e in edges_l])),
+           "ms_per_batch_launch": ms_b, "frames_per_s": B / (ms_b * 1e-3), "ms_b1_launch": ms_1,
+           "ms_b1_wall": float(np.median(lat)), "iterations_per_frame": float(res["iterations"].mean()),
+           "lm_trials_per_frame": float(res["lm_trials"].mean())}
+    if args.oracle:
+        from oracle import oracle_py
+
+        n = min(B, 64)
+        t0 = time.perf_counter()
+        ok = 0
+        outs = t_o.cpu().numpy()
+        for f in range(n):
+            no, oo, (qo, to), _ = oracle_py.pose_optimization_edges(poses[f], cam, edges_l[f])
+            ok += int(no == res[f]["n_inliers"] and np.array_equal(oo, outs[f, :len(edges_l[f])]) and
+                      np.max(np.abs(res[f]["q"] - qo)) < 1e-4 and np.max(np.abs(res[f]["t"] - to)) < 1e-4)
+        out["oracle_ms_per_frame"] = (time.perf_counter() - t0) * 1e3 / n
+        out["parity_frames"] = f"{ok}/{n}"
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -5,7 +5,8 @@
 //   test_host_api gpu   the wrappers end to end on the GPU vs the CPU oracle (liboracle.so, test
 //                       infrastructure): ORBextractor bit-exact, both SearchByProjection and
 //                       SearchForTriangulation index-exact with the reference's side effects on mvpMapPoints,
-//                       LocalBundleAdjustment write-back / outlier erase vs the oracle solve.
+//                       LocalBundleAdjustment write-back / outlier erase vs the oracle solve, PoseOptimization
+//                       (mvbOutlier, pose, return value) vs the oracle.
 //
 // Prints "OK <n> checks" and exits 0, or prints the first failure and exits 1.
 #include <cmath>
@@ -36,6 +37,8 @@ int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_k
                                     const mam_featvec* fv2, const float* F12, const float* ep, int check_ori,
                                     int coarse, int32_t* out);
 int oracle_lba_solve(const mam_lba_problem* p, const volatile uint8_t* stop_flag, mam_lba_result* r);
+int oracle_pose_optimization(const mam_pose* tcw, const mam_pinhole* cam, int n, const mam_pose_edge* edges,
+                             uint8_t* outlier, mam_pose_result* res);
 }
 
 using namespace MAM3SLAM;
@@ -511,6 +514,60 @@ static void testLocalBA() {
     CHECK(std::memcmp(&before, &after, sizeof(SE3f)) == 0 && S2.map.GetMapChangeIndex() == 0, "stop flag");
 }
 
+static void testPoseOptimization() {
+    Scene S(4, 500, 1, 33, 0.1f);
+    // a frame that sees the scene's points from the first keyframe's pose: keypoints = its observations
+    KeyFrame* pKF = S.kfs[0].get();
+    Frame F = emptyFrame(pKF->N, 640, 480, S.scales, S.sig2, &S.cam);
+    std::vector<MapPoint*> mpm = pKF->GetMapPointMatches();
+    std::vector<mam_pose_edge> edges;
+    int slot = 0;
+    for (int i = 0; i < pKF->N; i++) {
+        if (i % 7 == 3) continue;   // keypoints without a MapPoint stay NULL
+        F.mvKeysUn[i] = pKF->mvKeysUn[i];
+        F.mvKeys[i] = pKF->mvKeys[i];
+        F.mvpMapPoints[i] = mpm[i];
+        if (!mpm[i]) continue;
+        mam_pose_edge e;
+        e.obs[0] = F.mvKeysUn[i].pt.x;
+        e.obs[1] = F.mvKeysUn[i].pt.y;
+        mpm[i]->GetWorldPos(e.xw);
+        e.inv_sigma2 = F.mvInvLevelSigma2[F.mvKeysUn[i].octave];
+        edges.push_back(e);
+        slot++;
+    }
+    SE3f T0 = pKF->GetPose();
+    T0.t[0] += 0.05f;
+    T0.t[2] -= 0.04f;
+    F.SetPose(T0);
+    std::vector<uint8_t> out(edges.size());
+    mam_pose_result r;
+    const mam_pose tcw = T0.toC();
+    const mam_pinhole cam = S.cam.toC();
+    const int no = oracle_pose_optimization(&tcw, &cam, (int)edges.size(), edges.data(), out.data(), &r);
+    CHECK(no > 0 && no < (int)edges.size(), "oracle inliers %d of %zu", no, edges.size());
+    const int ng = Optimizer::PoseOptimization(&F);
+    CHECK(ng == no, "PoseOptimization returned %d, oracle %d", ng, no);
+    size_t e = 0;
+    for (int i = 0; i < F.N; i++) {
+        if (!F.mvpMapPoints[i]) {
+            CHECK(!F.mvbOutlier[i], "keypoint %d without MapPoint flagged", i);
+            continue;
+        }
+        CHECK(F.mvbOutlier[i] == (out[e] != 0), "mvbOutlier[%d]", i);
+        e++;
+    }
+    const SE3f T = F.GetPose();
+    for (int j = 0; j < 3; j++) CHECK(std::fabs((double)T.t[j] - r.t[j]) <= 1e-4 * (1.0 + std::fabs(r.t[j])), "t[%d]", j);
+    for (int j = 0; j < 4; j++) CHECK(std::fabs((double)T.q[j] - r.q[j]) <= 1e-4, "q[%d]", j);
+    // fewer than 3 correspondences: 0, pose untouched
+    Frame G = emptyFrame(5, 640, 480, S.scales, S.sig2, &S.cam);
+    G.SetPose(T0);
+    G.mvKeysUn[0] = pKF->mvKeysUn[0];
+    G.mvpMapPoints[0] = mpm[0];
+    CHECK(Optimizer::PoseOptimization(&G) == 0 && std::memcmp(&G.GetPose(), &T0, sizeof(SE3f)) == 0, "n < 3");
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     testAlgebra();
@@ -520,6 +577,7 @@ int main(int argc, char** argv) {
         testExtractor();
         testMatcher();
         testLocalBA();
+        testPoseOptimization();
     }
     std::printf("OK %d checks (%s)\n", g_checks, mode.c_str());
     return 0;
