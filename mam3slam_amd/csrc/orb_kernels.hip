@@ -1167,23 +1167,30 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, Le
     const uint8_t* center = lev + (size_t)y * pitch + x;
     // lane = (column u, half): the disk column u spans |v| <= vmax(u) (umax decreases with |v|), lanes 0..30 take
     // v in [-vmax, 0], lanes 32..62 take v in [1, vmax]; integer sums are order-independent
+    // all 16 loads of a lane's column in flight at once (a v-loop would wait out one global latency per pixel);
+    // umax is non-increasing, so vmax(u) = #{v in 1..15 : umax[v] >= |u|}
     int m10 = 0, m01 = 0;
     {
         const int col = lane & 31;
-        if (col < 31) {
-            const int u = col - 15;
-            const int au = u < 0 ? -u : u;
-            int vmax = 0;
-            while (vmax < 15 && au <= g->umax[vmax + 1]) vmax++;
-            const int v0 = lane < 32 ? -vmax : 1, v1 = lane < 32 ? 0 : vmax;
-            const uint8_t* cp = center + u;
-            for (int v = v0; v <= v1; v++) {
-                const int val = cp[v * pitch];
-                m10 += val;
-                m01 += v * val;
-            }
-            m10 *= u;
+        int um[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) um[k] = g->umax[k];
+        const int u = col - 15;
+        const int au = u < 0 ? -u : u;
+        int vmax = 0;
+#pragma unroll
+        for (int k = 1; k < 16; k++) vmax += au <= um[k] ? 1 : 0;
+        const int v0 = lane < 32 ? -vmax : 1, n = col < 31 ? (lane < 32 ? vmax + 1 : vmax) : 0;
+        const uint8_t* cp = center + u + (ptrdiff_t)v0 * pitch;
+        int val[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) val[k] = k < n ? cp[(ptrdiff_t)k * pitch] : 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            m10 += val[k];
+            m01 += (v0 + k) * val[k];
         }
+        m10 *= u;
     }
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);

@@ -1,5 +1,7 @@
 set -u
 R=${GRAFT_REPO_ROOT:-/root/repo}; O=$R/gpurun_out; mkdir -p $O; cd $R
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pt_all.log 2>&1; st=$?; tail -5 $O/pt_all.log; [ $st -ne 0 ] && exit $st
-timeout -k 10 400 python bench.py > $O/bench_c1.json 2>$O/bench_c1.err || { tail -5 $O/bench_c1.err; exit 1; }
-cat $O/bench_c1.json
+for cfg in "256 4" "256 8" "512 4" "512 8" "1024 8" "1024 16"; do
+  set -- $cfg
+  timeout -k 10 300 python bench.py --batch $1 --lanes $2 --no-cpu-baseline --no-latency --no-pose > $O/bl_$1_$2.json 2>$O/bl_$1_$2.err || { tail -3 $O/bl_$1_$2.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bl_$1_$2.json'));print('B $1 lanes $2', round(d['value']), round(d['ms_per_step'],3))"
+done
