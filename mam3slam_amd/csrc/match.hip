@@ -11,7 +11,7 @@
 //   k_grid     per frame: PosInGrid for every keypoint, LDS counting sort by cell (atomics) + per-cell insertion
 //              sort by index -> cell-major list with ascending idx per cell = AssignFeaturesToGrid's cell vectors,
 //              stored as 48-byte records (x, y, idx | octave, descriptor) for one-load candidate tests.
-//   k_gather   one wave per search unit (MapPoint / last-frame entry): the window's candidates flattened in
+//   k_gather   16 lanes (one frame: 64) per search unit (MapPoint / last-frame entry): the window's candidates flattened in
 //              GetFeaturesInArea's order (cells ix -> iy, index order inside) and dealt to the lanes; level +
 //              radius filters, Hamming distance; only the candidates that can change a result kept (dist <=
 //              TH_HIGH, or <= TH_HIGH / nnratio for the ratio test), placed in enumeration order by ballot into a
@@ -32,6 +32,10 @@
 #include "runtime.hpp"
 
 #include <cstdio>
+
+#ifndef MAM_GATHER_LANES
+#define MAM_GATHER_LANES 16   // lanes per search unit in k_gather (64 / lanes units per wave)
+#endif
 
 namespace mam {
 
@@ -278,21 +282,27 @@ __device__ __forceinline__ int rel_threshold(const ProjArgs& p) {
                        : (p.nnratio > 0.f ? min(256, (int)ceilf((float)MAM_TH_HIGH / p.nnratio) + 1) : 256);
 }
 
-// One pass over a unit's window: the window's candidates (cells in ix -> iy order, each cell's keypoints in index
-// order: GetFeaturesInArea's enumeration) are flattened and dealt to the lanes 64 at a time; each lane finds its
-// cell by a binary search over the cell-count scan, tests level / radius / distance, and a ballot places the
-// relevant ones in order. Entries at positions < lim are written to dst. Returns the relevant count.
+// One pass over a unit's window by a group of GW lanes (64 / GW units per wave): the window's candidates (cells in
+// ix -> iy order, each cell's keypoints in index order: GetFeaturesInArea's enumeration) are flattened and dealt
+// to the group's lanes GW at a time; each lane finds its cell by a binary search over the group's cell-count scan,
+// tests level / radius / distance, and a ballot (restricted to the group) places the relevant ones in order.
+// Entries at positions < lim are written to dst. Returns the relevant count. Loop bounds are group-uniform, so a
+// group is either wholly active or wholly idle in every iteration (the width-GW shuffles stay inside it).
+template <int GW>
 __device__ int gather_pass(const ProjArgs& p, int f, const Window& w, int rel, const uint4 u0, const uint4 u1,
                            uint32_t* dst, int lim) {
     const int lane = lane_id();
+    const int gl = lane & (GW - 1);
+    const int gb = lane & ~(GW - 1);   // first lane of the group
     const int ny = w.cy1 - w.cy0 + 1;
     const int ncell = (w.cx1 - w.cx0 + 1) * ny;
     const int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
     const GridEnt* G = p.grid_ent + (size_t)f * p.fr.kp_stride;
-    const uint64_t below = (1ull << lane) - 1ull;
+    const uint64_t below = (1ull << lane) - (1ull << gb);
+    const uint64_t gmask = GW == 64 ? ~0ull : (((1ull << GW) - 1ull) << gb);
     int base = 0;
-    for (int e0 = 0; e0 < ncell; e0 += 64) {
-        const int e = e0 + lane;
+    for (int e0 = 0; e0 < ncell; e0 += GW) {
+        const int e = e0 + gl;
         int k0 = 0, c = 0;
         if (e < ncell) {
             const int ix = w.cx0 + e / ny, iy = w.cy0 + e % ny;
@@ -300,16 +310,21 @@ __device__ int gather_pass(const ProjArgs& p, int f, const Window& w, int rel, c
             k0 = gs[cell];
             c = gs[cell + 1] - k0;
         }
-        const int incl = wave_incl_scan(c);
-        const int tot = __shfl(incl, 63, 64);
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < GW; o <<= 1) {
+            const int t = __shfl_up(incl, o, GW);
+            if (gl >= o) incl += t;
+        }
+        const int tot = __shfl(incl, GW - 1, GW);
         const int kb = k0 - (incl - c);   // record index of candidate t in this lane's cell = kb + t
-        for (int t0 = 0; t0 < tot; t0 += 64) {
-            const int t = t0 + lane;
+        for (int t0 = 0; t0 < tot; t0 += GW) {
+            const int t = t0 + gl;
             int m = 0;   // owner cell: first m with incl[m] > t
 #pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
-                if (__shfl(incl, m + step - 1, 64) <= t) m += step;
-            const int k = __shfl(kb, m, 64) + t;
+            for (int step = GW / 2; step >= 1; step >>= 1)
+                if (__shfl(incl, m + step - 1, GW) <= t) m += step;
+            const int k = __shfl(kb, m, GW) + t;
             bool ok = false;
             uint32_t ent = 0;
             if (t < tot) {
@@ -327,48 +342,50 @@ __device__ int gather_pass(const ProjArgs& p, int f, const Window& w, int rel, c
                     }
                 }
             }
-            const uint64_t b = __ballot(ok);
-            const int o = base + __popcll(b & below);
+            const uint64_t bal = __ballot(ok) & gmask;
+            const int o = base + __popcll(bal & below);
             if (ok && o < lim) dst[o] = ent;
-            base += __popcll(b);
+            base += __popcll(bal);
         }
     }
     return base;
 }
 
-// One wave per unit. Lists go to a fixed slot of slot_cap entries per unit; a longer list is written again into
-// the frame's overflow area (atomic allocation; the list stays contiguous and in order).
+// GW lanes per unit (64 / GW units per wave). Lists go to a fixed slot of slot_cap entries per unit; a longer list
+// is written again into the frame's overflow area (atomic allocation; the list stays contiguous and in order).
+template <int GW>
 __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
-    const long long gw = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
-    const int f = (int)(gw / p.unit_stride);
-    const int j = (int)(gw - (long long)f * p.unit_stride);
-    if (f >= nframes) return;
-    const int lane = lane_id();
+    const long long gu = ((long long)blockIdx.x * 256 + threadIdx.x) / GW;   // global unit slot
+    const int f = (int)(gu / p.unit_stride);
+    const int j = (int)(gu - (long long)f * p.unit_stride);
+    const bool live = f < nframes;
+    const int gl = lane_id() & (GW - 1);
     int32_t* cntp = p.cand_cnt + (size_t)f * p.unit_stride + j;
     int32_t* offp = p.cand_off + (size_t)f * p.unit_stride + j;
     Window w;
+    if (!live) return;
     if (!unit_window(p, f, j, &w)) {
-        if (lane == 0) { *cntp = 0; *offp = 0; }
+        if (gl == 0) { *cntp = 0; *offp = 0; }
         return;
     }
     uint32_t* fpool = p.pool + (size_t)f * p.pool_per_frame;
     const int rel = rel_threshold(p);
     const int CAP = p.slot_cap;
     const uint4 u0 = reinterpret_cast<const uint4*>(w.desc)[0], u1 = reinterpret_cast<const uint4*>(w.desc)[1];
-    int total = gather_pass(p, f, w, rel, u0, u1, fpool + (size_t)j * CAP, CAP);
+    int total = gather_pass<GW>(p, f, w, rel, u0, u1, fpool + (size_t)j * CAP, CAP);
     int off = j * CAP;
     if (total > CAP) {
         int o2 = 0;
-        if (lane == 0) o2 = atomicAdd(&p.pool_total[f], total);
-        o2 = __shfl(o2, 0, 64);
+        if (gl == 0) o2 = atomicAdd(&p.pool_total[f], total);
+        o2 = __shfl(o2, 0, GW);
         if (o2 + total <= p.ovf_cap) {
             off = p.unit_stride * CAP + o2;
-            gather_pass(p, f, w, rel, u0, u1, fpool + off, total);
+            gather_pass<GW>(p, f, w, rel, u0, u1, fpool + off, total);
         } else {
             total = 0;   // capacity: pool_total > ovf_cap makes the resolve stage report the frame
         }
     }
-    if (lane == 0) { *cntp = total; *offp = off; }
+    if (gl == 0) { *cntp = total; *offp = off; }
 }
 
 // ------------------------------------------------------------------------------------------------ resolve
@@ -1027,11 +1044,18 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
         mam::StageTimer::Scope sc(&c->timer, s, 0);
         hipLaunchKernelGGL(mam::k_grid, dim3(F), dim3(1024), 0, s, a);
     }
-    const long long waves = (long long)F * a.unit_stride;
-    const int blocks = (int)((waves + 3) / 4);
     {
+        // batches: 16 lanes per unit (windows hold a few to a few tens of candidates, so four units share a wave and
+        // their dependent global-memory round trips overlap: 0.38 -> 0.22 ms per 256 c1 frames); a single frame:
+        // a whole wave per unit (fewer passes per unit, 26 -> 17 us)
+        const long long units = (long long)F * a.unit_stride;
         mam::StageTimer::Scope sc(&c->timer, s, 1);
-        hipLaunchKernelGGL(mam::k_gather, dim3(blocks), dim3(256), 0, s, a, F);
+        if (F <= 4) {
+            hipLaunchKernelGGL(mam::k_gather<64>, dim3((int)((units * 64 + 255) / 256)), dim3(256), 0, s, a, F);
+        } else {
+            constexpr int GW = MAM_GATHER_LANES;
+            hipLaunchKernelGGL(mam::k_gather<GW>, dim3((int)((units * GW + 255) / 256)), dim3(256), 0, s, a, F);
+        }
     }
     {
         mam::StageTimer::Scope sc(&c->timer, s, 2);
