@@ -68,7 +68,8 @@ def stage_bytes(w, h, n_kp, n_cand, n_last, n_mps, cand_motion, cand_local):
         "blur": 2 * P,                             # read + write every level
         "distribute": 4 * n_cand + 8 * n_kp,       # read candidates, write kept keypoints + ranks
         "describe": n_kp * (961 + 37 * 37 + 60),   # 31x31 moment disk + 37x37 blurred patch + 60 B out
-        "grid": 2 * n_kp * (28 + 2),               # both searches: read keypoints, write cell-sorted index
+        "grid": n_kp * (28 + 32 + 48),             # once per frame (the local search reuses it): keypoints +
+                                                   # descriptors in, 48-B cell-ordered records out
         "gather": n_last * 64 + n_mps * 64 + (cand_motion + cand_local) * (2 + 28 + 32 + 4),
         "resolve": (cand_motion + cand_local) * 4 + (n_last + n_mps) * 8 + 2 * n_kp * 4,
     }
@@ -307,12 +308,14 @@ def main():
     for ln in lanes:
         lo = ln["lo"]
         ln["mm"] = ORBmatcher(0.9, True, device=local)
-        ln["ml"] = ORBmatcher(0.8, True, device=local)
+        # the local-map search shares the motion search's context and reuses the frames' cell grid it built
+        # (AssignFeaturesToGrid runs once per Frame in the reference)
+        ln["ml"] = ORBmatcher(0.8, True, device=local, share=ln["mm"])
         # the motion search leaves the frame's slot state in d_taken (taken_out): the local search's `taken` input
         ln["fr1"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(), None,
                               d_taken[lo].data_ptr())
         ln["fr2"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(),
-                              d_taken[lo].data_ptr())
+                              d_taken[lo].data_ptr(), None, 1)
     m_motion, m_local = lanes[0]["mm"], lanes[0]["ml"]
 
     def match_lane(ln):
@@ -429,7 +432,7 @@ def main():
     # eager tracking steps after the timed region: events cannot sit inside the replayed graph
     # The lanes run one after another here (synchronised in between), so every launch is timed standalone, as
     # in a --lanes 1 rocprofv3 kernel trace; stage_ms_per_step sums the lanes (work per step, not wall time).
-    objs = [o for ln in lanes for o in (ln["ext"], ln["mm"], ln["ml"])]
+    objs = [o for ln in lanes for o in (ln["ext"], ln["mm"])]   # ml shares mm's context (and its stage timer)
     for o in objs:
         o.set_profiling(True)
     torch.cuda.synchronize(dev)
@@ -445,10 +448,10 @@ def main():
         for k, v in ln["ext"].stage_times().items():
             a = stages.get(k, (0.0, 0))
             stages[k] = (a[0] + v[0], a[1] + v[1])
-        sm1, sm2 = ln["mm"].stage_times(), ln["ml"].stage_times()
+        sm = ln["mm"].stage_times()   # both searches of the lane (one context)
         for k in ("grid", "gather", "resolve"):
             a = stages.get(k, (0.0, 0))
-            stages[k] = (a[0] + sm1[k][0] + sm2[k][0], a[1] + sm1[k][1] + sm2[k][1])
+            stages[k] = (a[0] + sm[k][0], a[1] + sm[k][1])
     for o in objs:
         o.set_profiling(False)
     lba_stage = lba_solver.stage_times() if lba_solver is not None else None
@@ -457,7 +460,7 @@ def main():
     m_motion.set_profiling(False)
     m_local.set_profiling(False)
     fr1_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), None, d_taken.data_ptr())
-    fr2_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), d_taken.data_ptr())
+    fr2_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), d_taken.data_ptr(), None, 1)
 
     def one_frame_launch():
         ext.extract_batch_device(d_img.data_ptr(), 1, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap,

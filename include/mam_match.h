@@ -143,6 +143,10 @@ typedef struct mam_frames_dev {
     uint8_t* taken_out;       /* [nframes][kp_stride] or NULL: the slot state after a projection search (1 =
                                  mvpMapPoints[i] holds a MapPoint with Observations() > 0, rotation-cleared
                                  slots 0), i.e. the `taken` input of the frame's next search */
+    int32_t reuse_grid;       /* nonzero: the frames' cell grid (AssignFeaturesToGrid, Frame.cc:385-416 — built once
+                                 per Frame in the reference) is the one this context built in its previous search
+                                 over the same keys/counts/nframes/kp_stride; the search skips rebuilding it
+                                 (MAM_ERR_ARG if the context's last search was over other frames) */
 } mam_frames_dev;
 
 /* Frame f matches n_mps[f] MapPoints at mps + f*mp_stride. Outputs at out_kp_to_mp + f*kp_stride and

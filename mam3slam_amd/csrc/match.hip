@@ -440,8 +440,16 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
 #ifdef MAM_RESOLVE_PROFILE
     long long rp0 = clock64();
 #endif
-    if (p.out_n[f] < 0) return;   // grid stage flagged this frame
-    if (p.pool_total[f] > p.ovf_cap) {   // a list did not fit its slot nor the overflow area
+    const int ptot = p.pool_total[f];
+    __syncthreads();
+    // reset for the next search on this context: a search that reuses the grid (mam_frames_dev.reuse_grid) skips
+    // k_grid, which otherwise zeroes it
+    if (t == 0) p.pool_total[f] = 0;
+    if (n > GRID_SORT_MAX) {   // the grid stage could not sort this frame
+        if (t == 0) p.out_n[f] = MAM_ERR_CAPACITY;
+        return;
+    }
+    if (ptot > p.ovf_cap) {   // a list did not fit its slot nor the overflow area
         if (t == 0) p.out_n[f] = MAM_ERR_CAPACITY;
         return;
     }
@@ -996,6 +1004,10 @@ struct mam_match_ctx {
     DevBuf<mam::GridEnt> grid_ent;
     DevBuf<int32_t> grid_start, cand_cnt, cand_off, pool_total, out_n_tmp;
     DevBuf<uint32_t> pool, events;
+    // frames the grid scratch holds (mam_frames_dev.reuse_grid is accepted only for the same frames)
+    const void* grid_keys = nullptr;
+    const void* grid_counts = nullptr;
+    int grid_nframes = 0, grid_stride = 0;
     // host-API staging
     DevBuf<uint8_t> stage;
 };
@@ -1040,9 +1052,20 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     a.pool = c->pool.p;
     a.pool_total = c->pool_total.p;
     a.events = c->events.p;
-    {
+    if (a.fr.reuse_grid) {
+        // AssignFeaturesToGrid runs once per Frame (Frame.cc:385-416): the previous search on this context built it
+        if (c->grid_keys != (const void*)a.fr.keys || c->grid_counts != (const void*)a.fr.counts ||
+            c->grid_nframes != F || c->grid_stride != a.fr.kp_stride) {
+            mam::set_last_error("reuse_grid: this context's last search was not over the same frames");
+            return MAM_ERR_ARG;
+        }
+    } else {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
         hipLaunchKernelGGL(mam::k_grid, dim3(F), dim3(1024), 0, s, a);
+        c->grid_keys = a.fr.keys;
+        c->grid_counts = a.fr.counts;
+        c->grid_nframes = F;
+        c->grid_stride = a.fr.kp_stride;
     }
     {
         // batches: 16 lanes per unit (windows hold a few to a few tens of candidates, so four units share a wave and
@@ -1224,6 +1247,7 @@ static int stage_frame(mam_match_ctx* c, int n, const mam_keypoint* keys, const 
     fr->counts = *dcount;
     fr->taken = taken ? dt : nullptr;
     fr->taken_out = nullptr;
+    fr->reuse_grid = 0;
     return MAM_OK;
 }
 

@@ -49,7 +49,7 @@ class FeatVec(C.Structure):
 
 class FramesDev(C.Structure):
     _fields_ = [("nframes", C.c_int32), ("kp_stride", C.c_int32), ("keys", C.c_void_p), ("desc", C.c_void_p),
-                ("counts", C.c_void_p), ("taken", C.c_void_p), ("taken_out", C.c_void_p)]
+                ("counts", C.c_void_p), ("taken", C.c_void_p), ("taken_out", C.c_void_p), ("reuse_grid", C.c_int32)]
 
 
 MP_TRACK_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("view_cos", "<f4"), ("track_depth", "<f4"),
@@ -170,14 +170,24 @@ def epipole_12(pose1, pose2, cam2: Pinhole):
 class ORBmatcher:
     TH_HIGH, TH_LOW, HISTO_LENGTH = TH_HIGH, TH_LOW, HISTO_LENGTH
 
-    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0, share: "ORBmatcher" = None):
+        """share: use another matcher's device context (its scratch and stream state), so a search can reuse the
+        cell grid that matcher's last search built over the same frames (FramesDev.reuse_grid)."""
         self.mfNNratio = float(nnratio)
         self.mbCheckOrientation = bool(checkOri)
         self._L = _bind()
-        self._ctx = C.c_void_p()
-        check(self._L.mam_match_create(int(device), C.byref(self._ctx)), "mam_match_create")
+        self._owner = share is None
+        if share is not None:
+            self._share = share   # keep the owner alive
+            self._ctx = share._ctx
+        else:
+            self._ctx = C.c_void_p()
+            check(self._L.mam_match_create(int(device), C.byref(self._ctx)), "mam_match_create")
 
     def close(self):
+        if not getattr(self, "_owner", False):
+            self._ctx = C.c_void_p()
+            return
         if getattr(self, "_ctx", None) and self._ctx.value:
             self._L.mam_match_destroy(self._ctx)
             self._ctx = C.c_void_p()

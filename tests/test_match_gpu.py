@@ -217,3 +217,57 @@ def test_motion_batch_device_taken_out(gpu_lib, oracle, frames):
         exp = np.where(oo >= 0, lasts[f]["nobs"][np.maximum(oo, 0)] > 0, (oo == -1) & (taken[f, :n] > 0))
         assert np.array_equal(tout[f, :n], exp.astype(np.uint8)), f
         assert not tout[f, n:].any()
+
+
+def test_reuse_grid_shared_context(gpu_lib, oracle, frames):
+    """The local-map search on the motion search's context reuses its cell grid (FramesDev.reuse_grid): same results
+    as a fresh build; a reuse request over other frames is refused (MAM_ERR_ARG)."""
+    import torch
+
+    from mam3slam_amd._lib import MamError
+    from mam3slam_amd.match import MP_TRACK_DTYPE, FramesDev, ORBmatcher
+
+    w, h, k, d = frames[0]
+    cam = scene.pinhole(w, h)
+    Fn, S = 3, 1100
+    keys = np.zeros((Fn, S), k.dtype)
+    desc = np.zeros((Fn, S, 32), np.uint8)
+    counts = np.zeros((Fn, 2), np.int32)
+    FD, mp_list = [], []
+    for f in range(Fn):
+        rng = np.random.default_rng(90 + f)
+        sel = np.sort(rng.choice(len(k), size=len(k) - 3 * f, replace=False))
+        F = scene.make_frame_data(k[sel], d[sel], w, h)
+        keys[f, :len(sel)], desc[f, :len(sel)], counts[f, 0] = F.keys, F.desc, len(sel)
+        FD.append(F)
+        mp_list.append(scene.local_mappoints(F, rng))
+    ms = max(len(m) for m in mp_list)
+    mps = np.zeros((Fn, ms), MP_TRACK_DTYPE)
+    for f in range(Fn):
+        mps[f, :len(mp_list[f])] = mp_list[f]
+    dev = torch.device("cuda")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    t_keys, t_desc, t_cnt = T(keys.view(np.uint8).reshape(Fn, -1)), T(desc), T(counts)
+    t_mps, t_nmps = T(mps.view(np.uint8).reshape(Fn, -1)), T(np.array([len(m) for m in mp_list], np.int32))
+    outs = []
+    owner = ORBmatcher(0.8, True)
+    sharer = ORBmatcher(0.8, True, share=owner)
+    for reuse, M in ((0, owner), (1, sharer)):
+        t_out = torch.zeros((Fn, S), dtype=torch.int32, device=dev)
+        t_nm = torch.zeros(Fn, dtype=torch.int32, device=dev)
+        fr = FramesDev(Fn, S, t_keys.data_ptr(), t_desc.data_ptr(), t_cnt.data_ptr(), None, None, reuse)
+        M.search_by_projection_batch_device(FD[0], fr, t_mps.data_ptr(), ms, t_nmps.data_ptr(), 1.0, t_out.data_ptr(),
+                                            t_nm.data_ptr())
+        torch.cuda.synchronize()
+        outs.append((t_out.cpu().numpy(), t_nm.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    for f in range(Fn):
+        no, oo = oracle.search_by_projection(FD[f], mp_list[f], 1.0, nnratio=0.8)
+        assert outs[1][1][f] == no and np.array_equal(outs[1][0][f, :counts[f, 0]], oo)
+    # reuse over a different frame set (fewer frames) is refused
+    fr_bad = FramesDev(Fn - 1, S, t_keys.data_ptr(), t_desc.data_ptr(), t_cnt.data_ptr(), None, None, 1)
+    t_out = torch.zeros((Fn, S), dtype=torch.int32, device=dev)
+    t_nm = torch.zeros(Fn, dtype=torch.int32, device=dev)
+    with pytest.raises(MamError):
+        sharer.search_by_projection_batch_device(FD[0], fr_bad, t_mps.data_ptr(), ms, t_nmps.data_ptr(), 1.0,
+                                                 t_out.data_ptr(), t_nm.data_ptr())
