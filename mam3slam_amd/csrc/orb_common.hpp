@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/mam_orb.h"
 
 namespace mam {
@@ -49,6 +51,10 @@ struct LevelGeom {
     int tile_base;          // first blur tile of this level within a frame
     int tiles_x, tiles_y;
     int pad1;
+    // packed resize coefficients (k_pyr_flat): per output quad two uint4 {base | o0..o3 << 12.. | vec << 28,
+    // a0|a1<<16 x4}, per output row int2 {yofs, ibeta0 | ibeta1 << 16}
+    const uint4* qcoef;
+    const int2* rcoef;
 };
 
 struct Geom {

@@ -55,6 +55,8 @@ struct mam_orb_ctx {
     DevBuf<mam::CellDesc> d_cells;
     DevBuf<int> d_tabs_i;
     DevBuf<short> d_tabs_s;
+    DevBuf<uint4> d_qcoef;
+    DevBuf<int2> d_rcoef;
     // per-batch device scratch
     DevBuf<uint8_t> d_pyr, d_blur, d_input;
     DevBuf<uint32_t> d_cand, d_keys, d_okey, d_orank;
@@ -163,6 +165,7 @@ size_t distribute_lds_bytes(int NC, int max_cells) {
 
 int build_pyr_plan(mam_orb_ctx* c, int nb);
 int pyr_forced_bands();
+bool pyr_flat_enabled();
 
 // Geometry for a W x H frame and capacity F (reallocates device scratch when either grows/changes).
 int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
@@ -262,6 +265,9 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         std::vector<short> al, be;
         std::vector<size_t> ioff(L, 0), soff(L, 0);
         std::vector<int> xmaxv(L, 0), xvecv(L, 0);
+        std::vector<uint4> qtab;
+        std::vector<int2> rtab;
+        std::vector<size_t> qoff(L, 0), roff(L, 0);
         c->h_yofs.assign(L, {});
         c->pyr_plans.clear();
         for (int l = 1; l < L; l++) {
@@ -276,6 +282,32 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
             ts.insert(ts.end(), be.begin(), be.end());
             xmaxv[l] = xmax;
             xvecv[l] = xvec;
+            // packed coefficients of k_pyr_flat (see LevelGeom.qcoef)
+            {
+                const int dw = g.L[l].w, dh = g.L[l].h, nq = (dw + 3) / 4;
+                qoff[l] = qtab.size();
+                for (int q = 0; q < nq; q++) {
+                    uint32_t w0 = 0, pa[4] = {0, 0, 0, 0};
+                    int sx[4];
+                    for (int i = 0; i < 4; i++) sx[i] = xo[std::min(4 * q + i, dw - 1)];
+                    const int base = sx[0] & ~3;
+                    w0 = (uint32_t)base;
+                    for (int i = 0; i < 4; i++) {
+                        const int dx = 4 * q + i, x = std::min(dx, dw - 1);
+                        const bool edge = dx >= xmax;
+                        const int a0 = edge ? 2048 : al[2 * x], a1 = edge ? 0 : al[2 * x + 1];
+                        w0 |= (uint32_t)(sx[i] - base) << (12 + 4 * i);
+                        if (dx < xvec) w0 |= 1u << (28 + i);
+                        pa[i] = (uint32_t)(a0 & 0xFFFF) | ((uint32_t)(a1 & 0xFFFF) << 16);
+                    }
+                    qtab.push_back(make_uint4(w0, pa[0], pa[1], pa[2]));
+                    qtab.push_back(make_uint4(pa[3], 0, 0, 0));
+                }
+                roff[l] = rtab.size();
+                for (int dy = 0; dy < dh; dy++)
+                    rtab.push_back(make_int2(yo[dy], (be[2 * dy] & 0xFFFF) | ((int)be[2 * dy + 1] << 16)));
+                if (xo[dw - 1] > 4095) { g_last_error = "level too wide for the packed resize table"; return MAM_ERR_ARG; }
+            }
             // pyr_quad reads three source words per row: the four source columns of an output quad (and the +1 tap)
             // must lie within 12 bytes of the quad's word-aligned first column (scale factors up to ~2.6)
             for (int dx = 0; dx < g.L[l].w; dx += 4)
@@ -299,8 +331,14 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         if (int rc = c->d_tabs_s.alloc(std::max<size_t>(ts.size(), 1))) return rc;
         if (!ti.empty()) MAM_HIP(hipMemcpy(c->d_tabs_i.p, ti.data(), ti.size() * sizeof(int), hipMemcpyHostToDevice));
         if (!ts.empty()) MAM_HIP(hipMemcpy(c->d_tabs_s.p, ts.data(), ts.size() * sizeof(short), hipMemcpyHostToDevice));
+        if (int rc = c->d_qcoef.alloc(std::max<size_t>(qtab.size(), 1))) return rc;
+        if (int rc = c->d_rcoef.alloc(std::max<size_t>(rtab.size(), 1))) return rc;
+        if (!qtab.empty()) MAM_HIP(hipMemcpy(c->d_qcoef.p, qtab.data(), qtab.size() * sizeof(uint4), hipMemcpyHostToDevice));
+        if (!rtab.empty()) MAM_HIP(hipMemcpy(c->d_rcoef.p, rtab.data(), rtab.size() * sizeof(int2), hipMemcpyHostToDevice));
         for (int l = 1; l < L; l++) {
             mam::LevelGeom& lv = g.L[l];
+            lv.qcoef = c->d_qcoef.p + qoff[l];
+            lv.rcoef = c->d_rcoef.p + roff[l];
             lv.xofs = c->d_tabs_i.p + ioff[l];
             lv.yofs = c->d_tabs_i.p + ioff[l] + lv.w;
             lv.ialpha = c->d_tabs_s.p + soff[l];
@@ -411,6 +449,15 @@ int build_pyr_plan(mam_orb_ctx* c, int nb) {
     return MAM_OK;
 }
 
+// MAM_PYR_FLAT=0 forces the LDS block kernel for the per-level launches (experiments / parity cross-check)
+bool pyr_flat_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("MAM_PYR_FLAT");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 int pyr_forced_bands() {
     static const int forced = [] {
         const char* e = getenv("MAM_PYR_BANDS");
@@ -449,11 +496,20 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
             hipLaunchKernelGGL(mam::k_pyr_bands, dim3(pp->nb, F), dim3(256), pp->lds, s, c->d_geom.p, src, c->d_pyr.p,
                                pp->bands.p, pp->buf1_off, pp->rc_off);
         } else {
+            // k_pyr_flat reads whole source words: level 0 rows must be word-aligned and a multiple of 4 wide (the
+            // last word of the frame's last row must not run past the caller's buffer)
+            const bool flat = pyr_flat_enabled() && ((stride | (size_t)d_in | (size_t)g.L[0].w) & 3) == 0;
             const size_t lds = (size_t)g.pyr_seg_w * g.pyr_rows + 16;   // pyr_quad's window past the last row
             for (int l = 1; l < L; l++) {
                 const mam::LevelGeom& lv = g.L[l];
-                dim3 grid((lv.w + mam::PYR_XB - 1) / mam::PYR_XB, (lv.h + mam::PYR_RB - 1) / mam::PYR_RB, F);
-                hipLaunchKernelGGL(mam::k_pyr_down, grid, dim3(256), lds, s, c->d_geom.p, l, src, c->d_pyr.p);
+                if (flat) {
+                    const long long nq = (long long)((lv.w + 3) / 4) * lv.h;
+                    hipLaunchKernelGGL(mam::k_pyr_flat, dim3((int)((nq + 255) / 256), F), dim3(256), 0, s, c->d_geom.p,
+                                       l, src, c->d_pyr.p);
+                } else {
+                    dim3 grid((lv.w + mam::PYR_XB - 1) / mam::PYR_XB, (lv.h + mam::PYR_RB - 1) / mam::PYR_RB, F);
+                    hipLaunchKernelGGL(mam::k_pyr_down, grid, dim3(256), lds, s, c->d_geom.p, l, src, c->d_pyr.p);
+                }
             }
         }
     }

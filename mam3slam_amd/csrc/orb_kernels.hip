@@ -171,6 +171,48 @@ __device__ __forceinline__ uint32_t pyr_quad(const uint8_t* S0, const uint8_t* S
     return packed;
 }
 
+// One thread per output quad of the whole level (row-major over every frame's level): no LDS staging, every lane
+// busy (the block kernel leaves most lanes idle on levels narrower than its 1024-pixel tiles), the quad's column
+// coefficients pre-packed (LevelGeom.qcoef) and its three source words per row read straight from the level
+// above. Requires word-aligned source rows (the host falls back to k_pyr_down otherwise).
+__global__ __launch_bounds__(256) void k_pyr_flat(const Geom* __restrict__ g, int l, LevelSrc s, uint8_t* pyr) {
+    const LevelGeom& L = g->L[l];
+    const int nq = (L.w + 3) >> 2;
+    const int qi = blockIdx.x * 256 + threadIdx.x;
+    const int f = blockIdx.y;
+    if (qi >= nq * L.h) return;
+    const int dy = qi / nq, q = qi - dy * nq;
+    const uint4 c0 = L.qcoef[2 * q], c1 = L.qcoef[2 * q + 1];
+    const int2 rc = L.rcoef[dy];
+    PyrQuad cq;
+    cq.base = (int)(c0.x & 0xFFFu);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        cq.o[i] = (int)((c0.x >> (12 + 4 * i)) & 0xFu);
+        cq.vec[i] = ((c0.x >> (28 + i)) & 1u) != 0;
+    }
+    const uint32_t pa[4] = {c0.y, c0.z, c0.w, c1.x};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        cq.a0[i] = (int)(pa[i] & 0xFFFFu);
+        cq.a1[i] = (int)(pa[i] >> 16);
+    }
+    const int sh = g->L[l - 1].h;
+    const int sy = rc.x;
+    const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
+    const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
+    int spitch;
+    const uint8_t* src = level_ptr(g, s, f, l - 1, &spitch);
+    const uint32_t packed = pyr_quad(src + (size_t)ry0 * spitch, src + (size_t)ry1 * spitch, cq,
+                                     (int)(short)(rc.y & 0xFFFF), rc.y >> 16);
+    uint8_t* o = pyr + L.pyr_off + (size_t)f * L.frame_bytes + (size_t)dy * L.pitch + 4 * q;
+    if (4 * q + 4 <= L.w) {
+        *reinterpret_cast<uint32_t*>(o) = packed;
+    } else {
+        for (int i = 0; i < 4 && 4 * q + i < L.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+    }
+}
+
 // One workgroup per PYR_XB x PYR_RB output block: the source rows/columns the block reads are staged in LDS
 // (32-bit loads where aligned), each thread owns one 4-pixel column quad for the block's rows and keeps its
 // xofs/alpha coefficients in registers.

@@ -126,3 +126,30 @@ def test_error_contract(gpu_lib):
     # flat image: no corners at all -> zero keypoints, monoIndex 0
     k, d, m = ext(np.full((480, 640), 128, np.uint8))
     assert len(k) == 0 and m == 0
+
+
+@pytest.mark.parametrize("w,h,nfeat", CASES[:3])
+def test_batch_pyramid_levels(gpu_lib, oracle, w, h, nfeat):
+    """Batches (> 4 frames) take the per-level one-thread-per-quad resize (k_pyr_flat), single frames the one-launch
+    band pyramid: both bit-exact vs cv::resize's fixed-point restatement on every level and frame."""
+    import torch
+
+    F = 6
+    ext = _extractor(nfeat)
+    imgs = np.stack([synth.make_frame(w, h, agent=6, frame=i) for i in range(F)])
+    cap = ext.max_keypoints()
+    d_img = torch.from_numpy(imgs).cuda()
+    d_kps = torch.zeros((F, cap * 28), dtype=torch.uint8, device="cuda")
+    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.zeros((F, 2), dtype=torch.int32, device="cuda")
+    ext.extract_batch_device(d_img.data_ptr(), F, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                             d_cnt.data_ptr())
+    torch.cuda.synchronize()
+    p = oracle.params(nfeat)
+    for i in (0, F - 1):
+        levels = oracle.pyramid(imgs[i], p)
+        for l, lev in enumerate(levels):
+            d = _first_diff(ext.level(l, i), lev)
+            assert d is None, f"frame {i} level {l} pixel {d}"
+            d = _first_diff(ext.debug_blurred(l, i), oracle.gaussian7(lev))
+            assert d is None, f"frame {i} blurred level {l} pixel {d}"
