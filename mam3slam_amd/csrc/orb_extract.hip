@@ -472,8 +472,9 @@ mam_orb_ctx::PyrPlan* pyr_plan(mam_orb_ctx* c, int nb, size_t lds_max) {
 }
 
 // The single-launch pyramid pays ~1.2-2x the arithmetic for one launch instead of nlevels-1: it wins for a few frames
-// (latency-bound launches), the per-level launches win for batches (MI355X, c1: 1 frame 34 vs 54 us; 64 frames
-// 0.67 vs 0.52 ms per 256). Few frames: as many bands as fit (shortest chain per workgroup).
+// (latency-bound launches), the per-level launches win for batches (MI355X, c1: one frame 33 vs 54 us; batches: the
+// per-level k_pyr_flat launches 0.37 ms per 256 frames vs 0.67 for the bands). Few frames: as many bands as fit
+// (shortest chain per workgroup).
 // MAM_PYR_BANDS=n forces n bands (0: per-level k_pyr_down launches).
 mam_orb_ctx::PyrPlan* choose_pyr_plan(mam_orb_ctx* c, int F) {
     const int forced = pyr_forced_bands();

@@ -8,6 +8,10 @@
         coalesced reads: x2), keyed by bench.py stage name for the single-kernel stages.
     python scripts/profile_summary.py gaps <run_results.db> [first_kernel]
         per-frame kernel timeline of a B=1 latency run (durations and inter-kernel gaps)
+    python scripts/profile_summary.py mfma <pmc_results.db> <out.json>
+        per-kernel FP64 MFMA flops (SQ_INSTS_VALU_MFMA_MOPS_F64 x 512), MFMA-busy fraction of the run
+        (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 1024 SIMDs)) and the achieved FP64-MFMA rate over the kernel's
+        dispatch duration vs the gfx950 dense FP64 peak
 """
 from __future__ import annotations
 
@@ -81,6 +85,35 @@ def traffic(fetch_db: str, write_db: str, out: str) -> None:
         print(f"{v['bytes_per_launch'] / 1e6:10.2f} MB/launch  fetch {v['fetch_kb_raw']:10.0f} KB  write {v['write_kb']:10.0f} KB  {k[:70]}")
 
 
+def mfma(db: str, out: str, simds: int = 1024, fp64_peak_tflops: float = 78.6) -> None:
+    c = sqlite3.connect(db)
+    rows = c.execute("select kernel_name, counter_name, value, duration, dispatch_id from counters_collection").fetchall()
+    agg = defaultdict(lambda: defaultdict(list))
+    dur = defaultdict(dict)
+    for name, cn, v, d, did in rows:
+        agg[name][cn].append(float(v))
+        dur[name][did] = float(d)
+    res = {"_note": "FP64 MFMA flops = SQ_INSTS_VALU_MFMA_MOPS_F64 * 512 (rocprofv3 MfmaFlopsF64); busy = "
+                    "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 1024 SIMDs) (rocprofv3 MfmaUtil, gfx94x formula); "
+                    "tflops = flops / mean dispatch duration; peak = MI355X dense FP64 (78.6 TF/s)", "kernels": {}}
+    for name, cs in agg.items():
+        n = max(len(dur[name]), 1)
+        flops = sum(cs.get("SQ_INSTS_VALU_MFMA_MOPS_F64", [0.0])) / n * 512.0
+        busy = sum(cs.get("SQ_VALU_MFMA_BUSY_CYCLES", [0.0])) / n
+        gui = sum(cs.get("GRBM_GUI_ACTIVE", [0.0])) / max(len(cs.get("GRBM_GUI_ACTIVE", [1])), 1)
+        d_ns = sum(dur[name].values()) / n
+        if flops <= 0 and busy <= 0:
+            continue
+        tf = flops / (d_ns * 1e-9) / 1e12 if d_ns > 0 else 0.0
+        res["kernels"][name] = {"mfma_f64_flops_per_launch": flops, "mean_duration_us": d_ns / 1e3,
+                                "mfma_f64_tflops": tf, "frac_of_fp64_peak": tf / fp64_peak_tflops,
+                                "mfma_busy_frac": busy / (gui * simds) if gui > 0 else None}
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in res["kernels"].items():
+        print(f"{k[:60]:60s} {v['mfma_f64_flops_per_launch'] / 1e6:8.2f} MFLOP {v['mean_duration_us']:8.1f} us "
+              f"{v['mfma_f64_tflops']:6.3f} TF/s busy {v['mfma_busy_frac']}")
+
+
 def gaps(db: str, first_kernel: str = "k_pyr_down", frames: int = 40) -> None:
     """Per-frame timeline of a B=1 latency run: the kernels of the last `frames` frames (a frame starts at each
     launch of `first_kernel` that follows a launch of another kernel), their mean durations in launch order, and the
@@ -120,6 +153,8 @@ if __name__ == "__main__":
         stats(sys.argv[2], sys.argv[3])
     elif mode == "traffic":
         traffic(sys.argv[2], sys.argv[3], sys.argv[4])
+    elif mode == "mfma":
+        mfma(sys.argv[2], sys.argv[3])
     elif mode == "gaps":
         gaps(sys.argv[2], *(sys.argv[3:4]))
     else:
