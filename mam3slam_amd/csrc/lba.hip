@@ -22,6 +22,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <limits>
@@ -749,9 +750,18 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
         }
         (void)hipGetLastError();
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        return MAM_ERR_DEVICE;
+    // Highest stream priority: LocalMapping's solve shares the GPU with Tracking's full-chip launches, and its small
+    // latency-bound kernels (and the host round trip of every LM trial) should not queue behind them.
+    // MAM_LBA_PRIORITY=0 keeps the default priority.
+    int least = 0, greatest = 0;
+    const char* pe = std::getenv("MAM_LBA_PRIORITY");
+    const bool prio = !(pe && pe[0] == '0') && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
+    if (!(prio && hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest) == hipSuccess)) {
+        (void)hipGetLastError();
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete c;
+            return MAM_ERR_DEVICE;
+        }
     }
     *out = c;
     return MAM_OK;
