@@ -47,6 +47,7 @@ public:
 
     int mnScaleLevels = 0;
     float mfScaleFactor = 0.f;
+    float mfLogScaleFactor = 0.f;   /* log(mfScaleFactor) (Frame.cc:313) */
     std::vector<float> mvScaleFactors, mvInvScaleFactors, mvLevelSigma2, mvInvLevelSigma2;
 
     float mnMinX = 0.f, mnMaxX = 0.f, mnMinY = 0.f, mnMaxY = 0.f;
@@ -71,6 +72,7 @@ public:
     std::vector<MapPoint*> GetMapPointMatches();
     MapPoint* GetMapPoint(size_t idx);
     void AddMapPoint(MapPoint* pMP, size_t idx);
+    void ReplaceMapPointMatch(const int& idx, MapPoint* pMP);   /* KeyFrame.cc:320-323 */
     void EraseMapPointMatch(int idx);
     void EraseMapPointMatch(MapPoint* pMP);
 
@@ -90,6 +92,7 @@ public:
     std::vector<float> mvuRight;
     Mat8U mDescriptors;
     int mnScaleLevels;
+    float mfLogScaleFactor;
     std::vector<float> mvScaleFactors, mvLevelSigma2, mvInvLevelSigma2;
     float mnMinX, mnMaxX, mnMinY, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv;
     const Pinhole* mpCamera;
@@ -117,8 +120,15 @@ public:
     void AddObservation(KeyFrame* pKF, int idx);          /* MapPoint.cc:133-166, mono */
     void EraseObservation(KeyFrame* pKF);                 /* MapPoint.cc:168-201 */
     std::tuple<int, int> GetIndexInKeyFrame(KeyFrame* pKF);
+    bool IsInKeyFrame(KeyFrame* pKF);                     /* MapPoint.cc:420-424 */
     void SetBadFlag();                                    /* MapPoint.cc:216-239 */
     bool isBad();
+    void Replace(MapPoint* pMP);                          /* MapPoint.cc:248-300 */
+    MapPoint* GetReplaced();                              /* MapPoint.cc:241-246 */
+    void IncreaseVisible(int n = 1);
+    void IncreaseFound(int n = 1);
+    /* MapPoint.cc:329-403 on the GPU (one MapPoint; ORBmatcher::ComputeDistinctiveDescriptors batches many). */
+    void ComputeDistinctiveDescriptors();
     void UpdateNormalAndDepth();                          /* MapPoint.cc:426-493 */
     void SetDescriptor(const uint8_t d[32]);
     void GetDescriptor(uint8_t d[32]);
@@ -126,6 +136,9 @@ public:
     void GetNormal(float n[3]);
     float GetMinDistanceInvariance() { return 0.8f * mfMinDistance; }
     float GetMaxDistanceInvariance() { return 1.2f * mfMaxDistance; }
+    /* mfMinDistance / mfMaxDistance as stored (Fuse's PredictScale reads the latter). */
+    float GetMinDistance();
+    float GetMaxDistance();
 
     unsigned long mnId;
     unsigned long mnBALocalForKF = 0;
@@ -142,7 +155,9 @@ private:
     uint8_t mDescriptor[32] = {0};
     std::map<KeyFrame*, std::tuple<int, int>> mObservations;
     int nObs = 0;
+    int mnVisible = 1, mnFound = 1;
     bool mbBad = false;
+    MapPoint* mpReplaced = nullptr;
     KeyFrame* mpRefKF;
     Map* mpMap;
 };

@@ -36,6 +36,14 @@ public:
     int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<std::pair<size_t, size_t>>& vMatchedPairs,
                                const bool bOnlyStereo, const bool bCoarse = false);
 
+    /* LocalMapping::SearchInNeighbors: ORBmatcher.cc:1148-1338 (mono keyframe; bRight=true throws). The search
+     * runs on the GPU for every MapPoint at once; the replace-or-add side effects follow in list order. */
+    int Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, const float th = 3.0, const bool bRight = false);
+
+    /* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403) for every non-bad MapPoint of the list in one
+     * launch (the loop at the end of SearchInNeighbors, LocalMapping.cc:923-935). */
+    static void ComputeDistinctiveDescriptors(const std::vector<MapPoint*>& vpMapPoints);
+
     /* The epipolar quantities SearchForTriangulation derives from the poses (ORBmatcher.cc:913-930,
      * Pinhole.cpp:107-112): F12 row-major and the epipole of KF1's centre in KF2. */
     static void ComputeF12(KeyFrame* pKF1, KeyFrame* pKF2, float F12[9], float ep[2]);

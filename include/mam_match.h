@@ -9,6 +9,8 @@
  *                                                                 reference: src/ORBmatcher.cc:1676-1887, 2012-2053
  *   ORBmatcher::SearchForTriangulation(KF1, KF2, vMatchedPairs, bOnlyStereo=false, bCoarse)
  *                                                                 reference: src/ORBmatcher.cc:907-1146
+ *   ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight=false)          reference: src/ORBmatcher.cc:1148-1338
+ *   MapPoint::ComputeDistinctiveDescriptors()                     reference: src/MapPoint.cc:329-403
  *   with Frame::GetFeaturesInArea / PosInGrid / AssignFeaturesToGrid (src/Frame.cc:385-416, 657-735) built
  *   on the device, and Pinhole::project / epipolarConstrain (src/CameraModels/Pinhole.cpp:35-41, 107-129).
  *
@@ -86,6 +88,24 @@ typedef struct mam_last_entry {
     uint8_t desc[32];         /* pMP->GetDescriptor() */
 } mam_last_entry;
 
+/* MapPoint fields ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight=false) reads (ORBmatcher.cc:1179-1256). 80 bytes. */
+typedef struct mam_fuse_mp {
+    float pos[3];             /* GetWorldPos() */
+    float max_distance;       /* mfMaxDistance: GetMaxDistanceInvariance() = 1.2f * it, PredictScale's ratio */
+    float normal[3];          /* GetNormal() */
+    float min_distance;       /* mfMinDistance: GetMinDistanceInvariance() = 0.8f * it */
+    int32_t valid;            /* pMP != NULL && !pMP->isBad() && !pMP->IsInKeyFrame(pKF) (ORBmatcher.cc:1181-1196) */
+    int32_t pad[3];
+    uint8_t desc[32];         /* GetDescriptor() */
+} mam_fuse_mp;
+
+/* The keyframe side of a Fuse: Tcw, camera centre and mfLogScaleFactor (log of the float scale factor). */
+typedef struct mam_fuse_kf {
+    mam_pose tcw;             /* GetPose() */
+    float ow[3];              /* GetCameraCenter() */
+    float log_scale_factor;   /* mfLogScaleFactor (MapPoint::PredictScale, MapPoint.cc:514-529) */
+} mam_fuse_kf;
+
 /* DBoW2::FeatureVector flattened: node ids ascending, node_off[n_nodes+1] into feats (feature indices). */
 typedef struct mam_featvec {
     int32_t n_nodes;
@@ -129,6 +149,23 @@ int mam_search_for_triangulation(mam_match_ctx* ctx, const mam_frame_geom* geom,
                                  const mam_featvec* fv2, const float* F12, const float* ep, int check_ori,
                                  int coarse, int32_t* out_match12);
 
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight=false) for a mono Pinhole keyframe (ORBmatcher.cc:1148-1338):
+ * the per-MapPoint search. keys/desc = pKF->mvKeysUn / mDescriptors (n keypoints). out_idx[i] = the keypoint
+ * MapPoint i fuses with (bestDist <= TH_LOW), else -1; out_dist[i] = bestDist (256 = no candidate passed). The
+ * replace-or-add side effects (:1311-1330) are the caller's, applied in list order with the isBad / IsInKeyFrame
+ * tests re-evaluated: they never change another MapPoint's search. Returns the number of
+ * MapPoints with out_idx >= 0. */
+int mam_fuse(mam_match_ctx* ctx, const mam_frame_geom* geom, int n, const mam_keypoint* keys, const uint8_t* desc,
+             const mam_fuse_kf* kf, const mam_pinhole* cam, int n_mps, const mam_fuse_mp* mps, float th,
+             int32_t* out_idx, int32_t* out_dist);
+
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403) for n_mps MapPoints at once: MapPoint m's observed
+ * descriptors are rows desc_off[m] .. desc_off[m+1]-1 of descs (32 B each), in the caller's observation order (the
+ * reference's std::map<KeyFrame*> order, non-bad keyframes). out_best[m] = the row (relative to desc_off[m]) with
+ * the least median Hamming distance to the others, first on ties; -1 for a MapPoint without descriptors. */
+int mam_compute_distinctive_descriptors(mam_match_ctx* ctx, int n_mps, const int32_t* desc_off, const uint8_t* descs,
+                                        int32_t* out_best);
+
 /* ---- batched device-resident forms (asynchronous on `stream`; NULL = the context's stream) ---------- */
 
 /* A batch of frames laid out as the extractor's batched output: frame f's keypoints at
@@ -163,8 +200,21 @@ int mam_search_by_projection_motion_batch_device(mam_match_ctx* ctx, const mam_f
                                                  const int32_t* n_last, float th, int check_ori,
                                                  int32_t* out_kp_to_last, int32_t* out_nmatches, void* stream);
 
+/* Fuse into many keyframes in one launch (SearchInNeighbors' forward direction, LocalMapping.cc:881-890): keyframe f
+ * (frames: its keypoints) with kfs[f] searches n_mps[f] MapPoints at mps + f*mp_stride. Outputs at
+ * out_idx / out_dist + f*mp_stride and out_nfused[f]. */
+int mam_fuse_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_frames_dev* frames,
+                          const mam_fuse_kf* kfs, const mam_pinhole* cam, const mam_fuse_mp* mps, int mp_stride,
+                          const int32_t* n_mps, float th, int32_t* out_idx, int32_t* out_dist, int32_t* out_nfused,
+                          void* stream);
+
+/* ComputeDistinctiveDescriptors over device arrays (desc_off[n_mps+1], descs, out_best[n_mps]). */
+int mam_compute_distinctive_descriptors_batch_device(mam_match_ctx* ctx, int n_mps, const int32_t* desc_off,
+                                                     const uint8_t* descs, int32_t* out_best, void* stream);
+
 int mam_match_set_profiling(mam_match_ctx* ctx, int enable);
-/* ms_out/launches_out: [0] grid build, [1] candidate gather, [2] greedy resolve, [3] triangulation. */
+/* ms_out/launches_out (6 entries): [0] grid build, [1] candidate gather, [2] greedy resolve, [3] triangulation,
+ * [4] fuse, [5] distinctive descriptors. */
 int mam_match_stage_times(mam_match_ctx* ctx, double* ms_out, int64_t* launches_out);
 
 #ifdef __cplusplus

@@ -5,6 +5,8 @@
 //                                        MapPoint of the same call is skipped by later ones, :88-90)
 //   SearchByProjection(Cur, Last)        src/ORBmatcher.cc:1676-1887 + rotation histogram :1855-1884
 //   SearchForTriangulation               src/ORBmatcher.cc:907-1146 (per idx1 independent; last equal wins)
+//   Fuse(pKF, vpMapPoints, th)           src/ORBmatcher.cc:1148-1338, MapPoint::PredictScale src/MapPoint.cc:514-529
+//   MapPoint::ComputeDistinctiveDescriptors  src/MapPoint.cc:329-403
 //   Frame grid / GetFeaturesInArea       src/Frame.cc:385-416, 657-735
 //
 // Stages (one launch each, batched over frames):
@@ -21,9 +23,14 @@
 //              the same round have disjoint candidates and commit in parallel. Then the rotation-histogram pass.
 //   k_tri      SearchForTriangulation: one wave per idx1 of each shared vocabulary node; wave argmin on
 //              (dist, -position) implements "dist <= bestDist, last equal wins".
+//   k_fuse     Fuse(pKF, vpMapPoints): GW lanes per (keyframe, MapPoint): projection, distance / viewing-angle
+//              tests, PredictScale, the window scan of k_gather with Fuse's level + reprojection tests, first minimum
+//              distance; the replace-or-add side effects stay on the host (they never change another search).
+//   k_distinct MapPoint::ComputeDistinctiveDescriptors: one wave per MapPoint, row medians by binary search.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -216,6 +223,20 @@ struct Window {
     const uint8_t* desc;
 };
 
+// GetFeaturesInArea's cell range (Frame.cc:665-687, KeyFrame.cc:712-726); false = the call returns empty.
+__device__ __forceinline__ bool window_cells(const mam_frame_geom& g, Window* w) {
+    const float r = w->r;
+    w->cx0 = max(0, (int)floorf((w->x - g.min_x - r) * g.grid_inv_w));
+    if (w->cx0 >= MAM_GRID_COLS) return false;
+    w->cx1 = min(MAM_GRID_COLS - 1, (int)ceilf((w->x - g.min_x + r) * g.grid_inv_w));
+    if (w->cx1 < 0) return false;
+    w->cy0 = max(0, (int)floorf((w->y - g.min_y - r) * g.grid_inv_h));
+    if (w->cy0 >= MAM_GRID_ROWS) return false;
+    w->cy1 = min(MAM_GRID_ROWS - 1, (int)ceilf((w->y - g.min_y + r) * g.grid_inv_h));
+    if (w->cy1 < 0) return false;
+    return true;
+}
+
 // Search window of unit j of frame f; false = the reference `continue`s before or inside GetFeaturesInArea.
 __device__ bool unit_window(const ProjArgs& p, int f, int j, Window* w) {
     if (j >= p.n_units[f]) return false;
@@ -259,18 +280,8 @@ __device__ bool unit_window(const ProjArgs& p, int f, int j, Window* w) {
         w->maxL = L.octave + 1;
         w->desc = L.desc;
     }
-    // GetFeaturesInArea cell range (Frame.cc:657-683)
-    const float r = w->r;
-    w->cx0 = max(0, (int)floorf((w->x - p.g.min_x - r) * p.g.grid_inv_w));
-    if (w->cx0 >= MAM_GRID_COLS) return false;
-    w->cx1 = min(MAM_GRID_COLS - 1, (int)ceilf((w->x - p.g.min_x + r) * p.g.grid_inv_w));
-    if (w->cx1 < 0) return false;
-    w->cy0 = max(0, (int)floorf((w->y - p.g.min_y - r) * p.g.grid_inv_h));
-    if (w->cy0 >= MAM_GRID_ROWS) return false;
-    w->cy1 = min(MAM_GRID_ROWS - 1, (int)ceilf((w->y - p.g.min_y + r) * p.g.grid_inv_h));
-    if (w->cy1 < 0) return false;
     w->checkL = (w->minL > 0) || (w->maxL >= 0);
-    return true;
+    return window_cells(p.g, w);
 }
 
 // A candidate is RELEVANT to its unit if its taken state can change the unit's result: dist <= TH_HIGH (it could
@@ -989,6 +1000,211 @@ __global__ void k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* ou
     if (i < n) out[i] = desc_dist(a + (size_t)i * 32, b + (size_t)i * 32);
 }
 
+// ------------------------------------------------------------------------------------------------ fuse
+// ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight=false) (ORBmatcher.cc:1148-1338), mono Pinhole keyframe. A
+// MapPoint's search reads nothing that the replace-or-add side effects of earlier MapPoints of the same call change
+// (the MapPoints those touch are skipped by the caller's isBad / IsInKeyFrame re-check), so every MapPoint of every
+// target keyframe is searched in parallel, GW lanes per MapPoint as in k_gather; the caller applies the results in
+// list order.
+struct FuseArgs {
+    mam_frame_geom g;
+    mam_frames_dev fr;
+    const mam_fuse_kf* kfs;
+    mam_pinhole cam;
+    const mam_fuse_mp* mps;
+    int mp_stride;
+    const int32_t* n_mps;
+    float th;
+    const GridEnt* grid_ent;
+    const int32_t* grid_start;
+    int32_t* out_idx;
+    int32_t* out_dist;
+    int32_t* out_n;
+};
+
+// (int) of a float as x86's cvttss2si computes it (NaN / out of range -> INT_MIN): PredictScale's (int)ceil(...)
+__device__ __forceinline__ int cvt_i32_x86(float v) {
+    return (v >= -2147483648.0f && v < 2147483648.0f) ? (int)v : INT_MIN;
+}
+
+// The window of MapPoint mp in keyframe f; false where the reference `continue`s (ORBmatcher.cc:1179-1251).
+__device__ bool fuse_window(const FuseArgs& p, int f, const mam_fuse_mp& mp, Window* w) {
+    if (!mp.valid) return false;
+    const mam_fuse_kf& K = p.kfs[f];
+    // Tcw * p3Dw: Sophus SE3f action, evaluated as written (as in unit_window)
+    const float qx = K.tcw.q[0], qy = K.tcw.q[1], qz = K.tcw.q[2], qw = K.tcw.q[3];
+    const float px = mp.pos[0], py = mp.pos[1], pz = mp.pos[2];
+    float u0 = qy * pz - qz * py, u1 = qz * px - qx * pz, u2 = qx * py - qy * px;
+    u0 += u0; u1 += u1; u2 += u2;
+    const float c0 = qy * u2 - qz * u1, c1 = qz * u0 - qx * u2, c2 = qx * u1 - qy * u0;
+    const float xc = ((px + qw * u0) + c0) + K.tcw.t[0];
+    const float yc = ((py + qw * u1) + c1) + K.tcw.t[1];
+    const float zc = ((pz + qw * u2) + c2) + K.tcw.t[2];
+    if (zc < 0.0f) return false;
+    const float u = p.cam.fx * xc / zc + p.cam.cx;   // Pinhole::project
+    const float v = p.cam.fy * yc / zc + p.cam.cy;
+    if (!(u >= p.g.min_x && u < p.g.max_x && v >= p.g.min_y && v < p.g.max_y)) return false;   // KeyFrame::IsInImage
+    const float maxD = 1.2f * mp.max_distance, minD = 0.8f * mp.min_distance;
+    const float P0 = px - K.ow[0], P1 = py - K.ow[1], P2 = pz - K.ow[2];
+    // Eigen's unrolled 3-term reductions (norm, dot): e0 + (e1 + e2)
+    const float dist3D = sqrtf(P0 * P0 + (P1 * P1 + P2 * P2));
+    if (dist3D < minD || dist3D > maxD) return false;
+    const float dot = P0 * mp.normal[0] + (P1 * mp.normal[1] + P2 * mp.normal[2]);
+    if ((double)dot < 0.5 * (double)dist3D) return false;
+    // PredictScale (MapPoint.cc:514-529); log(float) as the correctly rounded float log
+    const float ratio = mp.max_distance / dist3D;
+    int lvl = cvt_i32_x86(ceilf((float)log((double)ratio) / K.log_scale_factor));
+    if (lvl < 0) lvl = 0;
+    else if (lvl >= p.g.nlevels) lvl = p.g.nlevels - 1;
+    w->x = u;
+    w->y = v;
+    w->r = p.th * p.g.scale_factors[lvl];
+    w->minL = lvl - 1;
+    w->maxL = lvl;
+    w->checkL = true;
+    w->desc = mp.desc;
+    return window_cells(p.g, w);
+}
+
+// Best keypoint of one MapPoint's window by a group of GW lanes: the window's candidates in GetFeaturesInArea order
+// (as gather_pass deals them), the level and reprojection tests of ORBmatcher.cc:1267-1296, and the first minimum
+// distance of the enumeration (dist < bestDist) as the group minimum of dist << 20 | position.
+template <int GW>
+__device__ void fuse_pass(const FuseArgs& p, int f, const Window& w, const uint4 u0, const uint4 u1, int* bdist,
+                          int* bidx) {
+    const int gl = lane_id() & (GW - 1);
+    const int ny = w.cy1 - w.cy0 + 1;
+    const int ncell = (w.cx1 - w.cx0 + 1) * ny;
+    const int32_t* gs = p.grid_start + (size_t)f * (NCELLS + 1);
+    const GridEnt* G = p.grid_ent + (size_t)f * p.fr.kp_stride;
+    unsigned best = 0xFFFFFFFFu;
+    int bi = -1;
+    int base = 0;   // enumeration position of the chunk's first candidate
+    for (int e0 = 0; e0 < ncell; e0 += GW) {
+        const int e = e0 + gl;
+        int k0 = 0, c = 0;
+        if (e < ncell) {
+            const int ix = w.cx0 + e / ny, iy = w.cy0 + e % ny;
+            const int cell = ix * MAM_GRID_ROWS + iy;
+            k0 = gs[cell];
+            c = gs[cell + 1] - k0;
+        }
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < GW; o <<= 1) {
+            const int t = __shfl_up(incl, o, GW);
+            if (gl >= o) incl += t;
+        }
+        const int tot = __shfl(incl, GW - 1, GW);
+        const int kb = k0 - (incl - c);
+        for (int t0 = 0; t0 < tot; t0 += GW) {
+            const int t = t0 + gl;
+            int m = 0;
+#pragma unroll
+            for (int step = GW / 2; step >= 1; step >>= 1)
+                if (__shfl(incl, m + step - 1, GW) <= t) m += step;
+            const int k = __shfl(kb, m, GW) + t;
+            if (t < tot) {
+                const GridEnt ge = G[k];
+                const int oct = (int)(ge.io >> 16);
+                const float dx = ge.x - w.x, dy = ge.y - w.y;
+                if (oct >= w.minL && oct <= w.maxL && fabsf(dx) < w.r && fabsf(dy) < w.r) {
+                    const float ex = w.x - ge.x, ey = w.y - ge.y;
+                    const float e2 = ex * ex + ey * ey;
+                    if (!((double)(e2 * (1.0f / p.g.level_sigma2[oct])) > 5.99)) {
+                        const int dist = __popc(u0.x ^ ge.d0.x) + __popc(u0.y ^ ge.d0.y) + __popc(u0.z ^ ge.d0.z) +
+                                         __popc(u0.w ^ ge.d0.w) + __popc(u1.x ^ ge.d1.x) + __popc(u1.y ^ ge.d1.y) +
+                                         __popc(u1.z ^ ge.d1.z) + __popc(u1.w ^ ge.d1.w);
+                        const unsigned key = ((unsigned)dist << 20) | (unsigned)(base + t);
+                        if (key < best) {
+                            best = key;
+                            bi = (int)(ge.io & 0xFFFFu);
+                        }
+                    }
+                }
+            }
+        }
+        base += tot;
+    }
+#pragma unroll
+    for (int o = GW / 2; o >= 1; o >>= 1) {
+        const unsigned ob = (unsigned)__shfl_xor((int)best, o, GW);
+        const int oi = __shfl_xor(bi, o, GW);
+        if (ob < best) {
+            best = ob;
+            bi = oi;
+        }
+    }
+    *bdist = best == 0xFFFFFFFFu ? 256 : (int)(best >> 20);
+    *bidx = bi;
+}
+
+template <int GW>
+__global__ __launch_bounds__(256) void k_fuse(FuseArgs p, int nframes) {
+    const long long gu = ((long long)blockIdx.x * 256 + threadIdx.x) / GW;   // global MapPoint slot
+    const int f = (int)(gu / p.mp_stride);
+    const int j = (int)(gu - (long long)f * p.mp_stride);
+    if (f >= nframes || j >= p.n_mps[f]) return;   // group-uniform
+    const size_t o = (size_t)f * p.mp_stride + j;
+    const mam_fuse_mp& mp = p.mps[o];
+    Window w;
+    int bd = 256, bi = -1;
+    if (fuse_window(p, f, mp, &w)) {
+        const uint4 u0 = reinterpret_cast<const uint4*>(mp.desc)[0], u1 = reinterpret_cast<const uint4*>(mp.desc)[1];
+        fuse_pass<GW>(p, f, w, u0, u1, &bd, &bi);
+    }
+    if ((lane_id() & (GW - 1)) == 0) {
+        const bool fused = bd <= MAM_TH_LOW;
+        p.out_idx[o] = fused ? bi : -1;
+        p.out_dist[o] = bd;
+        if (fused) atomicAdd(&p.out_n[f], 1);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ distinctive descriptor
+// MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403), one wave per MapPoint. Lane i takes row i of the
+// N x N distance matrix (rows i, i + 64, ...) and finds the row's median, element (N-1)/2 of the sorted row, by a
+// binary search over the distance value: 9 counting passes over the N descriptors, read at wave-uniform addresses.
+// The chosen descriptor (smallest median, first on ties) is the wave minimum of median << 20 | i.
+__global__ __launch_bounds__(256) void k_distinct(const int32_t* __restrict__ off, const uint8_t* __restrict__ descs,
+                                                  int n, int32_t* __restrict__ out) {
+    const int m = __builtin_amdgcn_readfirstlane((int)(((long long)blockIdx.x * 256 + threadIdx.x) >> 6));
+    if (m >= n) return;
+    const int lane = lane_id();
+    const int b = off[m], N = off[m + 1] - b;
+    if (N <= 0) {
+        if (lane == 0) out[m] = -1;
+        return;
+    }
+    const uint4* D = reinterpret_cast<const uint4*>(descs + (size_t)b * 32);
+    const int k = (N - 1) >> 1;   // vDists[0.5*(N-1)]
+    unsigned best = 0xFFFFFFFFu;
+    for (int i0 = 0; i0 < N; i0 += 64) {
+        const int i = i0 + lane;
+        uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
+        if (i < N) {
+            r0 = D[2 * i];
+            r1 = D[2 * i + 1];
+        }
+        int lo = 0, hi = 256;   // the median lies in [lo, hi]
+        for (int it = 0; it < 9; it++) {
+            const int mid = (lo + hi) >> 1;
+            int cnt = 0;
+            for (int j = 0; j < N; j++) {
+                const uint4 c0 = D[2 * j], c1 = D[2 * j + 1];
+                const int d = __popc(r0.x ^ c0.x) + __popc(r0.y ^ c0.y) + __popc(r0.z ^ c0.z) + __popc(r0.w ^ c0.w) +
+                              __popc(r1.x ^ c1.x) + __popc(r1.y ^ c1.y) + __popc(r1.z ^ c1.z) + __popc(r1.w ^ c1.w);
+                cnt += d <= mid;
+            }
+            if (cnt > k) hi = mid;
+            else lo = mid + 1;
+        }
+        if (i < N) best = min(best, ((unsigned)lo << 20) | (unsigned)i);
+    }
+    best = wave_minu(best);
+    if (lane == 0) out[m] = (int32_t)(best & 0xFFFFFu);
+}
+
 }  // namespace mam
 
 // ==================================================================================================== host
@@ -997,7 +1213,7 @@ using mam::DevBuf;
 struct mam_match_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    mam::StageTimer timer{4};
+    mam::StageTimer timer{6};
     int slot_cap = 32;        // candidate slots per unit (grows x4 when a host call overflows)
     size_t resolve_lds_max = 64 * 1024;
     // scratch
@@ -1040,6 +1256,27 @@ int ensure_scratch(mam_match_ctx* c, int F, int kp_stride, int unit_stride, int 
     return MAM_OK;
 }
 
+// The frames' cell grid (k_grid, which also resets out_n / pool_total of every frame), or the one this context's
+// previous search built over the same frames (mam_frames_dev.reuse_grid).
+int build_grid(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) {
+    if (a.fr.reuse_grid) {
+        // AssignFeaturesToGrid runs once per Frame (Frame.cc:385-416): the previous search on this context built it
+        if (c->grid_keys != (const void*)a.fr.keys || c->grid_counts != (const void*)a.fr.counts ||
+            c->grid_nframes != F || c->grid_stride != a.fr.kp_stride) {
+            mam::set_last_error("reuse_grid: this context's last search was not over the same frames");
+            return MAM_ERR_ARG;
+        }
+        return MAM_OK;
+    }
+    mam::StageTimer::Scope sc(&c->timer, s, 0);
+    hipLaunchKernelGGL(mam::k_grid, dim3(F), dim3(1024), 0, s, a);
+    c->grid_keys = a.fr.keys;
+    c->grid_counts = a.fr.counts;
+    c->grid_nframes = F;
+    c->grid_stride = a.fr.kp_stride;
+    return MAM_OK;
+}
+
 // Shared launcher for both projection searches.
 int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) {
     if (F <= 0) return MAM_OK;
@@ -1052,21 +1289,7 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
     a.pool = c->pool.p;
     a.pool_total = c->pool_total.p;
     a.events = c->events.p;
-    if (a.fr.reuse_grid) {
-        // AssignFeaturesToGrid runs once per Frame (Frame.cc:385-416): the previous search on this context built it
-        if (c->grid_keys != (const void*)a.fr.keys || c->grid_counts != (const void*)a.fr.counts ||
-            c->grid_nframes != F || c->grid_stride != a.fr.kp_stride) {
-            mam::set_last_error("reuse_grid: this context's last search was not over the same frames");
-            return MAM_ERR_ARG;
-        }
-    } else {
-        mam::StageTimer::Scope sc(&c->timer, s, 0);
-        hipLaunchKernelGGL(mam::k_grid, dim3(F), dim3(1024), 0, s, a);
-        c->grid_keys = a.fr.keys;
-        c->grid_counts = a.fr.counts;
-        c->grid_nframes = F;
-        c->grid_stride = a.fr.kp_stride;
-    }
+    if (int rc = build_grid(c, a, F, s)) return rc;
     {
         // batches: 16 lanes per unit (windows hold a few to a few tens of candidates, so four units share a wave and
         // their dependent global-memory round trips overlap: 0.38 -> 0.22 ms per 256 c1 frames); a single frame:
@@ -1114,6 +1337,37 @@ int launch_projection(mam_match_ctx* c, mam::ProjArgs& a, int F, hipStream_t s) 
 }
 
 bool geom_ok(const mam_frame_geom* g) { return g && g->nlevels >= 1 && g->nlevels <= MAM_MAX_LEVELS; }
+
+int launch_fuse(mam_match_ctx* c, mam::FuseArgs& a, int F, hipStream_t s) {
+    if (F <= 0) return MAM_OK;
+    if (a.fr.kp_stride > mam::GRID_SORT_MAX || a.fr.kp_stride <= 0 || a.mp_stride <= 0) return MAM_ERR_ARG;
+    if (int rc = c->grid_ent.alloc((size_t)F * a.fr.kp_stride)) return rc;
+    if (int rc = c->grid_start.alloc((size_t)F * (mam::NCELLS + 1))) return rc;
+    if (int rc = c->pool_total.alloc(F)) return rc;
+    mam::ProjArgs ga{};
+    ga.g = a.g;
+    ga.fr = a.fr;
+    ga.grid_ent = c->grid_ent.p;
+    ga.grid_start = c->grid_start.p;
+    ga.pool_total = c->pool_total.p;
+    ga.out_n = a.out_n;
+    if (a.fr.reuse_grid) MAM_HIP(hipMemsetAsync(a.out_n, 0, sizeof(int32_t) * (size_t)F, s));
+    if (int rc = build_grid(c, ga, F, s)) return rc;
+    a.grid_ent = c->grid_ent.p;
+    a.grid_start = c->grid_start.p;
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 4);
+        const long long units = (long long)F * a.mp_stride;
+        if (F <= 4) {
+            hipLaunchKernelGGL(mam::k_fuse<64>, dim3((int)((units * 64 + 255) / 256)), dim3(256), 0, s, a, F);
+        } else {
+            constexpr int GW = MAM_GATHER_LANES;
+            hipLaunchKernelGGL(mam::k_fuse<GW>, dim3((int)((units * GW + 255) / 256)), dim3(256), 0, s, a, F);
+        }
+    }
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
 
 }  // namespace
 
@@ -1414,6 +1668,98 @@ int mam_search_for_triangulation(mam_match_ctx* c, const mam_frame_geom* g, int 
     return nm;
 }
 
+int mam_fuse_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_frames_dev* fr, const mam_fuse_kf* kfs,
+                          const mam_pinhole* cam, const mam_fuse_mp* mps, int mp_stride, const int32_t* n_mps, float th,
+                          int32_t* out_idx, int32_t* out_dist, int32_t* out_n, void* stream) {
+    if (!c || !geom_ok(g) || !fr || !kfs || !cam || !mps || !n_mps || !out_idx || !out_dist || !out_n || mp_stride <= 0)
+        return MAM_ERR_ARG;
+    MAM_HIP(hipSetDevice(c->device));
+    mam::FuseArgs a{};
+    a.g = *g;
+    a.fr = *fr;
+    a.kfs = kfs;
+    a.cam = *cam;
+    a.mps = mps;
+    a.mp_stride = mp_stride;
+    a.n_mps = n_mps;
+    a.th = th;
+    a.out_idx = out_idx;
+    a.out_dist = out_dist;
+    a.out_n = out_n;
+    return launch_fuse(c, a, fr->nframes, stream ? (hipStream_t)stream : c->stream);
+}
+
+int mam_fuse(mam_match_ctx* c, const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc,
+             const mam_fuse_kf* kf, const mam_pinhole* cam, int n_mps, const mam_fuse_mp* mps, float th,
+             int32_t* out_idx, int32_t* out_dist) {
+    if (!c || !geom_ok(g) || !kf || !cam || n < 0 || n_mps < 0 || (n > 0 && (!keys || !desc)) ||
+        (n_mps > 0 && (!mps || !out_idx || !out_dist)))
+        return MAM_ERR_ARG;
+    if (n > mam::GRID_SORT_MAX) return MAM_ERR_CAPACITY;
+    if (n_mps == 0) return 0;
+    MAM_HIP(hipSetDevice(c->device));
+    mam_frames_dev fr;
+    uint8_t* extra;
+    int32_t *dout, *dcount, *dn;
+    const size_t eb = carve_bytes(n_mps, sizeof(mam_fuse_mp)) + 2 * carve_bytes(n_mps, 4) + carve_bytes(1, 4) +
+                      carve_bytes(1, sizeof(mam_fuse_kf));
+    if (int rc = stage_frame(c, n, keys, desc, nullptr, eb, &extra, &fr, &dout, &dcount, &dn)) return rc;
+    mam_fuse_mp* dm = carve<mam_fuse_mp>(extra, n_mps);
+    int32_t* di = carve<int32_t>(extra, n_mps);
+    int32_t* dd = carve<int32_t>(extra, n_mps);
+    int32_t* dnu = carve<int32_t>(extra, 1);
+    mam_fuse_kf* dk = carve<mam_fuse_kf>(extra, 1);
+    MAM_HIP(hipMemcpyAsync(dm, mps, sizeof(mam_fuse_mp) * n_mps, hipMemcpyHostToDevice, c->stream));
+    MAM_HIP(hipMemcpyAsync(dnu, &n_mps, 4, hipMemcpyHostToDevice, c->stream));
+    MAM_HIP(hipMemcpyAsync(dk, kf, sizeof(mam_fuse_kf), hipMemcpyHostToDevice, c->stream));
+    if (int rc = mam_fuse_batch_device(c, g, &fr, dk, cam, dm, n_mps, dnu, th, di, dd, dn, c->stream)) return rc;
+    int32_t nf = 0;
+    MAM_HIP(hipMemcpyAsync(&nf, dn, 4, hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipMemcpyAsync(out_idx, di, sizeof(int32_t) * n_mps, hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipMemcpyAsync(out_dist, dd, sizeof(int32_t) * n_mps, hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipStreamSynchronize(c->stream));
+    return nf;
+}
+
+int mam_compute_distinctive_descriptors_batch_device(mam_match_ctx* c, int n_mps, const int32_t* off,
+                                                     const uint8_t* descs, int32_t* out, void* stream) {
+    if (!c || n_mps < 0 || (n_mps > 0 && (!off || !descs || !out))) return MAM_ERR_ARG;
+    if (n_mps == 0) return MAM_OK;
+    MAM_HIP(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 5);
+        hipLaunchKernelGGL(mam::k_distinct, dim3((n_mps + 3) / 4), dim3(256), 0, s, off, descs, n_mps, out);
+    }
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
+
+int mam_compute_distinctive_descriptors(mam_match_ctx* c, int n_mps, const int32_t* off, const uint8_t* descs,
+                                        int32_t* out) {
+    if (!c || n_mps < 0 || (n_mps > 0 && (!off || !out))) return MAM_ERR_ARG;
+    if (n_mps == 0) return MAM_OK;
+    if (off[0] < 0) return MAM_ERR_ARG;
+    for (int m = 0; m < n_mps; m++)
+        if (off[m + 1] < off[m]) return MAM_ERR_ARG;
+    const int total = off[n_mps];
+    if (total > 0 && !descs) return MAM_ERR_ARG;
+    MAM_HIP(hipSetDevice(c->device));
+    const size_t rows = (size_t)std::max(total, 1);
+    const size_t bytes = carve_bytes((size_t)n_mps + 1, 4) + carve_bytes(rows * 32, 1) + carve_bytes(n_mps, 4);
+    if (int rc = c->stage.alloc(bytes)) return rc;
+    uint8_t* p = c->stage.p;
+    int32_t* doff = carve<int32_t>(p, (size_t)n_mps + 1);
+    uint8_t* dd = carve<uint8_t>(p, rows * 32);
+    int32_t* dout = carve<int32_t>(p, n_mps);
+    MAM_HIP(hipMemcpyAsync(doff, off, sizeof(int32_t) * ((size_t)n_mps + 1), hipMemcpyHostToDevice, c->stream));
+    if (total > 0) MAM_HIP(hipMemcpyAsync(dd, descs, (size_t)total * 32, hipMemcpyHostToDevice, c->stream));
+    if (int rc = mam_compute_distinctive_descriptors_batch_device(c, n_mps, doff, dd, dout, c->stream)) return rc;
+    MAM_HIP(hipMemcpyAsync(out, dout, sizeof(int32_t) * n_mps, hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipStreamSynchronize(c->stream));
+    return MAM_OK;
+}
+
 int mam_match_set_profiling(mam_match_ctx* c, int enable) {
     if (!c) return MAM_ERR_ARG;
     c->timer.reset(enable != 0);
@@ -1423,7 +1769,7 @@ int mam_match_set_profiling(mam_match_ctx* c, int enable) {
 int mam_match_stage_times(mam_match_ctx* c, double* ms_out, int64_t* launches_out) {
     if (!c) return MAM_ERR_ARG;
     c->timer.collect();
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < 6; i++) {
         if (ms_out) ms_out[i] = c->timer.ms[i];
         if (launches_out) launches_out[i] = c->timer.n[i];
     }

@@ -6,6 +6,7 @@
 
 #include "mam3slam/Map.h"
 #include "mam3slam/ORBextractor.h"
+#include "mam3slam/ORBmatcher.h"
 
 namespace MAM3SLAM {
 
@@ -109,6 +110,7 @@ Frame::Frame(const ImageView& imGray, ORBextractor* extractor, const Pinhole* pC
     // synthetic pinhole agents have zero distortion), grid bounds.
     mnScaleLevels = extractor->GetLevels();
     mfScaleFactor = extractor->GetScaleFactor();
+    mfLogScaleFactor = std::log(mfScaleFactor);
     mvScaleFactors = extractor->GetScaleFactors();
     mvInvScaleFactors = extractor->GetInverseScaleFactors();
     mvLevelSigma2 = extractor->GetScaleSigmaSquares();
@@ -139,7 +141,7 @@ mam_frame_geom Frame::Geom() const {
 
 KeyFrame::KeyFrame(const Frame& F, Map* pMap, unsigned long id)
     : mnId(id), N(F.N), mvKeys(F.mvKeys), mvKeysUn(F.mvKeysUn), mvuRight(F.N, -1.0f), mDescriptors(F.mDescriptors),
-      mnScaleLevels(F.mnScaleLevels), mvScaleFactors(F.mvScaleFactors), mvLevelSigma2(F.mvLevelSigma2),
+      mnScaleLevels(F.mnScaleLevels), mfLogScaleFactor(F.mfLogScaleFactor), mvScaleFactors(F.mvScaleFactors), mvLevelSigma2(F.mvLevelSigma2),
       mvInvLevelSigma2(F.mvInvLevelSigma2), mnMinX(F.mnMinX), mnMaxX(F.mnMaxX), mnMinY(F.mnMinY), mnMaxY(F.mnMaxY),
       mfGridElementWidthInv(F.mfGridElementWidthInv), mfGridElementHeightInv(F.mfGridElementHeightInv),
       mpCamera(F.mpCamera), mvpMapPoints(F.mvpMapPoints), mpMap(pMap) {
@@ -181,6 +183,8 @@ void KeyFrame::AddMapPoint(MapPoint* pMP, size_t idx) {
     std::lock_guard<std::mutex> l(mMutexFeatures);
     mvpMapPoints[idx] = pMP;
 }
+
+void KeyFrame::ReplaceMapPointMatch(const int& idx, MapPoint* pMP) { mvpMapPoints[idx] = pMP; }
 
 void KeyFrame::EraseMapPointMatch(int idx) {
     std::lock_guard<std::mutex> l(mMutexFeatures);
@@ -262,6 +266,11 @@ std::tuple<int, int> MapPoint::GetIndexInKeyFrame(KeyFrame* pKF) {
     return it != mObservations.end() ? it->second : std::tuple<int, int>(-1, -1);
 }
 
+bool MapPoint::IsInKeyFrame(KeyFrame* pKF) {
+    std::lock_guard<std::mutex> l(mMutexFeatures);
+    return mObservations.count(pKF) != 0;
+}
+
 void MapPoint::SetBadFlag() {
     std::map<KeyFrame*, std::tuple<int, int>> obs;
     {
@@ -281,6 +290,73 @@ bool MapPoint::isBad() {
     std::lock_guard<std::mutex> l1(mMutexFeatures);
     std::lock_guard<std::mutex> l2(mMutexPos);
     return mbBad;
+}
+
+MapPoint* MapPoint::GetReplaced() {
+    std::lock_guard<std::mutex> l1(mMutexFeatures);
+    std::lock_guard<std::mutex> l2(mMutexPos);
+    return mpReplaced;
+}
+
+void MapPoint::Replace(MapPoint* pMP) {
+    // MapPoint.cc:248-300: pMP takes over this point's observations (or the keyframe slot is cleared where pMP is
+    // already observed), then recomputes its descriptor; this point becomes bad
+    if (pMP->mnId == this->mnId) return;
+    int nvisible, nfound;
+    std::map<KeyFrame*, std::tuple<int, int>> obs;
+    {
+        std::lock_guard<std::mutex> l1(mMutexFeatures);
+        std::lock_guard<std::mutex> l2(mMutexPos);
+        obs = mObservations;
+        mObservations.clear();
+        mbBad = true;
+        nvisible = mnVisible;
+        nfound = mnFound;
+        mpReplaced = pMP;
+    }
+    for (auto& o : obs) {
+        KeyFrame* pKF = o.first;
+        const int leftIndex = std::get<0>(o.second), rightIndex = std::get<1>(o.second);
+        if (!pMP->IsInKeyFrame(pKF)) {
+            if (leftIndex != -1) {
+                pKF->ReplaceMapPointMatch(leftIndex, pMP);
+                pMP->AddObservation(pKF, leftIndex);
+            }
+            if (rightIndex != -1) {
+                pKF->ReplaceMapPointMatch(rightIndex, pMP);
+                pMP->AddObservation(pKF, rightIndex);
+            }
+        } else {
+            if (leftIndex != -1) pKF->EraseMapPointMatch(leftIndex);
+            if (rightIndex != -1) pKF->EraseMapPointMatch(rightIndex);
+        }
+    }
+    pMP->IncreaseFound(nfound);
+    pMP->IncreaseVisible(nvisible);
+    pMP->ComputeDistinctiveDescriptors();
+    if (mpMap) mpMap->EraseMapPoint(this);
+}
+
+void MapPoint::IncreaseVisible(int n) {
+    std::lock_guard<std::mutex> l(mMutexFeatures);
+    mnVisible += n;
+}
+
+void MapPoint::IncreaseFound(int n) {
+    std::lock_guard<std::mutex> l(mMutexFeatures);
+    mnFound += n;
+}
+
+void MapPoint::ComputeDistinctiveDescriptors() { ORBmatcher::ComputeDistinctiveDescriptors(std::vector<MapPoint*>{this}); }
+
+float MapPoint::GetMinDistance() {
+    std::lock_guard<std::mutex> l(mMutexPos);
+    return mfMinDistance;
+}
+
+float MapPoint::GetMaxDistance() {
+    std::lock_guard<std::mutex> l(mMutexPos);
+    return mfMaxDistance;
 }
 
 void MapPoint::SetDescriptor(const uint8_t d[32]) {

@@ -1,6 +1,7 @@
 // MAM3SLAM::ORBmatcher over the gfx950 searches (include/mam3slam/ORBmatcher.h, include/mam_match.h).
 // The wrapper only marshals: object pointers -> indices and flags going in, indices -> pointers coming out, with
-// the reference's side effects on Frame::mvpMapPoints (src/ORBmatcher.cc:43-213, 907-1146, 1676-1887).
+// the reference's side effects on Frame::mvpMapPoints (src/ORBmatcher.cc:43-213, 907-1146, 1676-1887) and on the
+// keyframe / MapPoint graph (Fuse, :1148-1338).
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -210,6 +211,84 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2,
     for (int i = 0; i < n1; i++)   // ORBmatcher.cc:1135-1143: ascending idx1
         if (out[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)out[i]));
     return nm;
+}
+
+int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, const float th, const bool bRight) {
+    if (bRight) throw std::invalid_argument("Fuse(bRight=true): stereo is out of scope (mono agents)");
+    mam_fuse_kf kf;
+    kf.tcw = pKF->GetPose().toC();
+    pKF->GetCameraCenter(kf.ow);
+    kf.log_scale_factor = pKF->mfLogScaleFactor;
+    const size_t M = vpMapPoints.size();
+    std::vector<mam_fuse_mp> mps(M);
+    for (size_t i = 0; i < M; i++) {
+        mam_fuse_mp& m = mps[i];
+        std::memset(&m, 0, sizeof(m));
+        MapPoint* pMP = vpMapPoints[i];
+        if (!pMP || pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;   // ORBmatcher.cc:1181-1196
+        m.valid = 1;
+        pMP->GetWorldPos(m.pos);
+        pMP->GetNormal(m.normal);
+        m.max_distance = pMP->GetMaxDistance();
+        m.min_distance = pMP->GetMinDistance();
+        pMP->GetDescriptor(m.desc);
+    }
+    std::vector<int32_t> idx(M > 0 ? M : 1, -1), dist(M > 0 ? M : 1, 256);
+    const mam_frame_geom g = pKF->Geom();
+    const mam_pinhole cam = pKF->mpCamera->toC();
+    throwOn(mam_fuse(ctx(), &g, pKF->N, reinterpret_cast<const mam_keypoint*>(pKF->mvKeysUn.data()),
+                     pKF->mDescriptors.data.data(), &kf, &cam, (int)M, mps.data(), th, idx.data(), dist.data()),
+            "mam_fuse");
+    // ORBmatcher.cc:1177-1335 in list order; the isBad / IsInKeyFrame tests see the effects of earlier MapPoints
+    int nFused = 0;
+    for (size_t i = 0; i < M; i++) {
+        MapPoint* pMP = vpMapPoints[i];
+        if (!pMP) continue;
+        if (pMP->isBad()) continue;
+        else if (pMP->IsInKeyFrame(pKF)) continue;
+        if (idx[i] < 0) continue;   // a geometric `continue` or bestDist > TH_LOW
+        const int bestIdx = idx[i];
+        MapPoint* pMPinKF = pKF->GetMapPoint(bestIdx);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) {
+                if (pMPinKF->Observations() > pMP->Observations())
+                    pMP->Replace(pMPinKF);
+                else
+                    pMPinKF->Replace(pMP);
+            }
+        } else {
+            pMP->AddObservation(pKF, bestIdx);
+            pKF->AddMapPoint(pMP, bestIdx);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+
+void ORBmatcher::ComputeDistinctiveDescriptors(const std::vector<MapPoint*>& vpMapPoints) {
+    // MapPoint.cc:331-366: the descriptors of the non-bad observing keyframes, in observation (std::map) order
+    std::vector<int32_t> off(1, 0);
+    std::vector<uint8_t> descs;
+    std::vector<MapPoint*> todo;
+    for (MapPoint* pMP : vpMapPoints) {
+        if (!pMP || pMP->isBad()) continue;
+        const std::map<KeyFrame*, std::tuple<int, int>> observations = pMP->GetObservations();
+        const size_t before = descs.size();
+        for (const auto& o : observations) {
+            KeyFrame* pKF = o.first;
+            if (pKF->isBad()) continue;
+            for (const int i : {std::get<0>(o.second), std::get<1>(o.second)})
+                if (i != -1) descs.insert(descs.end(), pKF->mDescriptors.ptr(i), pKF->mDescriptors.ptr(i) + 32);
+        }
+        if (descs.size() == before) continue;   // no descriptor: unchanged (:343-344, :365-366)
+        todo.push_back(pMP);
+        off.push_back((int32_t)(descs.size() / 32));
+    }
+    if (todo.empty()) return;
+    std::vector<int32_t> best(todo.size());
+    throwOn(mam_compute_distinctive_descriptors(ctx(), (int)todo.size(), off.data(), descs.data(), best.data()),
+            "mam_compute_distinctive_descriptors");
+    for (size_t m = 0; m < todo.size(); m++) todo[m]->SetDescriptor(descs.data() + (size_t)(off[m] + best[m]) * 32);
 }
 
 }  // namespace MAM3SLAM

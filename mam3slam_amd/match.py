@@ -8,6 +8,8 @@ Reference interface (include/ORBmatcher.h:40-93, src/ORBmatcher.cc):
     int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, float th, bool bMono)
     int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pair<size_t,size_t>>& vMatchedPairs,
                                bool bOnlyStereo, bool bCoarse=false)
+    int Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th=3.0, bool bRight=false)
+and MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:329-403), batched over many MapPoints.
     TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30
 
 Frames/KeyFrames are passed as FrameData (numpy views of the fields the searches read). Object pointers are
@@ -58,6 +60,37 @@ MP_TRACK_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("view_cos", "<
 LAST_ENTRY_DTYPE = np.dtype([("pos", "<f4", (3,)), ("angle", "<f4"), ("octave", "<i4"), ("valid", "<i4"),
                              ("nobs", "<i4"), ("pad", "<i4"), ("desc", "u1", (32,))])
 assert MP_TRACK_DTYPE.itemsize == 64 and LAST_ENTRY_DTYPE.itemsize == 64
+FUSE_MP_DTYPE = np.dtype([("pos", "<f4", (3,)), ("max_distance", "<f4"), ("normal", "<f4", (3,)),
+                          ("min_distance", "<f4"), ("valid", "<i4"), ("pad", "<i4", (3,)), ("desc", "u1", (32,))])
+assert FUSE_MP_DTYPE.itemsize == 80
+
+
+class FuseKF(C.Structure):
+    _fields_ = [("tcw", Pose), ("ow", C.c_float * 3), ("log_scale_factor", C.c_float)]
+
+
+def camera_center(pose):
+    """KeyFrame::GetCameraCenter: translation of Tcw^-1 (Sophus: conjugate quaternion applied to -t), float32."""
+    q = np.asarray(pose[0], np.float32)
+    p = -np.asarray(pose[1], np.float32)
+    qv, w = -q[:3], q[3]
+    uv = np.cross(qv, p).astype(np.float32)
+    uv = uv + uv
+    return (p + w * uv + np.cross(qv, uv)).astype(np.float32)
+
+
+def fuse_kf(pose, scale_factor: float = 1.2) -> FuseKF:
+    """The keyframe side of Fuse: Tcw, camera centre, mfLogScaleFactor = log of the float scale factor."""
+    k = FuseKF()
+    for i in range(4):
+        k.tcw.q[i] = float(pose[0][i])
+    for i in range(3):
+        k.tcw.t[i] = float(pose[1][i])
+    ow = camera_center(pose)
+    for i in range(3):
+        k.ow[i] = float(ow[i])
+    k.log_scale_factor = float(np.log(np.float32(scale_factor)))
+    return k
 
 _SIGS = {
     "mam_match_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -79,6 +112,13 @@ _SIGS = {
                                                                C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                                                C.c_float, C.c_int, C.c_void_p, C.c_void_p,
                                                                C.c_void_p]),
+    "mam_fuse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                           C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]),
+    "mam_fuse_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                        C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mam_compute_distinctive_descriptors": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mam_compute_distinctive_descriptors_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                                                   C.c_void_p, C.c_void_p]),
     "mam_match_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "mam_match_stage_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
 }
@@ -273,6 +313,37 @@ class ORBmatcher:
         idx = np.nonzero(out >= 0)[0]
         return n, np.stack([idx, out[idx]], 1).astype(np.int64)
 
+    def Fuse(self, KF: FrameData, mps: np.ndarray, cam: Pinhole, th: float = 3.0, bRight: bool = False):
+        """ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight) (ORBmatcher.cc:1148-1338): the per-MapPoint search of a
+        mono keyframe. KF.pose = Tcw; mps: FUSE_MP_DTYPE (valid = non-NULL, not bad, not already in the keyframe).
+        Returns (n, idx, dist): idx[i] = the keypoint MapPoint i fuses with (bestDist <= TH_LOW) or -1, dist[i] =
+        bestDist (256 = no candidate). The replace-or-add side effects are the caller's, in list order."""
+        if bRight:
+            raise MamError("Fuse(bRight=true): stereo is out of scope (mono agents only)")
+        keys = np.ascontiguousarray(KF.keys, KP_DTYPE)
+        desc = np.ascontiguousarray(KF.desc, np.uint8)
+        mps = np.ascontiguousarray(mps, FUSE_MP_DTYPE)
+        kf = fuse_kf(KF.pose)
+        idx = np.full(max(len(mps), 1), -1, np.int32)
+        dist = np.full(max(len(mps), 1), 256, np.int32)
+        g = KF.geom()
+        n = self._L.mam_fuse(self._ctx, C.byref(g), len(keys), _p(keys), _p(desc), C.byref(kf), C.byref(cam), len(mps),
+                             _p(mps), float(th), _p(idx), _p(dist))
+        check(n, "Fuse")
+        return n, idx[:len(mps)], dist[:len(mps)]
+
+    def ComputeDistinctiveDescriptors(self, desc_off: np.ndarray, descs: np.ndarray) -> np.ndarray:
+        """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403) for many MapPoints in one launch: MapPoint
+        m's observed descriptors are rows desc_off[m] .. desc_off[m+1]-1 of descs. Returns the chosen row of each
+        (relative to desc_off[m]; -1 = no descriptor)."""
+        off = np.ascontiguousarray(desc_off, np.int32)
+        d = np.ascontiguousarray(descs, np.uint8).reshape(-1, 32)
+        n = len(off) - 1
+        out = np.full(max(n, 1), -1, np.int32)
+        check(self._L.mam_compute_distinctive_descriptors(self._ctx, n, _p(off), _p(d) if len(d) else None, _p(out)),
+              "ComputeDistinctiveDescriptors")
+        return out[:n]
+
     # ---- batched device-resident (bench / multi-agent harness)
     def search_by_projection_batch_device(self, F: FrameData, frames: FramesDev, d_mps: int, mp_stride: int,
                                           d_nmps: int, th: float, d_out: int, d_nmatch: int, stream: int = 0,
@@ -292,11 +363,25 @@ class ORBmatcher:
             last_stride, C.c_void_p(d_nlast), float(th), int(self.mbCheckOrientation), C.c_void_p(d_out),
             C.c_void_p(d_nmatch), C.c_void_p(stream)), "search_motion_batch_device")
 
+    def fuse_batch_device(self, F: FrameData, frames: FramesDev, d_kfs: int, cam: Pinhole, d_mps: int, mp_stride: int,
+                          d_nmps: int, th: float, d_idx: int, d_dist: int, d_nfused: int, stream: int = 0):
+        g = F.geom()
+        return check(self._L.mam_fuse_batch_device(
+            self._ctx, C.byref(g), C.byref(frames), C.c_void_p(d_kfs), C.byref(cam), C.c_void_p(d_mps), mp_stride,
+            C.c_void_p(d_nmps), float(th), C.c_void_p(d_idx), C.c_void_p(d_dist), C.c_void_p(d_nfused),
+            C.c_void_p(stream)), "fuse_batch_device")
+
+    def distinctive_batch_device(self, n_mps: int, d_off: int, d_descs: int, d_out: int, stream: int = 0):
+        return check(self._L.mam_compute_distinctive_descriptors_batch_device(
+            self._ctx, int(n_mps), C.c_void_p(d_off), C.c_void_p(d_descs), C.c_void_p(d_out), C.c_void_p(stream)),
+            "distinctive_batch_device")
+
     def set_profiling(self, enable: bool):
         check(self._L.mam_match_set_profiling(self._ctx, 1 if enable else 0), "match_set_profiling")
 
     def stage_times(self):
-        ms = np.zeros(4, np.float64)
-        n = np.zeros(4, np.int64)
+        ms = np.zeros(6, np.float64)
+        n = np.zeros(6, np.int64)
         check(self._L.mam_match_stage_times(self._ctx, _p(ms), _p(n)), "match_stage_times")
-        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(["grid", "gather", "resolve", "triangulation"])}
+        names = ["grid", "gather", "resolve", "triangulation", "fuse", "distinctive"]
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}

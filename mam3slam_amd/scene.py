@@ -9,7 +9,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from .match import LAST_ENTRY_DTYPE, MP_TRACK_DTYPE, FrameData, Pinhole, epipole_12, fundamental_12
+from .match import (FUSE_MP_DTYPE, LAST_ENTRY_DTYPE, MP_TRACK_DTYPE, FrameData, Pinhole, camera_center,
+                    epipole_12, fundamental_12)
 from .orb import KP_DTYPE
 
 
@@ -219,3 +220,57 @@ def pose_problem(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.7,
     F.map_point = mp
     F.outlier = None
     return xyz, (qt, tt)
+
+
+def fuse_mappoints(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.7, dup_frac=0.1, n_out=120, kflip=60):
+    """MapPoints as ORBmatcher::Fuse(pKF, vpMapPoints) sees them (ORBmatcher.cc:1177-1256), around keyframe F's
+    keypoints under F.pose: world positions that re-project within a few pixels (scaled by the level), normals
+    inside the 60-degree cone (5 % reversed), distance-invariance ranges whose PredictScale lands on the keypoint's
+    level or the one above, descriptors with 0..kflip flipped bits (so some fail TH_LOW), 5 % invalid, near
+    duplicates, 3 % outside their distance range, and random points (behind the camera, outside the image)."""
+    from .match import quat_to_rot
+
+    q, t = F.pose
+    R = quat_to_rot(q).astype(np.float64)
+    n = len(F.keys)
+    sel = rng.choice(n, size=int(n * frac), replace=False)
+    m = len(sel)
+    k = F.keys[sel]
+    s = F.scale_factors[k["octave"]].astype(np.float64)
+    z = rng.uniform(1.5, 25.0, m)
+    u = k["x"] + rng.normal(0, 0.8, m) * s
+    v = k["y"] + rng.normal(0, 0.8, m) * s
+    Xc = np.stack([(u - cam.cx) / cam.fx * z, (v - cam.cy) / cam.fy * z, z], 1)
+    Xw = (Xc - t[None, :].astype(np.float64)) @ R   # R^T (Xc - t)
+    PO = Xw - camera_center(F.pose).astype(np.float64)[None, :]
+    d = np.linalg.norm(PO, axis=1)
+    nrm = PO / d[:, None] + rng.normal(0, 0.15, (m, 3))
+    back = rng.random(m) < 0.05
+    nrm[back] = -nrm[back]
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    # PredictScale = ceil(log(maxD / dist) / log 1.2): maxD = dist * 1.2^(level - x), x in (0.05, 0.95)
+    lvl = k["octave"] + rng.integers(0, 2, m)
+    maxd = d * 1.2 ** (lvl - rng.uniform(0.05, 0.95, m))
+    mps = np.zeros(m, FUSE_MP_DTYPE)
+    mps["pos"] = Xw.astype(np.float32)
+    mps["normal"] = nrm.astype(np.float32)
+    mps["max_distance"] = maxd.astype(np.float32)
+    mps["min_distance"] = (maxd / float(F.scale_factors[-1])).astype(np.float32)
+    far = rng.random(m) < 0.03
+    mps["max_distance"][far] *= np.float32(0.5)
+    mps["valid"] = (rng.random(m) < 0.95).astype(np.int32)
+    mps["desc"] = flip_bits(F.desc[sel], rng, kflip)
+    nd = int(m * dup_frac)
+    dup = mps[rng.choice(m, size=nd, replace=False)].copy()
+    dup["pos"] += rng.normal(0, 0.003, (nd, 3)).astype(np.float32)
+    dup["desc"] = flip_bits(dup["desc"], rng, 6)
+    out = np.zeros(n_out, FUSE_MP_DTYPE)
+    out["pos"] = rng.uniform(-10, 10, (n_out, 3)).astype(np.float32)
+    nr = rng.normal(size=(n_out, 3))
+    out["normal"] = (nr / np.linalg.norm(nr, axis=1)[:, None]).astype(np.float32)
+    out["max_distance"] = rng.uniform(1, 40, n_out).astype(np.float32)
+    out["min_distance"] = out["max_distance"] / np.float32(F.scale_factors[-1])
+    out["valid"] = 1
+    out["desc"] = rng.integers(0, 256, (n_out, 32), dtype=np.uint8)
+    allm = np.concatenate([mps, dup, out])
+    return allm[rng.permutation(len(allm))]

@@ -7,11 +7,16 @@
 //   src/ORBmatcher.cc:1676-1887 SearchByProjection(Frame&, const Frame&) (mono branch)
 //   src/ORBmatcher.cc:907-1146  SearchForTriangulation (mono, Pinhole), :2012-2053 ComputeThreeMaxima
 //   src/ORBmatcher.cc:2058-2074 DescriptorDistance
+//   src/ORBmatcher.cc:1148-1338 Fuse(pKF, vpMapPoints, th, bRight=false) (the per-MapPoint search), with
+//                               KeyFrame::GetFeaturesInArea / IsInImage (src/KeyFrame.cc:704-753) and
+//                               MapPoint::PredictScale (src/MapPoint.cc:514-529)
+//   src/MapPoint.cc:329-403     ComputeDistinctiveDescriptors
 //   src/CameraModels/Pinhole.cpp:35-41 project, :107-129 epipolarConstrain (F12 supplied by the caller)
 //   Thirdparty/Sophus/sophus/so3.hpp:358-367, se3.hpp:321-324 point action
 // Float expressions are evaluated as written, left to right, without contraction.
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -112,6 +117,9 @@ void se3Apply(const mam_pose* T, const float p[3], float out[3]) {
     out[1] = ((p[1] + qw * uv[1]) + cy) + T->t[1];
     out[2] = ((p[2] + qw * uv[2]) + cz) + T->t[2];
 }
+
+// (int) of a float as x86's cvttss2si computes it (NaN / out of range -> INT_MIN): the reference's (int)ceil(...)
+int cvtX86(float v) { return (v >= -2147483648.0f && v < 2147483648.0f) ? (int)v : INT_MIN; }
 
 int roundBin(float rot) {
     const float factor = 1.0f / MAM_HISTO_LENGTH;
@@ -294,6 +302,97 @@ int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_k
         }
     }
     return nmatches;
+}
+
+// Fuse's per-MapPoint search. PredictScale uses std::log(float) and std::ceil(float): the reference's unqualified
+// log/ceil of a float resolve to the std overloads (TemplatedVocabulary.h:36 puts `using namespace std` in scope).
+// Eigen's 3-vector norm() and dot() sum as e0 + (e1 + e2) (its unrolled redux). out_dist = bestDist (256 = none).
+int oracle_fuse(const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc, const mam_fuse_kf* kf,
+                const mam_pinhole* cam, int n_mps, const mam_fuse_mp* mps, float th, int32_t* out_idx,
+                int32_t* out_dist) {
+    FrameO F(g, n, keys);
+    int nfused = 0;
+    for (int i = 0; i < n_mps; i++) {
+        out_idx[i] = -1;
+        out_dist[i] = 256;
+        const mam_fuse_mp& mp = mps[i];
+        if (!mp.valid) continue;   // NULL, isBad(), IsInKeyFrame(pKF)
+        float p3Dc[3];
+        se3Apply(&kf->tcw, mp.pos, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float u = cam->fx * p3Dc[0] / p3Dc[2] + cam->cx;
+        const float v = cam->fy * p3Dc[1] / p3Dc[2] + cam->cy;
+        if (!(u >= g->min_x && u < g->max_x && v >= g->min_y && v < g->max_y)) continue;   // IsInImage
+        const float maxDistance = 1.2f * mp.max_distance;
+        const float minDistance = 0.8f * mp.min_distance;
+        const float PO[3] = {mp.pos[0] - kf->ow[0], mp.pos[1] - kf->ow[1], mp.pos[2] - kf->ow[2]};
+        const float dist3D = std::sqrt(PO[0] * PO[0] + (PO[1] * PO[1] + PO[2] * PO[2]));
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float dot = PO[0] * mp.normal[0] + (PO[1] * mp.normal[1] + PO[2] * mp.normal[2]);
+        if (dot < 0.5 * dist3D) continue;
+        const float ratio = mp.max_distance / dist3D;
+        int nPredictedLevel = cvtX86(std::ceil(std::log(ratio) / kf->log_scale_factor));
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= g->nlevels) nPredictedLevel = g->nlevels - 1;
+        const float radius = th * g->scale_factors[nPredictedLevel];
+        const std::vector<size_t> vIndices = F.GetFeaturesInArea(u, v, radius, -1, -1);
+        if (vIndices.empty()) continue;
+        int bestDist = 256, bestIdx = -1;
+        for (size_t idx : vIndices) {
+            const mam_keypoint& kp = keys[idx];
+            const int kpLevel = kp.octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const float ex = u - kp.x;
+            const float ey = v - kp.y;
+            const float e2 = ex * ex + ey * ey;
+            const float invSigma2 = 1.0f / g->level_sigma2[kpLevel];   // mvInvLevelSigma2
+            if (e2 * invSigma2 > 5.99) continue;
+            const int dist = descDist(mp.desc, desc + idx * 32);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = (int)idx;
+            }
+        }
+        out_dist[i] = bestDist;
+        if (bestDist <= MAM_TH_LOW) {
+            out_idx[i] = bestIdx;
+            nfused++;
+        }
+    }
+    return nfused;
+}
+
+// ComputeDistinctiveDescriptors for n_mps MapPoints: rows off[m] .. off[m+1]-1 of descs, in observation order.
+int oracle_distinctive_descriptors(int n_mps, const int32_t* off, const uint8_t* descs, int32_t* out) {
+    for (int m = 0; m < n_mps; m++) {
+        const int N = off[m + 1] - off[m];
+        if (N <= 0) {
+            out[m] = -1;
+            continue;
+        }
+        const uint8_t* D = descs + (size_t)off[m] * 32;
+        std::vector<float> Distances((size_t)N * N);   // float Distances[N][N]
+        for (int i = 0; i < N; i++) {
+            Distances[(size_t)i * N + i] = 0;
+            for (int j = i + 1; j < N; j++) {
+                const int distij = descDist(D + (size_t)i * 32, D + (size_t)j * 32);
+                Distances[(size_t)i * N + j] = (float)distij;
+                Distances[(size_t)j * N + i] = (float)distij;
+            }
+        }
+        int BestMedian = INT_MAX, BestIdx = 0;
+        for (int i = 0; i < N; i++) {
+            std::vector<int> vDists(Distances.begin() + (size_t)i * N, Distances.begin() + (size_t)(i + 1) * N);
+            std::sort(vDists.begin(), vDists.end());
+            const int median = vDists[(size_t)(0.5 * (N - 1))];
+            if (median < BestMedian) {
+                BestMedian = median;
+                BestIdx = i;
+            }
+        }
+        out[m] = BestIdx;
+    }
+    return 0;
 }
 
 }  // extern "C"

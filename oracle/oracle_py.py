@@ -260,6 +260,38 @@ def search_for_triangulation(KF1, KF2, F12, ep, check_ori=False, coarse=False):
     return n, out[:len(k1)]
 
 
+def fuse(KF, mps, cam, th=3.0):
+    """ORBmatcher::Fuse per-MapPoint search. Returns (n, idx, dist) like mam3slam_amd.match.ORBmatcher.Fuse."""
+    from mam3slam_amd.match import FUSE_MP_DTYPE, KP_DTYPE, fuse_kf
+
+    L = lib()
+    L.oracle_fuse.restype = C.c_int
+    L.oracle_fuse.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                              C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]
+    keys = np.ascontiguousarray(KF.keys, KP_DTYPE)
+    desc = np.ascontiguousarray(KF.desc, np.uint8)
+    mps = np.ascontiguousarray(mps, FUSE_MP_DTYPE)
+    kf = fuse_kf(KF.pose)
+    idx = np.full(max(len(mps), 1), -1, np.int32)
+    dist = np.full(max(len(mps), 1), 256, np.int32)
+    g = KF.geom()
+    n = L.oracle_fuse(C.byref(g), len(keys), _vp(keys), _vp(desc), C.byref(kf), C.byref(cam), len(mps), _vp(mps),
+                      float(th), _vp(idx), _vp(dist))
+    return n, idx[:len(mps)], dist[:len(mps)]
+
+
+def distinctive_descriptors(desc_off, descs):
+    L = lib()
+    L.oracle_distinctive_descriptors.restype = C.c_int
+    L.oracle_distinctive_descriptors.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    off = np.ascontiguousarray(desc_off, np.int32)
+    d = np.ascontiguousarray(descs, np.uint8).reshape(-1, 32)
+    n = len(off) - 1
+    out = np.full(max(n, 1), -1, np.int32)
+    L.oracle_distinctive_descriptors(n, _vp(off), _vp(d) if len(d) else None, _vp(out))
+    return out[:n]
+
+
 # ---------------------------------------------------------------- LBA oracle (oracle/lba_oracle.cpp)
 def lba_solve(prob, stop=None):
     """g2o LocalBundleAdjustment solve restatement. prob: mam3slam_amd.lba.LBAProblem."""

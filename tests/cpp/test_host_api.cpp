@@ -6,12 +6,14 @@
 //                       infrastructure): ORBextractor bit-exact, both SearchByProjection and
 //                       SearchForTriangulation index-exact with the reference's side effects on mvpMapPoints,
 //                       LocalBundleAdjustment write-back / outlier erase vs the oracle solve, PoseOptimization
-//                       (mvbOutlier, pose, return value) vs the oracle.
+//                       (mvbOutlier, pose, return value) vs the oracle, Fuse (return value, the keyframe slots and
+//                       the Replace chains) and ComputeDistinctiveDescriptors vs the oracle.
 //
 // Prints "OK <n> checks" and exits 0, or prints the first failure and exits 1.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <array>
 #include <cstring>
 #include <memory>
 #include <random>
@@ -39,6 +41,10 @@ int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_k
 int oracle_lba_solve(const mam_lba_problem* p, const volatile uint8_t* stop_flag, mam_lba_result* r);
 int oracle_pose_optimization(const mam_pose* tcw, const mam_pinhole* cam, int n, const mam_pose_edge* edges,
                              uint8_t* outlier, mam_pose_result* res);
+int oracle_fuse(const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc, const mam_fuse_kf* kf,
+                const mam_pinhole* cam, int n_mps, const mam_fuse_mp* mps, float th, int32_t* out_idx,
+                int32_t* out_dist);
+int oracle_distinctive_descriptors(int n_mps, const int32_t* off, const uint8_t* descs, int32_t* out);
 }
 
 using namespace MAM3SLAM;
@@ -568,6 +574,147 @@ static void testPoseOptimization() {
     CHECK(Optimizer::PoseOptimization(&G) == 0 && std::memcmp(&G.GetPose(), &T0, sizeof(SE3f)) == 0, "n < 3");
 }
 
+static void testFuse() {
+    // keyframe K: 300 keypoints = projections of points X_i (+ noise), random descriptors, octaves 0..3. Slots
+    // 0..149 hold MapPoints (observed by K, every other one also by O, a second keyframe at K's pose); 150..299 are
+    // free. Fused list: 200 new MapPoints near random slots (descriptor = the slot's with 0..39 flipped bits,
+    // observed once in O so UpdateNormalAndDepth gives them K's level) and 20 points behind the camera.
+    Pinhole cam(500.f, 500.f, 320.f, 240.f);
+    std::vector<float> scales, sig2;
+    float sc = 1.f;
+    for (int l = 0; l < 8; l++) {
+        scales.push_back(sc);
+        sig2.push_back(sc * sc);
+        sc = (float)((double)sc * (double)1.2f);
+    }
+    Map map(0);
+    const int N = 300;
+    Frame F = emptyFrame(N, 640, 480, scales, sig2, &cam);
+    F.mfScaleFactor = 1.2f;
+    F.mfLogScaleFactor = std::log(1.2f);
+    F.SetPose(poseAround(0.3f, 6.f));
+    std::mt19937 rng(123);
+    std::uniform_real_distribution<float> U(-1.5f, 1.5f);
+    std::normal_distribution<float> N01(0.f, 1.f);
+    std::vector<std::array<float, 3>> X(N);
+    for (int i = 0; i < N; i++) {
+        float Xc[3], uv[2];
+        X[i] = {U(rng), U(rng), U(rng)};
+        F.GetPose().map(X[i].data(), Xc);
+        cam.project(Xc, uv);
+        KeyPoint& kp = F.mvKeysUn[i];
+        kp.octave = (int)(rng() % 4u);
+        kp.pt.x = uv[0] + 0.5f * N01(rng);
+        kp.pt.y = uv[1] + 0.5f * N01(rng);
+        F.mvKeys[i] = kp;
+        for (int b = 0; b < 32; b++) F.mDescriptors.ptr(i)[b] = (uint8_t)rng();
+    }
+    KeyFrame K(F, &map, 1), O(F, &map, 2);
+    std::vector<std::unique_ptr<MapPoint>> owned;
+    for (int i = 0; i < 150; i++) {
+        owned.emplace_back(new MapPoint(X[i].data(), &K, &map, owned.size()));
+        MapPoint* p = owned.back().get();
+        map.AddMapPoint(p);
+        p->SetDescriptor(F.mDescriptors.ptr(i));
+        K.AddMapPoint(p, i);
+        p->AddObservation(&K, i);
+        if (i % 2) {
+            O.AddMapPoint(p, i);
+            p->AddObservation(&O, i);
+        }
+        p->UpdateNormalAndDepth();
+    }
+    std::vector<MapPoint*> vp;
+    for (int j = 0; j < 220; j++) {
+        const int i = (int)(rng() % (unsigned)N);
+        float Xp[3] = {X[i][0] + 0.002f * N01(rng), X[i][1] + 0.002f * N01(rng), X[i][2] + 0.002f * N01(rng)};
+        if (j >= 200) {   // mirrored through the camera centre: behind the camera
+            float Ow[3];
+            K.GetCameraCenter(Ow);
+            for (int a = 0; a < 3; a++) Xp[a] = 2.f * Ow[a] - Xp[a];
+        }
+        owned.emplace_back(new MapPoint(Xp, &O, &map, owned.size()));
+        MapPoint* p = owned.back().get();
+        map.AddMapPoint(p);
+        uint8_t d[32];
+        std::memcpy(d, F.mDescriptors.ptr(i), 32);
+        for (int f = 0; f < (int)(rng() % 40u); f++) d[rng() % 32] ^= (uint8_t)(1u << (rng() % 8));
+        p->SetDescriptor(d);
+        p->AddObservation(&O, i);
+        p->UpdateNormalAndDepth();
+        vp.push_back(p);
+    }
+    vp.push_back(nullptr);
+    vp.push_back(owned[3].get());   // already in K: skipped
+
+    // expected: the oracle search on the same marshalled inputs
+    mam_fuse_kf kf;
+    kf.tcw = K.GetPose().toC();
+    K.GetCameraCenter(kf.ow);
+    kf.log_scale_factor = K.mfLogScaleFactor;
+    std::vector<mam_fuse_mp> mm(vp.size());
+    for (size_t j = 0; j < vp.size(); j++) {
+        std::memset(&mm[j], 0, sizeof(mm[j]));
+        MapPoint* p = vp[j];
+        if (!p || p->isBad() || p->IsInKeyFrame(&K)) continue;
+        mm[j].valid = 1;
+        p->GetWorldPos(mm[j].pos);
+        p->GetNormal(mm[j].normal);
+        mm[j].max_distance = p->GetMaxDistance();
+        mm[j].min_distance = p->GetMinDistance();
+        p->GetDescriptor(mm[j].desc);
+    }
+    std::vector<int32_t> oi(vp.size()), od(vp.size());
+    const mam_frame_geom g = K.Geom();
+    const mam_pinhole pc = cam.toC();
+    const int no = oracle_fuse(&g, K.N, reinterpret_cast<const mam_keypoint*>(K.mvKeysUn.data()),
+                               K.mDescriptors.data.data(), &kf, &pc, (int)mm.size(), mm.data(), 3.f, oi.data(),
+                               od.data());
+    ORBmatcher matcher;
+    const int ng = matcher.Fuse(&K, vp, 3.f);
+    // no MapPoint of the list is made bad or put in K by an earlier one before its turn, so every oracle hit fuses
+    CHECK(ng == no && ng > 100, "Fuse fused %d, oracle %d", ng, no);
+    int replaced = 0;
+    for (size_t j = 0; j < vp.size(); j++) {
+        if (oi[j] < 0) continue;
+        MapPoint* slot = K.GetMapPoint(oi[j]);
+        CHECK(slot && !slot->isBad(), "slot %d empty or bad", oi[j]);
+        MapPoint* p = vp[j];
+        for (int hop = 0; p->isBad() && hop < 16; hop++) p = p->GetReplaced();
+        CHECK(p == slot, "MapPoint %zu: the survivor of its Replace chain is not slot %d's", j, oi[j]);
+        CHECK(slot->IsInKeyFrame(&K) && std::get<0>(slot->GetIndexInKeyFrame(&K)) == oi[j], "observation of slot %d", oi[j]);
+        replaced += vp[j]->isBad() ? 1 : 0;
+    }
+    CHECK(replaced > 0, "the scene must exercise Replace");
+    for (size_t j = 200; j < 220; j++) CHECK(oi[j] < 0 && !vp[j]->IsInKeyFrame(&K), "behind the camera: %zu", j);
+
+    // ComputeDistinctiveDescriptors over every MapPoint vs the oracle on the same observation order
+    std::vector<MapPoint*> all;
+    for (auto& p : owned) all.push_back(p.get());
+    ORBmatcher::ComputeDistinctiveDescriptors(all);
+    int checked = 0;
+    for (MapPoint* p : all) {
+        if (p->isBad()) continue;
+        std::vector<int32_t> off(1, 0);
+        std::vector<uint8_t> dd;
+        for (auto& o : p->GetObservations()) {
+            const int i = std::get<0>(o.second);
+            if (i == -1) continue;
+            dd.insert(dd.end(), o.first->mDescriptors.ptr(i), o.first->mDescriptors.ptr(i) + 32);
+        }
+        if (dd.empty()) continue;
+        off.push_back((int32_t)(dd.size() / 32));
+        int32_t best = -1;
+        oracle_distinctive_descriptors(1, off.data(), dd.data(), &best);
+        uint8_t got[32];
+        p->GetDescriptor(got);
+        CHECK(best >= 0 && std::memcmp(got, dd.data() + (size_t)best * 32, 32) == 0, "distinctive descriptor of %lu",
+              p->mnId);
+        checked++;
+    }
+    CHECK(checked > 200, "distinctive descriptors checked: %d", checked);
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     testAlgebra();
@@ -578,6 +725,7 @@ int main(int argc, char** argv) {
         testMatcher();
         testLocalBA();
         testPoseOptimization();
+        testFuse();
     }
     std::printf("OK %d checks (%s)\n", g_checks, mode.c_str());
     return 0;

@@ -227,3 +227,60 @@ def test_pose_oracle_too_few_correspondences(oracle):
     n, out, (qo, to), st = oracle.pose_optimization_edges((q, t), cam, e)
     assert n == 0 and st["rounds"] == 0 and not out.any()
     assert np.array_equal(qo, q.astype(np.float64)) and np.array_equal(to, t.astype(np.float64))
+
+
+def test_distinctive_oracle_median_rule(oracle):
+    """ComputeDistinctiveDescriptors (MapPoint.cc:383-397): median = element (N-1)/2 of the sorted distance row,
+    smallest median wins, first on ties."""
+    a = np.zeros(32, np.uint8)
+    b = a.copy()
+    b[:2] = 0xFF     # 16 bits from a
+    c = np.full(32, 0xFF, np.uint8)   # 256 from a, 240 from b
+    # MapPoint 0 rows (c, a, b): medians c [0,240,256] -> 240, a [0,16,256] -> 16, b [0,16,240] -> 16 -> row 1
+    # MapPoint 1 (N = 2): both medians are element 0 = 0 -> row 0; MapPoint 2: no rows -> -1
+    # MapPoint 3 (c, a, a, c): every sorted row is [0, 0, 256, 256], element 1 = 0 -> row 0
+    off = np.array([0, 3, 5, 5, 9], np.int32)
+    d = np.stack([c, a, b, c, a, c, a, a, c])
+    assert list(oracle.distinctive_descriptors(off, d)) == [1, 0, -1, 0]
+
+
+def test_fuse_oracle_hand_example(oracle):
+    """Fuse (ORBmatcher.cc:1177-1333) on a 3-keypoint keyframe at the identity pose."""
+    from mam3slam_amd import scene
+    from mam3slam_amd.match import FUSE_MP_DTYPE, Pinhole
+    from mam3slam_amd.orb import KP_DTYPE
+
+    keys = np.zeros(3, KP_DTYPE)
+    keys["x"] = [100.0, 300.0, 302.0]
+    keys["y"] = [100.0, 200.0, 200.0]
+    keys["octave"] = [0, 1, 1]
+    desc = np.zeros((3, 32), np.uint8)
+    desc[1:] = 0x0F
+    desc[2, 0] = 0x00    # 4 bits from keypoint 1
+    KF = scene.make_frame_data(keys, desc, 640, 480)
+    KF.pose = (np.array([0, 0, 0, 1], np.float32), np.zeros(3, np.float32))
+    cam = Pinhole(500.0, 500.0, 320.0, 240.0)
+
+    def mp(u, v, z, drow, lvl):
+        m = np.zeros(1, FUSE_MP_DTYPE)
+        X = np.array([(u - 320) / 500 * z, (v - 240) / 500 * z, z], np.float64)
+        dist = np.linalg.norm(X)
+        m["pos"] = X
+        m["normal"] = X / dist
+        m["max_distance"] = dist * 1.2 ** (lvl - 0.5)   # PredictScale -> lvl
+        m["min_distance"] = m["max_distance"] / np.float32(1.2 ** 7)
+        m["valid"] = 1
+        m["desc"] = drow
+        return m
+
+    mps = np.concatenate([
+        mp(300.5, 200.0, 4.0, desc[1], 1),    # keypoints 1 and 2 in the window: 1 is 0 bits away -> 1
+        mp(301.5, 200.0, 4.0, desc[2], 1),    # -> 2 (0 bits)
+        mp(300.5, 200.0, -4.0, desc[1], 1),   # behind the camera
+        mp(100.2, 100.0, 3.0, ~desc[0], 0),   # 256 bits from keypoint 0: not < bestDist = 256
+        mp(300.5, 200.0, 4.0, desc[1], 4),    # predicted level 4: the level-1 keypoints fail the level test
+        mp(300.5, 200.0, 4.0, desc[1], 1),    # invalid (NULL / bad / already in the keyframe)
+    ])
+    mps["valid"][5] = 0
+    n, idx, dist = oracle.fuse(KF, mps, cam, 3.0)
+    assert n == 2 and list(idx) == [1, 2, -1, -1, -1, -1] and list(dist) == [0, 0, 256, 256, 256, 256]
