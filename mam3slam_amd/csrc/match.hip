@@ -1053,7 +1053,11 @@ __device__ bool fuse_window(const FuseArgs& p, int f, const mam_fuse_mp& mp, Win
     if ((double)dot < 0.5 * (double)dist3D) return false;
     // PredictScale (MapPoint.cc:514-529); log(float) as the correctly rounded float log
     const float ratio = mp.max_distance / dist3D;
+#if defined(MAM_FUSE_EXPERIMENT) && (MAM_FUSE_EXPERIMENT & 2)
+    int lvl = cvt_i32_x86(ceilf(logf(ratio) / K.log_scale_factor));   // timing experiment only
+#else
     int lvl = cvt_i32_x86(ceilf((float)log((double)ratio) / K.log_scale_factor));
+#endif
     if (lvl < 0) lvl = 0;
     else if (lvl >= p.g.nlevels) lvl = p.g.nlevels - 1;
     w->x = u;
@@ -1149,16 +1153,31 @@ __global__ __launch_bounds__(256) void k_fuse(FuseArgs p, int nframes) {
     const mam_fuse_mp& mp = p.mps[o];
     Window w;
     int bd = 256, bi = -1;
+#if defined(MAM_FUSE_EXPERIMENT) && (MAM_FUSE_EXPERIMENT & 1)
+    if (fuse_window(p, f, mp, &w) && w.r < 0.f) {   // timing experiment only: no window scan
+#else
     if (fuse_window(p, f, mp, &w)) {
+#endif
         const uint4 u0 = reinterpret_cast<const uint4*>(mp.desc)[0], u1 = reinterpret_cast<const uint4*>(mp.desc)[1];
         fuse_pass<GW>(p, f, w, u0, u1, &bd, &bi);
     }
     if ((lane_id() & (GW - 1)) == 0) {
-        const bool fused = bd <= MAM_TH_LOW;
-        p.out_idx[o] = fused ? bi : -1;
+        p.out_idx[o] = bd <= MAM_TH_LOW ? bi : -1;
         p.out_dist[o] = bd;
-        if (fused) atomicAdd(&p.out_n[f], 1);
     }
+}
+
+// nFused per keyframe (a per-MapPoint atomicAdd on one counter per keyframe serialises in L2: ~7 ns per MapPoint)
+__global__ __launch_bounds__(256) void k_fuse_count(FuseArgs p) {
+    __shared__ int red[4];
+    const int f = blockIdx.x, n = p.n_mps[f];
+    const int32_t* idx = p.out_idx + (size_t)f * p.mp_stride;
+    int c = 0;
+    for (int j = threadIdx.x; j < n; j += 256) c += idx[j] >= 0;
+    c = wave_sum(c);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0 && p.out_n[f] >= 0) p.out_n[f] = red[0] + red[1] + red[2] + red[3];
 }
 
 // ------------------------------------------------------------------------------------------------ distinctive descriptor
@@ -1364,6 +1383,7 @@ int launch_fuse(mam_match_ctx* c, mam::FuseArgs& a, int F, hipStream_t s) {
             constexpr int GW = MAM_GATHER_LANES;
             hipLaunchKernelGGL(mam::k_fuse<GW>, dim3((int)((units * GW + 255) / 256)), dim3(256), 0, s, a, F);
         }
+        hipLaunchKernelGGL(mam::k_fuse_count, dim3(F), dim3(256), 0, s, a);
     }
     MAM_HIP(hipGetLastError());
     return MAM_OK;

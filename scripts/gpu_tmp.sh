@@ -1,14 +1,12 @@
 #!/bin/bash
-# c2 bench with the LBA stream at the highest priority vs the default priority
+# Fuse timing variants: base / no window scan / logf
 set -u
-O=${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out
+R=${GRAFT_REPO_ROOT:-/root/repo}
+O=$R/gpurun_out
 mkdir -p $O
-cd ${GRAFT_REPO_ROOT:-/root/repo}
-timeout -k 10 300 python bench.py --config c2 --no-cpu-baseline --no-pose > $O/c2_prio.json 2> $O/c2_prio.err || { tail -5 $O/c2_prio.err; exit 1; }
-MAM_LBA_PRIORITY=0 timeout -k 10 300 python bench.py --config c2 --no-cpu-baseline --no-pose > $O/c2_noprio.json 2> $O/c2_noprio.err || { tail -5 $O/c2_noprio.err; exit 1; }
-python - <<'PY'
-import json
-for f in ("c2_prio", "c2_noprio"):
-    d = json.load(open(f"gpurun_out/{f}.json"))
-    print(f, round(d["value"]), d["ms_per_step"], d["lba"]["ms_per_solve_wall"])
-PY
+cd $R
+for V in base fz1 fz2; do
+  if [ $V = base ]; then L=""; else L=$R/build/libmam_gpu_$V.so; fi
+  MAM3SLAM_GPU_LIB=$L timeout -k 10 300 python scripts/fuse_bench.py --config c2 > $O/fz_$V.json 2> $O/fz_$V.err || { tail -20 $O/fz_$V.err; exit 1; }
+  echo $V; cat $O/fz_$V.json
+done
