@@ -205,6 +205,8 @@ def main():
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the B=1 latency section (profiling runs: every launch then covers one lane's batch)")
     ap.add_argument("--no-pose", action="store_true", help="skip the PoseOptimization section")
+    ap.add_argument("--no-sin", action="store_true",
+                    help="skip the SearchInNeighbors section (Fuse + ComputeDistinctiveDescriptors)")
     ap.add_argument("--lanes", type=int, default=4,
                     help="independent sub-batches (agent groups) per GPU, each with its own contexts and HIP stream, "
                          "so one group's latency-bound stages overlap another's compute")
@@ -500,6 +502,14 @@ def main():
     latency_ms = None if args.no_latency else measure_latency()
     pose_info = None if args.no_pose else pose_section(args, B, W, H, NF, cam, kps_h, cnt_h, d_out1, lasts, dev,
                                                        tstream)
+    sin_info = None
+    if not args.no_sin:
+        # LocalMapping::SearchInNeighbors' Hamming work, measured beside the step like the pose
+        # section: Fuse into 30 target keyframes + Fuse of 8000 candidates + ComputeDistinctiveDescriptors
+        from scripts import fuse_bench
+
+        sin_info = fuse_bench.run(args.config, reps=max(args.steps, 5), device=dev.index or 0,
+                                  oracle=not args.no_cpu_baseline and rank == 0)
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -559,6 +569,8 @@ def main():
         }
         if pose_info is not None:
             out["pose_optimization"] = pose_info
+        if sin_info is not None:
+            out["search_in_neighbors"] = sin_info
         if cfg["lba"]:
             out["lba"] = {"solves": lba_stats["n"], "ms_per_solve_wall": lba_stats["ms"] / max(lba_stats["n"], 1),
                           "iterations": lba_stats["its"], "edges": int(len(lba_prob.edge_point)),

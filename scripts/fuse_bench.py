@@ -24,24 +24,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c1", "c2"])
-    ap.add_argument("--targets", type=int, default=30)   # nn = 30 for monocular agents (LocalMapping.cc:833-835)
-    ap.add_argument("--candidates", type=int, default=8000)
-    ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--oracle", action="store_true")
-    args = ap.parse_args()
+def run(config="c2", targets=30, candidates=8000, reps=20, oracle=False, device=0) -> dict:
+    """One SearchInNeighbors workload (see the module docstring); returns the JSON object."""
     import torch
 
     from mam3slam_amd import ORBextractor, scene, synth
     from mam3slam_amd.match import FUSE_MP_DTYPE, FramesDev, FuseKF, ORBmatcher, fuse_kf
     from mam3slam_amd.orb import KP_DTYPE
 
-    W, H, NF = (640, 480, 1000) if args.config == "c1" else (1280, 720, 2000)
-    ext = ORBextractor(NF, 1.2, 8, 20, 7)
+    W, H, NF = (640, 480, 1000) if config == "c1" else (1280, 720, 2000)
+    ext = ORBextractor(NF, 1.2, 8, 20, 7, device=device)
     cam = scene.pinhole(W, H)
-    T = args.targets
+    T = targets
     feats = [ext(synth.make_frame(W, H, agent=1, frame=i))[:2] for i in range(4)]
     cases = []
     for i in range(T + 1):   # T targets + the current keyframe (backward direction)
@@ -51,9 +45,9 @@ def main():
         KF.pose = scene.small_pose(rng, rot=0.3, trans=0.5)
         cases.append((KF, scene.fuse_mappoints(KF, cam, rng)))
     cur, cur_mps = cases[T][0], scene.fuse_mappoints(cases[T][0], cam, np.random.default_rng(99), frac=1.0,
-                                                     n_out=args.candidates // 10)
-    cur_mps = np.resize(cur_mps, args.candidates)   # vpFuseCandidates: the targets' MapPoints, deduplicated
-    dev = torch.device("cuda")
+                                                     n_out=candidates // 10)
+    cur_mps = np.resize(cur_mps, candidates)   # vpFuseCandidates: the targets' MapPoints, deduplicated
+    dev = torch.device("cuda", device)
 
     def device_batch(items):
         B = len(items)
@@ -95,9 +89,9 @@ def main():
     t_off = torch.from_numpy(off).to(dev)
     t_desc = torch.from_numpy(descs).to(dev)
     t_best = torch.zeros(n_upd, dtype=torch.int32, device=dev)
-    M = ORBmatcher()
-    st = torch.cuda.Stream()
-    torch.cuda.synchronize()
+    M = ORBmatcher(device=device)
+    st = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize(dev)
 
     def fuse(t):
         M.fuse_batch_device(cur, t["fr"], t["kfs"].data_ptr(), cam, t["mps"].data_ptr(), t["U"], t["nm"].data_ptr(),
@@ -110,28 +104,28 @@ def main():
         fuse(fwd)
         fuse(bwd)
         update()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize(dev)
     ms = {}
     for name, fn in (("forward", lambda: fuse(fwd)), ("backward", lambda: fuse(bwd)), ("update", update)):
         M.set_profiling(True)
-        for _ in range(args.reps):
+        for _ in range(reps):
             fn()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(dev)
         stt = M.stage_times()
-        ms[name] = sum(v[0] for v in stt.values()) / args.reps
+        ms[name] = sum(v[0] for v in stt.values()) / reps
     M.set_profiling(False)
     t0 = time.perf_counter()
-    for _ in range(args.reps):
+    for _ in range(reps):
         fuse(fwd)
         fuse(bwd)
         update()
         st.synchronize()
-    wall = (time.perf_counter() - t0) * 1e3 / args.reps
-    out = {"config": args.config, "targets": T, "mps_per_target": float(np.mean([len(c[1]) for c in cases[:T]])),
+    wall = (time.perf_counter() - t0) * 1e3 / reps
+    out = {"config": config, "targets": T, "mps_per_target": float(np.mean([len(c[1]) for c in cases[:T]])),
            "candidates": len(cur_mps), "update_mps": n_upd, "update_obs_per_mp": float(sizes.mean()),
            "ms_forward": ms["forward"], "ms_backward": ms["backward"], "ms_update": ms["update"],
            "ms_total_kernels": ms["forward"] + ms["backward"] + ms["update"], "ms_total_wall": wall}
-    if args.oracle:
+    if oracle:
         from oracle import oracle_py
 
         gi, gd, gn = fwd["idx"].cpu().numpy(), fwd["dist"].cpu().numpy(), fwd["n"].cpu().numpy()
@@ -152,7 +146,18 @@ def main():
                     "oracle_ms_update": (t3 - t2) * 1e3, "oracle_ms_total": (t3 - t0) * 1e3,
                     "parity": {"forward_keyframes": f"{ok}/{T}", "backward": bool(ok_b), "update": bool(ok_u)}})
         out["speedup_wall"] = out["oracle_ms_total"] / wall
-    print(json.dumps(out), flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2", choices=["c1", "c2"])
+    ap.add_argument("--targets", type=int, default=30)   # nn = 30 for monocular agents (LocalMapping.cc:833-835)
+    ap.add_argument("--candidates", type=int, default=8000)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--oracle", action="store_true")
+    a = ap.parse_args()
+    print(json.dumps(run(a.config, a.targets, a.candidates, a.reps, a.oracle)), flush=True)
 
 
 if __name__ == "__main__":
