@@ -21,6 +21,7 @@
 namespace MAM3SLAM {
 
 class ORBextractor;
+class ORBVocabulary;
 class KeyFrame;
 class MapPoint;
 class Map;
@@ -96,8 +97,12 @@ public:
     std::vector<float> mvScaleFactors, mvLevelSigma2, mvInvLevelSigma2;
     float mnMinX, mnMaxX, mnMinY, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv;
     const Pinhole* mpCamera;
-    /* DBoW2::FeatureVector: node id -> feature indices (ascending node ids). */
+    /* DBoW2::BowVector / FeatureVector (node id -> feature indices, ascending node ids), set by ComputeBoW. */
+    std::map<unsigned int, double> mBowVec;
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+    ORBVocabulary* mpORBvocabulary = nullptr;
+    /* KeyFrame.cc:98-107: transform(mDescriptors, mBowVec, mFeatVec, 4) once (on the GPU). */
+    void ComputeBoW();
 
 private:
     std::mutex mMutexPose, mMutexFeatures;

@@ -59,8 +59,9 @@ def _match_sigs():
     from .lba import _SIGS as lba_sigs
     from .match import _SIGS
     from .pose import _SIGS as pose_sigs
+    from .bow import _SIGS as bow_sigs
 
-    return {**_SIGS, **lba_sigs, **ex_sigs, **pose_sigs}
+    return {**_SIGS, **lba_sigs, **ex_sigs, **pose_sigs, **bow_sigs}
 
 
 def lib() -> C.CDLL:

@@ -6,6 +6,7 @@
 
 #include "mam3slam/Map.h"
 #include "mam3slam/ORBextractor.h"
+#include "mam3slam/ORBVocabulary.h"
 #include "mam3slam/ORBmatcher.h"
 
 namespace MAM3SLAM {
@@ -195,6 +196,11 @@ void KeyFrame::EraseMapPointMatch(MapPoint* pMP) {
     const std::tuple<int, int> idx = pMP->GetIndexInKeyFrame(this);   // KeyFrame.cc:309-317
     if (std::get<0>(idx) != -1) mvpMapPoints[std::get<0>(idx)] = nullptr;
     if (std::get<1>(idx) != -1) mvpMapPoints[std::get<1>(idx)] = nullptr;
+}
+
+void KeyFrame::ComputeBoW() {
+    if ((mBowVec.empty() || mFeatVec.empty()) && mpORBvocabulary)
+        mpORBvocabulary->transform(mDescriptors, mBowVec, mFeatVec, 4);
 }
 
 mam_frame_geom KeyFrame::Geom() const {

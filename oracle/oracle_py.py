@@ -292,6 +292,28 @@ def distinctive_descriptors(desc_off, descs):
     return out[:n]
 
 
+# ---------------------------------------------------------------- DBoW2 oracle (oracle/bow_oracle.cpp)
+def bow_transform(v, descs, levelsup=4):
+    """v: mam3slam_amd.bow.VocabularyArrays. Returns ((word, weight, nid) per feature, bow dict, featvec dict)."""
+    L = lib()
+    L.oracle_bow_transform.restype = C.c_int
+    L.oracle_bow_transform.argtypes = [C.c_int] * 4 + [C.c_void_p] * 4 + [C.c_int, C.c_void_p, C.c_int] + \
+        [C.c_void_p] * 9
+    d = np.ascontiguousarray(descs, np.uint8).reshape(-1, 32)
+    n = len(d)
+    m = max(n, 1)
+    w, x, nid = np.zeros(m, np.uint32), np.zeros(m, np.float64), np.zeros(m, np.uint32)
+    bw, bv = np.zeros(m, np.uint32), np.zeros(m, np.float64)
+    fi, fo, ff = np.zeros(m, np.uint32), np.zeros(m + 1, np.int32), np.zeros(m, np.uint32)
+    nf = C.c_int(0)
+    nb = L.oracle_bow_transform(v.L, v.weighting, v.scoring, v.n_nodes, _vp(v.parent), _vp(v.is_leaf), _vp(v.desc),
+                                _vp(v.weight), n, _vp(d), int(levelsup), _vp(w), _vp(x), _vp(nid), _vp(bw), _vp(bv),
+                                _vp(fi), _vp(fo), _vp(ff), C.byref(nf))
+    bow = {int(bw[i]): float(bv[i]) for i in range(nb)}
+    fv = {int(fi[j]): [int(t) for t in ff[fo[j]:fo[j + 1]]] for j in range(nf.value)}
+    return (w[:n], x[:n], nid[:n]), bow, fv
+
+
 # ---------------------------------------------------------------- LBA oracle (oracle/lba_oracle.cpp)
 def lba_solve(prob, stop=None):
     """g2o LocalBundleAdjustment solve restatement. prob: mam3slam_amd.lba.LBAProblem."""

@@ -15,12 +15,14 @@
 #include <cstdlib>
 #include <array>
 #include <cstring>
+#include <fstream>
 #include <memory>
 #include <random>
 #include <string>
 #include <vector>
 
 #include "mam3slam/ORBextractor.h"
+#include "mam3slam/ORBVocabulary.h"
 #include "mam3slam/ORBmatcher.h"
 #include "mam3slam/Optimizer.h"
 
@@ -45,6 +47,10 @@ int oracle_fuse(const mam_frame_geom* g, int n, const mam_keypoint* keys, const 
                 const mam_pinhole* cam, int n_mps, const mam_fuse_mp* mps, float th, int32_t* out_idx,
                 int32_t* out_dist);
 int oracle_distinctive_descriptors(int n_mps, const int32_t* off, const uint8_t* descs, int32_t* out);
+int oracle_bow_transform(int L, int weighting, int scoring, int n_nodes, const int32_t* parent, const uint8_t* is_leaf,
+                         const uint8_t* vdesc, const double* vweight, int n, const uint8_t* desc, int levelsup,
+                         uint32_t* out_word, double* out_weight, uint32_t* out_nid, uint32_t* bow_words,
+                         double* bow_values, uint32_t* fv_ids, int32_t* fv_off, uint32_t* fv_feats, int* fv_nodes);
 }
 
 using namespace MAM3SLAM;
@@ -715,6 +721,70 @@ static void testFuse() {
     CHECK(checked > 200, "distinctive descriptors checked: %d", checked);
 }
 
+static void testBoW() {
+    // a 3-level, 6-ary vocabulary written in the reference's text format, loaded by ORBVocabulary, then
+    // KeyFrame::ComputeBoW vs the oracle's BowVector / FeatureVector on the same arrays
+    std::mt19937 rng(31);
+    const int k = 6, L = 3;
+    std::vector<int32_t> parent(1, 0);
+    std::vector<uint8_t> leaf(1, 0), desc(32, 0);
+    std::vector<double> weight(1, 0.0);
+    std::vector<int> level(1, 0);
+    for (size_t i = 0; i < parent.size(); i++) {
+        if (level[i] == L) continue;
+        for (int c = 0; c < k; c++) {
+            parent.push_back((int32_t)i);
+            level.push_back(level[i] + 1);
+            for (int b = 0; b < 32; b++) desc.push_back((uint8_t)(desc[i * 32 + b] ^ (rng() & rng() & 0xFF)));
+            leaf.push_back(level[i] + 1 == L ? 1 : 0);
+            weight.push_back(level[i] + 1 == L ? (double)(rng() % 1000) / 100.0 : 0.0);
+        }
+    }
+    const std::string path = "/tmp/mam_test_voc.txt";
+    {
+        std::ofstream f(path);
+        f << k << " " << L << "  0 0\n";
+        f.precision(17);
+        for (size_t i = 1; i < parent.size(); i++) {
+            f << parent[i] << " " << (int)leaf[i] << " ";
+            for (int b = 0; b < 32; b++) f << (int)desc[i * 32 + b] << " ";
+            f << " " << weight[i] << "\n";
+        }
+    }
+    ORBVocabulary voc;
+    CHECK(voc.loadFromTextFile(path), "loadFromTextFile");
+    CHECK(voc.size() == 216u, "words %u", voc.size());
+    Pinhole cam(500.f, 500.f, 320.f, 240.f);
+    std::vector<float> scales(8, 1.f), sig2(8, 1.f);
+    Frame F = emptyFrame(400, 640, 480, scales, sig2, &cam);
+    for (int i = 0; i < 400; i++)
+        for (int b = 0; b < 32; b++) F.mDescriptors.ptr(i)[b] = (uint8_t)rng();
+    Map map(0);
+    KeyFrame K(F, &map, 1);
+    K.mpORBvocabulary = &voc;
+    K.ComputeBoW();
+    const int n = K.N;
+    std::vector<uint32_t> w(n), nid(n), bw(n), fi(n), ff(n);
+    std::vector<double> x(n), bv(n);
+    std::vector<int32_t> fo(n + 1);
+    int nf = 0;
+    const int nb = oracle_bow_transform(L, 0, 0, (int)parent.size(), parent.data(), leaf.data(), desc.data(),
+                                        weight.data(), n, K.mDescriptors.data.data(), 4, w.data(), x.data(),
+                                        nid.data(), bw.data(), bv.data(), fi.data(), fo.data(), ff.data(), &nf);
+    CHECK(nb == (int)K.mBowVec.size() && nf == (int)K.mFeatVec.size() && nb > 50, "BowVector %zu vs %d", K.mBowVec.size(), nb);
+    int j = 0;
+    for (auto& e : K.mBowVec) {
+        CHECK(e.first == bw[j] && e.second == bv[j], "BowVector entry %d", j);
+        j++;
+    }
+    j = 0;
+    for (auto& e : K.mFeatVec) {
+        CHECK(e.first == fi[j] && (int)e.second.size() == fo[j + 1] - fo[j], "FeatureVector node %d", j);
+        for (size_t t = 0; t < e.second.size(); t++) CHECK(e.second[t] == ff[fo[j] + t], "FeatureVector feature");
+        j++;
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     testAlgebra();
@@ -726,6 +796,7 @@ int main(int argc, char** argv) {
         testLocalBA();
         testPoseOptimization();
         testFuse();
+        testBoW();
     }
     std::printf("OK %d checks (%s)\n", g_checks, mode.c_str());
     return 0;

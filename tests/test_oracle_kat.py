@@ -284,3 +284,40 @@ def test_fuse_oracle_hand_example(oracle):
     mps["valid"][5] = 0
     n, idx, dist = oracle.fuse(KF, mps, cam, 3.0)
     assert n == 2 and list(idx) == [1, 2, -1, -1, -1, -1] and list(dist) == [0, 0, 256, 256, 256, 256]
+
+
+def test_bow_oracle_hand_tree(oracle):
+    """DBoW2 transform (TemplatedVocabulary.h:1216-1259) on a hand-built tree: root -> A, B; A -> A1, A2 (leaves);
+    B leaf. Descent by the first minimum Hamming distance, the node at level L - levelsup, TF-IDF + L1."""
+    from mam3slam_amd import bow
+
+    z = np.zeros(32, np.uint8)
+    A = z.copy()
+    Bd = np.full(32, 0xFF, np.uint8)
+    A1 = z.copy()
+    A1[0] = 0x0F
+    A2 = z.copy()
+    A2[1] = 0xF0
+    # nodes: 0 root, 1 A, 2 B (leaf, word 0), 3 A1 (word 1), 4 A2 (word 2)
+    v = bow.VocabularyArrays(2, 2, bow.L1_NORM, bow.TF_IDF, [0, 0, 0, 1, 1], [0, 0, 1, 1, 1],
+                             np.stack([z, A, Bd, A1, A2]), [0.0, 0.0, 2.0, 1.0, 3.0])
+    f0 = A1.copy()                      # -> A (0 bits) -> A1 (0 bits): word 1
+    f1 = A2.copy()                      # -> A -> A2: word 2
+    f2 = np.full(32, 0xFF, np.uint8)    # -> B: word 0 (a leaf at level 1)
+    f3 = z.copy()                       # A1 and A2 both 4 bits away: the first child, A1
+    (w, x, nid), B, F = oracle.bow_transform(v, np.stack([f0, f1, f2, f3]), 1)   # node level 1
+    assert list(w) == [1, 2, 0, 1] and list(x) == [1.0, 3.0, 2.0, 1.0] and list(nid) == [1, 1, 2, 1]
+    assert B == {0: 2.0 / 7.0, 1: 2.0 / 7.0, 2: 3.0 / 7.0} and F == {1: [0, 1, 3], 2: [2]}
+    assert bow.bow_from_words(w, x, nid) == (B, F)
+
+
+def test_bow_text_round_trip(tmp_path):
+    from mam3slam_amd import bow
+
+    v = bow.synthetic_vocabulary(6, 3, np.random.default_rng(2), early_leaf=0.2)
+    p = tmp_path / "v.txt"
+    bow.save_to_text_file(v, str(p))
+    r = bow.load_from_text_file(str(p))
+    assert (r.k, r.L, r.scoring, r.weighting) == (6, 3, bow.L1_NORM, bow.TF_IDF)
+    assert np.array_equal(r.parent, v.parent) and np.array_equal(r.is_leaf, v.is_leaf)
+    assert np.array_equal(r.desc[1:], v.desc[1:]) and np.array_equal(r.weight, v.weight)
