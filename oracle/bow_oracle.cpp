@@ -91,11 +91,19 @@ extern "C" {
 // Per-feature outputs (as mam_bow_transform), plus the BowVector (words ascending, values) and the FeatureVector
 // (node ids ascending, offsets, feature indices) of transform(features, v, fv, levelsup). Capacities: n each.
 // Returns the BowVector size; *fv_nodes = the FeatureVector size.
-int oracle_bow_transform(int L, int weighting, int scoring, int n_nodes, const int32_t* parent, const uint8_t* is_leaf,
-                         const uint8_t* vdesc, const double* vweight, int n, const uint8_t* desc, int levelsup,
-                         uint32_t* out_word, double* out_weight, uint32_t* out_nid, uint32_t* bow_words,
-                         double* bow_values, uint32_t* fv_ids, int32_t* fv_off, uint32_t* fv_feats, int* fv_nodes) {
-    const Vocab V = build(L, weighting, scoring, n_nodes, parent, is_leaf, vdesc, vweight);
+// A built tree kept across calls (bench: the oracle's transform time without the tree build).
+void* oracle_bow_build(int L, int weighting, int scoring, int n_nodes, const int32_t* parent, const uint8_t* is_leaf,
+                       const uint8_t* vdesc, const double* vweight) {
+    return new Vocab(build(L, weighting, scoring, n_nodes, parent, is_leaf, vdesc, vweight));
+}
+
+void oracle_bow_free(void* h) { delete static_cast<Vocab*>(h); }
+
+int oracle_bow_run(const void* h, int n, const uint8_t* desc, int levelsup, uint32_t* out_word, double* out_weight,
+                   uint32_t* out_nid, uint32_t* bow_words, double* bow_values, uint32_t* fv_ids, int32_t* fv_off,
+                   uint32_t* fv_feats, int* fv_nodes) {
+    const Vocab& V = *static_cast<const Vocab*>(h);
+    const int weighting = V.weighting, scoring = V.scoring;
     std::map<unsigned, double> bow;
     std::map<unsigned, std::vector<unsigned>> fv;
     const bool must = scoring != 5;   // mustNormalize: every scoring but DOT_PRODUCT; L2_NORM with L2, else L1
@@ -143,6 +151,15 @@ int oracle_bow_transform(int L, int weighting, int scoring, int n_nodes, const i
     }
     *fv_nodes = m;
     return k;
+}
+
+int oracle_bow_transform(int L, int weighting, int scoring, int n_nodes, const int32_t* parent, const uint8_t* is_leaf,
+                         const uint8_t* vdesc, const double* vweight, int n, const uint8_t* desc, int levelsup,
+                         uint32_t* out_word, double* out_weight, uint32_t* out_nid, uint32_t* bow_words,
+                         double* bow_values, uint32_t* fv_ids, int32_t* fv_off, uint32_t* fv_feats, int* fv_nodes) {
+    const Vocab V = build(L, weighting, scoring, n_nodes, parent, is_leaf, vdesc, vweight);
+    return oracle_bow_run(&V, n, desc, levelsup, out_word, out_weight, out_nid, bow_words, bow_values, fv_ids, fv_off,
+                          fv_feats, fv_nodes);
 }
 
 }  // extern "C"

@@ -293,12 +293,30 @@ def distinctive_descriptors(desc_off, descs):
 
 
 # ---------------------------------------------------------------- DBoW2 oracle (oracle/bow_oracle.cpp)
-def bow_transform(v, descs, levelsup=4):
+class BowTree:
+    """A tree built once by the oracle (oracle_bow_build), for repeated transforms."""
+
+    def __init__(self, v):
+        L = lib()
+        L.oracle_bow_build.restype = C.c_void_p
+        L.oracle_bow_build.argtypes = [C.c_int] * 4 + [C.c_void_p] * 4
+        L.oracle_bow_free.argtypes = [C.c_void_p]
+        self._L = L
+        self.h = L.oracle_bow_build(v.L, v.weighting, v.scoring, v.n_nodes, _vp(v.parent), _vp(v.is_leaf),
+                                    _vp(v.desc), _vp(v.weight))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self._L.oracle_bow_free(self.h)
+            self.h = None
+
+
+def bow_transform(v, descs, levelsup=4, tree: BowTree | None = None):
     """v: mam3slam_amd.bow.VocabularyArrays. Returns ((word, weight, nid) per feature, bow dict, featvec dict)."""
+    t = BowTree(v) if tree is None else tree
     L = lib()
-    L.oracle_bow_transform.restype = C.c_int
-    L.oracle_bow_transform.argtypes = [C.c_int] * 4 + [C.c_void_p] * 4 + [C.c_int, C.c_void_p, C.c_int] + \
-        [C.c_void_p] * 9
+    L.oracle_bow_run.restype = C.c_int
+    L.oracle_bow_run.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int] + [C.c_void_p] * 9
     d = np.ascontiguousarray(descs, np.uint8).reshape(-1, 32)
     n = len(d)
     m = max(n, 1)
@@ -306,11 +324,10 @@ def bow_transform(v, descs, levelsup=4):
     bw, bv = np.zeros(m, np.uint32), np.zeros(m, np.float64)
     fi, fo, ff = np.zeros(m, np.uint32), np.zeros(m + 1, np.int32), np.zeros(m, np.uint32)
     nf = C.c_int(0)
-    nb = L.oracle_bow_transform(v.L, v.weighting, v.scoring, v.n_nodes, _vp(v.parent), _vp(v.is_leaf), _vp(v.desc),
-                                _vp(v.weight), n, _vp(d), int(levelsup), _vp(w), _vp(x), _vp(nid), _vp(bw), _vp(bv),
-                                _vp(fi), _vp(fo), _vp(ff), C.byref(nf))
+    nb = L.oracle_bow_run(t.h, n, _vp(d), int(levelsup), _vp(w), _vp(x), _vp(nid), _vp(bw), _vp(bv), _vp(fi), _vp(fo),
+                          _vp(ff), C.byref(nf))
     bow = {int(bw[i]): float(bv[i]) for i in range(nb)}
-    fv = {int(fi[j]): [int(t) for t in ff[fo[j]:fo[j + 1]]] for j in range(nf.value)}
+    fv = {int(fi[j]): [int(q) for q in ff[fo[j]:fo[j + 1]]] for j in range(nf.value)}
     return (w[:n], x[:n], nid[:n]), bow, fv
 
 

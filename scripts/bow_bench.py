@@ -72,18 +72,16 @@ def run(config="c2", keyframes=64, reps=20, oracle=False, device=0, L=6) -> dict
         from oracle import oracle_py
 
         gw, gx, gn = t_w.cpu().numpy().view(np.uint32), t_x.cpu().numpy(), t_n.cpu().numpy().view(np.uint32)
-        t0 = time.perf_counter()
-        oracle_py.bow_transform(v, D[0, :0], 4)   # the tree build alone
-        t1 = time.perf_counter()
+        tree = oracle_py.BowTree(v)
         ok = 0
         nk = 4
+        t1 = time.perf_counter()
         for f in range(nk):
             n = int(cnt[f, 0])
-            (wo, xo, no), _, _ = oracle_py.bow_transform(v, D[f, :n], 4)
+            (wo, xo, no), _, _ = oracle_py.bow_transform(v, D[f, :n], 4, tree)
             ok += int(np.array_equal(wo, gw[f, :n]) and np.array_equal(xo, gx[f, :n]) and np.array_equal(no, gn[f, :n]))
         t2 = time.perf_counter()
-        build = t1 - t0
-        out["oracle_ms_per_keyframe"] = ((t2 - t1) - nk * build) * 1e3 / nk
+        out["oracle_ms_per_keyframe"] = (t2 - t1) * 1e3 / nk
         out["parity_keyframes"] = f"{ok}/{nk}"
     return out
 

@@ -38,7 +38,7 @@ def test_bow_transform(gpu_lib, oracle, descs, tmp_path, k, L, levelsup):
         assert np.array_equal(w, wo) and np.array_equal(x, xo) and np.array_equal(nid, nido)
         B, F = voc.transform(d, levelsup)
         assert B == Bo and F == Fo   # exact doubles: same summation and normalisation order
-        assert len(F) > 1 and abs(sum(B.values()) - 1.0) < 1e-12
+        assert (len(F) > 1 or L - levelsup <= 0) and abs(sum(B.values()) - 1.0) < 1e-12
 
 
 def test_bow_edges(gpu_lib, oracle, descs):
@@ -86,3 +86,25 @@ def test_bow_batch_device(gpu_lib, oracle, descs):
         (wo, xo, nido), _, _ = oracle.bow_transform(v, d, 4)
         n = len(d)
         assert np.array_equal(gw[f, :n], wo) and np.array_equal(gx[f, :n], xo) and np.array_equal(gn[f, :n], nido)
+
+
+def test_triangulation_on_bow_feature_vectors(gpu_lib, oracle):
+    """SearchForTriangulation (a15) walking FeatureVectors made by the GPU transform (levelsup 4, as
+    KeyFrame::ComputeBoW), GPU search vs oracle search — the LocalMapping chain ComputeBoW -> CreateNewMapPoints."""
+    from mam3slam_amd import scene
+    from mam3slam_amd.match import ORBmatcher
+
+    img = synth.make_frame(640, 480, agent=6, frame=1)
+    k, d, _ = oracle.extract(img, oracle.params(1000))
+    rng = np.random.default_rng(21)
+    F = scene.make_frame_data(k, d, 640, 480)
+    KF1, KF2, F12, ep = scene.keyframe_pair(F, scene.pinhole(640, 480), rng)
+    voc = bow.ORBVocabulary(bow.synthetic_vocabulary(10, 6, np.random.default_rng(4), early_leaf=0.02))
+    KF1.featvec = voc.transform(KF1.desc, 4)[1]
+    KF2.featvec = voc.transform(KF2.desc, 4)[1]
+    assert len(KF1.featvec) > 20
+    for coarse in (False, True):
+        ng, pg = ORBmatcher(0.6, True).SearchForTriangulation(KF1, KF2, F12, ep, False, coarse)
+        no, oo = oracle.search_for_triangulation(KF1, KF2, F12, ep, True, coarse)
+        idx = np.nonzero(oo >= 0)[0]
+        assert ng == no and np.array_equal(pg, np.stack([idx, oo[idx]], 1)), coarse
