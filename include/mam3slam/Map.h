@@ -71,6 +71,7 @@ public:
     void GetCameraCenter(float Ow[3]);
 
     std::vector<MapPoint*> GetMapPointMatches();
+    std::set<MapPoint*> GetMapPoints();                   /* KeyFrame.cc:325-340: non-NULL, non-bad */
     MapPoint* GetMapPoint(size_t idx);
     void AddMapPoint(MapPoint* pMP, size_t idx);
     void ReplaceMapPointMatch(const int& idx, MapPoint* pMP);   /* KeyFrame.cc:320-323 */
@@ -87,7 +88,7 @@ public:
     mam_frame_geom Geom() const;
 
     unsigned long mnId;
-    unsigned long mnBALocalForKF = 0, mnBAFixedForKF = 0;
+    unsigned long mnBALocalForKF = 0, mnBAFixedForKF = 0, mnBALocalForMerge = 0;
     const int N;
     std::vector<KeyPoint> mvKeys, mvKeysUn;
     std::vector<float> mvuRight;
@@ -146,7 +147,7 @@ public:
     float GetMaxDistance();
 
     unsigned long mnId;
-    unsigned long mnBALocalForKF = 0;
+    unsigned long mnBALocalForKF = 0, mnBALocalForMerge = 0;
     /* Tracking fields written by Frame::isInFrustum (Frame.cc:512-586), read by SearchByProjection. */
     bool mbTrackInView = false;
     float mTrackProjX = 0.f, mTrackProjY = 0.f, mTrackDepth = 0.f, mTrackViewCos = 0.f;

@@ -10,6 +10,7 @@
 #define MAM3SLAM_OPTIMIZER_H
 
 #include <list>
+#include <set>
 #include <vector>
 
 #include "../mam_lba.h"
@@ -49,6 +50,18 @@ public:
     /* Optimizer.cc:1118-1180 + vertex/edge setup :1212-1394. Returns false where the reference returns before
      * optimizing because no keyframe is fixed (:1182-1186). */
     static bool BuildLocalBAWindow(KeyFrame* pKF, Map* pMap, LocalBAWindow& w);
+
+    /* The merge-window (welding) LocalBundleAdjustment, Optimizer.cc:3505-3952 (used when maps are merged,
+     * LoopClosing.cc:2670): vpFixedKF fixed, vpAdjustKF optimised, their MapPoints; optimize(5) with Huber
+     * (delta sqrt(5.99)), then the edges with chi2 > 5.991 or negative depth set to level 1 and every robust kernel
+     * removed, optimize(10) over level 0; outlier erase and write-back of the adjusted keyframes and the points. */
+    static void LocalBundleAdjustment(KeyFrame* pMainKF, std::vector<KeyFrame*> vpAdjustKF,
+                                      std::vector<KeyFrame*> vpFixedKF, bool* pbStopFlag);
+
+    /* Optimizer.cc:3531-3724: the merge window's vertices (fixed then adjusted keyframes, their MapPoints in
+     * GetMapPoints() order) and mono edges; marks mnBALocalForMerge. lLocalKeyFrames = the adjusted keyframes. */
+    static void BuildMergeBAWindow(KeyFrame* pMainKF, const std::vector<KeyFrame*>& vpAdjustKF,
+                                   const std::vector<KeyFrame*>& vpFixedKF, LocalBAWindow& w);
 };
 
 }  // namespace MAM3SLAM

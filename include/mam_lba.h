@@ -47,8 +47,11 @@ typedef struct mam_lba_problem {
     const double* edge_inv_sigma2; /* information = invSigma2 * I2 */
     int32_t n_cams;
     const float* cams;             /* [n_cams][4] Pinhole fx, fy, cx, cy (mvParameters, float) */
-    double huber_delta;            /* (double)(float)sqrt(5.991) */
+    double huber_delta;            /* (double)(float)sqrt(5.991); <= 0: no robust kernel (setRobustKernel(0)) */
     int32_t iterations;            /* optimize(10) */
+    const uint8_t* edge_active;    /* [n_edges] 1 = level 0, 0 = setLevel(1): left out of the optimisation
+                                      (initializeOptimization(0)); NULL = all edges. A vertex left without active
+                                      edges keeps its estimate. edge_chi2 of an inactive edge is not written. */
 } mam_lba_problem;
 
 typedef struct mam_lba_result {

@@ -58,7 +58,8 @@ struct Dev {
     int32_t* eidx;               // [Np][L] edge of (pose block, Hessian point), -1 if none
     int npad;                    // padded dimension of S (ldlt_pad(6 Np))
     double* ws;                  // global LDL^T workspace when it does not fit in LDS
-    double delta;
+    double delta;                // Huber delta; <= 0: no robust kernel
+    const uint8_t* active;       // [E] level-0 edges (NULL = all)
     // state
     const double* pose;          // [P][7] q(xyzw) t
     const double* pt;            // [L][3]
@@ -99,7 +100,7 @@ __device__ __forceinline__ void map_point(const double* T, const double* X, doub
 
 __device__ __forceinline__ void huber(double e, double delta, double* r0, double* r1) {
     const double dsqr = delta * delta;
-    if (e <= dsqr) { *r0 = e; *r1 = 1.0; }
+    if (delta <= 0.0 || e <= dsqr) { *r0 = e; *r1 = 1.0; }   // no kernel: rho(e) = e, rho' = 1
     else {
         const double s = sqrt(e);
         *r0 = 2 * s * delta - dsqr;
@@ -123,6 +124,17 @@ __global__ __launch_bounds__(256) void k_linearize(Dev d, int want_jac) {
     const double e0 = d.edge_obs[2 * e] - u, e1 = d.edge_obs[2 * e + 1] - v;
     d.err[2 * e] = e0;
     d.err[2 * e + 1] = e1;
+    if (d.active && !d.active[e]) {
+        // setLevel(1): outside initializeOptimization(0), no term in chi2 / H / b (zeros add exactly nothing)
+        d.rho0[e] = 0.0;
+        if (want_jac) {
+            double* o = d.jac + 21 * (size_t)e;
+            for (int k = 0; k < 21; k++) o[k] = 0.0;
+            if (d.pose_h[ipose] >= 0)
+                for (int k = 0; k < 18; k++) d.hpl[18 * (size_t)e + k] = 0.0;
+        }
+        return;
+    }
     const double w = d.edge_w[e];
     const double chi = e0 * (w * e0) + e1 * (w * e1);
     double r0, r1;
@@ -856,7 +868,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
                    sz<double>(6 * (size_t)E) + sz<double>(36 * (size_t)Np) + sz<double>(9 * (size_t)L) + sz<double>(nx) +
                    sz<double>(9 * (size_t)L) + sz<double>((size_t)npad * npad) + sz<double>(nx) + sz<double>(npad) + sz<double>(8) +
                    sz<double>(mam::lba::ldlt_ws_doubles(npad)) +
-                   sz<int>(4) + sz<uint8_t>(E) + 4096;
+                   sz<int>(4) + sz<uint8_t>(E) * 2 + 4096;
     if (int rc = c->arena.alloc(bytes)) return rc;
     if (int rc = c->staging.alloc(bytes)) return rc;
     Carver cv{c->arena.p};
@@ -875,6 +887,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     d.edge_pose = put(p->edge_pose, E);
     d.edge_obs = put(p->edge_obs, 2 * (size_t)E);
     d.edge_w = put(p->edge_inv_sigma2, E);
+    d.active = p->edge_active ? put(p->edge_active, E) : nullptr;
     d.cams = put(p->cams, 4 * (size_t)p->n_cams);
     {
         const int32_t* pcm = put(p->pose_cam ? p->pose_cam : pose_h.data(), P);
@@ -1073,6 +1086,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         MAM_HIP(hipMemcpyAsync(err.data(), d.err, sizeof(double) * 2 * E, hipMemcpyDeviceToHost, s));
         MAM_HIP(hipStreamSynchronize(s));
         for (int e = 0; e < E; e++) {
+            if (p->edge_active && !p->edge_active[e]) continue;   // not computed at level 0: left to the caller
             const double w = p->edge_inv_sigma2[e], e0 = err[2 * e], e1 = err[2 * e + 1];
             r->edge_chi2[e] = e0 * (w * e0) + e1 * (w * e1);
         }

@@ -175,6 +175,14 @@ std::vector<MapPoint*> KeyFrame::GetMapPointMatches() {
     return mvpMapPoints;
 }
 
+std::set<MapPoint*> KeyFrame::GetMapPoints() {
+    std::lock_guard<std::mutex> l(mMutexFeatures);
+    std::set<MapPoint*> s;
+    for (MapPoint* pMP : mvpMapPoints)
+        if (pMP && !pMP->isBad()) s.insert(pMP);
+    return s;
+}
+
 MapPoint* KeyFrame::GetMapPoint(size_t idx) {
     std::lock_guard<std::mutex> l(mMutexFeatures);
     return mvpMapPoints[idx];

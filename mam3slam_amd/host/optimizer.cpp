@@ -105,6 +105,7 @@ mam_lba_problem LocalBAWindow::Problem(int iterations) const {
     p.cams = cams.data();
     p.huber_delta = (double)(float)std::sqrt(5.991);   // const float thHuberMono = sqrt(5.991) (:1275)
     p.iterations = iterations;
+    p.edge_active = nullptr;
     return p;
 }
 
@@ -256,6 +257,137 @@ void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap
         p++;
     }
     pMap->IncreaseChangeIndex();
+}
+
+void Optimizer::BuildMergeBAWindow(KeyFrame* pMainKF, const std::vector<KeyFrame*>& vpAdjustKF,
+                                   const std::vector<KeyFrame*>& vpFixedKF, LocalBAWindow& w) {
+    w = LocalBAWindow();
+    Map* pCurrentMap = pMainKF->GetMap();
+    auto camIndex = [&](const Pinhole* c) {
+        for (size_t i = 0; i < w.camera_list.size(); i++)
+            if (w.camera_list[i] == c) return (int32_t)i;
+        w.camera_list.push_back(c);
+        for (int k = 0; k < 4; k++) w.cams.push_back(c->mvParameters[k]);
+        return (int32_t)(w.camera_list.size() - 1);
+    };
+    std::map<KeyFrame*, int32_t> kfIndex;
+    std::vector<MapPoint*> vpMPs;
+    // fixed, then non-fixed keyframe vertices with their MapPoints (:3531-3605)
+    auto addKF = [&](KeyFrame* pKFi, bool fixed) {
+        if (pKFi->isBad() || pKFi->GetMap() != pCurrentMap) return;
+        pKFi->mnBALocalForMerge = pMainKF->mnId;
+        const SE3f Tcw = pKFi->GetPose();
+        kfIndex[pKFi] = (int32_t)w.vpKF.size();
+        w.vpKF.push_back(pKFi);
+        w.pose_id.push_back((int64_t)pKFi->mnId);
+        w.pose_fixed.push_back(fixed ? 1 : 0);
+        for (int k = 0; k < 4; k++) w.pose_q.push_back((double)Tcw.q[k]);
+        for (int k = 0; k < 3; k++) w.pose_t.push_back((double)Tcw.t[k]);
+        w.pose_cam.push_back(camIndex(pKFi->mpCamera));
+        if (pKFi->mnId > w.maxKFid) w.maxKFid = pKFi->mnId;
+        (fixed ? w.lFixedCameras : w.lLocalKeyFrames).push_back(pKFi);
+        for (MapPoint* pMPi : pKFi->GetMapPoints())
+            if (pMPi && !pMPi->isBad() && pMPi->GetMap() == pCurrentMap && pMPi->mnBALocalForMerge != pMainKF->mnId) {
+                vpMPs.push_back(pMPi);
+                pMPi->mnBALocalForMerge = pMainKF->mnId;
+            }
+    };
+    for (KeyFrame* pKFi : vpFixedKF) addKF(pKFi, true);
+    for (KeyFrame* pKFi : vpAdjustKF) addKF(pKFi, false);
+    w.num_fixedKF = (int)w.lFixedCameras.size();
+    // MapPoint vertices and mono edges (:3634-3724)
+    for (MapPoint* pMPi : vpMPs) {
+        if (pMPi->isBad()) continue;
+        float pos[3];
+        pMPi->GetWorldPos(pos);
+        const int32_t pi = (int32_t)w.vpMP.size();
+        w.vpMP.push_back(pMPi);
+        w.lLocalMapPoints.push_back(pMPi);
+        w.point_id.push_back((int64_t)(pMPi->mnId + w.maxKFid + 1));
+        for (int k = 0; k < 3; k++) w.point_xyz.push_back((double)pos[k]);
+        for (const auto& obs : pMPi->GetObservations()) {
+            KeyFrame* pKF = obs.first;
+            const int idx = std::get<0>(obs.second);
+            if (pKF->isBad() || pKF->mnId > w.maxKFid || pKF->mnBALocalForMerge != pMainKF->mnId || idx == -1 ||
+                !pKF->GetMapPoint(idx))
+                continue;
+            if (pKF->mvuRight[idx] >= 0)
+                throw std::invalid_argument("LocalBundleAdjustment(merge): stereo observations are out of scope");
+            const KeyPoint& kpUn = pKF->mvKeysUn[idx];
+            w.edge_point.push_back(pi);
+            w.edge_pose.push_back(kfIndex.at(pKF));
+            w.edge_obs.push_back((double)kpUn.pt.x);
+            w.edge_obs.push_back((double)kpUn.pt.y);
+            w.edge_inv_sigma2.push_back((double)pKF->mvInvLevelSigma2[kpUn.octave]);
+        }
+    }
+}
+
+void Optimizer::LocalBundleAdjustment(KeyFrame* pMainKF, std::vector<KeyFrame*> vpAdjustKF,
+                                      std::vector<KeyFrame*> vpFixedKF, bool* pbStopFlag) {
+    LocalBAWindow w;
+    BuildMergeBAWindow(pMainKF, vpAdjustKF, vpFixedKF, w);
+    if (pbStopFlag && *pbStopFlag) return;   // :3725-3727
+    const size_t E = w.edge_point.size();
+    std::vector<double> q(w.pose_q.size()), t(w.pose_t.size()), x(w.point_xyz.size()), chi2(E);
+    std::vector<uint8_t> depth(E), active(E, 1);
+    const volatile uint8_t* stop = reinterpret_cast<const volatile uint8_t*>(pbStopFlag);
+    // optimize(5) with Huber kernels, delta thHuber2D = sqrt(5.99) as float (:3627, :3675-3677, :3730-3731)
+    mam_lba_problem prob = w.Problem(5);
+    prob.huber_delta = (double)(float)std::sqrt(5.99);
+    mam_lba_result res{q.data(), t.data(), x.data(), chi2.data(), depth.data(), 0, 0, 0, 0, 0};
+    int rc = mam_lba_solve(lbaCtx(), &prob, stop, &res);
+    if (rc < 0) throw std::runtime_error(std::string("mam_lba_solve failed: ") + mam_last_error());
+    if (!(pbStopFlag && *pbStopFlag)) {   // bDoMore (:3733-3737)
+        // chi2 > 5.991 or negative depth -> setLevel(1); every kernel removed (:3742-3757); a level-1 edge keeps
+        // the chi2 of the first optimisation (chi2() reads its last computed error)
+        for (size_t i = 0; i < E; i++) {
+            if (w.vpMP[w.edge_point[i]]->isBad()) continue;
+            if (chi2[i] > 5.991 || !depth[i]) active[i] = 0;
+        }
+        // initializeOptimization(0); optimize(10), from the first optimisation's estimates (:3778-3779)
+        const std::vector<double> q1 = q, t1 = t, x1 = x;
+        mam_lba_problem p2 = prob;
+        p2.pose_q = q1.data();
+        p2.pose_t = t1.data();
+        p2.point_xyz = x1.data();
+        p2.huber_delta = 0.0;
+        p2.iterations = 10;
+        p2.edge_active = active.data();
+        rc = mam_lba_solve(lbaCtx(), &p2, stop, &res);
+        if (rc < 0) throw std::runtime_error(std::string("mam_lba_solve failed: ") + mam_last_error());
+    }
+    // outliers (:3788-3807), erase under the map mutex (:3832-3843), recover the adjusted keyframes and the points
+    // (:3868-3951)
+    std::vector<std::pair<KeyFrame*, MapPoint*>> vToErase;
+    for (size_t i = 0; i < E; i++) {
+        MapPoint* pMP = w.vpMP[w.edge_point[i]];
+        if (pMP->isBad()) continue;
+        if (chi2[i] > 5.991 || !depth[i]) vToErase.push_back(std::make_pair(w.vpKF[w.edge_pose[i]], pMP));
+    }
+    std::unique_lock<std::mutex> lock(pMainKF->GetMap()->mMutexMapUpdate);
+    for (auto& e : vToErase) {
+        e.first->EraseMapPointMatch(e.second);
+        e.second->EraseObservation(e.first);
+    }
+    for (size_t k = 0; k < w.vpKF.size(); k++) {
+        if (w.pose_fixed[k]) continue;
+        KeyFrame* pKFi = w.vpKF[k];
+        if (pKFi->isBad()) continue;
+        SE3f Tiw;
+        for (int j = 0; j < 4; j++) Tiw.q[j] = (float)q[4 * k + j];
+        for (int j = 0; j < 3; j++) Tiw.t[j] = (float)t[3 * k + j];
+        const float n = std::sqrt(Tiw.q[0] * Tiw.q[0] + Tiw.q[1] * Tiw.q[1] + Tiw.q[2] * Tiw.q[2] + Tiw.q[3] * Tiw.q[3]);
+        for (int j = 0; j < 4; j++) Tiw.q[j] /= n;
+        pKFi->SetPose(Tiw);
+    }
+    for (size_t p = 0; p < w.vpMP.size(); p++) {
+        MapPoint* pMPi = w.vpMP[p];
+        if (pMPi->isBad()) continue;
+        const float pos[3] = {(float)x[3 * p], (float)x[3 * p + 1], (float)x[3 * p + 2]};
+        pMPi->SetWorldPos(pos);
+        pMPi->UpdateNormalAndDepth();
+    }
 }
 
 }  // namespace MAM3SLAM

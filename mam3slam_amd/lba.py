@@ -26,7 +26,8 @@ class _Problem(C.Structure):
                 ("pose_t", C.c_void_p), ("pose_cam", C.c_void_p), ("n_points", C.c_int32), ("point_id", C.c_void_p),
                 ("point_xyz", C.c_void_p), ("n_edges", C.c_int32), ("edge_point", C.c_void_p),
                 ("edge_pose", C.c_void_p), ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p),
-                ("n_cams", C.c_int32), ("cams", C.c_void_p), ("huber_delta", C.c_double), ("iterations", C.c_int32)]
+                ("n_cams", C.c_int32), ("cams", C.c_void_p), ("huber_delta", C.c_double), ("iterations", C.c_int32),
+                ("edge_active", C.c_void_p)]
 
 
 class _Result(C.Structure):
@@ -60,6 +61,7 @@ class LBAProblem:
     pose_cam: np.ndarray | None = None
     huber_delta: float = HUBER_MONO
     iterations: int = 10
+    edge_active: np.ndarray | None = None   # uint8 per edge: 0 = setLevel(1) (left out)
 
     def contiguous(self):
         for k, dt in [("pose_id", np.int64), ("pose_fixed", np.uint8), ("pose_q", np.float64), ("pose_t", np.float64),
@@ -69,6 +71,8 @@ class LBAProblem:
             setattr(self, k, np.ascontiguousarray(getattr(self, k), dt))
         if self.pose_cam is not None:
             self.pose_cam = np.ascontiguousarray(self.pose_cam, np.int32)
+        if self.edge_active is not None:
+            self.edge_active = np.ascontiguousarray(self.edge_active, np.uint8)
         return self
 
     def as_c(self) -> _Problem:
@@ -87,6 +91,7 @@ class LBAProblem:
         P.cams = self.cams.ctypes.data
         P.huber_delta = float(self.huber_delta)
         P.iterations = int(self.iterations)
+        P.edge_active = None if self.edge_active is None else self.edge_active.ctypes.data
         return P
 
 

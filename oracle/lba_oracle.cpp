@@ -72,9 +72,10 @@ struct Graph {
         const double e0 = err[2 * e], e1 = err[2 * e + 1];
         return e0 * (w * e0) + e1 * (w * e1);
     }
+    bool active(int e) const { return !p->edge_active || p->edge_active[e]; }   // level 0
     void robustify(double e, double rho[3]) const {
         const double delta = p->huber_delta, dsqr = delta * delta;
-        if (e <= dsqr) { rho[0] = e; rho[1] = 1.; rho[2] = 0.; }
+        if (delta <= 0.0 || e <= dsqr) { rho[0] = e; rho[1] = 1.; rho[2] = 0.; }   // no kernel: rho(e) = e
         else {
             const double sqrte = std::sqrt(e);
             rho[0] = 2 * sqrte * delta - dsqr;
@@ -85,6 +86,7 @@ struct Graph {
     double activeRobustChi2() const {
         double chi = 0.0, rho[3];
         for (int e = 0; e < p->n_edges; e++) {
+            if (!active(e)) continue;
             robustify(chi2(e), rho);
             chi += rho[0];
         }
@@ -97,6 +99,7 @@ struct Graph {
         std::fill(Hpl.begin(), Hpl.end(), 0.0);
         std::fill(b.begin(), b.end(), 0.0);
         for (int e = 0; e < p->n_edges; e++) {
+            if (!active(e)) continue;
             const int ip = p->edge_pose[e], il = p->edge_point[e];
             const SE3& T = pose[ip];
             double Xc[3];
@@ -361,7 +364,7 @@ extern "C" int oracle_lba_solve(const mam_lba_problem* p, const volatile uint8_t
     // chi2() reads the error of the LAST computeActiveErrors (a rejected trial's, if the run ended on one);
     // isDepthPositive() recomputes from the current estimates (OptimizableTypes.h:99-110)
     for (int e = 0; e < p->n_edges; e++) {
-        if (r->edge_chi2) r->edge_chi2[e] = g.chi2(e);
+        if (r->edge_chi2 && g.active(e)) r->edge_chi2[e] = g.chi2(e);
         if (r->edge_depth_ok) {
             double Xc[3];
             se3Map(g.pose[p->edge_pose[e]], &g.pt[3 * p->edge_point[e]], Xc);

@@ -180,8 +180,8 @@ struct Scene {
         }
     }
     void resetMarks() {
-        for (auto& k : kfs) k->mnBALocalForKF = k->mnBAFixedForKF = 0;
-        for (auto& p : mps) p->mnBALocalForKF = 0;
+        for (auto& k : kfs) k->mnBALocalForKF = k->mnBAFixedForKF = k->mnBALocalForMerge = 0;
+        for (auto& p : mps) p->mnBALocalForKF = p->mnBALocalForMerge = 0;
     }
 };
 
@@ -721,6 +721,65 @@ static void testFuse() {
     CHECK(checked > 200, "distinctive descriptors checked: %d", checked);
 }
 
+static void testMergeBA() {
+    // the welding-window LBA (Optimizer.cc:3505-3952) vs the oracle running the same two-stage schedule
+    Scene S(10, 500, 4, 57, 0.1f);
+    KeyFrame* pMain = S.kfs[5].get();
+    std::vector<KeyFrame*> adjust = {S.kfs[3].get(), S.kfs[4].get(), S.kfs[5].get(), S.kfs[6].get(), S.kfs[7].get()};
+    std::vector<KeyFrame*> fixed = {S.kfs[1].get(), S.kfs[2].get(), S.kfs[8].get()};
+    LocalBAWindow w;
+    Optimizer::BuildMergeBAWindow(pMain, adjust, fixed, w);
+    CHECK(w.lLocalKeyFrames.size() == 5 && w.lFixedCameras.size() == 3 && w.edge_point.size() > 1000,
+          "merge window %zu edges", w.edge_point.size());
+    const size_t E = w.edge_point.size();
+    std::vector<double> q(w.pose_q.size()), t(w.pose_t.size()), x(w.point_xyz.size()), chi2(E);
+    std::vector<uint8_t> depth(E), active(E, 1);
+    mam_lba_problem p1 = w.Problem(5);
+    p1.huber_delta = (double)(float)std::sqrt(5.99);
+    mam_lba_result r{q.data(), t.data(), x.data(), chi2.data(), depth.data(), 0, 0, 0, 0, 0};
+    CHECK(oracle_lba_solve(&p1, nullptr, &r) == 0 && r.status == 0, "oracle stage 1");
+    int nout = 0;
+    for (size_t i = 0; i < E; i++)
+        if (chi2[i] > 5.991 || !depth[i]) { active[i] = 0; nout++; }
+    CHECK(nout > 10, "stage 1 outliers %d", nout);
+    const std::vector<double> q1 = q, t1 = t, x1 = x;
+    mam_lba_problem p2 = p1;
+    p2.pose_q = q1.data(); p2.pose_t = t1.data(); p2.point_xyz = x1.data();
+    p2.huber_delta = 0.0; p2.iterations = 10; p2.edge_active = active.data();
+    CHECK(oracle_lba_solve(&p2, nullptr, &r) == 0 && r.status == 0 && r.final_chi2 < r.initial_chi2, "oracle stage 2");
+    std::vector<std::pair<KeyFrame*, MapPoint*>> erase;
+    for (size_t i = 0; i < E; i++)
+        if (chi2[i] > 5.991 || !depth[i]) erase.push_back({w.vpKF[w.edge_pose[i]], w.vpMP[w.edge_point[i]]});
+    std::vector<SE3f> fixedBefore;
+    for (KeyFrame* k : fixed) fixedBefore.push_back(k->GetPose());
+
+    S.resetMarks();
+    bool stop = false;
+    Optimizer::LocalBundleAdjustment(pMain, adjust, fixed, &stop);
+    double worst = 0.0;
+    for (size_t k = 0; k < w.vpKF.size(); k++) {
+        if (w.pose_fixed[k]) continue;
+        const SE3f T = w.vpKF[k]->GetPose();
+        for (int j = 0; j < 3; j++) worst = std::max(worst, std::fabs((double)T.t[j] - t[3 * k + j]) / (1.0 + std::fabs(t[3 * k + j])));
+        for (int j = 0; j < 4; j++) worst = std::max(worst, std::fabs((double)T.q[j] - q[4 * k + j]));
+    }
+    int written = 0;
+    for (size_t p = 0; p < w.vpMP.size(); p++) {
+        if (w.vpMP[p]->isBad()) continue;   // made bad by the outlier erase: not written back (:3944-3945)
+        float X[3];
+        w.vpMP[p]->GetWorldPos(X);
+        const double n = std::sqrt(x[3 * p] * x[3 * p] + x[3 * p + 1] * x[3 * p + 1] + x[3 * p + 2] * x[3 * p + 2]);
+        for (int j = 0; j < 3; j++) worst = std::max(worst, std::fabs((double)X[j] - x[3 * p + j]) / std::max(n, 1e-9));
+        written++;
+    }
+    CHECK(worst <= 1e-4 && written > 300, "merge LBA write-back vs oracle: worst rel %.3g (%d points)", worst, written);
+    for (size_t i = 0; i < fixed.size(); i++) {
+        const SE3f after = fixed[i]->GetPose();
+        CHECK(std::memcmp(&fixedBefore[i], &after, sizeof(SE3f)) == 0, "fixed keyframe %zu moved", i);
+    }
+    for (auto& e : erase) CHECK(std::get<0>(e.second->GetIndexInKeyFrame(e.first)) == -1, "outlier not erased");
+}
+
 static void testBoW() {
     // a 3-level, 6-ary vocabulary written in the reference's text format, loaded by ORBVocabulary, then
     // KeyFrame::ComputeBoW vs the oracle's BowVector / FeatureVector on the same arrays
@@ -797,6 +856,7 @@ int main(int argc, char** argv) {
         testPoseOptimization();
         testFuse();
         testBoW();
+        testMergeBA();
     }
     std::printf("OK %d checks (%s)\n", g_checks, mode.c_str());
     return 0;

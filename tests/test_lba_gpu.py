@@ -68,3 +68,40 @@ def test_lba_stop_flag(solver, oracle):
     ro = oracle.lba_solve(prob, stop)
     assert rg.iterations == ro.iterations == 0 and rg.status == ro.status == 1
     assert _rel(rg.point_xyz, prob.point_xyz) == 0.0
+
+
+def _stage2(prob, r, iterations=10):
+    """The merge-window LBA's second optimisation (Optimizer.cc:3742-3779): chi2 > 5.991 or negative depth ->
+    setLevel(1), every robust kernel removed, optimize(10) over level 0 from the first optimisation's estimates."""
+    import dataclasses
+
+    active = ~((r.edge_chi2 > 5.991) | ~r.edge_depth_ok.astype(bool))
+    return dataclasses.replace(prob, pose_q=np.array(r.pose_q), pose_t=np.array(r.pose_t),
+                               point_xyz=np.array(r.point_xyz), huber_delta=0.0, iterations=iterations,
+                               edge_active=active.astype(np.uint8)), active
+
+
+@pytest.mark.parametrize("seed", [4, 13])
+def test_lba_merge_schedule(solver, oracle, seed):
+    """Welding LBA schedule (Optimizer.cc:3730-3779): optimize(5) with Huber delta sqrt(5.99), then level-1 outliers
+    and no kernels for optimize(10). Each side runs both stages on its own estimates."""
+    prob = synthetic_problem(n_opt=12, n_fixed=4, n_points=600, obs_per_point=6, seed=seed, outlier_frac=0.12)
+    prob.huber_delta = float(np.float32(np.sqrt(5.99)))
+    prob.iterations = 5
+    rg1, ro1 = solver.solve(prob), oracle.lba_solve(prob)
+    pg, ag = _stage2(prob, rg1)
+    po, ao = _stage2(prob, ro1)
+    assert np.array_equal(ag, ao) and (~ao).sum() > 10
+    rg, ro = solver.solve(pg), oracle.lba_solve(po)
+    assert rg.status == 0 and ro.status == 0
+    assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials)
+    assert abs(rg.final_chi2 - ro.final_chi2) <= 1e-6 * ro.final_chi2 and ro.final_chi2 < ro.initial_chi2
+    assert _rel(rg.pose_t, ro.pose_t) <= 1e-4 and _rel(rg.pose_q, ro.pose_q) <= 1e-4
+    assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
+    assert np.allclose(rg.edge_chi2[ao], ro.edge_chi2[ao], rtol=1e-6, atol=1e-9)
+    # a point whose every edge is at level 1 keeps its stage-1 estimate
+    ep = np.asarray(prob.edge_point)
+    alive = np.zeros(len(prob.point_id), bool)
+    alive[ep[ao]] = True
+    if (~alive).any():
+        assert np.array_equal(np.asarray(rg.point_xyz)[~alive], np.asarray(rg1.point_xyz)[~alive])
