@@ -89,6 +89,9 @@ public:
 
     unsigned long mnId;
     unsigned long mnBALocalForKF = 0, mnBAFixedForKF = 0, mnBALocalForMerge = 0;
+    /* global BA results kept for the loop closer (Optimizer.cc:299-300) */
+    SE3f mTcwGBA;
+    unsigned long mnBAGlobalForKF = 0;
     const int N;
     std::vector<KeyPoint> mvKeys, mvKeysUn;
     std::vector<float> mvuRight;
@@ -148,6 +151,8 @@ public:
 
     unsigned long mnId;
     unsigned long mnBALocalForKF = 0, mnBALocalForMerge = 0;
+    float mPosGBA[3] = {0.f, 0.f, 0.f};   /* global BA result kept for the loop closer (Optimizer.cc:386-387) */
+    unsigned long mnBAGlobalForKF = 0;
     /* Tracking fields written by Frame::isInFrustum (Frame.cc:512-586), read by SearchByProjection. */
     bool mbTrackInView = false;
     float mTrackProjX = 0.f, mTrackProjY = 0.f, mTrackDepth = 0.f, mTrackViewCos = 0.f;
@@ -176,6 +181,21 @@ public:
     bool IsInertial() const { return false; }
     void EraseMapPoint(MapPoint* pMP) { std::lock_guard<std::mutex> l(mMutexMap); mspMapPoints.erase(pMP); }
     void AddMapPoint(MapPoint* pMP) { std::lock_guard<std::mutex> l(mMutexMap); mspMapPoints.insert(pMP); }
+    /* Map.cc: AddKeyFrame (the first one is the origin), GetAllKeyFrames / GetAllMapPoints (std::set order) */
+    void AddKeyFrame(KeyFrame* pKF) {
+        std::lock_guard<std::mutex> l(mMutexMap);
+        if (mspKeyFrames.empty()) mpKFinitial = pKF;
+        mspKeyFrames.insert(pKF);
+    }
+    std::vector<KeyFrame*> GetAllKeyFrames() {
+        std::lock_guard<std::mutex> l(mMutexMap);
+        return std::vector<KeyFrame*>(mspKeyFrames.begin(), mspKeyFrames.end());
+    }
+    std::vector<MapPoint*> GetAllMapPoints() {
+        std::lock_guard<std::mutex> l(mMutexMap);
+        return std::vector<MapPoint*>(mspMapPoints.begin(), mspMapPoints.end());
+    }
+    KeyFrame* GetOriginKF() { return mpKFinitial; }
     void IncreaseChangeIndex() { std::lock_guard<std::mutex> l(mMutexMap); mnMapChange++; }
     int GetMapChangeIndex() { std::lock_guard<std::mutex> l(mMutexMap); return mnMapChange; }
 
@@ -185,6 +205,8 @@ private:
     unsigned long mnInitKFid;
     std::mutex mMutexMap;
     std::set<MapPoint*> mspMapPoints;
+    std::set<KeyFrame*> mspKeyFrames;
+    KeyFrame* mpKFinitial = nullptr;
     int mnMapChange = 0;
 };
 

@@ -58,6 +58,19 @@ public:
     static void LocalBundleAdjustment(KeyFrame* pMainKF, std::vector<KeyFrame*> vpAdjustKF,
                                       std::vector<KeyFrame*> vpFixedKF, bool* pbStopFlag);
 
+    /* GlobalBundleAdjustemnt / BundleAdjustment (Optimizer.cc:52-390), mono: every non-bad keyframe (the map's
+     * initial keyframe fixed) and MapPoint with at least one edge, optimize(nIterations) with Huber kernels if
+     * bRobust; written back directly when nLoopKF is the origin keyframe's id, else into mTcwGBA / mPosGBA with
+     * mnBAGlobalForKF = nLoopKF. */
+    static void GlobalBundleAdjustemnt(Map* pMap, int nIterations = 5, bool* pbStopFlag = nullptr,
+                                       const unsigned long nLoopKF = 0, const bool bRobust = true);
+    static void BundleAdjustment(const std::vector<KeyFrame*>& vpKFs, const std::vector<MapPoint*>& vpMP,
+                                 int nIterations = 5, bool* pbStopFlag = nullptr, const unsigned long nLoopKF = 0,
+                                 const bool bRobust = true);
+    /* Optimizer.cc:88-275: the graph BundleAdjustment builds; vbNotIncludedMP[i] = MapPoint i has no edge. */
+    static void BuildBAWindow(const std::vector<KeyFrame*>& vpKFs, const std::vector<MapPoint*>& vpMP,
+                              LocalBAWindow& w, std::vector<bool>& vbNotIncludedMP);
+
     /* Optimizer.cc:3531-3724: the merge window's vertices (fixed then adjusted keyframes, their MapPoints in
      * GetMapPoints() order) and mono edges; marks mnBALocalForMerge. lLocalKeyFrames = the adjusted keyframes. */
     static void BuildMergeBAWindow(KeyFrame* pMainKF, const std::vector<KeyFrame*>& vpAdjustKF,

@@ -259,6 +259,122 @@ void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap
     pMap->IncreaseChangeIndex();
 }
 
+void Optimizer::BuildBAWindow(const std::vector<KeyFrame*>& vpKFs, const std::vector<MapPoint*>& vpMP,
+                              LocalBAWindow& w, std::vector<bool>& vbNotIncludedMP) {
+    w = LocalBAWindow();
+    vbNotIncludedMP.assign(vpMP.size(), false);
+    if (vpKFs.empty()) return;
+    Map* pMap = vpKFs[0]->GetMap();
+    auto camIndex = [&](const Pinhole* c) {
+        for (size_t i = 0; i < w.camera_list.size(); i++)
+            if (w.camera_list[i] == c) return (int32_t)i;
+        w.camera_list.push_back(c);
+        for (int k = 0; k < 4; k++) w.cams.push_back(c->mvParameters[k]);
+        return (int32_t)(w.camera_list.size() - 1);
+    };
+    std::map<KeyFrame*, int32_t> kfIndex;
+    // KeyFrame vertices (:100-117): the initial keyframe fixed
+    for (KeyFrame* pKF : vpKFs) {
+        if (pKF->isBad()) continue;
+        const SE3f Tcw = pKF->GetPose();
+        const bool fixed = pKF->mnId == pMap->GetInitKFid();
+        kfIndex[pKF] = (int32_t)w.vpKF.size();
+        w.vpKF.push_back(pKF);
+        w.pose_id.push_back((int64_t)pKF->mnId);
+        w.pose_fixed.push_back(fixed ? 1 : 0);
+        for (int k = 0; k < 4; k++) w.pose_q.push_back((double)Tcw.q[k]);
+        for (int k = 0; k < 3; k++) w.pose_t.push_back((double)Tcw.t[k]);
+        w.pose_cam.push_back(camIndex(pKF->mpCamera));
+        if (pKF->mnId > w.maxKFid) w.maxKFid = pKF->mnId;
+        (fixed ? w.lFixedCameras : w.lLocalKeyFrames).push_back(pKF);
+    }
+    w.num_fixedKF = (int)w.lFixedCameras.size();
+    // MapPoint vertices and mono edges (:122-275); a point without edges is removed again (:266-270)
+    for (size_t i = 0; i < vpMP.size(); i++) {
+        MapPoint* pMP = vpMP[i];
+        if (pMP->isBad()) continue;
+        const int32_t pi = (int32_t)w.vpMP.size();
+        const size_t e0 = w.edge_point.size();
+        for (const auto& obs : pMP->GetObservations()) {
+            KeyFrame* pKF = obs.first;
+            if (pKF->isBad() || pKF->mnId > w.maxKFid) continue;
+            auto it = kfIndex.find(pKF);
+            if (it == kfIndex.end()) continue;   // optimizer.vertex(pKF->mnId) == NULL
+            const int leftIndex = std::get<0>(obs.second);
+            if (leftIndex == -1) continue;
+            if (pKF->mvuRight[leftIndex] >= 0)
+                throw std::invalid_argument("BundleAdjustment: stereo observations are out of scope");
+            const KeyPoint& kpUn = pKF->mvKeysUn[leftIndex];
+            w.edge_point.push_back(pi);
+            w.edge_pose.push_back(it->second);
+            w.edge_obs.push_back((double)kpUn.pt.x);
+            w.edge_obs.push_back((double)kpUn.pt.y);
+            w.edge_inv_sigma2.push_back((double)pKF->mvInvLevelSigma2[kpUn.octave]);
+        }
+        if (w.edge_point.size() == e0) {
+            vbNotIncludedMP[i] = true;
+            continue;
+        }
+        float pos[3];
+        pMP->GetWorldPos(pos);
+        w.vpMP.push_back(pMP);
+        w.lLocalMapPoints.push_back(pMP);
+        w.point_id.push_back((int64_t)(pMP->mnId + w.maxKFid + 1));
+        for (int k = 0; k < 3; k++) w.point_xyz.push_back((double)pos[k]);
+    }
+}
+
+void Optimizer::GlobalBundleAdjustemnt(Map* pMap, int nIterations, bool* pbStopFlag, const unsigned long nLoopKF,
+                                       const bool bRobust) {
+    const std::vector<KeyFrame*> vpKFs = pMap->GetAllKeyFrames();
+    const std::vector<MapPoint*> vpMP = pMap->GetAllMapPoints();
+    BundleAdjustment(vpKFs, vpMP, nIterations, pbStopFlag, nLoopKF, bRobust);
+}
+
+void Optimizer::BundleAdjustment(const std::vector<KeyFrame*>& vpKFs, const std::vector<MapPoint*>& vpMP,
+                                 int nIterations, bool* pbStopFlag, const unsigned long nLoopKF, const bool bRobust) {
+    if (vpKFs.empty()) return;
+    Map* pMap = vpKFs[0]->GetMap();
+    LocalBAWindow w;
+    std::vector<bool> vbNotIncludedMP;
+    BuildBAWindow(vpKFs, vpMP, w, vbNotIncludedMP);
+    mam_lba_problem prob = w.Problem(nIterations);
+    prob.huber_delta = bRobust ? (double)(float)std::sqrt(5.99) : 0.0;   // thHuber2D (:119, :166-171)
+    std::vector<double> q(w.pose_q.size()), t(w.pose_t.size()), x(w.point_xyz.size());
+    mam_lba_result res{q.data(), t.data(), x.data(), nullptr, nullptr, 0, 0, 0, 0, 0};
+    const int rc = mam_lba_solve(lbaCtx(), &prob, reinterpret_cast<const volatile uint8_t*>(pbStopFlag), &res);
+    if (rc < 0) throw std::runtime_error(std::string("mam_lba_solve failed: ") + mam_last_error());
+    // Recover optimized data (:283-389)
+    KeyFrame* pOrigin = pMap->GetOriginKF();
+    const bool direct = pOrigin && nLoopKF == pOrigin->mnId;
+    for (size_t k = 0; k < w.vpKF.size(); k++) {
+        KeyFrame* pKF = w.vpKF[k];
+        SE3f T;
+        for (int j = 0; j < 4; j++) T.q[j] = (float)q[4 * k + j];
+        for (int j = 0; j < 3; j++) T.t[j] = (float)t[3 * k + j];
+        const float n = std::sqrt(T.q[0] * T.q[0] + T.q[1] * T.q[1] + T.q[2] * T.q[2] + T.q[3] * T.q[3]);
+        for (int j = 0; j < 4; j++) T.q[j] /= n;
+        if (direct) {
+            pKF->SetPose(T);
+        } else {
+            pKF->mTcwGBA = T;
+            pKF->mnBAGlobalForKF = nLoopKF;
+        }
+    }
+    for (size_t p = 0; p < w.vpMP.size(); p++) {
+        MapPoint* pMP = w.vpMP[p];
+        if (pMP->isBad()) continue;
+        const float pos[3] = {(float)x[3 * p], (float)x[3 * p + 1], (float)x[3 * p + 2]};
+        if (direct) {
+            pMP->SetWorldPos(pos);
+            pMP->UpdateNormalAndDepth();
+        } else {
+            for (int j = 0; j < 3; j++) pMP->mPosGBA[j] = pos[j];
+            pMP->mnBAGlobalForKF = nLoopKF;
+        }
+    }
+}
+
 void Optimizer::BuildMergeBAWindow(KeyFrame* pMainKF, const std::vector<KeyFrame*>& vpAdjustKF,
                                    const std::vector<KeyFrame*>& vpFixedKF, LocalBAWindow& w) {
     w = LocalBAWindow();

@@ -780,6 +780,40 @@ static void testMergeBA() {
     for (auto& e : erase) CHECK(std::get<0>(e.second->GetIndexInKeyFrame(e.first)) == -1, "outlier not erased");
 }
 
+static void testGlobalBA() {
+    // GlobalBundleAdjustemnt (Optimizer.cc:52-390) vs the oracle solve of the same graph, both write-back modes
+    for (int mode = 0; mode < 2; mode++) {
+        Scene S(8, 300, 3, 71 + mode, 0.05f);
+        for (auto& k : S.kfs) S.map.AddKeyFrame(k.get());
+        LocalBAWindow w;
+        std::vector<bool> notIncluded;
+        Optimizer::BuildBAWindow(S.map.GetAllKeyFrames(), S.map.GetAllMapPoints(), w, notIncluded);
+        CHECK(w.vpKF.size() == 8 && w.lFixedCameras.size() == 1 && w.vpMP.size() == 300, "global window");
+        mam_lba_problem prob = w.Problem(10);
+        prob.huber_delta = (double)(float)std::sqrt(5.99);
+        std::vector<double> q(w.pose_q.size()), t(w.pose_t.size()), x(w.point_xyz.size());
+        mam_lba_result r{q.data(), t.data(), x.data(), nullptr, nullptr, 0, 0, 0, 0, 0};
+        CHECK(oracle_lba_solve(&prob, nullptr, &r) == 0 && r.final_chi2 < r.initial_chi2, "oracle global BA");
+        const unsigned long nLoopKF = mode == 0 ? S.kfs[0]->mnId : 77;   // origin: direct write-back; else GBA fields
+        Optimizer::GlobalBundleAdjustemnt(&S.map, 10, nullptr, nLoopKF, true);
+        double worst = 0.0;
+        for (size_t k = 0; k < w.vpKF.size(); k++) {
+            const SE3f T = mode == 0 ? w.vpKF[k]->GetPose() : w.vpKF[k]->mTcwGBA;
+            for (int j = 0; j < 3; j++) worst = std::max(worst, std::fabs((double)T.t[j] - t[3 * k + j]) / (1.0 + std::fabs(t[3 * k + j])));
+            for (int j = 0; j < 4; j++) worst = std::max(worst, std::fabs((double)T.q[j] - q[4 * k + j]));
+            CHECK(mode == 0 || w.vpKF[k]->mnBAGlobalForKF == 77, "mnBAGlobalForKF");
+        }
+        for (size_t p = 0; p < w.vpMP.size(); p++) {
+            float X[3];
+            if (mode == 0) w.vpMP[p]->GetWorldPos(X);
+            else std::memcpy(X, w.vpMP[p]->mPosGBA, sizeof(X));
+            const double n = std::sqrt(x[3 * p] * x[3 * p] + x[3 * p + 1] * x[3 * p + 1] + x[3 * p + 2] * x[3 * p + 2]);
+            for (int j = 0; j < 3; j++) worst = std::max(worst, std::fabs((double)X[j] - x[3 * p + j]) / std::max(n, 1e-9));
+        }
+        CHECK(worst <= 1e-4, "global BA (mode %d) vs oracle: worst rel %.3g", mode, worst);
+    }
+}
+
 static void testBoW() {
     // a 3-level, 6-ary vocabulary written in the reference's text format, loaded by ORBVocabulary, then
     // KeyFrame::ComputeBoW vs the oracle's BowVector / FeatureVector on the same arrays
@@ -857,6 +891,7 @@ int main(int argc, char** argv) {
         testFuse();
         testBoW();
         testMergeBA();
+        testGlobalBA();
     }
     std::printf("OK %d checks (%s)\n", g_checks, mode.c_str());
     return 0;
