@@ -69,6 +69,7 @@ struct Dev {
     double* err;                 // [E][2]
     double* jac;                 // [E][21]: A(6) B(12) orr(2) wo(1)
     double* rho0;                // [E]
+    double* part;                // [ceil(E / 256)] rho0 partial sums of k_linearize's blocks
     double* hpl;                 // [E][18] H_pl pose x landmark
     double* bdinv;               // [E][18] H_pl D^-1
     double* coef;                // [E][6]  H_pl D^-1 b_l
@@ -108,10 +109,8 @@ __device__ __forceinline__ void huber(double e, double delta, double* r0, double
     }
 }
 
-// ---- per edge: error, robust weight, Jacobians (EdgeSE3ProjectXYZ)
-__global__ __launch_bounds__(256) void k_linearize(Dev d, int want_jac) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= d.E) return;
+// ---- per edge: error, robust weight, Jacobians (EdgeSE3ProjectXYZ); returns the edge's rho0
+__device__ __forceinline__ double linearize_edge(const Dev& d, int e, int want_jac) {
     const int ip = d.edge_point[e] , ipose = d.edge_pose[e];
     const double* T = d.pose + 7 * (size_t)ipose;
     const double* X = d.pt + 3 * (size_t)ip;
@@ -133,14 +132,14 @@ __global__ __launch_bounds__(256) void k_linearize(Dev d, int want_jac) {
             if (d.pose_h[ipose] >= 0)
                 for (int k = 0; k < 18; k++) d.hpl[18 * (size_t)e + k] = 0.0;
         }
-        return;
+        return 0.0;
     }
     const double w = d.edge_w[e];
     const double chi = e0 * (w * e0) + e1 * (w * e1);
     double r0, r1;
     huber(chi, d.delta, &r0, &r1);
     d.rho0[e] = r0;
-    if (!want_jac) return;
+    if (!want_jac) return r0;
     const double x = Xc[0], y = Xc[1], z = Xc[2];
     const double J0 = -(fx / z), J2 = -(-fx * x / (z * z)), J4 = -(fy / z), J5 = -(-fy * y / (z * z));
     // rotation matrix of T (Eigen toRotationMatrix)
@@ -169,6 +168,20 @@ __global__ __launch_bounds__(256) void k_linearize(Dev d, int want_jac) {
         for (int a = 0; a < 6; a++)
             for (int c = 0; c < 3; c++) hp[3 * a + c] = o[6 + a] * wo * o[c] + o[12 + a] * wo * o[3 + c];
     }
+    return r0;
+}
+
+// Per block of 256 edges: the rho0 partial sum in a fixed order (butterfly per wave, then the 4 waves in order), so
+// the chi2 reduction is one short pass over the partials
+__global__ __launch_bounds__(256) void k_linearize(Dev d, int want_jac) {
+    __shared__ double ws[4];
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    double r = e < d.E ? linearize_edge(d, e, want_jac) : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) d.part[blockIdx.x] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
 }
 
 // ---- per point: H_ll, b_l (edge order, as constructQuadraticForm runs edge by edge)
@@ -228,30 +241,37 @@ __global__ __launch_bounds__(64) void k_pose_sys(Dev d) {
     }
 }
 
-// ---- fixed-order sum of rho0 (and max diag) in one workgroup
-__global__ __launch_bounds__(1024) void k_reduce_chi(Dev d, int slot) {
-    __shared__ double s[1024];
+// ---- fixed-order sum of rho0 (and max diag) in one workgroup. RED threads: a small workgroup finds room on a CU
+// that Tracking's concurrent launches keep busy (a 1024-thread one waits for 16 free wave slots at once).
+#ifndef MAM_LBA_RED_THREADS
+#define MAM_LBA_RED_THREADS 256
+#endif
+constexpr int RED = MAM_LBA_RED_THREADS;
+
+__global__ __launch_bounds__(RED) void k_reduce_chi(Dev d, int slot) {
+    __shared__ double s[RED];
     const int t = threadIdx.x;
     double acc = 0.0;
-    for (int e = t; e < d.E; e += 1024) acc += d.rho0[e];
+    const int nb = (d.E + 255) / 256;
+    for (int b = t; b < nb; b += RED) acc += d.part[b];
     s[t] = acc;
     __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
+    for (int o = RED / 2; o > 0; o >>= 1) {
         if (t < o) s[t] += s[t + o];
         __syncthreads();
     }
     if (t == 0) d.red[slot] = s[0];
 }
 
-__global__ __launch_bounds__(1024) void k_max_diag(Dev d) {
-    __shared__ double s[1024];
+__global__ __launch_bounds__(RED) void k_max_diag(Dev d) {
+    __shared__ double s[RED];
     const int t = threadIdx.x;
     double m = 0.0;
-    for (int i = t; i < 6 * d.Np; i += 1024) m = fmax(m, fabs(d.Hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
-    for (int i = t; i < 3 * d.L; i += 1024) m = fmax(m, fabs(d.Hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
+    for (int i = t; i < 6 * d.Np; i += RED) m = fmax(m, fabs(d.Hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
+    for (int i = t; i < 3 * d.L; i += RED) m = fmax(m, fabs(d.Hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
     s[t] = m;
     __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
+    for (int o = RED / 2; o > 0; o >>= 1) {
         if (t < o) s[t] = fmax(s[t], s[t + o]);
         __syncthreads();
     }
@@ -370,7 +390,7 @@ __global__ __launch_bounds__(64) void k_schur_rhs(Dev d) {
 // The workspace (panel + y) is LDS when it fits (use_lds), else a global scratch buffer.
 constexpr int NB = 16;
 #ifndef MAM_LDLT_THREADS
-#define MAM_LDLT_THREADS 1024
+#define MAM_LDLT_THREADS 512
 #endif
 constexpr int LDLT_THREADS = MAM_LDLT_THREADS;   // 16 waves: 4 per SIMD hide the MFMA / memory latency
 
@@ -685,15 +705,15 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
 }
 
 // sum_j x_j (lambda x_j + b_j) in fixed order (computeScale)
-__global__ __launch_bounds__(1024) void k_scale(Dev d, double lambda) {
-    __shared__ double s[1024];
+__global__ __launch_bounds__(RED) void k_scale(Dev d, double lambda) {
+    __shared__ double s[RED];
     const int t = threadIdx.x;
     const int n = 6 * d.Np + 3 * d.L;
     double acc = 0.0;
-    for (int j = t; j < n; j += 1024) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
+    for (int j = t; j < n; j += RED) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
     s[t] = acc;
     __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
+    for (int o = RED / 2; o > 0; o >>= 1) {
         if (t < o) s[t] += s[t + o];
         __syncthreads();
     }
@@ -868,7 +888,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
                    sz<double>(6 * (size_t)E) + sz<double>(36 * (size_t)Np) + sz<double>(9 * (size_t)L) + sz<double>(nx) +
                    sz<double>(9 * (size_t)L) + sz<double>((size_t)npad * npad) + sz<double>(nx) + sz<double>(npad) + sz<double>(8) +
                    sz<double>(mam::lba::ldlt_ws_doubles(npad)) +
-                   sz<int>(4) + sz<uint8_t>(E) * 2 + 4096;
+                   sz<int>(4) + sz<uint8_t>(E) * 2 + sz<double>((size_t)(E + 255) / 256 + 1) + 4096;
     if (int rc = c->arena.alloc(bytes)) return rc;
     if (int rc = c->staging.alloc(bytes)) return rc;
     Carver cv{c->arena.p};
@@ -928,6 +948,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     d.err = cv.take<double>(2 * (size_t)E);
     d.jac = cv.take<double>(21 * (size_t)E);
     d.rho0 = cv.take<double>(E);
+    d.part = cv.take<double>((size_t)(E + 255) / 256 + 1);
     d.hpl = cv.take<double>(18 * (size_t)E);
     d.bdinv = cv.take<double>(18 * (size_t)E);
     d.coef = cv.take<double>(6 * (size_t)E);
@@ -956,7 +977,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     auto chi_of = [&](const double* pose, const double* pt, bool jac, double* out_chi) -> int {
         state(pose, pt, tr_pose, tr_pt);
         if (E > 0) hipLaunchKernelGGL(mam::lba::k_linearize, dim3(gE), dim3(256), 0, s, d, jac ? 1 : 0);
-        hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(1024), 0, s, d, 0);
+        hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(mam::lba::RED), 0, s, d, 0);
         MAM_HIP(hipMemcpyAsync(h_red, d.red, sizeof(double), hipMemcpyDeviceToHost, s));
         MAM_HIP(hipStreamSynchronize(s));
         *out_chi = h_red[0];
@@ -976,10 +997,10 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
             mam::StageTimer::Scope sc(&c->timer, s, 0);
             state(cur_pose, cur_pt, tr_pose, tr_pt);
             if (E > 0) hipLaunchKernelGGL(mam::lba::k_linearize, dim3(gE), dim3(256), 0, s, d, 1);
-            hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(1024), 0, s, d, 0);
+            hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(mam::lba::RED), 0, s, d, 0);
             if (L > 0) hipLaunchKernelGGL(mam::lba::k_point_sys, dim3((L + 63) / 64), dim3(64), 0, s, d);
             if (Np > 0) hipLaunchKernelGGL(mam::lba::k_pose_sys, dim3(Np), dim3(64), 0, s, d);
-            hipLaunchKernelGGL(mam::lba::k_max_diag, dim3(1), dim3(1024), 0, s, d);
+            hipLaunchKernelGGL(mam::lba::k_max_diag, dim3(1), dim3(mam::lba::RED), 0, s, d);
         }
         if (it == 0) {
             // lambda init needs max diag(H); afterwards the iteration-start chi2 is, bit for bit, the chi2 of the
@@ -1025,8 +1046,8 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
                 // chi2 of the trial state (errors kept: chi2() reads the last computeActiveErrors)
                 state(tr_pose, tr_pt, tr_pose, tr_pt);
                 if (E > 0) hipLaunchKernelGGL(mam::lba::k_linearize, dim3(gE), dim3(256), 0, s, d, 0);
-                hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(1024), 0, s, d, 0);
-                hipLaunchKernelGGL(mam::lba::k_scale, dim3(1), dim3(1024), 0, s, d, currentLambda);
+                hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(mam::lba::RED), 0, s, d, 0);
+                hipLaunchKernelGGL(mam::lba::k_scale, dim3(1), dim3(mam::lba::RED), 0, s, d, currentLambda);
             }
             int fail = 0;
             MAM_HIP(hipMemcpyAsync(h_red, d.red, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
