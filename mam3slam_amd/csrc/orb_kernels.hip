@@ -424,25 +424,27 @@ __device__ __forceinline__ half2_t fast_px(const half2_t* E) {
 }
 template <int CW>
 __device__ __forceinline__ half2_t fast_strength_h2(const half2_t* hp, int r, int pc) {
+    // On the circle samples p_k themselves (no per-sample difference): min over an arc of (v - p) is v - max over the
+    // arc of p, so S = max(v - min_k arcmax_p[k], max_k arcmin_p[k] - v). Exact in f16 (integers <= 255).
     const half2_t* E = hp + r * 2 * CW + pc;
     const half2_t v = fast_px<CW, 0, 0>(E);
     half2_t d[16];
-    d[0] = v - fast_px<CW, 3, 0>(E);
-    d[1] = v - fast_px<CW, 3, 1>(E);
-    d[2] = v - fast_px<CW, 2, 2>(E);
-    d[3] = v - fast_px<CW, 1, 3>(E);
-    d[4] = v - fast_px<CW, 0, 3>(E);
-    d[5] = v - fast_px<CW, -1, 3>(E);
-    d[6] = v - fast_px<CW, -2, 2>(E);
-    d[7] = v - fast_px<CW, -3, 1>(E);
-    d[8] = v - fast_px<CW, -3, 0>(E);
-    d[9] = v - fast_px<CW, -3, -1>(E);
-    d[10] = v - fast_px<CW, -2, -2>(E);
-    d[11] = v - fast_px<CW, -1, -3>(E);
-    d[12] = v - fast_px<CW, 0, -3>(E);
-    d[13] = v - fast_px<CW, 1, -3>(E);
-    d[14] = v - fast_px<CW, 2, -2>(E);
-    d[15] = v - fast_px<CW, 3, -1>(E);
+    d[0] = fast_px<CW, 3, 0>(E);
+    d[1] = fast_px<CW, 3, 1>(E);
+    d[2] = fast_px<CW, 2, 2>(E);
+    d[3] = fast_px<CW, 1, 3>(E);
+    d[4] = fast_px<CW, 0, 3>(E);
+    d[5] = fast_px<CW, -1, 3>(E);
+    d[6] = fast_px<CW, -2, 2>(E);
+    d[7] = fast_px<CW, -3, 1>(E);
+    d[8] = fast_px<CW, -3, 0>(E);
+    d[9] = fast_px<CW, -3, -1>(E);
+    d[10] = fast_px<CW, -2, -2>(E);
+    d[11] = fast_px<CW, -1, -3>(E);
+    d[12] = fast_px<CW, 0, -3>(E);
+    d[13] = fast_px<CW, 1, -3>(E);
+    d[14] = fast_px<CW, 2, -2>(E);
+    d[15] = fast_px<CW, 3, -1>(E);
     half2_t mn3[16], mx3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -455,15 +457,15 @@ __device__ __forceinline__ half2_t fast_strength_h2(const half2_t* hp, int r, in
         arcmin[k] = hmin3(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]);
         arcmax[k] = hmax3(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]);
     }
-    half2_t A = hmax3(arcmin[0], arcmin[1], arcmin[2]), Bm = hmin3(arcmax[0], arcmax[1], arcmax[2]);
+    half2_t Bmax = hmax3(arcmin[0], arcmin[1], arcmin[2]), Amin = hmin3(arcmax[0], arcmax[1], arcmax[2]);
 #pragma unroll
     for (int k = 3; k < 15; k += 2) {
-        A = hmax3(A, arcmin[k], arcmin[k + 1]);
-        Bm = hmin3(Bm, arcmax[k], arcmax[k + 1]);
+        Bmax = hmax3(Bmax, arcmin[k], arcmin[k + 1]);
+        Amin = hmin3(Amin, arcmax[k], arcmax[k + 1]);
     }
-    A = __builtin_elementwise_maximum(A, arcmin[15]);
-    Bm = __builtin_elementwise_minimum(Bm, arcmax[15]);
-    return __builtin_elementwise_maximum(A, -Bm);
+    Bmax = __builtin_elementwise_maximum(Bmax, arcmin[15]);
+    Amin = __builtin_elementwise_minimum(Amin, arcmax[15]);
+    return __builtin_elementwise_maximum(v - Amin, Bmax - v);
 }
 
 // One workgroup (FAST_THREADS) per cell, everything on pixel pairs (two horizontally adjacent pixels per lane):
@@ -519,20 +521,16 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
             const uint8_t* pr = src + (size_t)r * pitch + 4 * q;
             uint32_t w4;
             __builtin_memcpy(&w4, pr, 4);
-            const uint32_t b4 = pr[4];
-            _Float16 v[5];
-#pragma unroll
-            for (int k = 0; k < 4; k++) v[k] = (_Float16)(int)((w4 >> (8 * k)) & 0xFF);
-            v[4] = (_Float16)(int)b4;
-            half2_t* dE = hp + r * 2 * CW + 2 * q;
-            half2_t* dO = dE + CW;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                half2_t h;
-                h.x = v[k];
-                h.y = v[k + 1];
-                ((k & 1) ? dO : dE)[k >> 1] = h;
-            }
+            // byte b as the f16 0x64bb = 1024 + b (exact; the common offset cancels in every difference S takes):
+            // one v_perm_b32 per pixel pair instead of per-byte conversions
+            const uint32_t b4x = (uint32_t)pr[4] | 0x64646400u;
+            constexpr uint32_t K64 = 0x64646464u;
+            uint32_t* dE = reinterpret_cast<uint32_t*>(hp + r * 2 * CW + 2 * q);
+            uint32_t* dO = dE + CW;
+            dE[0] = __builtin_amdgcn_perm(K64, w4, 0x04010400u);   // (b0, b1)
+            dO[0] = __builtin_amdgcn_perm(K64, w4, 0x04020401u);   // (b1, b2)
+            dE[1] = __builtin_amdgcn_perm(K64, w4, 0x04030402u);   // (b2, b3)
+            dO[1] = __builtin_amdgcn_perm(b4x, w4, 0x05040503u);   // (b3, b4)
             r += dq;
             q += dr;
             if (q >= qc) { q -= qc; r++; }
