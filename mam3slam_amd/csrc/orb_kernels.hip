@@ -643,6 +643,11 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
 }
 
 // ------------------------------------------------------------------------------------------------ blur
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 u16_pair(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, sel));
+}
+
 __device__ __forceinline__ int refl101(int p, int n) {
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
     return p;
@@ -706,22 +711,20 @@ __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, Level
         const uint32_t wa = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q]);
         const uint32_t wb = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 4]);
         const uint32_t wc = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 8]);
-        int p[12];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            p[k] = (wa >> (8 * k)) & 0xFF;
-            p[4 + k] = (wb >> (8 * k)) & 0xFF;
-            p[8 + k] = (wc >> (8 * k)) & 0xFF;
-        }
-        uint32_t o[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int* pp = p + k + 1;
-            o[k] = GT0 * (pp[0] + pp[6]) + GT1 * (pp[1] + pp[5]) + GT2 * (pp[2] + pp[4]) + GT3 * pp[3];
-        }
+        // two outputs per packed u16 op: P_j = (p_j, p_j+1) by one v_perm_b32 each (selector 0x0c = a zero byte);
+        // every partial sum stays <= 255 * 256 (fits 16 bits exactly)
+        const u16x2 P1 = u16_pair(0u, wa, 0x0c020c01u), P2 = u16_pair(0u, wa, 0x0c030c02u);
+        const u16x2 P3 = u16_pair(wb, wa, 0x0c040c03u), P4 = u16_pair(0u, wb, 0x0c010c00u);
+        const u16x2 P5 = u16_pair(0u, wb, 0x0c020c01u), P6 = u16_pair(0u, wb, 0x0c030c02u);
+        const u16x2 P7 = u16_pair(wc, wb, 0x0c040c03u), P8 = u16_pair(0u, wc, 0x0c010c00u);
+        const u16x2 P9 = u16_pair(0u, wc, 0x0c020c01u);
+        const u16x2 c0 = (u16x2)(unsigned short)GT0, c1 = (u16x2)(unsigned short)GT1;
+        const u16x2 c2 = (u16x2)(unsigned short)GT2, c3 = (u16x2)(unsigned short)GT3;
+        const u16x2 o01 = c0 * (P1 + P7) + c1 * (P2 + P6) + c2 * (P3 + P5) + c3 * P4;
+        const u16x2 o23 = c0 * (P3 + P9) + c1 * (P4 + P8) + c2 * (P5 + P7) + c3 * P6;
         uint2 packed;
-        packed.x = o[0] | (o[1] << 16);
-        packed.y = o[2] | (o[3] << 16);
+        packed.x = __builtin_bit_cast(uint32_t, o01);
+        packed.y = __builtin_bit_cast(uint32_t, o23);
         *reinterpret_cast<uint2*>(&th_[r][4 * q]) = packed;
     }
     __syncthreads();
