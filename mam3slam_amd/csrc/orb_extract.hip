@@ -387,7 +387,7 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
     }
     const size_t cand = (size_t)Fcap * g.cand_per_frame;
     if (int rc = c->d_pyr.alloc(std::max<long long>(pyr, 64))) return rc;
-    if (int rc = c->d_blur.alloc(blur)) return rc;
+    if (int rc = c->d_blur.alloc(blur + 64)) return rc;   // k_describe's patch prefetch reads up to 3 bytes past a row
     if (int rc = c->d_cand.alloc(cand)) return rc;
     if (int rc = c->d_keys.alloc(cand)) return rc;
     if (int rc = c->d_knode.alloc(cand)) return rc;

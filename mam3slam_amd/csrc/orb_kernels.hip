@@ -1165,6 +1165,11 @@ __global__ __launch_bounds__(256) void k_distribute(const Geom* __restrict__ g, 
 }
 
 // ------------------------------------------------------------------------------------------------ describe
+constexpr int DESC_R = 18;                          // max |rotated pattern offset| (rounded)
+constexpr int DESC_ROWS = 2 * DESC_R + 1;            // 37 patch rows
+constexpr int DESC_WPR = 10;                         // words per patch row: 37 bytes + up to 3 bytes of alignment
+constexpr int DESC_NW = (DESC_ROWS * DESC_WPR + 63) / 64;   // words per lane
+
 __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, LevelSrc s,
                                                   const uint8_t* __restrict__ blur,
                                                   const uint32_t* __restrict__ out_key,
@@ -1212,6 +1217,25 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, Le
     // v in [-vmax, 0], lanes 32..62 take v in [1, vmax]; integer sums are order-independent
     // all 16 loads of a lane's column in flight at once (a v-loop would wait out one global latency per pixel);
     // umax is non-increasing, so vmax(u) = #{v in 1..15 : umax[v] >= |u|}
+    // the blurred patch the rBRIEF tests sample (rotated pattern offsets: |offset| <= 13 (|cos| + |sin|) <= 18.4, so
+    // rows y-18..y+18 and columns x-18..x+18), fetched into this wave's LDS slot in the same round trip as the IC
+    // loads, before the angle is known; rows as DESC_WPR aligned words from the word holding column x-18
+    const uint8_t* bl = blur + L.blur_off + (size_t)f * L.frame_bytes;
+    const int bpitch = L.pitch;
+    __shared__ uint32_t bpatch[4][DESC_ROWS * DESC_WPR];
+    uint32_t* patch = bpatch[(threadIdx.x >> 6) & 3];
+    const uintptr_t row0 = (uintptr_t)(bl + (size_t)(y - DESC_R) * bpitch + (x - DESC_R));
+    const int shift = (int)(row0 & 3);   // byte offset of column x-18 in the first word of each row
+    uint32_t pw[DESC_NW];
+    {
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(row0 - (uintptr_t)shift);
+#pragma unroll
+        for (int k = 0; k < DESC_NW; k++) {
+            const int i = k * 64 + lane;
+            const int rr = i / DESC_WPR, c = i - rr * DESC_WPR;
+            pw[k] = i < DESC_ROWS * DESC_WPR ? *reinterpret_cast<const uint32_t*>(base + (size_t)rr * bpitch + 4 * c) : 0u;
+        }
+    }
     int m10 = 0, m01 = 0;
     {
         const int col = lane & 31;
@@ -1242,9 +1266,16 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, Le
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float a, b;
     det_sincos(angle * factorPI, &b, &a);
-    const uint8_t* bl = blur + L.blur_off + (size_t)f * L.frame_bytes;
-    const int bpitch = L.pitch;
-    const uint8_t* bc = bl + (size_t)y * bpitch + x;
+#pragma unroll
+    for (int k = 0; k < DESC_NW; k++) {
+        const int i = k * 64 + lane;
+        if (i < DESC_ROWS * DESC_WPR) patch[i] = pw[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // pixel (y + dy, x + dx) = patch byte (dy + 18) * 4 * DESC_WPR + shift + dx + 18
+    const uint8_t* pc = reinterpret_cast<const uint8_t*>(patch) + DESC_R * 4 * DESC_WPR + shift + DESC_R;
     uint64_t words[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1264,7 +1295,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, Le
                 const float t2 = px * a, t3 = py * b;
                 fx = t2 - t3;
             }
-            val[e] = bc[__float2int_rn(fy) * bpitch + __float2int_rn(fx)];
+            val[e] = pc[__float2int_rn(fy) * (4 * DESC_WPR) + __float2int_rn(fx)];
         }
         words[k] = __ballot(val[0] < val[1]);
     }
