@@ -144,12 +144,16 @@ __device__ __forceinline__ void pyr_pair(uint32_t w0, uint32_t w1, uint32_t w2, 
 // Four output pixels of one output row from source rows S0 (ry0) and S1 (ry1) (word-aligned row starts): exact-int
 // horizontal pass (HResizeLinear), vertical pass with VResizeLinearVec_32s8u's mulhi formula for x < xvec and
 // FixedPtCast<int,uchar,22> beyond. Three word loads per source row.
+// nw: words in a source row; the words past it are read as 0 (only zero-weight edge columns reach them), so the
+// last row of the caller's last frame is never read past
 __device__ __forceinline__ uint32_t pyr_quad(const uint8_t* S0, const uint8_t* S1, const PyrQuad& c, int b0,
-                                             int b1) {
+                                             int b1, int nw = 1 << 30) {
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(S0 + c.base);
     const uint32_t* r1 = reinterpret_cast<const uint32_t*>(S1 + c.base);
-    const uint32_t x0 = r0[0], x1 = r0[1], x2 = r0[2];
-    const uint32_t y0 = r1[0], y1 = r1[1], y2 = r1[2];
+    const int wq = c.base >> 2;
+    const bool h1 = wq + 1 < nw, h2 = wq + 2 < nw;
+    const uint32_t x0 = r0[0], x1 = h1 ? r0[1] : 0u, x2 = h2 ? r0[2] : 0u;
+    const uint32_t y0 = r1[0], y1 = h1 ? r1[1] : 0u, y2 = h2 ? r1[2] : 0u;
     uint32_t packed = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(256) void k_pyr_flat(const Geom* __restrict__ g, in
     int spitch;
     const uint8_t* src = level_ptr(g, s, f, l - 1, &spitch);
     const uint32_t packed = pyr_quad(src + (size_t)ry0 * spitch, src + (size_t)ry1 * spitch, cq,
-                                     (int)(short)(rc.y & 0xFFFF), rc.y >> 16);
+                                     (int)(short)(rc.y & 0xFFFF), rc.y >> 16, (g->L[l - 1].w + 3) >> 2);
     uint8_t* o = pyr + L.pyr_off + (size_t)f * L.frame_bytes + (size_t)dy * L.pitch + 4 * q;
     if (4 * q + 4 <= L.w) {
         *reinterpret_cast<uint32_t*>(o) = packed;

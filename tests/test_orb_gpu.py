@@ -153,3 +153,30 @@ def test_batch_pyramid_levels(gpu_lib, oracle, w, h, nfeat):
             assert d is None, f"frame {i} level {l} pixel {d}"
             d = _first_diff(ext.debug_blurred(l, i), oracle.gaussian7(lev))
             assert d is None, f"frame {i} blurred level {l} pixel {d}"
+
+
+def test_batch_input_ends_at_last_row(gpu_lib, oracle):
+    """The caller's frames end exactly at the last row of the last frame (a 2 MiB-multiple device allocation with no
+    allocator slack): the word-wise level-0 reads of the batched resize must stay inside it (k_pyr_flat reads whole
+    source words; the words past a row are zero-weight edge columns). 4 frames of 1024 x 512 = exactly 2 MiB."""
+    import torch
+
+    w, h, F = 1024, 512, 4
+    ext = _extractor(1000)
+    imgs = np.stack([synth.make_frame(w, h, agent=8, frame=i) for i in range(F)])
+    cap = ext.max_keypoints()
+    d_img = torch.empty(F * w * h, dtype=torch.uint8, device="cuda")
+    assert d_img.untyped_storage().nbytes() == 2 * 1024 * 1024
+    d_img.copy_(torch.from_numpy(imgs.reshape(-1)))
+    d_kps = torch.zeros((F, cap * 28), dtype=torch.uint8, device="cuda")
+    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.zeros((F, 2), dtype=torch.int32, device="cuda")
+    ext.extract_batch_device(d_img.data_ptr(), F, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                             d_cnt.data_ptr())
+    torch.cuda.synchronize()
+    levels = oracle.pyramid(imgs[F - 1], oracle.params(1000))
+    for l, lev in enumerate(levels):
+        assert _first_diff(ext.level(l, F - 1), lev) is None, f"level {l}"
+    ko, do, _ = oracle.extract(imgs[F - 1], oracle.params(1000))
+    n = int(d_cnt[F - 1, 0])
+    assert n == len(ko) and np.array_equal(d_desc[F - 1, :n].cpu().numpy(), do)
