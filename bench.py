@@ -40,7 +40,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 # what actually limits each stage: the byte/integer path has no MFMA work and most stages issue far
 # more VALU work per byte than the HBM roofline can see
 ROOFLINE_NOTES = {
-    "fast": "VALU issue: FAST-9 strength is ~100 packed-f16 min3/max3/sub ops per pixel pair (DESIGN.md §3)",
+    "fast": "VALU issue: FAST-9 strength is ~85 packed-f16 min3/max3 ops per pixel pair (DESIGN.md §3)",
     "pyramid": "LDS-staged bilinear resize, latency-bound at 8 small launches",
     "describe": "one wave per keypoint: LDS-free gathers from the blurred level (latency)",
     "resolve": "one workgroup per frame, greedy dependency rounds (latency, LDS atomics)",
