@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) void k_pyr_bands(const Geom* __restrict__ g, L
 // Two horizontally adjacent pixels per lane in packed fp16 (every difference of two bytes, -255..255, is exact in
 // fp16): the ROI is staged as pixel pairs (p[c], p[c+1]), so one 32-bit LDS read gives a circle sample for both
 // pixels, and the arc minima / maxima use gfx950's 3-input packed v_pk_minimum3_f16 / v_pk_maximum3_f16:
-// m3[k] = min(d[k..k+2]), arc[k] = min(m3[k], m3[k+3], m3[k+6]).
+// arcs pairwise: max(arcmin[2i], arcmin[2i+1]) = min3(Q[2i+1], Q[2i+5], max(d[2i], d[2i+9])), Q = min of 4 samples.
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
@@ -449,26 +449,31 @@ __device__ __forceinline__ half2_t fast_strength_h2(const half2_t* hp, int r, in
     d[13] = fast_px<CW, 1, -3>(E);
     d[14] = fast_px<CW, 2, -2>(E);
     d[15] = fast_px<CW, 3, -1>(E);
-    half2_t mn3[16], mx3[16];
+    // The arcs starting at 2i and 2i+1 share the 8 samples 2i+1 .. 2i+8 (min M8 = min(Q[2i+1], Q[2i+5]) with Q[j] =
+    // min of d[j .. j+3]), so max(arcmin[2i], arcmin[2i+1]) = min3(Q[2i+1], Q[2i+5], max(d[2i], d[2i+9])): eight
+    // 3-input ops per direction instead of 32 for the sixteen arcs. Q at the odd starts from the four pair minima
+    // P = min(d[4m+3], d[4m+4]): Q[4m+1] = min3(d[4m+1], d[4m+2], P[m]), Q[4m+3] = min3(P[m], d[4m+5], d[4m+6]).
+    half2_t qn[8], qx[8];   // qn[i] = Q[2i+1] (min), qx[i] = the same window's max
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn3[k] = hmin3(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
-        mx3[k] = hmax3(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+    for (int m = 0; m < 4; m++) {
+        const half2_t pn = __builtin_elementwise_minimum(d[(4 * m + 3) & 15], d[(4 * m + 4) & 15]);
+        const half2_t px = __builtin_elementwise_maximum(d[(4 * m + 3) & 15], d[(4 * m + 4) & 15]);
+        qn[2 * m] = hmin3(d[4 * m + 1], d[4 * m + 2], pn);
+        qx[2 * m] = hmax3(d[4 * m + 1], d[4 * m + 2], px);
+        qn[2 * m + 1] = hmin3(pn, d[(4 * m + 5) & 15], d[(4 * m + 6) & 15]);
+        qx[2 * m + 1] = hmax3(px, d[(4 * m + 5) & 15], d[(4 * m + 6) & 15]);
     }
-    half2_t arcmin[16], arcmax[16];
+    half2_t vb[8], va[8];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        arcmin[k] = hmin3(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]);
-        arcmax[k] = hmax3(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]);
+    for (int i = 0; i < 8; i++) {
+        const half2_t a = d[2 * i], b = d[(2 * i + 9) & 15];
+        vb[i] = hmin3(qn[i], qn[(i + 2) & 7], __builtin_elementwise_maximum(a, b));
+        va[i] = hmax3(qx[i], qx[(i + 2) & 7], __builtin_elementwise_minimum(a, b));
     }
-    half2_t Bmax = hmax3(arcmin[0], arcmin[1], arcmin[2]), Amin = hmin3(arcmax[0], arcmax[1], arcmax[2]);
-#pragma unroll
-    for (int k = 3; k < 15; k += 2) {
-        Bmax = hmax3(Bmax, arcmin[k], arcmin[k + 1]);
-        Amin = hmin3(Amin, arcmax[k], arcmax[k + 1]);
-    }
-    Bmax = __builtin_elementwise_maximum(Bmax, arcmin[15]);
-    Amin = __builtin_elementwise_minimum(Amin, arcmax[15]);
+    const half2_t Bmax = __builtin_elementwise_maximum(hmax3(vb[0], vb[1], vb[2]),
+                                                       hmax3(vb[3], vb[4], hmax3(vb[5], vb[6], vb[7])));
+    const half2_t Amin = __builtin_elementwise_minimum(hmin3(va[0], va[1], va[2]),
+                                                       hmin3(va[3], va[4], hmin3(va[5], va[6], va[7])));
     return __builtin_elementwise_maximum(v - Amin, Bmax - v);
 }
 
@@ -481,7 +486,7 @@ __device__ __forceinline__ half2_t fast_strength_h2(const half2_t* hp, int r, in
 //     at both thresholds by ballot;
 // (d) iniThFAST if any P > iniTh, else minThFAST; every wave reads all count entries with broadcast LDS reads;
 // (e) corners written in row-major order (pair order = pixel order) at ballot prefix positions.
-// The whole kernel is VALU-bound (S is ~100 packed f16 ops per pixel pair); see DESIGN.md.
+// The whole kernel is VALU-bound (S is ~70 packed f16 ops per pixel pair); see DESIGN.md.
 template <int CW>
 __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restrict__ g,
                                                              const CellDesc* __restrict__ cells, LevelSrc s,
