@@ -685,18 +685,30 @@ __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, Level
     const uint8_t* lev = level_ptr(g, s, f, l, &pitch);
     const int tid = threadIdx.x;
     const int w = L.w, h = L.h;
-    const bool words = x0 >= 4 && x0 + BLUR_TILE_W + 4 <= w && ((pitch | (int)((uintptr_t)lev & 3)) & 3) == 0;
-    if (words) {
+    // Every staged word whose 4 columns lie inside the row is one aligned 32-bit load (row reflected per word); only
+    // the words straddling or past the left/right edge reflect per byte. All loads are issued before the LDS stores.
+    const bool aligned = ((pitch | (int)((uintptr_t)lev & 3)) & 3) == 0;
+    {
         constexpr int WPR = BLUR_IN_W / 4;
         constexpr int NWORDS = BLUR_IN_H * WPR, NIT = (NWORDS + 255) / 256;
-        uint32_t v[NIT];   // every load in flight before the LDS stores
+        uint32_t v[NIT];
 #pragma unroll
         for (int k = 0; k < NIT; k++) {
             const int i = k * 256 + tid;
             const int r = i / WPR, c = i - r * WPR;
-            v[k] = i < NWORDS ? *reinterpret_cast<const uint32_t*>(lev + (size_t)refl101(y0 - 3 + r, h) * pitch + x0 -
-                                                                    4 + 4 * c)
-                              : 0u;
+            uint32_t word = 0u;
+            if (i < NWORDS) {
+                const uint8_t* row = lev + (size_t)refl101(y0 - 3 + r, h) * pitch;
+                const int gx = x0 - 4 + 4 * c;
+                if (aligned && gx >= 0 && gx + 4 <= w) {
+                    word = *reinterpret_cast<const uint32_t*>(row + gx);
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        word |= (uint32_t)row[refl101(min(gx + b, 2 * w - 2), w)] << (8 * b);
+                }
+            }
+            v[k] = word;
         }
 #pragma unroll
         for (int k = 0; k < NIT; k++) {
@@ -704,19 +716,13 @@ __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, Level
             const int r = i / WPR, c = i - r * WPR;
             if (i < NWORDS) *reinterpret_cast<uint32_t*>(&tin[r][4 * c]) = v[k];
         }
-    } else {
-        for (int i = tid; i < BLUR_IN_H * BLUR_IN_W; i += 256) {
-            const int r = i / BLUR_IN_W, c = i - r * BLUR_IN_W;
-            const int gy = refl101(y0 - 3 + r, h);
-            const int gx = refl101(min(x0 - 4 + c, 2 * w - 2), w);
-            tin[r][c] = lev[(size_t)gy * pitch + gx];
-        }
     }
     __syncthreads();
     // horizontal: output column x0+4q+k uses staged columns 4q+k+1 .. 4q+k+7
     constexpr int QPR = BLUR_TILE_W / 4;
     for (int i = tid; i < BLUR_IN_H * QPR; i += 256) {
         const int r = i / QPR, q = i - r * QPR;
+        if (x0 + 4 * q >= w) continue;   // quad past the level's right edge: no output reads it
         const uint32_t wa = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q]);
         const uint32_t wb = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 4]);
         const uint32_t wc = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 8]);
@@ -738,28 +744,37 @@ __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, Level
     }
     __syncthreads();
     uint8_t* out = blur + L.blur_off + (size_t)f * L.frame_bytes;
-    for (int i = tid; i < BLUR_TILE_H * QPR; i += 256) {
-        const int r = i / QPR, q = i - r * QPR;
-        const int y = y0 + r, x = x0 + 4 * q;
-        if (y >= h || x >= w) continue;
-        uint32_t col[7][4];
+    // vertical: thread = one 4-column quad x BLUR_VR consecutive output rows; the BLUR_VR + 6 staged u16 rows it needs
+    // are read once (sliding window) instead of 7 per output row
+    constexpr int BLUR_VR = 4;
+    static_assert(BLUR_TILE_H % BLUR_VR == 0, "row groups");
+    for (int i = tid; i < (BLUR_TILE_H / BLUR_VR) * QPR; i += 256) {
+        const int rg = i / QPR, q = i - rg * QPR;
+        const int r = rg * BLUR_VR, x = x0 + 4 * q;
+        if (y0 + r >= h || x >= w) continue;
+        uint32_t col[BLUR_VR + 6][4];
 #pragma unroll
-        for (int k = 0; k < 7; k++) {
+        for (int k = 0; k < BLUR_VR + 6; k++) {
             const uint2 v = *reinterpret_cast<const uint2*>(&th_[r + k][4 * q]);
             col[k][0] = v.x & 0xFFFF; col[k][1] = v.x >> 16; col[k][2] = v.y & 0xFFFF; col[k][3] = v.y >> 16;
         }
-        uint32_t packed = 0;
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const uint32_t sum = GT0 * (col[0][c] + col[6][c]) + GT1 * (col[1][c] + col[5][c]) +
-                                 GT2 * (col[2][c] + col[4][c]) + GT3 * col[3][c];
-            const uint32_t v = (sum + 32768u) >> 16;
-            packed |= (v > 255u ? 255u : v) << (8 * c);
+        for (int rr = 0; rr < BLUR_VR; rr++) {
+            const int y = y0 + r + rr;
+            if (y >= h) break;
+            uint32_t packed = 0;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t sum = GT0 * (col[rr][c] + col[rr + 6][c]) + GT1 * (col[rr + 1][c] + col[rr + 5][c]) +
+                                     GT2 * (col[rr + 2][c] + col[rr + 4][c]) + GT3 * col[rr + 3][c];
+                const uint32_t v = (sum + 32768u) >> 16;
+                packed |= (v > 255u ? 255u : v) << (8 * c);
+            }
+            uint8_t* o = out + (size_t)y * L.pitch + x;
+            if (x + 4 <= w) *reinterpret_cast<uint32_t*>(o) = packed;
+            else
+                for (int c = 0; c < 4 && x + c < w; c++) o[c] = (uint8_t)(packed >> (8 * c));
         }
-        uint8_t* o = out + (size_t)y * L.pitch + x;
-        if (x + 4 <= w) *reinterpret_cast<uint32_t*>(o) = packed;
-        else
-            for (int c = 0; c < 4 && x + c < w; c++) o[c] = (uint8_t)(packed >> (8 * c));
     }
 }
 
