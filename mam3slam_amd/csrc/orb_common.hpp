@@ -17,6 +17,10 @@ constexpr int PYR_XB = 1024;        // k_pyr_down output columns per workgroup (
 constexpr int PYR_RB = 8;           // k_pyr_down output rows per workgroup
 constexpr int BLUR_TILE_W = 128;   // k_blur7 output tile: 4 px per thread-quad
 constexpr int BLUR_TILE_H = 32;
+#ifndef MAM_BLUR_TPB
+#define MAM_BLUR_TPB 1
+#endif
+constexpr int BLUR_TPB = MAM_BLUR_TPB;   // k_blur7 tiles per workgroup (next tile's loads overlap this one's passes)
 
 // One pyramid level of the current frame size (all frames in a batch share it).
 struct LevelGeom {

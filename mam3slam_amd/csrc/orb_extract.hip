@@ -518,7 +518,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
     // measured no gain, so the stages stay in order on one stream)
     {
         StageScope sc(&c->timer, s, MAM_STAGE_BLUR);
-        hipLaunchKernelGGL(mam::k_blur7, dim3(g.tiles_per_frame, F), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p);
+        hipLaunchKernelGGL(mam::k_blur7, dim3((g.tiles_per_frame + mam::BLUR_TPB - 1) / mam::BLUR_TPB, F), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p);
     }
     {
         StageScope sc(&c->timer, s, MAM_STAGE_FAST);

@@ -661,6 +661,11 @@ __device__ __forceinline__ int refl101(int p, int n) {
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
     return p;
 }
+// BORDER_REFLECT_101 for -(n - 1) <= p <= 2n - 2 (one reflection), branch-free
+__device__ __forceinline__ int refl101_1(int p, int n) {
+    p = p < 0 ? -p : p;
+    return p >= n ? 2 * n - 2 - p : p;
+}
 
 // Tile of BLUR_TILE_W x BLUR_TILE_H outputs. Input staged in LDS as bytes (rows y0-3 .. y0+H+2, cols x0-4 ..
 // x0+W+3); interior tiles load aligned 32-bit words, border tiles reflect per byte (BORDER_REFLECT_101).
@@ -669,111 +674,149 @@ __device__ __forceinline__ int refl101(int p, int n) {
 constexpr int BLUR_IN_W = BLUR_TILE_W + 8;   // staged columns (x0-4 .. x0+W+3), multiple of 4
 constexpr int BLUR_IN_H = BLUR_TILE_H + 6;
 
+// Geometry of blur tile `tile` (frame-local index over every level)
+struct BlurTile {
+    const uint8_t* lev;
+    int pitch, l, x0, y0, w, h;
+    bool aligned;
+};
+__device__ __forceinline__ BlurTile blur_tile(const Geom* g, const LevelSrc& s, int f, int tile) {
+    BlurTile t;
+    t.l = 0;
+    for (int i = 1; i < g->nlevels; i++)
+        if (tile >= g->L[i].tile_base) t.l = i;
+    const LevelGeom& L = g->L[t.l];
+    tile -= L.tile_base;
+    t.x0 = (tile % L.tiles_x) * BLUR_TILE_W;
+    t.y0 = (tile / L.tiles_x) * BLUR_TILE_H;
+    t.lev = level_ptr(g, s, f, t.l, &t.pitch);
+    t.w = L.w;
+    t.h = L.h;
+    t.aligned = ((t.pitch | (int)((uintptr_t)t.lev & 3)) & 3) == 0;
+    return t;
+}
+
+constexpr int BLUR_WPR = BLUR_IN_W / 4;
+constexpr int BLUR_NWORDS = BLUR_IN_H * BLUR_WPR, BLUR_NIT = (BLUR_NWORDS + 255) / 256;
+
+// Staged words of tile t into registers. Every word whose 4 columns lie inside the row is one aligned 32-bit load
+// (row reflected per word); only the words straddling or past the left/right edge reflect per byte.
+template <bool ONE_REFL>
+__device__ __forceinline__ void blur_fetch_t(const BlurTile& t, int tid, uint32_t (&v)[BLUR_NIT]) {
+#pragma unroll
+    for (int k = 0; k < BLUR_NIT; k++) {
+        const int i = k * 256 + tid;
+        const int r = i / BLUR_WPR, c = i - r * BLUR_WPR;
+        uint32_t word = 0u;
+        if (i < BLUR_NWORDS) {
+            const int y = t.y0 - 3 + r;
+            const uint8_t* row = t.lev + (size_t)(ONE_REFL ? refl101_1(y, t.h) : refl101(y, t.h)) * t.pitch;
+            const int gx = t.x0 - 4 + 4 * c;
+            if (t.aligned && gx >= 0 && gx + 4 <= t.w) {
+                word = *reinterpret_cast<const uint32_t*>(row + gx);
+            } else {
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int x = min(gx + b, 2 * t.w - 2);
+                    word |= (uint32_t)row[ONE_REFL ? refl101_1(x, t.w) : refl101(x, t.w)] << (8 * b);
+                }
+            }
+        }
+        v[k] = word;
+    }
+}
+// Staged rows span [y0 - 3, y0 + BLUR_IN_H - 4] with y0 <= h - 1, staged columns [-4, 2w - 2] after the clamp: one
+// reflection is enough when h >= BLUR_IN_H - 2 and w >= 5 (every level of the benchmark sizes); the general loop
+// otherwise. The choice is uniform over the workgroup.
+__device__ __forceinline__ void blur_fetch(const BlurTile& t, int tid, uint32_t (&v)[BLUR_NIT]) {
+    if (t.h >= BLUR_IN_H - 2 && t.w >= 5) blur_fetch_t<true>(t, tid, v);
+    else blur_fetch_t<false>(t, tid, v);
+}
+
+// Workgroup = BLUR_TPB consecutive tiles of one frame (possibly of different levels), software-pipelined: the next
+// tile's words are loaded into registers while this tile's horizontal and vertical passes run, so the load latency
+// of a tile is hidden behind the previous one's arithmetic.
 __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ blur) {
     __shared__ __attribute__((aligned(16))) uint8_t tin[BLUR_IN_H][BLUR_IN_W];
     __shared__ __attribute__((aligned(16))) uint16_t th_[BLUR_IN_H][BLUR_TILE_W];
     const int f = blockIdx.y;
-    int tile = blockIdx.x;
-    int l = 0;
-    for (int i = 1; i < g->nlevels; i++)
-        if (tile >= g->L[i].tile_base) l = i;
-    const LevelGeom& L = g->L[l];
-    tile -= L.tile_base;
-    const int x0 = (tile % L.tiles_x) * BLUR_TILE_W;
-    const int y0 = (tile / L.tiles_x) * BLUR_TILE_H;
-    int pitch;
-    const uint8_t* lev = level_ptr(g, s, f, l, &pitch);
     const int tid = threadIdx.x;
-    const int w = L.w, h = L.h;
-    // Every staged word whose 4 columns lie inside the row is one aligned 32-bit load (row reflected per word); only
-    // the words straddling or past the left/right edge reflect per byte. All loads are issued before the LDS stores.
-    const bool aligned = ((pitch | (int)((uintptr_t)lev & 3)) & 3) == 0;
-    {
-        constexpr int WPR = BLUR_IN_W / 4;
-        constexpr int NWORDS = BLUR_IN_H * WPR, NIT = (NWORDS + 255) / 256;
-        uint32_t v[NIT];
+    const int tile0 = blockIdx.x * BLUR_TPB;
+    const int ntiles = min(BLUR_TPB, g->tiles_per_frame - tile0);
+    uint32_t v[BLUR_NIT];
+    BlurTile t = blur_tile(g, s, f, tile0);
+    blur_fetch(t, tid, v);
+    for (int j = 0; j < ntiles; j++) {
 #pragma unroll
-        for (int k = 0; k < NIT; k++) {
+        for (int k = 0; k < BLUR_NIT; k++) {
             const int i = k * 256 + tid;
-            const int r = i / WPR, c = i - r * WPR;
-            uint32_t word = 0u;
-            if (i < NWORDS) {
-                const uint8_t* row = lev + (size_t)refl101(y0 - 3 + r, h) * pitch;
-                const int gx = x0 - 4 + 4 * c;
-                if (aligned && gx >= 0 && gx + 4 <= w) {
-                    word = *reinterpret_cast<const uint32_t*>(row + gx);
-                } else {
-#pragma unroll
-                    for (int b = 0; b < 4; b++)
-                        word |= (uint32_t)row[refl101(min(gx + b, 2 * w - 2), w)] << (8 * b);
+            const int r = i / BLUR_WPR, c = i - r * BLUR_WPR;
+            if (i < BLUR_NWORDS) *reinterpret_cast<uint32_t*>(&tin[r][4 * c]) = v[k];
+        }
+        __syncthreads();   // tin complete; every thread is past the previous tile's vertical pass (th_ free)
+        const LevelGeom& L = g->L[t.l];
+        const int x0 = t.x0, y0 = t.y0, w = t.w, h = t.h;
+        if (j + 1 < ntiles) {
+            t = blur_tile(g, s, f, tile0 + j + 1);
+            blur_fetch(t, tid, v);   // in flight during this tile's passes
+        }
+        // horizontal: output column x0+4q+k uses staged columns 4q+k+1 .. 4q+k+7
+        constexpr int QPR = BLUR_TILE_W / 4;
+        for (int i = tid; i < BLUR_IN_H * QPR; i += 256) {
+            const int r = i / QPR, q = i - r * QPR;
+            if (x0 + 4 * q >= w) continue;   // quad past the level's right edge: no output reads it
+            const uint32_t wa = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q]);
+            const uint32_t wb = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 4]);
+            const uint32_t wc = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 8]);
+            // two outputs per packed u16 op: P_j = (p_j, p_j+1) by one v_perm_b32 each (selector 0x0c = a zero byte);
+            // every partial sum stays <= 255 * 256 (fits 16 bits exactly)
+            const u16x2 P1 = u16_pair(0u, wa, 0x0c020c01u), P2 = u16_pair(0u, wa, 0x0c030c02u);
+            const u16x2 P3 = u16_pair(wb, wa, 0x0c040c03u), P4 = u16_pair(0u, wb, 0x0c010c00u);
+            const u16x2 P5 = u16_pair(0u, wb, 0x0c020c01u), P6 = u16_pair(0u, wb, 0x0c030c02u);
+            const u16x2 P7 = u16_pair(wc, wb, 0x0c040c03u), P8 = u16_pair(0u, wc, 0x0c010c00u);
+            const u16x2 P9 = u16_pair(0u, wc, 0x0c020c01u);
+            const u16x2 c0 = (u16x2)(unsigned short)GT0, c1 = (u16x2)(unsigned short)GT1;
+            const u16x2 c2 = (u16x2)(unsigned short)GT2, c3 = (u16x2)(unsigned short)GT3;
+            const u16x2 o01 = c0 * (P1 + P7) + c1 * (P2 + P6) + c2 * (P3 + P5) + c3 * P4;
+            const u16x2 o23 = c0 * (P3 + P9) + c1 * (P4 + P8) + c2 * (P5 + P7) + c3 * P6;
+            uint2 packed;
+            packed.x = __builtin_bit_cast(uint32_t, o01);
+            packed.y = __builtin_bit_cast(uint32_t, o23);
+            *reinterpret_cast<uint2*>(&th_[r][4 * q]) = packed;
+        }
+        __syncthreads();
+        uint8_t* out = blur + L.blur_off + (size_t)f * L.frame_bytes;
+        // vertical: thread = one 4-column quad x BLUR_VR consecutive output rows; the BLUR_VR + 6 staged u16 rows it needs
+        // are read once (sliding window) instead of 7 per output row
+        constexpr int BLUR_VR = 4;
+        static_assert(BLUR_TILE_H % BLUR_VR == 0, "row groups");
+        for (int i = tid; i < (BLUR_TILE_H / BLUR_VR) * QPR; i += 256) {
+            const int rg = i / QPR, q = i - rg * QPR;
+            const int r = rg * BLUR_VR, x = x0 + 4 * q;
+            if (y0 + r >= h || x >= w) continue;
+            uint32_t col[BLUR_VR + 6][4];
+    #pragma unroll
+            for (int k = 0; k < BLUR_VR + 6; k++) {
+                const uint2 v = *reinterpret_cast<const uint2*>(&th_[r + k][4 * q]);
+                col[k][0] = v.x & 0xFFFF; col[k][1] = v.x >> 16; col[k][2] = v.y & 0xFFFF; col[k][3] = v.y >> 16;
+            }
+    #pragma unroll
+            for (int rr = 0; rr < BLUR_VR; rr++) {
+                const int y = y0 + r + rr;
+                if (y >= h) break;
+                uint32_t packed = 0;
+    #pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t sum = GT0 * (col[rr][c] + col[rr + 6][c]) + GT1 * (col[rr + 1][c] + col[rr + 5][c]) +
+                                         GT2 * (col[rr + 2][c] + col[rr + 4][c]) + GT3 * col[rr + 3][c];
+                    const uint32_t v = (sum + 32768u) >> 16;
+                    packed |= (v > 255u ? 255u : v) << (8 * c);
                 }
+                uint8_t* o = out + (size_t)y * L.pitch + x;
+                if (x + 4 <= w) *reinterpret_cast<uint32_t*>(o) = packed;
+                else
+                    for (int c = 0; c < 4 && x + c < w; c++) o[c] = (uint8_t)(packed >> (8 * c));
             }
-            v[k] = word;
-        }
-#pragma unroll
-        for (int k = 0; k < NIT; k++) {
-            const int i = k * 256 + tid;
-            const int r = i / WPR, c = i - r * WPR;
-            if (i < NWORDS) *reinterpret_cast<uint32_t*>(&tin[r][4 * c]) = v[k];
-        }
-    }
-    __syncthreads();
-    // horizontal: output column x0+4q+k uses staged columns 4q+k+1 .. 4q+k+7
-    constexpr int QPR = BLUR_TILE_W / 4;
-    for (int i = tid; i < BLUR_IN_H * QPR; i += 256) {
-        const int r = i / QPR, q = i - r * QPR;
-        if (x0 + 4 * q >= w) continue;   // quad past the level's right edge: no output reads it
-        const uint32_t wa = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q]);
-        const uint32_t wb = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 4]);
-        const uint32_t wc = *reinterpret_cast<const uint32_t*>(&tin[r][4 * q + 8]);
-        // two outputs per packed u16 op: P_j = (p_j, p_j+1) by one v_perm_b32 each (selector 0x0c = a zero byte);
-        // every partial sum stays <= 255 * 256 (fits 16 bits exactly)
-        const u16x2 P1 = u16_pair(0u, wa, 0x0c020c01u), P2 = u16_pair(0u, wa, 0x0c030c02u);
-        const u16x2 P3 = u16_pair(wb, wa, 0x0c040c03u), P4 = u16_pair(0u, wb, 0x0c010c00u);
-        const u16x2 P5 = u16_pair(0u, wb, 0x0c020c01u), P6 = u16_pair(0u, wb, 0x0c030c02u);
-        const u16x2 P7 = u16_pair(wc, wb, 0x0c040c03u), P8 = u16_pair(0u, wc, 0x0c010c00u);
-        const u16x2 P9 = u16_pair(0u, wc, 0x0c020c01u);
-        const u16x2 c0 = (u16x2)(unsigned short)GT0, c1 = (u16x2)(unsigned short)GT1;
-        const u16x2 c2 = (u16x2)(unsigned short)GT2, c3 = (u16x2)(unsigned short)GT3;
-        const u16x2 o01 = c0 * (P1 + P7) + c1 * (P2 + P6) + c2 * (P3 + P5) + c3 * P4;
-        const u16x2 o23 = c0 * (P3 + P9) + c1 * (P4 + P8) + c2 * (P5 + P7) + c3 * P6;
-        uint2 packed;
-        packed.x = __builtin_bit_cast(uint32_t, o01);
-        packed.y = __builtin_bit_cast(uint32_t, o23);
-        *reinterpret_cast<uint2*>(&th_[r][4 * q]) = packed;
-    }
-    __syncthreads();
-    uint8_t* out = blur + L.blur_off + (size_t)f * L.frame_bytes;
-    // vertical: thread = one 4-column quad x BLUR_VR consecutive output rows; the BLUR_VR + 6 staged u16 rows it needs
-    // are read once (sliding window) instead of 7 per output row
-    constexpr int BLUR_VR = 4;
-    static_assert(BLUR_TILE_H % BLUR_VR == 0, "row groups");
-    for (int i = tid; i < (BLUR_TILE_H / BLUR_VR) * QPR; i += 256) {
-        const int rg = i / QPR, q = i - rg * QPR;
-        const int r = rg * BLUR_VR, x = x0 + 4 * q;
-        if (y0 + r >= h || x >= w) continue;
-        uint32_t col[BLUR_VR + 6][4];
-#pragma unroll
-        for (int k = 0; k < BLUR_VR + 6; k++) {
-            const uint2 v = *reinterpret_cast<const uint2*>(&th_[r + k][4 * q]);
-            col[k][0] = v.x & 0xFFFF; col[k][1] = v.x >> 16; col[k][2] = v.y & 0xFFFF; col[k][3] = v.y >> 16;
-        }
-#pragma unroll
-        for (int rr = 0; rr < BLUR_VR; rr++) {
-            const int y = y0 + r + rr;
-            if (y >= h) break;
-            uint32_t packed = 0;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const uint32_t sum = GT0 * (col[rr][c] + col[rr + 6][c]) + GT1 * (col[rr + 1][c] + col[rr + 5][c]) +
-                                     GT2 * (col[rr + 2][c] + col[rr + 4][c]) + GT3 * col[rr + 3][c];
-                const uint32_t v = (sum + 32768u) >> 16;
-                packed |= (v > 255u ? 255u : v) << (8 * c);
-            }
-            uint8_t* o = out + (size_t)y * L.pitch + x;
-            if (x + 4 <= w) *reinterpret_cast<uint32_t*>(o) = packed;
-            else
-                for (int c = 0; c < 4 && x + c < w; c++) o[c] = (uint8_t)(packed >> (8 * c));
         }
     }
 }
