@@ -15,8 +15,12 @@ constexpr int PATCH_SIZE = 31;
 constexpr int HALF_PATCH_SIZE = 15;
 constexpr int PYR_XB = 1024;        // k_pyr_down output columns per workgroup (4 per thread)
 constexpr int PYR_RB = 8;           // k_pyr_down output rows per workgroup
-constexpr int BLUR_TILE_W = 128;   // k_blur7 output tile: 4 px per thread-quad
-constexpr int BLUR_TILE_H = 32;
+#ifndef MAM_BLUR_TW
+#define MAM_BLUR_TW 64
+#define MAM_BLUR_TH 64
+#endif
+constexpr int BLUR_TILE_W = MAM_BLUR_TW;   // k_blur7 output tile: 4 px per thread-quad
+constexpr int BLUR_TILE_H = MAM_BLUR_TH;
 #ifndef MAM_BLUR_TPB
 #define MAM_BLUR_TPB 1
 #endif
