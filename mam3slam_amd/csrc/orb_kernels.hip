@@ -788,7 +788,10 @@ __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, Level
         uint8_t* out = blur + L.blur_off + (size_t)f * L.frame_bytes;
         // vertical: thread = one 4-column quad x BLUR_VR consecutive output rows; the BLUR_VR + 6 staged u16 rows it needs
         // are read once (sliding window) instead of 7 per output row
-        constexpr int BLUR_VR = 4;
+#ifndef MAM_BLUR_VR
+#define MAM_BLUR_VR 4
+#endif
+        constexpr int BLUR_VR = MAM_BLUR_VR;
         static_assert(BLUR_TILE_H % BLUR_VR == 0, "row groups");
         for (int i = tid; i < (BLUR_TILE_H / BLUR_VR) * QPR; i += 256) {
             const int rg = i / QPR, q = i - rg * QPR;
