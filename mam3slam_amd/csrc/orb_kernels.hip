@@ -739,9 +739,22 @@ __device__ __forceinline__ void blur_fetch(const BlurTile& t, int tid, uint32_t 
 __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ blur) {
     __shared__ __attribute__((aligned(16))) uint8_t tin[BLUR_IN_H][BLUR_IN_W];
     __shared__ __attribute__((aligned(16))) uint16_t th_[BLUR_IN_H][BLUR_TILE_W];
-    const int f = blockIdx.y;
+#ifndef MAM_BLUR_XCD
+#define MAM_BLUR_XCD 1
+#endif
+    // XCD-aware order: the hardware deals linear block ids round-robin over the 8 XCDs; remap them (bijectively, any
+    // grid size) so each XCD works a contiguous range of (frame, tile) ids, putting vertically adjacent tiles, whose
+    // staged halo rows overlap, on the same L2
+    const int nlin = gridDim.x * gridDim.y;
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    int logical = lin;
+    if (MAM_BLUR_XCD) {
+        const int q = nlin >> 3, rem = nlin & 7, x = lin & 7, k = lin >> 3;
+        logical = x < rem ? x * (q + 1) + k : rem * (q + 1) + (x - rem) * q + k;
+    }
+    const int f = logical / gridDim.x;
     const int tid = threadIdx.x;
-    const int tile0 = blockIdx.x * BLUR_TPB;
+    const int tile0 = (logical - f * gridDim.x) * BLUR_TPB;
     const int ntiles = min(BLUR_TPB, g->tiles_per_frame - tile0);
     uint32_t v[BLUR_NIT];
     BlurTile t = blur_tile(g, s, f, tile0);
