@@ -192,6 +192,26 @@ def pose_section(args, B, W, H, NF, cam, kps_h, cnt_h, d_out1, lasts, dev, strea
     return info
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`--gpus N` without a launcher: start N rank processes (one per GPU) under torch.distributed.run as CHILD
+    processes of this one, which has not touched the GPU, and return their exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -210,14 +230,34 @@ def main():
     ap.add_argument("--lanes", type=int, default=4,
                     help="independent sub-batches (agent groups) per GPU, each with its own contexts and HIP stream, "
                          "so one group's latency-bound stages overlap another's compute")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rendezvous + barrier over gloo on the CPU and exit (tests the --gpus N launcher, no GPU)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # before any HIP call: the ranks are children, never an exec of this process
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        if world > 1:
+            dist.init_process_group(backend="gloo")
+            t = torch.tensor([rank], dtype=torch.int64)
+            dist.all_reduce(t)
+            dist.barrier()
+            dist.destroy_process_group()
+            if rank == 0:
+                print(json.dumps({"launch_check": "ok", "world": world, "rank_sum": int(t.item())}), flush=True)
+        else:
+            print(json.dumps({"launch_check": "ok", "world": 1, "rank_sum": 0}), flush=True)
+        return
     if world > 1:
         dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)

@@ -19,6 +19,12 @@
 
 namespace MAM3SLAM {
 
+/* The HIP device that the calling thread's ORBmatcher / Optimizer calls run on (their device contexts are per
+ * thread). One agent per GPU: each of an agent's threads (Tracking, LocalMapping) calls SetDevice(g) once.
+ * Default 0. Changing it releases the thread's contexts on the old device. */
+void SetDevice(int device);
+int GetDevice();
+
 struct Point2f {
     float x = 0.f, y = 0.f;
 };

@@ -145,7 +145,7 @@ int mam_bow_create(int device, int k, int L, int weighting, int scoring, int n_n
     int ndev = 0;
     MAM_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) { mam::set_last_error("no such HIP device"); return MAM_ERR_ARG; }
-    MAM_HIP(hipSetDevice(device));
+    MAM_DEVICE_SCOPE(device);
     // children in file order (m_nodes[pid].children.push_back(nid)), CSR by parent
     std::vector<int32_t> cnt(n_nodes, 0), off(n_nodes + 1, 0), pos(n_nodes, 0);
     for (int i = 1; i < n_nodes; i++) cnt[parent[i]]++;
@@ -192,7 +192,7 @@ int mam_bow_create(int device, int k, int L, int weighting, int scoring, int n_n
 
 void mam_bow_destroy(mam_bow_vocab* v) {
     if (!v) return;
-    (void)hipSetDevice(v->device);
+    ::mam::DeviceScope mam_dev_scope_(v->device);
     (void)hipStreamSynchronize(v->stream);
     (void)hipStreamDestroy(v->stream);
     delete v;
@@ -205,7 +205,7 @@ int mam_bow_transform_batch_device(mam_bow_vocab* v, int nframes, const uint8_t*
                                    void* stream) {
     if (!v || nframes < 0 || stride < 0 || (nframes > 0 && (!desc || !counts || !ow || !oweight || !onid)))
         return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(v->device));
+    MAM_DEVICE_SCOPE(v->device);
     return launch(v, nframes, desc, stride, counts, levelsup, ow, oweight, onid,
                   stream ? (hipStream_t)stream : v->stream);
 }
@@ -214,7 +214,7 @@ int mam_bow_transform(mam_bow_vocab* v, int n, const uint8_t* desc, int levelsup
                       uint32_t* onid) {
     if (!v || n < 0 || (n > 0 && (!desc || !ow || !oweight || !onid))) return MAM_ERR_ARG;
     if (n == 0) return MAM_OK;
-    MAM_HIP(hipSetDevice(v->device));
+    MAM_DEVICE_SCOPE(v->device);
     const size_t bytes = carve_bytes((size_t)n * 32, 1) + carve_bytes(2, 4) + 2 * carve_bytes(n, 4) + carve_bytes(n, 8);
     if (int rc = v->stage.alloc(bytes)) return rc;
     uint8_t* p = v->stage.p;

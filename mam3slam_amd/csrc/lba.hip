@@ -769,7 +769,7 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
     int ndev = 0;
     MAM_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) { mam::set_last_error("no such HIP device"); return MAM_ERR_ARG; }
-    MAM_HIP(hipSetDevice(device));
+    MAM_DEVICE_SCOPE(device);
     mam_lba_ctx* c = new mam_lba_ctx();
     c->device = device;
     // gfx950: 160 KB of LDS per workgroup; fall back to the 64 KB default if the opt-in is refused
@@ -801,7 +801,7 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
 
 void mam_lba_destroy(mam_lba_ctx* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    ::mam::DeviceScope mam_dev_scope_(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -835,7 +835,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     for (int e = 0; e < E; e++)
         if (p->edge_point[e] < 0 || p->edge_point[e] >= L || p->edge_pose[e] < 0 || p->edge_pose[e] >= P)
             return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
 #ifdef MAM_LDLT_PROFILE
     const auto h_t0 = std::chrono::steady_clock::now();
 #endif

@@ -1399,7 +1399,7 @@ int mam_match_create(int device, mam_match_ctx** out) {
     int ndev = 0;
     MAM_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) { mam::set_last_error("no such HIP device"); return MAM_ERR_ARG; }
-    MAM_HIP(hipSetDevice(device));
+    MAM_DEVICE_SCOPE(device);
     mam_match_ctx* c = new mam_match_ctx();
     c->device = device;
     // the resolve stage may stage up to ~110 KB in LDS (gfx950: 160 KB per workgroup)
@@ -1420,7 +1420,7 @@ int mam_match_create(int device, mam_match_ctx** out) {
 
 void mam_match_destroy(mam_match_ctx* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    ::mam::DeviceScope mam_dev_scope_(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1429,7 +1429,7 @@ void mam_match_destroy(mam_match_ctx* c) {
 int mam_descriptor_distance(mam_match_ctx* c, const uint8_t* a, const uint8_t* b, int n, int32_t* out) {
     if (!c || n < 0 || (n > 0 && (!a || !b || !out))) return MAM_ERR_ARG;
     if (n == 0) return MAM_OK;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     const size_t bytes = carve_bytes((size_t)n * 32, 1) * 2 + carve_bytes(n, 4);
     if (int rc = c->stage.alloc(bytes)) return rc;
     uint8_t* p = c->stage.p;
@@ -1449,7 +1449,7 @@ int mam_search_by_projection_batch_device(mam_match_ctx* c, const mam_frame_geom
                                           int far_points, float th_far_points, float nnratio, int32_t* out,
                                           int32_t* out_n, void* stream) {
     if (!c || !geom_ok(g) || !fr || !mps || !n_mps || !out || !out_n || mp_stride <= 0) return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     mam::ProjArgs a{};
     a.g = *g;
     a.fr = *fr;
@@ -1473,7 +1473,7 @@ int mam_search_by_projection_motion_batch_device(mam_match_ctx* c, const mam_fra
                                                  float th, int check_ori, int32_t* out, int32_t* out_n, void* stream) {
     if (!c || !geom_ok(g) || !fr || !tcw || !cam || !last || !n_last || !out || !out_n || last_stride <= 0)
         return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     mam::ProjArgs a{};
     a.g = *g;
     a.fr = *fr;
@@ -1531,7 +1531,7 @@ int mam_search_by_projection(mam_match_ctx* c, const mam_frame_geom* g, int n, c
     if (!c || !geom_ok(g) || n < 0 || n_mps < 0 || (n > 0 && (!keys || !desc || !out)) || (n_mps > 0 && !mps))
         return MAM_ERR_ARG;
     if (n > mam::GRID_SORT_MAX) return MAM_ERR_CAPACITY;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     for (int attempt = 0; attempt < 6; attempt++) {
         mam_frames_dev fr;
         uint8_t* extra;
@@ -1567,7 +1567,7 @@ int mam_search_by_projection_motion(mam_match_ctx* c, const mam_frame_geom* g, i
         return MAM_ERR_ARG;
     if (!mono) { mam::set_last_error("stereo motion search is out of scope (mono agents only)"); return MAM_ERR_ARG; }
     if (n > mam::GRID_SORT_MAX) return MAM_ERR_CAPACITY;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     for (int attempt = 0; attempt < 6; attempt++) {
         mam_frames_dev fr;
         uint8_t* extra;
@@ -1605,7 +1605,7 @@ int mam_search_for_triangulation(mam_match_ctx* c, const mam_frame_geom* g, int 
     if (!c || !geom_ok(g) || !fv1 || !fv2 || !F12 || !ep || n1 < 0 || n2 < 0 || (n1 > 0 && (!keys1 || !desc1 || !has1 || !out)) ||
         (n2 > 0 && (!keys2 || !desc2 || !has2)))
         return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     for (int i = 0; i < n1; i++) out[i] = -1;
     if (n1 == 0) return 0;
     // shared vocabulary nodes: the reference's merge walk visits exactly the node ids present in both
@@ -1693,7 +1693,7 @@ int mam_fuse_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_f
                           int32_t* out_idx, int32_t* out_dist, int32_t* out_n, void* stream) {
     if (!c || !geom_ok(g) || !fr || !kfs || !cam || !mps || !n_mps || !out_idx || !out_dist || !out_n || mp_stride <= 0)
         return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     mam::FuseArgs a{};
     a.g = *g;
     a.fr = *fr;
@@ -1717,7 +1717,7 @@ int mam_fuse(mam_match_ctx* c, const mam_frame_geom* g, int n, const mam_keypoin
         return MAM_ERR_ARG;
     if (n > mam::GRID_SORT_MAX) return MAM_ERR_CAPACITY;
     if (n_mps == 0) return 0;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     mam_frames_dev fr;
     uint8_t* extra;
     int32_t *dout, *dcount, *dn;
@@ -1745,7 +1745,7 @@ int mam_compute_distinctive_descriptors_batch_device(mam_match_ctx* c, int n_mps
                                                      const uint8_t* descs, int32_t* out, void* stream) {
     if (!c || n_mps < 0 || (n_mps > 0 && (!off || !descs || !out))) return MAM_ERR_ARG;
     if (n_mps == 0) return MAM_OK;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     {
         mam::StageTimer::Scope sc(&c->timer, s, 5);
@@ -1764,7 +1764,7 @@ int mam_compute_distinctive_descriptors(mam_match_ctx* c, int n_mps, const int32
         if (off[m + 1] < off[m]) return MAM_ERR_ARG;
     const int total = off[n_mps];
     if (total > 0 && !descs) return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     const size_t rows = (size_t)std::max(total, 1);
     const size_t bytes = carve_bytes((size_t)n_mps + 1, 4) + carve_bytes(rows * 32, 1) + carve_bytes(n_mps, 4);
     if (int rc = c->stage.alloc(bytes)) return rc;

@@ -586,7 +586,7 @@ int mam_orb_create(const mam_orb_params* params, int device, mam_orb_ctx** out) 
     int ndev = 0;
     MAM_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) { g_last_error = "no such HIP device"; return MAM_ERR_ARG; }
-    MAM_HIP(hipSetDevice(device));
+    MAM_DEVICE_SCOPE(device);
     mam_orb_ctx* c = new mam_orb_ctx();
     c->prm = *params;
     c->device = device;
@@ -603,7 +603,7 @@ int mam_orb_create(const mam_orb_params* params, int device, mam_orb_ctx** out) 
 
 void mam_orb_destroy(mam_orb_ctx* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    ::mam::DeviceScope mam_dev_scope_(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->d_geom.release(); c->d_cells.release(); c->d_tabs_i.release(); c->d_tabs_s.release();
     c->d_pyr.release(); c->d_blur.release(); c->d_input.release();
@@ -645,7 +645,7 @@ int mam_orb_extract_batch_device(mam_orb_ctx* c, const uint8_t* d_imgs, int nfra
         capacity < 0)
         return MAM_ERR_ARG;
     if (nframes > 1 && frame_stride < stride * h) return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     if (int rc = ensure_geometry(c, w, h, nframes)) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return run_pipeline(c, d_imgs, nframes, stride, frame_stride, lap0, lap1, d_kps, d_desc, capacity, d_counts, s);
@@ -658,7 +658,7 @@ int mam_orb_extract(mam_orb_ctx* c, const uint8_t* img, int w, int h, size_t str
     *mono_out = 0;
     if (!img || w <= 0 || h <= 0) return MAM_ERR_EMPTY;
     if (stride < (size_t)w || capacity < 0) return MAM_ERR_ARG;
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     if (int rc = ensure_geometry(c, w, h, 1)) return rc;
     const int kcap = c->geom.kp_slots;
     if (int rc = c->d_input.alloc((size_t)w * h)) return rc;
@@ -691,6 +691,7 @@ int mam_orb_get_level(mam_orb_ctx* c, int frame, int level, uint8_t* out, int* w
     if (w_out) *w_out = lv.w;
     if (h_out) *h_out = lv.h;
     if (!out) return MAM_OK;
+    MAM_DEVICE_SCOPE(c->device);
     MAM_HIP(hipStreamSynchronize(c->stream));
     const uint8_t* src;
     size_t pitch;
@@ -704,6 +705,7 @@ int mam_orb_debug_blurred(mam_orb_ctx* c, int frame, int level, uint8_t* out) {
     if (!c || !out || level < 0 || level >= c->prm.nlevels || frame < 0 || frame >= c->last_nframes)
         return MAM_ERR_ARG;
     const mam::LevelGeom& lv = c->geom.L[level];
+    MAM_DEVICE_SCOPE(c->device);
     MAM_HIP(hipStreamSynchronize(c->stream));
     MAM_HIP(hipMemcpy2D(out, lv.w, c->d_blur.p + lv.blur_off + (size_t)frame * lv.frame_bytes, lv.pitch, lv.w, lv.h,
                         hipMemcpyDeviceToHost));
@@ -712,6 +714,7 @@ int mam_orb_debug_blurred(mam_orb_ctx* c, int frame, int level, uint8_t* out) {
 
 int mam_orb_debug_candidates(mam_orb_ctx* c, int frame, int level, uint32_t* out, int capacity) {
     if (!c || level < 0 || level >= c->prm.nlevels || frame < 0 || frame >= c->last_nframes) return MAM_ERR_ARG;
+    MAM_DEVICE_SCOPE(c->device);
     MAM_HIP(hipStreamSynchronize(c->stream));
     const mam::LevelGeom& lv = c->geom.L[level];
     std::vector<int> cnt(lv.ncells);

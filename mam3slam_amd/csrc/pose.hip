@@ -458,7 +458,7 @@ int mam_pose_create(int device, mam_pose_ctx** out) {
     int ndev = 0;
     MAM_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) { mam::set_last_error("no such HIP device"); return MAM_ERR_ARG; }
-    MAM_HIP(hipSetDevice(device));
+    MAM_DEVICE_SCOPE(device);
     mam_pose_ctx* c = new mam_pose_ctx();
     c->device = device;
     // LDS carve: as many edges as fit in 160 KB next to the kernel's static scratch
@@ -483,7 +483,7 @@ int mam_pose_create(int device, mam_pose_ctx** out) {
 
 void mam_pose_destroy(mam_pose_ctx* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    ::mam::DeviceScope mam_dev_scope_(c->device);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -500,7 +500,7 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_p
         mam::set_last_error("edge_stride exceeds mam_pose_max_edges()");
         return MAM_ERR_CAPACITY;
     }
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     mam::pose::Args a;
     a.nframes = nframes;
@@ -527,7 +527,7 @@ int mam_pose_optimization(mam_pose_ctx* c, const mam_pose* tcw, const mam_pinhol
         mam::set_last_error("more edges than mam_pose_max_edges()");
         return MAM_ERR_CAPACITY;
     }
-    MAM_HIP(hipSetDevice(c->device));
+    MAM_DEVICE_SCOPE(c->device);
     const size_t S = std::max(n, 1);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t bytes = al(S * sizeof(mam_pose_edge)) + al(S) + al(sizeof(mam_pose_result)) + al(sizeof(mam_pose)) + al(4);

@@ -22,6 +22,27 @@ void set_last_error(const std::string& s);   // defined in orb_extract.hip (one 
         }                                                                                        \
     } while (0)
 
+// Switches the calling thread to a context's device for the duration of one C-ABI call and restores the caller's
+// current device on return: an agent thread that drives GPU g keeps GPU g current across library calls.
+struct DeviceScope {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceScope(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(device) == hipSuccess;
+        if (!ok) set_last_error("hipSetDevice failed");
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
+#define MAM_DEVICE_SCOPE(dev)                               \
+    ::mam::DeviceScope mam_dev_scope_(dev);                 \
+    if (!mam_dev_scope_.ok) return MAM_ERR_DEVICE
+
 template <typename T>
 struct DevBuf {
     T* p = nullptr;

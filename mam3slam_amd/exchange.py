@@ -53,6 +53,19 @@ class MapUpdateExchange:
         self.send = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         self.recv = torch.zeros(self.world * nbytes, dtype=torch.uint8, device=device)
         self._L = None
+        self._pack_stream = None   # raw HIP stream the last pack_lba ran on (the collective must wait for it)
+
+    def _torch_stream(self, stream: int):
+        import torch
+
+        if stream is None or not self.send.is_cuda:
+            return None
+        cur = torch.cuda.current_stream(self.send.device)
+        if int(stream) == cur.cuda_stream:
+            return cur
+        if int(stream) == 0:
+            return torch.cuda.default_stream(self.send.device)
+        return torch.cuda.ExternalStream(int(stream), device=self.send.device)
 
     @property
     def block_bytes(self) -> int:
@@ -60,8 +73,14 @@ class MapUpdateExchange:
 
     def gather(self):
         """All-gather every agent's block into `recv` (rank order). Returns `recv`."""
+        import torch
         import torch.distributed as dist
 
+        # order the collective after the pack kernel: torch runs it on its current stream, pack_lba ran on a raw one
+        if self._pack_stream is not None:
+            ps = self._torch_stream(self._pack_stream)
+            if ps is not None:
+                torch.cuda.current_stream(self.send.device).wait_stream(ps)
         if self.world == 1:
             self.recv.copy_(self.send)
         elif dist.get_backend(self.group) == "gloo":
@@ -85,11 +104,26 @@ class MapUpdateExchange:
             C.c_void_p(d_pose_q), C.c_void_p(d_pose_t), C.c_void_p(d_pose_id), C.c_void_p(d_pose_fixed), n_poses,
             C.c_void_p(d_point_xyz), C.c_void_p(d_point_id), C.c_void_p(d_point_bad or 0), n_points, a,
             C.c_void_p(self.send.data_ptr()), self.capacity, C.c_void_p(stream)), "mam_exchange_pack_lba")
+        self._pack_stream = int(stream)
 
     def apply(self, d_kf_table: int, kf_cap: int, d_mp_table: int, mp_cap: int, d_status: int, stream: int = 0,
               gathered: int | None = None, n_agents: int | None = None):
-        """Apply the gathered blocks (default: `recv`) to the device tables, agent 0 first."""
+        """Apply the gathered blocks (default: `recv`) to the device tables, agent 0 first. `stream` is ordered after
+        the collective (torch's current stream) before the apply kernel reads `recv`."""
+        import torch
+
+        if self.send.is_cuda:
+            st = self._torch_stream(stream)
+            if st is not None:
+                st.wait_stream(torch.cuda.current_stream(self.send.device))
         check(self._lib().mam_exchange_apply(
             C.c_void_p(gathered or self.recv.data_ptr()), n_agents or self.world, self.capacity,
             C.c_void_p(d_kf_table), int(kf_cap), C.c_void_p(d_mp_table), int(mp_cap), C.c_void_p(d_status),
             C.c_void_p(stream)), "mam_exchange_apply")
+
+    @staticmethod
+    def check_status(status_tensor):
+        """Raise if an apply flagged a malformed block or an id outside the tables (synchronises)."""
+        v = int(status_tensor.reshape(-1)[0].item())
+        if v != 0:
+            raise RuntimeError(f"mam_exchange_apply: status {v} (malformed header or id outside the tables)")

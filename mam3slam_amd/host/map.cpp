@@ -11,6 +11,12 @@
 
 namespace MAM3SLAM {
 
+namespace {
+thread_local int t_device = 0;
+}
+void SetDevice(int device) { t_device = device; }
+int GetDevice() { return t_device; }
+
 // ---- SE3f (Sophus::SE3f) ----------------------------------------------------------------------------------
 
 void SE3f::rotationMatrix(float R[9]) const {

@@ -14,6 +14,7 @@ namespace {
 
 struct ThreadLBA {
     mam_lba_ctx* ctx = nullptr;
+    int device = -1;
     ~ThreadLBA() {
         if (ctx) mam_lba_destroy(ctx);
     }
@@ -22,24 +23,36 @@ thread_local ThreadLBA t_lba;
 
 struct ThreadPose {
     mam_pose_ctx* ctx = nullptr;
+    int device = -1;
     ~ThreadPose() {
         if (ctx) mam_pose_destroy(ctx);
     }
 };
 thread_local ThreadPose t_pose;
 
+// contexts follow the thread's device (SetDevice): recreated when it changes
 mam_pose_ctx* poseCtx() {
+    if (t_pose.ctx && t_pose.device != GetDevice()) {
+        mam_pose_destroy(t_pose.ctx);
+        t_pose.ctx = nullptr;
+    }
     if (!t_pose.ctx) {
-        const int rc = mam_pose_create(0, &t_pose.ctx);
+        const int rc = mam_pose_create(GetDevice(), &t_pose.ctx);
         if (rc < 0) throw std::runtime_error(std::string("mam_pose_create failed: ") + mam_last_error());
+        t_pose.device = GetDevice();
     }
     return t_pose.ctx;
 }
 
 mam_lba_ctx* lbaCtx() {
+    if (t_lba.ctx && t_lba.device != GetDevice()) {
+        mam_lba_destroy(t_lba.ctx);
+        t_lba.ctx = nullptr;
+    }
     if (!t_lba.ctx) {
-        const int rc = mam_lba_create(0, &t_lba.ctx);
+        const int rc = mam_lba_create(GetDevice(), &t_lba.ctx);
         if (rc < 0) throw std::runtime_error(std::string("mam_lba_create failed: ") + mam_last_error());
+        t_lba.device = GetDevice();
     }
     return t_lba.ctx;
 }

@@ -29,10 +29,17 @@ struct ThreadCtx {
     }
 };
 thread_local ThreadCtx t_ctx;
-thread_local int t_device = 0;
+thread_local int t_ctx_device = -1;
 
 mam_match_ctx* ctx() {
-    if (!t_ctx.ctx) throwOn(mam_match_create(t_device, &t_ctx.ctx), "mam_match_create");
+    if (t_ctx.ctx && t_ctx_device != GetDevice()) {
+        mam_match_destroy(t_ctx.ctx);
+        t_ctx.ctx = nullptr;
+    }
+    if (!t_ctx.ctx) {
+        throwOn(mam_match_create(GetDevice(), &t_ctx.ctx), "mam_match_create");
+        t_ctx_device = GetDevice();
+    }
     return t_ctx.ctx;
 }
 
