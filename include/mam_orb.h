@@ -34,19 +34,24 @@ typedef struct mam_keypoint {
     int32_t class_id;
 } mam_keypoint;
 
-/* The five ORBextractor constructor arguments (Settings.cc:443-451 keys ORBextractor.*) plus one
- * floating-point policy knob for the rBRIEF sample-position arithmetic (DESIGN.md §Parity policy):
- *   desc_fma = 0 : pattern.x*b + pattern.y*a evaluated as two rounded products and a rounded sum
- *                  (the C++ source read literally; default);
- *   desc_fma = 1 : fma(x, b, y*a) / fma(x, a, -(y*b)) — the form GCC -O3 -march=native contracts
- *                  GET_VALUE (src/ORBextractor.cc:117-119) into on FMA hardware. */
+/* The five ORBextractor constructor arguments (Settings.cc:443-451 keys ORBextractor.*) plus the floating-point
+ * policy of the rBRIEF steering. fp_policy = 0 (the default, a zero-initialised struct) is the
+ * reference binary's arithmetic: g++ 11.4 -O3 -march=native on an FMA + AVX2 x86-64 host, glibc 2.35
+ * (ros:humble, Dockerfile:18):
+ *   - sin/cos of the angle (src/ORBextractor.cc:111): glibc 2.35 sincosf, the ifunc's FMA build;
+ *   - GET_VALUE (src/ORBextractor.cc:117-119): fma(x, b, y*a) and fma(x, a, -(y*b)), the contraction GCC emits
+ *     (vfmadd231ss / vfmsub132ss, asm checked).
+ * Flags select other hosts/builds: */
+#define MAM_FP_DESC_UNCONTRACTED 1      /* GET_VALUE as two rounded products and a rounded sum (no FMA build) */
+#define MAM_FP_TRIG_SSE2 2              /* glibc sincosf SSE2 build (host without FMA/AVX2) */
+#define MAM_FP_TRIG_CORRECTLY_ROUNDED 4 /* (float) of the double-precision sin/cos (libm-independent) */
 typedef struct mam_orb_params {
     int32_t nfeatures;
     float   scale_factor;
     int32_t nlevels;
     int32_t ini_th_fast;
     int32_t min_th_fast;
-    int32_t desc_fma;
+    int32_t fp_policy;   /* MAM_FP_* flags; 0 = the reference binary */
 } mam_orb_params;
 
 enum {

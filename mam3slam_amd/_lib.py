@@ -25,7 +25,7 @@ class KeyPoint(C.Structure):
 
 class OrbParams(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
-                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("desc_fma", C.c_int32)]
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("fp_policy", C.c_int32)]
 
 
 MAM_OK, MAM_ERR_EMPTY, MAM_ERR_CAPACITY, MAM_ERR_DEVICE, MAM_ERR_ARG = 0, -1, -2, -3, -4

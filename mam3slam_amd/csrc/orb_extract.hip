@@ -546,7 +546,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
         const int blocks = (int)((waves + 3) / 4);
         hipLaunchKernelGGL(mam::k_describe, dim3(blocks), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p,
                            c->d_okey.p, c->d_orank.p, c->d_lvlcnt.p, F, d_kps, d_desc, capacity, d_counts,
-                           c->prm.desc_fma);
+                           c->prm.fp_policy);
     }
     MAM_HIP(hipGetLastError());
 #ifdef MAM_DIST_PROFILE

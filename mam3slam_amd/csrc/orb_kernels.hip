@@ -1259,7 +1259,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, Le
                                                   const uint32_t* __restrict__ out_rank,
                                                   const int* __restrict__ lvl_counts, int nframes,
                                                   mam_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                  int capacity, int32_t* __restrict__ counts, int desc_fma) {
+                                                  int capacity, int32_t* __restrict__ counts, int fp_policy) {
     const int gw = (blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = lane_id();
     const int f = gw / g->kp_slots;
@@ -1347,8 +1347,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, Le
     const float angle = fast_atan2((float)m01, (float)m10);
     // rBRIEF on the blurred level (ORBextractor.cc:107-146): lane owns pairs lane, lane+64, ...
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    float a, b;
-    det_sincos(angle * factorPI, &b, &a);
+    float a, b;   // a = (float)cos(angle), b = (float)sin(angle) under the fp policy (mam_orb.h MAM_FP_*)
+    if (fp_policy & MAM_FP_TRIG_CORRECTLY_ROUNDED) det_sincos(angle * factorPI, &b, &a);
+    else if (fp_policy & MAM_FP_TRIG_SSE2) glibc_sincosf<false>(angle * factorPI, &b, &a);
+    else glibc_sincosf<true>(angle * factorPI, &b, &a);
+    const bool desc_fma = !(fp_policy & MAM_FP_DESC_UNCONTRACTED);
 #pragma unroll
     for (int k = 0; k < DESC_NW; k++) {
         const int i = k * 64 + lane;

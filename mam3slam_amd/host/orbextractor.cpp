@@ -22,7 +22,7 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
     p.nlevels = _nlevels;
     p.ini_th_fast = _iniThFAST;
     p.min_th_fast = _minThFAST;
-    p.desc_fma = 0;
+    p.fp_policy = 0;   // the reference binary's arithmetic (mam_orb.h)
     throwOn(mam_orb_create(&p, device, &ctx), "mam_orb_create");
     std::vector<float> s(4 * (size_t)nlevels);
     mnFeaturesPerLevel.resize(nlevels);

@@ -28,9 +28,9 @@ class ORBextractor:
     HARRIS_SCORE, FAST_SCORE = 0, 1
 
     def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int, minThFAST: int,
-                 device: int = 0, desc_fma: bool = False):
+                 device: int = 0, fp_policy: int = 0):
         self._p = OrbParams(int(nfeatures), float(scaleFactor), int(nlevels), int(iniThFAST), int(minThFAST),
-                            1 if desc_fma else 0)
+                            int(fp_policy))
         self._ctx = C.c_void_p()
         check(lib().mam_orb_create(C.byref(self._p), int(device), C.byref(self._ctx)), "mam_orb_create")
         self.nfeatures, self.nlevels = int(nfeatures), int(nlevels)

@@ -22,7 +22,7 @@ class KeyPoint(C.Structure):
 
 class OrbParams(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
-                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("desc_fma", C.c_int32)]
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("fp_policy", C.c_int32)]
 
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
@@ -46,8 +46,8 @@ def lib():
     return _lib
 
 
-def params(nfeatures=1000, scale_factor=1.2, nlevels=8, ini=20, mn=7, desc_fma=0) -> OrbParams:
-    return OrbParams(nfeatures, scale_factor, nlevels, ini, mn, desc_fma)
+def params(nfeatures=1000, scale_factor=1.2, nlevels=8, ini=20, mn=7, fp_policy=0) -> OrbParams:
+    return OrbParams(nfeatures, scale_factor, nlevels, ini, mn, fp_policy)
 
 
 def _u8p(a):
@@ -139,6 +139,12 @@ def fast_atan2(y: float, x: float) -> float:
 def sincos(a: float):
     s, c = C.c_float(), C.c_float()
     lib().oracle_sincos(C.c_float(a), C.byref(s), C.byref(c))
+    return s.value, c.value
+
+
+def sincos_policy(fp_policy: int, a: float):
+    s, c = C.c_float(), C.c_float()
+    lib().oracle_sincos_policy(int(fp_policy), C.c_float(a), C.byref(s), C.byref(c))
     return s.value, c.value
 
 

@@ -393,6 +393,81 @@ void detSinCos(float af, float* s_out, float* c_out) {
     *c_out = (float)c;
 }
 
+// ---------------------------------------------------------------- glibc 2.35 sincosf (the reference's sin/cos)
+// computeOrbDescriptor's `(float)cos(angle), (float)sin(angle)` (ORBextractor.cc:111) on a float argument under
+// `using namespace std` call the float overloads; g++ 11.4 -O3 fuses them into one sincosf call. The reference
+// image (ros:humble = Ubuntu 22.04, glibc 2.35) resolves it through the x86-64 ifunc to the copy of
+// sysdeps/ieee754/flt-32/s_sincosf.c built with -mfma -mavx2 (FMA hosts) or the SSE2 copy. Restated from the
+// published source (sincosf.h: abstop12, reduce_fast, sincosf_poly; sincosf_data.c: __sincosf_table) for the
+// |y| < 120 range it covers; `fused` selects the FMA build (every a + b*c is one fma, as GCC contracts it).
+namespace glibc235 {
+struct sincos_t {
+    double sign[4];
+    double hpi_inv, hpi;
+    double c0, c1, c2, c3, c4;
+    double s1, s2, s3;
+};
+static const sincos_t table[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2,
+     0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2,
+     -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+};
+static inline uint32_t abstop12(float x) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    return (u >> 20) & 0x7ff;
+}
+// a + b * c as the selected build evaluates it
+static inline double mla(bool fused, double a, double b, double c) { return fused ? std::fma(b, c, a) : a + b * c; }
+
+static void sincosf_poly(bool fused, double x, double x2, const sincos_t* p, int n, float* sinp, float* cosp) {
+    double x4 = x2 * x2;
+    double x3 = x2 * x;
+    double c2 = mla(fused, p->c3, x2, p->c4);
+    double s1 = mla(fused, p->s2, x2, p->s3);
+    float* tmp = (n & 1 ? cosp : sinp);
+    cosp = (n & 1 ? sinp : cosp);
+    sinp = tmp;
+    double c1 = mla(fused, p->c0, x2, p->c1);
+    double x5 = x3 * x2;
+    double x6 = x4 * x2;
+    double s = mla(fused, x, x3, p->s1);
+    double c = mla(fused, c1, x4, p->c2);
+    *sinp = (float)mla(fused, s, x5, s1);
+    *cosp = (float)mla(fused, c, x6, c2);
+}
+
+static double reduce_fast(bool fused, double x, const sincos_t* p, int* np) {
+    double r = x * p->hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return fused ? std::fma(-(double)n, p->hpi, x) : x - n * p->hpi;
+}
+
+void sincosf(bool fused, float y, float* sinp, float* cosp) {
+    double x = y;
+    int n;
+    const sincos_t* p = &table[0];
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) {
+            *sinp = y;
+            *cosp = 1.0f;
+            return;
+        }
+        sincosf_poly(fused, x, x2, p, 0, sinp, cosp);
+    } else {   // abstop12(y) < abstop12(120.0f) for every rBRIEF angle (<= 2*pi)
+        x = reduce_fast(fused, x, p, &n);
+        double s = p->sign[n & 3];
+        if (n & 2) p = &table[1];
+        sincosf_poly(fused, x * s, x * x, p, n, sinp, cosp);
+    }
+}
+}  // namespace glibc235
+
 // ---------------------------------------------------------------- IC_Angle / descriptor (ORBextractor.cc:76-146)
 float IC_Angle(const uint8_t* image, size_t step, float ptx, float pty, const std::vector<int>& u_max) {
     int m_01 = 0, m_10 = 0;
@@ -414,10 +489,18 @@ float IC_Angle(const uint8_t* image, size_t step, float ptx, float pty, const st
 
 const float factorPI = (float)(M_PI / 180.f);
 
-void computeOrbDescriptor(const KeyPoint& kpt, const uint8_t* img, size_t imgstep, int desc_fma, uint8_t* desc) {
+// sin/cos of the steering angle under fp_policy (mam_orb.h MAM_FP_*): glibc 2.35 sincosf (FMA or SSE2 build) or the
+// correctly rounded double evaluation
+void policySinCos(int fp_policy, float angle, float* s, float* c) {
+    if (fp_policy & MAM_FP_TRIG_CORRECTLY_ROUNDED) detSinCos(angle, s, c);
+    else glibc235::sincosf(!(fp_policy & MAM_FP_TRIG_SSE2), angle, s, c);
+}
+
+void computeOrbDescriptor(const KeyPoint& kpt, const uint8_t* img, size_t imgstep, int fp_policy, uint8_t* desc) {
     float angle = (float)kpt.angle * factorPI;
     float a, b;
-    detSinCos(angle, &b, &a);       // a = (float)cos(angle), b = (float)sin(angle)
+    policySinCos(fp_policy, angle, &b, &a);       // a = (float)cos(angle), b = (float)sin(angle)
+    const bool desc_fma = !(fp_policy & MAM_FP_DESC_UNCONTRACTED);
     const uint8_t* center = img + (size_t)cvRoundF(kpt.y) * imgstep + cvRoundF(kpt.x);
     const int step = (int)imgstep;
     const int* pattern = bit_pattern_31;
@@ -730,6 +813,7 @@ void oracle_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst) { gaussian
 void oracle_gaussian7_taps(int32_t* taps7) { for (int i = 0; i < 7; i++) taps7[i] = g_taps[i]; }
 float oracle_fast_atan2(float y, float x) { return fastAtan2(y, x); }
 void oracle_sincos(float a, float* s, float* c) { detSinCos(a, s, c); }
+void oracle_sincos_policy(int fp_policy, float a, float* s, float* c) { policySinCos(fp_policy, a, s, c); }
 
 int oracle_distribute(const uint32_t* cand, int n, int minX, int maxX, int minY, int maxY, int N, uint32_t* out,
                       int cap) {
@@ -790,7 +874,7 @@ int oracle_orb_extract(const mam_orb_params* p, const uint8_t* img, int w, int h
         gaussian7(P.lev[level].data(), lw, lh, lw, blurred.data(), lw);
         float scale = t.scale[level];
         for (auto& kp : keypoints) {
-            computeOrbDescriptor(kp, blurred.data(), lw, p->desc_fma, d);
+            computeOrbDescriptor(kp, blurred.data(), lw, p->fp_policy, d);
             if (level != 0) { kp.x *= scale; kp.y *= scale; }
             int dst = (kp.x >= (float)lap0 && kp.x <= (float)lap1) ? stereoIndex-- : monoIndex++;
             mam_keypoint& o = kps[dst];

@@ -46,6 +46,8 @@ float oracle_fast_atan2(float y, float x);
 
 /* Deterministic (float)cos((double)a), (float)sin((double)a) (DESIGN.md §Parity policy). */
 void oracle_sincos(float a, float* s, float* c);
+/* sin/cos of the rBRIEF steering angle under an fp_policy (mam_orb.h MAM_FP_*; 0 = glibc 2.35 sincosf, FMA build). */
+void oracle_sincos_policy(int fp_policy, float a, float* s, float* c);
 
 /* Per-level FAST candidates (reference order, packed as above, coordinates relative to minBorder)
  * and the DistributeOctTree output for level `level`. Returns counts via *ncand / *nkeep. */

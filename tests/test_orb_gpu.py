@@ -16,10 +16,10 @@ pytestmark = pytest.mark.gpu
 CASES = [(640, 480, 1000), (1280, 720, 2000), (960, 960, 700), (640, 480, 5000)]
 
 
-def _extractor(nfeat, desc_fma=False):
+def _extractor(nfeat, fp_policy=0):
     from mam3slam_amd import ORBextractor
 
-    return ORBextractor(nfeat, 1.2, 8, 20, 7, desc_fma=desc_fma)
+    return ORBextractor(nfeat, 1.2, 8, 20, 7, fp_policy=fp_policy)
 
 
 def _first_diff(a, b):
@@ -73,12 +73,15 @@ def test_extract_bit_exact(gpu_lib, oracle, w, h, nfeat):
         _assert_kps_equal(kg, dg, mg, ko, do, mo, f"{w}x{h}/{nfeat} frame {fr}")
 
 
-def test_extract_desc_fma_policy(gpu_lib, oracle):
-    ext = _extractor(1000, desc_fma=True)
+@pytest.mark.parametrize("policy", [1, 2, 4, 5])
+def test_extract_fp_policies(gpu_lib, oracle, policy):
+    """Non-default arithmetic policies (mam_orb.h MAM_FP_*: uncontracted GET_VALUE, glibc's SSE2 sincosf, correctly
+    rounded trig) are bit-exact against the oracle under the same policy."""
+    ext = _extractor(1000, fp_policy=policy)
     img = synth.make_frame(640, 480, agent=2, frame=5)
     kg, dg, mg = ext(img)
-    ko, do, mo = oracle.extract(img, oracle.params(1000, desc_fma=1))
-    _assert_kps_equal(kg, dg, mg, ko, do, mo, "desc_fma=1")
+    ko, do, mo = oracle.extract(img, oracle.params(1000, fp_policy=policy))
+    _assert_kps_equal(kg, dg, mg, ko, do, mo, f"fp_policy={policy}")
 
 
 def test_lapping_area_placement(gpu_lib, oracle):
