@@ -218,7 +218,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU (independent frame streams)")
-    ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="c2 (1280x720/2000 + LocalBundleAdjustment) is BASELINE.json's headline metric config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-graph", action="store_true", help="launch the tracking step eagerly instead of a HIP graph")
