@@ -66,6 +66,20 @@ typedef struct mam_mp_track {
     uint8_t desc[32];         /* GetDescriptor() */
 } mam_mp_track;
 
+/* MapPoint fields Tracking::SearchLocalPoints and Frame::isInFrustum read (Tracking.cc:3103-3139, Frame.cc:512-571,
+ * MapPoint::PredictScale MapPoint.cc:531-546). 80 bytes. */
+typedef struct mam_local_mp {
+    float pos[3];             /* GetWorldPos() */
+    float max_distance;       /* mfMaxDistance (GetMaxDistanceInvariance() = 1.2f * it; PredictScale's ratio) */
+    float normal[3];          /* GetNormal() */
+    float min_distance;       /* mfMinDistance (GetMinDistanceInvariance() = 0.8f * it) */
+    int32_t is_bad;           /* isBad() */
+    int32_t nobs;             /* Observations() */
+    int32_t seen;             /* mnLastFrameSeen == CurrentFrame.mnId: already in the frame (skipped, not in view) */
+    int32_t pad;
+    uint8_t desc[32];         /* GetDescriptor() */
+} mam_local_mp;
+
 /* Sophus::SE3f as stored: unit quaternion (x, y, z, w) + translation. */
 typedef struct mam_pose {
     float q[4];
@@ -212,9 +226,26 @@ int mam_fuse_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const 
 int mam_compute_distinctive_descriptors_batch_device(mam_match_ctx* ctx, int n_mps, const int32_t* desc_off,
                                                      const uint8_t* descs, int32_t* out_best, void* stream);
 
+/* Tracking::SearchLocalPoints' projection loop (Tracking.cc:3119-3139): Frame::isInFrustum(pMP, view_cos_limit)
+ * (Frame.cc:512-571, mono Pinhole) + MapPoint::PredictScale(dist, Frame*) (MapPoint.cc:531-546) for n_mps local
+ * MapPoints of a frame with pose tcw (Sophus SE3f: mRcw = rotationMatrix(), mOw = inverse().translation()).
+ * out[i] = the track fields SearchByProjection(F, vpMapPoints) reads (proj_x/proj_y = -1 where the projection left
+ * the image; view_cos/track_depth/scale_level are 0 for a MapPoint not in view; is_bad, nobs and desc copied).
+ * log_scale_factor = mfLogScaleFactor (log of the float scale factor). Returns nToMatch (MapPoints in view). */
+int mam_is_in_frustum(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_pose* tcw, const mam_pinhole* cam,
+                      float log_scale_factor, int n_mps, const mam_local_mp* mps, float view_cos_limit,
+                      mam_mp_track* out);
+
+/* Batched: frame f (pose tcw[f]) projects n_mps[f] MapPoints at mps + f*mp_stride into out + f*mp_stride (the mps
+ * input of mam_search_by_projection_batch_device); out_n_to_match[f] (may be NULL) = nToMatch. */
+int mam_is_in_frustum_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, int nframes, const mam_pose* tcw,
+                                   const mam_pinhole* cam, float log_scale_factor, const mam_local_mp* mps,
+                                   int mp_stride, const int32_t* n_mps, float view_cos_limit, mam_mp_track* out,
+                                   int32_t* out_n_to_match, void* stream);
+
 int mam_match_set_profiling(mam_match_ctx* ctx, int enable);
-/* ms_out/launches_out (6 entries): [0] grid build, [1] candidate gather, [2] greedy resolve, [3] triangulation,
- * [4] fuse, [5] distinctive descriptors. */
+/* ms_out/launches_out (7 entries): [0] grid build, [1] candidate gather, [2] greedy resolve, [3] triangulation,
+ * [4] fuse, [5] distinctive descriptors, [6] frustum (isInFrustum + PredictScale). */
 int mam_match_stage_times(mam_match_ctx* ctx, double* ms_out, int64_t* launches_out);
 
 #ifdef __cplusplus

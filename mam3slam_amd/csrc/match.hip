@@ -1224,6 +1224,113 @@ __global__ __launch_bounds__(256) void k_distinct(const int32_t* __restrict__ of
     if (lane == 0) out[m] = (int32_t)(best & 0xFFFFFu);
 }
 
+// ------------------------------------------------------------------------------------------------ frustum
+// Tracking::SearchLocalPoints' projection loop (Tracking.cc:3119-3139): Frame::isInFrustum(pMP, 0.5) (Frame.cc:512-571,
+// mono) + MapPoint::PredictScale(dist, Frame*) (MapPoint.cc:531-546) for every local MapPoint of every frame, one
+// thread each, writing the mam_mp_track record the local-map search reads. Frame side per block: mRcw (Eigen
+// toRotationMatrix of the Sophus quaternion) and mOw (Tcw.inverse().translation()), Frame.cc:472-479. Eigen's 3x3 * 3
+// rows, norm() and dot() sum as e0 + (e1 + e2). Per-frame nToMatch by one atomic per block.
+struct FrustumArgs {
+    mam_frame_geom g;
+    const mam_pose* tcw;
+    mam_pinhole cam;
+    float log_scale_factor, view_cos_limit;
+    const mam_local_mp* mps;
+    int mp_stride;
+    const int32_t* n_mps;
+    mam_mp_track* out;
+    int32_t* out_n;
+};
+
+__global__ __launch_bounds__(256) void k_frustum(FrustumArgs a) {
+    __shared__ float fr[15];   // R (9), t (3), Ow (3)
+    __shared__ int wcount[4];
+    const int f = blockIdx.y;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (threadIdx.x == 0) {
+        const mam_pose T = a.tcw[f];
+        const float qx = T.q[0], qy = T.q[1], qz = T.q[2], qw = T.q[3];
+        const float tx = 2.0f * qx, ty = 2.0f * qy, tz = 2.0f * qz;
+        const float twx = tx * qw, twy = ty * qw, twz = tz * qw, txx = tx * qx, txy = ty * qx, txz = tz * qx;
+        const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+        fr[0] = 1.0f - (tyy + tzz); fr[1] = txy - twz; fr[2] = txz + twy;
+        fr[3] = txy + twz; fr[4] = 1.0f - (txx + tzz); fr[5] = tyz - twx;
+        fr[6] = txz - twy; fr[7] = tyz + twx; fr[8] = 1.0f - (txx + tyy);
+        fr[9] = T.t[0]; fr[10] = T.t[1]; fr[11] = T.t[2];
+        // Ow = conj(q) * (-t) (Sophus SO3 action, as unit_window evaluates it)
+        const float px = T.t[0] * -1.0f, py = T.t[1] * -1.0f, pz = T.t[2] * -1.0f;
+        const float ix = -qx, iy = -qy, iz = -qz;
+        float u0 = iy * pz - iz * py, u1 = iz * px - ix * pz, u2 = ix * py - iy * px;
+        u0 += u0; u1 += u1; u2 += u2;
+        const float c0 = iy * u2 - iz * u1, c1 = iz * u0 - ix * u2, c2 = ix * u1 - iy * u0;
+        fr[12] = ((px + qw * u0) + c0) + 0.0f;
+        fr[13] = ((py + qw * u1) + c1) + 0.0f;
+        fr[14] = ((pz + qw * u2) + c2) + 0.0f;
+    }
+    __syncthreads();
+    const int n = a.n_mps[f];
+    int in_view = 0;
+    if (j < n && j < a.mp_stride) {
+        const mam_local_mp& mp = a.mps[(size_t)f * a.mp_stride + j];
+        mam_mp_track o;
+        o.proj_x = -1.0f;
+        o.proj_y = -1.0f;
+        o.view_cos = 0.0f;
+        o.track_depth = 0.0f;
+        o.track_in_view = 0;
+        o.scale_level = 0;
+        o.is_bad = mp.is_bad;
+        o.nobs = mp.nobs;
+        const uint4* sd = reinterpret_cast<const uint4*>(mp.desc);
+        uint4* od = reinterpret_cast<uint4*>(o.desc);
+        od[0] = sd[0];
+        od[1] = sd[1];
+        if (!mp.seen && !mp.is_bad) {
+            const float P0 = mp.pos[0], P1 = mp.pos[1], P2 = mp.pos[2];
+            const float x = (fr[0] * P0 + (fr[1] * P1 + fr[2] * P2)) + fr[9];
+            const float y = (fr[3] * P0 + (fr[4] * P1 + fr[5] * P2)) + fr[10];
+            const float z = (fr[6] * P0 + (fr[7] * P1 + fr[8] * P2)) + fr[11];
+            const float pc_dist = sqrtf(x * x + (y * y + z * z));
+            if (z >= 0.0f) {
+                const float u = a.cam.fx * x / z + a.cam.cx;   // Pinhole::project(Vector3f)
+                const float v = a.cam.fy * y / z + a.cam.cy;
+                if (!(u < a.g.min_x || u > a.g.max_x || v < a.g.min_y || v > a.g.max_y)) {
+                    o.proj_x = u;
+                    o.proj_y = v;
+                    const float maxD = 1.2f * mp.max_distance, minD = 0.8f * mp.min_distance;
+                    const float O0 = P0 - fr[12], O1 = P1 - fr[13], O2 = P2 - fr[14];
+                    const float dist = sqrtf(O0 * O0 + (O1 * O1 + O2 * O2));
+                    if (!(dist < minD || dist > maxD)) {
+                        const float vc = (O0 * mp.normal[0] + (O1 * mp.normal[1] + O2 * mp.normal[2])) / dist;
+                        if (!(vc < a.view_cos_limit)) {
+                            // PredictScale; log(float) as the correctly rounded float log
+                            const float ratio = mp.max_distance / dist;
+                            int lvl = cvt_i32_x86(ceilf((float)log((double)ratio) / a.log_scale_factor));
+                            if (lvl < 0) lvl = 0;
+                            else if (lvl >= a.g.nlevels) lvl = a.g.nlevels - 1;
+                            o.track_in_view = 1;
+                            o.track_depth = pc_dist;
+                            o.scale_level = lvl;
+                            o.view_cos = vc;
+                            in_view = 1;
+                        }
+                    }
+                }
+            }
+        }
+        a.out[(size_t)f * a.mp_stride + j] = o;
+    }
+    if (a.out_n) {
+        const int c = __popcll(__ballot(in_view));
+        if ((threadIdx.x & 63) == 0) wcount[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int s = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+            if (s) atomicAdd(&a.out_n[f], s);
+        }
+    }
+}
+
 }  // namespace mam
 
 // ==================================================================================================== host
@@ -1232,7 +1339,7 @@ using mam::DevBuf;
 struct mam_match_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    mam::StageTimer timer{6};
+    mam::StageTimer timer{7};
     int slot_cap = 32;        // candidate slots per unit (grows x4 when a host call overflows)
     size_t resolve_lds_max = 64 * 1024;
     // scratch
@@ -1780,6 +1887,61 @@ int mam_compute_distinctive_descriptors(mam_match_ctx* c, int n_mps, const int32
     return MAM_OK;
 }
 
+int mam_is_in_frustum_batch_device(mam_match_ctx* c, const mam_frame_geom* g, int nframes, const mam_pose* tcw,
+                                   const mam_pinhole* cam, float log_scale_factor, const mam_local_mp* mps,
+                                   int mp_stride, const int32_t* n_mps, float view_cos_limit, mam_mp_track* out,
+                                   int32_t* out_n_to_match, void* stream) {
+    if (!c || !geom_ok(g) || nframes < 0 || !cam || mp_stride <= 0 || (nframes > 0 && (!tcw || !mps || !n_mps || !out)))
+        return MAM_ERR_ARG;
+    if (nframes == 0) return MAM_OK;
+    MAM_DEVICE_SCOPE(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    mam::FrustumArgs a{};
+    a.g = *g;
+    a.tcw = tcw;
+    a.cam = *cam;
+    a.log_scale_factor = log_scale_factor;
+    a.view_cos_limit = view_cos_limit;
+    a.mps = mps;
+    a.mp_stride = mp_stride;
+    a.n_mps = n_mps;
+    a.out = out;
+    a.out_n = out_n_to_match;
+    mam::StageTimer::Scope sc(&c->timer, s, 6);
+    if (out_n_to_match) MAM_HIP(hipMemsetAsync(out_n_to_match, 0, sizeof(int32_t) * (size_t)nframes, s));
+    hipLaunchKernelGGL(mam::k_frustum, dim3((mp_stride + 255) / 256, nframes), dim3(256), 0, s, a);
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
+
+int mam_is_in_frustum(mam_match_ctx* c, const mam_frame_geom* g, const mam_pose* tcw, const mam_pinhole* cam,
+                      float log_scale_factor, int n_mps, const mam_local_mp* mps, float view_cos_limit,
+                      mam_mp_track* out) {
+    if (!c || !geom_ok(g) || !tcw || !cam || n_mps < 0 || (n_mps > 0 && (!mps || !out))) return MAM_ERR_ARG;
+    if (n_mps == 0) return 0;
+    MAM_DEVICE_SCOPE(c->device);
+    const size_t bytes = carve_bytes(sizeof(mam_pose), 1) + carve_bytes(n_mps, sizeof(mam_local_mp)) +
+                         carve_bytes(n_mps, sizeof(mam_mp_track)) + carve_bytes(2, 4);
+    if (int rc = c->stage.alloc(bytes)) return rc;
+    uint8_t* p = c->stage.p;
+    mam_pose* dT = carve<mam_pose>(p, 1);
+    mam_local_mp* dm = carve<mam_local_mp>(p, n_mps);
+    mam_mp_track* dout = carve<mam_mp_track>(p, n_mps);
+    int32_t* dn = carve<int32_t>(p, 2);
+    hipStream_t s = c->stream;
+    MAM_HIP(hipMemcpyAsync(dT, tcw, sizeof(mam_pose), hipMemcpyHostToDevice, s));
+    MAM_HIP(hipMemcpyAsync(dm, mps, sizeof(mam_local_mp) * (size_t)n_mps, hipMemcpyHostToDevice, s));
+    MAM_HIP(hipMemcpyAsync(dn, &n_mps, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (int rc = mam_is_in_frustum_batch_device(c, g, 1, dT, cam, log_scale_factor, dm, n_mps, dn, view_cos_limit,
+                                                dout, dn + 1, s))
+        return rc;
+    int32_t nt = 0;
+    MAM_HIP(hipMemcpyAsync(out, dout, sizeof(mam_mp_track) * (size_t)n_mps, hipMemcpyDeviceToHost, s));
+    MAM_HIP(hipMemcpyAsync(&nt, dn + 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    MAM_HIP(hipStreamSynchronize(s));
+    return nt;
+}
+
 int mam_match_set_profiling(mam_match_ctx* c, int enable) {
     if (!c) return MAM_ERR_ARG;
     c->timer.reset(enable != 0);
@@ -1789,7 +1951,7 @@ int mam_match_set_profiling(mam_match_ctx* c, int enable) {
 int mam_match_stage_times(mam_match_ctx* c, double* ms_out, int64_t* launches_out) {
     if (!c) return MAM_ERR_ARG;
     c->timer.collect();
-    for (int i = 0; i < 6; i++) {
+    for (int i = 0; i < 7; i++) {
         if (ms_out) ms_out[i] = c->timer.ms[i];
         if (launches_out) launches_out[i] = c->timer.n[i];
     }

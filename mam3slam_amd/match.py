@@ -63,6 +63,11 @@ assert MP_TRACK_DTYPE.itemsize == 64 and LAST_ENTRY_DTYPE.itemsize == 64
 FUSE_MP_DTYPE = np.dtype([("pos", "<f4", (3,)), ("max_distance", "<f4"), ("normal", "<f4", (3,)),
                           ("min_distance", "<f4"), ("valid", "<i4"), ("pad", "<i4", (3,)), ("desc", "u1", (32,))])
 assert FUSE_MP_DTYPE.itemsize == 80
+# mam_local_mp: the MapPoint fields SearchLocalPoints / Frame::isInFrustum read (Tracking.cc:3103-3139)
+LOCAL_MP_DTYPE = np.dtype([("pos", "<f4", (3,)), ("max_distance", "<f4"), ("normal", "<f4", (3,)),
+                           ("min_distance", "<f4"), ("is_bad", "<i4"), ("nobs", "<i4"), ("seen", "<i4"),
+                           ("pad", "<i4"), ("desc", "u1", (32,))])
+assert LOCAL_MP_DTYPE.itemsize == 80
 
 
 class FuseKF(C.Structure):
@@ -119,6 +124,11 @@ _SIGS = {
     "mam_compute_distinctive_descriptors": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mam_compute_distinctive_descriptors_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                                                    C.c_void_p, C.c_void_p]),
+    "mam_is_in_frustum": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_int, C.c_void_p,
+                                    C.c_float, C.c_void_p]),
+    "mam_is_in_frustum_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_float,
+                                                 C.c_void_p, C.c_int, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p,
+                                                 C.c_void_p]),
     "mam_match_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "mam_match_stage_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
 }
@@ -344,7 +354,36 @@ class ORBmatcher:
               "ComputeDistinctiveDescriptors")
         return out[:n]
 
+    def IsInFrustum(self, F: FrameData, mps: np.ndarray, cam: Pinhole, viewingCosLimit: float = 0.5,
+                    scale_factor: float = 1.2):
+        """SearchLocalPoints' projection loop (Tracking.cc:3119-3139): Frame::isInFrustum(pMP, viewingCosLimit) +
+        PredictScale for every local MapPoint (LOCAL_MP_DTYPE) of frame F (F.pose = Tcw). Returns (nToMatch, tracks):
+        MP_TRACK_DTYPE records, the `mps` input of SearchByProjection."""
+        mps = np.ascontiguousarray(mps, LOCAL_MP_DTYPE)
+        out = np.zeros(max(len(mps), 1), MP_TRACK_DTYPE)
+        T = Pose()
+        for i in range(4):
+            T.q[i] = float(F.pose[0][i])
+        for i in range(3):
+            T.t[i] = float(F.pose[1][i])
+        g = F.geom()
+        n = self._L.mam_is_in_frustum(self._ctx, C.byref(g), C.byref(T), C.byref(cam),
+                                      float(np.log(np.float32(scale_factor))), len(mps), _p(mps),
+                                      float(viewingCosLimit), _p(out))
+        check(n, "isInFrustum")
+        return n, out[:len(mps)]
+
     # ---- batched device-resident (bench / multi-agent harness)
+    def is_in_frustum_batch_device(self, F: FrameData, nframes: int, d_tcw: int, cam: Pinhole, d_mps: int,
+                                   mp_stride: int, d_nmps: int, d_out: int, d_nmatch: int = 0, stream: int = 0,
+                                   view_cos_limit: float = 0.5, scale_factor: float = 1.2):
+        g = F.geom()
+        return check(self._L.mam_is_in_frustum_batch_device(
+            self._ctx, C.byref(g), int(nframes), C.c_void_p(d_tcw), C.byref(cam),
+            float(np.log(np.float32(scale_factor))), C.c_void_p(d_mps), int(mp_stride), C.c_void_p(d_nmps),
+            float(view_cos_limit), C.c_void_p(d_out), C.c_void_p(d_nmatch or None), C.c_void_p(stream)),
+            "is_in_frustum_batch_device")
+
     def search_by_projection_batch_device(self, F: FrameData, frames: FramesDev, d_mps: int, mp_stride: int,
                                           d_nmps: int, th: float, d_out: int, d_nmatch: int, stream: int = 0,
                                           far=False, th_far=50.0):
@@ -380,8 +419,8 @@ class ORBmatcher:
         check(self._L.mam_match_set_profiling(self._ctx, 1 if enable else 0), "match_set_profiling")
 
     def stage_times(self):
-        ms = np.zeros(6, np.float64)
-        n = np.zeros(6, np.int64)
+        ms = np.zeros(7, np.float64)
+        n = np.zeros(7, np.int64)
         check(self._L.mam_match_stage_times(self._ctx, _p(ms), _p(n)), "match_stage_times")
-        names = ["grid", "gather", "resolve", "triangulation", "fuse", "distinctive"]
+        names = ["grid", "gather", "resolve", "triangulation", "fuse", "distinctive", "frustum"]
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .match import (FUSE_MP_DTYPE, LAST_ENTRY_DTYPE, MP_TRACK_DTYPE, FrameData, Pinhole, camera_center,
+from .match import (FUSE_MP_DTYPE, LAST_ENTRY_DTYPE, LOCAL_MP_DTYPE, MP_TRACK_DTYPE, FrameData, Pinhole, camera_center,
                     epipole_12, fundamental_12)
 from .orb import KP_DTYPE
 
@@ -68,6 +68,61 @@ def local_mappoints(F: FrameData, rng: np.random.Generator, frac=0.8, dup_frac=0
     rnd["view_cos"] = rng.uniform(0.9, 1.0, n_random)
     rnd["track_in_view"] = 1
     rnd["scale_level"] = rng.integers(0, 8, n_random)
+    rnd["nobs"] = 1
+    rnd["desc"] = rng.integers(0, 256, (n_random, 32), dtype=np.uint8)
+    allm = np.concatenate([mps, dup, rnd])
+    return allm[rng.permutation(len(allm))]
+
+
+def local_world_mappoints(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.8, dup_frac=0.15,
+                          n_random=60, kflip=14, seen_frac=0.05):
+    """Local-map MapPoints in world coordinates around frame F (F.pose = Tcw): Tracking::mvpLocalMapPoints as
+    SearchLocalPoints receives them (LOCAL_MP_DTYPE). Points back-project F's keypoints to depths 1.5-40 m, so
+    Frame::isInFrustum re-projects them near their keypoints; their normals point from the camera centre with a
+    spread (a few beyond the 60 deg viewing limit), the scale-invariance range brackets the current distance (a few
+    outside it, so PredictScale sees every level), and the usual adversarial cases ride along: bad points, points
+    already seen this frame, duplicates competing for one keypoint, points behind the camera or outside the image."""
+    from .match import camera_center, quat_to_rot
+
+    q, t = F.pose
+    R = quat_to_rot(q).astype(np.float64)
+    Ow = camera_center(F.pose).astype(np.float64)
+    n = len(F.keys)
+    sel = rng.choice(n, size=int(n * frac), replace=False)
+    m = len(sel)
+    k = F.keys[sel]
+    z = rng.uniform(1.5, 40.0, m)
+    u = k["x"] + rng.normal(0, 0.8, m)
+    v = k["y"] + rng.normal(0, 0.8, m)
+    Xc = np.stack([(u - cam.cx) / cam.fx * z, (v - cam.cy) / cam.fy * z, z], 1)
+    Xw = (Xc - t[None, :].astype(np.float64)) @ R
+    mps = np.zeros(m, LOCAL_MP_DTYPE)
+    mps["pos"] = Xw.astype(np.float32)
+    d = Xw - Ow[None, :]
+    dist = np.linalg.norm(d, axis=1)
+    nrm = d / dist[:, None] + rng.normal(0, 0.35, (m, 3))
+    mps["normal"] = (nrm / np.linalg.norm(nrm, axis=1)[:, None]).astype(np.float32)
+    # mfMaxDistance = dist * 1.2^level_ref (the level the MapPoint was created at), mfMinDistance = max / 1.2^7
+    lvl_ref = rng.integers(0, 8, m)
+    maxd = dist * (1.2 ** lvl_ref) * rng.uniform(0.95, 1.05, m)
+    out_rng = rng.random(m) < 0.05
+    maxd[out_rng] = dist[out_rng] * rng.uniform(0.3, 0.8, out_rng.sum())
+    mps["max_distance"] = maxd.astype(np.float32)
+    mps["min_distance"] = (maxd / 1.2 ** 7).astype(np.float32)
+    mps["is_bad"] = (rng.random(m) < 0.02).astype(np.int32)
+    mps["seen"] = (rng.random(m) < seen_frac).astype(np.int32)
+    mps["nobs"] = rng.integers(0, 6, m) * (rng.random(m) < 0.97) + (rng.random(m) < 0.97)
+    mps["desc"] = flip_bits(F.desc[sel], rng, kflip)
+    nd = int(m * dup_frac)
+    dup = mps[rng.choice(m, size=nd, replace=False)].copy()
+    dup["pos"] += rng.normal(0, 0.004, (nd, 3)).astype(np.float32)
+    dup["desc"] = flip_bits(dup["desc"], rng, 3)
+    rnd = np.zeros(n_random, LOCAL_MP_DTYPE)
+    rnd["pos"] = (Ow[None, :] + rng.uniform(-30, 30, (n_random, 3))).astype(np.float32)
+    rnd["normal"] = rng.normal(0, 1, (n_random, 3)).astype(np.float32)
+    rnd["normal"] /= np.linalg.norm(rnd["normal"], axis=1)[:, None]
+    rnd["max_distance"] = rng.uniform(5, 80, n_random).astype(np.float32)
+    rnd["min_distance"] = rnd["max_distance"] / np.float32(1.2 ** 7)
     rnd["nobs"] = 1
     rnd["desc"] = rng.integers(0, 256, (n_random, 32), dtype=np.uint8)
     allm = np.concatenate([mps, dup, rnd])

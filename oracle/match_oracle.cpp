@@ -13,6 +13,8 @@
 //   src/MapPoint.cc:329-403     ComputeDistinctiveDescriptors
 //   src/CameraModels/Pinhole.cpp:35-41 project, :107-129 epipolarConstrain (F12 supplied by the caller)
 //   Thirdparty/Sophus/sophus/so3.hpp:358-367, se3.hpp:321-324 point action
+//   src/Frame.cc:512-571 isInFrustum (mono), src/MapPoint.cc:531-546 PredictScale(dist, Frame*),
+//   src/Tracking.cc:3098-3139 SearchLocalPoints' projection loop
 // Float expressions are evaluated as written, left to right, without contraction.
 
 #include <algorithm>
@@ -360,6 +362,69 @@ int oracle_fuse(const mam_frame_geom* g, int n, const mam_keypoint* keys, const 
         }
     }
     return nfused;
+}
+
+// Tracking::SearchLocalPoints' projection loop (Tracking.cc:3119-3139) with Frame::isInFrustum (Frame.cc:512-571,
+// mono) and MapPoint::PredictScale(dist, Frame*) (MapPoint.cc:531-546) for every local MapPoint, writing the track
+// fields SearchByProjection(F, vpMapPoints) reads. The frame pose enters as Sophus SE3f (q, t): mRcw =
+// rotationMatrix() (Eigen toRotationMatrix), mOw = Tcw.inverse().translation() (Frame.cc:472-479). Eigen's 3x3 * 3
+// product rows, norm() and dot() sum as e0 + (e1 + e2). A MapPoint seen this frame or bad is skipped with
+// mbTrackInView false. Returns nToMatch.
+int oracle_is_in_frustum(const mam_frame_geom* g, const mam_pose* tcw, const mam_pinhole* cam, float log_scale_factor,
+                         int n_mps, const mam_local_mp* mps, float view_cos_limit, mam_mp_track* out) {
+    const float qx = tcw->q[0], qy = tcw->q[1], qz = tcw->q[2], qw = tcw->q[3];
+    const float tx = 2.0f * qx, ty = 2.0f * qy, tz = 2.0f * qz;
+    const float twx = tx * qw, twy = ty * qw, twz = tz * qw, txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    const float R[9] = {1.0f - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1.0f - (txx + tzz), tyz - twx,
+                        txz - twy, tyz + twx, 1.0f - (txx + tyy)};
+    // Twc = Tcw.inverse(): conjugate rotation applied to -t
+    mam_pose inv;
+    inv.q[0] = -qx; inv.q[1] = -qy; inv.q[2] = -qz; inv.q[3] = qw;
+    inv.t[0] = inv.t[1] = inv.t[2] = 0.0f;
+    const float mt[3] = {tcw->t[0] * -1.0f, tcw->t[1] * -1.0f, tcw->t[2] * -1.0f};
+    float Ow[3];
+    se3Apply(&inv, mt, Ow);
+    int nToMatch = 0;
+    for (int i = 0; i < n_mps; i++) {
+        const mam_local_mp& mp = mps[i];
+        mam_mp_track& o = out[i];
+        std::memset(&o, 0, sizeof(o));
+        o.proj_x = -1.0f;
+        o.proj_y = -1.0f;
+        o.is_bad = mp.is_bad;
+        o.nobs = mp.nobs;
+        std::memcpy(o.desc, mp.desc, 32);
+        if (mp.seen || mp.is_bad) continue;
+        const float* P = mp.pos;
+        float Pc[3];
+        for (int r = 0; r < 3; r++) Pc[r] = (R[3 * r] * P[0] + (R[3 * r + 1] * P[1] + R[3 * r + 2] * P[2])) + tcw->t[r];
+        const float Pc_dist = std::sqrt(Pc[0] * Pc[0] + (Pc[1] * Pc[1] + Pc[2] * Pc[2]));
+        if (Pc[2] < 0.0f) continue;
+        const float u = cam->fx * Pc[0] / Pc[2] + cam->cx;   // Pinhole::project(Vector3f)
+        const float v = cam->fy * Pc[1] / Pc[2] + cam->cy;
+        if (u < g->min_x || u > g->max_x) continue;
+        if (v < g->min_y || v > g->max_y) continue;
+        o.proj_x = u;
+        o.proj_y = v;
+        const float maxDistance = 1.2f * mp.max_distance;
+        const float minDistance = 0.8f * mp.min_distance;
+        const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+        const float dist = std::sqrt(PO[0] * PO[0] + (PO[1] * PO[1] + PO[2] * PO[2]));
+        if (dist < minDistance || dist > maxDistance) continue;
+        const float viewCos = (PO[0] * mp.normal[0] + (PO[1] * mp.normal[1] + PO[2] * mp.normal[2])) / dist;
+        if (viewCos < view_cos_limit) continue;
+        const float ratio = mp.max_distance / dist;
+        int nScale = cvtX86(std::ceil(std::log(ratio) / log_scale_factor));
+        if (nScale < 0) nScale = 0;
+        else if (nScale >= g->nlevels) nScale = g->nlevels - 1;
+        o.track_in_view = 1;
+        o.track_depth = Pc_dist;
+        o.scale_level = nScale;
+        o.view_cos = viewCos;
+        nToMatch++;
+    }
+    return nToMatch;
 }
 
 // ComputeDistinctiveDescriptors for n_mps MapPoints: rows off[m] .. off[m+1]-1 of descs, in observation order.

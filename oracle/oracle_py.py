@@ -286,6 +286,27 @@ def fuse(KF, mps, cam, th=3.0):
     return n, idx[:len(mps)], dist[:len(mps)]
 
 
+def is_in_frustum(F, mps, cam, view_cos_limit=0.5, scale_factor=1.2):
+    """SearchLocalPoints' isInFrustum + PredictScale loop. Returns (nToMatch, MP_TRACK_DTYPE tracks)."""
+    from mam3slam_amd.match import LOCAL_MP_DTYPE, MP_TRACK_DTYPE, Pose
+
+    L = lib()
+    L.oracle_is_in_frustum.restype = C.c_int
+    L.oracle_is_in_frustum.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_int, C.c_void_p, C.c_float,
+                                       C.c_void_p]
+    mps = np.ascontiguousarray(mps, LOCAL_MP_DTYPE)
+    out = np.zeros(max(len(mps), 1), MP_TRACK_DTYPE)
+    T = Pose()
+    for i in range(4):
+        T.q[i] = float(F.pose[0][i])
+    for i in range(3):
+        T.t[i] = float(F.pose[1][i])
+    g = F.geom()
+    n = L.oracle_is_in_frustum(C.byref(g), C.byref(T), C.byref(cam), float(np.log(np.float32(scale_factor))), len(mps),
+                               _vp(mps), float(view_cos_limit), _vp(out))
+    return n, out[:len(mps)]
+
+
 def distinctive_descriptors(desc_off, descs):
     L = lib()
     L.oracle_distinctive_descriptors.restype = C.c_int

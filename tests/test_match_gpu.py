@@ -271,3 +271,91 @@ def test_reuse_grid_shared_context(gpu_lib, oracle, frames):
     with pytest.raises(MamError):
         sharer.search_by_projection_batch_device(FD[0], fr_bad, t_mps.data_ptr(), ms, t_nmps.data_ptr(), 1.0,
                                                  t_out.data_ptr(), t_nm.data_ptr())
+
+
+def _frustum_frame(frames, fi, seed):
+    w, h, k, d = frames[fi]
+    rng = np.random.default_rng(900 + 10 * fi + seed)
+    F = scene.make_frame_data(k, d, w, h)
+    F.pose = scene.small_pose(rng, rot=0.2, trans=0.5)
+    cam = scene.pinhole(w, h)
+    return F, cam, scene.local_world_mappoints(F, cam, rng)
+
+
+def _assert_tracks_equal(tg, to, what):
+    for f in ("proj_x", "proj_y", "track_in_view", "is_bad", "nobs", "desc"):
+        assert np.array_equal(tg[f], to[f]), f"{what}: {f}"
+    v = to["track_in_view"] == 1
+    for f in ("view_cos", "track_depth", "scale_level"):
+        assert np.array_equal(tg[f][v], to[f][v]), f"{what}: {f}"
+
+
+@pytest.mark.parametrize("fi", [0, 2])
+def test_is_in_frustum(gpu_lib, oracle, frames, fi):
+    """Frame::isInFrustum + PredictScale (SearchLocalPoints' projection loop): track fields bit-exact, nToMatch equal;
+    every level predicted somewhere, and the reject branches (behind, outside, distance, angle, bad, seen) hit."""
+    M = _matcher(0.8)
+    levels = set()
+    for seed in range(3):
+        F, cam, mps = _frustum_frame(frames, fi, seed)
+        ng, tg = M.IsInFrustum(F, mps, cam)
+        no, to = oracle.is_in_frustum(F, mps, cam)
+        assert ng == no and 0 < ng < len(mps), (ng, no, len(mps))
+        _assert_tracks_equal(tg, to, f"seed {seed}")
+        levels |= set(to["scale_level"][to["track_in_view"] == 1].tolist())
+        assert (to["proj_x"] == -1).any() and ((to["proj_x"] != -1) & (to["track_in_view"] == 0)).any()
+    assert levels == set(range(8)), levels
+
+
+def test_frustum_then_local_search_batch(gpu_lib, oracle, frames):
+    """SearchLocalPoints end to end on the device: isInFrustum for a batch of frames feeds the batched local-map
+    search (th 1, nnratio 0.8) directly in HBM; per-frame matches index-exact vs the oracle chain."""
+    import torch
+
+    from mam3slam_amd.match import LOCAL_MP_DTYPE, MP_TRACK_DTYPE, FramesDev, Pose
+
+    w, h, k, d = frames[0]
+    M = _matcher(0.8)
+    B = 4
+    Fs, mpl, cam = [], [], None
+    for s in range(B):
+        F, cam, mps = _frustum_frame(frames, 0, 10 + s)
+        Fs.append(F)
+        mpl.append(mps)
+    cap = len(k)
+    S = max(len(m) for m in mpl)
+    mp_all = np.zeros((B, S), LOCAL_MP_DTYPE)
+    tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+    for s in range(B):
+        mp_all[s, :len(mpl[s])] = mpl[s]
+        tcw[s]["q"], tcw[s]["t"] = Fs[s].pose
+    dev = torch.device("cuda", 0)
+    keys = np.zeros((B, cap), k.dtype)
+    keys[:] = k
+    desc = np.zeros((B, cap, 32), np.uint8)
+    desc[:] = d
+    d_keys = torch.from_numpy(keys.view(np.uint8).reshape(B, -1).copy()).to(dev)
+    d_desc = torch.from_numpy(desc).to(dev)
+    d_cnt = torch.tensor([[len(k), 0]] * B, dtype=torch.int32, device=dev)
+    d_mps = torch.from_numpy(mp_all.view(np.uint8).reshape(B, -1).copy()).to(dev)
+    d_n = torch.tensor([len(m) for m in mpl], dtype=torch.int32, device=dev)
+    d_tcw = torch.from_numpy(tcw.view(np.uint8).copy()).to(dev)
+    d_tr = torch.zeros((B, S * MP_TRACK_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    d_ntm = torch.zeros(B, dtype=torch.int32, device=dev)
+    d_out = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    d_nm = torch.zeros(B, dtype=torch.int32, device=dev)
+    M.is_in_frustum_batch_device(Fs[0], B, d_tcw.data_ptr(), cam, d_mps.data_ptr(), S, d_n.data_ptr(),
+                                 d_tr.data_ptr(), d_ntm.data_ptr())
+    fr = FramesDev(B, cap, d_keys.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), None, None)
+    M.search_by_projection_batch_device(Fs[0], fr, d_tr.data_ptr(), S, d_n.data_ptr(), 1.0, d_out.data_ptr(),
+                                        d_nm.data_ptr())
+    torch.cuda.synchronize()
+    tr = d_tr.cpu().numpy().view(MP_TRACK_DTYPE).reshape(B, S)
+    out, nm, ntm = d_out.cpu().numpy(), d_nm.cpu().numpy(), d_ntm.cpu().numpy()
+    for s in range(B):
+        n = len(mpl[s])
+        no, to = oracle.is_in_frustum(Fs[s], mpl[s], cam)
+        assert ntm[s] == no
+        _assert_tracks_equal(tr[s, :n], to, f"frame {s}")
+        nmo, oo = oracle.search_by_projection(Fs[s], to, 1.0, False, 50.0, 0.8)
+        assert nm[s] == nmo and np.array_equal(out[s, :len(k)], oo), s

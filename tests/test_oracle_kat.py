@@ -335,3 +335,65 @@ def test_bow_text_round_trip(tmp_path):
     assert (r.k, r.L, r.scoring, r.weighting) == (6, 3, bow.L1_NORM, bow.TF_IDF)
     assert np.array_equal(r.parent, v.parent) and np.array_equal(r.is_leaf, v.is_leaf)
     assert np.array_equal(r.desc[1:], v.desc[1:]) and np.array_equal(r.weight, v.weight)
+
+
+def _np_is_in_frustum(F, mps, cam, limit=np.float32(0.5)):
+    """isInFrustum + PredictScale (Frame.cc:512-571, MapPoint.cc:531-546) restated in numpy float32, op for op in the
+    oracle's order (Eigen rows / norm / dot as e0 + (e1 + e2)); log via float64 rounded to float32."""
+    f32 = np.float32
+    q, t = (np.asarray(F.pose[0], f32), np.asarray(F.pose[1], f32))
+    qx, qy, qz, qw = q
+    tx, ty, tz = f32(2) * qx, f32(2) * qy, f32(2) * qz
+    twx, twy, twz, txx, txy, txz = tx * qw, ty * qw, tz * qw, tx * qx, ty * qx, tz * qx
+    tyy, tyz, tzz = ty * qy, tz * qy, tz * qz
+    R = np.array([f32(1) - (tyy + tzz), txy - twz, txz + twy, txy + twz, f32(1) - (txx + tzz), tyz - twx,
+                  txz - twy, tyz + twx, f32(1) - (txx + tyy)], f32)
+    p = -t
+    iv = -q[:3]
+    uv = np.array([iv[1] * p[2] - iv[2] * p[1], iv[2] * p[0] - iv[0] * p[2], iv[0] * p[1] - iv[1] * p[0]], f32)
+    uv = uv + uv
+    cr = np.array([iv[1] * uv[2] - iv[2] * uv[1], iv[2] * uv[0] - iv[0] * uv[2], iv[0] * uv[1] - iv[1] * uv[0]], f32)
+    Ow = ((p + qw * uv) + cr) + f32(0)
+    P = mps["pos"].astype(f32)
+    Pc = [(R[3 * r] * P[:, 0] + (R[3 * r + 1] * P[:, 1] + R[3 * r + 2] * P[:, 2])) + t[r] for r in range(3)]
+    pcd = np.sqrt(Pc[0] * Pc[0] + (Pc[1] * Pc[1] + Pc[2] * Pc[2]))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        u = f32(cam.fx) * Pc[0] / Pc[2] + f32(cam.cx)
+        v = f32(cam.fy) * Pc[1] / Pc[2] + f32(cam.cy)
+    alive = (mps["seen"] == 0) & (mps["is_bad"] == 0) & ~(Pc[2] < 0)
+    inimg = alive & ~((u < 0) | (u > f32(F.width)) | (v < 0) | (v > f32(F.height)))
+    PO = [P[:, r] - Ow[r] for r in range(3)]
+    dist = np.sqrt(PO[0] * PO[0] + (PO[1] * PO[1] + PO[2] * PO[2]))
+    nr = mps["normal"].astype(f32)
+    vc = (PO[0] * nr[:, 0] + (PO[1] * nr[:, 1] + PO[2] * nr[:, 2])) / dist
+    ok = inimg & ~((dist < f32(0.8) * mps["min_distance"]) | (dist > f32(1.2) * mps["max_distance"])) & ~(vc < limit)
+    ratio = mps["max_distance"].astype(f32) / dist
+    lg = np.log(ratio.astype(np.float64)).astype(f32)
+    lvl = np.ceil(lg / f32(np.log(f32(1.2)))).astype(np.int64)
+    lvl = np.clip(lvl, 0, 7)
+    return inimg, np.where(inimg, u, f32(-1)), np.where(inimg, v, f32(-1)), ok, pcd, vc, lvl
+
+
+def test_is_in_frustum_oracle_vs_numpy(oracle):
+    """The oracle's isInFrustum loop against an independent numpy float32 restatement of the same reference lines;
+    every reject branch and every predicted level occurs."""
+    from mam3slam_amd import scene, synth
+
+    img = synth.make_frame(640, 480, agent=4, frame=2)
+    k, d, _ = oracle.extract(img, oracle.params(1000))
+    levels = set()
+    for seed in range(4):
+        rng = np.random.default_rng(70 + seed)
+        F = scene.make_frame_data(k, d, 640, 480)
+        F.pose = scene.small_pose(rng, rot=0.2, trans=0.5)
+        cam = scene.pinhole(640, 480)
+        mps = scene.local_world_mappoints(F, cam, rng)
+        n, tr = oracle.is_in_frustum(F, mps, cam)
+        inimg, u, v, ok, pcd, vc, lvl = _np_is_in_frustum(F, mps, cam)
+        assert n == int(ok.sum()) and np.array_equal(tr["track_in_view"] == 1, ok)
+        assert np.array_equal(tr["proj_x"], u) and np.array_equal(tr["proj_y"], v)
+        assert np.array_equal(tr["track_depth"][ok], pcd[ok]) and np.array_equal(tr["view_cos"][ok], vc[ok])
+        assert np.array_equal(tr["scale_level"][ok], lvl[ok])
+        levels |= set(lvl[ok].tolist())
+        assert (inimg & ~ok).any() and (~inimg).any()
+    assert levels == set(range(8))
