@@ -52,6 +52,9 @@ typedef struct mam_lba_problem {
     const uint8_t* edge_active;    /* [n_edges] 1 = level 0, 0 = setLevel(1): left out of the optimisation
                                       (initializeOptimization(0)); NULL = all edges. A vertex left without active
                                       edges keeps its estimate. edge_chi2 of an inactive edge is not written. */
+    int32_t cam_model;             /* 0 = Pinhole (cams [n_cams][4]) */
+    int32_t n_opt_poses;           /* number of poses with pose_fixed == 0: required by mam_lba_solve_batch_device
+                                      (sizes the device work before the flags are read), ignored by mam_lba_solve */
 } mam_lba_problem;
 
 typedef struct mam_lba_result {
@@ -73,13 +76,24 @@ int mam_lba_create(int device, mam_lba_ctx** out);
 void mam_lba_destroy(mam_lba_ctx* ctx);
 
 /* Host buffers in, host buffers out; synchronous. stop_flag (may be NULL) is the caller's `bool* pbStopFlag`
- * (one byte, written by another thread), polled between iterations and Levenberg trials like g2o's force-stop
- * flag (sparse_optimizer.cpp:377, levenberg.cpp:149). */
+ * (one byte, written by another thread): a flag set before the call returns the initial estimate with status 1 and
+ * no iteration, like g2o's force-stop test (sparse_optimizer.cpp:377); set during the solve, it is seen between
+ * chunks of Levenberg trials (the control flow runs on the device). */
 int mam_lba_solve(mam_lba_ctx* ctx, const mam_lba_problem* problem, const volatile uint8_t* stop_flag,
                   mam_lba_result* result);
 
+/* Q independent solves in one set of launches, everything in device memory (the multi-agent / keyframe-batch path):
+ * every array pointer of problems[q] and of results[q] (pose_q, pose_t, point_xyz, edge_chi2, edge_depth_ok) is
+ * device memory; the problem and result structs themselves are host memory. Contract: poses in ascending pose_id and
+ * points in ascending point_id order (g2o's Hessian order, sparse_optimizer.cpp:166-190; pose_id / point_id are not
+ * read) and n_opt_poses set. The Levenberg control flow runs on the device: the call enqueues whole iterations of
+ * every problem and reads the problems' states back once per chunk of trials (no host round trip per trial);
+ * results[q].iterations / lm_trials / initial_chi2 / final_chi2 / status are filled on return. Synchronous. */
+int mam_lba_solve_batch_device(mam_lba_ctx* ctx, int n_problems, const mam_lba_problem* problems,
+                               mam_lba_result* results, void* stream);
+
 int mam_lba_set_profiling(mam_lba_ctx* ctx, int enable);
-/* [0] linearize+blocks, [1] Schur, [2] dense solve, [3] back-substitution+update+chi2 */
+/* [0] structure + linearize + blocks, [1] Schur, [2] dense solve, [3] back-substitution + update + chi2 */
 int mam_lba_stage_times(mam_lba_ctx* ctx, double* ms_out, int64_t* launches_out);
 
 #ifdef __cplusplus

@@ -1,33 +1,38 @@
-// lba.hip — gfx950 Levenberg-Marquardt / Schur solve of Optimizer::LocalBundleAdjustment (include/mam_lba.h).
+// lba.hip — gfx950 Levenberg-Marquardt / Schur solve of Optimizer::LocalBundleAdjustment (include/mam_lba.h),
+// batched over independent problems (one per agent / keyframe) with the LM control flow ON THE DEVICE.
 //
-// g2o semantics (BlockSolver_6_3 + LinearSolverEigen + OptimizationAlgorithmLevenberg, FP64) re-laid out for
-// the GPU; every reduction has a fixed order so results are run-to-run reproducible:
-//   k_linearize   per edge: map, error, chi2, Huber rho, Jacobians (OptimizableTypes.cpp:139-160), the
-//                 robust-weighted terms constructQuadraticForm needs (base_binary_edge.hpp:75-112)
-//   k_point_sys   per point: H_ll, b_l over its edge segment (insertion order) and per-edge H_pl = B^T W A
-//   k_pose_sys    one wave per non-fixed pose: lanes own the 36+6 entries of H_pp, b_p; edges in order
-//   k_schur_prep  per point: D = H_ll + lambda I, D^-1, D^-1 b_l, per-edge H_pl D^-1 and H_pl D^-1 b_l
-//   k_schur_blk   one wave per 6x6 block (i1 <= i2) of the reduced camera system: lanes own entries,
-//                 contributions summed in landmark order (block_solver.hpp:372-439)
-//   k_schur_rhs   b_s = b_p - sum coefficients
-//   k_ldlt        single-workgroup blocked right-looking LDL^T of S (zero pivot = failure, as SimplicialLDLT)
-//                 + forward / diagonal / backward substitution
-//   k_backsub     x_l = D^-1 (b_l - H_pl^T x_p)  (block_solver.hpp:461-482)
-//   k_update      T <- exp(dx) T (se3quat.h), X <- X + dx on the trial copy
-//   k_chi2        robust chi2 of the trial state + computeScale terms; fixed-order block reduction
-// The LM control flow (levenberg.cpp:61-169) stays on the host and reads 3 scalars per trial.
+// g2o semantics (BlockSolver_6_3 + LinearSolverEigen + OptimizationAlgorithmLevenberg, FP64) re-laid out for the
+// GPU; every reduction has a fixed order so results are run-to-run reproducible:
+//   k_linearize   per edge: map, error, chi2, Huber rho, Jacobians (OptimizableTypes.cpp:139-160), the robust-
+//                 weighted terms constructQuadraticForm needs (base_binary_edge.hpp:75-112); chi2 partial sums
+//   k_sys         per point: H_ll, b_l over its edge segment; one wave per non-fixed pose: H_pp, b_p
+//   k_ctl_begin   iteration start (levenberg.cpp:61-77, 171-185): chi2, max diag(H), lambda_0 = 1e-5 max diag
+//   k_schur_prep  per point: D = H_ll + lambda I, D^-1, and per edge H_pl D^-1, H_pl D^-1 b_l (block_solver.hpp:
+//                 405-427)
+//   k_schur_blk   one wave per 6x6 block (i1 <= i2) of the reduced camera system, contributions in landmark
+//                 order (block_solver.hpp:372-439), and b_s = b_p - sum of coefficients
+//   k_ldlt        one workgroup per problem: blocked right-looking LDL^T of S (zero pivot = failure, as
+//                 SimplicialLDLT), f64 MFMA trailing updates, fused forward / diagonal / backward substitution
+//   k_backsub_update  x_l = D^-1 (b_l - H_pl^T x_p) (block_solver.hpp:461-482) and the trial state:
+//                 T <- exp(dx) T (se3quat.h), X <- X + dx
+//   k_ctl_end     the trial's chi2, computeScale, rho, accept (discardTop) / reject (pop), lambda update and the
+//                 termination tests of levenberg.cpp:78-169 and sparse_optimizer.cpp:355-420
+// Each kernel reads its problem's LM state (struct LM, device memory) and returns at once when the state says the
+// stage is not due: the host enqueues whole "slots" (iteration start + one trial) for every problem of a batch and
+// only synchronises once per chunk of slots (no host round trip per trial). Problems in different phases share the
+// same launches.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <type_traits>
 #include <limits>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mam_lba.h"
@@ -36,54 +41,67 @@
 namespace mam {
 namespace lba {
 
-struct Dev {
-    // problem
-    int P, L, E, Np;
+// Levenberg state of one problem (levenberg.cpp members + the optimize() loop counters)
+struct LM {
+    double lambda, ni;
+    double currentChi, iniChi, acceptedChi, initialChi;
+    int its, trials, qmax, nBad;
+    int need_lin;    // the next slot starts an iteration (linearize + build)
+    int done;        // optimize() returned
+    int cur;         // which state buffer holds the current estimate
+    int fail;        // the last LDL^T hit a zero pivot
+    int status;      // MAM_OK or MAM_ERR_*
+    int iterations;  // optimize(iterations)
+};
+
+struct Prob {
+    int P, L, E, Np, npad, n_cams, cam_model;
+    double delta;                // Huber delta; <= 0: no robust kernel
+    // inputs (point index = Hessian point index: points in ascending id order)
     const int32_t* edge_point;
     const int32_t* edge_pose;
     const double* edge_obs;
     const double* edge_w;        // invSigma2
-    const float* cams;
-    const int32_t* pose_cam;
-    const int32_t* pose_h;       // Hessian pose block of pose (-1 fixed)
-    const int32_t* hpose;        // Hessian pose block -> pose
-    const int32_t* point_h;      // Hessian point of point
-    const int32_t* hpoint;       // Hessian point -> point
-    const int32_t* pe_off;       // per Hessian point: edge segment [pe_off[h], pe_off[h+1]) into pe_idx
-    const int32_t* pe_idx;
-    const int32_t* qe_off;       // per Hessian pose: edges
-    const int32_t* qe_idx;
-    const int32_t* bp_ij;        // (i1 <= i2) per block of the upper triangle of S, row-major
-    int nbp;
-    int32_t* eidx;               // [Np][L] edge of (pose block, Hessian point), -1 if none
-    int npad;                    // padded dimension of S (ldlt_pad(6 Np))
-    double* ws;                  // global LDL^T workspace when it does not fit in LDS
-    double delta;                // Huber delta; <= 0: no robust kernel
     const uint8_t* active;       // [E] level-0 edges (NULL = all)
-    // state
-    const double* pose;          // [P][7] q(xyzw) t
-    const double* pt;            // [L][3]
-    double* pose_out;            // trial
-    double* pt_out;
+    const float* cams;           // [n_cams][4] pinhole or [n_cams][8] KB8
+    const int32_t* pose_cam;     // NULL = camera 0
+    const uint8_t* pose_fixed;
+    const double* pose_q;        // [P][4] (input, device problems)
+    const double* pose_t;        // [P][3]
+    const double* point_xyz;     // [L][3]
+    // structure
+    int32_t* pose_h;             // Hessian pose block of pose (-1 fixed)
+    int32_t* hpose;              // Hessian pose block -> pose
+    int32_t* pe_off;             // per point: edge segment [pe_off[h], pe_off[h+1]) into pe_idx (edge order)
+    int32_t* pe_idx;
+    int32_t* qe_off;             // per Hessian pose: edges (edge order)
+    int32_t* qe_idx;
+    int32_t* cnt;                // [L + Np] counters / cursors of the device structure build
+    int32_t* eidx;               // [Np][L] edge of (pose block, point), -1 if none
+    // state: [2] buffers, lm->cur is the current one
+    double* pose[2];             // [P][7] q(xyzw) t
+    double* pt[2];               // [L][3]
     // per edge
     double* err;                 // [E][2]
     double* jac;                 // [E][21]: A(6) B(12) orr(2) wo(1)
-    double* rho0;                // [E]
     double* part;                // [ceil(E / 256)] rho0 partial sums of k_linearize's blocks
     double* hpl;                 // [E][18] H_pl pose x landmark
     double* bdinv;               // [E][18] H_pl D^-1
     double* coef;                // [E][6]  H_pl D^-1 b_l
     // system
     double* Hpp;                 // [Np][36]
-    double* Hll;                 // [L][9] (Hessian point order)
+    double* Hll;                 // [L][9]
     double* b;                   // [6Np + 3L]
     double* Dinv;                // [L][9]
-    double* S;                   // [n][n]
+    double* S;                   // [npad][npad]
     double* x;                   // [6Np + 3L]
-    double* bs;                  // [6Np]
-    double* red;                 // reduction scratch
-    int* flag;
+    double* bs;                  // [npad]
+    double* ws;                  // LDL^T workspace when it does not fit in LDS
+    uint8_t* depth;              // [E] isDepthPositive of the final state
+    LM* lm;
 };
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ void quat_rotate(const double q[4], const double v[3], double o[3]) {
     double uv0 = q[1] * v[2] - q[2] * v[1], uv1 = q[2] * v[0] - q[0] * v[2], uv2 = q[0] * v[1] - q[1] * v[0];
@@ -109,11 +127,19 @@ __device__ __forceinline__ void huber(double e, double delta, double* r0, double
     }
 }
 
+// fixed-order (butterfly) wave sum: every lane ends with the same value, deterministic run to run
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 // ---- per edge: error, robust weight, Jacobians (EdgeSE3ProjectXYZ); returns the edge's rho0
-__device__ __forceinline__ double linearize_edge(const Dev& d, int e, int want_jac) {
-    const int ip = d.edge_point[e] , ipose = d.edge_pose[e];
-    const double* T = d.pose + 7 * (size_t)ipose;
-    const double* X = d.pt + 3 * (size_t)ip;
+__device__ __forceinline__ double linearize_edge(const Prob& d, const double* pose, const double* pts, int e,
+                                                 bool want_jac) {
+    const int ip = d.edge_point[e], ipose = d.edge_pose[e];
+    const double* T = pose + 7 * (size_t)ipose;
+    const double* X = pts + 3 * (size_t)ip;
     double Xc[3];
     map_point(T, X, Xc);
     const float* c = d.cams + 4 * (d.pose_cam ? d.pose_cam[ipose] : 0);
@@ -125,7 +151,6 @@ __device__ __forceinline__ double linearize_edge(const Dev& d, int e, int want_j
     d.err[2 * e + 1] = e1;
     if (d.active && !d.active[e]) {
         // setLevel(1): outside initializeOptimization(0), no term in chi2 / H / b (zeros add exactly nothing)
-        d.rho0[e] = 0.0;
         if (want_jac) {
             double* o = d.jac + 21 * (size_t)e;
             for (int k = 0; k < 21; k++) o[k] = 0.0;
@@ -138,7 +163,6 @@ __device__ __forceinline__ double linearize_edge(const Dev& d, int e, int want_j
     const double chi = e0 * (w * e0) + e1 * (w * e1);
     double r0, r1;
     huber(chi, d.delta, &r0, &r1);
-    d.rho0[e] = r0;
     if (!want_jac) return r0;
     const double x = Xc[0], y = Xc[1], z = Xc[2];
     const double J0 = -(fx / z), J2 = -(-fx * x / (z * z)), J4 = -(fy / z), J5 = -(-fy * y / (z * z));
@@ -166,53 +190,225 @@ __device__ __forceinline__ double linearize_edge(const Dev& d, int e, int want_j
         const double wo = r1 * w;
         double* hp = d.hpl + 18 * (size_t)e;
         for (int a = 0; a < 6; a++)
-            for (int c = 0; c < 3; c++) hp[3 * a + c] = o[6 + a] * wo * o[c] + o[12 + a] * wo * o[3 + c];
+            for (int c2 = 0; c2 < 3; c2++) hp[3 * a + c2] = o[6 + a] * wo * o[c2] + o[12 + a] * wo * o[3 + c2];
     }
     return r0;
 }
 
-// Per block of 256 edges: the rho0 partial sum in a fixed order (butterfly per wave, then the 4 waves in order), so
-// the chi2 reduction is one short pass over the partials
-__global__ __launch_bounds__(256) void k_linearize(Dev d, int want_jac) {
-    __shared__ double ws[4];
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    double r = e < d.E ? linearize_edge(d, e, want_jac) : 0.0;
+// ================================================================================== device structure build
+// For problems whose arrays are already in HBM (mam_lba_solve_batch_device): poses and points come in ascending id
+// order (g2o's Hessian order, sparse_optimizer.cpp:166-190), so the pose blocks are a prefix count of the non-fixed
+// poses and the point blocks are the identity; the per-point / per-pose edge lists (edge order) and the pose x point
+// edge table are built here.
+
+// grid (32, Q) x 1024: block 0 scans pose_fixed -> pose_h / hpose; every block clears counters, eidx and S and seeds
+// the state buffers (SE3Quat(q, t) normalises: w >= 0, unit).
+__global__ __launch_bounds__(1024) void k_struct_init(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    if (d.lm->status) return;
+    const int t = threadIdx.x;
+    const int gstride = gridDim.x * 1024, g0 = blockIdx.x * 1024 + t;
+    if (blockIdx.x == 0) {
+        __shared__ int wsum[16];
+        // pose_h: prefix count of non-fixed poses, P <= 1024 per pass
+        int base = 0;
+        for (int c0 = 0; c0 < d.P; c0 += 1024) {
+            const int i = c0 + t;
+            const int nf = (i < d.P && !d.pose_fixed[i]) ? 1 : 0;
+            int v = nf;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = r;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int u = __shfl_up(v, o, 64);
+                if (lane_id() >= o) v += u;
+            }
+            if (lane_id() == 63) wsum[t >> 6] = v;
+            __syncthreads();
+            int pre = 0, tot = 0;
+            for (int w = 0; w < 16; w++) {
+                if (w < (t >> 6)) pre += wsum[w];
+                tot += wsum[w];
+            }
+            if (i < d.P) {
+                const int h = base + pre + v - nf;
+                d.pose_h[i] = nf ? h : -1;
+                if (nf) d.hpose[h] = i;
+            }
+            base += tot;
+            __syncthreads();
+        }
+    }
+    for (int i = g0; i < d.L + d.Np; i += gstride) d.cnt[i] = 0;
+    for (size_t i = g0; i < (size_t)d.Np * d.L; i += gstride) d.eidx[i] = -1;
+    for (size_t i = g0; i < (size_t)d.npad * d.npad; i += gstride) d.S[i] = 0.0;
+    for (int i = g0; i < d.P; i += gstride) {
+        double q[4] = {d.pose_q[4 * i], d.pose_q[4 * i + 1], d.pose_q[4 * i + 2], d.pose_q[4 * i + 3]};
+        if (q[3] < 0) for (int k = 0; k < 4; k++) q[k] = -q[k];
+        const double nq = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        for (int k = 0; k < 4; k++) d.pose[0][7 * (size_t)i + k] = q[k] / nq;
+        for (int k = 0; k < 3; k++) d.pose[0][7 * (size_t)i + 4 + k] = d.pose_t[3 * i + k];
+    }
+    for (int i = g0; i < 3 * d.L; i += gstride) d.pt[0][i] = d.point_xyz[i];
+}
+
+// grid (ceil(E/256), Q): per-point and per-pose edge counts; index validation
+__global__ __launch_bounds__(256) void k_struct_count(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= d.E || d.lm->status) return;
+    const int ip = d.edge_point[e], ipose = d.edge_pose[e];
+    if (ip < 0 || ip >= d.L || ipose < 0 || ipose >= d.P) {
+        d.lm->status = MAM_ERR_ARG;
+        return;
+    }
+    atomicAdd(&d.cnt[ip], 1);
+    const int h = d.pose_h[ipose];
+    if (h >= 0) atomicAdd(&d.cnt[d.L + h], 1);
+}
+
+__device__ void block_excl_scan(const int32_t* in, int32_t* out, int n, int32_t* total_out) {
+    __shared__ int wsum[16];
+    __shared__ int carry;
+    const int t = threadIdx.x;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+        const int i = c0 + t;
+        const int a = i < n ? in[i] : 0;
+        int v = a;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(v, o, 64);
+            if (lane_id() >= o) v += u;
+        }
+        if (lane_id() == 63) wsum[t >> 6] = v;
+        __syncthreads();
+        int pre = 0, tot = 0;
+        for (int w = 0; w < 16; w++) {
+            if (w < (t >> 6)) pre += wsum[w];
+            tot += wsum[w];
+        }
+        if (i < n) out[i] = carry + pre + v - a;
+        __syncthreads();
+        if (t == 0) carry += tot;
+        __syncthreads();
+    }
+    if (t == 0) *total_out = carry;
+}
+
+// grid (1, Q) x 1024: exclusive scans -> pe_off, qe_off; counters reset to be the scatter cursors
+__global__ __launch_bounds__(1024) void k_struct_scan(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    if (d.lm->status) return;
+    block_excl_scan(d.cnt, d.pe_off, d.L, d.pe_off + d.L);
+    block_excl_scan(d.cnt + d.L, d.qe_off, d.Np, d.qe_off + d.Np);
+    __syncthreads();
+    for (int i = threadIdx.x; i < d.L + d.Np; i += 1024) d.cnt[i] = 0;
+}
+
+// grid (ceil(E/256), Q): scatter into the lists (order fixed by k_struct_sort) and the pose x point table
+__global__ __launch_bounds__(256) void k_struct_scatter(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= d.E || d.lm->status) return;
+    const int ip = d.edge_point[e];
+    d.pe_idx[d.pe_off[ip] + atomicAdd(&d.cnt[ip], 1)] = e;
+    const int h = d.pose_h[d.edge_pose[e]];
+    if (h >= 0) {
+        d.qe_idx[d.qe_off[h] + atomicAdd(&d.cnt[d.L + h], 1)] = e;
+        d.eidx[(size_t)h * d.L + ip] = e;
+    }
+}
+
+// grid (ceil(L/256) + Np, Q) x 256: restore edge order inside every list — per point an insertion sort by one thread
+// (a handful of observations), per pose a rank sort of its segment staged in LDS (chunks of 4096 when longer: a
+// bitonic-free merge is not needed because every chunk's ranks are counted over the whole segment)
+__global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    if (d.lm->status) return;
+    const int nb_pts = (d.L + 255) / 256;
+    if ((int)blockIdx.x < nb_pts) {
+        const int h = blockIdx.x * 256 + threadIdx.x;
+        if (h >= d.L) return;
+        int32_t* s = d.pe_idx + d.pe_off[h];
+        const int n = d.pe_off[h + 1] - d.pe_off[h];
+        for (int k = 1; k < n; k++) {
+            const int v = s[k];
+            int m = k - 1;
+            while (m >= 0 && s[m] > v) { s[m + 1] = s[m]; m--; }
+            s[m + 1] = v;
+        }
+        return;
+    }
+    const int h = blockIdx.x - nb_pts;
+    if (h >= d.Np) return;
+    constexpr int CH = 4096;
+    __shared__ int32_t seg[CH];
+    int32_t* s = d.qe_idx + d.qe_off[h];
+    const int n = d.qe_off[h + 1] - d.qe_off[h];
+    if (n <= CH) {
+        for (int i = threadIdx.x; i < n; i += 256) seg[i] = s[i];
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += 256) {
+            const int v = seg[i];
+            int r = 0;
+            for (int j = 0; j < n; j++) r += seg[j] < v;   // edge ids are distinct
+            s[r] = v;
+        }
+    } else {
+        // long segments (global BA): odd-even transposition in place, n rounds
+        for (int round = 0; round < n; round++) {
+            for (int i = 2 * threadIdx.x + (round & 1); i + 1 < n; i += 512) {
+                const int a = s[i], b = s[i + 1];
+                if (a > b) { s[i] = b; s[i + 1] = a; }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ======================================================================================================= solve
+// Per block of 256 edges: the rho0 partial sum in a fixed order (butterfly per wave, then the 4 waves in order).
+// mode 0: iteration start (Jacobians, current state); 1: trial (errors only, trial state); 2: initial chi2.
+__global__ __launch_bounds__(256) void k_linearize(const Prob* __restrict__ probs, int mode) {
+    const Prob& d = probs[blockIdx.y];
+    const LM& lm = *d.lm;
+    if (lm.status || (mode != 2 && lm.done) || (mode == 0 && !lm.need_lin)) return;
+    if ((int)blockIdx.x * 256 >= d.E) return;
+    __shared__ double ws[4];
+    const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0) : 0.0;
+    r = wave_sum_d(r);
+    if (lane_id() == 0) ws[threadIdx.x >> 6] = r;
     __syncthreads();
     if (threadIdx.x == 0) d.part[blockIdx.x] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
 }
 
-// ---- per point: H_ll, b_l (edge order, as constructQuadraticForm runs edge by edge)
-__global__ __launch_bounds__(64) void k_point_sys(Dev d) {
-    const int h = blockIdx.x * 64 + threadIdx.x;
-    if (h >= d.L) return;
-    double H[9] = {0}, bl[3] = {0};
-    for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
-        const int e = d.pe_idx[s];
-        const double* j = d.jac + 21 * (size_t)e;
-        const double wo = j[20];
-        for (int a = 0; a < 3; a++) {
-            bl[a] += j[a] * j[18] + j[3 + a] * j[19];
-            for (int c = 0; c < 3; c++) H[3 * a + c] += j[a] * wo * j[c] + j[3 + a] * wo * j[3 + c];
+// grid (ceil(L/64) + Np, Q) x 64: H_ll, b_l per point (edge order, one thread each) and H_pp, b_p per optimised pose
+// (one wave: lanes own strided edges, 27 register sums, fixed-order wave reduction)
+__global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const LM& lm = *d.lm;
+    if (lm.status || lm.done || !lm.need_lin) return;
+    const int nb_pts = (d.L + 63) / 64;
+    if ((int)blockIdx.x < nb_pts) {
+        const int h = blockIdx.x * 64 + threadIdx.x;
+        if (h >= d.L) return;
+        double H[9] = {0}, bl[3] = {0};
+        for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
+            const double* j = d.jac + 21 * (size_t)d.pe_idx[s];
+            const double wo = j[20];
+            for (int a = 0; a < 3; a++) {
+                bl[a] += j[a] * j[18] + j[3 + a] * j[19];
+                for (int c = 0; c < 3; c++) H[3 * a + c] += j[a] * wo * j[c] + j[3 + a] * wo * j[3 + c];
+            }
         }
+        for (int k = 0; k < 9; k++) d.Hll[9 * (size_t)h + k] = H[k];
+        for (int k = 0; k < 3; k++) d.b[6 * (size_t)d.Np + 3 * (size_t)h + k] = bl[k];
+        return;
     }
-    for (int k = 0; k < 9; k++) d.Hll[9 * (size_t)h + k] = H[k];
-    for (int k = 0; k < 3; k++) d.b[6 * (size_t)d.Np + 3 * (size_t)h + k] = bl[k];
-}
-
-// fixed-order (butterfly) wave sum: every lane ends with the same value, deterministic run to run
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// ---- one wave per non-fixed pose: lanes stride over the pose's edges, accumulate the 21 upper entries of
-// H_pp and the 6 of b_p in registers, then a fixed-order wave reduction
-__global__ __launch_bounds__(64) void k_pose_sys(Dev d) {
-    const int h = blockIdx.x, lane = threadIdx.x;
+    const int h = blockIdx.x - nb_pts, lane = threadIdx.x;
+    if (h >= d.Np) return;
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
@@ -241,47 +437,90 @@ __global__ __launch_bounds__(64) void k_pose_sys(Dev d) {
     }
 }
 
-// ---- fixed-order sum of rho0 (and max diag) in one workgroup. RED threads: a small workgroup finds room on a CU
-// that Tracking's concurrent launches keep busy (a 1024-thread one waits for 16 free wave slots at once).
-#ifndef MAM_LBA_RED_THREADS
-#define MAM_LBA_RED_THREADS 256
-#endif
-constexpr int RED = MAM_LBA_RED_THREADS;
-
-__global__ __launch_bounds__(RED) void k_reduce_chi(Dev d, int slot) {
-    __shared__ double s[RED];
+// fixed-order sum over a 256-thread block (strided per-thread sums, then a tree): the order k_reduce_chi used
+constexpr int RED = 256;
+__device__ double block_sum(double acc, double* s) {
     const int t = threadIdx.x;
-    double acc = 0.0;
-    const int nb = (d.E + 255) / 256;
-    for (int b = t; b < nb; b += RED) acc += d.part[b];
     s[t] = acc;
     __syncthreads();
     for (int o = RED / 2; o > 0; o >>= 1) {
         if (t < o) s[t] += s[t + o];
         __syncthreads();
     }
-    if (t == 0) d.red[slot] = s[0];
+    const double r = s[0];
+    __syncthreads();
+    return r;
 }
 
-__global__ __launch_bounds__(RED) void k_max_diag(Dev d) {
+__device__ double chi_of_parts(const Prob& d, double* s) {
+    double acc = 0.0;
+    const int nb = (d.E + 255) / 256;
+    for (int b = threadIdx.x; b < nb; b += RED) acc += d.part[b];
+    return block_sum(acc, s);
+}
+
+// grid (Q) x 256: the initial activeRobustChi2 (optimize() entry)
+__global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs) {
     __shared__ double s[RED];
-    const int t = threadIdx.x;
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status) return;
+    const double chi = chi_of_parts(d, s);
+    if (threadIdx.x == 0) {
+        lm.initialChi = chi;
+        lm.acceptedChi = chi;
+        lm.currentChi = chi;
+        lm.lambda = -1.0;
+        lm.ni = 2.0;
+        lm.its = lm.trials = lm.qmax = lm.nBad = 0;
+        lm.fail = 0;
+        lm.need_lin = 1;
+        lm.done = (d.Np + d.L == 0 || lm.iterations <= 0) ? 1 : 0;
+    }
+}
+
+// grid (Q) x 256: iteration start
+__global__ __launch_bounds__(RED) void k_ctl_begin(const Prob* __restrict__ probs) {
+    __shared__ double s[RED];
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done || !lm.need_lin) return;
+    const double chi = chi_of_parts(d, s);
     double m = 0.0;
-    for (int i = t; i < 6 * d.Np; i += RED) m = fmax(m, fabs(d.Hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
-    for (int i = t; i < 3 * d.L; i += RED) m = fmax(m, fabs(d.Hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
-    s[t] = m;
+    for (int i = threadIdx.x; i < 6 * d.Np; i += RED) m = fmax(m, fabs(d.Hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
+    for (int i = threadIdx.x; i < 3 * d.L; i += RED) m = fmax(m, fabs(d.Hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
+    s[threadIdx.x] = m;
     __syncthreads();
     for (int o = RED / 2; o > 0; o >>= 1) {
-        if (t < o) s[t] = fmax(s[t], s[t + o]);
+        if (threadIdx.x < o) s[threadIdx.x] = fmax(s[threadIdx.x], s[threadIdx.x + o]);
         __syncthreads();
     }
-    if (t == 0) d.red[2] = s[0];
+    if (threadIdx.x == 0) {
+        if (lm.its == 0) {
+            // levenberg.cpp:71-77: lambda_0 = tau * max diag(H), tau = 1e-5 (computeLambdaInit :171-185)
+            lm.currentChi = chi;
+            lm.lambda = 1e-5 * s[0];
+            lm.ni = 2.0;
+            lm.nBad = 0;
+        } else {
+            // the chi2 of the accepted trial, bit for bit (same kernels on the same state)
+            lm.currentChi = lm.acceptedChi;
+        }
+        lm.iniChi = lm.currentChi;
+        lm.qmax = 0;
+        lm.need_lin = 0;
+    }
 }
 
 // ---- Schur
-__global__ __launch_bounds__(64) void k_schur_prep(Dev d, double lambda) {
+// grid (ceil(L/64), Q) x 64: per point D^-1 and its edges' H_pl D^-1 and coefficients (block_solver.hpp:405-427)
+__global__ __launch_bounds__(64) void k_schur_prep(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const LM& lm = *d.lm;
+    if (lm.status || lm.done) return;
     const int h = blockIdx.x * 64 + threadIdx.x;
     if (h >= d.L) return;
+    const double lambda = lm.lambda;
     double D[9];
     for (int k = 0; k < 9; k++) D[k] = d.Hll[9 * (size_t)h + k] + ((k % 4 == 0) ? lambda : 0.0);
     const double c00 = D[4] * D[8] - D[5] * D[7], c01 = D[5] * D[6] - D[3] * D[8], c02 = D[3] * D[7] - D[4] * D[6];
@@ -293,44 +532,60 @@ __global__ __launch_bounds__(64) void k_schur_prep(Dev d, double lambda) {
     Di[2] = (D[1] * D[5] - D[2] * D[4]) / det; Di[5] = (D[2] * D[3] - D[0] * D[5]) / det;
     Di[8] = (D[0] * D[4] - D[1] * D[3]) / det;
     for (int k = 0; k < 9; k++) d.Dinv[9 * (size_t)h + k] = Di[k];
-}
-
-// per edge (optimised pose): H_pl D^-1 and the coefficient H_pl D^-1 b_l (block_solver.hpp:405-427)
-__global__ __launch_bounds__(256) void k_schur_edge(Dev d) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= d.E || d.pose_h[d.edge_pose[e]] < 0) return;
-    const int h = d.point_h[d.edge_point[e]];
-    const double* Di = d.Dinv + 9 * (size_t)h;
     const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)h;
     double db[3];
     for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
-    const double* B = d.hpl + 18 * (size_t)e;
-    double* o = d.bdinv + 18 * (size_t)e;
-    double* cf = d.coef + 6 * (size_t)e;
-    for (int i = 0; i < 6; i++) {
-        for (int j = 0; j < 3; j++) o[3 * i + j] = B[3 * i] * Di[j] + B[3 * i + 1] * Di[3 + j] + B[3 * i + 2] * Di[6 + j];
-        cf[i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
+    for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
+        const int e = d.pe_idx[s];
+        if (d.pose_h[d.edge_pose[e]] < 0) continue;
+        const double* B = d.hpl + 18 * (size_t)e;
+        double* o = d.bdinv + 18 * (size_t)e;
+        double* cf = d.coef + 6 * (size_t)e;
+        for (int i = 0; i < 6; i++) {
+            for (int j = 0; j < 3; j++)
+                o[3 * i + j] = B[3 * i] * Di[j] + B[3 * i + 1] * Di[3 + j] + B[3 * i + 2] * Di[6 + j];
+            cf[i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
+        }
     }
 }
 
-__global__ __launch_bounds__(256) void k_eidx(Dev d) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= d.E) return;
-    const int hp = d.pose_h[d.edge_pose[e]];
-    if (hp >= 0) d.eidx[(size_t)hp * d.L + d.point_h[d.edge_point[e]]] = e;
-}
-
-__global__ __launch_bounds__(64) void k_schur_blk(Dev d, double lambda) {
-    const int bp = blockIdx.x, lane = threadIdx.x;
-    const int i1 = d.bp_ij[2 * bp], i2 = d.bp_ij[2 * bp + 1];
+// grid (Np * Np + Np, Q) x 64: one wave per block (i1 <= i2) of S (blocks with i2 < i1 exit), landmarks seen by both
+// poses walked through pose i2's edges and pose i1's edge-table row; then one wave per pose for b_s.
+__global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const LM& lm = *d.lm;
+    if (lm.status || lm.done) return;
+    const int lane = threadIdx.x;
+    const int nb2 = d.Np * d.Np;
+    if ((int)blockIdx.x >= nb2) {
+        const int h = blockIdx.x - nb2;
+        if (h >= d.Np) return;
+        double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int s = d.qe_off[h] + lane; s < d.qe_off[h + 1]; s += 64) {
+            const double* c = d.coef + 6 * (size_t)d.qe_idx[s];
+#pragma unroll
+            for (int k = 0; k < 6; k++) acc[k] += c[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) acc[k] = wave_sum_d(acc[k]);
+        if (lane < 6) {
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; k++) v = (k == lane) ? acc[k] : v;
+            d.bs[6 * (size_t)h + lane] = d.b[6 * (size_t)h + lane] - v;
+        }
+        return;
+    }
+    const int i1 = blockIdx.x / d.Np, i2 = blockIdx.x % d.Np;
+    if (i2 < i1) return;
+    const double lambda = lm.lambda;
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
-    // landmarks seen by both poses: walk pose i2's edges, look up pose i1's edge of the same landmark
     const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
     for (int s = d.qe_off[i2] + lane; s < d.qe_off[i2 + 1]; s += 64) {
         const int ec = d.qe_idx[s];
-        const int ea = ei1[d.point_h[d.edge_point[ec]]];
+        const int ea = ei1[d.edge_point[ec]];
         if (ea < 0) continue;
         const double* W = d.bdinv + 18 * (size_t)ea;
         const double* B = d.hpl + 18 * (size_t)ec;
@@ -340,7 +595,8 @@ __global__ __launch_bounds__(64) void k_schur_blk(Dev d, double lambda) {
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int c = 0; c < 6; c++) acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
+            for (int c = 0; c < 6; c++)
+                acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
     }
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = wave_sum_d(acc[k]);
@@ -357,26 +613,7 @@ __global__ __launch_bounds__(64) void k_schur_blk(Dev d, double lambda) {
     }
 }
 
-// b_s = b_p - sum of the pose's coefficients: lanes stride the pose's edges, fixed-order wave reduction
-__global__ __launch_bounds__(64) void k_schur_rhs(Dev d) {
-    const int h = blockIdx.x, lane = threadIdx.x;
-    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int s = d.qe_off[h] + lane; s < d.qe_off[h + 1]; s += 64) {
-        const double* c = d.coef + 6 * (size_t)d.qe_idx[s];
-#pragma unroll
-        for (int k = 0; k < 6; k++) acc[k] += c[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 6; k++) acc[k] = wave_sum_d(acc[k]);
-    if (lane < 6) {
-        double v = 0.0;
-#pragma unroll
-        for (int k = 0; k < 6; k++) v = (k == lane) ? acc[k] : v;
-        d.bs[6 * (size_t)h + lane] = d.b[6 * (size_t)h + lane] - v;
-    }
-}
-
-// ---- dense LDL^T solve of S x = bs: one workgroup of 1024 threads, blocked right-looking, NB = 16 panels.
+// ---- dense LDL^T solve of S x = bs: one workgroup per problem, blocked right-looking, NB = 16 panels.
 // S is npad x npad (npad = 6 Np rounded up to 16; the padding is an identity block after the real unknowns, so it
 // changes nothing and every panel is full). Per panel:
 //   (1) wave 0 factors the 16x16 diagonal block in registers: lane i owns row i, the pivot row is read with
@@ -385,14 +622,14 @@ __global__ __launch_bounds__(64) void k_schur_rhs(Dev d) {
 //       workspace for the trailing update) and the fused forward-substitution update y2 -= L21 y1;
 //   (3) the trailing lower triangle A22 -= L21 W21^T in 16x16 blocks, one wave each, as f64 MFMAs
 //       (v_mfma_f64_16x16x4_f64) with both operands from the workspace.
-// An exact zero pivot sets flag[0] (the failure rule of Eigen's SimplicialLDLT) and skips the solve.
+// An exact zero pivot sets lm.fail (the failure rule of Eigen's SimplicialLDLT) and skips the solve.
 // Then y /= D and the backward substitution L^T x = y, block by block, each thread updating its own y_i.
-// The workspace (panel + y) is LDS when it fits (use_lds), else a global scratch buffer.
+// The workspace (panel + y) is LDS when it fits (use_lds), else the problem's global scratch.
 constexpr int NB = 16;
 #ifndef MAM_LDLT_THREADS
 #define MAM_LDLT_THREADS 512
 #endif
-constexpr int LDLT_THREADS = MAM_LDLT_THREADS;   // 16 waves: 4 per SIMD hide the MFMA / memory latency
+constexpr int LDLT_THREADS = MAM_LDLT_THREADS;
 
 __host__ __device__ inline int ldlt_pad(int n) { return (n + NB - 1) / NB * NB; }
 
@@ -412,8 +649,6 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 
 // wave 0: LDL^T of the 16x16 diagonal block at kb (final on entry), written back to A (L below, D on the diagonal),
 // plus Ld (L11, row-major), dk / invdk (D and 1/D) for the panel rows, and the forward block solve of y.
-// Right-looking inside the block: at step j the pivot d_j is lane j's current diagonal, column j is scaled
-// (l_ij = a_ij / d_j) and broadcast by v_readlane, and every lane i > j updates a_ik -= l_ij d_j l_kj, j < k <= i.
 __device__ __forceinline__ void ldlt_diag(double* A, int N, int kb, double* Y, double* Ld, double* dk, double* invdk,
                                           int* fail, int lane) {
     double row[NB];
@@ -486,13 +721,20 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
     *tc = q - r * (r + 1) / 2;
 }
 
-// With lookahead: after a panel's rows (B), the next block column is updated first (C1); then wave 0 factors the
-// next diagonal block while the other waves update the rest of the trailing matrix (C2).
+// grid (Q): with lookahead — after a panel's rows (B), the next block column is updated first (C1); then wave 0
+// factors the next diagonal block while the other waves update the rest of the trailing matrix (C2).
 template <bool use_lds>
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
     extern __shared__ __attribute__((aligned(16))) double lds_ws[];
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done) return;
     const int n = 6 * d.Np, N = d.npad;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (n == 0) {
+        if (t == 0) lm.fail = 0;
+        return;
+    }
     double* A = d.S;
     double* ws = use_lds ? lds_ws : d.ws;
     double* Y = ws + (size_t)2 * NB * (N - NB);
@@ -502,19 +744,12 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
     __shared__ int fail;
     if (t == 0) fail = 0;
     for (int i = t; i < N; i += LDLT_THREADS) {
-        Y[i] = d.bs[i];
+        Y[i] = i < n ? d.bs[i] : 0.0;
         if (i >= n) A[(size_t)i * N + i] = 1.0;
     }
     __syncthreads();
-#ifdef MAM_LDLT_PROFILE
-    long long tp0 = clock64(), tacc[4] = {0, 0, 0, 0};
-#define LDLT_PHASE(k) do { const long long tn = clock64(); tacc[k] += tn - tp0; tp0 = tn; } while (0)
-#else
-#define LDLT_PHASE(k) do {} while (0)
-#endif
     if (wid == 0) ldlt_diag(A, N, 0, Y, Ld, dk, invdk, &fail, lane);
     __syncthreads();
-    LDLT_PHASE(0);
     for (int kb = 0; kb < N; kb += NB) {
         // (B) panel rows: L21 = A21 L11^-T D^-1, W21 = L21 D (staged transposed), y2 -= L21 y1
         const int m = N - kb - NB;
@@ -543,13 +778,11 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
             Y[i] = yi;
         }
         __syncthreads();
-        LDLT_PHASE(1);
         if (m == 0) break;
         const int T16 = m / 16;
         // (C1) the next block column: blocks (br, 0), one wave each
         for (int br = wid; br < T16; br += LDLT_THREADS / 64) ldlt_tile16(A, N, kb, PL, PW, m, br, 0, lane);
         __syncthreads();
-        LDLT_PHASE(2);
         // (C2) wave 0 factors the next diagonal block; the other waves update the blocks with bc >= 1
         if (wid == 0) {
             ldlt_diag(A, N, kb + NB, Y, Ld, dk, invdk, &fail, lane);
@@ -563,12 +796,8 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
             }
         }
         __syncthreads();
-        LDLT_PHASE(0);
     }
-#ifdef MAM_LDLT_PROFILE
-    if (t == 0) for (int k = 0; k < 3; k++) d.red[4 + k] += (double)tacc[k];
-#endif
-    if (t == 0) d.flag[0] = fail;
+    if (t == 0) lm.fail = fail;
     if (fail) return;   // uniform (LDS flag after the last barrier)
     // y /= D
     for (int i = t; i < N; i += LDLT_THREADS) Y[i] /= A[(size_t)i * N + i];
@@ -597,28 +826,6 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(Dev d) {
         __syncthreads();
     }
     for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
-#ifdef MAM_LDLT_PROFILE
-    __syncthreads();
-    if (t == 0) d.red[7] += (double)(clock64() - tp0);
-#endif
-}
-
-__global__ __launch_bounds__(256) void k_backsub(Dev d) {
-    const int h = blockIdx.x * 256 + threadIdx.x;
-    if (h >= d.L) return;
-    double cl[3];
-    for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)h + k];
-    for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
-        const int e = d.pe_idx[s];
-        const int hp = d.pose_h[d.edge_pose[e]];
-        if (hp < 0) continue;
-        const double* B = d.hpl + 18 * (size_t)e;
-        for (int j = 0; j < 3; j++)
-            for (int i = 0; i < 6; i++) cl[j] -= B[3 * i + j] * d.x[6 * (size_t)hp + i];
-    }
-    const double* Di = d.Dinv + 9 * (size_t)h;
-    for (int i = 0; i < 3; i++)
-        d.x[6 * (size_t)d.Np + 3 * (size_t)h + i] = Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1] + Di[3 * i + 2] * cl[2];
 }
 
 // Eigen Quaterniond(Matrix3d)
@@ -651,12 +858,39 @@ __device__ void normalize_q(double q[4]) {
     q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
 }
 
-// T <- exp(dx) * T (VertexSE3Expmap::oplusImpl) for non-fixed poses; X <- X + dx for points; fixed copied.
-__global__ __launch_bounds__(256) void k_update(Dev d) {
+// grid (ceil(max(P, L)/256), Q): x_l = D^-1 (b_l - H_pl^T x_p) per point (skipped after a failed factorization:
+// BlockSolver::solve returns before the back-substitution and the update applies the old x), then the trial state:
+// T <- exp(dx) * T (VertexSE3Expmap::oplusImpl) for optimised poses, X <- X + dx, fixed poses copied.
+__global__ __launch_bounds__(256) void k_backsub_update(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const LM& lm = *d.lm;
+    if (lm.status || lm.done) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
+    const double* pose = d.pose[lm.cur];
+    const double* pts = d.pt[lm.cur];
+    double* pose_out = d.pose[1 - lm.cur];
+    double* pt_out = d.pt[1 - lm.cur];
+    if (i < d.L) {
+        double* xl = d.x + 6 * (size_t)d.Np + 3 * (size_t)i;
+        if (!lm.fail) {
+            double cl[3];
+            for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)i + k];
+            for (int s = d.pe_off[i]; s < d.pe_off[i + 1]; s++) {
+                const int e = d.pe_idx[s];
+                const int hp = d.pose_h[d.edge_pose[e]];
+                if (hp < 0) continue;
+                const double* B = d.hpl + 18 * (size_t)e;
+                for (int j = 0; j < 3; j++)
+                    for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * d.x[6 * (size_t)hp + k];
+            }
+            const double* Di = d.Dinv + 9 * (size_t)i;
+            for (int k = 0; k < 3; k++) xl[k] = Di[3 * k] * cl[0] + Di[3 * k + 1] * cl[1] + Di[3 * k + 2] * cl[2];
+        }
+        for (int k = 0; k < 3; k++) pt_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + xl[k];
+    }
     if (i < d.P) {
-        const double* T = d.pose + 7 * (size_t)i;
-        double* O = d.pose_out + 7 * (size_t)i;
+        const double* T = pose + 7 * (size_t)i;
+        double* O = pose_out + 7 * (size_t)i;
         const int h = d.pose_h[i];
         if (h < 0) {
             for (int k = 0; k < 7; k++) O[k] = T[k];
@@ -667,7 +901,8 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
             const double Om[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
             double Om2[9];
             for (int r = 0; r < 3; r++)
-                for (int c = 0; c < 3; c++) Om2[3 * r + c] = Om[3 * r] * Om[c] + Om[3 * r + 1] * Om[3 + c] + Om[3 * r + 2] * Om[6 + c];
+                for (int c = 0; c < 3; c++)
+                    Om2[3 * r + c] = Om[3 * r] * Om[c] + Om[3 * r + 1] * Om[3 + c] + Om[3 * r + 2] * Om[6 + c];
             double R[9], V[9];
             if (theta < 0.00001) {
                 for (int k = 0; k < 9; k++) { R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + Om2[k]; V[k] = R[k]; }
@@ -698,34 +933,64 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
             O[4] = te[0] + rt[0]; O[5] = te[1] + rt[1]; O[6] = te[2] + rt[2];
         }
     }
-    if (i < d.L) {
-        const int p = d.hpoint[i];
-        for (int k = 0; k < 3; k++) d.pt_out[3 * (size_t)p + k] = d.pt[3 * (size_t)p + k] + d.x[6 * (size_t)d.Np + 3 * (size_t)i + k];
-    }
 }
 
-// sum_j x_j (lambda x_j + b_j) in fixed order (computeScale)
-__global__ __launch_bounds__(RED) void k_scale(Dev d, double lambda) {
+// grid (Q) x 256: end of a trial — levenberg.cpp:108-158 (rho, accept / reject, lambda), then the iteration-end
+// tests of levenberg.cpp:159-168 and sparse_optimizer.cpp:381-409.
+__global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs) {
     __shared__ double s[RED];
-    const int t = threadIdx.x;
-    const int n = 6 * d.Np + 3 * d.L;
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done) return;
+    const double lambda = lm.lambda;
+    double tempChi = chi_of_parts(d, s);
+    // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194)
     double acc = 0.0;
-    for (int j = t; j < n; j += RED) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
-    s[t] = acc;
-    __syncthreads();
-    for (int o = RED / 2; o > 0; o >>= 1) {
-        if (t < o) s[t] += s[t + o];
-        __syncthreads();
+    const int nx = 6 * d.Np + 3 * d.L;
+    for (int j = threadIdx.x; j < nx; j += RED) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
+    const double scale0 = block_sum(acc, s);
+    if (threadIdx.x != 0) return;
+    if (lm.fail) tempChi = DBL_MAX;
+    double rho = lm.currentChi - tempChi;
+    const double scale = scale0 + 1e-3;
+    rho /= scale;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow((2 * rho - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        const double scaleFactor = fmax(1. / 3., alpha);
+        lm.lambda = lambda * scaleFactor;
+        lm.ni = 2;
+        lm.currentChi = tempChi;
+        lm.acceptedChi = tempChi;
+        lm.cur = 1 - lm.cur;   // accept: discardTop
+    } else {
+        lm.lambda = lambda * lm.ni;   // reject: pop
+        lm.ni *= 2;
     }
-    if (t == 0) d.red[1] = s[0];
+    lm.qmax++;
+    lm.trials++;
+    if (rho < 0 && lm.qmax < 10) return;   // another trial of this iteration
+    lm.its++;
+    bool term = false;
+    if (lm.qmax == 10 || rho == 0) term = true;
+    else {
+        if ((lm.iniChi - lm.currentChi) * 1e3 < lm.iniChi) lm.nBad++;
+        else lm.nBad = 0;
+        if (lm.nBad >= 3) term = true;
+    }
+    if (term || lm.its >= lm.iterations) lm.done = 1;
+    else lm.need_lin = 1;
 }
 
-__global__ __launch_bounds__(256) void k_depth(Dev d, uint8_t* out) {
+// grid (ceil(E/256), Q): isDepthPositive of the final estimate
+__global__ __launch_bounds__(256) void k_depth(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
     const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= d.E) return;
+    if (e >= d.E || d.lm->status) return;
+    const int c = d.lm->cur;
     double Xc[3];
-    map_point(d.pose + 7 * (size_t)d.edge_pose[e], d.pt + 3 * (size_t)d.edge_point[e], Xc);
-    out[e] = Xc[2] > 0.0;
+    map_point(d.pose[c] + 7 * (size_t)d.edge_pose[e], d.pt[c] + 3 * (size_t)d.edge_point[e], Xc);
+    d.depth[e] = Xc[2] > 0.0;
 }
 
 }  // namespace lba
@@ -733,17 +998,27 @@ __global__ __launch_bounds__(256) void k_depth(Dev d, uint8_t* out) {
 
 // ==================================================================================================== host
 using mam::DevBuf;
+using mam::lba::LM;
+using mam::lba::Prob;
 
 struct mam_lba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     size_t ldlt_lds_budget = 0;   // dynamic LDS the factorization may use (panel staging)
-    mam::PinnedBuf staging;       // host mirror of the uploaded part of the arena (one copy per solve)
+    mam::PinnedBuf staging;       // host mirror of the uploaded inputs (host API: one copy per solve)
+    mam::PinnedBuf lm_host;       // LM states read back once per chunk of slots
     mam::StageTimer timer{4};
-    DevBuf<uint8_t> arena;
+    DevBuf<uint8_t> arena;        // per-problem structure, state and scratch of the current batch
+    DevBuf<uint8_t> io;           // host API: inputs + outputs of the one problem
+    DevBuf<Prob> probs;
+    DevBuf<LM> lms;
+    double trials_ema = 8.0;      // slots enqueued before the first read-back (tracks the trials solves take)
 };
 
 namespace {
+
+constexpr size_t kAlign = 256;
+size_t al(size_t b) { return (b + kAlign - 1) & ~(kAlign - 1); }
 
 struct Carver {
     uint8_t* base;
@@ -751,13 +1026,257 @@ struct Carver {
     template <typename T>
     T* take(size_t n) {
         T* p = reinterpret_cast<T*>(base + off);
-        off += (n * sizeof(T) + 255) & ~(size_t)255;
+        off += al(n * sizeof(T));
         return p;
     }
 };
 
-template <typename T>
-size_t sz(size_t n) { return (n * sizeof(T) + 255) & ~(size_t)255; }
+// Arena bytes of one problem's structure, state and scratch (the inputs and outputs live elsewhere)
+size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
+    const size_t nx = 6 * (size_t)Np + 3 * (size_t)L;
+    return al(4 * (size_t)P) + al(4 * (size_t)Np) + al(4 * (size_t)(L + 1)) + al(4 * (size_t)E) +
+           al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) +
+           2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
+           al(8 * (size_t)((E + 255) / 256 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
+           al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
+           al(8 * (size_t)npad * npad) + al(8 * nx) + al(8 * (size_t)npad) +
+           al(8 * mam::lba::ldlt_ws_doubles(npad)) + al((size_t)E);
+}
+
+void carve_scratch(Carver& cv, Prob& d) {
+    const size_t nx = 6 * (size_t)d.Np + 3 * (size_t)d.L;
+    d.pose_h = cv.take<int32_t>(d.P);
+    d.hpose = cv.take<int32_t>(d.Np);
+    d.pe_off = cv.take<int32_t>(d.L + 1);
+    d.pe_idx = cv.take<int32_t>(d.E);
+    d.qe_off = cv.take<int32_t>(d.Np + 1);
+    d.qe_idx = cv.take<int32_t>(d.E);
+    d.cnt = cv.take<int32_t>(d.L + d.Np);
+    d.eidx = cv.take<int32_t>((size_t)d.Np * d.L);
+    d.pose[0] = cv.take<double>(7 * (size_t)d.P);
+    d.pose[1] = cv.take<double>(7 * (size_t)d.P);
+    d.pt[0] = cv.take<double>(3 * (size_t)d.L);
+    d.pt[1] = cv.take<double>(3 * (size_t)d.L);
+    d.err = cv.take<double>(2 * (size_t)d.E);
+    d.jac = cv.take<double>(21 * (size_t)d.E);
+    d.part = cv.take<double>((size_t)(d.E + 255) / 256 + 1);
+    d.hpl = cv.take<double>(18 * (size_t)d.E);
+    d.bdinv = cv.take<double>(18 * (size_t)d.E);
+    d.coef = cv.take<double>(6 * (size_t)d.E);
+    d.Hpp = cv.take<double>(36 * (size_t)d.Np);
+    d.Hll = cv.take<double>(9 * (size_t)d.L);
+    d.b = cv.take<double>(nx);
+    d.Dinv = cv.take<double>(9 * (size_t)d.L);
+    d.S = cv.take<double>((size_t)d.npad * d.npad);
+    d.x = cv.take<double>(nx);
+    d.bs = cv.take<double>(d.npad);
+    d.ws = cv.take<double>(mam::lba::ldlt_ws_doubles(d.npad));
+    d.depth = cv.take<uint8_t>(d.E);
+}
+
+// Output pointers of a batch problem (device memory); chi2 / depth may be NULL
+struct Outs {
+    double* q;
+    double* t;
+    double* xyz;
+    double* chi2;
+    uint8_t* depth;
+};
+
+}  // namespace
+
+namespace mam {
+namespace lba {
+
+// grid (ceil(max(E, P, L)/256), Q): results of the final estimate (cur): poses split into q / t, points, per-edge
+// chi2() = e^T Omega e of the last computed errors (level-0 edges only) and isDepthPositive()
+__global__ __launch_bounds__(256) void k_finish(const Prob* __restrict__ probs, const Outs* __restrict__ outs) {
+    const Prob& d = probs[blockIdx.y];
+    const Outs& o = outs[blockIdx.y];
+    if (d.lm->status) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int c = d.lm->cur;
+    if (i < d.P) {
+        const double* T = d.pose[c] + 7 * (size_t)i;
+        for (int k = 0; k < 4; k++) o.q[4 * (size_t)i + k] = T[k];
+        for (int k = 0; k < 3; k++) o.t[3 * (size_t)i + k] = T[4 + k];
+    }
+    if (i < d.L)
+        for (int k = 0; k < 3; k++) o.xyz[3 * (size_t)i + k] = d.pt[c][3 * (size_t)i + k];
+    if (i < d.E) {
+        if (o.chi2 && !(d.active && !d.active[i])) {
+            const double w = d.edge_w[i], e0 = d.err[2 * i], e1 = d.err[2 * i + 1];
+            o.chi2[i] = e0 * (w * e0) + e1 * (w * e1);
+        }
+        if (o.depth) {
+            double Xc[3];
+            map_point(d.pose[c] + 7 * (size_t)d.edge_pose[i], d.pt[c] + 3 * (size_t)d.edge_point[i], Xc);
+            o.depth[i] = Xc[2] > 0.0;
+        }
+    }
+}
+
+}  // namespace lba
+}  // namespace mam
+
+namespace {
+
+DevBuf<Outs>& outs_buf() {
+    static thread_local DevBuf<Outs> b;
+    return b;
+}
+
+// The shared driver: Q problems whose inputs (id-ordered) are already in device memory, described by hp[q] (input
+// pointers, dimensions, delta, iterations in lm0[q]). Builds the structure on the device, runs the LM slots, writes
+// the outputs and fills the host-side scalars of res[q] (iterations, trials, chi2s, status).
+int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const std::vector<Outs>& outs,
+              const volatile uint8_t* stop_flag, hipStream_t s, mam_lba_result* res) {
+    using namespace mam::lba;
+    const int Q = (int)hp.size();
+    if (Q == 0) return MAM_OK;
+    size_t bytes = 0;
+    int maxE = 0, maxL = 0, maxP = 0, maxNp = 0, maxLb = 0;
+    size_t max_lds = 0;
+    bool lds_ok = true;
+    for (auto& d : hp) {
+        d.npad = ldlt_pad(6 * d.Np);
+        bytes += scratch_bytes(d.P, d.L, d.E, d.Np, d.npad);
+        maxE = std::max(maxE, d.E);
+        maxL = std::max(maxL, d.L);
+        maxP = std::max(maxP, d.P);
+        maxNp = std::max(maxNp, d.Np);
+        maxLb = std::max(maxLb, (d.L + 255) / 256 + d.Np);
+        max_lds = std::max(max_lds, ldlt_lds_bytes(d.npad));
+    }
+    if (max_lds > c->ldlt_lds_budget) lds_ok = false;
+    if (int rc = c->arena.alloc(bytes + kAlign)) return rc;
+    if (int rc = c->probs.alloc(Q)) return rc;
+    if (int rc = c->lms.alloc(Q)) return rc;
+    if (int rc = outs_buf().alloc(Q)) return rc;
+    Carver cv{c->arena.p};
+    for (auto& d : hp) carve_scratch(cv, d);
+    for (int q = 0; q < Q; q++) hp[q].lm = c->lms.p + q;
+    // one pinned block: Prob[Q] | LM[Q] | Outs[Q]
+    const size_t pb = al(sizeof(Prob) * Q), lb = al(sizeof(LM) * Q), ob = al(sizeof(Outs) * Q);
+    if (int rc = c->lm_host.alloc(pb + lb + ob)) return rc;
+    std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
+    std::memcpy(c->lm_host.p + pb, lm0.data(), sizeof(LM) * Q);
+    std::memcpy(c->lm_host.p + pb + lb, outs.data(), sizeof(Outs) * Q);
+    MAM_HIP(hipMemcpyAsync(c->probs.p, c->lm_host.p, sizeof(Prob) * Q, hipMemcpyHostToDevice, s));
+    MAM_HIP(hipMemcpyAsync(c->lms.p, c->lm_host.p + pb, sizeof(LM) * Q, hipMemcpyHostToDevice, s));
+    MAM_HIP(hipMemcpyAsync(outs_buf().p, c->lm_host.p + pb + lb, sizeof(Outs) * Q, hipMemcpyHostToDevice, s));
+    const Prob* P = c->probs.p;
+    const dim3 gE((maxE + 255) / 256 > 0 ? (maxE + 255) / 256 : 1, Q);
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 0);
+        hipLaunchKernelGGL(k_struct_init, dim3(32, Q), dim3(1024), 0, s, P);
+        hipLaunchKernelGGL(k_struct_count, gE, dim3(256), 0, s, P);
+        hipLaunchKernelGGL(k_struct_scan, dim3(1, Q), dim3(1024), 0, s, P);
+        hipLaunchKernelGGL(k_struct_scatter, gE, dim3(256), 0, s, P);
+        hipLaunchKernelGGL(k_struct_sort, dim3(std::max(maxLb, 1), Q), dim3(256), 0, s, P);
+        hipLaunchKernelGGL(k_linearize, gE, dim3(256), 0, s, P, 2);
+        hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
+    }
+    const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
+    const dim3 gPrep((maxL + 63) / 64 > 0 ? (maxL + 63) / 64 : 1, Q);
+    const dim3 gBlk(maxNp * maxNp + maxNp > 0 ? maxNp * maxNp + maxNp : 1, Q);
+    const int maxPL = std::max(maxP, maxL);
+    const dim3 gUpd((maxPL + 255) / 256 > 0 ? (maxPL + 255) / 256 : 1, Q);
+    auto slot = [&]() {
+        {
+            mam::StageTimer::Scope sc(&c->timer, s, 0);
+            hipLaunchKernelGGL(k_linearize, gE, dim3(256), 0, s, P, 0);
+            hipLaunchKernelGGL(k_sys, gSys, dim3(64), 0, s, P);
+            hipLaunchKernelGGL(k_ctl_begin, dim3(Q), dim3(RED), 0, s, P);
+        }
+        {
+            mam::StageTimer::Scope sc(&c->timer, s, 1);
+            hipLaunchKernelGGL(k_schur_prep, gPrep, dim3(64), 0, s, P);
+            hipLaunchKernelGGL(k_schur_blk, gBlk, dim3(64), 0, s, P);
+        }
+        {
+            mam::StageTimer::Scope sc(&c->timer, s, 2);
+            if (lds_ok)
+                hipLaunchKernelGGL(k_ldlt<true>, dim3(Q), dim3(LDLT_THREADS), max_lds, s, P);
+            else
+                hipLaunchKernelGGL(k_ldlt<false>, dim3(Q), dim3(LDLT_THREADS), 0, s, P);
+        }
+        {
+            mam::StageTimer::Scope sc(&c->timer, s, 3);
+            hipLaunchKernelGGL(k_backsub_update, gUpd, dim3(256), 0, s, P);
+            hipLaunchKernelGGL(k_linearize, gE, dim3(256), 0, s, P, 1);
+            hipLaunchKernelGGL(k_ctl_end, dim3(Q), dim3(RED), 0, s, P);
+        }
+    };
+    auto stopped = [&]() { return stop_flag && *stop_flag; };
+    // Every slot is one Levenberg trial of every unfinished problem, so a solve needs at most iterations x 10 slots;
+    // the host reads the states back once per chunk (the first chunk sized by the trials recent solves took).
+    int max_slots = 0;
+    for (auto& l : lm0) max_slots = std::max(max_slots, 10 * std::max(l.iterations, 0));
+    int chunk = std::max(1, (int)std::ceil(c->trials_ema));
+    int enq = 0;
+    LM* lh = reinterpret_cast<LM*>(c->lm_host.p + pb);
+    bool was_stopped = false;
+    while (enq < max_slots) {
+        if (stopped()) { was_stopped = true; break; }
+        const int k = std::min(chunk, max_slots - enq);
+        for (int i = 0; i < k; i++) slot();
+        enq += k;
+        MAM_HIP(hipGetLastError());
+        MAM_HIP(hipMemcpyAsync(lh, c->lms.p, sizeof(LM) * Q, hipMemcpyDeviceToHost, s));
+        MAM_HIP(hipStreamSynchronize(s));
+        bool all = true;
+        for (int q = 0; q < Q; q++) all = all && (lh[q].done || lh[q].status);
+        if (all) break;
+        chunk = 2;
+    }
+    hipLaunchKernelGGL(mam::lba::k_finish, dim3(std::max({(maxE + 255) / 256, (maxPL + 255) / 256, 1}), Q), dim3(256),
+                       0, s, P, outs_buf().p);
+    MAM_HIP(hipGetLastError());
+    MAM_HIP(hipMemcpyAsync(lh, c->lms.p, sizeof(LM) * Q, hipMemcpyDeviceToHost, s));
+    MAM_HIP(hipStreamSynchronize(s));
+    int max_trials = 0;
+    for (int q = 0; q < Q; q++) {
+        res[q].iterations = lh[q].its;
+        res[q].lm_trials = lh[q].trials;
+        res[q].initial_chi2 = lh[q].initialChi;
+        res[q].final_chi2 = lh[q].acceptedChi;   // activeRobustChi2 of the final state
+        res[q].status = lh[q].status ? lh[q].status : ((was_stopped || stopped()) ? 1 : 0);
+        max_trials = std::max(max_trials, lh[q].trials);
+    }
+    if (!was_stopped) c->trials_ema = 0.75 * c->trials_ema + 0.25 * std::max(1, max_trials);
+    return MAM_OK;
+}
+
+bool problem_ok(const mam_lba_problem* p) {
+    if (!p || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || !p->cams || p->n_cams < 1) return false;
+    if ((p->n_poses > 0 && (!p->pose_fixed || !p->pose_q || !p->pose_t)) || (p->n_points > 0 && !p->point_xyz) ||
+        (p->n_edges > 0 && (!p->edge_point || !p->edge_pose || !p->edge_obs || !p->edge_inv_sigma2)))
+        return false;
+    return true;
+}
+
+Prob desc_of(const mam_lba_problem* p) {
+    Prob d{};
+    d.P = p->n_poses;
+    d.L = p->n_points;
+    d.E = p->n_edges;
+    d.n_cams = p->n_cams;
+    d.cam_model = 0;
+    d.delta = p->huber_delta;
+    d.edge_point = p->edge_point;
+    d.edge_pose = p->edge_pose;
+    d.edge_obs = p->edge_obs;
+    d.edge_w = p->edge_inv_sigma2;
+    d.active = p->edge_active;
+    d.cams = p->cams;
+    d.pose_cam = p->pose_cam;
+    d.pose_fixed = p->pose_fixed;
+    d.pose_q = p->pose_q;
+    d.pose_t = p->pose_t;
+    d.point_xyz = p->point_xyz;
+    return d;
+}
 
 }  // namespace
 
@@ -783,8 +1302,7 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
         (void)hipGetLastError();
     }
     // Highest stream priority: LocalMapping's solve shares the GPU with Tracking's full-chip launches, and its small
-    // latency-bound kernels (and the host round trip of every LM trial) should not queue behind them.
-    // MAM_LBA_PRIORITY=0 keeps the default priority.
+    // latency-bound kernels should not queue behind them. MAM_LBA_PRIORITY=0 keeps the default priority.
     int least = 0, greatest = 0;
     const char* pe = std::getenv("MAM_LBA_PRIORITY");
     const bool prio = !(pe && pe[0] == '0') && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
@@ -824,11 +1342,7 @@ int mam_lba_stage_times(mam_lba_ctx* c, double* ms_out, int64_t* launches_out) {
 }
 
 int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8_t* stop_flag, mam_lba_result* r) {
-    if (!c || !p || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || !p->cams || p->n_cams < 1)
-        return MAM_ERR_ARG;
-    if ((p->n_poses > 0 && (!p->pose_id || !p->pose_fixed || !p->pose_q || !p->pose_t)) ||
-        (p->n_points > 0 && (!p->point_id || !p->point_xyz)) ||
-        (p->n_edges > 0 && (!p->edge_point || !p->edge_pose || !p->edge_obs || !p->edge_inv_sigma2)) ||
+    if (!c || !problem_ok(p) || !r || (p->n_poses > 0 && !p->pose_id) || (p->n_points > 0 && !p->point_id) ||
         !r->pose_q || !r->pose_t || (p->n_points > 0 && !r->point_xyz))
         return MAM_ERR_ARG;
     const int P = p->n_poses, L = p->n_points, E = p->n_edges;
@@ -836,297 +1350,135 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         if (p->edge_point[e] < 0 || p->edge_point[e] >= L || p->edge_pose[e] < 0 || p->edge_pose[e] >= P)
             return MAM_ERR_ARG;
     MAM_DEVICE_SCOPE(c->device);
-#ifdef MAM_LDLT_PROFILE
-    const auto h_t0 = std::chrono::steady_clock::now();
-#endif
-    // ---- structure (sparse_optimizer.cpp:166-190): Hessian order = vertices sorted by id
-    std::vector<int> po(P), pl(L);
+    // g2o's Hessian order = vertices sorted by id (sparse_optimizer.cpp:166-190): the device path takes id-ordered
+    // poses and points, so permute here and map the results back
+    std::vector<int> po(P), pl(L), ipo(P), ipl(L);
     std::iota(po.begin(), po.end(), 0);
     std::iota(pl.begin(), pl.end(), 0);
     std::stable_sort(po.begin(), po.end(), [&](int a, int b) { return p->pose_id[a] < p->pose_id[b]; });
     std::stable_sort(pl.begin(), pl.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
-    std::vector<int32_t> pose_h(P, -1), hpose, point_h(L, -1), hpoint;
-    hpose.reserve(P);
-    hpoint.reserve(L);
-    for (int i : po)
-        if (!p->pose_fixed[i]) { pose_h[i] = (int)hpose.size(); hpose.push_back(i); }
-    for (int i : pl) { point_h[i] = (int)hpoint.size(); hpoint.push_back(i); }
-    const int Np = (int)hpose.size();
-    // per Hessian point / pose edge lists (counting sorts, edge order kept)
-    std::vector<int32_t> pe_off(L + 1, 0), pe_idx(E), qe_off(Np + 1, 0), qe_idx;
+    for (int i = 0; i < P; i++) ipo[po[i]] = i;
+    for (int i = 0; i < L; i++) ipl[pl[i]] = i;
+    int Np = 0;
+    for (int i = 0; i < P; i++) Np += p->pose_fixed[i] ? 0 : 1;
+    const int ncw = 4 * p->n_cams;
+    // staging layout (one H2D copy): inputs, then room for the outputs
+    const size_t in_bytes = al(4 * (size_t)E) * 2 + al(16 * (size_t)E) + al(8 * (size_t)E) + al((size_t)E) +
+                            al(4 * (size_t)ncw) + al(4 * (size_t)P) + al((size_t)P) + al(32 * (size_t)P) +
+                            al(24 * (size_t)P) + al(24 * (size_t)L);
+    const size_t out_bytes = al(32 * (size_t)P) + al(24 * (size_t)P) + al(24 * (size_t)L) + al(8 * (size_t)E) +
+                             al((size_t)E);
+    if (int rc = c->staging.alloc(in_bytes + out_bytes)) return rc;
+    if (int rc = c->io.alloc(in_bytes + out_bytes)) return rc;
+    uint8_t* hb = c->staging.p;
+    Carver dv{c->io.p};
+    auto put = [&](auto* dst_host_typed, size_t count) {
+        using T = std::remove_pointer_t<decltype(dst_host_typed)>;
+        T* d = dv.take<T>(count);
+        return std::make_pair(d, reinterpret_cast<T*>(hb + (reinterpret_cast<uint8_t*>(d) - c->io.p)));
+    };
+    auto [d_ep, h_ep] = put((int32_t*)nullptr, E);
+    auto [d_eo, h_eo] = put((int32_t*)nullptr, E);
+    auto [d_obs, h_obs] = put((double*)nullptr, 2 * (size_t)E);
+    auto [d_w, h_w] = put((double*)nullptr, E);
+    auto [d_act, h_act] = put((uint8_t*)nullptr, E);
+    auto [d_cams, h_cams] = put((float*)nullptr, ncw);
+    auto [d_pc, h_pc] = put((int32_t*)nullptr, P);
+    auto [d_fix, h_fix] = put((uint8_t*)nullptr, P);
+    auto [d_q, h_q] = put((double*)nullptr, 4 * (size_t)P);
+    auto [d_t, h_t] = put((double*)nullptr, 3 * (size_t)P);
+    auto [d_x, h_x] = put((double*)nullptr, 3 * (size_t)L);
+    const size_t upload = dv.off;
     for (int e = 0; e < E; e++) {
-        pe_off[point_h[p->edge_point[e]] + 1]++;
-        const int h = pose_h[p->edge_pose[e]];
-        if (h >= 0) qe_off[h + 1]++;
+        h_ep[e] = ipl[p->edge_point[e]];
+        h_eo[e] = ipo[p->edge_pose[e]];
+        h_obs[2 * e] = p->edge_obs[2 * e];
+        h_obs[2 * e + 1] = p->edge_obs[2 * e + 1];
+        h_w[e] = p->edge_inv_sigma2[e];
+        if (p->edge_active) h_act[e] = p->edge_active[e];
     }
-    for (int h = 0; h < L; h++) pe_off[h + 1] += pe_off[h];
-    for (int h = 0; h < Np; h++) qe_off[h + 1] += qe_off[h];
-    qe_idx.resize(qe_off[Np]);
-    {
-        std::vector<int32_t> cp(pe_off.begin(), pe_off.end() - 1), cq(qe_off.begin(), qe_off.end() - 1);
-        for (int e = 0; e < E; e++) {
-            pe_idx[cp[point_h[p->edge_point[e]]]++] = e;
-            const int h = pose_h[p->edge_pose[e]];
-            if (h >= 0) qe_idx[cq[h]++] = e;
-        }
+    std::memcpy(h_cams, p->cams, sizeof(float) * ncw);
+    for (int i = 0; i < P; i++) {
+        const int s = po[i];
+        h_pc[i] = p->pose_cam ? p->pose_cam[s] : 0;
+        h_fix[i] = p->pose_fixed[s];
+        for (int k = 0; k < 4; k++) h_q[4 * i + k] = p->pose_q[4 * s + k];
+        for (int k = 0; k < 3; k++) h_t[3 * i + k] = p->pose_t[3 * s + k];
     }
-    // S block pairs (i1 <= i2, row-major; diagonal blocks always present) with their contributions in landmark
-    // (Hessian point) order, then edge order within the landmark
-    // every block of the upper triangle of S (g2o keeps only the non-empty ones; the empty ones are zero here)
-    std::vector<int32_t> bp_ij;
-    bp_ij.reserve((size_t)Np * (Np + 1));
-    for (int a = 0; a < Np; a++)
-        for (int b = a; b < Np; b++) { bp_ij.push_back(a); bp_ij.push_back(b); }
-    const int nbp = (int)bp_ij.size() / 2;
-    const int n = 6 * Np, nx = 6 * Np + 3 * L, npad = mam::lba::ldlt_pad(n);
-    // ---- device arena: the uploaded inputs first (mirrored in pinned host memory, one copy), scratch after
-    size_t bytes = sz<int32_t>(E) * 2 + sz<double>(2 * (size_t)E) + sz<double>(E) + sz<float>(4 * (size_t)p->n_cams) +
-                   sz<int32_t>(P) * 2 + sz<int32_t>(Np) + sz<int32_t>(L) * 2 + sz<int32_t>(L + 1) + sz<int32_t>(E) +
-                   sz<int32_t>(Np + 1) + sz<int32_t>(E) + sz<int32_t>((size_t)Np * L) +
-                   sz<int32_t>(2 * (size_t)nbp) + 2 * sz<double>(7 * (size_t)P) + 2 * sz<double>(3 * (size_t)L) +
-                   sz<double>(2 * (size_t)E) + sz<double>(21 * (size_t)E) + sz<double>(E) + sz<double>(18 * (size_t)E) * 2 +
-                   sz<double>(6 * (size_t)E) + sz<double>(36 * (size_t)Np) + sz<double>(9 * (size_t)L) + sz<double>(nx) +
-                   sz<double>(9 * (size_t)L) + sz<double>((size_t)npad * npad) + sz<double>(nx) + sz<double>(npad) + sz<double>(8) +
-                   sz<double>(mam::lba::ldlt_ws_doubles(npad)) +
-                   sz<int>(4) + sz<uint8_t>(E) * 2 + sz<double>((size_t)(E + 255) / 256 + 1) + 4096;
-    if (int rc = c->arena.alloc(bytes)) return rc;
-    if (int rc = c->staging.alloc(bytes)) return rc;
-    Carver cv{c->arena.p};
-    uint8_t* const host_base = c->staging.p;
-    mam::lba::Dev d{};
-    d.P = P; d.L = L; d.E = E; d.Np = Np; d.nbp = nbp; d.npad = npad; d.delta = p->huber_delta;
+    for (int i = 0; i < L; i++)
+        for (int k = 0; k < 3; k++) h_x[3 * i + k] = p->point_xyz[3 * pl[i] + k];
+    Outs o{};
+    o.q = dv.take<double>(4 * (size_t)P);
+    o.t = dv.take<double>(3 * (size_t)P);
+    o.xyz = dv.take<double>(3 * (size_t)L);
+    o.chi2 = r->edge_chi2 ? dv.take<double>(E) : nullptr;
+    o.depth = r->edge_depth_ok ? dv.take<uint8_t>(E) : nullptr;
     hipStream_t s = c->stream;
-    // carve a device array and fill its pinned mirror
-    auto put = [&](auto* src, size_t count) {
-        using T = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
-        T* dst = cv.take<T>(count);
-        if (count) std::memcpy(host_base + (reinterpret_cast<uint8_t*>(dst) - c->arena.p), src, count * sizeof(T));
-        return dst;
-    };
-    d.edge_point = put(p->edge_point, E);
-    d.edge_pose = put(p->edge_pose, E);
-    d.edge_obs = put(p->edge_obs, 2 * (size_t)E);
-    d.edge_w = put(p->edge_inv_sigma2, E);
-    d.active = p->edge_active ? put(p->edge_active, E) : nullptr;
-    d.cams = put(p->cams, 4 * (size_t)p->n_cams);
-    {
-        const int32_t* pcm = put(p->pose_cam ? p->pose_cam : pose_h.data(), P);
-        d.pose_cam = p->pose_cam ? pcm : nullptr;
-    }
-    d.pose_h = put(pose_h.data(), P);
-    d.hpose = put(hpose.data(), Np);
-    d.hpoint = put(hpoint.data(), L);
-    d.point_h = put(point_h.data(), L);
-    d.pe_off = put(pe_off.data(), L + 1);
-    d.pe_idx = put(pe_idx.data(), E);
-    d.qe_off = put(qe_off.data(), Np + 1);
-    d.qe_idx = put(qe_idx.data(), qe_idx.size());
-    d.bp_ij = put(bp_ij.data(), 2 * (size_t)nbp);
-    // state: poses packed [q t], SE3Quat(q, t) normalises on construction
-    std::vector<double> pose0(7 * (size_t)P);
-    for (int i = 0; i < P; i++) {
-        double q[4] = {p->pose_q[4 * i], p->pose_q[4 * i + 1], p->pose_q[4 * i + 2], p->pose_q[4 * i + 3]};
-        if (q[3] < 0) for (double& v : q) v = -v;
-        const double nq = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-        for (int k = 0; k < 4; k++) pose0[7 * i + k] = q[k] / nq;
-        for (int k = 0; k < 3; k++) pose0[7 * i + 4 + k] = p->pose_t[3 * i + k];
-    }
-    double* poseA = put(pose0.data(), 7 * (size_t)P);
-    double* ptA = put(p->point_xyz, 3 * (size_t)L);
-    const size_t upload = cv.off;
-#ifdef MAM_LDLT_PROFILE
-    const auto h_t1 = std::chrono::steady_clock::now();
-#endif
-    MAM_HIP(hipMemcpyAsync(c->arena.p, host_base, upload, hipMemcpyHostToDevice, s));
-    d.eidx = cv.take<int32_t>((size_t)Np * L);
-    if ((size_t)Np * L > 0) {
-        MAM_HIP(hipMemsetAsync(d.eidx, 0xFF, sizeof(int32_t) * (size_t)Np * L, s));
-        if (E > 0) hipLaunchKernelGGL(mam::lba::k_eidx, dim3((E + 255) / 256), dim3(256), 0, s, d);
-    }
-    double* poseB = cv.take<double>(7 * (size_t)P);
-    double* ptB = cv.take<double>(3 * (size_t)L);
-    d.err = cv.take<double>(2 * (size_t)E);
-    d.jac = cv.take<double>(21 * (size_t)E);
-    d.rho0 = cv.take<double>(E);
-    d.part = cv.take<double>((size_t)(E + 255) / 256 + 1);
-    d.hpl = cv.take<double>(18 * (size_t)E);
-    d.bdinv = cv.take<double>(18 * (size_t)E);
-    d.coef = cv.take<double>(6 * (size_t)E);
-    d.Hpp = cv.take<double>(36 * (size_t)Np);
-    d.Hll = cv.take<double>(9 * (size_t)L);
-    d.b = cv.take<double>(nx);
-    d.Dinv = cv.take<double>(9 * (size_t)L);
-    d.S = cv.take<double>((size_t)npad * npad);
-    d.x = cv.take<double>(nx);
-    d.bs = cv.take<double>(npad);
-    d.ws = cv.take<double>(mam::lba::ldlt_ws_doubles(npad));
-    d.red = cv.take<double>(8);
-    MAM_HIP(hipMemsetAsync(d.red, 0, sizeof(double) * 8, s));
-    d.flag = cv.take<int>(4);
-    uint8_t* depth = cv.take<uint8_t>(E);
-    MAM_HIP(hipMemsetAsync(d.x, 0, sizeof(double) * nx, s));
-    if (npad > 0) MAM_HIP(hipMemsetAsync(d.bs, 0, sizeof(double) * npad, s));
-
-    const int gE = (E + 255) / 256, gL = (L + 255) / 256, gPL = (std::max(P, L) + 255) / 256;
-    double* cur_pose = poseA; double* cur_pt = ptA;
-    double* tr_pose = poseB;  double* tr_pt = ptB;
-    auto state = [&](const double* pose, const double* pt, double* opose, double* opt) {
-        d.pose = pose; d.pt = pt; d.pose_out = opose; d.pt_out = opt;
-    };
-    double h_red[3];
-    auto chi_of = [&](const double* pose, const double* pt, bool jac, double* out_chi) -> int {
-        state(pose, pt, tr_pose, tr_pt);
-        if (E > 0) hipLaunchKernelGGL(mam::lba::k_linearize, dim3(gE), dim3(256), 0, s, d, jac ? 1 : 0);
-        hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(mam::lba::RED), 0, s, d, 0);
-        MAM_HIP(hipMemcpyAsync(h_red, d.red, sizeof(double), hipMemcpyDeviceToHost, s));
-        MAM_HIP(hipStreamSynchronize(s));
-        *out_chi = h_red[0];
-        return MAM_OK;
-    };
-    auto stopped = [&]() { return stop_flag && *stop_flag; };
-
-    double chi0 = 0;
-    if (int rc = chi_of(cur_pose, cur_pt, false, &chi0)) return rc;
-    r->initial_chi2 = chi0;
-    double currentLambda = -1.0, ni = 2.0, acceptedChi = chi0;
-    int nBad = 0, trials = 0, its = 0;
-    bool ok = Np + L > 0;
-    for (int it = 0; it < p->iterations && !stopped() && ok; it++) {
-        double currentChi;
-        {
-            mam::StageTimer::Scope sc(&c->timer, s, 0);
-            state(cur_pose, cur_pt, tr_pose, tr_pt);
-            if (E > 0) hipLaunchKernelGGL(mam::lba::k_linearize, dim3(gE), dim3(256), 0, s, d, 1);
-            hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(mam::lba::RED), 0, s, d, 0);
-            if (L > 0) hipLaunchKernelGGL(mam::lba::k_point_sys, dim3((L + 63) / 64), dim3(64), 0, s, d);
-            if (Np > 0) hipLaunchKernelGGL(mam::lba::k_pose_sys, dim3(Np), dim3(64), 0, s, d);
-            hipLaunchKernelGGL(mam::lba::k_max_diag, dim3(1), dim3(mam::lba::RED), 0, s, d);
-        }
-        if (it == 0) {
-            // lambda init needs max diag(H); afterwards the iteration-start chi2 is, bit for bit, the chi2 of the
-            // trial that was just accepted (same kernels on the same state), so no round trip is needed
-            MAM_HIP(hipMemcpyAsync(h_red, d.red, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
-            MAM_HIP(hipStreamSynchronize(s));
-            currentChi = h_red[0];
-            currentLambda = 1e-5 * h_red[2];
-            ni = 2;
-            nBad = 0;
-        } else {
-            currentChi = acceptedChi;
-        }
-        const double iniChi = currentChi;
-        double rho = 0;
-        int qmax = 0;
-        do {
-            {
-                mam::StageTimer::Scope sc(&c->timer, s, 1);
-                if (L > 0) hipLaunchKernelGGL(mam::lba::k_schur_prep, dim3((L + 63) / 64), dim3(64), 0, s, d, currentLambda);
-                if (E > 0) hipLaunchKernelGGL(mam::lba::k_schur_edge, dim3(gE), dim3(256), 0, s, d);
-                // the factorization leaves fill-in in S: clear the whole matrix before the blocks are rewritten
-                if (npad > 0) MAM_HIP(hipMemsetAsync(d.S, 0, sizeof(double) * (size_t)npad * npad, s));
-                if (nbp > 0) hipLaunchKernelGGL(mam::lba::k_schur_blk, dim3(nbp), dim3(64), 0, s, d, currentLambda);
-                if (Np > 0) hipLaunchKernelGGL(mam::lba::k_schur_rhs, dim3(Np), dim3(64), 0, s, d);
-            }
-            {
-                mam::StageTimer::Scope sc(&c->timer, s, 2);
-                MAM_HIP(hipMemsetAsync(d.flag, 0, sizeof(int), s));
-                if (Np > 0) {
-                    const size_t lds = mam::lba::ldlt_lds_bytes(npad);
-                    if (lds <= c->ldlt_lds_budget)
-                        hipLaunchKernelGGL(mam::lba::k_ldlt<true>, dim3(1), dim3(mam::lba::LDLT_THREADS), lds, s, d);
-                    else
-                        hipLaunchKernelGGL(mam::lba::k_ldlt<false>, dim3(1), dim3(mam::lba::LDLT_THREADS), 0, s, d);
-                }
-            }
-            {
-                mam::StageTimer::Scope sc(&c->timer, s, 3);
-                if (L > 0) hipLaunchKernelGGL(mam::lba::k_backsub, dim3(gL), dim3(256), 0, s, d);
-                state(cur_pose, cur_pt, tr_pose, tr_pt);
-                if (std::max(P, L) > 0) hipLaunchKernelGGL(mam::lba::k_update, dim3(gPL), dim3(256), 0, s, d);
-                // chi2 of the trial state (errors kept: chi2() reads the last computeActiveErrors)
-                state(tr_pose, tr_pt, tr_pose, tr_pt);
-                if (E > 0) hipLaunchKernelGGL(mam::lba::k_linearize, dim3(gE), dim3(256), 0, s, d, 0);
-                hipLaunchKernelGGL(mam::lba::k_reduce_chi, dim3(1), dim3(mam::lba::RED), 0, s, d, 0);
-                hipLaunchKernelGGL(mam::lba::k_scale, dim3(1), dim3(mam::lba::RED), 0, s, d, currentLambda);
-            }
-            int fail = 0;
-            MAM_HIP(hipMemcpyAsync(h_red, d.red, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
-            MAM_HIP(hipMemcpyAsync(&fail, d.flag, sizeof(int), hipMemcpyDeviceToHost, s));
-            MAM_HIP(hipStreamSynchronize(s));
-            double tempChi = h_red[0];
-            if (fail) tempChi = std::numeric_limits<double>::max();
-            rho = currentChi - tempChi;
-            double scale = h_red[1] + 1e-3;
-            rho /= scale;
-            if (rho > 0 && std::isfinite(tempChi)) {
-                double alpha = 1. - std::pow((2 * rho - 1), 3);
-                alpha = std::min(alpha, 2. / 3.);
-                const double scaleFactor = std::max(1. / 3., alpha);
-                currentLambda *= scaleFactor;
-                ni = 2;
-                currentChi = tempChi;
-                acceptedChi = tempChi;
-                std::swap(cur_pose, tr_pose);   // accept: discardTop
-                std::swap(cur_pt, tr_pt);
-            } else {
-                currentLambda *= ni;             // reject: pop
-                ni *= 2;
-            }
-            qmax++;
-            trials++;
-        } while (rho < 0 && qmax < 10 && !stopped());
-        its++;
-        bool term = false;
-        if (qmax == 10 || rho == 0) term = true;
-        else {
-            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
-            else nBad = 0;
-            if (nBad >= 3) term = true;
-        }
-        ok = !term;
-    }
-    MAM_HIP(hipGetLastError());
-#ifdef MAM_LDLT_PROFILE
-    {
-        double ph[4];
-        MAM_HIP(hipMemcpy(ph, d.red + 4, sizeof(ph), hipMemcpyDeviceToHost));
-        const auto h_t2 = std::chrono::steady_clock::now();
-        fprintf(stderr, "ldlt cycles: diag+trailing-rest %.0f panel %.0f next-column %.0f subst %.0f (trials %d); host setup %.3f ms, "
-                "loop %.3f ms\n", ph[0], ph[1], ph[2], ph[3], trials,
-                std::chrono::duration<double, std::milli>(h_t1 - h_t0).count(),
-                std::chrono::duration<double, std::milli>(h_t2 - h_t1).count());
-    }
-#endif
-    // ---- results
-    std::vector<double> pose_h_out(7 * (size_t)P);
-    if (P) MAM_HIP(hipMemcpyAsync(pose_h_out.data(), cur_pose, sizeof(double) * 7 * P, hipMemcpyDeviceToHost, s));
-    if (L) MAM_HIP(hipMemcpyAsync(r->point_xyz, cur_pt, sizeof(double) * 3 * L, hipMemcpyDeviceToHost, s));
-    if (r->edge_chi2 && E) {
-        // chi2() = e^T Omega e of the last computed errors
-        std::vector<double> err(2 * (size_t)E);
-        MAM_HIP(hipMemcpyAsync(err.data(), d.err, sizeof(double) * 2 * E, hipMemcpyDeviceToHost, s));
-        MAM_HIP(hipStreamSynchronize(s));
-        for (int e = 0; e < E; e++) {
-            if (p->edge_active && !p->edge_active[e]) continue;   // not computed at level 0: left to the caller
-            const double w = p->edge_inv_sigma2[e], e0 = err[2 * e], e1 = err[2 * e + 1];
-            r->edge_chi2[e] = e0 * (w * e0) + e1 * (w * e1);
-        }
-    }
-    state(cur_pose, cur_pt, tr_pose, tr_pt);
-    if (r->edge_depth_ok && E) {
-        hipLaunchKernelGGL(mam::lba::k_depth, dim3(gE), dim3(256), 0, s, d, depth);
-        MAM_HIP(hipMemcpyAsync(r->edge_depth_ok, depth, E, hipMemcpyDeviceToHost, s));
-    }
+    if (upload) MAM_HIP(hipMemcpyAsync(c->io.p, hb, upload, hipMemcpyHostToDevice, s));
+    mam_lba_problem pd = *p;
+    pd.edge_point = d_ep;
+    pd.edge_pose = d_eo;
+    pd.edge_obs = d_obs;
+    pd.edge_inv_sigma2 = d_w;
+    pd.edge_active = p->edge_active ? d_act : nullptr;
+    pd.cams = d_cams;
+    pd.pose_cam = d_pc;
+    pd.pose_fixed = d_fix;
+    pd.pose_q = d_q;
+    pd.pose_t = d_t;
+    pd.point_xyz = d_x;
+    std::vector<Prob> hp{desc_of(&pd)};
+    hp[0].Np = Np;
+    std::vector<LM> lm0(1);
+    std::memset(lm0.data(), 0, sizeof(LM));
+    lm0[0].iterations = p->iterations;
+    std::vector<Outs> outs{o};
+    if (int rc = run_batch(c, hp, lm0, outs, stop_flag, s, r)) return rc;
+    // results back to the caller's order
+    std::vector<double> q(4 * (size_t)P), t(3 * (size_t)P), x(3 * (size_t)L), chi(o.chi2 ? E : 0);
+    std::vector<uint8_t> dep(o.depth ? E : 0);
+    if (P) MAM_HIP(hipMemcpyAsync(q.data(), o.q, 32 * (size_t)P, hipMemcpyDeviceToHost, s));
+    if (P) MAM_HIP(hipMemcpyAsync(t.data(), o.t, 24 * (size_t)P, hipMemcpyDeviceToHost, s));
+    if (L) MAM_HIP(hipMemcpyAsync(x.data(), o.xyz, 24 * (size_t)L, hipMemcpyDeviceToHost, s));
+    if (o.chi2 && E) MAM_HIP(hipMemcpyAsync(chi.data(), o.chi2, 8 * (size_t)E, hipMemcpyDeviceToHost, s));
+    if (o.depth && E) MAM_HIP(hipMemcpyAsync(dep.data(), o.depth, (size_t)E, hipMemcpyDeviceToHost, s));
     MAM_HIP(hipStreamSynchronize(s));
+    if (r->status < 0) return r->status;
     for (int i = 0; i < P; i++) {
-        for (int k = 0; k < 4; k++) r->pose_q[4 * i + k] = pose_h_out[7 * i + k];
-        for (int k = 0; k < 3; k++) r->pose_t[3 * i + k] = pose_h_out[7 * i + 4 + k];
+        const int d = po[i];
+        for (int k = 0; k < 4; k++) r->pose_q[4 * d + k] = q[4 * i + k];
+        for (int k = 0; k < 3; k++) r->pose_t[3 * d + k] = t[3 * i + k];
     }
-    r->final_chi2 = acceptedChi;   // activeRobustChi2 of the final state: the last accepted trial's (or initial) chi2
-    r->iterations = its;
-    r->lm_trials = trials;
-    r->status = stopped() ? 1 : 0;
+    for (int i = 0; i < L; i++)
+        for (int k = 0; k < 3; k++) r->point_xyz[3 * pl[i] + k] = x[3 * i + k];
+    for (int e = 0; e < E; e++) {
+        if (o.chi2 && !(p->edge_active && !p->edge_active[e])) r->edge_chi2[e] = chi[e];
+        if (o.depth) r->edge_depth_ok[e] = dep[e];
+    }
     return MAM_OK;
+}
+
+int mam_lba_solve_batch_device(mam_lba_ctx* c, int n_problems, const mam_lba_problem* problems,
+                               mam_lba_result* results, void* stream) {
+    if (!c || n_problems < 0 || (n_problems > 0 && (!problems || !results))) return MAM_ERR_ARG;
+    if (n_problems == 0) return MAM_OK;
+    MAM_DEVICE_SCOPE(c->device);
+    std::vector<Prob> hp(n_problems);
+    std::vector<LM> lm0(n_problems);
+    std::vector<Outs> outs(n_problems);
+    for (int q = 0; q < n_problems; q++) {
+        const mam_lba_problem* p = problems + q;
+        const mam_lba_result* r = results + q;
+        if (!problem_ok(p) || !r->pose_q || !r->pose_t || (p->n_points > 0 && !r->point_xyz) ||
+            p->n_opt_poses < 0 || p->n_opt_poses > p->n_poses || p->cam_model != 0)
+            return MAM_ERR_ARG;
+        hp[q] = desc_of(p);
+        hp[q].Np = p->n_opt_poses;
+        std::memset(&lm0[q], 0, sizeof(LM));
+        lm0[q].iterations = p->iterations;
+        outs[q] = Outs{r->pose_q, r->pose_t, r->point_xyz, r->edge_chi2, r->edge_depth_ok};
+    }
+    return run_batch(c, hp, lm0, outs, nullptr, stream ? (hipStream_t)stream : c->stream, results);
 }
 
 }  // extern "C"

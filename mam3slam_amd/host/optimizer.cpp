@@ -99,7 +99,7 @@ int Optimizer::PoseOptimization(Frame* pFrame) {
 }
 
 mam_lba_problem LocalBAWindow::Problem(int iterations) const {
-    mam_lba_problem p;
+    mam_lba_problem p{};
     p.n_poses = (int32_t)vpKF.size();
     p.pose_id = pose_id.data();
     p.pose_fixed = pose_fixed.data();

@@ -27,7 +27,7 @@ class _Problem(C.Structure):
                 ("point_xyz", C.c_void_p), ("n_edges", C.c_int32), ("edge_point", C.c_void_p),
                 ("edge_pose", C.c_void_p), ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p),
                 ("n_cams", C.c_int32), ("cams", C.c_void_p), ("huber_delta", C.c_double), ("iterations", C.c_int32),
-                ("edge_active", C.c_void_p)]
+                ("edge_active", C.c_void_p), ("cam_model", C.c_int32), ("n_opt_poses", C.c_int32)]
 
 
 class _Result(C.Structure):
@@ -40,6 +40,7 @@ _SIGS = {
     "mam_lba_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     "mam_lba_destroy": (None, [C.c_void_p]),
     "mam_lba_solve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mam_lba_solve_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mam_lba_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "mam_lba_stage_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
 }
@@ -92,6 +93,8 @@ class LBAProblem:
         P.huber_delta = float(self.huber_delta)
         P.iterations = int(self.iterations)
         P.edge_active = None if self.edge_active is None else self.edge_active.ctypes.data
+        P.cam_model = 0
+        P.n_opt_poses = int((self.pose_fixed == 0).sum())
         return P
 
 
@@ -157,6 +160,14 @@ class LBASolver:
         check(self._L.mam_lba_solve(self._ctx, C.byref(P), sf, C.byref(R)), "mam_lba_solve")
         return wrap_result(R, arrs)
 
+    def solve_batch_device(self, batch: "DeviceBatch", stream: int = 0):
+        """All problems of `batch` (device-resident, id-ordered) in one set of launches; fills batch.stats."""
+        check(self._L.mam_lba_solve_batch_device(self._ctx, len(batch.probs), C.byref(batch.c_probs),
+                                                 C.byref(batch.c_res), C.c_void_p(stream)), "mam_lba_solve_batch_device")
+        batch.stats = [dict(iterations=int(r.iterations), lm_trials=int(r.lm_trials), initial_chi2=float(r.initial_chi2),
+                            final_chi2=float(r.final_chi2), status=int(r.status)) for r in batch.c_res]
+        return batch.stats
+
     def set_profiling(self, enable: bool):
         check(self._L.mam_lba_set_profiling(self._ctx, 1 if enable else 0), "lba_set_profiling")
 
@@ -166,6 +177,77 @@ class LBASolver:
         check(self._L.mam_lba_stage_times(self._ctx, ms.ctypes.data_as(C.c_void_p), n.ctypes.data_as(C.c_void_p)),
               "lba_stage_times")
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(["linearize", "schur", "solve", "update"])}
+
+
+def id_ordered(prob: LBAProblem):
+    """The same g2o graph with poses and points listed in ascending id (the Hessian order the device batch path
+    takes, sparse_optimizer.cpp:166-190); edges keep their insertion order. Returns (problem, pose_order,
+    point_order): row i of the new problem is row pose_order[i] / point_order[i] of the old one."""
+    import dataclasses
+
+    po = np.argsort(prob.pose_id, kind="stable")
+    pl = np.argsort(prob.point_id, kind="stable")
+    ipo = np.empty_like(po)
+    ipo[po] = np.arange(len(po))
+    ipl = np.empty_like(pl)
+    ipl[pl] = np.arange(len(pl))
+    q = dataclasses.replace(prob, pose_id=prob.pose_id[po], pose_fixed=prob.pose_fixed[po], pose_q=prob.pose_q[po],
+                            pose_t=prob.pose_t[po], point_id=prob.point_id[pl], point_xyz=prob.point_xyz[pl],
+                            edge_point=ipl[prob.edge_point].astype(np.int32),
+                            edge_pose=ipo[prob.edge_pose].astype(np.int32),
+                            pose_cam=None if prob.pose_cam is None else prob.pose_cam[po])
+    return q.contiguous(), po, pl
+
+
+class DeviceBatch:
+    """Q LocalBundleAdjustment problems resident in HBM (torch tensors), id-ordered, with device result arrays, for
+    LBASolver.solve_batch_device (mam_lba_solve_batch_device)."""
+
+    def __init__(self, probs, device):
+        import torch
+
+        self.probs = [id_ordered(p)[0] for p in probs]
+        self._keep = []
+        Q = len(self.probs)
+        self.c_probs = (_Problem * Q)()
+        self.c_res = (_Result * Q)()
+        self.res = []
+
+        def dev(a, dt=None):
+            t = torch.from_numpy(np.ascontiguousarray(a if dt is None else a.astype(dt))).to(device)
+            self._keep.append(t)
+            return t.data_ptr()
+
+        for i, p in enumerate(self.probs):
+            P = p.as_c()   # host struct; pointers replaced by device copies
+            P.pose_id = P.point_id = None
+            P.pose_fixed = dev(p.pose_fixed)
+            P.pose_q, P.pose_t, P.point_xyz = dev(p.pose_q), dev(p.pose_t), dev(p.point_xyz)
+            P.pose_cam = None if p.pose_cam is None else dev(p.pose_cam)
+            P.edge_point, P.edge_pose = dev(p.edge_point), dev(p.edge_pose)
+            P.edge_obs, P.edge_inv_sigma2 = dev(p.edge_obs), dev(p.edge_inv_sigma2)
+            P.cams = dev(p.cams)
+            P.edge_active = None if p.edge_active is None else dev(p.edge_active)
+            self.c_probs[i] = P
+            Pn, L, E = len(p.pose_id), len(p.point_id), len(p.edge_point)
+            out = dict(pose_q=torch.zeros((Pn, 4), dtype=torch.float64, device=device),
+                       pose_t=torch.zeros((Pn, 3), dtype=torch.float64, device=device),
+                       point_xyz=torch.zeros((L, 3), dtype=torch.float64, device=device),
+                       edge_chi2=torch.zeros(E, dtype=torch.float64, device=device),
+                       edge_depth_ok=torch.zeros(E, dtype=torch.uint8, device=device))
+            self.res.append(out)
+            R = self.c_res[i]
+            R.pose_q, R.pose_t = out["pose_q"].data_ptr(), out["pose_t"].data_ptr()
+            R.point_xyz = out["point_xyz"].data_ptr()
+            R.edge_chi2, R.edge_depth_ok = out["edge_chi2"].data_ptr(), out["edge_depth_ok"].data_ptr()
+        self.stats = None
+
+    def result(self, i) -> LBAResult:
+        """Problem i's result (host copies, id order) as an LBAResult."""
+        o = {k: v.cpu().numpy() for k, v in self.res[i].items()}
+        s = self.stats[i]
+        return LBAResult(o["pose_q"], o["pose_t"], o["point_xyz"], o["edge_chi2"], o["edge_depth_ok"],
+                         s["iterations"], s["lm_trials"], s["initial_chi2"], s["final_chi2"], s["status"])
 
 
 # ------------------------------------------------------------------------------------------------ synthetic

@@ -21,7 +21,12 @@ def main():
     ap.add_argument("--kf", type=int, default=50)
     ap.add_argument("--points", type=int, default=3000)
     ap.add_argument("--oracle", action="store_true")
+    ap.add_argument("--batch", type=int, default=0, help="also time Q problems solved together on the device path")
     a = ap.parse_args()
+    if a.batch:
+        import torch
+
+        torch.cuda.init()   # torch's HIP runtime first: it does not attach after the library has initialised HIP
     from mam3slam_amd.lba import LBASolver, synthetic_problem
 
     prob = synthetic_problem(n_opt=a.kf, n_fixed=10, n_points=a.points, obs_per_point=a.obs, seed=1)
@@ -38,6 +43,25 @@ def main():
            "trials": r.lm_trials, "ms_per_solve_median": float(np.median(ts)), "ms_per_solve_min": float(min(ts)),
            "stage_ms_per_solve": {k: v[0] / a.solves for k, v in st.items()},
            "stage_launches_per_solve": {k: v[1] / a.solves for k, v in st.items()}}
+    if a.batch:
+        import torch
+
+        from mam3slam_amd.lba import DeviceBatch
+
+        probs = [synthetic_problem(n_opt=a.kf, n_fixed=10, n_points=a.points, obs_per_point=a.obs, seed=1 + q)
+                 for q in range(a.batch)]
+        for Q in sorted({1, a.batch}):
+            B = DeviceBatch(probs[:Q], torch.device("cuda", 0))
+            S.solve_batch_device(B)
+            torch.cuda.synchronize()
+            tb = []
+            for _ in range(max(3, a.solves // 2)):
+                t = time.perf_counter()
+                S.solve_batch_device(B)
+                tb.append((time.perf_counter() - t) * 1e3)
+            out[f"device_batch_{Q}"] = {"ms_per_batch_median": float(np.median(tb)),
+                                        "solves_per_s": Q / (float(np.median(tb)) * 1e-3),
+                                        "trials": [s["lm_trials"] for s in B.stats]}
     if a.oracle:
         from oracle import oracle_py
 
