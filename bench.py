@@ -1,20 +1,23 @@
 #!/usr/bin/env python3
 """bench.py — tracked frames/s of the MI355X ORB + local-BA hot path (BASELINE.json metric); one JSON line.
 
-Step = one pass of the hot path over one batch of B synthetic frames resident in HBM, i.e. what Tracking does
-per frame, batched:
-  1. ORB extraction (pyramid, per-cell FAST, DistributeOctTree, orientation, rBRIEF, lapping placement)
-  2. SearchByProjection(CurrentFrame, LastFrame, th=15)     (TrackWithMotionModel, Tracking.cc:2810)
-  3. SearchByProjection(F, localMapPoints, th=1), nnratio 0.8 (SearchLocalPoints, Tracking.cc:3146-3156),
-     with the keypoints matched in (2) taken
-and for --config c2 additionally one LocalBundleAdjustment (50 KF / 3000 MP, BASELINE configs[2]) per step,
-solved concurrently on its own HIP stream (the LocalMapping thread's work, Optimizer.cc:1116), followed by the
-shared-map exchange: the LBA write-back packed into fixed-size records, all-gathered over RCCL, applied in agent
-order.
-N GPUs = N agents, one process per GPU, each with its own frame stream: independent units, weak scaling; the only
-collective is that exchange (c2).
+A step is one pass of the hot path over B synthetic frames resident in HBM, one frame from each of B frame streams
+(agent sequences) on this GPU, with the keyframe cadence of the reference's Tracking -> LocalMapping hand-off:
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c1|c2]
+  Tracking, every frame, one HIP graph:
+    1. ORB extraction (pyramid, per-cell FAST, DistributeOctTree, orientation, rBRIEF, lapping placement)
+    2. SearchByProjection(CurrentFrame, LastFrame, th=15)            (TrackWithMotionModel, Tracking.cc:2810)
+    3. Frame::isInFrustum + MapPoint::PredictScale for every local MapPoint  (SearchLocalPoints, Tracking.cc:3119-3139)
+    4. SearchByProjection(F, localMapPoints, th=1), nnratio 0.8, matched keypoints taken (Tracking.cc:3146-3156)
+  LocalMapping (c2), concurrently on its own stream: every stream inserts a keyframe every K frames (--kf-every), so
+  B/K keyframes per step, each running LocalBundleAdjustment (LocalMapping.cc:162-172) on its 50-keyframe window of a
+  shared map in HBM (mam3slam_amd/mapping.py): window read from the map, the B/K solves batched with the Levenberg
+  control on the device, the write-backs all-gathered over RCCL and applied to every GPU's map, which the next
+  step's windows read.
+N GPUs = N processes, each with its own B streams and B/K windows (weak scaling); the one collective is the map
+exchange.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c1|c2] [--kf-every K]
 """
 from __future__ import annotations
 
@@ -33,19 +36,18 @@ sys.path.insert(0, ROOT)
 CONFIGS = {
     # BASELINE.json configs[1]: single-agent mono 640x480, 1000 features, 8 levels, extract + match
     "c1": dict(width=640, height=480, nfeatures=1000, lba=False),
-    # BASELINE.json configs[2]: 1280x720, 2000 features + LocalBundleAdjustment (50 KF / 3000 MapPoints)
+    # BASELINE.json configs[2]: 1280x720, 2000 features + LocalBundleAdjustment (50 KF / ~3000 MapPoints windows)
     "c2": dict(width=1280, height=720, nfeatures=2000, lba=True),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
-# what actually limits each stage: the byte/integer path has no MFMA work and most stages issue far
-# more VALU work per byte than the HBM roofline can see
+FP64_PEAK_TFS = 78.6    # MI355X FP64 vector / matrix (spec)
+# what limits each stage; the byte/integer path has no MFMA work
 ROOFLINE_NOTES = {
-    "fast": "VALU issue: FAST-9 strength is ~85 packed-f16 min3/max3 ops per pixel pair (DESIGN.md §3)",
-    "pyramid": "LDS-staged bilinear resize, latency-bound at 8 small launches",
-    "describe": "one wave per keypoint: LDS-free gathers from the blurred level (latency)",
+    "fast": "VALU issue: FAST-9 strength is 69 packed-f16 min3/max3 ops per pixel pair (DESIGN.md §3)",
+    "pyramid": "bilinear resize, latency-bound at 7 dependent launches",
+    "describe": "one wave per keypoint: IC-angle loads + the 37x37 blurred patch in LDS, two dependent round trips",
     "resolve": "one workgroup per frame, greedy dependency rounds (latency, LDS atomics)",
 }
-FP64_PEAK_TFS = 78.6    # MI355X FP64 vector (spec)
 
 
 def level_sizes(w, h, nlevels=8, scale=1.2):
@@ -57,7 +59,7 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
 
 
 def stage_bytes(w, h, n_kp, n_cand, n_last, n_mps, cand_motion, cand_local):
-    """Algorithmic HBM bytes per frame for each kernel stage (DESIGN.md §Roofline)."""
+    """Algorithmic HBM bytes per frame for each kernel stage (DESIGN.md §3)."""
     lv = level_sizes(w, h)
     P = sum(a * b for a, b in lv)
     P_ge1 = P - w * h
@@ -68,128 +70,19 @@ def stage_bytes(w, h, n_kp, n_cand, n_last, n_mps, cand_motion, cand_local):
         "blur": 2 * P,                             # read + write every level
         "distribute": 4 * n_cand + 8 * n_kp,       # read candidates, write kept keypoints + ranks
         "describe": n_kp * (961 + 37 * 37 + 60),   # 31x31 moment disk + 37x37 blurred patch + 60 B out
-        "grid": n_kp * (28 + 32 + 48),             # once per frame (the local search reuses it): keypoints +
-                                                   # descriptors in, 48-B cell-ordered records out
+        "grid": n_kp * (28 + 32 + 48),             # keypoints + descriptors in, 48-B cell-ordered records out
         "gather": n_last * 64 + n_mps * 64 + (cand_motion + cand_local) * (2 + 28 + 32 + 4),
         "resolve": (cand_motion + cand_local) * 4 + (n_last + n_mps) * 8 + 2 * n_kp * 4,
+        "frustum": n_mps * (80 + 64),              # mam_local_mp in, mam_mp_track out
     }
 
 
-def cpu_baseline(cfg, seconds=10.0):
-    """The oracle (single-thread C++ restatement of the reference path) on a bounded sample of the same
-    step workload: extraction + motion search + local-map search per frame."""
-    from mam3slam_amd import scene, synth
-    from oracle import oracle_py
-
-    p = oracle_py.params(cfg["nfeatures"])
-    W, H = cfg["width"], cfg["height"]
-    items = []
-    for i in range(4):
-        img = synth.make_frame(W, H, agent=0, frame=i)
-        k, d, _ = oracle_py.extract(img, p)
-        rng = np.random.default_rng(i)
-        F = scene.make_frame_data(k, d, W, H)
-        F.pose = scene.small_pose(rng)
-        cam = scene.pinhole(W, H)
-        items.append((img, scene.motion_last_frame(F, cam, rng), scene.local_mappoints(F, rng), F.pose, cam))
-    n, t0 = 0, time.perf_counter()
-    while True:
-        img, last, mps, pose, cam = items[n % len(items)]
-        k, d, _ = oracle_py.extract(img, p)
-        F = scene.make_frame_data(k, d, W, H)
-        F.pose = pose
-        _, out = oracle_py.search_by_projection_motion(F, last, cam, 15.0, True)
-        F.taken = (out >= 0).astype(np.uint8)
-        oracle_py.search_by_projection(F, mps, 1.0, nnratio=0.8)
-        n += 1
-        el = time.perf_counter() - t0
-        if (el >= seconds and n >= 5) or n >= 2000:
-            break
-    res = {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
-           "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15) + "
-                     f"SearchByProjection(local map, th 1) on the oracle C++ restatement, single thread, {el:.1f}s"}
-    if cfg["lba"]:
-        from mam3slam_amd.lba import synthetic_problem
-
-        prob = synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, seed=1)
-        t1 = time.perf_counter()
-        r = oracle_py.lba_solve(prob)
-        lba_ms = (time.perf_counter() - t1) * 1e3
-        res["lba_ms"] = lba_ms
-        res["sample"] += f"; LocalBundleAdjustment 50 KF/3000 MP ({len(prob.edge_point)} edges, {r.iterations} it) " \
-                         f"{lba_ms:.1f} ms"
-    return res
-
-
-def pose_section(args, B, W, H, NF, cam, kps_h, cnt_h, d_out1, lasts, dev, stream):
-    """Optimizer::PoseOptimization after the motion-model search (Tracking.cc:2836), measured beside the step (it is
-    not part of the headline metric): every frame's edges are its motion-search matches (keypoint, last-frame
-    MapPoint position), one workgroup per frame, B frames per launch; plus the single-frame launch and the oracle
-    on one host core (same edges)."""
-    import torch
-
-    from mam3slam_amd import pose, scene
-    from mam3slam_amd.orb import KP_DTYPE
-
-    out1 = d_out1.cpu().numpy()
-    sf, s2 = scene.scale_tables()
-    inv_s2 = (np.float32(1.0) / s2).astype(np.float32)
-    edges_l = []
-    for f in range(B):
-        n = int(cnt_h[f, 0])
-        o = out1[f, :n]
-        idx = np.nonzero(o >= 0)[0]
-        edges_l.append(pose.make_edges(kps_h[f, :n].view(KP_DTYPE), inv_s2, idx, lasts[f]["pos"][o[idx]]))
-    S = max(len(e) for e in edges_l)
-    E = np.zeros((B, S), pose.POSE_EDGE_DTYPE)
-    for f, e in enumerate(edges_l):
-        E[f, :len(e)] = e
-    P = pose.PoseOptimizer(device=dev.index or 0)
-    t_e = torch.from_numpy(E.view(np.uint8).reshape(B, -1)).to(dev)
-    t_n = torch.tensor([len(e) for e in edges_l], dtype=torch.int32, device=dev)
-    tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
-    rng = np.random.default_rng(7)
-    for f in range(B):
-        tcw[f]["q"], tcw[f]["t"] = scene.small_pose(rng)   # the motion model's guess around the frame's pose
-    t_p = torch.from_numpy(tcw.view(np.uint8)).to(dev)
-    t_o = torch.zeros((B, S), dtype=torch.uint8, device=dev)
-    t_r = torch.zeros((B, pose.POSE_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-
-    def run(nf):
-        P.optimize_batch_device(nf, t_p.data_ptr(), cam, t_e.data_ptr(), S, t_n.data_ptr(), t_o.data_ptr(),
-                                t_r.data_ptr(), stream=stream.cuda_stream)
-
-    run(B)
-    run(1)
-    torch.cuda.synchronize(dev)
-    reps = max(args.steps, 5)
-    P.set_profiling(True)
-    for _ in range(reps):
-        run(B)
-    torch.cuda.synchronize(dev)
-    ms_b = P.stage_times()["pose"][0] / reps
-    P.set_profiling(True)
-    for _ in range(reps):
-        run(1)
-    torch.cuda.synchronize(dev)
-    ms_1 = P.stage_times()["pose"][0] / reps
-    P.set_profiling(False)
-    res = t_r.cpu().numpy().view(pose.POSE_RESULT_DTYPE).reshape(B)
-    info = {"frames_per_launch": B, "edges_per_frame": float(np.mean([len(e) for e in edges_l])),
-            "ms_per_launch": ms_b, "frames_per_s": B / (ms_b * 1e-3), "ms_single_frame_launch": ms_1,
-            "iterations_per_frame": float(res["iterations"].mean()),
-            "lm_trials_per_frame": float(res["lm_trials"].mean()),
-            "inliers_per_frame": float(res["n_inliers"].mean())}
-    if not args.no_cpu_baseline and int(os.environ.get("RANK", "0")) == 0:
-        from oracle import oracle_py
-
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < 2.0 and n < B:
-            oracle_py.pose_optimization_edges((tcw[n]["q"], tcw[n]["t"]), cam, edges_l[n])
-            n += 1
-        info["cpu_ms_per_frame"] = (time.perf_counter() - t0) * 1e3 / n
-        info["cpu_sample"] = f"{n} frames, oracle C++ restatement, 1 thread"
-    return info
+def lba_flops(E, L, Np, m_avg, trials, iterations):
+    """Algorithmic FP64 flops of one LocalBundleAdjustment: per iteration E*420 (linearize + H
+    blocks), per trial Schur sum_l m_l (m_l + 1) / 2 * 216 + L (60 + 144 m) + (6 Np)^3 / 3 + L (36 m + 18) + E * 60."""
+    n = 6 * Np
+    per_trial = L * m_avg * (m_avg + 1) / 2 * 216 + L * (60 + 144 * m_avg) + n ** 3 / 3 + L * (36 * m_avg + 18) + E * 60
+    return iterations * E * 420 + trials * per_trial
 
 
 def _free_port() -> int:
@@ -212,6 +105,349 @@ def spawn_ranks(n: int, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
+# ------------------------------------------------------------------------------------------------------ tracking
+class TrackingLeg:
+    """B frames resident in HBM, split into lanes (sub-batches with their own contexts and HIP stream, captured
+    together into one HIP graph) so one lane's latency-bound stages overlap another's compute."""
+
+    def __init__(self, cfg, B, lanes, rank, dev):
+        import torch
+
+        from mam3slam_amd import ORBextractor, scene, synth
+        from mam3slam_amd.match import LAST_ENTRY_DTYPE, LOCAL_MP_DTYPE, MP_TRACK_DTYPE, FramesDev, ORBmatcher
+        from mam3slam_amd.orb import KP_DTYPE
+
+        self.dev, self.B, self.NL = dev, B, lanes
+        W, H, NF = cfg["width"], cfg["height"], cfg["nfeatures"]
+        self.W, self.H, self.NF = W, H, NF
+        BL = B // lanes
+        self.BL = BL
+        di = dev.index or 0
+        self.ext = ORBextractor(NF, 1.2, 8, 20, 7, device=di)
+        cap = self.ext.max_keypoints()
+        self.cap = cap
+        self.frames = np.stack([synth.make_frame(W, H, agent=rank, frame=i) for i in range(B)])
+        self.d_img = torch.from_numpy(self.frames).to(dev)
+        self.d_kps = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)
+        self.d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+        self.d_cnt = torch.zeros((B, 2), dtype=torch.int32, device=dev)
+        # one explicit stream orders extraction -> motion search -> frustum -> local search
+        self.tstream = torch.cuda.Stream(dev)
+        self.lanes = []
+        for l in range(lanes):
+            self.lanes.append({"lo": l * BL, "ext": self.ext if l == 0 else ORBextractor(NF, 1.2, 8, 20, 7, device=di),
+                               "stream": self.tstream if l == 0 else torch.cuda.Stream(dev)})
+        with torch.cuda.stream(self.tstream):
+            self._fork()
+            self._extract()
+            self._join()
+        torch.cuda.synchronize(dev)
+        kps_h = self.d_kps.cpu().numpy().view(KP_DTYPE).reshape(B, cap)
+        desc_h = self.d_desc.cpu().numpy()
+        cnt_h = self.d_cnt.cpu().numpy()
+        self.kps_h, self.cnt_h = kps_h, cnt_h
+        cam = scene.pinhole(W, H)
+        self.cam = cam
+        lasts, mpls, poses = [], [], []
+        F0 = None
+        for f in range(B):
+            rng = np.random.default_rng(1000 * rank + f)
+            F = scene.make_frame_data(kps_h[f, :cnt_h[f, 0]], desc_h[f, :cnt_h[f, 0]], W, H)
+            F.pose = scene.small_pose(rng, rot=0.1, trans=0.3)
+            F0 = F0 or F
+            lasts.append(scene.motion_last_frame(F, cam, rng))
+            mpls.append(scene.local_world_mappoints(F, cam, rng))
+            poses.append(F.pose)
+        self.F0, self.lasts, self.mpls, self.poses = F0, lasts, mpls, poses
+        Ls, Ms = max(len(x) for x in lasts), max(len(x) for x in mpls)
+        self.Ls, self.Ms = Ls, Ms
+        last = np.zeros((B, Ls), LAST_ENTRY_DTYPE)
+        mpw = np.zeros((B, Ms), LOCAL_MP_DTYPE)
+        tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+        for f in range(B):
+            last[f, :len(lasts[f])] = lasts[f]
+            mpw[f, :len(mpls[f])] = mpls[f]
+            tcw[f]["q"], tcw[f]["t"] = poses[f]
+        self.tcw_bytes = tcw.dtype.itemsize
+        self.d_last = torch.from_numpy(last.view(np.uint8).reshape(B, -1).copy()).to(dev)
+        self.d_mpw = torch.from_numpy(mpw.view(np.uint8).reshape(B, -1).copy()).to(dev)
+        self.d_mps = torch.zeros((B, Ms * MP_TRACK_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        self.d_tcw = torch.from_numpy(tcw.view(np.uint8).copy()).to(dev)
+        self.d_nlast = torch.tensor([len(x) for x in lasts], dtype=torch.int32, device=dev)
+        self.d_nmps = torch.tensor([len(x) for x in mpls], dtype=torch.int32, device=dev)
+        self.d_ntm = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_out1 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+        self.d_out2 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+        self.d_nm1 = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_nm2 = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_taken = torch.zeros((B, cap), dtype=torch.uint8, device=dev)
+        for ln in self.lanes:
+            lo = ln["lo"]
+            ln["mm"] = ORBmatcher(0.9, True, device=di)
+            # the local-map search shares the motion search's context and reuses the cell grid it built
+            ln["ml"] = ORBmatcher(0.8, True, device=di, share=ln["mm"])
+            ln["fr1"] = FramesDev(BL, cap, self.d_kps[lo].data_ptr(), self.d_desc[lo].data_ptr(),
+                                  self.d_cnt[lo].data_ptr(), None, self.d_taken[lo].data_ptr())
+            ln["fr2"] = FramesDev(BL, cap, self.d_kps[lo].data_ptr(), self.d_desc[lo].data_ptr(),
+                                  self.d_cnt[lo].data_ptr(), self.d_taken[lo].data_ptr(), None, 1)
+        self.graph = None
+
+    def _fork(self):
+        for ln in self.lanes[1:]:
+            ln["stream"].wait_stream(self.tstream)
+
+    def _join(self):
+        for ln in self.lanes[1:]:
+            self.tstream.wait_stream(ln["stream"])
+
+    def _extract_lane(self, ln):
+        lo, BL, W, H = ln["lo"], self.BL, self.W, self.H
+        ln["ext"].extract_batch_device(self.d_img[lo].data_ptr(), BL, W, H, W, W * H, self.d_kps[lo].data_ptr(),
+                                       self.d_desc[lo].data_ptr(), self.cap, self.d_cnt[lo].data_ptr(),
+                                       stream=ln["stream"].cuda_stream)
+
+    def _extract(self):
+        for ln in self.lanes:
+            self._extract_lane(ln)
+
+    def _match_lane(self, ln):
+        lo, st = ln["lo"], ln["stream"].cuda_stream
+        tcw = self.d_tcw.data_ptr() + lo * self.tcw_bytes
+        ln["mm"].search_motion_batch_device(self.F0, ln["fr1"], tcw, self.cam, self.d_last[lo].data_ptr(), self.Ls,
+                                            self.d_nlast[lo:].data_ptr(), 15.0, self.d_out1[lo].data_ptr(),
+                                            self.d_nm1[lo:].data_ptr(), stream=st)
+        ln["ml"].is_in_frustum_batch_device(self.F0, self.BL, tcw, self.cam, self.d_mpw[lo].data_ptr(), self.Ms,
+                                            self.d_nmps[lo:].data_ptr(), self.d_mps[lo].data_ptr(),
+                                            self.d_ntm[lo:].data_ptr(), stream=st)
+        ln["ml"].search_by_projection_batch_device(self.F0, ln["fr2"], self.d_mps[lo].data_ptr(), self.Ms,
+                                                   self.d_nmps[lo:].data_ptr(), 1.0, self.d_out2[lo].data_ptr(),
+                                                   self.d_nm2[lo:].data_ptr(), stream=st)
+
+    def launch(self):
+        self._fork()
+        self._extract()
+        for ln in self.lanes:
+            self._match_lane(ln)
+        self._join()
+
+    def capture(self):
+        import torch
+
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.tstream):
+            self.launch()
+
+    def step(self):
+        import torch
+
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            with torch.cuda.stream(self.tstream):
+                self.launch()
+
+    def stage_pass(self, steps):
+        """Per-stage kernel time (HIP events on the launch stream) over `steps` eager steps with the lanes run one
+        after another, so every launch is timed standalone (as in a --lanes 1 rocprofv3 kernel trace)."""
+        import torch
+
+        objs = [o for ln in self.lanes for o in (ln["ext"], ln["mm"])]
+        for o in objs:
+            o.set_profiling(True)
+        torch.cuda.synchronize(self.dev)
+        with torch.cuda.stream(self.tstream):
+            for _ in range(steps):
+                for ln in self.lanes:
+                    ln["stream"].wait_stream(self.tstream)
+                    self._extract_lane(ln)
+                    self._match_lane(ln)
+                    self.tstream.wait_stream(ln["stream"])
+                    torch.cuda.synchronize(self.dev)
+        stages = {}
+        for ln in self.lanes:
+            for k, v in ln["ext"].stage_times().items():
+                a = stages.get(k, (0.0, 0))
+                stages[k] = (a[0] + v[0], a[1] + v[1])
+            sm = ln["mm"].stage_times()
+            for k in ("grid", "gather", "resolve", "frustum"):
+                a = stages.get(k, (0.0, 0))
+                stages[k] = (a[0] + sm[k][0], a[1] + sm[k][1])
+        for o in objs:
+            o.set_profiling(False)
+        return stages
+
+
+# ------------------------------------------------------------------------------------------------------ sections
+def latency_section(tr):
+    """Single-frame latency: (a) one frame through the device-resident HIP graph (extract + motion search + frustum +
+    local search); (b) ORBextractor::operator() through the host C-ABI (mam_orb_extract: host image in, host
+    keypoints / descriptors out, synchronous), the drop-in path a Frame constructor calls."""
+    import torch
+
+    from mam3slam_amd.match import FramesDev
+
+    dev, cap = tr.dev, tr.cap
+    fr1 = FramesDev(1, cap, tr.d_kps.data_ptr(), tr.d_desc.data_ptr(), tr.d_cnt.data_ptr(), None,
+                    tr.d_taken.data_ptr())
+    fr2 = FramesDev(1, cap, tr.d_kps.data_ptr(), tr.d_desc.data_ptr(), tr.d_cnt.data_ptr(), tr.d_taken.data_ptr(),
+                    None, 1)
+    ln = tr.lanes[0]
+    st = tr.tstream.cuda_stream
+
+    def one_frame_launch():
+        tr.ext.extract_batch_device(tr.d_img.data_ptr(), 1, tr.W, tr.H, tr.W, tr.W * tr.H, tr.d_kps.data_ptr(),
+                                    tr.d_desc.data_ptr(), cap, tr.d_cnt.data_ptr(), stream=st)
+        ln["mm"].search_motion_batch_device(tr.F0, fr1, tr.d_tcw.data_ptr(), tr.cam, tr.d_last.data_ptr(), tr.Ls,
+                                            tr.d_nlast.data_ptr(), 15.0, tr.d_out1.data_ptr(), tr.d_nm1.data_ptr(),
+                                            stream=st)
+        ln["ml"].is_in_frustum_batch_device(tr.F0, 1, tr.d_tcw.data_ptr(), tr.cam, tr.d_mpw.data_ptr(), tr.Ms,
+                                            tr.d_nmps.data_ptr(), tr.d_mps.data_ptr(), tr.d_ntm.data_ptr(), stream=st)
+        ln["ml"].search_by_projection_batch_device(tr.F0, fr2, tr.d_mps.data_ptr(), tr.Ms, tr.d_nmps.data_ptr(), 1.0,
+                                                   tr.d_out2.data_ptr(), tr.d_nm2.data_ptr(), stream=st)
+
+    with torch.cuda.stream(tr.tstream):
+        one_frame_launch()
+    torch.cuda.synchronize(dev)
+    g1 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g1, stream=tr.tstream):
+        one_frame_launch()
+    torch.cuda.synchronize(dev)
+    for _ in range(5):
+        g1.replay()
+        torch.cuda.synchronize(dev)
+    lat = []
+    for _ in range(50):
+        t1 = time.perf_counter()
+        g1.replay()
+        torch.cuda.synchronize(dev)
+        lat.append((time.perf_counter() - t1) * 1e3)
+    img = tr.frames[0]
+    for _ in range(3):
+        tr.ext(img)
+    host = []
+    for _ in range(30):
+        t1 = time.perf_counter()
+        tr.ext(img)
+        host.append((time.perf_counter() - t1) * 1e3)
+    return {"device_graph_ms": float(np.median(lat)), "host_api_extract_ms": float(np.median(host))}
+
+
+def ingest_section(tr, reps=5):
+    """The PCIe legs the device-resident step leaves out: B frames host -> device from pinned memory, and the
+    keypoints + descriptors + counts device -> host, each timed alone (events on the copy stream); DESIGN.md §6
+    quotes the PCIe-inclusive rate."""
+    import torch
+
+    dev = tr.dev
+    h_img = torch.from_numpy(tr.frames).pin_memory()
+    h_kps = torch.empty(tuple(tr.d_kps.shape), dtype=torch.uint8).pin_memory()
+    h_desc = torch.empty(tuple(tr.d_desc.shape), dtype=torch.uint8).pin_memory()
+    h_cnt = torch.empty(tuple(tr.d_cnt.shape), dtype=torch.int32).pin_memory()
+    s = torch.cuda.Stream(dev)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    h2d, d2h = [], []
+    torch.cuda.synchronize(dev)
+    with torch.cuda.stream(s):
+        for _ in range(reps):
+            e[0].record(s)
+            tr.d_img.copy_(h_img, non_blocking=True)
+            e[1].record(s)
+            h_kps.copy_(tr.d_kps, non_blocking=True)
+            h_desc.copy_(tr.d_desc, non_blocking=True)
+            h_cnt.copy_(tr.d_cnt, non_blocking=True)
+            e[2].record(s)
+            s.synchronize()
+            h2d.append(e[0].elapsed_time(e[1]))
+            d2h.append(e[1].elapsed_time(e[2]))
+    bi = tr.frames.nbytes
+    bo = tr.d_kps.numel() + tr.d_desc.numel() + 4 * tr.d_cnt.numel()
+    m_in, m_out = float(np.median(h2d)), float(np.median(d2h))
+    return {"h2d_ms_per_step": m_in, "d2h_ms_per_step": m_out, "h2d_bytes_per_step": int(bi),
+            "d2h_bytes_per_step": int(bo), "h2d_GBs": bi / (m_in * 1e-3) / 1e9, "d2h_GBs": bo / (m_out * 1e-3) / 1e9}
+
+
+def parity_section(tr, mapping):
+    """In-run parity against the oracle: one frame's extraction, the same frame's frustum + local search chain, and
+    one LocalBundleAdjustment window of the timed region (the same inputs): bit-exact / index-exact / <= 1e-4 with
+    the same Levenberg control flow."""
+    from mam3slam_amd import scene
+    from mam3slam_amd.match import MP_TRACK_DTYPE
+    from oracle import oracle_py
+
+    out = {}
+    f = 1
+    ko, do, _ = oracle_py.extract(tr.frames[f], oracle_py.params(tr.NF))
+    n = int(tr.cnt_h[f, 0])
+    kg = tr.kps_h[f, :n]
+    dg = tr.d_desc[f, :n].cpu().numpy()
+    out["extract_bit_exact"] = bool(len(ko) == n and all(np.array_equal(kg[k], ko[k])
+                                                         for k in ("x", "y", "angle", "response", "octave"))
+                                    and np.array_equal(dg, do))
+    F = scene.make_frame_data(kg, dg, tr.W, tr.H)
+    F.pose = tr.poses[f]
+    no, to = oracle_py.is_in_frustum(F, tr.mpls[f], tr.cam)
+    tg = tr.d_mps[f].cpu().numpy().view(MP_TRACK_DTYPE)[:len(tr.mpls[f])]
+    v = to["track_in_view"] == 1
+    out["frustum_exact"] = bool(int(tr.d_ntm[f].item()) == no and np.array_equal(tg["proj_x"], to["proj_x"]) and
+                                np.array_equal(tg["proj_y"], to["proj_y"]) and
+                                np.array_equal(tg["scale_level"][v], to["scale_level"][v]))
+    # the local search's `taken` input: the slot state the motion search left (mvpMapPoints[i] holds a MapPoint with
+    # Observations() > 0), taken_out of the motion search of the same step
+    F.taken = tr.d_taken[f, :n].cpu().numpy()
+    nmo, oo = oracle_py.search_by_projection(F, to, 1.0, False, 50.0, 0.8)
+    out["local_search_index_exact"] = bool(int(tr.d_nm2[f].item()) == nmo and
+                                           np.array_equal(tr.d_out2[f, :n].cpu().numpy(), oo))
+    if mapping is not None:
+        w = 0
+        prob = mapping.window_inputs(w)
+        rg = mapping.window_result(w)
+        t0 = time.perf_counter()
+        ro = oracle_py.lba_solve(prob)
+        lba_cpu_ms = (time.perf_counter() - t0) * 1e3
+        rel = float(np.abs(ro.point_xyz - rg.point_xyz).max() / max(np.abs(ro.point_xyz).max(), 1e-12))
+        out["lba_same_control_flow"] = bool((ro.iterations, ro.lm_trials) == (rg.iterations, rg.lm_trials))
+        out["lba_max_point_rel_diff"] = rel
+        out["lba_window"] = {"iterations": int(ro.iterations), "trials": int(ro.lm_trials),
+                             "edges": int(len(prob.edge_point)), "oracle_ms": lba_cpu_ms}
+    return out
+
+
+def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0):
+    """The oracle (single-thread C++ restatement of the reference path) on a bounded sample of the same per-frame
+    work: extraction + motion search + isInFrustum + local search, plus 1/K of a LocalBundleAdjustment of a window of
+    the timed region (its oracle time measured in parity_section on the same inputs)."""
+    from mam3slam_amd import scene
+    from oracle import oracle_py
+
+    p = oracle_py.params(cfg["nfeatures"])
+    W, H = cfg["width"], cfg["height"]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        f = n % len(tr.frames)
+        k, d, _ = oracle_py.extract(tr.frames[f], p)
+        F = scene.make_frame_data(k, d, W, H)
+        F.pose = tr.poses[f]
+        _, out = oracle_py.search_by_projection_motion(F, tr.lasts[f], tr.cam, 15.0, True)
+        F.taken = (out >= 0).astype(np.uint8)
+        _, tracks = oracle_py.is_in_frustum(F, tr.mpls[f], tr.cam)
+        oracle_py.search_by_projection(F, tracks, 1.0, nnratio=0.8)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and n >= 5) or n >= 2000:
+            break
+    track_ms = el * 1e3 / n
+    per_frame_ms = track_ms + (lba_window_ms / K if lba_window_ms is not None else 0.0)
+    res = {"value": 1e3 / per_frame_ms, "unit": "frames/s", "cores": 1, "kind": "port",
+           "tracking_ms_per_frame": track_ms,
+           "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15) + "
+                     f"isInFrustum + SearchByProjection(local map, th 1) on the oracle C++ restatement, single thread, "
+                     f"{el:.1f}s"}
+    if lba_window_ms is not None:
+        res["lba_ms_per_window"] = lba_window_ms
+        res["sample"] += f"; + LocalBundleAdjustment of a timed-region window ({lba_window_ms:.1f} ms) / {K} frames"
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,17 +456,15 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU (independent frame streams)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
                     help="c2 (1280x720/2000 + LocalBundleAdjustment) is BASELINE.json's headline metric config")
+    ap.add_argument("--kf-every", type=int, default=8,
+                    help="keyframe cadence: each stream inserts a keyframe (one LocalBundleAdjustment) every K frames")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-graph", action="store_true", help="launch the tracking step eagerly instead of a HIP graph")
-    ap.add_argument("--no-latency", action="store_true",
-                    help="skip the B=1 latency section (profiling runs: every launch then covers one lane's batch)")
+    ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency and ingest sections")
     ap.add_argument("--no-pose", action="store_true", help="skip the PoseOptimization section")
-    ap.add_argument("--no-sin", action="store_true",
-                    help="skip the SearchInNeighbors section (Fuse + ComputeDistinctiveDescriptors)")
-    ap.add_argument("--lanes", type=int, default=4,
-                    help="independent sub-batches (agent groups) per GPU, each with its own contexts and HIP stream, "
-                         "so one group's latency-bound stages overlap another's compute")
+    ap.add_argument("--no-sin", action="store_true", help="skip the SearchInNeighbors section")
+    ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--launch-check", action="store_true",
                     help="rendezvous + barrier over gloo on the CPU and exit (tests the --gpus N launcher, no GPU)")
     args = ap.parse_args()
@@ -259,208 +493,61 @@ def main():
         else:
             print(json.dumps({"launch_check": "ok", "world": 1, "rank_sum": 0}), flush=True)
         return
-    if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    from mam3slam_amd import ORBextractor, scene, synth
-    from mam3slam_amd.match import LAST_ENTRY_DTYPE, MP_TRACK_DTYPE, FramesDev, ORBmatcher, Pose
-    from mam3slam_amd.orb import KP_DTYPE
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=dev)
 
     cfg = CONFIGS[args.config]
-    W, H, NF, B = cfg["width"], cfg["height"], cfg["nfeatures"], args.batch
-    NL = max(1, args.lanes)
+    B, NL, K = args.batch, max(1, args.lanes), max(1, args.kf_every)
     if B % NL:
         raise SystemExit(f"--batch {B} is not a multiple of --lanes {NL}")
-    BL = B // NL
-    ext = ORBextractor(NF, 1.2, 8, 20, 7, device=local)
-    cap = ext.max_keypoints()
-    frames = np.stack([synth.make_frame(W, H, agent=rank, frame=i) for i in range(B)])
-    d_img = torch.from_numpy(frames).to(dev)
-    d_kps = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)
-    d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
-    d_cnt = torch.zeros((B, 2), dtype=torch.int32, device=dev)
-    # one explicit stream orders extraction -> motion search -> local search (NULL would mean each library
-    # context's own stream: unordered with each other)
-    tstream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(tstream)
-    stream = tstream.cuda_stream
-
-    # lanes: frames [l * BL, (l + 1) * BL) run on lane l's stream with lane l's contexts
-    lanes = []
-    for l in range(NL):
-        lanes.append({"lo": l * BL, "ext": ext if l == 0 else ORBextractor(NF, 1.2, 8, 20, 7, device=local),
-                      "stream": tstream if l == 0 else torch.cuda.Stream(dev)})
-
-    def extract_lane(ln):
-        lo = ln["lo"]
-        ln["ext"].extract_batch_device(d_img[lo].data_ptr(), BL, W, H, W, W * H, d_kps[lo].data_ptr(),
-                                       d_desc[lo].data_ptr(), cap, d_cnt[lo].data_ptr(), stream=ln["stream"].cuda_stream)
-
-    def extract():
-        for ln in lanes:
-            extract_lane(ln)
-
-    def fork():
-        for ln in lanes[1:]:
-            ln["stream"].wait_stream(tstream)
-
-    def join():
-        for ln in lanes[1:]:
-            tstream.wait_stream(ln["stream"])
-
-    # ---- per-frame map structures around the frame's own features (built once; resident in HBM)
-    fork()
-    extract()
-    join()
-    torch.cuda.synchronize(dev)
-    kps_h = d_kps.cpu().numpy().view(KP_DTYPE).reshape(B, cap)
-    desc_h = d_desc.cpu().numpy()
-    cnt_h = d_cnt.cpu().numpy()
-    cam = scene.pinhole(W, H)
-    lasts, mpss, poses = [], [], []
-    F0 = None
-    for f in range(B):
-        rng = np.random.default_rng(1000 * rank + f)
-        F = scene.make_frame_data(kps_h[f, :cnt_h[f, 0]], desc_h[f, :cnt_h[f, 0]], W, H)
-        F.pose = scene.small_pose(rng)
-        F0 = F0 or F
-        lasts.append(scene.motion_last_frame(F, cam, rng))
-        mpss.append(scene.local_mappoints(F, rng))
-        poses.append(F.pose)
-    Ls, Ms = max(len(x) for x in lasts), max(len(x) for x in mpss)
-    last = np.zeros((B, Ls), LAST_ENTRY_DTYPE)
-    mps = np.zeros((B, Ms), MP_TRACK_DTYPE)
-    tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
-    for f in range(B):
-        last[f, :len(lasts[f])] = lasts[f]
-        mps[f, :len(mpss[f])] = mpss[f]
-        tcw[f]["q"], tcw[f]["t"] = poses[f]
-    d_last = torch.from_numpy(last.view(np.uint8).reshape(B, -1).copy()).to(dev)
-    d_mps = torch.from_numpy(mps.view(np.uint8).reshape(B, -1).copy()).to(dev)
-    d_tcw = torch.from_numpy(tcw.view(np.uint8).copy()).to(dev)
-    d_nlast = torch.tensor([len(x) for x in lasts], dtype=torch.int32, device=dev)
-    d_nmps = torch.tensor([len(x) for x in mpss], dtype=torch.int32, device=dev)
-    d_out1 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
-    d_out2 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
-    d_nm1 = torch.zeros(B, dtype=torch.int32, device=dev)
-    d_nm2 = torch.zeros(B, dtype=torch.int32, device=dev)
-    d_taken = torch.zeros((B, cap), dtype=torch.uint8, device=dev)
-    tcw_bytes = tcw.dtype.itemsize
-    for ln in lanes:
-        lo = ln["lo"]
-        ln["mm"] = ORBmatcher(0.9, True, device=local)
-        # the local-map search shares the motion search's context and reuses the frames' cell grid it built
-        # (AssignFeaturesToGrid runs once per Frame in the reference)
-        ln["ml"] = ORBmatcher(0.8, True, device=local, share=ln["mm"])
-        # the motion search leaves the frame's slot state in d_taken (taken_out): the local search's `taken` input
-        ln["fr1"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(), None,
-                              d_taken[lo].data_ptr())
-        ln["fr2"] = FramesDev(BL, cap, d_kps[lo].data_ptr(), d_desc[lo].data_ptr(), d_cnt[lo].data_ptr(),
-                              d_taken[lo].data_ptr(), None, 1)
-    m_motion, m_local = lanes[0]["mm"], lanes[0]["ml"]
-
-    def match_lane(ln):
-        lo, st = ln["lo"], ln["stream"]
-        ln["mm"].search_motion_batch_device(F0, ln["fr1"], d_tcw.data_ptr() + lo * tcw_bytes, cam,
-                                            d_last[lo].data_ptr(), Ls, d_nlast[lo:].data_ptr(), 15.0,
-                                            d_out1[lo].data_ptr(), d_nm1[lo:].data_ptr(), stream=st.cuda_stream)
-        ln["ml"].search_by_projection_batch_device(F0, ln["fr2"], d_mps[lo].data_ptr(), Ms, d_nmps[lo:].data_ptr(),
-                                                   1.0, d_out2[lo].data_ptr(), d_nm2[lo:].data_ptr(),
-                                                   stream=st.cuda_stream)
-
-    def match():
-        for ln in lanes:
-            match_lane(ln)
-
-    def track_launch():
-        fork()
-        extract()
-        match()
-        join()
-
-    lba_solver, lba_prob = None, None
+    tr = TrackingLeg(cfg, B, NL, rank, dev)
+    mapping = None
     if cfg["lba"]:
-        from mam3slam_amd.lba import LBASolver, synthetic_problem
+        from mam3slam_amd.mapping import LocalMappingLeg
 
-        from mam3slam_amd.exchange import MapUpdateExchange
+        mapping = LocalMappingLeg(max(1, B // K), rank, world, dev)
 
-        lba_solver = LBASolver(device=local)
-        lba_prob = synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, seed=1 + rank)
-        # shared-map exchange after every LBA: the agents' windows overlap in id space (a merged
-        # map), so replicas see conflicting writes resolved in agent order
-        exch = MapUpdateExchange(capacity=4096, device=dev)
-        d_pose_id = torch.from_numpy(lba_prob.pose_id).to(dev)
-        d_pose_fixed = torch.from_numpy(lba_prob.pose_fixed).to(dev)
-        d_point_id = torch.from_numpy(lba_prob.point_id - (int(lba_prob.pose_id.max()) + 1)).to(dev)
-        kf_cap, mp_cap = 1024, 1 << 16
-        d_kf_table = torch.zeros((kf_cap, 8), dtype=torch.float32, device=dev)
-        d_mp_table = torch.zeros((mp_cap, 4), dtype=torch.float32, device=dev)
-        d_xstatus = torch.zeros(1, dtype=torch.int32, device=dev)
+    lba_ms = []
 
-    lba_stats = {"n": 0, "ms": 0.0, "its": 0, "res": None}
-
-    def lba_worker():
+    def mapping_worker(step_idx):
         t = time.perf_counter()
-        r = lba_solver.solve(lba_prob)
-        lba_stats["ms"] += (time.perf_counter() - t) * 1e3
-        lba_stats["n"] += 1
-        lba_stats["its"] = r.iterations
-        lba_stats["res"] = r
+        mapping.run(step_idx)
+        lba_ms.append((time.perf_counter() - t) * 1e3)
 
-    def exchange_updates():
-        r = lba_stats["res"]
-        bad = None   # bad flags come from the host-side erase (nObs <= 2); the synthetic window tracks no counts
-        d_q = torch.from_numpy(r.pose_q).to(dev)
-        d_t = torch.from_numpy(r.pose_t).to(dev)
-        d_x = torch.from_numpy(r.point_xyz).to(dev)
-        exch.pack_lba(d_q.data_ptr(), d_t.data_ptr(), d_pose_id.data_ptr(), d_pose_fixed.data_ptr(), len(r.pose_q),
-                      d_x.data_ptr(), d_point_id.data_ptr(), bad, len(r.point_xyz), stream=stream)
-        exch.gather()
-        exch.apply(d_kf_table.data_ptr(), kf_cap, d_mp_table.data_ptr(), mp_cap, d_xstatus.data_ptr(), stream=stream)
-
-    graph = None
-
-    def track():
-        if graph is not None:
-            graph.replay()
-        else:
-            track_launch()
+    step_no = [0]
 
     def step():
         th = None
-        if lba_solver is not None:
-            th = threading.Thread(target=lba_worker)
+        if mapping is not None:
+            th = threading.Thread(target=mapping_worker, args=(step_no[0],))
             th.start()
-        track()
+        tr.step()
         if th is not None:
             th.join()
-            exchange_updates()
+        step_no[0] += 1
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if not args.no_graph:
-        # the tracking step (~30 launches) replayed as one HIP graph: no per-launch host gaps
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=tstream):
-            track_launch()
+        tr.capture()   # the tracking step (~40 launches) replayed as one HIP graph
         torch.cuda.synchronize(dev)
         for _ in range(2):
             step()
         torch.cuda.synchronize(dev)
-    cnt = d_cnt.cpu().numpy()
+    cnt = tr.d_cnt.cpu().numpy()
     n_kp = float(cnt[:, 0].mean())
     nf_probe = min(B, 4)
-    n_cand = float(sum(len(ext.debug_candidates(l, f)) for l in range(8) for f in range(nf_probe))) / nf_probe
-    nm1, nm2 = d_nm1.cpu().numpy(), d_nm2.cpu().numpy()
+    n_cand = float(sum(len(tr.ext.debug_candidates(l, f)) for l in range(8) for f in range(nf_probe))) / nf_probe
+    nm1, nm2, ntm = tr.d_nm1.cpu().numpy(), tr.d_nm2.cpu().numpy(), tr.d_ntm.cpu().numpy()
     if (nm1 < 0).any() or (nm2 < 0).any() or (cnt[:, 0] < 0).any():
         raise RuntimeError(f"device error codes in outputs: {nm1.min()} {nm2.min()} {cnt[:, 0].min()}")
 
-    lba_stats.update(n=0, ms=0.0)
-    if lba_solver is not None:
-        lba_solver.set_profiling(True)
+    lba_ms.clear()
+    if mapping is not None:
+        mapping.solver.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -471,97 +558,40 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    # per-stage kernel times (HIP events around every launch, on the stream it runs on) from the same number of
-    # eager tracking steps after the timed region: events cannot sit inside the replayed graph
-    # The lanes run one after another here (synchronised in between), so every launch is timed standalone, as
-    # in a --lanes 1 rocprofv3 kernel trace; stage_ms_per_step sums the lanes (work per step, not wall time).
-    objs = [o for ln in lanes for o in (ln["ext"], ln["mm"])]   # ml shares mm's context (and its stage timer)
-    for o in objs:
-        o.set_profiling(True)
-    torch.cuda.synchronize(dev)
-    for _ in range(args.steps):
-        for ln in lanes:
-            ln["stream"].wait_stream(tstream)
-            extract_lane(ln)
-            match_lane(ln)
-            tstream.wait_stream(ln["stream"])
-            torch.cuda.synchronize(dev)
-    stages = {}
-    for ln in lanes:
-        for k, v in ln["ext"].stage_times().items():
-            a = stages.get(k, (0.0, 0))
-            stages[k] = (a[0] + v[0], a[1] + v[1])
-        sm = ln["mm"].stage_times()   # both searches of the lane (one context)
-        for k in ("grid", "gather", "resolve"):
-            a = stages.get(k, (0.0, 0))
-            stages[k] = (a[0] + sm[k][0], a[1] + sm[k][1])
-    for o in objs:
-        o.set_profiling(False)
-    lba_stage = lba_solver.stage_times() if lba_solver is not None else None
-    # single-frame latency (B = 1, one HIP graph, synchronised per frame): the per-frame view of the north-star target
-    ext.set_profiling(False)
-    m_motion.set_profiling(False)
-    m_local.set_profiling(False)
-    fr1_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), None, d_taken.data_ptr())
-    fr2_1 = FramesDev(1, cap, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), d_taken.data_ptr(), None, 1)
+    lba_stage = None
+    if mapping is not None:
+        lba_stage = mapping.solver.stage_times()
+        mapping.solver.set_profiling(False)
+        stv = int(mapping.status.cpu().numpy()[0])
+        if stv != 0 or any(s[2] < 0 for s in mapping.stats):
+            raise RuntimeError(f"LocalMapping leg status {stv} / {mapping.stats}")
+    stages = tr.stage_pass(args.steps)
+    lat = None if args.no_latency else latency_section(tr)
+    ingest = None if args.no_latency else ingest_section(tr)
+    pose_info = None
+    if not args.no_pose:
+        from scripts import pose_bench
 
-    def one_frame_launch():
-        ext.extract_batch_device(d_img.data_ptr(), 1, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap,
-                                 d_cnt.data_ptr(), stream=stream)
-        m_motion.search_motion_batch_device(F0, fr1_1, d_tcw.data_ptr(), cam, d_last.data_ptr(), Ls,
-                                            d_nlast.data_ptr(), 15.0, d_out1.data_ptr(), d_nm1.data_ptr(),
-                                            stream=stream)
-        m_local.search_by_projection_batch_device(F0, fr2_1, d_mps.data_ptr(), Ms, d_nmps.data_ptr(), 1.0,
-                                                  d_out2.data_ptr(), d_nm2.data_ptr(), stream=stream)
-
-    def measure_latency():
-        one_frame_launch()
-        torch.cuda.synchronize(dev)
-        g1 = None
-        if not args.no_graph:
-            g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1, stream=tstream):
-                one_frame_launch()
-            torch.cuda.synchronize(dev)
-
-        def one_frame():
-            if g1 is not None:
-                g1.replay()
-            else:
-                one_frame_launch()
-            torch.cuda.synchronize(dev)
-
-        for _ in range(5):
-            one_frame()
-        lat = []
-        for _ in range(50):
-            t1 = time.perf_counter()
-            one_frame()
-            lat.append((time.perf_counter() - t1) * 1e3)
-        return float(np.median(lat))
-
-    latency_ms = None if args.no_latency else measure_latency()
-    pose_info = None if args.no_pose else pose_section(args, B, W, H, NF, cam, kps_h, cnt_h, d_out1, lasts, dev,
-                                                       tstream)
+        pose_info = pose_bench.section(tr, reps=max(args.steps, 5), oracle=not args.no_cpu_baseline and rank == 0)
     sin_info = None
     if not args.no_sin:
-        # LocalMapping::SearchInNeighbors' Hamming work, measured beside the step like the pose
-        # section: Fuse into 30 target keyframes + Fuse of 8000 candidates + ComputeDistinctiveDescriptors
         from scripts import fuse_bench
 
         sin_info = fuse_bench.run(args.config, reps=max(args.steps, 5), device=dev.index or 0,
                                   oracle=not args.no_cpu_baseline and rank == 0)
+    parity = parity_section(tr, mapping) if rank == 0 else None
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     T = float(t.item())
     frames_total = world * B * args.steps
 
-    # roofline of the dominant kernel stage: algorithmic bytes per launch / mean launch duration (HIP events
-    # recorded around each launch on the stream it runs on)
-    mean_last = float(np.mean([len(x) for x in lasts]))
-    mean_mps = float(np.mean([len(x) for x in mpss]))
-    sb = stage_bytes(W, H, n_kp, n_cand, mean_last, mean_mps, cand_motion=mean_last * 6.0, cand_local=mean_mps * 3.0)
+    # roofline of the dominant kernel stage: algorithmic bytes per launch / mean launch duration (HIP events on the
+    # stream each launch runs on)
+    mean_last = float(np.mean([len(x) for x in tr.lasts]))
+    mean_mps = float(np.mean([len(x) for x in tr.mpls]))
+    sb = stage_bytes(tr.W, tr.H, n_kp, n_cand, mean_last, mean_mps, cand_motion=mean_last * 6.0,
+                     cand_local=mean_mps * 3.0)
     per_step_ms = {k: v[0] / args.steps for k, v in stages.items()}
     dom = max(stages, key=lambda k: stages[k][0])
     ms_tot, launches = stages[dom]
@@ -578,10 +608,14 @@ def main():
             traffic = None
 
     if rank == 0:
-        workload = (f"{args.config}: mono {W}x{H}, {NF} features, 8 levels; step = {B} frames x (ORB extract + "
-                    f"SearchByProjection motion th15 + SearchByProjection local map th1)")
-        if cfg["lba"]:
-            workload += " + 1 LocalBundleAdjustment 50KF/3000MP per step (concurrent stream)"
+        W, H, NF = tr.W, tr.H, tr.NF
+        workload = (f"{args.config}: mono {W}x{H}, {NF} features, 8 levels; step = {B} frame streams x (ORB extract + "
+                    f"SearchByProjection motion th15 + isInFrustum + SearchByProjection local map th1)")
+        if mapping is not None:
+            workload += (f" + a keyframe every {K} frames per stream: {mapping.W} LocalBundleAdjustment windows "
+                         f"(50 KF + fixed, ~{int(np.mean([len(p.point_id) for p in mapping.probs]))} MapPoints) per "
+                         f"step over the shared map, batched, concurrent with tracking; write-backs exchanged and "
+                         f"applied to the map the next windows read")
         out = {
             "metric": "tracked frames/sec (ORB extract+match+localBA) at 1/2/4/8 GPUs vs CPU ref",
             "value": frames_total / T,
@@ -596,31 +630,52 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": workload, "frames_per_step_per_gpu": B, "width": W, "height": H,
-                       "nfeatures": NF, "keypoints_per_frame": n_kp, "fast_candidates_per_frame": n_cand,
+                       "nfeatures": NF, "keyframe_every": K if mapping is not None else None,
+                       "keypoints_per_frame": n_kp, "fast_candidates_per_frame": n_cand,
                        "last_frame_points": mean_last, "local_map_points": mean_mps,
+                       "local_points_in_view": float(ntm.mean()),
                        "matches_motion_per_frame": float(nm1.mean()), "matches_local_per_frame": float(nm2.mean()),
-                       "parallelism": f"agents{world} (one agent per GPU, independent)",
-                       "lanes": NL,
-                       "launch": "hip graph per tracking step" if graph is not None else "eager"},
+                       "parallelism": f"agents{world} (one process per GPU; {B} frame streams per GPU)",
+                       "lanes": NL, "launch": "hip graph per tracking step" if tr.graph is not None else "eager"},
             "stage_ms_per_step": per_step_ms,
-            "latency_ms_per_frame_b1": latency_ms,
-            "roofline": {"bound": "hbm", "kernel": dom, "limiter": ROOFLINE_NOTES.get(dom), "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": avg_ms},
+            "roofline": {"bound": "hbm", "kernel": dom, "limiter": ROOFLINE_NOTES.get(dom), "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms},
         }
+        if lat is not None:
+            out["latency_ms_per_frame_b1"] = lat["device_graph_ms"]
+            out["latency"] = lat
+        if ingest is not None:
+            out["ingest"] = ingest
+        if mapping is not None:
+            its = [s[0] for s in mapping.stats]
+            trials = [s[1] for s in mapping.stats]
+            E = float(np.mean(mapping.edges))
+            L = float(np.mean([len(p.point_id) for p in mapping.probs]))
+            Np = float(np.mean([int((p.pose_fixed == 0).sum()) for p in mapping.probs]))
+            fl = lba_flops(E, L, Np, E / L, float(np.mean(trials)), float(np.mean(its)))
+            solve_ms = float(np.mean(lba_ms)) if lba_ms else None
+            out["lba"] = {"windows_per_step": mapping.W, "ms_per_step_wall": solve_ms,
+                          "ms_per_window_wall": solve_ms / mapping.W if solve_ms else None,
+                          "iterations_mean": float(np.mean(its)), "trials_mean": float(np.mean(trials)),
+                          "edges_per_window": E, "points_per_window": L, "opt_keyframes": Np,
+                          "algorithmic_gflop_per_window": fl / 1e9,
+                          "achieved_fp64_tflops": (fl * mapping.W) / (solve_ms * 1e-3) / 1e12 if solve_ms else None,
+                          "fp64_peak_tflops": FP64_PEAK_TFS,
+                          "stage_ms_total": {k: v[0] for k, v in lba_stage.items()},
+                          "exchange_bytes_per_step": int(mapping.exch.send.numel() * world)}
         if pose_info is not None:
             out["pose_optimization"] = pose_info
         if sin_info is not None:
             out["search_in_neighbors"] = sin_info
-        if cfg["lba"]:
-            out["lba"] = {"solves": lba_stats["n"], "ms_per_solve_wall": lba_stats["ms"] / max(lba_stats["n"], 1),
-                          "iterations": lba_stats["its"], "edges": int(len(lba_prob.edge_point)),
-                          "stage_ms_total": {k: v[0] for k, v in lba_stage.items()}}
+        if parity is not None:
+            out["parity"] = parity
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
-            out["cpu_baseline"]["latency_ms_per_frame"] = 1e3 / out["cpu_baseline"]["value"]
-            if latency_ms:
-                out["speedup_latency_b1"] = out["cpu_baseline"]["latency_ms_per_frame"] / latency_ms
+            lba_cpu = parity.get("lba_window", {}).get("oracle_ms") if parity else None
+            out["cpu_baseline"] = cpu_baseline(tr, cfg, lba_cpu, K, args.cpu_seconds)
+            out["cpu_baseline"]["ms_per_frame"] = 1e3 / out["cpu_baseline"]["value"]
+            if lat is not None:
+                out["speedup_latency_b1"] = out["cpu_baseline"]["tracking_ms_per_frame"] / lat["device_graph_ms"]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

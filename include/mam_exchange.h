@@ -50,6 +50,35 @@ int mam_exchange_pack_lba(const double* pose_q, const double* pose_t, const int6
                           const uint8_t* point_bad, int n_points, int agent, mam_map_update* out, int capacity,
                           void* stream);
 
+/* An LBA window as the shared map sees it (DEVICE pointers): the vertex ids (pose_id = KeyFrame table row, point_id -
+ * mp_id_base = MapPoint table row) and the window's double-precision vertex arrays — the LBA inputs for
+ * mam_map_read_windows, the LBA results for mam_exchange_pack_windows. pose_fixed selects what the write-back
+ * carries (non-fixed poses), point_bad may be NULL. */
+typedef struct mam_map_window {
+    int32_t n_poses;
+    int32_t n_points;
+    const int64_t* pose_id;
+    const uint8_t* pose_fixed;
+    const int64_t* point_id;
+    const uint8_t* point_bad;
+    double* pose_q;
+    double* pose_t;
+    double* point_xyz;
+} mam_map_window;
+
+/* Build the vertex estimates of n_windows LBA windows from the shared tables (Optimizer.cc:1218, 1235, 1286: the
+ * float KeyFrame pose / MapPoint position cast to double): windows is a DEVICE array of descriptors; max_rows >=
+ * every window's max(n_poses, n_points). Ids outside the tables set *status to MAM_ERR_ARG. Asynchronous. */
+int mam_map_read_windows(const float* kf_table, int64_t kf_cap, const float* mp_table, int64_t mp_cap,
+                         int64_t mp_id_base, int n_windows, const mam_map_window* windows, int max_rows,
+                         int32_t* status, void* stream);
+
+/* mam_exchange_pack_lba for n_windows LBA results in one launch: window w (DEVICE descriptor array, result arrays)
+ * goes to block w of out (capacity + 1 records each); MapPoint record ids are point_id - mp_id_base. The blocks are
+ * applied like agents' blocks (mam_exchange_apply with n_agents = all gathered windows, in order). */
+int mam_exchange_pack_windows(int n_windows, const mam_map_window* windows, int64_t mp_id_base, int agent,
+                              mam_map_update* out, int capacity, void* stream);
+
 /* Apply gathered blocks (n_agents x (capacity+1) records, DEVICE) to device tables, agent 0 first:
  *   kf_table [kf_cap][8] floats (q xyzw, t, 1.0 = written), mp_table [mp_cap][4] floats (xyz, bad flag).
  * Records with an id outside the table or a malformed header set *status (device int32) to MAM_ERR_ARG and are

@@ -10,13 +10,13 @@
 
 namespace mam {
 
-// One workgroup: poses are compacted (non-fixed only, original order) with a block scan, points follow.
-__global__ __launch_bounds__(1024) void k_pack_lba(const double* __restrict__ pq, const double* __restrict__ pt,
-                                                   const int64_t* __restrict__ pid, const uint8_t* __restrict__ pfix,
-                                                   int n_poses, const double* __restrict__ xyz,
-                                                   const int64_t* __restrict__ mid, const uint8_t* __restrict__ mbad,
-                                                   int n_points, int agent, mam_map_update* __restrict__ out,
-                                                   int capacity) {
+// One workgroup: poses are compacted (non-fixed only, original order) with a block scan, points follow. MapPoint
+// record ids are point_id - mp_id_base (the table row).
+__device__ void pack_block(const double* __restrict__ pq, const double* __restrict__ pt,
+                           const int64_t* __restrict__ pid, const uint8_t* __restrict__ pfix, int n_poses,
+                           const double* __restrict__ xyz, const int64_t* __restrict__ mid,
+                           const uint8_t* __restrict__ mbad, int n_points, int64_t mp_id_base, int agent,
+                           mam_map_update* __restrict__ out, int capacity) {
     __shared__ int wsum[16];
     __shared__ int base;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(1024) void k_pack_lba(const double* __restrict__ pq
         const int r = n_opt + i;
         if (r >= capacity) break;
         mam_map_update u;
-        u.id = mid[i];
+        u.id = mid[i] - mp_id_base;
         u.kind = MAM_UPDATE_MP;
         u.agent = agent;
         for (int k = 0; k < 3; k++) u.v[k] = (float)xyz[3 * i + k];
@@ -78,6 +78,52 @@ __global__ __launch_bounds__(1024) void k_pack_lba(const double* __restrict__ pq
         h.kind = MAM_UPDATE_HEADER;
         h.agent = agent;
         out[0] = h;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_pack_lba(const double* __restrict__ pq, const double* __restrict__ pt,
+                                                   const int64_t* __restrict__ pid, const uint8_t* __restrict__ pfix,
+                                                   int n_poses, const double* __restrict__ xyz,
+                                                   const int64_t* __restrict__ mid, const uint8_t* __restrict__ mbad,
+                                                   int n_points, int agent, mam_map_update* __restrict__ out,
+                                                   int capacity) {
+    pack_block(pq, pt, pid, pfix, n_poses, xyz, mid, mbad, n_points, 0, agent, out, capacity);
+}
+
+// grid (n_windows): window w's write-back into block w of out (capacity + 1 records each)
+__global__ __launch_bounds__(1024) void k_pack_windows(const mam_map_window* __restrict__ win, int64_t mp_id_base,
+                                                       int agent, mam_map_update* __restrict__ out, int capacity) {
+    const mam_map_window& w = win[blockIdx.x];
+    pack_block(w.pose_q, w.pose_t, w.pose_id, w.pose_fixed, w.n_poses, w.point_xyz, w.point_id, w.point_bad,
+               w.n_points, mp_id_base, agent, out + (size_t)blockIdx.x * (capacity + 1), capacity);
+}
+
+// grid (ceil(max(P, L) / 256), n_windows): the window's vertex estimates from the shared tables, the float map values
+// cast to double as the reference builds its graph (Optimizer.cc:1218, 1235: SE3Quat(GetPose().unit_quaternion()
+// .cast<double>(), translation().cast<double>()); :1286: GetWorldPos().cast<double>())
+__global__ __launch_bounds__(256) void k_read_windows(const float* __restrict__ kf, int64_t kf_cap,
+                                                      const float* __restrict__ mp, int64_t mp_cap, int64_t mp_id_base,
+                                                      const mam_map_window* __restrict__ win,
+                                                      int32_t* __restrict__ status) {
+    const mam_map_window& w = win[blockIdx.y];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < w.n_poses) {
+        const int64_t id = w.pose_id[i];
+        if (id < 0 || id >= kf_cap) {
+            atomicExch(status, MAM_ERR_ARG);
+        } else {
+            const float* s = kf + id * 8;
+            for (int k = 0; k < 4; k++) w.pose_q[4 * (size_t)i + k] = (double)s[k];
+            for (int k = 0; k < 3; k++) w.pose_t[3 * (size_t)i + k] = (double)s[4 + k];
+        }
+    }
+    if (i < w.n_points) {
+        const int64_t r = w.point_id[i] - mp_id_base;
+        if (r < 0 || r >= mp_cap) {
+            atomicExch(status, MAM_ERR_ARG);
+        } else {
+            for (int k = 0; k < 3; k++) w.point_xyz[3 * (size_t)i + k] = (double)mp[r * 4 + k];
+        }
     }
 }
 
@@ -120,6 +166,28 @@ extern "C" int mam_exchange_pack_lba(const double* pose_q, const double* pose_t,
     if (n_points > capacity) return MAM_ERR_CAPACITY;
     hipLaunchKernelGGL(mam::k_pack_lba, dim3(1), dim3(1024), 0, (hipStream_t)stream, pose_q, pose_t, pose_id,
                        pose_fixed, n_poses, point_xyz, point_id, point_bad, n_points, agent, out, capacity);
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
+
+extern "C" int mam_exchange_pack_windows(int n_windows, const mam_map_window* windows, int64_t mp_id_base, int agent,
+                                         mam_map_update* out, int capacity, void* stream) {
+    if (n_windows < 0 || (n_windows > 0 && (!windows || !out)) || capacity < 0) return MAM_ERR_ARG;
+    if (n_windows == 0) return MAM_OK;
+    hipLaunchKernelGGL(mam::k_pack_windows, dim3(n_windows), dim3(1024), 0, (hipStream_t)stream, windows, mp_id_base,
+                       agent, out, capacity);
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
+
+extern "C" int mam_map_read_windows(const float* kf_table, int64_t kf_cap, const float* mp_table, int64_t mp_cap,
+                                    int64_t mp_id_base, int n_windows, const mam_map_window* windows, int max_rows,
+                                    int32_t* status, void* stream) {
+    if (!kf_table || !mp_table || !status || n_windows < 0 || max_rows < 0 || (n_windows > 0 && !windows))
+        return MAM_ERR_ARG;
+    if (n_windows == 0 || max_rows == 0) return MAM_OK;
+    hipLaunchKernelGGL(mam::k_read_windows, dim3((max_rows + 255) / 256, n_windows), dim3(256), 0, (hipStream_t)stream,
+                       kf_table, kf_cap, mp_table, mp_cap, mp_id_base, windows, status);
     MAM_HIP(hipGetLastError());
     return MAM_OK;
 }

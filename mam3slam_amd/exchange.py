@@ -26,7 +26,17 @@ _SIGS = {
                                         C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p]),
     "mam_exchange_apply": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                      C.c_void_p, C.c_void_p]),
+    "mam_exchange_pack_windows": (C.c_int, [C.c_int, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int, C.c_void_p]),
+    "mam_map_read_windows": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p,
+                                       C.c_int, C.c_void_p, C.c_void_p]),
 }
+
+
+class MapWindow(C.Structure):
+    """mam_map_window: an LBA window's vertex ids and double vertex arrays (device pointers)."""
+    _fields_ = [("n_poses", C.c_int32), ("n_points", C.c_int32), ("pose_id", C.c_void_p), ("pose_fixed", C.c_void_p),
+                ("point_id", C.c_void_p), ("point_bad", C.c_void_p), ("pose_q", C.c_void_p), ("pose_t", C.c_void_p),
+                ("point_xyz", C.c_void_p)]
 
 
 def _bind():
@@ -107,9 +117,14 @@ class MapUpdateExchange:
         self._pack_stream = int(stream)
 
     def apply(self, d_kf_table: int, kf_cap: int, d_mp_table: int, mp_cap: int, d_status: int, stream: int = 0,
-              gathered: int | None = None, n_agents: int | None = None):
+              gathered: int | None = None, n_agents: int | None = None, capacity: int | None = None):
         """Apply the gathered blocks (default: `recv`) to the device tables, agent 0 first. `stream` is ordered after
-        the collective (torch's current stream) before the apply kernel reads `recv`."""
+        the collective (torch's current stream) before the apply kernel reads `recv`. With window blocks
+        (pack_windows) pass the per-window capacity and n_agents = world x windows."""
+        cap = self.capacity if capacity is None else int(capacity)
+        nb = n_agents or self.world
+        if gathered is None and nb * (cap + 1) * RECORD_BYTES > self.recv.numel():
+            raise ValueError(f"apply: {nb} blocks of {cap + 1} records exceed the receive buffer")
         import torch
 
         if self.send.is_cuda:
@@ -117,9 +132,30 @@ class MapUpdateExchange:
             if st is not None:
                 st.wait_stream(torch.cuda.current_stream(self.send.device))
         check(self._lib().mam_exchange_apply(
-            C.c_void_p(gathered or self.recv.data_ptr()), n_agents or self.world, self.capacity,
+            C.c_void_p(gathered or self.recv.data_ptr()), nb, cap,
             C.c_void_p(d_kf_table), int(kf_cap), C.c_void_p(d_mp_table), int(mp_cap), C.c_void_p(d_status),
             C.c_void_p(stream)), "mam_exchange_apply")
+
+    def pack_windows(self, d_windows: int, n_windows: int, mp_id_base: int, capacity: int, stream: int = 0,
+                     agent: int | None = None):
+        """Pack n_windows LBA results (device descriptor array) into the send buffer, one block of `capacity` + 1
+        records per window (the send buffer must hold n_windows blocks: construct with capacity = n_windows *
+        (capacity + 1) - 1)."""
+        a = self.rank if agent is None else int(agent)
+        if n_windows * (capacity + 1) * RECORD_BYTES > self.send.numel():
+            raise ValueError(f"pack_windows: {n_windows} blocks of {capacity + 1} records exceed the send buffer")
+        check(self._lib().mam_exchange_pack_windows(int(n_windows), C.c_void_p(d_windows), int(mp_id_base), a,
+                                                    C.c_void_p(self.send.data_ptr()), int(capacity),
+                                                    C.c_void_p(stream)), "mam_exchange_pack_windows")
+        self._pack_stream = int(stream)
+
+    def read_windows(self, d_kf_table: int, kf_cap: int, d_mp_table: int, mp_cap: int, mp_id_base: int,
+                     d_windows: int, n_windows: int, max_rows: int, d_status: int, stream: int = 0):
+        """The windows' LBA inputs from the (just applied) shared tables, on `stream`."""
+        check(self._lib().mam_map_read_windows(C.c_void_p(d_kf_table), int(kf_cap), C.c_void_p(d_mp_table),
+                                               int(mp_cap), int(mp_id_base), int(n_windows), C.c_void_p(d_windows),
+                                               int(max_rows), C.c_void_p(d_status), C.c_void_p(stream)),
+              "mam_map_read_windows")
 
     @staticmethod
     def check_status(status_tensor):

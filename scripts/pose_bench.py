@@ -111,3 +111,75 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def section(tr, reps=20, oracle=True) -> dict:
+    """Optimizer::PoseOptimization after the motion-model search (Tracking.cc:2836), measured beside bench.py's step
+    (not part of the headline metric): every frame's edges are its motion-search matches (keypoint, last-frame
+    MapPoint position), one workgroup per frame, B frames per launch; plus the single-frame launch and the oracle on
+    one host core (same edges). `tr` is bench.py's TrackingLeg after a step."""
+    import torch
+
+    from mam3slam_amd import pose, scene
+    from mam3slam_amd.orb import KP_DTYPE
+
+    B, dev, cam = tr.B, tr.dev, tr.cam
+    out1 = tr.d_out1.cpu().numpy()
+    sf, s2 = scene.scale_tables()
+    inv_s2 = (np.float32(1.0) / s2).astype(np.float32)
+    edges_l = []
+    for f in range(B):
+        n = int(tr.cnt_h[f, 0])
+        o = out1[f, :n]
+        idx = np.nonzero(o >= 0)[0]
+        edges_l.append(pose.make_edges(tr.kps_h[f, :n].view(KP_DTYPE), inv_s2, idx, tr.lasts[f]["pos"][o[idx]]))
+    S = max(len(e) for e in edges_l)
+    E = np.zeros((B, S), pose.POSE_EDGE_DTYPE)
+    for f, e in enumerate(edges_l):
+        E[f, :len(e)] = e
+    P = pose.PoseOptimizer(device=dev.index or 0)
+    t_e = torch.from_numpy(E.view(np.uint8).reshape(B, -1)).to(dev)
+    t_n = torch.tensor([len(e) for e in edges_l], dtype=torch.int32, device=dev)
+    tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+    rng = np.random.default_rng(7)
+    for f in range(B):
+        tcw[f]["q"], tcw[f]["t"] = scene.small_pose(rng)   # the motion model's guess around the frame's pose
+    t_p = torch.from_numpy(tcw.view(np.uint8)).to(dev)
+    t_o = torch.zeros((B, S), dtype=torch.uint8, device=dev)
+    t_r = torch.zeros((B, pose.POSE_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    stream = tr.tstream.cuda_stream
+
+    def run(nf):
+        P.optimize_batch_device(nf, t_p.data_ptr(), cam, t_e.data_ptr(), S, t_n.data_ptr(), t_o.data_ptr(),
+                                t_r.data_ptr(), stream=stream)
+
+    run(B)
+    run(1)
+    torch.cuda.synchronize(dev)
+    P.set_profiling(True)
+    for _ in range(reps):
+        run(B)
+    torch.cuda.synchronize(dev)
+    ms_b = P.stage_times()["pose"][0] / reps
+    P.set_profiling(True)
+    for _ in range(reps):
+        run(1)
+    torch.cuda.synchronize(dev)
+    ms_1 = P.stage_times()["pose"][0] / reps
+    P.set_profiling(False)
+    res = t_r.cpu().numpy().view(pose.POSE_RESULT_DTYPE).reshape(B)
+    info = {"frames_per_launch": B, "edges_per_frame": float(np.mean([len(e) for e in edges_l])),
+            "ms_per_launch": ms_b, "frames_per_s": B / (ms_b * 1e-3), "ms_single_frame_launch": ms_1,
+            "iterations_per_frame": float(res["iterations"].mean()),
+            "lm_trials_per_frame": float(res["lm_trials"].mean()),
+            "inliers_per_frame": float(res["n_inliers"].mean())}
+    if oracle:
+        from oracle import oracle_py
+
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 2.0 and n < B:
+            oracle_py.pose_optimization_edges((tcw[n]["q"], tcw[n]["t"]), cam, edges_l[n])
+            n += 1
+        info["cpu_ms_per_frame"] = (time.perf_counter() - t0) * 1e3 / n
+        info["cpu_sample"] = f"{n} frames, oracle C++ restatement, 1 thread"
+    return info

@@ -134,3 +134,22 @@ def test_pack_apply_kernels(gpu_lib):
                 T[5].data_ptr(), T[6].data_ptr(), len(mid), stream=st.cuda_stream, agent=0)
     torch.cuda.synchronize()
     assert int(ex.send.cpu().numpy().view(xo.UPDATE_DTYPE)[0]["id"]) == xo.ERR_CAPACITY
+
+
+def test_world_windows_are_consistent():
+    """The synthetic shared map (mam3slam_amd/world.py): windows cut from it are the reference's LBA graphs —
+    50 local keyframes optimised (the init keyframe fixed), the keyframes observing their points outside the window
+    fixed, every observation of a window point an edge — and overlapping windows share keyframes and MapPoints."""
+    from mam3slam_amd import world as W
+
+    wd = W.make_world(n_kf=200, seed=3)
+    p0, k0, m0 = W.window(wd, 0)
+    p1, k1, m1 = W.window(wd, 25)
+    for p, k, s in ((p0, k0, 0), (p1, k1, 25)):
+        assert np.all(np.diff(p.pose_id) > 0) and np.all(np.diff(p.point_id) > 0)
+        local = (k >= s) & (k < s + 50) & (k != 0)
+        assert np.array_equal(p.pose_fixed == 0, local)
+        assert set(np.unique(p.edge_pose)) == set(range(len(k)))
+        assert len(p.point_id) > 2500 and len(p.edge_point) > 8 * 2500 * 0.9
+    assert len(np.intersect1d(k0, k1)) >= 25 and len(np.intersect1d(m0, m1)) > 1000
+    assert p0.pose_fixed[0] == 1   # keyframe 0: the map's init keyframe (Optimizer.cc:1220)
