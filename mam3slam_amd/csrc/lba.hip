@@ -78,6 +78,7 @@ struct Prob {
     int32_t* qe_idx;
     int32_t* cnt;                // [L + Np] counters / cursors of the device structure build
     int32_t* eidx;               // [Np][L] edge of (pose block, point), -1 if none
+    uint8_t* pairmask;           // [Np][Np] (i1 < i2): the two poses share a landmark (S block non-zero)
     // state: [2] buffers, lm->cur is the current one
     double* pose[2];             // [P][7] q(xyzw) t
     double* pt[2];               // [L][3]
@@ -239,6 +240,7 @@ __global__ __launch_bounds__(1024) void k_struct_init(const Prob* __restrict__ p
     }
     for (int i = g0; i < d.L + d.Np; i += gstride) d.cnt[i] = 0;
     for (size_t i = g0; i < (size_t)d.Np * d.L; i += gstride) d.eidx[i] = -1;
+    for (size_t i = g0; i < (size_t)d.Np * d.Np; i += gstride) d.pairmask[i] = 0;
     for (size_t i = g0; i < (size_t)d.npad * d.npad; i += gstride) d.S[i] = 0.0;
     for (int i = g0; i < d.P; i += gstride) {
         double q[4] = {d.pose_q[4 * i], d.pose_q[4 * i + 1], d.pose_q[4 * i + 2], d.pose_q[4 * i + 3]};
@@ -336,6 +338,15 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
             int m = k - 1;
             while (m >= 0 && s[m] > v) { s[m + 1] = s[m]; m--; }
             s[m + 1] = v;
+        }
+        // the S blocks this landmark contributes to (g2o's BlockSolver keeps only these, block_solver.hpp:181-224)
+        for (int a = 0; a < n; a++) {
+            const int ha = d.pose_h[d.edge_pose[s[a]]];
+            if (ha < 0) continue;
+            for (int b = a + 1; b < n; b++) {
+                const int hb = d.pose_h[d.edge_pose[s[b]]];
+                if (hb >= 0 && hb != ha) d.pairmask[(size_t)min(ha, hb) * d.Np + max(ha, hb)] = 1;
+            }
         }
         return;
     }
@@ -578,6 +589,15 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
     }
     const int i1 = blockIdx.x / d.Np, i2 = blockIdx.x % d.Np;
     if (i2 < i1) return;
+    if (i1 != i2 && !d.pairmask[(size_t)i1 * d.Np + i2]) {
+        // no shared landmark: a zero block (the factorization's fill-in of the previous trial is overwritten)
+        if (lane < 36) {
+            const int r = lane / 6, c = lane % 6, N = d.npad;
+            d.S[(size_t)(6 * i1 + r) * N + 6 * i2 + c] = 0.0;
+            d.S[(size_t)(6 * i2 + c) * N + 6 * i1 + r] = 0.0;
+        }
+        return;
+    }
     const double lambda = lm.lambda;
     double acc[36];
 #pragma unroll
@@ -1035,7 +1055,7 @@ struct Carver {
 size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
     const size_t nx = 6 * (size_t)Np + 3 * (size_t)L;
     return al(4 * (size_t)P) + al(4 * (size_t)Np) + al(4 * (size_t)(L + 1)) + al(4 * (size_t)E) +
-           al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) +
+           al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) +
            2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
            al(8 * (size_t)((E + 255) / 256 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
            al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
@@ -1053,6 +1073,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.qe_idx = cv.take<int32_t>(d.E);
     d.cnt = cv.take<int32_t>(d.L + d.Np);
     d.eidx = cv.take<int32_t>((size_t)d.Np * d.L);
+    d.pairmask = cv.take<uint8_t>((size_t)d.Np * d.Np);
     d.pose[0] = cv.take<double>(7 * (size_t)d.P);
     d.pose[1] = cv.take<double>(7 * (size_t)d.P);
     d.pt[0] = cv.take<double>(3 * (size_t)d.L);

@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--points", type=int, default=3000)
     ap.add_argument("--oracle", action="store_true")
     ap.add_argument("--batch", type=int, default=0, help="also time Q problems solved together on the device path")
+    ap.add_argument("--world", action="store_true",
+                    help="windows of the shared synthetic map (mam3slam_amd/world.py, banded covisibility) instead of "
+                         "synthetic_problem's random covisibility")
     a = ap.parse_args()
     if a.batch:
         import torch
@@ -29,7 +32,15 @@ def main():
         torch.cuda.init()   # torch's HIP runtime first: it does not attach after the library has initialised HIP
     from mam3slam_amd.lba import LBASolver, synthetic_problem
 
-    prob = synthetic_problem(n_opt=a.kf, n_fixed=10, n_points=a.points, obs_per_point=a.obs, seed=1)
+    if a.world:
+        from mam3slam_amd import world as W
+
+        wd = W.make_world(n_kf=25 * max(a.batch, 1) + 80, seed=7)
+        mk = lambda q: W.window(wd, 25 * q, n_opt=a.kf)[0]   # noqa: E731
+    else:
+        mk = lambda q: synthetic_problem(n_opt=a.kf, n_fixed=10, n_points=a.points, obs_per_point=a.obs,  # noqa: E731
+                                         seed=1 + q)
+    prob = mk(0)
     S = LBASolver()
     r = S.solve(prob)   # warm-up (allocations, code objects)
     S.set_profiling(True)
@@ -39,7 +50,8 @@ def main():
         r = S.solve(prob)
         ts.append((time.perf_counter() - t) * 1e3)
     st = S.stage_times()
-    out = {"kf": a.kf, "points": a.points, "edges": int(len(prob.edge_point)), "iterations": r.iterations,
+    out = {"kf": a.kf, "points": int(len(prob.point_id)), "edges": int(len(prob.edge_point)), "world": a.world,
+           "iterations": r.iterations,
            "trials": r.lm_trials, "ms_per_solve_median": float(np.median(ts)), "ms_per_solve_min": float(min(ts)),
            "stage_ms_per_solve": {k: v[0] / a.solves for k, v in st.items()},
            "stage_launches_per_solve": {k: v[1] / a.solves for k, v in st.items()}}
@@ -48,8 +60,7 @@ def main():
 
         from mam3slam_amd.lba import DeviceBatch
 
-        probs = [synthetic_problem(n_opt=a.kf, n_fixed=10, n_points=a.points, obs_per_point=a.obs, seed=1 + q)
-                 for q in range(a.batch)]
+        probs = [mk(q) for q in range(a.batch)]
         for Q in sorted({1, a.batch}):
             B = DeviceBatch(probs[:Q], torch.device("cuda", 0))
             S.solve_batch_device(B)
