@@ -4,7 +4,7 @@
  * the reference signatures. In the reference these are the real classes (src/Frame.cc, src/KeyFrame.cc,
  * src/MapPoint.cc, src/Map.cc); INTEGRATION.md shows the wrappers compiled against them instead.
  *
- * Scope: mono agents (mvuRight = -1, no second camera), Pinhole camera, no IMU. Mutex discipline follows the
+ * Scope: mono agents (mvuRight = -1, no second camera), Pinhole or KannalaBrandt8 camera, no IMU. Mutex discipline follows the
  * reference where the hot path takes locks (observations, pose, Map::mMutexMapUpdate).
  */
 #ifndef MAM3SLAM_MAP_H
@@ -30,7 +30,7 @@ class Map;
 class Frame {
 public:
     Frame() = default;
-    Frame(const ImageView& imGray, ORBextractor* extractor, const Pinhole* pCamera, unsigned long id = 0);
+    Frame(const ImageView& imGray, ORBextractor* extractor, const GeometricCamera* pCamera, unsigned long id = 0);
 
     void SetPose(const SE3f& Tcw) { mTcw = Tcw; mbHasPose = true; }
     const SE3f& GetPose() const { return mTcw; }
@@ -54,7 +54,7 @@ public:
     float mnMinX = 0.f, mnMaxX = 0.f, mnMinY = 0.f, mnMaxY = 0.f;
     float mfGridElementWidthInv = 0.f, mfGridElementHeightInv = 0.f;
 
-    const Pinhole* mpCamera = nullptr;
+    const GeometricCamera* mpCamera = nullptr;
     SE3f mTcw;
     bool mbHasPose = false;
 };
@@ -100,7 +100,7 @@ public:
     float mfLogScaleFactor;
     std::vector<float> mvScaleFactors, mvLevelSigma2, mvInvLevelSigma2;
     float mnMinX, mnMaxX, mnMinY, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv;
-    const Pinhole* mpCamera;
+    const GeometricCamera* mpCamera;
     /* DBoW2::BowVector / FeatureVector (node id -> feature indices, ascending node ids), set by ComputeBoW. */
     std::map<unsigned int, double> mBowVec;
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;

@@ -33,13 +33,17 @@ struct LocalBAWindow {
     std::vector<double> pose_q, pose_t, point_xyz, edge_obs, edge_inv_sigma2;
     std::vector<int32_t> pose_cam, edge_point, edge_pose;
     std::vector<float> cams;
-    std::vector<const Pinhole*> camera_list;
+    std::vector<const GeometricCamera*> camera_list;
+    int32_t cam_model = 0;
+    /* index of camera c in camera_list (appended with its parameters on first use); every camera of one window
+     * must be of the same model (mam_lba_problem.cam_model) */
+    int32_t cameraIndex(const GeometricCamera* c);
     mam_lba_problem Problem(int iterations = 10) const;
 };
 
 class Optimizer {
 public:
-    /* Optimizer::PoseOptimization(Frame*) (include/Optimizer.h, src/Optimizer.cc:814-1115), mono Pinhole frames: one
+    /* Optimizer::PoseOptimization(Frame*) (include/Optimizer.h, src/Optimizer.cc:814-1115), mono frames (Pinhole or KannalaBrandt8): one
      * edge per keypoint with a MapPoint (in keypoint order), the 4-round g2o solve on the GPU (include/mam_pose.h),
      * pFrame->mvbOutlier and the pose written back. Returns nInitialCorrespondences - nBad (0 below 3). */
     static int PoseOptimization(Frame* pFrame);

@@ -66,14 +66,36 @@ struct SE3f {
     mam_pose toC() const;
 };
 
-/* Pinhole camera (GeometricCamera::mvParameters = fx, fy, cx, cy as float; src/CameraModels/Pinhole.cpp). */
-struct Pinhole {
-    float mvParameters[4] = {0.f, 0.f, 0.f, 0.f};
+/* GeometricCamera (include/CameraModels/GeometricCamera.h:95-101) as a value: a Pinhole (mvParameters = fx, fy, cx, cy;
+ * src/CameraModels/Pinhole.cpp) or a KannalaBrandt8 (+ k0..k3, precision; src/CameraModels/KannalaBrandt8.cpp),
+ * float parameters as the reference stores them. project / unproject run the same code as the device
+ * (mam3slam_amd/csrc/camera.hpp). */
+struct GeometricCamera {
+    static const unsigned int CAM_PINHOLE = 0;
+    static const unsigned int CAM_FISHEYE = 1;
+    unsigned int mnType = CAM_PINHOLE;
+    float mvParameters[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float precision = 1e-6f;                                /* KannalaBrandt8::precision */
+    unsigned int GetType() const { return mnType; }
+    int size() const { return mnType == CAM_FISHEYE ? 8 : 4; }
+    void project(const float p3[3], float uv[2]) const;     /* Pinhole.cpp:35-41 / KannalaBrandt8.cpp:67-84 */
+    void unproject(const float p2[2], float ray[3]) const;  /* Pinhole.cpp:83-86 / KannalaBrandt8.cpp:116-143 */
+    void toK(float K[9]) const;                             /* Pinhole.cpp:100-104 / KannalaBrandt8.cpp:204-213 */
+    mam_camera toC() const;
+};
+
+struct Pinhole : GeometricCamera {
     Pinhole() = default;
-    Pinhole(float fx, float fy, float cx, float cy) : mvParameters{fx, fy, cx, cy} {}
-    void project(const float p3[3], float uv[2]) const;    /* Pinhole.cpp:35-41 */
-    void toK(float K[9]) const;                            /* Pinhole.cpp:100-104 */
-    mam_pinhole toC() const { return mam_pinhole{mvParameters[0], mvParameters[1], mvParameters[2], mvParameters[3]}; }
+    Pinhole(float fx, float fy, float cx, float cy) { mvParameters[0] = fx; mvParameters[1] = fy; mvParameters[2] = cx; mvParameters[3] = cy; }
+};
+
+struct KannalaBrandt8 : GeometricCamera {
+    KannalaBrandt8(float fx, float fy, float cx, float cy, float k0, float k1, float k2, float k3, float prec = 1e-6f) {
+        mnType = CAM_FISHEYE;
+        const float v[8] = {fx, fy, cx, cy, k0, k1, k2, k3};
+        for (int i = 0; i < 8; i++) mvParameters[i] = v[i];
+        precision = prec;
+    }
 };
 
 }  // namespace MAM3SLAM

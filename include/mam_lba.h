@@ -9,7 +9,7 @@
  * g2o sources followed: core/optimization_algorithm_levenberg.cpp:61-194, core/block_solver.hpp:353-604,
  *   core/base_binary_edge.hpp:54-120, core/robust_kernel_impl.cpp:76-91, core/sparse_optimizer.cpp:166-190,
  *   355-436, types/se3quat.h, types/types_six_dof_expmap.h:73-76, src/OptimizableTypes.cpp:139-160,
- *   src/CameraModels/Pinhole.cpp:35-81.
+ *   src/CameraModels/Pinhole.cpp:35-81, src/CameraModels/KannalaBrandt8.cpp:46-65, 145-175.
  *
  * The window construction (local / fixed keyframes, local MapPoints), the outlier erase and the write-back
  * under Map::mMutexMapUpdate stay in the host wrapper (mam3slam_amd/lba.py, the analogue of Optimizer.cc:1118-
@@ -20,6 +20,8 @@
 
 #include <stddef.h>
 #include <stdint.h>
+
+#include "mam_camera.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -46,13 +48,16 @@ typedef struct mam_lba_problem {
     const double* edge_obs;        /* [n_edges][2] keypoint (mvKeysUn) */
     const double* edge_inv_sigma2; /* information = invSigma2 * I2 */
     int32_t n_cams;
-    const float* cams;             /* [n_cams][4] Pinhole fx, fy, cx, cy (mvParameters, float) */
+    const float* cams;             /* [n_cams][4] Pinhole fx, fy, cx, cy or [n_cams][8] KannalaBrandt8 fx, fy, cx, cy,
+                                      k0..k3 (mvParameters, float), per cam_model */
     double huber_delta;            /* (double)(float)sqrt(5.991); <= 0: no robust kernel (setRobustKernel(0)) */
     int32_t iterations;            /* optimize(10) */
     const uint8_t* edge_active;    /* [n_edges] 1 = level 0, 0 = setLevel(1): left out of the optimisation
                                       (initializeOptimization(0)); NULL = all edges. A vertex left without active
                                       edges keeps its estimate. edge_chi2 of an inactive edge is not written. */
-    int32_t cam_model;             /* 0 = Pinhole (cams [n_cams][4]) */
+    int32_t cam_model;             /* MAM_CAM_PINHOLE (0) or MAM_CAM_KANNALA_BRANDT8 (1): EdgeSE3ProjectXYZ's
+                                      pCamera->project / projectJac (Pinhole.cpp:35-81, KannalaBrandt8.cpp:46-65,
+                                      145-175) */
     int32_t n_opt_poses;           /* number of poses with pose_fixed == 0: required by mam_lba_solve_batch_device
                                       (sizes the device work before the flags are read), ignored by mam_lba_solve */
 } mam_lba_problem;

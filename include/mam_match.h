@@ -1,7 +1,7 @@
 /*
  * mam_match.h — C-ABI drop-in boundary for MAM3SLAM's ORBmatcher hot-path searches (gfx950 / MI355X).
  *
- * Replaces (mono agents, Pinhole camera):
+ * Replaces (mono agents, Pinhole or KannalaBrandt8 camera, include/mam_camera.h):
  *   ORBmatcher::DescriptorDistance(a, b)                          reference: src/ORBmatcher.cc:2058-2074
  *   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
  *                                                                 reference: src/ORBmatcher.cc:43-213, 215-221
@@ -12,7 +12,8 @@
  *   ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight=false)          reference: src/ORBmatcher.cc:1148-1338
  *   MapPoint::ComputeDistinctiveDescriptors()                     reference: src/MapPoint.cc:329-403
  *   with Frame::GetFeaturesInArea / PosInGrid / AssignFeaturesToGrid (src/Frame.cc:385-416, 657-735) built
- *   on the device, and Pinhole::project / epipolarConstrain (src/CameraModels/Pinhole.cpp:35-41, 107-129).
+ *   on the device, and GeometricCamera::project / epipolarConstrain (src/CameraModels/Pinhole.cpp:35-41, 107-129,
+ *   src/CameraModels/KannalaBrandt8.cpp:67-84, 116-143, 216-220, 306-406).
  *
  * Pointers/objects of the reference become indices: a Frame's mvpMapPoints is passed as `taken` flags
  * (1 = slot holds a MapPoint with Observations() > 0, the only property the searches read) and results come
@@ -29,6 +30,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "mam_camera.h"
 #include "mam_orb.h"
 
 #ifdef __cplusplus
@@ -86,10 +88,8 @@ typedef struct mam_pose {
     float t[3];
 } mam_pose;
 
-/* Pinhole intrinsics (GeometricCamera::mvParameters, float). */
-typedef struct mam_pinhole {
-    float fx, fy, cx, cy;
-} mam_pinhole;
+/* Cameras: mam_camera (mam_camera.h) — Pinhole or KannalaBrandt8; mam_pinhole is its round-1 name. Every
+ * projection below goes through the camera's project (Pinhole.cpp:35-41 / KannalaBrandt8.cpp:67-84). */
 
 /* Last-frame entry for SearchByProjection(Cur, Last) (ORBmatcher.cc:1695-1712). 48 bytes. */
 typedef struct mam_last_entry {
@@ -149,7 +149,7 @@ int mam_search_by_projection(mam_match_ctx* ctx, const mam_frame_geom* geom, int
  * if the assignment was removed by the rotation-consistency pass (slot must become NULL), else -1 (untouched). tlw/mb are only read when !mono (bForward/bBackward, ORBmatcher.cc:1688-1692). */
 int mam_search_by_projection_motion(mam_match_ctx* ctx, const mam_frame_geom* geom, int n_cur,
                                     const mam_keypoint* keys, const uint8_t* desc, const uint8_t* taken,
-                                    const mam_pose* tcw, const mam_pose* tlw, float mb, const mam_pinhole* cam,
+                                    const mam_pose* tcw, const mam_pose* tlw, float mb, const mam_camera* cam,
                                     int n_last, const mam_last_entry* last, float th, int mono, int check_ori,
                                     int32_t* out_kp_to_last);
 
@@ -163,14 +163,40 @@ int mam_search_for_triangulation(mam_match_ctx* ctx, const mam_frame_geom* geom,
                                  const mam_featvec* fv2, const float* F12, const float* ep, int check_ori,
                                  int coarse, int32_t* out_match12);
 
-/* ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight=false) for a mono Pinhole keyframe (ORBmatcher.cc:1148-1338):
+/* The keyframe side of SearchForTriangulation(pKF1, pKF2, ...): mvKeysUn, mDescriptors, GetMapPoint(i) != NULL,
+ * mFeatVec, GetPose() and mpCamera. */
+typedef struct mam_tri_kf {
+    int32_t n;
+    const mam_keypoint* keys;
+    const uint8_t* desc;
+    const uint8_t* has_mp;
+    mam_featvec fv;
+    mam_pose tcw;
+    mam_camera cam;
+} mam_tri_kf;
+
+/* SearchForTriangulation(pKF1, pKF2, pairs, bOnlyStereo=false, bCoarse) for mono keyframes with Pinhole or
+ * KannalaBrandt8 cameras (ORBmatcher.cc:907-1146): the pair geometry of ORBmatcher.cc:913-930 (T12, the epipole) is
+ * computed here (mam_triangulation_geometry), then pCamera1->epipolarConstrain(pCamera2, ...): the F12 line test
+ * (Pinhole.cpp:107-129) or the two-view triangulation (KannalaBrandt8.cpp:216-220, 306-406). out_match12[kf1->n]:
+ * idx2 or -1; returns nmatches. */
+int mam_search_for_triangulation_kf(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_tri_kf* kf1,
+                                    const mam_tri_kf* kf2, int check_ori, int coarse, int32_t* out_match12);
+
+/* SearchForTriangulation's pair geometry (ORBmatcher.cc:913-930, Pinhole.cpp:109-112): T12 = T1w * T2w^-1 as R12
+ * (row-major 3x3) and t12, F12 = K1^T^-1 [t12]x R12 K2^-1 (row-major; meaningful for Pinhole cameras) and ep = cam2's
+ * projection of KF1's centre. Any output may be NULL. Host-only arithmetic, no device work. */
+int mam_triangulation_geometry(const mam_pose* t1w, const mam_pose* t2w, const mam_camera* cam1,
+                               const mam_camera* cam2, float* R12, float* t12, float* F12, float* ep);
+
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight=false) for a mono keyframe (ORBmatcher.cc:1148-1338):
  * the per-MapPoint search. keys/desc = pKF->mvKeysUn / mDescriptors (n keypoints). out_idx[i] = the keypoint
  * MapPoint i fuses with (bestDist <= TH_LOW), else -1; out_dist[i] = bestDist (256 = no candidate passed). The
  * replace-or-add side effects (:1311-1330) are the caller's, applied in list order with the isBad / IsInKeyFrame
  * tests re-evaluated: they never change another MapPoint's search. Returns the number of
  * MapPoints with out_idx >= 0. */
 int mam_fuse(mam_match_ctx* ctx, const mam_frame_geom* geom, int n, const mam_keypoint* keys, const uint8_t* desc,
-             const mam_fuse_kf* kf, const mam_pinhole* cam, int n_mps, const mam_fuse_mp* mps, float th,
+             const mam_fuse_kf* kf, const mam_camera* cam, int n_mps, const mam_fuse_mp* mps, float th,
              int32_t* out_idx, int32_t* out_dist);
 
 /* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403) for n_mps MapPoints at once: MapPoint m's observed
@@ -210,7 +236,7 @@ int mam_search_by_projection_batch_device(mam_match_ctx* ctx, const mam_frame_ge
 /* Frame f (current) matches n_last[f] last-frame entries at last + f*last_stride with pose tcw[f]. */
 int mam_search_by_projection_motion_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom,
                                                  const mam_frames_dev* frames, const mam_pose* tcw,
-                                                 const mam_pinhole* cam, const mam_last_entry* last, int last_stride,
+                                                 const mam_camera* cam, const mam_last_entry* last, int last_stride,
                                                  const int32_t* n_last, float th, int check_ori,
                                                  int32_t* out_kp_to_last, int32_t* out_nmatches, void* stream);
 
@@ -218,7 +244,7 @@ int mam_search_by_projection_motion_batch_device(mam_match_ctx* ctx, const mam_f
  * (frames: its keypoints) with kfs[f] searches n_mps[f] MapPoints at mps + f*mp_stride. Outputs at
  * out_idx / out_dist + f*mp_stride and out_nfused[f]. */
 int mam_fuse_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_frames_dev* frames,
-                          const mam_fuse_kf* kfs, const mam_pinhole* cam, const mam_fuse_mp* mps, int mp_stride,
+                          const mam_fuse_kf* kfs, const mam_camera* cam, const mam_fuse_mp* mps, int mp_stride,
                           const int32_t* n_mps, float th, int32_t* out_idx, int32_t* out_dist, int32_t* out_nfused,
                           void* stream);
 
@@ -227,19 +253,19 @@ int mam_compute_distinctive_descriptors_batch_device(mam_match_ctx* ctx, int n_m
                                                      const uint8_t* descs, int32_t* out_best, void* stream);
 
 /* Tracking::SearchLocalPoints' projection loop (Tracking.cc:3119-3139): Frame::isInFrustum(pMP, view_cos_limit)
- * (Frame.cc:512-571, mono Pinhole) + MapPoint::PredictScale(dist, Frame*) (MapPoint.cc:531-546) for n_mps local
+ * (Frame.cc:512-571, mono) + MapPoint::PredictScale(dist, Frame*) (MapPoint.cc:531-546) for n_mps local
  * MapPoints of a frame with pose tcw (Sophus SE3f: mRcw = rotationMatrix(), mOw = inverse().translation()).
  * out[i] = the track fields SearchByProjection(F, vpMapPoints) reads (proj_x/proj_y = -1 where the projection left
  * the image; view_cos/track_depth/scale_level are 0 for a MapPoint not in view; is_bad, nobs and desc copied).
  * log_scale_factor = mfLogScaleFactor (log of the float scale factor). Returns nToMatch (MapPoints in view). */
-int mam_is_in_frustum(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_pose* tcw, const mam_pinhole* cam,
+int mam_is_in_frustum(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_pose* tcw, const mam_camera* cam,
                       float log_scale_factor, int n_mps, const mam_local_mp* mps, float view_cos_limit,
                       mam_mp_track* out);
 
 /* Batched: frame f (pose tcw[f]) projects n_mps[f] MapPoints at mps + f*mp_stride into out + f*mp_stride (the mps
  * input of mam_search_by_projection_batch_device); out_n_to_match[f] (may be NULL) = nToMatch. */
 int mam_is_in_frustum_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, int nframes, const mam_pose* tcw,
-                                   const mam_pinhole* cam, float log_scale_factor, const mam_local_mp* mps,
+                                   const mam_camera* cam, float log_scale_factor, const mam_local_mp* mps,
                                    int mp_stride, const int32_t* n_mps, float view_cos_limit, mam_mp_track* out,
                                    int32_t* out_n_to_match, void* stream);
 

@@ -1,8 +1,9 @@
 /*
  * mam_pose.h — C-ABI drop-in boundary for Optimizer::PoseOptimization (gfx950 / MI355X).
  *
- * Replaces the g2o solve of the reference call (src/Optimizer.cc:814-1115) for mono agents with a Pinhole
- * camera: one VertexSE3Expmap, EdgeSE3ProjectXYZOnlyPose mono edges (include/OptimizableTypes.h:31-57,
+ * Replaces the g2o solve of the reference call (src/Optimizer.cc:814-1115) for mono agents with a Pinhole or
+ * KannalaBrandt8 camera (include/mam_camera.h; project / projectJac of Pinhole.cpp:35-81, KannalaBrandt8.cpp:46-65,
+ * 145-175): one VertexSE3Expmap, EdgeSE3ProjectXYZOnlyPose mono edges (include/OptimizableTypes.h:31-57,
  * src/OptimizableTypes.cpp:49-63) with RobustKernelHuber(sqrt(5.991)), BlockSolver_6_3 + LinearSolverDense
  * (Eigen LDLT, solvers/linear_solver_dense.h:65-118) + OptimizationAlgorithmLevenberg
  * (core/optimization_algorithm_levenberg.cpp:61-169); four rounds of optimize(10), each restarted from the
@@ -18,6 +19,8 @@
 
 #include <stddef.h>
 #include <stdint.h>
+
+#include "mam_camera.h"
 
 #include "mam_match.h"
 
@@ -50,12 +53,12 @@ void mam_pose_destroy(mam_pose_ctx* ctx);
 
 /* One frame, host buffers, synchronous. tcw: the frame's current pose (Frame::GetPose()). outlier[n]:
  * mvbOutlier of edge e after the last round. Returns n_inliers (>= 0) or a negative MAM_ERR_*. */
-int mam_pose_optimization(mam_pose_ctx* ctx, const mam_pose* tcw, const mam_pinhole* cam, int n,
+int mam_pose_optimization(mam_pose_ctx* ctx, const mam_pose* tcw, const mam_camera* cam, int n,
                           const mam_pose_edge* edges, uint8_t* outlier, mam_pose_result* result);
 
 /* Batched, device-resident, asynchronous on `stream` (NULL = the context's stream): frame f has n_edges[f]
  * edges at edges + f * edge_stride and pose tcw[f]; outliers at outlier + f * edge_stride, results[f]. */
-int mam_pose_optimization_batch_device(mam_pose_ctx* ctx, int nframes, const mam_pose* tcw, const mam_pinhole* cam,
+int mam_pose_optimization_batch_device(mam_pose_ctx* ctx, int nframes, const mam_pose* tcw, const mam_camera* cam,
                                        const mam_pose_edge* edges, int edge_stride, const int32_t* n_edges,
                                        uint8_t* outlier, mam_pose_result* results, void* stream);
 

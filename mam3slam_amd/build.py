@@ -62,6 +62,7 @@ def host_needs_build() -> bool:
         return True
     t = os.path.getmtime(HOST_LIB)
     deps = _host_sources() + [os.path.join(r, f) for r, _, fs in os.walk(INCLUDE) for f in fs] + [LIB]
+    deps += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hpp")]   # camera.hpp, det_math.hpp
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 

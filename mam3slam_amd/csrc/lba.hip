@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "../../include/mam_lba.h"
+#include "camera.hpp"
 #include "runtime.hpp"
 
 namespace mam {
@@ -143,10 +144,20 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     const double* X = pts + 3 * (size_t)ip;
     double Xc[3];
     map_point(T, X, Xc);
-    const float* c = d.cams + 4 * (d.pose_cam ? d.pose_cam[ipose] : 0);
-    const double fx = c[0], fy = c[1];
-    const double u = c[0] * Xc[0] / Xc[2] + c[2];
-    const double v = c[1] * Xc[1] / Xc[2] + c[3];
+    const bool kb8 = d.cam_model == MAM_CAM_KANNALA_BRANDT8;
+    const float* c = d.cams + (kb8 ? 8 : 4) * (d.pose_cam ? d.pose_cam[ipose] : 0);
+    double u, v;
+    mam_camera cm;
+    if (kb8) {
+        cm.fx = c[0]; cm.fy = c[1]; cm.cx = c[2]; cm.cy = c[3];
+        cm.k[0] = c[4]; cm.k[1] = c[5]; cm.k[2] = c[6]; cm.k[3] = c[7];
+        cm.model = MAM_CAM_KANNALA_BRANDT8;
+        cm.precision = 0.0f;
+        cam::project_d(cm, Xc, &u, &v);   // KannalaBrandt8::project(Vector3d) (KannalaBrandt8.cpp:46-65)
+    } else {
+        u = c[0] * Xc[0] / Xc[2] + c[2];   // Pinhole::project (Pinhole.cpp:35-41)
+        v = c[1] * Xc[1] / Xc[2] + c[3];
+    }
     const double e0 = d.edge_obs[2 * e] - u, e1 = d.edge_obs[2 * e + 1] - v;
     d.err[2 * e] = e0;
     d.err[2 * e + 1] = e1;
@@ -166,7 +177,6 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     huber(chi, d.delta, &r0, &r1);
     if (!want_jac) return r0;
     const double x = Xc[0], y = Xc[1], z = Xc[2];
-    const double J0 = -(fx / z), J2 = -(-fx * x / (z * z)), J4 = -(fy / z), J5 = -(-fy * y / (z * z));
     // rotation matrix of T (Eigen toRotationMatrix)
     const double qx = T[0], qy = T[1], qz = T[2], qw = T[3];
     const double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
@@ -175,14 +185,35 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     const double R[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
                          txz - twy, tyz + twx, 1 - (txx + tyy)};
     double* o = d.jac + 21 * (size_t)e;
-    // A = J R (2x3), J = [[J0, 0, J2], [0, J4, J5]]
-    for (int k = 0; k < 3; k++) {
-        o[k] = J0 * R[k] + J2 * R[6 + k];
-        o[3 + k] = J4 * R[3 + k] + J5 * R[6 + k];
+    if (kb8) {
+        // J = -projectJac(Xc) (KannalaBrandt8.cpp:145-175), A = J R, B = J * SE3deriv (OptimizableTypes.cpp:150-159)
+        double P[6];
+        cam::project_jac_d(cm, Xc, P);
+        const double J[6] = {-P[0], -P[1], -P[2], -P[3], -P[4], -P[5]};
+        for (int r = 0; r < 2; r++) {
+            const double a0 = J[3 * r], a1 = J[3 * r + 1], a2 = J[3 * r + 2];
+            for (int k = 0; k < 3; k++) o[3 * r + k] = a0 * R[k] + a1 * R[3 + k] + a2 * R[6 + k];
+            double* B = o + 6 + 6 * r;
+            // SE3deriv = [[0,z,-y,1,0,0],[-z,0,x,0,1,0],[y,-x,0,0,0,1]]
+            B[0] = -a1 * z + a2 * y;
+            B[1] = a0 * z - a2 * x;
+            B[2] = -a0 * y + a1 * x;
+            B[3] = a0;
+            B[4] = a1;
+            B[5] = a2;
+        }
+    } else {
+        const double fx = c[0], fy = c[1];
+        const double J0 = -(fx / z), J2 = -(-fx * x / (z * z)), J4 = -(fy / z), J5 = -(-fy * y / (z * z));
+        // A = J R (2x3), J = [[J0, 0, J2], [0, J4, J5]]
+        for (int k = 0; k < 3; k++) {
+            o[k] = J0 * R[k] + J2 * R[6 + k];
+            o[3 + k] = J4 * R[3 + k] + J5 * R[6 + k];
+        }
+        // B = J * SE3deriv, SE3deriv = [[0,z,-y,1,0,0],[-z,0,x,0,1,0],[y,-x,0,0,0,1]]
+        o[6] = J2 * y;  o[7] = J0 * z - J2 * x; o[8] = -J0 * y; o[9] = J0; o[10] = 0.0; o[11] = J2;
+        o[12] = -J4 * z + J5 * y; o[13] = -J5 * x; o[14] = J4 * x; o[15] = 0.0; o[16] = J4; o[17] = J5;
     }
-    // B = J * SE3deriv, SE3deriv = [[0,z,-y,1,0,0],[-z,0,x,0,1,0],[y,-x,0,0,0,1]]
-    o[6] = J2 * y;  o[7] = J0 * z - J2 * x; o[8] = -J0 * y; o[9] = J0; o[10] = 0.0; o[11] = J2;
-    o[12] = -J4 * z + J5 * y; o[13] = -J5 * x; o[14] = J4 * x; o[15] = 0.0; o[16] = J4; o[17] = J5;
     o[18] = -(w * e0) * r1;
     o[19] = -(w * e1) * r1;
     o[20] = r1 * w;
@@ -1271,6 +1302,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
 
 bool problem_ok(const mam_lba_problem* p) {
     if (!p || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || !p->cams || p->n_cams < 1) return false;
+    if (p->cam_model != MAM_CAM_PINHOLE && p->cam_model != MAM_CAM_KANNALA_BRANDT8) return false;
     if ((p->n_poses > 0 && (!p->pose_fixed || !p->pose_q || !p->pose_t)) || (p->n_points > 0 && !p->point_xyz) ||
         (p->n_edges > 0 && (!p->edge_point || !p->edge_pose || !p->edge_obs || !p->edge_inv_sigma2)))
         return false;
@@ -1283,7 +1315,7 @@ Prob desc_of(const mam_lba_problem* p) {
     d.L = p->n_points;
     d.E = p->n_edges;
     d.n_cams = p->n_cams;
-    d.cam_model = 0;
+    d.cam_model = p->cam_model;
     d.delta = p->huber_delta;
     d.edge_point = p->edge_point;
     d.edge_pose = p->edge_pose;
@@ -1382,7 +1414,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     for (int i = 0; i < L; i++) ipl[pl[i]] = i;
     int Np = 0;
     for (int i = 0; i < P; i++) Np += p->pose_fixed[i] ? 0 : 1;
-    const int ncw = 4 * p->n_cams;
+    const int ncw = (p->cam_model == MAM_CAM_KANNALA_BRANDT8 ? 8 : 4) * p->n_cams;
     // staging layout (one H2D copy): inputs, then room for the outputs
     const size_t in_bytes = al(4 * (size_t)E) * 2 + al(16 * (size_t)E) + al(8 * (size_t)E) + al((size_t)E) +
                             al(4 * (size_t)ncw) + al(4 * (size_t)P) + al((size_t)P) + al(32 * (size_t)P) +
@@ -1491,7 +1523,7 @@ int mam_lba_solve_batch_device(mam_lba_ctx* c, int n_problems, const mam_lba_pro
         const mam_lba_problem* p = problems + q;
         const mam_lba_result* r = results + q;
         if (!problem_ok(p) || !r->pose_q || !r->pose_t || (p->n_points > 0 && !r->point_xyz) ||
-            p->n_opt_poses < 0 || p->n_opt_poses > p->n_poses || p->cam_model != 0)
+            p->n_opt_poses < 0 || p->n_opt_poses > p->n_poses)
             return MAM_ERR_ARG;
         hp[q] = desc_of(p);
         hp[q].Np = p->n_opt_poses;

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "../../include/mam_match.h"
+#include "camera.hpp"
 #include "runtime.hpp"
 
 #include <cstdio>
@@ -70,7 +71,7 @@ struct ProjArgs {
     int far_points;
     // mode 1
     const mam_pose* tcw;
-    mam_pinhole cam;
+    mam_camera cam;
     const mam_last_entry* last;
     int check_ori;
     // scratch
@@ -269,8 +270,8 @@ __device__ bool unit_window(const ProjArgs& p, int f, int j, Window* w) {
         const float zc = ((pz + qw * u2) + c2) + T.t[2];
         const float invzc = (float)(1.0 / (double)zc);
         if (invzc < 0) return false;
-        const float u = p.cam.fx * xc / zc + p.cam.cx;   // Pinhole::project (Pinhole.cpp:35-41)
-        const float v = p.cam.fy * yc / zc + p.cam.cy;
+        float u, v;
+        cam::project_f(p.cam, xc, yc, zc, &u, &v);   // CurrentFrame.mpCamera->project(x3Dc) (ORBmatcher.cc:1713)
         if (u < p.g.min_x || u > p.g.max_x) return false;
         if (v < p.g.min_y || v > p.g.max_y) return false;
         w->x = u;
@@ -902,11 +903,32 @@ struct TriArgs {
     const int32_t* work;      // per work item: position in feats1
     const int32_t* work_n2;   // per work item: [begin, end) in feats2 (2 ints)
     int nwork;
-    float F[9];
+    mam_camera cam1, cam2;    // pKF1->mpCamera, pKF2->mpCamera (pCamera1->epipolarConstrain(pCamera2, ...))
+    float F[9];               // Pinhole pairs: F12
+    float R12[9], t12[3];     // KannalaBrandt8 pairs: T12
     float ep[2];
     int coarse;
     int32_t* out;             // [n1]
 };
+
+// pCamera1->epipolarConstrain(pCamera2, kp1, kp2, R12, t12, sigma2[kp1.octave], sigma2[kp2.octave])
+// (ORBmatcher.cc:1069): Pinhole.cpp:107-129 for a Pinhole KF1 (line of kp1 through F12, the 3.84 sigma2 test),
+// KannalaBrandt8.cpp:216-220 (two-view triangulation, z1 > 1e-4) for a fisheye one. la/lb/lc: kp1's epipolar line,
+// r1: kp1's unprojected ray (per idx1, computed once).
+__device__ __forceinline__ bool tri_epipolar_ok(const TriArgs& a, const mam_keypoint& kp1, float la, float lb, float lc,
+                                                const float r1[3], const mam_keypoint& kp2) {
+    if (a.cam1.model == MAM_CAM_KANNALA_BRANDT8) {
+        float r2[3];
+        cam::kb8_unproject_f(a.cam2, kp2.x, kp2.y, r2);
+        return cam::kb8_triangulate_matches(a.cam1, a.cam2, kp1.x, kp1.y, r1, kp2.x, kp2.y, r2, a.R12, a.t12,
+                                            a.g.level_sigma2[kp1.octave], a.g.level_sigma2[kp2.octave]) > 0.0001f;
+    }
+    const float num = la * kp2.x + lb * kp2.y + lc;
+    const float den = la * la + lb * lb;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * a.g.level_sigma2[kp2.octave];
+}
 
 __global__ __launch_bounds__(256) void k_tri(TriArgs a) {
     const int gw = (int)(((long long)blockIdx.x * 256 + threadIdx.x) >> 6);
@@ -917,10 +939,12 @@ __global__ __launch_bounds__(256) void k_tri(TriArgs a) {
     const mam_keypoint kp1 = a.keys1[idx1];
     const uint8_t* d1 = a.desc1 + (size_t)idx1 * 32;
     const int b = a.work_n2[2 * gw], e = a.work_n2[2 * gw + 1];
-    // epipolar line of kp1 in image 2 (Pinhole::epipolarConstrain, Pinhole.cpp:114-117)
+    // epipolar line of kp1 in image 2 (Pinhole::epipolarConstrain, Pinhole.cpp:114-117) / kp1's ray (fisheye)
     const float la = kp1.x * a.F[0] + kp1.y * a.F[3] + a.F[6];
     const float lb = kp1.x * a.F[1] + kp1.y * a.F[4] + a.F[7];
     const float lc = kp1.x * a.F[2] + kp1.y * a.F[5] + a.F[8];
+    float r1[3] = {0.0f, 0.0f, 1.0f};
+    if (a.cam1.model == MAM_CAM_KANNALA_BRANDT8 && !a.coarse) cam::kb8_unproject_f(a.cam1, kp1.x, kp1.y, r1);
     unsigned best = 0xFFFFFFFFu;   // (dist << 16) | (0xFFFF - position): min = smallest dist, LAST position
     for (int i0 = b; i0 < e; i0 += 64) {
         const int i2 = i0 + lane;
@@ -933,15 +957,7 @@ __global__ __launch_bounds__(256) void k_tri(TriArgs a) {
                     const float distex = a.ep[0] - kp2.x;
                     const float distey = a.ep[1] - kp2.y;
                     if (!(distex * distex + distey * distey < 100 * a.g.scale_factors[kp2.octave])) {
-                        bool ok = a.coarse != 0;
-                        if (!ok) {
-                            const float num = la * kp2.x + lb * kp2.y + lc;
-                            const float den = la * la + lb * lb;
-                            if (den != 0) {
-                                const float dsqr = num * num / den;
-                                ok = dsqr < 3.84 * a.g.level_sigma2[kp2.octave];
-                            }
-                        }
+                        const bool ok = a.coarse != 0 || tri_epipolar_ok(a, kp1, la, lb, lc, r1, kp2);
                         if (ok) best = min(best, ((unsigned)dist << 16) | (0xFFFFu - (unsigned)(i2 - b)));
                     }
                 }
@@ -1010,7 +1026,7 @@ struct FuseArgs {
     mam_frame_geom g;
     mam_frames_dev fr;
     const mam_fuse_kf* kfs;
-    mam_pinhole cam;
+    mam_camera cam;
     const mam_fuse_mp* mps;
     int mp_stride;
     const int32_t* n_mps;
@@ -1041,8 +1057,8 @@ __device__ bool fuse_window(const FuseArgs& p, int f, const mam_fuse_mp& mp, Win
     const float yc = ((py + qw * u1) + c1) + K.tcw.t[1];
     const float zc = ((pz + qw * u2) + c2) + K.tcw.t[2];
     if (zc < 0.0f) return false;
-    const float u = p.cam.fx * xc / zc + p.cam.cx;   // Pinhole::project
-    const float v = p.cam.fy * yc / zc + p.cam.cy;
+    float u, v;
+    cam::project_f(p.cam, xc, yc, zc, &u, &v);   // pCamera->project(p3Dc) (ORBmatcher.cc:1210)
     if (!(u >= p.g.min_x && u < p.g.max_x && v >= p.g.min_y && v < p.g.max_y)) return false;   // KeyFrame::IsInImage
     const float maxD = 1.2f * mp.max_distance, minD = 0.8f * mp.min_distance;
     const float P0 = px - K.ow[0], P1 = py - K.ow[1], P2 = pz - K.ow[2];
@@ -1233,7 +1249,7 @@ __global__ __launch_bounds__(256) void k_distinct(const int32_t* __restrict__ of
 struct FrustumArgs {
     mam_frame_geom g;
     const mam_pose* tcw;
-    mam_pinhole cam;
+    mam_camera cam;
     float log_scale_factor, view_cos_limit;
     const mam_local_mp* mps;
     int mp_stride;
@@ -1292,8 +1308,8 @@ __global__ __launch_bounds__(256) void k_frustum(FrustumArgs a) {
             const float z = (fr[6] * P0 + (fr[7] * P1 + fr[8] * P2)) + fr[11];
             const float pc_dist = sqrtf(x * x + (y * y + z * z));
             if (z >= 0.0f) {
-                const float u = a.cam.fx * x / z + a.cam.cx;   // Pinhole::project(Vector3f)
-                const float v = a.cam.fy * y / z + a.cam.cy;
+                float u, v;
+                cam::project_f(a.cam, x, y, z, &u, &v);   // mpCamera->project(Pc) (Frame.cc:532)
                 if (!(u < a.g.min_x || u > a.g.max_x || v < a.g.min_y || v > a.g.max_y)) {
                     o.proj_x = u;
                     o.proj_y = v;
@@ -1575,7 +1591,7 @@ int mam_search_by_projection_batch_device(mam_match_ctx* c, const mam_frame_geom
 }
 
 int mam_search_by_projection_motion_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_frames_dev* fr,
-                                                 const mam_pose* tcw, const mam_pinhole* cam,
+                                                 const mam_pose* tcw, const mam_camera* cam,
                                                  const mam_last_entry* last, int last_stride, const int32_t* n_last,
                                                  float th, int check_ori, int32_t* out, int32_t* out_n, void* stream) {
     if (!c || !geom_ok(g) || !fr || !tcw || !cam || !last || !n_last || !out || !out_n || last_stride <= 0)
@@ -1666,7 +1682,7 @@ int mam_search_by_projection(mam_match_ctx* c, const mam_frame_geom* g, int n, c
 
 int mam_search_by_projection_motion(mam_match_ctx* c, const mam_frame_geom* g, int n, const mam_keypoint* keys,
                                     const uint8_t* desc, const uint8_t* taken, const mam_pose* tcw,
-                                    const mam_pose* tlw, float mb, const mam_pinhole* cam, int n_last,
+                                    const mam_pose* tlw, float mb, const mam_camera* cam, int n_last,
                                     const mam_last_entry* last, float th, int mono, int check_ori, int32_t* out) {
     (void)tlw; (void)mb;
     if (!c || !geom_ok(g) || !tcw || !cam || n < 0 || n_last < 0 || (n > 0 && (!keys || !desc || !out)) ||
@@ -1704,12 +1720,12 @@ int mam_search_by_projection_motion(mam_match_ctx* c, const mam_frame_geom* g, i
     return MAM_ERR_CAPACITY;
 }
 
-int mam_search_for_triangulation(mam_match_ctx* c, const mam_frame_geom* g, int n1, const mam_keypoint* keys1,
-                                 const uint8_t* desc1, const uint8_t* has1, const mam_featvec* fv1, int n2,
-                                 const mam_keypoint* keys2, const uint8_t* desc2, const uint8_t* has2,
-                                 const mam_featvec* fv2, const float* F12, const float* ep, int check_ori, int coarse,
-                                 int32_t* out) {
-    if (!c || !geom_ok(g) || !fv1 || !fv2 || !F12 || !ep || n1 < 0 || n2 < 0 || (n1 > 0 && (!keys1 || !desc1 || !has1 || !out)) ||
+// The search of one keyframe pair; geometry (F12 / R12, t12 / ep) and cameras already set in `ga`.
+static int tri_search(mam_match_ctx* c, const mam_frame_geom* g, int n1, const mam_keypoint* keys1,
+                      const uint8_t* desc1, const uint8_t* has1, const mam_featvec* fv1, int n2,
+                      const mam_keypoint* keys2, const uint8_t* desc2, const uint8_t* has2, const mam_featvec* fv2,
+                      const mam::TriArgs& ga, int check_ori, int coarse, int32_t* out) {
+    if (!c || !geom_ok(g) || !fv1 || !fv2 || n1 < 0 || n2 < 0 || (n1 > 0 && (!keys1 || !desc1 || !has1 || !out)) ||
         (n2 > 0 && (!keys2 || !desc2 || !has2)))
         return MAM_ERR_ARG;
     MAM_DEVICE_SCOPE(c->device);
@@ -1744,7 +1760,7 @@ int mam_search_for_triangulation(mam_match_ctx* c, const mam_frame_geom* g, int 
                          carve_bytes(2 * std::max(nw, 1), 4) + carve_bytes(n1, 4) + carve_bytes(1, 4);
     if (int rc = c->stage.alloc(bytes)) return rc;
     uint8_t* p = c->stage.p;
-    mam::TriArgs a{};
+    mam::TriArgs a = ga;
     a.g = *g;
     mam_keypoint* dk1 = carve<mam_keypoint>(p, n1);
     uint8_t* dd1 = carve<uint8_t>(p, (size_t)n1 * 32);
@@ -1778,8 +1794,6 @@ int mam_search_for_triangulation(mam_match_ctx* c, const mam_frame_geom* g, int 
     a.keys2 = dk2; a.desc2 = dd2; a.has2 = dh2;
     a.feats1 = df1; a.feats2 = df2;
     a.work = dw; a.work_n2 = dw2; a.nwork = nw;
-    for (int i = 0; i < 9; i++) a.F[i] = F12[i];
-    a.ep[0] = ep[0]; a.ep[1] = ep[1];
     a.coarse = coarse;
     a.out = dout;
     {
@@ -1795,8 +1809,52 @@ int mam_search_for_triangulation(mam_match_ctx* c, const mam_frame_geom* g, int 
     return nm;
 }
 
+int mam_search_for_triangulation(mam_match_ctx* c, const mam_frame_geom* g, int n1, const mam_keypoint* keys1,
+                                 const uint8_t* desc1, const uint8_t* has1, const mam_featvec* fv1, int n2,
+                                 const mam_keypoint* keys2, const uint8_t* desc2, const uint8_t* has2,
+                                 const mam_featvec* fv2, const float* F12, const float* ep, int check_ori, int coarse,
+                                 int32_t* out) {
+    if (!F12 || !ep) return MAM_ERR_ARG;
+    mam::TriArgs a{};   // Pinhole cameras (model 0): only F12 / ep are read
+    for (int i = 0; i < 9; i++) a.F[i] = F12[i];
+    a.ep[0] = ep[0];
+    a.ep[1] = ep[1];
+    return tri_search(c, g, n1, keys1, desc1, has1, fv1, n2, keys2, desc2, has2, fv2, a, check_ori, coarse, out);
+}
+
+int mam_triangulation_geometry(const mam_pose* t1w, const mam_pose* t2w, const mam_camera* cam1,
+                               const mam_camera* cam2, float* R12, float* t12, float* F12, float* ep) {
+    if (!t1w || !t2w || !cam1 || !cam2) return MAM_ERR_ARG;
+    mam::cam::PairGeom pg;
+    mam::cam::pair_geometry(t1w->q, t1w->t, t2w->q, t2w->t, *cam1, *cam2, &pg);
+    if (R12) for (int i = 0; i < 9; i++) R12[i] = pg.R12[i];
+    if (t12) for (int i = 0; i < 3; i++) t12[i] = pg.t12[i];
+    if (F12) for (int i = 0; i < 9; i++) F12[i] = pg.F12[i];
+    if (ep) { ep[0] = pg.ep[0]; ep[1] = pg.ep[1]; }
+    return MAM_OK;
+}
+
+int mam_search_for_triangulation_kf(mam_match_ctx* c, const mam_frame_geom* g, const mam_tri_kf* kf1,
+                                    const mam_tri_kf* kf2, int check_ori, int coarse, int32_t* out) {
+    if (!kf1 || !kf2) return MAM_ERR_ARG;
+    if ((kf1->cam.model != MAM_CAM_PINHOLE && kf1->cam.model != MAM_CAM_KANNALA_BRANDT8) ||
+        (kf2->cam.model != MAM_CAM_PINHOLE && kf2->cam.model != MAM_CAM_KANNALA_BRANDT8))
+        return MAM_ERR_ARG;
+    mam::cam::PairGeom pg;
+    mam::cam::pair_geometry(kf1->tcw.q, kf1->tcw.t, kf2->tcw.q, kf2->tcw.t, kf1->cam, kf2->cam, &pg);
+    mam::TriArgs a{};
+    a.cam1 = kf1->cam;
+    a.cam2 = kf2->cam;
+    for (int i = 0; i < 9; i++) { a.F[i] = pg.F12[i]; a.R12[i] = pg.R12[i]; }
+    for (int i = 0; i < 3; i++) a.t12[i] = pg.t12[i];
+    a.ep[0] = pg.ep[0];
+    a.ep[1] = pg.ep[1];
+    return tri_search(c, g, kf1->n, kf1->keys, kf1->desc, kf1->has_mp, &kf1->fv, kf2->n, kf2->keys, kf2->desc,
+                      kf2->has_mp, &kf2->fv, a, check_ori, coarse, out);
+}
+
 int mam_fuse_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_frames_dev* fr, const mam_fuse_kf* kfs,
-                          const mam_pinhole* cam, const mam_fuse_mp* mps, int mp_stride, const int32_t* n_mps, float th,
+                          const mam_camera* cam, const mam_fuse_mp* mps, int mp_stride, const int32_t* n_mps, float th,
                           int32_t* out_idx, int32_t* out_dist, int32_t* out_n, void* stream) {
     if (!c || !geom_ok(g) || !fr || !kfs || !cam || !mps || !n_mps || !out_idx || !out_dist || !out_n || mp_stride <= 0)
         return MAM_ERR_ARG;
@@ -1817,7 +1875,7 @@ int mam_fuse_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_f
 }
 
 int mam_fuse(mam_match_ctx* c, const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc,
-             const mam_fuse_kf* kf, const mam_pinhole* cam, int n_mps, const mam_fuse_mp* mps, float th,
+             const mam_fuse_kf* kf, const mam_camera* cam, int n_mps, const mam_fuse_mp* mps, float th,
              int32_t* out_idx, int32_t* out_dist) {
     if (!c || !geom_ok(g) || !kf || !cam || n < 0 || n_mps < 0 || (n > 0 && (!keys || !desc)) ||
         (n_mps > 0 && (!mps || !out_idx || !out_dist)))
@@ -1888,7 +1946,7 @@ int mam_compute_distinctive_descriptors(mam_match_ctx* c, int n_mps, const int32
 }
 
 int mam_is_in_frustum_batch_device(mam_match_ctx* c, const mam_frame_geom* g, int nframes, const mam_pose* tcw,
-                                   const mam_pinhole* cam, float log_scale_factor, const mam_local_mp* mps,
+                                   const mam_camera* cam, float log_scale_factor, const mam_local_mp* mps,
                                    int mp_stride, const int32_t* n_mps, float view_cos_limit, mam_mp_track* out,
                                    int32_t* out_n_to_match, void* stream) {
     if (!c || !geom_ok(g) || nframes < 0 || !cam || mp_stride <= 0 || (nframes > 0 && (!tcw || !mps || !n_mps || !out)))
@@ -1914,7 +1972,7 @@ int mam_is_in_frustum_batch_device(mam_match_ctx* c, const mam_frame_geom* g, in
     return MAM_OK;
 }
 
-int mam_is_in_frustum(mam_match_ctx* c, const mam_frame_geom* g, const mam_pose* tcw, const mam_pinhole* cam,
+int mam_is_in_frustum(mam_match_ctx* c, const mam_frame_geom* g, const mam_pose* tcw, const mam_camera* cam,
                       float log_scale_factor, int n_mps, const mam_local_mp* mps, float view_cos_limit,
                       mam_mp_track* out) {
     if (!c || !geom_ok(g) || !tcw || !cam || n_mps < 0 || (n_mps > 0 && (!mps || !out))) return MAM_ERR_ARG;

@@ -20,6 +20,7 @@
 #include <string>
 
 #include "../../include/mam_pose.h"
+#include "camera.hpp"
 #include "runtime.hpp"
 #include "se3.hpp"
 
@@ -33,7 +34,7 @@ constexpr int NRED = 27;       // 21 upper entries of H + 6 of b
 struct Args {
     int nframes;
     const mam_pose* tcw;
-    mam_pinhole cam;
+    mam_camera cam;
     const mam_pose_edge* edges;
     int stride;
     const int32_t* n_edges;
@@ -99,13 +100,18 @@ struct Edges {
 };
 
 // EdgeSE3ProjectXYZOnlyPose::computeError: obs - Pinhole::project(T.map(Xw)); returns chi2 = e^T (w I) e
-__device__ __forceinline__ double edge_error(const Edges& E, int i, const double T[7], const mam_pinhole& c,
+__device__ __forceinline__ double edge_error(const Edges& E, int i, const double T[7], const mam_camera& c,
                                              double* e0o, double* e1o) {
     const double Xw[3] = {(double)E.X[i], (double)E.Y[i], (double)E.Z[i]};
     double Xc[3];
     se3::map_point(T, Xw, Xc);
-    const double u = (double)c.fx * Xc[0] / Xc[2] + (double)c.cx;
-    const double v = (double)c.fy * Xc[1] / Xc[2] + (double)c.cy;
+    double u, v;
+    if (c.model == MAM_CAM_KANNALA_BRANDT8) {
+        cam::project_d(c, Xc, &u, &v);   // KannalaBrandt8::project(Vector3d)
+    } else {
+        u = (double)c.fx * Xc[0] / Xc[2] + (double)c.cx;
+        v = (double)c.fy * Xc[1] / Xc[2] + (double)c.cy;
+    }
     const double e0 = (double)E.ox[i] - u, e1 = (double)E.oy[i] - v;
     *e0o = e0;
     *e1o = e1;
@@ -119,7 +125,7 @@ __device__ __forceinline__ void rho_of(double chi, bool robust, double delta, do
 }
 
 // computeActiveErrors at T (errors stored) + activeRobustChi2
-__device__ double active_chi(const Edges& E, const double T[7], const mam_pinhole& c, bool robust, double delta,
+__device__ double active_chi(const Edges& E, const double T[7], const mam_camera& c, bool robust, double delta,
                              double* scr) {
     double acc[1] = {0.0};
     for (int i = threadIdx.x; i < E.n; i += PT) {
@@ -138,7 +144,7 @@ __device__ double active_chi(const Edges& E, const double T[7], const mam_pinhol
 
 // One pass: computeActiveErrors + activeRobustChi2 + buildSystem (BaseUnaryEdge::constructQuadraticForm,
 // base_unary_edge.hpp:43-71). H upper (row-major i <= j, 21) then b (6) in red[0..26]; returns the chi.
-__device__ double build_system(const Edges& E, const double T[7], const mam_pinhole& c, bool robust, double delta,
+__device__ double build_system(const Edges& E, const double T[7], const mam_camera& c, bool robust, double delta,
                                double* scr, double* red) {
     double acc[NRED + 1];
 #pragma unroll
@@ -149,8 +155,14 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_pinh
         double Xc[3];
         se3::map_point(T, Xw, Xc);
         const double x = Xc[0], y = Xc[1], z = Xc[2];
-        const double u = (double)c.fx * x / z + (double)c.cx;
-        const double v = (double)c.fy * y / z + (double)c.cy;
+        const bool kb8 = c.model == MAM_CAM_KANNALA_BRANDT8;
+        double u, v;
+        if (kb8) {
+            cam::project_d(c, Xc, &u, &v);
+        } else {
+            u = (double)c.fx * x / z + (double)c.cx;
+            v = (double)c.fy * y / z + (double)c.cy;
+        }
         const double e0 = (double)E.ox[i] - u, e1 = (double)E.oy[i] - v;
         E.err[2 * i] = e0;
         E.err[2 * i + 1] = e1;
@@ -160,8 +172,16 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_pinh
         rho_of(chi, robust, delta, &r0, &r1);
         acc[NRED] += r0;
         // _jacobianOplusXi = -projectJac(Xc) * SE3deriv (OptimizableTypes.cpp:49-63)
-        const double fx = c.fx, fy = c.fy;
-        const double J[6] = {-(fx / z), -0.0, -(-fx * x / (z * z)), -0.0, -(fy / z), -(-fy * y / (z * z))};
+        double J[6];
+        if (kb8) {
+            cam::project_jac_d(c, Xc, J);   // KannalaBrandt8::projectJac (KannalaBrandt8.cpp:145-175)
+#pragma unroll
+            for (int k = 0; k < 6; k++) J[k] = -J[k];
+        } else {
+            const double fx = c.fx, fy = c.fy;
+            J[0] = -(fx / z); J[1] = -0.0; J[2] = -(-fx * x / (z * z));
+            J[3] = -0.0; J[4] = -(fy / z); J[5] = -(-fy * y / (z * z));
+        }
         const double D[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
         double A[12];
 #pragma unroll
@@ -286,7 +306,7 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
 }
 
 // SparseOptimizer::optimize(10) on the single pose vertex; T is updated in place. Returns the iterations run.
-__device__ int optimize(const Edges& E, double T[7], const mam_pinhole& c, bool robust, double delta, double* scr,
+__device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool robust, double delta, double* scr,
                         int* trials) {
     // initializeOptimization(0): no level-0 edge -> optimize() returns -1 before the loop
     __shared__ int s_any;
@@ -490,7 +510,7 @@ void mam_pose_destroy(mam_pose_ctx* c) {
 
 int mam_pose_max_edges(mam_pose_ctx* c) { return c ? c->cap : MAM_ERR_ARG; }
 
-int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_pose* tcw, const mam_pinhole* cam,
+int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_pose* tcw, const mam_camera* cam,
                                        const mam_pose_edge* edges, int edge_stride, const int32_t* n_edges,
                                        uint8_t* outlier, mam_pose_result* results, void* stream) {
     if (!c || nframes < 0 || !cam || edge_stride < 0) return MAM_ERR_ARG;
@@ -520,7 +540,7 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_p
     return MAM_OK;
 }
 
-int mam_pose_optimization(mam_pose_ctx* c, const mam_pose* tcw, const mam_pinhole* cam, int n,
+int mam_pose_optimization(mam_pose_ctx* c, const mam_pose* tcw, const mam_camera* cam, int n,
                           const mam_pose_edge* edges, uint8_t* outlier, mam_pose_result* result) {
     if (!c || !tcw || !cam || n < 0 || (n > 0 && (!edges || !outlier)) || !result) return MAM_ERR_ARG;
     if (n > c->cap) {

@@ -5,6 +5,7 @@
 #include <stdexcept>
 
 #include "mam3slam/Map.h"
+#include "../csrc/camera.hpp"
 #include "mam3slam/ORBextractor.h"
 #include "mam3slam/ORBVocabulary.h"
 #include "mam3slam/ORBmatcher.h"
@@ -83,12 +84,32 @@ mam_pose SE3f::toC() const {
     return p;
 }
 
-void Pinhole::project(const float v[3], float uv[2]) const {
-    uv[0] = mvParameters[0] * v[0] / v[2] + mvParameters[2];
-    uv[1] = mvParameters[1] * v[1] / v[2] + mvParameters[3];
+mam_camera GeometricCamera::toC() const {
+    mam_camera c{};
+    c.fx = mvParameters[0]; c.fy = mvParameters[1]; c.cx = mvParameters[2]; c.cy = mvParameters[3];
+    if (mnType == CAM_FISHEYE) {
+        for (int k = 0; k < 4; k++) c.k[k] = mvParameters[4 + k];
+        c.model = MAM_CAM_KANNALA_BRANDT8;
+        c.precision = precision;
+    }
+    return c;
 }
 
-void Pinhole::toK(float K[9]) const {
+void GeometricCamera::project(const float v[3], float uv[2]) const {
+    mam::cam::project_f(toC(), v[0], v[1], v[2], &uv[0], &uv[1]);
+}
+
+void GeometricCamera::unproject(const float p[2], float ray[3]) const {
+    if (mnType == CAM_FISHEYE) {
+        mam::cam::kb8_unproject_f(toC(), p[0], p[1], ray);
+        return;
+    }
+    ray[0] = (p[0] - mvParameters[2]) / mvParameters[0];
+    ray[1] = (p[1] - mvParameters[3]) / mvParameters[1];
+    ray[2] = 1.f;
+}
+
+void GeometricCamera::toK(float K[9]) const {
     K[0] = mvParameters[0]; K[1] = 0.f;             K[2] = mvParameters[2];
     K[3] = 0.f;             K[4] = mvParameters[1]; K[5] = mvParameters[3];
     K[6] = 0.f;             K[7] = 0.f;             K[8] = 1.f;
@@ -111,7 +132,7 @@ static mam_frame_geom makeGeom(float minX, float maxX, float minY, float maxY, f
     return g;
 }
 
-Frame::Frame(const ImageView& imGray, ORBextractor* extractor, const Pinhole* pCamera, unsigned long id)
+Frame::Frame(const ImageView& imGray, ORBextractor* extractor, const GeometricCamera* pCamera, unsigned long id)
     : mnId(id), mpCamera(pCamera) {
     // Frame.cc:289-382 (mono): scale info, ExtractORB(0, imGray, 0, 1000), N, undistortion (identity: the
     // synthetic pinhole agents have zero distortion), grid bounds.

@@ -98,6 +98,18 @@ int Optimizer::PoseOptimization(Frame* pFrame) {
     return n;
 }
 
+int32_t LocalBAWindow::cameraIndex(const GeometricCamera* c) {
+    for (size_t i = 0; i < camera_list.size(); i++)
+        if (camera_list[i] == c) return (int32_t)i;
+    const int32_t model = c->GetType() == GeometricCamera::CAM_FISHEYE ? MAM_CAM_KANNALA_BRANDT8 : MAM_CAM_PINHOLE;
+    if (camera_list.empty()) cam_model = model;
+    else if (model != cam_model)
+        throw std::invalid_argument("LocalBundleAdjustment: Pinhole and KannalaBrandt8 keyframes in one window");
+    camera_list.push_back(c);
+    for (int k = 0; k < c->size(); k++) cams.push_back(c->mvParameters[k]);
+    return (int32_t)(camera_list.size() - 1);
+}
+
 mam_lba_problem LocalBAWindow::Problem(int iterations) const {
     mam_lba_problem p{};
     p.n_poses = (int32_t)vpKF.size();
@@ -115,6 +127,7 @@ mam_lba_problem LocalBAWindow::Problem(int iterations) const {
     p.edge_obs = edge_obs.data();
     p.edge_inv_sigma2 = edge_inv_sigma2.data();
     p.n_cams = (int32_t)camera_list.size();
+    p.cam_model = cam_model;
     p.cams = cams.data();
     p.huber_delta = (double)(float)std::sqrt(5.991);   // const float thHuberMono = sqrt(5.991) (:1275)
     p.iterations = iterations;
@@ -160,13 +173,7 @@ bool Optimizer::BuildLocalBAWindow(KeyFrame* pKF, Map* pMap, LocalBAWindow& w) {
     if (w.num_fixedKF == 0) return false;   // :1182-1186
 
     // Vertices (:1212-1243): local keyframes (init KF fixed), then fixed cameras
-    auto camIndex = [&](const Pinhole* c) {
-        for (size_t i = 0; i < w.camera_list.size(); i++)
-            if (w.camera_list[i] == c) return (int32_t)i;
-        w.camera_list.push_back(c);
-        for (int k = 0; k < 4; k++) w.cams.push_back(c->mvParameters[k]);
-        return (int32_t)(w.camera_list.size() - 1);
-    };
+    auto camIndex = [&](const GeometricCamera* c) { return w.cameraIndex(c); };
     std::map<KeyFrame*, int32_t> kfIndex;
     auto addPose = [&](KeyFrame* pKFi, bool fixed) {
         const SE3f Tcw = pKFi->GetPose();
@@ -278,13 +285,7 @@ void Optimizer::BuildBAWindow(const std::vector<KeyFrame*>& vpKFs, const std::ve
     vbNotIncludedMP.assign(vpMP.size(), false);
     if (vpKFs.empty()) return;
     Map* pMap = vpKFs[0]->GetMap();
-    auto camIndex = [&](const Pinhole* c) {
-        for (size_t i = 0; i < w.camera_list.size(); i++)
-            if (w.camera_list[i] == c) return (int32_t)i;
-        w.camera_list.push_back(c);
-        for (int k = 0; k < 4; k++) w.cams.push_back(c->mvParameters[k]);
-        return (int32_t)(w.camera_list.size() - 1);
-    };
+    auto camIndex = [&](const GeometricCamera* c) { return w.cameraIndex(c); };
     std::map<KeyFrame*, int32_t> kfIndex;
     // KeyFrame vertices (:100-117): the initial keyframe fixed
     for (KeyFrame* pKF : vpKFs) {
@@ -392,13 +393,7 @@ void Optimizer::BuildMergeBAWindow(KeyFrame* pMainKF, const std::vector<KeyFrame
                                    const std::vector<KeyFrame*>& vpFixedKF, LocalBAWindow& w) {
     w = LocalBAWindow();
     Map* pCurrentMap = pMainKF->GetMap();
-    auto camIndex = [&](const Pinhole* c) {
-        for (size_t i = 0; i < w.camera_list.size(); i++)
-            if (w.camera_list[i] == c) return (int32_t)i;
-        w.camera_list.push_back(c);
-        for (int k = 0; k < 4; k++) w.cams.push_back(c->mvParameters[k]);
-        return (int32_t)(w.camera_list.size() - 1);
-    };
+    auto camIndex = [&](const GeometricCamera* c) { return w.cameraIndex(c); };
     std::map<KeyFrame*, int32_t> kfIndex;
     std::vector<MapPoint*> vpMPs;
     // fixed, then non-fixed keyframe vertices with their MapPoints (:3531-3605)

@@ -43,32 +43,6 @@ mam_match_ctx* ctx() {
     return t_ctx.ctx;
 }
 
-// Eigen's 3x3 inverse (cofactors, Eigen/src/LU/InverseImpl.h compute_inverse<3x3>), row-major arrays.
-void inverse3(const float m[9], float r[9]) {
-    auto M = [&](int i, int j) { return m[3 * i + j]; };
-    auto cof = [&](int i, int j) {
-        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-        return M(i1, j1) * M(i2, j2) - M(i1, j2) * M(i2, j1);
-    };
-    const float c0[3] = {cof(0, 0), cof(1, 0), cof(2, 0)};
-    const float det = (c0[0] * M(0, 0) + c0[1] * M(1, 0)) + c0[2] * M(2, 0);
-    const float invdet = 1.0f / det;
-    r[1 * 3 + 0] = cof(0, 1) * invdet;
-    r[1 * 3 + 1] = cof(1, 1) * invdet;
-    r[2 * 3 + 0] = cof(0, 2) * invdet;
-    r[1 * 3 + 2] = cof(2, 1) * invdet;
-    r[2 * 3 + 1] = cof(1, 2) * invdet;
-    r[2 * 3 + 2] = cof(2, 2) * invdet;
-    r[0] = c0[0] * invdet;
-    r[1] = c0[1] * invdet;
-    r[2] = c0[2] * invdet;
-}
-
-void mul3(const float a[9], const float b[9], float c[9]) {
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) c[3 * i + j] = (a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j]) + a[3 * i + 2] * b[6 + j];
-}
-
 }  // namespace
 
 ORBmatcher::ORBmatcher(float nnratio, bool checkOri) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
@@ -153,27 +127,10 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
 }
 
 void ORBmatcher::ComputeF12(KeyFrame* pKF1, KeyFrame* pKF2, float F12[9], float ep[2]) {
-    // ORBmatcher.cc:913-930: epipole and relative pose; Pinhole.cpp:107-112: F12 = K1^-T [t12]x R12 K2^-1
-    const SE3f T1w = pKF1->GetPose(), T2w = pKF2->GetPose(), Tw2 = pKF2->GetPoseInverse();
-    float Cw[3], C2[3];
-    pKF1->GetCameraCenter(Cw);
-    T2w.map(Cw, C2);
-    pKF2->mpCamera->project(C2, ep);
-    const SE3f T12 = T1w * Tw2;
-    float R12[9];
-    T12.rotationMatrix(R12);
-    const float* t = T12.t;
-    const float tx[9] = {0.f, -t[2], t[1], t[2], 0.f, -t[0], -t[1], t[0], 0.f};
-    float K1[9], K2[9], K1t[9], K1ti[9], K2i[9], A[9], B[9];
-    pKF1->mpCamera->toK(K1);
-    pKF2->mpCamera->toK(K2);
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) K1t[3 * i + j] = K1[3 * j + i];
-    inverse3(K1t, K1ti);
-    inverse3(K2, K2i);
-    mul3(K1ti, tx, A);
-    mul3(A, R12, B);
-    mul3(B, K2i, F12);
+    // ORBmatcher.cc:913-930 (T12, the epipole) and Pinhole.cpp:107-112 (F12), as the device search computes them
+    const mam_pose t1 = pKF1->GetPose().toC(), t2 = pKF2->GetPose().toC();
+    const mam_camera c1 = pKF1->mpCamera->toC(), c2 = pKF2->mpCamera->toC();
+    throwOn(mam_triangulation_geometry(&t1, &t2, &c1, &c2, nullptr, nullptr, F12, ep), "mam_triangulation_geometry");
 }
 
 int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2,
@@ -181,8 +138,6 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2,
                                        const bool bCoarse) {
     vMatchedPairs.clear();
     if (bOnlyStereo) return 0;   // mono keyframes: every candidate fails the stereo test (ORBmatcher.cc:1000-1002)
-    float F12[9], ep[2];
-    ComputeF12(pKF1, pKF2, F12, ep);
     const int n1 = pKF1->N, n2 = pKF2->N;
     std::vector<uint8_t> has1(n1 > 0 ? n1 : 1, 0), has2(n2 > 0 ? n2 : 1, 0);
     for (int i = 0; i < n1; i++) has1[i] = pKF1->GetMapPoint(i) ? 1 : 0;
@@ -204,16 +159,26 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2,
     std::vector<int32_t> o1, o2;
     flatten(pKF1->mFeatVec, i1, o1, f1);
     flatten(pKF2->mFeatVec, i2, o2, f2);
-    const mam_featvec fv1{(int32_t)pKF1->mFeatVec.size(), i1.data(), o1.data(), f1.data()};
-    const mam_featvec fv2{(int32_t)pKF2->mFeatVec.size(), i2.data(), o2.data(), f2.data()};
+    mam_tri_kf k1{}, k2{};
+    k1.n = n1;
+    k1.keys = reinterpret_cast<const mam_keypoint*>(pKF1->mvKeysUn.data());
+    k1.desc = pKF1->mDescriptors.data.data();
+    k1.has_mp = has1.data();
+    k1.fv = mam_featvec{(int32_t)pKF1->mFeatVec.size(), i1.data(), o1.data(), f1.data()};
+    k1.tcw = pKF1->GetPose().toC();
+    k1.cam = pKF1->mpCamera->toC();
+    k2.n = n2;
+    k2.keys = reinterpret_cast<const mam_keypoint*>(pKF2->mvKeysUn.data());
+    k2.desc = pKF2->mDescriptors.data.data();
+    k2.has_mp = has2.data();
+    k2.fv = mam_featvec{(int32_t)pKF2->mFeatVec.size(), i2.data(), o2.data(), f2.data()};
+    k2.tcw = pKF2->GetPose().toC();
+    k2.cam = pKF2->mpCamera->toC();
     std::vector<int32_t> out(n1 > 0 ? n1 : 1, -1);
     const mam_frame_geom g = pKF2->Geom();
-    const int nm = mam_search_for_triangulation(
-        ctx(), &g, n1, reinterpret_cast<const mam_keypoint*>(pKF1->mvKeysUn.data()), pKF1->mDescriptors.data.data(),
-        has1.data(), &fv1, n2, reinterpret_cast<const mam_keypoint*>(pKF2->mvKeysUn.data()),
-        pKF2->mDescriptors.data.data(), has2.data(), &fv2, F12, ep, mbCheckOrientation ? 1 : 0, bCoarse ? 1 : 0,
-        out.data());
-    throwOn(nm, "mam_search_for_triangulation");
+    const int nm = mam_search_for_triangulation_kf(ctx(), &g, &k1, &k2, mbCheckOrientation ? 1 : 0, bCoarse ? 1 : 0,
+                                                   out.data());
+    throwOn(nm, "mam_search_for_triangulation_kf");
     vMatchedPairs.reserve(nm);
     for (int i = 0; i < n1; i++)   // ORBmatcher.cc:1135-1143: ascending idx1
         if (out[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)out[i]));

@@ -58,11 +58,12 @@ class LBAProblem:
     edge_pose: np.ndarray        # int32 [E]
     edge_obs: np.ndarray         # float64 [E,2]
     edge_inv_sigma2: np.ndarray  # float64 [E]
-    cams: np.ndarray             # float32 [C,4]
+    cams: np.ndarray             # float32 [C,4] Pinhole / [C,8] KannalaBrandt8 (cam_model 1)
     pose_cam: np.ndarray | None = None
     huber_delta: float = HUBER_MONO
     iterations: int = 10
     edge_active: np.ndarray | None = None   # uint8 per edge: 0 = setLevel(1) (left out)
+    cam_model: int = 0                        # MAM_CAM_PINHOLE / MAM_CAM_KANNALA_BRANDT8
 
     def contiguous(self):
         for k, dt in [("pose_id", np.int64), ("pose_fixed", np.uint8), ("pose_q", np.float64), ("pose_t", np.float64),
@@ -93,7 +94,7 @@ class LBAProblem:
         P.huber_delta = float(self.huber_delta)
         P.iterations = int(self.iterations)
         P.edge_active = None if self.edge_active is None else self.edge_active.ctypes.data
-        P.cam_model = 0
+        P.cam_model = int(self.cam_model)
         P.n_opt_poses = int((self.pose_fixed == 0).sum())
         return P
 
@@ -276,11 +277,12 @@ def _quat_to_rot(q):
 
 
 def synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, obs_per_point=8, seed=0, outlier_frac=0.05,
-                      width=1280, height=720, f=500.0, init_kf_local=True) -> LBAProblem:
+                      width=1280, height=720, f=500.0, init_kf_local=True, camera=None) -> LBAProblem:
     """SURVEY.md §8(d) LBA workload: optimizable KFs on a circle (r = 5 m) looking inward + fixed KFs,
     points U[-2,2]^3 each seen by `obs_per_point` KFs, pixel noise N(0, scale[oct]), gross outliers +20 px,
     initial poses perturbed by ~0.5 deg / 2 cm and points by 3 cm. Values pass through float32 as the map
-    stores them (Optimizer.cc:1218, 1286)."""
+    stores them (Optimizer.cc:1218, 1286). camera: a match.Camera (Pinhole / KannalaBrandt8) instead of the
+    f-pinhole centred in width x height."""
     rng = np.random.default_rng(seed)
     n_kf = n_opt + n_fixed
     scale = [1.0]
@@ -288,7 +290,7 @@ def synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, obs_per_point=8, seed
         scale.append(float(np.float32(np.float64(np.float32(scale[-1])) * np.float64(np.float32(1.2)))))
     scale = np.array(scale, np.float32)
     inv_sigma2 = (np.float32(1.0) / (scale * scale)).astype(np.float32)
-    cam = np.array([[f, f, width / 2, height / 2]], np.float32)
+    cam = np.array([[f, f, width / 2, height / 2]], np.float32) if camera is None else camera.params()[None, :]
     ang = np.linspace(0, 2 * np.pi, n_kf, endpoint=False) + rng.uniform(0, 0.05, n_kf)
     Rs, ts = [], []
     for a in ang:
@@ -320,8 +322,11 @@ def synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, obs_per_point=8, seed
         for k in ks:
             Xc = Rs[k] @ X[l] + ts[k]
             oct_ = int(rng.integers(0, 8))
-            u = f * Xc[0] / Xc[2] + width / 2 + rng.normal(0, scale[oct_])
-            v = f * Xc[1] / Xc[2] + height / 2 + rng.normal(0, scale[oct_])
+            if camera is None:
+                u = f * Xc[0] / Xc[2] + width / 2 + rng.normal(0, scale[oct_])
+                v = f * Xc[1] / Xc[2] + height / 2 + rng.normal(0, scale[oct_])
+            else:
+                u, v = camera.project_np(Xc) + rng.normal(0, scale[oct_], 2)
             if rng.random() < outlier_frac:
                 u += 20.0
             ep.append(l)
@@ -349,4 +354,5 @@ def synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, obs_per_point=8, seed
     Xn = (X + rng.normal(0, 0.03 / np.sqrt(3), X.shape)).astype(np.float32).astype(np.float64)
     return LBAProblem(pose_id=kf_ids, pose_fixed=pose_fixed, pose_q=np.array(q0), pose_t=np.array(t0),
                       point_id=mp_ids, point_xyz=Xn, edge_point=np.array(ep, np.int32), edge_pose=np.array(eo, np.int32),
-                      edge_obs=np.array(eobs, np.float64), edge_inv_sigma2=np.array(einf, np.float64), cams=cam).contiguous()
+                      edge_obs=np.array(eobs, np.float64), edge_inv_sigma2=np.array(einf, np.float64), cams=cam,
+                      cam_model=0 if camera is None else int(camera.model)).contiguous()

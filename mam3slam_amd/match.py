@@ -41,12 +41,77 @@ class Pose(C.Structure):
     _fields_ = [("q", C.c_float * 4), ("t", C.c_float * 3)]
 
 
-class Pinhole(C.Structure):
-    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float)]
+class Camera(C.Structure):
+    """mam_camera (include/mam_camera.h): GeometricCamera as a value, model 0 = Pinhole, 1 = KannalaBrandt8.
+    project_np / unproject_np are float64 numpy forms for the synthetic-scene generators only (the searches and the
+    solves project on the device, bit-exact with the reference's float code: mam3slam_amd/csrc/camera.hpp)."""
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("k", C.c_float * 4),
+                ("model", C.c_int32), ("precision", C.c_float)]
+    PINHOLE, KANNALA_BRANDT8 = 0, 1
+
+    @property
+    def is_kb8(self) -> bool:
+        return self.model == Camera.KANNALA_BRANDT8
+
+    def params(self) -> np.ndarray:
+        """mvParameters (float32): 4 for a Pinhole, 8 for a KannalaBrandt8 (mam_lba_problem.cams rows)."""
+        base = [self.fx, self.fy, self.cx, self.cy]
+        return np.array(base + (list(self.k) if self.is_kb8 else []), np.float32)
+
+    def project_np(self, X: np.ndarray) -> np.ndarray:
+        X = np.asarray(X, np.float64)
+        x, y, z = X[..., 0], X[..., 1], X[..., 2]
+        if not self.is_kb8:
+            return np.stack([self.fx * x / z + self.cx, self.fy * y / z + self.cy], -1)
+        th = np.arctan2(np.sqrt(x * x + y * y), z)
+        psi = np.arctan2(y, x)
+        k = [float(v) for v in self.k]
+        r = th + k[0] * th ** 3 + k[1] * th ** 5 + k[2] * th ** 7 + k[3] * th ** 9
+        return np.stack([self.fx * r * np.cos(psi) + self.cx, self.fy * r * np.sin(psi) + self.cy], -1)
+
+    def unproject_np(self, u, v) -> np.ndarray:
+        """Rays (x/z, y/z) of pixels (KannalaBrandt8::unproject's Newton solve in float64)."""
+        px = (np.asarray(u, np.float64) - self.cx) / self.fx
+        py = (np.asarray(v, np.float64) - self.cy) / self.fy
+        if not self.is_kb8:
+            return np.stack([px, py], -1)
+        thd = np.clip(np.sqrt(px * px + py * py), 0, np.pi / 2)
+        k = [float(v) for v in self.k]
+        th = thd.copy()
+        for _ in range(20):
+            t2 = th * th
+            f = th * (1 + k[0] * t2 + k[1] * t2 ** 2 + k[2] * t2 ** 3 + k[3] * t2 ** 4) - thd
+            df = 1 + 3 * k[0] * t2 + 5 * k[1] * t2 ** 2 + 7 * k[2] * t2 ** 3 + 9 * k[3] * t2 ** 4
+            th = th - f / df
+        sc = np.where(thd > 1e-8, np.tan(th) / np.maximum(thd, 1e-30), 1.0)
+        return np.stack([px * sc, py * sc], -1)
+
+
+class Pinhole(Camera):
+    """Pinhole (src/CameraModels/Pinhole.cpp): mvParameters fx, fy, cx, cy."""
+
+    def __init__(self, fx=0.0, fy=0.0, cx=0.0, cy=0.0):
+        super().__init__(fx, fy, cx, cy, (C.c_float * 4)(), Camera.PINHOLE, 0.0)
+
+
+class KannalaBrandt8(Camera):
+    """KannalaBrandt8 (src/CameraModels/KannalaBrandt8.cpp): fx, fy, cx, cy, k0..k3; precision 1e-6
+    (KannalaBrandt8.h:42-47)."""
+
+    def __init__(self, fx=0.0, fy=0.0, cx=0.0, cy=0.0, k0=0.0, k1=0.0, k2=0.0, k3=0.0, precision=1e-6):
+        super().__init__(fx, fy, cx, cy, (C.c_float * 4)(k0, k1, k2, k3), Camera.KANNALA_BRANDT8, precision)
+
 
 
 class FeatVec(C.Structure):
     _fields_ = [("n_nodes", C.c_int32), ("node_ids", C.c_void_p), ("node_off", C.c_void_p), ("feats", C.c_void_p)]
+
+
+class TriKF(C.Structure):
+    """mam_tri_kf: the keyframe side of SearchForTriangulation (keys, descriptors, MapPoint flags, FeatureVector,
+    pose, camera)."""
+    _fields_ = [("n", C.c_int32), ("keys", C.c_void_p), ("desc", C.c_void_p), ("has_mp", C.c_void_p),
+                ("fv", FeatVec), ("tcw", Pose), ("cam", Camera)]
 
 
 class FramesDev(C.Structure):
@@ -84,6 +149,28 @@ def camera_center(pose):
     return (p + w * uv + np.cross(qv, uv)).astype(np.float32)
 
 
+def pose_c(pose) -> Pose:
+    """(q xyzw, t) -> mam_pose."""
+    T = Pose()
+    for i in range(4):
+        T.q[i] = float(pose[0][i])
+    for i in range(3):
+        T.t[i] = float(pose[1][i])
+    return T
+
+
+def triangulation_geometry(pose1, pose2, cam1: Camera, cam2: Camera | None = None):
+    """SearchForTriangulation's pair geometry as the library computes it (mam_triangulation_geometry,
+    ORBmatcher.cc:913-930): (R12 3x3, t12, F12 3x3, ep) float32."""
+    cam2 = cam1 if cam2 is None else cam2
+    R12, t12 = np.zeros(9, np.float32), np.zeros(3, np.float32)
+    F12, ep = np.zeros(9, np.float32), np.zeros(2, np.float32)
+    t1, t2 = pose_c(pose1), pose_c(pose2)
+    check(_bind().mam_triangulation_geometry(C.byref(t1), C.byref(t2), C.byref(cam1), C.byref(cam2), _p(R12), _p(t12),
+                                             _p(F12), _p(ep)), "mam_triangulation_geometry")
+    return R12.reshape(3, 3), t12, F12.reshape(3, 3), ep
+
+
 def fuse_kf(pose, scale_factor: float = 1.2) -> FuseKF:
     """The keyframe side of Fuse: Tcw, camera centre, mfLogScaleFactor = log of the float scale factor."""
     k = FuseKF()
@@ -110,6 +197,10 @@ _SIGS = {
     "mam_search_for_triangulation": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                                C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "mam_search_for_triangulation_kf": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                                  C.c_void_p]),
+    "mam_triangulation_geometry": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_void_p]),
     "mam_search_by_projection_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                                         C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_float,
                                                         C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -320,6 +411,38 @@ class ORBmatcher:
                                                  _p(F12), _p(ep), int(self.mbCheckOrientation), int(bCoarse), _p(out))
         check(n, "SearchForTriangulation")
         out = out[:len(k1)]
+        idx = np.nonzero(out >= 0)[0]
+        return n, np.stack([idx, out[idx]], 1).astype(np.int64)
+
+    def SearchForTriangulationKF(self, KF1: FrameData, KF2: FrameData, cam1: Camera, cam2: Camera | None = None,
+                                 bOnlyStereo: bool = False, bCoarse: bool = False):
+        """ORBmatcher.cc:907-1146 from the keyframes' poses (KF.pose) and cameras, Pinhole or KannalaBrandt8: the pair
+        geometry of :913-930 and pCamera1->epipolarConstrain are computed by the library. Returns (nmatches,
+        vMatchedPairs as (k,2) int array)."""
+        if bOnlyStereo:
+            return 0, np.zeros((0, 2), np.int64)
+        cam2 = cam1 if cam2 is None else cam2
+        keep = []
+        kf = []
+        for KF, cam in ((KF1, cam1), (KF2, cam2)):
+            k = np.ascontiguousarray(KF.keys, KP_DTYPE)
+            d = np.ascontiguousarray(KF.desc, np.uint8)
+            h = np.ascontiguousarray(KF.has_mp if KF.has_mp is not None else np.zeros(len(k)), np.uint8)
+            ids, off, feats = flatten_featvec(KF.featvec)
+            keep += [k, d, h, ids, off, feats]
+            t = TriKF()
+            t.n = len(k)
+            t.keys, t.desc, t.has_mp = _p(k), _p(d), _p(h)
+            t.fv = FeatVec(len(ids), ids.ctypes.data, off.ctypes.data, feats.ctypes.data)
+            t.tcw = pose_c(KF.pose)
+            t.cam = cam
+            kf.append(t)
+        out = np.full(max(len(KF1.keys), 1), -1, np.int32)
+        g = KF2.geom()
+        n = self._L.mam_search_for_triangulation_kf(self._ctx, C.byref(g), C.byref(kf[0]), C.byref(kf[1]),
+                                                    int(self.mbCheckOrientation), int(bCoarse), _p(out))
+        check(n, "SearchForTriangulationKF")
+        out = out[:len(KF1.keys)]
         idx = np.nonzero(out >= 0)[0]
         return n, np.stack([idx, out[idx]], 1).astype(np.int64)
 

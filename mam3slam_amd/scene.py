@@ -9,9 +9,16 @@ from __future__ import annotations
 
 import numpy as np
 
-from .match import (FUSE_MP_DTYPE, LAST_ENTRY_DTYPE, LOCAL_MP_DTYPE, MP_TRACK_DTYPE, FrameData, Pinhole, camera_center,
-                    epipole_12, fundamental_12)
+from .match import (FUSE_MP_DTYPE, LAST_ENTRY_DTYPE, LOCAL_MP_DTYPE, MP_TRACK_DTYPE, Camera, FrameData,
+                    KannalaBrandt8, Pinhole, camera_center, epipole_12, fundamental_12)
 from .orb import KP_DTYPE
+
+
+def _backproject(cam: Camera, u, v, z):
+    """Camera-frame points at depth z whose projections are the pixels (u, v) (Pinhole or KannalaBrandt8)."""
+    r = cam.unproject_np(u, v)
+    z = np.asarray(z, np.float64)
+    return np.stack([r[..., 0] * z, r[..., 1] * z, z], -1)
 
 
 def scale_tables(nlevels=8, scale=1.2):
@@ -94,7 +101,7 @@ def local_world_mappoints(F: FrameData, cam: Pinhole, rng: np.random.Generator, 
     z = rng.uniform(1.5, 40.0, m)
     u = k["x"] + rng.normal(0, 0.8, m)
     v = k["y"] + rng.normal(0, 0.8, m)
-    Xc = np.stack([(u - cam.cx) / cam.fx * z, (v - cam.cy) / cam.fy * z, z], 1)
+    Xc = _backproject(cam, u, v, z)
     Xw = (Xc - t[None, :].astype(np.float64)) @ R
     mps = np.zeros(m, LOCAL_MP_DTYPE)
     mps["pos"] = Xw.astype(np.float32)
@@ -133,6 +140,22 @@ def pinhole(w, h, f=500.0) -> Pinhole:
     return Pinhole(np.float32(f), np.float32(f), np.float32(w / 2), np.float32(h / 2))
 
 
+# test/settingsForTest_00.yaml (the testMultiAgentSystem agents): KannalaBrandt8 at 960 x 960
+KB8_TEST_YAML = dict(fx=322.7022465231787, fy=322.25818444649866, cx=473.48961846063645, cy=484.62594873664256,
+                     k0=0.052348933344686564, k1=0.014590092715993354, k2=-0.030877354788616376,
+                     k3=0.00650873486325155, width=960, height=960)
+
+
+def kannala_brandt8(w=960, h=960) -> KannalaBrandt8:
+    """The test-YAML fisheye camera; other image sizes scale fx, cx by w / 960 and fy, cy by h / 960 (the distortion
+    acts on the ray angle and is unchanged)."""
+    y = KB8_TEST_YAML
+    sx, sy = w / y["width"], h / y["height"]
+    return KannalaBrandt8(np.float32(y["fx"] * sx), np.float32(y["fy"] * sy), np.float32(y["cx"] * sx),
+                          np.float32(y["cy"] * sy), np.float32(y["k0"]), np.float32(y["k1"]), np.float32(y["k2"]),
+                          np.float32(y["k3"]))
+
+
 def small_pose(rng, rot=0.01, trans=0.05):
     axis = rng.normal(size=3)
     axis /= np.linalg.norm(axis)
@@ -156,7 +179,7 @@ def motion_last_frame(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac
     z = rng.uniform(2.0, 12.0, m)
     u = k["x"] + rng.normal(0, 0.7, m)
     v = k["y"] + rng.normal(0, 0.7, m)
-    Xc = np.stack([(u - cam.cx) / cam.fx * z, (v - cam.cy) / cam.fy * z, z], 1)
+    Xc = _backproject(cam, u, v, z)
     Xw = (Xc - t[None, :].astype(np.float64)) @ R.astype(np.float64)   # R^T (Xc - t)
     last = np.zeros(m, LAST_ENTRY_DTYPE)
     last["pos"] = Xw.astype(np.float32)
@@ -233,6 +256,57 @@ def keyframe_pair(F: FrameData, cam: Pinhole, rng: np.random.Generator, n_nodes=
     return KF1, KF2, F12, ep
 
 
+def keyframe_pair_3d(F: FrameData, cam: Camera, rng: np.random.Generator, n_nodes=24, kflip=10, baseline=0.3,
+                     noise=0.6):
+    """(KF1, KF2) for SearchForTriangulation with any camera model: KF1's keypoints back-projected to 2-12 m and
+    re-projected into KF2 (baselined, slightly rotated; project_np) with pixel noise, so the pairs satisfy Pinhole
+    epipolar lines or KannalaBrandt8 two-view triangulation up to the noise; plus random extra features, MapPoint
+    flags and FeatureVectors from a one-level quantizer. Poses are set (Tcw)."""
+    from .match import quat_to_rot
+
+    n = len(F.keys)
+    k1 = F.keys.copy()
+    sel = rng.choice(n, size=int(n * 0.8), replace=False)
+    z = rng.uniform(2.0, 12.0, len(sel))
+    X1 = _backproject(cam, k1["x"][sel], k1["y"][sel], z)
+    ang = 0.03
+    q2 = np.array([0.0, np.sin(ang / 2), 0.0, np.cos(ang / 2)], np.float32)
+    t2 = np.array([-baseline, 0.02, -0.05], np.float32)
+    X2 = X1 @ quat_to_rot(q2).astype(np.float64).T + t2[None, :].astype(np.float64)
+    uv = cam.project_np(X2) + rng.normal(0, noise, (len(sel), 2))
+    ok = (X2[:, 2] > 0.1) & (uv[:, 0] >= 0) & (uv[:, 0] < F.width - 1) & (uv[:, 1] >= 0) & (uv[:, 1] < F.height - 1)
+    sel, uv = sel[ok], uv[ok]
+    k2 = F.keys[sel].copy()
+    k2["x"] = uv[:, 0].astype(np.float32)
+    k2["y"] = uv[:, 1].astype(np.float32)
+    k2["octave"] = np.clip(k2["octave"] + rng.integers(-1, 2, len(sel)), 0, 7)
+    k2["angle"] = ((k2["angle"] + rng.normal(0, 5, len(sel))) % 360).astype(np.float32)
+    d2 = flip_bits(F.desc[sel], rng, kflip)
+    ne = n // 5
+    ke = np.zeros(ne, KP_DTYPE)
+    ke["x"] = rng.uniform(0, F.width - 1, ne)
+    ke["y"] = rng.uniform(0, F.height - 1, ne)
+    ke["octave"] = rng.integers(0, 8, ne)
+    ke["angle"] = rng.uniform(0, 360, ne)
+    ke["size"] = 31
+    de = rng.integers(0, 256, (ne, 32), dtype=np.uint8)
+    k2 = np.concatenate([k2, ke])
+    d2 = np.concatenate([d2, de])
+    perm = rng.permutation(len(k2))
+    k2, d2 = k2[perm], d2[perm]
+    centroids = rng.integers(0, 256, (n_nodes, 32), dtype=np.uint8)
+    node_ids = np.sort(rng.choice(1_000_000, size=n_nodes, replace=False)).astype(np.uint32)
+    KF1 = make_frame_data(k1, F.desc, F.width, F.height)
+    KF2 = make_frame_data(k2, d2, F.width, F.height)
+    KF1.has_mp = (rng.random(len(k1)) < 0.2).astype(np.uint8)
+    KF2.has_mp = (rng.random(len(k2)) < 0.2).astype(np.uint8)
+    KF1.featvec = quantize(KF1.desc, centroids, node_ids)
+    KF2.featvec = quantize(KF2.desc, centroids, node_ids)
+    KF1.pose = (np.array([0, 0, 0, 1], np.float32), np.zeros(3, np.float32))
+    KF2.pose = (q2, t2)
+    return KF1, KF2
+
+
 def pose_problem(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.7, outlier_frac=0.08, noise=1.0,
                  rot=0.02, trans=0.06):
     """Inputs of Optimizer::PoseOptimization around F's keypoints: a true pose, matched MapPoints (world positions)
@@ -257,7 +331,7 @@ def pose_problem(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.7,
     r = rng.uniform(15.0, 60.0, m)
     u = np.where(bad, u + r * np.cos(ang), u)
     v = np.where(bad, v + r * np.sin(ang), v)
-    Xc = np.stack([(u - cam.cx) / cam.fx * z, (v - cam.cy) / cam.fy * z, z], 1)
+    Xc = _backproject(cam, u, v, z)
     Xw = (Xc - tt[None, :].astype(np.float64)) @ Rt   # Rt^T (Xc - t)
     mp = np.full(n, -1, np.int32)
     perm = rng.permutation(m)   # MapPoint table order unrelated to keypoint order
@@ -295,7 +369,7 @@ def fuse_mappoints(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.
     z = rng.uniform(1.5, 25.0, m)
     u = k["x"] + rng.normal(0, 0.8, m) * s
     v = k["y"] + rng.normal(0, 0.8, m) * s
-    Xc = np.stack([(u - cam.cx) / cam.fx * z, (v - cam.cy) / cam.fy * z, z], 1)
+    Xc = _backproject(cam, u, v, z)
     Xw = (Xc - t[None, :].astype(np.float64)) @ R   # R^T (Xc - t)
     PO = Xw - camera_center(F.pose).astype(np.float64)[None, :]
     d = np.linalg.norm(PO, axis=1)

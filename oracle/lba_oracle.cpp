@@ -27,6 +27,7 @@
 #include "../include/mam_lba.h"
 #include "../include/mam_orb.h"
 #include "g2o_se3.h"
+#include "../mam3slam_amd/csrc/camera.hpp"
 
 namespace {
 
@@ -50,9 +51,21 @@ struct Graph {
     std::vector<double> b;                 // 6 Np + 3 Nl
     std::vector<double> x;
 
+    bool kb8() const { return p->cam_model == MAM_CAM_KANNALA_BRANDT8; }
     const float* cam(int pose_idx) const {
         const int c = p->pose_cam ? p->pose_cam[pose_idx] : 0;
-        return p->cams + 4 * c;
+        return p->cams + (kb8() ? 8 : 4) * c;
+    }
+    // pCamera of an edge as a mam_camera (KannalaBrandt8: mvParameters fx, fy, cx, cy, k0..k3)
+    mam_camera camera(int pose_idx) const {
+        const float* c = cam(pose_idx);
+        mam_camera m{};
+        m.fx = c[0]; m.fy = c[1]; m.cx = c[2]; m.cy = c[3];
+        if (kb8()) {
+            for (int k = 0; k < 4; k++) m.k[k] = c[4 + k];
+            m.model = MAM_CAM_KANNALA_BRANDT8;
+        }
+        return m;
     }
 
     void computeActiveErrors() {
@@ -61,8 +74,13 @@ struct Graph {
             double Xc[3];
             se3Map(pose[ip], &pt[3 * il], Xc);
             const float* c = cam(ip);
-            const double u = c[0] * Xc[0] / Xc[2] + c[2];
-            const double v = c[1] * Xc[1] / Xc[2] + c[3];
+            double u, v;
+            if (kb8()) {
+                mam::cam::project_d(camera(ip), Xc, &u, &v);   // KannalaBrandt8::project(Vector3d) :46-65
+            } else {
+                u = c[0] * Xc[0] / Xc[2] + c[2];
+                v = c[1] * Xc[1] / Xc[2] + c[3];
+            }
             err[2 * e] = p->edge_obs[2 * e] - u;
             err[2 * e + 1] = p->edge_obs[2 * e + 1] - v;
         }
@@ -106,8 +124,12 @@ struct Graph {
             se3Map(T, &pt[3 * il], Xc);
             const double x = Xc[0], y = Xc[1], z = Xc[2];
             const float* c = cam(ip);
-            // -projectJac (Pinhole.cpp:71-81)
-            const double J[6] = {-(c[0] / z), -0.0, -(-c[0] * x / (z * z)), -0.0, -(c[1] / z), -(-c[1] * y / (z * z))};
+            // -projectJac (Pinhole.cpp:71-81 / KannalaBrandt8.cpp:145-175)
+            double J[6] = {-(c[0] / z), -0.0, -(-c[0] * x / (z * z)), -0.0, -(c[1] / z), -(-c[1] * y / (z * z))};
+            if (kb8()) {
+                mam::cam::project_jac_d(camera(ip), Xc, J);
+                for (int k = 0; k < 6; k++) J[k] = -J[k];
+            }
             double R[9];
             toRotationMatrix(T.r, R);
             double A[6];   // 2x3 jacobianOplusXi = J R

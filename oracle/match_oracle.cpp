@@ -5,13 +5,17 @@
 //   src/Frame.cc:657-723        GetFeaturesInArea (enumeration order ix -> iy -> cell vector)
 //   src/ORBmatcher.cc:43-213    SearchByProjection(Frame&, vector<MapPoint*>) (mono branch), :215-221 radius
 //   src/ORBmatcher.cc:1676-1887 SearchByProjection(Frame&, const Frame&) (mono branch)
-//   src/ORBmatcher.cc:907-1146  SearchForTriangulation (mono, Pinhole), :2012-2053 ComputeThreeMaxima
+//   src/ORBmatcher.cc:907-1146  SearchForTriangulation (mono; Pinhole F12 line test or KannalaBrandt8 two-view
+//                               triangulation), :2012-2053 ComputeThreeMaxima
 //   src/ORBmatcher.cc:2058-2074 DescriptorDistance
 //   src/ORBmatcher.cc:1148-1338 Fuse(pKF, vpMapPoints, th, bRight=false) (the per-MapPoint search), with
 //                               KeyFrame::GetFeaturesInArea / IsInImage (src/KeyFrame.cc:704-753) and
 //                               MapPoint::PredictScale (src/MapPoint.cc:514-529)
 //   src/MapPoint.cc:329-403     ComputeDistinctiveDescriptors
-//   src/CameraModels/Pinhole.cpp:35-41 project, :107-129 epipolarConstrain (F12 supplied by the caller)
+//   src/CameraModels/Pinhole.cpp:35-41 project, :107-129 epipolarConstrain;
+//   src/CameraModels/KannalaBrandt8.cpp:67-84 project, :116-143 unproject, :216-220 + 306-406 epipolarConstrain /
+//                               TriangulateMatches / Triangulate: mam3slam_amd/csrc/camera.hpp (shared with the
+//                               device; pinned to glibc 2.35 and g++ 11.4's contraction by tests/cpp/test_glibc_camera.cpp)
 //   Thirdparty/Sophus/sophus/so3.hpp:358-367, se3.hpp:321-324 point action
 //   src/Frame.cc:512-571 isInFrustum (mono), src/MapPoint.cc:531-546 PredictScale(dist, Frame*),
 //   src/Tracking.cc:3098-3139 SearchLocalPoints' projection loop
@@ -25,6 +29,7 @@
 #include <vector>
 
 #include "../include/mam_match.h"
+#include "../mam3slam_amd/csrc/camera.hpp"
 
 namespace {
 
@@ -198,8 +203,8 @@ int oracle_search_by_projection_motion(const mam_frame_geom* g, int n, const mam
         se3Apply(tcw, L.pos, x3Dc);
         const float invzc = (float)(1.0 / (double)x3Dc[2]);
         if (invzc < 0) continue;
-        const float u = cam->fx * x3Dc[0] / x3Dc[2] + cam->cx;
-        const float v = cam->fy * x3Dc[1] / x3Dc[2] + cam->cy;
+        float u, v;
+        mam::cam::project_f(*cam, x3Dc[0], x3Dc[1], x3Dc[2], &u, &v);   // CurrentFrame.mpCamera->project (:1713)
         if (u < g->min_x || u > g->max_x) continue;
         if (v < g->min_y || v > g->max_y) continue;
         const int nLastOctave = L.octave;
@@ -234,12 +239,23 @@ int oracle_search_by_projection_motion(const mam_frame_geom* g, int n, const mam
     return nmatches;
 }
 
-int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_keypoint* keys1, const uint8_t* desc1,
-                                    const uint8_t* has_mp1, const mam_featvec* fv1, int n2,
-                                    const mam_keypoint* keys2, const uint8_t* desc2, const uint8_t* has_mp2,
-                                    const mam_featvec* fv2, const float* F12, const float* ep, int check_ori,
-                                    int coarse, int32_t* out) {
-    (void)n2;
+namespace {
+struct TriGeom {
+    const float* F12;          // Pinhole pairs
+    const float* ep;
+    const mam_camera* cam1;    // NULL: Pinhole with F12
+    const mam_camera* cam2;
+    const float* R12;
+    const float* t12;
+};
+
+int searchForTriangulation(const mam_frame_geom* g, int n1, const mam_keypoint* keys1, const uint8_t* desc1,
+                           const uint8_t* has_mp1, const mam_featvec* fv1, const mam_keypoint* keys2,
+                           const uint8_t* desc2, const uint8_t* has_mp2, const mam_featvec* fv2, const TriGeom& tg,
+                           int check_ori, int coarse, int32_t* out) {
+    const float* F12 = tg.F12;
+    const float* ep = tg.ep;
+    const bool kb8 = tg.cam1 && tg.cam1->model == MAM_CAM_KANNALA_BRANDT8;
     std::vector<int> rotHist[MAM_HISTO_LENGTH];
     for (int i = 0; i < n1; i++) out[i] = -1;
     int nmatches = 0;
@@ -264,7 +280,15 @@ int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_k
                     const float distey = ep[1] - kp2.y;
                     if (distex * distex + distey * distey < 100 * g->scale_factors[kp2.octave]) continue;
                     bool ok = coarse != 0;
-                    if (!ok) {
+                    if (!ok && kb8) {
+                        // KannalaBrandt8::epipolarConstrain = TriangulateMatches(...) > 0.0001f (KannalaBrandt8.cpp:216-220)
+                        float r1[3], r2[3];
+                        mam::cam::kb8_unproject_f(*tg.cam1, kp1.x, kp1.y, r1);
+                        mam::cam::kb8_unproject_f(*tg.cam2, kp2.x, kp2.y, r2);
+                        ok = mam::cam::kb8_triangulate_matches(*tg.cam1, *tg.cam2, kp1.x, kp1.y, r1, kp2.x, kp2.y, r2,
+                                                               tg.R12, tg.t12, g->level_sigma2[kp1.octave],
+                                                               g->level_sigma2[kp2.octave]) > 0.0001f;
+                    } else if (!ok) {
                         const float a = kp1.x * F(0, 0) + kp1.y * F(1, 0) + F(2, 0);
                         const float b = kp1.x * F(0, 1) + kp1.y * F(1, 1) + F(2, 1);
                         const float c = kp1.x * F(0, 2) + kp1.y * F(1, 2) + F(2, 2);
@@ -305,6 +329,43 @@ int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_k
     }
     return nmatches;
 }
+}  // namespace
+
+extern "C" int oracle_search_for_triangulation(const mam_frame_geom* g, int n1, const mam_keypoint* keys1,
+                                               const uint8_t* desc1, const uint8_t* has_mp1, const mam_featvec* fv1,
+                                               int n2, const mam_keypoint* keys2, const uint8_t* desc2,
+                                               const uint8_t* has_mp2, const mam_featvec* fv2, const float* F12,
+                                               const float* ep, int check_ori, int coarse, int32_t* out) {
+    (void)n2;
+    const TriGeom tg{F12, ep, nullptr, nullptr, nullptr, nullptr};
+    return searchForTriangulation(g, n1, keys1, desc1, has_mp1, fv1, keys2, desc2, has_mp2, fv2, tg, check_ori, coarse,
+                                  out);
+}
+
+// SearchForTriangulation(pKF1, pKF2, ...) from the keyframes' poses and cameras (ORBmatcher.cc:913-930 geometry)
+extern "C" int oracle_search_for_triangulation_kf(const mam_frame_geom* g, const mam_tri_kf* kf1, const mam_tri_kf* kf2,
+                                                  int check_ori, int coarse, int32_t* out) {
+    mam::cam::PairGeom pg;
+    mam::cam::pair_geometry(kf1->tcw.q, kf1->tcw.t, kf2->tcw.q, kf2->tcw.t, kf1->cam, kf2->cam, &pg);
+    const TriGeom tg{pg.F12, pg.ep, &kf1->cam, &kf2->cam, pg.R12, pg.t12};
+    return searchForTriangulation(g, kf1->n, kf1->keys, kf1->desc, kf1->has_mp, &kf1->fv, kf2->keys, kf2->desc,
+                                  kf2->has_mp, &kf2->fv, tg, check_ori, coarse, out);
+}
+
+// KannalaBrandt8 pieces for the KATs (tests/test_oracle_kat.py)
+extern "C" void oracle_kb8_project(const mam_camera* c, const float* X, float* uv) {
+    mam::cam::project_f(*c, X[0], X[1], X[2], &uv[0], &uv[1]);
+}
+extern "C" void oracle_kb8_unproject(const mam_camera* c, float px, float py, float* r) {
+    mam::cam::kb8_unproject_f(*c, px, py, r);
+}
+extern "C" float oracle_kb8_triangulate(const mam_camera* c1, const mam_camera* c2, const float* kp1, const float* kp2,
+                                        const float* R12, const float* t12, float sigma1, float sigma2) {
+    float r1[3], r2[3];
+    mam::cam::kb8_unproject_f(*c1, kp1[0], kp1[1], r1);
+    mam::cam::kb8_unproject_f(*c2, kp2[0], kp2[1], r2);
+    return mam::cam::kb8_triangulate_matches(*c1, *c2, kp1[0], kp1[1], r1, kp2[0], kp2[1], r2, R12, t12, sigma1, sigma2);
+}
 
 // Fuse's per-MapPoint search. PredictScale uses std::log(float) and std::ceil(float): the reference's unqualified
 // log/ceil of a float resolve to the std overloads (TemplatedVocabulary.h:36 puts `using namespace std` in scope).
@@ -322,8 +383,8 @@ int oracle_fuse(const mam_frame_geom* g, int n, const mam_keypoint* keys, const 
         float p3Dc[3];
         se3Apply(&kf->tcw, mp.pos, p3Dc);
         if (p3Dc[2] < 0.0f) continue;
-        const float u = cam->fx * p3Dc[0] / p3Dc[2] + cam->cx;
-        const float v = cam->fy * p3Dc[1] / p3Dc[2] + cam->cy;
+        float u, v;
+        mam::cam::project_f(*cam, p3Dc[0], p3Dc[1], p3Dc[2], &u, &v);   // pCamera->project(p3Dc) (:1210)
         if (!(u >= g->min_x && u < g->max_x && v >= g->min_y && v < g->max_y)) continue;   // IsInImage
         const float maxDistance = 1.2f * mp.max_distance;
         const float minDistance = 0.8f * mp.min_distance;
@@ -401,8 +462,8 @@ int oracle_is_in_frustum(const mam_frame_geom* g, const mam_pose* tcw, const mam
         for (int r = 0; r < 3; r++) Pc[r] = (R[3 * r] * P[0] + (R[3 * r + 1] * P[1] + R[3 * r + 2] * P[2])) + tcw->t[r];
         const float Pc_dist = std::sqrt(Pc[0] * Pc[0] + (Pc[1] * Pc[1] + Pc[2] * Pc[2]));
         if (Pc[2] < 0.0f) continue;
-        const float u = cam->fx * Pc[0] / Pc[2] + cam->cx;   // Pinhole::project(Vector3f)
-        const float v = cam->fy * Pc[1] / Pc[2] + cam->cy;
+        float u, v;
+        mam::cam::project_f(*cam, Pc[0], Pc[1], Pc[2], &u, &v);   // mpCamera->project(Pc) (Frame.cc:532)
         if (u < g->min_x || u > g->max_x) continue;
         if (v < g->min_y || v > g->max_y) continue;
         o.proj_x = u;

@@ -266,6 +266,66 @@ def search_for_triangulation(KF1, KF2, F12, ep, check_ori=False, coarse=False):
     return n, out[:len(k1)]
 
 
+def search_for_triangulation_kf(KF1, KF2, cam1, cam2=None, check_ori=False, coarse=False):
+    """SearchForTriangulation from poses + cameras (Pinhole or KannalaBrandt8), the oracle's own pair geometry."""
+    from mam3slam_amd.match import KP_DTYPE, FeatVec, TriKF, flatten_featvec, pose_c
+
+    L = lib()
+    L.oracle_search_for_triangulation_kf.restype = C.c_int
+    L.oracle_search_for_triangulation_kf.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    cam2 = cam1 if cam2 is None else cam2
+    keep, kf = [], []
+    for KF, cam in ((KF1, cam1), (KF2, cam2)):
+        k = np.ascontiguousarray(KF.keys, KP_DTYPE)
+        d = np.ascontiguousarray(KF.desc, np.uint8)
+        h = np.ascontiguousarray(KF.has_mp if KF.has_mp is not None else np.zeros(len(k)), np.uint8)
+        ids, off, feats = flatten_featvec(KF.featvec)
+        keep += [k, d, h, ids, off, feats]
+        t = TriKF()
+        t.n = len(k)
+        t.keys, t.desc, t.has_mp = _vp(k), _vp(d), _vp(h)
+        t.fv = FeatVec(len(ids), ids.ctypes.data, off.ctypes.data, feats.ctypes.data)
+        t.tcw = pose_c(KF.pose)
+        t.cam = cam
+        kf.append(t)
+    out = np.full(max(len(KF1.keys), 1), -1, np.int32)
+    g = KF2.geom()
+    n = L.oracle_search_for_triangulation_kf(C.byref(g), C.byref(kf[0]), C.byref(kf[1]), int(check_ori), int(coarse),
+                                             _vp(out))
+    return n, out[:len(KF1.keys)]
+
+
+def kb8_project(cam, X):
+    """KannalaBrandt8::project(Vector3f) / Pinhole::project as the oracle evaluates it (float32 u, v)."""
+    L = lib()
+    L.oracle_kb8_project.restype = None
+    L.oracle_kb8_project.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    X = np.ascontiguousarray(X, np.float32)
+    uv = np.zeros(2, np.float32)
+    L.oracle_kb8_project(C.byref(cam), _vp(X), _vp(uv))
+    return uv
+
+
+def kb8_unproject(cam, px, py):
+    L = lib()
+    L.oracle_kb8_unproject.restype = None
+    L.oracle_kb8_unproject.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_void_p]
+    r = np.zeros(3, np.float32)
+    L.oracle_kb8_unproject(C.byref(cam), float(px), float(py), _vp(r))
+    return r
+
+
+def kb8_triangulate(cam1, cam2, kp1, kp2, R12, t12, sigma1, sigma2):
+    """KannalaBrandt8::TriangulateMatches: z1 > 0 or the reference's negative codes -1..-5."""
+    L = lib()
+    L.oracle_kb8_triangulate.restype = C.c_float
+    L.oracle_kb8_triangulate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_float, C.c_float]
+    a = [np.ascontiguousarray(v, np.float32).reshape(-1) for v in (kp1, kp2, R12, t12)]
+    return float(L.oracle_kb8_triangulate(C.byref(cam1), C.byref(cam2), *[_vp(v) for v in a], float(sigma1),
+                                          float(sigma2)))
+
+
 def fuse(KF, mps, cam, th=3.0):
     """ORBmatcher::Fuse per-MapPoint search. Returns (n, idx, dist) like mam3slam_amd.match.ORBmatcher.Fuse."""
     from mam3slam_amd.match import FUSE_MP_DTYPE, KP_DTYPE, fuse_kf

@@ -25,6 +25,7 @@
 
 #include "../include/mam_pose.h"
 #include "g2o_se3.h"
+#include "../mam3slam_amd/csrc/camera.hpp"
 
 namespace {
 
@@ -43,8 +44,13 @@ struct PoseProblem {
         const double X[3] = {(double)e[i].xw[0], (double)e[i].xw[1], (double)e[i].xw[2]};
         double Xc[3];
         se3Map(T, X, Xc);
-        const double u = (double)cam->fx * Xc[0] / Xc[2] + (double)cam->cx;
-        const double v = (double)cam->fy * Xc[1] / Xc[2] + (double)cam->cy;
+        double u, v;
+        if (cam->model == MAM_CAM_KANNALA_BRANDT8) {
+            mam::cam::project_d(*cam, Xc, &u, &v);   // KannalaBrandt8::project(Vector3d)
+        } else {
+            u = (double)cam->fx * Xc[0] / Xc[2] + (double)cam->cx;
+            v = (double)cam->fy * Xc[1] / Xc[2] + (double)cam->cy;
+        }
         err[2 * i] = (double)e[i].obs[0] - u;
         err[2 * i + 1] = (double)e[i].obs[1] - v;
     }
@@ -89,7 +95,11 @@ struct PoseProblem {
             const double x = Xc[0], y = Xc[1], z = Xc[2];
             const double fx = cam->fx, fy = cam->fy;
             // -projectJac (Pinhole.cpp:71-81) * SE3deriv (OptimizableTypes.cpp:49-63)
-            const double J[6] = {-(fx / z), -0.0, -(-fx * x / (z * z)), -0.0, -(fy / z), -(-fy * y / (z * z))};
+            double J[6] = {-(fx / z), -0.0, -(-fx * x / (z * z)), -0.0, -(fy / z), -(-fy * y / (z * z))};
+            if (cam->model == MAM_CAM_KANNALA_BRANDT8) {   // KannalaBrandt8::projectJac
+                mam::cam::project_jac_d(*cam, Xc, J);
+                for (int k = 0; k < 6; k++) J[k] = -J[k];
+            }
             const double D[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
             double A[12];
             for (int r = 0; r < 2; r++)

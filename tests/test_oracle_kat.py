@@ -397,3 +397,103 @@ def test_is_in_frustum_oracle_vs_numpy(oracle):
         levels |= set(lvl[ok].tolist())
         assert (inimg & ~ok).any() and (~inimg).any()
     assert levels == set(range(8))
+
+
+def test_glibc_camera_restatement_exact(oracle, tmp_path):
+    """The camera restatements (mam3slam_amd/csrc/camera.hpp, shared by the oracle and gfx950) equal this container's
+    glibc 2.35 libm (the reference image's) bit for bit — atanf on every 97th float, atan2f on 4M pairs, tanf on every
+    97th float of [-2.4, 2.4] — and KannalaBrandt8::project(Vector3f) / unproject equal the reference's scalar code
+    built as the reference is built (g++ 11.4 -O3 -march=x86-64-v3: FMA contraction; tests/cpp/kb8_codegen_probe.cpp)
+    on 2M random points / pixels of the test-YAML camera."""
+    probe = tmp_path / "probe.o"
+    exe = tmp_path / "tgc"
+    subprocess.run(["g++", "-O3", "-march=x86-64-v3", "-c", "-o", str(probe),
+                    os.path.join(ROOT, "tests/cpp/kb8_codegen_probe.cpp")], check=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
+                    os.path.join(ROOT, "tests/cpp/test_glibc_camera.cpp"), str(probe), "-ldl"], check=True)
+    r = subprocess.run([str(exe), "97"], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
+def test_kb8_project_unproject_kat(oracle):
+    """KannalaBrandt8 (test/settingsForTest_00.yaml): unproject inverts project to float precision across the image,
+    the principal point maps to the optical axis, and the projection matches a float64 evaluation of the model."""
+    from mam3slam_amd import scene
+
+    cam = scene.kannala_brandt8()
+    r = oracle.kb8_unproject(cam, cam.cx, cam.cy)
+    assert abs(r[0]) < 1e-6 and abs(r[1]) < 1e-6 and r[2] == 1.0
+    rng = np.random.default_rng(4)
+    for _ in range(200):
+        # inside the lens' monotonic field (theta_d < ~1.2 rad: 380 px); beyond it the reference's Newton solve leaves
+        # the valid branch exactly as the restatement does
+        rad, phi = 380 * np.sqrt(rng.uniform()), rng.uniform(0, 2 * np.pi)
+        u, v = cam.cx + rad * np.cos(phi), cam.cy + rad * np.sin(phi)
+        ray = oracle.kb8_unproject(cam, u, v)
+        uv = oracle.kb8_project(cam, ray * np.float32(rng.uniform(0.5, 20)))
+        assert abs(uv[0] - u) < 2e-3 and abs(uv[1] - v) < 2e-3, (u, v, uv)
+        X = np.array([rng.uniform(-3, 3), rng.uniform(-3, 3), rng.uniform(0.3, 9)], np.float32)
+        ref = cam.project_np(X.astype(np.float64))
+        assert np.abs(oracle.kb8_project(cam, X) - ref).max() < 2e-3
+
+
+def test_kb8_triangulate_matches_kat(oracle):
+    """KannalaBrandt8::TriangulateMatches on exact correspondences: z1 = the point's depth in camera 1; parallel rays
+    -> -1; a point behind both cameras -> -2; a correspondence far off its epipolar curve -> -4 / -5."""
+    from mam3slam_amd import scene
+    from mam3slam_amd.match import quat_to_rot
+
+    cam = scene.kannala_brandt8()
+    s2 = np.float32(1.44)
+    ang = 0.05
+    q2 = np.array([0, np.sin(ang / 2), 0, np.cos(ang / 2)], np.float32)
+    t2 = np.array([-0.4, 0.05, 0.02], np.float32)
+    R2 = quat_to_rot(q2).astype(np.float64)
+    # T12 = T1w T2w^-1 with T1w = I: R12 = R2^T, t12 = -R2^T t2
+    R12 = R2.T.astype(np.float32)
+    t12 = (-R2.T @ t2.astype(np.float64)).astype(np.float32)
+    rng = np.random.default_rng(8)
+    for _ in range(50):
+        X = np.array([rng.uniform(-4, 4), rng.uniform(-4, 4), rng.uniform(3, 15)])
+        kp1 = cam.project_np(X)
+        kp2 = cam.project_np(R2 @ X + t2)
+        if not (0 < kp2[0] < 960 and 0 < kp2[1] < 960):
+            continue
+        z1 = oracle.kb8_triangulate(cam, cam, kp1, kp2, R12, t12, s2, s2)
+        assert z1 > 0 and abs(z1 - X[2]) < 0.02 * X[2], (z1, X)
+        assert oracle.kb8_triangulate(cam, cam, kp1, kp2 + np.array([0, 25.0]), R12, t12, s2, s2) in (-4.0, -5.0,
+                                                                                                      -2.0, -3.0)
+    kp = cam.project_np(np.array([0.5, 0.2, 5.0]))
+    assert oracle.kb8_triangulate(cam, cam, kp, kp, np.eye(3), np.zeros(3), s2, s2) == -1.0
+
+
+def test_kb8_triangulation_search_oracle(oracle):
+    """SearchForTriangulation with KannalaBrandt8 keyframes on the oracle: a 3D-consistent pair (scene.keyframe_pair_3d)
+    matches many features, and the two-view test rejects some of what bCoarse (no geometric test) accepts."""
+    from mam3slam_amd import scene, synth
+
+    img = synth.make_frame(960, 960, agent=1, frame=0)
+    k, d, _ = oracle.extract(img, oracle.params(700))
+    cam = scene.kannala_brandt8()
+    F = scene.make_frame_data(k, d, 960, 960)
+    KF1, KF2 = scene.keyframe_pair_3d(F, cam, np.random.default_rng(1))
+    n, out = oracle.search_for_triangulation_kf(KF1, KF2, cam, cam, False, False)
+    nc, outc = oracle.search_for_triangulation_kf(KF1, KF2, cam, cam, False, True)
+    assert n > 50 and nc > n
+
+
+def test_pinhole_kf_triangulation_oracle_equals_f12_entry(oracle):
+    """The oracle's keyframe-level entry (its own pair geometry) equals its F12 entry fed the C-ABI's geometry
+    (mam_triangulation_geometry, host arithmetic in libmam_gpu.so): both sides compute T12 / ep / F12 identically."""
+    from mam3slam_amd import scene, synth
+    from mam3slam_amd.match import triangulation_geometry
+
+    img = synth.make_frame(640, 480, agent=2, frame=3)
+    k, d, _ = oracle.extract(img, oracle.params(1000))
+    pin = scene.pinhole(640, 480)
+    F = scene.make_frame_data(k, d, 640, 480)
+    KF1, KF2 = scene.keyframe_pair_3d(F, pin, np.random.default_rng(2))
+    _, _, F12, ep = triangulation_geometry(KF1.pose, KF2.pose, pin)
+    n1, o1 = oracle.search_for_triangulation_kf(KF1, KF2, pin, pin, True, False)
+    n2, o2 = oracle.search_for_triangulation(KF1, KF2, F12, ep, True, False)
+    assert n1 == n2 and np.array_equal(o1, o2) and n1 > 50
