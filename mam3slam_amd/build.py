@@ -30,6 +30,7 @@ FLAGS = [
     "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-Wall",
     "-Wno-unused-function",
+    "-Werror=return-type",
 ]
 
 

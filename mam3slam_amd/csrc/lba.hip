@@ -80,6 +80,8 @@ struct Prob {
     int32_t* cnt;                // [L + Np] counters / cursors of the device structure build
     int32_t* eidx;               // [Np][L] edge of (pose block, point), -1 if none
     uint8_t* pairmask;           // [Np][Np] (i1 < i2): the two poses share a landmark (S block non-zero)
+    uint8_t* tmask;              // [nt][nt] (r >= c): 16x16 tile (r, c) of L is structurally non-zero (S + fill)
+    int nt;                      // npad / 16
     // state: [2] buffers, lm->cur is the current one
     double* pose[2];             // [P][7] q(xyzw) t
     double* pt[2];               // [L][3]
@@ -137,8 +139,10 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // ---- per edge: error, robust weight, Jacobians (EdgeSE3ProjectXYZ); returns the edge's rho0
+// jo / ho: where the edge's jac (21) and H_pl (18) records go (the caller's LDS staging slots); both are always
+// written when want_jac (zeros where the edge is inactive or its pose fixed).
 __device__ __forceinline__ double linearize_edge(const Prob& d, const double* pose, const double* pts, int e,
-                                                 bool want_jac) {
+                                                 bool want_jac, double* jo, double* ho) {
     const int ip = d.edge_point[e], ipose = d.edge_pose[e];
     const double* T = pose + 7 * (size_t)ipose;
     const double* X = pts + 3 * (size_t)ip;
@@ -164,10 +168,8 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     if (d.active && !d.active[e]) {
         // setLevel(1): outside initializeOptimization(0), no term in chi2 / H / b (zeros add exactly nothing)
         if (want_jac) {
-            double* o = d.jac + 21 * (size_t)e;
-            for (int k = 0; k < 21; k++) o[k] = 0.0;
-            if (d.pose_h[ipose] >= 0)
-                for (int k = 0; k < 18; k++) d.hpl[18 * (size_t)e + k] = 0.0;
+            for (int k = 0; k < 21; k++) jo[k] = 0.0;
+            for (int k = 0; k < 18; k++) ho[k] = 0.0;
         }
         return 0.0;
     }
@@ -184,7 +186,7 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
     const double R[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
                          txz - twy, tyz + twx, 1 - (txx + tyy)};
-    double* o = d.jac + 21 * (size_t)e;
+    double* o = jo;
     if (kb8) {
         // J = -projectJac(Xc) (KannalaBrandt8.cpp:145-175), A = J R, B = J * SE3deriv (OptimizableTypes.cpp:150-159)
         double P[6];
@@ -220,9 +222,10 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     // H_pl = B^T (rho' Omega) A for edges whose pose is optimised (base_binary_edge.hpp:54-120)
     if (d.pose_h[ipose] >= 0) {
         const double wo = r1 * w;
-        double* hp = d.hpl + 18 * (size_t)e;
         for (int a = 0; a < 6; a++)
-            for (int c2 = 0; c2 < 3; c2++) hp[3 * a + c2] = o[6 + a] * wo * o[c2] + o[12 + a] * wo * o[3 + c2];
+            for (int c2 = 0; c2 < 3; c2++) ho[3 * a + c2] = o[6 + a] * wo * o[c2] + o[12 + a] * wo * o[3 + c2];
+    } else {
+        for (int k = 0; k < 18; k++) ho[k] = 0.0;
     }
     return r0;
 }
@@ -409,21 +412,47 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
 }
 
 // ======================================================================================================= solve
-// Per block of 256 edges: the rho0 partial sum in a fixed order (butterfly per wave, then the 4 waves in order).
+// Per-edge records (jac 21 doubles, H_pl 18, W = H_pl D^-1 18, coefficients 6) are laid out edge-major; a wave owns 64
+// consecutive edges and moves its records between HBM and LDS as contiguous 16-byte chunks (one cache line per 4
+// lanes), the lanes computing on their own edge's record in LDS. (Per-lane strided 8-byte stores of a 168-byte record
+// cost one L2 transaction per lane per store.)
+constexpr int EW = 64;   // edges per wave
+__device__ __forceinline__ void wave_copy_out(double* __restrict__ dst, const double* __restrict__ src, int n) {
+    // n doubles from LDS to global, dst 16-byte aligned
+    for (int i = 2 * lane_id(); i < n; i += 128) {
+        if (i + 1 < n) *reinterpret_cast<double2*>(dst + i) = *reinterpret_cast<const double2*>(src + i);
+        else dst[i] = src[i];
+    }
+}
+__device__ __forceinline__ void wave_copy_in(double* __restrict__ dst, const double* __restrict__ src, int n) {
+    for (int i = 2 * lane_id(); i < n; i += 128) {
+        if (i + 1 < n) *reinterpret_cast<double2*>(dst + i) = *reinterpret_cast<const double2*>(src + i);
+        else dst[i] = src[i];
+    }
+}
+
+// grid (ceil(E/64), Q) x 64: one wave per 64 edges; the rho0 partial sum per wave (fixed-order butterfly).
 // mode 0: iteration start (Jacobians, current state); 1: trial (errors only, trial state); 2: initial chi2.
-__global__ __launch_bounds__(256) void k_linearize(const Prob* __restrict__ probs, int mode) {
+__global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs, int mode) {
     const Prob& d = probs[blockIdx.y];
     const LM& lm = *d.lm;
     if (lm.status || (mode != 2 && lm.done) || (mode == 0 && !lm.need_lin)) return;
-    if ((int)blockIdx.x * 256 >= d.E) return;
-    __shared__ double ws[4];
+    const int e0 = blockIdx.x * EW;
+    if (e0 >= d.E) return;
+    __shared__ double sj[EW * 21];
+    __shared__ double sh[EW * 18];
     const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0) : 0.0;
+    const int lane = lane_id(), e = e0 + lane;
+    double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0, sj + 21 * lane, sh + 18 * lane)
+                       : 0.0;
     r = wave_sum_d(r);
-    if (lane_id() == 0) ws[threadIdx.x >> 6] = r;
-    __syncthreads();
-    if (threadIdx.x == 0) d.part[blockIdx.x] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+    if (lane == 0) d.part[blockIdx.x] = r;
+    if (mode == 0) {
+        const int ne = min(EW, d.E - e0);
+        __syncthreads();
+        wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
+        wave_copy_out(d.hpl + 18 * (size_t)e0, sh, 18 * ne);
+    }
 }
 
 // grid (ceil(L/64) + Np, Q) x 64: H_ll, b_l per point (edge order, one thread each) and H_pp, b_p per optimised pose
@@ -495,9 +524,14 @@ __device__ double block_sum(double acc, double* s) {
 }
 
 __device__ double chi_of_parts(const Prob& d, double* s) {
+    // parts of 64 edges, grouped by 256 as ((p0 + p1) + p2) + p3 (a missing part adds nothing), then strided + tree
     double acc = 0.0;
-    const int nb = (d.E + 255) / 256;
-    for (int b = threadIdx.x; b < nb; b += RED) acc += d.part[b];
+    const int np = (d.E + EW - 1) / EW, nb = (d.E + 255) / 256;
+    for (int b = threadIdx.x; b < nb; b += RED) {
+        double g = d.part[4 * b];
+        for (int k = 1; k < 4; k++) g = g + (4 * b + k < np ? d.part[4 * b + k] : 0.0);
+        acc += g;
+    }
     return block_sum(acc, s);
 }
 
@@ -555,44 +589,73 @@ __global__ __launch_bounds__(RED) void k_ctl_begin(const Prob* __restrict__ prob
 }
 
 // ---- Schur
-// grid (ceil(L/64), Q) x 64: per point D^-1 and its edges' H_pl D^-1 and coefficients (block_solver.hpp:405-427)
-__global__ __launch_bounds__(64) void k_schur_prep(const Prob* __restrict__ probs) {
-    const Prob& d = probs[blockIdx.y];
-    const LM& lm = *d.lm;
-    if (lm.status || lm.done) return;
-    const int h = blockIdx.x * 64 + threadIdx.x;
-    if (h >= d.L) return;
-    const double lambda = lm.lambda;
+// D = H_ll + lambda I (setLambda, block_solver.hpp:563-589) and its inverse (Eigen's 3x3 cofactor inverse, :389)
+__device__ __forceinline__ void point_dinv(const Prob& d, int h, double lambda, double Di[9]) {
     double D[9];
     for (int k = 0; k < 9; k++) D[k] = d.Hll[9 * (size_t)h + k] + ((k % 4 == 0) ? lambda : 0.0);
     const double c00 = D[4] * D[8] - D[5] * D[7], c01 = D[5] * D[6] - D[3] * D[8], c02 = D[3] * D[7] - D[4] * D[6];
     const double det = D[0] * c00 + D[1] * c01 + D[2] * c02;
-    double Di[9];
     Di[0] = c00 / det; Di[3] = c01 / det; Di[6] = c02 / det;
     Di[1] = (D[2] * D[7] - D[1] * D[8]) / det; Di[4] = (D[0] * D[8] - D[2] * D[6]) / det;
     Di[7] = (D[1] * D[6] - D[0] * D[7]) / det;
     Di[2] = (D[1] * D[5] - D[2] * D[4]) / det; Di[5] = (D[2] * D[3] - D[0] * D[5]) / det;
     Di[8] = (D[0] * D[4] - D[1] * D[3]) / det;
-    for (int k = 0; k < 9; k++) d.Dinv[9 * (size_t)h + k] = Di[k];
-    const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)h;
-    double db[3];
-    for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
-    for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
-        const int e = d.pe_idx[s];
-        if (d.pose_h[d.edge_pose[e]] < 0) continue;
-        const double* B = d.hpl + 18 * (size_t)e;
-        double* o = d.bdinv + 18 * (size_t)e;
-        double* cf = d.coef + 6 * (size_t)e;
-        for (int i = 0; i < 6; i++) {
-            for (int j = 0; j < 3; j++)
-                o[3 * i + j] = B[3 * i] * Di[j] + B[3 * i + 1] * Di[3 + j] + B[3 * i + 2] * Di[6 + j];
-            cf[i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
+}
+
+// grid (ceil(max(E, L)/64), Q) x 64: one wave per 64 edges (block_solver.hpp:405-427): the edge's point D^-1 (the
+// point's first edge stores it for the back-substitution), W = H_pl D^-1 and the coefficient H_pl D^-1 b_l; H_pl in
+// and W / coefficients out as contiguous per-wave blocks through LDS. Points without edges get D^-1 from lane h.
+__global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const LM& lm = *d.lm;
+    if (lm.status || lm.done) return;
+    const double lambda = lm.lambda;
+    const int lane = lane_id();
+    {
+        const int h = blockIdx.x * EW + lane;
+        if (h < d.L && d.pe_off[h + 1] == d.pe_off[h]) {
+            double Di[9];
+            point_dinv(d, h, lambda, Di);
+            for (int k = 0; k < 9; k++) d.Dinv[9 * (size_t)h + k] = Di[k];
         }
     }
+    const int e0 = blockIdx.x * EW;
+    if (e0 >= d.E) return;
+    __shared__ double sh[EW * 18];
+    __shared__ double sw[EW * 18];
+    __shared__ double sc[EW * 6];
+    const int ne = min(EW, d.E - e0);
+    wave_copy_in(sh, d.hpl + 18 * (size_t)e0, 18 * ne);
+    __syncthreads();
+    const int e = e0 + lane;
+    if (e < d.E) {
+        double* o = sw + 18 * lane;
+        double* cf = sc + 6 * lane;
+        if (d.pose_h[d.edge_pose[e]] >= 0 || d.pe_idx[d.pe_off[d.edge_point[e]]] == e) {
+            const int h = d.edge_point[e];
+            double Di[9];
+            point_dinv(d, h, lambda, Di);
+            if (d.pe_idx[d.pe_off[h]] == e)
+                for (int k = 0; k < 9; k++) d.Dinv[9 * (size_t)h + k] = Di[k];
+            const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)h;
+            double db[3];
+            for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
+            const double* B = sh + 18 * lane;
+            for (int i = 0; i < 6; i++) {
+                for (int j = 0; j < 3; j++)
+                    o[3 * i + j] = B[3 * i] * Di[j] + B[3 * i + 1] * Di[3 + j] + B[3 * i + 2] * Di[6 + j];
+                cf[i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
+            }
+        }
+    }
+    __syncthreads();
+    wave_copy_out(d.bdinv + 18 * (size_t)e0, sw, 18 * ne);
+    wave_copy_out(d.coef + 6 * (size_t)e0, sc, 6 * ne);
 }
 
 // grid (Np * Np + Np, Q) x 64: one wave per block (i1 <= i2) of S (blocks with i2 < i1 exit), landmarks seen by both
-// poses walked through pose i2's edges and pose i1's edge-table row; then one wave per pose for b_s.
+// poses walked through pose i2's edges and pose i1's edge-table row; then one wave per pose for b_s. Only the lower
+// triangle of S is written (the one the factorization reads).
 __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     const LM& lm = *d.lm;
@@ -624,7 +687,6 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
         // no shared landmark: a zero block (the factorization's fill-in of the previous trial is overwritten)
         if (lane < 36) {
             const int r = lane / 6, c = lane % 6, N = d.npad;
-            d.S[(size_t)(6 * i1 + r) * N + 6 * i2 + c] = 0.0;
             d.S[(size_t)(6 * i2 + c) * N + 6 * i1 + r] = 0.0;
         }
         return;
@@ -659,8 +721,7 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
         double out = -v;
         if (i1 == i2) out = (d.Hpp[36 * (size_t)i1 + lane] + (r == c ? lambda : 0.0)) - v;
         const int N = d.npad;
-        d.S[(size_t)(6 * i1 + r) * N + 6 * i2 + c] = out;
-        d.S[(size_t)(6 * i2 + c) * N + 6 * i1 + r] = out;
+        d.S[(size_t)(6 * i2 + c) * N + 6 * i1 + r] = out;   // the lower triangle, the one the factorization reads
     }
 }
 
@@ -683,6 +744,44 @@ constexpr int NB = 16;
 constexpr int LDLT_THREADS = MAM_LDLT_THREADS;
 
 __host__ __device__ inline int ldlt_pad(int n) { return (n + NB - 1) / NB * NB; }
+
+// grid (Q) x 1024, after k_struct_sort: the 16x16 tile pattern of L. A tile of S is non-zero when it holds a pose
+// diagonal block or the block of two poses sharing a landmark (pairmask); the right-looking factorization then fills
+// tile (r1, r2) whenever tiles (r1, c) and (r2, c) are non-zero for some c < r2 (the symbolic LDL^T at tile
+// granularity, column by column — what SimplicialLDLT's symbolic phase does per entry, linear_solver_eigen.h:147-201).
+// Structurally zero tiles of L stay exact zeros, so k_ldlt skips them: every non-zero entry sees the same arithmetic
+// as in the dense factorization. Windows whose covisibility is banded (keyframes along a trajectory) factor in
+// O(n b^2) instead of O(n^3).
+__global__ __launch_bounds__(1024) void k_struct_tiles(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.x];
+    if (d.lm->status) return;
+    const int nt = d.nt, n = 6 * d.Np;
+    for (int q = threadIdx.x; q < nt * nt; q += 1024) {
+        const int r = q / nt, c = q % nt;
+        uint8_t v = 0;
+        if (r == c) {
+            v = 1;
+        } else if (r > c) {
+            const int r0 = NB * r, r1 = min(NB * r + NB, n), c0 = NB * c, c1 = min(NB * c + NB, n);
+            if (r0 < r1 && c0 < c1) {
+                for (int i1 = c0 / 6; i1 <= (c1 - 1) / 6 && !v; i1++)
+                    for (int i2 = r0 / 6; i2 <= (r1 - 1) / 6 && !v; i2++)
+                        if (i1 == i2 || d.pairmask[(size_t)min(i1, i2) * d.Np + max(i1, i2)]) v = 1;
+            }
+        }
+        d.tmask[q] = v;
+    }
+    __syncthreads();
+    for (int c = 0; c + 1 < nt; c++) {
+        const int m = nt - 1 - c;
+        for (int q = threadIdx.x; q < m * m; q += 1024) {
+            const int r1 = c + 1 + q / m, r2 = c + 1 + q % m;
+            if (r2 <= r1 && d.tmask[(size_t)r1 * nt + c] && d.tmask[(size_t)r2 * nt + c]) d.tmask[(size_t)r1 * nt + r2] = 1;
+        }
+        __syncthreads();
+    }
+}
+
 
 // workspace doubles: PL and PW (NB x (npad - NB) each) + y (npad)
 __host__ __device__ inline size_t ldlt_ws_doubles(int npad) {
@@ -804,9 +903,12 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
     for (int kb = 0; kb < N; kb += NB) {
         // (B) panel rows: L21 = A21 L11^-T D^-1, W21 = L21 D (staged transposed), y2 -= L21 y1
         const int m = N - kb - NB;
+        const int kc = kb / NB;
+        const uint8_t* tcol = d.tmask + kc;   // tcol[r * nt]: tile (r, kc) of L non-zero
         double* PL = ws;
         double* PW = ws + (size_t)NB * m;
         for (int i = kb + NB + t; i < N; i += LDLT_THREADS) {
+            if (!tcol[(size_t)(i / NB) * d.nt]) continue;   // structurally zero row of L21: no update, no y change
             // keep the L11 factors in LDS (reading them per row): hoisting all 120 into registers spills
             asm volatile("" ::: "memory");
             double w[NB];
@@ -832,7 +934,9 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
         if (m == 0) break;
         const int T16 = m / 16;
         // (C1) the next block column: blocks (br, 0), one wave each
-        for (int br = wid; br < T16; br += LDLT_THREADS / 64) ldlt_tile16(A, N, kb, PL, PW, m, br, 0, lane);
+        const bool c1nz = tcol[(size_t)(kc + 1) * d.nt] != 0;
+        for (int br = wid; br < T16; br += LDLT_THREADS / 64)
+            if (c1nz && tcol[(size_t)(kc + 1 + br) * d.nt]) ldlt_tile16(A, N, kb, PL, PW, m, br, 0, lane);
         __syncthreads();
         // (C2) wave 0 factors the next diagonal block; the other waves update the blocks with bc >= 1
         if (wid == 0) {
@@ -843,7 +947,8 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
             for (int q = wid - 1; q < n2; q += LDLT_THREADS / 64 - 1) {
                 int tr, tc;
                 tri_index(q, &tr, &tc);
-                ldlt_tile16(A, N, kb, PL, PW, m, tr + 1, tc + 1, lane);
+                if (tcol[(size_t)(kc + 2 + tr) * d.nt] && tcol[(size_t)(kc + 2 + tc) * d.nt])
+                    ldlt_tile16(A, N, kb, PL, PW, m, tr + 1, tc + 1, lane);
             }
         }
         __syncthreads();
@@ -869,6 +974,7 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
         }
         __syncthreads();
         for (int i = t; i < kb; i += LDLT_THREADS) {
+            if (!d.tmask[(size_t)(kb / NB) * d.nt + i / NB]) continue;   // L(kb.., i) structurally zero
             double sy = Y[i];
 #pragma unroll
             for (int j = 0; j < NB; j++) sy -= A[(size_t)(kb + j) * N + i] * Y[kb + j];
@@ -1063,6 +1169,8 @@ struct mam_lba_ctx {
     DevBuf<uint8_t> io;           // host API: inputs + outputs of the one problem
     DevBuf<Prob> probs;
     DevBuf<LM> lms;
+    hipStream_t stream2 = nullptr;   // the second half of a split batch (created on first use, the caller's priority)
+    hipEvent_t ev[2] = {nullptr, nullptr};
     double trials_ema = 8.0;      // slots enqueued before the first read-back (tracks the trials solves take)
 };
 
@@ -1087,8 +1195,9 @@ size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
     const size_t nx = 6 * (size_t)Np + 3 * (size_t)L;
     return al(4 * (size_t)P) + al(4 * (size_t)Np) + al(4 * (size_t)(L + 1)) + al(4 * (size_t)E) +
            al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) +
+           al((size_t)(npad / 16) * (npad / 16)) +
            2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
-           al(8 * (size_t)((E + 255) / 256 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
+           al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
            al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
            al(8 * (size_t)npad * npad) + al(8 * nx) + al(8 * (size_t)npad) +
            al(8 * mam::lba::ldlt_ws_doubles(npad)) + al((size_t)E);
@@ -1105,13 +1214,15 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.cnt = cv.take<int32_t>(d.L + d.Np);
     d.eidx = cv.take<int32_t>((size_t)d.Np * d.L);
     d.pairmask = cv.take<uint8_t>((size_t)d.Np * d.Np);
+    d.nt = d.npad / mam::lba::NB;
+    d.tmask = cv.take<uint8_t>((size_t)d.nt * d.nt);
     d.pose[0] = cv.take<double>(7 * (size_t)d.P);
     d.pose[1] = cv.take<double>(7 * (size_t)d.P);
     d.pt[0] = cv.take<double>(3 * (size_t)d.L);
     d.pt[1] = cv.take<double>(3 * (size_t)d.L);
     d.err = cv.take<double>(2 * (size_t)d.E);
     d.jac = cv.take<double>(21 * (size_t)d.E);
-    d.part = cv.take<double>((size_t)(d.E + 255) / 256 + 1);
+    d.part = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
     d.hpl = cv.take<double>(18 * (size_t)d.E);
     d.bdinv = cv.take<double>(18 * (size_t)d.E);
     d.coef = cv.take<double>(6 * (size_t)d.E);
@@ -1219,6 +1330,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     MAM_HIP(hipMemcpyAsync(outs_buf().p, c->lm_host.p + pb + lb, sizeof(Outs) * Q, hipMemcpyHostToDevice, s));
     const Prob* P = c->probs.p;
     const dim3 gE((maxE + 255) / 256 > 0 ? (maxE + 255) / 256 : 1, Q);
+    const dim3 gE64((maxE + EW - 1) / EW > 0 ? (maxE + EW - 1) / EW : 1, Q);
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
         hipLaunchKernelGGL(k_struct_init, dim3(32, Q), dim3(1024), 0, s, P);
@@ -1226,39 +1338,75 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_struct_scan, dim3(1, Q), dim3(1024), 0, s, P);
         hipLaunchKernelGGL(k_struct_scatter, gE, dim3(256), 0, s, P);
         hipLaunchKernelGGL(k_struct_sort, dim3(std::max(maxLb, 1), Q), dim3(256), 0, s, P);
-        hipLaunchKernelGGL(k_linearize, gE, dim3(256), 0, s, P, 2);
+        hipLaunchKernelGGL(k_struct_tiles, dim3(Q), dim3(1024), 0, s, P);
+        hipLaunchKernelGGL(k_linearize, gE64, dim3(EW), 0, s, P, 2);
         hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
     }
     const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
-    const dim3 gPrep((maxL + 63) / 64 > 0 ? (maxL + 63) / 64 : 1, Q);
+    const dim3 gPrep((std::max(maxE, maxL) + EW - 1) / EW > 0 ? (std::max(maxE, maxL) + EW - 1) / EW : 1, Q);
     const dim3 gBlk(maxNp * maxNp + maxNp > 0 ? maxNp * maxNp + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
     const dim3 gUpd((maxPL + 255) / 256 > 0 ? (maxPL + 255) / 256 : 1, Q);
-    auto slot = [&]() {
+    // The batch runs as G interleaved halves on two streams: one half's latency-bound factorization (one workgroup
+    // per problem) overlaps the other half's throughput kernels. Every kernel indexes its problems from the Prob
+    // pointer it is given, so a half is the sub-array P + first with Q_g problems. MAM_LBA_SPLIT=1 disables.
+    const char* sp = std::getenv("MAM_LBA_SPLIT");
+    const int G = (Q >= 4 && !(sp && sp[0] == '1')) ? 2 : 1;
+    hipStream_t sg[2] = {s, s};
+    if (G == 2) {
+        if (!c->stream2) {
+            int prio = 0;
+            if (hipStreamGetPriority(s, &prio) != hipSuccess) prio = 0;
+            if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio) != hipSuccess) {
+                (void)hipGetLastError();
+                MAM_HIP(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+            }
+            for (auto& e : c->ev) MAM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        sg[1] = c->stream2;
+        MAM_HIP(hipEventRecord(c->ev[0], s));   // the structure build precedes both halves
+        MAM_HIP(hipStreamWaitEvent(c->stream2, c->ev[0], 0));
+    }
+    auto slot_g = [&](int g) {
+        const int q0 = g * Q / G, q1 = (g + 1) * Q / G, Qg = q1 - q0;
+        const Prob* Pg = P + q0;
+        hipStream_t st = sg[g];
+        const dim3 gE64g(gE64.x, Qg), gSysg(gSys.x, Qg), gPrepg(gPrep.x, Qg), gBlkg(gBlk.x, Qg), gUpdg(gUpd.x, Qg);
+        mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
-            mam::StageTimer::Scope sc(&c->timer, s, 0);
-            hipLaunchKernelGGL(k_linearize, gE, dim3(256), 0, s, P, 0);
-            hipLaunchKernelGGL(k_sys, gSys, dim3(64), 0, s, P);
-            hipLaunchKernelGGL(k_ctl_begin, dim3(Q), dim3(RED), 0, s, P);
+            mam::StageTimer::Scope sc(tm, st, 0);
+            hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 0);
+            hipLaunchKernelGGL(k_sys, gSysg, dim3(64), 0, st, Pg);
+            hipLaunchKernelGGL(k_ctl_begin, dim3(Qg), dim3(RED), 0, st, Pg);
         }
         {
-            mam::StageTimer::Scope sc(&c->timer, s, 1);
-            hipLaunchKernelGGL(k_schur_prep, gPrep, dim3(64), 0, s, P);
-            hipLaunchKernelGGL(k_schur_blk, gBlk, dim3(64), 0, s, P);
+            mam::StageTimer::Scope sc(tm, st, 1);
+            hipLaunchKernelGGL(k_schur_prep, gPrepg, dim3(64), 0, st, Pg);
+            hipLaunchKernelGGL(k_schur_blk, gBlkg, dim3(64), 0, st, Pg);
         }
         {
-            mam::StageTimer::Scope sc(&c->timer, s, 2);
+            mam::StageTimer::Scope sc(tm, st, 2);
             if (lds_ok)
-                hipLaunchKernelGGL(k_ldlt<true>, dim3(Q), dim3(LDLT_THREADS), max_lds, s, P);
+                hipLaunchKernelGGL(k_ldlt<true>, dim3(Qg), dim3(LDLT_THREADS), max_lds, st, Pg);
             else
-                hipLaunchKernelGGL(k_ldlt<false>, dim3(Q), dim3(LDLT_THREADS), 0, s, P);
+                hipLaunchKernelGGL(k_ldlt<false>, dim3(Qg), dim3(LDLT_THREADS), 0, st, Pg);
         }
         {
-            mam::StageTimer::Scope sc(&c->timer, s, 3);
-            hipLaunchKernelGGL(k_backsub_update, gUpd, dim3(256), 0, s, P);
-            hipLaunchKernelGGL(k_linearize, gE, dim3(256), 0, s, P, 1);
-            hipLaunchKernelGGL(k_ctl_end, dim3(Q), dim3(RED), 0, s, P);
+            mam::StageTimer::Scope sc(tm, st, 3);
+            hipLaunchKernelGGL(k_backsub_update, gUpdg, dim3(256), 0, st, Pg);
+            hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 1);
+            hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
+    };
+    auto slot = [&]() {
+        for (int g = 0; g < G; g++) slot_g(g);
+    };
+    auto join = [&]() -> int {   // the second half's work before anything the first stream does next
+        if (G == 2) {
+            MAM_HIP(hipEventRecord(c->ev[1], c->stream2));
+            MAM_HIP(hipStreamWaitEvent(s, c->ev[1], 0));
+        }
+        return MAM_OK;
     };
     auto stopped = [&]() { return stop_flag && *stop_flag; };
     // Every slot is one Levenberg trial of every unfinished problem, so a solve needs at most iterations x 10 slots;
@@ -1275,6 +1423,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         for (int i = 0; i < k; i++) slot();
         enq += k;
         MAM_HIP(hipGetLastError());
+        if (int rc = join()) return rc;
         MAM_HIP(hipMemcpyAsync(lh, c->lms.p, sizeof(LM) * Q, hipMemcpyDeviceToHost, s));
         MAM_HIP(hipStreamSynchronize(s));
         bool all = true;
@@ -1282,6 +1431,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         if (all) break;
         chunk = 2;
     }
+    if (int rc = join()) return rc;
     hipLaunchKernelGGL(mam::lba::k_finish, dim3(std::max({(maxE + 255) / 256, (maxPL + 255) / 256, 1}), Q), dim3(256),
                        0, s, P, outs_buf().p);
     MAM_HIP(hipGetLastError());
@@ -1375,6 +1525,12 @@ void mam_lba_destroy(mam_lba_ctx* c) {
     ::mam::DeviceScope mam_dev_scope_(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
+    if (c->stream2) {
+        (void)hipStreamSynchronize(c->stream2);
+        (void)hipStreamDestroy(c->stream2);
+    }
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
     delete c;
 }
 

@@ -131,10 +131,10 @@ struct StageTimer {
         int stage;
         hipEvent_t a = nullptr;
         Scope(StageTimer* t_, hipStream_t s_, int st) : t(t_), s(s_), stage(st) {
-            if (t->enabled) { a = t->take(); (void)hipEventRecord(a, s); }
+            if (t && t->enabled) { a = t->take(); (void)hipEventRecord(a, s); }
         }
         ~Scope() {
-            if (t->enabled) {
+            if (t && t->enabled) {
                 hipEvent_t b = t->take();
                 (void)hipEventRecord(b, s);
                 t->pending.push_back({stage, a, b});
