@@ -657,13 +657,18 @@ __global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ prob
 // poses walked through pose i2's edges and pose i1's edge-table row; then one wave per pose for b_s. Only the lower
 // triangle of S is written (the one the factorization reads).
 __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs) {
-    const Prob& d = probs[blockIdx.y];
+    // XCD-aware: each XCD takes a contiguous range of (problem, block row) ids, so the W / H_pl records of the
+    // landmarks its rows share stay in its L2
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int logical = xcd_logical(lin, gridDim.x * gridDim.y);
+    const int bx = logical % gridDim.x;
+    const Prob& d = probs[logical / gridDim.x];
     const LM& lm = *d.lm;
     if (lm.status || lm.done) return;
     const int lane = threadIdx.x;
     const int nb2 = d.Np * d.Np;
-    if ((int)blockIdx.x >= nb2) {
-        const int h = blockIdx.x - nb2;
+    if (bx >= nb2) {
+        const int h = bx - nb2;
         if (h >= d.Np) return;
         double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         for (int s = d.qe_off[h] + lane; s < d.qe_off[h + 1]; s += 64) {
@@ -681,7 +686,7 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
         }
         return;
     }
-    const int i1 = blockIdx.x / d.Np, i2 = blockIdx.x % d.Np;
+    const int i1 = bx / d.Np, i2 = bx % d.Np;
     if (i2 < i1) return;
     if (i1 != i2 && !d.pairmask[(size_t)i1 * d.Np + i2]) {
         // no shared landmark: a zero block (the factorization's fill-in of the previous trial is overwritten)

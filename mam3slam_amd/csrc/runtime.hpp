@@ -43,6 +43,13 @@ struct DeviceScope {
     ::mam::DeviceScope mam_dev_scope_(dev);                 \
     if (!mam_dev_scope_.ok) return MAM_ERR_DEVICE
 
+// XCD-aware block order: the hardware deals linear workgroup ids round-robin over the 8 XCDs (each with its own L2);
+// map the linear id bijectively (any grid size) to a logical id so that each XCD works one contiguous range.
+__host__ __device__ inline int xcd_logical(int lin, int nlin) {
+    const int q = nlin >> 3, rem = nlin & 7, x = lin & 7, k = lin >> 3;
+    return x < rem ? x * (q + 1) + k : rem * (q + 1) + (x - rem) * q + k;
+}
+
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
