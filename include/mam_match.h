@@ -226,6 +226,29 @@ typedef struct mam_frames_dev {
                                  (MAM_ERR_ARG if the context's last search was over other frames) */
 } mam_frames_dev;
 
+/* A batch of keyframes in device memory for SearchForTriangulation (LocalMapping::CreateNewMapPoints runs it against
+ * the new keyframe's 30 best covisible keyframes, LocalMapping.cc:504-582). kfs: the keyframe slots in the extractor's
+ * batched layout (nframes = keyframes; taken / taken_out / reuse_grid unused). has_mp[k][i]: GetMapPoint(i) != NULL.
+ * The FeatureVector of slot k is given as the BoW transform's per-feature node and weight
+ * (mam_bow_transform_batch_device out_nid / out_weight at levelsup 4): feature i belongs to node nid[k][i] iff
+ * weight[k][i] > 0 (DBoW2 does not add stopped words). pairs[q] = (kf1 slot, kf2 slot). */
+typedef struct mam_tri_batch {
+    mam_frames_dev kfs;
+    const uint8_t* has_mp;     /* [nkf][kp_stride] */
+    const uint32_t* nid;       /* [nkf][kp_stride] */
+    const double* weight;      /* [nkf][kp_stride] */
+    const mam_pose* tcw;       /* [nkf] GetPose() */
+    int32_t npairs;
+    const int32_t* pairs;      /* [npairs][2] */
+} mam_tri_batch;
+
+/* npairs SearchForTriangulation(pKF1, pKF2, pairs, false, bCoarse) in one set of launches, every keyframe with camera
+ * `cam` (Pinhole or KannalaBrandt8): out_match12[q][i] = idx2 or -1 for i < kf1's count (kp_stride entries per pair),
+ * out_nmatches[q]. Asynchronous on `stream` (NULL = the context's). kp_stride <= 8192. */
+int mam_search_for_triangulation_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_camera* cam,
+                                              const mam_tri_batch* batch, int check_ori, int coarse,
+                                              int32_t* out_match12, int32_t* out_nmatches, void* stream);
+
 /* Frame f matches n_mps[f] MapPoints at mps + f*mp_stride. Outputs at out_kp_to_mp + f*kp_stride and
  * out_nmatches[f]. */
 int mam_search_by_projection_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_frames_dev* frames,

@@ -1011,6 +1011,203 @@ __global__ __launch_bounds__(256) void k_tri_rot(const mam_keypoint* keys1, cons
     if (tid == 0) *nmatch = red[0] + red[1] + red[2] + red[3];
 }
 
+// ---- batched SearchForTriangulation (CreateNewMapPoints' 30 searches per new keyframe, LocalMapping.cc:504-582):
+// keyframe slots with device-resident features, FeatureVectors given as the BoW transform's per-feature node and
+// weight (DBoW2 adds feature i to node nid iff its word weight > 0), pairs (kf1, kf2).
+struct TriBatchArgs {
+    mam_frame_geom g;
+    mam_frames_dev kfs;
+    const uint8_t* has_mp;
+    const uint32_t* nid;
+    const double* weight;
+    const mam_pose* tcw;
+    const int32_t* pairs;
+    int npairs;
+    mam_camera cam;
+    int coarse, check_ori;
+    unsigned long long* skey;   // [nkf][skey_stride] (nid << 32 | idx) ascending, ~0 past the FeatureVector
+    int skey_stride;            // power of two >= kp_stride
+    int32_t* nfv;               // [nkf] features in the FeatureVector
+    cam::PairGeom* pg;          // [npairs]
+    int32_t* out;               // [npairs][kp_stride]
+    int32_t* out_n;             // [npairs]
+};
+
+// grid (nkf) x 1024: every keyframe's FeatureVector as one sorted key array (node id, then feature index: the order
+// the reference walks a FeatureVector, std::map by node + insertion order), bitonic sort in LDS
+__global__ __launch_bounds__(1024) void k_tri_fv_sort(TriBatchArgs a) {
+    extern __shared__ unsigned long long sk[];
+    const int k = blockIdx.x, P = a.skey_stride;
+    const int n = frame_n(a.kfs, k);
+    const size_t base = (size_t)k * a.kfs.kp_stride;
+    for (int i = threadIdx.x; i < P; i += 1024) {
+        unsigned long long v = ~0ull;
+        if (i < n && a.weight[base + i] > 0.0) v = ((unsigned long long)a.nid[base + i] << 32) | (unsigned)i;
+        sk[i] = v;
+    }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < P / 2; i += 1024) {
+                const int lo = 2 * i - (i & (stride - 1));
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const unsigned long long x = sk[lo], y = sk[hi];
+                if ((x > y) == up) { sk[lo] = y; sk[hi] = x; }
+            }
+            __syncthreads();
+        }
+    }
+    int cnt = 0;
+    for (int i = threadIdx.x; i < P; i += 1024) {
+        a.skey[(size_t)k * P + i] = sk[i];
+        cnt += sk[i] != ~0ull;
+    }
+    __shared__ int red[16];
+    cnt = wave_sum(cnt);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < 16; w++) t += red[w];
+        a.nfv[k] = t;
+    }
+}
+
+// grid (ceil(npairs / 256)) x 256: the pair geometry of ORBmatcher.cc:913-930
+__global__ __launch_bounds__(256) void k_tri_pair_geom(TriBatchArgs a) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= a.npairs) return;
+    const mam_pose& t1 = a.tcw[a.pairs[2 * q]];
+    const mam_pose& t2 = a.tcw[a.pairs[2 * q + 1]];
+    cam::pair_geometry(t1.q, t1.t, t2.q, t2.t, a.cam, a.cam, &a.pg[q]);
+}
+
+// grid (ceil(kp_stride / 4), npairs) x 64: 16 lanes per idx1 of kf1 (four per wave): its node's features in kf2 found
+// by binary search in kf2's sorted FeatureVector keys, the candidates dealt to the lanes, (dist, last position)
+// argmin over the lanes = "dist <= bestDist, last equal wins" (ORBmatcher.cc:1015-1074)
+__global__ __launch_bounds__(64) void k_tri_batch(TriBatchArgs a) {
+    const int q = blockIdx.y;
+    const int k1 = a.pairs[2 * q], k2 = a.pairs[2 * q + 1];
+    const int sub = lane_id() & 15;
+    const int idx1 = blockIdx.x * 4 + (lane_id() >> 4);
+    const int n1 = frame_n(a.kfs, k1);
+    const int S = a.kfs.kp_stride;
+    int32_t* out = a.out + (size_t)q * S;
+    if (idx1 >= S) return;
+    const size_t b1 = (size_t)k1 * S, b2 = (size_t)k2 * S;
+    bool active = idx1 < n1 && a.weight[b1 + idx1] > 0.0 && !a.has_mp[b1 + idx1];
+    unsigned best = 0xFFFFFFFFu;
+    if (active) {
+        const cam::PairGeom& G = a.pg[q];
+        const mam_keypoint kp1 = a.kfs.keys[b1 + idx1];
+        const uint8_t* d1 = a.kfs.desc + (b1 + idx1) * 32;
+        const unsigned long long key = (unsigned long long)a.nid[b1 + idx1] << 32;
+        const unsigned long long* sk = a.skey + (size_t)k2 * a.skey_stride;
+        // [b, e): kf2's features of the node
+        int lo = 0, hi = a.nfv[k2];
+        while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            if (sk[m] < key) lo = m + 1;
+            else hi = m;
+        }
+        const int b = lo;
+        hi = a.nfv[k2];
+        while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            if (sk[m] <= (key | 0xFFFFFFFFull)) lo = m + 1;
+            else hi = m;
+        }
+        const int e = lo;
+        const float la = kp1.x * G.F12[0] + kp1.y * G.F12[3] + G.F12[6];
+        const float lb = kp1.x * G.F12[1] + kp1.y * G.F12[4] + G.F12[7];
+        const float lc = kp1.x * G.F12[2] + kp1.y * G.F12[5] + G.F12[8];
+        float r1[3] = {0.0f, 0.0f, 1.0f};
+        const bool kb8 = a.cam.model == MAM_CAM_KANNALA_BRANDT8;
+        if (kb8 && !a.coarse) cam::kb8_unproject_f(a.cam, kp1.x, kp1.y, r1);
+        for (int i2 = b + sub; i2 < e; i2 += 16) {
+            const int idx2 = (int)(sk[i2] & 0xFFFFFFFFull);
+            if (a.has_mp[b2 + idx2]) continue;
+            const int dist = desc_dist(d1, a.kfs.desc + (b2 + idx2) * 32);
+            if (dist > MAM_TH_LOW) continue;
+            const mam_keypoint kp2 = a.kfs.keys[b2 + idx2];
+            const float distex = G.ep[0] - kp2.x;
+            const float distey = G.ep[1] - kp2.y;
+            if (distex * distex + distey * distey < 100 * a.g.scale_factors[kp2.octave]) continue;
+            bool ok = a.coarse != 0;
+            if (!ok) {
+                if (kb8) {
+                    float r2[3];
+                    cam::kb8_unproject_f(a.cam, kp2.x, kp2.y, r2);
+                    ok = cam::kb8_triangulate_matches(a.cam, a.cam, kp1.x, kp1.y, r1, kp2.x, kp2.y, r2, G.R12, G.t12,
+                                                      a.g.level_sigma2[kp1.octave],
+                                                      a.g.level_sigma2[kp2.octave]) > 0.0001f;
+                } else {
+                    const float num = la * kp2.x + lb * kp2.y + lc;
+                    const float den = la * la + lb * lb;
+                    ok = den != 0 && num * num / den < 3.84 * a.g.level_sigma2[kp2.octave];
+                }
+            }
+            if (ok) best = min(best, ((unsigned)dist << 16) | (0xFFFFu - (unsigned)(i2 - b)));
+        }
+        for (int o = 8; o > 0; o >>= 1) best = min(best, (unsigned)__shfl_xor((int)best, o, 16));
+        if (sub == 0)
+            out[idx1] = best != 0xFFFFFFFFu ? (int)(sk[b + (int)(0xFFFFu - (best & 0xFFFFu))] & 0xFFFFFFFFull) : -1;
+    } else if (sub == 0) {
+        out[idx1] = -1;
+    }
+}
+
+// grid (npairs) x 256: nmatches per pair, with the rotation-histogram filter when check_ori (ORBmatcher.cc:1114-1133)
+__global__ __launch_bounds__(256) void k_tri_batch_rot(TriBatchArgs a) {
+    const int q = blockIdx.x;
+    const int k1 = a.pairs[2 * q], k2 = a.pairs[2 * q + 1];
+    const int S = a.kfs.kp_stride;
+    const int n1 = frame_n(a.kfs, k1);
+    const mam_keypoint* keys1 = a.kfs.keys + (size_t)k1 * S;
+    const mam_keypoint* keys2 = a.kfs.keys + (size_t)k2 * S;
+    int32_t* out = a.out + (size_t)q * S;
+    __shared__ int hist[MAM_HISTO_LENGTH];
+    __shared__ int top[3];
+    __shared__ int red[4];
+    const int tid = threadIdx.x;
+    if (tid < MAM_HISTO_LENGTH) hist[tid] = 0;
+    __syncthreads();
+    int cnt = 0;
+    for (int i = tid; i < n1; i += 256) {
+        if (out[i] >= 0) {
+            cnt++;
+            if (a.check_ori) atomicAdd(&hist[rot_bin(keys1[i].angle - keys2[out[i]].angle)], 1);
+        }
+    }
+    __syncthreads();
+    if (a.check_ori) {
+        if (tid == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < MAM_HISTO_LENGTH; i++) {
+                const int s = hist[i];
+                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+                else if (s > max3) { max3 = s; ind3 = i; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            top[0] = ind1; top[1] = ind2; top[2] = ind3;
+        }
+        __syncthreads();
+        for (int i = tid; i < n1; i += 256) {
+            if (out[i] >= 0) {
+                const int bin = rot_bin(keys1[i].angle - keys2[out[i]].angle);
+                if (bin != top[0] && bin != top[1] && bin != top[2]) { out[i] = -1; cnt--; }
+            }
+        }
+    }
+    cnt = wave_sum(cnt);
+    if (lane_id() == 0) red[tid >> 6] = cnt;
+    __syncthreads();
+    if (tid == 0) a.out_n[q] = red[0] + red[1] + red[2] + red[3];
+}
+
 __global__ void k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = desc_dist(a + (size_t)i * 32, b + (size_t)i * 32);
@@ -1368,6 +1565,10 @@ struct mam_match_ctx {
     int grid_nframes = 0, grid_stride = 0;
     // host-API staging
     DevBuf<uint8_t> stage;
+    // batched triangulation scratch
+    DevBuf<unsigned long long> tri_skey;
+    DevBuf<int32_t> tri_nfv;
+    DevBuf<mam::cam::PairGeom> tri_pg;
 };
 
 namespace {
@@ -1851,6 +2052,52 @@ int mam_search_for_triangulation_kf(mam_match_ctx* c, const mam_frame_geom* g, c
     a.ep[1] = pg.ep[1];
     return tri_search(c, g, kf1->n, kf1->keys, kf1->desc, kf1->has_mp, &kf1->fv, kf2->n, kf2->keys, kf2->desc,
                       kf2->has_mp, &kf2->fv, a, check_ori, coarse, out);
+}
+
+int mam_search_for_triangulation_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_camera* cam,
+                                              const mam_tri_batch* b, int check_ori, int coarse, int32_t* out_match12,
+                                              int32_t* out_nmatches, void* stream) {
+    if (!c || !geom_ok(g) || !cam || !b || !out_match12 || !out_nmatches || b->npairs < 0 || b->kfs.nframes < 0 ||
+        b->kfs.kp_stride <= 0 || b->kfs.kp_stride > 8192 || !b->kfs.keys || !b->kfs.desc || !b->kfs.counts ||
+        !b->has_mp || !b->nid || !b->weight || !b->tcw || (b->npairs > 0 && !b->pairs))
+        return MAM_ERR_ARG;
+    if (cam->model != MAM_CAM_PINHOLE && cam->model != MAM_CAM_KANNALA_BRANDT8) return MAM_ERR_ARG;
+    if (b->npairs == 0 || b->kfs.nframes == 0) return MAM_OK;
+    MAM_DEVICE_SCOPE(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const int nkf = b->kfs.nframes, S = b->kfs.kp_stride;
+    int P = 1;
+    while (P < S) P <<= 1;
+    if (int rc = c->tri_skey.alloc((size_t)nkf * P)) return rc;
+    if (int rc = c->tri_nfv.alloc(nkf)) return rc;
+    if (int rc = c->tri_pg.alloc(b->npairs)) return rc;
+    mam::TriBatchArgs a{};
+    a.g = *g;
+    a.kfs = b->kfs;
+    a.has_mp = b->has_mp;
+    a.nid = b->nid;
+    a.weight = b->weight;
+    a.tcw = b->tcw;
+    a.pairs = b->pairs;
+    a.npairs = b->npairs;
+    a.cam = *cam;
+    a.coarse = coarse;
+    a.check_ori = check_ori;
+    a.skey = c->tri_skey.p;
+    a.skey_stride = P;
+    a.nfv = c->tri_nfv.p;
+    a.pg = c->tri_pg.p;
+    a.out = out_match12;
+    a.out_n = out_nmatches;
+    {
+        mam::StageTimer::Scope sc(&c->timer, s, 3);
+        hipLaunchKernelGGL(mam::k_tri_fv_sort, dim3(nkf), dim3(1024), sizeof(unsigned long long) * P, s, a);
+        hipLaunchKernelGGL(mam::k_tri_pair_geom, dim3((b->npairs + 255) / 256), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(mam::k_tri_batch, dim3((S + 3) / 4, b->npairs), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(mam::k_tri_batch_rot, dim3(b->npairs), dim3(256), 0, s, a);
+    }
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
 }
 
 int mam_fuse_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_frames_dev* fr, const mam_fuse_kf* kfs,

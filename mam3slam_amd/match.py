@@ -119,6 +119,12 @@ class FramesDev(C.Structure):
                 ("counts", C.c_void_p), ("taken", C.c_void_p), ("taken_out", C.c_void_p), ("reuse_grid", C.c_int32)]
 
 
+class TriBatch(C.Structure):
+    """mam_tri_batch: keyframe slots in HBM + FeatureVectors as per-feature (node, weight) + pairs."""
+    _fields_ = [("kfs", FramesDev), ("has_mp", C.c_void_p), ("nid", C.c_void_p), ("weight", C.c_void_p),
+                ("tcw", C.c_void_p), ("npairs", C.c_int32), ("pairs", C.c_void_p)]
+
+
 MP_TRACK_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("view_cos", "<f4"), ("track_depth", "<f4"),
                            ("track_in_view", "<i4"), ("scale_level", "<i4"), ("is_bad", "<i4"), ("nobs", "<i4"),
                            ("desc", "u1", (32,))])
@@ -199,6 +205,8 @@ _SIGS = {
                                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "mam_search_for_triangulation_kf": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
                                                   C.c_void_p]),
+    "mam_search_for_triangulation_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                                            C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mam_triangulation_geometry": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_void_p]),
     "mam_search_by_projection_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
@@ -413,6 +421,17 @@ class ORBmatcher:
         out = out[:len(k1)]
         idx = np.nonzero(out >= 0)[0]
         return n, np.stack([idx, out[idx]], 1).astype(np.int64)
+
+    def search_for_triangulation_batch_device(self, F: FrameData, cam: Camera, batch: TriBatch, d_out: int,
+                                              d_nmatches: int, bCoarse: bool = False, stream=None):
+        """mam_search_for_triangulation_batch_device: batch.npairs SearchForTriangulation calls over device-resident
+        keyframes; F supplies the frame geometry (scale / sigma tables, image bounds)."""
+        g = F.geom()
+        check(self._L.mam_search_for_triangulation_batch_device(self._ctx, C.byref(g), C.byref(cam), C.byref(batch),
+                                                                 int(self.mbCheckOrientation), int(bCoarse),
+                                                                 C.c_void_p(d_out), C.c_void_p(d_nmatches),
+                                                                 C.c_void_p(stream or 0)),
+              "SearchForTriangulation(batch)")
 
     def SearchForTriangulationKF(self, KF1: FrameData, KF2: FrameData, cam1: Camera, cam2: Camera | None = None,
                                  bOnlyStereo: bool = False, bCoarse: bool = False):

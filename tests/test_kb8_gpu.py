@@ -181,3 +181,68 @@ def test_kb8_local_bundle_adjustment(gpu_lib, oracle, cam, cfg):
         den = np.maximum(np.linalg.norm(np.asarray(b), axis=-1), 1e-9)
         assert float((num / den).max()) <= 1e-4
     assert ro.final_chi2 < ro.initial_chi2
+
+
+@pytest.mark.parametrize("model", ["pinhole", "kb8"])
+@pytest.mark.parametrize("ori", [False, True])
+def test_search_for_triangulation_batch_device(gpu_lib, oracle, frames, cam, model, ori):
+    """The batched device form (CreateNewMapPoints' searches over keyframe slots in HBM, FeatureVectors as per-feature
+    node + weight): every pair's matches equal the oracle's SearchForTriangulation on the same keyframes, with stopped
+    words (weight 0) left out of the FeatureVectors and keyframes of different sizes."""
+    import torch
+
+    from mam3slam_amd.match import FramesDev, TriBatch
+
+    dev = torch.device("cuda", 0)
+    w, h, k, d = frames[1]
+    c = cam if model == "kb8" else scene.pinhole(w, h, 450.0)
+    M = _matcher(0.6, ori)
+    rng = np.random.default_rng(3600 + ori)
+    F = scene.make_frame_data(k, d, w, h)
+    kfs = []
+    for j in range(3):   # three pairs of keyframes generated around the frame, 6 slots
+        KF1, KF2 = scene.keyframe_pair_3d(F, c, rng)
+        kfs += [KF1, KF2]
+    S = max(len(x.keys) for x in kfs) + 5
+    nkf = len(kfs)
+    keys = np.zeros((nkf, S), kfs[0].keys.dtype)
+    desc = np.zeros((nkf, S, 32), np.uint8)
+    cnt = np.zeros((nkf, 2), np.int32)
+    has = np.zeros((nkf, S), np.uint8)
+    nid = np.zeros((nkf, S), np.uint32)
+    wt = np.zeros((nkf, S), np.float64)
+    tcw = np.zeros(nkf, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+    for s_, KF in enumerate(kfs):
+        n = len(KF.keys)
+        keys[s_, :n], desc[s_, :n], cnt[s_, 0] = KF.keys, KF.desc, n
+        has[s_, :n] = KF.has_mp
+        stopped = rng.random(n) < 0.05   # stopped words: not in the FeatureVector
+        fv = {}
+        for node, feats in KF.featvec.items():
+            for i in feats:
+                nid[s_, i] = node
+                if not stopped[i]:
+                    wt[s_, i] = 1.0
+                    fv.setdefault(node, []).append(i)
+        KF.featvec = fv
+        tcw[s_]["q"], tcw[s_]["t"] = KF.pose
+    pairs = np.array([[0, 1], [2, 3], [4, 5], [1, 0], [0, 3], [5, 2]], np.int32)
+    t = {n: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for n, v in
+         dict(keys=keys.view(np.uint8), desc=desc, cnt=cnt, has=has, nid=nid, wt=wt, tcw=tcw.view(np.uint8),
+              pairs=pairs).items()}
+    out = torch.full((len(pairs), S), -7, dtype=torch.int32, device=dev)
+    nm = torch.zeros(len(pairs), dtype=torch.int32, device=dev)
+    b = TriBatch()
+    b.kfs = FramesDev(nkf, S, t["keys"].data_ptr(), t["desc"].data_ptr(), t["cnt"].data_ptr(), None, None, 0)
+    b.has_mp, b.nid, b.weight, b.tcw = t["has"].data_ptr(), t["nid"].data_ptr(), t["wt"].data_ptr(), t["tcw"].data_ptr()
+    b.npairs, b.pairs = len(pairs), t["pairs"].data_ptr()
+    M.search_for_triangulation_batch_device(kfs[0], c, b, out.data_ptr(), nm.data_ptr())
+    torch.cuda.synchronize()
+    og, ng = out.cpu().numpy(), nm.cpu().numpy()
+    total = 0
+    for q, (a1, a2) in enumerate(pairs):
+        no, oo = oracle.search_for_triangulation_kf(kfs[a1], kfs[a2], c, c, ori, False)
+        n1 = len(kfs[a1].keys)
+        assert ng[q] == no and np.array_equal(og[q, :n1], oo), (q, ng[q], no)
+        total += no
+    assert total > 100
