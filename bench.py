@@ -38,6 +38,9 @@ CONFIGS = {
     "c1": dict(width=640, height=480, nfeatures=1000, lba=False),
     # BASELINE.json configs[2]: 1280x720, 2000 features + LocalBundleAdjustment (50 KF / ~3000 MapPoints windows)
     "c2": dict(width=1280, height=720, nfeatures=2000, lba=True),
+    # BASELINE.json configs[3]: the testMultiAgentSystem agents (test/settingsForTest_00.yaml: KannalaBrandt8, 700
+    # features) at 640x480, two agents in total (both on one GPU at --gpus 1, one per GPU at --gpus 2)
+    "c3": dict(width=640, height=480, nfeatures=700, lba=True, camera="kb8", agents=2),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFS = 78.6    # MI355X FP64 vector / matrix (spec)
@@ -146,7 +149,7 @@ class TrackingLeg:
         desc_h = self.d_desc.cpu().numpy()
         cnt_h = self.d_cnt.cpu().numpy()
         self.kps_h, self.cnt_h = kps_h, cnt_h
-        cam = scene.pinhole(W, H)
+        cam = scene.kannala_brandt8(W, H) if cfg.get("camera") == "kb8" else scene.pinhole(W, H)
         self.cam = cam
         lasts, mpls, poses = [], [], []
         F0 = None
@@ -366,7 +369,7 @@ def ingest_section(tr, reps=5):
             "d2h_bytes_per_step": int(bo), "h2d_GBs": bi / (m_in * 1e-3) / 1e9, "d2h_GBs": bo / (m_out * 1e-3) / 1e9}
 
 
-def parity_section(tr, mapping):
+def parity_section(tr, mapping, newmp=None):
     """In-run parity against the oracle: one frame's extraction, the same frame's frustum + local search chain, and
     one LocalBundleAdjustment window of the timed region (the same inputs): bit-exact / index-exact / <= 1e-4 with
     the same Levenberg control flow."""
@@ -375,7 +378,7 @@ def parity_section(tr, mapping):
     from oracle import oracle_py
 
     out = {}
-    f = 1
+    f = min(1, tr.B - 1)
     ko, do, _ = oracle_py.extract(tr.frames[f], oracle_py.params(tr.NF))
     n = int(tr.cnt_h[f, 0])
     kg = tr.kps_h[f, :n]
@@ -397,6 +400,16 @@ def parity_section(tr, mapping):
     nmo, oo = oracle_py.search_by_projection(F, to, 1.0, False, 50.0, 0.8)
     out["local_search_index_exact"] = bool(int(tr.d_nm2[f].item()) == nmo and
                                            np.array_equal(tr.d_out2[f, :n].cpu().numpy(), oo))
+    if newmp is not None:
+        # pair 0 of the last step's CreateNewMapPoints searches, FeatureVectors from the device BoW
+        K1, K2 = newmp.pair_inputs(0)
+        t0 = time.perf_counter()
+        no, oo = oracle_py.search_for_triangulation_kf(K1, K2, tr.cam, tr.cam, False, False)
+        tri_ms = (time.perf_counter() - t0) * 1e3
+        n1 = len(K1.keys)
+        out["triangulation_index_exact"] = bool(int(newmp.nmatch[0].item()) == no and
+                                                np.array_equal(newmp.out[0, :n1].cpu().numpy(), oo))
+        out["triangulation_pair"] = {"matches": int(no), "n1": n1, "n2": len(K2.keys), "oracle_ms": tri_ms}
     if mapping is not None:
         w = 0
         prob = mapping.window_inputs(w)
@@ -412,7 +425,7 @@ def parity_section(tr, mapping):
     return out
 
 
-def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0):
+def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
     """The oracle (single-thread C++ restatement of the reference path) on a bounded sample of the same per-frame
     work: extraction + motion search + isInFrustum + local search, plus 1/K of a LocalBundleAdjustment of a window of
     the timed region (its oracle time measured in parity_section on the same inputs)."""
@@ -437,6 +450,22 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0):
             break
     track_ms = el * 1e3 / n
     per_frame_ms = track_ms + (lba_window_ms / K if lba_window_ms is not None else 0.0)
+    tri_ms = None
+    if newmp is not None:
+        # one new keyframe's LocalMapping search work on the oracle: its 30 SearchForTriangulation (the device BoW's
+        # FeatureVectors) and its ComputeBoW (the oracle's DBoW2 transform over the same vocabulary)
+        tri_ms = 0.0
+        for q in range(newmp.NN):
+            K1, K2 = newmp.pair_inputs(q)
+            t2 = time.perf_counter()
+            oracle_py.search_for_triangulation_kf(K1, K2, tr.cam, tr.cam, False, False)
+            tri_ms += (time.perf_counter() - t2) * 1e3
+        tree = oracle_py.BowTree(newmp.voc.v)   # built once, as ORBVocabulary is loaded once (not timed)
+        d = newmp.desc[newmp.head, :int(newmp.cnt[newmp.head, 0].item())].cpu().numpy()
+        t2 = time.perf_counter()
+        oracle_py.bow_transform(newmp.voc.v, d, 4, tree=tree)
+        bow_ms = (time.perf_counter() - t2) * 1e3
+        per_frame_ms += (tri_ms + bow_ms) / K
     res = {"value": 1e3 / per_frame_ms, "unit": "frames/s", "cores": 1, "kind": "port",
            "tracking_ms_per_frame": track_ms,
            "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15) + "
@@ -445,6 +474,10 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0):
     if lba_window_ms is not None:
         res["lba_ms_per_window"] = lba_window_ms
         res["sample"] += f"; + LocalBundleAdjustment of a timed-region window ({lba_window_ms:.1f} ms) / {K} frames"
+    if tri_ms is not None:
+        res["new_keyframe_search_ms"] = {"triangulation_30_pairs": tri_ms, "compute_bow": bow_ms}
+        res["sample"] += (f"; + one new keyframe's 30 SearchForTriangulation ({tri_ms:.1f} ms) and ComputeBoW "
+                          f"({bow_ms:.2f} ms) / {K} frames")
     return res
 
 
@@ -453,7 +486,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU (independent frame streams)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per step per GPU (independent frame streams); default 256, c3: its 2 agents / N")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
                     help="c2 (1280x720/2000 + LocalBundleAdjustment) is BASELINE.json's headline metric config")
     ap.add_argument("--kf-every", type=int, default=8,
@@ -499,47 +533,66 @@ def main():
         dist.init_process_group(backend="nccl", device_id=dev)
 
     cfg = CONFIGS[args.config]
-    B, NL, K = args.batch, max(1, args.lanes), max(1, args.kf_every)
+    agents_total = cfg.get("agents")
+    B = args.batch if args.batch is not None else (max(1, agents_total // world) if agents_total else 256)
+    NL, K = min(max(1, args.lanes), B), max(1, args.kf_every)
     if B % NL:
         raise SystemExit(f"--batch {B} is not a multiple of --lanes {NL}")
+    # keyframe cadence: B/K new keyframes (LBA windows) per step; with fewer streams than K, one every K/B steps
+    map_every = max(1, K // B)
     tr = TrackingLeg(cfg, B, NL, rank, dev)
-    mapping = None
+    mapping = newmp = None
     if cfg["lba"]:
-        from mam3slam_amd.mapping import LocalMappingLeg
+        from mam3slam_amd.mapping import LocalMappingLeg, NewMapPointsLeg
 
-        mapping = LocalMappingLeg(max(1, B // K), rank, world, dev)
+        mapping = LocalMappingLeg(max(1, B // K), rank, world, dev, camera=tr.cam if cfg.get("camera") else None,
+                                  width=tr.W, height=tr.H)
+        newmp = NewMapPointsLeg(tr, max(1, B // K), dev)
 
     lba_ms = []
 
-    def mapping_worker(step_idx):
+    def mapping_worker(step_idx, head):
         t = time.perf_counter()
+        # LocalMapping per new keyframe: ComputeBoW + CreateNewMapPoints' 30 SearchForTriangulation (the keyframes the
+        # previous tracking steps inserted), then the LocalBundleAdjustment windows
+        newmp.run(mapping.stream, head)
         mapping.run(step_idx)
         lba_ms.append((time.perf_counter() - t) * 1e3)
 
     step_no = [0]
+    worker = [None]
+
+    def finish_mapping():
+        if worker[0] is not None:
+            worker[0].join()
+            worker[0] = None
 
     def step():
-        th = None
-        if mapping is not None:
-            th = threading.Thread(target=mapping_worker, args=(step_no[0],))
-            th.start()
+        # LocalMapping runs beside Tracking as in the reference (its own thread and stream): a mapping run started
+        # at one step may overlap the following tracking steps and is joined when the next one starts
+        if mapping is not None and step_no[0] % map_every == 0:
+            finish_mapping()
+            worker[0] = threading.Thread(target=mapping_worker, args=(step_no[0] // map_every, newmp.take()))
+            worker[0].start()
         tr.step()
-        if th is not None:
-            th.join()
+        if mapping is not None and (step_no[0] + 1) % map_every == 0:
+            newmp.ingest(step_no[0])
         step_no[0] += 1
 
     for _ in range(args.warmup):
         step()
+    finish_mapping()
     torch.cuda.synchronize(dev)
     if not args.no_graph:
         tr.capture()   # the tracking step (~40 launches) replayed as one HIP graph
         torch.cuda.synchronize(dev)
         for _ in range(2):
             step()
+        finish_mapping()
         torch.cuda.synchronize(dev)
     cnt = tr.d_cnt.cpu().numpy()
     n_kp = float(cnt[:, 0].mean())
-    nf_probe = min(B, 4)
+    nf_probe = min(tr.BL, 4)   # frames lane 0's extractor (tr.ext) processed
     n_cand = float(sum(len(tr.ext.debug_candidates(l, f)) for l in range(8) for f in range(nf_probe))) / nf_probe
     nm1, nm2, ntm = tr.d_nm1.cpu().numpy(), tr.d_nm2.cpu().numpy(), tr.d_ntm.cpu().numpy()
     if (nm1 < 0).any() or (nm2 < 0).any() or (cnt[:, 0] < 0).any():
@@ -548,20 +601,28 @@ def main():
     lba_ms.clear()
     if mapping is not None:
         mapping.solver.set_profiling(True)
+        newmp.matcher.set_profiling(True)
+        newmp.voc.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    finish_mapping()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     lba_stage = None
+    tri_stage = None
     if mapping is not None:
         lba_stage = mapping.solver.stage_times()
         mapping.solver.set_profiling(False)
+        tri_stage = {"triangulation": newmp.matcher.stage_times()["triangulation"],
+                     "compute_bow": newmp.voc.stage_times()["transform"]}
+        newmp.matcher.set_profiling(False)
+        newmp.voc.set_profiling(False)
         stv = int(mapping.status.cpu().numpy()[0])
         if stv != 0 or any(s[2] < 0 for s in mapping.stats):
             raise RuntimeError(f"LocalMapping leg status {stv} / {mapping.stats}")
@@ -579,7 +640,7 @@ def main():
 
         sin_info = fuse_bench.run(args.config, reps=max(args.steps, 5), device=dev.index or 0,
                                   oracle=not args.no_cpu_baseline and rank == 0)
-    parity = parity_section(tr, mapping) if rank == 0 else None
+    parity = parity_section(tr, mapping, newmp) if rank == 0 else None
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -609,12 +670,17 @@ def main():
 
     if rank == 0:
         W, H, NF = tr.W, tr.H, tr.NF
-        workload = (f"{args.config}: mono {W}x{H}, {NF} features, 8 levels; step = {B} frame streams x (ORB extract + "
-                    f"SearchByProjection motion th15 + isInFrustum + SearchByProjection local map th1)")
+        camd = "KannalaBrandt8 (test YAML)" if cfg.get("camera") == "kb8" else "Pinhole"
+        workload = (f"{args.config}: mono {W}x{H}, {NF} features, 8 levels, {camd}; step = {B} frame streams x (ORB "
+                    f"extract + SearchByProjection motion th15 + isInFrustum + SearchByProjection local map th1)")
+        if agents_total:
+            workload += f"; {agents_total} agents in total, {B} per GPU"
         if mapping is not None:
-            workload += (f" + a keyframe every {K} frames per stream: {mapping.W} LocalBundleAdjustment windows "
-                         f"(50 KF + fixed, ~{int(np.mean([len(p.point_id) for p in mapping.probs]))} MapPoints) per "
-                         f"step over the shared map, batched, concurrent with tracking; write-backs exchanged and "
+            workload += (f" + a keyframe every {K} frames per stream: {mapping.W} new keyframes per "
+                         f"{'step' if map_every == 1 else f'{map_every} steps'}, each with "
+                         f"ComputeBoW + 30 SearchForTriangulation (CreateNewMapPoints) and a LocalBundleAdjustment window "
+                         f"(50 KF + fixed, ~{int(np.mean([len(p.point_id) for p in mapping.probs]))} MapPoints) "
+                         f"over the shared map, batched, concurrent with tracking; write-backs exchanged and "
                          f"applied to the map the next windows read")
         out = {
             "metric": "tracked frames/sec (ORB extract+match+localBA) at 1/2/4/8 GPUs vs CPU ref",
@@ -625,7 +691,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": T / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if agents_total else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
@@ -664,6 +730,16 @@ def main():
                           "fp64_peak_tflops": FP64_PEAK_TFS,
                           "stage_ms_total": {k: v[0] for k, v in lba_stage.items()},
                           "exchange_bytes_per_step": int(mapping.exch.send.numel() * world)}
+        if newmp is not None:
+            nmv = newmp.nmatch.cpu().numpy()
+            out["new_keyframes"] = {
+                "keyframes_per_step": newmp.W, "searches_per_step": newmp.npairs, "neighbours": newmp.NN,
+                "matches_per_search": float(nmv.mean()),
+                "ms_per_step_triangulation": tri_stage["triangulation"][0] / args.steps,
+                "ms_per_step_compute_bow": tri_stage["compute_bow"][0] / args.steps,
+                "note": "ComputeBoW (levelsup 4, synthetic k=10 L=6 vocabulary) + CreateNewMapPoints' "
+                        "SearchForTriangulation against the 30 previously inserted keyframes, on the LocalMapping "
+                        "stream before the LBA windows (stage times on that stream, concurrent with tracking)"}
         if pose_info is not None:
             out["pose_optimization"] = pose_info
         if sin_info is not None:
@@ -672,7 +748,7 @@ def main():
             out["parity"] = parity
         if not args.no_cpu_baseline:
             lba_cpu = parity.get("lba_window", {}).get("oracle_ms") if parity else None
-            out["cpu_baseline"] = cpu_baseline(tr, cfg, lba_cpu, K, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(tr, cfg, lba_cpu, K, args.cpu_seconds, newmp)
             out["cpu_baseline"]["ms_per_frame"] = 1e3 / out["cpu_baseline"]["value"]
             if lat is not None:
                 out["speedup_latency_b1"] = out["cpu_baseline"]["tracking_ms_per_frame"] / lat["device_graph_ms"]

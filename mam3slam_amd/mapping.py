@@ -25,7 +25,7 @@ from .lba import LBASolver, _Problem, _Result
 
 class LocalMappingLeg:
     def __init__(self, n_windows: int, rank: int, world_size: int, device, max_gpus: int = 8, n_opt: int = 50,
-                 stride: int = 25, seed: int = 7, stream=None):
+                 stride: int = 25, seed: int = 7, stream=None, camera=None, width: int = 1280, height: int = 720):
         import torch
 
         self.dev = device
@@ -33,7 +33,7 @@ class LocalMappingLeg:
         self.rank, self.world_size = rank, world_size
         # one world for every world size (weak scaling: the same windows per GPU for any N)
         n_kf = (max_gpus * self.W + 1) * stride + n_opt + 8
-        self.world = W.make_world(n_kf=n_kf, seed=seed)
+        self.world = W.make_world(n_kf=n_kf, seed=seed, width=width, height=height, camera=camera)
         self.mp_base = self.world.n_kf          # MapPoint vertex id = mnId + maxKFid + 1
         self.starts = [(rank * self.W + w) * stride for w in range(self.W)]
         self.solver = LBASolver(device=device.index or 0)
@@ -166,3 +166,140 @@ class LocalMappingLeg:
 
         return LBAResult(o["pose_q"], o["pose_t"], o["point_xyz"], o["edge_chi2"], o["edge_depth_ok"], it, tr,
                          float(r.initial_chi2), float(r.final_chi2), st)
+
+
+class NewMapPointsLeg:
+    """LocalMapping::ProcessNewKeyFrame's ComputeBoW and CreateNewMapPoints' SearchForTriangulation against the new
+    keyframe's 30 neighbours (LocalMapping.cc:504-582, nn = 30 for monocular; ORBmatcher(0.6, false): no rotation
+    check), for the W keyframes the agents on this GPU insert per step, on the device.
+
+    The keyframes live in a ring of R slots in HBM (keypoints, descriptors, MapPoint flags, pose, BoW node + weight at
+    levelsup 4): `ingest` copies the step's new keyframes out of the tracking buffers (on the tracking stream, after
+    the step that tracked them: the reference's Tracking -> LocalMapping hand-off); `run` computes their BoW (DBoW2
+    transform, synthetic k=10 L=6 vocabulary — ORBvoc.txt is a missing blob) and searches each against the 30 slots
+    inserted before it (the synthetic map has no covisibility graph: the most recent keyframes stand in for the best
+    covisible ones). The triangulation and MapPoint creation that follow the search (LocalMapping.cc:590-828) are
+    outside the hot path; the map's new MapPoints enter through LocalMappingLeg.new_keyframes."""
+
+    NN = 30
+
+    def __init__(self, tr, n_new: int, device, seed: int = 0):
+        import torch
+
+        from . import bow
+        from .match import FramesDev, ORBmatcher, TriBatch
+
+        self.dev, self.tr, self.W = device, tr, int(n_new)
+        # new slots + at least NN older ones + one spare group (the next ingest writes while a search may run),
+        # a multiple of W
+        self.R = self.W * (2 + -(-self.NN // self.W))
+        R, S = self.R, tr.cap
+        self.S = S
+        self.keys = torch.zeros((R, S * 28), dtype=torch.uint8, device=device)
+        self.desc = torch.zeros((R, S, 32), dtype=torch.uint8, device=device)
+        self.cnt = torch.zeros((R, 2), dtype=torch.int32, device=device)
+        self.has_mp = torch.zeros((R, S), dtype=torch.uint8, device=device)
+        self.tcw = torch.zeros((R, tr.tcw_bytes), dtype=torch.uint8, device=device)
+        self.nid = torch.zeros((R, S), dtype=torch.int32, device=device)
+        self.weight = torch.zeros((R, S), dtype=torch.float64, device=device)
+        self.word = torch.zeros((R, S), dtype=torch.int32, device=device)
+        self.voc = bow.ORBVocabulary(bow.synthetic_vocabulary(10, 6, np.random.default_rng(seed), early_leaf=0.02),
+                                     device=device.index or 0)
+        self.matcher = ORBmatcher(0.6, False, device=device.index or 0)
+        self.head = 0
+        self.ready = {h: torch.cuda.Event() for h in range(0, self.R, self.W)}
+        # pairs for each head position: new slot j = head + i searches the NN slots inserted before it
+        self.pairs = {}
+        for head in range(0, R, self.W):
+            p = []
+            for i in range(self.W):
+                j = (head + i) % R
+                for k in range(1, self.NN + 1):
+                    p.append((j, (j - k) % R))
+            self.pairs[head] = torch.tensor(np.array(p, np.int32), device=device)
+        self.npairs = self.W * self.NN
+        self.out = torch.zeros((self.npairs, S), dtype=torch.int32, device=device)
+        self.nmatch = torch.zeros(self.npairs, dtype=torch.int32, device=device)
+        self._FramesDev, self._TriBatch = FramesDev, TriBatch
+        # initial ring: the first R frames, BoW on the device, no MapPoints yet
+        with torch.cuda.stream(tr.tstream):
+            fr = torch.arange(R, device=device) % tr.B
+            self.keys.copy_(tr.d_kps[fr])
+            self.desc.copy_(tr.d_desc[fr])
+            self.cnt.copy_(tr.d_cnt[fr])
+            self.tcw.copy_(tr.d_tcw.view(tr.B, -1)[fr])
+            self.voc.transform_batch_device(R, self.desc.data_ptr(), S, self.cnt.data_ptr(), 4, self.word.data_ptr(),
+                                            self.weight.data_ptr(), self.nid.data_ptr(), stream=tr.tstream.cuda_stream)
+            for ev in self.ready.values():
+                ev.record(tr.tstream)
+        self.pending = None
+
+    def ingest(self, step: int):
+        """Copy step `step`'s new keyframes (frames f = step mod K + i K) into the ring at the next head; on the
+        tracking stream after the tracking step. Their BoW is computed by the next `run`."""
+        import torch
+
+        tr, W, R = self.tr, self.W, self.R
+        K = max(1, tr.B // W)
+        head = (self.head + W) % R
+        fr = (torch.arange(W, device=self.dev) * K + step % K) % tr.B
+        sl = slice(head, head + W)
+        with torch.cuda.stream(tr.tstream):
+            self.keys[sl] = tr.d_kps[fr]
+            self.desc[sl] = tr.d_desc[fr]
+            self.cnt[sl] = tr.d_cnt[fr]
+            self.tcw[sl] = tr.d_tcw.view(tr.B, -1)[fr]
+            # GetMapPoint(i) != NULL: the keypoints Tracking matched (motion model or local map)
+            self.has_mp[sl] = ((tr.d_out1[fr] >= 0) | (tr.d_out2[fr] >= 0)).to(torch.uint8)
+            self.ready[head].record(tr.tstream)
+        self.pending = head
+
+    def take(self):
+        """The ring head of the keyframes ingested since the last take (None if none): the next run's work. Called
+        by the thread that starts the run, so a run never sees a later ingest."""
+        h, self.pending = self.pending, None
+        return h
+
+    def run(self, stream, head):
+        """ComputeBoW of the new keyframes at `head` + their W x 30 SearchForTriangulation, asynchronous on
+        `stream`."""
+        if head is None:
+            return
+        stream.wait_event(self.ready[head])
+        self.head = head
+        W, S, h = self.W, self.S, self.head
+        s = stream.cuda_stream
+        self.voc.transform_batch_device(W, self.desc[h].data_ptr(), S, self.cnt[h].data_ptr(), 4,
+                                        self.word[h].data_ptr(), self.weight[h].data_ptr(), self.nid[h].data_ptr(),
+                                        stream=s)
+        b = self._TriBatch()
+        b.kfs = self._FramesDev(self.R, S, self.keys.data_ptr(), self.desc.data_ptr(), self.cnt.data_ptr(), None, None, 0)
+        b.has_mp, b.nid, b.weight = self.has_mp.data_ptr(), self.nid.data_ptr(), self.weight.data_ptr()
+        b.tcw = self.tcw.data_ptr()
+        pairs = self.pairs[h]
+        b.npairs, b.pairs = int(pairs.shape[0]), pairs.data_ptr()
+        self.matcher.search_for_triangulation_batch_device(self.tr.F0, self.tr.cam, b, self.out.data_ptr(),
+                                                           self.nmatch.data_ptr(), False, stream=s)
+
+    def pair_inputs(self, q: int):
+        """Host FrameData of pair q of the last run (keys, desc, has_mp, FeatureVector from the device BoW, pose)."""
+        from .match import FrameData
+        from .orb import KP_DTYPE
+
+        out = []
+        for slot in self.pairs[self.head][q].cpu().numpy():
+            n = int(self.cnt[slot, 0].item())
+            keys = self.keys[slot].cpu().numpy().view(KP_DTYPE)[:n]
+            F = FrameData(keys=keys, desc=self.desc[slot, :n].cpu().numpy(), width=self.tr.W, height=self.tr.H,
+                          scale_factors=self.tr.F0.scale_factors, level_sigma2=self.tr.F0.level_sigma2)
+            F.has_mp = self.has_mp[slot, :n].cpu().numpy()
+            nid, w = self.nid[slot, :n].cpu().numpy(), self.weight[slot, :n].cpu().numpy()
+            fv = {}
+            for i in range(n):
+                if w[i] > 0:
+                    fv.setdefault(int(np.uint32(nid[i])), []).append(i)
+            F.featvec = dict(sorted(fv.items()))
+            t = self.tcw[slot].cpu().numpy().view(np.float32)
+            F.pose = (t[:4].copy(), t[4:7].copy())
+            out.append(F)
+        return out

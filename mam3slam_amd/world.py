@@ -34,9 +34,10 @@ class World:
     obs_w: np.ndarray        # float32 [n_obs] invSigma2 of the keypoint's level
     mp_obs_off: np.ndarray   # int32 [n_mp + 1]
     home: np.ndarray         # int32 [n_mp] keyframe a MapPoint is homed at
-    cam: np.ndarray          # float32 [1][4] pinhole fx, fy, cx, cy
+    cam: np.ndarray          # float32 [1][4] pinhole fx, fy, cx, cy or [1][8] KannalaBrandt8 (cam_model 1)
     width: int
     height: int
+    cam_model: int = 0
 
 
 def _scale_tables():
@@ -48,10 +49,11 @@ def _scale_tables():
 
 
 def make_world(n_kf: int = 800, pts_per_kf: int = 60, obs_span=(-3, 5), seed: int = 0, outlier_frac: float = 0.05,
-               width: int = 1280, height: int = 720, f: float = 500.0) -> World:
+               width: int = 1280, height: int = 720, f: float = 500.0, camera=None) -> World:
+    """camera: a match.Camera (Pinhole / KannalaBrandt8) for the observations instead of the f-pinhole."""
     rng = np.random.default_rng(seed)
     scale, inv_s2 = _scale_tables()
-    cam = np.array([[f, f, width / 2, height / 2]], np.float32)
+    cam = np.array([[f, f, width / 2, height / 2]], np.float32) if camera is None else camera.params()[None, :]
     k = np.arange(n_kf)
     centres = np.stack([0.1 * k, 0.3 * np.sin(k / 7.0), np.zeros(n_kf)], 1)
     yaw = 0.05 * np.sin(k / 5.0)
@@ -74,8 +76,13 @@ def make_world(n_kf: int = 800, pts_per_kf: int = 60, obs_span=(-3, 5), seed: in
     okf, omp = okf[keep].astype(np.int32), omp[keep].astype(np.int32)
     Xc = np.einsum("nij,nj->ni", Rs[okf], X[omp]) + ts[okf]
     octv = rng.integers(0, 8, len(okf))
-    u = f * Xc[:, 0] / Xc[:, 2] + width / 2 + rng.normal(0, 1, len(okf)) * scale[octv]
-    v = f * Xc[:, 1] / Xc[:, 2] + height / 2 + rng.normal(0, 1, len(okf)) * scale[octv]
+    if camera is None:
+        u = f * Xc[:, 0] / Xc[:, 2] + width / 2
+        v = f * Xc[:, 1] / Xc[:, 2] + height / 2
+    else:
+        u, v = camera.project_np(Xc).T
+    u = u + rng.normal(0, 1, len(okf)) * scale[octv]
+    v = v + rng.normal(0, 1, len(okf)) * scale[octv]
     u = u + 20.0 * (rng.random(len(okf)) < outlier_frac)
     obs_uv = np.stack([u, v], 1).astype(np.float32)          # mvKeysUn are float
     off = np.zeros(n_mp + 1, np.int32)
@@ -100,7 +107,7 @@ def make_world(n_kf: int = 800, pts_per_kf: int = 60, obs_span=(-3, 5), seed: in
     mp_table = np.zeros((n_mp, 4), np.float32)
     mp_table[:, :3] = X + rng.normal(0, 0.03 / np.sqrt(3), X.shape)
     return World(n_kf, n_mp, kf_table, mp_table, okf, omp, obs_uv, inv_s2[octv].astype(np.float32), off, home, cam,
-                 width, height)
+                 width, height, 0 if camera is None else int(camera.model))
 
 
 def window(world: World, start: int, n_opt: int = 50, huber_delta: float = HUBER_MONO, iterations: int = 10):
@@ -128,6 +135,6 @@ def window(world: World, start: int, n_opt: int = 50, huber_delta: float = HUBER
                       edge_pose=np.array([kf_index[int(x)] for x in okf], np.int32),
                       edge_obs=world.obs_uv[sel].astype(np.float64),
                       edge_inv_sigma2=world.obs_w[sel].astype(np.float64), cams=world.cam,
-                      huber_delta=huber_delta, iterations=iterations).contiguous()
+                      huber_delta=huber_delta, iterations=iterations, cam_model=world.cam_model).contiguous()
     assert P == len(prob.pose_id)
     return prob, kfs.astype(np.int64), mps.astype(np.int64)
