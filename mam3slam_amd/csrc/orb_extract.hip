@@ -18,8 +18,8 @@
 #include <vector>
 
 #include "orb_common.hpp"
-#include "orb_kernels.hip"
 #include "runtime.hpp"
+#include "orb_kernels.hip"
 
 namespace {
 

@@ -494,12 +494,22 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
                                                              int* __restrict__ cell_counts, int iniTh, int minTh) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int T = FAST_THREADS, NW = FAST_THREADS / 64;
-    const CellDesc c = cells[blockIdx.x];
-    const int f = blockIdx.y;
+#ifndef MAM_FAST_XCD
+#define MAM_FAST_XCD 1
+#endif
+    // XCD-aware order (as k_blur7): each XCD works a contiguous range of (frame, cell) ids, so the ROI rows adjacent
+    // cells share (6-pixel overlaps, 128-byte lines spanning ~4 cells) are fetched into one L2 instead of up to four
+    int cell_i = blockIdx.x, f = blockIdx.y;
+    if (MAM_FAST_XCD) {
+        const int logical = xcd_logical(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+        f = logical / gridDim.x;
+        cell_i = logical - f * gridDim.x;
+    }
+    const CellDesc c = cells[cell_i];
     const LevelGeom& L = g->L[c.level];
     const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
 #if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 4)
-    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = 0;   // timing experiment only
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = 0;   // timing experiment only
     return;
 #endif
     int pitch;
@@ -551,7 +561,7 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
     }
     __syncthreads();
 #if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 2)
-    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = (int)hp[tid].x;   // timing only
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = (int)hp[tid].x;   // timing only
     return;
 #endif
     const int pwm = max(pw, 1);
@@ -648,7 +658,7 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
             }
         }
     }
-    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + blockIdx.x] = use_hi ? tot_hi : tot_lo;
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = use_hi ? tot_hi : tot_lo;
 }
 
 // ------------------------------------------------------------------------------------------------ blur
@@ -1260,7 +1270,13 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, Le
                                                   const int* __restrict__ lvl_counts, int nframes,
                                                   mam_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int capacity, int32_t* __restrict__ counts, int fp_policy) {
-    const int gw = (blockIdx.x * 256 + threadIdx.x) >> 6;
+#ifndef MAM_DESC_XCD
+#define MAM_DESC_XCD 1
+#endif
+    // XCD-aware order: each XCD describes a contiguous range of (frame, keypoint) slots, so the patches of a frame's
+    // nearby keypoints share its L2
+    const int blk = MAM_DESC_XCD ? xcd_logical(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int gw = (blk * 256 + threadIdx.x) >> 6;
     const int lane = lane_id();
     const int f = gw / g->kp_slots;
     const int r = gw - f * g->kp_slots;
