@@ -554,8 +554,9 @@ def main():
     def mapping_worker(step_idx, head):
         t = time.perf_counter()
         # LocalMapping per new keyframe: ComputeBoW + CreateNewMapPoints' 30 SearchForTriangulation (the keyframes the
-        # previous tracking steps inserted), then the LocalBundleAdjustment windows
-        newmp.run(mapping.stream, head)
+        # previous tracking steps inserted; started on the leg's stream when they were ingested), then the
+        # LocalBundleAdjustment windows after them
+        newmp.wait(mapping.stream, head)
         mapping.run(step_idx)
         lba_ms.append((time.perf_counter() - t) * 1e3)
 
@@ -577,6 +578,7 @@ def main():
         tr.step()
         if mapping is not None and (step_no[0] + 1) % map_every == 0:
             newmp.ingest(step_no[0])
+            newmp.launch(newmp.pending)
         step_no[0] += 1
 
     for _ in range(args.warmup):

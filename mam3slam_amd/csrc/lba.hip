@@ -6,7 +6,8 @@
 //   k_linearize   per edge: map, error, chi2, Huber rho, Jacobians (OptimizableTypes.cpp:139-160), the robust-
 //                 weighted terms constructQuadraticForm needs (base_binary_edge.hpp:75-112); chi2 partial sums
 //   k_sys         per point: H_ll, b_l over its edge segment; one wave per non-fixed pose: H_pp, b_p
-//   k_ctl_begin   iteration start (levenberg.cpp:61-77, 171-185): chi2, max diag(H), lambda_0 = 1e-5 max diag
+//   k_ctl_begin   iteration start (levenberg.cpp:61-77, 171-185): chi2, max diag(H) (gathered by k_sys),
+//                 lambda_0 = 1e-5 max diag
 //   k_schur_prep  per point: D = H_ll + lambda I, D^-1, and per edge H_pl D^-1, H_pl D^-1 b_l (block_solver.hpp:
 //                 405-427)
 //   k_schur_blk   one wave per 6x6 block (i1 <= i2) of the reduced camera system, contributions in landmark
@@ -15,8 +16,9 @@
 //                 SimplicialLDLT), f64 MFMA trailing updates, fused forward / diagonal / backward substitution
 //   k_backsub_update  x_l = D^-1 (b_l - H_pl^T x_p) (block_solver.hpp:461-482) and the trial state:
 //                 T <- exp(dx) T (se3quat.h), X <- X + dx
-//   k_ctl_end     the trial's chi2, computeScale, rho, accept (discardTop) / reject (pop), lambda update and the
-//                 termination tests of levenberg.cpp:78-169 and sparse_optimizer.cpp:355-420
+//   k_ctl_end     the trial's chi2, computeScale (partial sums from k_linearize), rho, accept (discardTop) /
+//                 reject (pop), lambda update and the termination tests of levenberg.cpp:78-169 and
+//                 sparse_optimizer.cpp:355-420
 // Each kernel reads its problem's LM state (struct LM, device memory) and returns at once when the state says the
 // stage is not due: the host enqueues whole "slots" (iteration start + one trial) for every problem of a batch and
 // only synchronises once per chunk of slots (no host round trip per trial). Problems in different phases share the
@@ -53,6 +55,7 @@ struct LM {
     int fail;        // the last LDL^T hit a zero pivot
     int status;      // MAM_OK or MAM_ERR_*
     int iterations;  // optimize(iterations)
+    unsigned long long maxdiag;   // max |diag(H)| of the iteration's system (bits of a non-negative double)
 };
 
 struct Prob {
@@ -88,6 +91,7 @@ struct Prob {
     // per edge
     double* err;                 // [E][2]
     double* jac;                 // [E][21]: A(6) B(12) orr(2) wo(1)
+    double* part_s;              // [ceil(E / 64) + 1] computeScale partial sums of k_linearize(trial)'s blocks
     double* part;                // [ceil(E / 256)] rho0 partial sums of k_linearize's blocks
     double* hpl;                 // [E][18] H_pl pose x landmark
     double* bdinv;               // [E][18] H_pl D^-1
@@ -432,39 +436,52 @@ __device__ __forceinline__ void wave_copy_in(double* __restrict__ dst, const dou
 }
 
 // grid (ceil(E/64), Q) x 64: one wave per 64 edges; the rho0 partial sum per wave (fixed-order butterfly).
-// mode 0: iteration start (Jacobians, current state); 1: trial (errors only, trial state); 2: initial chi2.
+// mode 0: iteration start (Jacobians, current state); 1: trial (errors only, trial state) and the computeScale
+// partial sums; 2: initial chi2.
 __global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs, int mode) {
     const Prob& d = probs[blockIdx.y];
     const LM& lm = *d.lm;
     if (lm.status || (mode != 2 && lm.done) || (mode == 0 && !lm.need_lin)) return;
-    const int e0 = blockIdx.x * EW;
-    if (e0 >= d.E) return;
     __shared__ double sj[EW * 21];
     __shared__ double sh[EW * 18];
-    const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
-    const int lane = lane_id(), e = e0 + lane;
-    double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0, sj + 21 * lane, sh + 18 * lane)
-                       : 0.0;
-    r = wave_sum_d(r);
-    if (lane == 0) d.part[blockIdx.x] = r;
-    if (mode == 0) {
-        const int ne = min(EW, d.E - e0);
-        __syncthreads();
-        wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
-        wave_copy_out(d.hpl + 18 * (size_t)e0, sh, 18 * ne);
+    const int e0 = blockIdx.x * EW;
+    if (e0 < d.E) {
+        const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
+        const int lane = lane_id(), e = e0 + lane;
+        double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0, sj + 21 * lane,
+                                            sh + 18 * lane)
+                           : 0.0;
+        r = wave_sum_d(r);
+        if (lane == 0) d.part[blockIdx.x] = r;
+        if (mode == 0) {
+            const int ne = min(EW, d.E - e0);
+            __syncthreads();
+            wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
+            wave_copy_out(d.hpl + 18 * (size_t)e0, sh, 18 * ne);
+        }
+    }
+    if (mode == 1) {
+        // computeScale partials: block b < nbl sums x_j (lambda x_j + b_j) over the 64-chunks b, b + nbl, ... of x
+        const int nbl = max(1, (d.E + EW - 1) / EW);
+        if ((int)blockIdx.x < nbl) {
+            const double lambda = lm.lambda;
+            const int nx = 6 * d.Np + 3 * d.L;
+            double acc = 0.0;
+            for (int j = blockIdx.x * EW + lane_id(); j < nx; j += nbl * EW) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
+            acc = wave_sum_d(acc);
+            if (lane_id() == 0) d.part_s[blockIdx.x] = acc;
+        }
     }
 }
 
 // grid (ceil(L/64) + Np, Q) x 64: H_ll, b_l per point (edge order, one thread each) and H_pp, b_p per optimised pose
 // (one wave: lanes own strided edges, 27 register sums, fixed-order wave reduction)
-__global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
-    const Prob& d = probs[blockIdx.y];
-    const LM& lm = *d.lm;
-    if (lm.status || lm.done || !lm.need_lin) return;
+// returns this thread's max |diag| of the blocks it wrote (0 for none; fmax drops NaN as the reference's max does)
+__device__ double sys_body(const Prob& d) {
     const int nb_pts = (d.L + 63) / 64;
     if ((int)blockIdx.x < nb_pts) {
         const int h = blockIdx.x * 64 + threadIdx.x;
-        if (h >= d.L) return;
+        if (h >= d.L) return 0.0;
         double H[9] = {0}, bl[3] = {0};
         for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
             const double* j = d.jac + 21 * (size_t)d.pe_idx[s];
@@ -476,10 +493,10 @@ __global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
         }
         for (int k = 0; k < 9; k++) d.Hll[9 * (size_t)h + k] = H[k];
         for (int k = 0; k < 3; k++) d.b[6 * (size_t)d.Np + 3 * (size_t)h + k] = bl[k];
-        return;
+        return fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
     }
     const int h = blockIdx.x - nb_pts, lane = threadIdx.x;
-    if (h >= d.Np) return;
+    if (h >= d.Np) return 0.0;
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
@@ -499,23 +516,33 @@ __global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
     }
 #pragma unroll
     for (int k = 0; k < 27; k++) acc[k] = wave_sum_d(acc[k]);
+    double m = 0.0;
     if (lane == 0) {
         int q = 0;
         double* H = d.Hpp + 36 * (size_t)h;
         for (int a = 0; a < 6; a++)
-            for (int c = a; c < 6; c++) { H[6 * a + c] = acc[q]; H[6 * c + a] = acc[q]; q++; }
+            for (int c = a; c < 6; c++) {
+                H[6 * a + c] = acc[q];
+                H[6 * c + a] = acc[q];
+                if (c == a) m = fmax(m, fabs(acc[q]));
+                q++;
+            }
         for (int a = 0; a < 6; a++) d.b[6 * (size_t)h + a] = acc[21 + a];
     }
+    return m;
 }
 
-// fixed-order sum over a 256-thread block (strided per-thread sums, then a tree): the order k_reduce_chi used
+// Fixed-order sums over RED = 256 virtual threads (strided per-thread sums, then a tree), run by T real threads
+// (T = 256, or 64 in a fused tail): thread t plays virtual threads t, t + T, ...; the same additions in the same
+// order for every T, so a fused control step computes bit for bit what the one-workgroup kernel did.
 constexpr int RED = 256;
-__device__ double block_sum(double acc, double* s) {
-    const int t = threadIdx.x;
-    s[t] = acc;
+template <int T>
+__device__ double block_sum(const double* acc, double* s) {
+#pragma unroll
+    for (int v = 0; v < RED / T; v++) s[threadIdx.x + T * v] = acc[v];
     __syncthreads();
     for (int o = RED / 2; o > 0; o >>= 1) {
-        if (t < o) s[t] += s[t + o];
+        for (int t = threadIdx.x; t < o; t += T) s[t] += s[t + o];
         __syncthreads();
     }
     const double r = s[0];
@@ -523,16 +550,21 @@ __device__ double block_sum(double acc, double* s) {
     return r;
 }
 
+template <int T>
 __device__ double chi_of_parts(const Prob& d, double* s) {
     // parts of 64 edges, grouped by 256 as ((p0 + p1) + p2) + p3 (a missing part adds nothing), then strided + tree
-    double acc = 0.0;
+    double acc[RED / T];
     const int np = (d.E + EW - 1) / EW, nb = (d.E + 255) / 256;
-    for (int b = threadIdx.x; b < nb; b += RED) {
-        double g = d.part[4 * b];
-        for (int k = 1; k < 4; k++) g = g + (4 * b + k < np ? d.part[4 * b + k] : 0.0);
-        acc += g;
+#pragma unroll
+    for (int v = 0; v < RED / T; v++) {
+        acc[v] = 0.0;
+        for (int b = threadIdx.x + T * v; b < nb; b += RED) {
+            double g = d.part[4 * b];
+            for (int k = 1; k < 4; k++) g = g + (4 * b + k < np ? d.part[4 * b + k] : 0.0);
+            acc[v] += g;
+        }
     }
-    return block_sum(acc, s);
+    return block_sum<T>(acc, s);
 }
 
 // grid (Q) x 256: the initial activeRobustChi2 (optimize() entry)
@@ -541,7 +573,7 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
     const Prob& d = probs[blockIdx.x];
     LM& lm = *d.lm;
     if (lm.status) return;
-    const double chi = chi_of_parts(d, s);
+    const double chi = chi_of_parts<RED>(d, s);
     if (threadIdx.x == 0) {
         lm.initialChi = chi;
         lm.acceptedChi = chi;
@@ -557,25 +589,19 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
 
 // grid (Q) x 256: iteration start
 __global__ __launch_bounds__(RED) void k_ctl_begin(const Prob* __restrict__ probs) {
+    constexpr int T = RED;
     __shared__ double s[RED];
     const Prob& d = probs[blockIdx.x];
     LM& lm = *d.lm;
     if (lm.status || lm.done || !lm.need_lin) return;
-    const double chi = chi_of_parts(d, s);
-    double m = 0.0;
-    for (int i = threadIdx.x; i < 6 * d.Np; i += RED) m = fmax(m, fabs(d.Hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
-    for (int i = threadIdx.x; i < 3 * d.L; i += RED) m = fmax(m, fabs(d.Hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
-    s[threadIdx.x] = m;
-    __syncthreads();
-    for (int o = RED / 2; o > 0; o >>= 1) {
-        if (threadIdx.x < o) s[threadIdx.x] = fmax(s[threadIdx.x], s[threadIdx.x + o]);
-        __syncthreads();
-    }
+    const double chi = chi_of_parts<T>(d, s);
     if (threadIdx.x == 0) {
+        // max |diag(H)| gathered by k_sys's blocks (max is exact in any order), reset for the next iteration
+        const double maxdiag = __longlong_as_double((long long)atomicExch(&lm.maxdiag, 0ull));
         if (lm.its == 0) {
             // levenberg.cpp:71-77: lambda_0 = tau * max diag(H), tau = 1e-5 (computeLambdaInit :171-185)
             lm.currentChi = chi;
-            lm.lambda = 1e-5 * s[0];
+            lm.lambda = 1e-5 * maxdiag;
             lm.ni = 2.0;
             lm.nBad = 0;
         } else {
@@ -586,6 +612,17 @@ __global__ __launch_bounds__(RED) void k_ctl_begin(const Prob* __restrict__ prob
         lm.qmax = 0;
         lm.need_lin = 0;
     }
+}
+
+// grid (ceil(L/64) + Np, Q) x 64: the system (sys_body) and max |diag(H)| (one device atomic per wave)
+__global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done || !lm.need_lin) return;
+    double m = sys_body(d);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+    if (threadIdx.x == 0 && m > 0.0) atomicMax(&lm.maxdiag, (unsigned long long)__double_as_longlong(m));
 }
 
 // ---- Schur
@@ -844,28 +881,65 @@ __device__ __forceinline__ void ldlt_diag(double* A, int N, int kb, double* Y, d
     }
 }
 
-// One wave: the 16x16 block (br, bc) of A22 (block indices relative to row/col kb + NB) -= L21 W21^T as four
-// chained v_mfma_f64_16x16x4_f64 (K = 16), accumulator initialised with the A block. Lane maps (gfx950, f64):
-// A operand L[R0 + (lane&15)][k0 + (lane>>4)], B operand W[C0 + (lane&15)][k0 + (lane>>4)],
+// One wave: NT 16x16 blocks (br[t], bc[t]) of A22 (block indices relative to row/col kb + NB) -= L21 W21^T, each as
+// four chained v_mfma_f64_16x16x4_f64 (K = 16), accumulator initialised with the A block. The NT tiles' loads are
+// issued together, so their L2 round trips overlap (the update is latency-bound at one workgroup per problem).
+// Lane maps (gfx950, f64): A operand L[R0 + (lane&15)][k0 + (lane>>4)], B operand W[C0 + (lane&15)][k0 + (lane>>4)],
 // C/D col = lane&15, row = (lane>>4) + 4 reg.
 typedef double dbl4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void ldlt_tile16(double* A, int N, int kb, const double* PL, const double* PW, int m, int br,
-                                            int bc, int lane) {
-    const int R0 = kb + NB + 16 * br, C0 = kb + NB + 16 * bc;
+template <int NT>
+__device__ __forceinline__ void ldlt_tiles16(double* A, int N, int kb, const double* PL, const double* PW, int m,
+                                             const int* br, const int* bc, int lane) {
     const int col = lane & 15, rq = lane >> 4;
-    dbl4 c;
+    dbl4 c[NT];
 #pragma unroll
-    for (int r = 0; r < 4; r++) c[r] = A[(size_t)(R0 + rq + 4 * r) * N + C0 + col];
+    for (int u = 0; u < NT; u++) {
+        const int R0 = kb + NB + 16 * br[u], C0 = kb + NB + 16 * bc[u];
+#pragma unroll
+        for (int r = 0; r < 4; r++) c[u][r] = A[(size_t)(R0 + rq + 4 * r) * N + C0 + col];
+    }
 #pragma unroll
     for (int k0 = 0; k0 < NB; k0 += 4) {
         const int k = k0 + rq;
-        const double av = -PL[(size_t)k * m + 16 * br + col];
-        const double bv = PW[(size_t)k * m + 16 * bc + col];
-        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < NT; u++) {
+            const double av = -PL[(size_t)k * m + 16 * br[u] + col];
+            const double bv = PW[(size_t)k * m + 16 * bc[u] + col];
+            c[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c[u], 0, 0, 0);
+        }
     }
 #pragma unroll
-    for (int r = 0; r < 4; r++) A[(size_t)(R0 + rq + 4 * r) * N + C0 + col] = c[r];
+    for (int u = 0; u < NT; u++) {
+        const int R0 = kb + NB + 16 * br[u], C0 = kb + NB + 16 * bc[u];
+#pragma unroll
+        for (int r = 0; r < 4; r++) A[(size_t)(R0 + rq + 4 * r) * N + C0 + col] = c[u][r];
+    }
 }
+
+// A wave's queue of non-zero tiles, flushed LDLT_BATCH at a time (wave-uniform: the tile ids and the tile mask are
+// the same in every lane)
+#ifndef MAM_LDLT_BATCH
+#define MAM_LDLT_BATCH 4
+#endif
+constexpr int LDLT_BATCH = MAM_LDLT_BATCH;
+struct TileQueue {
+    int br[LDLT_BATCH], bc[LDLT_BATCH];
+    int n = 0;
+    __device__ __forceinline__ void push(double* A, int N, int kb, const double* PL, const double* PW, int m, int r,
+                                         int c, int lane) {
+        br[n] = r;
+        bc[n] = c;
+        if (++n == LDLT_BATCH) {
+            ldlt_tiles16<LDLT_BATCH>(A, N, kb, PL, PW, m, br, bc, lane);
+            n = 0;
+        }
+    }
+    __device__ __forceinline__ void flush(double* A, int N, int kb, const double* PL, const double* PW, int m,
+                                          int lane) {
+        for (int u = 0; u < n; u++) ldlt_tiles16<1>(A, N, kb, PL, PW, m, br + u, bc + u, lane);
+        n = 0;
+    }
+};
 
 // triangle index q -> (tr, tc), tc <= tr
 __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
@@ -875,6 +949,23 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
     *tr = r;
     *tc = q - r * (r + 1) / 2;
 }
+
+#ifdef MAM_LDLT_PROFILE
+// cycles per phase summed over workgroups (thread 0 after each barrier): init, B, C1, C2, solve, diag (wave 0), -, WGs
+__device__ unsigned long long g_lprof[8];
+#define LPROF(k)                                                                     \
+    do {                                                                             \
+        if (t == 0) {                                                                \
+            const long long tn = clock64();                                          \
+            atomicAdd(&g_lprof[k], (unsigned long long)(tn - lp0));                  \
+            lp0 = tn;                                                                \
+        }                                                                            \
+    } while (0)
+#else
+#define LPROF(k) \
+    do {         \
+    } while (0)
+#endif
 
 // grid (Q): with lookahead — after a panel's rows (B), the next block column is updated first (C1); then wave 0
 // factors the next diagonal block while the other waves update the rest of the trailing matrix (C2).
@@ -897,6 +988,9 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
     __shared__ double dk[NB];
     __shared__ double invdk[NB];
     __shared__ int fail;
+#ifdef MAM_LDLT_PROFILE
+    long long lp0 = clock64();
+#endif
     if (t == 0) fail = 0;
     for (int i = t; i < N; i += LDLT_THREADS) {
         Y[i] = i < n ? d.bs[i] : 0.0;
@@ -905,6 +999,7 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
     __syncthreads();
     if (wid == 0) ldlt_diag(A, N, 0, Y, Ld, dk, invdk, &fail, lane);
     __syncthreads();
+    LPROF(0);
     for (int kb = 0; kb < N; kb += NB) {
         // (B) panel rows: L21 = A21 L11^-T D^-1, W21 = L21 D (staged transposed), y2 -= L21 y1
         const int m = N - kb - NB;
@@ -936,27 +1031,42 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
             Y[i] = yi;
         }
         __syncthreads();
+        LPROF(1);
         if (m == 0) break;
         const int T16 = m / 16;
         // (C1) the next block column: blocks (br, 0), one wave each
         const bool c1nz = tcol[(size_t)(kc + 1) * d.nt] != 0;
-        for (int br = wid; br < T16; br += LDLT_THREADS / 64)
-            if (c1nz && tcol[(size_t)(kc + 1 + br) * d.nt]) ldlt_tile16(A, N, kb, PL, PW, m, br, 0, lane);
+        if (c1nz) {
+            TileQueue tq;
+            for (int br = wid; br < T16; br += LDLT_THREADS / 64)
+                if (tcol[(size_t)(kc + 1 + br) * d.nt]) tq.push(A, N, kb, PL, PW, m, br, 0, lane);
+            tq.flush(A, N, kb, PL, PW, m, lane);
+        }
         __syncthreads();
+        LPROF(2);
         // (C2) wave 0 factors the next diagonal block; the other waves update the blocks with bc >= 1
         if (wid == 0) {
+#ifdef MAM_LDLT_PROFILE
+            const long long td = clock64();
+#endif
             ldlt_diag(A, N, kb + NB, Y, Ld, dk, invdk, &fail, lane);
+#ifdef MAM_LDLT_PROFILE
+            if (lane == 0) atomicAdd(&g_lprof[5], (unsigned long long)(clock64() - td));
+#endif
         } else {
             const int T2 = T16 - 1;
             const int n2 = T2 * (T2 + 1) / 2;
+            TileQueue tq;
             for (int q = wid - 1; q < n2; q += LDLT_THREADS / 64 - 1) {
                 int tr, tc;
                 tri_index(q, &tr, &tc);
                 if (tcol[(size_t)(kc + 2 + tr) * d.nt] && tcol[(size_t)(kc + 2 + tc) * d.nt])
-                    ldlt_tile16(A, N, kb, PL, PW, m, tr + 1, tc + 1, lane);
+                    tq.push(A, N, kb, PL, PW, m, tr + 1, tc + 1, lane);
             }
+            tq.flush(A, N, kb, PL, PW, m, lane);
         }
         __syncthreads();
+        LPROF(3);
     }
     if (t == 0) lm.fail = fail;
     if (fail) return;   // uniform (LDS flag after the last barrier)
@@ -988,6 +1098,10 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
         __syncthreads();
     }
     for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+    LPROF(4);
+#ifdef MAM_LDLT_PROFILE
+    if (t == 0) atomicAdd(&g_lprof[7], 1ull);
+#endif
 }
 
 // Eigen Quaterniond(Matrix3d)
@@ -1100,17 +1214,22 @@ __global__ __launch_bounds__(256) void k_backsub_update(const Prob* __restrict__
 // grid (Q) x 256: end of a trial — levenberg.cpp:108-158 (rho, accept / reject, lambda), then the iteration-end
 // tests of levenberg.cpp:159-168 and sparse_optimizer.cpp:381-409.
 __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs) {
+    constexpr int T = RED;
     __shared__ double s[RED];
     const Prob& d = probs[blockIdx.x];
     LM& lm = *d.lm;
     if (lm.status || lm.done) return;
     const double lambda = lm.lambda;
-    double tempChi = chi_of_parts(d, s);
+    double tempChi = chi_of_parts<T>(d, s);
     // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194)
-    double acc = 0.0;
-    const int nx = 6 * d.Np + 3 * d.L;
-    for (int j = threadIdx.x; j < nx; j += RED) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
-    const double scale0 = block_sum(acc, s);
+    double acc[RED / T];
+    const int nbl = max(1, (d.E + EW - 1) / EW);
+#pragma unroll
+    for (int v = 0; v < RED / T; v++) {
+        acc[v] = 0.0;
+        for (int j = threadIdx.x + T * v; j < nbl; j += RED) acc[v] += d.part_s[j];
+    }
+    const double scale0 = block_sum<T>(acc, s);
     if (threadIdx.x != 0) return;
     if (lm.fail) tempChi = DBL_MAX;
     double rho = lm.currentChi - tempChi;
@@ -1228,6 +1347,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.err = cv.take<double>(2 * (size_t)d.E);
     d.jac = cv.take<double>(21 * (size_t)d.E);
     d.part = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
+    d.part_s = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
     d.hpl = cv.take<double>(18 * (size_t)d.E);
     d.bdinv = cv.take<double>(18 * (size_t)d.E);
     d.coef = cv.take<double>(6 * (size_t)d.E);
@@ -1452,6 +1572,15 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         max_trials = std::max(max_trials, lh[q].trials);
     }
     if (!was_stopped) c->trials_ema = 0.75 * c->trials_ema + 0.25 * std::max(1, max_trials);
+#ifdef MAM_LDLT_PROFILE
+    {
+        unsigned long long h[8];
+        MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::lba::g_lprof), sizeof(h)));
+        const double w = (double)std::max(1ull, h[7]);
+        fprintf(stderr, "ldlt cycles per WG: init %.0f B %.0f C1 %.0f C2 %.0f solve %.0f diag(w0) %.0f; WGs %llu\n",
+                h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7]);
+    }
+#endif
     return MAM_OK;
 }
 

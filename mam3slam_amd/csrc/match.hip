@@ -1083,51 +1083,82 @@ __global__ __launch_bounds__(256) void k_tri_pair_geom(TriBatchArgs a) {
     cam::pair_geometry(t1.q, t1.t, t2.q, t2.t, a.cam, a.cam, &a.pg[q]);
 }
 
-// grid (ceil(kp_stride / 4), npairs) x 64: 16 lanes per idx1 of kf1 (four per wave): its node's features in kf2 found
-// by binary search in kf2's sorted FeatureVector keys, the candidates dealt to the lanes, (dist, last position)
-// argmin over the lanes = "dist <= bestDist, last equal wins" (ORBmatcher.cc:1015-1074)
-__global__ __launch_bounds__(64) void k_tri_batch(TriBatchArgs a) {
-    const int q = blockIdx.y;
+// grid (npairs) x 512, one workgroup per pair (the pairs of one kf1 on one XCD: kf1's keys, descriptors and sorted
+// FeatureVector stay in its L2). kf2's sorted FeatureVector keys are staged in LDS; the 32 groups of 16 lanes take
+// contiguous ranges of kf1's sorted FeatureVector (node by node, in the order ORBmatcher.cc:974-1074 walks the two
+// FeatureVectors) and look each new node up in kf2's keys by a binary search in LDS. Per idx1 the node's kf2
+// candidates are dealt to the 16 lanes; (dist, last position) argmin over the lanes = "dist <= bestDist, last equal
+// wins". Then, in the same workgroup, nmatches and the rotation-histogram filter when check_ori
+// (ORBmatcher.cc:1114-1133).
+constexpr int TRI_THREADS = 1024;
+__global__ __launch_bounds__(TRI_THREADS) void k_tri_pair(TriBatchArgs a) {
+    extern __shared__ unsigned long long sk2[];   // [skey_stride] kf2's sorted keys, then kf2's has_mp bytes
+    __shared__ int hist[MAM_HISTO_LENGTH];
+    __shared__ int top[3];
+    __shared__ int red[TRI_THREADS / 64];
+    const int q = xcd_logical(blockIdx.x, gridDim.x);
     const int k1 = a.pairs[2 * q], k2 = a.pairs[2 * q + 1];
-    const int sub = lane_id() & 15;
-    const int idx1 = blockIdx.x * 4 + (lane_id() >> 4);
+    const int S = a.kfs.kp_stride, tid = threadIdx.x;
     const int n1 = frame_n(a.kfs, k1);
-    const int S = a.kfs.kp_stride;
-    int32_t* out = a.out + (size_t)q * S;
-    if (idx1 >= S) return;
+    const int nfv1 = a.nfv[k1], nfv2 = a.nfv[k2];
     const size_t b1 = (size_t)k1 * S, b2 = (size_t)k2 * S;
-    bool active = idx1 < n1 && a.weight[b1 + idx1] > 0.0 && !a.has_mp[b1 + idx1];
-    unsigned best = 0xFFFFFFFFu;
-    if (active) {
-        const cam::PairGeom& G = a.pg[q];
+    int32_t* out = a.out + (size_t)q * S;
+    const unsigned long long* sk1 = a.skey + (size_t)k1 * a.skey_stride;
+    uint8_t* has2 = reinterpret_cast<uint8_t*>(sk2 + a.skey_stride);
+    for (int i = tid; i < nfv2; i += TRI_THREADS) sk2[i] = a.skey[(size_t)k2 * a.skey_stride + i];
+    for (int i = tid; i < S; i += TRI_THREADS) has2[i] = a.has_mp[b2 + i];
+    for (int i = tid; i < S; i += TRI_THREADS) out[i] = -1;
+    if (tid < MAM_HISTO_LENGTH) hist[tid] = 0;
+    __syncthreads();
+    const cam::PairGeom& G = a.pg[q];
+    const bool kb8 = a.cam.model == MAM_CAM_KANNALA_BRANDT8;
+    const int grp = tid >> 4, sub = tid & 15, ngrp = TRI_THREADS / 16;
+    const int per = (nfv1 + ngrp - 1) / ngrp;
+    const int p0 = grp * per, p1 = min(nfv1, p0 + per);
+    unsigned cur = 0xFFFFFFFFu;
+    int b = 0, e = 0;
+    // one position ahead: its key and has_mp are in flight while the current position's candidates are scored
+    unsigned long long kn = p0 < p1 ? sk1[p0] : 0ull;
+    uint8_t hn = p0 < p1 ? a.has_mp[b1 + (kn & 0xFFFFFFFFull)] : 1;
+    for (int p = p0; p < p1; p++) {
+        const unsigned long long k = kn;
+        const uint8_t has1 = hn;
+        if (p + 1 < p1) {
+            kn = sk1[p + 1];
+            hn = a.has_mp[b1 + (kn & 0xFFFFFFFFull)];
+        }
+        const unsigned nid = (unsigned)(k >> 32);
+        const int idx1 = (int)(k & 0xFFFFFFFFull);
+        if (nid != cur) {   // kf2's features of the node: [b, e) of its sorted keys
+            cur = nid;
+            const unsigned long long key = (unsigned long long)nid << 32;
+            int lo = 0, hi = nfv2;
+            while (lo < hi) {
+                const int m = (lo + hi) >> 1;
+                if (sk2[m] < key) lo = m + 1;
+                else hi = m;
+            }
+            b = lo;
+            hi = nfv2;
+            while (lo < hi) {
+                const int m = (lo + hi) >> 1;
+                if (sk2[m] <= (key | 0xFFFFFFFFull)) lo = m + 1;
+                else hi = m;
+            }
+            e = lo;
+        }
+        if (b == e || has1) continue;   // uniform over the group
         const mam_keypoint kp1 = a.kfs.keys[b1 + idx1];
         const uint8_t* d1 = a.kfs.desc + (b1 + idx1) * 32;
-        const unsigned long long key = (unsigned long long)a.nid[b1 + idx1] << 32;
-        const unsigned long long* sk = a.skey + (size_t)k2 * a.skey_stride;
-        // [b, e): kf2's features of the node
-        int lo = 0, hi = a.nfv[k2];
-        while (lo < hi) {
-            const int m = (lo + hi) >> 1;
-            if (sk[m] < key) lo = m + 1;
-            else hi = m;
-        }
-        const int b = lo;
-        hi = a.nfv[k2];
-        while (lo < hi) {
-            const int m = (lo + hi) >> 1;
-            if (sk[m] <= (key | 0xFFFFFFFFull)) lo = m + 1;
-            else hi = m;
-        }
-        const int e = lo;
         const float la = kp1.x * G.F12[0] + kp1.y * G.F12[3] + G.F12[6];
         const float lb = kp1.x * G.F12[1] + kp1.y * G.F12[4] + G.F12[7];
         const float lc = kp1.x * G.F12[2] + kp1.y * G.F12[5] + G.F12[8];
         float r1[3] = {0.0f, 0.0f, 1.0f};
-        const bool kb8 = a.cam.model == MAM_CAM_KANNALA_BRANDT8;
         if (kb8 && !a.coarse) cam::kb8_unproject_f(a.cam, kp1.x, kp1.y, r1);
+        unsigned best = 0xFFFFFFFFu;
         for (int i2 = b + sub; i2 < e; i2 += 16) {
-            const int idx2 = (int)(sk[i2] & 0xFFFFFFFFull);
-            if (a.has_mp[b2 + idx2]) continue;
+            const int idx2 = (int)(sk2[i2] & 0xFFFFFFFFull);
+            if (has2[idx2]) continue;
             const int dist = desc_dist(d1, a.kfs.desc + (b2 + idx2) * 32);
             if (dist > MAM_TH_LOW) continue;
             const mam_keypoint kp2 = a.kfs.keys[b2 + idx2];
@@ -1151,30 +1182,13 @@ __global__ __launch_bounds__(64) void k_tri_batch(TriBatchArgs a) {
             if (ok) best = min(best, ((unsigned)dist << 16) | (0xFFFFu - (unsigned)(i2 - b)));
         }
         for (int o = 8; o > 0; o >>= 1) best = min(best, (unsigned)__shfl_xor((int)best, o, 16));
-        if (sub == 0)
-            out[idx1] = best != 0xFFFFFFFFu ? (int)(sk[b + (int)(0xFFFFu - (best & 0xFFFFu))] & 0xFFFFFFFFull) : -1;
-    } else if (sub == 0) {
-        out[idx1] = -1;
+        if (sub == 0 && best != 0xFFFFFFFFu) out[idx1] = (int)(sk2[b + (int)(0xFFFFu - (best & 0xFFFFu))] & 0xFFFFFFFFull);
     }
-}
-
-// grid (npairs) x 256: nmatches per pair, with the rotation-histogram filter when check_ori (ORBmatcher.cc:1114-1133)
-__global__ __launch_bounds__(256) void k_tri_batch_rot(TriBatchArgs a) {
-    const int q = blockIdx.x;
-    const int k1 = a.pairs[2 * q], k2 = a.pairs[2 * q + 1];
-    const int S = a.kfs.kp_stride;
-    const int n1 = frame_n(a.kfs, k1);
-    const mam_keypoint* keys1 = a.kfs.keys + (size_t)k1 * S;
-    const mam_keypoint* keys2 = a.kfs.keys + (size_t)k2 * S;
-    int32_t* out = a.out + (size_t)q * S;
-    __shared__ int hist[MAM_HISTO_LENGTH];
-    __shared__ int top[3];
-    __shared__ int red[4];
-    const int tid = threadIdx.x;
-    if (tid < MAM_HISTO_LENGTH) hist[tid] = 0;
     __syncthreads();
+    const mam_keypoint* keys1 = a.kfs.keys + b1;
+    const mam_keypoint* keys2 = a.kfs.keys + b2;
     int cnt = 0;
-    for (int i = tid; i < n1; i += 256) {
+    for (int i = tid; i < n1; i += TRI_THREADS) {
         if (out[i] >= 0) {
             cnt++;
             if (a.check_ori) atomicAdd(&hist[rot_bin(keys1[i].angle - keys2[out[i]].angle)], 1);
@@ -1195,7 +1209,7 @@ __global__ __launch_bounds__(256) void k_tri_batch_rot(TriBatchArgs a) {
             top[0] = ind1; top[1] = ind2; top[2] = ind3;
         }
         __syncthreads();
-        for (int i = tid; i < n1; i += 256) {
+        for (int i = tid; i < n1; i += TRI_THREADS) {
             if (out[i] >= 0) {
                 const int bin = rot_bin(keys1[i].angle - keys2[out[i]].angle);
                 if (bin != top[0] && bin != top[1] && bin != top[2]) { out[i] = -1; cnt--; }
@@ -1205,7 +1219,11 @@ __global__ __launch_bounds__(256) void k_tri_batch_rot(TriBatchArgs a) {
     cnt = wave_sum(cnt);
     if (lane_id() == 0) red[tid >> 6] = cnt;
     __syncthreads();
-    if (tid == 0) a.out_n[q] = red[0] + red[1] + red[2] + red[3];
+    if (tid == 0) {
+        int t = 0;
+        for (int w = 0; w < TRI_THREADS / 64; w++) t += red[w];
+        a.out_n[q] = t;
+    }
 }
 
 __global__ void k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out) {
@@ -2093,8 +2111,16 @@ int mam_search_for_triangulation_batch_device(mam_match_ctx* c, const mam_frame_
         mam::StageTimer::Scope sc(&c->timer, s, 3);
         hipLaunchKernelGGL(mam::k_tri_fv_sort, dim3(nkf), dim3(1024), sizeof(unsigned long long) * P, s, a);
         hipLaunchKernelGGL(mam::k_tri_pair_geom, dim3((b->npairs + 255) / 256), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(mam::k_tri_batch, dim3((S + 3) / 4, b->npairs), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(mam::k_tri_batch_rot, dim3(b->npairs), dim3(256), 0, s, a);
+        const size_t lds_pair = sizeof(unsigned long long) * P + (size_t)S;
+        if (lds_pair > 65536 &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_tri_pair),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pair) != hipSuccess) {
+            (void)hipGetLastError();
+            mam::set_last_error("k_tri_pair: LDS request above the device limit");
+            return MAM_ERR_CAPACITY;
+        }
+        hipLaunchKernelGGL(mam::k_tri_pair, dim3(b->npairs), dim3(mam::TRI_THREADS),
+                           sizeof(unsigned long long) * P + (size_t)S, s, a);
     }
     MAM_HIP(hipGetLastError());
     return MAM_OK;

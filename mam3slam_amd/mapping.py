@@ -208,6 +208,9 @@ class NewMapPointsLeg:
         self.matcher = ORBmatcher(0.6, False, device=device.index or 0)
         self.head = 0
         self.ready = {h: torch.cuda.Event() for h in range(0, self.R, self.W)}
+        # completion of the search run at each head (None until one was issued there)
+        self.done = {h: None for h in range(0, self.R, self.W)}
+        self.stream = torch.cuda.Stream(device, priority=-1)
         # pairs for each head position: new slot j = head + i searches the NN slots inserted before it
         self.pairs = {}
         for head in range(0, R, self.W):
@@ -241,10 +244,14 @@ class NewMapPointsLeg:
 
         tr, W, R = self.tr, self.W, self.R
         K = max(1, tr.B // W)
-        head = (self.head + W) % R
+        head = (self.head + W) % R   # the run at self.head was launched right after its ingest
         fr = (torch.arange(W, device=self.dev) * K + step % K) % tr.B
         sl = slice(head, head + W)
+        # the latest search that read these slots is the one two heads back (R >= 2 W + NN): it must be done
+        prev = self.done[(head - 2 * W) % R]
         with torch.cuda.stream(tr.tstream):
+            if prev is not None:
+                tr.tstream.wait_event(prev)
             self.keys[sl] = tr.d_kps[fr]
             self.desc[sl] = tr.d_desc[fr]
             self.cnt[sl] = tr.d_cnt[fr]
@@ -259,6 +266,22 @@ class NewMapPointsLeg:
         by the thread that starts the run, so a run never sees a later ingest."""
         h, self.pending = self.pending, None
         return h
+
+    def launch(self, head):
+        """Start the run of the keyframes ingested at `head` on this leg's own stream as soon as they are ingested (a
+        search of one step's keyframes overlaps the LocalBundleAdjustment of the previous step's: different agents'
+        keyframes, as with the reference's per-agent LocalMapping threads); `wait(stream, head)` orders a consumer of
+        the same keyframes after it."""
+        import torch
+
+        self.run(self.stream, head)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        self.done[head] = ev
+
+    def wait(self, stream, head):
+        if head is not None and self.done[head] is not None:
+            stream.wait_event(self.done[head])
 
     def run(self, stream, head):
         """ComputeBoW of the new keyframes at `head` + their W x 30 SearchForTriangulation, asynchronous on
