@@ -46,9 +46,12 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFS = 78.6    # MI355X FP64 vector / matrix (spec)
 # what limits each stage; the byte/integer path has no MFMA work
 ROOFLINE_NOTES = {
-    "fast": "VALU issue: FAST-9 strength is 69 packed-f16 min3/max3 ops per pixel pair (DESIGN.md §3)",
+    "fast": ("latency / issue: per 64-frame launch VALU busy 11%, 33% of wave cycles waiting (s_waitcnt, barriers) and "
+             "37% issue-stalled; FETCH_SIZE 28 MB raw = algorithmic after the XCD-aware cell order "
+             "(profiles/r02/pmc_c1_tracking.json)"),
     "pyramid": "bilinear resize, latency-bound at 7 dependent launches",
-    "describe": "one wave per keypoint: IC-angle loads + the 37x37 blurred patch in LDS, two dependent round trips",
+    "describe": ("one wave per keypoint: IC-angle loads + the 37x37 blurred patch in LDS, two dependent round trips; "
+                 "57% of wave cycles waiting, VALU busy 9% (profiles/r02/pmc_c1_tracking.json)"),
     "resolve": "one workgroup per frame, greedy dependency rounds (latency, LDS atomics)",
 }
 
@@ -662,13 +665,14 @@ def main():
     launches_per_step = launches / args.steps
     bytes_per_launch = sb[dom] * B / launches_per_step
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = traffic_raw = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath):   # PMC passes of the same launches (scripts/gpu_fast_pmc.sh)
         try:
-            traffic = json.load(open(tpath)).get(dom)
+            tj = json.load(open(tpath))
+            traffic, traffic_raw = tj.get(dom), tj.get("raw", {}).get(dom)
         except Exception:
-            traffic = None
+            traffic = traffic_raw = None
 
     if rank == 0:
         W, H, NF = tr.W, tr.H, tr.NF
@@ -708,6 +712,7 @@ def main():
             "stage_ms_per_step": per_step_ms,
             "roofline": {"bound": "hbm", "kernel": dom, "limiter": ROOFLINE_NOTES.get(dom), "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_raw_fetch": traffic_raw,
                          "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms},
         }
         if lat is not None:

@@ -54,6 +54,11 @@ public:
     /* Optimizer.cc:1118-1180 + vertex/edge setup :1212-1394. Returns false where the reference returns before
      * optimizing because no keyframe is fixed (:1182-1186). */
     static bool BuildLocalBAWindow(KeyFrame* pKF, Map* pMap, LocalBAWindow& w);
+    /* Optimizer.cc:1413-1497, the part of LocalBundleAdjustment after the solve: erase the observations of edges with
+     * chi2 > 5.991 or a non-positive depth, then under Map::mMutexMapUpdate write the local keyframes' poses (q / t
+     * per pose of w.vpKF, local ones first) and the local points (x per point of w.vpMP) back. */
+    static void ApplyLocalBAResult(const LocalBAWindow& w, Map* pMap, const double* q, const double* t,
+                                   const double* x, const double* chi2, const uint8_t* depth);
 
     /* The merge-window (welding) LocalBundleAdjustment, Optimizer.cc:3505-3952 (used when maps are merged,
      * LoopClosing.cc:2670): vpFixedKF fixed, vpAdjustKF optimised, their MapPoints; optimize(5) with Huber

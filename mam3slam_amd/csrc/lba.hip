@@ -1437,6 +1437,26 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         max_lds = std::max(max_lds, ldlt_lds_bytes(d.npad));
     }
     if (max_lds > c->ldlt_lds_budget) lds_ok = false;
+    // size bounds before any allocation: the dense pose x landmark edge table (Np L int32) and S (npad^2 f64) of one
+    // problem stay under 4 GiB each, and the batch's scratch fits the device's free memory
+    for (auto& d : hp) {
+        const double eidx_b = 4.0 * d.Np * (double)d.L, s_b = 8.0 * d.npad * (double)d.npad;
+        if (eidx_b > 4294967296.0 || s_b > 4294967296.0) {
+            mam::set_last_error("LBA problem too large for the dense solve: " + std::to_string(d.Np) +
+                                " optimised poses x " + std::to_string(d.L) + " points (pose x landmark table " +
+                                std::to_string((long long)(eidx_b / 1048576)) + " MiB, S " +
+                                std::to_string((long long)(s_b / 1048576)) + " MiB; bound 4096 MiB each)");
+            return MAM_ERR_CAPACITY;
+        }
+    }
+    if (bytes + kAlign > c->arena.n) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && bytes + kAlign > free_b + c->arena.n) {
+            mam::set_last_error("LBA batch scratch of " + std::to_string(bytes >> 20) + " MiB exceeds the device's free " +
+                                std::to_string(free_b >> 20) + " MiB");
+            return MAM_ERR_CAPACITY;
+        }
+    }
     if (int rc = c->arena.alloc(bytes + kAlign)) return rc;
     if (int rc = c->probs.alloc(Q)) return rc;
     if (int rc = c->lms.alloc(Q)) return rc;

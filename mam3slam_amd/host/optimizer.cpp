@@ -243,6 +243,11 @@ void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap
     const int rc = mam_lba_solve(lbaCtx(), &prob, reinterpret_cast<const volatile uint8_t*>(pbStopFlag), &res);
     if (rc < 0) throw std::runtime_error(std::string("mam_lba_solve failed: ") + mam_last_error());
 
+    ApplyLocalBAResult(w, pMap, q.data(), t.data(), x.data(), chi2.data(), depth.data());
+}
+
+void Optimizer::ApplyLocalBAResult(const LocalBAWindow& w, Map* pMap, const double* q, const double* t,
+                                   const double* x, const double* chi2, const uint8_t* depth) {
     // Check inlier observations (:1413-1430)
     std::vector<std::pair<KeyFrame*, MapPoint*>> vToErase;
     vToErase.reserve(w.edge_point.size());

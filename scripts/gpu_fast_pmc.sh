@@ -13,4 +13,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$T -o run -
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/pmcf_$T -o run -- python3 $R/bench.py $A > $O/pmcf_$T.log 2>&1 || { tail -5 $O/pmcf_$T.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/pmcw_$T -o run -- python3 $R/bench.py $A > $O/pmcw_$T.log 2>&1 || { tail -5 $O/pmcw_$T.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -f csv -d $O/pmcs_$T -o run -- python3 $R/bench.py $A > $O/pmcs_$T.log 2>&1 || { tail -5 $O/pmcs_$T.log; exit 1; }
-python3 $R/scripts/pmc_summary.py $O/prof_$T $O/pmcf_$T $O/pmcw_$T $O/pmcs_$T > $O/pmc_$T.json && cat $O/pmc_$T.json
+python3 $R/scripts/pmc_summary.py $O/prof_$T $O/pmcf_$T $O/pmcw_$T $O/pmcs_$T --traffic $O/traffic_$CFG.json > $O/pmc_$T.json && cat $O/pmc_$T.json

@@ -1,10 +1,10 @@
 """Per-kernel PMC summary of rocprofv3 CSV runs (the kernel trace and the counter passes of scripts/gpu_fast_pmc.sh):
 
-    python scripts/pmc_summary.py <trace_dir> <fetch_dir> <write_dir> <sq_dir>
+    python scripts/pmc_summary.py <trace_dir> <fetch_dir> <write_dir> <sq_dir> [--traffic <profiles/traffic_cN.json>]
 
 For each kernel: mean duration (kernel trace), FETCH_SIZE / WRITE_SIZE per launch (raw KB; `hbm_bytes` applies the
 gfx950 x2 FETCH correction of MI355X_MICROARCH.md §HBM for wide coalesced reads — an upper bound for narrower loads,
-the raw value the lower), and from the SQ pass: VALU busy = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE)
+the raw value the lower; --traffic writes both per bench.py stage for roofline.traffic), and from the SQ pass: VALU busy = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE)
 (the gfx94x VALUBusy formula; SQ_* count quad-cycles), the fraction of wave cycles issuing VALU, waiting (s_waitcnt /
 barrier) and stalled on issue, and VALU / LDS instructions per wave.
 """
@@ -41,8 +41,34 @@ def short(name):
     return n.split("(")[0]
 
 
+# bench.py stage -> kernel (the stages that are one kernel launch)
+STAGES = {"pyramid": "mam::k_pyr_flat", "fast": "mam::k_fast_cells", "blur": "mam::k_blur7",
+          "distribute": "mam::k_distribute", "describe": "mam::k_describe", "grid": "mam::k_grid",
+          "gather": "mam::k_gather", "resolve": "mam::k_resolve", "frustum": "mam::k_frustum"}
+
+
+def write_traffic(out, path):
+    t = {"_note": "HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (separate rocprofv3 passes, KB): stage values "
+                  "apply the gfx950 x2 FETCH_SIZE correction of MI355X_MICROARCH.md (exact for wide coalesced reads, "
+                  "an upper bound for narrower loads); 'raw' holds the uncorrected lower bound",
+         "raw": {}}
+    for stage, kern in STAGES.items():
+        for name, e in out.items():
+            if name.startswith(kern) and "hbm_bytes_x2fetch" in e:
+                t[stage] = e["hbm_bytes_x2fetch"]
+                t["raw"][stage] = e["hbm_bytes_raw"]
+    with open(path, "w") as f:
+        json.dump(t, f, indent=1)
+
+
 def main():
-    tr, fe, wr, sq = trace(sys.argv[1]), counters(sys.argv[2]), counters(sys.argv[3]), counters(sys.argv[4])
+    args = sys.argv[1:]
+    tpath = None
+    if "--traffic" in args:
+        i = args.index("--traffic")
+        tpath = args[i + 1]
+        args = args[:i] + args[i + 2:]
+    tr, fe, wr, sq = trace(args[0]), counters(args[1]), counters(args[2]), counters(args[3])
     out = {}
     for k in sorted(set(fe) | set(wr) | set(sq)):
         name = short(k)
@@ -72,6 +98,8 @@ def main():
             e["insts_valu"] = s.get("SQ_INSTS_VALU")
             e["insts_lds"] = s.get("SQ_INSTS_LDS")
     print(json.dumps(out, indent=1))
+    if tpath:
+        write_traffic(out, tpath)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,9 @@
 // Tests of the C++ host API (include/mam3slam/*.h): the reference-signature wrappers over the C-ABI.
 //
 //   test_host_api cpu   host logic only (no device calls): Sophus-equivalent algebra, MapPoint observation
-//                       bookkeeping, the LocalBundleAdjustment window build (Optimizer.cc:1118-1394).
+//                       bookkeeping, the LocalBundleAdjustment window build (Optimizer.cc:1118-1394), and a
+//                       Tracking thread reading the map while a LocalMapping thread builds windows and writes
+//                       results back (run under ASan / UBSan and TSan builds by tests/test_host_api.py).
 //   test_host_api gpu   the wrappers end to end on the GPU vs the CPU oracle (liboracle.so, test
 //                       infrastructure): ORBextractor bit-exact, both SearchByProjection and
 //                       SearchForTriangulation index-exact with the reference's side effects on mvpMapPoints,
@@ -14,11 +16,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <array>
+#include <atomic>
 #include <cstring>
 #include <fstream>
 #include <memory>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mam3slam/ORBextractor.h"
@@ -277,6 +281,72 @@ static void testWindow() {
     S2.resetMarks();
     Optimizer::LocalBundleAdjustment(p2, nullptr, &other, nf, no, nm, ne);
     CHECK(nf == 0 && no == -1 && nm == -7 && ne == -1, "early return leaves outputs: %d %d %d %d", nf, no, nm, ne);
+}
+
+// Tracking and LocalMapping on one map from two threads, host side only: the Tracking thread reads every MapPoint
+// (position, descriptor, isBad, observation count — SearchLocalPoints / the motion model's host work) and bumps
+// Visible / Found, reads keyframe poses; the LocalMapping thread builds LocalBundleAdjustment windows for every
+// keyframe and applies a synthetic solution (Optimizer::ApplyLocalBAResult: outlier erase + write-back under
+// mMutexMapUpdate). Under TSan any unsynchronised access of the two is reported.
+static void testConcurrentHost() {
+    const int NK = 16;
+    Scene S(NK, 800, 4, 91, 0.1f);
+    for (int k = 0; k < NK; k++) {
+        std::vector<KeyFrame*> cov;
+        for (int d = 1; d <= 3; d++) {
+            if (k - d >= 0) cov.push_back(S.kfs[k - d].get());
+            if (k + d < NK) cov.push_back(S.kfs[k + d].get());
+        }
+        S.kfs[k]->SetVectorCovisibleKeyFrames(cov);
+    }
+    std::atomic<bool> stop{false};
+    std::atomic<long> tracked{0};
+    std::thread tracking([&] {
+        Frame F = emptyFrame((int)S.mps.size(), 640, 480, S.scales, S.sig2, &S.cam);
+        for (size_t i = 0; i < S.mps.size(); i++) F.mvpMapPoints[i] = S.mps[i].get();
+        long it = 0;
+        do {
+            double acc = 0.0;
+            for (MapPoint* pMP : F.mvpMapPoints) {
+                if (!pMP || pMP->isBad()) continue;
+                float X[3];
+                uint8_t d[32];
+                pMP->GetWorldPos(X);
+                pMP->GetDescriptor(d);
+                pMP->IncreaseVisible();
+                if (d[0] & 1) pMP->IncreaseFound();
+                acc += X[2] + pMP->Observations();
+            }
+            for (auto& k : S.kfs) acc += k->GetPose().t[0];
+            F.SetPose(S.kfs[it % NK]->GetPose());
+            CHECK(std::isfinite(acc), "tracking read a non-finite value");
+            it++;
+            tracked.store(it);
+        } while (!stop.load());
+    });
+    int windows = 0;
+    for (int round = 0; round < 3; round++) {
+        S.resetMarks();
+        for (int k = 1; k < NK; k++) {
+            LocalBAWindow w;
+            if (!Optimizer::BuildLocalBAWindow(S.kfs[k].get(), &S.map, w)) continue;
+            std::vector<double> q(w.pose_q), t(w.pose_t), x(w.point_xyz), chi2(w.edge_point.size());
+            std::vector<uint8_t> depth(w.edge_point.size(), 1);
+            for (auto& v : x) v += 1e-3;
+            for (size_t e = 0; e < chi2.size(); e++) chi2[e] = (e % 97 == 0) ? 10.0 : 1.0;
+            Optimizer::ApplyLocalBAResult(w, &S.map, q.data(), t.data(), x.data(), chi2.data(), depth.data());
+            windows++;
+        }
+    }
+    stop.store(true);
+    tracking.join();
+    CHECK(windows >= 15 && tracked.load() > 0, "windows %d tracked %ld", windows, tracked.load());
+    CHECK(S.map.GetMapChangeIndex() == windows, "change index %d vs %d windows", S.map.GetMapChangeIndex(), windows);
+    for (auto& mp : S.mps) {
+        if (mp->isBad()) continue;
+        for (auto& o : mp->GetObservations())
+            CHECK(o.first->GetMapPoint(std::get<0>(o.second)) == mp.get(), "observation / keyframe match disagree");
+    }
 }
 
 // ---- GPU tests ----------------------------------------------------------------------------------------------
@@ -878,12 +948,67 @@ static void testBoW() {
     }
 }
 
+// Tracking (ORBextractor + SearchForTriangulation's device search) and LocalBundleAdjustment issued concurrently from
+// two threads, each on its own thread-local device contexts: every result equals the one computed alone.
+static void testConcurrentGPU() {
+    const int w = 640, h = 480;
+    auto img = makeImage(w, h, 9);
+    std::vector<int> lap = {0, 1000};
+    std::vector<KeyPoint> k0;
+    Mat8U d0;
+    {
+        ORBextractor ext(1000, 1.2f, 8, 20, 7);
+        ext(ImageView(img.data(), w, h), ImageView(), k0, d0, lap);
+    }
+    auto lbaOnce = [](std::vector<float>* out) {
+        Scene S(12, 400, 4, 61, 0.08f);
+        KeyFrame* pKF = S.kfs[6].get();
+        std::vector<KeyFrame*> cov;
+        for (int k = 2; k < 11; k++)
+            if (k != 6) cov.push_back(S.kfs[k].get());
+        pKF->SetVectorCovisibleKeyFrames(cov);
+        int nf = 0, no = 0, nm = 0, ne = 0;
+        Optimizer::LocalBundleAdjustment(pKF, nullptr, &S.map, nf, no, nm, ne);
+        out->clear();
+        for (auto& k : S.kfs) {
+            const SE3f T = k->GetPose();
+            out->insert(out->end(), T.q, T.q + 4);
+            out->insert(out->end(), T.t, T.t + 3);
+        }
+    };
+    std::vector<float> ref;
+    lbaOnce(&ref);
+    std::atomic<int> bad_extract{0};
+    std::thread tracking([&] {
+        ORBextractor ext(1000, 1.2f, 8, 20, 7);
+        for (int i = 0; i < 12; i++) {
+            std::vector<KeyPoint> k;
+            Mat8U d;
+            ext(ImageView(img.data(), w, h), ImageView(), k, d, lap);
+            if (k.size() != k0.size() || std::memcmp(k.data(), k0.data(), sizeof(KeyPoint) * k.size()) != 0 ||
+                std::memcmp(d.data.data(), d0.data.data(), 32 * k.size()) != 0)
+                bad_extract++;
+        }
+    });
+    int bad_lba = 0;
+    for (int i = 0; i < 4; i++) {
+        std::vector<float> got;
+        lbaOnce(&got);
+        bad_lba += std::memcmp(got.data(), ref.data(), sizeof(float) * ref.size()) != 0;
+    }
+    tracking.join();
+    CHECK(bad_extract.load() == 0 && bad_lba == 0, "concurrent results differ: extract %d lba %d", bad_extract.load(),
+          bad_lba);
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     testAlgebra();
     testObservations();
     testWindow();
+    testConcurrentHost();
     if (mode == "gpu") {
+        testConcurrentGPU();
         testExtractor();
         testMatcher();
         testLocalBA();

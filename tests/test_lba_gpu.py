@@ -139,3 +139,24 @@ def test_lba_batch_device(solver, oracle):
     solver.solve_batch_device(B)
     for i in range(len(probs)):
         assert np.array_equal(B.result(i).point_xyz, first[i].point_xyz)
+
+
+def test_lba_size_bound(solver):
+    """A problem whose dense pose x landmark table would exceed 4 GiB (1100 optimised poses x 1M points) is refused
+    with MAM_ERR_CAPACITY and a message naming the sizes, before any scratch allocation."""
+    from mam3slam_amd._lib import MamError
+    from mam3slam_amd.lba import LBAProblem
+
+    P, L = 1100, 1_000_000
+    q = np.zeros((P, 4))
+    q[:, 3] = 1.0
+    prob = LBAProblem(pose_id=np.arange(P), pose_fixed=np.zeros(P, np.uint8), pose_q=q, pose_t=np.zeros((P, 3)),
+                      point_id=np.arange(L), point_xyz=np.tile([0.0, 0.0, 5.0], (L, 1)),
+                      edge_point=np.arange(P, dtype=np.int32), edge_pose=np.arange(P, dtype=np.int32),
+                      edge_obs=np.zeros((P, 2)), edge_inv_sigma2=np.ones(P),
+                      cams=np.array([[500.0, 500.0, 320.0, 240.0]], np.float32))
+    with pytest.raises(MamError, match="rc=-2.*too large"):
+        solver.solve(prob)
+    # the context stays usable
+    small = synthetic_problem(n_opt=5, n_fixed=2, n_points=100, obs_per_point=4, seed=3)
+    assert solver.solve(small).status == 0
