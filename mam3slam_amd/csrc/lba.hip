@@ -1293,8 +1293,9 @@ struct mam_lba_ctx {
     DevBuf<uint8_t> io;           // host API: inputs + outputs of the one problem
     DevBuf<Prob> probs;
     DevBuf<LM> lms;
-    hipStream_t stream2 = nullptr;   // the second half of a split batch (created on first use, the caller's priority)
-    hipEvent_t ev[2] = {nullptr, nullptr};
+    static constexpr int kMaxGroups = 4;
+    hipStream_t gstream[kMaxGroups - 1] = {};   // groups 1.. of a split batch (created on first use, caller's priority)
+    hipEvent_t ev_start = nullptr, ev_done[kMaxGroups - 1] = {};
     double trials_ema = 8.0;      // slots enqueued before the first read-back (tracks the trials solves take)
 };
 
@@ -1492,25 +1493,30 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     const dim3 gBlk(maxNp * maxNp + maxNp > 0 ? maxNp * maxNp + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
     const dim3 gUpd((maxPL + 255) / 256 > 0 ? (maxPL + 255) / 256 : 1, Q);
-    // The batch runs as G interleaved halves on two streams: one half's latency-bound factorization (one workgroup
-    // per problem) overlaps the other half's throughput kernels. Every kernel indexes its problems from the Prob
-    // pointer it is given, so a half is the sub-array P + first with Q_g problems. MAM_LBA_SPLIT=1 disables.
+    // The batch runs as G interleaved groups on G streams: one group's latency-bound factorization (one workgroup
+    // per problem) overlaps the other groups' throughput kernels. Every kernel indexes its problems from the Prob
+    // pointer it is given, so a group is the sub-array P + first with Q_g problems. MAM_LBA_SPLIT=<G> overrides
+    // (1 disables).
     const char* sp = std::getenv("MAM_LBA_SPLIT");
-    const int G = (Q >= 4 && !(sp && sp[0] == '1')) ? 2 : 1;
-    hipStream_t sg[2] = {s, s};
-    if (G == 2) {
-        if (!c->stream2) {
-            int prio = 0;
-            if (hipStreamGetPriority(s, &prio) != hipSuccess) prio = 0;
-            if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio) != hipSuccess) {
-                (void)hipGetLastError();
-                MAM_HIP(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    int G = Q < 4 ? 1 : 2;   // batch of 32 world windows: 8.56 / 7.92 / 7.76 / 9.10 ms at G = 1 / 2 / 3 / 4; c2: 2
+    if (sp && sp[0] >= '1' && sp[0] <= '9') G = std::max(1, std::min({mam_lba_ctx::kMaxGroups, Q, sp[0] - '0'}));
+    hipStream_t sg[mam_lba_ctx::kMaxGroups] = {s, s, s, s};
+    if (G > 1) {
+        int prio = 0;
+        if (hipStreamGetPriority(s, &prio) != hipSuccess) prio = 0;
+        if (!c->ev_start) MAM_HIP(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+        for (int g = 1; g < G; g++) {
+            if (!c->gstream[g - 1]) {
+                if (hipStreamCreateWithPriority(&c->gstream[g - 1], hipStreamNonBlocking, prio) != hipSuccess) {
+                    (void)hipGetLastError();
+                    MAM_HIP(hipStreamCreateWithFlags(&c->gstream[g - 1], hipStreamNonBlocking));
+                }
+                MAM_HIP(hipEventCreateWithFlags(&c->ev_done[g - 1], hipEventDisableTiming));
             }
-            for (auto& e : c->ev) MAM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            sg[g] = c->gstream[g - 1];
         }
-        sg[1] = c->stream2;
-        MAM_HIP(hipEventRecord(c->ev[0], s));   // the structure build precedes both halves
-        MAM_HIP(hipStreamWaitEvent(c->stream2, c->ev[0], 0));
+        MAM_HIP(hipEventRecord(c->ev_start, s));   // the structure build precedes every group
+        for (int g = 1; g < G; g++) MAM_HIP(hipStreamWaitEvent(sg[g], c->ev_start, 0));
     }
     auto slot_g = [&](int g) {
         const int q0 = g * Q / G, q1 = (g + 1) * Q / G, Qg = q1 - q0;
@@ -1546,10 +1552,10 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     auto slot = [&]() {
         for (int g = 0; g < G; g++) slot_g(g);
     };
-    auto join = [&]() -> int {   // the second half's work before anything the first stream does next
-        if (G == 2) {
-            MAM_HIP(hipEventRecord(c->ev[1], c->stream2));
-            MAM_HIP(hipStreamWaitEvent(s, c->ev[1], 0));
+    auto join = [&]() -> int {   // the other groups' work before anything the first stream does next
+        for (int g = 1; g < G; g++) {
+            MAM_HIP(hipEventRecord(c->ev_done[g - 1], sg[g]));
+            MAM_HIP(hipStreamWaitEvent(s, c->ev_done[g - 1], 0));
         }
         return MAM_OK;
     };
@@ -1679,12 +1685,14 @@ void mam_lba_destroy(mam_lba_ctx* c) {
     ::mam::DeviceScope mam_dev_scope_(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
-    if (c->stream2) {
-        (void)hipStreamSynchronize(c->stream2);
-        (void)hipStreamDestroy(c->stream2);
-    }
-    for (auto& e : c->ev)
+    for (auto& st : c->gstream)
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    for (auto& e : c->ev_done)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     delete c;
 }
 
