@@ -1,9 +1,11 @@
 #!/bin/bash
-# Full measurement session (the files committed under profiles/): GPU parity tests, the c1 and c2 bench lines,
-# kernel traces of standalone 64-frame launches (--lanes 1 --batch 64, as bench.py's serialised stage-timing pass
-# measures them), FETCH_SIZE / WRITE_SIZE passes for roofline.traffic (they do not fit one PMC pass on gfx950), the
-# B=1 timeline, the standalone LocalBundleAdjustment with its kernel trace and an FP64-MFMA counter pass, and the
-# PoseOptimization, SearchInNeighbors (Fuse) and ComputeBoW benches with their kernel traces. Stops at the first step that fails, faults or times out.
+# Full measurement session (round 2; the files committed under profiles/r02/ come from it, copied by
+# scripts/collect_profiles.py): the GPU parity suite; the c1 / c2 / c3 bench lines (default flags, CPU baseline on);
+# standalone LocalBundleAdjustment (oracle-timed), PoseOptimization, SearchInNeighbors, ComputeBoW and batched
+# SearchForTriangulation benches; per config c1 / c2 a kernel trace of standalone 64-frame launches (the launch shape
+# bench.py's stage pass times) with FETCH_SIZE, WRITE_SIZE and SQ/GRBM passes (scripts/gpu_fast_pmc.sh ->
+# traffic_cN.json); a kernel trace of the default c2 bench (tracking and LocalMapping concurrently); the LBA kernel
+# trace and its FP64-MFMA counter pass. Stops at the first step that fails, faults or times out.
 set -u
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out
@@ -11,27 +13,24 @@ mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -20 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
-for CFG in c1 c2; do
+for CFG in c1 c2 c3; do
   timeout -k 10 600 python bench.py --config $CFG > $O/bench_$CFG.json 2> $O/bench_$CFG.err || { tail -5 $O/bench_$CFG.err; exit 1; }
-  cat $O/bench_$CFG.json
+  python3 -c "import json; d=json.load(open('$O/bench_$CFG.json')); print('$CFG', d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_launch_ms'])"
 done
-timeout -k 10 300 python scripts/lba_bench.py --oracle > $O/lba_bench.json 2> $O/lba_bench.err || exit 1
-cat $O/lba_bench.json
-timeout -k 10 300 python scripts/pose_bench.py --config c1 --oracle > $O/pose_c1.json 2> $O/pose_c1.err || exit 1
+timeout -k 10 300 python scripts/lba_bench.py --world --batch 32 --oracle > $O/lba_bench.json 2> $O/lba_bench.err || exit 1
+timeout -k 10 300 python scripts/tri_bench.py > $O/tri_bench.json 2> $O/tri_bench.err || exit 1
 timeout -k 10 300 python scripts/pose_bench.py --config c2 --oracle > $O/pose_c2.json 2> $O/pose_c2.err || exit 1
 timeout -k 10 300 python scripts/fuse_bench.py --config c2 --oracle > $O/fuse_c2.json 2> $O/fuse_c2.err || exit 1
 timeout -k 10 300 python scripts/bow_bench.py --config c2 --oracle > $O/bow_c2.json 2> $O/bow_c2.err || exit 1
+bash scripts/gpu_fast_pmc.sh r02c1 c1 > $O/pmc_r02c1.out || exit 1
+bash scripts/gpu_fast_pmc.sh r02c2 c2 > $O/pmc_r02c2.out || exit 1
+bash scripts/gpu_c2_trace.sh r02c2load > $O/prof_r02c2load.out || exit 1
 cd /tmp && export TMPDIR=/tmp
-for CFG in c1 c2; do
-  A="--config $CFG --no-cpu-baseline --lanes 1 --batch 64 --no-latency --no-pose --no-sin"
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$CFG -o run -- python3 $R/bench.py $A > $O/prof_$CFG.log 2>&1 || exit 1
-  timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$CFG -o run -- python3 $R/bench.py $A --steps 4 --warmup 1 > $O/pmc_fetch_$CFG.log 2>&1 || exit 1
-  timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$CFG -o run -- python3 $R/bench.py $A --steps 4 --warmup 1 > $O/pmc_write_$CFG.log 2>&1 || exit 1
+for CFG in c1 c2; do   # the default bench command under a kernel trace: its stage-pass launches vs bench.py's roofline
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_r02default_$CFG -o run -- python3 $R/bench.py --config $CFG > $O/bench_traced_$CFG.json 2> $O/prof_r02default_$CFG.log || { tail -5 $O/prof_r02default_$CFG.log; exit 1; }
+  python3 $R/scripts/roofline_check.py $O/prof_r02default_$CFG/run_kernel_trace.csv $O/bench_traced_$CFG.json > $O/roofline_check_$CFG.json || exit 1
+  cat $O/roofline_check_$CFG.json
 done
-timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $O/prof_b1 -o run -- python3 $R/bench.py --batch 1 --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-pose --no-sin > $O/prof_b1.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_lba -o run -- python3 $R/scripts/lba_bench.py --solves 10 > $O/prof_lba.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_lba -o run -- python3 $R/scripts/lba_bench.py --solves 5 > $O/pmc_lba.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_pose -o run -- python3 $R/scripts/pose_bench.py --config c1 --reps 10 > $O/prof_pose.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_fuse -o run -- python3 $R/scripts/fuse_bench.py --config c2 --reps 10 > $O/prof_fuse.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_bow -o run -- python3 $R/scripts/bow_bench.py --config c2 --reps 10 > $O/prof_bow.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_r02lba -o run -- python3 $R/scripts/lba_bench.py --world --batch 32 --solves 4 > $O/prof_r02lba.log 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -f csv -d $O/pmc_r02lba -o run -- python3 $R/scripts/lba_bench.py --world --batch 32 --solves 3 > $O/pmc_r02lba.log 2>&1 || exit 1
 echo done
