@@ -83,6 +83,8 @@ struct Prob {
     int32_t* cnt;                // [L + Np] counters / cursors of the device structure build
     int32_t* eidx;               // [Np][L] edge of (pose block, point), -1 if none
     uint8_t* pairmask;           // [Np][Np] (i1 < i2): the two poses share a landmark (S block non-zero)
+    int32_t* blk_off;            // [Np * Np + 1] start of block (i1, i2)'s landmark pairs in blk_pair (i1 <= i2)
+    int2* blk_pair;              // (edge of pose i1, edge of pose i2) per shared landmark, i2's edge order
     uint8_t* tmask;              // [nt][nt] (r >= c): 16x16 tile (r, c) of L is structurally non-zero (S + fill)
     int nt;                      // npad / 16
     // state: [2] buffers, lm->cur is the current one
@@ -690,8 +692,8 @@ __global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ prob
     wave_copy_out(d.coef + 6 * (size_t)e0, sc, 6 * ne);
 }
 
-// grid (Np * Np + Np, Q) x 64: one wave per block (i1 <= i2) of S (blocks with i2 < i1 exit), landmarks seen by both
-// poses walked through pose i2's edges and pose i1's edge-table row; then one wave per pose for b_s. Only the lower
+// grid (Np * Np + Np, Q) x 64: one wave per block (i1 <= i2) of S (blocks with i2 < i1 exit) over its landmark pairs
+// (k_blk_fill), lanes strided over the pairs + a fixed-order wave sum; then one wave per pose for b_s. Only the lower
 // triangle of S is written (the one the factorization reads).
 __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs) {
     // XCD-aware: each XCD takes a contiguous range of (problem, block row) ids, so the W / H_pl records of the
@@ -737,13 +739,10 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
-    const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
-    for (int s = d.qe_off[i2] + lane; s < d.qe_off[i2 + 1]; s += 64) {
-        const int ec = d.qe_idx[s];
-        const int ea = ei1[d.edge_point[ec]];
-        if (ea < 0) continue;
-        const double* W = d.bdinv + 18 * (size_t)ea;
-        const double* B = d.hpl + 18 * (size_t)ec;
+    for (int k = d.blk_off[bx] + lane; k < d.blk_off[bx + 1]; k += 64) {
+        const int2 pr = d.blk_pair[k];
+        const double* W = d.bdinv + 18 * (size_t)pr.x;
+        const double* B = d.hpl + 18 * (size_t)pr.y;
         double w[18], b[18];
 #pragma unroll
         for (int k = 0; k < 18; k++) { w[k] = W[k]; b[k] = B[k]; }
@@ -786,6 +785,84 @@ constexpr int NB = 16;
 constexpr int LDLT_THREADS = MAM_LDLT_THREADS;
 
 __host__ __device__ inline int ldlt_pad(int n) { return (n + NB - 1) / NB * NB; }
+
+// ---- the landmark pairs of every S block, once per batch (the structure is fixed across the LM iterations):
+// block (i1 <= i2) gets the (edge of pose i1, edge of pose i2) pairs of the landmarks both observe, in pose i2's
+// edge order — k_schur_blk then walks only those instead of all of pose i2's edges through the pose x landmark table
+__device__ __forceinline__ bool blk_nonzero(const Prob& d, int i1, int i2) {
+    return i2 >= i1 && (i1 == i2 || d.pairmask[(size_t)i1 * d.Np + i2]);
+}
+// grid (Np * Np, Q) x 64: pairs per block
+__global__ __launch_bounds__(64) void k_blk_count(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    if (d.lm->status) return;
+    const int bx = blockIdx.x;
+    if (bx >= d.Np * d.Np) return;
+    const int i1 = bx / d.Np, i2 = bx % d.Np, lane = threadIdx.x;
+    int n = 0;
+    if (blk_nonzero(d, i1, i2)) {
+        const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
+        for (int s = d.qe_off[i2] + lane; s < d.qe_off[i2 + 1]; s += 64) n += ei1[d.edge_point[d.qe_idx[s]]] >= 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+    }
+    if (lane == 0) d.blk_off[bx] = n;
+}
+// grid (1, Q) x 1024: exclusive scan of the counts, the total at [Np * Np]
+__global__ __launch_bounds__(1024) void k_blk_scan(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    if (d.lm->status) return;
+    __shared__ int part[1024];
+    const int n = d.Np * d.Np, t = threadIdx.x;
+    const int per = (n + 1023) / 1024, b = t * per, e = min(n, b + per);
+    int sum = 0;
+    for (int i = b; i < e; i++) sum += d.blk_off[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {   // inclusive Hillis-Steele
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = t > 0 ? part[t - 1] : 0;
+    for (int i = b; i < e; i++) {
+        const int c = d.blk_off[i];
+        d.blk_off[i] = run;
+        run += c;
+    }
+    if (t == 1023) d.blk_off[n] = part[1023];
+}
+__global__ void k_blk_total(const Prob* __restrict__ probs, int Q, int* __restrict__ out) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= Q) return;
+    const Prob& d = probs[q];
+    out[q] = d.lm->status ? 0 : d.blk_off[d.Np * d.Np];
+}
+// grid (Np * Np, Q) x 64: the pairs, compacted in edge order by ballot
+__global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    if (d.lm->status) return;
+    const int bx = blockIdx.x;
+    if (bx >= d.Np * d.Np) return;
+    const int i1 = bx / d.Np, i2 = bx % d.Np, lane = threadIdx.x;
+    if (!blk_nonzero(d, i1, i2)) return;
+    const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
+    int base = d.blk_off[bx];
+    const int end = d.qe_off[i2 + 1];
+    for (int s0 = d.qe_off[i2]; s0 < end; s0 += 64) {
+        const int s = s0 + lane;
+        int ec = -1, ea = -1;
+        if (s < end) {
+            ec = d.qe_idx[s];
+            ea = ei1[d.edge_point[ec]];
+        }
+        const bool hit = ea >= 0;
+        const uint64_t m = __ballot(hit);
+        if (hit) d.blk_pair[base + __popcll(m & ((1ull << lane) - 1ull))] = make_int2(ea, ec);
+        base += __popcll(m);
+    }
+}
 
 // grid (Q) x 1024, after k_struct_sort: the 16x16 tile pattern of L. A tile of S is non-zero when it holds a pose
 // diagonal block or the block of two poses sharing a landmark (pairmask); the right-looking factorization then fills
@@ -1293,6 +1370,9 @@ struct mam_lba_ctx {
     DevBuf<uint8_t> io;           // host API: inputs + outputs of the one problem
     DevBuf<Prob> probs;
     DevBuf<LM> lms;
+    DevBuf<int2> blk_pairs;       // the S blocks' landmark pairs of the current batch
+    DevBuf<int> blk_tot;
+    mam::PinnedBuf blk_tot_host;
     static constexpr int kMaxGroups = 4;
     hipStream_t gstream[kMaxGroups - 1] = {};   // groups 1.. of a split batch (created on first use, caller's priority)
     hipEvent_t ev_start = nullptr, ev_done[kMaxGroups - 1] = {};
@@ -1319,10 +1399,10 @@ struct Carver {
 size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
     const size_t nx = 6 * (size_t)Np + 3 * (size_t)L;
     return al(4 * (size_t)P) + al(4 * (size_t)Np) + al(4 * (size_t)(L + 1)) + al(4 * (size_t)E) +
-           al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) +
+           al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) + al(4 * ((size_t)Np * Np + 1)) +
            al((size_t)(npad / 16) * (npad / 16)) +
            2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
-           al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
+           2 * al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
            al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
            al(8 * (size_t)npad * npad) + al(8 * nx) + al(8 * (size_t)npad) +
            al(8 * mam::lba::ldlt_ws_doubles(npad)) + al((size_t)E);
@@ -1339,6 +1419,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.cnt = cv.take<int32_t>(d.L + d.Np);
     d.eidx = cv.take<int32_t>((size_t)d.Np * d.L);
     d.pairmask = cv.take<uint8_t>((size_t)d.Np * d.Np);
+    d.blk_off = cv.take<int32_t>((size_t)d.Np * d.Np + 1);
     d.nt = d.npad / mam::lba::NB;
     d.tmask = cv.take<uint8_t>((size_t)d.nt * d.nt);
     d.pose[0] = cv.take<double>(7 * (size_t)d.P);
@@ -1485,6 +1566,28 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_struct_scatter, gE, dim3(256), 0, s, P);
         hipLaunchKernelGGL(k_struct_sort, dim3(std::max(maxLb, 1), Q), dim3(256), 0, s, P);
         hipLaunchKernelGGL(k_struct_tiles, dim3(Q), dim3(1024), 0, s, P);
+        // the S blocks' landmark pairs: counts, offsets, one read-back of the totals to size the pair buffer
+        const dim3 gB(std::max(maxNp * maxNp, 1), Q);
+        hipLaunchKernelGGL(k_blk_count, gB, dim3(64), 0, s, P);
+        hipLaunchKernelGGL(k_blk_scan, dim3(1, Q), dim3(1024), 0, s, P);
+        if (int rc = c->blk_tot.alloc(Q)) return rc;
+        if (int rc = c->blk_tot_host.alloc(sizeof(int) * (size_t)Q)) return rc;
+        hipLaunchKernelGGL(k_blk_total, dim3((Q + 255) / 256), dim3(256), 0, s, P, Q, c->blk_tot.p);
+        MAM_HIP(hipGetLastError());
+        MAM_HIP(hipMemcpyAsync(c->blk_tot_host.p, c->blk_tot.p, sizeof(int) * (size_t)Q, hipMemcpyDeviceToHost, s));
+        MAM_HIP(hipStreamSynchronize(s));
+        const int* tot = reinterpret_cast<const int*>(c->blk_tot_host.p);
+        size_t npairs = 0;
+        for (int q = 0; q < Q; q++) npairs += (size_t)std::max(tot[q], 0);
+        if (int rc = c->blk_pairs.alloc(std::max<size_t>(npairs, 1))) return rc;
+        size_t base = 0;
+        for (int q = 0; q < Q; q++) {
+            hp[q].blk_pair = c->blk_pairs.p + base;
+            base += (size_t)std::max(tot[q], 0);
+        }
+        std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
+        MAM_HIP(hipMemcpyAsync(c->probs.p, c->lm_host.p, sizeof(Prob) * Q, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_blk_fill, gB, dim3(64), 0, s, P);
         hipLaunchKernelGGL(k_linearize, gE64, dim3(EW), 0, s, P, 2);
         hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
     }

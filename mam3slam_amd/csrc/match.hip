@@ -1090,7 +1090,10 @@ __global__ __launch_bounds__(256) void k_tri_pair_geom(TriBatchArgs a) {
 // candidates are dealt to the 16 lanes; (dist, last position) argmin over the lanes = "dist <= bestDist, last equal
 // wins". Then, in the same workgroup, nmatches and the rotation-histogram filter when check_ori
 // (ORBmatcher.cc:1114-1133).
-constexpr int TRI_THREADS = 1024;
+#ifndef MAM_TRI_THREADS
+#define MAM_TRI_THREADS 1024
+#endif
+constexpr int TRI_THREADS = MAM_TRI_THREADS;
 __global__ __launch_bounds__(TRI_THREADS) void k_tri_pair(TriBatchArgs a) {
     extern __shared__ unsigned long long sk2[];   // [skey_stride] kf2's sorted keys, then kf2's has_mp bytes
     __shared__ int hist[MAM_HISTO_LENGTH];
