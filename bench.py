@@ -744,14 +744,22 @@ def main():
                           "exchange_bytes_per_step": int(mapping.exch.send.numel() * world)}
         if newmp is not None:
             nmv = newmp.nmatch.cpu().numpy()
+            tri_b = newmp.algorithmic_bytes()
+            tri_ms = tri_stage["triangulation"][0] / args.steps
             out["new_keyframes"] = {
                 "keyframes_per_step": newmp.W, "searches_per_step": newmp.npairs, "neighbours": newmp.NN,
                 "matches_per_search": float(nmv.mean()),
-                "ms_per_step_triangulation": tri_stage["triangulation"][0] / args.steps,
+                "ms_per_step_triangulation": tri_ms,
                 "ms_per_step_compute_bow": tri_stage["compute_bow"][0] / args.steps,
+                "candidate_pairs_per_search": tri_b["candidate_pairs"] / newmp.npairs,
+                "algorithmic_bytes_per_step_triangulation": tri_b["bytes"],
+                "achieved_GBs_triangulation": tri_b["bytes"] / (tri_ms * 1e-3) / 1e9 if tri_ms > 0 else None,
                 "note": "ComputeBoW (levelsup 4, synthetic k=10 L=6 vocabulary) + CreateNewMapPoints' "
-                        "SearchForTriangulation against the 30 previously inserted keyframes, on the LocalMapping "
-                        "stream before the LBA windows (stage times on that stream, concurrent with tracking)"}
+                        "SearchForTriangulation against the 30 previously inserted keyframes, on their own stream as "
+                        "soon as the keyframes are ingested, before the LBA windows of the same keyframes (stage "
+                        "times on that stream, concurrent with tracking); algorithmic bytes per SURVEY §8(d): "
+                        "sum over shared BoW nodes of |f1| x |f2| x 32 B of descriptors + the two FeatureVectors' "
+                        "keypoints, flags and keys (the last run's pairs)"}
         if pose_info is not None:
             out["pose_optimization"] = pose_info
         if sin_info is not None:

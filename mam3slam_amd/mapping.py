@@ -304,6 +304,26 @@ class NewMapPointsLeg:
         self.matcher.search_for_triangulation_batch_device(self.tr.F0, self.tr.cam, b, self.out.data_ptr(),
                                                            self.nmatch.data_ptr(), False, stream=s)
 
+    def algorithmic_bytes(self):
+        """SURVEY §8(d) bytes of the last run's searches: per pair, sum over the BoW nodes both FeatureVectors hold of
+        |f1| x |f2| descriptor pairs x 32 B, plus per FeatureVector feature its sorted key (8 B), MapPoint flag (1 B),
+        keypoint (28 B) and descriptor (32 B) once."""
+        nid = self.nid.cpu().numpy().view(np.uint32)
+        w = self.weight.cpu().numpy()
+        cnt = self.cnt.cpu().numpy()[:, 0]
+        per_slot = []
+        for k in range(self.R):
+            n = int(min(max(cnt[k], 0), self.S))
+            v = nid[k, :n][w[k, :n] > 0]
+            u, c = np.unique(v, return_counts=True)
+            per_slot.append(dict(zip(u.tolist(), c.tolist())))
+        cand, fv = 0, 0
+        for a, b in self.pairs[self.head].cpu().numpy():
+            A, B = per_slot[a], per_slot[b]
+            cand += sum(c * B[u] for u, c in A.items() if u in B)
+            fv += sum(A.values()) + sum(B.values())
+        return {"candidate_pairs": int(cand), "bytes": int(cand * 32 + fv * (8 + 1 + 28 + 32))}
+
     def pair_inputs(self, q: int):
         """Host FrameData of pair q of the last run (keys, desc, has_mp, FeatureVector from the device BoW, pose)."""
         from .match import FrameData

@@ -1,0 +1,40 @@
+"""GPU: the CreateNewMapPoints leg bench.py times (mam3slam_amd/mapping.py NewMapPointsLeg) — tracked frames ingested
+as keyframes into the HBM ring, ComputeBoW on the device, each new keyframe searched against the 30 slots before it
+(mam_search_for_triangulation_batch_device) — every pair index-exact against the oracle's SearchForTriangulation on
+the same keyframes with the device-made FeatureVectors, over several ring heads (ring wrap-around included)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cfg", ["c1", "c3"])
+def test_new_map_points_leg_matches_oracle(gpu_lib, oracle, cfg):
+    import torch
+
+    import bench
+    from mam3slam_amd.mapping import NewMapPointsLeg
+
+    dev = torch.device("cuda", 0)
+    conf = dict(bench.CONFIGS[cfg])
+    tr = bench.TrackingLeg(conf, 16, 1, 0, dev)
+    nm = NewMapPointsLeg(tr, 2, dev)
+    checked = total = 0
+    for step in range(nm.R // nm.W + 2):   # past one full turn of the ring
+        tr.step()
+        nm.ingest(step)
+        nm.launch(nm.pending)
+        if step % 7 != 6:
+            continue
+        torch.cuda.synchronize()
+        out, nmatch = nm.out.cpu().numpy(), nm.nmatch.cpu().numpy()
+        for q in range(0, nm.npairs, 3):
+            K1, K2 = nm.pair_inputs(q)
+            no, oo = oracle.search_for_triangulation_kf(K1, K2, tr.cam, tr.cam, False, False)
+            n1 = len(K1.keys)
+            assert int(nmatch[q]) == no and np.array_equal(out[q, :n1], oo), (step, q, int(nmatch[q]), no)
+            checked += 1
+            total += no
+    assert checked >= 20
+    b = nm.algorithmic_bytes()
+    assert b["candidate_pairs"] > 0 and b["bytes"] > 32 * b["candidate_pairs"]
