@@ -671,11 +671,13 @@ def main():
     bytes_per_launch = sb[dom] * B / launches_per_step
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = traffic_raw = None
+    pmc_counters = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath):   # PMC passes of the same launches (scripts/gpu_fast_pmc.sh)
         try:
             tj = json.load(open(tpath))
             traffic, traffic_raw = tj.get(dom), tj.get("raw", {}).get(dom)
+            pmc_counters = {k: tj.get(k, {}).get(dom) for k in ("valu_busy", "wave_frac_wait", "wave_frac_issue_stall")}
         except Exception:
             traffic = traffic_raw = None
 
@@ -717,7 +719,7 @@ def main():
             "stage_ms_per_step": per_step_ms,
             "roofline": {"bound": "hbm", "kernel": dom, "limiter": ROOFLINE_NOTES.get(dom), "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_raw_fetch": traffic_raw,
+                         "traffic_raw_fetch": traffic_raw, "pmc": pmc_counters,
                          "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms},
         }
         if lat is not None:

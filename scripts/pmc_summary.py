@@ -51,12 +51,16 @@ def write_traffic(out, path):
     t = {"_note": "HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (separate rocprofv3 passes, KB): stage values "
                   "apply the gfx950 x2 FETCH_SIZE correction of MI355X_MICROARCH.md (exact for wide coalesced reads, "
                   "an upper bound for narrower loads); 'raw' holds the uncorrected lower bound",
-         "raw": {}}
+         "raw": {}, "valu_busy": {}, "wave_frac_wait": {}, "wave_frac_issue_stall": {}}
     for stage, kern in STAGES.items():
         for name, e in out.items():
             if name.startswith(kern) and "hbm_bytes_x2fetch" in e:
                 t[stage] = e["hbm_bytes_x2fetch"]
                 t["raw"][stage] = e["hbm_bytes_raw"]
+            if name.startswith(kern) and "valu_busy" in e:
+                t["valu_busy"][stage] = e["valu_busy"]
+                t["wave_frac_wait"][stage] = e["wave_frac_wait"]
+                t["wave_frac_issue_stall"][stage] = e["wave_frac_issue_stall"]
     with open(path, "w") as f:
         json.dump(t, f, indent=1)
 
