@@ -535,10 +535,18 @@ def main():
         else:
             print(json.dumps({"launch_check": "ok", "world": 1, "rank_sum": 0}), flush=True)
         return
+    # MAM_BENCH_ONE_DEVICE=1 + MAM_DIST_BACKEND=gloo (tests only): every rank on GPU 0, the exchange over gloo — the
+    # whole multi-rank path on a one-GPU box (RCCL refuses two ranks on one device)
+    if os.environ.get("MAM_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=dev)
+        backend = os.environ.get("MAM_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend=backend)
 
     cfg = CONFIGS[args.config]
     agents_total = cfg.get("agents")

@@ -94,7 +94,13 @@ class MapUpdateExchange:
         if self.world == 1:
             self.recv.copy_(self.send)
         elif dist.get_backend(self.group) == "gloo":
-            dist.all_gather(list(self.recv.view(self.world, -1).unbind(0)), self.send, group=self.group)
+            if self.send.is_cuda:   # gloo gathers host tensors: stage through the host (tests of the multi-rank path)
+                torch.cuda.current_stream(self.send.device).synchronize()
+                parts = [torch.empty(self.send.numel(), dtype=torch.uint8) for _ in range(self.world)]
+                dist.all_gather(parts, self.send.cpu(), group=self.group)
+                self.recv.copy_(torch.cat(parts))
+            else:
+                dist.all_gather(list(self.recv.view(self.world, -1).unbind(0)), self.send, group=self.group)
         else:
             dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
         return self.recv

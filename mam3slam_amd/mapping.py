@@ -96,6 +96,15 @@ class LocalMappingLeg:
                 d.pose_id, d.pose_fixed, d.point_id, d.point_bad = pid.data_ptr(), fix.data_ptr(), mid.data_ptr(), None
                 d.pose_q, d.pose_t, d.point_xyz = q.data_ptr(), t.data_ptr(), x.data_ptr()
         self.max_rows = max_rows
+        # the exchange's fixed block size must be the same on every rank (a collective over blocks of different
+        # sizes fails or hangs): the largest window of any rank
+        import torch.distributed as dist
+
+        if world_size > 1 and dist.is_available() and dist.is_initialized():
+            on_gpu = dist.get_backend() == "nccl"
+            t = torch.tensor([cap], dtype=torch.int64, device=device if on_gpu else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            cap = int(t.item())
         self.cap = cap
         self.d_read = dev(np.frombuffer(bytes(rd), np.uint8))
         self.d_pack = dev(np.frombuffer(bytes(pk), np.uint8))
