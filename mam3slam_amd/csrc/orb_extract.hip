@@ -514,7 +514,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
             }
         }
     }
-    // (blur and FAST are both VALU-bound: running the blur on a second stream beside FAST + DistributeOctTree
+    // (blur and FAST both keep the CUs' issue slots busy: running the blur on a second stream beside FAST + DistributeOctTree
     // measured no gain, so the stages stay in order on one stream)
     {
         StageScope sc(&c->timer, s, MAM_STAGE_BLUR);

@@ -486,7 +486,8 @@ __device__ __forceinline__ half2_t fast_strength_h2(const half2_t* hp, int r, in
 //     at both thresholds by ballot;
 // (d) iniThFAST if any P > iniTh, else minThFAST; every wave reads all count entries with broadcast LDS reads;
 // (e) corners written in row-major order (pair order = pixel order) at ballot prefix positions.
-// The whole kernel is VALU-bound (S is ~70 packed f16 ops per pixel pair); see DESIGN.md.
+// Issue/latency-bound per workgroup (PMC: VALU busy ~11 %, a third of the wave cycles waiting, a third issue-stalled;
+// the circle test is ~a quarter of the time, staging without global loads is no faster): DESIGN.md §3 / §6.
 template <int CW>
 __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restrict__ g,
                                                              const CellDesc* __restrict__ cells, LevelSrc s,
