@@ -166,6 +166,7 @@ size_t distribute_lds_bytes(int NC, int max_cells) {
 int build_pyr_plan(mam_orb_ctx* c, int nb);
 int pyr_forced_bands();
 bool pyr_flat_enabled();
+int pyr_rows_per_thread();
 
 // Geometry for a W x H frame and capacity F (reallocates device scratch when either grows/changes).
 int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
@@ -449,6 +450,17 @@ int build_pyr_plan(mam_orb_ctx* c, int nb) {
     return MAM_OK;
 }
 
+// output rows per k_pyr_flat thread (MAM_PYR_RQ = 1 / 2 / 4, default 4: one column-coefficient load per 4 rows and
+// 4 quads' loads in flight; pyramid stage per 256 frames c1 0.394 / 0.377 / 0.387 ms, c2 0.939 / 0.823 / 0.787 ms)
+int pyr_rows_per_thread() {
+    static const int v = [] {
+        const char* e = getenv("MAM_PYR_RQ");
+        const int x = e ? atoi(e) : 4;
+        return (x == 1 || x == 2) ? x : 4;
+    }();
+    return v;
+}
+
 // MAM_PYR_FLAT=0 forces the LDS block kernel for the per-level launches (experiments / parity cross-check)
 bool pyr_flat_enabled() {
     static const bool on = [] {
@@ -504,9 +516,14 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
             for (int l = 1; l < L; l++) {
                 const mam::LevelGeom& lv = g.L[l];
                 if (flat) {
-                    const long long nq = (long long)((lv.w + 3) / 4) * lv.h;
-                    hipLaunchKernelGGL(mam::k_pyr_flat, dim3((int)((nq + 255) / 256), F), dim3(256), 0, s, c->d_geom.p,
-                                       l, src, c->d_pyr.p);
+                    const int rq = pyr_rows_per_thread();
+                    const long long nq = (long long)((lv.w + 3) / 4) * ((lv.h + rq - 1) / rq);
+                    const dim3 pg((int)((nq + 255) / 256), F);
+                    switch (rq) {
+                        case 1: hipLaunchKernelGGL(mam::k_pyr_flat<1>, pg, dim3(256), 0, s, c->d_geom.p, l, src, c->d_pyr.p); break;
+                        case 2: hipLaunchKernelGGL(mam::k_pyr_flat<2>, pg, dim3(256), 0, s, c->d_geom.p, l, src, c->d_pyr.p); break;
+                        default: hipLaunchKernelGGL(mam::k_pyr_flat<4>, pg, dim3(256), 0, s, c->d_geom.p, l, src, c->d_pyr.p); break;
+                    }
                 } else {
                     dim3 grid((lv.w + mam::PYR_XB - 1) / mam::PYR_XB, (lv.h + mam::PYR_RB - 1) / mam::PYR_RB, F);
                     hipLaunchKernelGGL(mam::k_pyr_down, grid, dim3(256), lds, s, c->d_geom.p, l, src, c->d_pyr.p);

@@ -175,19 +175,21 @@ __device__ __forceinline__ uint32_t pyr_quad(const uint8_t* S0, const uint8_t* S
     return packed;
 }
 
-// One thread per output quad of the whole level (row-major over every frame's level): no LDS staging, every lane
-// busy (the block kernel leaves most lanes idle on levels narrower than its 1024-pixel tiles), the quad's column
-// coefficients pre-packed (LevelGeom.qcoef) and its three source words per row read straight from the level
-// above. Requires word-aligned source rows (the host falls back to k_pyr_down otherwise).
+// One thread per output quad column and RQ consecutive output rows of the whole level (row-major over every frame's
+// level): no LDS staging, every lane busy (the block kernel leaves most lanes idle on levels narrower than its
+// 1024-pixel tiles), the quad's column coefficients pre-packed (LevelGeom.qcoef) and loaded once for its RQ rows, the
+// three source words per row read straight from the level above, all RQ rows' loads issued before the first store.
+// Requires word-aligned source rows (the host falls back to k_pyr_down otherwise).
+template <int RQ>
 __global__ __launch_bounds__(256) void k_pyr_flat(const Geom* __restrict__ g, int l, LevelSrc s, uint8_t* pyr) {
     const LevelGeom& L = g->L[l];
     const int nq = (L.w + 3) >> 2;
+    const int nrg = (L.h + RQ - 1) / RQ;
     const int qi = blockIdx.x * 256 + threadIdx.x;
     const int f = blockIdx.y;
-    if (qi >= nq * L.h) return;
-    const int dy = qi / nq, q = qi - dy * nq;
+    if (qi >= nq * nrg) return;
+    const int rg = qi / nq, q = qi - rg * nq;
     const uint4 c0 = L.qcoef[2 * q], c1 = L.qcoef[2 * q + 1];
-    const int2 rc = L.rcoef[dy];
     PyrQuad cq;
     cq.base = (int)(c0.x & 0xFFFu);
 #pragma unroll
@@ -202,18 +204,31 @@ __global__ __launch_bounds__(256) void k_pyr_flat(const Geom* __restrict__ g, in
         cq.a1[i] = (int)(pa[i] >> 16);
     }
     const int sh = g->L[l - 1].h;
-    const int sy = rc.x;
-    const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
-    const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
+    const int snw = (g->L[l - 1].w + 3) >> 2;
     int spitch;
     const uint8_t* src = level_ptr(g, s, f, l - 1, &spitch);
-    const uint32_t packed = pyr_quad(src + (size_t)ry0 * spitch, src + (size_t)ry1 * spitch, cq,
-                                     (int)(short)(rc.y & 0xFFFF), rc.y >> 16, (g->L[l - 1].w + 3) >> 2);
-    uint8_t* o = pyr + L.pyr_off + (size_t)f * L.frame_bytes + (size_t)dy * L.pitch + 4 * q;
-    if (4 * q + 4 <= L.w) {
-        *reinterpret_cast<uint32_t*>(o) = packed;
-    } else {
-        for (int i = 0; i < 4 && 4 * q + i < L.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+    uint32_t packed[RQ];
+#pragma unroll
+    for (int k = 0; k < RQ; k++) {
+        const int dy = min(rg * RQ + k, L.h - 1);   // rows past the level repeat the last one (not stored)
+        const int2 rc = L.rcoef[dy];
+        const int sy = rc.x;
+        const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
+        const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
+        packed[k] = pyr_quad(src + (size_t)ry0 * spitch, src + (size_t)ry1 * spitch, cq, (int)(short)(rc.y & 0xFFFF),
+                             rc.y >> 16, snw);
+    }
+    uint8_t* o = pyr + L.pyr_off + (size_t)f * L.frame_bytes + 4 * q;
+#pragma unroll
+    for (int k = 0; k < RQ; k++) {
+        const int dy = rg * RQ + k;
+        if (dy >= L.h) break;
+        uint8_t* od = o + (size_t)dy * L.pitch;
+        if (4 * q + 4 <= L.w) {
+            *reinterpret_cast<uint32_t*>(od) = packed[k];
+        } else {
+            for (int i = 0; i < 4 && 4 * q + i < L.w; i++) od[i] = (uint8_t)(packed[k] >> (8 * i));
+        }
     }
 }
 
