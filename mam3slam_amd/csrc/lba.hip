@@ -628,17 +628,21 @@ __global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
 }
 
 // ---- Schur
-// D = H_ll + lambda I (setLambda, block_solver.hpp:563-589) and its inverse (Eigen's 3x3 cofactor inverse, :389)
+// D = H_ll + lambda I (setLambda, block_solver.hpp:563-589) and its inverse (Eigen's 3x3 inverse, :389)
 __device__ __forceinline__ void point_dinv(const Prob& d, int h, double lambda, double Di[9]) {
-    double D[9];
-    for (int k = 0; k < 9; k++) D[k] = d.Hll[9 * (size_t)h + k] + ((k % 4 == 0) ? lambda : 0.0);
-    const double c00 = D[4] * D[8] - D[5] * D[7], c01 = D[5] * D[6] - D[3] * D[8], c02 = D[3] * D[7] - D[4] * D[6];
-    const double det = D[0] * c00 + D[1] * c01 + D[2] * c02;
-    Di[0] = c00 / det; Di[3] = c01 / det; Di[6] = c02 / det;
-    Di[1] = (D[2] * D[7] - D[1] * D[8]) / det; Di[4] = (D[0] * D[8] - D[2] * D[6]) / det;
-    Di[7] = (D[1] * D[6] - D[0] * D[7]) / det;
-    Di[2] = (D[1] * D[5] - D[2] * D[4]) / det; Di[5] = (D[2] * D[3] - D[0] * D[5]) / det;
-    Di[8] = (D[0] * D[4] - D[1] * D[3]) / det;
+    double m[9];
+    for (int k = 0; k < 9; k++) m[k] = d.Hll[9 * (size_t)h + k] + ((k % 4 == 0) ? lambda : 0.0);
+    double* o = Di;
+    // Eigen 3.4 compute_inverse<3> (LU/InverseImpl.h): the column-0 cofactors, det = their dot with column 0
+    // summed c0 m00 + (c1 m10 + c2 m20) (the unrolled redux of a 3-vector, as camera.hpp inv3), invdet = 1 / det, result(r, c) = cofactor(c, r) * invdet
+    const double c00 = m[4] * m[8] - m[5] * m[7], c10 = m[7] * m[2] - m[8] * m[1], c20 = m[1] * m[5] - m[2] * m[4];
+    const double det = c00 * m[0] + (c10 * m[3] + c20 * m[6]);
+    const double inv = 1.0 / det;
+    o[0] = c00 * inv; o[1] = c10 * inv; o[2] = c20 * inv;
+    o[3] = (m[5] * m[6] - m[3] * m[8]) * inv; o[4] = (m[8] * m[0] - m[6] * m[2]) * inv;
+    o[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
+    o[6] = (m[3] * m[7] - m[4] * m[6]) * inv; o[7] = (m[6] * m[1] - m[7] * m[0]) * inv;
+    o[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
 }
 
 // grid (ceil(max(E, L)/64), Q) x 64: one wave per 64 edges (block_solver.hpp:405-427): the edge's point D^-1 (the

@@ -179,13 +179,16 @@ struct Graph {
     }
 
     static bool inv3(const double m[9], double o[9]) {
-        const double c00 = m[4] * m[8] - m[5] * m[7], c01 = m[5] * m[6] - m[3] * m[8], c02 = m[3] * m[7] - m[4] * m[6];
-        const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
-        o[0] = c00 / det; o[3] = c01 / det; o[6] = c02 / det;
-        o[1] = (m[2] * m[7] - m[1] * m[8]) / det; o[4] = (m[0] * m[8] - m[2] * m[6]) / det;
-        o[7] = (m[1] * m[6] - m[0] * m[7]) / det;
-        o[2] = (m[1] * m[5] - m[2] * m[4]) / det; o[5] = (m[2] * m[3] - m[0] * m[5]) / det;
-        o[8] = (m[0] * m[4] - m[1] * m[3]) / det;
+        // Eigen 3.4 compute_inverse<3> (LU/InverseImpl.h): the column-0 cofactors, det = their dot with column 0
+        // summed c0 m00 + (c1 m10 + c2 m20) (the unrolled redux of a 3-vector, as camera.hpp inv3), invdet = 1 / det, result(r, c) = cofactor(c, r) * invdet
+        const double c00 = m[4] * m[8] - m[5] * m[7], c10 = m[7] * m[2] - m[8] * m[1], c20 = m[1] * m[5] - m[2] * m[4];
+        const double det = c00 * m[0] + (c10 * m[3] + c20 * m[6]);
+        const double inv = 1.0 / det;
+        o[0] = c00 * inv; o[1] = c10 * inv; o[2] = c20 * inv;
+        o[3] = (m[5] * m[6] - m[3] * m[8]) * inv; o[4] = (m[8] * m[0] - m[6] * m[2]) * inv;
+        o[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
+        o[6] = (m[3] * m[7] - m[4] * m[6]) * inv; o[7] = (m[6] * m[1] - m[7] * m[0]) * inv;
+        o[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
         return true;
     }
 
