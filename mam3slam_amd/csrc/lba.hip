@@ -775,10 +775,11 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
 // changes nothing and every panel is full). Per panel:
 //   (1) wave 0 factors the 16x16 diagonal block in registers: lane i owns row i, the pivot row is read with
 //       v_readlane (uniform), and solves the block of the forward substitution L11 y1 = y1;
-//   (2) every thread takes one panel row: L21 = A21 L11^-T D^-1, W21 = L21 D (staged transposed in the panel
-//       workspace for the trailing update) and the fused forward-substitution update y2 -= L21 y1;
-//   (3) the trailing lower triangle A22 -= L21 W21^T in 16x16 blocks, one wave each, as f64 MFMAs
-//       (v_mfma_f64_16x16x4_f64) with both operands from the workspace.
+//   (2) every thread takes one panel row: L21 = A21 L11^-T D^-1 (staged transposed in the panel workspace for the
+//       trailing update) and the fused forward-substitution update y2 -= L21 y1;
+//   (3) the trailing lower triangle A22 -= L21 D L21^T in 16x16 blocks, one wave each, as f64 MFMAs
+//       (v_mfma_f64_16x16x4_f64) with both operands from the workspace; the next block column goes to an LDS
+//       buffer that (1) and (2) of the next panel read.
 // An exact zero pivot sets lm.fail (the failure rule of Eigen's SimplicialLDLT) and skips the solve.
 // Then y /= D and the backward substitution L^T x = y, block by block, each thread updating its own y_i.
 // The workspace (panel + y) is LDS when it fits (use_lds), else the problem's global scratch.
@@ -906,13 +907,18 @@ __global__ __launch_bounds__(1024) void k_struct_tiles(const Prob* __restrict__ 
 }
 
 
-// workspace doubles: PL and PW (NB x (npad - NB) each) + y (npad)
+// workspace doubles: the panel PL (NB x (npad - NB), L21 transposed), the block column CB (NB x (npad + 1),
+// column-major with an odd stride) and y (npad)
+__host__ __device__ inline int ldlt_cb_stride(int npad) { return npad + 1; }
 __host__ __device__ inline size_t ldlt_ws_doubles(int npad) {
     const int m = npad > NB ? npad - NB : 0;
-    return (size_t)2 * NB * (size_t)m + (size_t)npad;
+    return (size_t)NB * (size_t)m + (size_t)NB * (size_t)ldlt_cb_stride(npad) + (size_t)npad;
 }
 __host__ __device__ inline size_t ldlt_lds_bytes(int npad) { return ldlt_ws_doubles(npad) * sizeof(double); }
 
+// S in the global address space: flat accesses would count in lgkmcnt too, so every LDS wait would also wait for the
+// A loads in flight (the prefetches across the panel rows)
+typedef __attribute__((address_space(1))) double gdouble;
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned long long u = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), l);
@@ -920,33 +926,42 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-// wave 0: LDL^T of the 16x16 diagonal block at kb (final on entry), written back to A (L below, D on the diagonal),
-// plus Ld (L11, row-major), dk / invdk (D and 1/D) for the panel rows, and the forward block solve of y.
-__device__ __forceinline__ void ldlt_diag(double* A, int N, int kb, double* Y, double* Ld, double* dk, double* invdk,
-                                          int* fail, int lane) {
+// wave 0: LDL^T of the 16x16 diagonal block at kb, read from the block-column buffer (CB[c * cs + r] = A(kb + r,
+// kb + c), final), written back to A (L below, D on the diagonal), plus Ld (L11, row-major), dk / invdk (D and 1/D)
+// for the panel rows and the trailing update, and the forward block solve of y.
+__device__ __forceinline__ void ldlt_diag(gdouble* A, int N, int kb, const double* CB, int cs, double* Y, double* Ld,
+                                          double* dk, double* invdk, int* fail, int lane) {
     double row[NB];
 #pragma unroll
-    for (int c = 0; c < NB; c++) row[c] = lane < NB ? A[(size_t)(kb + lane) * N + kb + c] : 0.0;
+    for (int c = 0; c < NB; c++) row[c] = lane < NB ? CB[(size_t)c * cs + lane] : 0.0;
+    // step j: A(r, k) -= L(r, j) a(k, j) with a(k, j) = L(k, j) D(j) the column before scaling, so its broadcast
+    // (read-lanes) does not wait for the pivot's reciprocal; every lane updates every k > j without a mask — the
+    // entries above the diagonal become don't-care values that nothing reads (lower triangle and diagonal only)
     double dmine = 1.0;
 #pragma unroll
     for (int j = 0; j < NB; j++) {
         const double dj = readlane_d(row[j], j);
+        double akj[NB];
+#pragma unroll
+        for (int k = j + 1; k < NB; k++) akj[k] = readlane_d(row[j], k);
         if (lane == j) dmine = dj;
-        const double inv = dj != 0.0 ? 1.0 / dj : 0.0;
+        // the pivot's reciprocal by v_rcp_f64 and two Newton steps (within an ulp of 1/dj; the divide's scale /
+        // fixup steps guard denormal and huge pivots, which a damped system's diagonal does not have) — it is the
+        // serial part of every step
+        double inv = __builtin_amdgcn_rcp(dj);
+        inv = fma(inv, fma(-dj, inv, 1.0), inv);
+        inv = fma(inv, fma(-dj, inv, 1.0), inv);
+        if (dj == 0.0) inv = 0.0;
         const double l = row[j] * inv;
         if (lane > j) row[j] = l;
-        const double ldj = l * dj;
 #pragma unroll
-        for (int k = j + 1; k < NB; k++) {
-            const double lk = readlane_d(l, k);
-            if (k <= lane) row[k] -= ldj * lk;
-        }
+        for (int k = j + 1; k < NB; k++) row[k] = fma(-l, akj[k], row[k]);
     }
     double yv = lane < NB ? Y[kb + lane] : 0.0;
 #pragma unroll
     for (int j = 0; j < NB; j++) {
         const double yj = readlane_d(yv, j);
-        if (lane > j) yv -= row[j] * yj;
+        if (lane > j) yv = fma(-row[j], yj, yv);
     }
     if (lane < NB) {
 #pragma unroll
@@ -962,15 +977,18 @@ __device__ __forceinline__ void ldlt_diag(double* A, int N, int kb, double* Y, d
     }
 }
 
-// One wave: NT 16x16 blocks (br[t], bc[t]) of A22 (block indices relative to row/col kb + NB) -= L21 W21^T, each as
-// four chained v_mfma_f64_16x16x4_f64 (K = 16), accumulator initialised with the A block. The NT tiles' loads are
-// issued together, so their L2 round trips overlap (the update is latency-bound at one workgroup per problem).
-// Lane maps (gfx950, f64): A operand L[R0 + (lane&15)][k0 + (lane>>4)], B operand W[C0 + (lane&15)][k0 + (lane>>4)],
-// C/D col = lane&15, row = (lane>>4) + 4 reg.
+// One wave: NT 16x16 blocks (br[t], bc[t]) (block indices relative to row/col kb + NB) -= L21 D L21^T, each as four
+// chained v_mfma_f64_16x16x4_f64 (K = 16), accumulator initialised with the A block; the B operand is the staged L21
+// scaled by D on the fly. The NT tiles' loads are issued together, so their L2 round trips overlap (the update is
+// latency-bound at one workgroup per problem). to_cb: the tiles are the next block column (bc = 0), written to the
+// block-column buffer (the next panel rows and diagonal block read them there) instead of back to A; upd = false:
+// copied there without an update.
+// Lane maps (gfx950, f64): A operand L[R0 + (lane&15)][k0 + (lane>>4)], B operand L[C0 + (lane&15)][k0 + (lane>>4)]
+// D[k0 + (lane>>4)], C/D col = lane&15, row = (lane>>4) + 4 reg.
 typedef double dbl4 __attribute__((ext_vector_type(4)));
-template <int NT>
-__device__ __forceinline__ void ldlt_tiles16(double* A, int N, int kb, const double* PL, const double* PW, int m,
-                                             const int* br, const int* bc, int lane) {
+template <int NT, bool to_cb>
+__device__ __forceinline__ void ldlt_tiles16(gdouble* A, int N, int kb, const double* PL, const double* dkp, int m,
+                                             double* CB, int cs, const int* br, const int* bc, bool upd, int lane) {
     const int col = lane & 15, rq = lane >> 4;
     dbl4 c[NT];
 #pragma unroll
@@ -979,21 +997,27 @@ __device__ __forceinline__ void ldlt_tiles16(double* A, int N, int kb, const dou
 #pragma unroll
         for (int r = 0; r < 4; r++) c[u][r] = A[(size_t)(R0 + rq + 4 * r) * N + C0 + col];
     }
+    if (upd) {
 #pragma unroll
-    for (int k0 = 0; k0 < NB; k0 += 4) {
-        const int k = k0 + rq;
+        for (int k0 = 0; k0 < NB; k0 += 4) {
+            const int k = k0 + rq;
+            const double dkk = dkp[k];
 #pragma unroll
-        for (int u = 0; u < NT; u++) {
-            const double av = -PL[(size_t)k * m + 16 * br[u] + col];
-            const double bv = PW[(size_t)k * m + 16 * bc[u] + col];
-            c[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c[u], 0, 0, 0);
+            for (int u = 0; u < NT; u++) {
+                const double av = -PL[(size_t)k * m + 16 * br[u] + col];
+                const double bv = PL[(size_t)k * m + 16 * bc[u] + col] * dkk;
+                c[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c[u], 0, 0, 0);
+            }
         }
     }
 #pragma unroll
     for (int u = 0; u < NT; u++) {
         const int R0 = kb + NB + 16 * br[u], C0 = kb + NB + 16 * bc[u];
 #pragma unroll
-        for (int r = 0; r < 4; r++) A[(size_t)(R0 + rq + 4 * r) * N + C0 + col] = c[u][r];
+        for (int r = 0; r < 4; r++) {
+            if (to_cb) CB[(size_t)col * cs + 16 * br[u] + rq + 4 * r] = c[u][r];
+            else A[(size_t)(R0 + rq + 4 * r) * N + C0 + col] = c[u][r];
+        }
     }
 }
 
@@ -1003,21 +1027,22 @@ __device__ __forceinline__ void ldlt_tiles16(double* A, int N, int kb, const dou
 #define MAM_LDLT_BATCH 4
 #endif
 constexpr int LDLT_BATCH = MAM_LDLT_BATCH;
+template <bool to_cb>
 struct TileQueue {
     int br[LDLT_BATCH], bc[LDLT_BATCH];
     int n = 0;
-    __device__ __forceinline__ void push(double* A, int N, int kb, const double* PL, const double* PW, int m, int r,
-                                         int c, int lane) {
+    __device__ __forceinline__ void push(gdouble* A, int N, int kb, const double* PL, const double* dkp, int m,
+                                         double* CB, int cs, int r, int c, int lane) {
         br[n] = r;
         bc[n] = c;
         if (++n == LDLT_BATCH) {
-            ldlt_tiles16<LDLT_BATCH>(A, N, kb, PL, PW, m, br, bc, lane);
+            ldlt_tiles16<LDLT_BATCH, to_cb>(A, N, kb, PL, dkp, m, CB, cs, br, bc, true, lane);
             n = 0;
         }
     }
-    __device__ __forceinline__ void flush(double* A, int N, int kb, const double* PL, const double* PW, int m,
-                                          int lane) {
-        for (int u = 0; u < n; u++) ldlt_tiles16<1>(A, N, kb, PL, PW, m, br + u, bc + u, lane);
+    __device__ __forceinline__ void flush(gdouble* A, int N, int kb, const double* PL, const double* dkp, int m,
+                                          double* CB, int cs, int lane) {
+        for (int u = 0; u < n; u++) ldlt_tiles16<1, to_cb>(A, N, kb, PL, dkp, m, CB, cs, br + u, bc + u, true, lane);
         n = 0;
     }
 };
@@ -1048,8 +1073,15 @@ __device__ unsigned long long g_lprof[8];
     } while (0)
 #endif
 
-// grid (Q): with lookahead — after a panel's rows (B), the next block column is updated first (C1); then wave 0
-// factors the next diagonal block while the other waves update the rest of the trailing matrix (C2).
+// grid (Q): with lookahead — after a panel's rows (B), the next block column is updated first (C1) into the
+// block-column buffer CB (so the next diagonal block and panel rows read it from LDS, not back from A); then wave 0
+// factors the next diagonal block while the other waves update the rest of the trailing matrix (C2). dk alternates
+// between two slots: C2's trailing update reads the panel's D while wave 0 writes the next one.
+#ifndef MAM_LDLT_C1_PF
+#define MAM_LDLT_C1_PF 3
+#endif
+constexpr int C1_PF = MAM_LDLT_C1_PF;   // (C1) tiles per wave prefetched across (B)
+constexpr int LDLT_TM_MAX = 40;         // the LDS path's tile-mask copy: nt <= 40 (npad <= 640)
 template <bool use_lds>
 __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
     extern __shared__ __attribute__((aligned(16))) double lds_ws[];
@@ -1062,43 +1094,74 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
         if (t == 0) lm.fail = 0;
         return;
     }
-    double* A = d.S;
+    gdouble* A = (gdouble*)d.S;   // global address space: its loads must not count in lgkmcnt (flat)
     double* ws = use_lds ? lds_ws : d.ws;
-    double* Y = ws + (size_t)2 * NB * (N - NB);
+    const int cs = ldlt_cb_stride(N);
+    double* PL = ws;
+    double* CB = ws + (size_t)NB * (N - NB);
+    double* Y = CB + (size_t)NB * cs;
     __shared__ double Ld[NB * NB];
-    __shared__ double dk[NB];
+    __shared__ double dk[2][NB];
     __shared__ double invdk[NB];
     __shared__ int fail;
+    // the tile mask: the phases below test it before their loads, so its reads sit on their critical paths
+    __shared__ uint8_t tm_lds[use_lds ? LDLT_TM_MAX * LDLT_TM_MAX : 1];
+    const uint8_t* tmask = use_lds ? tm_lds : d.tmask;
 #ifdef MAM_LDLT_PROFILE
     long long lp0 = clock64();
 #endif
     if (t == 0) fail = 0;
+    if (use_lds)
+        for (int q = t; q < d.nt * d.nt; q += LDLT_THREADS) tm_lds[q] = d.tmask[q];
     for (int i = t; i < N; i += LDLT_THREADS) {
         Y[i] = i < n ? d.bs[i] : 0.0;
         if (i >= n) A[(size_t)i * N + i] = 1.0;
     }
     __syncthreads();
-    if (wid == 0) ldlt_diag(A, N, 0, Y, Ld, dk, invdk, &fail, lane);
+    // block column 0 into CB (its non-zero tiles)
+    for (int i = t; i < N; i += LDLT_THREADS) {
+        if (!tmask[(size_t)(i / NB) * d.nt]) continue;
+#pragma unroll
+        for (int j = 0; j < NB; j++) CB[(size_t)j * cs + i] = A[(size_t)i * N + j];
+    }
+    __syncthreads();
+    if (wid == 0) ldlt_diag(A, N, 0, CB, cs, Y, Ld, dk[0], invdk, &fail, lane);
     __syncthreads();
     LPROF(0);
-    for (int kb = 0; kb < N; kb += NB) {
-        // (B) panel rows: L21 = A21 L11^-T D^-1, W21 = L21 D (staged transposed), y2 -= L21 y1
+    for (int kb = 0, p = 0; kb < N; kb += NB, p ^= 1) {
+        // (B) panel rows: L21 = A21 L11^-T D^-1 (into A and, transposed, into PL), y2 -= L21 y1; A21 from CB
         const int m = N - kb - NB;
         const int kc = kb / NB;
-        const uint8_t* tcol = d.tmask + kc;   // tcol[r * nt]: tile (r, kc) of L non-zero
-        double* PL = ws;
-        double* PW = ws + (size_t)NB * m;
-        for (int i = kb + NB + t; i < N; i += LDLT_THREADS) {
-            if (!tcol[(size_t)(i / NB) * d.nt]) continue;   // structurally zero row of L21: no update, no y change
+        const uint8_t* tcol = tmask + kc;   // tcol[r * nt]: tile (r, kc) of L non-zero
+        const uint8_t* ncol = tmask + kc + 1;   // tile (r, kc + 1) of L non-zero
+        const double* dkp = dk[p];
+        const int T16 = m / 16;
+        const int i0 = kb + NB + t;
+        const bool row0 = i0 < N && tcol[(size_t)(i0 / NB) * d.nt];
+        // (C1)'s first tiles of this wave (br = wid + 8 u), loaded from A before (B): their L2 round trip overlaps it
+        const int col16 = lane & 15, rq = lane >> 4;
+        dbl4 pc[C1_PF];
+#pragma unroll
+        for (int u = 0; u < C1_PF; u++) {
+            const int br = wid + (LDLT_THREADS / 64) * u;
+            if (br < T16 && ncol[(size_t)(kc + 1 + br) * d.nt]) {
+                const int R0 = kb + NB + 16 * br, C0 = kb + NB;
+#pragma unroll
+                for (int r = 0; r < 4; r++) pc[u][r] = A[(size_t)(R0 + rq + 4 * r) * N + C0 + col16];
+            }
+        }
+        for (int i = i0; i < N; i += LDLT_THREADS) {
+            // structurally zero row of L21: no update, no y change
+            if (!(i == i0 ? row0 : tcol[(size_t)(i / NB) * d.nt] != 0)) continue;
             // keep the L11 factors in LDS (reading them per row): hoisting all 120 into registers spills
             asm volatile("" ::: "memory");
             double w[NB];
 #pragma unroll
-            for (int j = 0; j < NB; j++) w[j] = A[(size_t)i * N + kb + j];
+            for (int j = 0; j < NB; j++) w[j] = CB[(size_t)j * cs + (i - kb)];
 #pragma unroll
             for (int j = 1; j < NB; j++) {
 #pragma unroll
-                for (int k = 0; k < j; k++) w[j] -= w[k] * Ld[j * NB + k];
+                for (int k = 0; k < j; k++) w[j] = fma(-w[k], Ld[j * NB + k], w[j]);
             }
             double yi = Y[i];
 #pragma unroll
@@ -1106,22 +1169,44 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
                 const double lij = w[j] * invdk[j];
                 A[(size_t)i * N + kb + j] = lij;
                 PL[(size_t)j * m + (i - kb - NB)] = lij;
-                PW[(size_t)j * m + (i - kb - NB)] = w[j];
-                yi -= lij * Y[kb + j];
+                yi = fma(-lij, Y[kb + j], yi);
             }
             Y[i] = yi;
         }
         __syncthreads();
         LPROF(1);
         if (m == 0) break;
-        const int T16 = m / 16;
-        // (C1) the next block column: blocks (br, 0), one wave each
-        const bool c1nz = tcol[(size_t)(kc + 1) * d.nt] != 0;
-        if (c1nz) {
-            TileQueue tq;
-            for (int br = wid; br < T16; br += LDLT_THREADS / 64)
-                if (tcol[(size_t)(kc + 1 + br) * d.nt]) tq.push(A, N, kb, PL, PW, m, br, 0, lane);
-            tq.flush(A, N, kb, PL, PW, m, lane);
+        // (C1) the next block column into CB: its non-zero tiles (br, 0), one wave each, updated where L(kc + 1 + br,
+        // kc) and L(kc + 1, kc) are non-zero, copied otherwise
+        {
+            const bool c1nz = tcol[(size_t)(kc + 1) * d.nt] != 0;
+#pragma unroll
+            for (int u = 0; u < C1_PF; u++) {
+                const int br = wid + (LDLT_THREADS / 64) * u;
+                if (br >= T16 || !ncol[(size_t)(kc + 1 + br) * d.nt]) continue;
+                if (c1nz && tcol[(size_t)(kc + 1 + br) * d.nt]) {
+#pragma unroll
+                    for (int k0 = 0; k0 < NB; k0 += 4) {
+                        const int k = k0 + rq;
+                        const double av = -PL[(size_t)k * m + 16 * br + col16];
+                        const double bv = PL[(size_t)k * m + col16] * dkp[k];
+                        pc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, pc[u], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) CB[(size_t)col16 * cs + 16 * br + rq + 4 * r] = pc[u][r];
+            }
+            TileQueue<true> tq;
+            for (int br = wid + (LDLT_THREADS / 64) * C1_PF; br < T16; br += LDLT_THREADS / 64) {
+                if (!ncol[(size_t)(kc + 1 + br) * d.nt]) continue;
+                if (c1nz && tcol[(size_t)(kc + 1 + br) * d.nt]) {
+                    tq.push(A, N, kb, PL, dkp, m, CB, cs, br, 0, lane);
+                } else {
+                    const int z = 0;
+                    ldlt_tiles16<1, true>(A, N, kb, PL, dkp, m, CB, cs, &br, &z, false, lane);
+                }
+            }
+            tq.flush(A, N, kb, PL, dkp, m, CB, cs, lane);
         }
         __syncthreads();
         LPROF(2);
@@ -1130,21 +1215,21 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
 #ifdef MAM_LDLT_PROFILE
             const long long td = clock64();
 #endif
-            ldlt_diag(A, N, kb + NB, Y, Ld, dk, invdk, &fail, lane);
+            ldlt_diag(A, N, kb + NB, CB, cs, Y, Ld, dk[p ^ 1], invdk, &fail, lane);
 #ifdef MAM_LDLT_PROFILE
             if (lane == 0) atomicAdd(&g_lprof[5], (unsigned long long)(clock64() - td));
 #endif
         } else {
             const int T2 = T16 - 1;
             const int n2 = T2 * (T2 + 1) / 2;
-            TileQueue tq;
+            TileQueue<false> tq;
             for (int q = wid - 1; q < n2; q += LDLT_THREADS / 64 - 1) {
                 int tr, tc;
                 tri_index(q, &tr, &tc);
                 if (tcol[(size_t)(kc + 2 + tr) * d.nt] && tcol[(size_t)(kc + 2 + tc) * d.nt])
-                    tq.push(A, N, kb, PL, PW, m, tr + 1, tc + 1, lane);
+                    tq.push(A, N, kb, PL, dkp, m, CB, cs, tr + 1, tc + 1, lane);
             }
-            tq.flush(A, N, kb, PL, PW, m, lane);
+            tq.flush(A, N, kb, PL, dkp, m, CB, cs, lane);
         }
         __syncthreads();
         LPROF(3);
@@ -1156,6 +1241,12 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
     __syncthreads();
     // backward substitution L^T x = y: block solve by wave 0, then each thread i < kb updates its own y_i
     for (int kb = N - NB; kb >= 0; kb -= NB) {
+        const bool pre = t < kb && tmask[(size_t)(kb / NB) * d.nt + t / NB];   // L(kb.., t) not structurally zero
+        double a[NB];
+        if (pre) {
+#pragma unroll
+            for (int j = 0; j < NB; j++) a[j] = A[(size_t)(kb + j) * N + t];
+        }
         if (wid == 0) {
             double col[NB];   // lane c holds L(kb + j, kb + c) for j > c
 #pragma unroll
@@ -1164,16 +1255,23 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
 #pragma unroll
             for (int j = NB - 1; j >= 0; j--) {
                 const double xj = readlane_d(v, j);
-                if (lane < j) v -= col[j] * xj;
+                if (lane < j) v = fma(-col[j], xj, v);
             }
             if (lane < NB) Y[kb + lane] = v;
         }
         __syncthreads();
-        for (int i = t; i < kb; i += LDLT_THREADS) {
-            if (!d.tmask[(size_t)(kb / NB) * d.nt + i / NB]) continue;   // L(kb.., i) structurally zero
+        // the first row's L column was loaded before the barrier, beside the block solve
+        if (pre) {
+            double sy = Y[t];
+#pragma unroll
+            for (int j = 0; j < NB; j++) sy = fma(-a[j], Y[kb + j], sy);
+            Y[t] = sy;
+        }
+        for (int i = t + LDLT_THREADS; i < kb; i += LDLT_THREADS) {
+            if (!tmask[(size_t)(kb / NB) * d.nt + i / NB]) continue;   // L(kb.., i) structurally zero
             double sy = Y[i];
 #pragma unroll
-            for (int j = 0; j < NB; j++) sy -= A[(size_t)(kb + j) * N + i] * Y[kb + j];
+            for (int j = 0; j < NB; j++) sy = fma(-A[(size_t)(kb + j) * N + i], Y[kb + j], sy);
             Y[i] = sy;
         }
         __syncthreads();
@@ -1523,6 +1621,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         max_lds = std::max(max_lds, ldlt_lds_bytes(d.npad));
     }
     if (max_lds > c->ldlt_lds_budget) lds_ok = false;
+    if (ldlt_pad(6 * maxNp) / NB > LDLT_TM_MAX) lds_ok = false;   // the LDS path keeps the tile mask in LDS too
     // size bounds before any allocation: the dense pose x landmark edge table (Np L int32) and S (npad^2 f64) of one
     // problem stay under 4 GiB each, and the batch's scratch fits the device's free memory
     for (auto& d : hp) {
