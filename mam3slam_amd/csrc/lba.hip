@@ -774,7 +774,7 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
 // S is npad x npad (npad = 6 Np rounded up to 16; the padding is an identity block after the real unknowns, so it
 // changes nothing and every panel is full). Per panel:
 //   (1) wave 0 factors the 16x16 diagonal block in registers: lane i owns row i, the pivot row is read with
-//       v_readlane (uniform), and solves the block of the forward substitution L11 y1 = y1;
+//       a DPP broadcast within lanes 0..15, and solves the block of the forward substitution L11 y1 = y1;
 //   (2) every thread takes one panel row: L21 = A21 L11^-T D^-1 (staged transposed in the panel workspace for the
 //       trailing update) and the fused forward-substitution update y2 -= L21 y1;
 //   (3) the trailing lower triangle A22 -= L21 D L21^T in 16x16 blocks, one wave each, as f64 MFMAs
@@ -919,10 +919,22 @@ __host__ __device__ inline size_t ldlt_lds_bytes(int npad) { return ldlt_ws_doub
 // S in the global address space: flat accesses would count in lgkmcnt too, so every LDS wait would also wait for the
 // A loads in flight (the prefetches across the panel rows)
 typedef __attribute__((address_space(1))) double gdouble;
-__device__ __forceinline__ double readlane_d(double v, int l) {
+// lane k of each 16-lane row, in every lane of that row (DPP row_newbcast: a VGPR result, no SGPR round trip and none
+// of v_readlane's hazards); k a constant after unrolling
+__device__ __forceinline__ int bcast16_i(int v, int k) {
+    switch (k) {
+#define MAM_BC(n) \
+    case n: return __builtin_amdgcn_mov_dpp(v, 0x150 + n, 0xf, 0xf, false);
+        MAM_BC(0) MAM_BC(1) MAM_BC(2) MAM_BC(3) MAM_BC(4) MAM_BC(5) MAM_BC(6) MAM_BC(7)
+        MAM_BC(8) MAM_BC(9) MAM_BC(10) MAM_BC(11) MAM_BC(12) MAM_BC(13) MAM_BC(14) MAM_BC(15)
+#undef MAM_BC
+    }
+    return 0;
+}
+__device__ __forceinline__ double bcast16_d(double v, int k) {
     const unsigned long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), l);
-    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    const int lo = bcast16_i((int)(u & 0xffffffffu), k);
+    const int hi = bcast16_i((int)(u >> 32), k);
     return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
@@ -935,15 +947,15 @@ __device__ __forceinline__ void ldlt_diag(gdouble* A, int N, int kb, const doubl
 #pragma unroll
     for (int c = 0; c < NB; c++) row[c] = lane < NB ? CB[(size_t)c * cs + lane] : 0.0;
     // step j: A(r, k) -= L(r, j) a(k, j) with a(k, j) = L(k, j) D(j) the column before scaling, so its broadcast
-    // (read-lanes) does not wait for the pivot's reciprocal; every lane updates every k > j without a mask — the
+    // (DPP broadcasts within lanes 0..15) does not wait for the pivot's reciprocal; every lane updates every k > j without a mask — the
     // entries above the diagonal become don't-care values that nothing reads (lower triangle and diagonal only)
     double dmine = 1.0;
 #pragma unroll
     for (int j = 0; j < NB; j++) {
-        const double dj = readlane_d(row[j], j);
+        const double dj = bcast16_d(row[j], j);
         double akj[NB];
 #pragma unroll
-        for (int k = j + 1; k < NB; k++) akj[k] = readlane_d(row[j], k);
+        for (int k = j + 1; k < NB; k++) akj[k] = bcast16_d(row[j], k);
         if (lane == j) dmine = dj;
         // the pivot's reciprocal by v_rcp_f64 and two Newton steps (within an ulp of 1/dj; the divide's scale /
         // fixup steps guard denormal and huge pivots, which a damped system's diagonal does not have) — it is the
@@ -960,7 +972,7 @@ __device__ __forceinline__ void ldlt_diag(gdouble* A, int N, int kb, const doubl
     double yv = lane < NB ? Y[kb + lane] : 0.0;
 #pragma unroll
     for (int j = 0; j < NB; j++) {
-        const double yj = readlane_d(yv, j);
+        const double yj = bcast16_d(yv, j);
         if (lane > j) yv = fma(-row[j], yj, yv);
     }
     if (lane < NB) {
@@ -1254,7 +1266,7 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
             double v = lane < NB ? Y[kb + lane] : 0.0;
 #pragma unroll
             for (int j = NB - 1; j >= 0; j--) {
-                const double xj = readlane_d(v, j);
+                const double xj = bcast16_d(v, j);
                 if (lane < j) v = fma(-col[j], xj, v);
             }
             if (lane < NB) Y[kb + lane] = v;
