@@ -477,8 +477,9 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
     res = {"value": 1e3 / per_frame_ms, "unit": "frames/s", "cores": 1, "kind": "port",
            "tracking_ms_per_frame": track_ms,
            "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15) + "
-                     f"isInFrustum + SearchByProjection(local map, th 1) on the oracle C++ restatement, single thread, "
-                     f"{el:.1f}s"}
+                     f"isInFrustum + SearchByProjection(local map, th 1) on the oracle C++ restatement "
+                     f"(g++ -O3 -march=x86-64-v3, the reference's CMake -O3 -march=native level; scalar), "
+                     f"single thread, {el:.1f}s"}
     if lba_window_ms is not None:
         res["lba_ms_per_window"] = lba_window_ms
         res["sample"] += f"; + LocalBundleAdjustment of a timed-region window ({lba_window_ms:.1f} ms) / {K} frames"
