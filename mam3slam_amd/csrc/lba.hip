@@ -81,7 +81,7 @@ struct Prob {
     int32_t* qe_off;             // per Hessian pose: edges (edge order)
     int32_t* qe_idx;
     int32_t* cnt;                // [L + Np] counters / cursors of the device structure build
-    int32_t* eidx;               // [Np][L] edge of (pose block, point), -1 if none
+    int32_t* eidx;               // [Np][L] edge of (pose block, point), never cleared: read through eidx_at
     uint8_t* pairmask;           // [Np][Np] (i1 < i2): the two poses share a landmark (S block non-zero)
     int32_t* blk_off;            // [Np * Np + 1] start of block (i1, i2)'s landmark pairs in blk_pair (i1 <= i2)
     int2* blk_pair;              // (edge of pose i1, edge of pose i2) per shared landmark, i2's edge order
@@ -237,23 +237,37 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
 }
 
 // ================================================================================== device structure build
+// The structure kernels run 256-thread workgroups: under the tracking load a 1024-thread workgroup waits for a CU
+// with 16 free wave slots (their one-workgroup-per-problem scans took ~0.4 ms each beside tracking, µs alone).
+constexpr int SB = 256;
+// the pose x point table entry of (pose block h, point ip): the edge it holds when that edge really joins them, else
+// -1 (the table is never cleared, so an entry left from an earlier problem in the arena is rejected here)
+__device__ __forceinline__ int eidx_at(const Prob& d, const int32_t* row, int h, int ip) {
+    const int e = row[ip];
+    return ((unsigned)e < (unsigned)d.E && d.edge_point[e] == ip && d.pose_h[d.edge_pose[e]] == h) ? e : -1;
+}
+
 // For problems whose arrays are already in HBM (mam_lba_solve_batch_device): poses and points come in ascending id
 // order (g2o's Hessian order, sparse_optimizer.cpp:166-190), so the pose blocks are a prefix count of the non-fixed
 // poses and the point blocks are the identity; the per-point / per-pose edge lists (edge order) and the pose x point
 // edge table are built here.
 
-// grid (32, Q) x 1024: block 0 scans pose_fixed -> pose_h / hpose; every block clears counters, eidx and S and seeds
-// the state buffers (SE3Quat(q, t) normalises: w >= 0, unit).
-__global__ __launch_bounds__(1024) void k_struct_init(const Prob* __restrict__ probs) {
+// grid (8, Q) x SB: block 0 scans pose_fixed -> pose_h / hpose; every block clears the counters, the pair mask
+// and S's padding rows and seeds the state buffers (SE3Quat(q, t) normalises: w >= 0, unit). Neither the pose x point
+// table nor the rest of S is cleared: a table entry is trusted only when it names an edge of that pose and point
+// (eidx_at), and k_schur_blk writes every lower-triangle block of S each trial, the only part the factorization reads
+// (its padding rows, below the identity block, stay the zeros written here). Under the tracking load these clears
+// were ~1.4 MB per window of writes from workgroups waiting for CUs.
+__global__ __launch_bounds__(SB) void k_struct_init(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     if (d.lm->status) return;
     const int t = threadIdx.x;
-    const int gstride = gridDim.x * 1024, g0 = blockIdx.x * 1024 + t;
+    const int gstride = gridDim.x * SB, g0 = blockIdx.x * SB + t;
     if (blockIdx.x == 0) {
-        __shared__ int wsum[16];
-        // pose_h: prefix count of non-fixed poses, P <= 1024 per pass
+        __shared__ int wsum[SB / 64];
+        // pose_h: prefix count of non-fixed poses, SB per pass
         int base = 0;
-        for (int c0 = 0; c0 < d.P; c0 += 1024) {
+        for (int c0 = 0; c0 < d.P; c0 += SB) {
             const int i = c0 + t;
             const int nf = (i < d.P && !d.pose_fixed[i]) ? 1 : 0;
             int v = nf;
@@ -265,7 +279,7 @@ __global__ __launch_bounds__(1024) void k_struct_init(const Prob* __restrict__ p
             if (lane_id() == 63) wsum[t >> 6] = v;
             __syncthreads();
             int pre = 0, tot = 0;
-            for (int w = 0; w < 16; w++) {
+            for (int w = 0; w < SB / 64; w++) {
                 if (w < (t >> 6)) pre += wsum[w];
                 tot += wsum[w];
             }
@@ -279,9 +293,9 @@ __global__ __launch_bounds__(1024) void k_struct_init(const Prob* __restrict__ p
         }
     }
     for (int i = g0; i < d.L + d.Np; i += gstride) d.cnt[i] = 0;
-    for (size_t i = g0; i < (size_t)d.Np * d.L; i += gstride) d.eidx[i] = -1;
     for (size_t i = g0; i < (size_t)d.Np * d.Np; i += gstride) d.pairmask[i] = 0;
-    for (size_t i = g0; i < (size_t)d.npad * d.npad; i += gstride) d.S[i] = 0.0;
+    const size_t n6 = 6 * (size_t)d.Np;
+    for (size_t i = g0; i < ((size_t)d.npad - n6) * d.npad; i += gstride) d.S[n6 * d.npad + i] = 0.0;
     for (int i = g0; i < d.P; i += gstride) {
         double q[4] = {d.pose_q[4 * i], d.pose_q[4 * i + 1], d.pose_q[4 * i + 2], d.pose_q[4 * i + 3]};
         if (q[3] < 0) for (int k = 0; k < 4; k++) q[k] = -q[k];
@@ -308,12 +322,12 @@ __global__ __launch_bounds__(256) void k_struct_count(const Prob* __restrict__ p
 }
 
 __device__ void block_excl_scan(const int32_t* in, int32_t* out, int n, int32_t* total_out) {
-    __shared__ int wsum[16];
+    __shared__ int wsum[SB / 64];
     __shared__ int carry;
     const int t = threadIdx.x;
     if (t == 0) carry = 0;
     __syncthreads();
-    for (int c0 = 0; c0 < n; c0 += 1024) {
+    for (int c0 = 0; c0 < n; c0 += SB) {
         const int i = c0 + t;
         const int a = i < n ? in[i] : 0;
         int v = a;
@@ -325,7 +339,7 @@ __device__ void block_excl_scan(const int32_t* in, int32_t* out, int n, int32_t*
         if (lane_id() == 63) wsum[t >> 6] = v;
         __syncthreads();
         int pre = 0, tot = 0;
-        for (int w = 0; w < 16; w++) {
+        for (int w = 0; w < SB / 64; w++) {
             if (w < (t >> 6)) pre += wsum[w];
             tot += wsum[w];
         }
@@ -337,14 +351,14 @@ __device__ void block_excl_scan(const int32_t* in, int32_t* out, int n, int32_t*
     if (t == 0) *total_out = carry;
 }
 
-// grid (1, Q) x 1024: exclusive scans -> pe_off, qe_off; counters reset to be the scatter cursors
-__global__ __launch_bounds__(1024) void k_struct_scan(const Prob* __restrict__ probs) {
+// grid (1, Q) x SB: exclusive scans -> pe_off, qe_off; counters reset to be the scatter cursors
+__global__ __launch_bounds__(SB) void k_struct_scan(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     if (d.lm->status) return;
     block_excl_scan(d.cnt, d.pe_off, d.L, d.pe_off + d.L);
     block_excl_scan(d.cnt + d.L, d.qe_off, d.Np, d.qe_off + d.Np);
     __syncthreads();
-    for (int i = threadIdx.x; i < d.L + d.Np; i += 1024) d.cnt[i] = 0;
+    for (int i = threadIdx.x; i < d.L + d.Np; i += SB) d.cnt[i] = 0;
 }
 
 // grid (ceil(E/256), Q): scatter into the lists (order fixed by k_struct_sort) and the pose x point table
@@ -807,24 +821,24 @@ __global__ __launch_bounds__(64) void k_blk_count(const Prob* __restrict__ probs
     int n = 0;
     if (blk_nonzero(d, i1, i2)) {
         const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
-        for (int s = d.qe_off[i2] + lane; s < d.qe_off[i2 + 1]; s += 64) n += ei1[d.edge_point[d.qe_idx[s]]] >= 0;
+        for (int s = d.qe_off[i2] + lane; s < d.qe_off[i2 + 1]; s += 64) n += eidx_at(d, ei1, i1, d.edge_point[d.qe_idx[s]]) >= 0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
     }
     if (lane == 0) d.blk_off[bx] = n;
 }
-// grid (1, Q) x 1024: exclusive scan of the counts, the total at [Np * Np]
-__global__ __launch_bounds__(1024) void k_blk_scan(const Prob* __restrict__ probs) {
+// grid (1, Q) x SB: exclusive scan of the counts, the total at [Np * Np]
+__global__ __launch_bounds__(SB) void k_blk_scan(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     if (d.lm->status) return;
-    __shared__ int part[1024];
+    __shared__ int part[SB];
     const int n = d.Np * d.Np, t = threadIdx.x;
-    const int per = (n + 1023) / 1024, b = t * per, e = min(n, b + per);
+    const int per = (n + SB - 1) / SB, b = t * per, e = min(n, b + per);
     int sum = 0;
     for (int i = b; i < e; i++) sum += d.blk_off[i];
     part[t] = sum;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {   // inclusive Hillis-Steele
+    for (int o = 1; o < SB; o <<= 1) {   // inclusive Hillis-Steele
         const int v = t >= o ? part[t - o] : 0;
         __syncthreads();
         part[t] += v;
@@ -836,7 +850,7 @@ __global__ __launch_bounds__(1024) void k_blk_scan(const Prob* __restrict__ prob
         d.blk_off[i] = run;
         run += c;
     }
-    if (t == 1023) d.blk_off[n] = part[1023];
+    if (t == SB - 1) d.blk_off[n] = part[SB - 1];
 }
 __global__ void k_blk_total(const Prob* __restrict__ probs, int Q, int* __restrict__ out) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -860,7 +874,7 @@ __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs)
         int ec = -1, ea = -1;
         if (s < end) {
             ec = d.qe_idx[s];
-            ea = ei1[d.edge_point[ec]];
+            ea = eidx_at(d, ei1, i1, d.edge_point[ec]);
         }
         const bool hit = ea >= 0;
         const uint64_t m = __ballot(hit);
@@ -869,18 +883,18 @@ __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs)
     }
 }
 
-// grid (Q) x 1024, after k_struct_sort: the 16x16 tile pattern of L. A tile of S is non-zero when it holds a pose
+// grid (Q) x SB, after k_struct_sort: the 16x16 tile pattern of L. A tile of S is non-zero when it holds a pose
 // diagonal block or the block of two poses sharing a landmark (pairmask); the right-looking factorization then fills
 // tile (r1, r2) whenever tiles (r1, c) and (r2, c) are non-zero for some c < r2 (the symbolic LDL^T at tile
 // granularity, column by column — what SimplicialLDLT's symbolic phase does per entry, linear_solver_eigen.h:147-201).
 // Structurally zero tiles of L stay exact zeros, so k_ldlt skips them: every non-zero entry sees the same arithmetic
 // as in the dense factorization. Windows whose covisibility is banded (keyframes along a trajectory) factor in
 // O(n b^2) instead of O(n^3).
-__global__ __launch_bounds__(1024) void k_struct_tiles(const Prob* __restrict__ probs) {
+__global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.x];
     if (d.lm->status) return;
     const int nt = d.nt, n = 6 * d.Np;
-    for (int q = threadIdx.x; q < nt * nt; q += 1024) {
+    for (int q = threadIdx.x; q < nt * nt; q += SB) {
         const int r = q / nt, c = q % nt;
         uint8_t v = 0;
         if (r == c) {
@@ -898,7 +912,7 @@ __global__ __launch_bounds__(1024) void k_struct_tiles(const Prob* __restrict__ 
     __syncthreads();
     for (int c = 0; c + 1 < nt; c++) {
         const int m = nt - 1 - c;
-        for (int q = threadIdx.x; q < m * m; q += 1024) {
+        for (int q = threadIdx.x; q < m * m; q += SB) {
             const int r1 = c + 1 + q / m, r2 = c + 1 + q % m;
             if (r2 <= r1 && d.tmask[(size_t)r1 * nt + c] && d.tmask[(size_t)r2 * nt + c]) d.tmask[(size_t)r1 * nt + r2] = 1;
         }
@@ -1675,16 +1689,16 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     const dim3 gE64((maxE + EW - 1) / EW > 0 ? (maxE + EW - 1) / EW : 1, Q);
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
-        hipLaunchKernelGGL(k_struct_init, dim3(32, Q), dim3(1024), 0, s, P);
+        hipLaunchKernelGGL(k_struct_init, dim3(8, Q), dim3(SB), 0, s, P);
         hipLaunchKernelGGL(k_struct_count, gE, dim3(256), 0, s, P);
-        hipLaunchKernelGGL(k_struct_scan, dim3(1, Q), dim3(1024), 0, s, P);
+        hipLaunchKernelGGL(k_struct_scan, dim3(1, Q), dim3(SB), 0, s, P);
         hipLaunchKernelGGL(k_struct_scatter, gE, dim3(256), 0, s, P);
         hipLaunchKernelGGL(k_struct_sort, dim3(std::max(maxLb, 1), Q), dim3(256), 0, s, P);
-        hipLaunchKernelGGL(k_struct_tiles, dim3(Q), dim3(1024), 0, s, P);
+        hipLaunchKernelGGL(k_struct_tiles, dim3(Q), dim3(SB), 0, s, P);
         // the S blocks' landmark pairs: counts, offsets, one read-back of the totals to size the pair buffer
         const dim3 gB(std::max(maxNp * maxNp, 1), Q);
         hipLaunchKernelGGL(k_blk_count, gB, dim3(64), 0, s, P);
-        hipLaunchKernelGGL(k_blk_scan, dim3(1, Q), dim3(1024), 0, s, P);
+        hipLaunchKernelGGL(k_blk_scan, dim3(1, Q), dim3(SB), 0, s, P);
         if (int rc = c->blk_tot.alloc(Q)) return rc;
         if (int rc = c->blk_tot_host.alloc(sizeof(int) * (size_t)Q)) return rc;
         hipLaunchKernelGGL(k_blk_total, dim3((Q + 255) / 256), dim3(256), 0, s, P, Q, c->blk_tot.p);
