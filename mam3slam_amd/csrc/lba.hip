@@ -6,8 +6,6 @@
 //   k_linearize   per edge: map, error, chi2, Huber rho, Jacobians (OptimizableTypes.cpp:139-160), the robust-
 //                 weighted terms constructQuadraticForm needs (base_binary_edge.hpp:75-112); chi2 partial sums
 //   k_sys         per point: H_ll, b_l over its edge segment; one wave per non-fixed pose: H_pp, b_p
-//   k_ctl_begin   iteration start (levenberg.cpp:61-77, 171-185): chi2, max diag(H) (gathered by k_sys),
-//                 lambda_0 = 1e-5 max diag
 //   k_schur_prep  per point: D = H_ll + lambda I, D^-1, and per edge H_pl D^-1, H_pl D^-1 b_l (block_solver.hpp:
 //                 405-427)
 //   k_schur_blk   one wave per 6x6 block (i1 <= i2) of the reduced camera system, contributions in landmark
@@ -16,7 +14,9 @@
 //                 SimplicialLDLT), f64 MFMA trailing updates, fused forward / diagonal / backward substitution
 //   k_backsub_update  x_l = D^-1 (b_l - H_pl^T x_p) (block_solver.hpp:461-482) and the trial state:
 //                 T <- exp(dx) T (se3quat.h), X <- X + dx
-//   k_ctl_end     the trial's chi2, computeScale (partial sums from k_linearize), rho, accept (discardTop) /
+//   k_ctl_end     on an iteration's first trial the iteration-start state first (levenberg.cpp:61-77, 171-185:
+//                 chi2, lambda_0 = 1e-5 max diag(H) gathered by k_sys — the trial's kernels read lambda_0 through
+//                 trial_lambda); then the trial's chi2, computeScale (partial sums from k_linearize), rho, accept (discardTop) /
 //                 reject (pop), lambda update and the termination tests of levenberg.cpp:78-169 and
 //                 sparse_optimizer.cpp:355-420
 // Each kernel reads its problem's LM state (struct LM, device memory) and returns at once when the state says the
@@ -94,7 +94,8 @@ struct Prob {
     double* err;                 // [E][2]
     double* jac;                 // [E][21]: A(6) B(12) orr(2) wo(1)
     double* part_s;              // [ceil(E / 64) + 1] computeScale partial sums of k_linearize(trial)'s blocks
-    double* part;                // [ceil(E / 256)] rho0 partial sums of k_linearize's blocks
+    double* part;                // [ceil(E / 256)] rho0 partial sums of k_linearize's blocks (trial, initial)
+    double* part0;               // the same of k_linearize(iteration start), read by k_ctl_end's iteration-start step
     double* hpl;                 // [E][18] H_pl pose x landmark
     double* bdinv;               // [E][18] H_pl D^-1
     double* coef;                // [E][6]  H_pl D^-1 b_l
@@ -451,6 +452,14 @@ __device__ __forceinline__ void wave_copy_in(double* __restrict__ dst, const dou
     }
 }
 
+// The damping of this trial. On an iteration's first trial of the first iteration it is levenberg.cpp:71-77's
+// lambda_0 = tau * max diag(H), tau = 1e-5 (computeLambdaInit :171-185), from the max k_sys gathered (max is exact in
+// any order); k_ctl_end commits it to lm.lambda with the rest of the iteration-start state, so no control kernel runs
+// between k_sys and the Schur kernels (one launch, and one dependency wait under load, fewer per trial).
+__device__ __forceinline__ double trial_lambda(const LM& lm) {
+    return (lm.need_lin && lm.its == 0) ? 1e-5 * __longlong_as_double((long long)lm.maxdiag) : lm.lambda;
+}
+
 // grid (ceil(E/64), Q) x 64: one wave per 64 edges; the rho0 partial sum per wave (fixed-order butterfly).
 // mode 0: iteration start (Jacobians, current state); 1: trial (errors only, trial state) and the computeScale
 // partial sums; 2: initial chi2.
@@ -468,7 +477,7 @@ __global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs
                                             sh + 18 * lane)
                            : 0.0;
         r = wave_sum_d(r);
-        if (lane == 0) d.part[blockIdx.x] = r;
+        if (lane == 0) (mode == 0 ? d.part0 : d.part)[blockIdx.x] = r;
         if (mode == 0) {
             const int ne = min(EW, d.E - e0);
             __syncthreads();
@@ -480,7 +489,7 @@ __global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs
         // computeScale partials: block b < nbl sums x_j (lambda x_j + b_j) over the 64-chunks b, b + nbl, ... of x
         const int nbl = max(1, (d.E + EW - 1) / EW);
         if ((int)blockIdx.x < nbl) {
-            const double lambda = lm.lambda;
+            const double lambda = trial_lambda(lm);
             const int nx = 6 * d.Np + 3 * d.L;
             double acc = 0.0;
             for (int j = blockIdx.x * EW + lane_id(); j < nx; j += nbl * EW) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
@@ -567,7 +576,7 @@ __device__ double block_sum(const double* acc, double* s) {
 }
 
 template <int T>
-__device__ double chi_of_parts(const Prob& d, double* s) {
+__device__ double chi_of_parts(const Prob& d, const double* part, double* s) {
     // parts of 64 edges, grouped by 256 as ((p0 + p1) + p2) + p3 (a missing part adds nothing), then strided + tree
     double acc[RED / T];
     const int np = (d.E + EW - 1) / EW, nb = (d.E + 255) / 256;
@@ -575,8 +584,8 @@ __device__ double chi_of_parts(const Prob& d, double* s) {
     for (int v = 0; v < RED / T; v++) {
         acc[v] = 0.0;
         for (int b = threadIdx.x + T * v; b < nb; b += RED) {
-            double g = d.part[4 * b];
-            for (int k = 1; k < 4; k++) g = g + (4 * b + k < np ? d.part[4 * b + k] : 0.0);
+            double g = part[4 * b];
+            for (int k = 1; k < 4; k++) g = g + (4 * b + k < np ? part[4 * b + k] : 0.0);
             acc[v] += g;
         }
     }
@@ -589,7 +598,7 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
     const Prob& d = probs[blockIdx.x];
     LM& lm = *d.lm;
     if (lm.status) return;
-    const double chi = chi_of_parts<RED>(d, s);
+    const double chi = chi_of_parts<RED>(d, d.part, s);
     if (threadIdx.x == 0) {
         lm.initialChi = chi;
         lm.acceptedChi = chi;
@@ -603,32 +612,6 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
     }
 }
 
-// grid (Q) x 256: iteration start
-__global__ __launch_bounds__(RED) void k_ctl_begin(const Prob* __restrict__ probs) {
-    constexpr int T = RED;
-    __shared__ double s[RED];
-    const Prob& d = probs[blockIdx.x];
-    LM& lm = *d.lm;
-    if (lm.status || lm.done || !lm.need_lin) return;
-    const double chi = chi_of_parts<T>(d, s);
-    if (threadIdx.x == 0) {
-        // max |diag(H)| gathered by k_sys's blocks (max is exact in any order), reset for the next iteration
-        const double maxdiag = __longlong_as_double((long long)atomicExch(&lm.maxdiag, 0ull));
-        if (lm.its == 0) {
-            // levenberg.cpp:71-77: lambda_0 = tau * max diag(H), tau = 1e-5 (computeLambdaInit :171-185)
-            lm.currentChi = chi;
-            lm.lambda = 1e-5 * maxdiag;
-            lm.ni = 2.0;
-            lm.nBad = 0;
-        } else {
-            // the chi2 of the accepted trial, bit for bit (same kernels on the same state)
-            lm.currentChi = lm.acceptedChi;
-        }
-        lm.iniChi = lm.currentChi;
-        lm.qmax = 0;
-        lm.need_lin = 0;
-    }
-}
 
 // grid (ceil(L/64) + Np, Q) x 64: the system (sys_body) and max |diag(H)| (one device atomic per wave)
 __global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
@@ -666,7 +649,7 @@ __global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ prob
     const Prob& d = probs[blockIdx.y];
     const LM& lm = *d.lm;
     if (lm.status || lm.done) return;
-    const double lambda = lm.lambda;
+    const double lambda = trial_lambda(lm);
     const int lane = lane_id();
     {
         const int h = blockIdx.x * EW + lane;
@@ -710,7 +693,17 @@ __global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ prob
     wave_copy_out(d.coef + 6 * (size_t)e0, sc, 6 * ne);
 }
 
-// grid (Np * Np + Np, Q) x 64: one wave per block (i1 <= i2) of S (blocks with i2 < i1 exit) over its landmark pairs
+// triangle index q -> (tr, tc), tc <= tr
+__device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
+    int r = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+    while (r * (r + 1) / 2 > q) r--;
+    while ((r + 1) * (r + 2) / 2 <= q) r++;
+    *tr = r;
+    *tc = q - r * (r + 1) / 2;
+}
+
+// grid (Np (Np + 1) / 2 + Np, Q) x 64: one wave per block (i1 <= i2) of S (the triangle only: the upper half's
+// workgroups would exit at once, half of the dispatches) over its landmark pairs
 // (k_blk_fill), lanes strided over the pairs + a fixed-order wave sum; then one wave per pose for b_s. Only the lower
 // triangle of S is written (the one the factorization reads).
 __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs) {
@@ -718,14 +711,14 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
     // landmarks its rows share stay in its L2
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
     const int logical = xcd_logical(lin, gridDim.x * gridDim.y);
-    const int bx = logical % gridDim.x;
+    const int bt = logical % gridDim.x;
     const Prob& d = probs[logical / gridDim.x];
     const LM& lm = *d.lm;
     if (lm.status || lm.done) return;
     const int lane = threadIdx.x;
-    const int nb2 = d.Np * d.Np;
-    if (bx >= nb2) {
-        const int h = bx - nb2;
+    const int ntri = d.Np * (d.Np + 1) / 2;
+    if (bt >= ntri) {
+        const int h = bt - ntri;
         if (h >= d.Np) return;
         double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         for (int s = d.qe_off[h] + lane; s < d.qe_off[h + 1]; s += 64) {
@@ -743,8 +736,12 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
         }
         return;
     }
-    const int i1 = bx / d.Np, i2 = bx % d.Np;
-    if (i2 < i1) return;
+    // triangle row tr = the blocks of pose i1 = Np - 1 - tr (i2 = i1 .. Np - 1): a contiguous range of ids is a run
+    // of i1 rows, the W records of pose i1's edges reused from the XCD's L2 as in the square grid
+    int tr, tc;
+    tri_index(bt, &tr, &tc);
+    const int i1 = d.Np - 1 - tr, i2 = i1 + tc;
+    const int bx = i1 * d.Np + i2;   // the block's pair-list slot
     if (i1 != i2 && !d.pairmask[(size_t)i1 * d.Np + i2]) {
         // no shared landmark: a zero block (the factorization's fill-in of the previous trial is overwritten)
         if (lane < 36) {
@@ -753,7 +750,7 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
         }
         return;
     }
-    const double lambda = lm.lambda;
+    const double lambda = trial_lambda(lm);
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
@@ -1073,14 +1070,6 @@ struct TileQueue {
     }
 };
 
-// triangle index q -> (tr, tc), tc <= tr
-__device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
-    int r = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
-    while (r * (r + 1) / 2 > q) r--;
-    while ((r + 1) * (r + 2) / 2 <= q) r++;
-    *tr = r;
-    *tc = q - r * (r + 1) / 2;
-}
 
 #ifdef MAM_LDLT_PROFILE
 // cycles per phase summed over workgroups (thread 0 after each barrier): init, B, C1, C2, solve, diag (wave 0), -, WGs
@@ -1424,8 +1413,12 @@ __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs)
     const Prob& d = probs[blockIdx.x];
     LM& lm = *d.lm;
     if (lm.status || lm.done) return;
-    const double lambda = lm.lambda;
-    double tempChi = chi_of_parts<T>(d, s);
+    // an iteration's first trial: the iteration-start state first (the chi2 of the linearised state on the first
+    // iteration, else the accepted trial's, bit for bit the same kernels on the same state; lambda_0)
+    const bool begin = lm.need_lin != 0;
+    const double lambda = trial_lambda(lm);
+    const double chi0 = (begin && lm.its == 0) ? chi_of_parts<T>(d, d.part0, s) : 0.0;
+    double tempChi = chi_of_parts<T>(d, d.part, s);
     // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194)
     double acc[RED / T];
     const int nbl = max(1, (d.E + EW - 1) / EW);
@@ -1436,6 +1429,19 @@ __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs)
     }
     const double scale0 = block_sum<T>(acc, s);
     if (threadIdx.x != 0) return;
+    if (begin) {
+        if (lm.its == 0) {
+            lm.currentChi = chi0;
+            lm.ni = 2.0;
+            lm.nBad = 0;
+        } else {
+            lm.currentChi = lm.acceptedChi;
+        }
+        lm.iniChi = lm.currentChi;
+        lm.qmax = 0;
+        lm.need_lin = 0;
+        lm.maxdiag = 0ull;   // k_sys gathers the next iteration's max
+    }
     if (lm.fail) tempChi = DBL_MAX;
     double rho = lm.currentChi - tempChi;
     const double scale = scale0 + 1e-3;
@@ -1557,6 +1563,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.err = cv.take<double>(2 * (size_t)d.E);
     d.jac = cv.take<double>(21 * (size_t)d.E);
     d.part = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
+    d.part0 = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
     d.part_s = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
     d.hpl = cv.take<double>(18 * (size_t)d.E);
     d.bdinv = cv.take<double>(18 * (size_t)d.E);
@@ -1722,7 +1729,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     }
     const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
     const dim3 gPrep((std::max(maxE, maxL) + EW - 1) / EW > 0 ? (std::max(maxE, maxL) + EW - 1) / EW : 1, Q);
-    const dim3 gBlk(maxNp * maxNp + maxNp > 0 ? maxNp * maxNp + maxNp : 1, Q);
+    const dim3 gBlk(maxNp * (maxNp + 1) / 2 + maxNp > 0 ? maxNp * (maxNp + 1) / 2 + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
     const dim3 gUpd((maxPL + 255) / 256 > 0 ? (maxPL + 255) / 256 : 1, Q);
     // The batch runs as G interleaved groups on G streams: one group's latency-bound factorization (one workgroup
@@ -1760,7 +1767,6 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
             mam::StageTimer::Scope sc(tm, st, 0);
             hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 0);
             hipLaunchKernelGGL(k_sys, gSysg, dim3(64), 0, st, Pg);
-            hipLaunchKernelGGL(k_ctl_begin, dim3(Qg), dim3(RED), 0, st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 1);
