@@ -160,3 +160,17 @@ def test_lba_size_bound(solver):
     # the context stays usable
     small = synthetic_problem(n_opt=5, n_fixed=2, n_points=100, obs_per_point=4, seed=3)
     assert solver.solve(small).status == 0
+
+
+def test_lba_arena_reuse(solver, oracle):
+    # the pose x point table and S are not cleared between batches (lba.hip k_struct_init / eidx_at): a small window
+    # solved in the arena a large one left behind, then the large one again, must both match the oracle exactly as
+    # fresh solves do
+    big = synthetic_problem(n_opt=50, n_fixed=10, n_points=3000, obs_per_point=8, seed=21)
+    small = synthetic_problem(n_opt=7, n_fixed=2, n_points=400, obs_per_point=5, seed=22)
+    for prob in (big, small, big):
+        rg, ro = solver.solve(prob), oracle.lba_solve(prob)
+        assert rg.status == 0 and ro.status == 0
+        assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials)
+        assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
+        assert _rel(rg.pose_t, ro.pose_t) <= 1e-4
