@@ -53,10 +53,10 @@ FP64_PEAK_TFS = 78.6    # MI355X FP64 vector / matrix (spec)
 ROOFLINE_NOTES = {
     "fast": ("latency / issue: per 64-frame launch VALU busy 11%, 33% of wave cycles waiting (s_waitcnt, barriers) and "
              "37% issue-stalled; FETCH_SIZE 28 MB raw = algorithmic after the XCD-aware cell order "
-             "(profiles/r02/pmc_c1_tracking.json)"),
+             "(profiles/r02/pmc_c1_64frame.json)"),
     "pyramid": "bilinear resize, latency-bound at 7 dependent launches",
     "describe": ("one wave per keypoint: IC-angle loads + the 37x37 blurred patch in LDS, two dependent round trips; "
-                 "57% of wave cycles waiting, VALU busy 9% (profiles/r02/pmc_c1_tracking.json)"),
+                 "57% of wave cycles waiting, VALU busy 9% (profiles/r02/pmc_c1_64frame.json)"),
     "resolve": "one workgroup per frame, greedy dependency rounds (latency, LDS atomics)",
 }
 
