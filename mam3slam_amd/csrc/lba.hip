@@ -56,6 +56,8 @@ struct LM {
     int status;      // MAM_OK or MAM_ERR_*
     int iterations;  // optimize(iterations)
     unsigned long long maxdiag;   // max |diag(H)| of the iteration's system (bits of a non-negative double)
+    int ntiles;      // structurally non-zero 16x16 tiles of L (lower triangle incl. the diagonal; k_struct_tiles)
+    int tiles_lds;   // all of them + y fit the factorization's LDS: k_ldlt factors in LDS (ldlt_tiles)
 };
 
 struct Prob {
@@ -86,6 +88,8 @@ struct Prob {
     int32_t* blk_off;            // [Np * Np + 1] start of block (i1, i2)'s landmark pairs in blk_pair (i1 <= i2)
     int2* blk_pair;              // (edge of pose i1, edge of pose i2) per shared landmark, i2's edge order
     uint8_t* tmask;              // [nt][nt] (r >= c): 16x16 tile (r, c) of L is structurally non-zero (S + fill)
+    int16_t* tslot;              // [nt][nt]: the tile's slot in the LDS tile pool (ldlt_tiles), -1 structurally zero
+    int16_t* tlist;              // [ntiles][2]: (r, c) of each slot
     int nt;                      // npad / 16
     // state: [2] buffers, lm->cur is the current one
     double* pose[2];             // [P][7] q(xyzw) t
@@ -795,6 +799,7 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
 // Then y /= D and the backward substitution L^T x = y, block by block, each thread updating its own y_i.
 // The workspace (panel + y) is LDS when it fits (use_lds), else the problem's global scratch.
 constexpr int NB = 16;
+constexpr int LDLT_TILES_NT_MAX = 40;   // ldlt_tiles' slot map in static LDS: nt <= 40 (npad <= 640)
 #ifndef MAM_LDLT_THREADS
 #define MAM_LDLT_THREADS 512
 #endif
@@ -849,11 +854,15 @@ __global__ __launch_bounds__(SB) void k_blk_scan(const Prob* __restrict__ probs)
     }
     if (t == SB - 1) d.blk_off[n] = part[SB - 1];
 }
+// per problem: the S blocks' landmark pair total, and the LDS tile pool size when the factorization runs in LDS (the
+// host sizes the pair buffer and k_ldlt's dynamic LDS from them)
 __global__ void k_blk_total(const Prob* __restrict__ probs, int Q, int* __restrict__ out) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Q) return;
     const Prob& d = probs[q];
-    out[q] = d.lm->status ? 0 : d.blk_off[d.Np * d.Np];
+    const LM& lm = *d.lm;
+    out[2 * q] = lm.status ? 0 : d.blk_off[d.Np * d.Np];
+    out[2 * q + 1] = (lm.status || !lm.tiles_lds) ? -1 : lm.ntiles;
 }
 // grid (Np * Np, Q) x 64: the pairs, compacted in edge order by ballot
 __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs) {
@@ -887,7 +896,7 @@ __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs)
 // Structurally zero tiles of L stay exact zeros, so k_ldlt skips them: every non-zero entry sees the same arithmetic
 // as in the dense factorization. Windows whose covisibility is banded (keyframes along a trajectory) factor in
 // O(n b^2) instead of O(n^3).
-__global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ probs) {
+__global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ probs, int lds_bytes) {
     const Prob& d = probs[blockIdx.x];
     if (d.lm->status) return;
     const int nt = d.nt, n = 6 * d.Np;
@@ -914,6 +923,47 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
             if (r2 <= r1 && d.tmask[(size_t)r1 * nt + c] && d.tmask[(size_t)r2 * nt + c]) d.tmask[(size_t)r1 * nt + r2] = 1;
         }
         __syncthreads();
+    }
+    // the non-zero tiles' slots in ldlt_tiles' LDS pool (row-major order of (r, c), r >= c), their count, and whether
+    // the pool and y fit the factorization's dynamic LDS (lds_bytes)
+    __shared__ int wsum[SB / 64];
+    __shared__ int carry;
+    const int t = threadIdx.x;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < nt * nt; c0 += SB) {
+        const int q = c0 + t;
+        const int f = (q < nt * nt && d.tmask[q]) ? 1 : 0;
+        int v = f;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(v, o, 64);
+            if (lane_id() >= o) v += u;
+        }
+        if (lane_id() == 63) wsum[t >> 6] = v;
+        __syncthreads();
+        int pre = 0, tot = 0;
+        for (int w = 0; w < SB / 64; w++) {
+            if (w < (t >> 6)) pre += wsum[w];
+            tot += wsum[w];
+        }
+        if (q < nt * nt) {
+            const int sl = carry + pre + v - f;
+            d.tslot[q] = f ? (int16_t)sl : (int16_t)-1;
+            if (f) {
+                d.tlist[2 * sl] = (int16_t)(q / nt);
+                d.tlist[2 * sl + 1] = (int16_t)(q % nt);
+            }
+        }
+        __syncthreads();
+        if (t == 0) carry += tot;
+        __syncthreads();
+    }
+    if (t == 0) {
+        LM& lm = *d.lm;
+        lm.ntiles = carry;
+        lm.tiles_lds = (nt <= LDLT_TILES_NT_MAX && (size_t)carry * 256 * sizeof(double) + (size_t)d.npad * sizeof(double) <=
+                                                        (size_t)lds_bytes) ? 1 : 0;
     }
 }
 
@@ -942,11 +992,83 @@ __device__ __forceinline__ int bcast16_i(int v, int k) {
     }
     return 0;
 }
+// the double form: one v_mov_b64_dpp (gfx950 DPP64 supports row_newbcast) instead of two 32-bit moves
 __device__ __forceinline__ double bcast16_d(double v, int k) {
-    const unsigned long long u = __double_as_longlong(v);
-    const int lo = bcast16_i((int)(u & 0xffffffffu), k);
-    const int hi = bcast16_i((int)(u >> 32), k);
-    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+    switch (k) {
+#define MAM_BC(n) \
+    case n: return __builtin_amdgcn_mov_dpp(v, 0x150 + n, 0xf, 0xf, false);
+        MAM_BC(0) MAM_BC(1) MAM_BC(2) MAM_BC(3) MAM_BC(4) MAM_BC(5) MAM_BC(6) MAM_BC(7)
+        MAM_BC(8) MAM_BC(9) MAM_BC(10) MAM_BC(11) MAM_BC(12) MAM_BC(13) MAM_BC(14) MAM_BC(15)
+#undef MAM_BC
+    }
+    return 0.0;
+}
+
+// acc += (value of src in lane K of this lane's 16-lane row) * m: the broadcast folded into the FMA as one
+// v_fmac_f64_dpp row_newbcast (gfx950 DPP64); one instruction where a v_mov_b64_dpp + v_fma_f64 pair was. The s_nop
+// covers the VALU-write -> DPP-read hazard on src (inline asm is not seen by the hazard recognizer). Same rounding as
+// fma(src_K, m, acc).
+template <int K>
+__device__ __forceinline__ void fmac_bcast16(double& acc, double src, double m) {
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc)
+                 : "v"(src), "v"(m), "n"(K));
+}
+template <int J, int K>
+struct Fmac16 {
+    __device__ __forceinline__ static void run(double* row, double a, double ml) {
+        fmac_bcast16<K>(row[K], a, ml);
+        Fmac16<J, K + 1>::run(row, a, ml);
+    }
+};
+template <int J>
+struct Fmac16<J, NB> {
+    __device__ __forceinline__ static void run(double*, double, double) {}
+};
+template <int J>
+struct Diag16 {
+    // step J of the right-looking LDL^T of the lanes' rows: A(lane, k) -= l(lane, J) A(k, J), k > J, with
+    // l(lane, J) = A(lane, J) / d_J; A(k, J) is the pre-scaling column, broadcast from lane k, so the update does not
+    // wait for the pivot's reciprocal
+    __device__ __forceinline__ static void run(double* row, double& dmine, int lane) {
+        const double a = row[J];
+        const double dj = bcast16_d(a, J);
+        if (lane == J) dmine = dj;
+        // the pivot's reciprocal by v_rcp_f64 and two Newton steps (within an ulp of 1/dj; the divide's scale /
+        // fixup steps guard denormal and huge pivots, which a damped system's diagonal does not have) — it is the
+        // serial part of every step
+        double inv = __builtin_amdgcn_rcp(dj);
+        inv = fma(inv, fma(-dj, inv, 1.0), inv);
+        inv = fma(inv, fma(-dj, inv, 1.0), inv);
+        if (dj == 0.0) inv = 0.0;
+        const double l = a * inv;
+        Fmac16<J, J + 1>::run(row, a, -l);
+        if (lane > J) row[J] = l;
+        Diag16<J + 1>::run(row, dmine, lane);
+    }
+};
+template <>
+struct Diag16<NB> {
+    __device__ __forceinline__ static void run(double*, double&, int) {}
+};
+
+// wave-level LDL^T of a 16x16 block held one row per lane (lanes 0..15; the other lanes carry zeros): on entry
+// row[c] = A(lane, c) (c <= lane read), on exit row[c] = L(lane, c) for c < lane and D(lane) at c == lane (the entries
+// above the diagonal are don't-care values nothing reads); returns D(lane)
+__device__ __forceinline__ double diag16_factor(double row[NB], int lane) {
+    double dmine = 1.0;
+    Diag16<0>::run(row, dmine, lane);
+    return dmine;
+}
+
+// the forward block solve y1 <- L11^-1 y1 on the factored rows (lane i: y_i)
+__device__ __forceinline__ double diag16_forward(const double row[NB], double yv, int lane) {
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        const double yj = bcast16_d(yv, j);
+        if (lane > j) yv = fma(-row[j], yj, yv);
+    }
+    return yv;
 }
 
 // wave 0: LDL^T of the 16x16 diagonal block at kb, read from the block-column buffer (CB[c * cs + r] = A(kb + r,
@@ -957,35 +1079,8 @@ __device__ __forceinline__ void ldlt_diag(gdouble* A, int N, int kb, const doubl
     double row[NB];
 #pragma unroll
     for (int c = 0; c < NB; c++) row[c] = lane < NB ? CB[(size_t)c * cs + lane] : 0.0;
-    // step j: A(r, k) -= L(r, j) a(k, j) with a(k, j) = L(k, j) D(j) the column before scaling, so its broadcast
-    // (DPP broadcasts within lanes 0..15) does not wait for the pivot's reciprocal; every lane updates every k > j without a mask — the
-    // entries above the diagonal become don't-care values that nothing reads (lower triangle and diagonal only)
-    double dmine = 1.0;
-#pragma unroll
-    for (int j = 0; j < NB; j++) {
-        const double dj = bcast16_d(row[j], j);
-        double akj[NB];
-#pragma unroll
-        for (int k = j + 1; k < NB; k++) akj[k] = bcast16_d(row[j], k);
-        if (lane == j) dmine = dj;
-        // the pivot's reciprocal by v_rcp_f64 and two Newton steps (within an ulp of 1/dj; the divide's scale /
-        // fixup steps guard denormal and huge pivots, which a damped system's diagonal does not have) — it is the
-        // serial part of every step
-        double inv = __builtin_amdgcn_rcp(dj);
-        inv = fma(inv, fma(-dj, inv, 1.0), inv);
-        inv = fma(inv, fma(-dj, inv, 1.0), inv);
-        if (dj == 0.0) inv = 0.0;
-        const double l = row[j] * inv;
-        if (lane > j) row[j] = l;
-#pragma unroll
-        for (int k = j + 1; k < NB; k++) row[k] = fma(-l, akj[k], row[k]);
-    }
-    double yv = lane < NB ? Y[kb + lane] : 0.0;
-#pragma unroll
-    for (int j = 0; j < NB; j++) {
-        const double yj = bcast16_d(yv, j);
-        if (lane > j) yv = fma(-row[j], yj, yv);
-    }
+    const double dmine = diag16_factor(row, lane);
+    const double yv = diag16_forward(row, lane < NB ? Y[kb + lane] : 0.0, lane);
     if (lane < NB) {
 #pragma unroll
         for (int c = 0; c < NB; c++) {
@@ -1097,30 +1192,35 @@ __device__ unsigned long long g_lprof[8];
 #endif
 constexpr int C1_PF = MAM_LDLT_C1_PF;   // (C1) tiles per wave prefetched across (B)
 constexpr int LDLT_TM_MAX = 40;         // the LDS path's tile-mask copy: nt <= 40 (npad <= 640)
+// The factorization's static LDS, shared by both forms of k_ldlt (ldlt_global, ldlt_tiles)
+struct LdltShared {
+    double Ld[NB * NB];
+    double dk[2][NB];
+    double invdk[NB];
+    int fail;
+    // ldlt_global<true>: the tile mask (uint8 [nt][nt]); ldlt_tiles: the tile slot map (int16 [nt][nt])
+    int16_t map[LDLT_TM_MAX * LDLT_TM_MAX];
+};
+
+// S factored in place in HBM with the panel / block-column workspace in LDS (use_lds) or in the problem's scratch: the
+// form for problems whose non-zero tiles do not fit in LDS (dense covisibility, large windows)
 template <bool use_lds>
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
-    extern __shared__ __attribute__((aligned(16))) double lds_ws[];
-    const Prob& d = probs[blockIdx.x];
+__device__ __forceinline__ void ldlt_global(const Prob& d, double* lds_ws, LdltShared& sh) {
     LM& lm = *d.lm;
-    if (lm.status || lm.done) return;
     const int n = 6 * d.Np, N = d.npad;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    if (n == 0) {
-        if (t == 0) lm.fail = 0;
-        return;
-    }
     gdouble* A = (gdouble*)d.S;   // global address space: its loads must not count in lgkmcnt (flat)
     double* ws = use_lds ? lds_ws : d.ws;
     const int cs = ldlt_cb_stride(N);
     double* PL = ws;
     double* CB = ws + (size_t)NB * (N - NB);
     double* Y = CB + (size_t)NB * cs;
-    __shared__ double Ld[NB * NB];
-    __shared__ double dk[2][NB];
-    __shared__ double invdk[NB];
-    __shared__ int fail;
+    double* Ld = sh.Ld;
+    double (*dk)[NB] = sh.dk;
+    double* invdk = sh.invdk;
+    int& fail = sh.fail;
     // the tile mask: the phases below test it before their loads, so its reads sit on their critical paths
-    __shared__ uint8_t tm_lds[use_lds ? LDLT_TM_MAX * LDLT_TM_MAX : 1];
+    uint8_t* tm_lds = reinterpret_cast<uint8_t*>(sh.map);
     const uint8_t* tmask = use_lds ? tm_lds : d.tmask;
 #ifdef MAM_LDLT_PROFILE
     long long lp0 = clock64();
@@ -1296,6 +1396,213 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ 
 #ifdef MAM_LDLT_PROFILE
     if (t == 0) atomicAdd(&g_lprof[7], 1ull);
 #endif
+}
+
+// ---- the factorization with all of L in LDS (lm.tiles_lds: the structurally non-zero tiles + y fit the dynamic
+// LDS). The tiles S holds (k_schur_blk: pose blocks, lower triangle) are loaded once into a pool of 16x16 tiles
+// (k_struct_tiles' slots, tslot / tlist), factored there and never written back: only x leaves the workgroup. The
+// algorithm is ldlt_global's (the same panels, lookahead and tile skipping, so every non-zero entry sees the same
+// arithmetic): per panel k (B) the rows of the non-zero tiles (r, k) below the diagonal, L21 = A21 L11^-T D^-1 with
+// y2 -= L21 y1; (C1) the next block column's tiles updated by f64 MFMA; (C2) wave 0 factors the next diagonal tile
+// while the other waves update the rest of the trailing tiles. No global memory round trip inside the panel loop.
+// Tile layout: element (r, c) at c * 16 + (r ^ c) (column-major, rows XOR-swizzled by the column): the MFMA A / B
+// operand reads (16 rows of one column per 16 lanes), the accumulator reads / writes (16 columns of one row) and the
+// row-per-thread panel rows are all free of LDS bank conflicts within a 32-lane group.
+__device__ __forceinline__ int tsw(int r, int c) { return c * NB + (r ^ c); }
+
+// C(sc) -= L(sa) D L(sb)^T on tiles of the pool (one wave): four v_mfma_f64_16x16x4_f64, operands from LDS
+__device__ __forceinline__ void tile_update(double* TL, int sc, int sa, int sb, const double* dkp, int lane) {
+    const int col = lane & 15, rq = lane >> 4;
+    double* C = TL + (size_t)sc * 256;
+    const double* La = TL + (size_t)sa * 256;
+    const double* Lb = TL + (size_t)sb * 256;
+    dbl4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; r++) acc[r] = C[tsw(rq + 4 * r, col)];
+#pragma unroll
+    for (int k0 = 0; k0 < NB; k0 += 4) {
+        const int k = k0 + rq;
+        const double av = -La[tsw(col, k)];
+        const double bv = Lb[tsw(col, k)] * dkp[k];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) C[tsw(rq + 4 * r, col)] = acc[r];
+}
+
+// wave 0: LDL^T of diagonal tile kc of the pool, written back in place (L below, D on the diagonal), Ld / dk / invdk
+// for the panel rows and the trailing update, and the forward block solve of y
+__device__ __forceinline__ void tiles_diag(double* TL, int sd, int kb, double* Y, LdltShared& sh, double* dkp,
+                                           int lane) {
+    double* T = TL + (size_t)sd * 256;
+    double row[NB];
+#pragma unroll
+    for (int c = 0; c < NB; c++) row[c] = lane < NB ? T[tsw(lane, c)] : 0.0;
+    const double dmine = diag16_factor(row, lane);
+    const double yv = diag16_forward(row, lane < NB ? Y[kb + lane] : 0.0, lane);
+    if (lane < NB) {
+#pragma unroll
+        for (int c = 0; c < NB; c++) {
+            sh.Ld[lane * NB + c] = row[c];
+            if (c < lane) T[tsw(lane, c)] = row[c];
+        }
+        T[tsw(lane, lane)] = dmine;
+        dkp[lane] = dmine;
+        sh.invdk[lane] = dmine != 0.0 ? 1.0 / dmine : 0.0;
+        Y[kb + lane] = yv;
+        if (dmine == 0.0) sh.fail = 1;
+    }
+}
+
+__device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShared& sh) {
+    LM& lm = *d.lm;
+    const int n = 6 * d.Np, N = d.npad, nt = d.nt, T = lm.ntiles;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    constexpr int NW = LDLT_THREADS / 64;
+    double* TL = lds;                           // [T][256]
+    double* Y = lds + (size_t)T * 256;          // [N]
+    int16_t* slot = sh.map;                     // [nt][nt]
+    if (t == 0) sh.fail = 0;
+    for (int q = t; q < nt * nt; q += LDLT_THREADS) slot[q] = d.tslot[q];
+    // the pool: tile s = (r, c) holds S rows 16 r.., columns 16 c..; the padding rows' diagonal is 1 (an identity block
+    // after the unknowns: S's padding rows are zero)
+    for (int q = t; q < T * 256; q += LDLT_THREADS) {
+        const int s = q >> 8, e = q & 255, i = e >> 4, j = e & 15;
+        const int r = d.tlist[2 * s], c = d.tlist[2 * s + 1];
+        const int gi = NB * r + i, gj = NB * c + j;
+        double v = d.S[(size_t)gi * N + gj];
+        if (gi == gj && gi >= n) v = 1.0;
+        TL[(size_t)s * 256 + tsw(i, j)] = v;
+    }
+    for (int i = t; i < N; i += LDLT_THREADS) Y[i] = i < n ? d.bs[i] : 0.0;
+    __syncthreads();
+    if (wid == 0) tiles_diag(TL, slot[0], 0, Y, sh, sh.dk[0], lane);
+    __syncthreads();
+    for (int kc = 0, p = 0; kc < nt; kc++, p ^= 1) {
+        const int kb = NB * kc;
+        const double* dkp = sh.dk[p];
+        // (B) panel rows: one thread per row of the tiles (r, kc), r > kc
+        for (int i = kb + NB + t; i < N; i += LDLT_THREADS) {
+            const int s = slot[(i / NB) * nt + kc];
+            if (s < 0) continue;
+            double* Tr = TL + (size_t)s * 256;
+            const int ri = i & 15;
+            // keep the L11 factors in LDS (reading them per row): hoisting all 120 into registers spills
+            asm volatile("" ::: "memory");
+            double w[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j++) w[j] = Tr[tsw(ri, j)];
+#pragma unroll
+            for (int j = 1; j < NB; j++) {
+#pragma unroll
+                for (int k = 0; k < j; k++) w[j] = fma(-w[k], sh.Ld[j * NB + k], w[j]);
+            }
+            double yi = Y[i];
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const double lij = w[j] * sh.invdk[j];
+                Tr[tsw(ri, j)] = lij;
+                yi = fma(-lij, Y[kb + j], yi);
+            }
+            Y[i] = yi;
+        }
+        __syncthreads();
+        if (kc + 1 == nt) break;
+        // (C1) the next block column: tiles (r, kc + 1), r > kc, updated by L(r, kc) D L(kc + 1, kc)^T
+        const int s_n = slot[(kc + 1) * nt + kc];   // L(kc + 1, kc)
+        if (s_n >= 0) {
+            for (int r = kc + 1 + wid; r < nt; r += NW) {
+                const int sa = slot[r * nt + kc];
+                if (sa < 0) continue;
+                tile_update(TL, slot[r * nt + kc + 1], sa, s_n, dkp, lane);
+            }
+        }
+        __syncthreads();
+        // (C2) wave 0: the next diagonal tile; the other waves: tiles (r, c), kc + 1 < c <= r
+        if (wid == 0) {
+            tiles_diag(TL, slot[(kc + 1) * nt + kc + 1], kb + NB, Y, sh, sh.dk[p ^ 1], lane);
+        } else {
+            const int T2 = nt - kc - 2;
+            const int n2 = T2 * (T2 + 1) / 2;
+            for (int q = wid - 1; q < n2; q += NW - 1) {
+                int tr, tc;
+                tri_index(q, &tr, &tc);
+                const int r = kc + 2 + tr, c = kc + 2 + tc;
+                const int sa = slot[r * nt + kc], sb = slot[c * nt + kc];
+                if (sa < 0 || sb < 0) continue;
+                tile_update(TL, slot[r * nt + c], sa, sb, dkp, lane);
+            }
+        }
+        __syncthreads();
+    }
+    const int fl = sh.fail;
+    if (t == 0) lm.fail = fl;
+    if (fl) return;   // uniform (LDS flag after the last barrier)
+    // y /= D
+    for (int i = t; i < N; i += LDLT_THREADS) {
+        const int ii = i / NB;
+        Y[i] /= TL[(size_t)slot[ii * nt + ii] * 256 + tsw(i & 15, i & 15)];
+    }
+    __syncthreads();
+    // backward substitution L^T x = y: block solve by wave 0, then each thread i < kb updates its own y_i
+    for (int kc = nt - 1; kc >= 0; kc--) {
+        const int kb = NB * kc;
+        if (wid == 0) {
+            const double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
+            double col[NB];   // lane c holds L(kb + j, kb + c) for j > c
+#pragma unroll
+            for (int j = 0; j < NB; j++) col[j] = lane < NB ? Td[tsw(j, lane & 15)] : 0.0;
+            double v = lane < NB ? Y[kb + lane] : 0.0;
+#pragma unroll
+            for (int j = NB - 1; j >= 0; j--) {
+                const double xj = bcast16_d(v, j);
+                if (lane < j) v = fma(-col[j], xj, v);
+            }
+            if (lane < NB) Y[kb + lane] = v;
+        }
+        __syncthreads();
+        for (int i = t; i < kb; i += LDLT_THREADS) {
+            const int s = slot[kc * nt + i / NB];   // L(kb.., i) not structurally zero
+            if (s < 0) continue;
+            const double* Tr = TL + (size_t)s * 256;
+            double sy = Y[i];
+#pragma unroll
+            for (int j = 0; j < NB; j++) sy = fma(-Tr[tsw(j, i & 15)], Y[kb + j], sy);
+            Y[i] = sy;
+        }
+        __syncthreads();
+    }
+    for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+}
+
+// grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
+// largest pool + y of the batch)
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_tiles(const Prob* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done || !lm.tiles_lds) return;
+    if (d.Np == 0) {
+        if (threadIdx.x == 0) lm.fail = 0;
+        return;
+    }
+    ldlt_tiles(d, lds_dyn, sh);
+}
+
+// grid (Q) x LDLT_THREADS: the others, factored in place in HBM (the panel workspace in LDS when use_lds)
+template <bool use_lds>
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done || lm.tiles_lds) return;
+    if (d.Np == 0) {
+        if (threadIdx.x == 0) lm.fail = 0;
+        return;
+    }
+    ldlt_global<use_lds>(d, lds_dyn, sh);
 }
 
 // Eigen Quaterniond(Matrix3d)
@@ -1534,7 +1841,8 @@ size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
     const size_t nx = 6 * (size_t)Np + 3 * (size_t)L;
     return al(4 * (size_t)P) + al(4 * (size_t)Np) + al(4 * (size_t)(L + 1)) + al(4 * (size_t)E) +
            al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) + al(4 * ((size_t)Np * Np + 1)) +
-           al((size_t)(npad / 16) * (npad / 16)) +
+           al((size_t)(npad / 16) * (npad / 16)) + al(2 * (size_t)(npad / 16) * (npad / 16)) +
+           al(2 * (size_t)(npad / 16) * (npad / 16 + 1)) +
            2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
            2 * al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
            al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
@@ -1556,6 +1864,8 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.blk_off = cv.take<int32_t>((size_t)d.Np * d.Np + 1);
     d.nt = d.npad / mam::lba::NB;
     d.tmask = cv.take<uint8_t>((size_t)d.nt * d.nt);
+    d.tslot = cv.take<int16_t>((size_t)d.nt * d.nt);
+    d.tlist = cv.take<int16_t>((size_t)d.nt * (d.nt + 1));
     d.pose[0] = cv.take<double>(7 * (size_t)d.P);
     d.pose[1] = cv.take<double>(7 * (size_t)d.P);
     d.pt[0] = cv.take<double>(3 * (size_t)d.L);
@@ -1653,6 +1963,8 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         maxLb = std::max(maxLb, (d.L + 255) / 256 + d.Np);
         max_lds = std::max(max_lds, ldlt_lds_bytes(d.npad));
     }
+    size_t tiles_dyn = 0;                        // k_ldlt_tiles' dynamic LDS (set once the structure is known)
+    bool any_tiles = false, any_global = false;  // problems factored in LDS / in HBM
     if (max_lds > c->ldlt_lds_budget) lds_ok = false;
     if (ldlt_pad(6 * maxNp) / NB > LDLT_TM_MAX) lds_ok = false;   // the LDS path keeps the tile mask in LDS too
     // size bounds before any allocation: the dense pose x landmark edge table (Np L int32) and S (npad^2 f64) of one
@@ -1701,25 +2013,34 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_struct_scan, dim3(1, Q), dim3(SB), 0, s, P);
         hipLaunchKernelGGL(k_struct_scatter, gE, dim3(256), 0, s, P);
         hipLaunchKernelGGL(k_struct_sort, dim3(std::max(maxLb, 1), Q), dim3(256), 0, s, P);
-        hipLaunchKernelGGL(k_struct_tiles, dim3(Q), dim3(SB), 0, s, P);
+        hipLaunchKernelGGL(k_struct_tiles, dim3(Q), dim3(SB), 0, s, P, (int)c->ldlt_lds_budget);
         // the S blocks' landmark pairs: counts, offsets, one read-back of the totals to size the pair buffer
         const dim3 gB(std::max(maxNp * maxNp, 1), Q);
         hipLaunchKernelGGL(k_blk_count, gB, dim3(64), 0, s, P);
         hipLaunchKernelGGL(k_blk_scan, dim3(1, Q), dim3(SB), 0, s, P);
-        if (int rc = c->blk_tot.alloc(Q)) return rc;
-        if (int rc = c->blk_tot_host.alloc(sizeof(int) * (size_t)Q)) return rc;
+        if (int rc = c->blk_tot.alloc(2 * Q)) return rc;
+        if (int rc = c->blk_tot_host.alloc(2 * sizeof(int) * (size_t)Q)) return rc;
         hipLaunchKernelGGL(k_blk_total, dim3((Q + 255) / 256), dim3(256), 0, s, P, Q, c->blk_tot.p);
         MAM_HIP(hipGetLastError());
-        MAM_HIP(hipMemcpyAsync(c->blk_tot_host.p, c->blk_tot.p, sizeof(int) * (size_t)Q, hipMemcpyDeviceToHost, s));
+        MAM_HIP(hipMemcpyAsync(c->blk_tot_host.p, c->blk_tot.p, 2 * sizeof(int) * (size_t)Q, hipMemcpyDeviceToHost,
+                               s));
         MAM_HIP(hipStreamSynchronize(s));
         const int* tot = reinterpret_cast<const int*>(c->blk_tot_host.p);
         size_t npairs = 0;
-        for (int q = 0; q < Q; q++) npairs += (size_t)std::max(tot[q], 0);
+        for (int q = 0; q < Q; q++) npairs += (size_t)std::max(tot[2 * q], 0);
         if (int rc = c->blk_pairs.alloc(std::max<size_t>(npairs, 1))) return rc;
         size_t base = 0;
         for (int q = 0; q < Q; q++) {
             hp[q].blk_pair = c->blk_pairs.p + base;
-            base += (size_t)std::max(tot[q], 0);
+            base += (size_t)std::max(tot[2 * q], 0);
+            // k_ldlt_tiles' dynamic LDS: the batch's largest tile pool + y; the others go to k_ldlt
+            if (tot[2 * q + 1] >= 0) {
+                tiles_dyn = std::max(tiles_dyn, (size_t)tot[2 * q + 1] * 256 * sizeof(double) +
+                                                    (size_t)hp[q].npad * sizeof(double));
+                any_tiles = true;
+            } else {
+                any_global = true;
+            }
         }
         std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
         MAM_HIP(hipMemcpyAsync(c->probs.p, c->lm_host.p, sizeof(Prob) * Q, hipMemcpyHostToDevice, s));
@@ -1775,10 +2096,13 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 2);
-            if (lds_ok)
-                hipLaunchKernelGGL(k_ldlt<true>, dim3(Qg), dim3(LDLT_THREADS), max_lds, st, Pg);
-            else
-                hipLaunchKernelGGL(k_ldlt<false>, dim3(Qg), dim3(LDLT_THREADS), 0, st, Pg);
+            if (any_tiles) hipLaunchKernelGGL(k_ldlt_tiles, dim3(Qg), dim3(LDLT_THREADS), tiles_dyn, st, Pg);
+            if (any_global) {
+                if (lds_ok)
+                    hipLaunchKernelGGL(k_ldlt<true>, dim3(Qg), dim3(LDLT_THREADS), max_lds, st, Pg);
+                else
+                    hipLaunchKernelGGL(k_ldlt<false>, dim3(Qg), dim3(LDLT_THREADS), 0, st, Pg);
+            }
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
@@ -1892,10 +2216,19 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
     MAM_DEVICE_SCOPE(device);
     mam_lba_ctx* c = new mam_lba_ctx();
     c->device = device;
-    // gfx950: 160 KB of LDS per workgroup; fall back to the 64 KB default if the opt-in is refused
+    // gfx950: 160 KB of LDS per workgroup, less the factorization's static LDS; fall back to the 64 KB default if the
+    // opt-in is refused
     c->ldlt_lds_budget = 0;
-    for (size_t budget : {(size_t)160 * 1024 - 4096, (size_t)64 * 1024 - 4096}) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt<true>),
+    hipFuncAttributes fa{};
+    size_t stat = 8192;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&mam::lba::k_ldlt_tiles)) == hipSuccess)
+        stat = (fa.sharedSizeBytes + 255) / 256 * 256 + 256;
+    else
+        (void)hipGetLastError();
+    for (size_t budget : {(size_t)160 * 1024 - stat, (size_t)64 * 1024 - stat}) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_tiles),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt<true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess) {
             c->ldlt_lds_budget = budget;
             break;
