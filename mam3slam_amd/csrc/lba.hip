@@ -1459,6 +1459,9 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     const int n = 6 * d.Np, N = d.npad, nt = d.nt, T = lm.ntiles;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     constexpr int NW = LDLT_THREADS / 64;
+#ifdef MAM_LDLT_PROFILE
+    long long lp0 = clock64();
+#endif
     double* TL = lds;                           // [T][256]
     double* Y = lds + (size_t)T * 256;          // [N]
     int16_t* slot = sh.map;                     // [nt][nt]
@@ -1478,6 +1481,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     __syncthreads();
     if (wid == 0) tiles_diag(TL, slot[0], 0, Y, sh, sh.dk[0], lane);
     __syncthreads();
+    LPROF(0);
     for (int kc = 0, p = 0; kc < nt; kc++, p ^= 1) {
         const int kb = NB * kc;
         const double* dkp = sh.dk[p];
@@ -1507,6 +1511,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             Y[i] = yi;
         }
         __syncthreads();
+        LPROF(1);
         if (kc + 1 == nt) break;
         // (C1) the next block column: tiles (r, kc + 1), r > kc, updated by L(r, kc) D L(kc + 1, kc)^T
         const int s_n = slot[(kc + 1) * nt + kc];   // L(kc + 1, kc)
@@ -1518,9 +1523,16 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             }
         }
         __syncthreads();
+        LPROF(2);
         // (C2) wave 0: the next diagonal tile; the other waves: tiles (r, c), kc + 1 < c <= r
         if (wid == 0) {
+#ifdef MAM_LDLT_PROFILE
+            const long long td = clock64();
+#endif
             tiles_diag(TL, slot[(kc + 1) * nt + kc + 1], kb + NB, Y, sh, sh.dk[p ^ 1], lane);
+#ifdef MAM_LDLT_PROFILE
+            if (lane == 0) atomicAdd(&g_lprof[5], (unsigned long long)(clock64() - td));
+#endif
         } else {
             const int T2 = nt - kc - 2;
             const int n2 = T2 * (T2 + 1) / 2;
@@ -1534,6 +1546,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             }
         }
         __syncthreads();
+        LPROF(3);
     }
     const int fl = sh.fail;
     if (t == 0) lm.fail = fl;
@@ -1573,6 +1586,10 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         __syncthreads();
     }
     for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+    LPROF(4);
+#ifdef MAM_LDLT_PROFILE
+    if (t == 0) atomicAdd(&g_lprof[7], 1ull);
+#endif
 }
 
 // grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
