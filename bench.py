@@ -4,16 +4,19 @@
 A step is one pass of the hot path over B synthetic frames resident in HBM, one frame from each of B frame streams
 (agent sequences) on this GPU, with the keyframe cadence of the reference's Tracking -> LocalMapping hand-off:
 
-  Tracking, every frame, one HIP graph:
+  Tracking, every frame, one HIP graph; frames start at the motion model's guess of the pose of
+  the camera that rendered them (synth.frame_pose):
     1. ORB extraction (pyramid, per-cell FAST, DistributeOctTree, orientation, rBRIEF, lapping placement)
-    2. SearchByProjection(CurrentFrame, LastFrame, th=15)            (TrackWithMotionModel, Tracking.cc:2810)
-    3. Frame::isInFrustum + MapPoint::PredictScale for every local MapPoint  (SearchLocalPoints, Tracking.cc:3119-3139)
-    4. SearchByProjection(F, localMapPoints, th=1), nnratio 0.8, matched keypoints taken (Tracking.cc:3146-3156)
-  LocalMapping (c2), concurrently on its own stream: every stream inserts a keyframe every K frames (--kf-every), so
-  B/K keyframes per step, each running LocalBundleAdjustment (LocalMapping.cc:162-172) on its 50-keyframe window of a
-  shared map in HBM (mam3slam_amd/mapping.py): window read from the map, the B/K solves batched with the Levenberg
-  control on the device, the write-backs all-gathered over RCCL and applied to every GPU's map, which the next
-  step's windows read.
+    2. TrackWithMotionModel (Tracking.cc:2786-2862): SearchByProjection(CurrentFrame, LastFrame, th=15),
+       Optimizer::PoseOptimization, outliers' slots emptied
+    3. TrackLocalMap (Tracking.cc:2878-2901): Frame::isInFrustum + MapPoint::PredictScale for every local MapPoint,
+       SearchByProjection(F, localMapPoints, th=1) (nnratio 0.8, matched keypoints taken), PoseOptimization
+  LocalMapping (c2), concurrently on its own streams: every stream inserts a keyframe every K frames (--kf-every), so
+  B/K keyframes per step, each getting ComputeBoW and CreateNewMapPoints' 30 SearchForTriangulation against its
+  covisible keyframes, then LocalBundleAdjustment (LocalMapping.cc:162-172) on its 50-keyframe window of a shared
+  map in HBM (mam3slam_amd/mapping.py): window read from the map, the B/K solves batched with the Levenberg control
+  on the device, the write-backs all-gathered over RCCL and applied to every GPU's map, which the next step's windows
+  read.
 N GPUs = N processes, each with its own B streams and B/K windows (weak scaling); the one collective is the map
 exchange.
 
@@ -159,17 +162,24 @@ class TrackingLeg:
         self.kps_h, self.cnt_h = kps_h, cnt_h
         cam = scene.kannala_brandt8(W, H) if cfg.get("camera") == "kb8" else scene.pinhole(W, H)
         self.cam = cam
-        lasts, mpls, poses = [], [], []
+        lasts, mpls, poses, poses_init = [], [], [], []
         F0 = None
         for f in range(B):
             rng = np.random.default_rng(1000 * rank + f)
             F = scene.make_frame_data(kps_h[f, :cnt_h[f, 0]], desc_h[f, :cnt_h[f, 0]], W, H)
-            F.pose = scene.small_pose(rng, rot=0.1, trans=0.3)
+            # the pose of the camera that rendered the frame (synth.frame_pose: the canvas as a plane in front of a
+            # translating, rolling Pinhole camera), so keyframes' poses and image content agree (SearchForTriangulation's
+            # epipolar tests between keyframes pass for real correspondences)
+            F.pose = synth.frame_pose(W, H, f)
             F0 = F0 or F
+            # the last frame's and the local map's MapPoints re-project onto the frame's keypoints under that pose
             lasts.append(scene.motion_last_frame(F, cam, rng))
             mpls.append(scene.local_world_mappoints(F, cam, rng))
             poses.append(F.pose)
-        self.F0, self.lasts, self.mpls, self.poses = F0, lasts, mpls, poses
+            # the motion model's guess mVelocity * LastFrame.GetPose() (Tracking.cc:2796): the true pose, 0.3 deg /
+            # 2 cm off
+            poses_init.append(scene.perturb_pose(F.pose, rng, rot=0.005, trans=0.02))
+        self.F0, self.lasts, self.mpls, self.poses, self.poses_init = F0, lasts, mpls, poses, poses_init
         Ls, Ms = max(len(x) for x in lasts), max(len(x) for x in mpls)
         self.Ls, self.Ms = Ls, Ms
         last = np.zeros((B, Ls), LAST_ENTRY_DTYPE)
@@ -178,12 +188,14 @@ class TrackingLeg:
         for f in range(B):
             last[f, :len(lasts[f])] = lasts[f]
             mpw[f, :len(mpls[f])] = mpls[f]
-            tcw[f]["q"], tcw[f]["t"] = poses[f]
+            tcw[f]["q"], tcw[f]["t"] = poses_init[f]
         self.tcw_bytes = tcw.dtype.itemsize
         self.d_last = torch.from_numpy(last.view(np.uint8).reshape(B, -1).copy()).to(dev)
         self.d_mpw = torch.from_numpy(mpw.view(np.uint8).reshape(B, -1).copy()).to(dev)
         self.d_mps = torch.zeros((B, Ms * MP_TRACK_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-        self.d_tcw = torch.from_numpy(tcw.view(np.uint8).copy()).to(dev)
+        # the motion model's guess (input of the step, never written) and the frame's pose as Tracking refines it
+        self.d_tcw_init = torch.from_numpy(tcw.view(np.uint8).copy()).to(dev)
+        self.d_tcw = self.d_tcw_init.clone()
         self.d_nlast = torch.tensor([len(x) for x in lasts], dtype=torch.int32, device=dev)
         self.d_nmps = torch.tensor([len(x) for x in mpls], dtype=torch.int32, device=dev)
         self.d_ntm = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -192,6 +204,16 @@ class TrackingLeg:
         self.d_nm1 = torch.zeros(B, dtype=torch.int32, device=dev)
         self.d_nm2 = torch.zeros(B, dtype=torch.int32, device=dev)
         self.d_taken = torch.zeros((B, cap), dtype=torch.uint8, device=dev)
+        # Optimizer::PoseOptimization after each search (Tracking.cc:2836, 2901): edges, their keypoints, outliers
+        # and results of both calls
+        from mam3slam_amd.pose import POSE_EDGE_DTYPE, POSE_RESULT_DTYPE, PoseOptimizer
+
+        self.inv_s2 = (np.float32(1.0) / F0.level_sigma2).astype(np.float32)
+        self.d_pe = torch.zeros((B, cap * POSE_EDGE_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        self.d_pk = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+        self.d_pout = torch.zeros((2, B, cap), dtype=torch.uint8, device=dev)
+        self.d_pn = torch.zeros((2, B), dtype=torch.int32, device=dev)
+        self.d_pres = torch.zeros((2, B, POSE_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
         for ln in self.lanes:
             lo = ln["lo"]
             ln["mm"] = ORBmatcher(0.9, True, device=di)
@@ -201,6 +223,9 @@ class TrackingLeg:
                                   self.d_cnt[lo].data_ptr(), None, self.d_taken[lo].data_ptr())
             ln["fr2"] = FramesDev(BL, cap, self.d_kps[lo].data_ptr(), self.d_desc[lo].data_ptr(),
                                   self.d_cnt[lo].data_ptr(), self.d_taken[lo].data_ptr(), None, 1)
+            ln["po"] = PoseOptimizer(device=di)
+            if ln["po"].max_edges() < cap:
+                raise RuntimeError(f"PoseOptimization holds {ln['po'].max_edges()} edges per frame, frames have {cap}")
         self.graph = None
 
     def _fork(self):
@@ -221,20 +246,54 @@ class TrackingLeg:
         for ln in self.lanes:
             self._extract_lane(ln)
 
-    def _match_lane(self, ln):
-        lo, st = ln["lo"], ln["stream"].cuda_stream
+    def _pose_lane(self, ln, k, lo=None, nf=None, st=None):
+        """Optimizer::PoseOptimization(&mCurrentFrame) of the lane's frames: call k = 0 after the motion search
+        (TrackWithMotionModel, Tracking.cc:2836, then its outlier discard :2840-2857), k = 1 after the local-map search
+        (TrackLocalMap, :2901); edges from the frames' slots (Optimizer.cc:856-895), the pose written back as
+        Frame::SetPose does."""
+        lo = ln["lo"] if lo is None else lo
+        BL = self.BL if nf is None else nf
+        st = ln["stream"].cuda_stream if st is None else st
+        cap = self.cap
+        po = ln["po"]
         tcw = self.d_tcw.data_ptr() + lo * self.tcw_bytes
-        ln["mm"].search_motion_batch_device(self.F0, ln["fr1"], tcw, self.cam, self.d_last[lo].data_ptr(), self.Ls,
+        pe, pk = self.d_pe[lo].data_ptr(), self.d_pk[lo].data_ptr()
+        pn, pout, pres = self.d_pn[k, lo:].data_ptr(), self.d_pout[k, lo].data_ptr(), self.d_pres[k, lo].data_ptr()
+        po.frame_edges_batch_device(BL, self.d_kps[lo].data_ptr(), cap, self.d_cnt[lo].data_ptr(), 2, self.inv_s2,
+                                    self.d_out1[lo].data_ptr(), self.d_last[lo].data_ptr(), self.Ls,
+                                    self.d_out2[lo].data_ptr() if k == 1 else None,
+                                    self.d_mpw[lo].data_ptr() if k == 1 else None, self.Ms, pe, cap, pn, pk, stream=st)
+        po.optimize_batch_device(BL, tcw, self.cam, pe, cap, pn, pout, pres, stream=st)
+        po.frame_update_batch_device(BL, pres, tcw, pout, pk, cap, pn, k == 0, self.d_out1[lo].data_ptr(),
+                                     self.d_taken[lo].data_ptr(), cap, stream=st)
+
+    def _match_lane(self, ln, lo=None, nf=None, st=None, fr1=None, fr2=None):
+        """The lane's frames (or nf frames from lo, frame sets fr1 / fr2, stream st) after extraction."""
+        lo = ln["lo"] if lo is None else lo
+        BL = self.BL if nf is None else nf
+        st = ln["stream"].cuda_stream if st is None else st
+        fr1 = ln["fr1"] if fr1 is None else fr1
+        fr2 = ln["fr2"] if fr2 is None else fr2
+        tcw0 = self.d_tcw_init.data_ptr() + lo * self.tcw_bytes
+        tcw = self.d_tcw.data_ptr() + lo * self.tcw_bytes
+        # TrackWithMotionModel: the current frame at the motion model's guess, SearchByProjection(Cur, Last, th 15),
+        # PoseOptimization, outliers discarded
+        ln["mm"].search_motion_batch_device(self.F0, fr1, tcw0, self.cam, self.d_last[lo].data_ptr(), self.Ls,
                                             self.d_nlast[lo:].data_ptr(), 15.0, self.d_out1[lo].data_ptr(),
                                             self.d_nm1[lo:].data_ptr(), stream=st)
-        ln["ml"].is_in_frustum_batch_device(self.F0, self.BL, tcw, self.cam, self.d_mpw[lo].data_ptr(), self.Ms,
+        self._pose_lane(ln, 0, lo, BL, st)
+        # TrackLocalMap: SearchLocalPoints (isInFrustum + SearchByProjection(F, localMPs, th 1)) at the optimised pose,
+        # then PoseOptimization with every match
+        ln["ml"].is_in_frustum_batch_device(self.F0, BL, tcw, self.cam, self.d_mpw[lo].data_ptr(), self.Ms,
                                             self.d_nmps[lo:].data_ptr(), self.d_mps[lo].data_ptr(),
                                             self.d_ntm[lo:].data_ptr(), stream=st)
-        ln["ml"].search_by_projection_batch_device(self.F0, ln["fr2"], self.d_mps[lo].data_ptr(), self.Ms,
+        ln["ml"].search_by_projection_batch_device(self.F0, fr2, self.d_mps[lo].data_ptr(), self.Ms,
                                                    self.d_nmps[lo:].data_ptr(), 1.0, self.d_out2[lo].data_ptr(),
                                                    self.d_nm2[lo:].data_ptr(), stream=st)
+        self._pose_lane(ln, 1, lo, BL, st)
 
     def launch(self):
+        self.d_tcw.copy_(self.d_tcw_init)   # every step tracks its frames from the motion model's guess
         self._fork()
         self._extract()
         for ln in self.lanes:
@@ -262,12 +321,13 @@ class TrackingLeg:
         after another, so every launch is timed standalone (as in a --lanes 1 rocprofv3 kernel trace)."""
         import torch
 
-        objs = [o for ln in self.lanes for o in (ln["ext"], ln["mm"])]
+        objs = [o for ln in self.lanes for o in (ln["ext"], ln["mm"], ln["po"])]
         for o in objs:
             o.set_profiling(True)
         torch.cuda.synchronize(self.dev)
         with torch.cuda.stream(self.tstream):
             for _ in range(steps):
+                self.d_tcw.copy_(self.d_tcw_init)
                 for ln in self.lanes:
                     ln["stream"].wait_stream(self.tstream)
                     self._extract_lane(ln)
@@ -283,6 +343,9 @@ class TrackingLeg:
             for k in ("grid", "gather", "resolve", "frustum"):
                 a = stages.get(k, (0.0, 0))
                 stages[k] = (a[0] + sm[k][0], a[1] + sm[k][1])
+            sp = ln["po"].stage_times()["pose"]
+            a = stages.get("pose", (0.0, 0))
+            stages["pose"] = (a[0] + sp[0], a[1] + sp[1])
         for o in objs:
             o.set_profiling(False)
         return stages
@@ -306,15 +369,10 @@ def latency_section(tr):
     st = tr.tstream.cuda_stream
 
     def one_frame_launch():
+        tr.d_tcw[:1].copy_(tr.d_tcw_init[:1])
         tr.ext.extract_batch_device(tr.d_img.data_ptr(), 1, tr.W, tr.H, tr.W, tr.W * tr.H, tr.d_kps.data_ptr(),
                                     tr.d_desc.data_ptr(), cap, tr.d_cnt.data_ptr(), stream=st)
-        ln["mm"].search_motion_batch_device(tr.F0, fr1, tr.d_tcw.data_ptr(), tr.cam, tr.d_last.data_ptr(), tr.Ls,
-                                            tr.d_nlast.data_ptr(), 15.0, tr.d_out1.data_ptr(), tr.d_nm1.data_ptr(),
-                                            stream=st)
-        ln["ml"].is_in_frustum_batch_device(tr.F0, 1, tr.d_tcw.data_ptr(), tr.cam, tr.d_mpw.data_ptr(), tr.Ms,
-                                            tr.d_nmps.data_ptr(), tr.d_mps.data_ptr(), tr.d_ntm.data_ptr(), stream=st)
-        ln["ml"].search_by_projection_batch_device(tr.F0, fr2, tr.d_mps.data_ptr(), tr.Ms, tr.d_nmps.data_ptr(), 1.0,
-                                                   tr.d_out2.data_ptr(), tr.d_nm2.data_ptr(), stream=st)
+        tr._match_lane(ln, 0, 1, st, fr1, fr2)
 
     with torch.cuda.stream(tr.tstream):
         one_frame_launch()
@@ -378,11 +436,14 @@ def ingest_section(tr, reps=5):
 
 
 def parity_section(tr, mapping, newmp=None):
-    """In-run parity against the oracle: one frame's extraction, the same frame's frustum + local search chain, and
-    one LocalBundleAdjustment window of the timed region (the same inputs): bit-exact / index-exact / <= 1e-4 with
-    the same Levenberg control flow."""
+    """In-run parity against the oracle, stage by stage on each stage's own inputs from the timed region: one frame's
+    extraction; its TrackWithMotionModel (motion search, PoseOptimization, outlier discard) and TrackLocalMap
+    (isInFrustum + local-map search at the optimised pose, PoseOptimization); one CreateNewMapPoints search; one
+    LocalBundleAdjustment window: bit-exact / index-exact / identical outlier sets and LM control flow, floats within
+    1e-4."""
     from mam3slam_amd import scene
-    from mam3slam_amd.match import MP_TRACK_DTYPE
+    from mam3slam_amd.match import LAST_ENTRY_DTYPE, MP_TRACK_DTYPE
+    from mam3slam_amd.pose import POSE_RESULT_DTYPE, make_edges, set_pose_float
     from oracle import oracle_py
 
     out = {}
@@ -395,19 +456,43 @@ def parity_section(tr, mapping, newmp=None):
                                                          for k in ("x", "y", "angle", "response", "octave"))
                                     and np.array_equal(dg, do))
     F = scene.make_frame_data(kg, dg, tr.W, tr.H)
-    F.pose = tr.poses[f]
+    # TrackWithMotionModel
+    F.pose = tr.poses_init[f]
+    last = np.ascontiguousarray(tr.lasts[f], LAST_ENTRY_DTYPE)
+    _, o1 = oracle_py.search_by_projection_motion(F, last, tr.cam, 15.0, True)
+    idx = np.nonzero(o1 >= 0)[0]
+    e1 = make_edges(F.keys, tr.inv_s2, idx, last["pos"][o1[idx]])
+    res = tr.d_pres[:, f].cpu().numpy().view(POSE_RESULT_DTYPE).reshape(2)
+    pout = tr.d_pout[:, f].cpu().numpy()
+    _, ol1, (q1, t1), _ = oracle_py.pose_optimization_edges(tr.poses_init[f], tr.cam, e1)
+    o1 = o1.copy()
+    o1[idx[ol1 == 1]] = -1
+    out["motion_search_index_exact"] = bool(np.array_equal(tr.d_out1[f, :n].cpu().numpy(), o1))
+    d1 = float(max(np.abs(res[0]["t"] - t1).max() / max(np.abs(t1).max(), 1.0), np.abs(res[0]["q"] - q1).max()))
+    # TrackLocalMap at the optimised pose
+    F.pose = set_pose_float(res[0]["q"], res[0]["t"])
     no, to = oracle_py.is_in_frustum(F, tr.mpls[f], tr.cam)
     tg = tr.d_mps[f].cpu().numpy().view(MP_TRACK_DTYPE)[:len(tr.mpls[f])]
     v = to["track_in_view"] == 1
     out["frustum_exact"] = bool(int(tr.d_ntm[f].item()) == no and np.array_equal(tg["proj_x"], to["proj_x"]) and
                                 np.array_equal(tg["proj_y"], to["proj_y"]) and
                                 np.array_equal(tg["scale_level"][v], to["scale_level"][v]))
-    # the local search's `taken` input: the slot state the motion search left (mvpMapPoints[i] holds a MapPoint with
-    # Observations() > 0), taken_out of the motion search of the same step
+    # the local search's `taken` input: the slots the motion search filled with a MapPoint with observations, less the
+    # discarded outliers
     F.taken = tr.d_taken[f, :n].cpu().numpy()
     nmo, oo = oracle_py.search_by_projection(F, to, 1.0, False, 50.0, 0.8)
     out["local_search_index_exact"] = bool(int(tr.d_nm2[f].item()) == nmo and
                                            np.array_equal(tr.d_out2[f, :n].cpu().numpy(), oo))
+    idx2 = np.nonzero((oo >= 0) | (o1 >= 0))[0]
+    mp = np.ascontiguousarray(tr.mpls[f])
+    pos = np.where((oo[idx2] >= 0)[:, None], mp["pos"][np.maximum(oo[idx2], 0)], last["pos"][np.maximum(o1[idx2], 0)])
+    e2 = make_edges(F.keys, tr.inv_s2, idx2, pos)
+    _, ol2, (q2, t2), _ = oracle_py.pose_optimization_edges(F.pose, tr.cam, e2)
+    d2 = float(max(np.abs(res[1]["t"] - t2).max() / max(np.abs(t2).max(), 1.0), np.abs(res[1]["q"] - q2).max()))
+    out["pose_optimization_same_outliers"] = bool(np.array_equal(pout[0, :len(e1)], ol1) and
+                                                  np.array_equal(pout[1, :len(e2)], ol2))
+    out["pose_optimization_max_rel_diff"] = max(d1, d2)
+    out["pose_optimization_edges"] = [len(e1), len(e2)]
     if newmp is not None:
         # pair 0 of the last step's CreateNewMapPoints searches, FeatureVectors from the device BoW
         K1, K2 = newmp.pair_inputs(0)
@@ -418,6 +503,17 @@ def parity_section(tr, mapping, newmp=None):
         out["triangulation_index_exact"] = bool(int(newmp.nmatch[0].item()) == no and
                                                 np.array_equal(newmp.out[0, :n1].cpu().numpy(), oo))
         out["triangulation_pair"] = {"matches": int(no), "n1": n1, "n2": len(K2.keys), "oracle_ms": tri_ms}
+        # SearchInNeighbors: forward item 0 (keyframe 0's MapPoints into its nearest neighbour) and backward item 0
+        ok, fused = True, []
+        for backward, gi, gd, gn in ((False, newmp.fwd_idx, newmp.fwd_dist, newmp.fwd_n),
+                                     (True, newmp.bwd_idx, newmp.bwd_dist, newmp.bwd_n)):
+            KF, mps = newmp.fuse_inputs(backward, 0)
+            nf, io, do_ = oracle_py.fuse(KF, mps, tr.cam, 3.0)
+            ok = ok and int(gn[0].item()) == nf and np.array_equal(gi[0, :len(mps)].cpu().numpy(), io) and \
+                np.array_equal(gd[0, :len(mps)].cpu().numpy(), do_)
+            fused.append(int(nf))
+        out["fuse_index_exact"] = bool(ok)
+        out["fuse_items"] = {"forward_fused": fused[0], "backward_fused": fused[1]}
     if mapping is not None:
         w = 0
         prob = mapping.window_inputs(w)
@@ -433,25 +529,70 @@ def parity_section(tr, mapping, newmp=None):
     return out
 
 
+def host_info():
+    """The host the CPU baseline ran on: CPU model, cores online, the affinity list of this process."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = []
+
+    def ranges(v):
+        out, i = [], 0
+        while i < len(v):
+            j = i
+            while j + 1 < len(v) and v[j + 1] == v[j] + 1:
+                j += 1
+            out.append(f"{v[i]}-{v[j]}" if j > i else f"{v[i]}")
+            i = j + 1
+        return ",".join(out)
+
+    return {"cpu_model": model, "nproc_online": os.cpu_count(), "affinity": ranges(aff), "affinity_count": len(aff),
+            "threads_used": 1}
+
+
 def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
     """The oracle (single-thread C++ restatement of the reference path) on a bounded sample of the same per-frame
-    work: extraction + motion search + isInFrustum + local search, plus 1/K of a LocalBundleAdjustment of a window of
-    the timed region (its oracle time measured in parity_section on the same inputs)."""
+    work — extraction, TrackWithMotionModel (motion search, PoseOptimization, outlier discard) and TrackLocalMap
+    (isInFrustum + local-map search, PoseOptimization) — plus 1/K of a keyframe's LocalMapping work: a
+    LocalBundleAdjustment of a window of the timed region (its oracle time measured in parity_section on the same
+    inputs), its 30 SearchForTriangulation and ComputeBoW."""
     from mam3slam_amd import scene
+    from mam3slam_amd.match import LAST_ENTRY_DTYPE
+    from mam3slam_amd.pose import make_edges, set_pose_float
     from oracle import oracle_py
 
     p = oracle_py.params(cfg["nfeatures"])
     W, H = cfg["width"], cfg["height"]
+    lasts = [np.ascontiguousarray(x, LAST_ENTRY_DTYPE) for x in tr.lasts]
+    mpls = [np.ascontiguousarray(x) for x in tr.mpls]
     n, t0 = 0, time.perf_counter()
     while True:
         f = n % len(tr.frames)
         k, d, _ = oracle_py.extract(tr.frames[f], p)
         F = scene.make_frame_data(k, d, W, H)
-        F.pose = tr.poses[f]
-        _, out = oracle_py.search_by_projection_motion(F, tr.lasts[f], tr.cam, 15.0, True)
-        F.taken = (out >= 0).astype(np.uint8)
-        _, tracks = oracle_py.is_in_frustum(F, tr.mpls[f], tr.cam)
-        oracle_py.search_by_projection(F, tracks, 1.0, nnratio=0.8)
+        F.pose = tr.poses_init[f]
+        last = lasts[f]
+        _, o1 = oracle_py.search_by_projection_motion(F, last, tr.cam, 15.0, True)
+        idx = np.nonzero(o1 >= 0)[0]
+        _, ol1, (q, t), _ = oracle_py.pose_optimization_edges(
+            F.pose, tr.cam, make_edges(F.keys, tr.inv_s2, idx, last["pos"][o1[idx]]))
+        o1[idx[ol1 == 1]] = -1
+        F.pose = set_pose_float(q, t)
+        F.taken = ((o1 >= 0) & (last["nobs"][np.maximum(o1, 0)] > 0)).astype(np.uint8)
+        _, tracks = oracle_py.is_in_frustum(F, mpls[f], tr.cam)
+        _, o2 = oracle_py.search_by_projection(F, tracks, 1.0, nnratio=0.8)
+        idx2 = np.nonzero((o2 >= 0) | (o1 >= 0))[0]
+        pos = np.where((o2[idx2] >= 0)[:, None], mpls[f]["pos"][np.maximum(o2[idx2], 0)],
+                       last["pos"][np.maximum(o1[idx2], 0)])
+        oracle_py.pose_optimization_edges(F.pose, tr.cam, make_edges(F.keys, tr.inv_s2, idx2, pos))
         n += 1
         el = time.perf_counter() - t0
         if (el >= seconds and n >= 5) or n >= 2000:
@@ -473,20 +614,41 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
         t2 = time.perf_counter()
         oracle_py.bow_transform(newmp.voc.v, d, 4, tree=tree)
         bow_ms = (time.perf_counter() - t2) * 1e3
-        per_frame_ms += (tri_ms + bow_ms) / K
+        # its SearchInNeighbors: Fuse into its 30 neighbours, its fuse candidates into it, and the distinctive
+        # descriptors of its MapPoints (the update's share of one keyframe)
+        sin_ms = 0.0
+        for q in range(newmp.NN):
+            KF, mps = newmp.fuse_inputs(False, q)
+            t2 = time.perf_counter()
+            oracle_py.fuse(KF, mps, tr.cam, 3.0)
+            sin_ms += (time.perf_counter() - t2) * 1e3
+        for q in range(newmp.NB_BACK):
+            KF, mps = newmp.fuse_inputs(True, q)
+            t2 = time.perf_counter()
+            oracle_py.fuse(KF, mps, tr.cam, 3.0)
+            sin_ms += (time.perf_counter() - t2) * 1e3
+        off = newmp.upd_off.cpu().numpy()
+        n1 = newmp.upd_n // newmp.W
+        descs = newmp.upd_desc[:int(off[n1])].cpu().numpy()
+        t2 = time.perf_counter()
+        oracle_py.distinctive_descriptors(off[:n1 + 1], descs)
+        sin_ms += (time.perf_counter() - t2) * 1e3
+        per_frame_ms += (tri_ms + bow_ms + sin_ms) / K
     res = {"value": 1e3 / per_frame_ms, "unit": "frames/s", "cores": 1, "kind": "port",
-           "tracking_ms_per_frame": track_ms,
+           "tracking_ms_per_frame": track_ms, "host": host_info(),
            "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15) + "
-                     f"isInFrustum + SearchByProjection(local map, th 1) on the oracle C++ restatement "
-                     f"(g++ -O3 -march=x86-64-v3, the reference's CMake -O3 -march=native level; scalar), "
-                     f"single thread, {el:.1f}s"}
+                     f"PoseOptimization + isInFrustum + SearchByProjection(local map, th 1) + PoseOptimization on the "
+                     f"oracle C++ restatement (g++ -O3 -march=x86-64-v3, the reference's CMake -O3 -march=native "
+                     f"level; scalar code where the reference's OpenCV FAST / resize / blur are SIMD), single thread, "
+                     f"{el:.1f}s"}
     if lba_window_ms is not None:
         res["lba_ms_per_window"] = lba_window_ms
         res["sample"] += f"; + LocalBundleAdjustment of a timed-region window ({lba_window_ms:.1f} ms) / {K} frames"
     if tri_ms is not None:
-        res["new_keyframe_search_ms"] = {"triangulation_30_pairs": tri_ms, "compute_bow": bow_ms}
-        res["sample"] += (f"; + one new keyframe's 30 SearchForTriangulation ({tri_ms:.1f} ms) and ComputeBoW "
-                          f"({bow_ms:.2f} ms) / {K} frames")
+        res["new_keyframe_search_ms"] = {"triangulation_30_pairs": tri_ms, "compute_bow": bow_ms,
+                                         "search_in_neighbors": sin_ms}
+        res["sample"] += (f"; + one new keyframe's 30 SearchForTriangulation ({tri_ms:.1f} ms), ComputeBoW "
+                          f"({bow_ms:.2f} ms) and SearchInNeighbors ({sin_ms:.1f} ms) / {K} frames")
     return res
 
 
@@ -513,6 +675,7 @@ def main():
     ap.add_argument("--launch-check", action="store_true",
                     help="rendezvous + barrier over gloo on the CPU and exit (tests the --gpus N launcher, no GPU)")
     args = ap.parse_args()
+    parity_failed = [False]
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # before any HIP call: the ranks are children, never an exec of this process
@@ -653,8 +816,10 @@ def main():
     if mapping is not None:
         lba_stage = mapping.solver.stage_times()
         mapping.solver.set_profiling(False)
-        tri_stage = {"triangulation": newmp.matcher.stage_times()["triangulation"],
-                     "compute_bow": newmp.voc.stage_times()["transform"]}
+        mst = newmp.matcher.stage_times()
+        tri_stage = {"triangulation": mst["triangulation"], "compute_bow": newmp.voc.stage_times()["transform"],
+                     "search_in_neighbors": (mst["fuse"][0] + mst["distinctive"][0] + mst["grid"][0],
+                                             mst["fuse"][1] + mst["distinctive"][1])}
         newmp.matcher.set_profiling(False)
         newmp.voc.set_profiling(False)
         stv = int(mapping.status.cpu().numpy()[0])
@@ -688,7 +853,8 @@ def main():
     sb = stage_bytes(tr.W, tr.H, n_kp, n_cand, mean_last, mean_mps, cand_motion=mean_last * 6.0,
                      cand_local=mean_mps * 3.0)
     per_step_ms = {k: v[0] / args.steps for k, v in stages.items()}
-    dom = max(stages, key=lambda k: stages[k][0])
+    # the HBM roofline is over the byte-moving stages (PoseOptimization is FP64 compute: per_step_ms only)
+    dom = max((k for k in stages if k in sb), key=lambda k: stages[k][0])
     ms_tot, launches = stages[dom]
     avg_ms = ms_tot / max(launches, 1)
     launches_per_step = launches / args.steps
@@ -704,12 +870,22 @@ def main():
             pmc_counters = {k: tj.get(k, {}).get(dom) for k in ("valu_busy", "wave_frac_wait", "wave_frac_issue_stall")}
         except Exception:
             traffic = traffic_raw = None
+    limiter = ROOFLINE_NOTES.get(dom)
+    if pmc_counters and all(v is not None for v in pmc_counters.values()):
+        # the limiter as this config's counters give it (scripts/gpu_fast_pmc.sh -> profiles/traffic_<config>.json)
+        limiter = (f"latency / issue: per standalone launch VALU busy {100 * pmc_counters['valu_busy']:.1f}%, "
+                   f"{100 * pmc_counters['wave_frac_wait']:.0f}% of wave cycles waiting (s_waitcnt, barriers), "
+                   f"{100 * pmc_counters['wave_frac_issue_stall']:.0f}% issue-stalled; HBM traffic "
+                   f"{(traffic or 0) / 1e6:.1f} MB (raw FETCH {(traffic_raw or 0) / 1e6:.1f} MB) vs "
+                   f"{sb[dom] * B / (launches / args.steps) / 1e6:.1f} MB algorithmic per launch "
+                   f"(profiles/traffic_{args.config}.json)")
 
     if rank == 0:
         W, H, NF = tr.W, tr.H, tr.NF
         camd = "KannalaBrandt8 (test YAML)" if cfg.get("camera") == "kb8" else "Pinhole"
         workload = (f"{args.config}: mono {W}x{H}, {NF} features, 8 levels, {camd}; step = {B} frame streams x (ORB "
-                    f"extract + SearchByProjection motion th15 + isInFrustum + SearchByProjection local map th1)")
+                    f"extract + TrackWithMotionModel: SearchByProjection motion th15 + PoseOptimization + outlier "
+                    f"discard; TrackLocalMap: isInFrustum + SearchByProjection local map th1 + PoseOptimization)")
         if agents_total:
             workload += f"; {agents_total} agents in total, {B} per GPU"
         if mapping is not None:
@@ -741,7 +917,7 @@ def main():
                        "parallelism": f"agents{world} (one process per GPU; {B} frame streams per GPU)",
                        "lanes": NL, "launch": "hip graph per tracking step" if tr.graph is not None else "eager"},
             "stage_ms_per_step": per_step_ms,
-            "roofline": {"bound": "hbm", "kernel": dom, "limiter": ROOFLINE_NOTES.get(dom), "achieved": achieved,
+            "roofline": {"bound": "hbm", "kernel": dom, "limiter": limiter, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_raw_fetch": traffic_raw, "pmc": pmc_counters,
                          "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms},
@@ -777,11 +953,16 @@ def main():
                 "matches_per_search": float(nmv.mean()),
                 "ms_per_step_triangulation": tri_ms,
                 "ms_per_step_compute_bow": tri_stage["compute_bow"][0] / args.steps,
+                "ms_per_step_search_in_neighbors": tri_stage["search_in_neighbors"][0] / args.steps,
+                "fused_per_forward_fuse": float(newmp.fwd_n.float().mean().item()),
+                "fused_per_backward_fuse": float(newmp.bwd_n.float().mean().item()),
                 "candidate_pairs_per_search": tri_b["candidate_pairs"] / newmp.npairs,
                 "algorithmic_bytes_per_step_triangulation": tri_b["bytes"],
                 "achieved_GBs_triangulation": tri_b["bytes"] / (tri_ms * 1e-3) / 1e9 if tri_ms > 0 else None,
                 "note": "ComputeBoW (levelsup 4, synthetic k=10 L=6 vocabulary) + CreateNewMapPoints' "
-                        "SearchForTriangulation against the 30 previously inserted keyframes, on their own stream as "
+                        "SearchForTriangulation against the 30 nearest keyframes of the agent's sequence + "
+                        "SearchInNeighbors (Fuse into the 30, Fuse of 4 neighbours' MapPoints back, "
+                        "ComputeDistinctiveDescriptors), on their own stream as "
                         "soon as the keyframes are ingested, before the LBA windows of the same keyframes (stage "
                         "times on that stream, concurrent with tracking, from a second untimed pass of the same steps "
                         "with the HIP events on; --profile-timed records them inside the timed region); algorithmic bytes per SURVEY §8(d): "
@@ -793,6 +974,13 @@ def main():
             out["search_in_neighbors"] = sin_info
         if parity is not None:
             out["parity"] = parity
+            # every exactness flag must hold and every float difference stay inside the north star's 1e-4
+            bad = [k for k, v in parity.items() if isinstance(v, bool) and not v]
+            bad += [k for k in ("lba_max_point_rel_diff", "pose_optimization_max_rel_diff")
+                    if parity.get(k) is not None and not parity[k] <= 1e-4]
+            out["parity_ok"] = not bad
+            if bad:
+                out["invalid"] = "parity failed: " + ", ".join(bad)
         if not args.no_cpu_baseline:
             lba_cpu = parity.get("lba_window", {}).get("oracle_ms") if parity else None
             out["cpu_baseline"] = cpu_baseline(tr, cfg, lba_cpu, K, args.cpu_seconds, newmp)
@@ -800,8 +988,13 @@ def main():
             if lat is not None:
                 out["speedup_latency_b1"] = out["cpu_baseline"]["tracking_ms_per_frame"] / lat["device_graph_ms"]
         print(json.dumps(out), flush=True)
+        if out.get("invalid"):
+            print(out["invalid"], file=sys.stderr)
+            parity_failed[0] = True
     if world > 1:
         dist.destroy_process_group()
+    if parity_failed[0]:
+        raise SystemExit(1)
 
 
 if __name__ == "__main__":

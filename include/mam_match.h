@@ -266,6 +266,19 @@ int mam_search_by_projection_motion_batch_device(mam_match_ctx* ctx, const mam_f
 /* Fuse into many keyframes in one launch (SearchInNeighbors' forward direction, LocalMapping.cc:881-890): keyframe f
  * (frames: its keypoints) with kfs[f] searches n_mps[f] MapPoints at mps + f*mp_stride. Outputs at
  * out_idx / out_dist + f*mp_stride and out_nfused[f]. */
+/* Fuse(pKF, vpMapPoints, th) for n_items (keyframe, MapPoint list) pairs over one device-resident keyframe set:
+ * SearchInNeighbors' two directions (LocalMapping.cc:881-918), the current keyframe's MapPoints into each target
+ * keyframe and the targets' fuse candidates into the current keyframe, where one keyframe and one MapPoint list serve
+ * many pairs. Item b fuses MapPoint list mp_of[b] (mps + mp_of[b] * mp_stride, n_mps[mp_of[b]] entries) into keyframe
+ * frame_of[b] of `frames` (its pose kf_tcw[frame_of[b]] = GetPose(), the camera centre derived as
+ * KeyFrame::GetCameraCenter does; log_scale_factor = mfLogScaleFactor); every keyframe's cell grid is built once per
+ * call. Results as mam_fuse_batch_device's per item: out_idx / out_dist + b * mp_stride, out_nfused[b]. */
+int mam_fuse_items_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_frames_dev* frames,
+                                const mam_pose* kf_tcw, float log_scale_factor, const mam_camera* cam, int n_items,
+                                const int32_t* frame_of, const int32_t* mp_of, const mam_fuse_mp* mps, int mp_stride,
+                                const int32_t* n_mps, float th, int32_t* out_idx, int32_t* out_dist,
+                                int32_t* out_nfused, void* stream);
+
 int mam_fuse_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_frames_dev* frames,
                           const mam_fuse_kf* kfs, const mam_camera* cam, const mam_fuse_mp* mps, int mp_stride,
                           const int32_t* n_mps, float th, int32_t* out_idx, int32_t* out_dist, int32_t* out_nfused,

@@ -62,6 +62,27 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* ctx, int nframes, const mam
                                        const mam_pose_edge* edges, int edge_stride, const int32_t* n_edges,
                                        uint8_t* outlier, mam_pose_result* results, void* stream);
 
+/* The frame side of the call for device-resident tracked frames (the Tracking sequence of bench.py):
+ * Optimizer::PoseOptimization's edge build (Optimizer.cc:856-895): frame f's keypoints (kps + f * kp_stride,
+ * kp_count[f * count_stride] of them) whose slot holds a MapPoint — match_local[i] >= 0 (index into local_mps of the
+ * frame, SearchByProjection(F, vpMapPoints)'s match; may be NULL) else match_last[i] >= 0 (index into last, the motion
+ * search's) — one edge each in increasing i with information inv_level_sigma2[octave] (host array of nlevels);
+ * n_edges[f] (MAM_ERR_CAPACITY beyond edge_stride) and edge_kp (the keypoint of each edge). Asynchronous. */
+int mam_pose_frame_edges_batch_device(mam_pose_ctx* ctx, int nframes, const mam_keypoint* kps, int kp_stride,
+                                      const int32_t* kp_count, int count_stride, const float* inv_level_sigma2,
+                                      int nlevels, const int32_t* match_last, const mam_last_entry* last,
+                                      int last_stride, const int32_t* match_local, const mam_local_mp* local_mps,
+                                      int local_stride, mam_pose_edge* edges, int edge_stride, int32_t* n_edges,
+                                      int32_t* edge_kp, void* stream);
+
+/* Tracking's use of the result: Frame::SetPose(SE3f(q.cast<float>(), t.cast<float>())) into tcw[f], and with discard
+ * the outliers' slots emptied as TrackWithMotionModel does after its PoseOptimization (Tracking.cc:2840-2857):
+ * match_last[i] = -1 and taken[i] = 0 (taken may be NULL) for the keypoint of every outlier edge. Asynchronous. */
+int mam_pose_frame_update_batch_device(mam_pose_ctx* ctx, int nframes, const mam_pose_result* results, mam_pose* tcw,
+                                       const uint8_t* outlier, const int32_t* edge_kp, int edge_stride,
+                                       const int32_t* n_edges, int discard, int32_t* match_last, uint8_t* taken,
+                                       int kp_stride, void* stream);
+
 /* Largest edge_stride one frame's workgroup can hold (LDS). */
 int mam_pose_max_edges(mam_pose_ctx* ctx);
 

@@ -1006,11 +1006,11 @@ __device__ __forceinline__ double bcast16_d(double v, int k) {
 
 // acc += (value of src in lane K of this lane's 16-lane row) * m: the broadcast folded into the FMA as one
 // v_fmac_f64_dpp row_newbcast (gfx950 DPP64); one instruction where a v_mov_b64_dpp + v_fma_f64 pair was. The s_nop
-// covers the VALU-write -> DPP-read hazard on src (inline asm is not seen by the hazard recognizer). Same rounding as
-// fma(src_K, m, acc).
+// covers the VALU-write -> DPP-read hazard on src (inline asm is not seen by the hazard recognizer); not volatile, so
+// the scheduler may interleave independent work. Same rounding as fma(src_K, m, acc).
 template <int K>
 __device__ __forceinline__ void fmac_bcast16(double& acc, double src, double m) {
-    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
                  : "+v"(acc)
                  : "v"(src), "v"(m), "n"(K));
 }
@@ -1194,12 +1194,13 @@ constexpr int C1_PF = MAM_LDLT_C1_PF;   // (C1) tiles per wave prefetched across
 constexpr int LDLT_TM_MAX = 40;         // the LDS path's tile-mask copy: nt <= 40 (npad <= 640)
 // The factorization's static LDS, shared by both forms of k_ldlt (ldlt_global, ldlt_tiles)
 struct LdltShared {
-    double Ld[NB * NB];
+    double Ld[NB * NB];          // ldlt_global: L11 row-major; ldlt_tiles: M = L11^-T D^-1 row-major
     double dk[2][NB];
     double invdk[NB];
     int fail;
     // ldlt_global<true>: the tile mask (uint8 [nt][nt]); ldlt_tiles: the tile slot map (int16 [nt][nt])
     int16_t map[LDLT_TM_MAX * LDLT_TM_MAX];
+    int16_t tl[2 * 96];          // ldlt_tiles: (r, c) of each pool slot
 };
 
 // S factored in place in HBM with the panel / block-column workspace in LDS (use_lds) or in the problem's scratch: the
@@ -1430,8 +1431,27 @@ __device__ __forceinline__ void tile_update(double* TL, int sc, int sa, int sb, 
     for (int r = 0; r < 4; r++) C[tsw(rq + 4 * r, col)] = acc[r];
 }
 
-// wave 0: LDL^T of diagonal tile kc of the pool, written back in place (L below, D on the diagonal), Ld / dk / invdk
-// for the panel rows and the trailing update, and the forward block solve of y
+// X = L11^-1 by columns, lane c holding column c (x[r] = X(r, c)): x[R] -= L(R, J) x[J] for J < R, L(R, J) broadcast
+// from lane R (row[J] there) into the FMA
+template <int R, int J>
+struct Inv16 {
+    __device__ __forceinline__ static void run(double* x, const double* row) {
+        fmac_bcast16<R>(x[R], row[J], -x[J]);
+        Inv16<R, J + 1>::run(x, row);
+    }
+};
+template <int R>
+struct Inv16<R, R> {
+    __device__ __forceinline__ static void run(double* x, const double* row) { Inv16<R + 1, 0>::run(x, row); }
+};
+template <>
+struct Inv16<NB, 0> {
+    __device__ __forceinline__ static void run(double*, const double*) {}
+};
+
+// wave 0: LDL^T of diagonal tile sd of the pool, written back in place (L below, D on the diagonal, and L^-T above it
+// for the backward solve), dk / invdk, M = L11^-T D^-1 (row-major, sh.Ld) for the panel rows (L21 = A21 M, an MFMA
+// product instead of a per-row forward substitution), and the forward block solve of y
 __device__ __forceinline__ void tiles_diag(double* TL, int sd, int kb, double* Y, LdltShared& sh, double* dkp,
                                            int lane) {
     double* T = TL + (size_t)sd * 256;
@@ -1440,17 +1460,28 @@ __device__ __forceinline__ void tiles_diag(double* TL, int sd, int kb, double* Y
     for (int c = 0; c < NB; c++) row[c] = lane < NB ? T[tsw(lane, c)] : 0.0;
     const double dmine = diag16_factor(row, lane);
     const double yv = diag16_forward(row, lane < NB ? Y[kb + lane] : 0.0, lane);
+    const double invd = dmine != 0.0 ? 1.0 / dmine : 0.0;
     if (lane < NB) {
 #pragma unroll
-        for (int c = 0; c < NB; c++) {
-            sh.Ld[lane * NB + c] = row[c];
+        for (int c = 0; c < NB; c++)
             if (c < lane) T[tsw(lane, c)] = row[c];
-        }
         T[tsw(lane, lane)] = dmine;
         dkp[lane] = dmine;
-        sh.invdk[lane] = dmine != 0.0 ? 1.0 / dmine : 0.0;
+        sh.invdk[lane] = invd;
         Y[kb + lane] = yv;
         if (dmine == 0.0) sh.fail = 1;
+    }
+    double x[NB];
+#pragma unroll
+    for (int r = 0; r < NB; r++) x[r] = (r == lane) ? 1.0 : 0.0;
+    Inv16<1, 0>::run(x, row);
+    if (lane < NB) {
+        // lane c: row c of L^-T is column c of X; M(c, r) = X(r, c) / d_r
+#pragma unroll
+        for (int r = 0; r < NB; r++) {
+            sh.Ld[lane * NB + r] = x[r] * sh.invdk[r];
+            if (r > lane) T[tsw(lane, r)] = x[r];
+        }
     }
 }
 
@@ -1467,17 +1498,43 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     int16_t* slot = sh.map;                     // [nt][nt]
     if (t == 0) sh.fail = 0;
     for (int q = t; q < nt * nt; q += LDLT_THREADS) slot[q] = d.tslot[q];
-    // the pool: tile s = (r, c) holds S rows 16 r.., columns 16 c..; the padding rows' diagonal is 1 (an identity block
-    // after the unknowns: S's padding rows are zero)
-    for (int q = t; q < T * 256; q += LDLT_THREADS) {
-        const int s = q >> 8, e = q & 255, i = e >> 4, j = e & 15;
-        const int r = d.tlist[2 * s], c = d.tlist[2 * s + 1];
-        const int gi = NB * r + i, gj = NB * c + j;
-        double v = d.S[(size_t)gi * N + gj];
-        if (gi == gj && gi >= n) v = 1.0;
-        TL[(size_t)s * 256 + tsw(i, j)] = v;
-    }
+    for (int q = t; q < 2 * T; q += LDLT_THREADS) sh.tl[q] = d.tlist[q];
     for (int i = t; i < N; i += LDLT_THREADS) Y[i] = i < n ? d.bs[i] : 0.0;
+    __syncthreads();
+    // the pool: tile s = (r, c) holds S rows 16 r.., columns 16 c..; the padding rows' diagonal is 1 (an identity block
+    // after the unknowns: S's padding rows are zero). One wave per tile, lane = (row, 4 columns): two 16-byte loads per
+    // lane, the wave's tiles' loads issued together
+    {
+        const int i = lane >> 2, j0 = 4 * (lane & 3);
+        for (int s0 = wid; s0 < T; s0 += 2 * NW) {
+            double2 v[2][2];
+            int rr[2], cc[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int s = s0 + u * NW;
+                rr[u] = s < T ? sh.tl[2 * s] : 0;
+                cc[u] = s < T ? sh.tl[2 * s + 1] : 0;
+                const double2* src = reinterpret_cast<const double2*>(d.S + (size_t)(NB * rr[u] + i) * N + NB * cc[u] + j0);
+                if (s < T) {
+                    v[u][0] = src[0];
+                    v[u][1] = src[1];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int s = s0 + u * NW;
+                if (s >= T) continue;
+                double e[4] = {v[u][0].x, v[u][0].y, v[u][1].x, v[u][1].y};
+                double* D = TL + (size_t)s * 256;
+                const int gi = NB * rr[u] + i;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int gj = NB * cc[u] + j0 + k;
+                    D[tsw(i, j0 + k)] = (gi == gj && gi >= n) ? 1.0 : e[k];
+                }
+            }
+        }
+    }
     __syncthreads();
     if (wid == 0) tiles_diag(TL, slot[0], 0, Y, sh, sh.dk[0], lane);
     __syncthreads();
@@ -1485,30 +1542,30 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     for (int kc = 0, p = 0; kc < nt; kc++, p ^= 1) {
         const int kb = NB * kc;
         const double* dkp = sh.dk[p];
-        // (B) panel rows: one thread per row of the tiles (r, kc), r > kc
-        for (int i = kb + NB + t; i < N; i += LDLT_THREADS) {
-            const int s = slot[(i / NB) * nt + kc];
-            if (s < 0) continue;
-            double* Tr = TL + (size_t)s * 256;
-            const int ri = i & 15;
-            // keep the L11 factors in LDS (reading them per row): hoisting all 120 into registers spills
-            asm volatile("" ::: "memory");
-            double w[NB];
+        // (B) panel rows: one wave per non-zero tile (r, kc), r > kc: L21 = A21 M (M = L11^-T D^-1 from the diagonal
+        // factorization) as four f64 MFMAs, in place; then y_r -= L21 y_kc, one row per lane
+        {
+            const int col = lane & 15, rq = lane >> 4;
+            for (int r = kc + 1 + wid; r < nt; r += NW) {
+                const int s = slot[r * nt + kc];
+                if (s < 0) continue;
+                double* Tr = TL + (size_t)s * 256;
+                dbl4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < NB; j++) w[j] = Tr[tsw(ri, j)];
+                for (int k0 = 0; k0 < NB; k0 += 4) {
+                    const int k = k0 + rq;
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tsw(col, k)], sh.Ld[k * NB + col], acc, 0, 0, 0);
+                }
 #pragma unroll
-            for (int j = 1; j < NB; j++) {
+                for (int q = 0; q < 4; q++) Tr[tsw(rq + 4 * q, col)] = acc[q];
+                if (lane < NB) {
+                    const int gi = NB * r + lane;
+                    double yi = Y[gi];
 #pragma unroll
-                for (int k = 0; k < j; k++) w[j] = fma(-w[k], sh.Ld[j * NB + k], w[j]);
+                    for (int j = 0; j < NB; j++) yi = fma(-Tr[tsw(lane, j)], Y[kb + j], yi);
+                    Y[gi] = yi;
+                }
             }
-            double yi = Y[i];
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const double lij = w[j] * sh.invdk[j];
-                Tr[tsw(ri, j)] = lij;
-                yi = fma(-lij, Y[kb + j], yi);
-            }
-            Y[i] = yi;
         }
         __syncthreads();
         LPROF(1);
@@ -1557,21 +1614,17 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         Y[i] /= TL[(size_t)slot[ii * nt + ii] * 256 + tsw(i & 15, i & 15)];
     }
     __syncthreads();
-    // backward substitution L^T x = y: block solve by wave 0, then each thread i < kb updates its own y_i
+    // backward substitution L^T x = y: the block by wave 0 as x_b = L11^-T y_b (the diagonal tile's upper triangle,
+    // written by tiles_diag), then each thread i < kb updates its own y_i
     for (int kc = nt - 1; kc >= 0; kc--) {
         const int kb = NB * kc;
-        if (wid == 0) {
+        if (wid == 0 && lane < NB) {
             const double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
-            double col[NB];   // lane c holds L(kb + j, kb + c) for j > c
+            double v = Y[kb + lane];
 #pragma unroll
-            for (int j = 0; j < NB; j++) col[j] = lane < NB ? Td[tsw(j, lane & 15)] : 0.0;
-            double v = lane < NB ? Y[kb + lane] : 0.0;
-#pragma unroll
-            for (int j = NB - 1; j >= 0; j--) {
-                const double xj = bcast16_d(v, j);
-                if (lane < j) v = fma(-col[j], xj, v);
-            }
-            if (lane < NB) Y[kb + lane] = v;
+            for (int j = 1; j < NB; j++)
+                if (j > lane) v = fma(Td[tsw(lane, j)], Y[kb + j], v);
+            Y[kb + lane] = v;
         }
         __syncthreads();
         for (int i = t; i < kb; i += LDLT_THREADS) {

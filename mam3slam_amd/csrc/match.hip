@@ -1243,7 +1243,7 @@ __global__ void k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* ou
 struct FuseArgs {
     mam_frame_geom g;
     mam_frames_dev fr;
-    const mam_fuse_kf* kfs;
+    const mam_fuse_kf* kfs;      // per item (NULL: from kf_tcw of the item's keyframe)
     mam_camera cam;
     const mam_fuse_mp* mps;
     int mp_stride;
@@ -1254,7 +1254,29 @@ struct FuseArgs {
     int32_t* out_idx;
     int32_t* out_dist;
     int32_t* out_n;
+    // item indirection (mam_fuse_items_batch_device; NULL = item b is keyframe b with MapPoint list b)
+    const int32_t* frame_of;     // keyframe of the frame set item b fuses into
+    const int32_t* mp_of;        // MapPoint list item b fuses
+    const mam_pose* kf_tcw;      // per keyframe of the set: GetPose()
+    float log_scale_factor;      // mfLogScaleFactor
+    const int32_t* grid_status;  // per keyframe of the set: k_grid's status (< 0: too many keypoints)
 };
+
+// KeyFrame::GetCameraCenter of a Tcw as Sophus computes Twc = Tcw^-1 in float: the conjugate quaternion applied to -t
+// (match.py camera_center, the same operations in the same order)
+__device__ __forceinline__ mam_fuse_kf fuse_kf_of(const mam_pose& T, float log_sf) {
+    mam_fuse_kf k;
+    k.tcw = T;
+    const float px = -T.t[0], py = -T.t[1], pz = -T.t[2];
+    const float qx = -T.q[0], qy = -T.q[1], qz = -T.q[2], w = T.q[3];
+    float u0 = qy * pz - qz * py, u1 = qz * px - qx * pz, u2 = qx * py - qy * px;
+    u0 = u0 + u0; u1 = u1 + u1; u2 = u2 + u2;
+    k.ow[0] = (px + w * u0) + (qy * u2 - qz * u1);
+    k.ow[1] = (py + w * u1) + (qz * u0 - qx * u2);
+    k.ow[2] = (pz + w * u2) + (qx * u1 - qy * u0);
+    k.log_scale_factor = log_sf;
+    return k;
+}
 
 // (int) of a float as x86's cvttss2si computes it (NaN / out of range -> INT_MIN): PredictScale's (int)ceil(...)
 __device__ __forceinline__ int cvt_i32_x86(float v) {
@@ -1264,7 +1286,7 @@ __device__ __forceinline__ int cvt_i32_x86(float v) {
 // The window of MapPoint mp in keyframe f; false where the reference `continue`s (ORBmatcher.cc:1179-1251).
 __device__ bool fuse_window(const FuseArgs& p, int f, const mam_fuse_mp& mp, Window* w) {
     if (!mp.valid) return false;
-    const mam_fuse_kf& K = p.kfs[f];
+    const mam_fuse_kf K = p.kfs ? p.kfs[f] : fuse_kf_of(p.kf_tcw[p.frame_of[f]], p.log_scale_factor);
     // Tcw * p3Dw: Sophus SE3f action, evaluated as written (as in unit_window)
     const float qx = K.tcw.q[0], qy = K.tcw.q[1], qz = K.tcw.q[2], qw = K.tcw.q[3];
     const float px = mp.pos[0], py = mp.pos[1], pz = mp.pos[2];
@@ -1382,9 +1404,13 @@ __global__ __launch_bounds__(256) void k_fuse(FuseArgs p, int nframes) {
     const long long gu = ((long long)blockIdx.x * 256 + threadIdx.x) / GW;   // global MapPoint slot
     const int f = (int)(gu / p.mp_stride);
     const int j = (int)(gu - (long long)f * p.mp_stride);
-    if (f >= nframes || j >= p.n_mps[f]) return;   // group-uniform
+    if (f >= nframes) return;
+    const int m = p.mp_of ? p.mp_of[f] : f;
+    if (j >= p.n_mps[m]) return;   // group-uniform
+    const int fk = p.frame_of ? p.frame_of[f] : f;   // the keyframe (its cell grid)
+    if (p.grid_status && p.grid_status[fk] < 0) return;
     const size_t o = (size_t)f * p.mp_stride + j;
-    const mam_fuse_mp& mp = p.mps[o];
+    const mam_fuse_mp& mp = p.mps[(size_t)m * p.mp_stride + j];
     Window w;
     int bd = 256, bi = -1;
 #if defined(MAM_FUSE_EXPERIMENT) && (MAM_FUSE_EXPERIMENT & 1)
@@ -1393,7 +1419,7 @@ __global__ __launch_bounds__(256) void k_fuse(FuseArgs p, int nframes) {
     if (fuse_window(p, f, mp, &w)) {
 #endif
         const uint4 u0 = reinterpret_cast<const uint4*>(mp.desc)[0], u1 = reinterpret_cast<const uint4*>(mp.desc)[1];
-        fuse_pass<GW>(p, f, w, u0, u1, &bd, &bi);
+        fuse_pass<GW>(p, fk, w, u0, u1, &bd, &bi);
     }
     if ((lane_id() & (GW - 1)) == 0) {
         p.out_idx[o] = bd <= MAM_TH_LOW ? bi : -1;
@@ -1404,14 +1430,19 @@ __global__ __launch_bounds__(256) void k_fuse(FuseArgs p, int nframes) {
 // nFused per keyframe (a per-MapPoint atomicAdd on one counter per keyframe serialises in L2: ~7 ns per MapPoint)
 __global__ __launch_bounds__(256) void k_fuse_count(FuseArgs p) {
     __shared__ int red[4];
-    const int f = blockIdx.x, n = p.n_mps[f];
+    const int f = blockIdx.x, n = p.n_mps[p.mp_of ? p.mp_of[f] : f];
     const int32_t* idx = p.out_idx + (size_t)f * p.mp_stride;
+    const int st = p.grid_status ? p.grid_status[p.frame_of[f]] : 0;
     int c = 0;
-    for (int j = threadIdx.x; j < n; j += 256) c += idx[j] >= 0;
+    if (st >= 0)
+        for (int j = threadIdx.x; j < n; j += 256) c += idx[j] >= 0;
     c = wave_sum(c);
     if (lane_id() == 0) red[threadIdx.x >> 6] = c;
     __syncthreads();
-    if (threadIdx.x == 0 && p.out_n[f] >= 0) p.out_n[f] = red[0] + red[1] + red[2] + red[3];
+    if (threadIdx.x == 0) {
+        if (p.grid_status) p.out_n[f] = st < 0 ? st : red[0] + red[1] + red[2] + red[3];
+        else if (p.out_n[f] >= 0) p.out_n[f] = red[0] + red[1] + red[2] + red[3];
+    }
 }
 
 // ------------------------------------------------------------------------------------------------ distinctive descriptor
@@ -1578,7 +1609,7 @@ struct mam_match_ctx {
     size_t resolve_lds_max = 64 * 1024;
     // scratch
     DevBuf<mam::GridEnt> grid_ent;
-    DevBuf<int32_t> grid_start, cand_cnt, cand_off, pool_total, out_n_tmp;
+    DevBuf<int32_t> grid_start, cand_cnt, cand_off, pool_total, out_n_tmp, grid_status;
     DevBuf<uint32_t> pool, events;
     // frames the grid scratch holds (mam_frames_dev.reuse_grid is accepted only for the same frames)
     const void* grid_keys = nullptr;
@@ -1705,18 +1736,22 @@ bool geom_ok(const mam_frame_geom* g) { return g && g->nlevels >= 1 && g->nlevel
 int launch_fuse(mam_match_ctx* c, mam::FuseArgs& a, int F, hipStream_t s) {
     if (F <= 0) return MAM_OK;
     if (a.fr.kp_stride > mam::GRID_SORT_MAX || a.fr.kp_stride <= 0 || a.mp_stride <= 0) return MAM_ERR_ARG;
-    if (int rc = c->grid_ent.alloc((size_t)F * a.fr.kp_stride)) return rc;
-    if (int rc = c->grid_start.alloc((size_t)F * (mam::NCELLS + 1))) return rc;
-    if (int rc = c->pool_total.alloc(F)) return rc;
+    const int G = a.frame_of ? a.fr.nframes : F;   // keyframes with a cell grid
+    if (G <= 0) return MAM_ERR_ARG;
+    if (int rc = c->grid_ent.alloc((size_t)G * a.fr.kp_stride)) return rc;
+    if (int rc = c->grid_start.alloc((size_t)G * (mam::NCELLS + 1))) return rc;
+    if (int rc = c->pool_total.alloc(G)) return rc;
+    if (a.frame_of && (c->grid_status.alloc(G) != MAM_OK)) return MAM_ERR_DEVICE;
     mam::ProjArgs ga{};
     ga.g = a.g;
     ga.fr = a.fr;
     ga.grid_ent = c->grid_ent.p;
     ga.grid_start = c->grid_start.p;
     ga.pool_total = c->pool_total.p;
-    ga.out_n = a.out_n;
-    if (a.fr.reuse_grid) MAM_HIP(hipMemsetAsync(a.out_n, 0, sizeof(int32_t) * (size_t)F, s));
-    if (int rc = build_grid(c, ga, F, s)) return rc;
+    ga.out_n = a.frame_of ? c->grid_status.p : a.out_n;
+    a.grid_status = a.frame_of ? c->grid_status.p : nullptr;
+    if (a.fr.reuse_grid) MAM_HIP(hipMemsetAsync(ga.out_n, 0, sizeof(int32_t) * (size_t)G, s));
+    if (int rc = build_grid(c, ga, G, s)) return rc;
     a.grid_ent = c->grid_ent.p;
     a.grid_start = c->grid_start.p;
     {
@@ -2148,6 +2183,35 @@ int mam_fuse_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_f
     a.out_dist = out_dist;
     a.out_n = out_n;
     return launch_fuse(c, a, fr->nframes, stream ? (hipStream_t)stream : c->stream);
+}
+
+int mam_fuse_items_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_frames_dev* fr,
+                                const mam_pose* kf_tcw, float log_scale_factor, const mam_camera* cam, int n_items,
+                                const int32_t* frame_of, const int32_t* mp_of, const mam_fuse_mp* mps, int mp_stride,
+                                const int32_t* n_mps, float th, int32_t* out_idx, int32_t* out_dist,
+                                int32_t* out_nfused, void* stream) {
+    if (!c || !geom_ok(g) || !fr || !kf_tcw || !cam || n_items < 0 || !frame_of || !mp_of || !mps || !n_mps ||
+        !out_idx || !out_dist || !out_nfused || mp_stride <= 0 || fr->nframes <= 0)
+        return MAM_ERR_ARG;
+    if (n_items == 0) return MAM_OK;
+    MAM_DEVICE_SCOPE(c->device);
+    mam::FuseArgs a{};
+    a.g = *g;
+    a.fr = *fr;
+    a.kfs = nullptr;
+    a.cam = *cam;
+    a.mps = mps;
+    a.mp_stride = mp_stride;
+    a.n_mps = n_mps;
+    a.th = th;
+    a.out_idx = out_idx;
+    a.out_dist = out_dist;
+    a.out_n = out_nfused;
+    a.frame_of = frame_of;
+    a.mp_of = mp_of;
+    a.kf_tcw = kf_tcw;
+    a.log_scale_factor = log_scale_factor;
+    return launch_fuse(c, a, n_items, stream ? (hipStream_t)stream : c->stream);
 }
 
 int mam_fuse(mam_match_ctx* c, const mam_frame_geom* g, int n, const mam_keypoint* keys, const uint8_t* desc,

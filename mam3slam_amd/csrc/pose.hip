@@ -457,6 +457,106 @@ __global__ __launch_bounds__(PT) void k_pose_opt(Args a) {
     }
 }
 
+// ---- the frame side of the call (device-resident tracked frames)
+// Optimizer::PoseOptimization's edge list (Optimizer.cc:856-895): one mono edge per keypoint i whose slot holds a
+// MapPoint (mvpMapPoints[i] != NULL), in increasing i, observation mvKeysUn[i].pt (= mvKeys: k1 = 0), information
+// mvInvLevelSigma2[octave], the MapPoint's world position. A slot's MapPoint is the local-map search's match when it
+// made one (SearchByProjection(F, vpMapPoints) overwrites a slot whose MapPoint has no observations), else the motion
+// search's (an index into the last frame's entries). edge_kp[e] = i.
+struct FrameEdgeArgs {
+    const mam_keypoint* kps;
+    int kp_stride;
+    const int32_t* kp_count;
+    int count_stride;
+    float inv_sigma2[MAM_MAX_LEVELS];
+    int nlevels;
+    const int32_t* match_last;
+    const mam_last_entry* last;
+    int last_stride;
+    const int32_t* match_local;
+    const mam_local_mp* local;
+    int local_stride;
+    mam_pose_edge* edges;
+    int edge_stride;
+    int32_t* n_edges;
+    int32_t* edge_kp;
+};
+
+// grid (nframes) x 256: the slots in keypoint order, compacted by a block prefix count
+__global__ __launch_bounds__(256) void k_frame_edges(FrameEdgeArgs a) {
+    __shared__ int wsum[4];
+    __shared__ int base_s;
+    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int n = min(max(a.kp_count[(size_t)f * a.count_stride], 0), a.kp_stride);
+    const mam_keypoint* K = a.kps + (size_t)f * a.kp_stride;
+    const int32_t* ml = a.match_last + (size_t)f * a.kp_stride;
+    const int32_t* mo = a.match_local ? a.match_local + (size_t)f * a.kp_stride : nullptr;
+    mam_pose_edge* E = a.edges + (size_t)f * a.edge_stride;
+    int32_t* EK = a.edge_kp + (size_t)f * a.edge_stride;
+    if (t == 0) base_s = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < n; c0 += 256) {
+        const int i = c0 + t;
+        int jl = -1, jm = -1;
+        if (i < n) {
+            jm = mo ? mo[i] : -1;
+            jl = ml[i];
+        }
+        const bool has = jm >= 0 || jl >= 0;
+        const uint64_t m = __ballot(has);
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = base_s;
+        for (int k = 0; k < w; k++) off += wsum[k];
+        const int r = off + __popcll(m & ((1ull << lane) - 1ull));
+        if (has && r < a.edge_stride) {
+            const mam_keypoint kp = K[i];
+            mam_pose_edge e;
+            e.obs[0] = kp.x;
+            e.obs[1] = kp.y;
+            const float* X = jm >= 0 ? a.local[(size_t)f * a.local_stride + jm].pos
+                                     : a.last[(size_t)f * a.last_stride + jl].pos;
+            e.xw[0] = X[0];
+            e.xw[1] = X[1];
+            e.xw[2] = X[2];
+            e.inv_sigma2 = a.inv_sigma2[min(max(kp.octave, 0), a.nlevels - 1)];
+            E[r] = e;
+            EK[r] = i;
+        }
+        __syncthreads();
+        if (t == 0) base_s += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+    if (t == 0) a.n_edges[f] = base_s <= a.edge_stride ? base_s : MAM_ERR_CAPACITY;
+}
+
+// grid (ceil(nframes * edge_stride / 256)): Tracking's use of the result — Frame::SetPose(SE3f(q.cast<float>(),
+// t.cast<float>())) (Sophus normalises the float quaternion; Optimizer.cc:1108-1111) and, with discard, the outliers'
+// slots emptied (Tracking.cc:2840-2857: mvpMapPoints[i] = NULL — no match, not taken by the local-map search)
+__global__ __launch_bounds__(256) void k_frame_update(int nframes, const mam_pose_result* __restrict__ res,
+                                                      mam_pose* __restrict__ tcw, const uint8_t* __restrict__ outlier,
+                                                      const int32_t* __restrict__ edge_kp, int edge_stride,
+                                                      const int32_t* __restrict__ n_edges, int discard,
+                                                      int32_t* __restrict__ match_last, uint8_t* __restrict__ taken,
+                                                      int kp_stride) {
+    const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const int f = (int)(g / (size_t)max(edge_stride, 1)), e = (int)(g % (size_t)max(edge_stride, 1));
+    if (f >= nframes) return;
+    const mam_pose_result& R = res[f];
+    if (e == 0 && R.n_inliers >= 0 && R.rounds > 0) {
+        float q[4];
+        for (int k = 0; k < 4; k++) q[k] = (float)R.q[k];
+        // Sophus SO3::normalize: coeffs / norm(), Eigen's SSE 4-float reduction (x^2 + z^2) + (y^2 + w^2)
+        const float nq = sqrtf((q[0] * q[0] + q[2] * q[2]) + (q[1] * q[1] + q[3] * q[3]));
+        for (int k = 0; k < 4; k++) tcw[f].q[k] = q[k] / nq;
+        for (int k = 0; k < 3; k++) tcw[f].t[k] = (float)R.t[k];
+    }
+    if (!discard || e >= n_edges[f] || !outlier[(size_t)f * edge_stride + e]) return;
+    const int i = edge_kp[(size_t)f * edge_stride + e];
+    match_last[(size_t)f * kp_stride + i] = -1;
+    if (taken) taken[(size_t)f * kp_stride + i] = 0;
+}
+
 }  // namespace pose
 }  // namespace mam
 
@@ -566,6 +666,59 @@ int mam_pose_optimization(mam_pose_ctx* c, const mam_pose* tcw, const mam_camera
     MAM_HIP(hipMemcpyAsync(result, dres, sizeof(mam_pose_result), hipMemcpyDeviceToHost, c->stream));
     MAM_HIP(hipStreamSynchronize(c->stream));
     return result->n_inliers;
+}
+
+int mam_pose_frame_edges_batch_device(mam_pose_ctx* c, int nframes, const mam_keypoint* kps, int kp_stride,
+                                      const int32_t* kp_count, int count_stride, const float* inv_level_sigma2,
+                                      int nlevels, const int32_t* match_last, const mam_last_entry* last,
+                                      int last_stride, const int32_t* match_local, const mam_local_mp* local_mps,
+                                      int local_stride, mam_pose_edge* edges, int edge_stride, int32_t* n_edges,
+                                      int32_t* edge_kp, void* stream) {
+    if (!c || nframes < 0 || kp_stride < 0 || count_stride < 1 || nlevels < 1 || nlevels > MAM_MAX_LEVELS ||
+        !inv_level_sigma2 || edge_stride < 0)
+        return MAM_ERR_ARG;
+    if (nframes == 0) return MAM_OK;
+    if (!kps || !kp_count || !match_last || !last || !edges || !n_edges || !edge_kp ||
+        (match_local && !local_mps))
+        return MAM_ERR_ARG;
+    MAM_DEVICE_SCOPE(c->device);
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    mam::pose::FrameEdgeArgs a{};
+    a.kps = kps;
+    a.kp_stride = kp_stride;
+    a.kp_count = kp_count;
+    a.count_stride = count_stride;
+    for (int l = 0; l < nlevels; l++) a.inv_sigma2[l] = inv_level_sigma2[l];
+    a.nlevels = nlevels;
+    a.match_last = match_last;
+    a.last = last;
+    a.last_stride = last_stride;
+    a.match_local = match_local;
+    a.local = local_mps;
+    a.local_stride = local_stride;
+    a.edges = edges;
+    a.edge_stride = edge_stride;
+    a.n_edges = n_edges;
+    a.edge_kp = edge_kp;
+    hipLaunchKernelGGL(mam::pose::k_frame_edges, dim3(nframes), dim3(256), 0, s, a);
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
+
+int mam_pose_frame_update_batch_device(mam_pose_ctx* c, int nframes, const mam_pose_result* results, mam_pose* tcw,
+                                       const uint8_t* outlier, const int32_t* edge_kp, int edge_stride,
+                                       const int32_t* n_edges, int discard, int32_t* match_last, uint8_t* taken,
+                                       int kp_stride, void* stream) {
+    if (!c || nframes < 0 || edge_stride < 0 || kp_stride < 0) return MAM_ERR_ARG;
+    if (nframes == 0) return MAM_OK;
+    if (!results || !tcw || !n_edges || (discard && (!outlier || !edge_kp || !match_last))) return MAM_ERR_ARG;
+    MAM_DEVICE_SCOPE(c->device);
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    const size_t total = (size_t)nframes * (size_t)std::max(edge_stride, 1);
+    hipLaunchKernelGGL(mam::pose::k_frame_update, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, nframes,
+                       results, tcw, outlier, edge_kp, edge_stride, n_edges, discard, match_last, taken, kp_stride);
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
 }
 
 int mam_pose_set_profiling(mam_pose_ctx* c, int enable) {

@@ -185,9 +185,12 @@ class NewMapPointsLeg:
     The keyframes live in a ring of R slots in HBM (keypoints, descriptors, MapPoint flags, pose, BoW node + weight at
     levelsup 4): `ingest` copies the step's new keyframes out of the tracking buffers (on the tracking stream, after
     the step that tracked them: the reference's Tracking -> LocalMapping hand-off); `run` computes their BoW (DBoW2
-    transform, synthetic k=10 L=6 vocabulary — ORBvoc.txt is a missing blob) and searches each against the 30 slots
-    inserted before it (the synthetic map has no covisibility graph: the most recent keyframes stand in for the best
-    covisible ones). The triangulation and MapPoint creation that follow the search (LocalMapping.cc:590-828) are
+    transform, synthetic k=10 L=6 vocabulary — ORBvoc.txt is a missing blob) and searches each against its 30
+    neighbours (the synthetic map has no covisibility graph: the keyframes nearest in the agent's frame sequence stand
+    in for the best covisible ones; the keyframes' poses are those of the camera that rendered them,
+    synth.frame_pose, refined by Tracking's PoseOptimization); then SearchInNeighbors (LocalMapping.cc:830-939):
+    Fuse of the keyframe's MapPoints into its 30 neighbours, Fuse of the neighbours' fuse candidates into the keyframe
+    and ComputeDistinctiveDescriptors of its MapPoints (`search_in_neighbors`). The triangulation and MapPoint creation that follow the search (LocalMapping.cc:590-828) are
     outside the hot path; the map's new MapPoints enter through LocalMappingLeg.new_keyframes."""
 
     NN = 30
@@ -220,18 +223,26 @@ class NewMapPointsLeg:
         # completion of the search run at each head (None until one was issued there)
         self.done = {h: None for h in range(0, self.R, self.W)}
         self.stream = torch.cuda.Stream(device, priority=-1)
-        # pairs for each head position: new slot j = head + i searches the NN slots inserted before it
+        # pairs for each head position. With at least NN + 1 keyframes per ingest (c2: 32), new keyframe i (frame
+        # i K + s of the agent's sequence) searches the NN keyframes of the same ingest nearest to it in the sequence
+        # (frames i' K + s, |i - i'| smallest, earlier first on a tie): the covisible keyframes
+        # GetBestCovisibilityKeyFrames(30) returns for a camera moving through one scene. With fewer, slot j = head + i
+        # searches the NN slots inserted before it.
         self.pairs = {}
         for head in range(0, R, self.W):
             p = []
             for i in range(self.W):
                 j = (head + i) % R
-                for k in range(1, self.NN + 1):
-                    p.append((j, (j - k) % R))
+                if self.W > self.NN:
+                    near = sorted((x for x in range(self.W) if x != i), key=lambda x: (abs(x - i), x))[:self.NN]
+                    p += [(j, (head + x) % R) for x in near]
+                else:
+                    p += [(j, (j - k) % R) for k in range(1, self.NN + 1)]
             self.pairs[head] = torch.tensor(np.array(p, np.int32), device=device)
         self.npairs = self.W * self.NN
         self.out = torch.zeros((self.npairs, S), dtype=torch.int32, device=device)
         self.nmatch = torch.zeros(self.npairs, dtype=torch.int32, device=device)
+        self._init_search_in_neighbors(seed)
         self._FramesDev, self._TriBatch = FramesDev, TriBatch
         # initial ring: the first R frames, BoW on the device, no MapPoints yet
         with torch.cuda.stream(tr.tstream):
@@ -240,6 +251,7 @@ class NewMapPointsLeg:
             self.desc.copy_(tr.d_desc[fr])
             self.cnt.copy_(tr.d_cnt[fr])
             self.tcw.copy_(tr.d_tcw.view(tr.B, -1)[fr])
+            self.fmp.copy_(self.fmp_frames[fr])
             self.voc.transform_batch_device(R, self.desc.data_ptr(), S, self.cnt.data_ptr(), 4, self.word.data_ptr(),
                                             self.weight.data_ptr(), self.nid.data_ptr(), stream=tr.tstream.cuda_stream)
             for ev in self.ready.values():
@@ -265,6 +277,7 @@ class NewMapPointsLeg:
             self.desc[sl] = tr.d_desc[fr]
             self.cnt[sl] = tr.d_cnt[fr]
             self.tcw[sl] = tr.d_tcw.view(tr.B, -1)[fr]
+            self.fmp[sl] = self.fmp_frames[fr]
             # GetMapPoint(i) != NULL: the keypoints Tracking matched (motion model or local map)
             self.has_mp[sl] = ((tr.d_out1[fr] >= 0) | (tr.d_out2[fr] >= 0)).to(torch.uint8)
             self.ready[head].record(tr.tstream)
@@ -312,6 +325,123 @@ class NewMapPointsLeg:
         b.npairs, b.pairs = int(pairs.shape[0]), pairs.data_ptr()
         self.matcher.search_for_triangulation_batch_device(self.tr.F0, self.tr.cam, b, self.out.data_ptr(),
                                                            self.nmatch.data_ptr(), False, stream=s)
+        self.search_in_neighbors(stream, h)
+
+    # ------------------------------------------------------------------------------------------ SearchInNeighbors
+    NB_BACK = 4   # neighbours whose MapPoints form a keyframe's fuse candidates
+
+    def _init_search_in_neighbors(self, seed):
+        """MapPoints of every tracked frame (the ring copies them with the keyframe) and the update's observation
+        descriptors. A keyframe's MapPoints: its keypoints on the scene plane (synth.PLANE_DEPTH, world coordinates
+        under the pose of the camera that rendered the frame), as MapPoint::UpdateNormalAndDepth leaves them
+        (MapPoint.cc:426-494: normal = viewing direction, mfMaxDistance = distance x scale factor of the keypoint's
+        level, mfMinDistance = mfMaxDistance / scale factor of the last level), descriptor = the keypoint's."""
+        import torch
+
+        from . import synth
+        from .match import FUSE_MP_DTYPE, quat_to_rot
+
+        tr, S = self.tr, self.S
+        sf = tr.F0.scale_factors.astype(np.float64)
+        fmp = np.zeros((tr.B, S), FUSE_MP_DTYPE)
+        desc_h = tr.d_desc.cpu().numpy()
+        for f in range(tr.B):
+            n = int(tr.cnt_h[f, 0])
+            k = tr.kps_h[f, :n]
+            q, t = tr.poses[f]
+            R = quat_to_rot(q).astype(np.float64)
+            Ow = -R.T @ t.astype(np.float64)
+            ray_c = np.concatenate([tr.cam.unproject_np(k["x"], k["y"]), np.ones((n, 1))], 1)
+            ray_w = ray_c @ R   # R^T d
+            sc = (synth.PLANE_DEPTH - Ow[2]) / ray_w[:, 2]
+            X = Ow[None, :] + sc[:, None] * ray_w
+            d = X - Ow[None, :]
+            dist = np.linalg.norm(d, axis=1)
+            m = fmp[f, :n]
+            m["pos"] = X.astype(np.float32)
+            m["normal"] = (d / dist[:, None]).astype(np.float32)
+            m["max_distance"] = (dist * sf[k["octave"]]).astype(np.float32)
+            m["min_distance"] = (m["max_distance"] / np.float32(sf[-1])).astype(np.float32)
+            m["valid"] = 1
+            m["desc"] = desc_h[f, :n]
+        self.fmp_frames = torch.from_numpy(fmp.view(np.uint8).reshape(tr.B, -1)).to(self.dev)
+        self.fmp = torch.zeros((self.R, S * FUSE_MP_DTYPE.itemsize), dtype=torch.uint8, device=self.dev)
+        self.cnt_col = torch.zeros(self.R, dtype=torch.int32, device=self.dev)
+        W, NN, NBK = self.W, self.NN, self.NB_BACK
+        # items per ring head: forward (slot's MapPoints -> each of its NN neighbours), backward (the NB_BACK nearest
+        # neighbours' MapPoints -> the slot)
+        self.sin_items = {}
+        for head, pr in self.pairs.items():
+            pr = pr.cpu().numpy()
+            fwd_frame, fwd_mp = pr[:, 1], pr[:, 0]
+            bwd_frame = np.repeat(pr[::NN, 0], NBK)
+            bwd_mp = pr.reshape(W, NN)[:, :NBK, 1].reshape(-1)
+            self.sin_items[head] = tuple(torch.tensor(np.ascontiguousarray(a, np.int32), device=self.dev)
+                                         for a in (fwd_frame, fwd_mp, bwd_frame, bwd_mp))
+        nf, nb = W * NN, W * NBK
+        self.fwd_idx = torch.zeros((nf, S), dtype=torch.int32, device=self.dev)
+        self.fwd_dist = torch.zeros((nf, S), dtype=torch.int32, device=self.dev)
+        self.fwd_n = torch.zeros(nf, dtype=torch.int32, device=self.dev)
+        self.bwd_idx = torch.zeros((nb, S), dtype=torch.int32, device=self.dev)
+        self.bwd_dist = torch.zeros((nb, S), dtype=torch.int32, device=self.dev)
+        self.bwd_n = torch.zeros(nb, dtype=torch.int32, device=self.dev)
+        # update: the W keyframes' MapPoints, 2..12 observations each, the observing keypoints' descriptors (the
+        # keyframe's with up to 20 flipped bits: views of the point from other keyframes)
+        from .scene import flip_bits
+
+        rng = np.random.default_rng(seed + 11)
+        n_upd = int(sum(int(tr.cnt_h[f % tr.B, 0]) for f in range(W)))
+        sizes = rng.integers(2, 13, n_upd)
+        off = np.zeros(n_upd + 1, np.int32)
+        off[1:] = np.cumsum(sizes)
+        base = np.concatenate([desc_h[f % tr.B, :int(tr.cnt_h[f % tr.B, 0])] for f in range(W)])
+        descs = flip_bits(np.repeat(base, sizes, 0), rng, 20)
+        self.upd_n = n_upd
+        self.upd_off = torch.from_numpy(off).to(self.dev)
+        self.upd_desc = torch.from_numpy(descs).to(self.dev)
+        self.upd_best = torch.zeros(n_upd, dtype=torch.int32, device=self.dev)
+
+    def search_in_neighbors(self, stream, head):
+        """SearchInNeighbors of the keyframes at `head` (after their CreateNewMapPoints searches, on `stream`):
+        forward Fuse of each keyframe's MapPoints into its NN neighbours, backward Fuse of its NB_BACK nearest
+        neighbours' MapPoints (the fuse candidates) into it, ComputeDistinctiveDescriptors of the keyframes' MapPoints
+        (UpdateNormalAndDepth and the map updates Fuse implies are host-side bookkeeping, not searched)."""
+        fwd_frame, fwd_mp, bwd_frame, bwd_mp = self.sin_items[head]
+        s = stream.cuda_stream
+        fr = self._FramesDev(self.R, self.S, self.keys.data_ptr(), self.desc.data_ptr(), self.cnt.data_ptr(), None,
+                             None, 0)
+        tcw = self.tcw.data_ptr()
+        import torch
+
+        with torch.cuda.stream(stream):
+            self.cnt_col.copy_(self.cnt[:, 0])   # MapPoints of list m (ring slot m): the slot's keypoints
+        m = self.matcher
+        m.fuse_items_batch_device(self.tr.F0, fr, tcw, self.tr.cam, len(fwd_frame), fwd_frame.data_ptr(),
+                                  fwd_mp.data_ptr(), self.fmp.data_ptr(), self.S, self.cnt_col.data_ptr(), 3.0,
+                                  self.fwd_idx.data_ptr(), self.fwd_dist.data_ptr(), self.fwd_n.data_ptr(), stream=s)
+        m.fuse_items_batch_device(self.tr.F0, fr, tcw, self.tr.cam, len(bwd_frame), bwd_frame.data_ptr(),
+                                  bwd_mp.data_ptr(), self.fmp.data_ptr(), self.S, self.cnt_col.data_ptr(), 3.0,
+                                  self.bwd_idx.data_ptr(), self.bwd_dist.data_ptr(), self.bwd_n.data_ptr(), stream=s)
+        m.distinctive_batch_device(self.upd_n, self.upd_off.data_ptr(), self.upd_desc.data_ptr(),
+                                   self.upd_best.data_ptr(), stream=s)
+
+    def fuse_inputs(self, backward: bool, b: int):
+        """Host (KeyFrame FrameData with pose, MapPoints) of forward / backward Fuse item b of the last run."""
+        from .match import FUSE_MP_DTYPE, FrameData
+        from .orb import KP_DTYPE
+
+        fwd_frame, fwd_mp, bwd_frame, bwd_mp = self.sin_items[self.head]
+        slot = int((bwd_frame if backward else fwd_frame)[b].item())
+        ms = int((bwd_mp if backward else fwd_mp)[b].item())
+        n = int(self.cnt[slot, 0].item())
+        keys = self.keys[slot].cpu().numpy().view(KP_DTYPE)[:n]
+        KF = FrameData(keys=keys, desc=self.desc[slot, :n].cpu().numpy(), width=self.tr.W, height=self.tr.H,
+                       scale_factors=self.tr.F0.scale_factors, level_sigma2=self.tr.F0.level_sigma2)
+        t = self.tcw[slot].cpu().numpy().view(np.float32)
+        KF.pose = (t[:4].copy(), t[4:7].copy())
+        nm = int(self.cnt[ms, 0].item())
+        mps = self.fmp[ms].cpu().numpy().view(FUSE_MP_DTYPE)[:nm]
+        return KF, mps
 
     def algorithmic_bytes(self):
         """SURVEY §8(d) bytes of the last run's searches: per pair, sum over the BoW nodes both FeatureVectors hold of

@@ -220,6 +220,9 @@ _SIGS = {
                            C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]),
     "mam_fuse_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                         C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mam_fuse_items_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p,
+                                              C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                              C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mam_compute_distinctive_descriptors": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mam_compute_distinctive_descriptors_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                                                    C.c_void_p, C.c_void_p]),
@@ -551,6 +554,17 @@ class ORBmatcher:
             self._ctx, C.byref(g), C.byref(frames), C.c_void_p(d_kfs), C.byref(cam), C.c_void_p(d_mps), mp_stride,
             C.c_void_p(d_nmps), float(th), C.c_void_p(d_idx), C.c_void_p(d_dist), C.c_void_p(d_nfused),
             C.c_void_p(stream)), "fuse_batch_device")
+
+    def fuse_items_batch_device(self, F: FrameData, frames: FramesDev, d_kf_tcw: int, cam: Camera, n_items: int,
+                                d_frame_of: int, d_mp_of: int, d_mps: int, mp_stride: int, d_nmps: int, th: float,
+                                d_idx: int, d_dist: int, d_nfused: int, stream: int = 0, scale_factor: float = 1.2):
+        """Fuse of n_items (keyframe of `frames`, MapPoint list) pairs (mam_fuse_items_batch_device)."""
+        g = F.geom()
+        return check(self._L.mam_fuse_items_batch_device(
+            self._ctx, C.byref(g), C.byref(frames), C.c_void_p(d_kf_tcw), float(np.log(np.float32(scale_factor))),
+            C.byref(cam), int(n_items), C.c_void_p(d_frame_of), C.c_void_p(d_mp_of), C.c_void_p(d_mps), mp_stride,
+            C.c_void_p(d_nmps), float(th), C.c_void_p(d_idx), C.c_void_p(d_dist), C.c_void_p(d_nfused),
+            C.c_void_p(stream)), "fuse_items_batch_device")
 
     def distinctive_batch_device(self, n_mps: int, d_off: int, d_descs: int, d_out: int, stream: int = 0):
         return check(self._L.mam_compute_distinctive_descriptors_batch_device(

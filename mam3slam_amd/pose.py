@@ -36,6 +36,13 @@ _SIGS = {
                                         C.c_void_p]),
     "mam_pose_optimization_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                                      C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mam_pose_frame_edges_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                                    C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                                    C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                                    C.c_void_p]),
+    "mam_pose_frame_update_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                     C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                                     C.c_int, C.c_void_p]),
     "mam_pose_max_edges": (C.c_int, [C.c_void_p]),
     "mam_pose_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "mam_pose_stage_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -98,6 +105,30 @@ class PoseOptimizer:
             C.c_void_p(d_n_edges), C.c_void_p(d_outlier), C.c_void_p(d_results), C.c_void_p(stream)),
             "mam_pose_optimization_batch_device")
 
+    def frame_edges_batch_device(self, nframes: int, d_kps: int, kp_stride: int, d_count: int, count_stride: int,
+                                 inv_level_sigma2: np.ndarray, d_match_last: int, d_last: int, last_stride: int,
+                                 d_match_local: int | None, d_local: int | None, local_stride: int, d_edges: int,
+                                 edge_stride: int, d_n_edges: int, d_edge_kp: int, stream: int = 0):
+        """Optimizer::PoseOptimization's edge build for device-resident tracked frames (Optimizer.cc:856-895)."""
+        inv = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        return check(self._L.mam_pose_frame_edges_batch_device(
+            self._ctx, nframes, C.c_void_p(d_kps), kp_stride, C.c_void_p(d_count), count_stride,
+            inv.ctypes.data, len(inv), C.c_void_p(d_match_last), C.c_void_p(d_last), last_stride,
+            C.c_void_p(d_match_local) if d_match_local else None, C.c_void_p(d_local) if d_local else None,
+            local_stride, C.c_void_p(d_edges), edge_stride, C.c_void_p(d_n_edges), C.c_void_p(d_edge_kp),
+            C.c_void_p(stream)), "mam_pose_frame_edges_batch_device")
+
+    def frame_update_batch_device(self, nframes: int, d_results: int, d_tcw: int, d_outlier: int, d_edge_kp: int,
+                                  edge_stride: int, d_n_edges: int, discard: bool, d_match_last: int | None,
+                                  d_taken: int | None, kp_stride: int, stream: int = 0):
+        """Frame::SetPose from the result and, with discard, TrackWithMotionModel's outlier discard
+        (Tracking.cc:2836-2857)."""
+        return check(self._L.mam_pose_frame_update_batch_device(
+            self._ctx, nframes, C.c_void_p(d_results), C.c_void_p(d_tcw), C.c_void_p(d_outlier),
+            C.c_void_p(d_edge_kp), edge_stride, C.c_void_p(d_n_edges), 1 if discard else 0,
+            C.c_void_p(d_match_last) if d_match_last else None, C.c_void_p(d_taken) if d_taken else None,
+            kp_stride, C.c_void_p(stream)), "mam_pose_frame_update_batch_device")
+
     def set_profiling(self, enable: bool):
         check(self._L.mam_pose_set_profiling(self._ctx, 1 if enable else 0), "mam_pose_set_profiling")
 
@@ -118,5 +149,14 @@ def pose_optimization(F, mps_xyz: np.ndarray, cam: Pinhole, optimizer: PoseOptim
     outlier = np.zeros(len(F.keys), np.uint8) if getattr(F, "outlier", None) is None else F.outlier
     outlier[idx] = out
     F.outlier = outlier
-    F.pose = (q.astype(np.float32), t.astype(np.float32))
+    F.pose = set_pose_float(q, t)
     return n
+
+
+def set_pose_float(q, t):
+    """Frame::SetPose(Sophus::SE3f(q.cast<float>(), t.cast<float>())) (Optimizer.cc:1108-1111): Sophus normalises
+    the float quaternion, coeffs / norm() with Eigen's SSE 4-float reduction ((x^2 + z^2) + (y^2 + w^2))."""
+    qf = np.asarray(q, np.float64).astype(np.float32)
+    sq = qf * qf
+    n = np.sqrt(np.float32((sq[0] + sq[2]) + (sq[1] + sq[3])))
+    return (qf / n).astype(np.float32), np.asarray(t, np.float64).astype(np.float32)

@@ -166,6 +166,20 @@ def small_pose(rng, rot=0.01, trans=0.05):
     return q.astype(np.float32), t
 
 
+def perturb_pose(pose, rng, rot=0.005, trans=0.02):
+    """(dq, dt) * pose for a random small (dq, dt): a motion model's guess near the true Tcw (float32)."""
+    from .match import quat_to_rot
+
+    dq, dt = small_pose(rng, rot=rot, trans=trans)
+    ax, ay, az, aw = [float(x) for x in dq]
+    bx, by, bz, bw = [float(x) for x in pose[0]]
+    q = np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by + ay * bw + az * bx - ax * bz,
+                  aw * bz + az * bw + ax * by - ay * bx, aw * bw - ax * bx - ay * by - az * bz])
+    q = (q / np.linalg.norm(q)).astype(np.float32)
+    t = (quat_to_rot(dq).astype(np.float64) @ np.asarray(pose[1], np.float64) + dt).astype(np.float32)
+    return q, t
+
+
 def motion_last_frame(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.75, n_out=80, kflip=12):
     """LastFrame entries whose MapPoints re-project near F's keypoints under F.pose (Tcw)."""
     from .match import quat_to_rot

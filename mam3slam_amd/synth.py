@@ -84,5 +84,40 @@ def make_frame(w: int, h: int, agent: int = 0, frame: int = 0, motion: bool = Tr
     return np.ascontiguousarray(np.clip(np.rint(out), 0, 255).astype(np.uint8))
 
 
+# The camera that renders make_frame's images of the canvas, as a 3-D scene: the canvas is the plane z = PLANE_DEPTH in
+# front of a Pinhole camera (fx = fy = f, principal point (w/2, h/2): scene.pinhole) that translates along x and rolls
+# about its optical axis. make_frame maps canvas pixel P to image pixel p = R_k (P - o_k - c) + c with the crop offset
+# o_k = (2k + margin, margin), c = ((w - 1)/2, (h - 1)/2) (scipy's rotation centre) and R_k = [[cos a, sin a],
+# [-sin a, cos a]], a = 0.2 k degrees (scipy.ndimage.rotate turns the content counter-clockwise on screen). With the
+# world point of canvas pixel P at ((P - o_0 - c) Z / f, Z), camera k = (R_k about z, t = (Z / f)(R_k (o_0 - o_k) + c -
+# (w/2, h/2), 0)) projects it onto p exactly.
+PLANE_DEPTH = 5.0
+
+
+def frame_pose(w: int, h: int, frame: int, f: float = 500.0, depth: float = PLANE_DEPTH, motion: bool = True):
+    """Tcw (q xyzw float32, t float32) of the camera that rendered make_frame(w, h, agent, frame) (any agent)."""
+    k = frame if motion else 0
+    a = np.deg2rad(0.2 * k)
+    ca, sa = np.cos(a), np.sin(a)
+    R2 = np.array([[ca, sa], [-sa, ca]])
+    d = np.array([-float(int(2.0 * k)), 0.0])   # o_0 - o_k
+    txy = depth / f * (R2 @ d + np.array([(w - 1) / 2.0 - w / 2.0, (h - 1) / 2.0 - h / 2.0]))
+    # R = [[R2, 0], [0, 1]]: quaternion of a rotation about z by angle -a (R2 is that rotation in x-right, y-down axes)
+    q = np.array([0.0, 0.0, np.sin(-a / 2.0), np.cos(-a / 2.0)])
+    return q.astype(np.float32), np.array([txy[0], txy[1], 0.0], np.float32)
+
+
+def canvas_point(w: int, h: int, frame: int, px: np.ndarray, py: np.ndarray, motion: bool = True):
+    """Canvas pixel coordinates of image pixels (px, py) of make_frame(w, h, agent, frame) (the inverse warp)."""
+    k = frame if motion else 0
+    a = np.deg2rad(0.2 * k)
+    ca, sa = np.cos(a), np.sin(a)
+    cx, cy = (w - 1) / 2.0, (h - 1) / 2.0
+    dx, dy = np.asarray(px, np.float64) - cx, np.asarray(py, np.float64) - cy
+    margin = 64
+    # R^-1 = R^T = [[cos, -sin], [sin, cos]]
+    return ca * dx - sa * dy + cx + int(2.0 * k) + margin, sa * dx + ca * dy + cy + margin
+
+
 def make_batch(w: int, h: int, n: int, agent: int = 0, start: int = 0) -> np.ndarray:
     return np.stack([make_frame(w, h, agent, start + i) for i in range(n)])
