@@ -784,6 +784,8 @@ def main():
 
     def set_profiling(on):
         # LocalMapping's per-stage HIP events (8 event records per LM trial on the LBA stream, 2 per search batch)
+        # and the all-gather's wall time
+        mapping.time_gather = on
         mapping.solver.set_profiling(on)
         newmp.matcher.set_profiling(on)
         newmp.voc.set_profiling(on)
@@ -943,7 +945,16 @@ def main():
                           "achieved_fp64_tflops": (fl * mapping.W) / (solve_ms * 1e-3) / 1e12 if solve_ms else None,
                           "fp64_peak_tflops": FP64_PEAK_TFS,
                           "stage_ms_total": {k: v[0] for k, v in lba_stage.items()},
-                          "exchange_bytes_per_step": int(mapping.exch.send.numel() * world)}
+                          "exchange_bytes_per_step": int(mapping.exch.send.numel() * world),
+                          "exchange": {"bytes_per_rank_block": int(mapping.exch.block_bytes),
+                                       "keyframe_records": mapping.n_kf_upd, "mappoint_records": mapping.n_mp_upd,
+                                       "bytes_per_window": mapping.exch.block_bytes / mapping.W,
+                                       "allgather_ms_median": float(np.median(mapping.exch.gather_ms))
+                                       if mapping.exch.gather_ms else None,
+                                       "note": "one fixed-size all_gather_into_tensor per step of each GPU's "
+                                               "deduplicated write-back (32-B KeyFrame, 16-B MapPoint records); "
+                                               "gather time = host wall around the collective with the stream "
+                                               "synchronised, from the untimed profiling pass"}}
         if newmp is not None:
             nmv = newmp.nmatch.cpu().numpy()
             tri_b = newmp.algorithmic_bytes()

@@ -86,6 +86,38 @@ int mam_exchange_pack_windows(int n_windows, const mam_map_window* windows, int6
 int mam_exchange_apply(const mam_map_update* gathered, int n_agents, int capacity, float* kf_table, int64_t kf_cap,
                        float* mp_table, int64_t mp_cap, int32_t* status, void* stream);
 
+/* ---- Compact blocks: one per agent per step, the write-back of ALL its LBA windows of the step, deduplicated (each
+ * KeyFrame / MapPoint once, with the value of the last window that optimised it: the value the per-window blocks,
+ * applied in window order, would leave), in records sized to what changes. Block = header (16 B) | kf_cap KeyFrame
+ * records (32 B) | mp_cap MapPoint records (16 B); gathered = n_agents blocks back to back, applied in agent order. */
+typedef struct mam_update_header {
+    int32_t n_kf, n_mp, agent, status;   /* status: MAM_ERR_CAPACITY when the lists did not fit */
+} mam_update_header;
+typedef struct mam_kf_update {
+    int32_t row;                         /* KeyFrame table row (= pose_id) */
+    float q[4];                          /* Tcw unit quaternion x, y, z, w as KeyFrame::SetPose stores it */
+    float t[3];
+} mam_kf_update;
+typedef struct mam_mp_update {
+    int32_t row;                         /* MapPoint table row (point_id - mp_id_base); bit 31 = marked bad */
+    float xyz[3];                        /* MapPoint::SetWorldPos(pos.cast<float>()) */
+} mam_mp_update;
+
+size_t mam_exchange_compact_block_bytes(int kf_cap, int mp_cap);
+
+/* Pack the deduplicated write-back of n_windows LBA results (DEVICE window descriptors, as for
+ * mam_exchange_pack_windows): KeyFrame record i from kf_src[2 i] = window, kf_src[2 i + 1] = pose index in it (a
+ * non-fixed pose), MapPoint record i from mp_src[2 i], mp_src[2 i + 1] (DEVICE arrays; the host builds them with the
+ * windows: every vertex once, from the last window holding it). Asynchronous. */
+int mam_exchange_pack_sources(int n_windows, const mam_map_window* windows, const int32_t* kf_src, int n_kf,
+                              const int32_t* mp_src, int n_mp, int64_t mp_id_base, int agent, void* block,
+                              int kf_cap, int mp_cap, void* stream);
+
+/* Apply n_agents gathered compact blocks (DEVICE) to the tables, agent 0 first (rows within a block are unique).
+ * A block with status != 0 or counts beyond the caps, or rows outside the tables, set *status to MAM_ERR_ARG. */
+int mam_exchange_apply_compact(const void* gathered, int n_agents, int kf_cap, int mp_cap, float* kf_table,
+                               int64_t kf_rows, float* mp_table, int64_t mp_rows, int32_t* status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

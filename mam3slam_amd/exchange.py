@@ -29,7 +29,39 @@ _SIGS = {
     "mam_exchange_pack_windows": (C.c_int, [C.c_int, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int, C.c_void_p]),
     "mam_map_read_windows": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p,
                                        C.c_int, C.c_void_p, C.c_void_p]),
+    "mam_exchange_compact_block_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+    "mam_exchange_pack_sources": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int64,
+                                            C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "mam_exchange_apply_compact": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64,
+                                             C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),
 }
+
+# compact blocks (include/mam_exchange.h): header | KeyFrame records | MapPoint records
+HEADER_DTYPE = np.dtype([("n_kf", "<i4"), ("n_mp", "<i4"), ("agent", "<i4"), ("status", "<i4")])
+KF_UPDATE_DTYPE = np.dtype([("row", "<i4"), ("q", "<f4", (4,)), ("t", "<f4", (3,))])
+MP_UPDATE_DTYPE = np.dtype([("row", "<i4"), ("xyz", "<f4", (3,))])
+assert HEADER_DTYPE.itemsize == 16 and KF_UPDATE_DTYPE.itemsize == 32 and MP_UPDATE_DTYPE.itemsize == 16
+
+
+def compact_block_bytes(kf_cap: int, mp_cap: int) -> int:
+    return HEADER_DTYPE.itemsize + kf_cap * KF_UPDATE_DTYPE.itemsize + mp_cap * MP_UPDATE_DTYPE.itemsize
+
+
+def dedup_sources(windows):
+    """The write-back of a batch of LBA windows as one deduplicated record set: `windows` = [(pose_id, pose_fixed,
+    point_id)] per window, in the order the windows' results are applied. Every optimised KeyFrame and every MapPoint
+    once, taken from the LAST window holding it — the value the per-window write-backs (Optimizer.cc:1463-1497),
+    applied in window order, leave in the map. Returns (kf_src, mp_src): int32 [n][2] (window, vertex index), in
+    ascending vertex id."""
+    kf, mp = {}, {}
+    for w, (pid, fixed, mid) in enumerate(windows):
+        for i in np.nonzero(np.asarray(fixed) == 0)[0]:
+            kf[int(pid[i])] = (w, int(i))
+        for i, m in enumerate(np.asarray(mid)):
+            mp[int(m)] = (w, i)
+    kf_src = np.array([kf[k] for k in sorted(kf)], np.int32).reshape(-1, 2)
+    mp_src = np.array([mp[k] for k in sorted(mp)], np.int32).reshape(-1, 2)
+    return kf_src, mp_src
 
 
 class MapWindow(C.Structure):
@@ -45,6 +77,102 @@ def _bind():
         fn = getattr(L, name)
         fn.restype, fn.argtypes = res, args
     return L
+
+
+def _as_torch_stream(stream: int, device):
+    """A raw HIP stream handle as a torch stream (0 = the device's default stream)."""
+    import torch
+
+    cur = torch.cuda.current_stream(device)
+    if int(stream) == cur.cuda_stream:
+        return cur
+    if int(stream) == 0:
+        return torch.cuda.default_stream(device)
+    return torch.cuda.ExternalStream(int(stream), device=device)
+
+
+def _all_gather(recv, send, world, group):
+    """all_gather_into_tensor of one block per rank (RCCL on the GPU; gloo on host tensors, or staged through the
+    host for CUDA tensors in the one-GPU multi-rank tests)."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        recv.copy_(send)
+    elif dist.get_backend(group) == "gloo":
+        if send.is_cuda:
+            torch.cuda.current_stream(send.device).synchronize()
+            parts = [torch.empty(send.numel(), dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(parts, send.cpu(), group=group)
+            recv.copy_(torch.cat(parts))
+        else:
+            dist.all_gather(list(recv.view(world, -1).unbind(0)), send, group=group)
+    else:
+        dist.all_gather_into_tensor(recv, send, group=group)
+
+
+class CompactExchange:
+    """The per-step exchange of the bench's LocalMapping leg: each rank packs the deduplicated write-back of all its
+    windows (mam_exchange_pack_sources: 32-byte KeyFrame and 16-byte MapPoint records), one fixed-size all-gather of
+    the blocks (capacities agreed at setup: the largest of any rank), every rank applies all blocks in rank order
+    (mam_exchange_apply_compact)."""
+
+    def __init__(self, kf_cap: int, mp_cap: int, device="cuda", group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.kf_cap, self.mp_cap = int(kf_cap), int(mp_cap)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.block_bytes = compact_block_bytes(self.kf_cap, self.mp_cap)
+        self.send = torch.zeros(self.block_bytes, dtype=torch.uint8, device=device)
+        self.recv = torch.zeros(self.world * self.block_bytes, dtype=torch.uint8, device=device)
+        self._L = _bind()
+        self._pack_stream = None
+        self.gather_ms = []   # host wall of each all-gather (collective on torch's current stream, synchronised)
+
+    def pack(self, d_windows: int, n_windows: int, d_kf_src: int, n_kf: int, d_mp_src: int, n_mp: int,
+             mp_id_base: int, stream: int = 0):
+        check(self._L.mam_exchange_pack_sources(int(n_windows), C.c_void_p(d_windows), C.c_void_p(d_kf_src), int(n_kf),
+                                                C.c_void_p(d_mp_src), int(n_mp), int(mp_id_base), self.rank,
+                                                C.c_void_p(self.send.data_ptr()), self.kf_cap, self.mp_cap,
+                                                C.c_void_p(stream)), "mam_exchange_pack_sources")
+        self._pack_stream = int(stream)
+
+    def gather(self, timed: bool = False):
+        import time
+
+        import torch
+
+        if self._pack_stream is not None and self.send.is_cuda:
+            torch.cuda.current_stream(self.send.device).wait_stream(_as_torch_stream(self._pack_stream, self.send.device))
+        if timed and self.send.is_cuda:
+            torch.cuda.current_stream(self.send.device).synchronize()
+            t0 = time.perf_counter()
+        _all_gather(self.recv, self.send, self.world, self.group)
+        if timed and self.send.is_cuda:
+            torch.cuda.current_stream(self.send.device).synchronize()
+            self.gather_ms.append((time.perf_counter() - t0) * 1e3)
+        return self.recv
+
+    def apply(self, d_kf_table: int, kf_rows: int, d_mp_table: int, mp_rows: int, d_status: int, stream: int = 0):
+        import torch
+
+        if self.send.is_cuda:
+            _as_torch_stream(stream, self.send.device).wait_stream(torch.cuda.current_stream(self.send.device))
+        check(self._L.mam_exchange_apply_compact(C.c_void_p(self.recv.data_ptr()), self.world, self.kf_cap,
+                                                 self.mp_cap, C.c_void_p(d_kf_table), int(kf_rows),
+                                                 C.c_void_p(d_mp_table), int(mp_rows), C.c_void_p(d_status),
+                                                 C.c_void_p(stream)), "mam_exchange_apply_compact")
+
+
+    def read_windows(self, d_kf_table: int, kf_cap: int, d_mp_table: int, mp_cap: int, mp_id_base: int,
+                     d_windows: int, n_windows: int, max_rows: int, d_status: int, stream: int = 0):
+        """The windows' LBA inputs from the (just applied) shared tables, on `stream` (mam_map_read_windows)."""
+        check(self._L.mam_map_read_windows(C.c_void_p(d_kf_table), int(kf_cap), C.c_void_p(d_mp_table), int(mp_cap),
+                                           int(mp_id_base), int(n_windows), C.c_void_p(d_windows), int(max_rows),
+                                           C.c_void_p(d_status), C.c_void_p(stream)), "mam_map_read_windows")
 
 
 class MapUpdateExchange:

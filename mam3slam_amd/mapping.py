@@ -8,9 +8,11 @@ Per step (one call of `run`), for the W keyframes the agents on this GPU inserte
   2. the windows' vertex estimates are read from the shared map tables (mam_map_read_windows: the graph build of
      Optimizer.cc:1218-1286 takes the float map values cast to double);
   3. all W LocalBundleAdjustment solves run together (mam_lba_solve_batch_device: Levenberg control on the device);
-  4. the write-backs (Optimizer.cc:1463-1497) are packed (mam_exchange_pack_windows), all-gathered across GPUs
-     (RCCL over xGMI) and applied in (GPU, window) order to the map every GPU holds — which the next step's windows
-     read. Overlapping windows (shared keyframes / MapPoints) resolve deterministically: later blocks win.
+  4. the write-backs (Optimizer.cc:1463-1497) of all W windows are packed as one deduplicated block per GPU
+     (mam_exchange_pack_sources: every optimised KeyFrame and MapPoint once, from the last window holding it, in
+     32-byte / 16-byte records), all-gathered across GPUs (RCCL over xGMI) and applied in GPU order to the map every
+     GPU holds — which the next step's windows read. Overlapping windows (shared keyframes / MapPoints) resolve
+     deterministically: the later window within a GPU, the higher GPU across GPUs.
 """
 from __future__ import annotations
 
@@ -19,7 +21,7 @@ import ctypes as C
 import numpy as np
 
 from . import world as W
-from .exchange import MapUpdateExchange, MapWindow
+from .exchange import CompactExchange, MapWindow, dedup_sources
 from .lba import LBASolver, _Problem, _Result
 
 
@@ -96,19 +98,25 @@ class LocalMappingLeg:
                 d.pose_id, d.pose_fixed, d.point_id, d.point_bad = pid.data_ptr(), fix.data_ptr(), mid.data_ptr(), None
                 d.pose_q, d.pose_t, d.point_xyz = q.data_ptr(), t.data_ptr(), x.data_ptr()
         self.max_rows = max_rows
-        # the exchange's fixed block size must be the same on every rank (a collective over blocks of different
-        # sizes fails or hangs): the largest window of any rank
+        # the write-back of all W windows as one deduplicated record set (every optimised KeyFrame / MapPoint once, from
+        # the last window holding it), and the exchange's fixed block size: it must be the same on every rank (a
+        # collective over blocks of different sizes fails or hangs), the largest of any rank
+        kf_src, mp_src = dedup_sources([(p.pose_id, p.pose_fixed, p.point_id) for p in self.probs])
+        self.n_kf_upd, self.n_mp_upd = len(kf_src), len(mp_src)
+        self.d_kf_src, self.d_mp_src = dev(kf_src), dev(mp_src)
+        caps = [self.n_kf_upd, self.n_mp_upd]
         import torch.distributed as dist
 
         if world_size > 1 and dist.is_available() and dist.is_initialized():
             on_gpu = dist.get_backend() == "nccl"
-            t = torch.tensor([cap], dtype=torch.int64, device=device if on_gpu else "cpu")
+            t = torch.tensor(caps, dtype=torch.int64, device=device if on_gpu else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            cap = int(t.item())
-        self.cap = cap
+            caps = [int(v) for v in t.tolist()]
+        self.cap = cap   # the largest window's records (per-window blocks of the tests' reference path)
         self.d_read = dev(np.frombuffer(bytes(rd), np.uint8))
         self.d_pack = dev(np.frombuffer(bytes(pk), np.uint8))
-        self.exch = MapUpdateExchange(capacity=self.W * (cap + 1) - 1, device=device)
+        self.exch = CompactExchange(caps[0], caps[1], device=device)
+        self.time_gather = False
         # the new keyframe of window w: its last local keyframe; its new MapPoints: those homed there
         self.new_kf = torch.tensor([min(s + n_opt - 1, self.world.n_kf - 1) for s in self.starts], device=device)
         homes = [np.nonzero(self.world.home == int(k))[0] for k in self.new_kf.cpu().numpy()]
@@ -137,7 +145,9 @@ class LocalMappingLeg:
         self.mp_table[self.new_mp, :3] += torch.randn((len(self.new_mp), 3), generator=g, device=self.dev) * 0.017
 
     def run(self, step: int, new_keyframes: bool = True):
-        """One LocalMapping step on self.stream (synchronous: returns when the map holds every GPU's write-backs)."""
+        """One LocalMapping step: the solves are synchronous (mam_lba_solve_batch_device returns with the Levenberg
+        state read back), the pack / all-gather / apply are queued: on return the map tables are final for work
+        ordered after self.stream (a consumer on another stream waits on it)."""
         import torch
 
         with torch.cuda.stream(self.stream):
@@ -153,10 +163,11 @@ class LocalMappingLeg:
                 raise RuntimeError(f"mam_lba_solve_batch_device: {check}")
             self.stats = [(int(r.iterations), int(r.lm_trials), int(r.status)) for r in self.c_res]
             self.windows_solved += self.W
-            self.exch.pack_windows(self.d_pack.data_ptr(), self.W, self.mp_base, self.cap, stream=s)
-            self.exch.gather()
+            self.exch.pack(self.d_pack.data_ptr(), self.W, self.d_kf_src.data_ptr(), self.n_kf_upd,
+                           self.d_mp_src.data_ptr(), self.n_mp_upd, self.mp_base, stream=s)
+            self.exch.gather(timed=self.time_gather)
             self.exch.apply(self.kf_table.data_ptr(), self.world.n_kf, self.mp_table.data_ptr(), self.world.n_mp,
-                            self.status.data_ptr(), stream=s, n_agents=self.world_size * self.W, capacity=self.cap)
+                            self.status.data_ptr(), stream=s)
         return self.stats
 
     def window_inputs(self, w: int):
@@ -375,7 +386,7 @@ class NewMapPointsLeg:
             pr = pr.cpu().numpy()
             fwd_frame, fwd_mp = pr[:, 1], pr[:, 0]
             bwd_frame = np.repeat(pr[::NN, 0], NBK)
-            bwd_mp = pr.reshape(W, NN)[:, :NBK, 1].reshape(-1)
+            bwd_mp = pr.reshape(W, NN, 2)[:, :NBK, 1].reshape(-1)
             self.sin_items[head] = tuple(torch.tensor(np.ascontiguousarray(a, np.int32), device=self.dev)
                                          for a in (fwd_frame, fwd_mp, bwd_frame, bwd_mp))
         nf, nb = W * NN, W * NBK

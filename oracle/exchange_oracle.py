@@ -68,3 +68,64 @@ def apply(gathered, n_agents, capacity, kf_table, mp_table):
             else:
                 status = ERR_ARG
     return status
+
+
+# ---- compact blocks (mam_exchange_pack_sources / mam_exchange_apply_compact)
+def pack_sources(results, kf_src, mp_src, mp_id_base, agent, kf_cap, mp_cap):
+    """results: per window (pose_q, pose_t, pose_id, point_xyz, point_id, point_bad or None); returns the block bytes."""
+    from mam3slam_amd.exchange import HEADER_DTYPE, KF_UPDATE_DTYPE, MP_UPDATE_DTYPE
+
+    h = np.zeros(1, HEADER_DTYPE)
+    K = np.zeros(kf_cap, KF_UPDATE_DTYPE)
+    M = np.zeros(mp_cap, MP_UPDATE_DTYPE)
+    nk, nm = len(kf_src), len(mp_src)
+    h["n_kf"], h["n_mp"], h["agent"] = nk, nm, agent
+    h["status"] = ERR_CAPACITY if (nk > kf_cap or nm > mp_cap) else 0
+    for i, (w, v) in enumerate(np.asarray(kf_src)[:kf_cap]):
+        pq, pt, pid = results[w][0], results[w][1], results[w][2]
+        q = np.asarray(pq[v], np.float64).astype(np.float32)
+        n = np.float32(np.sqrt(np.float32(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3])))
+        K[i]["row"] = int(pid[v])
+        K[i]["q"] = (q / n).astype(np.float32)
+        K[i]["t"] = np.asarray(pt[v], np.float64).astype(np.float32)
+    for i, (w, v) in enumerate(np.asarray(mp_src)[:mp_cap]):
+        xyz, mid, bad = results[w][3], results[w][4], results[w][5]
+        row = int(mid[v]) - int(mp_id_base)
+        if bad is not None and bad[v]:
+            row = row | -0x80000000
+        M[i]["row"] = row
+        M[i]["xyz"] = np.asarray(xyz[v], np.float64).astype(np.float32)
+    return h.tobytes() + K.tobytes() + M.tobytes()
+
+
+def apply_compact(gathered: bytes, n_agents, kf_cap, mp_cap, kf_table, mp_table):
+    """In place, agent order; returns the status (0 or ERR_ARG)."""
+    from mam3slam_amd.exchange import HEADER_DTYPE, KF_UPDATE_DTYPE, MP_UPDATE_DTYPE, compact_block_bytes
+
+    bb = compact_block_bytes(kf_cap, mp_cap)
+    status = 0
+    for a in range(n_agents):
+        blk = gathered[a * bb:(a + 1) * bb]
+        h = np.frombuffer(blk[:16], HEADER_DTYPE)[0]
+        if int(h["status"]) != 0 or not (0 <= h["n_kf"] <= kf_cap) or not (0 <= h["n_mp"] <= mp_cap):
+            status = ERR_ARG
+            continue
+        K = np.frombuffer(blk[16:16 + 32 * kf_cap], KF_UPDATE_DTYPE)[:int(h["n_kf"])]
+        M = np.frombuffer(blk[16 + 32 * kf_cap:], MP_UPDATE_DTYPE)[:int(h["n_mp"])]
+        for u in K:
+            r = int(u["row"])
+            if 0 <= r < len(kf_table):
+                kf_table[r, :4] = u["q"]
+                kf_table[r, 4:7] = u["t"]
+                kf_table[r, 7] = 1.0
+            else:
+                status = ERR_ARG
+        for u in M:
+            raw = int(u["row"])
+            r = raw & 0x7FFFFFFF
+            if r < len(mp_table):
+                mp_table[r, :3] = u["xyz"]
+                mp_table[r, 3] = 1.0 if raw < 0 else 0.0
+            else:
+                status = ERR_ARG
+    return status

@@ -153,3 +153,102 @@ def test_world_windows_are_consistent():
         assert len(p.point_id) > 2500 and len(p.edge_point) > 8 * 2500 * 0.9
     assert len(np.intersect1d(k0, k1)) >= 25 and len(np.intersect1d(m0, m1)) > 1000
     assert p0.pose_fixed[0] == 1   # keyframe 0: the map's init keyframe (Optimizer.cc:1220)
+
+
+def _windows_results(n_windows=4, seed=0):
+    """Per-window LBA results over overlapping vertex sets (windows of one agent in one step)."""
+    rng = np.random.default_rng(seed)
+    res, wins = [], []
+    for w in range(n_windows):
+        pid = np.arange(10 * w, 10 * w + 25, dtype=np.int64)
+        fixed = ((pid % 7) == 0).astype(np.uint8)
+        mid = np.sort(rng.choice(np.arange(100 * w, 100 * w + 400), size=250, replace=False)).astype(np.int64) + 1000
+        q = rng.normal(size=(len(pid), 4))
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+        t = rng.normal(size=(len(pid), 3))
+        xyz = rng.normal(size=(len(mid), 3)) * 4
+        bad = (rng.random(len(mid)) < 0.05).astype(np.uint8)
+        res.append((q, t, pid, xyz, mid, bad))
+        wins.append((pid, fixed, mid))
+    return res, wins
+
+
+def test_compact_block_equals_per_window_blocks():
+    """The deduplicated block (every vertex once, from the last window holding it) leaves the tables exactly as the
+    per-window write-backs applied in window order do, at 16 / 32 bytes per record instead of 64."""
+    from mam3slam_amd.exchange import compact_block_bytes, dedup_sources
+
+    res, wins = _windows_results()
+    mp_base = 1000
+    kf_src, mp_src = dedup_sources(wins)
+    ids_kf = [int(wins[w][0][i]) for w, i in kf_src]
+    ids_mp = [int(wins[w][2][i]) for w, i in mp_src]
+    assert ids_kf == sorted(set(ids_kf)) and ids_mp == sorted(set(ids_mp))
+    blk = xo.pack_sources(res, kf_src, mp_src, mp_base, 0, len(kf_src), len(mp_src))
+    assert len(blk) == compact_block_bytes(len(kf_src), len(mp_src))
+    kf_a, mp_a = np.zeros((64, 8), np.float32), np.zeros((1000, 4), np.float32)
+    assert xo.apply_compact(blk, 1, len(kf_src), len(mp_src), kf_a, mp_a) == 0
+    kf_b, mp_b = np.zeros((64, 8), np.float32), np.zeros((1000, 4), np.float32)
+    cap = max(int((f == 0).sum()) + len(m) for _, f, m in wins)
+    blocks = [xo.pack_lba(q, t, pid, wins[w][1], xyz, mid - mp_base, bad, 0, cap)
+              for w, (q, t, pid, xyz, mid, bad) in enumerate(res)]
+    assert xo.apply(np.concatenate(blocks), len(blocks), cap, kf_b, mp_b) == 0
+    assert np.array_equal(kf_a, kf_b) and np.array_equal(mp_a, mp_b)
+    assert len(blk) < sum(b.nbytes for b in blocks) / 3
+    # capacity overflow is flagged and the block is rejected whole
+    small = xo.pack_sources(res, kf_src, mp_src, mp_base, 0, len(kf_src), len(mp_src) - 1)
+    kf_c, mp_c = np.zeros((64, 8), np.float32), np.zeros((1000, 4), np.float32)
+    assert xo.apply_compact(small, 1, len(kf_src), len(mp_src) - 1, kf_c, mp_c) == xo.ERR_ARG and not mp_c.any()
+
+
+@pytest.mark.gpu
+def test_compact_pack_apply_kernels(gpu_lib):
+    """mam_exchange_pack_sources / mam_exchange_apply_compact byte-exact vs the restatement, two agents' blocks
+    applied in agent order."""
+    import torch
+
+    from mam3slam_amd.exchange import CompactExchange, MapWindow, compact_block_bytes, dedup_sources
+
+    dev = torch.device("cuda")
+    mp_base = 1000
+    blocks, keep = [], []
+    caps = None
+    for agent in range(2):
+        res, wins = _windows_results(seed=agent)
+        kf_src, mp_src = dedup_sources(wins)
+        caps = caps or (len(kf_src) + 8, len(mp_src) + 8)
+        ex = CompactExchange(caps[0], caps[1], device=dev)
+        ex.rank = agent
+        desc = (MapWindow * len(res))()
+        for w, (q, t, pid, xyz, mid, bad) in enumerate(res):
+            T = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (q, t, pid, wins[w][1], xyz, mid, bad)]
+            keep += T
+            d = desc[w]
+            d.n_poses, d.n_points = len(pid), len(mid)
+            d.pose_q, d.pose_t, d.pose_id, d.pose_fixed = T[0].data_ptr(), T[1].data_ptr(), T[2].data_ptr(), T[3].data_ptr()
+            d.point_xyz, d.point_id, d.point_bad = T[4].data_ptr(), T[5].data_ptr(), T[6].data_ptr()
+        d_desc = torch.from_numpy(np.frombuffer(bytes(desc), np.uint8).copy()).to(dev)
+        d_k, d_m = torch.from_numpy(kf_src).to(dev), torch.from_numpy(mp_src).to(dev)
+        keep += [d_desc, d_k, d_m]
+        ex.send.fill_(0xCD)
+        ex.pack(d_desc.data_ptr(), len(res), d_k.data_ptr(), len(kf_src), d_m.data_ptr(), len(mp_src), mp_base)
+        torch.cuda.synchronize()
+        exp = xo.pack_sources(res, kf_src, mp_src, mp_base, agent, caps[0], caps[1])
+        got = ex.send.cpu().numpy().tobytes()
+        nk, nm = len(kf_src), len(mp_src)
+        used = [(0, 16), (16, 16 + 32 * nk), (16 + 32 * caps[0], 16 + 32 * caps[0] + 16 * nm)]
+        for a, b in used:
+            assert got[a:b] == exp[a:b], (agent, a, b)
+        blocks.append(exp)
+    assert compact_block_bytes(*caps) == len(blocks[0])
+    gathered = b"".join(blocks)
+    ex.recv = torch.from_numpy(np.frombuffer(gathered, np.uint8).copy()).to(dev)
+    ex.world = 2
+    kf = torch.zeros((128, 8), dtype=torch.float32, device=dev)
+    mpt = torch.zeros((1000, 4), dtype=torch.float32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ex.apply(kf.data_ptr(), 128, mpt.data_ptr(), 1000, status.data_ptr())
+    torch.cuda.synchronize()
+    kf_o, mp_o = np.zeros((128, 8), np.float32), np.zeros((1000, 4), np.float32)
+    assert xo.apply_compact(gathered, 2, caps[0], caps[1], kf_o, mp_o) == 0 == int(status.item())
+    assert np.array_equal(kf.cpu().numpy(), kf_o) and np.array_equal(mpt.cpu().numpy(), mp_o)
