@@ -49,6 +49,10 @@ CONFIGS = {
     # BASELINE.json configs[3]: the testMultiAgentSystem agents (test/settingsForTest_00.yaml: KannalaBrandt8, 700
     # features) at 640x480, two agents in total (both on one GPU at --gpus 1, one per GPU at --gpus 2)
     "c3": dict(width=640, height=480, nfeatures=700, lba=True, camera="kb8", agents=2),
+    # BASELINE.json configs[4]: 8 synthetic mono agents at 1280x720 / 2000 features, shared-map local BA, one agent
+    # per GPU at --gpus 8 (all 8 on one GPU at --gpus 1); neighbouring agents' LBA windows overlap (keyframes and
+    # MapPoints of the merged map), so the exchange resolves cross-GPU write conflicts in GPU order
+    "c4": dict(width=1280, height=720, nfeatures=2000, lba=True, agents=8),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFS = 78.6    # MI355X FP64 vector / matrix (spec)
@@ -658,7 +662,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None,
-                    help="frames per step per GPU (independent frame streams); default 256, c3: its 2 agents / N")
+                    help="frames per step per GPU (independent frame streams); default 256, c3 / c4: their 2 / 8 "
+                         "agents / N")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
                     help="c2 (1280x720/2000 + LocalBundleAdjustment) is BASELINE.json's headline metric config")
     ap.add_argument("--kf-every", type=int, default=8,

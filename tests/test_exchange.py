@@ -212,11 +212,12 @@ def test_compact_pack_apply_kernels(gpu_lib):
     dev = torch.device("cuda")
     mp_base = 1000
     blocks, keep = [], []
-    caps = None
+    data = [_windows_results(seed=agent) for agent in range(2)]
+    srcs = [dedup_sources(wins) for _, wins in data]
+    caps = (max(len(k) for k, _ in srcs) + 8, max(len(m) for _, m in srcs) + 8)   # the same block on every agent
     for agent in range(2):
-        res, wins = _windows_results(seed=agent)
-        kf_src, mp_src = dedup_sources(wins)
-        caps = caps or (len(kf_src) + 8, len(mp_src) + 8)
+        res, wins = data[agent]
+        kf_src, mp_src = srcs[agent]
         ex = CompactExchange(caps[0], caps[1], device=dev)
         ex.rank = agent
         desc = (MapWindow * len(res))()
