@@ -7,6 +7,8 @@ predictions, Hamming ties, outliers behind the camera, empty windows).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from .match import (FUSE_MP_DTYPE, LAST_ENTRY_DTYPE, LOCAL_MP_DTYPE, MP_TRACK_DTYPE, Camera, FrameData,
@@ -140,20 +142,19 @@ def pinhole(w, h, f=500.0) -> Pinhole:
     return Pinhole(np.float32(f), np.float32(f), np.float32(w / 2), np.float32(h / 2))
 
 
-# test/settingsForTest_00.yaml (the testMultiAgentSystem agents): KannalaBrandt8 at 960 x 960
-KB8_TEST_YAML = dict(fx=322.7022465231787, fy=322.25818444649866, cx=473.48961846063645, cy=484.62594873664256,
-                     k0=0.052348933344686564, k1=0.014590092715993354, k2=-0.030877354788616376,
-                     k3=0.00650873486325155, width=960, height=960)
+# the reference's test/settingsForTest_00.yaml (the testMultiAgentSystem agents' KannalaBrandt8 at 960 x 960), kept
+# as a fixture with its sibling settingsForTest_01.yaml
+TEST_SETTINGS = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                              "settings", f"settingsForTest_0{i}.yaml") for i in (0, 1)]
 
 
-def kannala_brandt8(w=960, h=960) -> KannalaBrandt8:
-    """The test-YAML fisheye camera; other image sizes scale fx, cx by w / 960 and fy, cy by h / 960 (the distortion
-    acts on the ray angle and is unchanged)."""
-    y = KB8_TEST_YAML
-    sx, sy = w / y["width"], h / y["height"]
-    return KannalaBrandt8(np.float32(y["fx"] * sx), np.float32(y["fy"] * sy), np.float32(y["cx"] * sx),
-                          np.float32(y["cy"] * sy), np.float32(y["k0"]), np.float32(y["k1"]), np.float32(y["k2"]),
-                          np.float32(y["k3"]))
+def kannala_brandt8(w=960, h=960, settings: str | None = None) -> KannalaBrandt8:
+    """Camera 1 of the test settings file (Camera.type KannalaBrandt8, Camera1.*), read with settings.Settings; other
+    image sizes scale fx, cx by w / Camera.width and fy, cy by h / Camera.height (the distortion acts on the ray angle
+    and is unchanged)."""
+    from .settings import Settings
+
+    return Settings(settings or TEST_SETTINGS[0]).camera_scaled(w, h)
 
 
 def small_pose(rng, rot=0.01, trans=0.05):

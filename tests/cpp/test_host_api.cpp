@@ -25,6 +25,7 @@
 #include <thread>
 #include <vector>
 
+#include "mam3slam/Settings.h"
 #include "mam3slam/ORBextractor.h"
 #include "mam3slam/ORBVocabulary.h"
 #include "mam3slam/ORBmatcher.h"
@@ -1001,8 +1002,45 @@ static void testConcurrentGPU() {
           bad_lba);
 }
 
+// The reference's settings keys (Settings.cc:184-270, 443-451) from its two test files: the testMultiAgentSystem agents'
+// KannalaBrandt8 camera and their 700 / 1500-feature extractors; with a device, the extractor built from them
+static void testSettings(bool gpu) {
+    const char* dir = std::getenv("MAM3SLAM_SETTINGS_DIR");
+    const std::string base = dir ? dir : "tests/golden/settings";
+    const int nf[2] = {700, 1500};
+    const float fx[2] = {322.7022465231787f, 319.5669139636673f};
+    for (int i = 0; i < 2; i++) {
+        MAM3SLAM::Settings s(base + "/settingsForTest_0" + std::to_string(i) + ".yaml");
+        CHECK(s.cameraType() == MAM3SLAM::Settings::KannalaBrandt, "settings %d: camera type %d", i, (int)s.cameraType());
+        const MAM3SLAM::GeometricCamera& c = s.camera1();
+        CHECK(c.GetType() == MAM3SLAM::GeometricCamera::CAM_FISHEYE && c.mvParameters[0] == fx[i] &&
+                  c.mvParameters[4] == (float)0.052348933344686564 && c.mvParameters[7] == (float)0.00650873486325155,
+              "settings %d: camera parameters", i);
+        CHECK(s.nFeatures() == nf[i] && s.scaleFactor() == 1.2f && s.nLevels() == 8 && s.initThFAST() == 20 &&
+                  s.minThFAST() == 7,
+              "settings %d: ORB parameters %d %g %d %d %d", i, s.nFeatures(), s.scaleFactor(), s.nLevels(),
+              s.initThFAST(), s.minThFAST());
+        CHECK(s.imageWidth() == 960 && s.imageHeight() == 960 && s.fps() == 20.f, "settings %d: image size", i);
+        if (gpu) {
+            auto ext = s.makeORBextractor();
+            int total = 0;
+            for (int n : ext->GetFeaturesPerLevel()) total += n;
+            CHECK(total == nf[i] && ext->GetLevels() == 8 && ext->GetScaleFactor() == 1.2f,
+                  "settings %d: extractor %d features", i, total);
+        }
+    }
+    bool threw = false;
+    try {
+        MAM3SLAM::Settings bad(base + "/no_such_file.yaml");
+    } catch (const std::runtime_error&) {
+        threw = true;
+    }
+    CHECK(threw, "missing settings file accepted");
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
+    testSettings(mode == "gpu");
     testAlgebra();
     testObservations();
     testWindow();

@@ -68,8 +68,8 @@ def _sanitized_binary(kind):
 
 
 def _run(mode, timeout, binary=None, env=None):
-    r = subprocess.run([binary or _binary(), mode], capture_output=True, text=True, timeout=timeout,
-                       env=None if env is None else {**os.environ, **env})
+    e = {**os.environ, "MAM3SLAM_SETTINGS_DIR": os.path.join(ROOT, "tests", "golden", "settings"), **(env or {})}
+    r = subprocess.run([binary or _binary(), mode], capture_output=True, text=True, timeout=timeout, env=e)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert r.stdout.startswith("OK"), r.stdout
     return r.stdout
