@@ -1008,16 +1008,24 @@ __device__ __forceinline__ double bcast16_d(double v, int k) {
 // v_fmac_f64_dpp row_newbcast (gfx950 DPP64); one instruction where a v_mov_b64_dpp + v_fma_f64 pair was. The s_nop
 // covers the VALU-write -> DPP-read hazard on src (inline asm is not seen by the hazard recognizer); not volatile, so
 // the scheduler may interleave independent work. Same rounding as fma(src_K, m, acc).
-template <int K>
+// NOP = false where src was last written many instructions earlier (the later FMAs of one step, all of Inv16).
+template <int K, bool NOP = true>
 __device__ __forceinline__ void fmac_bcast16(double& acc, double src, double m) {
-    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                 : "+v"(acc)
-                 : "v"(src), "v"(m), "n"(K));
+    if constexpr (NOP)
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+            : "+v"(acc)
+            : "v"(src), "v"(m), "n"(K));
+    else
+        asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+            : "+v"(acc)
+            : "v"(src), "v"(m), "n"(K));
 }
 template <int J, int K>
 struct Fmac16 {
+    // step J's FMAs all read src = A(., J) (written by step J - 1's first FMA, at least a step earlier); the first
+    // keeps the hazard nop, the DPP reads after it are two or more instructions past any write of src
     __device__ __forceinline__ static void run(double* row, double a, double ml) {
-        fmac_bcast16<K>(row[K], a, ml);
+        fmac_bcast16<K, K == J + 1>(row[K], a, ml);
         Fmac16<J, K + 1>::run(row, a, ml);
     }
 };
@@ -1436,7 +1444,8 @@ __device__ __forceinline__ void tile_update(double* TL, int sc, int sa, int sb, 
 template <int R, int J>
 struct Inv16 {
     __device__ __forceinline__ static void run(double* x, const double* row) {
-        fmac_bcast16<R>(x[R], row[J], -x[J]);
+        // row[] is final since the factorization (no write of it in the hazard window)
+        fmac_bcast16<R, false>(x[R], row[J], -x[J]);
         Inv16<R, J + 1>::run(x, row);
     }
 };
@@ -1505,12 +1514,13 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     // after the unknowns: S's padding rows are zero). One wave per tile, lane = (row, 4 columns): two 16-byte loads per
     // lane, the wave's tiles' loads issued together
     {
+        constexpr int U = 6;   // tiles per wave per pass (12 loads of 16 bytes in flight per lane)
         const int i = lane >> 2, j0 = 4 * (lane & 3);
-        for (int s0 = wid; s0 < T; s0 += 2 * NW) {
-            double2 v[2][2];
-            int rr[2], cc[2];
+        for (int s0 = wid; s0 < T; s0 += U * NW) {
+            double2 v[U][2];
+            int rr[U], cc[U];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < U; u++) {
                 const int s = s0 + u * NW;
                 rr[u] = s < T ? sh.tl[2 * s] : 0;
                 cc[u] = s < T ? sh.tl[2 * s + 1] : 0;
@@ -1521,7 +1531,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < U; u++) {
                 const int s = s0 + u * NW;
                 if (s >= T) continue;
                 double e[4] = {v[u][0].x, v[u][0].y, v[u][1].x, v[u][1].y};
@@ -1608,17 +1618,17 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     const int fl = sh.fail;
     if (t == 0) lm.fail = fl;
     if (fl) return;   // uniform (LDS flag after the last barrier)
-    // y /= D
-    for (int i = t; i < N; i += LDLT_THREADS) {
+    // y /= D and the backward substitution L^T x = y by wave 0 alone (a wave's LDS accesses complete in order, so no
+    // barrier): per block x_b = L11^-T y_b from the diagonal tile's upper triangle (written by tiles_diag), then
+    // y_i -= L(kb.., i)^T x_b for the rows i of the block row's non-zero tiles, four tiles per pass
+    if (wid != 0) return;
+    for (int i = lane; i < N; i += 64) {
         const int ii = i / NB;
         Y[i] /= TL[(size_t)slot[ii * nt + ii] * 256 + tsw(i & 15, i & 15)];
     }
-    __syncthreads();
-    // backward substitution L^T x = y: the block by wave 0 as x_b = L11^-T y_b (the diagonal tile's upper triangle,
-    // written by tiles_diag), then each thread i < kb updates its own y_i
     for (int kc = nt - 1; kc >= 0; kc--) {
         const int kb = NB * kc;
-        if (wid == 0 && lane < NB) {
+        if (lane < NB) {
             const double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
             double v = Y[kb + lane];
 #pragma unroll
@@ -1626,19 +1636,21 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
                 if (j > lane) v = fma(Td[tsw(lane, j)], Y[kb + j], v);
             Y[kb + lane] = v;
         }
-        __syncthreads();
-        for (int i = t; i < kb; i += LDLT_THREADS) {
-            const int s = slot[kc * nt + i / NB];   // L(kb.., i) not structurally zero
-            if (s < 0) continue;
-            const double* Tr = TL + (size_t)s * 256;
-            double sy = Y[i];
+        const int g = lane >> 4, il = lane & 15;
+        for (int c0 = kc - 1; c0 >= 0; c0 -= 4) {
+            const int c = c0 - g;
+            const int s = c >= 0 ? slot[kc * nt + c] : -1;   // L(kb.., 16 c..) not structurally zero
+            if (s >= 0) {
+                const double* Tr = TL + (size_t)s * 256;
+                const int i = NB * c + il;
+                double sy = Y[i];
 #pragma unroll
-            for (int j = 0; j < NB; j++) sy = fma(-Tr[tsw(j, i & 15)], Y[kb + j], sy);
-            Y[i] = sy;
+                for (int j = 0; j < NB; j++) sy = fma(-Tr[tsw(j, il)], Y[kb + j], sy);
+                Y[i] = sy;
+            }
         }
-        __syncthreads();
     }
-    for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+    for (int i = lane; i < n; i += 64) d.x[i] = Y[i];
     LPROF(4);
 #ifdef MAM_LDLT_PROFILE
     if (t == 0) atomicAdd(&g_lprof[7], 1ull);
