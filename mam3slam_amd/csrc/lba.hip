@@ -1580,33 +1580,27 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         __syncthreads();
         LPROF(1);
         if (kc + 1 == nt) break;
-        // (C1) the next block column: tiles (r, kc + 1), r > kc, updated by L(r, kc) D L(kc + 1, kc)^T
-        const int s_n = slot[(kc + 1) * nt + kc];   // L(kc + 1, kc)
-        if (s_n >= 0) {
-            for (int r = kc + 1 + wid; r < nt; r += NW) {
-                const int sa = slot[r * nt + kc];
-                if (sa < 0) continue;
-                tile_update(TL, slot[r * nt + kc + 1], sa, s_n, dkp, lane);
-            }
-        }
-        __syncthreads();
-        LPROF(2);
-        // (C2) wave 0: the next diagonal tile; the other waves: tiles (r, c), kc + 1 < c <= r
+        // (C) wave 0: the next diagonal tile, updated by L(kc + 1, kc) D L(kc + 1, kc)^T, then factored (the critical
+        // path: no barrier between); the other waves: every other trailing tile (r, c), kc + 1 <= c <= r, (r, c) !=
+        // (kc + 1, kc + 1), updated by L(r, kc) D L(c, kc)^T
         if (wid == 0) {
 #ifdef MAM_LDLT_PROFILE
             const long long td = clock64();
 #endif
-            tiles_diag(TL, slot[(kc + 1) * nt + kc + 1], kb + NB, Y, sh, sh.dk[p ^ 1], lane);
+            const int s_n = slot[(kc + 1) * nt + kc];
+            const int sd = slot[(kc + 1) * nt + kc + 1];
+            if (s_n >= 0) tile_update(TL, sd, s_n, s_n, dkp, lane);
+            tiles_diag(TL, sd, kb + NB, Y, sh, sh.dk[p ^ 1], lane);
 #ifdef MAM_LDLT_PROFILE
             if (lane == 0) atomicAdd(&g_lprof[5], (unsigned long long)(clock64() - td));
 #endif
         } else {
-            const int T2 = nt - kc - 2;
+            const int T2 = nt - kc - 1;
             const int n2 = T2 * (T2 + 1) / 2;
-            for (int q = wid - 1; q < n2; q += NW - 1) {
+            for (int q = wid; q < n2; q += NW - 1) {   // q = 0 is the diagonal tile
                 int tr, tc;
                 tri_index(q, &tr, &tc);
-                const int r = kc + 2 + tr, c = kc + 2 + tc;
+                const int r = kc + 1 + tr, c = kc + 1 + tc;
                 const int sa = slot[r * nt + kc], sb = slot[c * nt + kc];
                 if (sa < 0 || sb < 0) continue;
                 tile_update(TL, slot[r * nt + c], sa, sb, dkp, lane);
@@ -1631,9 +1625,12 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         if (lane < NB) {
             const double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
             double v = Y[kb + lane];
+            // predicated, not branched: every lane's loads issue together (a branch per j was one LDS round trip each)
 #pragma unroll
-            for (int j = 1; j < NB; j++)
-                if (j > lane) v = fma(Td[tsw(lane, j)], Y[kb + j], v);
+            for (int j = 1; j < NB; j++) {
+                const double f = fma(Td[tsw(lane, j)], Y[kb + j], v);
+                v = j > lane ? f : v;
+            }
             Y[kb + lane] = v;
         }
         const int g = lane >> 4, il = lane & 15;
