@@ -149,6 +149,33 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// The same butterfly sums for 4 Q values at once, reduce-scatter style: the xor-32 and xor-16 steps each exchange
+// only the half of the values the lane keeps (a lane with the bit clear keeps the lower half), then the xor 8..1 steps
+// on the Q values left. Lane group g = lane >> 4 ends with values [g Q, g Q + Q) — each one bit for bit what
+// wave_sum_d returns for it (the same pairs added in the same order) — for 7 Q shuffles instead of 24 Q.
+template <int Q>
+__device__ __forceinline__ void wave_sum_scatter4(const double (&v)[4 * Q], double (&out)[Q]) {
+    const int lane = lane_id();
+    const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0;
+    double h[2 * Q];
+#pragma unroll
+    for (int i = 0; i < 2 * Q; i++) {
+        const double send = b5 ? v[i] : v[2 * Q + i];
+        const double keep = b5 ? v[2 * Q + i] : v[i];
+        h[i] = keep + __shfl_xor(send, 32, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < Q; i++) {
+        const double send = b4 ? h[i] : h[Q + i];
+        const double keep = b4 ? h[Q + i] : h[i];
+        out[i] = keep + __shfl_xor(send, 16, 64);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1)
+#pragma unroll
+        for (int i = 0; i < Q; i++) out[i] += __shfl_xor(out[i], o, 64);
+}
+
 // ---- per edge: error, robust weight, Jacobians (EdgeSE3ProjectXYZ); returns the edge's rho0
 // jo / ho: where the edge's jac (21) and H_pl (18) records go (the caller's LDS staging slots); both are always
 // written when want_jac (zeros where the edge is inactive or its pose fixed).
@@ -543,20 +570,33 @@ __device__ double sys_body(const Prob& d) {
 #pragma unroll
         for (int a = 0; a < 6; a++) acc[21 + a] += B0[a] * o0 + B1[a] * o1;
     }
+    // 27 sums (+ one zero pad) reduce-scattered: lane group g holds sums [7 g, 7 g + 7), lane g * 16 + i sum 7 g + i
+    double tot[7];
+    {
+        double v28[28];
 #pragma unroll
-    for (int k = 0; k < 27; k++) acc[k] = wave_sum_d(acc[k]);
+        for (int k = 0; k < 27; k++) v28[k] = acc[k];
+        v28[27] = 0.0;
+        wave_sum_scatter4<7>(v28, tot);
+    }
+    const int g = lane >> 4, il = lane & 15;
+    double val = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) val = (il == i) ? tot[i] : val;
+    const int q = 7 * g + il;   // this lane's sum (upper-triangle order of H, then b)
     double m = 0.0;
-    if (lane == 0) {
-        int q = 0;
-        double* H = d.Hpp + 36 * (size_t)h;
-        for (int a = 0; a < 6; a++)
-            for (int c = a; c < 6; c++) {
-                H[6 * a + c] = acc[q];
-                H[6 * c + a] = acc[q];
-                if (c == a) m = fmax(m, fabs(acc[q]));
-                q++;
-            }
-        for (int a = 0; a < 6; a++) d.b[6 * (size_t)h + a] = acc[21 + a];
+    if (il < 7 && q < 27) {
+        if (q < 21) {
+            int a = 0, r = q;
+            while (r >= 6 - a) { r -= 6 - a; a++; }
+            const int c = a + r;
+            double* H = d.Hpp + 36 * (size_t)h;
+            H[6 * a + c] = val;
+            H[6 * c + a] = val;
+            if (c == a) m = fabs(val);
+        } else {
+            d.b[6 * (size_t)h + (q - 21)] = val;
+        }
     }
     return m;
 }
@@ -762,24 +802,30 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
         const int2 pr = d.blk_pair[k];
         const double* W = d.bdinv + 18 * (size_t)pr.x;
         const double* B = d.hpl + 18 * (size_t)pr.y;
-        double w[18], b[18];
+        double w[18], b[18];   // 144-byte records, 16-byte aligned: nine 16-byte loads each
 #pragma unroll
-        for (int k = 0; k < 18; k++) { w[k] = W[k]; b[k] = B[k]; }
+        for (int k = 0; k < 9; k++) {
+            const double2 wv = reinterpret_cast<const double2*>(W)[k], bv = reinterpret_cast<const double2*>(B)[k];
+            w[2 * k] = wv.x; w[2 * k + 1] = wv.y;
+            b[2 * k] = bv.x; b[2 * k + 1] = bv.y;
+        }
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
             for (int c = 0; c < 6; c++)
                 acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
     }
-#pragma unroll
-    for (int k = 0; k < 36; k++) acc[k] = wave_sum_d(acc[k]);
-    if (lane < 36) {
-        const int r = lane / 6, c = lane % 6;
+    // the 36 sums reduce-scattered: lane group g holds sums [9 g, 9 g + 9)
+    double tot[9];
+    wave_sum_scatter4<9>(acc, tot);
+    const int il = lane & 15, k = 9 * (lane >> 4) + il;
+    if (il < 9) {
         double v = 0.0;
 #pragma unroll
-        for (int k = 0; k < 36; k++) v = (k == lane) ? acc[k] : v;
+        for (int i = 0; i < 9; i++) v = (il == i) ? tot[i] : v;
+        const int r = k / 6, c = k % 6;
         double out = -v;
-        if (i1 == i2) out = (d.Hpp[36 * (size_t)i1 + lane] + (r == c ? lambda : 0.0)) - v;
+        if (i1 == i2) out = (d.Hpp[36 * (size_t)i1 + k] + (r == c ? lambda : 0.0)) - v;
         const int N = d.npad;
         d.S[(size_t)(6 * i2 + c) * N + 6 * i1 + r] = out;   // the lower triangle, the one the factorization reads
     }
