@@ -676,6 +676,7 @@ def main():
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency and ingest sections")
     ap.add_argument("--no-pose", action="store_true", help="skip the PoseOptimization section")
     ap.add_argument("--no-sin", action="store_true", help="skip the SearchInNeighbors section")
+    ap.add_argument("--no-overlap", action="store_true", help="skip timing each leg alone")
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--profile-timed", action="store_true",
                     help="record LocalMapping's stage events inside the timed region (default: a second pass)")
@@ -834,6 +835,30 @@ def main():
         stv = int(mapping.status.cpu().numpy()[0])
         if stv != 0 or any(s[2] < 0 for s in mapping.stats):
             raise RuntimeError(f"LocalMapping leg status {stv} / {mapping.stats}")
+    overlap = None
+    if mapping is not None and not args.no_overlap:
+        # each leg alone over the same number of steps (outside the timed region): Tracking's step (the HIP graph),
+        # then LocalMapping's run (the LocalBundleAdjustment windows + exchange) — how much of the combined step is
+        # overlap and how much is the legs contending for CUs
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            tr.step()
+        torch.cuda.synchronize(dev)
+        tr_only = (time.perf_counter() - t1) * 1e3 / args.steps
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            mapping.run(10_000 + i)
+        torch.cuda.synchronize(dev)
+        lm_only = (time.perf_counter() - t1) * 1e3 / args.steps
+        overlap = {"combined_ms_per_step": el * 1e3 / args.steps, "tracking_only_ms_per_step": tr_only,
+                   "local_mapping_only_ms_per_step": lm_only,
+                   "note": "the same steps with one leg only (tracking: the step's HIP graph; LocalMapping: its "
+                           "LocalBundleAdjustment windows + exchange, no concurrent tracking), rank-local wall time"}
     stages = tr.stage_pass(args.steps)
     lat = None if args.no_latency else latency_section(tr)
     ingest = None if args.no_latency else ingest_section(tr)
@@ -936,6 +961,8 @@ def main():
             out["latency"] = lat
         if ingest is not None:
             out["ingest"] = ingest
+        if overlap is not None:
+            out["overlap"] = overlap
         if mapping is not None:
             its = [s[0] for s in mapping.stats]
             trials = [s[1] for s in mapping.stats]
