@@ -498,22 +498,26 @@ __global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs
     const Prob& d = probs[blockIdx.y];
     const LM& lm = *d.lm;
     if (lm.status || (mode != 2 && lm.done) || (mode == 0 && !lm.need_lin)) return;
-    __shared__ double sj[EW * 21];
-    __shared__ double sh[EW * 18];
+    __shared__ double sj[EW * 21];   // one staging buffer (LDS bounds the resident waves of this one-wave kernel)
     const int e0 = blockIdx.x * EW;
     if (e0 < d.E) {
         const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
         const int lane = lane_id(), e = e0 + lane;
-        double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0, sj + 21 * lane,
-                                            sh + 18 * lane)
-                           : 0.0;
+        double jr[21], hr[18];   // the edge's records in registers, staged through one LDS buffer in turn
+        double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0, jr, hr) : 0.0;
         r = wave_sum_d(r);
         if (lane == 0) (mode == 0 ? d.part0 : d.part)[blockIdx.x] = r;
         if (mode == 0) {
             const int ne = min(EW, d.E - e0);
+#pragma unroll
+            for (int k = 0; k < 21; k++) sj[21 * lane + k] = jr[k];
             __syncthreads();
             wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
-            wave_copy_out(d.hpl + 18 * (size_t)e0, sh, 18 * ne);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 18; k++) sj[18 * lane + k] = hr[k];
+            __syncthreads();
+            wave_copy_out(d.hpl + 18 * (size_t)e0, sj, 18 * ne);
         }
     }
     if (mode == 1) {
@@ -705,16 +709,17 @@ __global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ prob
     }
     const int e0 = blockIdx.x * EW;
     if (e0 >= d.E) return;
-    __shared__ double sh[EW * 18];
-    __shared__ double sw[EW * 18];
-    __shared__ double sc[EW * 6];
+    __shared__ double sh[EW * 18];   // H_pl in, then W, then the coefficients out (one buffer: occupancy)
     const int ne = min(EW, d.E - e0);
     wave_copy_in(sh, d.hpl + 18 * (size_t)e0, 18 * ne);
     __syncthreads();
     const int e = e0 + lane;
+    double o[18], cf[6];
+#pragma unroll
+    for (int k = 0; k < 18; k++) o[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) cf[k] = 0.0;
     if (e < d.E) {
-        double* o = sw + 18 * lane;
-        double* cf = sc + 6 * lane;
         if (d.pose_h[d.edge_pose[e]] >= 0 || d.pe_idx[d.pe_off[d.edge_point[e]]] == e) {
             const int h = d.edge_point[e];
             double Di[9];
@@ -733,8 +738,15 @@ __global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ prob
         }
     }
     __syncthreads();
-    wave_copy_out(d.bdinv + 18 * (size_t)e0, sw, 18 * ne);
-    wave_copy_out(d.coef + 6 * (size_t)e0, sc, 6 * ne);
+#pragma unroll
+    for (int k = 0; k < 18; k++) sh[18 * lane + k] = o[k];
+    __syncthreads();
+    wave_copy_out(d.bdinv + 18 * (size_t)e0, sh, 18 * ne);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 6; k++) sh[6 * lane + k] = cf[k];
+    __syncthreads();
+    wave_copy_out(d.coef + 6 * (size_t)e0, sh, 6 * ne);
 }
 
 // triangle index q -> (tr, tc), tc <= tr
@@ -798,22 +810,40 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
-    for (int k = d.blk_off[bx] + lane; k < d.blk_off[bx + 1]; k += 64) {
-        const int2 pr = d.blk_pair[k];
-        const double* W = d.bdinv + 18 * (size_t)pr.x;
-        const double* B = d.hpl + 18 * (size_t)pr.y;
-        double w[18], b[18];   // 144-byte records, 16-byte aligned: nine 16-byte loads each
+    // 64 pairs per pass: the pass's 128 records (W of the pose-i1 edges, H_pl of the pose-i2 edges, 144 bytes each)
+    // loaded cooperatively — lane-consecutive 16-byte chunks of 9-chunk records, 18 loads per lane in flight — into
+    // LDS, then lane p takes pair p (the same pairs per lane, in the same order, as a lane-strided loop)
+    __shared__ int2 spr[64];
+    __shared__ double2 stg[128 * 9];
+    const int k0 = d.blk_off[bx], k1 = d.blk_off[bx + 1];
+    for (int base = k0; base < k1; base += 64) {
+        const int np = min(64, k1 - base);
+        spr[lane] = lane < np ? d.blk_pair[base + lane] : make_int2(0, 0);
+        __syncthreads();
+        double2 v[18];
 #pragma unroll
-        for (int k = 0; k < 9; k++) {
-            const double2 wv = reinterpret_cast<const double2*>(W)[k], bv = reinterpret_cast<const double2*>(B)[k];
-            w[2 * k] = wv.x; w[2 * k + 1] = wv.y;
-            b[2 * k] = bv.x; b[2 * k + 1] = bv.y;
+        for (int it = 0; it < 18; it++) {
+            const int c = it * 64 + lane, r = c / 9, part = c - 9 * r, pr = r & 63;
+            const int2 ee = spr[pr];
+            const double* src = r < 64 ? d.bdinv + 18 * (size_t)ee.x : d.hpl + 18 * (size_t)ee.y;
+            v[it] = pr < np ? reinterpret_cast<const double2*>(src)[part] : make_double2(0.0, 0.0);
         }
 #pragma unroll
-        for (int r = 0; r < 6; r++)
+        for (int it = 0; it < 18; it++) stg[it * 64 + lane] = v[it];
+        __syncthreads();
+        if (lane < np) {
+            const double* W = reinterpret_cast<const double*>(stg + 9 * lane);
+            const double* B = reinterpret_cast<const double*>(stg + 9 * (64 + lane));
+            double w[18], b[18];
 #pragma unroll
-            for (int c = 0; c < 6; c++)
-                acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
+            for (int k = 0; k < 18; k++) { w[k] = W[k]; b[k] = B[k]; }
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int c = 0; c < 6; c++)
+                    acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
+        }
+        __syncthreads();
     }
     // the 36 sums reduce-scattered: lane group g holds sums [9 g, 9 g + 9)
     double tot[9];
