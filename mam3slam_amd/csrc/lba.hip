@@ -810,40 +810,23 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
-    // 64 pairs per pass: the pass's 128 records (W of the pose-i1 edges, H_pl of the pose-i2 edges, 144 bytes each)
-    // loaded cooperatively — lane-consecutive 16-byte chunks of 9-chunk records, 18 loads per lane in flight — into
-    // LDS, then lane p takes pair p (the same pairs per lane, in the same order, as a lane-strided loop)
-    __shared__ int2 spr[64];
-    __shared__ double2 stg[128 * 9];
-    const int k0 = d.blk_off[bx], k1 = d.blk_off[bx + 1];
-    for (int base = k0; base < k1; base += 64) {
-        const int np = min(64, k1 - base);
-        spr[lane] = lane < np ? d.blk_pair[base + lane] : make_int2(0, 0);
-        __syncthreads();
-        double2 v[18];
+    for (int k = d.blk_off[bx] + lane; k < d.blk_off[bx + 1]; k += 64) {
+        const int2 pr = d.blk_pair[k];
+        const double* W = d.bdinv + 18 * (size_t)pr.x;
+        const double* B = d.hpl + 18 * (size_t)pr.y;
+        double w[18], b[18];   // 144-byte records, 16-byte aligned: nine 16-byte loads each (staging the records
+                               // cooperatively through LDS measured slower: 18 KB per wave halves the resident waves)
 #pragma unroll
-        for (int it = 0; it < 18; it++) {
-            const int c = it * 64 + lane, r = c / 9, part = c - 9 * r, pr = r & 63;
-            const int2 ee = spr[pr];
-            const double* src = r < 64 ? d.bdinv + 18 * (size_t)ee.x : d.hpl + 18 * (size_t)ee.y;
-            v[it] = pr < np ? reinterpret_cast<const double2*>(src)[part] : make_double2(0.0, 0.0);
+        for (int q = 0; q < 9; q++) {
+            const double2 wv = reinterpret_cast<const double2*>(W)[q], bv = reinterpret_cast<const double2*>(B)[q];
+            w[2 * q] = wv.x; w[2 * q + 1] = wv.y;
+            b[2 * q] = bv.x; b[2 * q + 1] = bv.y;
         }
 #pragma unroll
-        for (int it = 0; it < 18; it++) stg[it * 64 + lane] = v[it];
-        __syncthreads();
-        if (lane < np) {
-            const double* W = reinterpret_cast<const double*>(stg + 9 * lane);
-            const double* B = reinterpret_cast<const double*>(stg + 9 * (64 + lane));
-            double w[18], b[18];
+        for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int k = 0; k < 18; k++) { w[k] = W[k]; b[k] = B[k]; }
-#pragma unroll
-            for (int r = 0; r < 6; r++)
-#pragma unroll
-                for (int c = 0; c < 6; c++)
-                    acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
-        }
-        __syncthreads();
+            for (int c = 0; c < 6; c++)
+                acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
     }
     // the 36 sums reduce-scattered: lane group g holds sums [9 g, 9 g + 9)
     double tot[9];
