@@ -57,13 +57,12 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFS = 78.6    # MI355X FP64 vector / matrix (spec)
 # what limits each stage; the byte/integer path has no MFMA work
+# the limiter of a stage when no counter file of the config is present (with one, bench.py writes the limiter from
+# that config's counters: profiles/traffic_<config>.json)
 ROOFLINE_NOTES = {
-    "fast": ("latency / issue: per 64-frame launch VALU busy 11%, 33% of wave cycles waiting (s_waitcnt, barriers) and "
-             "37% issue-stalled; FETCH_SIZE 28 MB raw = algorithmic after the XCD-aware cell order "
-             "(profiles/r02/pmc_c1_64frame.json)"),
+    "fast": "latency / issue: per-cell workgroups over ~630 pixel pairs each (no PMC file for this config)",
     "pyramid": "bilinear resize, latency-bound at 7 dependent launches",
-    "describe": ("one wave per keypoint: IC-angle loads + the 37x37 blurred patch in LDS, two dependent round trips; "
-                 "57% of wave cycles waiting, VALU busy 9% (profiles/r02/pmc_c1_64frame.json)"),
+    "describe": "one wave per keypoint: IC-angle loads + the 37x37 blurred patch in LDS, two dependent round trips",
     "resolve": "one workgroup per frame, greedy dependency rounds (latency, LDS atomics)",
 }
 
@@ -101,6 +100,47 @@ def lba_flops(E, L, Np, m_avg, trials, iterations):
     n = 6 * Np
     per_trial = L * m_avg * (m_avg + 1) / 2 * 216 + L * (60 + 144 * m_avg) + n ** 3 / 3 + L * (36 * m_avg + 18) + E * 60
     return iterations * E * 420 + trials * per_trial
+
+
+def ldlt_tile_flops(prob) -> float:
+    """Algorithmic FP64 flops of one tile-skipping LDL^T factorization + solve of the window's reduced camera system
+    (what k_ldlt_tiles must compute given the structure): S's 16x16 tiles that are non-zero (pose blocks sharing a
+    landmark) plus the symbolic fill; per panel the diagonal tile's LDL^T and inverse (2 * 16^3 / 3 each), each panel
+    tile L21 = A21 M (2 * 16^3), each trailing update L(r) D L(c)^T of two non-zero panel tiles (2 * 16^3, half for a
+    diagonal tile), and the forward / backward solves (2 * 2 * 256 per non-zero tile)."""
+    fixed = np.asarray(prob.pose_fixed).astype(bool)
+    hp = -np.ones(len(fixed), int)
+    hp[~fixed] = np.arange(int((~fixed).sum()))
+    Np = int((~fixed).sum())
+    nt = (6 * Np + 15) // 16
+    if nt == 0:
+        return 0.0
+    T = np.eye(nt, dtype=bool)
+    obs = {}
+    for pt, po in zip(np.asarray(prob.edge_point), np.asarray(prob.edge_pose)):
+        if hp[po] >= 0:
+            obs.setdefault(int(pt), set()).add(int(hp[po]))
+    blocks = set()
+    for v in obs.values():
+        v = sorted(v)
+        for a in range(len(v)):
+            for b in range(a, len(v)):
+                blocks.add((v[b], v[a]))
+    for i2, i1 in blocks:
+        for r in range(6 * i2 // 16, (6 * i2 + 5) // 16 + 1):
+            for c in range(6 * i1 // 16, (6 * i1 + 5) // 16 + 1):
+                T[max(r, c), min(r, c)] = True
+    tile = 2.0 * 16 ** 3
+    fl = 0.0
+    for c in range(nt):
+        rows = [r for r in range(c + 1, nt) if T[r, c]]
+        fl += 2 * tile / 3 + len(rows) * tile
+        for a in rows:
+            for b in rows:
+                if b <= a:
+                    T[a, b] = True
+                    fl += tile / 2 if a == b else tile
+    return fl + 4.0 * 256 * int(np.tril(T).sum())
 
 
 def _free_port() -> int:
@@ -949,7 +989,8 @@ def main():
                        "local_points_in_view": float(ntm.mean()),
                        "matches_motion_per_frame": float(nm1.mean()), "matches_local_per_frame": float(nm2.mean()),
                        "parallelism": f"agents{world} (one process per GPU; {B} frame streams per GPU)",
-                       "lanes": NL, "launch": "hip graph per tracking step" if tr.graph is not None else "eager"},
+                       "lanes": NL, "launch": "hip graph per tracking step" if tr.graph is not None else "eager",
+                       "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")},
             "stage_ms_per_step": per_step_ms,
             "roofline": {"bound": "hbm", "kernel": dom, "limiter": limiter, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -979,6 +1020,7 @@ def main():
                           "achieved_fp64_tflops": (fl * mapping.W) / (solve_ms * 1e-3) / 1e12 if solve_ms else None,
                           "fp64_peak_tflops": FP64_PEAK_TFS,
                           "stage_ms_total": {k: v[0] for k, v in lba_stage.items()},
+                          "stage_launches": {k: v[1] for k, v in lba_stage.items()},
                           "exchange_bytes_per_step": int(mapping.exch.send.numel() * world),
                           "exchange": {"bytes_per_rank_block": int(mapping.exch.block_bytes),
                                        "keyframe_records": mapping.n_kf_upd, "mappoint_records": mapping.n_mp_upd,
@@ -989,6 +1031,35 @@ def main():
                                                "deduplicated write-back (32-B KeyFrame, 16-B MapPoint records); "
                                                "gather time = host wall around the collective with the stream "
                                                "synchronised, from the untimed profiling pass"}}
+            # the LocalBundleAdjustment's roofline: its dominant kernel, the tile LDL^T (one workgroup per window,
+            # FP64 MFMA), from the profiled pass's solve-stage events (the first stream group's launches: windows
+            # [0, Q / G) of the batch) and the tile structure of those windows
+            G = 2 if mapping.W >= 4 else 1
+            g0 = mapping.probs[:mapping.W // G]
+            fl_ldlt = [ldlt_tile_flops(p) for p in g0]
+            ms_solve, n_solve = lba_stage["solve"]
+            tr_mean = float(np.mean(trials[:len(g0)]))
+            ach = args.steps * tr_mean * sum(fl_ldlt) / (ms_solve * 1e-3) / 1e12 if ms_solve else None
+            mpath = os.path.join(ROOT, "profiles", "r03", "lba_mfma_f64.json")
+            mfma = None
+            if os.path.exists(mpath):
+                try:
+                    mj = json.load(open(mpath))
+                    mfma = {k: v for k, v in mj.items() if "k_ldlt" in k}
+                except Exception:
+                    mfma = None
+            out["roofline_lba"] = {
+                "bound": "mfma", "kernel": "k_ldlt_tiles", "unit": "TFLOP/s", "achieved": ach,
+                "peak": FP64_PEAK_TFS, "frac": ach / FP64_PEAK_TFS if ach else None,
+                "frac_of_cus_used": ach / (FP64_PEAK_TFS * len(g0) / 256.0) if ach else None,
+                "flop_per_factorization": float(np.mean(fl_ldlt)), "windows_per_launch": len(g0),
+                "avg_launch_ms": ms_solve / max(n_solve, 1), "launches": n_solve,
+                "mfma_counters": mfma, "mfma_counters_file": "profiles/r03/lba_mfma_f64.json" if mfma else None,
+                "limiter": ("latency: one workgroup per window factors a 19-panel chain; per panel the diagonal "
+                            "tile's 16-step LDL^T + inverse runs on one wave (DPP-broadcast FP64 FMAs, ~6k cycles) "
+                            "between two barriers, the MFMA tile products beside it"),
+                "note": "algorithmic = tile-skipping LDL^T + solves (ldlt_tile_flops); frac_of_cus_used prices "
+                        "against the FP64 MFMA peak of the CUs the launch's workgroups occupy (one per window)"}
         if newmp is not None:
             nmv = newmp.nmatch.cpu().numpy()
             tri_b = newmp.algorithmic_bytes()

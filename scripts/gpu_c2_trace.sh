@@ -7,6 +7,7 @@ O=$R/gpurun_out
 T=${1:-c2t}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
+export GPU_MAX_HW_QUEUES=16   # what bench.py sets for itself; under rocprofv3 the profiler initialises HIP first
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$T -o run -- python3 $R/bench.py ${BENCH_ARGS:---no-cpu-baseline --steps 8 --warmup 2 --no-latency --no-pose --no-sin} > $O/prof_$T.log 2>&1 || { tail -20 $O/prof_$T.log; exit 1; }
 python3 - $O/prof_$T/run_kernel_stats.csv <<'PY'
 import csv, sys

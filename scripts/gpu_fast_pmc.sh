@@ -8,6 +8,7 @@ T=${1:-fast}
 CFG=${2:-c1}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
+export GPU_MAX_HW_QUEUES=16   # what bench.py sets for itself; under rocprofv3 the profiler initialises HIP first
 A="--config $CFG --no-cpu-baseline --lanes 1 --batch 64 --no-latency --no-pose --no-sin --steps 4 --warmup 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$T -o run -- python3 $R/bench.py $A > $O/prof_$T.log 2>&1 || { tail -5 $O/prof_$T.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/pmcf_$T -o run -- python3 $R/bench.py $A > $O/pmcf_$T.log 2>&1 || { tail -5 $O/pmcf_$T.log; exit 1; }

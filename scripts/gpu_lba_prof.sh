@@ -10,6 +10,7 @@ cd $R
 timeout -k 10 300 python scripts/lba_bench.py --world --batch 32 --solves 6 > $O/${T}_bench.json 2> $O/${T}_bench.err || { tail -20 $O/${T}_bench.err; exit 1; }
 cat $O/${T}_bench.json
 cd /tmp && export TMPDIR=/tmp
+export GPU_MAX_HW_QUEUES=16   # what bench.py sets for itself; under rocprofv3 the profiler initialises HIP first
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$T -o run -- python3 $R/scripts/lba_bench.py --world --batch 32 --solves 4 > $O/prof_$T.log 2>&1 || { tail -20 $O/prof_$T.log; exit 1; }
 python3 - $O/prof_$T/run_kernel_stats.csv <<'PY'
 import csv, sys

@@ -1,5 +1,7 @@
 """Golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py from the CPU oracle on seeded inputs,
-stored together with the inputs).
+stored together with the inputs). They are SELF-GENERATED (the reference ships no fixtures and cannot be built
+here): they pin the oracle against regressions, not against the reference. The LBA oracle is cross-checked
+independently by tests/test_lba_dense_xcheck.py (a dense numpy restatement).
 
 CPU: the oracle still reproduces every fixture exactly (pins the restatement against regressions).
 GPU: the HIP path reproduces them — bit-exact keypoints / descriptors / match indices, LBA within 1e-4.
