@@ -4,8 +4,9 @@
  * Frame::mvpMapPoints / vMatchedPairs, same return values. The matcher is a cheap value object like the
  * reference's (constructed on the stack at each call site); device state lives in one per-thread context.
  *
- * Scope: mono agents with the Pinhole camera. bMono=false (stereo motion search) and bOnlyStereo=true are not
- * on this path and throw std::invalid_argument / return 0 respectively.
+ * Scope: mono agents, Pinhole or KannalaBrandt8 camera (the frame's / keyframe's mpCamera; the KB8 epipolar test and
+ * two-view triangulation of SearchForTriangulation included). bMono=false (stereo motion search) and
+ * bOnlyStereo=true are not on this path and throw std::invalid_argument / return 0 respectively.
  */
 #ifndef MAM3SLAM_ORBMATCHER_H
 #define MAM3SLAM_ORBMATCHER_H

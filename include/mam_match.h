@@ -91,7 +91,7 @@ typedef struct mam_pose {
 /* Cameras: mam_camera (mam_camera.h) — Pinhole or KannalaBrandt8; mam_pinhole is its round-1 name. Every
  * projection below goes through the camera's project (Pinhole.cpp:35-41 / KannalaBrandt8.cpp:67-84). */
 
-/* Last-frame entry for SearchByProjection(Cur, Last) (ORBmatcher.cc:1695-1712). 48 bytes. */
+/* Last-frame entry for SearchByProjection(Cur, Last) (ORBmatcher.cc:1695-1712). 64 bytes. */
 typedef struct mam_last_entry {
     float pos[3];             /* pMP->GetWorldPos() */
     float angle;              /* LastFrame.mvKeysUn[i].angle */
