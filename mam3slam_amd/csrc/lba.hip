@@ -100,6 +100,7 @@ struct Prob {
     double* err;                 // [E][2]
     double* jac;                 // [E][21]: A(6) B(12) orr(2) wo(1)
     double* part;                // [E / 64 + 1] rho0 partial sums of k_plin's point chunks (trial, initial)
+    double* part_s;              // [E / 64 + 1] the trial points' computeScale partial sums per chunk (k_plin)
     double* part0;               // the same of k_plin(iteration start), read by k_ctl_end's iteration-start step
     double* hpl;                 // [E][18] H_pl pose x landmark
     double* bdinv;               // [E][18] H_pl D^-1
@@ -204,19 +205,14 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     const double e0 = d.edge_obs[2 * e] - u, e1 = d.edge_obs[2 * e + 1] - v;
     d.err[2 * e] = e0;
     d.err[2 * e + 1] = e1;
-    if (d.active && !d.active[e]) {
-        // setLevel(1): outside initializeOptimization(0), no term in chi2 / H / b (zeros add exactly nothing)
-        if (want_jac) {
-            for (int k = 0; k < 21; k++) jo[k] = 0.0;
-            if (ho)
-                for (int k = 0; k < 18; k++) ho[k] = 0.0;
-        }
-        return 0.0;
-    }
+    // setLevel(1): outside initializeOptimization(0), no term in chi2 / H / b — the records are zeroed by selects at
+    // the end (an early return here kept jo in scratch memory)
+    const bool inactive = d.active && !d.active[e];
     const double w = d.edge_w[e];
     const double chi = e0 * (w * e0) + e1 * (w * e1);
     double r0, r1;
     huber(chi, d.delta, &r0, &r1);
+    if (inactive) r0 = 0.0;
     if (!want_jac) return r0;
     const double x = Xc[0], y = Xc[1], z = Xc[2];
     // rotation matrix of T (Eigen toRotationMatrix)
@@ -232,8 +228,10 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
         double P[6];
         cam::project_jac_d(cm, Xc, P);
         const double J[6] = {-P[0], -P[1], -P[2], -P[3], -P[4], -P[5]};
+#pragma unroll
         for (int r = 0; r < 2; r++) {
             const double a0 = J[3 * r], a1 = J[3 * r + 1], a2 = J[3 * r + 2];
+#pragma unroll
             for (int k = 0; k < 3; k++) o[3 * r + k] = a0 * R[k] + a1 * R[3 + k] + a2 * R[6 + k];
             double* B = o + 6 + 6 * r;
             // SE3deriv = [[0,z,-y,1,0,0],[-z,0,x,0,1,0],[y,-x,0,0,0,1]]
@@ -248,6 +246,7 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
         const double fx = c[0], fy = c[1];
         const double J0 = -(fx / z), J2 = -(-fx * x / (z * z)), J4 = -(fy / z), J5 = -(-fy * y / (z * z));
         // A = J R (2x3), J = [[J0, 0, J2], [0, J4, J5]]
+#pragma unroll
         for (int k = 0; k < 3; k++) {
             o[k] = J0 * R[k] + J2 * R[6 + k];
             o[3 + k] = J4 * R[3 + k] + J5 * R[6 + k];
@@ -260,12 +259,17 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     o[19] = -(w * e1) * r1;
     o[20] = r1 * w;
     // H_pl = B^T (rho' Omega) A for edges whose pose is optimised (base_binary_edge.hpp:54-120)
+#pragma unroll
+    for (int k = 0; k < 21; k++) o[k] = inactive ? 0.0 : o[k];
     if (!ho) return r0;   // H_pl not wanted (the caller derives it from jo)
-    if (d.pose_h[ipose] >= 0) {
+    if (!inactive && d.pose_h[ipose] >= 0) {
         const double wo = r1 * w;
+#pragma unroll
         for (int a = 0; a < 6; a++)
+#pragma unroll
             for (int c2 = 0; c2 < 3; c2++) ho[3 * a + c2] = o[6 + a] * wo * o[c2] + o[12 + a] * wo * o[3 + c2];
     } else {
+#pragma unroll
         for (int k = 0; k < 18; k++) ho[k] = 0.0;
     }
     return r0;
@@ -522,11 +526,10 @@ template <int mode>
 __global__ __launch_bounds__(EW) void k_plin(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     LM& lm = *d.lm;
-    if (lm.status || (mode != 2 && lm.done) || (mode == 0 && !lm.need_lin)) return;
+    if (lm.status || (mode != 2 && lm.done)) return;
     const int c = blockIdx.x;
     if (c >= nchunks(d)) return;
-    __shared__ double sj[EW * 21];   // one staging buffer
-    __shared__ int32_t se[EW];
+    __shared__ double sj[EW * 18];   // H_pl staging (trial)
     const int lane = lane_id();
     const int p0 = lower_bound_off(d.pe_off, d.L, EW * c), p1 = lower_bound_off(d.pe_off, d.L, EW * c + EW);
     const int s0 = d.pe_off[p0], s1 = d.pe_off[p1];
@@ -544,145 +547,161 @@ __global__ __launch_bounds__(EW) void k_plin(const Prob* __restrict__ probs) {
     const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
     double rsum = 0.0;
     if constexpr (mode == 1) {
-        // (1) back-substitution over the chunk's slots, 64 per pass
+        // (1) back-substitution over the chunk's slots, 64 per pass: the edge lanes stage their slot's H_pl record
+        // (contiguous 16-byte chunks when the pass's edges are consecutive), pose block and x_p in LDS in parallel, then
+        // each owner lane runs its point's sum over its slots in order from LDS only
+        __shared__ double sxp[EW * 6];
+        __shared__ int32_t shp[EW];
         double cl[3] = {0.0, 0.0, 0.0};
         if (po >= 0)
+#pragma unroll
             for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)po + k];
         for (int ps = s0; ps < s1; ps += EW) {
             const int ne = min(EW, s1 - ps);
             const int e = lane < ne ? d.pe_idx[ps + lane] : -1;
-            se[lane] = e;
+            const int hp = e >= 0 ? d.pose_h[d.edge_pose[e]] : -1;
+            shp[lane] = hp;
+            if (hp >= 0) {
+                const double2* xs = reinterpret_cast<const double2*>(d.x + 6 * (size_t)hp);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const double2 v = xs[k];
+                    sxp[6 * lane + 2 * k] = v.x;
+                    sxp[6 * lane + 2 * k + 1] = v.y;
+                }
+            }
             const int e_first = __shfl(e, 0, 64);
             const bool contig = __all(lane >= ne || e == e_first + lane);
             if (contig) {
                 wave_copy_in(sj, d.hpl + 18 * (size_t)e_first, 18 * ne);
             } else if (e >= 0) {
+                const double2* src = reinterpret_cast<const double2*>(d.hpl + 18 * (size_t)e);
 #pragma unroll
-                for (int k = 0; k < 18; k++) sj[18 * lane + k] = d.hpl[18 * (size_t)e + k];
+                for (int k = 0; k < 9; k++) {
+                    const double2 v = src[k];
+                    sj[18 * lane + 2 * k] = v.x;
+                    sj[18 * lane + 2 * k + 1] = v.y;
+                }
             }
             __syncthreads();
             if (po >= 0 && !lm.fail) {
                 const int a = max(o0, ps), z = min(o1, ps + ne);
                 for (int sl = a; sl < z; sl++) {
-                    const int ee = se[sl - ps];
-                    const int hp = d.pose_h[d.edge_pose[ee]];
-                    if (hp < 0) continue;
+                    if (shp[sl - ps] < 0) continue;
                     const double* B = sj + 18 * (sl - ps);
+                    const double* xp = sxp + 6 * (sl - ps);
+#pragma unroll
                     for (int j = 0; j < 3; j++)
-                        for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * d.x[6 * (size_t)hp + k];
+#pragma unroll
+                        for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * xp[k];
                 }
             }
             __syncthreads();
         }
         const double* pts = d.pt[lm.cur];
         double* pt_out = d.pt[1 - lm.cur];
+        const double lambda = trial_lambda(lm);
+        double ssum = 0.0;   // computeScale over the chunk's points: x_l (lambda x_l + b_l)
         auto update_point = [&](int i, const double* clp) {
             double* xl = d.x + 6 * (size_t)d.Np + 3 * (size_t)i;
+            const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)i;
+            double xv[3];
             if (!lm.fail) {
                 const double* Di = d.Dinv + 9 * (size_t)i;
-                for (int k = 0; k < 3; k++)
-                    xl[k] = Di[3 * k] * clp[0] + Di[3 * k + 1] * clp[1] + Di[3 * k + 2] * clp[2];
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    xv[k] = Di[3 * k] * clp[0] + Di[3 * k + 1] * clp[1] + Di[3 * k + 2] * clp[2];
+                    xl[k] = xv[k];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; k++) xv[k] = xl[k];
             }
-            for (int k = 0; k < 3; k++) pt_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + xl[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                pt_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + xv[k];
+                ssum += xv[k] * (lambda * xv[k] + bl[k]);
+            }
         };
         if (po >= 0) update_point(po, cl);
         // edgeless points of the chunk: x_l = D^-1 b_l
         for (int i = p0 + lane; i < p1; i += EW) {
             if (d.pe_off[i + 1] != d.pe_off[i]) continue;
             double bl[3];
+#pragma unroll
             for (int k = 0; k < 3; k++) bl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)i + k];
             update_point(i, bl);
         }
+        ssum = wave_sum_d(ssum);
+        if (lane == 0) d.part_s[c] = ssum;
         __syncthreads();   // the trial points are visible to the chunk's edge lanes
         // (2) errors at the trial state
         for (int ps = s0; ps < s1; ps += EW) {
             const int ne = min(EW, s1 - ps);
-            double jr[21], hr[18];
-            if (lane < ne) rsum += linearize_edge(d, d.pose[sidx], d.pt[sidx], d.pe_idx[ps + lane], false, jr, hr);
+            if (lane < ne) rsum += linearize_edge(d, d.pose[sidx], d.pt[sidx], d.pe_idx[ps + lane], false, nullptr, nullptr);
         }
     } else {
-        double H[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, bl[3] = {0.0, 0.0, 0.0};
+        // mode 2: the initial chi2 at the current state
         for (int ps = s0; ps < s1; ps += EW) {
             const int ne = min(EW, s1 - ps);
-            const int e = lane < ne ? d.pe_idx[ps + lane] : -1;
-            double jr[21];
-            if (e >= 0) rsum += linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0, jr, nullptr);
-            if constexpr (mode != 0) continue;
-            const int e_first = __shfl(e, 0, 64);
-            const bool contig = __all(lane >= ne || e == e_first + lane);
-            // jac and H_pl records out
-#pragma unroll
-            for (int k = 0; k < 21; k++) sj[21 * lane + k] = jr[k];
-            __syncthreads();
-            if (contig) wave_copy_out(d.jac + 21 * (size_t)e_first, sj, 21 * ne);
-            else if (e >= 0)
-                for (int k = 0; k < 21; k++) d.jac[21 * (size_t)e + k] = sj[21 * lane + k];
-            __syncthreads();
-            {
-                // H_pl = B^T (rho' Omega) A for an edge whose pose is optimised (base_binary_edge.hpp:54-120), else 0
-                const bool opt = e >= 0 && d.pose_h[d.edge_pose[e]] >= 0;
-                const double wo = jr[20];
-#pragma unroll
-                for (int a2 = 0; a2 < 6; a2++)
-#pragma unroll
-                    for (int c2 = 0; c2 < 3; c2++)
-                        sj[18 * lane + 3 * a2 + c2] =
-                            opt ? jr[6 + a2] * wo * jr[c2] + jr[12 + a2] * wo * jr[3 + c2] : 0.0;
-            }
-            __syncthreads();
-            if (contig) wave_copy_out(d.hpl + 18 * (size_t)e_first, sj, 18 * ne);
-            else if (e >= 0)
-                for (int k = 0; k < 18; k++) d.hpl[18 * (size_t)e + k] = sj[18 * lane + k];
-            __syncthreads();
-            // the edge's H_ll / b_l terms (sys_body's expressions), summed by the owner lanes in slot order
-            {
-                double* t = sj + 12 * lane;
-                const double wo = jr[20];
-#pragma unroll
-                for (int a2 = 0; a2 < 3; a2++) {
-                    t[9 + a2] = jr[a2] * jr[18] + jr[3 + a2] * jr[19];
-#pragma unroll
-                    for (int c2 = 0; c2 < 3; c2++) t[3 * a2 + c2] = jr[a2] * wo * jr[c2] + jr[3 + a2] * wo * jr[3 + c2];
-                }
-            }
-            __syncthreads();
-            if (po >= 0) {
-                const int a = max(o0, ps), z = min(o1, ps + ne);
-                for (int sl = a; sl < z; sl++) {
-                    const double* t = sj + 12 * (sl - ps);
-#pragma unroll
-                    for (int k = 0; k < 9; k++) H[k] += t[k];
-#pragma unroll
-                    for (int k = 0; k < 3; k++) bl[k] += t[9 + k];
-                }
-            }
-            __syncthreads();
-        }
-        if constexpr (mode == 0) {
-            double m = 0.0;
-            auto put = [&](int i, const double* Hp, const double* bp) {
-                for (int k = 0; k < 9; k++) d.Hll[9 * (size_t)i + k] = Hp[k];
-                for (int k = 0; k < 3; k++) d.b[6 * (size_t)d.Np + 3 * (size_t)i + k] = bp[k];
-                m = fmax(m, fmax(fmax(fabs(Hp[0]), fabs(Hp[4])), fabs(Hp[8])));
-            };
-            if (po >= 0) put(po, H, bl);
-            const double zero[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-            for (int i = p0 + lane; i < p1; i += EW)
-                if (d.pe_off[i + 1] == d.pe_off[i]) put(i, zero, zero);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
-            if (lane == 0 && m > 0.0) atomicMax(&lm.maxdiag, (unsigned long long)__double_as_longlong(m));
+            if (lane < ne) rsum += linearize_edge(d, d.pose[sidx], d.pt[sidx], d.pe_idx[ps + lane], false, nullptr, nullptr);
         }
     }
     rsum = wave_sum_d(rsum);
-    if (lane == 0) (mode == 0 ? d.part0 : d.part)[c] = rsum;
+    if (lane == 0) d.part[c] = rsum;
 }
 
-// grid (Np, Q) x 64: H_pp, b_p per optimised pose (one wave: lanes own strided edges, 27 register sums, fixed-order
-// wave reduction); the point blocks are k_plin's (mode 0)
+// grid (E / 64 + 1, Q) x 64: the iteration start: one wave per 64 edges (in edge order), every edge linearised at the
+// current state (jac / H_pl records out through one LDS buffer as contiguous 16-byte chunks), the rho0 partial sum
+// per wave (fixed-order butterfly) to part0 (a block past the edges writes 0)
+__global__ __launch_bounds__(EW) void k_lin0(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const LM& lm = *d.lm;
+    if (lm.status || lm.done || !lm.need_lin) return;
+    __shared__ double sj[EW * 21];   // one staging buffer (LDS bounds the resident waves of this one-wave kernel)
+    const int e0 = blockIdx.x * EW;
+    if ((int)blockIdx.x >= nchunks(d)) return;
+    const int lane = lane_id(), e = e0 + lane;
+    double jr[21], hr[18];   // the edge's records in registers, staged through one LDS buffer in turn
+    double r = e < d.E ? linearize_edge(d, d.pose[lm.cur], d.pt[lm.cur], e, true, jr, hr) : 0.0;
+    r = wave_sum_d(r);
+    if (lane == 0) d.part0[blockIdx.x] = r;
+    if (e0 >= d.E) return;
+    const int ne = min(EW, d.E - e0);
+#pragma unroll
+    for (int k = 0; k < 21; k++) sj[21 * lane + k] = jr[k];
+    __syncthreads();
+    wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 18; k++) sj[18 * lane + k] = hr[k];
+    __syncthreads();
+    wave_copy_out(d.hpl + 18 * (size_t)e0, sj, 18 * ne);
+}
+
+
+// grid (ceil(L/64) + Np, Q) x 64: H_ll, b_l per point (edge order, one thread each) and H_pp, b_p per optimised pose
+// (one wave: lanes own strided edges, 27 register sums, fixed-order wave reduction)
 // returns this thread's max |diag| of the blocks it wrote (0 for none; fmax drops NaN as the reference's max does)
 __device__ double sys_body(const Prob& d) {
-    const int h = blockIdx.x, lane = threadIdx.x;
+    const int nb_pts = (d.L + 63) / 64;
+    if ((int)blockIdx.x < nb_pts) {
+        const int h = blockIdx.x * 64 + threadIdx.x;
+        if (h >= d.L) return 0.0;
+        double H[9] = {0}, bl[3] = {0};
+        for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
+            const double* j = d.jac + 21 * (size_t)d.pe_idx[s];
+            const double wo = j[20];
+            for (int a = 0; a < 3; a++) {
+                bl[a] += j[a] * j[18] + j[3 + a] * j[19];
+                for (int c = 0; c < 3; c++) H[3 * a + c] += j[a] * wo * j[c] + j[3 + a] * wo * j[3 + c];
+            }
+        }
+        for (int k = 0; k < 9; k++) d.Hll[9 * (size_t)h + k] = H[k];
+        for (int k = 0; k < 3; k++) d.b[6 * (size_t)d.Np + 3 * (size_t)h + k] = bl[k];
+        return fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
+    }
+    const int h = blockIdx.x - nb_pts, lane = threadIdx.x;
     if (h >= d.Np) return 0.0;
     double acc[27];
 #pragma unroll
@@ -789,7 +808,7 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
 }
 
 
-// grid (Np, Q) x 64: the pose blocks of the system (sys_body) and their max |diag(H)| (one device atomic per wave)
+// grid (ceil(L/64) + Np, Q) x 64: the system (sys_body) and max |diag(H)| (one device atomic per wave)
 __global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     LM& lm = *d.lm;
@@ -1984,13 +2003,15 @@ __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs)
     const double lambda = trial_lambda(lm);
     const double chi0 = (begin && lm.its == 0) ? chi_of_parts<T>(d, d.part0, s) : 0.0;
     double tempChi = chi_of_parts<T>(d, d.part, s);
-    // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194), strided + tree
+    // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194): the pose entries strided
+    // here, the points' per-chunk partials from k_plin(trial), then the tree
     double acc[RED / T];
-    const int nx = 6 * d.Np + 3 * d.L;
+    const int np6 = 6 * d.Np, nch = nchunks(d);
 #pragma unroll
     for (int v = 0; v < RED / T; v++) {
         acc[v] = 0.0;
-        for (int j = threadIdx.x + T * v; j < nx; j += RED) acc[v] += d.x[j] * (lambda * d.x[j] + d.b[j]);
+        for (int j = threadIdx.x + T * v; j < np6; j += RED) acc[v] += d.x[j] * (lambda * d.x[j] + d.b[j]);
+        for (int j = threadIdx.x + T * v; j < nch; j += RED) acc[v] += d.part_s[j];
     }
     const double scale0 = block_sum<T>(acc, s);
     if (threadIdx.x != 0) return;
@@ -2102,7 +2123,7 @@ size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
            al((size_t)(npad / 16) * (npad / 16)) + al(2 * (size_t)(npad / 16) * (npad / 16)) +
            al(2 * (size_t)(npad / 16) * (npad / 16 + 1)) +
            2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
-           2 * al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
+           3 * al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
            al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
            al(8 * (size_t)npad * npad) + al(8 * nx) + al(8 * (size_t)npad) +
            al(8 * mam::lba::ldlt_ws_doubles(npad)) + al((size_t)E);
@@ -2132,6 +2153,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.jac = cv.take<double>(21 * (size_t)d.E);
     d.part = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
     d.part0 = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
+    d.part_s = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
     d.hpl = cv.take<double>(18 * (size_t)d.E);
     d.bdinv = cv.take<double>(18 * (size_t)d.E);
     d.coef = cv.take<double>(6 * (size_t)d.E);
@@ -2305,7 +2327,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_plin<2>, gCh, dim3(EW), 0, s, P);
         hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
     }
-    const dim3 gSys(maxNp > 0 ? maxNp : 1, Q);
+    const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
     const dim3 gPrep((std::max(maxE, maxL) + EW - 1) / EW > 0 ? (std::max(maxE, maxL) + EW - 1) / EW : 1, Q);
     const dim3 gBlk(maxNp * (maxNp + 1) / 2 + maxNp > 0 ? maxNp * (maxNp + 1) / 2 + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
@@ -2342,7 +2364,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
-            hipLaunchKernelGGL(k_plin<0>, gChg, dim3(EW), 0, st, Pg);
+            hipLaunchKernelGGL(k_lin0, gChg, dim3(EW), 0, st, Pg);
             hipLaunchKernelGGL(k_sys, gSysg, dim3(64), 0, st, Pg);
         }
         {
