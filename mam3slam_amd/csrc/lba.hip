@@ -3,22 +3,20 @@
 //
 // g2o semantics (BlockSolver_6_3 + LinearSolverEigen + OptimizationAlgorithmLevenberg, FP64) re-laid out for the
 // GPU; every reduction has a fixed order so results are run-to-run reproducible:
-//   k_plin        per point chunk (the edge slots in point order cut at point boundaries, one wave): mode 0
-//                 linearises every edge — map, error, chi2, Huber rho, Jacobians (OptimizableTypes.cpp:139-160), the
-//                 robust-weighted terms constructQuadraticForm needs (base_binary_edge.hpp:75-112) — and sums the point
-//                 blocks H_ll, b_l; mode 1 back-substitutes x_l = D^-1 (b_l - H_pl^T x_p) (block_solver.hpp:461-482)
-//                 into the trial points and takes every edge's error at the trial state; chi2 partial sums per chunk
-//   k_sys         one wave per non-fixed pose: H_pp, b_p
+//   k_linearize   per edge: map, error, chi2, Huber rho, Jacobians (OptimizableTypes.cpp:139-160), the robust-
+//                 weighted terms constructQuadraticForm needs (base_binary_edge.hpp:75-112); chi2 partial sums
+//   k_sys         per point: H_ll, b_l over its edge segment; one wave per non-fixed pose: H_pp, b_p
 //   k_schur_prep  per point: D = H_ll + lambda I, D^-1, and per edge H_pl D^-1, H_pl D^-1 b_l (block_solver.hpp:
 //                 405-427)
 //   k_schur_blk   one wave per 6x6 block (i1 <= i2) of the reduced camera system, contributions in landmark
 //                 order (block_solver.hpp:372-439), and b_s = b_p - sum of coefficients
 //   k_ldlt        one workgroup per problem: blocked right-looking LDL^T of S (zero pivot = failure, as
-//                 SimplicialLDLT), f64 MFMA trailing updates, fused forward / diagonal / backward substitution; its
-//                 epilogue writes the trial poses T <- exp(dx) T (se3quat.h)
+//                 SimplicialLDLT), f64 MFMA trailing updates, fused forward / diagonal / backward substitution
+//   k_backsub_update  x_l = D^-1 (b_l - H_pl^T x_p) (block_solver.hpp:461-482) and the trial state:
+//                 T <- exp(dx) T (se3quat.h), X <- X + dx
 //   k_ctl_end     on an iteration's first trial the iteration-start state first (levenberg.cpp:61-77, 171-185:
-//                 chi2, lambda_0 = 1e-5 max diag(H) gathered by k_plin / k_sys — the trial's kernels read lambda_0
-//                 through trial_lambda); then the trial's chi2, computeScale, rho, accept (discardTop) /
+//                 chi2, lambda_0 = 1e-5 max diag(H) gathered by k_sys — the trial's kernels read lambda_0 through
+//                 trial_lambda); then the trial's chi2, computeScale (partial sums from k_linearize), rho, accept (discardTop) /
 //                 reject (pop), lambda update and the termination tests of levenberg.cpp:78-169 and
 //                 sparse_optimizer.cpp:355-420
 // Each kernel reads its problem's LM state (struct LM, device memory) and returns at once when the state says the
@@ -99,9 +97,9 @@ struct Prob {
     // per edge
     double* err;                 // [E][2]
     double* jac;                 // [E][21]: A(6) B(12) orr(2) wo(1)
-    double* part;                // [E / 64 + 1] rho0 partial sums of k_plin's point chunks (trial, initial)
-    double* part_s;              // [E / 64 + 1] the trial points' computeScale partial sums per chunk (k_plin)
-    double* part0;               // the same of k_plin(iteration start), read by k_ctl_end's iteration-start step
+    double* part_s;              // [ceil(E / 64) + 1] computeScale partial sums of k_linearize(trial)'s blocks
+    double* part;                // [ceil(E / 256)] rho0 partial sums of k_linearize's blocks (trial, initial)
+    double* part0;               // the same of k_linearize(iteration start), read by k_ctl_end's iteration-start step
     double* hpl;                 // [E][18] H_pl pose x landmark
     double* bdinv;               // [E][18] H_pl D^-1
     double* coef;                // [E][6]  H_pl D^-1 b_l
@@ -205,14 +203,18 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     const double e0 = d.edge_obs[2 * e] - u, e1 = d.edge_obs[2 * e + 1] - v;
     d.err[2 * e] = e0;
     d.err[2 * e + 1] = e1;
-    // setLevel(1): outside initializeOptimization(0), no term in chi2 / H / b — the records are zeroed by selects at
-    // the end (an early return here kept jo in scratch memory)
-    const bool inactive = d.active && !d.active[e];
+    if (d.active && !d.active[e]) {
+        // setLevel(1): outside initializeOptimization(0), no term in chi2 / H / b (zeros add exactly nothing)
+        if (want_jac) {
+            for (int k = 0; k < 21; k++) jo[k] = 0.0;
+            for (int k = 0; k < 18; k++) ho[k] = 0.0;
+        }
+        return 0.0;
+    }
     const double w = d.edge_w[e];
     const double chi = e0 * (w * e0) + e1 * (w * e1);
     double r0, r1;
     huber(chi, d.delta, &r0, &r1);
-    if (inactive) r0 = 0.0;
     if (!want_jac) return r0;
     const double x = Xc[0], y = Xc[1], z = Xc[2];
     // rotation matrix of T (Eigen toRotationMatrix)
@@ -228,10 +230,8 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
         double P[6];
         cam::project_jac_d(cm, Xc, P);
         const double J[6] = {-P[0], -P[1], -P[2], -P[3], -P[4], -P[5]};
-#pragma unroll
         for (int r = 0; r < 2; r++) {
             const double a0 = J[3 * r], a1 = J[3 * r + 1], a2 = J[3 * r + 2];
-#pragma unroll
             for (int k = 0; k < 3; k++) o[3 * r + k] = a0 * R[k] + a1 * R[3 + k] + a2 * R[6 + k];
             double* B = o + 6 + 6 * r;
             // SE3deriv = [[0,z,-y,1,0,0],[-z,0,x,0,1,0],[y,-x,0,0,0,1]]
@@ -246,7 +246,6 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
         const double fx = c[0], fy = c[1];
         const double J0 = -(fx / z), J2 = -(-fx * x / (z * z)), J4 = -(fy / z), J5 = -(-fy * y / (z * z));
         // A = J R (2x3), J = [[J0, 0, J2], [0, J4, J5]]
-#pragma unroll
         for (int k = 0; k < 3; k++) {
             o[k] = J0 * R[k] + J2 * R[6 + k];
             o[3 + k] = J4 * R[3 + k] + J5 * R[6 + k];
@@ -259,17 +258,11 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
     o[19] = -(w * e1) * r1;
     o[20] = r1 * w;
     // H_pl = B^T (rho' Omega) A for edges whose pose is optimised (base_binary_edge.hpp:54-120)
-#pragma unroll
-    for (int k = 0; k < 21; k++) o[k] = inactive ? 0.0 : o[k];
-    if (!ho) return r0;   // H_pl not wanted (the caller derives it from jo)
-    if (!inactive && d.pose_h[ipose] >= 0) {
+    if (d.pose_h[ipose] >= 0) {
         const double wo = r1 * w;
-#pragma unroll
         for (int a = 0; a < 6; a++)
-#pragma unroll
             for (int c2 = 0; c2 < 3; c2++) ho[3 * a + c2] = o[6 + a] * wo * o[c2] + o[12 + a] * wo * o[3 + c2];
     } else {
-#pragma unroll
         for (int k = 0; k < 18; k++) ho[k] = 0.0;
     }
     return r0;
@@ -498,187 +491,48 @@ __device__ __forceinline__ double trial_lambda(const LM& lm) {
     return (lm.need_lin && lm.its == 0) ? 1e-5 * __longlong_as_double((long long)lm.maxdiag) : lm.lambda;
 }
 
-// ---- point chunks: the edge slots in point order (pe_idx, per point in edge order) cut at point boundaries. Chunk c
-// holds the points whose first slot lies in [64 c, 64 c + 64) (every point with edges belongs to exactly one chunk,
-// and its owner lane there is that offset), plus the edgeless points whose pe_off falls in the range; its slots are
-// [pe_off[p0], pe_off[p1]), at most 64 + (max edges of a point) - 1, worked in passes of 64. E / 64 + 1 chunks.
-__device__ __forceinline__ int nchunks(const Prob& d) { return d.E / EW + 1; }
-__device__ __forceinline__ int lower_bound_off(const int32_t* off, int n, int v) {   // first p in [0, n] with off[p] >= v
-    int lo = 0, hi = n + 1;
-    while (lo < hi) {
-        const int m = (lo + hi) >> 1;
-        if (off[m] >= v) hi = m;
-        else lo = m + 1;
-    }
-    return lo > n ? n : lo;
-}
-
-// grid (E / 64 + 1, Q) x 64: one wave per point chunk. The chunk's rho0 sum (its edges in slot order, fixed-order
-// butterfly per pass) goes to part0 (mode 0) / part (modes 1, 2).
-//   mode 2: the initial chi2 (current state).
-//   mode 0: iteration start: every edge linearised (jac / H_pl records out, through LDS as contiguous 16-byte chunks
-//           when the pass's edges are consecutive — point-major inputs — else per lane), and the point blocks H_ll,
-//           b_l (sys_body's per-edge terms, summed by the point's owner lane over its slots in order) + max |diag|.
-//   mode 1: trial: the back-substitution x_l = D^-1 (b_l - sum H_pl^T x_p) (block_solver.hpp:461-482) by the owner
-//           lanes over their slots in order (H_pl staged in LDS), X + x_l written to the trial state, then every
-//           edge's error at the trial state (the poses: updated by the factorization's epilogue, pose_trial_update).
-template <int mode>
-__global__ __launch_bounds__(EW) void k_plin(const Prob* __restrict__ probs) {
-    const Prob& d = probs[blockIdx.y];
-    LM& lm = *d.lm;
-    if (lm.status || (mode != 2 && lm.done)) return;
-    const int c = blockIdx.x;
-    if (c >= nchunks(d)) return;
-    __shared__ double sj[EW * 18];   // H_pl staging (trial)
-    const int lane = lane_id();
-    const int p0 = lower_bound_off(d.pe_off, d.L, EW * c), p1 = lower_bound_off(d.pe_off, d.L, EW * c + EW);
-    const int s0 = d.pe_off[p0], s1 = d.pe_off[p1];
-    // the owner lane's point: the point whose first slot is 64 c + lane (none when that slot starts no point)
-    int po = -1;
-    {
-        const int sl = EW * c + lane;
-        if (sl < d.E) {
-            // the last point with pe_off == sl (edgeless points before it share that offset)
-            const int q = lower_bound_off(d.pe_off, d.L, sl + 1) - 1;
-            if (q >= 0 && q < d.L && d.pe_off[q] == sl && d.pe_off[q + 1] > sl) po = q;
-        }
-    }
-    const int o0 = po >= 0 ? d.pe_off[po] : 0, o1 = po >= 0 ? d.pe_off[po + 1] : 0;
-    const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
-    double rsum = 0.0;
-    if constexpr (mode == 1) {
-        // (1) back-substitution over the chunk's slots, 64 per pass: the edge lanes stage their slot's H_pl record
-        // (contiguous 16-byte chunks when the pass's edges are consecutive), pose block and x_p in LDS in parallel, then
-        // each owner lane runs its point's sum over its slots in order from LDS only
-        __shared__ double sxp[EW * 6];
-        __shared__ int32_t shp[EW];
-        double cl[3] = {0.0, 0.0, 0.0};
-        if (po >= 0)
-#pragma unroll
-            for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)po + k];
-        for (int ps = s0; ps < s1; ps += EW) {
-            const int ne = min(EW, s1 - ps);
-            const int e = lane < ne ? d.pe_idx[ps + lane] : -1;
-            const int hp = e >= 0 ? d.pose_h[d.edge_pose[e]] : -1;
-            shp[lane] = hp;
-            if (hp >= 0) {
-                const double2* xs = reinterpret_cast<const double2*>(d.x + 6 * (size_t)hp);
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    const double2 v = xs[k];
-                    sxp[6 * lane + 2 * k] = v.x;
-                    sxp[6 * lane + 2 * k + 1] = v.y;
-                }
-            }
-            const int e_first = __shfl(e, 0, 64);
-            const bool contig = __all(lane >= ne || e == e_first + lane);
-            if (contig) {
-                wave_copy_in(sj, d.hpl + 18 * (size_t)e_first, 18 * ne);
-            } else if (e >= 0) {
-                const double2* src = reinterpret_cast<const double2*>(d.hpl + 18 * (size_t)e);
-#pragma unroll
-                for (int k = 0; k < 9; k++) {
-                    const double2 v = src[k];
-                    sj[18 * lane + 2 * k] = v.x;
-                    sj[18 * lane + 2 * k + 1] = v.y;
-                }
-            }
-            __syncthreads();
-            if (po >= 0 && !lm.fail) {
-                const int a = max(o0, ps), z = min(o1, ps + ne);
-                for (int sl = a; sl < z; sl++) {
-                    if (shp[sl - ps] < 0) continue;
-                    const double* B = sj + 18 * (sl - ps);
-                    const double* xp = sxp + 6 * (sl - ps);
-#pragma unroll
-                    for (int j = 0; j < 3; j++)
-#pragma unroll
-                        for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * xp[k];
-                }
-            }
-            __syncthreads();
-        }
-        const double* pts = d.pt[lm.cur];
-        double* pt_out = d.pt[1 - lm.cur];
-        const double lambda = trial_lambda(lm);
-        double ssum = 0.0;   // computeScale over the chunk's points: x_l (lambda x_l + b_l)
-        auto update_point = [&](int i, const double* clp) {
-            double* xl = d.x + 6 * (size_t)d.Np + 3 * (size_t)i;
-            const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)i;
-            double xv[3];
-            if (!lm.fail) {
-                const double* Di = d.Dinv + 9 * (size_t)i;
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    xv[k] = Di[3 * k] * clp[0] + Di[3 * k + 1] * clp[1] + Di[3 * k + 2] * clp[2];
-                    xl[k] = xv[k];
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 3; k++) xv[k] = xl[k];
-            }
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                pt_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + xv[k];
-                ssum += xv[k] * (lambda * xv[k] + bl[k]);
-            }
-        };
-        if (po >= 0) update_point(po, cl);
-        // edgeless points of the chunk: x_l = D^-1 b_l
-        for (int i = p0 + lane; i < p1; i += EW) {
-            if (d.pe_off[i + 1] != d.pe_off[i]) continue;
-            double bl[3];
-#pragma unroll
-            for (int k = 0; k < 3; k++) bl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)i + k];
-            update_point(i, bl);
-        }
-        ssum = wave_sum_d(ssum);
-        if (lane == 0) d.part_s[c] = ssum;
-        __syncthreads();   // the trial points are visible to the chunk's edge lanes
-        // (2) errors at the trial state
-        for (int ps = s0; ps < s1; ps += EW) {
-            const int ne = min(EW, s1 - ps);
-            if (lane < ne) rsum += linearize_edge(d, d.pose[sidx], d.pt[sidx], d.pe_idx[ps + lane], false, nullptr, nullptr);
-        }
-    } else {
-        // mode 2: the initial chi2 at the current state
-        for (int ps = s0; ps < s1; ps += EW) {
-            const int ne = min(EW, s1 - ps);
-            if (lane < ne) rsum += linearize_edge(d, d.pose[sidx], d.pt[sidx], d.pe_idx[ps + lane], false, nullptr, nullptr);
-        }
-    }
-    rsum = wave_sum_d(rsum);
-    if (lane == 0) d.part[c] = rsum;
-}
-
-// grid (E / 64 + 1, Q) x 64: the iteration start: one wave per 64 edges (in edge order), every edge linearised at the
-// current state (jac / H_pl records out through one LDS buffer as contiguous 16-byte chunks), the rho0 partial sum
-// per wave (fixed-order butterfly) to part0 (a block past the edges writes 0)
-__global__ __launch_bounds__(EW) void k_lin0(const Prob* __restrict__ probs) {
+// grid (ceil(E/64), Q) x 64: one wave per 64 edges; the rho0 partial sum per wave (fixed-order butterfly).
+// mode 0: iteration start (Jacobians, current state); 1: trial (errors only, trial state) and the computeScale
+// partial sums; 2: initial chi2.
+__global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs, int mode) {
     const Prob& d = probs[blockIdx.y];
     const LM& lm = *d.lm;
-    if (lm.status || lm.done || !lm.need_lin) return;
+    if (lm.status || (mode != 2 && lm.done) || (mode == 0 && !lm.need_lin)) return;
     __shared__ double sj[EW * 21];   // one staging buffer (LDS bounds the resident waves of this one-wave kernel)
     const int e0 = blockIdx.x * EW;
-    if ((int)blockIdx.x >= nchunks(d)) return;
-    const int lane = lane_id(), e = e0 + lane;
-    double jr[21], hr[18];   // the edge's records in registers, staged through one LDS buffer in turn
-    double r = e < d.E ? linearize_edge(d, d.pose[lm.cur], d.pt[lm.cur], e, true, jr, hr) : 0.0;
-    r = wave_sum_d(r);
-    if (lane == 0) d.part0[blockIdx.x] = r;
-    if (e0 >= d.E) return;
-    const int ne = min(EW, d.E - e0);
+    if (e0 < d.E) {
+        const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
+        const int lane = lane_id(), e = e0 + lane;
+        double jr[21], hr[18];   // the edge's records in registers, staged through one LDS buffer in turn
+        double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0, jr, hr) : 0.0;
+        r = wave_sum_d(r);
+        if (lane == 0) (mode == 0 ? d.part0 : d.part)[blockIdx.x] = r;
+        if (mode == 0) {
+            const int ne = min(EW, d.E - e0);
 #pragma unroll
-    for (int k = 0; k < 21; k++) sj[21 * lane + k] = jr[k];
-    __syncthreads();
-    wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
-    __syncthreads();
+            for (int k = 0; k < 21; k++) sj[21 * lane + k] = jr[k];
+            __syncthreads();
+            wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
+            __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 18; k++) sj[18 * lane + k] = hr[k];
-    __syncthreads();
-    wave_copy_out(d.hpl + 18 * (size_t)e0, sj, 18 * ne);
+            for (int k = 0; k < 18; k++) sj[18 * lane + k] = hr[k];
+            __syncthreads();
+            wave_copy_out(d.hpl + 18 * (size_t)e0, sj, 18 * ne);
+        }
+    }
+    if (mode == 1) {
+        // computeScale partials: block b < nbl sums x_j (lambda x_j + b_j) over the 64-chunks b, b + nbl, ... of x
+        const int nbl = max(1, (d.E + EW - 1) / EW);
+        if ((int)blockIdx.x < nbl) {
+            const double lambda = trial_lambda(lm);
+            const int nx = 6 * d.Np + 3 * d.L;
+            double acc = 0.0;
+            for (int j = blockIdx.x * EW + lane_id(); j < nx; j += nbl * EW) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
+            acc = wave_sum_d(acc);
+            if (lane_id() == 0) d.part_s[blockIdx.x] = acc;
+        }
+    }
 }
-
 
 // grid (ceil(L/64) + Np, Q) x 64: H_ll, b_l per point (edge order, one thread each) and H_pp, b_p per optimised pose
 // (one wave: lanes own strided edges, 27 register sums, fixed-order wave reduction)
@@ -771,10 +625,9 @@ __device__ double block_sum(const double* acc, double* s) {
 
 template <int T>
 __device__ double chi_of_parts(const Prob& d, const double* part, double* s) {
-    // the point chunks' parts, grouped by four as ((p0 + p1) + p2) + p3 (a missing part adds nothing), then
-    // strided + tree
+    // parts of 64 edges, grouped by 256 as ((p0 + p1) + p2) + p3 (a missing part adds nothing), then strided + tree
     double acc[RED / T];
-    const int np = nchunks(d), nb = (np + 3) / 4;
+    const int np = (d.E + EW - 1) / EW, nb = (d.E + 255) / 256;
 #pragma unroll
     for (int v = 0; v < RED / T; v++) {
         acc[v] = 0.0;
@@ -1860,6 +1713,36 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
 #endif
 }
 
+// grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
+// largest pool + y of the batch)
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_tiles(const Prob* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done || !lm.tiles_lds) return;
+    if (d.Np == 0) {
+        if (threadIdx.x == 0) lm.fail = 0;
+        return;
+    }
+    ldlt_tiles(d, lds_dyn, sh);
+}
+
+// grid (Q) x LDLT_THREADS: the others, factored in place in HBM (the panel workspace in LDS when use_lds)
+template <bool use_lds>
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done || lm.tiles_lds) return;
+    if (d.Np == 0) {
+        if (threadIdx.x == 0) lm.fail = 0;
+        return;
+    }
+    ldlt_global<use_lds>(d, lds_dyn, sh);
+}
+
 // Eigen Quaterniond(Matrix3d)
 __device__ void rot_to_quat(const double m[9], double q[4]) {
     const double t = m[0] + m[4] + m[8];
@@ -1874,19 +1757,13 @@ __device__ void rot_to_quat(const double m[9], double q[4]) {
         int i = 0;
         if (m[4] > m[0]) i = 1;
         if (m[8] > m[3 * i + i]) i = 2;
-        // the branch per i with compile-time indices (a runtime-indexed q / m lands in scratch memory)
-        auto br = [&](auto I) {
-            constexpr int ii = decltype(I)::value, j = (ii + 1) % 3, k = (j + 1) % 3;
-            double s = sqrt(m[3 * ii + ii] - m[3 * j + j] - m[3 * k + k] + 1.0);
-            q[ii] = 0.5 * s;
-            s = 0.5 / s;
-            q[3] = (m[3 * k + j] - m[3 * j + k]) * s;
-            q[j] = (m[3 * j + ii] + m[3 * ii + j]) * s;
-            q[k] = (m[3 * k + ii] + m[3 * ii + k]) * s;
-        };
-        if (i == 0) br(std::integral_constant<int, 0>());
-        else if (i == 1) br(std::integral_constant<int, 1>());
-        else br(std::integral_constant<int, 2>());
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
+        q[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[3] = (m[3 * k + j] - m[3 * j + k]) * s;
+        q[j] = (m[3 * j + i] + m[3 * i + j]) * s;
+        q[k] = (m[3 * k + i] + m[3 * i + k]) * s;
     }
 }
 
@@ -1896,18 +1773,41 @@ __device__ void normalize_q(double q[4]) {
     q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
 }
 
-// The trial poses T <- exp(dx) T (se3quat.h; VertexSE3Expmap::oplusImpl), fixed poses copied: the factorization
-// kernels' epilogue (every thread of the workgroup strided over the poses, dx from d.x), so the trial kernel (k_plin
-// mode 1) reads them from the previous launch
-__device__ void pose_trial_updates(const Prob& d, const LM& lm) {
+// grid (ceil(max(P, L)/256), Q): x_l = D^-1 (b_l - H_pl^T x_p) per point (skipped after a failed factorization:
+// BlockSolver::solve returns before the back-substitution and the update applies the old x), then the trial state:
+// T <- exp(dx) * T (VertexSE3Expmap::oplusImpl) for optimised poses, X <- X + dx, fixed poses copied.
+__global__ __launch_bounds__(256) void k_backsub_update(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const LM& lm = *d.lm;
+    if (lm.status || lm.done) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
     const double* pose = d.pose[lm.cur];
+    const double* pts = d.pt[lm.cur];
     double* pose_out = d.pose[1 - lm.cur];
-    for (int i = threadIdx.x; i < d.P; i += blockDim.x) {
+    double* pt_out = d.pt[1 - lm.cur];
+    if (i < d.L) {
+        double* xl = d.x + 6 * (size_t)d.Np + 3 * (size_t)i;
+        if (!lm.fail) {
+            double cl[3];
+            for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)i + k];
+            for (int s = d.pe_off[i]; s < d.pe_off[i + 1]; s++) {
+                const int e = d.pe_idx[s];
+                const int hp = d.pose_h[d.edge_pose[e]];
+                if (hp < 0) continue;
+                const double* B = d.hpl + 18 * (size_t)e;
+                for (int j = 0; j < 3; j++)
+                    for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * d.x[6 * (size_t)hp + k];
+            }
+            const double* Di = d.Dinv + 9 * (size_t)i;
+            for (int k = 0; k < 3; k++) xl[k] = Di[3 * k] * cl[0] + Di[3 * k + 1] * cl[1] + Di[3 * k + 2] * cl[2];
+        }
+        for (int k = 0; k < 3; k++) pt_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + xl[k];
+    }
+    if (i < d.P) {
         const double* T = pose + 7 * (size_t)i;
         double* O = pose_out + 7 * (size_t)i;
         const int h = d.pose_h[i];
         if (h < 0) {
-#pragma unroll
             for (int k = 0; k < 7; k++) O[k] = T[k];
         } else {
             const double* u = d.x + 6 * (size_t)h;
@@ -1915,18 +1815,15 @@ __device__ void pose_trial_updates(const Prob& d, const LM& lm) {
             const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
             const double Om[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
             double Om2[9];
-#pragma unroll
             for (int r = 0; r < 3; r++)
                 for (int c = 0; c < 3; c++)
                     Om2[3 * r + c] = Om[3 * r] * Om[c] + Om[3 * r + 1] * Om[3 + c] + Om[3 * r + 2] * Om[6 + c];
             double R[9], V[9];
             if (theta < 0.00001) {
-#pragma unroll
                 for (int k = 0; k < 9; k++) { R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + Om2[k]; V[k] = R[k]; }
             } else {
                 const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
                 const double c = (theta - sin(theta)) / (theta * theta * theta);
-#pragma unroll
                 for (int k = 0; k < 9; k++) {
                     const double I = (k % 4 == 0) ? 1.0 : 0.0;
                     R[k] = I + a * Om[k] + b * Om2[k];
@@ -1936,7 +1833,6 @@ __device__ void pose_trial_updates(const Prob& d, const LM& lm) {
             double qe[4];
             rot_to_quat(R, qe);
             double te[3];
-#pragma unroll
             for (int r = 0; r < 3; r++) te[r] = V[3 * r] * u[3] + V[3 * r + 1] * u[4] + V[3 * r + 2] * u[5];
             normalize_q(qe);
             // exp * T
@@ -1950,44 +1846,9 @@ __device__ void pose_trial_updates(const Prob& d, const LM& lm) {
             normalize_q(q);
             O[0] = q[0]; O[1] = q[1]; O[2] = q[2]; O[3] = q[3];
             O[4] = te[0] + rt[0]; O[5] = te[1] + rt[1]; O[6] = te[2] + rt[2];
-    }
+        }
     }
 }
-
-// grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
-// largest pool + y of the batch)
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_tiles(const Prob* __restrict__ probs) {
-    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-    __shared__ LdltShared sh;
-    const Prob& d = probs[blockIdx.x];
-    LM& lm = *d.lm;
-    if (lm.status || lm.done || !lm.tiles_lds) return;
-    if (d.Np == 0) {
-        if (threadIdx.x == 0) lm.fail = 0;
-    } else {
-        ldlt_tiles(d, lds_dyn, sh);
-        __syncthreads();   // x is written (wave 0's backward substitution)
-    }
-    pose_trial_updates(d, lm);
-}
-
-// grid (Q) x LDLT_THREADS: the others, factored in place in HBM (the panel workspace in LDS when use_lds)
-template <bool use_lds>
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
-    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-    __shared__ LdltShared sh;
-    const Prob& d = probs[blockIdx.x];
-    LM& lm = *d.lm;
-    if (lm.status || lm.done || lm.tiles_lds) return;
-    if (d.Np == 0) {
-        if (threadIdx.x == 0) lm.fail = 0;
-    } else {
-        ldlt_global<use_lds>(d, lds_dyn, sh);
-        __syncthreads();
-    }
-    pose_trial_updates(d, lm);
-}
-
 
 // grid (Q) x 256: end of a trial — levenberg.cpp:108-158 (rho, accept / reject, lambda), then the iteration-end
 // tests of levenberg.cpp:159-168 and sparse_optimizer.cpp:381-409.
@@ -2003,15 +1864,13 @@ __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs)
     const double lambda = trial_lambda(lm);
     const double chi0 = (begin && lm.its == 0) ? chi_of_parts<T>(d, d.part0, s) : 0.0;
     double tempChi = chi_of_parts<T>(d, d.part, s);
-    // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194): the pose entries strided
-    // here, the points' per-chunk partials from k_plin(trial), then the tree
+    // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194)
     double acc[RED / T];
-    const int np6 = 6 * d.Np, nch = nchunks(d);
+    const int nbl = max(1, (d.E + EW - 1) / EW);
 #pragma unroll
     for (int v = 0; v < RED / T; v++) {
         acc[v] = 0.0;
-        for (int j = threadIdx.x + T * v; j < np6; j += RED) acc[v] += d.x[j] * (lambda * d.x[j] + d.b[j]);
-        for (int j = threadIdx.x + T * v; j < nch; j += RED) acc[v] += d.part_s[j];
+        for (int j = threadIdx.x + T * v; j < nbl; j += RED) acc[v] += d.part_s[j];
     }
     const double scale0 = block_sum<T>(acc, s);
     if (threadIdx.x != 0) return;
@@ -2123,7 +1982,7 @@ size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
            al((size_t)(npad / 16) * (npad / 16)) + al(2 * (size_t)(npad / 16) * (npad / 16)) +
            al(2 * (size_t)(npad / 16) * (npad / 16 + 1)) +
            2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
-           3 * al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
+           2 * al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
            al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
            al(8 * (size_t)npad * npad) + al(8 * nx) + al(8 * (size_t)npad) +
            al(8 * mam::lba::ldlt_ws_doubles(npad)) + al((size_t)E);
@@ -2284,7 +2143,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     MAM_HIP(hipMemcpyAsync(outs_buf().p, c->lm_host.p + pb + lb, sizeof(Outs) * Q, hipMemcpyHostToDevice, s));
     const Prob* P = c->probs.p;
     const dim3 gE((maxE + 255) / 256 > 0 ? (maxE + 255) / 256 : 1, Q);
-    const dim3 gCh(maxE / EW + 1, Q);   // point chunks (k_plin)
+    const dim3 gE64((maxE + EW - 1) / EW > 0 ? (maxE + EW - 1) / EW : 1, Q);
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
         hipLaunchKernelGGL(k_struct_init, dim3(8, Q), dim3(SB), 0, s, P);
@@ -2324,13 +2183,14 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
         MAM_HIP(hipMemcpyAsync(c->probs.p, c->lm_host.p, sizeof(Prob) * Q, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_blk_fill, gB, dim3(64), 0, s, P);
-        hipLaunchKernelGGL(k_plin<2>, gCh, dim3(EW), 0, s, P);
+        hipLaunchKernelGGL(k_linearize, gE64, dim3(EW), 0, s, P, 2);
         hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
     }
     const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
     const dim3 gPrep((std::max(maxE, maxL) + EW - 1) / EW > 0 ? (std::max(maxE, maxL) + EW - 1) / EW : 1, Q);
     const dim3 gBlk(maxNp * (maxNp + 1) / 2 + maxNp > 0 ? maxNp * (maxNp + 1) / 2 + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
+    const dim3 gUpd((maxPL + 255) / 256 > 0 ? (maxPL + 255) / 256 : 1, Q);
     // The batch runs as G interleaved groups on G streams: one group's latency-bound factorization (one workgroup
     // per problem) overlaps the other groups' throughput kernels. Every kernel indexes its problems from the Prob
     // pointer it is given, so a group is the sub-array P + first with Q_g problems. MAM_LBA_SPLIT=<G> overrides
@@ -2360,11 +2220,11 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         const int q0 = g * Q / G, q1 = (g + 1) * Q / G, Qg = q1 - q0;
         const Prob* Pg = P + q0;
         hipStream_t st = sg[g];
-        const dim3 gChg(gCh.x, Qg), gSysg(gSys.x, Qg), gPrepg(gPrep.x, Qg), gBlkg(gBlk.x, Qg);
+        const dim3 gE64g(gE64.x, Qg), gSysg(gSys.x, Qg), gPrepg(gPrep.x, Qg), gBlkg(gBlk.x, Qg), gUpdg(gUpd.x, Qg);
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
-            hipLaunchKernelGGL(k_lin0, gChg, dim3(EW), 0, st, Pg);
+            hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 0);
             hipLaunchKernelGGL(k_sys, gSysg, dim3(64), 0, st, Pg);
         }
         {
@@ -2384,7 +2244,8 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
-            hipLaunchKernelGGL(k_plin<1>, gChg, dim3(EW), 0, st, Pg);
+            hipLaunchKernelGGL(k_backsub_update, gUpdg, dim3(256), 0, st, Pg);
+            hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 1);
             hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
     };
