@@ -601,6 +601,10 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
         }
     }
     __syncthreads();
+#if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 16)
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = (int)Sh[tid].x;   // timing only: up to S
+    return;
+#endif
     const int tlo = max(iniTh, 1), thi = max(minTh, 1);
     const int iters = (np + T - 1) / T;
     // (c) NMS peaks + per-(iteration, wave) counts at both thresholds, packed (hi << 16) | lo
@@ -632,6 +636,10 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
         }
     }
     __syncthreads();
+#if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 8)
+    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = cnt[0] & 1;   // timing only: up to NMS
+    return;
+#endif
     // (d) cell totals and this wave's bases: every lane reads the entries (same address: LDS broadcast)
     int tot = 0, mybase_first = 0;
     const int nent = iters * NW;
