@@ -577,7 +577,12 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
     }
     __syncthreads();
 #if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 2)
-    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = (int)hp[tid].x;   // timing only
+    // timing only: the count stays 0 (nothing downstream reads a candidate), the value kept live through the
+    // cell's first candidate slot
+    if (tid == 0) {
+        cand[(size_t)f * g->cand_per_frame + L.cand_base + (size_t)c.slot * L.cellcap] = (uint32_t)(int)hp[tid].x;
+        cell_counts[(size_t)f * g->cells_per_frame + cell_i] = 0;
+    }
     return;
 #endif
     const int pwm = max(pw, 1);
@@ -602,7 +607,10 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
     }
     __syncthreads();
 #if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 16)
-    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = (int)Sh[tid].x;   // timing only: up to S
+    if (tid == 0) {   // timing only: up to S (count 0, the value kept live through the cell's first slot)
+        cand[(size_t)f * g->cand_per_frame + L.cand_base + (size_t)c.slot * L.cellcap] = (uint32_t)(int)Sh[tid].x;
+        cell_counts[(size_t)f * g->cells_per_frame + cell_i] = 0;
+    }
     return;
 #endif
     const int tlo = max(iniTh, 1), thi = max(minTh, 1);
@@ -637,7 +645,10 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
     }
     __syncthreads();
 #if defined(MAM_FAST_EXPERIMENT) && (MAM_FAST_EXPERIMENT & 8)
-    if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = cnt[0] & 1;   // timing only: up to NMS
+    if (tid == 0) {   // timing only: up to NMS + counts (count 0, the value kept live through the cell's first slot)
+        cand[(size_t)f * g->cand_per_frame + L.cand_base + (size_t)c.slot * L.cellcap] = (uint32_t)cnt[0];
+        cell_counts[(size_t)f * g->cells_per_frame + cell_i] = 0;
+    }
     return;
 #endif
     // (d) cell totals and this wave's bases: every lane reads the entries (same address: LDS broadcast)
