@@ -80,6 +80,8 @@ struct Prob {
     int32_t* hpose;              // Hessian pose block -> pose
     int32_t* pe_off;             // per point: edge segment [pe_off[h], pe_off[h+1]) into pe_idx (edge order)
     int32_t* pe_idx;
+    int32_t* slot_hp;            // per slot s of pe_idx: the Hessian pose block of edge pe_idx[s] (-1 fixed)
+    int4* emeta;                 // per edge: (point, Hessian pose block or -1, first edge of its point, 0)
     int32_t* qe_off;             // per Hessian pose: edges (edge order)
     int32_t* qe_idx;
     int32_t* cnt;                // [L + Np] counters / cursors of the device structure build
@@ -425,6 +427,13 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
             while (m >= 0 && s[m] > v) { s[m + 1] = s[m]; m--; }
             s[m + 1] = v;
         }
+        // per slot / per edge metadata the per-trial kernels read with one load instead of a chain of dependent ones
+        for (int a = 0; a < n; a++) {
+            const int e = s[a];
+            const int hp = d.pose_h[d.edge_pose[e]];
+            d.slot_hp[d.pe_off[h] + a] = hp;
+            d.emeta[e] = make_int4(h, hp, a == 0 ? 1 : 0, 0);
+        }
         // the S blocks this landmark contributes to (g2o's BlockSolver keeps only these, block_solver.hpp:181-224)
         for (int a = 0; a < n; a++) {
             const int ha = d.pose_h[d.edge_pose[s[a]]];
@@ -543,7 +552,9 @@ __device__ double sys_body(const Prob& d) {
         const int h = blockIdx.x * 64 + threadIdx.x;
         if (h >= d.L) return 0.0;
         double H[9] = {0}, bl[3] = {0};
-        for (int s = d.pe_off[h]; s < d.pe_off[h + 1]; s++) {
+        const int s1 = d.pe_off[h + 1];
+#pragma unroll 2
+        for (int s = d.pe_off[h]; s < s1; s++) {
             const double* j = d.jac + 21 * (size_t)d.pe_idx[s];
             const double wo = j[20];
             for (int a = 0; a < 3; a++) {
@@ -720,11 +731,12 @@ __global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ prob
 #pragma unroll
     for (int k = 0; k < 6; k++) cf[k] = 0.0;
     if (e < d.E) {
-        if (d.pose_h[d.edge_pose[e]] >= 0 || d.pe_idx[d.pe_off[d.edge_point[e]]] == e) {
-            const int h = d.edge_point[e];
+        const int4 em = d.emeta[e];
+        if (em.y >= 0 || em.z) {
+            const int h = em.x;
             double Di[9];
             point_dinv(d, h, lambda, Di);
-            if (d.pe_idx[d.pe_off[h]] == e)
+            if (em.z)
                 for (int k = 0; k < 9; k++) d.Dinv[9 * (size_t)h + k] = Di[k];
             const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)h;
             double db[3];
@@ -1790,13 +1802,17 @@ __global__ __launch_bounds__(256) void k_backsub_update(const Prob* __restrict__
         if (!lm.fail) {
             double cl[3];
             for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)i + k];
-            for (int s = d.pe_off[i]; s < d.pe_off[i + 1]; s++) {
-                const int e = d.pe_idx[s];
-                const int hp = d.pose_h[d.edge_pose[e]];
+            const int s1 = d.pe_off[i + 1];
+#pragma unroll 2
+            for (int s = d.pe_off[i]; s < s1; s++) {
+                const int hp = d.slot_hp[s];
                 if (hp < 0) continue;
-                const double* B = d.hpl + 18 * (size_t)e;
+                const double* B = d.hpl + 18 * (size_t)d.pe_idx[s];
+                const double* xp = d.x + 6 * (size_t)hp;
+#pragma unroll
                 for (int j = 0; j < 3; j++)
-                    for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * d.x[6 * (size_t)hp + k];
+#pragma unroll
+                    for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * xp[k];
             }
             const double* Di = d.Dinv + 9 * (size_t)i;
             for (int k = 0; k < 3; k++) xl[k] = Di[3 * k] * cl[0] + Di[3 * k + 1] * cl[1] + Di[3 * k + 2] * cl[2];
@@ -1978,6 +1994,7 @@ struct Carver {
 size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
     const size_t nx = 6 * (size_t)Np + 3 * (size_t)L;
     return al(4 * (size_t)P) + al(4 * (size_t)Np) + al(4 * (size_t)(L + 1)) + al(4 * (size_t)E) +
+           al(4 * (size_t)E) + al(16 * (size_t)E) +
            al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) + al(4 * ((size_t)Np * Np + 1)) +
            al((size_t)(npad / 16) * (npad / 16)) + al(2 * (size_t)(npad / 16) * (npad / 16)) +
            al(2 * (size_t)(npad / 16) * (npad / 16 + 1)) +
@@ -1994,6 +2011,8 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.hpose = cv.take<int32_t>(d.Np);
     d.pe_off = cv.take<int32_t>(d.L + 1);
     d.pe_idx = cv.take<int32_t>(d.E);
+    d.slot_hp = cv.take<int32_t>(d.E);
+    d.emeta = cv.take<int4>(d.E);
     d.qe_off = cv.take<int32_t>(d.Np + 1);
     d.qe_idx = cv.take<int32_t>(d.E);
     d.cnt = cv.take<int32_t>(d.L + d.Np);
