@@ -7,7 +7,7 @@
 //
 // Layout: the frame's edges are staged in LDS as float SoA (obs x/y, Xw, invSigma2; the reference's float inputs,
 // widened to double where used) next to each edge's last error (2 doubles, the stale-after-rejected-trial value
-// g2o's chi2() reads) and its level (0 active, 1 outlier). Every pass deals the edges to the 256 threads; the
+// g2o's chi2() reads) and its level (0 active, 1 outlier). Every pass deals the edges to the PT threads; the
 // per-thread partial sums (robust chi2, or the 21 upper entries of H plus b) are reduced by a fixed DPP pattern
 // per wave and a fixed wave order, so every thread ends with the same bits and runs the LM control flow, the 6x6
 // pivoted LDL^T and the SE3 update redundantly: no host round trip, no broadcast, block-uniform branches.
@@ -27,7 +27,11 @@
 namespace mam {
 namespace pose {
 
-constexpr int PT = 256;        // threads per frame
+#ifndef MAM_POSE_THREADS
+#define MAM_POSE_THREADS 1024
+#endif
+constexpr int PT = MAM_POSE_THREADS;   // threads per frame: the frame's LDS carve takes the whole CU, so its 16 waves
+                                       // (4 per SIMD) are what hides the FP64 and LDS latency of every pass
 constexpr int NW = PT / 64;
 constexpr int NRED = 27;       // 21 upper entries of H + 6 of b
 
@@ -72,15 +76,52 @@ __device__ __forceinline__ double lane63(double v) {
                             __builtin_amdgcn_readlane(__double2loint(v), 63));
 }
 
-// Block sum of N per-thread values into out[0..N) (LDS; waves summed in order 0..NW-1, fixed DPP pattern inside a
+// 4 Q wave sums at once, reduce-scatter style: the xor-32 and xor-16 steps exchange only the half of the values the
+// lane keeps, then xor 8 .. 1 on the Q left; lane group g = lane >> 4 ends with sums [g Q, g Q + Q) (fixed pattern:
+// the bits do not depend on timing) — 7 Q shuffles instead of a full reduction per value
+template <int Q>
+__device__ __forceinline__ void wave_sum_scatter4(const double (&v)[4 * Q], double (&out)[Q]) {
+    const int lane = threadIdx.x & 63;
+    const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0;
+    double h[2 * Q];
+#pragma unroll
+    for (int i = 0; i < 2 * Q; i++) {
+        const double send = b5 ? v[i] : v[2 * Q + i];
+        const double keep = b5 ? v[2 * Q + i] : v[i];
+        h[i] = keep + __shfl_xor(send, 32, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < Q; i++) {
+        const double send = b4 ? h[i] : h[Q + i];
+        const double keep = b4 ? h[Q + i] : h[i];
+        out[i] = keep + __shfl_xor(send, 16, 64);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1)
+#pragma unroll
+        for (int i = 0; i < Q; i++) out[i] += __shfl_xor(out[i], o, 64);
+}
+
+// Block sum of N per-thread values into out[0..N) (LDS; waves summed in order 0..NW-1, a fixed pattern inside a
 // wave, so the bits do not depend on timing). Ends with a barrier: out[] is readable by every thread.
 template <int N>
 __device__ __forceinline__ void block_sum(const double (&v)[N], double* scr, double* out) {
     const int w = threadIdx.x >> 6;
+    if constexpr (N % 4 == 0 && N >= 8) {
+        constexpr int Q = N / 4;
+        double tot[Q];
+        wave_sum_scatter4<Q>(v, tot);
+        const int lane = threadIdx.x & 63, il = lane & 15;
+        double val = 0.0;
 #pragma unroll
-    for (int k = 0; k < N; k++) {
-        const double s = lane63(wave_sum63(v[k]));
-        if ((threadIdx.x & 63) == 0) scr[w * N + k] = s;
+        for (int i = 0; i < Q; i++) val = il == i ? tot[i] : val;
+        if (il < Q) scr[w * N + Q * (lane >> 4) + il] = val;
+    } else {
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const double s = lane63(wave_sum63(v[k]));
+            if ((threadIdx.x & 63) == 0) scr[w * N + k] = s;
+        }
     }
     __syncthreads();
     if (threadIdx.x < N) {
