@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -28,10 +29,10 @@ namespace mam {
 namespace pose {
 
 #ifndef MAM_POSE_THREADS
-#define MAM_POSE_THREADS 1024
+#define MAM_POSE_THREADS 256
 #endif
-constexpr int PT = MAM_POSE_THREADS;   // threads per frame: the frame's LDS carve takes the whole CU, so its 16 waves
-                                       // (4 per SIMD) are what hides the FP64 and LDS latency of every pass
+constexpr int PT = MAM_POSE_THREADS;   // threads per frame (512 / 1024 measured slower: the LM step of every trial
+                                       // runs redundantly in every wave, and 1024 spills)
 constexpr int NW = PT / 64;
 constexpr int NRED = 27;       // 21 upper entries of H + 6 of b
 
@@ -346,6 +347,22 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
     return sign == 1 || sign == 0;
 }
 
+#ifdef MAM_POSE_PROFILE
+// phase cycles (thread 0 of every workgroup): 0 build pass + sums, 1 LDL^T solve, 2 exp * T, 3 trial pass + sum,
+// 4 LM control, 5 trials, 6 build passes
+__device__ unsigned long long g_pprof[8];
+#define PPROF(k, t0)                                                                    \
+    do {                                                                                \
+        const long long tn_ = clock64();                                               \
+        if (threadIdx.x == 0) atomicAdd(&g_pprof[k], (unsigned long long)(tn_ - (t0))); \
+        (t0) = tn_;                                                                     \
+    } while (0)
+#else
+#define PPROF(k, t0) \
+    do {             \
+    } while (0)
+#endif
+
 // SparseOptimizer::optimize(10) on the single pose vertex; T is updated in place. Returns the iterations run.
 __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool robust, double delta, double* scr,
                         int* trials) {
@@ -364,7 +381,14 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
     bool ok = true;
     for (int it = 0; it < 10 && ok; it++) {
         double* red = scr + NW * (NRED + 1) + 8;   // H upper, b, chi (LDS)
+#ifdef MAM_POSE_PROFILE
+        long long tp = clock64();
+#endif
         double currentChi = build_system(E, T, c, robust, delta, scr, red);
+        PPROF(0, tp);
+#ifdef MAM_POSE_PROFILE
+        if (threadIdx.x == 0) atomicAdd(&g_pprof[6], 1ull);
+#endif
         const double iniChi = currentChi;
         if (it == 0) {
             double md = 0.0;
@@ -382,10 +406,17 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
         int qmax = 0;
         do {
             double x[6];
+            PPROF(4, tp);   // LM control since the last pass
             const bool ok2 = ldlt6(red, lambda, x);
+            PPROF(1, tp);
             double Tn[7];
             se3::exp_mul(x, T, Tn);
+            PPROF(2, tp);
             double tempChi = active_chi(E, Tn, c, robust, delta, scr);
+            PPROF(3, tp);
+#ifdef MAM_POSE_PROFILE
+            if (threadIdx.x == 0) atomicAdd(&g_pprof[5], 1ull);
+#endif
             if (!ok2) tempChi = 1.7976931348623157e308;
             rho = currentChi - tempChi;
             double scale = 0.0;
@@ -678,6 +709,16 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_p
         hipLaunchKernelGGL(mam::pose::k_pose_opt, dim3(nframes), dim3(mam::pose::PT), c->lds, s, a);
     }
     MAM_HIP(hipGetLastError());
+#ifdef MAM_POSE_PROFILE
+    {
+        MAM_HIP(hipStreamSynchronize(s));
+        unsigned long long h[8];
+        MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::pose::g_pprof), sizeof(h)));
+        const double nb = (double)std::max(1ull, h[6]), nt = (double)std::max(1ull, h[5]);
+        fprintf(stderr, "pose cycles (cumulative): build %.0f/pass ldlt %.0f exp %.0f trial %.0f/trial control %.0f; "
+                        "builds %llu trials %llu\n", h[0] / nb, h[1] / nt, h[2] / nt, h[3] / nt, h[4] / nt, h[6], h[5]);
+    }
+#endif
     return MAM_OK;
 }
 
