@@ -774,7 +774,10 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
 // workgroups would exit at once, half of the dispatches) over its landmark pairs
 // (k_blk_fill), lanes strided over the pairs + a fixed-order wave sum; then one wave per pose for b_s. Only the lower
 // triangle of S is written (the one the factorization reads).
-__global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs) {
+#ifndef MAM_SCHUR_WAVES
+#define MAM_SCHUR_WAVES 3   // resident waves per SIMD the register budget is sized for
+#endif
+__global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* __restrict__ probs) {
     // XCD-aware: each XCD takes a contiguous range of (problem, block row) ids, so the W / H_pl records of the
     // landmarks its rows share stay in its L2
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
@@ -822,10 +825,35 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
+#ifndef MAM_SCHUR_HALVES
+#define MAM_SCHUR_HALVES 0
+#endif
     for (int k = d.blk_off[bx] + lane; k < d.blk_off[bx + 1]; k += 64) {
         const int2 pr = d.blk_pair[k];
         const double* W = d.bdinv + 18 * (size_t)pr.x;
         const double* B = d.hpl + 18 * (size_t)pr.y;
+#if MAM_SCHUR_HALVES
+        // rows of W and of H_pl three at a time (9 doubles each): the live set stays under 128 VGPRs (4 waves per
+        // SIMD instead of 3); the same products summed in the same order per accumulator
+#pragma unroll
+        for (int hr = 0; hr < 2; hr++) {
+            double w[9];
+#pragma unroll
+            for (int q = 0; q < 9; q++) w[q] = W[9 * hr + q];
+#pragma unroll
+            for (int hc = 0; hc < 2; hc++) {
+                double b[9];
+#pragma unroll
+                for (int q = 0; q < 9; q++) b[q] = B[9 * hc + q];
+#pragma unroll
+                for (int r = 0; r < 3; r++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+                        acc[6 * (3 * hr + r) + 3 * hc + c] +=
+                            w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
+            }
+        }
+#else
         double w[18], b[18];   // 144-byte records, 16-byte aligned: nine 16-byte loads each (staging the records
                                // cooperatively through LDS measured slower: 18 KB per wave halves the resident waves)
 #pragma unroll
@@ -839,6 +867,7 @@ __global__ __launch_bounds__(64) void k_schur_blk(const Prob* __restrict__ probs
 #pragma unroll
             for (int c = 0; c < 6; c++)
                 acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
+#endif
     }
     // the 36 sums reduce-scattered: lane group g holds sums [9 g, 9 g + 9)
     double tot[9];
