@@ -826,15 +826,16 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
 #ifndef MAM_SCHUR_HALVES
-#define MAM_SCHUR_HALVES 0
+#define MAM_SCHUR_HALVES 1
 #endif
     for (int k = d.blk_off[bx] + lane; k < d.blk_off[bx + 1]; k += 64) {
         const int2 pr = d.blk_pair[k];
         const double* W = d.bdinv + 18 * (size_t)pr.x;
         const double* B = d.hpl + 18 * (size_t)pr.y;
 #if MAM_SCHUR_HALVES
-        // rows of W and of H_pl three at a time (9 doubles each): the live set stays under 128 VGPRs (4 waves per
-        // SIMD instead of 3); the same products summed in the same order per accumulator
+        // rows of W and of H_pl three at a time (9 doubles each): 152 instead of 166 VGPRs, no spill (batch of 32
+        // windows 6.11 vs 6.27 ms; capped at 128 for 4 waves per SIMD it spills and is 11 % slower); the same products
+        // summed in the same order per accumulator
 #pragma unroll
         for (int hr = 0; hr < 2; hr++) {
             double w[9];
