@@ -620,9 +620,12 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
     lasts = [np.ascontiguousarray(x, LAST_ENTRY_DTYPE) for x in tr.lasts]
     mpls = [np.ascontiguousarray(x) for x in tr.mpls]
     n, t0 = 0, time.perf_counter()
+    ext_s = 0.0
     while True:
         f = n % len(tr.frames)
+        te = time.perf_counter()
         k, d, _ = oracle_py.extract(tr.frames[f], p)
+        ext_s += time.perf_counter() - te
         F = scene.make_frame_data(k, d, W, H)
         F.pose = tr.poses_init[f]
         last = lasts[f]
@@ -681,7 +684,7 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
         sin_ms += (time.perf_counter() - t2) * 1e3
         per_frame_ms += (tri_ms + bow_ms + sin_ms) / K
     res = {"value": 1e3 / per_frame_ms, "unit": "frames/s", "cores": 1, "kind": "port",
-           "tracking_ms_per_frame": track_ms, "host": host_info(),
+           "tracking_ms_per_frame": track_ms, "extract_ms_per_frame": ext_s * 1e3 / n, "host": host_info(),
            "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15) + "
                      f"PoseOptimization + isInFrustum + SearchByProjection(local map, th 1) + PoseOptimization on the "
                      f"oracle C++ restatement (g++ -O3 -march=x86-64-v3, the reference's CMake -O3 -march=native "
@@ -1103,6 +1106,28 @@ def main():
             out["cpu_baseline"]["ms_per_frame"] = 1e3 / out["cpu_baseline"]["value"]
             if lat is not None:
                 out["speedup_latency_b1"] = out["cpu_baseline"]["tracking_ms_per_frame"] / lat["device_graph_ms"]
+            if lat is not None and mapping is not None and lba_cpu is not None:
+                # the north star's per-frame figure: ORBextractor (the host-API call a Frame constructor makes, B = 1)
+                # + a lone LocalBundleAdjustment window every K frames, GPU vs the oracle on the same inputs
+                from mam3slam_amd.lba import LBASolver
+
+                sol = LBASolver(device=dev.index or 0)
+                prob = mapping.probs[0]
+                sol.solve(prob)
+                ts = []
+                for _ in range(5):
+                    t1 = time.perf_counter()
+                    sol.solve(prob)
+                    ts.append((time.perf_counter() - t1) * 1e3)
+                lone = float(np.median(ts))
+                ext_gpu, ext_cpu = lat["host_api_extract_ms"], out["cpu_baseline"]["extract_ms_per_frame"]
+                g, c_ = ext_gpu + lone / K, ext_cpu + lba_cpu / K
+                out["north_star"] = {
+                    "extract_ms_gpu_host_api": ext_gpu, "extract_ms_cpu": ext_cpu,
+                    "lba_lone_window_ms_gpu": lone, "lba_window_ms_cpu": lba_cpu, "keyframe_every": K,
+                    "per_frame_ms_gpu": g, "per_frame_ms_cpu": c_, "ratio": c_ / g,
+                    "note": "ORBextractor per frame + one LocalBundleAdjustment window per K frames (the same timed-region "
+                            "window alone through mam_lba_solve, host arrays in and out), target >= 50x"}
         print(json.dumps(out), flush=True)
         if out.get("invalid"):
             print(out["invalid"], file=sys.stderr)
