@@ -1571,27 +1571,25 @@ __device__ __forceinline__ void tiles_diag(double* TL, int sd, int kb, double* Y
     const double dmine = diag16_factor(row, lane);
     const double yv = diag16_forward(row, lane < NB ? Y[kb + lane] : 0.0, lane);
     const double invd = dmine != 0.0 ? 1.0 / dmine : 0.0;
-    if (lane < NB) {
-#pragma unroll
-        for (int c = 0; c < NB; c++)
-            if (c < lane) T[tsw(lane, c)] = row[c];
-        T[tsw(lane, lane)] = dmine;
-        dkp[lane] = dmine;
-        sh.invdk[lane] = invd;
-        Y[kb + lane] = yv;
-        if (dmine == 0.0) sh.fail = 1;
-    }
     double x[NB];
 #pragma unroll
     for (int r = 0; r < NB; r++) x[r] = (r == lane) ? 1.0 : 0.0;
     Inv16<1, 0>::run(x, row);
-    if (lane < NB) {
-        // lane c: row c of L^-T is column c of X; M(c, r) = X(r, c) / d_r
+    // lane c: row c of L^-T is column c of X; M(c, r) = X(r, c) / d_r with 1 / d_r broadcast from lane r (DPP, no LDS
+    // round trip)
+    double m[NB];
 #pragma unroll
-        for (int r = 0; r < NB; r++) {
-            sh.Ld[lane * NB + r] = x[r] * sh.invdk[r];
-            if (r > lane) T[tsw(lane, r)] = x[r];
-        }
+    for (int r = 0; r < NB; r++) m[r] = x[r] * bcast16_d(invd, r);
+    if (lane < NB) {
+        // one unconditional store per entry of the tile: L below the diagonal, D on it, L^-T above it (the backward
+        // solve's block); then M
+#pragma unroll
+        for (int c = 0; c < NB; c++) T[tsw(lane, c)] = c < lane ? row[c] : (c == lane ? dmine : x[c]);
+        dkp[lane] = dmine;
+        Y[kb + lane] = yv;
+        if (dmine == 0.0) sh.fail = 1;
+#pragma unroll
+        for (int r = 0; r < NB; r++) sh.Ld[lane * NB + r] = m[r];
     }
 }
 
