@@ -1310,6 +1310,12 @@ struct LdltShared {
     // ldlt_global<true>: the tile mask (uint8 [nt][nt]); ldlt_tiles: the tile slot map (int16 [nt][nt])
     int16_t map[LDLT_TM_MAX * LDLT_TM_MAX];
     int16_t tl[2 * 96];          // ldlt_tiles: (r, c) of each pool slot
+    // ldlt_tiles: per block column kc the rows r > kc of its non-zero tiles (ascending), per block row kc the columns
+    // c < kc of its non-zero tiles — the panel / trailing / backward loops walk only those
+    int8_t clist[40 * 40];
+    int8_t rlist[40 * 40];
+    uint8_t ccount[40];
+    uint8_t rcount[40];
 };
 
 // S factored in place in HBM with the panel / block-column workspace in LDS (use_lds) or in the problem's scratch: the
@@ -1609,6 +1615,15 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     for (int q = t; q < 2 * T; q += LDLT_THREADS) sh.tl[q] = d.tlist[q];
     for (int i = t; i < N; i += LDLT_THREADS) Y[i] = i < n ? d.bs[i] : 0.0;
     __syncthreads();
+    if (t < nt) {   // the column / row lists of the non-zero tiles
+        int nc = 0, nr = 0;
+        for (int r = t + 1; r < nt; r++)
+            if (slot[r * nt + t] >= 0) sh.clist[t * 40 + nc++] = (int8_t)r;
+        for (int c = 0; c < t; c++)
+            if (slot[t * nt + c] >= 0) sh.rlist[t * 40 + nr++] = (int8_t)c;
+        sh.ccount[t] = (uint8_t)nc;
+        sh.rcount[t] = (uint8_t)nr;
+    }
     // the pool: tile s = (r, c) holds S rows 16 r.., columns 16 c..; the padding rows' diagonal is 1 (an identity block
     // after the unknowns: S's padding rows are zero). One wave per tile, lane = (row, 4 columns): two 16-byte loads per
     // lane, the wave's tiles' loads issued together
@@ -1654,10 +1669,10 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         // (B) panel rows: one wave per non-zero tile (r, kc), r > kc: L21 = A21 M (M = L11^-T D^-1 from the diagonal
         // factorization) as four f64 MFMAs, in place; then y_r -= L21 y_kc, one row per lane
         {
-            const int col = lane & 15, rq = lane >> 4;
-            for (int r = kc + 1 + wid; r < nt; r += NW) {
+            const int col = lane & 15, rq = lane >> 4, ncl = sh.ccount[kc];
+            for (int i = wid; i < ncl; i += NW) {   // wave 0 takes the first: row kc + 1 when it is non-zero
+                const int r = sh.clist[kc * 40 + i];
                 const int s = slot[r * nt + kc];
-                if (s < 0) continue;
                 double* Tr = TL + (size_t)s * 256;
                 dbl4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1694,15 +1709,16 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             if (lane == 0) atomicAdd(&g_lprof[5], (unsigned long long)(clock64() - td));
 #endif
         } else {
-            const int T2 = nt - kc - 1;
-            const int n2 = T2 * (T2 + 1) / 2;
-            for (int q = wid; q < n2; q += NW - 1) {   // q = 0 is the diagonal tile
-                int tr, tc;
-                tri_index(q, &tr, &tc);
-                const int r = kc + 1 + tr, c = kc + 1 + tc;
-                const int sa = slot[r * nt + kc], sb = slot[c * nt + kc];
-                if (sa < 0 || sb < 0) continue;
-                tile_update(TL, slot[r * nt + c], sa, sb, dkp, lane);
+            // the pairs (a >= b) of the column's non-zero rows; pair (0, 0) is the diagonal tile when row kc + 1 is
+            // among them (wave 0's)
+            const int ncl = sh.ccount[kc];
+            const int q0 = (ncl > 0 && sh.clist[kc * 40] == kc + 1) ? 1 : 0;
+            const int n2 = ncl * (ncl + 1) / 2;
+            for (int q = q0 + wid - 1; q < n2; q += NW - 1) {
+                int a, b;
+                tri_index(q, &a, &b);
+                const int r = sh.clist[kc * 40 + a], c = sh.clist[kc * 40 + b];
+                tile_update(TL, slot[r * nt + c], slot[r * nt + kc], slot[c * nt + kc], dkp, lane);
             }
         }
         __syncthreads();
@@ -1732,10 +1748,11 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             }
             Y[kb + lane] = v;
         }
-        const int g = lane >> 4, il = lane & 15;
-        for (int c0 = kc - 1; c0 >= 0; c0 -= 4) {
-            const int c = c0 - g;
-            const int s = c >= 0 ? slot[kc * nt + c] : -1;   // L(kb.., 16 c..) not structurally zero
+        const int g = lane >> 4, il = lane & 15, nrl = sh.rcount[kc];
+        for (int i0 = 0; i0 < nrl; i0 += 4) {
+            const int i = i0 + g;
+            const int c = i < nrl ? sh.rlist[kc * 40 + i] : -1;   // L(kb.., 16 c..) not structurally zero
+            const int s = c >= 0 ? slot[kc * nt + c] : -1;
             if (s >= 0) {
                 const double* Tr = TL + (size_t)s * 256;
                 const int i = NB * c + il;
