@@ -1546,6 +1546,20 @@ __device__ __forceinline__ void tile_update(double* TL, int sc, int sa, int sb, 
     for (int r = 0; r < 4; r++) C[tsw(rq + 4 * r, col)] = acc[r];
 }
 
+// sy += x_J * mt[J], J = 0 .. 15 in order, x_J broadcast from lane J of the 16-lane row into the FMA (the source v
+// was last written just before the first: the hazard nop there only)
+template <int J>
+struct BackUpd16 {
+    __device__ __forceinline__ static void run(double& sy, double v, const double* mt) {
+        fmac_bcast16<J, J == 0>(sy, v, mt[J]);
+        BackUpd16<J + 1>::run(sy, v, mt);
+    }
+};
+template <>
+struct BackUpd16<NB> {
+    __device__ __forceinline__ static void run(double&, double, const double*) {}
+};
+
 // X = L11^-1 by columns, lane c holding column c (x[r] = X(r, c)): x[R] -= L(R, J) x[J] for J < R, L(R, J) broadcast
 // from lane R (row[J] there) into the FMA
 template <int R, int J>
@@ -1615,15 +1629,6 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     for (int q = t; q < 2 * T; q += LDLT_THREADS) sh.tl[q] = d.tlist[q];
     for (int i = t; i < N; i += LDLT_THREADS) Y[i] = i < n ? d.bs[i] : 0.0;
     __syncthreads();
-    if (t < nt) {   // the column / row lists of the non-zero tiles
-        int nc = 0, nr = 0;
-        for (int r = t + 1; r < nt; r++)
-            if (slot[r * nt + t] >= 0) sh.clist[t * 40 + nc++] = (int8_t)r;
-        for (int c = 0; c < t; c++)
-            if (slot[t * nt + c] >= 0) sh.rlist[t * 40 + nr++] = (int8_t)c;
-        sh.ccount[t] = (uint8_t)nc;
-        sh.rcount[t] = (uint8_t)nr;
-    }
     // the pool: tile s = (r, c) holds S rows 16 r.., columns 16 c..; the padding rows' diagonal is 1 (an identity block
     // after the unknowns: S's padding rows are zero). One wave per tile, lane = (row, 4 columns): two 16-byte loads per
     // lane, the wave's tiles' loads issued together
@@ -1658,6 +1663,16 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
                 }
             }
         }
+    }
+    if (t >= LDLT_THREADS - 64 && t - (LDLT_THREADS - 64) < nt) {   // the column / row lists of the non-zero tiles
+        const int k = t - (LDLT_THREADS - 64);                       // (the last wave, after its pool loads)
+        int nc = 0, nr = 0;
+        for (int r = k + 1; r < nt; r++)
+            if (slot[r * nt + k] >= 0) sh.clist[k * 40 + nc++] = (int8_t)r;
+        for (int c = 0; c < k; c++)
+            if (slot[k * nt + c] >= 0) sh.rlist[k * 40 + nr++] = (int8_t)c;
+        sh.ccount[k] = (uint8_t)nc;
+        sh.rcount[k] = (uint8_t)nr;
     }
     __syncthreads();
     if (wid == 0) tiles_diag(TL, slot[0], 0, Y, sh, sh.dk[0], lane);
@@ -1735,32 +1750,33 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         const int ii = i / NB;
         Y[i] /= TL[(size_t)slot[ii * nt + ii] * 256 + tsw(i & 15, i & 15)];
     }
+    const int g = lane >> 4, il = lane & 15;
     for (int kc = nt - 1; kc >= 0; kc--) {
         const int kb = NB * kc;
-        if (lane < NB) {
-            const double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
-            double v = Y[kb + lane];
-            // predicated, not branched: every lane's loads issue together (a branch per j was one LDS round trip each)
+        // x_b in every 16-lane row (the same arithmetic in each), so the update below takes x_j from lane j of its own
+        // row by DPP instead of an LDS round trip
+        const double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
+        double v = Y[kb + il];
+        // predicated, not branched: every lane's loads issue together (a branch per j was one LDS round trip each)
 #pragma unroll
-            for (int j = 1; j < NB; j++) {
-                const double f = fma(Td[tsw(lane, j)], Y[kb + j], v);
-                v = j > lane ? f : v;
-            }
-            Y[kb + lane] = v;
+        for (int j = 1; j < NB; j++) {
+            const double f = fma(Td[tsw(il, j)], Y[kb + j], v);
+            v = j > il ? f : v;
         }
-        const int g = lane >> 4, il = lane & 15, nrl = sh.rcount[kc];
+        if (lane < NB) Y[kb + lane] = v;
+        const int nrl = sh.rcount[kc];
         for (int i0 = 0; i0 < nrl; i0 += 4) {
             const int i = i0 + g;
             const int c = i < nrl ? sh.rlist[kc * 40 + i] : -1;   // L(kb.., 16 c..) not structurally zero
-            const int s = c >= 0 ? slot[kc * nt + c] : -1;
-            if (s >= 0) {
-                const double* Tr = TL + (size_t)s * 256;
-                const int i = NB * c + il;
-                double sy = Y[i];
+            const int s = c >= 0 ? slot[kc * nt + c] : slot[kc * nt + kc];   // (a valid tile; result unused)
+            const double* Tr = TL + (size_t)s * 256;
+            const int yi = NB * (c >= 0 ? c : kc) + il;
+            double mt[NB];
 #pragma unroll
-                for (int j = 0; j < NB; j++) sy = fma(-Tr[tsw(j, il)], Y[kb + j], sy);
-                Y[i] = sy;
-            }
+            for (int j = 0; j < NB; j++) mt[j] = -Tr[tsw(j, il)];
+            double sy = Y[yi];
+            BackUpd16<0>::run(sy, v, mt);   // sy = fma(-L(kb + j, yi), x_j, sy), j = 0 .. 15, in order
+            if (c >= 0) Y[yi] = sy;
         }
     }
     for (int i = lane; i < n; i += 64) d.x[i] = Y[i];
