@@ -492,17 +492,6 @@ __device__ __forceinline__ void wave_copy_in(double* __restrict__ dst, const dou
     }
 }
 
-__device__ __forceinline__ int nchunks(const Prob& d) { return d.E / EW + 1; }
-__device__ __forceinline__ int lower_bound_off(const int32_t* off, int n, int v) {   // first p in [0, n] with off[p] >= v
-    int lo = 0, hi = n + 1;
-    while (lo < hi) {
-        const int m = (lo + hi) >> 1;
-        if (off[m] >= v) hi = m;
-        else lo = m + 1;
-    }
-    return lo > n ? n : lo;
-}
-
 // The damping of this trial. On an iteration's first trial of the first iteration it is levenberg.cpp:71-77's
 // lambda_0 = tau * max diag(H), tau = 1e-5 (computeLambdaInit :171-185), from the max k_sys gathered (max is exact in
 // any order); k_ctl_end commits it to lm.lambda with the rest of the iteration-start state, so no control kernel runs
@@ -520,9 +509,6 @@ __global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs
     if (lm.status || (mode != 2 && lm.done) || (mode == 0 && !lm.need_lin)) return;
     __shared__ double sj[EW * 21];   // one staging buffer (LDS bounds the resident waves of this one-wave kernel)
     const int e0 = blockIdx.x * EW;
-    // E / 64 + 1 blocks (the point-chunk count, so k_plin's and these parts are summed alike): a block past the edges
-    // writes a zero part
-    if (e0 >= d.E && (int)blockIdx.x < nchunks(d) && lane_id() == 0) (mode == 0 ? d.part0 : d.part)[blockIdx.x] = 0.0;
     if (e0 < d.E) {
         const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
         const int lane = lane_id(), e = e0 + lane;
@@ -555,150 +541,6 @@ __global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs
             if (lane_id() == 0) d.part_s[blockIdx.x] = acc;
         }
     }
-}
-
-// ---- point chunks: the edge slots in point order (pe_idx, per point in edge order) cut at point boundaries. Chunk c
-// holds the points whose first slot lies in [64 c, 64 c + 64) (every point with edges belongs to exactly one chunk,
-// and its owner lane there is that offset), plus the edgeless points whose pe_off falls in the range; its slots are
-// [pe_off[p0], pe_off[p1]), at most 64 + (max edges of a point) - 1, worked in passes of 64. E / 64 + 1 chunks.
-
-// grid (E / 64 + 1, Q) x 64: one wave per point chunk (the fused trial path of small batches: the factorization
-// kernels' epilogue wrote the trial poses). The chunk's rho0 sum (its edges in slot order, fixed-order
-// butterfly per pass) goes to part0 (mode 0) / part (modes 1, 2).
-//   mode 2: the initial chi2 (current state).
-//   mode 0: iteration start: every edge linearised (jac / H_pl records out, through LDS as contiguous 16-byte chunks
-//           when the pass's edges are consecutive — point-major inputs — else per lane), and the point blocks H_ll,
-//           b_l (sys_body's per-edge terms, summed by the point's owner lane over its slots in order) + max |diag|.
-//   mode 1: trial: the back-substitution x_l = D^-1 (b_l - sum H_pl^T x_p) (block_solver.hpp:461-482) by the owner
-//           lanes over their slots in order (H_pl staged in LDS), X + x_l written to the trial state, then every
-//           edge's error at the trial state (the poses: updated by the factorization's epilogue, pose_trial_update).
-template <int mode>
-__global__ __launch_bounds__(EW) void k_plin(const Prob* __restrict__ probs) {
-    const Prob& d = probs[blockIdx.y];
-    LM& lm = *d.lm;
-    if (lm.status || (mode != 2 && lm.done)) return;
-    const int c = blockIdx.x;
-    if (c >= nchunks(d)) return;
-    __shared__ double sj[EW * 18];   // H_pl staging (trial)
-    const int lane = lane_id();
-    const int p0 = lower_bound_off(d.pe_off, d.L, EW * c), p1 = lower_bound_off(d.pe_off, d.L, EW * c + EW);
-    const int s0 = d.pe_off[p0], s1 = d.pe_off[p1];
-    // the owner lane's point: the point whose first slot is 64 c + lane (none when that slot starts no point)
-    int po = -1;
-    {
-        const int sl = EW * c + lane;
-        if (sl < d.E) {
-            // the last point with pe_off == sl (edgeless points before it share that offset)
-            const int q = lower_bound_off(d.pe_off, d.L, sl + 1) - 1;
-            if (q >= 0 && q < d.L && d.pe_off[q] == sl && d.pe_off[q + 1] > sl) po = q;
-        }
-    }
-    const int o0 = po >= 0 ? d.pe_off[po] : 0, o1 = po >= 0 ? d.pe_off[po + 1] : 0;
-    const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
-    double rsum = 0.0;
-    if constexpr (mode == 1) {
-        // (1) back-substitution over the chunk's slots, 64 per pass: the edge lanes stage their slot's H_pl record
-        // (contiguous 16-byte chunks when the pass's edges are consecutive), pose block and x_p in LDS in parallel, then
-        // each owner lane runs its point's sum over its slots in order from LDS only
-        __shared__ double sxp[EW * 6];
-        __shared__ int32_t shp[EW];
-        double cl[3] = {0.0, 0.0, 0.0};
-        if (po >= 0)
-#pragma unroll
-            for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)po + k];
-        for (int ps = s0; ps < s1; ps += EW) {
-            const int ne = min(EW, s1 - ps);
-            const int e = lane < ne ? d.pe_idx[ps + lane] : -1;
-            const int hp = e >= 0 ? d.pose_h[d.edge_pose[e]] : -1;
-            shp[lane] = hp;
-            if (hp >= 0) {
-                const double2* xs = reinterpret_cast<const double2*>(d.x + 6 * (size_t)hp);
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    const double2 v = xs[k];
-                    sxp[6 * lane + 2 * k] = v.x;
-                    sxp[6 * lane + 2 * k + 1] = v.y;
-                }
-            }
-            const int e_first = __shfl(e, 0, 64);
-            const bool contig = __all(lane >= ne || e == e_first + lane);
-            if (contig) {
-                wave_copy_in(sj, d.hpl + 18 * (size_t)e_first, 18 * ne);
-            } else if (e >= 0) {
-                const double2* src = reinterpret_cast<const double2*>(d.hpl + 18 * (size_t)e);
-#pragma unroll
-                for (int k = 0; k < 9; k++) {
-                    const double2 v = src[k];
-                    sj[18 * lane + 2 * k] = v.x;
-                    sj[18 * lane + 2 * k + 1] = v.y;
-                }
-            }
-            __syncthreads();
-            if (po >= 0 && !lm.fail) {
-                const int a = max(o0, ps), z = min(o1, ps + ne);
-                for (int sl = a; sl < z; sl++) {
-                    if (shp[sl - ps] < 0) continue;
-                    const double* B = sj + 18 * (sl - ps);
-                    const double* xp = sxp + 6 * (sl - ps);
-#pragma unroll
-                    for (int j = 0; j < 3; j++)
-#pragma unroll
-                        for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * xp[k];
-                }
-            }
-            __syncthreads();
-        }
-        const double* pts = d.pt[lm.cur];
-        double* pt_out = d.pt[1 - lm.cur];
-        const double lambda = trial_lambda(lm);
-        double ssum = 0.0;   // computeScale over the chunk's points: x_l (lambda x_l + b_l)
-        auto update_point = [&](int i, const double* clp) {
-            double* xl = d.x + 6 * (size_t)d.Np + 3 * (size_t)i;
-            const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)i;
-            double xv[3];
-            if (!lm.fail) {
-                const double* Di = d.Dinv + 9 * (size_t)i;
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    xv[k] = Di[3 * k] * clp[0] + Di[3 * k + 1] * clp[1] + Di[3 * k + 2] * clp[2];
-                    xl[k] = xv[k];
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 3; k++) xv[k] = xl[k];
-            }
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                pt_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + xv[k];
-                ssum += xv[k] * (lambda * xv[k] + bl[k]);
-            }
-        };
-        if (po >= 0) update_point(po, cl);
-        // edgeless points of the chunk: x_l = D^-1 b_l
-        for (int i = p0 + lane; i < p1; i += EW) {
-            if (d.pe_off[i + 1] != d.pe_off[i]) continue;
-            double bl[3];
-#pragma unroll
-            for (int k = 0; k < 3; k++) bl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)i + k];
-            update_point(i, bl);
-        }
-        ssum = wave_sum_d(ssum);
-        if (lane == 0) d.part_s[c] = ssum;
-        __syncthreads();   // the trial points are visible to the chunk's edge lanes
-        // (2) errors at the trial state
-        for (int ps = s0; ps < s1; ps += EW) {
-            const int ne = min(EW, s1 - ps);
-            if (lane < ne) rsum += linearize_edge(d, d.pose[sidx], d.pt[sidx], d.pe_idx[ps + lane], false, nullptr, nullptr);
-        }
-    } else {
-        // mode 2: the initial chi2 at the current state
-        for (int ps = s0; ps < s1; ps += EW) {
-            const int ne = min(EW, s1 - ps);
-            if (lane < ne) rsum += linearize_edge(d, d.pose[sidx], d.pt[sidx], d.pe_idx[ps + lane], false, nullptr, nullptr);
-        }
-    }
-    rsum = wave_sum_d(rsum);
-    if (lane == 0) d.part[c] = rsum;
 }
 
 // grid (ceil(L/64) + Np, Q) x 64: H_ll, b_l per point (edge order, one thread each) and H_pp, b_p per optimised pose
@@ -796,7 +638,7 @@ template <int T>
 __device__ double chi_of_parts(const Prob& d, const double* part, double* s) {
     // parts of 64 edges, grouped by 256 as ((p0 + p1) + p2) + p3 (a missing part adds nothing), then strided + tree
     double acc[RED / T];
-    const int np = nchunks(d), nb = (np + 3) / 4;
+    const int np = (d.E + EW - 1) / EW, nb = (d.E + 255) / 256;
 #pragma unroll
     for (int v = 0; v < RED / T; v++) {
         acc[v] = 0.0;
@@ -1944,6 +1786,36 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
 #endif
 }
 
+// grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
+// largest pool + y of the batch)
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_tiles(const Prob* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done || !lm.tiles_lds) return;
+    if (d.Np == 0) {
+        if (threadIdx.x == 0) lm.fail = 0;
+        return;
+    }
+    ldlt_tiles(d, lds_dyn, sh);
+}
+
+// grid (Q) x LDLT_THREADS: the others, factored in place in HBM (the panel workspace in LDS when use_lds)
+template <bool use_lds>
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    LM& lm = *d.lm;
+    if (lm.status || lm.done || lm.tiles_lds) return;
+    if (d.Np == 0) {
+        if (threadIdx.x == 0) lm.fail = 0;
+        return;
+    }
+    ldlt_global<use_lds>(d, lds_dyn, sh);
+}
+
 // Eigen Quaterniond(Matrix3d)
 __device__ void rot_to_quat(const double m[9], double q[4]) {
     const double t = m[0] + m[4] + m[8];
@@ -1958,19 +1830,13 @@ __device__ void rot_to_quat(const double m[9], double q[4]) {
         int i = 0;
         if (m[4] > m[0]) i = 1;
         if (m[8] > m[3 * i + i]) i = 2;
-        // the branch per i with compile-time indices (a runtime-indexed q / m lands in scratch memory)
-        auto br = [&](auto I) {
-            constexpr int ii = decltype(I)::value, j = (ii + 1) % 3, k = (j + 1) % 3;
-            double s = sqrt(m[3 * ii + ii] - m[3 * j + j] - m[3 * k + k] + 1.0);
-            q[ii] = 0.5 * s;
-            s = 0.5 / s;
-            q[3] = (m[3 * k + j] - m[3 * j + k]) * s;
-            q[j] = (m[3 * j + ii] + m[3 * ii + j]) * s;
-            q[k] = (m[3 * k + ii] + m[3 * ii + k]) * s;
-        };
-        if (i == 0) br(std::integral_constant<int, 0>());
-        else if (i == 1) br(std::integral_constant<int, 1>());
-        else br(std::integral_constant<int, 2>());
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
+        q[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[3] = (m[3 * k + j] - m[3 * j + k]) * s;
+        q[j] = (m[3 * j + i] + m[3 * i + j]) * s;
+        q[k] = (m[3 * k + i] + m[3 * i + k]) * s;
     }
 }
 
@@ -1979,98 +1845,6 @@ __device__ void normalize_q(double q[4]) {
     const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
     q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
 }
-
-// One trial pose: T <- exp(dx) T (se3quat.h; VertexSE3Expmap::oplusImpl) for an optimised pose, a fixed pose copied
-__device__ void pose_update_one(const Prob& d, int i, const double* pose, double* pose_out) {
-    const double* T = pose + 7 * (size_t)i;
-    double* O = pose_out + 7 * (size_t)i;
-    const int h = d.pose_h[i];
-    if (h < 0) {
-        for (int k = 0; k < 7; k++) O[k] = T[k];
-    } else {
-        const double* u = d.x + 6 * (size_t)h;
-        const double w0 = u[0], w1 = u[1], w2 = u[2];
-        const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
-        const double Om[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
-        double Om2[9];
-        for (int r = 0; r < 3; r++)
-            for (int c = 0; c < 3; c++)
-                Om2[3 * r + c] = Om[3 * r] * Om[c] + Om[3 * r + 1] * Om[3 + c] + Om[3 * r + 2] * Om[6 + c];
-        double R[9], V[9];
-        if (theta < 0.00001) {
-            for (int k = 0; k < 9; k++) { R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + Om2[k]; V[k] = R[k]; }
-        } else {
-            const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-            const double c = (theta - sin(theta)) / (theta * theta * theta);
-            for (int k = 0; k < 9; k++) {
-                const double I = (k % 4 == 0) ? 1.0 : 0.0;
-                R[k] = I + a * Om[k] + b * Om2[k];
-                V[k] = I + b * Om[k] + c * Om2[k];
-            }
-        }
-        double qe[4];
-        rot_to_quat(R, qe);
-        double te[3];
-        for (int r = 0; r < 3; r++) te[r] = V[3 * r] * u[3] + V[3 * r + 1] * u[4] + V[3 * r + 2] * u[5];
-        normalize_q(qe);
-        // exp * T
-        double rt[3];
-        quat_rotate(qe, T + 4, rt);
-        double q[4];
-        q[3] = qe[3] * T[3] - qe[0] * T[0] - qe[1] * T[1] - qe[2] * T[2];
-        q[0] = qe[3] * T[0] + qe[0] * T[3] + qe[1] * T[2] - qe[2] * T[1];
-        q[1] = qe[3] * T[1] + qe[1] * T[3] + qe[2] * T[0] - qe[0] * T[2];
-        q[2] = qe[3] * T[2] + qe[2] * T[3] + qe[0] * T[1] - qe[1] * T[0];
-        normalize_q(q);
-        O[0] = q[0]; O[1] = q[1]; O[2] = q[2]; O[3] = q[3];
-        O[4] = te[0] + rt[0]; O[5] = te[1] + rt[1]; O[6] = te[2] + rt[2];
-    }
-}
-
-// The trial poses as the factorization kernels' epilogue (small batches: the fused trial path, k_plin): every thread of
-// the workgroup strided over the poses, dx from d.x
-__device__ void pose_trial_updates(const Prob& d, const LM& lm) {
-    for (int i = threadIdx.x; i < d.P; i += blockDim.x) pose_update_one(d, i, d.pose[lm.cur], d.pose[1 - lm.cur]);
-}
-
-// grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
-// largest pool + y of the batch)
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_tiles(const Prob* __restrict__ probs, int fused) {
-    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-    __shared__ LdltShared sh;
-    const Prob& d = probs[blockIdx.x];
-    LM& lm = *d.lm;
-    if (lm.status || lm.done || !lm.tiles_lds) return;
-    if (d.Np == 0) {
-        if (threadIdx.x == 0) lm.fail = 0;
-    } else {
-        ldlt_tiles(d, lds_dyn, sh);
-    }
-    if (fused) {
-        __syncthreads();   // x is written (wave 0's backward substitution)
-        pose_trial_updates(d, lm);
-    }
-}
-
-// grid (Q) x LDLT_THREADS: the others, factored in place in HBM (the panel workspace in LDS when use_lds)
-template <bool use_lds>
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs, int fused) {
-    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-    __shared__ LdltShared sh;
-    const Prob& d = probs[blockIdx.x];
-    LM& lm = *d.lm;
-    if (lm.status || lm.done || lm.tiles_lds) return;
-    if (d.Np == 0) {
-        if (threadIdx.x == 0) lm.fail = 0;
-    } else {
-        ldlt_global<use_lds>(d, lds_dyn, sh);
-    }
-    if (fused) {
-        __syncthreads();
-        pose_trial_updates(d, lm);
-    }
-}
-
 
 // grid (ceil(max(P, L)/256), Q): x_l = D^-1 (b_l - H_pl^T x_p) per point (skipped after a failed factorization:
 // BlockSolver::solve returns before the back-substitution and the update applies the old x), then the trial state:
@@ -2106,12 +1880,56 @@ __global__ __launch_bounds__(256) void k_backsub_update(const Prob* __restrict__
         }
         for (int k = 0; k < 3; k++) pt_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + xl[k];
     }
-    if (i < d.P) pose_update_one(d, i, pose, pose_out);
+    if (i < d.P) {
+        const double* T = pose + 7 * (size_t)i;
+        double* O = pose_out + 7 * (size_t)i;
+        const int h = d.pose_h[i];
+        if (h < 0) {
+            for (int k = 0; k < 7; k++) O[k] = T[k];
+        } else {
+            const double* u = d.x + 6 * (size_t)h;
+            const double w0 = u[0], w1 = u[1], w2 = u[2];
+            const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+            const double Om[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+            double Om2[9];
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++)
+                    Om2[3 * r + c] = Om[3 * r] * Om[c] + Om[3 * r + 1] * Om[3 + c] + Om[3 * r + 2] * Om[6 + c];
+            double R[9], V[9];
+            if (theta < 0.00001) {
+                for (int k = 0; k < 9; k++) { R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + Om2[k]; V[k] = R[k]; }
+            } else {
+                const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+                const double c = (theta - sin(theta)) / (theta * theta * theta);
+                for (int k = 0; k < 9; k++) {
+                    const double I = (k % 4 == 0) ? 1.0 : 0.0;
+                    R[k] = I + a * Om[k] + b * Om2[k];
+                    V[k] = I + b * Om[k] + c * Om2[k];
+                }
+            }
+            double qe[4];
+            rot_to_quat(R, qe);
+            double te[3];
+            for (int r = 0; r < 3; r++) te[r] = V[3 * r] * u[3] + V[3 * r + 1] * u[4] + V[3 * r + 2] * u[5];
+            normalize_q(qe);
+            // exp * T
+            double rt[3];
+            quat_rotate(qe, T + 4, rt);
+            double q[4];
+            q[3] = qe[3] * T[3] - qe[0] * T[0] - qe[1] * T[1] - qe[2] * T[2];
+            q[0] = qe[3] * T[0] + qe[0] * T[3] + qe[1] * T[2] - qe[2] * T[1];
+            q[1] = qe[3] * T[1] + qe[1] * T[3] + qe[2] * T[0] - qe[0] * T[2];
+            q[2] = qe[3] * T[2] + qe[2] * T[3] + qe[0] * T[1] - qe[1] * T[0];
+            normalize_q(q);
+            O[0] = q[0]; O[1] = q[1]; O[2] = q[2]; O[3] = q[3];
+            O[4] = te[0] + rt[0]; O[5] = te[1] + rt[1]; O[6] = te[2] + rt[2];
+        }
+    }
 }
 
 // grid (Q) x 256: end of a trial — levenberg.cpp:108-158 (rho, accept / reject, lambda), then the iteration-end
 // tests of levenberg.cpp:159-168 and sparse_optimizer.cpp:381-409.
-__global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs, int fused) {
+__global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs) {
     constexpr int T = RED;
     __shared__ double s[RED];
     const Prob& d = probs[blockIdx.x];
@@ -2124,14 +1942,11 @@ __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs,
     const double chi0 = (begin && lm.its == 0) ? chi_of_parts<T>(d, d.part0, s) : 0.0;
     double tempChi = chi_of_parts<T>(d, d.part, s);
     // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194)
-    // (the non-fused trial: k_linearize's per-block partials over the whole x; the fused trial: the pose entries here
-    // and k_plin's per-chunk partials of the points)
     double acc[RED / T];
-    const int nbl = fused ? nchunks(d) : max(1, (d.E + EW - 1) / EW), np6 = fused ? 6 * d.Np : 0;
+    const int nbl = max(1, (d.E + EW - 1) / EW);
 #pragma unroll
     for (int v = 0; v < RED / T; v++) {
         acc[v] = 0.0;
-        for (int j = threadIdx.x + T * v; j < np6; j += RED) acc[v] += d.x[j] * (lambda * d.x[j] + d.b[j]);
         for (int j = threadIdx.x + T * v; j < nbl; j += RED) acc[v] += d.part_s[j];
     }
     const double scale0 = block_sum<T>(acc, s);
@@ -2408,7 +2223,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     MAM_HIP(hipMemcpyAsync(outs_buf().p, c->lm_host.p + pb + lb, sizeof(Outs) * Q, hipMemcpyHostToDevice, s));
     const Prob* P = c->probs.p;
     const dim3 gE((maxE + 255) / 256 > 0 ? (maxE + 255) / 256 : 1, Q);
-    const dim3 gE64(maxE / EW + 1, Q);   // the point-chunk count (k_plin) covers the 64-edge blocks + one
+    const dim3 gE64((maxE + EW - 1) / EW > 0 ? (maxE + EW - 1) / EW : 1, Q);
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
         hipLaunchKernelGGL(k_struct_init, dim3(8, Q), dim3(SB), 0, s, P);
@@ -2463,12 +2278,6 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     const char* sp = std::getenv("MAM_LBA_SPLIT");
     int G = Q < 4 ? 1 : 2;   // batch of 32 world windows: 8.56 / 7.92 / 7.76 / 9.10 ms at G = 1 / 2 / 3 / 4; c2: 2
     if (sp && sp[0] >= '1' && sp[0] <= '9') G = std::max(1, std::min({mam_lba_ctx::kMaxGroups, Q, sp[0] - '0'}));
-    // Small batches (a lone window, one per agent): the trial back-substitution fused with the trial errors in one
-    // point-chunk kernel (k_plin) and the pose update in the factorization's epilogue — fewer dependent launches per
-    // trial (lone window 1.92 -> 1.89 ms when measured); large batches keep the per-point / per-edge kernels, which
-    // are faster at throughput (batch of 32: 6.33 vs 7.13 ms). MAM_LBA_FUSED=0/1 overrides.
-    int fused = Q <= 4 ? 1 : 0;
-    if (const char* fz = std::getenv("MAM_LBA_FUSED")) fused = fz[0] == '1' ? 1 : 0;
     hipStream_t sg[mam_lba_ctx::kMaxGroups] = {s, s, s, s};
     if (G > 1) {
         int prio = 0;
@@ -2505,23 +2314,19 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 2);
-            if (any_tiles) hipLaunchKernelGGL(k_ldlt_tiles, dim3(Qg), dim3(LDLT_THREADS), tiles_dyn, st, Pg, fused);
+            if (any_tiles) hipLaunchKernelGGL(k_ldlt_tiles, dim3(Qg), dim3(LDLT_THREADS), tiles_dyn, st, Pg);
             if (any_global) {
                 if (lds_ok)
-                    hipLaunchKernelGGL(k_ldlt<true>, dim3(Qg), dim3(LDLT_THREADS), max_lds, st, Pg, fused);
+                    hipLaunchKernelGGL(k_ldlt<true>, dim3(Qg), dim3(LDLT_THREADS), max_lds, st, Pg);
                 else
-                    hipLaunchKernelGGL(k_ldlt<false>, dim3(Qg), dim3(LDLT_THREADS), 0, st, Pg, fused);
+                    hipLaunchKernelGGL(k_ldlt<false>, dim3(Qg), dim3(LDLT_THREADS), 0, st, Pg);
             }
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
-            if (fused) {
-                hipLaunchKernelGGL(k_plin<1>, gE64g, dim3(EW), 0, st, Pg);
-            } else {
-                hipLaunchKernelGGL(k_backsub_update, gUpdg, dim3(256), 0, st, Pg);
-                hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 1);
-            }
-            hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg, fused);
+            hipLaunchKernelGGL(k_backsub_update, gUpdg, dim3(256), 0, st, Pg);
+            hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 1);
+            hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
     };
     auto slot = [&]() {
