@@ -1560,43 +1560,23 @@ struct BackUpd16<NB> {
     __device__ __forceinline__ static void run(double&, double, const double*) {}
 };
 
-// The diagonal tile's LDL^T (Diag16's steps) with the forward block solve and the inverse X = L11^-1 interleaved:
-// step J's column of L is all the forward step J (y_i -= L(i, J) y_J) and the inverse's column J (X(R, .) -=
-// L(R, J) X(J, .), R > J) need, so both run in the shadow of the next pivot's reciprocal chain instead of after the
-// factorization. Every accumulator sees the same operations in the same order as the separate loops (bit-identical).
-template <int J, int R>
-struct InvCol16 {
+// X = L11^-1 by columns, lane c holding column c (x[r] = X(r, c)): x[R] -= L(R, J) x[J] for J < R, L(R, J) broadcast
+// from lane R (row[J] there) into the FMA
+template <int R, int J>
+struct Inv16 {
     __device__ __forceinline__ static void run(double* x, const double* row) {
-        fmac_bcast16<R, R == J + 1>(x[R], row[J], -x[J]);   // row[J] was just written: the first read waits
-        InvCol16<J, R + 1>::run(x, row);
+        // row[] is final since the factorization (no write of it in the hazard window)
+        fmac_bcast16<R, false>(x[R], row[J], -x[J]);
+        Inv16<R, J + 1>::run(x, row);
     }
 };
-template <int J>
-struct InvCol16<J, NB> {
-    __device__ __forceinline__ static void run(double*, const double*) {}
-};
-template <int J>
-struct DiagInv16 {
-    __device__ __forceinline__ static void run(double* row, double* x, double& yv, double& dmine, int lane) {
-        const double a = row[J];
-        const double dj = bcast16_d(a, J);
-        if (lane == J) dmine = dj;
-        double inv = __builtin_amdgcn_rcp(dj);
-        inv = fma(inv, fma(-dj, inv, 1.0), inv);
-        inv = fma(inv, fma(-dj, inv, 1.0), inv);
-        if (dj == 0.0) inv = 0.0;
-        const double l = a * inv;
-        Fmac16<J, J + 1>::run(row, a, -l);
-        if (lane > J) row[J] = l;
-        const double yJ = bcast16_d(yv, J);
-        if (lane > J) yv = fma(-row[J], yJ, yv);
-        InvCol16<J, J + 1>::run(x, row);
-        DiagInv16<J + 1>::run(row, x, yv, dmine, lane);
-    }
+template <int R>
+struct Inv16<R, R> {
+    __device__ __forceinline__ static void run(double* x, const double* row) { Inv16<R + 1, 0>::run(x, row); }
 };
 template <>
-struct DiagInv16<NB> {
-    __device__ __forceinline__ static void run(double*, double*, double&, double&, int) {}
+struct Inv16<NB, 0> {
+    __device__ __forceinline__ static void run(double*, const double*) {}
 };
 
 // wave 0: LDL^T of diagonal tile sd of the pool, written back in place (L below, D on the diagonal, and L^-T above it
@@ -1608,12 +1588,13 @@ __device__ __forceinline__ void tiles_diag(double* TL, int sd, int kb, double* Y
     double row[NB];
 #pragma unroll
     for (int c = 0; c < NB; c++) row[c] = lane < NB ? T[tsw(lane, c)] : 0.0;
+    const double dmine = diag16_factor(row, lane);
+    const double yv = diag16_forward(row, lane < NB ? Y[kb + lane] : 0.0, lane);
+    const double invd = dmine != 0.0 ? 1.0 / dmine : 0.0;
     double x[NB];
 #pragma unroll
     for (int r = 0; r < NB; r++) x[r] = (r == lane) ? 1.0 : 0.0;
-    double yv = lane < NB ? Y[kb + lane] : 0.0, dmine = 1.0;
-    DiagInv16<0>::run(row, x, yv, dmine, lane);
-    const double invd = dmine != 0.0 ? 1.0 / dmine : 0.0;
+    Inv16<1, 0>::run(x, row);
     // lane c: row c of L^-T is column c of X; M(c, r) = X(r, c) / d_r with 1 / d_r broadcast from lane r (DPP, no LDS
     // round trip)
     double m[NB];
