@@ -224,19 +224,34 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
             J[0] = -(fx / z); J[1] = -0.0; J[2] = -(-fx * x / (z * z));
             J[3] = -0.0; J[4] = -(fy / z); J[5] = -(-fy * y / (z * z));
         }
-        const double D[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
         double A[12];
+        if (kb8) {
+            const double D[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
 #pragma unroll
-        for (int r = 0; r < 2; r++)
+            for (int r = 0; r < 2; r++)
 #pragma unroll
-            for (int k = 0; k < 6; k++) A[6 * r + k] = J[3 * r] * D[k] + J[3 * r + 1] * D[6 + k] + J[3 * r + 2] * D[12 + k];
+                for (int k = 0; k < 6; k++)
+                    A[6 * r + k] = J[3 * r] * D[k] + J[3 * r + 1] * D[6 + k] + J[3 * r + 2] * D[12 + k];
+        } else {
+            // the same product with Pinhole's zero Jacobian entries and SE3deriv's zeros / ones folded: every
+            // non-zero entry gets the same operations (a product with an exact zero adds a signed zero, which leaves
+            // a non-zero sum unchanged); the entries that are exactly zero become +0
+            const double J0 = J[0], J2 = J[2], J4 = J[4], J5 = J[5];
+            A[0] = J2 * y;          A[1] = J0 * z + J2 * -x; A[2] = J0 * -y;
+            A[3] = J0;              A[4] = 0.0;              A[5] = J2;
+            A[6] = J4 * -z + J5 * y; A[7] = J5 * -x;         A[8] = J4 * x;
+            A[9] = 0.0;             A[10] = J4;              A[11] = J5;
+        }
         const double o0 = -(w * e0) * r1, o1 = -(w * e1) * r1;
         const double wo = r1 * w;
+        double wA[12];   // A * wo once per entry: (A[a] * wo) * A[b] is the same product as before
+#pragma unroll
+        for (int k = 0; k < 12; k++) wA[k] = A[k] * wo;
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; a++)
 #pragma unroll
-            for (int b = a; b < 6; b++) acc[q++] += A[a] * wo * A[b] + A[6 + a] * wo * A[6 + b];
+            for (int b = a; b < 6; b++) acc[q++] += wA[a] * A[b] + wA[6 + a] * A[6 + b];
 #pragma unroll
         for (int a = 0; a < 6; a++) acc[21 + a] += A[a] * o0 + A[6 + a] * o1;
     }
