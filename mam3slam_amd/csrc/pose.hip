@@ -166,6 +166,22 @@ __device__ __forceinline__ void rho_of(double chi, bool robust, double delta, do
     else { *r0 = chi; *r1 = 1.0; }
 }
 
+#ifdef MAM_POSE_PROFILE
+// phase cycles (thread 0 of every workgroup): 0 build pass + sums, 1 LDL^T solve, 2 exp * T, 3 trial pass + sum,
+// 4 LM control, 5 trials, 6 build passes
+__device__ unsigned long long g_pprof[8];
+#define PPROF(k, t0)                                                                    \
+    do {                                                                                \
+        const long long tn_ = clock64();                                               \
+        if (threadIdx.x == 0) atomicAdd(&g_pprof[k], (unsigned long long)(tn_ - (t0))); \
+        (t0) = tn_;                                                                     \
+    } while (0)
+#else
+#define PPROF(k, t0) \
+    do {             \
+    } while (0)
+#endif
+
 // computeActiveErrors at T (errors stored) + activeRobustChi2
 __device__ double active_chi(const Edges& E, const double T[7], const mam_camera& c, bool robust, double delta,
                              double* scr) {
@@ -191,6 +207,9 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
     double acc[NRED + 1];
 #pragma unroll
     for (int k = 0; k <= NRED; k++) acc[k] = 0.0;
+#ifdef MAM_POSE_PROFILE
+    long long tb = clock64();
+#endif
     for (int i = threadIdx.x; i < E.n; i += PT) {
         if (E.level[i]) continue;
         const double Xw[3] = {(double)E.X[i], (double)E.Y[i], (double)E.Z[i]};
@@ -255,6 +274,7 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
 #pragma unroll
         for (int a = 0; a < 6; a++) acc[21 + a] += A[a] * o0 + A[6 + a] * o1;
     }
+    PPROF(7, tb);   // the edge loop alone (thread 0's view)
     block_sum<NRED + 1>(acc, scr, red);
     return red[NRED];
 }
@@ -362,21 +382,6 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
     return sign == 1 || sign == 0;
 }
 
-#ifdef MAM_POSE_PROFILE
-// phase cycles (thread 0 of every workgroup): 0 build pass + sums, 1 LDL^T solve, 2 exp * T, 3 trial pass + sum,
-// 4 LM control, 5 trials, 6 build passes
-__device__ unsigned long long g_pprof[8];
-#define PPROF(k, t0)                                                                    \
-    do {                                                                                \
-        const long long tn_ = clock64();                                               \
-        if (threadIdx.x == 0) atomicAdd(&g_pprof[k], (unsigned long long)(tn_ - (t0))); \
-        (t0) = tn_;                                                                     \
-    } while (0)
-#else
-#define PPROF(k, t0) \
-    do {             \
-    } while (0)
-#endif
 
 // SparseOptimizer::optimize(10) on the single pose vertex; T is updated in place. Returns the iterations run.
 __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool robust, double delta, double* scr,
@@ -730,8 +735,9 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_p
         unsigned long long h[8];
         MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::pose::g_pprof), sizeof(h)));
         const double nb = (double)std::max(1ull, h[6]), nt = (double)std::max(1ull, h[5]);
-        fprintf(stderr, "pose cycles (cumulative): build %.0f/pass ldlt %.0f exp %.0f trial %.0f/trial control %.0f; "
-                        "builds %llu trials %llu\n", h[0] / nb, h[1] / nt, h[2] / nt, h[3] / nt, h[4] / nt, h[6], h[5]);
+        fprintf(stderr, "pose cycles (cumulative): build %.0f/pass (edge loop %.0f) ldlt %.0f exp %.0f trial %.0f/trial "
+                        "control %.0f; builds %llu trials %llu\n", h[0] / nb, h[7] / nb, h[1] / nt, h[2] / nt, h[3] / nt,
+                h[4] / nt, h[6], h[5]);
     }
 #endif
     return MAM_OK;
