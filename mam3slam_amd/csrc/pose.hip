@@ -186,6 +186,7 @@ __device__ unsigned long long g_pprof[8];
 __device__ double active_chi(const Edges& E, const double T[7], const mam_camera& c, bool robust, double delta,
                              double* scr) {
     double acc[1] = {0.0};
+#pragma unroll 2
     for (int i = threadIdx.x; i < E.n; i += PT) {
         if (E.level[i]) continue;
         double e0, e1;
@@ -210,6 +211,9 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
 #ifdef MAM_POSE_PROFILE
     long long tb = clock64();
 #endif
+    // two edges per iteration: their dependency chains (map, divisions, robust weight, Jacobian, sums) interleave —
+    // one wave per SIMD has nothing else to hide the FP64 latency with
+#pragma unroll 2
     for (int i = threadIdx.x; i < E.n; i += PT) {
         if (E.level[i]) continue;
         const double Xw[3] = {(double)E.X[i], (double)E.Y[i], (double)E.Z[i]};
