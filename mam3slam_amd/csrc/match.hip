@@ -409,8 +409,6 @@ __device__ __forceinline__ int rot_bin(float rot) {
     return bin;
 }
 
-constexpr int CAND_LDS = 4096;    // candidate entries of one 64-unit chunk staged in LDS (16 KB)
-
 // Greedy resolve as dependency rounds. Unit u's outcome depends only on the taken-state of its candidate
 // keypoints, which only earlier units sharing a candidate can change. Each round: every open unit writes its index
 // into minU[k] (atomicMin) for each candidate k; a unit is READY when it is the minimum on all its candidates
@@ -715,7 +713,6 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
             RPROF(5);
         }
     } else {
-        const int rel = rel_threshold(p);
         int mysum = 0;
     #pragma unroll
         for (int k = 0; k < UPT; k++) mysum += ucnt[k];

@@ -142,13 +142,14 @@ struct Edges {
 };
 
 // EdgeSE3ProjectXYZOnlyPose::computeError: obs - Pinhole::project(T.map(Xw)); returns chi2 = e^T (w I) e
+template <bool KB8>
 __device__ __forceinline__ double edge_error(const Edges& E, int i, const double T[7], const mam_camera& c,
                                              double* e0o, double* e1o) {
     const double Xw[3] = {(double)E.X[i], (double)E.Y[i], (double)E.Z[i]};
     double Xc[3];
     se3::map_point(T, Xw, Xc);
     double u, v;
-    if (c.model == MAM_CAM_KANNALA_BRANDT8) {
+    if (KB8) {
         cam::project_d(c, Xc, &u, &v);   // KannalaBrandt8::project(Vector3d)
     } else {
         u = (double)c.fx * Xc[0] / Xc[2] + (double)c.cx;
@@ -183,6 +184,7 @@ __device__ unsigned long long g_pprof[8];
 #endif
 
 // computeActiveErrors at T (errors stored) + activeRobustChi2
+template <bool KB8>
 __device__ double active_chi(const Edges& E, const double T[7], const mam_camera& c, bool robust, double delta,
                              double* scr) {
     double acc[1] = {0.0};
@@ -190,7 +192,7 @@ __device__ double active_chi(const Edges& E, const double T[7], const mam_camera
     for (int i = threadIdx.x; i < E.n; i += PT) {
         if (E.level[i]) continue;
         double e0, e1;
-        const double chi = edge_error(E, i, T, c, &e0, &e1);
+        const double chi = edge_error<KB8>(E, i, T, c, &e0, &e1);
         E.err[2 * i] = e0;
         E.err[2 * i + 1] = e1;
         double r0, r1;
@@ -203,6 +205,7 @@ __device__ double active_chi(const Edges& E, const double T[7], const mam_camera
 
 // One pass: computeActiveErrors + activeRobustChi2 + buildSystem (BaseUnaryEdge::constructQuadraticForm,
 // base_unary_edge.hpp:43-71). H upper (row-major i <= j, 21) then b (6) in red[0..26]; returns the chi.
+template <bool KB8>
 __device__ double build_system(const Edges& E, const double T[7], const mam_camera& c, bool robust, double delta,
                                double* scr, double* red) {
     double acc[NRED + 1];
@@ -220,7 +223,7 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
         double Xc[3];
         se3::map_point(T, Xw, Xc);
         const double x = Xc[0], y = Xc[1], z = Xc[2];
-        const bool kb8 = c.model == MAM_CAM_KANNALA_BRANDT8;
+        constexpr bool kb8 = KB8;
         double u, v;
         if (kb8) {
             cam::project_d(c, Xc, &u, &v);
@@ -388,6 +391,7 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
 
 
 // SparseOptimizer::optimize(10) on the single pose vertex; T is updated in place. Returns the iterations run.
+template <bool KB8>
 __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool robust, double delta, double* scr,
                         int* trials) {
     // initializeOptimization(0): no level-0 edge -> optimize() returns -1 before the loop
@@ -408,7 +412,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
 #ifdef MAM_POSE_PROFILE
         long long tp = clock64();
 #endif
-        double currentChi = build_system(E, T, c, robust, delta, scr, red);
+        double currentChi = build_system<KB8>(E, T, c, robust, delta, scr, red);
         PPROF(0, tp);
 #ifdef MAM_POSE_PROFILE
         if (threadIdx.x == 0) atomicAdd(&g_pprof[6], 1ull);
@@ -436,7 +440,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
             double Tn[7];
             se3::exp_mul(x, T, Tn);
             PPROF(2, tp);
-            double tempChi = active_chi(E, Tn, c, robust, delta, scr);
+            double tempChi = active_chi<KB8>(E, Tn, c, robust, delta, scr);
             PPROF(3, tp);
 #ifdef MAM_POSE_PROFILE
             if (threadIdx.x == 0) atomicAdd(&g_pprof[5], 1ull);
@@ -472,6 +476,8 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
     return its;
 }
 
+// the camera model is a template parameter: a Pinhole launch carries no KannalaBrandt8 code in its edge loops
+template <bool KB8>
 __global__ __launch_bounds__(PT) void k_pose_opt(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ double scr[NW * (NRED + 1) + 8 + NRED + 1];   // wave partials | chi sum | H, b, chi sums
@@ -516,7 +522,7 @@ __global__ __launch_bounds__(PT) void k_pose_opt(Args a) {
         bool robust = true;
         for (int it = 0; it < 4; it++) {
             for (int k = 0; k < 7; k++) T[k] = T0[k];   // vSE3->setEstimate(pFrame->GetPose())
-            its += optimize(E, T, a.cam, robust, delta, scr, &trials);
+            its += optimize<KB8>(E, T, a.cam, robust, delta, scr, &trials);
             rounds++;
             if (t == 0) s_nbad = 0;
             __syncthreads();
@@ -524,7 +530,7 @@ __global__ __launch_bounds__(PT) void k_pose_opt(Args a) {
             for (int i = t; i < n; i += PT) {
                 if (E.level[i]) {   // outliers of the last classification: computeError() at the new pose
                     double e0, e1;
-                    edge_error(E, i, T, a.cam, &e0, &e1);
+                    edge_error<KB8>(E, i, T, a.cam, &e0, &e1);
                     E.err[2 * i] = e0;
                     E.err[2 * i + 1] = e1;
                 }
@@ -679,7 +685,9 @@ int mam_pose_create(int device, mam_pose_ctx** out) {
     c->device = device;
     // LDS carve: as many edges as fit in 160 KB next to the kernel's static scratch
     size_t lim = 64 * 1024;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::pose::k_pose_opt),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::pose::k_pose_opt<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::pose::k_pose_opt<true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess)
         lim = 150 * 1024;
     else
@@ -730,7 +738,10 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_p
     a.cap = c->cap;
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
-        hipLaunchKernelGGL(mam::pose::k_pose_opt, dim3(nframes), dim3(mam::pose::PT), c->lds, s, a);
+        if (cam->model == MAM_CAM_KANNALA_BRANDT8)
+            hipLaunchKernelGGL(mam::pose::k_pose_opt<true>, dim3(nframes), dim3(mam::pose::PT), c->lds, s, a);
+        else
+            hipLaunchKernelGGL(mam::pose::k_pose_opt<false>, dim3(nframes), dim3(mam::pose::PT), c->lds, s, a);
     }
     MAM_HIP(hipGetLastError());
 #ifdef MAM_POSE_PROFILE
