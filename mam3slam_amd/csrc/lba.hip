@@ -546,6 +546,11 @@ __global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs
 // grid (ceil(L/64) + Np, Q) x 64: H_ll, b_l per point (edge order, one thread each) and H_pp, b_p per optimised pose
 // (one wave: lanes own strided edges, 27 register sums, fixed-order wave reduction)
 // returns this thread's max |diag| of the blocks it wrote (0 for none; fmax drops NaN as the reference's max does)
+#ifndef MAM_SYS_PF
+#define MAM_SYS_PF 4
+#endif
+constexpr int SYS_PF = MAM_SYS_PF;   // edge indices per lane prefetched per pass (a pose: ~480 edges)
+constexpr int PT_PF = 8;             // a point's edge indices prefetched per pass (a window's points: <= 8 edges)
 __device__ double sys_body(const Prob& d) {
     const int nb_pts = (d.L + 63) / 64;
     if ((int)blockIdx.x < nb_pts) {
@@ -553,13 +558,19 @@ __device__ double sys_body(const Prob& d) {
         if (h >= d.L) return 0.0;
         double H[9] = {0}, bl[3] = {0};
         const int s1 = d.pe_off[h + 1];
-#pragma unroll 2
-        for (int s = d.pe_off[h]; s < s1; s++) {
-            const double* j = d.jac + 21 * (size_t)d.pe_idx[s];
-            const double wo = j[20];
-            for (int a = 0; a < 3; a++) {
-                bl[a] += j[a] * j[18] + j[3 + a] * j[19];
-                for (int c = 0; c < 3; c++) H[3 * a + c] += j[a] * wo * j[c] + j[3 + a] * wo * j[3 + c];
+        for (int sb = d.pe_off[h]; sb < s1; sb += PT_PF) {
+            int pi[PT_PF];   // the point's edge indices loaded together, then their records in edge order
+#pragma unroll
+            for (int u = 0; u < PT_PF; u++) pi[u] = sb + u < s1 ? d.pe_idx[sb + u] : -1;
+#pragma unroll
+            for (int u = 0; u < PT_PF; u++) {
+                if (pi[u] < 0) break;
+                const double* j = d.jac + 21 * (size_t)pi[u];
+                const double wo = j[20];
+                for (int a = 0; a < 3; a++) {
+                    bl[a] += j[a] * j[18] + j[3 + a] * j[19];
+                    for (int c = 0; c < 3; c++) H[3 * a + c] += j[a] * wo * j[c] + j[3 + a] * wo * j[3 + c];
+                }
             }
         }
         for (int k = 0; k < 9; k++) d.Hll[9 * (size_t)h + k] = H[k];
@@ -571,19 +582,29 @@ __device__ double sys_body(const Prob& d) {
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
-    for (int s = d.qe_off[h] + lane; s < d.qe_off[h + 1]; s += 64) {
-        const double* j = d.jac + 21 * (size_t)d.qe_idx[s];
-        double B0[6], B1[6];
+    // the lane's edge indices of up to SYS_PF strides loaded together first (one memory round trip where there was
+    // one per edge before its record's loads); the records then summed in the same order as before
+    const int qs0 = d.qe_off[h], qs1 = d.qe_off[h + 1];
+    for (int base = qs0 + lane; base < qs1; base += 64 * SYS_PF) {
+        int qi[SYS_PF];
 #pragma unroll
-        for (int k = 0; k < 6; k++) { B0[k] = j[6 + k]; B1[k] = j[12 + k]; }
-        const double wo = j[20], o0 = j[18], o1 = j[19];
-        int q = 0;
+        for (int u = 0; u < SYS_PF; u++) qi[u] = base + 64 * u < qs1 ? d.qe_idx[base + 64 * u] : -1;
 #pragma unroll
-        for (int a = 0; a < 6; a++)
+        for (int u = 0; u < SYS_PF; u++) {
+            if (qi[u] < 0) break;
+            const double* j = d.jac + 21 * (size_t)qi[u];
+            double B0[6], B1[6];
 #pragma unroll
-            for (int c = a; c < 6; c++) acc[q++] += B0[a] * wo * B0[c] + B1[a] * wo * B1[c];
+            for (int k = 0; k < 6; k++) { B0[k] = j[6 + k]; B1[k] = j[12 + k]; }
+            const double wo = j[20], o0 = j[18], o1 = j[19];
+            int q = 0;
 #pragma unroll
-        for (int a = 0; a < 6; a++) acc[21 + a] += B0[a] * o0 + B1[a] * o1;
+            for (int a = 0; a < 6; a++)
+#pragma unroll
+                for (int c = a; c < 6; c++) acc[q++] += B0[a] * wo * B0[c] + B1[a] * wo * B1[c];
+#pragma unroll
+            for (int a = 0; a < 6; a++) acc[21 + a] += B0[a] * o0 + B1[a] * o1;
+        }
     }
     // 27 sums (+ one zero pad) reduce-scattered: lane group g holds sums [7 g, 7 g + 7), lane g * 16 + i sum 7 g + i
     double tot[7];
@@ -777,6 +798,10 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
 #ifndef MAM_SCHUR_WAVES
 #define MAM_SCHUR_WAVES 3   // resident waves per SIMD the register budget is sized for
 #endif
+#ifndef MAM_SCHUR_PF
+#define MAM_SCHUR_PF 2
+#endif
+constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per pass (2 / 4 / 8: the same time)
 __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* __restrict__ probs) {
     // XCD-aware: each XCD takes a contiguous range of (problem, block row) ids, so the W / H_pl records of the
     // landmarks its rows share stay in its L2
@@ -828,47 +853,56 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
 #ifndef MAM_SCHUR_HALVES
 #define MAM_SCHUR_HALVES 1
 #endif
-    for (int k = d.blk_off[bx] + lane; k < d.blk_off[bx + 1]; k += 64) {
-        const int2 pr = d.blk_pair[k];
-        const double* W = d.bdinv + 18 * (size_t)pr.x;
-        const double* B = d.hpl + 18 * (size_t)pr.y;
+    const int k1 = d.blk_off[bx + 1];
+    for (int kb = d.blk_off[bx] + lane; kb < k1; kb += 64 * SCHUR_PF) {
+        // the lane's pair records of up to SCHUR_PF strides loaded together (one round trip, not one per pair)
+        int2 prs[SCHUR_PF];
+#pragma unroll
+        for (int u = 0; u < SCHUR_PF; u++) prs[u] = kb + 64 * u < k1 ? d.blk_pair[kb + 64 * u] : make_int2(-1, -1);
+#pragma unroll
+        for (int u = 0; u < SCHUR_PF; u++) {
+            if (prs[u].x < 0) break;
+            const int2 pr = prs[u];
+            const double* W = d.bdinv + 18 * (size_t)pr.x;
+            const double* B = d.hpl + 18 * (size_t)pr.y;
 #if MAM_SCHUR_HALVES
-        // rows of W and of H_pl three at a time (9 doubles each): 152 instead of 166 VGPRs, no spill (batch of 32
-        // windows 6.11 vs 6.27 ms; capped at 128 for 4 waves per SIMD it spills and is 11 % slower); the same products
-        // summed in the same order per accumulator
+            // rows of W and of H_pl three at a time (9 doubles each): 152 instead of 166 VGPRs, no spill (batch of 32
+            // windows 6.11 vs 6.27 ms; capped at 128 for 4 waves per SIMD it spills and is 11 % slower); the same products
+            // summed in the same order per accumulator
 #pragma unroll
-        for (int hr = 0; hr < 2; hr++) {
-            double w[9];
+            for (int hr = 0; hr < 2; hr++) {
+                double w[9];
 #pragma unroll
-            for (int q = 0; q < 9; q++) w[q] = W[9 * hr + q];
+                for (int q = 0; q < 9; q++) w[q] = W[9 * hr + q];
 #pragma unroll
-            for (int hc = 0; hc < 2; hc++) {
-                double b[9];
+                for (int hc = 0; hc < 2; hc++) {
+                    double b[9];
 #pragma unroll
-                for (int q = 0; q < 9; q++) b[q] = B[9 * hc + q];
+                    for (int q = 0; q < 9; q++) b[q] = B[9 * hc + q];
 #pragma unroll
-                for (int r = 0; r < 3; r++)
+                    for (int r = 0; r < 3; r++)
 #pragma unroll
-                    for (int c = 0; c < 3; c++)
-                        acc[6 * (3 * hr + r) + 3 * hc + c] +=
-                            w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
+                        for (int c = 0; c < 3; c++)
+                            acc[6 * (3 * hr + r) + 3 * hc + c] +=
+                                w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
+                }
             }
-        }
 #else
-        double w[18], b[18];   // 144-byte records, 16-byte aligned: nine 16-byte loads each (staging the records
-                               // cooperatively through LDS measured slower: 18 KB per wave halves the resident waves)
+            double w[18], b[18];   // 144-byte records, 16-byte aligned: nine 16-byte loads each (staging the records
+                                   // cooperatively through LDS measured slower: 18 KB per wave halves the resident waves)
 #pragma unroll
-        for (int q = 0; q < 9; q++) {
-            const double2 wv = reinterpret_cast<const double2*>(W)[q], bv = reinterpret_cast<const double2*>(B)[q];
-            w[2 * q] = wv.x; w[2 * q + 1] = wv.y;
-            b[2 * q] = bv.x; b[2 * q + 1] = bv.y;
-        }
+            for (int q = 0; q < 9; q++) {
+                const double2 wv = reinterpret_cast<const double2*>(W)[q], bv = reinterpret_cast<const double2*>(B)[q];
+                w[2 * q] = wv.x; w[2 * q + 1] = wv.y;
+                b[2 * q] = bv.x; b[2 * q + 1] = bv.y;
+            }
 #pragma unroll
-        for (int r = 0; r < 6; r++)
+            for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int c = 0; c < 6; c++)
-                acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
+                for (int c = 0; c < 6; c++)
+                    acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
 #endif
+        }
     }
     // the 36 sums reduce-scattered: lane group g holds sums [9 g, 9 g + 9)
     double tot[9];
@@ -1849,11 +1883,13 @@ __device__ void normalize_q(double q[4]) {
 // grid (ceil(max(P, L)/256), Q): x_l = D^-1 (b_l - H_pl^T x_p) per point (skipped after a failed factorization:
 // BlockSolver::solve returns before the back-substitution and the update applies the old x), then the trial state:
 // T <- exp(dx) * T (VertexSE3Expmap::oplusImpl) for optimised poses, X <- X + dx, fixed poses copied.
-__global__ __launch_bounds__(256) void k_backsub_update(const Prob* __restrict__ probs) {
+// one-wave workgroups: a lone window's 3.2k points spread over 50 CUs' load pipes instead of 13
+constexpr int UPD_T = 64;
+__global__ __launch_bounds__(UPD_T) void k_backsub_update(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     const LM& lm = *d.lm;
     if (lm.status || lm.done) return;
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * UPD_T + threadIdx.x;
     const double* pose = d.pose[lm.cur];
     const double* pts = d.pt[lm.cur];
     double* pose_out = d.pose[1 - lm.cur];
@@ -1864,16 +1900,24 @@ __global__ __launch_bounds__(256) void k_backsub_update(const Prob* __restrict__
             double cl[3];
             for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)i + k];
             const int s1 = d.pe_off[i + 1];
-#pragma unroll 2
-            for (int s = d.pe_off[i]; s < s1; s++) {
-                const int hp = d.slot_hp[s];
-                if (hp < 0) continue;
-                const double* B = d.hpl + 18 * (size_t)d.pe_idx[s];
-                const double* xp = d.x + 6 * (size_t)hp;
+            for (int sb = d.pe_off[i]; sb < s1; sb += PT_PF) {
+                int hps[PT_PF], pis[PT_PF];   // the point's slots loaded together, then its records in edge order
 #pragma unroll
-                for (int j = 0; j < 3; j++)
+                for (int u = 0; u < PT_PF; u++) {
+                    hps[u] = sb + u < s1 ? d.slot_hp[sb + u] : -2;
+                    pis[u] = sb + u < s1 ? d.pe_idx[sb + u] : 0;
+                }
 #pragma unroll
-                    for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * xp[k];
+                for (int u = 0; u < PT_PF; u++) {
+                    if (hps[u] == -2) break;
+                    if (hps[u] < 0) continue;
+                    const double* B = d.hpl + 18 * (size_t)pis[u];
+                    const double* xp = d.x + 6 * (size_t)hps[u];
+#pragma unroll
+                    for (int j = 0; j < 3; j++)
+#pragma unroll
+                        for (int k = 0; k < 6; k++) cl[j] -= B[3 * k + j] * xp[k];
+                }
             }
             const double* Di = d.Dinv + 9 * (size_t)i;
             for (int k = 0; k < 3; k++) xl[k] = Di[3 * k] * cl[0] + Di[3 * k + 1] * cl[1] + Di[3 * k + 2] * cl[2];
@@ -2270,7 +2314,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     const dim3 gPrep((std::max(maxE, maxL) + EW - 1) / EW > 0 ? (std::max(maxE, maxL) + EW - 1) / EW : 1, Q);
     const dim3 gBlk(maxNp * (maxNp + 1) / 2 + maxNp > 0 ? maxNp * (maxNp + 1) / 2 + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
-    const dim3 gUpd((maxPL + 255) / 256 > 0 ? (maxPL + 255) / 256 : 1, Q);
+    const dim3 gUpd((maxPL + UPD_T - 1) / UPD_T > 0 ? (maxPL + UPD_T - 1) / UPD_T : 1, Q);
     // The batch runs as G interleaved groups on G streams: one group's latency-bound factorization (one workgroup
     // per problem) overlaps the other groups' throughput kernels. Every kernel indexes its problems from the Prob
     // pointer it is given, so a group is the sub-array P + first with Q_g problems. MAM_LBA_SPLIT=<G> overrides
@@ -2324,7 +2368,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
-            hipLaunchKernelGGL(k_backsub_update, gUpdg, dim3(256), 0, st, Pg);
+            hipLaunchKernelGGL(k_backsub_update, gUpdg, dim3(UPD_T), 0, st, Pg);
             hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 1);
             hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
