@@ -735,13 +735,17 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_p
     a.n_edges = n_edges;
     a.outlier = outlier;
     a.res = results;
-    a.cap = c->cap;
+    // the LDS carve sized to the edge stride (a frame's edges never exceed it), not to the context's capacity: a c2
+    // frame's 2k-edge stride takes ~82 KB instead of 150, and the rest of the CU's LDS stays free for the other
+    // lanes' kernels (extraction, matching) running beside the optimisation
+    a.cap = std::min(c->cap, std::max(64, (edge_stride + 63) / 64 * 64));
+    const size_t lds = mam::pose::lds_bytes(a.cap);
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
         if (cam->model == MAM_CAM_KANNALA_BRANDT8)
-            hipLaunchKernelGGL(mam::pose::k_pose_opt<true>, dim3(nframes), dim3(mam::pose::PT), c->lds, s, a);
+            hipLaunchKernelGGL(mam::pose::k_pose_opt<true>, dim3(nframes), dim3(mam::pose::PT), lds, s, a);
         else
-            hipLaunchKernelGGL(mam::pose::k_pose_opt<false>, dim3(nframes), dim3(mam::pose::PT), c->lds, s, a);
+            hipLaunchKernelGGL(mam::pose::k_pose_opt<false>, dim3(nframes), dim3(mam::pose::PT), lds, s, a);
     }
     MAM_HIP(hipGetLastError());
 #ifdef MAM_POSE_PROFILE
