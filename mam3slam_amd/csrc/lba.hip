@@ -1143,7 +1143,7 @@ __device__ __forceinline__ double bcast16_d(double v, int k) {
 // v_fmac_f64_dpp row_newbcast (gfx950 DPP64); one instruction where a v_mov_b64_dpp + v_fma_f64 pair was. The s_nop
 // covers the VALU-write -> DPP-read hazard on src (inline asm is not seen by the hazard recognizer); not volatile, so
 // the scheduler may interleave independent work. Same rounding as fma(src_K, m, acc).
-// NOP = false where src was last written many instructions earlier (the later FMAs of one step, all of Inv16).
+// NOP = false where src was last written many instructions earlier (the later FMAs of one step).
 template <int K, bool NOP = true>
 __device__ __forceinline__ void fmac_bcast16(double& acc, double src, double m) {
     if constexpr (NOP)
@@ -1337,7 +1337,7 @@ constexpr int C1_PF = MAM_LDLT_C1_PF;   // (C1) tiles per wave prefetched across
 constexpr int LDLT_TM_MAX = 40;         // the LDS path's tile-mask copy: nt <= 40 (npad <= 640)
 // The factorization's static LDS, shared by both forms of k_ldlt (ldlt_global, ldlt_tiles)
 struct LdltShared {
-    double Ld[NB * NB];          // ldlt_global: L11 row-major; ldlt_tiles: M = L11^-T D^-1 row-major
+    double Ld[NB * NB];          // ldlt_global: L11 row-major
     double dk[2][NB];
     double invdk[NB];
     int fail;
@@ -1550,11 +1550,11 @@ __device__ __forceinline__ void ldlt_global(const Prob& d, double* lds_ws, LdltS
 
 // ---- the factorization with all of L in LDS (lm.tiles_lds: the structurally non-zero tiles + y fit the dynamic
 // LDS). The tiles S holds (k_schur_blk: pose blocks, lower triangle) are loaded once into a pool of 16x16 tiles
-// (k_struct_tiles' slots, tslot / tlist), factored there and never written back: only x leaves the workgroup. The
-// algorithm is ldlt_global's (the same panels, lookahead and tile skipping, so every non-zero entry sees the same
-// arithmetic): per panel k (B) the rows of the non-zero tiles (r, k) below the diagonal, L21 = A21 L11^-T D^-1 with
-// y2 -= L21 y1; (C1) the next block column's tiles updated by f64 MFMA; (C2) wave 0 factors the next diagonal tile
-// while the other waves update the rest of the trailing tiles. No global memory round trip inside the panel loop.
+// (k_struct_tiles' slots, tslot / tlist), factored there and never written back: only x leaves the workgroup. Blocked
+// right-looking LDL^T with tile skipping: per block column k, tall panels (the diagonal tile and the column's
+// non-zero tiles below it factored in one register pass, y's forward solve folded in), then the trailing tiles
+// updated by f64 MFMA — column k + 1's first (what the next panel reads), the rest beside the next panel. No global
+// memory round trip inside the panel loop.
 // Tile layout: element (r, c) at c * 16 + (r ^ c) (column-major, rows XOR-swizzled by the column): the MFMA A / B
 // operand reads (16 rows of one column per 16 lanes), the accumulator reads / writes (16 columns of one row) and the
 // row-per-thread panel rows are all free of LDS bank conflicts within a 32-lane group.
@@ -1580,70 +1580,117 @@ __device__ __forceinline__ void tile_update(double* TL, int sc, int sa, int sb, 
     for (int r = 0; r < 4; r++) C[tsw(rq + 4 * r, col)] = acc[r];
 }
 
-// sy += x_J * mt[J], J = 0 .. 15 in order, x_J broadcast from lane J of the 16-lane row into the FMA (the source v
-// was last written just before the first: the hazard nop there only)
+// ---- tall panels: the panel tiles factored together with the diagonal tile, lane (g, i) = (lane >> 4, lane & 15)
+// holding row i of the diagonal tile (the same row in all four 16-lane groups) and row i of panel tile g of the
+// column. The right-looking steps that factor the diagonal tile then also produce the panel rows' L (l = A(p, J) / d_J,
+// A(p, K) -= l A(K, J), A(K, J) broadcast from lane K of the lane's own group) and the forward solve of y for both, in
+// one pass: no M = L11^-T D^-1, no MFMA panel product and no barrier between the diagonal and its panel. The diagonal
+// rows and their y see exactly the arithmetic of diag16_factor + diag16_forward.
+// acc -= (value of src in lane K of this lane's 16-lane row) * m, the negation as the DPP form's src1 modifier (no
+// v_xor / v_mov pair for -m on the pivot chain). No hazard nop: in Tall16 every use's m waits on the pivot's
+// reciprocal chain, which starts from a DPP read of the same src, so src's last VALU write is many instructions back.
+template <int K>
+__device__ __forceinline__ void fnmac_bcast16(double& acc, double src, double m) {
+    asm("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(src), "v"(m), "n"(K));
+}
+template <int J, int K>
+struct FnmacRow16 {
+    __device__ __forceinline__ static void run(double* row, double a, double l) {
+        fnmac_bcast16<K>(row[K], a, l);
+        FnmacRow16<J, K + 1>::run(row, a, l);
+    }
+};
 template <int J>
-struct BackUpd16 {
-    __device__ __forceinline__ static void run(double& sy, double v, const double* mt) {
-        fmac_bcast16<J, J == 0>(sy, v, mt[J]);
-        BackUpd16<J + 1>::run(sy, v, mt);
-    }
+struct FnmacRow16<J, NB> {
+    __device__ __forceinline__ static void run(double*, double, double) {}
 };
-template <>
-struct BackUpd16<NB> {
-    __device__ __forceinline__ static void run(double&, double, const double*) {}
+template <int J>
+struct FnmacRow16<J, NB + 1> {
+    __device__ __forceinline__ static void run(double*, double, double) {}
 };
-
-// X = L11^-1 by columns, lane c holding column c (x[r] = X(r, c)): x[R] -= L(R, J) x[J] for J < R, L(R, J) broadcast
-// from lane R (row[J] there) into the FMA
-template <int R, int J>
-struct Inv16 {
+// X = L11^-1 by columns in right-looking order (lane c: x[r] = X(r, c)): for J, x[R] -= L(R, J) x[J], R > J, with
+// L(R, J) broadcast from lane R (row[J] there: loaded from LDS, no VALU write to wait on). Each x[R] sees the same
+// updates in the same order as Inv16 (bit-identical), but consecutive DPP FMAs no longer share an accumulator.
+template <int J, int R>
+struct InvR16 {
     __device__ __forceinline__ static void run(double* x, const double* row) {
-        // row[] is final since the factorization (no write of it in the hazard window)
-        fmac_bcast16<R, false>(x[R], row[J], -x[J]);
-        Inv16<R, J + 1>::run(x, row);
+        fnmac_bcast16<R>(x[R], row[J], x[J]);
+        InvR16<J, R + 1>::run(x, row);
     }
 };
-template <int R>
-struct Inv16<R, R> {
-    __device__ __forceinline__ static void run(double* x, const double* row) { Inv16<R + 1, 0>::run(x, row); }
+template <int J>
+struct InvR16<J, NB> {
+    __device__ __forceinline__ static void run(double* x, const double* row) { InvR16<J + 1, J + 2>::run(x, row); }
 };
 template <>
-struct Inv16<NB, 0> {
+struct InvR16<NB - 1, NB> {
     __device__ __forceinline__ static void run(double*, const double*) {}
 };
+template <int J>
+struct Tall16 {
+    __device__ __forceinline__ static void run(double* dr, double* pr, double& yd, double& yp, double& dmine, int il) {
+        const double a = dr[J];
+        const double dj = bcast16_d(a, J);
+        if (il == J) dmine = dj;
+        // the pivot's reciprocal: v_rcp_f64 and one third-order correction inv0 (1 + e + e^2), e = 1 - dj inv0 (the
+        // seed's error cubed: well under an ulp) — three dependent FMAs on the chain instead of four. A zero pivot
+        // is not masked: it fails the factorization (sh.fail), whose L and y nothing reads.
+        const double inv0 = __builtin_amdgcn_rcp(dj);
+        const double e = fma(-dj, inv0, 1.0);
+        const double inv = fma(inv0, fma(e, e, e), inv0);
+        const double l = a * inv, lp = pr[J] * inv;
+        const double yj = bcast16_d(yd, J);   // y_J final (steps 0 .. J - 1 applied)
+        // the next pivot's column first, as a DPP move (independent of l: issued early) + a plain FMA: a dependent
+        // v_fmac_f64_dpp takes ~40 cycles to its result on gfx950, the move + FMA pair ~16 (scripts/valu_probe.hip)
+        if constexpr (J + 1 < NB) dr[J + 1] = fma(-l, bcast16_d(a, J + 1), dr[J + 1]);
+        FnmacRow16<J, J + 2>::run(dr, a, l);
+        FnmacRow16<J, J + 1>::run(pr, a, lp);
+        if (il > J) {
+            dr[J] = l;
+            yd = fma(-l, yj, yd);
+        }
+        pr[J] = lp;
+        yp = fma(-lp, yj, yp);
+        Tall16<J + 1>::run(dr, pr, yd, yp, dmine, il);
+    }
+};
+template <>
+struct Tall16<NB> {
+    __device__ __forceinline__ static void run(double*, double*, double&, double&, double&, int) {}
+};
 
-// wave 0: LDL^T of diagonal tile sd of the pool, written back in place (L below, D on the diagonal, and L^-T above it
-// for the backward solve), dk / invdk, M = L11^-T D^-1 (row-major, sh.Ld) for the panel rows (L21 = A21 M, an MFMA
-// product instead of a per-row forward substitution), and the forward block solve of y
-__device__ __forceinline__ void tiles_diag(double* TL, int sd, int kb, double* Y, LdltShared& sh, double* dkp,
-                                           int lane) {
-    double* T = TL + (size_t)sd * 256;
-    double row[NB];
+// One tall-panel item of block column kc: the diagonal tile + the column's non-zero tiles clist[kc][4 q + g] (g = 0..3)
+// factored; the item-0 wave stores the diagonal tile (L below, D on it; the upper triangle is left to the inverse
+// pass), dk and y_kc, every group its panel tile's L and y rows
+__device__ __forceinline__ void tall_panel(double* TL, const int16_t* slot, int nt, int kc, int q, double* Y,
+                                           LdltShared& sh, double* dkp, int lane) {
+    const int g = lane >> 4, il = lane & 15, kb = NB * kc;
+    const int ncl = sh.ccount[kc];
+    const int ip = 4 * q + g;
+    const int r = ip < ncl ? sh.clist[kc * 40 + ip] : -1;
+    double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
+    double* Tp = TL + (size_t)slot[(r >= 0 ? r : kc) * nt + kc] * 256;
+    double dr[NB], pr[NB];
 #pragma unroll
-    for (int c = 0; c < NB; c++) row[c] = lane < NB ? T[tsw(lane, c)] : 0.0;
-    const double dmine = diag16_factor(row, lane);
-    const double yv = diag16_forward(row, lane < NB ? Y[kb + lane] : 0.0, lane);
-    const double invd = dmine != 0.0 ? 1.0 / dmine : 0.0;
-    double x[NB];
+    for (int c = 0; c < NB; c++) {
+        dr[c] = Td[tsw(il, c)];
+        pr[c] = r >= 0 ? Tp[tsw(il, c)] : 0.0;
+    }
+    double yd = Y[kb + il], yp = r >= 0 ? Y[NB * r + il] : 0.0;
+    double dmine = 1.0;
+    Tall16<0>::run(dr, pr, yd, yp, dmine, il);
+    if (q == 0 && g == 0) {
 #pragma unroll
-    for (int r = 0; r < NB; r++) x[r] = (r == lane) ? 1.0 : 0.0;
-    Inv16<1, 0>::run(x, row);
-    // lane c: row c of L^-T is column c of X; M(c, r) = X(r, c) / d_r with 1 / d_r broadcast from lane r (DPP, no LDS
-    // round trip)
-    double m[NB];
-#pragma unroll
-    for (int r = 0; r < NB; r++) m[r] = x[r] * bcast16_d(invd, r);
-    if (lane < NB) {
-        // one unconditional store per entry of the tile: L below the diagonal, D on it, L^-T above it (the backward
-        // solve's block); then M
-#pragma unroll
-        for (int c = 0; c < NB; c++) T[tsw(lane, c)] = c < lane ? row[c] : (c == lane ? dmine : x[c]);
-        dkp[lane] = dmine;
-        Y[kb + lane] = yv;
+        for (int c = 0; c < NB; c++)
+            if (c <= il) Td[tsw(il, c)] = c < il ? dr[c] : dmine;
+        dkp[il] = dmine;
+        Y[kb + il] = yd;
         if (dmine == 0.0) sh.fail = 1;
+    }
+    if (r >= 0) {
 #pragma unroll
-        for (int r = 0; r < NB; r++) sh.Ld[lane * NB + r] = m[r];
+        for (int c = 0; c < NB; c++) Tp[tsw(il, c)] = pr[c];
+        Y[NB * r + il] = yp;
     }
 }
 
@@ -1709,75 +1756,70 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         sh.rcount[k] = (uint8_t)nr;
     }
     __syncthreads();
-    if (wid == 0) tiles_diag(TL, slot[0], 0, Y, sh, sh.dk[0], lane);
-    __syncthreads();
     LPROF(0);
-    for (int kc = 0, p = 0; kc < nt; kc++, p ^= 1) {
-        const int kb = NB * kc;
-        const double* dkp = sh.dk[p];
-        // (B) panel rows: one wave per non-zero tile (r, kc), r > kc: L21 = A21 M (M = L11^-T D^-1 from the diagonal
-        // factorization) as four f64 MFMAs, in place; then y_r -= L21 y_kc, one row per lane
-        {
-            const int col = lane & 15, rq = lane >> 4, ncl = sh.ccount[kc];
-            for (int i = wid; i < ncl; i += NW) {   // wave 0 takes the first: row kc + 1 when it is non-zero
-                const int r = sh.clist[kc * 40 + i];
-                const int s = slot[r * nt + kc];
-                double* Tr = TL + (size_t)s * 256;
-                dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int k0 = 0; k0 < NB; k0 += 4) {
-                    const int k = k0 + rq;
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tsw(col, k)], sh.Ld[k * NB + col], acc, 0, 0, 0);
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++) Tr[tsw(rq + 4 * q, col)] = acc[q];
-                if (lane < NB) {
-                    const int gi = NB * r + lane;
-                    double yi = Y[gi];
-#pragma unroll
-                    for (int j = 0; j < NB; j++) yi = fma(-Tr[tsw(lane, j)], Y[kb + j], yi);
-                    Y[gi] = yi;
-                }
+    // per block column kc, phase A: the tall-panel items of column kc (waves 0 ..) beside the rest of column kc - 1's
+    // trailing update (the tiles (r, c), c >= kc + 1, by the other waves first); barrier; phase B (when L(kc + 1, kc) is
+    // non-zero): column kc + 1's tiles updated by L(., kc) — what the next panel reads; barrier. Every tile still sees
+    // its panels' updates in panel order.
+    for (int kc = 0; kc < nt; kc++) {
+        const int ncl = sh.ccount[kc];
+        const int np = (ncl + 3) / 4 > 0 ? (ncl + 3) / 4 : 1;
+#ifdef MAM_LDLT_PROFILE
+        const long long td = clock64();
+#endif
+        for (int q = wid; q < np; q += NW) tall_panel(TL, slot, nt, kc, q, Y, sh, sh.dk[kc & 1], lane);
+#ifdef MAM_LDLT_PROFILE
+        if (t == 0) atomicAdd(&g_lprof[5], (unsigned long long)(clock64() - td));
+#endif
+        if (kc > 0) {   // column kc - 1's pairs (a >= b) whose column c = clist[b] >= kc + 1
+            const int kp = kc - 1, nclp = sh.ccount[kp];
+            const int b0 = (nclp > 0 && sh.clist[kp * 40] == kc) ? 1 : 0;
+            const int m = nclp - b0, n2 = m * (m + 1) / 2;
+            for (int i = (wid - np % NW + NW) % NW; i < n2; i += NW) {
+                int a, b;
+                tri_index(i, &a, &b);
+                const int r = sh.clist[kp * 40 + a + b0], c = sh.clist[kp * 40 + b + b0];
+                tile_update(TL, slot[r * nt + c], slot[r * nt + kp], slot[c * nt + kp], sh.dk[kp & 1], lane);
             }
         }
         __syncthreads();
         LPROF(1);
         if (kc + 1 == nt) break;
-        // (C) wave 0: the next diagonal tile, updated by L(kc + 1, kc) D L(kc + 1, kc)^T, then factored (the critical
-        // path: no barrier between); the other waves: every other trailing tile (r, c), kc + 1 <= c <= r, (r, c) !=
-        // (kc + 1, kc + 1), updated by L(r, kc) D L(c, kc)^T
-        if (wid == 0) {
-#ifdef MAM_LDLT_PROFILE
-            const long long td = clock64();
-#endif
-            const int s_n = slot[(kc + 1) * nt + kc];
-            const int sd = slot[(kc + 1) * nt + kc + 1];
-            if (s_n >= 0) tile_update(TL, sd, s_n, s_n, dkp, lane);
-            tiles_diag(TL, sd, kb + NB, Y, sh, sh.dk[p ^ 1], lane);
-#ifdef MAM_LDLT_PROFILE
-            if (lane == 0) atomicAdd(&g_lprof[5], (unsigned long long)(clock64() - td));
-#endif
-        } else {
-            // the pairs (a >= b) of the column's non-zero rows; pair (0, 0) is the diagonal tile when row kc + 1 is
-            // among them (wave 0's)
-            const int ncl = sh.ccount[kc];
-            const int q0 = (ncl > 0 && sh.clist[kc * 40] == kc + 1) ? 1 : 0;
-            const int n2 = ncl * (ncl + 1) / 2;
-            for (int q = q0 + wid - 1; q < n2; q += NW - 1) {
-                int a, b;
-                tri_index(q, &a, &b);
-                const int r = sh.clist[kc * 40 + a], c = sh.clist[kc * 40 + b];
-                tile_update(TL, slot[r * nt + c], slot[r * nt + kc], slot[c * nt + kc], dkp, lane);
+        if (ncl > 0 && sh.clist[kc * 40] == kc + 1) {   // uniform
+            const int sb = slot[(kc + 1) * nt + kc];
+            for (int a = wid; a < ncl; a += NW) {
+                const int r = sh.clist[kc * 40 + a];
+                tile_update(TL, slot[r * nt + kc + 1], slot[r * nt + kc], sb, sh.dk[kc & 1], lane);
             }
+            __syncthreads();
         }
-        __syncthreads();
         LPROF(3);
     }
     const int fl = sh.fail;
     if (t == 0) lm.fail = fl;
     if (fl) return;   // uniform (LDS flag after the last barrier)
+    // the diagonal tiles' L^-T into their upper triangles (the backward solve's blocks): one tile per 16-lane group
+    {
+        const int g = lane >> 4, il = lane & 15;
+        for (int k0 = 4 * wid; k0 < nt; k0 += 4 * NW) {
+            const int kc = k0 + g;
+            if (kc >= nt) continue;   // uniform per 16-lane group (the DPP rows)
+            double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
+            double row[NB], x[NB];
+#pragma unroll
+            for (int c = 0; c < NB; c++) {
+                row[c] = Td[tsw(il, c)];
+                x[c] = (c == il) ? 1.0 : 0.0;
+            }
+            InvR16<0, 1>::run(x, row);
+#pragma unroll
+            for (int c = 0; c < NB; c++)
+                if (c > il) Td[tsw(il, c)] = x[c];
+        }
+    }
+    __syncthreads();
     // y /= D and the backward substitution L^T x = y by wave 0 alone (a wave's LDS accesses complete in order, so no
-    // barrier): per block x_b = L11^-T y_b from the diagonal tile's upper triangle (written by tiles_diag), then
+    // barrier): per block x_b = L11^-T y_b from the diagonal tile's upper triangle (written by the inverse pass), then
     // y_i -= L(kb.., i)^T x_b for the rows i of the block row's non-zero tiles, four tiles per pass
     if (wid != 0) return;
     for (int i = lane; i < N; i += 64) {
@@ -1799,6 +1841,11 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         }
         if (lane < NB) Y[kb + lane] = v;
         const int nrl = sh.rcount[kc];
+        // x_j in every lane of the row by DPP moves once per block, then plain FMAs: the same roundings as
+        // v_fmac_f64_dpp, without its ~40-cycle dependent latency on the 16-long accumulation chain
+        double xb[NB];
+#pragma unroll
+        for (int j = 0; j < NB; j++) xb[j] = bcast16_d(v, j);
         for (int i0 = 0; i0 < nrl; i0 += 4) {
             const int i = i0 + g;
             const int c = i < nrl ? sh.rlist[kc * 40 + i] : -1;   // L(kb.., 16 c..) not structurally zero
@@ -1809,7 +1856,8 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
 #pragma unroll
             for (int j = 0; j < NB; j++) mt[j] = -Tr[tsw(j, il)];
             double sy = Y[yi];
-            BackUpd16<0>::run(sy, v, mt);   // sy = fma(-L(kb + j, yi), x_j, sy), j = 0 .. 15, in order
+#pragma unroll
+            for (int j = 0; j < NB; j++) sy = fma(xb[j], mt[j], sy);   // sy -= L(kb + j, yi) x_j, j in order
             if (c >= 0) Y[yi] = sy;
         }
     }
