@@ -1714,7 +1714,8 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     // after the unknowns: S's padding rows are zero). One wave per tile, lane = (row, 4 columns): two 16-byte loads per
     // lane, the wave's tiles' loads issued together
     {
-        constexpr int U = 6;   // tiles per wave per pass (12 loads of 16 bytes in flight per lane)
+        constexpr int U = 10;   // tiles per wave per pass (20 loads of 16 bytes in flight per lane: a 50-KF window's
+                                // ~70 tiles in one pass)
         const int i = lane >> 2, j0 = 4 * (lane & 3);
         for (int s0 = wid; s0 < T; s0 += U * NW) {
             double2 v[U][2];
@@ -2436,7 +2437,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     // the host reads the states back once per chunk (the first chunk sized by the trials recent solves took).
     int max_slots = 0;
     for (auto& l : lm0) max_slots = std::max(max_slots, 10 * std::max(l.iterations, 0));
-    int chunk = std::max(1, (int)std::ceil(c->trials_ema));
+    int chunk = std::max(1, (int)std::lround(c->trials_ema));   // nearest: a ceil of 9.02 enqueued a 10th slot
     int enq = 0;
     LM* lh = reinterpret_cast<LM*>(c->lm_host.p + pb);
     bool was_stopped = false;
@@ -2686,15 +2687,19 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     lm0[0].iterations = p->iterations;
     std::vector<Outs> outs{o};
     if (int rc = run_batch(c, hp, lm0, outs, stop_flag, s, r)) return rc;
-    // results back to the caller's order
-    std::vector<double> q(4 * (size_t)P), t(3 * (size_t)P), x(3 * (size_t)L), chi(o.chi2 ? E : 0);
-    std::vector<uint8_t> dep(o.depth ? E : 0);
-    if (P) MAM_HIP(hipMemcpyAsync(q.data(), o.q, 32 * (size_t)P, hipMemcpyDeviceToHost, s));
-    if (P) MAM_HIP(hipMemcpyAsync(t.data(), o.t, 24 * (size_t)P, hipMemcpyDeviceToHost, s));
-    if (L) MAM_HIP(hipMemcpyAsync(x.data(), o.xyz, 24 * (size_t)L, hipMemcpyDeviceToHost, s));
-    if (o.chi2 && E) MAM_HIP(hipMemcpyAsync(chi.data(), o.chi2, 8 * (size_t)E, hipMemcpyDeviceToHost, s));
-    if (o.depth && E) MAM_HIP(hipMemcpyAsync(dep.data(), o.depth, (size_t)E, hipMemcpyDeviceToHost, s));
+    // results back to the caller's order: one D2H copy of the output region into the pinned staging block (pageable
+    // destinations were one staged, synchronous copy each)
+    if (dv.off > upload) MAM_HIP(hipMemcpyAsync(hb + upload, c->io.p + upload, dv.off - upload, hipMemcpyDeviceToHost, s));
     MAM_HIP(hipStreamSynchronize(s));
+    auto host_of = [&](auto* dptr) {
+        using T = std::remove_cv_t<std::remove_pointer_t<decltype(dptr)>>;
+        return reinterpret_cast<const T*>(hb + (reinterpret_cast<const uint8_t*>(dptr) - c->io.p));
+    };
+    const double* q = host_of(o.q);
+    const double* t = host_of(o.t);
+    const double* x = host_of(o.xyz);
+    const double* chi = o.chi2 ? host_of(o.chi2) : nullptr;
+    const uint8_t* dep = o.depth ? host_of(o.depth) : nullptr;
     if (r->status < 0) return r->status;
     for (int i = 0; i < P; i++) {
         const int d = po[i];
