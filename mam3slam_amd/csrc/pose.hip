@@ -9,8 +9,9 @@
 // widened to double where used) next to each edge's last error (2 doubles, the stale-after-rejected-trial value
 // g2o's chi2() reads) and its level (0 active, 1 outlier). Every pass deals the edges to the PT threads; the
 // per-thread partial sums (robust chi2, or the 21 upper entries of H plus b) are reduced by a fixed DPP pattern
-// per wave and a fixed wave order, so every thread ends with the same bits and runs the LM control flow, the 6x6
-// pivoted LDL^T and the SE3 update redundantly: no host round trip, no broadcast, block-uniform branches.
+// per wave and a fixed wave order, so every thread ends with the same bits and runs the LM control flow; the 6x6
+// pivoted LDL^T and the SE3 update run redundantly in every wave when there is one wave per SIMD, on wave 0 with an LDS
+// broadcast when there are more (no host round trip, block-uniform branches).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,12 +29,20 @@
 namespace mam {
 namespace pose {
 
+// threads per frame, per camera model: Pinhole 512 (two waves per SIMD hide the edge passes' FP64 latency; the serial
+// LM step then runs on wave 0 only: batch of 16 c2 frames 0.423 -> 0.368 ms), KannalaBrandt8 256 (its projection and
+// Jacobian spill at 512's register budget); 1024 spills either way
 #ifndef MAM_POSE_THREADS
-#define MAM_POSE_THREADS 256
+#define MAM_POSE_THREADS 512
 #endif
-constexpr int PT = MAM_POSE_THREADS;   // threads per frame (512 / 1024 measured slower: the LM step of every trial
-                                       // runs redundantly in every wave, and 1024 spills)
-constexpr int NW = PT / 64;
+#ifndef MAM_POSE_THREADS_KB8
+#define MAM_POSE_THREADS_KB8 256
+#endif
+template <bool KB8>
+struct Cfg {
+    static constexpr int PT = KB8 ? MAM_POSE_THREADS_KB8 : MAM_POSE_THREADS;
+    static constexpr int NW = PT / 64;
+};
 constexpr int NRED = 27;       // 21 upper entries of H + 6 of b
 
 struct Args {
@@ -105,7 +114,7 @@ __device__ __forceinline__ void wave_sum_scatter4(const double (&v)[4 * Q], doub
 
 // Block sum of N per-thread values into out[0..N) (LDS; waves summed in order 0..NW-1, a fixed pattern inside a
 // wave, so the bits do not depend on timing). Ends with a barrier: out[] is readable by every thread.
-template <int N>
+template <int N, int NW>
 __device__ __forceinline__ void block_sum(const double (&v)[N], double* scr, double* out) {
     const int w = threadIdx.x >> 6;
     if constexpr (N % 4 == 0 && N >= 8) {
@@ -187,6 +196,7 @@ __device__ unsigned long long g_pprof[8];
 template <bool KB8>
 __device__ double active_chi(const Edges& E, const double T[7], const mam_camera& c, bool robust, double delta,
                              double* scr) {
+    constexpr int PT = Cfg<KB8>::PT, NW = Cfg<KB8>::NW;
     double acc[1] = {0.0};
 #pragma unroll 2
     for (int i = threadIdx.x; i < E.n; i += PT) {
@@ -199,7 +209,7 @@ __device__ double active_chi(const Edges& E, const double T[7], const mam_camera
         rho_of(chi, robust, delta, &r0, &r1);
         acc[0] += r0;
     }
-    block_sum<1>(acc, scr, scr + NW * (NRED + 1));
+    block_sum<1, NW>(acc, scr, scr + NW * (NRED + 1));
     return scr[NW * (NRED + 1)];
 }
 
@@ -208,6 +218,7 @@ __device__ double active_chi(const Edges& E, const double T[7], const mam_camera
 template <bool KB8>
 __device__ double build_system(const Edges& E, const double T[7], const mam_camera& c, bool robust, double delta,
                                double* scr, double* red) {
+    constexpr int PT = Cfg<KB8>::PT, NW = Cfg<KB8>::NW;
     double acc[NRED + 1];
 #pragma unroll
     for (int k = 0; k <= NRED; k++) acc[k] = 0.0;
@@ -282,7 +293,7 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
         for (int a = 0; a < 6; a++) acc[21 + a] += A[a] * o0 + A[6 + a] * o1;
     }
     PPROF(7, tb);   // the edge loop alone (thread 0's view)
-    block_sum<NRED + 1>(acc, scr, red);
+    block_sum<NRED + 1, NW>(acc, scr, red);
     return red[NRED];
 }
 
@@ -394,6 +405,7 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
 template <bool KB8>
 __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool robust, double delta, double* scr,
                         int* trials) {
+    constexpr int PT = Cfg<KB8>::PT, NW = Cfg<KB8>::NW;
     // initializeOptimization(0): no level-0 edge -> optimize() returns -1 before the loop
     __shared__ int s_any;
     if (threadIdx.x == 0) s_any = 0;
@@ -435,11 +447,36 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
         do {
             double x[6];
             PPROF(4, tp);   // LM control since the last pass
-            const bool ok2 = ldlt6(red, lambda, x);
-            PPROF(1, tp);
+            bool ok2;
             double Tn[7];
-            se3::exp_mul(x, T, Tn);
-            PPROF(2, tp);
+            if constexpr (NW > 4) {
+                // more waves than SIMDs: the serial step on wave 0 only (redundant copies would share its SIMD's
+                // issue slots), x / Tn / the verdict broadcast through LDS
+                __shared__ double s_step[14];
+                if (threadIdx.x < 64) {
+                    ok2 = ldlt6(red, lambda, x);
+                    se3::exp_mul(x, T, Tn);
+                    if (threadIdx.x == 0) {
+#pragma unroll
+                        for (int k = 0; k < 6; k++) s_step[k] = x[k];
+#pragma unroll
+                        for (int k = 0; k < 7; k++) s_step[6 + k] = Tn[k];
+                        s_step[13] = ok2 ? 1.0 : 0.0;
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < 6; k++) x[k] = s_step[k];
+#pragma unroll
+                for (int k = 0; k < 7; k++) Tn[k] = s_step[6 + k];
+                ok2 = s_step[13] != 0.0;
+                PPROF(2, tp);
+            } else {
+                ok2 = ldlt6(red, lambda, x);
+                PPROF(1, tp);
+                se3::exp_mul(x, T, Tn);
+                PPROF(2, tp);
+            }
             double tempChi = active_chi<KB8>(E, Tn, c, robust, delta, scr);
             PPROF(3, tp);
 #ifdef MAM_POSE_PROFILE
@@ -478,7 +515,8 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
 
 // the camera model is a template parameter: a Pinhole launch carries no KannalaBrandt8 code in its edge loops
 template <bool KB8>
-__global__ __launch_bounds__(PT) void k_pose_opt(Args a) {
+__global__ __launch_bounds__(Cfg<KB8>::PT) void k_pose_opt(Args a) {
+    constexpr int PT = Cfg<KB8>::PT, NW = Cfg<KB8>::NW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ double scr[NW * (NRED + 1) + 8 + NRED + 1];   // wave partials | chi sum | H, b, chi sums
     __shared__ int s_nbad;
@@ -743,9 +781,9 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_p
     {
         mam::StageTimer::Scope sc(&c->timer, s, 0);
         if (cam->model == MAM_CAM_KANNALA_BRANDT8)
-            hipLaunchKernelGGL(mam::pose::k_pose_opt<true>, dim3(nframes), dim3(mam::pose::PT), lds, s, a);
+            hipLaunchKernelGGL(mam::pose::k_pose_opt<true>, dim3(nframes), dim3(mam::pose::Cfg<true>::PT), lds, s, a);
         else
-            hipLaunchKernelGGL(mam::pose::k_pose_opt<false>, dim3(nframes), dim3(mam::pose::PT), lds, s, a);
+            hipLaunchKernelGGL(mam::pose::k_pose_opt<false>, dim3(nframes), dim3(mam::pose::Cfg<false>::PT), lds, s, a);
     }
     MAM_HIP(hipGetLastError());
 #ifdef MAM_POSE_PROFILE
