@@ -1834,16 +1834,23 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         // row by DPP instead of an LDS round trip
         const double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
         double v = Y[kb + il];
-        // predicated, not branched: every lane's loads issue together (a branch per j was one LDS round trip each)
+        // predicated, not branched: every lane's loads issue together (a branch per j was one LDS round trip each);
+        // two independent partial sums (j < 8, j >= 8) halve the dependent FMA chain (~10 cycles a link)
+        double v1 = 0.0;
 #pragma unroll
-        for (int j = 1; j < NB; j++) {
+        for (int j = 1; j < NB / 2; j++) {
             const double f = fma(Td[tsw(il, j)], Y[kb + j], v);
             v = j > il ? f : v;
         }
+#pragma unroll
+        for (int j = NB / 2; j < NB; j++) {
+            const double f = fma(Td[tsw(il, j)], Y[kb + j], v1);
+            v1 = j > il ? f : v1;
+        }
+        v += v1;
         if (lane < NB) Y[kb + lane] = v;
         const int nrl = sh.rcount[kc];
-        // x_j in every lane of the row by DPP moves once per block, then plain FMAs: the same roundings as
-        // v_fmac_f64_dpp, without its ~40-cycle dependent latency on the 16-long accumulation chain
+        // x_j in every lane of the row by DPP moves once per block, then plain FMAs
         double xb[NB];
 #pragma unroll
         for (int j = 0; j < NB; j++) xb[j] = bcast16_d(v, j);
@@ -1858,7 +1865,11 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             for (int j = 0; j < NB; j++) mt[j] = -Tr[tsw(j, il)];
             double sy = Y[yi];
 #pragma unroll
-            for (int j = 0; j < NB; j++) sy = fma(xb[j], mt[j], sy);   // sy -= L(kb + j, yi) x_j, j in order
+            for (int j = 0; j < NB / 2; j++) sy = fma(xb[j], mt[j], sy);   // sy -= L(kb + j, yi) x_j: two partial
+            double sy1 = 0.0;                                               // chains of 8 (j < 8, j >= 8)
+#pragma unroll
+            for (int j = NB / 2; j < NB; j++) sy1 = fma(xb[j], mt[j], sy1);
+            sy += sy1;
             if (c >= 0) Y[yi] = sy;
         }
     }
