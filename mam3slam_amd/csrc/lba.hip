@@ -340,19 +340,36 @@ __global__ __launch_bounds__(SB) void k_struct_init(const Prob* __restrict__ pro
     for (int i = g0; i < 3 * d.L; i += gstride) d.pt[0][i] = d.point_xyz[i];
 }
 
-// grid (ceil(E/256), Q): per-point and per-pose edge counts; index validation
+// grid (ceil(E/256), Q): per-point and per-pose edge counts; index validation. The pose counts go through a
+// per-workgroup LDS histogram first (one device atomic per pose present in the workgroup instead of one per edge: a
+// window's ~50 pose counters each took ~500 device atomics in turn, the contended part of the structure build)
+constexpr int STRUCT_HIST = 512;   // poses the LDS histogram holds (larger windows: device atomics per edge)
 __global__ __launch_bounds__(256) void k_struct_count(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
+    if (d.lm->status) return;
+    __shared__ int hist[STRUCT_HIST];
+    const bool lds_hist = d.Np <= STRUCT_HIST;
+    if (lds_hist)
+        for (int i = threadIdx.x; i < d.Np; i += 256) hist[i] = 0;
+    __syncthreads();
     const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= d.E || d.lm->status) return;
-    const int ip = d.edge_point[e], ipose = d.edge_pose[e];
-    if (ip < 0 || ip >= d.L || ipose < 0 || ipose >= d.P) {
-        d.lm->status = MAM_ERR_ARG;
-        return;
+    if (e < d.E) {
+        const int ip = d.edge_point[e], ipose = d.edge_pose[e];
+        if (ip < 0 || ip >= d.L || ipose < 0 || ipose >= d.P) {
+            d.lm->status = MAM_ERR_ARG;
+        } else {
+            atomicAdd(&d.cnt[ip], 1);
+            const int h = d.pose_h[ipose];
+            if (h >= 0) {
+                if (lds_hist) atomicAdd(&hist[h], 1);
+                else atomicAdd(&d.cnt[d.L + h], 1);
+            }
+        }
     }
-    atomicAdd(&d.cnt[ip], 1);
-    const int h = d.pose_h[ipose];
-    if (h >= 0) atomicAdd(&d.cnt[d.L + h], 1);
+    __syncthreads();
+    if (lds_hist)
+        for (int i = threadIdx.x; i < d.Np; i += 256)
+            if (hist[i]) atomicAdd(&d.cnt[d.L + i], hist[i]);
 }
 
 __device__ void block_excl_scan(const int32_t* in, int32_t* out, int n, int32_t* total_out) {
@@ -395,18 +412,34 @@ __global__ __launch_bounds__(SB) void k_struct_scan(const Prob* __restrict__ pro
     for (int i = threadIdx.x; i < d.L + d.Np; i += SB) d.cnt[i] = 0;
 }
 
-// grid (ceil(E/256), Q): scatter into the lists (order fixed by k_struct_sort) and the pose x point table
+// grid (ceil(E/256), Q): scatter into the lists (order fixed by k_struct_sort) and the pose x point table; a pose's
+// slots for the workgroup's edges reserved by one device atomic (the LDS histogram's count), ranks from LDS atomics
 __global__ __launch_bounds__(256) void k_struct_scatter(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
+    if (d.lm->status) return;
+    __shared__ int hist[STRUCT_HIST];
+    const bool lds_hist = d.Np <= STRUCT_HIST;
+    if (lds_hist)
+        for (int i = threadIdx.x; i < d.Np; i += 256) hist[i] = 0;
+    __syncthreads();
     const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= d.E || d.lm->status) return;
-    const int ip = d.edge_point[e];
-    d.pe_idx[d.pe_off[ip] + atomicAdd(&d.cnt[ip], 1)] = e;
-    const int h = d.pose_h[d.edge_pose[e]];
-    if (h >= 0) {
-        d.qe_idx[d.qe_off[h] + atomicAdd(&d.cnt[d.L + h], 1)] = e;
-        d.eidx[(size_t)h * d.L + ip] = e;
+    int h = -1, r = 0, ip = 0;
+    if (e < d.E) {
+        ip = d.edge_point[e];
+        d.pe_idx[d.pe_off[ip] + atomicAdd(&d.cnt[ip], 1)] = e;
+        h = d.pose_h[d.edge_pose[e]];
+        if (h >= 0) {
+            d.eidx[(size_t)h * d.L + ip] = e;
+            if (lds_hist) r = atomicAdd(&hist[h], 1);
+            else d.qe_idx[d.qe_off[h] + atomicAdd(&d.cnt[d.L + h], 1)] = e;
+        }
     }
+    if (!lds_hist) return;   // uniform
+    __syncthreads();
+    for (int i = threadIdx.x; i < d.Np; i += 256)
+        if (hist[i]) hist[i] = atomicAdd(&d.cnt[d.L + i], hist[i]);   // the workgroup's base in pose i's list
+    __syncthreads();
+    if (h >= 0) d.qe_idx[d.qe_off[h] + hist[h] + r] = e;
 }
 
 // grid (ceil(L/256) + Np, Q) x 256: restore edge order inside every list — per point an insertion sort by one thread
@@ -428,13 +461,29 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
             s[m + 1] = v;
         }
         // per slot / per edge metadata the per-trial kernels read with one load instead of a chain of dependent ones
+        constexpr int NR = 8;   // a window's points: <= 8 observations, their pose blocks kept in registers
+        int hpv[NR];
+#pragma unroll
+        for (int a = 0; a < NR; a++) hpv[a] = -1;
         for (int a = 0; a < n; a++) {
             const int e = s[a];
             const int hp = d.pose_h[d.edge_pose[e]];
             d.slot_hp[d.pe_off[h] + a] = hp;
             d.emeta[e] = make_int4(h, hp, a == 0 ? 1 : 0, 0);
+#pragma unroll
+            for (int k = 0; k < NR; k++) hpv[k] = k == a ? hp : hpv[k];
         }
         // the S blocks this landmark contributes to (g2o's BlockSolver keeps only these, block_solver.hpp:181-224)
+        if (n <= NR) {   // from the registers (the general loop reloads through the stores it may alias)
+#pragma unroll
+            for (int a = 0; a < NR; a++)
+#pragma unroll
+                for (int b = a + 1; b < NR; b++) {
+                    const int ha = hpv[a], hb = hpv[b];
+                    if (ha >= 0 && hb >= 0 && hb != ha) d.pairmask[(size_t)min(ha, hb) * d.Np + max(ha, hb)] = 1;
+                }
+            return;
+        }
         for (int a = 0; a < n; a++) {
             const int ha = d.pose_h[d.edge_pose[s[a]]];
             if (ha < 0) continue;
@@ -701,7 +750,8 @@ __global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
     double m = sys_body(d);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
-    if (threadIdx.x == 0 && m > 0.0) atomicMax(&lm.maxdiag, (unsigned long long)__double_as_longlong(m));
+    // only the first iteration's max is read (lambda_0, trial_lambda): later iterations skip the contended atomics
+    if (threadIdx.x == 0 && m > 0.0 && lm.its == 0) atomicMax(&lm.maxdiag, (unsigned long long)__double_as_longlong(m));
 }
 
 // ---- Schur
@@ -2032,7 +2082,9 @@ __global__ __launch_bounds__(UPD_T) void k_backsub_update(const Prob* __restrict
 }
 
 // grid (Q) x 256: end of a trial — levenberg.cpp:108-158 (rho, accept / reject, lambda), then the iteration-end
-// tests of levenberg.cpp:159-168 and sparse_optimizer.cpp:381-409.
+// tests of levenberg.cpp:159-168 and sparse_optimizer.cpp:381-409. (Run instead by the last workgroup of the trial's
+// k_linearize, the kernel boundary replaced by a release / acquire per workgroup, the batch of 32 took 5.6 -> 9.5 ms:
+// every workgroup's agent-scope release writes its L2 back.)
 __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs) {
     constexpr int T = RED;
     __shared__ double s[RED];
