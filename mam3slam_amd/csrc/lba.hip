@@ -2668,11 +2668,14 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     MAM_DEVICE_SCOPE(c->device);
     // g2o's Hessian order = vertices sorted by id (sparse_optimizer.cpp:166-190): the device path takes id-ordered
     // poses and points, so permute here and map the results back
+    // (ids already ascending, as a window built in id order hands them over: identity, no sort)
     std::vector<int> po(P), pl(L), ipo(P), ipl(L);
     std::iota(po.begin(), po.end(), 0);
     std::iota(pl.begin(), pl.end(), 0);
-    std::stable_sort(po.begin(), po.end(), [&](int a, int b) { return p->pose_id[a] < p->pose_id[b]; });
-    std::stable_sort(pl.begin(), pl.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
+    if (!std::is_sorted(p->pose_id, p->pose_id + P))
+        std::stable_sort(po.begin(), po.end(), [&](int a, int b) { return p->pose_id[a] < p->pose_id[b]; });
+    if (!std::is_sorted(p->point_id, p->point_id + L))
+        std::stable_sort(pl.begin(), pl.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
     for (int i = 0; i < P; i++) ipo[po[i]] = i;
     for (int i = 0; i < L; i++) ipl[pl[i]] = i;
     int Np = 0;
