@@ -968,7 +968,8 @@ def main():
         if mapping is not None:
             workload += (f" + a keyframe every {K} frames per stream: {mapping.W} new keyframes per "
                          f"{'step' if map_every == 1 else f'{map_every} steps'}, each with "
-                         f"ComputeBoW + 30 SearchForTriangulation (CreateNewMapPoints) and a LocalBundleAdjustment window "
+                         f"ComputeBoW + 30 SearchForTriangulation (CreateNewMapPoints) + SearchInNeighbors (Fuse both ways + "
+                         f"ComputeDistinctiveDescriptors) and a LocalBundleAdjustment window "
                          f"(50 KF + fixed, ~{int(np.mean([len(p.point_id) for p in mapping.probs]))} MapPoints) "
                          f"over the shared map, batched, concurrent with tracking; write-backs exchanged and "
                          f"applied to the map the next windows read")
