@@ -14,6 +14,8 @@ pytestmark = pytest.mark.gpu
 CASES = [
     dict(n_opt=6, n_fixed=2, n_points=120, obs_per_point=4, seed=3),
     dict(n_opt=10, n_fixed=3, n_points=300, obs_per_point=6, seed=1),
+    # dense 20-KF system: 8 tile columns, 36 tiles in the LDS pool; the first columns hold 5-7 tiles below the
+    # diagonal, so their tall panels run as two items on two waves (the diagonal factored redundantly in both)
     dict(n_opt=20, n_fixed=5, n_points=1000, obs_per_point=8, seed=7, init_kf_local=False),
     dict(n_opt=50, n_fixed=10, n_points=3000, obs_per_point=8, seed=11),   # BASELINE configs[2]
     dict(n_opt=50, n_fixed=10, n_points=3000, obs_per_point=12, seed=12, outlier_frac=0.15),
