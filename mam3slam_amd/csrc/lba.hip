@@ -2678,6 +2678,9 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         std::stable_sort(pl.begin(), pl.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
     for (int i = 0; i < P; i++) ipo[po[i]] = i;
     for (int i = 0; i < L; i++) ipl[pl[i]] = i;
+    bool ident_po = true, ident_pl = true;
+    for (int i = 0; i < P && ident_po; i++) ident_po = po[i] == i;
+    for (int i = 0; i < L && ident_pl; i++) ident_pl = pl[i] == i;
     int Np = 0;
     for (int i = 0; i < P; i++) Np += p->pose_fixed[i] ? 0 : 1;
     const int ncw = (p->cam_model == MAM_CAM_KANNALA_BRANDT8 ? 8 : 4) * p->n_cams;
@@ -2708,13 +2711,15 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     auto [d_t, h_t] = put((double*)nullptr, 3 * (size_t)P);
     auto [d_x, h_x] = put((double*)nullptr, 3 * (size_t)L);
     const size_t upload = dv.off;
-    for (int e = 0; e < E; e++) {
-        h_ep[e] = ipl[p->edge_point[e]];
-        h_eo[e] = ipo[p->edge_pose[e]];
-        h_obs[2 * e] = p->edge_obs[2 * e];
-        h_obs[2 * e + 1] = p->edge_obs[2 * e + 1];
-        h_w[e] = p->edge_inv_sigma2[e];
-        if (p->edge_active) h_act[e] = p->edge_active[e];
+    // staging: plain copies when the ids are already in Hessian order, permuted copies otherwise
+    if (E) {
+        if (ident_pl) std::memcpy(h_ep, p->edge_point, sizeof(int32_t) * E);
+        else for (int e = 0; e < E; e++) h_ep[e] = ipl[p->edge_point[e]];
+        if (ident_po) std::memcpy(h_eo, p->edge_pose, sizeof(int32_t) * E);
+        else for (int e = 0; e < E; e++) h_eo[e] = ipo[p->edge_pose[e]];
+        std::memcpy(h_obs, p->edge_obs, sizeof(double) * 2 * (size_t)E);
+        std::memcpy(h_w, p->edge_inv_sigma2, sizeof(double) * E);
+        if (p->edge_active) std::memcpy(h_act, p->edge_active, E);
     }
     std::memcpy(h_cams, p->cams, sizeof(float) * ncw);
     for (int i = 0; i < P; i++) {
@@ -2724,8 +2729,10 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         for (int k = 0; k < 4; k++) h_q[4 * i + k] = p->pose_q[4 * s + k];
         for (int k = 0; k < 3; k++) h_t[3 * i + k] = p->pose_t[3 * s + k];
     }
-    for (int i = 0; i < L; i++)
-        for (int k = 0; k < 3; k++) h_x[3 * i + k] = p->point_xyz[3 * pl[i] + k];
+    if (L && ident_pl) std::memcpy(h_x, p->point_xyz, sizeof(double) * 3 * (size_t)L);
+    else
+        for (int i = 0; i < L; i++)
+            for (int k = 0; k < 3; k++) h_x[3 * i + k] = p->point_xyz[3 * pl[i] + k];
     Outs o{};
     o.q = dv.take<double>(4 * (size_t)P);
     o.t = dv.take<double>(3 * (size_t)P);
@@ -2772,8 +2779,10 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         for (int k = 0; k < 4; k++) r->pose_q[4 * d + k] = q[4 * i + k];
         for (int k = 0; k < 3; k++) r->pose_t[3 * d + k] = t[3 * i + k];
     }
-    for (int i = 0; i < L; i++)
-        for (int k = 0; k < 3; k++) r->point_xyz[3 * pl[i] + k] = x[3 * i + k];
+    if (L && ident_pl) std::memcpy(r->point_xyz, x, sizeof(double) * 3 * (size_t)L);
+    else
+        for (int i = 0; i < L; i++)
+            for (int k = 0; k < 3; k++) r->point_xyz[3 * pl[i] + k] = x[3 * i + k];
     for (int e = 0; e < E; e++) {
         if (o.chi2 && !(p->edge_active && !p->edge_active[e])) r->edge_chi2[e] = chi[e];
         if (o.depth) r->edge_depth_ok[e] = dep[e];
