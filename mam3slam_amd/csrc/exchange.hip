@@ -1,5 +1,6 @@
-// Shared-map update exchange: pack one LocalBundleAdjustment write-back into fixed-size records and apply the
-// all-gathered records of every agent in agent order (include/mam_exchange.h).
+// Shared-map update exchange: each agent packs the deduplicated write-back of its step's LocalBundleAdjustment windows
+// into one compact block, and every agent applies the all-gathered blocks in agent order (include/mam_exchange.h,
+// SURVEY.md §8(e)); plus the windows' vertex estimates read from the shared tables.
 // Reference semantics of the values: src/Optimizer.cc:1478-1494 (KeyFrame::SetPose(SE3f(q.cast<float>,
 // t.cast<float>)), MapPoint::SetWorldPos(pos.cast<float>)).
 #include <hip/hip_runtime.h>
@@ -11,94 +12,6 @@
 #include "runtime.hpp"
 
 namespace mam {
-
-// One workgroup: poses are compacted (non-fixed only, original order) with a block scan, points follow. MapPoint
-// record ids are point_id - mp_id_base (the table row).
-__device__ void pack_block(const double* __restrict__ pq, const double* __restrict__ pt,
-                           const int64_t* __restrict__ pid, const uint8_t* __restrict__ pfix, int n_poses,
-                           const double* __restrict__ xyz, const int64_t* __restrict__ mid,
-                           const uint8_t* __restrict__ mbad, int n_points, int64_t mp_id_base, int agent,
-                           mam_map_update* __restrict__ out, int capacity) {
-    __shared__ int wsum[16];
-    __shared__ int base;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid == 0) base = 0;
-    __syncthreads();
-    for (int c0 = 0; c0 < n_poses; c0 += 1024) {
-        const int i = c0 + tid;
-        const int keep = (i < n_poses && !pfix[i]) ? 1 : 0;
-        const unsigned long long m = __ballot(keep);
-        const int before = __popcll(m & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[wid] = __popcll(m);
-        __syncthreads();
-        int off = base;
-        for (int w = 0; w < wid; w++) off += wsum[w];
-        if (keep) {
-            const int r = off + before;
-            if (r < capacity) {
-                mam_map_update u;
-                u.id = pid[i];
-                u.kind = MAM_UPDATE_KF;
-                u.agent = agent;
-                float q[4];
-                for (int k = 0; k < 4; k++) q[k] = (float)pq[4 * i + k];
-                const float n = sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
-                for (int k = 0; k < 4; k++) u.v[k] = q[k] / n;
-                for (int k = 0; k < 3; k++) u.v[4 + k] = (float)pt[3 * i + k];
-                u.bad = 0;
-                for (int k = 0; k < 4; k++) u.reserved[k] = 0.f;
-                out[1 + r] = u;
-            }
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int s = 0;
-            for (int w = 0; w < 16; w++) s += wsum[w];
-            base += s;
-        }
-        if (tid < 16) wsum[tid] = 0;
-        __syncthreads();
-    }
-    const int n_opt = base;
-    const int total = n_opt + n_points;
-    for (int i = tid; i < n_points; i += 1024) {
-        const int r = n_opt + i;
-        if (r >= capacity) break;
-        mam_map_update u;
-        u.id = mid[i] - mp_id_base;
-        u.kind = MAM_UPDATE_MP;
-        u.agent = agent;
-        for (int k = 0; k < 3; k++) u.v[k] = (float)xyz[3 * i + k];
-        for (int k = 3; k < 7; k++) u.v[k] = 0.f;
-        u.bad = mbad ? (int32_t)(mbad[i] != 0) : 0;
-        for (int k = 0; k < 4; k++) u.reserved[k] = 0.f;
-        out[1 + r] = u;
-    }
-    if (tid == 0) {
-        mam_map_update h = {};
-        h.id = total <= capacity ? total : MAM_ERR_CAPACITY;
-        h.kind = MAM_UPDATE_HEADER;
-        h.agent = agent;
-        out[0] = h;
-    }
-}
-
-__global__ __launch_bounds__(1024) void k_pack_lba(const double* __restrict__ pq, const double* __restrict__ pt,
-                                                   const int64_t* __restrict__ pid, const uint8_t* __restrict__ pfix,
-                                                   int n_poses, const double* __restrict__ xyz,
-                                                   const int64_t* __restrict__ mid, const uint8_t* __restrict__ mbad,
-                                                   int n_points, int agent, mam_map_update* __restrict__ out,
-                                                   int capacity) {
-    pack_block(pq, pt, pid, pfix, n_poses, xyz, mid, mbad, n_points, 0, agent, out, capacity);
-}
-
-// grid (n_windows): window w's write-back into block w of out (capacity + 1 records each)
-__global__ __launch_bounds__(1024) void k_pack_windows(const mam_map_window* __restrict__ win, int64_t mp_id_base,
-                                                       int agent, mam_map_update* __restrict__ out, int capacity) {
-    const mam_map_window& w = win[blockIdx.x];
-    pack_block(w.pose_q, w.pose_t, w.pose_id, w.pose_fixed, w.n_poses, w.point_xyz, w.point_id, w.point_bad,
-               w.n_points, mp_id_base, agent, out + (size_t)blockIdx.x * (capacity + 1), capacity);
-}
 
 // grid (ceil(max(P, L) / 256), n_windows): the window's vertex estimates from the shared tables, the float map values
 // cast to double as the reference builds its graph (Optimizer.cc:1218, 1235: SE3Quat(GetPose().unit_quaternion()
@@ -126,33 +39,6 @@ __global__ __launch_bounds__(256) void k_read_windows(const float* __restrict__ 
         } else {
             for (int k = 0; k < 3; k++) w.point_xyz[3 * (size_t)i + k] = (double)mp[r * 4 + k];
         }
-    }
-}
-
-// One agent's block; launched once per agent in agent order on one stream, so a later agent's write to the same
-// id lands after an earlier one. Ids within a block are unique (one record per vertex).
-__global__ __launch_bounds__(256) void k_apply(const mam_map_update* __restrict__ blk, int capacity,
-                                               float* __restrict__ kf, int64_t kf_cap, float* __restrict__ mp,
-                                               int64_t mp_cap, int32_t* __restrict__ status) {
-    const mam_map_update& h = blk[0];
-    const int64_t count = h.id;
-    if (h.kind != MAM_UPDATE_HEADER || count < 0 || count > capacity) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(status, MAM_ERR_ARG);
-        return;
-    }
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= count) return;
-    const mam_map_update& u = blk[1 + r];
-    if (u.kind == MAM_UPDATE_KF && u.id >= 0 && u.id < kf_cap) {
-        float* d = kf + u.id * 8;
-        for (int k = 0; k < 7; k++) d[k] = u.v[k];
-        d[7] = 1.0f;
-    } else if (u.kind == MAM_UPDATE_MP && u.id >= 0 && u.id < mp_cap) {
-        float* d = mp + u.id * 4;
-        for (int k = 0; k < 3; k++) d[k] = u.v[k];
-        d[3] = u.bad ? 1.0f : 0.0f;
-    } else {
-        atomicExch(status, MAM_ERR_ARG);
     }
 }
 
@@ -185,10 +71,11 @@ __global__ __launch_bounds__(256) void k_pack_sources(const mam_map_window* __re
         mam_kf_update u;
         u.row = (int32_t)w.pose_id[v];
         // KeyFrame::SetPose(SE3f(q.cast<float>(), t.cast<float>())) (Optimizer.cc:1478-1486): Sophus normalises the
-        // float quaternion (coeffs / norm(), the same reduction as pack_block)
+        // float quaternion, coeffs / norm() with the norm as Eigen's SSE packet reduction sums the 4 floats,
+        // (x^2 + z^2) + (y^2 + w^2) — the same order as Frame::SetPose in pose.hip
         float q[4];
         for (int k = 0; k < 4; k++) q[k] = (float)w.pose_q[4 * (size_t)v + k];
-        const float nq = sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+        const float nq = sqrtf((q[0] * q[0] + q[2] * q[2]) + (q[1] * q[1] + q[3] * q[3]));
         for (int k = 0; k < 4; k++) u.q[k] = q[k] / nq;
         for (int k = 0; k < 3; k++) u.t[k] = (float)w.pose_t[3 * (size_t)v + k];
         K[i] = u;
@@ -276,30 +163,6 @@ extern "C" int mam_exchange_apply_compact(const void* gathered, int n_agents, in
     return MAM_OK;
 }
 
-extern "C" int mam_exchange_pack_lba(const double* pose_q, const double* pose_t, const int64_t* pose_id,
-                                     const uint8_t* pose_fixed, int n_poses, const double* point_xyz,
-                                     const int64_t* point_id, const uint8_t* point_bad, int n_points, int agent,
-                                     mam_map_update* out, int capacity, void* stream) {
-    if (!out || capacity < 0 || n_poses < 0 || n_points < 0) return MAM_ERR_ARG;
-    if ((n_poses && (!pose_q || !pose_t || !pose_id || !pose_fixed)) || (n_points && (!point_xyz || !point_id)))
-        return MAM_ERR_ARG;
-    if (n_points > capacity) return MAM_ERR_CAPACITY;
-    hipLaunchKernelGGL(mam::k_pack_lba, dim3(1), dim3(1024), 0, (hipStream_t)stream, pose_q, pose_t, pose_id,
-                       pose_fixed, n_poses, point_xyz, point_id, point_bad, n_points, agent, out, capacity);
-    MAM_HIP(hipGetLastError());
-    return MAM_OK;
-}
-
-extern "C" int mam_exchange_pack_windows(int n_windows, const mam_map_window* windows, int64_t mp_id_base, int agent,
-                                         mam_map_update* out, int capacity, void* stream) {
-    if (n_windows < 0 || (n_windows > 0 && (!windows || !out)) || capacity < 0) return MAM_ERR_ARG;
-    if (n_windows == 0) return MAM_OK;
-    hipLaunchKernelGGL(mam::k_pack_windows, dim3(n_windows), dim3(1024), 0, (hipStream_t)stream, windows, mp_id_base,
-                       agent, out, capacity);
-    MAM_HIP(hipGetLastError());
-    return MAM_OK;
-}
-
 extern "C" int mam_map_read_windows(const float* kf_table, int64_t kf_cap, const float* mp_table, int64_t mp_cap,
                                     int64_t mp_id_base, int n_windows, const mam_map_window* windows, int max_rows,
                                     int32_t* status, void* stream) {
@@ -309,18 +172,5 @@ extern "C" int mam_map_read_windows(const float* kf_table, int64_t kf_cap, const
     hipLaunchKernelGGL(mam::k_read_windows, dim3((max_rows + 255) / 256, n_windows), dim3(256), 0, (hipStream_t)stream,
                        kf_table, kf_cap, mp_table, mp_cap, mp_id_base, windows, status);
     MAM_HIP(hipGetLastError());
-    return MAM_OK;
-}
-
-extern "C" int mam_exchange_apply(const mam_map_update* gathered, int n_agents, int capacity, float* kf_table,
-                                  int64_t kf_cap, float* mp_table, int64_t mp_cap, int32_t* status, void* stream) {
-    if (!gathered || n_agents < 1 || capacity < 1 || !kf_table || !mp_table || !status) return MAM_ERR_ARG;
-    const int blocks = (capacity + 255) / 256;
-    for (int a = 0; a < n_agents; a++) {
-        hipLaunchKernelGGL(mam::k_apply, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                           gathered + (size_t)a * (size_t)(capacity + 1), capacity, kf_table, kf_cap, mp_table,
-                           mp_cap, status);
-        MAM_HIP(hipGetLastError());
-    }
     return MAM_OK;
 }

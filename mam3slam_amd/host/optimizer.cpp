@@ -30,6 +30,14 @@ struct ThreadPose {
 };
 thread_local ThreadPose t_pose;
 
+// Sophus::SO3f's normalize() (so3.hpp:481-487): coeffs / norm(), the norm of the 4-float vector as Eigen's SSE packet
+// reduction sums it, (x^2 + z^2) + (y^2 + w^2) (predux<Packet4f>: movehl add, then the two lanes) — one order for
+// every SE3f built from an optimised quaternion (Frame and KeyFrame SetPose), as csrc/pose.hip and csrc/exchange.hip
+void sophus_normalize(float q[4]) {
+    const float n = std::sqrt((q[0] * q[0] + q[2] * q[2]) + (q[1] * q[1] + q[3] * q[3]));
+    for (int j = 0; j < 4; j++) q[j] /= n;
+}
+
 // contexts follow the thread's device (SetDevice): recreated when it changes
 mam_pose_ctx* poseCtx() {
     if (t_pose.ctx && t_pose.device != GetDevice()) {
@@ -92,8 +100,7 @@ int Optimizer::PoseOptimization(Frame* pFrame) {
     SE3f pose;
     for (int j = 0; j < 4; j++) pose.q[j] = (float)res.q[j];
     for (int j = 0; j < 3; j++) pose.t[j] = (float)res.t[j];
-    const float qn = std::sqrt(pose.q[0] * pose.q[0] + pose.q[1] * pose.q[1] + pose.q[2] * pose.q[2] + pose.q[3] * pose.q[3]);
-    for (int j = 0; j < 4; j++) pose.q[j] /= qn;
+    sophus_normalize(pose.q);
     pFrame->SetPose(pose);
     return n;
 }
@@ -268,9 +275,7 @@ void Optimizer::ApplyLocalBAResult(const LocalBAWindow& w, Map* pMap, const doub
         SE3f Tiw;
         for (int j = 0; j < 4; j++) Tiw.q[j] = (float)q[4 * k + j];
         for (int j = 0; j < 3; j++) Tiw.t[j] = (float)t[3 * k + j];
-        // Sophus::SE3f(Quaternionf, t) normalises the quaternion (so3.hpp:481-487)
-        const float n = std::sqrt(Tiw.q[0] * Tiw.q[0] + Tiw.q[1] * Tiw.q[1] + Tiw.q[2] * Tiw.q[2] + Tiw.q[3] * Tiw.q[3]);
-        for (int j = 0; j < 4; j++) Tiw.q[j] /= n;
+        sophus_normalize(Tiw.q);   // Sophus::SE3f(Quaternionf, t) normalises the quaternion (so3.hpp:481-487)
         pKFi->SetPose(Tiw);
         k++;
     }
@@ -371,8 +376,7 @@ void Optimizer::BundleAdjustment(const std::vector<KeyFrame*>& vpKFs, const std:
         SE3f T;
         for (int j = 0; j < 4; j++) T.q[j] = (float)q[4 * k + j];
         for (int j = 0; j < 3; j++) T.t[j] = (float)t[3 * k + j];
-        const float n = std::sqrt(T.q[0] * T.q[0] + T.q[1] * T.q[1] + T.q[2] * T.q[2] + T.q[3] * T.q[3]);
-        for (int j = 0; j < 4; j++) T.q[j] /= n;
+        sophus_normalize(T.q);
         if (direct) {
             pKF->SetPose(T);
         } else {
@@ -506,8 +510,7 @@ void Optimizer::LocalBundleAdjustment(KeyFrame* pMainKF, std::vector<KeyFrame*> 
         SE3f Tiw;
         for (int j = 0; j < 4; j++) Tiw.q[j] = (float)q[4 * k + j];
         for (int j = 0; j < 3; j++) Tiw.t[j] = (float)t[3 * k + j];
-        const float n = std::sqrt(Tiw.q[0] * Tiw.q[0] + Tiw.q[1] * Tiw.q[1] + Tiw.q[2] * Tiw.q[2] + Tiw.q[3] * Tiw.q[3]);
-        for (int j = 0; j < 4; j++) Tiw.q[j] /= n;
+        sophus_normalize(Tiw.q);
         pKFi->SetPose(Tiw);
     }
     for (size_t p = 0; p < w.vpMP.size(); p++) {

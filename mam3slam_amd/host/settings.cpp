@@ -73,7 +73,7 @@ Settings::Settings(const std::string& configFile) {
     }
     width_ = readInt("Camera.width");
     height_ = readInt("Camera.height");
-    fps_ = readFloat("Camera.fps");
+    fps_ = (float)readInt("Camera.fps");   // readParameter<int> (Settings.cc:410) into the float member
     // readORB (Settings.cc:443-451)
     nFeatures_ = readInt("ORBextractor.nFeatures");
     scaleFactor_ = readFloat("ORBextractor.scaleFactor");
@@ -91,7 +91,8 @@ float Settings::readFloat(const std::string& k, bool required) const {
     errno = 0;
     char* end = nullptr;
     const double v = std::strtod(it->second.c_str(), &end);   // FileNode real (double), then (float)
-    if (end == it->second.c_str() || errno) throw std::runtime_error("Settings: " + k + " is not a real");
+    if (end == it->second.c_str() || *end != '\0' || errno)
+        throw std::runtime_error("Settings: " + k + " is not a real");
     return (float)v;
 }
 

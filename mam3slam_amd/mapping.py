@@ -51,7 +51,7 @@ class LocalMappingLeg:
         pk = (MapWindow * self.W)()
         self.res = []
         self.inputs = []
-        max_rows, cap = 0, 0
+        max_rows = 0
 
         def dev(a):
             t = torch.from_numpy(np.array(a, copy=True)).to(device)
@@ -65,7 +65,6 @@ class LocalMappingLeg:
             self.mp_ids.append(mps)
             P, L, E = len(p.pose_id), len(p.point_id), len(p.edge_point)
             max_rows = max(max_rows, P, L)
-            cap = max(cap, int((p.pose_fixed == 0).sum()) + L)
             pid, fix, mid = dev(p.pose_id), dev(p.pose_fixed), dev(p.point_id)
             q_in = torch.zeros((P, 4), dtype=torch.float64, device=device)
             t_in = torch.zeros((P, 3), dtype=torch.float64, device=device)
@@ -112,7 +111,6 @@ class LocalMappingLeg:
             t = torch.tensor(caps, dtype=torch.int64, device=device if on_gpu else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             caps = [int(v) for v in t.tolist()]
-        self.cap = cap   # the largest window's records (per-window blocks of the tests' reference path)
         self.d_read = dev(np.frombuffer(bytes(rd), np.uint8))
         self.d_pack = dev(np.frombuffer(bytes(pk), np.uint8))
         self.exch = CompactExchange(caps[0], caps[1], device=device)

@@ -142,10 +142,10 @@ def pinhole(w, h, f=500.0) -> Pinhole:
     return Pinhole(np.float32(f), np.float32(f), np.float32(w / 2), np.float32(h / 2))
 
 
-# the reference's test/settingsForTest_00.yaml (the testMultiAgentSystem agents' KannalaBrandt8 at 960 x 960), kept
-# as a fixture with its sibling settingsForTest_01.yaml
-TEST_SETTINGS = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
-                              "settings", f"settingsForTest_0{i}.yaml") for i in (0, 1)]
+# the reference's test/settingsForTest_00.yaml (the testMultiAgentSystem agents' KannalaBrandt8 at 960 x 960) and its
+# sibling settingsForTest_01.yaml: configuration data for BASELINE configs[3], kept in the package's data directory
+TEST_SETTINGS = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "settings",
+                              f"settingsForTest_0{i}.yaml") for i in (0, 1)]
 
 
 def kannala_brandt8(w=960, h=960, settings: str | None = None) -> KannalaBrandt8:

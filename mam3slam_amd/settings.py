@@ -50,7 +50,8 @@ class Settings:
                                          f("Camera1.k1"), f("Camera1.k2"), f("Camera1.k3"), f("Camera1.k4"))
         else:
             raise ValueError(f"{path}: unknown Camera.type {model}")
-        self.width, self.height, self.fps = self._int("Camera.width"), self._int("Camera.height"), f("Camera.fps")
+        self.width, self.height, self.fps = self._int("Camera.width"), self._int("Camera.height"), \
+            float(self._int("Camera.fps"))   # readParameter<int> (Settings.cc:410) into a float member
         self.n_features = self._int("ORBextractor.nFeatures")
         self.scale_factor = f("ORBextractor.scaleFactor")
         self.n_levels = self._int("ORBextractor.nLevels")

@@ -2,8 +2,10 @@
 
 Packing follows the LocalBundleAdjustment write-back (src/Optimizer.cc:1478-1494): non-fixed poses only (the
 reference writes back lLocalKeyFrames; fixed cameras are untouched), quaternion cast to float and renormalised in
-float (Sophus::SE3f(Quaternionf, t) normalises, so3.hpp:481-487), positions cast to float. Application is in agent
-order (deterministic replacement for the reference's mutex-ordered last-writer-wins, Optimizer.cc:1463).
+float (Sophus::SE3f(Quaternionf, t) normalises, so3.hpp:481-487, with Eigen's SSE reduction order), positions cast to
+float. `writeback` is one window's write-back applied directly (the reference's sequential semantics); the compact
+blocks (`pack_sources`, `apply_compact`) must leave the same tables. Application is in agent order (deterministic
+replacement for the reference's mutex-ordered last-writer-wins, Optimizer.cc:1463).
 Parity: the exchange has no reference counterpart to pin against (the reference shares pointers); the
 restatement defines the contract and the GPU kernels must match it byte for byte.
 """
@@ -11,63 +13,32 @@ from __future__ import annotations
 
 import numpy as np
 
-UPDATE_HEADER, UPDATE_KF, UPDATE_MP = 0, 1, 2
-UPDATE_DTYPE = np.dtype([("id", "<i8"), ("kind", "<i4"), ("agent", "<i4"), ("v", "<f4", (7,)), ("bad", "<i4"),
-                         ("reserved", "<f4", (4,))])
 ERR_CAPACITY, ERR_ARG = -2, -4
 
 
-def pack_lba(pose_q, pose_t, pose_id, pose_fixed, point_xyz, point_id, point_bad, agent, capacity):
-    out = np.zeros(capacity + 1, UPDATE_DTYPE)
-    keep = np.nonzero(np.asarray(pose_fixed) == 0)[0]
-    n_opt, n_pts = len(keep), len(point_id)
-    total = n_opt + n_pts
-    q = np.asarray(pose_q, np.float64)[keep].astype(np.float32)
-    n = np.sqrt(((q[:, 0] * q[:, 0] + q[:, 1] * q[:, 1]) + q[:, 2] * q[:, 2]) + q[:, 3] * q[:, 3]).astype(np.float32)
-    q = (q / n[:, None]).astype(np.float32)
-    t = np.asarray(pose_t, np.float64)[keep].astype(np.float32)
-    k = min(n_opt, capacity)
-    out["id"][1:1 + k] = np.asarray(pose_id)[keep][:k]
-    out["kind"][1:1 + k] = UPDATE_KF
-    out["agent"][1:1 + k] = agent
-    out["v"][1:1 + k, :4] = q[:k]
-    out["v"][1:1 + k, 4:] = t[:k]
-    m = max(0, min(n_pts, capacity - n_opt))
-    sl = slice(1 + n_opt, 1 + n_opt + m)
-    out["id"][sl] = np.asarray(point_id)[:m]
-    out["kind"][sl] = UPDATE_MP
-    out["agent"][sl] = agent
-    out["v"][sl, :3] = np.asarray(point_xyz, np.float64)[:m].astype(np.float32)
-    if point_bad is not None:
-        out["bad"][sl] = (np.asarray(point_bad)[:m] != 0).astype(np.int32)
-    out["id"][0] = total if total <= capacity else ERR_CAPACITY
-    out["kind"][0] = UPDATE_HEADER
-    out["agent"][0] = agent
-    return out
+def sophus_normalize(q):
+    """Sophus::SO3f::normalize (so3.hpp:481-487) of a float quaternion (x, y, z, w): coeffs / norm(), the norm of the
+    4-float vector as Eigen's SSE packet reduction sums it (predux<Packet4f>: (x^2 + z^2) + (y^2 + w^2))."""
+    q = np.asarray(q, np.float32)
+    sq = (q * q).astype(np.float32)
+    n = np.sqrt(np.float32(np.float32(sq[0] + sq[2]) + np.float32(sq[1] + sq[3])))
+    return (q / np.float32(n)).astype(np.float32)
 
 
-def apply(gathered, n_agents, capacity, kf_table, mp_table):
-    """gathered: UPDATE_DTYPE [n_agents*(capacity+1)]; kf_table float32 [K,8]; mp_table float32 [M,4]. In place.
-    Returns the status (0 or ERR_ARG)."""
-    status = 0
-    blocks = np.asarray(gathered).reshape(n_agents, capacity + 1)
-    for a in range(n_agents):
-        h = blocks[a, 0]
-        cnt = int(h["id"])
-        if int(h["kind"]) != UPDATE_HEADER or cnt < 0 or cnt > capacity:
-            status = ERR_ARG
-            continue
-        for u in blocks[a, 1:1 + cnt]:
-            i, kind = int(u["id"]), int(u["kind"])
-            if kind == UPDATE_KF and 0 <= i < len(kf_table):
-                kf_table[i, :7] = u["v"]
-                kf_table[i, 7] = 1.0
-            elif kind == UPDATE_MP and 0 <= i < len(mp_table):
-                mp_table[i, :3] = u["v"][:3]
-                mp_table[i, 3] = 1.0 if u["bad"] else 0.0
-            else:
-                status = ERR_ARG
-    return status
+def writeback(kf_table, mp_table, pose_q, pose_t, pose_id, pose_fixed, point_xyz, point_row, point_bad=None):
+    """One LocalBundleAdjustment window's write-back into the shared tables, in place (Optimizer.cc:1478-1494):
+    every non-fixed pose KeyFrame::SetPose(SE3f(q.cast<float>(), t.cast<float>())) (Sophus renormalises q), every
+    point MapPoint::SetWorldPos(pos.cast<float>()) and its bad flag. The reference applies the windows of several
+    agents one after another under mMutexMapUpdate; applying windows in order with this function is the sequential
+    semantics the compact blocks must reproduce."""
+    for i in np.nonzero(np.asarray(pose_fixed) == 0)[0]:
+        r = int(pose_id[i])
+        kf_table[r, :4] = sophus_normalize(np.asarray(pose_q[i], np.float64).astype(np.float32))
+        kf_table[r, 4:7] = np.asarray(pose_t[i], np.float64).astype(np.float32)
+        kf_table[r, 7] = 1.0
+    for i, r in enumerate(np.asarray(point_row)):
+        mp_table[int(r), :3] = np.asarray(point_xyz[i], np.float64).astype(np.float32)
+        mp_table[int(r), 3] = 1.0 if (point_bad is not None and point_bad[i]) else 0.0
 
 
 # ---- compact blocks (mam_exchange_pack_sources / mam_exchange_apply_compact)
@@ -83,10 +54,8 @@ def pack_sources(results, kf_src, mp_src, mp_id_base, agent, kf_cap, mp_cap):
     h["status"] = ERR_CAPACITY if (nk > kf_cap or nm > mp_cap) else 0
     for i, (w, v) in enumerate(np.asarray(kf_src)[:kf_cap]):
         pq, pt, pid = results[w][0], results[w][1], results[w][2]
-        q = np.asarray(pq[v], np.float64).astype(np.float32)
-        n = np.float32(np.sqrt(np.float32(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3])))
         K[i]["row"] = int(pid[v])
-        K[i]["q"] = (q / n).astype(np.float32)
+        K[i]["q"] = sophus_normalize(np.asarray(pq[v], np.float64).astype(np.float32))
         K[i]["t"] = np.asarray(pt[v], np.float64).astype(np.float32)
     for i, (w, v) in enumerate(np.asarray(mp_src)[:mp_cap]):
         xyz, mid, bad = results[w][3], results[w][4], results[w][5]

@@ -1006,7 +1006,7 @@ static void testConcurrentGPU() {
 // KannalaBrandt8 camera and their 700 / 1500-feature extractors; with a device, the extractor built from them
 static void testSettings(bool gpu) {
     const char* dir = std::getenv("MAM3SLAM_SETTINGS_DIR");
-    const std::string base = dir ? dir : "tests/golden/settings";
+    const std::string base = dir ? dir : "mam3slam_amd/data/settings";
     const int nf[2] = {700, 1500};
     const float fx[2] = {322.7022465231787f, 319.5669139636673f};
     for (int i = 0; i < 2; i++) {

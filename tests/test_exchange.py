@@ -1,9 +1,11 @@
-"""Shared-map update exchange (include/mam_exchange.h).
+"""Shared-map update exchange (include/mam_exchange.h): the compact blocks the bench's LocalMapping
+leg sends (CompactExchange: mam_exchange_pack_sources / mam_exchange_apply_compact).
 
-CPU: the collective itself — MapUpdateExchange.gather() at world_size 2 over gloo — with blocks packed and applied
-by the numpy restatement (oracle/exchange_oracle.py): both ranks receive identical bytes in rank order and end with
-identical tables where the higher agent wins a conflict. GPU: the pack / apply kernels byte-exact vs the
-restatement, including conflicts, bad flags, out-of-range ids and capacity overflow.
+CPU: the restatement (oracle/exchange_oracle.py) — the deduplicated block leaves exactly the tables the per-window
+write-backs applied in order leave (the reference's sequential semantics), with the quaternion renormalised as
+Sophus does; and the collective itself — CompactExchange.gather() at world_size 2 over gloo with windows that
+overlap ACROSS ranks: both ranks receive identical bytes in rank order and end with the tables of rank 0's windows
+then rank 1's applied in sequence. GPU: the pack / apply kernels byte-exact vs the restatement.
 """
 import os
 import socket
@@ -11,22 +13,7 @@ import socket
 import numpy as np
 import pytest
 
-from mam3slam_amd.exchange import MapUpdateExchange
 from oracle import exchange_oracle as xo
-
-
-def _agent_update(agent, n_poses=12, n_points=300, shared=200, seed=0):
-    """An agent's LBA write-back: poses ids 10*agent.., points drawn from a shared id pool (merged map)."""
-    rng = np.random.default_rng(seed + 17 * agent)
-    q = rng.normal(size=(n_poses, 4))
-    q /= np.linalg.norm(q, axis=1, keepdims=True)
-    t = rng.normal(size=(n_poses, 3))
-    pid = np.arange(n_poses, dtype=np.int64) + 5 * agent          # overlapping keyframe ids
-    fixed = (rng.random(n_poses) < 0.3).astype(np.uint8)
-    mid = np.sort(rng.choice(shared + n_points, size=n_points, replace=False)).astype(np.int64)
-    xyz = rng.normal(size=(n_points, 3)) * 3
-    bad = (rng.random(n_points) < 0.05).astype(np.uint8)
-    return q, t, pid, fixed, xyz, mid, bad
 
 
 def _free_port():
@@ -37,103 +24,25 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, cap, outdir):
-    import torch.distributed as dist
-
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    ex = MapUpdateExchange(capacity=cap, device="cpu")
-    q, t, pid, fixed, xyz, mid, bad = _agent_update(rank)
-    blk = xo.pack_lba(q, t, pid, fixed, xyz, mid, bad, rank, cap)
-    ex.send.numpy()[:] = blk.view(np.uint8)
-    got = ex.gather().numpy().copy()
-    kf = np.zeros((64, 8), np.float32)
-    mp = np.zeros((1024, 4), np.float32)
-    st = xo.apply(got.view(xo.UPDATE_DTYPE), world, cap, kf, mp)
-    np.savez(os.path.join(outdir, f"r{rank}.npz"), got=got, kf=kf, mp=mp, st=st)
-    dist.destroy_process_group()
+def _norm_orders_differ(q):
+    """Sophus's (x^2 + z^2) + (y^2 + w^2) and the sequential ((x^2 + y^2) + z^2) + w^2 give different floats."""
+    q = np.asarray(q, np.float32)
+    sq = (q * q).astype(np.float32)
+    n_seq = np.sqrt(np.float32(np.float32(np.float32(sq[0] + sq[1]) + sq[2]) + sq[3]))
+    return not np.array_equal(xo.sophus_normalize(q), (q / n_seq).astype(np.float32))
 
 
-def test_gather_gloo_world2(tmp_path):
-    import torch.multiprocessing as mp
-
-    cap, world = 512, 2
-    mp.start_processes(_rank_main, args=(world, _free_port(), cap, str(tmp_path)), nprocs=world, join=True,
-                       start_method="spawn")
-    r0, r1 = (np.load(tmp_path / f"r{r}.npz") for r in range(world))
-    assert np.array_equal(r0["got"], r1["got"])
-    assert np.array_equal(r0["kf"], r1["kf"]) and np.array_equal(r0["mp"], r1["mp"])
-    assert int(r0["st"]) == 0
-    blocks = r0["got"].view(xo.UPDATE_DTYPE).reshape(world, cap + 1)
-    for a in range(world):
-        exp = xo.pack_lba(*_agent_update(a), a, cap)
-        assert np.array_equal(blocks[a].view(np.uint8), exp.view(np.uint8)), f"block {a} not in rank order"
-    # conflicts: ids written by both agents hold agent 1's values (applied last)
-    q1, t1, pid1, fx1, xyz1, mid1, bad1 = _agent_update(1)
-    for i, m in enumerate(mid1):
-        assert np.array_equal(r0["mp"][m, :3], xyz1[i].astype(np.float32))
-    b1 = xo.pack_lba(q1, t1, pid1, fx1, xyz1, mid1, bad1, 1, cap)
-    for u in b1[1:1 + int(b1[0]["id"])]:
-        if u["kind"] == xo.UPDATE_KF:
-            assert np.array_equal(r0["kf"][u["id"], :7], u["v"]) and r0["kf"][u["id"], 7] == 1.0
-
-
-def test_pack_capacity_and_header():
-    q, t, pid, fixed, xyz, mid, bad = _agent_update(0)
-    n_opt = int((fixed == 0).sum())
-    blk = xo.pack_lba(q, t, pid, fixed, xyz, mid, bad, 3, n_opt + len(mid))
-    assert blk[0]["id"] == n_opt + len(mid) and blk[0]["agent"] == 3
-    assert (blk["kind"][1:1 + n_opt] == xo.UPDATE_KF).all() and (blk["kind"][1 + n_opt:] == xo.UPDATE_MP).all()
-    small = xo.pack_lba(q, t, pid, fixed, xyz, mid, bad, 3, n_opt + len(mid) - 1)
-    assert small[0]["id"] == xo.ERR_CAPACITY
-    kf, mpt = np.zeros((64, 8), np.float32), np.zeros((1024, 4), np.float32)
-    assert xo.apply(small, 1, n_opt + len(mid) - 1, kf, mpt) == xo.ERR_ARG and not kf.any()
-
-
-@pytest.mark.gpu
-def test_pack_apply_kernels(gpu_lib):
-    import torch
-
-    dev = torch.device("cuda")
-    cap, agents = 600, 3
-    st = torch.cuda.Stream()
-    st.wait_stream(torch.cuda.current_stream())
-    ex = MapUpdateExchange(capacity=cap, device=dev)
-    blocks = []
-    for a in range(agents):
-        q, t, pid, fixed, xyz, mid, bad = _agent_update(a, seed=5)
-        T = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (q, t, pid, fixed, xyz, mid, bad)]
-        ex.send.fill_(0xAB)
-        torch.cuda.synchronize()
-        ex.pack_lba(T[0].data_ptr(), T[1].data_ptr(), T[2].data_ptr(), T[3].data_ptr(), len(pid), T[4].data_ptr(),
-                    T[5].data_ptr(), T[6].data_ptr(), len(mid), stream=st.cuda_stream, agent=a)
-        torch.cuda.synchronize()
-        got = ex.send.cpu().numpy().view(xo.UPDATE_DTYPE)
-        exp = xo.pack_lba(q, t, pid, fixed, xyz, mid, bad, a, cap)
-        n = int(exp[0]["id"])
-        assert np.array_equal(got[:1 + n].view(np.uint8), exp[:1 + n].view(np.uint8)), f"agent {a} pack"
-        blocks.append(exp)
-    # an out-of-range id in agent 2's block -> status ERR_ARG, the record skipped
-    blocks[2][5]["id"] = 10 ** 6
-    gathered = np.concatenate(blocks)
-    d_g = torch.from_numpy(gathered.view(np.uint8).copy()).to(dev)
-    kf = torch.zeros((64, 8), dtype=torch.float32, device=dev)
-    mpt = torch.zeros((1024, 4), dtype=torch.float32, device=dev)
-    status = torch.zeros(1, dtype=torch.int32, device=dev)
-    ex.apply(kf.data_ptr(), 64, mpt.data_ptr(), 1024, status.data_ptr(), stream=st.cuda_stream,
-             gathered=d_g.data_ptr(), n_agents=agents)
-    torch.cuda.synchronize()
-    kf_o, mp_o = np.zeros((64, 8), np.float32), np.zeros((1024, 4), np.float32)
-    st_o = xo.apply(gathered, agents, cap, kf_o, mp_o)
-    assert int(status.item()) == st_o == xo.ERR_ARG
-    assert np.array_equal(kf.cpu().numpy(), kf_o) and np.array_equal(mpt.cpu().numpy(), mp_o)
-    # capacity overflow is reported in the header
-    q, t, pid, fixed, xyz, mid, bad = _agent_update(0, n_points=cap)
-    T = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (q, t, pid, fixed, xyz, mid, bad)]
-    ex.pack_lba(T[0].data_ptr(), T[1].data_ptr(), T[2].data_ptr(), T[3].data_ptr(), len(pid), T[4].data_ptr(),
-                T[5].data_ptr(), T[6].data_ptr(), len(mid), stream=st.cuda_stream, agent=0)
-    torch.cuda.synchronize()
-    assert int(ex.send.cpu().numpy().view(xo.UPDATE_DTYPE)[0]["id"]) == xo.ERR_CAPACITY
+def test_sophus_normalize_order():
+    """KeyFrame::SetPose(SE3f(q.cast<float>(), t)) renormalises with Eigen's SSE reduction order; the order matters
+    for ~15 % of quaternions (1 ulp), so the byte-exact tests below hold poses where the two orders differ."""
+    q = np.array([0.0021944, 0.9986104, -0.0317063, 0.0418517], np.float32)
+    rng = np.random.default_rng(1)
+    found = [x for x in rng.normal(size=(400, 4)).astype(np.float32) if _norm_orders_differ(x)]
+    assert len(found) > 20
+    x, y, z, w = (np.float32(v) for v in found[0])
+    n = np.sqrt(np.float32((x * x + z * z) + (y * y + w * w)))
+    assert np.array_equal(xo.sophus_normalize(found[0]), (found[0] / n).astype(np.float32))
+    assert np.abs(np.linalg.norm(xo.sophus_normalize(q).astype(np.float64)) - 1.0) < 1e-6
 
 
 def test_world_windows_are_consistent():
@@ -173,12 +82,21 @@ def _windows_results(n_windows=4, seed=0):
     return res, wins
 
 
-def test_compact_block_equals_per_window_blocks():
+def _sequential(res, wins, mp_base, kf_rows=64, mp_rows=1000, kf0=None, mp0=None):
+    kf = np.zeros((kf_rows, 8), np.float32) if kf0 is None else kf0.copy()
+    mp = np.zeros((mp_rows, 4), np.float32) if mp0 is None else mp0.copy()
+    for (q, t, pid, xyz, mid, bad), (_, fixed, _) in zip(res, wins):
+        xo.writeback(kf, mp, q, t, pid, fixed, xyz, np.asarray(mid) - mp_base, bad)
+    return kf, mp
+
+
+def test_compact_block_equals_sequential_writeback():
     """The deduplicated block (every vertex once, from the last window holding it) leaves the tables exactly as the
-    per-window write-backs applied in window order do, at 16 / 32 bytes per record instead of 64."""
+    windows' write-backs (Optimizer.cc:1478-1494) applied one after another do, at 16 / 32 bytes per record."""
     from mam3slam_amd.exchange import compact_block_bytes, dedup_sources
 
     res, wins = _windows_results()
+    assert any(_norm_orders_differ(q) for r in res for q in r[0])
     mp_base = 1000
     kf_src, mp_src = dedup_sources(wins)
     ids_kf = [int(wins[w][0][i]) for w, i in kf_src]
@@ -188,23 +106,91 @@ def test_compact_block_equals_per_window_blocks():
     assert len(blk) == compact_block_bytes(len(kf_src), len(mp_src))
     kf_a, mp_a = np.zeros((64, 8), np.float32), np.zeros((1000, 4), np.float32)
     assert xo.apply_compact(blk, 1, len(kf_src), len(mp_src), kf_a, mp_a) == 0
-    kf_b, mp_b = np.zeros((64, 8), np.float32), np.zeros((1000, 4), np.float32)
-    cap = max(int((f == 0).sum()) + len(m) for _, f, m in wins)
-    blocks = [xo.pack_lba(q, t, pid, wins[w][1], xyz, mid - mp_base, bad, 0, cap)
-              for w, (q, t, pid, xyz, mid, bad) in enumerate(res)]
-    assert xo.apply(np.concatenate(blocks), len(blocks), cap, kf_b, mp_b) == 0
+    kf_b, mp_b = _sequential(res, wins, mp_base)
     assert np.array_equal(kf_a, kf_b) and np.array_equal(mp_a, mp_b)
-    assert len(blk) < sum(b.nbytes for b in blocks) / 3
+    per_window = sum(16 + 64 * (int((f == 0).sum()) + len(m)) for _, f, m in wins)   # round 2's 64-byte records
+    assert len(blk) < per_window / 3
     # capacity overflow is flagged and the block is rejected whole
     small = xo.pack_sources(res, kf_src, mp_src, mp_base, 0, len(kf_src), len(mp_src) - 1)
     kf_c, mp_c = np.zeros((64, 8), np.float32), np.zeros((1000, 4), np.float32)
     assert xo.apply_compact(small, 1, len(kf_src), len(mp_src) - 1, kf_c, mp_c) == xo.ERR_ARG and not mp_c.any()
 
 
+def _rank_windows(rank):
+    """Rank r's windows of one step: 3 windows whose keyframes and MapPoints overlap each other AND the other rank's
+    (keyframe ids 8 r + 10 w .., MapPoint ids from a pool shared by both ranks), as neighbouring agents' windows over
+    a merged map do."""
+    rng = np.random.default_rng(100 + rank)
+    res, wins = [], []
+    for w in range(3):
+        pid = np.arange(8 * rank + 10 * w, 8 * rank + 10 * w + 20, dtype=np.int64)
+        fixed = ((pid % 5) == 0).astype(np.uint8)
+        mid = np.sort(rng.choice(np.arange(60 * w + 40 * rank, 60 * w + 40 * rank + 300), size=200,
+                                 replace=False)).astype(np.int64) + 1000
+        q = rng.normal(size=(len(pid), 4))
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+        res.append((q, rng.normal(size=(len(pid), 3)), pid, rng.normal(size=(len(mid), 3)) * 4, mid,
+                    (rng.random(len(mid)) < 0.05).astype(np.uint8)))
+        wins.append((pid, fixed, mid))
+    return res, wins
+
+
+def _compact_rank_main(rank, world, port, caps, outdir):
+    import torch.distributed as dist
+
+    from mam3slam_amd.exchange import CompactExchange, dedup_sources
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ex = CompactExchange(caps[0], caps[1], device="cpu")
+    res, wins = _rank_windows(rank)
+    kf_src, mp_src = dedup_sources(wins)
+    blk = xo.pack_sources(res, kf_src, mp_src, 1000, ex.rank, caps[0], caps[1])
+    ex.send.numpy()[:] = np.frombuffer(blk, np.uint8)
+    got = ex.gather().numpy().copy()
+    kf = np.zeros((64, 8), np.float32)
+    mp = np.zeros((1000, 4), np.float32)
+    st = xo.apply_compact(got.tobytes(), world, caps[0], caps[1], kf, mp)
+    np.savez(os.path.join(outdir, f"c{rank}.npz"), got=got, kf=kf, mp=mp, st=st)
+    dist.destroy_process_group()
+
+
+def test_compact_gather_gloo_world2(tmp_path):
+    """The all-gather the bench's exchange takes (CompactExchange.gather, world 2, gloo), with windows overlapping
+    across the ranks: identical bytes on both ranks in rank order, and the applied tables equal rank 0's windows then
+    rank 1's written back in sequence (the higher rank wins a conflict)."""
+    import torch.multiprocessing as mp
+
+    from mam3slam_amd.exchange import compact_block_bytes, dedup_sources
+
+    world = 2
+    srcs = [dedup_sources(_rank_windows(r)[1]) for r in range(world)]
+    caps = (max(len(k) for k, _ in srcs) + 4, max(len(m) for _, m in srcs) + 4)   # the all-reduce MAX of the bench
+    mp.start_processes(_compact_rank_main, args=(world, _free_port(), caps, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r0, r1 = (np.load(tmp_path / f"c{r}.npz") for r in range(world))
+    assert int(r0["st"]) == 0 == int(r1["st"])
+    assert np.array_equal(r0["got"], r1["got"])
+    assert np.array_equal(r0["kf"], r1["kf"]) and np.array_equal(r0["mp"], r1["mp"])
+    bb = compact_block_bytes(*caps)
+    for r in range(world):
+        res, wins = _rank_windows(r)
+        exp = xo.pack_sources(res, *srcs[r], 1000, r, *caps)
+        assert r0["got"][r * bb:(r + 1) * bb].tobytes() == exp, f"block {r} not in rank order"
+    k0 = set(int(x) for _, _, pid, _, _, _ in _rank_windows(0)[0] for x in pid)
+    k1 = set(int(x) for _, _, pid, _, _, _ in _rank_windows(1)[0] for x in pid)
+    assert len(k0 & k1) > 10   # the ranks' windows really conflict
+    res0, wins0 = _rank_windows(0)
+    res1, wins1 = _rank_windows(1)
+    kf_s, mp_s = _sequential(res0 + res1, wins0 + wins1, 1000)
+    assert np.array_equal(r0["kf"], kf_s) and np.array_equal(r0["mp"], mp_s)
+
+
 @pytest.mark.gpu
 def test_compact_pack_apply_kernels(gpu_lib):
-    """mam_exchange_pack_sources / mam_exchange_apply_compact byte-exact vs the restatement, two agents' blocks
-    applied in agent order."""
+    """mam_exchange_pack_sources / mam_exchange_apply_compact byte-exact vs the restatement (including quaternions
+    whose Sophus renormalisation differs from the sequential sum order), two agents' blocks applied in agent order,
+    and the applied tables equal the agents' windows written back in sequence."""
     import torch
 
     from mam3slam_amd.exchange import CompactExchange, MapWindow, compact_block_bytes, dedup_sources
@@ -253,3 +239,6 @@ def test_compact_pack_apply_kernels(gpu_lib):
     kf_o, mp_o = np.zeros((128, 8), np.float32), np.zeros((1000, 4), np.float32)
     assert xo.apply_compact(gathered, 2, caps[0], caps[1], kf_o, mp_o) == 0 == int(status.item())
     assert np.array_equal(kf.cpu().numpy(), kf_o) and np.array_equal(mpt.cpu().numpy(), mp_o)
+    assert any(_norm_orders_differ(q) for r in data[0][0] for q in r[0])
+    kf_s, mp_s = _sequential(data[0][0] + data[1][0], data[0][1] + data[1][1], mp_base, 128, 1000)
+    assert np.array_equal(kf.cpu().numpy(), kf_s) and np.array_equal(mpt.cpu().numpy(), mp_s)

@@ -68,7 +68,7 @@ def _sanitized_binary(kind):
 
 
 def _run(mode, timeout, binary=None, env=None):
-    e = {**os.environ, "MAM3SLAM_SETTINGS_DIR": os.path.join(ROOT, "tests", "golden", "settings"), **(env or {})}
+    e = {**os.environ, "MAM3SLAM_SETTINGS_DIR": os.path.join(ROOT, "mam3slam_amd", "data", "settings"), **(env or {})}
     r = subprocess.run([binary or _binary(), mode], capture_output=True, text=True, timeout=timeout, env=e)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert r.stdout.startswith("OK"), r.stdout

@@ -22,7 +22,7 @@ def test_mapping_leg_matches_oracle(gpu_lib, oracle):
         M.run(step, new_keyframes=False)
         torch.cuda.synchronize()
         assert int(M.status.item()) == 0
-        blocks = []
+        kf_ref, mp_ref = kf0.copy(), mp0.copy()
         for w in range(M.W):
             prob = M.window_inputs(w)
             # the graph's estimates are the float map values cast to double (Optimizer.cc:1218, 1286)
@@ -34,10 +34,9 @@ def test_mapping_leg_matches_oracle(gpu_lib, oracle):
             assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials), (step, w)
             rel = np.abs(rg.point_xyz - ro.point_xyz).max() / np.abs(ro.point_xyz).max()
             assert rel <= 1e-4 and np.abs(rg.pose_t - ro.pose_t).max() <= 1e-4 * np.abs(ro.pose_t).max()
-            blocks.append(X.pack_lba(rg.pose_q, rg.pose_t, prob.pose_id, prob.pose_fixed, rg.point_xyz,
-                                     prob.point_id - M.mp_base, None, 0, M.cap))
-        kf_ref, mp_ref = kf0.copy(), mp0.copy()
-        assert X.apply(np.concatenate(blocks), M.W, M.cap, kf_ref, mp_ref) == 0
+            # the window's write-back (Optimizer.cc:1478-1494), windows in order: what the compact block must leave
+            X.writeback(kf_ref, mp_ref, rg.pose_q, rg.pose_t, prob.pose_id, prob.pose_fixed, rg.point_xyz,
+                        prob.point_id - M.mp_base)
         assert np.array_equal(M.kf_table.cpu().numpy(), kf_ref)
         assert np.array_equal(M.mp_table.cpu().numpy(), mp_ref)
     # the next step's windows read the applied map
