@@ -184,7 +184,14 @@ class TrackingLeg:
         self.ext = ORBextractor(NF, 1.2, 8, 20, 7, device=di)
         cap = self.ext.max_keypoints()
         self.cap = cap
-        self.frames = np.stack([synth.make_frame(W, H, agent=rank, frame=i) for i in range(B)])
+        cam = scene.kannala_brandt8(W, H) if cfg.get("camera") == "kb8" else scene.pinhole(W, H)
+        self.cam = cam
+        # frames rendered through the camera they are tracked with (the KannalaBrandt8 agents see the scene through the
+        # fisheye: synth.make_frame_camera; the Pinhole frames are make_frame's crops, the same images)
+        if cam.is_kb8:
+            self.frames = np.stack([synth.make_frame_camera(W, H, cam, agent=rank, frame=i) for i in range(B)])
+        else:
+            self.frames = np.stack([synth.make_frame(W, H, agent=rank, frame=i) for i in range(B)])
         self.d_img = torch.from_numpy(self.frames).to(dev)
         self.d_kps = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)
         self.d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
@@ -204,16 +211,14 @@ class TrackingLeg:
         desc_h = self.d_desc.cpu().numpy()
         cnt_h = self.d_cnt.cpu().numpy()
         self.kps_h, self.cnt_h = kps_h, cnt_h
-        cam = scene.kannala_brandt8(W, H) if cfg.get("camera") == "kb8" else scene.pinhole(W, H)
-        self.cam = cam
         lasts, mpls, poses, poses_init = [], [], [], []
         F0 = None
         for f in range(B):
             rng = np.random.default_rng(1000 * rank + f)
             F = scene.make_frame_data(kps_h[f, :cnt_h[f, 0]], desc_h[f, :cnt_h[f, 0]], W, H)
             # the pose of the camera that rendered the frame (synth.frame_pose: the canvas as a plane in front of a
-            # translating, rolling Pinhole camera), so keyframes' poses and image content agree (SearchForTriangulation's
-            # epipolar tests between keyframes pass for real correspondences)
+            # translating, rolling camera), so keyframes' poses and image content agree (SearchForTriangulation's
+            # epipolar tests between keyframes pass for real correspondences, KannalaBrandt8 included)
             F.pose = synth.frame_pose(W, H, f)
             F0 = F0 or F
             # the last frame's and the local map's MapPoints re-project onto the frame's keypoints under that pose:
@@ -322,11 +327,11 @@ class TrackingLeg:
         fr2 = ln["fr2"] if fr2 is None else fr2
         tcw0 = self.d_tcw_init.data_ptr() + lo * self.tcw_bytes
         tcw = self.d_tcw.data_ptr() + lo * self.tcw_bytes
-        # TrackWithMotionModel: the current frame at the motion model's guess, SearchByProjection(Cur, Last, th 15),
-        # PoseOptimization, outliers discarded
-        ln["mm"].search_motion_batch_device(self.F0, fr1, tcw0, self.cam, self.d_last[lo].data_ptr(), self.Ls,
-                                            self.d_nlast[lo:].data_ptr(), 15.0, self.d_out1[lo].data_ptr(),
-                                            self.d_nm1[lo:].data_ptr(), stream=st)
+        # TrackWithMotionModel: the current frame at the motion model's guess, SearchByProjection(Cur, Last, th 15)
+        # (again at th 30 for a frame with fewer than 20 matches), PoseOptimization, outliers discarded
+        ln["mm"].track_motion_search_batch_device(self.F0, fr1, tcw0, self.cam, self.d_last[lo].data_ptr(), self.Ls,
+                                                  self.d_nlast[lo:].data_ptr(), 15.0, self.d_out1[lo].data_ptr(),
+                                                  self.d_nm1[lo:].data_ptr(), min_matches=20, stream=st)
         self._pose_lane(ln, 0, lo, BL, st)
         # TrackLocalMap: SearchLocalPoints (isInFrustum + SearchByProjection(F, localMPs, th 1)) at the optimised pose,
         # then PoseOptimization with every match
@@ -505,7 +510,7 @@ def parity_section(tr, mapping, newmp=None):
     # TrackWithMotionModel
     F.pose = tr.poses_init[f]
     last = np.ascontiguousarray(tr.lasts[f], LAST_ENTRY_DTYPE)
-    _, o1 = oracle_py.search_by_projection_motion(F, last, tr.cam, 15.0, True)
+    _, o1, _ = oracle_py.track_motion_search(F, last, tr.cam, 15.0, True)
     idx = np.nonzero(o1 >= 0)[0]
     e1 = make_edges(F.keys, tr.inv_s2, idx, last["pos"][o1[idx]])
     res = tr.d_pres[:, f].cpu().numpy().view(POSE_RESULT_DTYPE).reshape(2)
@@ -540,15 +545,20 @@ def parity_section(tr, mapping, newmp=None):
     out["pose_optimization_max_rel_diff"] = max(d1, d2)
     out["pose_optimization_edges"] = [len(e1), len(e2)]
     if newmp is not None:
-        # pair 0 of the last step's CreateNewMapPoints searches, FeatureVectors from the device BoW
-        K1, K2 = newmp.pair_inputs(0)
+        # the first of the last step's CreateNewMapPoints searches that found matches (FeatureVectors from the device
+        # BoW); none with a match fails the parity (a vacuous comparison proves nothing)
+        nmv = newmp.nmatch.cpu().numpy()
+        qs = np.nonzero(nmv[:newmp.npairs] > 0)[0]
+        qp = int(qs[0]) if len(qs) else 0
+        K1, K2 = newmp.pair_inputs(qp)
         t0 = time.perf_counter()
         no, oo = oracle_py.search_for_triangulation_kf(K1, K2, tr.cam, tr.cam, False, False)
         tri_ms = (time.perf_counter() - t0) * 1e3
         n1 = len(K1.keys)
-        out["triangulation_index_exact"] = bool(int(newmp.nmatch[0].item()) == no and
-                                                np.array_equal(newmp.out[0, :n1].cpu().numpy(), oo))
-        out["triangulation_pair"] = {"matches": int(no), "n1": n1, "n2": len(K2.keys), "oracle_ms": tri_ms}
+        out["triangulation_index_exact"] = bool(len(qs) > 0 and no > 0 and int(nmv[qp]) == no and
+                                                np.array_equal(newmp.out[qp, :n1].cpu().numpy(), oo))
+        out["triangulation_pair"] = {"pair": qp, "matches": int(no), "n1": n1, "n2": len(K2.keys),
+                                     "oracle_ms": tri_ms}
         # SearchInNeighbors: forward item 0 (keyframe 0's MapPoints into its nearest neighbour) and backward item 0
         ok, fused = True, []
         for backward, gi, gd, gn in ((False, newmp.fwd_idx, newmp.fwd_dist, newmp.fwd_n),
@@ -629,7 +639,7 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
         F = scene.make_frame_data(k, d, W, H)
         F.pose = tr.poses_init[f]
         last = lasts[f]
-        _, o1 = oracle_py.search_by_projection_motion(F, last, tr.cam, 15.0, True)
+        _, o1, _ = oracle_py.track_motion_search(F, last, tr.cam, 15.0, True)
         idx = np.nonzero(o1 >= 0)[0]
         _, ol1, (q, t), _ = oracle_py.pose_optimization_edges(
             F.pose, tr.cam, make_edges(F.keys, tr.inv_s2, idx, last["pos"][o1[idx]]))
@@ -685,7 +695,8 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
         per_frame_ms += (tri_ms + bow_ms + sin_ms) / K
     res = {"value": 1e3 / per_frame_ms, "unit": "frames/s", "cores": 1, "kind": "port",
            "tracking_ms_per_frame": track_ms, "extract_ms_per_frame": ext_s * 1e3 / n, "host": host_info(),
-           "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15) + "
+           "sample": f"{n} frames {W}x{H}/{cfg['nfeatures']}: extract + SearchByProjection(motion, th 15; 30 below 20 "
+                     f"matches) + "
                      f"PoseOptimization + isInFrustum + SearchByProjection(local map, th 1) + PoseOptimization on the "
                      f"oracle C++ restatement (g++ -O3 -march=x86-64-v3, the reference's CMake -O3 -march=native "
                      f"level; scalar code where the reference's OpenCV FAST / resize / blur are SIMD), single thread, "
@@ -968,7 +979,8 @@ def main():
         W, H, NF = tr.W, tr.H, tr.NF
         camd = "KannalaBrandt8 (test YAML)" if cfg.get("camera") == "kb8" else "Pinhole"
         workload = (f"{args.config}: mono {W}x{H}, {NF} features, 8 levels, {camd}; step = {B} frame streams x (ORB "
-                    f"extract + TrackWithMotionModel: SearchByProjection motion th15 + PoseOptimization + outlier "
+                    f"extract + TrackWithMotionModel: SearchByProjection motion th15 (th30 below 20 matches) + "
+                    f"PoseOptimization + outlier "
                     f"discard; TrackLocalMap: isInFrustum + SearchByProjection local map th1 + PoseOptimization)")
         if agents_total:
             workload += f"; {agents_total} agents in total, {B} per GPU"

@@ -263,6 +263,17 @@ int mam_search_by_projection_motion_batch_device(mam_match_ctx* ctx, const mam_f
                                                  const int32_t* n_last, float th, int check_ori,
                                                  int32_t* out_kp_to_last, int32_t* out_nmatches, void* stream);
 
+/* Tracking::TrackWithMotionModel's search (Tracking.cc:2811-2824), per frame of the batch: SearchByProjection(Cur,
+ * Last, th, check_ori); where it found fewer than min_matches (the reference's 20) matches, the frame's matches are
+ * cleared (fill(mvpMapPoints, NULL)) and the search runs again with 2 * th. out / out_nmatches hold each frame's final
+ * search (the count the reference then tests against 20 before PoseOptimization). frames->reuse_grid must be 0 (the
+ * call builds the grid). Asynchronous; min_matches = 0 is the plain batch search. */
+int mam_track_motion_search_batch_device(mam_match_ctx* ctx, const mam_frame_geom* geom, const mam_frames_dev* frames,
+                                         const mam_pose* tcw, const mam_camera* cam, const mam_last_entry* last,
+                                         int last_stride, const int32_t* n_last, float th, int check_ori,
+                                         int min_matches, int32_t* out_kp_to_last, int32_t* out_nmatches,
+                                         void* stream);
+
 /* Fuse into many keyframes in one launch (SearchInNeighbors' forward direction, LocalMapping.cc:881-890): keyframe f
  * (frames: its keypoints) with kfs[f] searches n_mps[f] MapPoints at mps + f*mp_stride. Outputs at
  * out_idx / out_dist + f*mp_stride and out_nfused[f]. */

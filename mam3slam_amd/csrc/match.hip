@@ -74,6 +74,9 @@ struct ProjArgs {
     mam_camera cam;
     const mam_last_entry* last;
     int check_ori;
+    // > 0: TrackWithMotionModel's wider-window retry (Tracking.cc:2816-2824): only frames whose previous search (out_n,
+    // on the same outputs) found fewer than retry_below matches search again, the others keep their result
+    int retry_below;
     // scratch
     struct GridEnt* grid_ent; // [F][kp_stride] cell-major keypoint records (cell vectors of AssignFeaturesToGrid)
     int32_t* grid_start;      // [F][NCELLS+1]
@@ -376,6 +379,10 @@ __global__ __launch_bounds__(256) void k_gather(ProjArgs p, int nframes) {
     int32_t* offp = p.cand_off + (size_t)f * p.unit_stride + j;
     Window w;
     if (!live) return;
+    if (p.retry_below > 0) {   // a frame the first search served (or reported an error for) is not searched again
+        const int pn = p.out_n[f];
+        if (pn < 0 || pn >= p.retry_below) return;
+    }
     if (!unit_window(p, f, j, &w)) {
         if (gl == 0) { *cntp = 0; *offp = 0; }
         return;
@@ -450,6 +457,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ProjArgs p) {
 #ifdef MAM_RESOLVE_PROFILE
     long long rp0 = clock64();
 #endif
+    if (p.retry_below > 0) {   // as k_gather: frames with enough matches (or an error) keep the first search's result
+        const int pn = p.out_n[f];
+        if (pn < 0 || pn >= p.retry_below) return;
+    }
     const int ptot = p.pool_total[f];
     __syncthreads();
     // reset for the next search on this context: a search that reuses the grid (mam_frames_dev.reuse_grid) skips
@@ -1866,6 +1877,39 @@ int mam_search_by_projection_motion_batch_device(mam_match_ctx* c, const mam_fra
     a.out = out;
     a.out_n = out_n;
     return launch_projection(c, a, fr->nframes, stream ? (hipStream_t)stream : c->stream);
+}
+
+int mam_track_motion_search_batch_device(mam_match_ctx* c, const mam_frame_geom* g, const mam_frames_dev* fr,
+                                         const mam_pose* tcw, const mam_camera* cam, const mam_last_entry* last,
+                                         int last_stride, const int32_t* n_last, float th, int check_ori,
+                                         int min_matches, int32_t* out, int32_t* out_n, void* stream) {
+    if (!c || !geom_ok(g) || !fr || !tcw || !cam || !last || !n_last || !out || !out_n || last_stride <= 0 ||
+        min_matches < 0 || fr->reuse_grid)
+        return MAM_ERR_ARG;
+    MAM_DEVICE_SCOPE(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    mam::ProjArgs a{};
+    a.g = *g;
+    a.fr = *fr;
+    a.mode = 1;
+    a.unit_stride = last_stride;
+    a.n_units = n_last;
+    a.tcw = tcw;
+    a.cam = *cam;
+    a.last = last;
+    a.th = th;
+    a.check_ori = check_ori;
+    set_pool(c, a, last_stride);
+    a.out = out;
+    a.out_n = out_n;
+    if (int rc = launch_projection(c, a, fr->nframes, s)) return rc;
+    if (min_matches == 0) return MAM_OK;
+    // nmatches < 20: mvpMapPoints cleared and SearchByProjection(Cur, Last, 2 th) over the grid the first search built
+    // (the resolve stage rewrites every output slot of a retried frame)
+    a.fr.reuse_grid = 1;
+    a.th = 2.0f * th;
+    a.retry_below = min_matches;
+    return launch_projection(c, a, fr->nframes, s);
 }
 
 // ---- synchronous single-frame forms over host buffers (reference semantics)

@@ -216,6 +216,10 @@ _SIGS = {
                                                                C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                                                C.c_float, C.c_int, C.c_void_p, C.c_void_p,
                                                                C.c_void_p]),
+    "mam_track_motion_search_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                       C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                                       C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                                       C.c_void_p]),
     "mam_fuse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                            C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]),
     "mam_fuse_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
@@ -546,6 +550,17 @@ class ORBmatcher:
             self._ctx, C.byref(g), C.byref(frames), C.c_void_p(d_tcw), C.byref(cam), C.c_void_p(d_last),
             last_stride, C.c_void_p(d_nlast), float(th), int(self.mbCheckOrientation), C.c_void_p(d_out),
             C.c_void_p(d_nmatch), C.c_void_p(stream)), "search_motion_batch_device")
+
+    def track_motion_search_batch_device(self, F: FrameData, frames: FramesDev, d_tcw: int, cam: Pinhole,
+                                         d_last: int, last_stride: int, d_nlast: int, th: float, d_out: int,
+                                         d_nmatch: int, min_matches: int = 20, stream: int = 0):
+        """Tracking::TrackWithMotionModel's search (Tracking.cc:2811-2824): th, and 2 th for the frames that found
+        fewer than min_matches."""
+        g = F.geom()
+        return check(self._L.mam_track_motion_search_batch_device(
+            self._ctx, C.byref(g), C.byref(frames), C.c_void_p(d_tcw), C.byref(cam), C.c_void_p(d_last),
+            last_stride, C.c_void_p(d_nlast), float(th), int(self.mbCheckOrientation), int(min_matches),
+            C.c_void_p(d_out), C.c_void_p(d_nmatch), C.c_void_p(stream)), "track_motion_search_batch_device")
 
     def fuse_batch_device(self, F: FrameData, frames: FramesDev, d_kfs: int, cam: Pinhole, d_mps: int, mp_stride: int,
                           d_nmps: int, th: float, d_idx: int, d_dist: int, d_nfused: int, stream: int = 0):

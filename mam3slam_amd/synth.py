@@ -107,6 +107,37 @@ def frame_pose(w: int, h: int, frame: int, f: float = 500.0, depth: float = PLAN
     return q.astype(np.float32), np.array([txy[0], txy[1], 0.0], np.float32)
 
 
+def make_frame_camera(w: int, h: int, cam, agent: int = 0, frame: int = 0, f: float = 500.0,
+                      depth: float = PLANE_DEPTH, motion: bool = True) -> np.ndarray:
+    """make_frame's scene seen through camera `cam` (a match.KannalaBrandt8 — the testMultiAgentSystem agents' fisheye —
+    or a Pinhole) from the same pose, frame_pose(w, h, frame): every pixel's ray (cam.unproject_np) meets the canvas
+    plane z = depth (the camera rolls about z and translates in x / y, so the plane is at camera depth `depth` too),
+    where the canvas is sampled bilinearly (mirrored beyond its border). Keyframes of these frames see the scene
+    through the camera they are tracked with, so SearchForTriangulation's camera-specific epipolar test
+    (KannalaBrandt8::epipolarConstrain: two-view triangulation + reprojection) passes for true correspondences. The
+    u8 quantisation and sensor noise are make_frame's."""
+    from scipy.ndimage import map_coordinates
+
+    canvas_seed = frame_seed(agent, 0)
+    margin = 64
+    ch, cw = h + 2 * margin, w + 2 * margin + 4 * 256
+    canvas = make_canvas(ch, cw, canvas_seed)
+    q, t = frame_pose(w, h, frame, f, depth, motion)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    ray = cam.unproject_np(xx, yy)                              # (x / z, y / z) in the camera
+    xc, yc = ray[..., 0] * depth, ray[..., 1] * depth
+    a = -2.0 * np.arctan2(float(q[2]), float(q[3]))             # roll of frame_pose's quaternion (about z by -a)
+    ca, sa = np.cos(a), np.sin(a)
+    dx, dy = xc - float(t[0]), yc - float(t[1])                 # R^T (Xc - t), R = [[ca, sa], [-sa, ca]]
+    xw, yw = ca * dx - sa * dy, sa * dx + ca * dy
+    px = xw * f / depth + margin + (w - 1) / 2.0                # canvas pixel of the world point (frame_pose's model)
+    py = yw * f / depth + margin + (h - 1) / 2.0
+    out = map_coordinates(canvas, [py, px], order=1, mode="mirror")
+    rng = np.random.default_rng(frame_seed(agent, frame) ^ 0x5A5A)
+    out = out + rng.normal(0.0, 1.5, size=out.shape).astype(np.float32)
+    return np.ascontiguousarray(np.clip(np.rint(out), 0, 255).astype(np.uint8))
+
+
 def canvas_point(w: int, h: int, frame: int, px: np.ndarray, py: np.ndarray, motion: bool = True):
     """Canvas pixel coordinates of image pixels (px, py) of make_frame(w, h, agent, frame) (the inverse warp)."""
     k = frame if motion else 0

@@ -238,6 +238,17 @@ def search_by_projection_motion(F, last, cam, th, check_ori=True):
     return n, out[:len(keys)]
 
 
+def track_motion_search(F, last, cam, th=15.0, check_ori=True, min_matches=20):
+    """Tracking::TrackWithMotionModel's search (Tracking.cc:2811-2824): SearchByProjection(Cur, Last, th); with fewer
+    than 20 matches the current frame's MapPoints are cleared and the search runs again at 2 th. Returns (n, out,
+    retried)."""
+    n, out = search_by_projection_motion(F, last, cam, th, check_ori)
+    if n < min_matches:
+        n, out = search_by_projection_motion(F, last, cam, 2 * th, check_ori)
+        return n, out, True
+    return n, out, False
+
+
 def search_for_triangulation(KF1, KF2, F12, ep, check_ori=False, coarse=False):
     from mam3slam_amd.match import KP_DTYPE, FeatVec, flatten_featvec
 

@@ -39,10 +39,8 @@ def test_new_map_points_leg_matches_oracle(gpu_lib, oracle, cfg, B, W):
             checked += 1
             total += no
     assert checked >= 20
-    # keyframes at the poses of the cameras that rendered them (synth.frame_pose): real correspondences pass the
-    # epipolar tests (the fisheye c3 frames are rendered as Pinhole images, so only some do)
-    assert total > 0
-    if cfg != "c3":
-        assert total / checked >= 20, total / checked
+    # keyframes at the poses of the cameras that rendered them (synth.frame_pose, the c3 frames through the
+    # KannalaBrandt8 fisheye: synth.make_frame_camera): real correspondences pass the epipolar tests
+    assert total / checked >= 20, total / checked
     b = nm.algorithmic_bytes()
     assert b["candidate_pairs"] > 0 and b["bytes"] > 32 * b["candidate_pairs"]

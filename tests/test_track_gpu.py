@@ -1,5 +1,6 @@
 """GPU: the per-frame Tracking sequence bench.py times — TrackWithMotionModel (SearchByProjection(Cur, Last, th 15),
-Optimizer::PoseOptimization, outlier discard: Tracking.cc:2786-2862) then TrackLocalMap (isInFrustum +
+again at th 30 where it found fewer than 20 matches, Optimizer::PoseOptimization, outlier discard:
+Tracking.cc:2786-2862) then TrackLocalMap (isInFrustum +
 SearchByProjection(F, localMPs, th 1), PoseOptimization: Tracking.cc:2878-2901) — on device-resident frames, every
 stage against the oracle on the stage's own inputs: the searches index-exact, the PoseOptimization edges exact, its
 outlier sets identical and its pose within 1e-4, the discard and Frame::SetPose exact."""
@@ -43,8 +44,7 @@ def test_tracking_sequence_matches_oracle(gpu_lib, oracle, cfg):
         # TrackWithMotionModel: motion search at the motion model's guess
         F.pose = tr.poses_init[f]
         last = np.ascontiguousarray(tr.lasts[f], LAST_ENTRY_DTYPE)
-        _, o1 = oracle.search_by_projection_motion(F, last, tr.cam, 15.0, True)
-        assert (o1 >= 0).sum() >= 20, "TrackWithMotionModel's wider-window retry (nmatches < 20) is not reproduced"
+        _, o1, _ = oracle.track_motion_search(F, last, tr.cam, 15.0, True)
         idx = np.nonzero(o1 >= 0)[0]
         e1 = make_edges(F.keys, tr.inv_s2, idx, last["pos"][o1[idx]])
         assert int(pn[0, f]) == len(e1)
@@ -84,3 +84,74 @@ def test_tracking_sequence_matches_oracle(gpu_lib, oracle, cfg):
         # and it is the rendering camera's pose up to the noise of the synthetic MapPoints
         assert np.abs(tf - tr.poses[f][1]).max() < 0.02, (tf, tr.poses[f][1])
     assert n_out > 0   # the last frame's outlier block is rejected somewhere
+
+
+def test_motion_search_wider_window_retry(gpu_lib, oracle):
+    """TrackWithMotionModel's `nmatches < 20` branch (Tracking.cc:2816-2824) in the device step: frames whose motion
+    model guess is off by a rotation, with few last-frame MapPoints, find fewer than 20 matches with
+    SearchByProjection(Cur, Last, 15) and are searched again at th 30 with their matches cleared; the other frames of
+    the batch keep their first search. Index-exact against the oracle's sequence, with retried frames that recover,
+    a retried frame that stays below 20, and frames that are not retried in one batch."""
+    import torch
+
+    import bench
+    from mam3slam_amd import scene
+    from mam3slam_amd.match import LAST_ENTRY_DTYPE, quat_to_rot
+    from mam3slam_amd.pose import make_edges
+
+    dev = torch.device("cuda", 0)
+    B = 8
+    tr = bench.TrackingLeg(dict(bench.CONFIGS["c1"]), B, 2, 0, dev)
+    kps, cnt = tr.kps_h, tr.cnt_h
+    desc = tr.d_desc.cpu().numpy()
+    tcw = tr.d_tcw_init.cpu().numpy().view(np.float32).reshape(B, 7).copy()
+    nlast = tr.d_nlast.cpu().numpy().copy()
+
+    def rotated(pose, ang):
+        dq = np.array([0.0, np.sin(ang / 2), 0.0, np.cos(ang / 2)], np.float32)
+        ax, ay, az, aw = [float(x) for x in dq]
+        bx, by, bz, bw = [float(x) for x in pose[0]]
+        q = np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by + ay * bw + az * bx - ax * bz,
+                      aw * bz + az * bw + ax * by - ay * bx, aw * bw - ax * bx - ay * by - az * bz])
+        q = (q / np.linalg.norm(q)).astype(np.float32)
+        return q, (quat_to_rot(dq).astype(np.float64) @ np.asarray(pose[1], np.float64)).astype(np.float32)
+
+    # frames 0, 2, 4: 40 last-frame MapPoints and a guess rotated until th 15 finds < 20 and th 30 >= 20; frame 6: 12
+    # MapPoints (the retry cannot reach 20 either); odd frames unchanged
+    expect = []
+    for f in range(B):
+        n = int(cnt[f, 0])
+        F = scene.make_frame_data(kps[f, :n], desc[f, :n], tr.W, tr.H)
+        last = np.ascontiguousarray(tr.lasts[f], LAST_ENTRY_DTYPE)
+        pose = tr.poses_init[f]
+        if f % 2 == 0:
+            nl = 12 if f == 6 else 40
+            last = last[:nl]
+            for ang in np.arange(0.02, 0.2, 0.01):
+                F.pose = rotated(tr.poses_init[f], ang)
+                n15, _ = oracle.search_by_projection_motion(F, last, tr.cam, 15.0, True)
+                n30, _ = oracle.search_by_projection_motion(F, last, tr.cam, 30.0, True)
+                if n15 < 20 and (n30 >= 20 or f == 6):
+                    break
+            assert n15 < 20 and (n30 >= 20 or f == 6), (f, n15, n30)
+            pose = F.pose
+            nlast[f] = nl
+            tcw[f, :4], tcw[f, 4:] = pose
+        F.pose = pose
+        expect.append(oracle.track_motion_search(F, last, tr.cam, 15.0, True) + (last,))
+    assert [e[2] for e in expect] == [f % 2 == 0 for f in range(B)]
+    assert expect[0][0] >= 20 and expect[6][0] < 20
+    tr.d_tcw_init.copy_(torch.from_numpy(tcw.view(np.uint8).reshape(-1)).to(dev))
+    tr.d_nlast.copy_(torch.from_numpy(nlast).to(dev))
+    tr.step()
+    torch.cuda.synchronize()
+    nm1 = tr.d_nm1.cpu().numpy()
+    pn = tr.d_pn.cpu().numpy()
+    for f in range(B):
+        n = int(cnt[f, 0])
+        no, oo, _, last = expect[f]
+        assert int(nm1[f]) == no, (f, int(nm1[f]), no)
+        # PoseOptimization call 1 received the final search's matches
+        idx = np.nonzero(oo >= 0)[0]
+        keys = scene.make_frame_data(kps[f, :n], desc[f, :n], tr.W, tr.H).keys
+        assert int(pn[0, f]) == len(make_edges(keys, tr.inv_s2, idx, last["pos"][oo[idx]])), f
