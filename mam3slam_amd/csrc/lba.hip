@@ -44,21 +44,44 @@
 namespace mam {
 namespace lba {
 
-// Levenberg state of one problem (levenberg.cpp members + the optimize() loop counters)
-struct LM {
-    double lambda, ni;
-    double currentChi, iniChi, acceptedChi, initialChi;
-    int its, trials, qmax, nBad;
-    int need_lin;    // the next slot starts an iteration (linearize + build)
+// Levenberg state of one problem (levenberg.cpp members + the optimize() loop counters). The first 80 bytes are what
+// kernels test and read on entry (LMHead: five 16-byte loads issued together, one memory round trip instead of a
+// dependent load per field).
+struct alignas(16) LM {
+    int status;      // MAM_OK or MAM_ERR_*
     int done;        // optimize() returned
+    int need_lin;    // the next slot starts an iteration (linearize + build)
     int cur;         // which state buffer holds the current estimate
     int fail;        // the last LDL^T hit a zero pivot
-    int status;      // MAM_OK or MAM_ERR_*
+    int sys_ready;   // the iteration start's linearisation and system are built (the setup pass did iteration 0's)
+    int tiles_lds;   // all non-zero tiles + y fit the factorization's LDS: k_ldlt_tiles factors in LDS
+    int maxc;        // the most non-zero tiles below the diagonal tile in any block column (k_struct_tiles)
+    int its, trials, qmax, nBad;
     int iterations;  // optimize(iterations)
-    unsigned long long maxdiag;   // max |diag(H)| of the iteration's system (bits of a non-negative double)
     int ntiles;      // structurally non-zero 16x16 tiles of L (lower triangle incl. the diagonal; k_struct_tiles)
-    int tiles_lds;   // all of them + y fit the factorization's LDS: k_ldlt factors in LDS (ldlt_tiles)
+    int pad0, pad1;
+    double lambda;
+    unsigned long long maxdiag;   // max |diag(H)| of the iteration's system (bits of a non-negative double)
+    double ni;
+    double currentChi, iniChi, acceptedChi, initialChi;
+    double scale_p;  // computeScale's pose part of the trial (the factorization's epilogue)
 };
+struct alignas(16) LMHead {
+    int status, done, need_lin, cur, fail, sys_ready, tiles_lds, maxc, its, trials, qmax, nBad, iterations, ntiles,
+        pad0, pad1;
+    double lambda;
+    unsigned long long maxdiag;
+};
+static_assert(sizeof(LMHead) == 80, "LMHead is the first 80 bytes of LM");
+__device__ __forceinline__ LMHead lm_head(const LM* lm) {
+    typedef __attribute__((address_space(1))) const int gi32;   // global loads (adjacent: merged into 16-byte loads)
+    int v[20];
+#pragma unroll
+    for (int k = 0; k < 20; k++) v[k] = ((gi32*)lm)[k];
+    LMHead h;
+    __builtin_memcpy(&h, v, sizeof(h));
+    return h;
+}
 
 struct Prob {
     int P, L, E, Np, npad, n_cams, cam_model;
@@ -92,6 +115,13 @@ struct Prob {
     uint8_t* tmask;              // [nt][nt] (r >= c): 16x16 tile (r, c) of L is structurally non-zero (S + fill)
     int16_t* tslot;              // [nt][nt]: the tile's slot in the LDS tile pool (ldlt_tiles), -1 structurally zero
     int16_t* tlist;              // [ntiles][2]: (r, c) of each slot
+    // per block column kc (nt <= 40, the LDS factorization): the rows r > kc of its non-zero tiles (clist, stride 40),
+    // per block row kc the columns c < kc (rlist), their counts (ccnt[kc], ccnt[nt + kc]); k_struct_tiles
+    int8_t* clist_g;
+    int8_t* rlist_g;
+    uint8_t* ccnt_g;
+    double* pool;                // [ntiles][256]: S's non-zero tiles in slot order, each 16 x 16 tile as the LDS
+                                 // factorization holds it (tsw layout); written by k_schur_blk when lm.tiles_lds
     int nt;                      // npad / 16
     // state: [2] buffers, lm->cur is the current one
     double* pose[2];             // [P][7] q(xyzw) t
@@ -181,11 +211,10 @@ __device__ __forceinline__ void wave_sum_scatter4(const double (&v)[4 * Q], doub
 // ---- per edge: error, robust weight, Jacobians (EdgeSE3ProjectXYZ); returns the edge's rho0
 // jo / ho: where the edge's jac (21) and H_pl (18) records go (the caller's LDS staging slots); both are always
 // written when want_jac (zeros where the edge is inactive or its pose fixed).
-__device__ __forceinline__ double linearize_edge(const Prob& d, const double* pose, const double* pts, int e,
-                                                 bool want_jac, double* jo, double* ho) {
-    const int ip = d.edge_point[e], ipose = d.edge_pose[e];
-    const double* T = pose + 7 * (size_t)ipose;
-    const double* X = pts + 3 * (size_t)ip;
+// linearize_edge_at: the same with the pose T and point X given (the fused point kernels hold X in LDS); write_err =
+// false leaves d.err alone (a pass that only needs the Jacobian terms).
+__device__ __forceinline__ double linearize_edge_at(const Prob& d, const double* T, const double* X, int ipose, int e,
+                                                    bool want_jac, bool write_err, double* jo, double* ho) {
     double Xc[3];
     map_point(T, X, Xc);
     const bool kb8 = d.cam_model == MAM_CAM_KANNALA_BRANDT8;
@@ -203,8 +232,10 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
         v = c[1] * Xc[1] / Xc[2] + c[3];
     }
     const double e0 = d.edge_obs[2 * e] - u, e1 = d.edge_obs[2 * e + 1] - v;
-    d.err[2 * e] = e0;
-    d.err[2 * e + 1] = e1;
+    if (write_err) {
+        d.err[2 * e] = e0;
+        d.err[2 * e + 1] = e1;
+    }
     if (d.active && !d.active[e]) {
         // setLevel(1): outside initializeOptimization(0), no term in chi2 / H / b (zeros add exactly nothing)
         if (want_jac) {
@@ -268,6 +299,12 @@ __device__ __forceinline__ double linearize_edge(const Prob& d, const double* po
         for (int k = 0; k < 18; k++) ho[k] = 0.0;
     }
     return r0;
+}
+
+__device__ __forceinline__ double linearize_edge(const Prob& d, const double* pose, const double* pts, int e,
+                                                 bool want_jac, double* jo, double* ho) {
+    const int ip = d.edge_point[e], ipose = d.edge_pose[e];
+    return linearize_edge_at(d, pose + 7 * (size_t)ipose, pts + 3 * (size_t)ip, ipose, e, want_jac, true, jo, ho);
 }
 
 // ================================================================================== device structure build
@@ -545,51 +582,39 @@ __device__ __forceinline__ void wave_copy_in(double* __restrict__ dst, const dou
 // lambda_0 = tau * max diag(H), tau = 1e-5 (computeLambdaInit :171-185), from the max k_sys gathered (max is exact in
 // any order); k_ctl_end commits it to lm.lambda with the rest of the iteration-start state, so no control kernel runs
 // between k_sys and the Schur kernels (one launch, and one dependency wait under load, fewer per trial).
+__device__ __forceinline__ double trial_lambda(const LMHead& h) {
+    return (h.need_lin && h.its == 0) ? 1e-5 * __longlong_as_double((long long)h.maxdiag) : h.lambda;
+}
 __device__ __forceinline__ double trial_lambda(const LM& lm) {
     return (lm.need_lin && lm.its == 0) ? 1e-5 * __longlong_as_double((long long)lm.maxdiag) : lm.lambda;
 }
 
-// grid (ceil(E/64), Q) x 64: one wave per 64 edges; the rho0 partial sum per wave (fixed-order butterfly).
-// mode 0: iteration start (Jacobians, current state); 1: trial (errors only, trial state) and the computeScale
-// partial sums; 2: initial chi2.
-__global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs, int mode) {
+// grid (ceil(E/64), Q) x 64, the setup pass (once per solve): iteration 0's linearisation at the initial state — one
+// wave per 64 edges: errors, Jacobians (jac, H_pl records, through one LDS staging buffer as contiguous 16-byte chunks)
+// and the rho0 partial sum per wave (fixed-order butterfly) of the initial chi2. The trials' linearisations are the
+// fused point kernels' (k_point_sys, k_point_trial).
+__global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
-    const LM& lm = *d.lm;
-    if (lm.status || (mode != 2 && lm.done) || (mode == 0 && !lm.need_lin)) return;
+    const LMHead hd = lm_head(d.lm);
+    if (hd.status) return;
     __shared__ double sj[EW * 21];   // one staging buffer (LDS bounds the resident waves of this one-wave kernel)
     const int e0 = blockIdx.x * EW;
-    if (e0 < d.E) {
-        const int sidx = mode == 1 ? 1 - lm.cur : lm.cur;
-        const int lane = lane_id(), e = e0 + lane;
-        double jr[21], hr[18];   // the edge's records in registers, staged through one LDS buffer in turn
-        double r = e < d.E ? linearize_edge(d, d.pose[sidx], d.pt[sidx], e, mode == 0, jr, hr) : 0.0;
-        r = wave_sum_d(r);
-        if (lane == 0) (mode == 0 ? d.part0 : d.part)[blockIdx.x] = r;
-        if (mode == 0) {
-            const int ne = min(EW, d.E - e0);
+    if (e0 >= d.E) return;
+    const int lane = lane_id(), e = e0 + lane;
+    double jr[21], hr[18];   // the edge's records in registers, staged through one LDS buffer in turn
+    double r = e < d.E ? linearize_edge(d, d.pose[hd.cur], d.pt[hd.cur], e, true, jr, hr) : 0.0;
+    r = wave_sum_d(r);
+    if (lane == 0) d.part0[blockIdx.x] = r;
+    const int ne = min(EW, d.E - e0);
 #pragma unroll
-            for (int k = 0; k < 21; k++) sj[21 * lane + k] = jr[k];
-            __syncthreads();
-            wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
-            __syncthreads();
+    for (int k = 0; k < 21; k++) sj[21 * lane + k] = jr[k];
+    __syncthreads();
+    wave_copy_out(d.jac + 21 * (size_t)e0, sj, 21 * ne);
+    __syncthreads();
 #pragma unroll
-            for (int k = 0; k < 18; k++) sj[18 * lane + k] = hr[k];
-            __syncthreads();
-            wave_copy_out(d.hpl + 18 * (size_t)e0, sj, 18 * ne);
-        }
-    }
-    if (mode == 1) {
-        // computeScale partials: block b < nbl sums x_j (lambda x_j + b_j) over the 64-chunks b, b + nbl, ... of x
-        const int nbl = max(1, (d.E + EW - 1) / EW);
-        if ((int)blockIdx.x < nbl) {
-            const double lambda = trial_lambda(lm);
-            const int nx = 6 * d.Np + 3 * d.L;
-            double acc = 0.0;
-            for (int j = blockIdx.x * EW + lane_id(); j < nx; j += nbl * EW) acc += d.x[j] * (lambda * d.x[j] + d.b[j]);
-            acc = wave_sum_d(acc);
-            if (lane_id() == 0) d.part_s[blockIdx.x] = acc;
-        }
-    }
+    for (int k = 0; k < 18; k++) sj[18 * lane + k] = hr[k];
+    __syncthreads();
+    wave_copy_out(d.hpl + 18 * (size_t)e0, sj, 18 * ne);
 }
 
 // grid (ceil(L/64) + Np, Q) x 64: H_ll, b_l per point (edge order, one thread each) and H_pp, b_p per optimised pose
@@ -727,7 +752,7 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
     const Prob& d = probs[blockIdx.x];
     LM& lm = *d.lm;
     if (lm.status) return;
-    const double chi = chi_of_parts<RED>(d, d.part, s);
+    const double chi = chi_of_parts<RED>(d, d.part0, s);
     if (threadIdx.x == 0) {
         lm.initialChi = chi;
         lm.acceptedChi = chi;
@@ -737,99 +762,38 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
         lm.its = lm.trials = lm.qmax = lm.nBad = 0;
         lm.fail = 0;
         lm.need_lin = 1;
+        lm.sys_ready = 1;   // the setup's k_linearize + k_sys built iteration 0's system
         lm.done = (d.Np + d.L == 0 || lm.iterations <= 0) ? 1 : 0;
     }
 }
 
 
 // grid (ceil(L/64) + Np, Q) x 64: the system (sys_body) and max |diag(H)| (one device atomic per wave)
+// (the setup pass: iteration 0's system; lambda_0 = 1e-5 max |diag(H)| is the only max the Levenberg loop reads)
 __global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     LM& lm = *d.lm;
-    if (lm.status || lm.done || !lm.need_lin) return;
+    if (lm.status) return;
     double m = sys_body(d);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
-    // only the first iteration's max is read (lambda_0, trial_lambda): later iterations skip the contended atomics
-    if (threadIdx.x == 0 && m > 0.0 && lm.its == 0) atomicMax(&lm.maxdiag, (unsigned long long)__double_as_longlong(m));
+    if (threadIdx.x == 0 && m > 0.0) atomicMax(&lm.maxdiag, (unsigned long long)__double_as_longlong(m));
 }
 
 // ---- Schur
-// D = H_ll + lambda I (setLambda, block_solver.hpp:563-589) and its inverse (Eigen's 3x3 inverse, :389)
-__device__ __forceinline__ void point_dinv(const Prob& d, int h, double lambda, double Di[9]) {
-    double m[9];
-    for (int k = 0; k < 9; k++) m[k] = d.Hll[9 * (size_t)h + k] + ((k % 4 == 0) ? lambda : 0.0);
-    double* o = Di;
-    // Eigen 3.4 compute_inverse<3> (LU/InverseImpl.h): the column-0 cofactors, det = their dot with column 0
-    // summed c0 m00 + (c1 m10 + c2 m20) (the unrolled redux of a 3-vector, as camera.hpp inv3), invdet = 1 / det, result(r, c) = cofactor(c, r) * invdet
-    const double c00 = m[4] * m[8] - m[5] * m[7], c10 = m[7] * m[2] - m[8] * m[1], c20 = m[1] * m[5] - m[2] * m[4];
-    const double det = c00 * m[0] + (c10 * m[3] + c20 * m[6]);
-    const double inv = 1.0 / det;
-    o[0] = c00 * inv; o[1] = c10 * inv; o[2] = c20 * inv;
-    o[3] = (m[5] * m[6] - m[3] * m[8]) * inv; o[4] = (m[8] * m[0] - m[6] * m[2]) * inv;
-    o[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
-    o[6] = (m[3] * m[7] - m[4] * m[6]) * inv; o[7] = (m[6] * m[1] - m[7] * m[0]) * inv;
-    o[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
-}
+// Entry (r, c) of a 16 x 16 tile in the LDS factorization's layout (column-major, rows XOR-swizzled by the column: the
+// MFMA operand reads, the accumulator reads / writes and the row-per-thread panel rows are free of bank conflicts)
+__host__ __device__ __forceinline__ int tsw(int r, int c) { return c * 16 + (r ^ c); }
 
-// grid (ceil(max(E, L)/64), Q) x 64: one wave per 64 edges (block_solver.hpp:405-427): the edge's point D^-1 (the
-// point's first edge stores it for the back-substitution), W = H_pl D^-1 and the coefficient H_pl D^-1 b_l; H_pl in
-// and W / coefficients out as contiguous per-wave blocks through LDS. Points without edges get D^-1 from lane h.
-__global__ __launch_bounds__(EW) void k_schur_prep(const Prob* __restrict__ probs) {
-    const Prob& d = probs[blockIdx.y];
-    const LM& lm = *d.lm;
-    if (lm.status || lm.done) return;
-    const double lambda = trial_lambda(lm);
-    const int lane = lane_id();
-    {
-        const int h = blockIdx.x * EW + lane;
-        if (h < d.L && d.pe_off[h + 1] == d.pe_off[h]) {
-            double Di[9];
-            point_dinv(d, h, lambda, Di);
-            for (int k = 0; k < 9; k++) d.Dinv[9 * (size_t)h + k] = Di[k];
-        }
+// S(row, col) of the lower triangle: into the tile pool (problems factored in LDS: the tile's slot, skipped for a
+// structurally zero tile, where only zeros land) or the dense npad x npad array
+__device__ __forceinline__ void s_store(const Prob& d, bool pool, int row, int col, double v) {
+    if (pool) {
+        const int sl = d.tslot[(size_t)(row >> 4) * d.nt + (col >> 4)];
+        if (sl >= 0) d.pool[(size_t)sl * 256 + tsw(row & 15, col & 15)] = v;
+    } else {
+        d.S[(size_t)row * d.npad + col] = v;
     }
-    const int e0 = blockIdx.x * EW;
-    if (e0 >= d.E) return;
-    __shared__ double sh[EW * 18];   // H_pl in, then W, then the coefficients out (one buffer: occupancy)
-    const int ne = min(EW, d.E - e0);
-    wave_copy_in(sh, d.hpl + 18 * (size_t)e0, 18 * ne);
-    __syncthreads();
-    const int e = e0 + lane;
-    double o[18], cf[6];
-#pragma unroll
-    for (int k = 0; k < 18; k++) o[k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; k++) cf[k] = 0.0;
-    if (e < d.E) {
-        const int4 em = d.emeta[e];
-        if (em.y >= 0 || em.z) {
-            const int h = em.x;
-            double Di[9];
-            point_dinv(d, h, lambda, Di);
-            if (em.z)
-                for (int k = 0; k < 9; k++) d.Dinv[9 * (size_t)h + k] = Di[k];
-            const double* bl = d.b + 6 * (size_t)d.Np + 3 * (size_t)h;
-            double db[3];
-            for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
-            const double* B = sh + 18 * lane;
-            for (int i = 0; i < 6; i++) {
-                for (int j = 0; j < 3; j++)
-                    o[3 * i + j] = B[3 * i] * Di[j] + B[3 * i + 1] * Di[3 + j] + B[3 * i + 2] * Di[6 + j];
-                cf[i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 18; k++) sh[18 * lane + k] = o[k];
-    __syncthreads();
-    wave_copy_out(d.bdinv + 18 * (size_t)e0, sh, 18 * ne);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 6; k++) sh[6 * lane + k] = cf[k];
-    __syncthreads();
-    wave_copy_out(d.coef + 6 * (size_t)e0, sh, 6 * ne);
 }
 
 // triangle index q -> (tr, tc), tc <= tr
@@ -891,8 +855,8 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
     if (i1 != i2 && !d.pairmask[(size_t)i1 * d.Np + i2]) {
         // no shared landmark: a zero block (the factorization's fill-in of the previous trial is overwritten)
         if (lane < 36) {
-            const int r = lane / 6, c = lane % 6, N = d.npad;
-            d.S[(size_t)(6 * i2 + c) * N + 6 * i1 + r] = 0.0;
+            const int r = lane / 6, c = lane % 6;
+            s_store(d, lm.tiles_lds != 0, 6 * i2 + c, 6 * i1 + r, 0.0);
         }
         return;
     }
@@ -965,8 +929,7 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
         const int r = k / 6, c = k % 6;
         double out = -v;
         if (i1 == i2) out = (d.Hpp[36 * (size_t)i1 + k] + (r == c ? lambda : 0.0)) - v;
-        const int N = d.npad;
-        d.S[(size_t)(6 * i2 + c) * N + 6 * i1 + r] = out;   // the lower triangle, the one the factorization reads
+        s_store(d, lm.tiles_lds != 0, 6 * i2 + c, 6 * i1 + r, out);   // the lower triangle, the one the factorization reads
     }
 }
 
@@ -1150,6 +1113,35 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
         lm.tiles_lds = (nt <= LDLT_TILES_NT_MAX && (size_t)carry * 256 * sizeof(double) + (size_t)d.npad * sizeof(double) <=
                                                         (size_t)lds_bytes) ? 1 : 0;
     }
+    __syncthreads();
+    // the factorization's column / row lists (what it walked its slot map for at every launch), and the pool's padding
+    // rows (the last tile row, rows >= n: an identity block after the unknowns, zeros elsewhere; k_schur_blk writes
+    // every other entry of the pool every trial)
+    __shared__ int maxc;
+    if (t == 0) maxc = 0;
+    __syncthreads();
+    if (nt <= LDLT_TILES_NT_MAX) {
+        for (int k = t; k < nt; k += SB) {
+            int nc = 0, nr = 0;
+            for (int r = k + 1; r < nt; r++)
+                if (d.tmask[(size_t)r * nt + k]) d.clist_g[k * 40 + nc++] = (int8_t)r;
+            for (int c = 0; c < k; c++)
+                if (d.tmask[(size_t)k * nt + c]) d.rlist_g[k * 40 + nr++] = (int8_t)c;
+            d.ccnt_g[k] = (uint8_t)nc;
+            d.ccnt_g[nt + k] = (uint8_t)nr;
+            atomicMax(&maxc, nc);
+        }
+        if (nt > 0)
+            for (int q = t; q < nt * 256; q += SB) {
+                const int c = q >> 8, e = q & 255;
+                const int j = e >> 4, i = (e & 15) ^ j;   // tsw(i, j) = j * 16 + (i ^ j)
+                const int gi = NB * (nt - 1) + i, gj = NB * c + j;
+                const int sl = d.tslot[(size_t)(nt - 1) * nt + c];
+                if (gi >= n && sl >= 0) d.pool[(size_t)sl * 256 + e] = gi == gj ? 1.0 : 0.0;
+            }
+    }
+    __syncthreads();
+    if (t == 0) d.lm->maxc = maxc;
 }
 
 
@@ -1396,10 +1388,15 @@ struct LdltShared {
     int16_t tl[2 * 96];          // ldlt_tiles: (r, c) of each pool slot
     // ldlt_tiles: per block column kc the rows r > kc of its non-zero tiles (ascending), per block row kc the columns
     // c < kc of its non-zero tiles — the panel / trailing / backward loops walk only those
-    int8_t clist[40 * 40];
-    int8_t rlist[40 * 40];
+    alignas(4) int8_t clist[40 * 40];
+    alignas(4) int8_t rlist[40 * 40];
     uint8_t ccount[40];
     uint8_t rcount[40];
+    // ldlt_tiles' dataflow form: every column's D, the columns' factored / solved flags, the widest column's tile count
+    double dkall[40][NB];
+    int cflag[40];
+    int bflag[40];
+    int maxc;
 };
 
 // S factored in place in HBM with the panel / block-column workspace in LDS (use_lds) or in the problem's scratch: the
@@ -1608,7 +1605,7 @@ __device__ __forceinline__ void ldlt_global(const Prob& d, double* lds_ws, LdltS
 // Tile layout: element (r, c) at c * 16 + (r ^ c) (column-major, rows XOR-swizzled by the column): the MFMA A / B
 // operand reads (16 rows of one column per 16 lanes), the accumulator reads / writes (16 columns of one row) and the
 // row-per-thread panel rows are all free of LDS bank conflicts within a 32-lane group.
-__device__ __forceinline__ int tsw(int r, int c) { return c * NB + (r ^ c); }
+// (tsw: see k_schur_blk)
 
 // C(sc) -= L(sa) D L(sb)^T on tiles of the pool (one wave): four v_mfma_f64_16x16x4_f64, operands from LDS
 __device__ __forceinline__ void tile_update(double* TL, int sc, int sa, int sb, const double* dkp, int lane) {
@@ -1628,6 +1625,58 @@ __device__ __forceinline__ void tile_update(double* TL, int sc, int sa, int sb, 
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) C[tsw(rq + 4 * r, col)] = acc[r];
+}
+
+// tile_update for N tiles that share the B operand L(sb) (the updates one column pulls from column j): every LDS load
+// first, then the N MFMA chains interleaved, then the stores — one tile's latency instead of N in turn (the pointers
+// may alias as far as the compiler knows, so separate tile_update calls run back to back). Per tile the same four
+// MFMAs in the same order as tile_update.
+// With yj: also y_kc -= L(kc, j) y_j for the lane's row il (L(kc, j) = L(sb)), the same sequential FMAs as the tall
+// panel's panel-row forward update, its operands loaded with the tiles'.
+template <int N>
+__device__ __forceinline__ void tile_update_multi(double* TL, const int* sc, const int* sa, int sb, const double* dkp,
+                                                  int lane, const double* yj = nullptr, double* yd = nullptr) {
+    const int col = lane & 15, rq = lane >> 4;
+    const double* Lb = TL + (size_t)sb * 256;
+    double bv[4], av[N][4], lv[NB], yv[NB];
+    dbl4 acc[N];
+    if (yj) {
+#pragma unroll
+        for (int k = 0; k < NB; k++) {
+            lv[k] = Lb[tsw(col, k)];
+            yv[k] = yj[k];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) bv[q] = Lb[tsw(col, 4 * q + rq)] * dkp[4 * q + rq];
+#pragma unroll
+    for (int u = 0; u < N; u++) {
+        if (sa[u] < 0) continue;   // uniform: no tile u
+        const double* C = TL + (size_t)sc[u] * 256;
+        const double* La = TL + (size_t)sa[u] * 256;
+#pragma unroll
+        for (int r = 0; r < 4; r++) acc[u][r] = C[tsw(rq + 4 * r, col)];
+#pragma unroll
+        for (int q = 0; q < 4; q++) av[u][q] = -La[tsw(col, 4 * q + rq)];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int u = 0; u < N; u++)
+            if (sa[u] >= 0) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u][q], bv[q], acc[u], 0, 0, 0);
+    if (yj) {
+        double v = *yd;
+#pragma unroll
+        for (int k = 0; k < NB; k++) v = fma(-lv[k], yv[k], v);
+        *yd = v;
+    }
+#pragma unroll
+    for (int u = 0; u < N; u++) {
+        if (sa[u] < 0) continue;
+        double* C = TL + (size_t)sc[u] * 256;
+#pragma unroll
+        for (int r = 0; r < 4; r++) C[tsw(rq + 4 * r, col)] = acc[u][r];
+    }
 }
 
 // ---- tall panels: the panel tiles factored together with the diagonal tile, lane (g, i) = (lane >> 4, lane & 15)
@@ -1744,9 +1793,154 @@ __device__ __forceinline__ void tall_panel(double* TL, const int16_t* slot, int 
     }
 }
 
-__device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShared& sh) {
+// ---- dataflow form for banded tile patterns (every column has at most 4 non-zero tiles below its diagonal tile, so one
+// tall-panel item per column): no workgroup barriers inside the factorization. Block column kc belongs to wave
+// kc % NW; the owner pulls every update its tiles receive — for each column j < kc with tile (kc, j) non-zero, in
+// ascending j: T(r, kc) -= L(r, j) D_j L(kc, j)^T for its non-zero rows r, and y_kc -= L(kc, j) y_j — waiting for
+// column j's LDS flag only when it gets there, so the updates from older columns run while the column before is still
+// being factored; then its tall panel (without the push of the panel rows' y: they pull theirs), the diagonal tile's
+// L^-T for the backward solve, and its flag. The backward solve runs the same way in reverse (column kc pulls
+// L(r, kc)^T x_r from its rows r once their flags are set). Every tile and every y entry sees the same updates in the
+// same order with the same arithmetic as in the right-looking schedule of ldlt_tiles.
+__device__ __forceinline__ int lds_flag_load(const int* f) {
+    return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_flag_wait(const int* f) {
+    while (!lds_flag_load(f)) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void lds_flag_set(int* f) {
+    __hip_atomic_store(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// column kc of the dataflow factorization (its owner wave)
+__device__ __forceinline__ void flow_factor_column(double* TL, const int16_t* slot, int nt, int kc, double* Y,
+                                                   LdltShared& sh, int lane) {
+    const int g = lane >> 4, il = lane & 15, kb = NB * kc;
+    // the column's structure (LDS, the same in every lane) as scalars: uniform loops and branches
+    const int ncl = __builtin_amdgcn_readfirstlane(sh.ccount[kc]), nrl = __builtin_amdgcn_readfirstlane(sh.rcount[kc]);
+    const int sd = __builtin_amdgcn_readfirstlane(slot[kc * nt + kc]);
+    int rows[4], rsl[4];
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        rows[a] = a < ncl ? __builtin_amdgcn_readfirstlane(sh.clist[kc * 40 + a]) : -1;
+        rsl[a] = a < ncl ? __builtin_amdgcn_readfirstlane(slot[rows[a] * nt + kc]) : -1;
+    }
+#ifdef MAM_LDLT_PROFILE
+    long long tp0 = clock64();
+#endif
+    double yd = Y[kb + il];
+    for (int q = 0; q < nrl; q++) {
+        const int j = __builtin_amdgcn_readfirstlane(sh.rlist[kc * 40 + q]);
+        const int sb = __builtin_amdgcn_readfirstlane(slot[kc * nt + j]);
+        // the diagonal tile and the panel tiles (r, kc) whose L(r, j) is non-zero (sa < 0: none), in row order
+        int sc[5], sa[5];
+        sc[0] = sd;
+        sa[0] = sb;
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+            sc[1 + a] = rsl[a];
+            sa[1 + a] = a < ncl ? __builtin_amdgcn_readfirstlane(slot[rows[a] * nt + j]) : -1;
+        }
+        const double* dkj = sh.dkall[j];
+        const double* yj = Y + NB * j;
+        lds_flag_wait(&sh.cflag[j]);
+#ifdef MAM_LDLT_PROFILE
+        tp0 = clock64();   // after the last wait: the column's critical pull
+#endif
+        // y_kc -= L(kc, j) y_j (the panel-row forward update column j's tall panel did in the right-looking form)
+        // rides on the batched tile update
+        tile_update_multi<5>(TL, sc, sa, sb, dkj, lane, yj, &yd);
+    }
+    // the tall panel: the diagonal tile and the (<= 4) panel tiles, lane (g, il)
+    const int r = g == 0 ? rows[0] : g == 1 ? rows[1] : g == 2 ? rows[2] : rows[3];
+    const int rs = g == 0 ? rsl[0] : g == 1 ? rsl[1] : g == 2 ? rsl[2] : rsl[3];
+    double* Td = TL + (size_t)sd * 256;
+    double* Tp = TL + (size_t)(r >= 0 ? rs : sd) * 256;
+    double dr[NB], pr[NB];
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        dr[c] = Td[tsw(il, c)];
+        pr[c] = r >= 0 ? Tp[tsw(il, c)] : 0.0;
+    }
+    double yp = 0.0, dmine = 1.0;
+#ifdef MAM_LDLT_PROFILE
+    long long tp1 = clock64();
+    if (lane == 0) atomicAdd(&g_lprof[6], (unsigned long long)(tp1 - tp0));   // the critical pull + the panel loads
+#endif
+    Tall16<0>::run(dr, pr, yd, yp, dmine, il);
+#ifdef MAM_LDLT_PROFILE
+    long long tp2 = clock64();
+    if (lane == 0) atomicAdd(&g_lprof[5], (unsigned long long)(tp2 - tp1));   // the tall panel's pivot steps
+#endif
+    if (g == 0) {
+#pragma unroll
+        for (int c = 0; c < NB; c++)
+            if (c <= il) Td[tsw(il, c)] = c < il ? dr[c] : dmine;
+        sh.dkall[kc][il] = dmine;
+        Y[kb + il] = yd;
+        if (dmine == 0.0) sh.fail = 1;
+    }
+    if (r >= 0) {
+#pragma unroll
+        for (int c = 0; c < NB; c++) Tp[tsw(il, c)] = pr[c];
+    }
+    lds_flag_set(&sh.cflag[kc]);
+#ifdef MAM_LDLT_PROFILE
+    if (lane == 0) atomicAdd(&g_lprof[2], (unsigned long long)(clock64() - tp2));   // stores + flag
+#endif
+    // the diagonal tile's L^-T into its upper triangle (the backward solve's block), from the factored rows in registers
+    // (lane R's dr[J] = L(R, J) for J < R): off the critical path, the next columns no longer read this tile's upper part
+    if (g == 0) {
+        double x[NB];
+#pragma unroll
+        for (int c = 0; c < NB; c++) x[c] = (c == il) ? 1.0 : 0.0;
+        InvR16<0, 1>::run(x, dr);
+#pragma unroll
+        for (int c = 0; c < NB; c++)
+            if (c > il) Td[tsw(il, c)] = x[c];
+    }
+}
+
+// backward step of column kc (its owner wave): x_kc = L_kc^-T (y_kc / D_kc - sum_r L(r, kc)^T x_r), r over the column's
+// non-zero tiles in descending order (the order the right-looking backward solve applied them in)
+__device__ __forceinline__ void flow_back_column(const double* TL, const int16_t* slot, int nt, int kc, double* Y,
+                                                 LdltShared& sh, int lane) {
+    const int il = lane & 15, kb = NB * kc;
+    const double* Td = TL + (size_t)slot[kc * nt + kc] * 256;
+    double v = Y[kb + il] / Td[tsw(il, il)];
+    for (int a = sh.ccount[kc] - 1; a >= 0; a--) {
+        const int r = sh.clist[kc * 40 + a];
+        lds_flag_wait(&sh.bflag[r]);
+        const double* Tr = TL + (size_t)slot[r * nt + kc] * 256;
+        const double* xr = Y + NB * r;
+        double sy1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < NB / 2; j++) v = fma(xr[j], -Tr[tsw(j, il)], v);   // y_i -= L(r + j, i) x_j: two partial
+#pragma unroll                                                                  // chains of 8 (j < 8, j >= 8)
+        for (int j = NB / 2; j < NB; j++) sy1 = fma(xr[j], -Tr[tsw(j, il)], sy1);
+        v += sy1;
+    }
+    // x_b = L11^-T y_b from the upper triangle the factor step wrote; y_j from lane j of the lane's own 16-lane row
+    // (every row holds the block's y) by DPP
+    double w = v, w1 = 0.0;
+#pragma unroll
+    for (int j = 1; j < NB / 2; j++) {
+        const double f = fma(Td[tsw(il, j)], bcast16_d(v, j), w);
+        w = j > il ? f : w;
+    }
+#pragma unroll
+    for (int j = NB / 2; j < NB; j++) {
+        const double f = fma(Td[tsw(il, j)], bcast16_d(v, j), w1);
+        w1 = j > il ? f : w1;
+    }
+    w += w1;
+    if (lane < NB) Y[kb + lane] = w;
+    lds_flag_set(&sh.bflag[kc]);
+}
+
+__device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShared& sh, const LMHead& hd) {
     LM& lm = *d.lm;
-    const int n = 6 * d.Np, N = d.npad, nt = d.nt, T = lm.ntiles;
+    const int n = 6 * d.Np, N = d.npad, nt = d.nt, T = hd.ntiles;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     constexpr int NW = LDLT_THREADS / 64;
 #ifdef MAM_LDLT_PROFILE
@@ -1755,59 +1949,93 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
     double* TL = lds;                           // [T][256]
     double* Y = lds + (size_t)T * 256;          // [N]
     int16_t* slot = sh.map;                     // [nt][nt]
-    if (t == 0) sh.fail = 0;
-    for (int q = t; q < nt * nt; q += LDLT_THREADS) slot[q] = d.tslot[q];
-    for (int q = t; q < 2 * T; q += LDLT_THREADS) sh.tl[q] = d.tlist[q];
-    for (int i = t; i < N; i += LDLT_THREADS) Y[i] = i < n ? d.bs[i] : 0.0;
-    __syncthreads();
-    // the pool: tile s = (r, c) holds S rows 16 r.., columns 16 c..; the padding rows' diagonal is 1 (an identity block
-    // after the unknowns: S's padding rows are zero). One wave per tile, lane = (row, 4 columns): two 16-byte loads per
-    // lane, the wave's tiles' loads issued together
+    // the prologue's global reads — the slot map, the column / row lists and counts k_struct_tiles made, y, and the
+    // tile pool k_schur_blk wrote in slot order and LDS layout (padding identity included) — all issued before the
+    // first LDS store, as global (not flat) loads: one memory round trip instead of one per small copy loop
     {
-        constexpr int U = 10;   // tiles per wave per pass (20 loads of 16 bytes in flight per lane: a 50-KF window's
-                                // ~70 tiles in one pass)
-        const int i = lane >> 2, j0 = 4 * (lane & 3);
-        for (int s0 = wid; s0 < T; s0 += U * NW) {
-            double2 v[U][2];
-            int rr[U], cc[U];
+        typedef __attribute__((address_space(1))) const int16_t gi16;
+        typedef __attribute__((address_space(1))) const uint32_t gu32;
+        typedef __attribute__((address_space(1))) const uint8_t gu8;
+        typedef __attribute__((address_space(1))) const double gd;
+        constexpr int SPT = (LDLT_TM_MAX * LDLT_TM_MAX + LDLT_THREADS - 1) / LDLT_THREADS;
+        constexpr int LPT = (LDLT_TM_MAX * 40 / 4 + LDLT_THREADS - 1) / LDLT_THREADS;
+        constexpr int YPT = (LDLT_TM_MAX * NB + LDLT_THREADS - 1) / LDLT_THREADS;
+        const int nn = nt * nt, nw = nt * 10;
+        int16_t sv[SPT];
+        uint32_t cw[LPT], rw[LPT];
+        uint8_t cv = 0;
+        double yv[YPT];
+        // the pool: LDS-DMA (global_load_lds, 16 bytes per lane: one wave instruction fills 1 KB of the contiguous
+        // image, no VGPRs), 1-KB chunks dealt to the waves
+        {
+            typedef __attribute__((address_space(1))) void gvoid;
+            typedef __attribute__((address_space(3))) void lvoid;
+            for (int c = wid; c < 2 * T; c += NW)
+                __builtin_amdgcn_global_load_lds((gvoid*)(d.pool + (size_t)c * 128 + 2 * lane), (lvoid*)(TL + (size_t)c * 128),
+                                                 16, 0, 0);
+        }
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int s = s0 + u * NW;
-                rr[u] = s < T ? sh.tl[2 * s] : 0;
-                cc[u] = s < T ? sh.tl[2 * s + 1] : 0;
-                const double2* src = reinterpret_cast<const double2*>(d.S + (size_t)(NB * rr[u] + i) * N + NB * cc[u] + j0);
-                if (s < T) {
-                    v[u][0] = src[0];
-                    v[u][1] = src[1];
-                }
-            }
+        for (int u = 0; u < SPT; u++) sv[u] = t + u * LDLT_THREADS < nn ? ((gi16*)d.tslot)[t + u * LDLT_THREADS] : 0;
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int s = s0 + u * NW;
-                if (s >= T) continue;
-                double e[4] = {v[u][0].x, v[u][0].y, v[u][1].x, v[u][1].y};
-                double* D = TL + (size_t)s * 256;
-                const int gi = NB * rr[u] + i;
+        for (int u = 0; u < LPT; u++) {
+            const int q = t + u * LDLT_THREADS;
+            cw[u] = q < nw ? ((gu32*)d.clist_g)[q] : 0u;
+            rw[u] = q < nw ? ((gu32*)d.rlist_g)[q] : 0u;
+        }
+        if (t < 2 * nt) cv = ((gu8*)d.ccnt_g)[t];
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const int gj = NB * cc[u] + j0 + k;
-                    D[tsw(i, j0 + k)] = (gi == gj && gi >= n) ? 1.0 : e[k];
-                }
+        for (int u = 0; u < YPT; u++) {
+            const int i = t + u * LDLT_THREADS;
+            yv[u] = i < n ? ((gd*)d.bs)[i] : 0.0;
+        }
+        if (t == 0) {
+            sh.fail = 0;
+            sh.maxc = hd.maxc;
+        }
+#pragma unroll
+        for (int u = 0; u < SPT; u++)
+            if (t + u * LDLT_THREADS < nn) slot[t + u * LDLT_THREADS] = sv[u];
+#pragma unroll
+        for (int u = 0; u < LPT; u++) {
+            const int q = t + u * LDLT_THREADS;
+            if (q < nw) {
+                reinterpret_cast<uint32_t*>(sh.clist)[q] = cw[u];
+                reinterpret_cast<uint32_t*>(sh.rlist)[q] = rw[u];
             }
         }
-    }
-    if (t >= LDLT_THREADS - 64 && t - (LDLT_THREADS - 64) < nt) {   // the column / row lists of the non-zero tiles
-        const int k = t - (LDLT_THREADS - 64);                       // (the last wave, after its pool loads)
-        int nc = 0, nr = 0;
-        for (int r = k + 1; r < nt; r++)
-            if (slot[r * nt + k] >= 0) sh.clist[k * 40 + nc++] = (int8_t)r;
-        for (int c = 0; c < k; c++)
-            if (slot[k * nt + c] >= 0) sh.rlist[k * 40 + nr++] = (int8_t)c;
-        sh.ccount[k] = (uint8_t)nc;
-        sh.rcount[k] = (uint8_t)nr;
+        if (t < nt) {
+            sh.ccount[t] = cv;
+            sh.cflag[t] = 0;
+            sh.bflag[t] = 0;
+        } else if (t < 2 * nt) {
+            sh.rcount[t - nt] = cv;
+        }
+#pragma unroll
+        for (int u = 0; u < YPT; u++)
+            if (t + u * LDLT_THREADS < N) Y[t + u * LDLT_THREADS] = yv[u];
     }
     __syncthreads();
     LPROF(0);
+#ifndef MAM_LDLT_FLOW
+#define MAM_LDLT_FLOW 1
+#endif
+    if (MAM_LDLT_FLOW && sh.maxc <= 4 && nt <= 40) {   // uniform: every column one tall-panel item
+        for (int kc = wid; kc < nt; kc += NW) flow_factor_column(TL, slot, nt, kc, Y, sh, lane);
+        __syncthreads();
+        LPROF(1);
+        const int fl = sh.fail;
+        if (t == 0) lm.fail = fl;
+        if (fl) return;   // uniform
+        if (wid < nt)   // the wave's columns, descending
+            for (int kc = wid + (nt - 1 - wid) / NW * NW; kc >= 0; kc -= NW) flow_back_column(TL, slot, nt, kc, Y, sh, lane);
+        __syncthreads();
+        for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+        LPROF(4);
+#ifdef MAM_LDLT_PROFILE
+        if (t == 0) atomicAdd(&g_lprof[7], 1ull);
+#endif
+        return;
+    }
     // per block column kc, phase A: the tall-panel items of column kc (waves 0 ..) beside the rest of column kc - 1's
     // trailing update (the tiles (r, c), c >= kc + 1, by the other waves first); barrier; phase B (when L(kc + 1, kc) is
     // non-zero): column kc + 1's tiles updated by L(., kc) — what the next panel reads; barrier. Every tile still sees
@@ -1930,38 +2158,8 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
 #endif
 }
 
-// grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
-// largest pool + y of the batch)
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_tiles(const Prob* __restrict__ probs) {
-    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-    __shared__ LdltShared sh;
-    const Prob& d = probs[blockIdx.x];
-    LM& lm = *d.lm;
-    if (lm.status || lm.done || !lm.tiles_lds) return;
-    if (d.Np == 0) {
-        if (threadIdx.x == 0) lm.fail = 0;
-        return;
-    }
-    ldlt_tiles(d, lds_dyn, sh);
-}
-
-// grid (Q) x LDLT_THREADS: the others, factored in place in HBM (the panel workspace in LDS when use_lds)
-template <bool use_lds>
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
-    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-    __shared__ LdltShared sh;
-    const Prob& d = probs[blockIdx.x];
-    LM& lm = *d.lm;
-    if (lm.status || lm.done || lm.tiles_lds) return;
-    if (d.Np == 0) {
-        if (threadIdx.x == 0) lm.fail = 0;
-        return;
-    }
-    ldlt_global<use_lds>(d, lds_dyn, sh);
-}
-
 // Eigen Quaterniond(Matrix3d)
-__device__ void rot_to_quat(const double m[9], double q[4]) {
+__device__ __forceinline__ void rot_to_quat(const double m[9], double q[4]) {
     const double t = m[0] + m[4] + m[8];
     if (t > 0) {
         double s = sqrt(t + 1.0);
@@ -1973,45 +2171,319 @@ __device__ void rot_to_quat(const double m[9], double q[4]) {
     } else {
         int i = 0;
         if (m[4] > m[0]) i = 1;
-        if (m[8] > m[3 * i + i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        double s = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
-        q[i] = 0.5 * s;
-        s = 0.5 / s;
-        q[3] = (m[3 * k + j] - m[3 * j + k]) * s;
-        q[j] = (m[3 * j + i] + m[3 * i + j]) * s;
-        q[k] = (m[3 * k + i] + m[3 * i + k]) * s;
+        if (m[8] > (i == 1 ? m[4] : m[0])) i = 2;
+        // the three cases with constant indices (no dynamically indexed arrays: they would live in scratch)
+        auto one = [&](auto I) {
+            constexpr int ii = decltype(I)::value, jj = (ii + 1) % 3, kk = (jj + 1) % 3;
+            double s = sqrt(m[3 * ii + ii] - m[3 * jj + jj] - m[3 * kk + kk] + 1.0);
+            q[ii] = 0.5 * s;
+            s = 0.5 / s;
+            q[3] = (m[3 * kk + jj] - m[3 * jj + kk]) * s;
+            q[jj] = (m[3 * jj + ii] + m[3 * ii + jj]) * s;
+            q[kk] = (m[3 * kk + ii] + m[3 * ii + kk]) * s;
+        };
+        if (i == 0) one(std::integral_constant<int, 0>{});
+        else if (i == 1) one(std::integral_constant<int, 1>{});
+        else one(std::integral_constant<int, 2>{});
     }
 }
 
-__device__ void normalize_q(double q[4]) {
+__device__ __forceinline__ void normalize_q(double q[4]) {
     if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
     const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
     q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
 }
 
-// grid (ceil(max(P, L)/256), Q): x_l = D^-1 (b_l - H_pl^T x_p) per point (skipped after a failed factorization:
-// BlockSolver::solve returns before the back-substitution and the update applies the old x), then the trial state:
-// T <- exp(dx) * T (VertexSE3Expmap::oplusImpl) for optimised poses, X <- X + dx, fixed poses copied.
-// one-wave workgroups: a lone window's 3.2k points spread over 50 CUs' load pipes instead of 13
-constexpr int UPD_T = 64;
-__global__ __launch_bounds__(UPD_T) void k_backsub_update(const Prob* __restrict__ probs) {
+// O = exp(u) * T (VertexSE3Expmap::oplusImpl: SE3Quat::exp of the 6-vector, se3quat.h, then the product)
+__device__ __forceinline__ void se3_exp_mul(const double u[6], const double* T, double* O) {
+    const double w0 = u[0], w1 = u[1], w2 = u[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double Om[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double Om2[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++)
+            Om2[3 * r + c] = Om[3 * r] * Om[c] + Om[3 * r + 1] * Om[3 + c] + Om[3 * r + 2] * Om[6 + c];
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int k = 0; k < 9; k++) { R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + Om2[k]; V[k] = R[k]; }
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+        const double c = (theta - sin(theta)) / (theta * theta * theta);
+        for (int k = 0; k < 9; k++) {
+            const double I = (k % 4 == 0) ? 1.0 : 0.0;
+            R[k] = I + a * Om[k] + b * Om2[k];
+            V[k] = I + b * Om[k] + c * Om2[k];
+        }
+    }
+    double qe[4];
+    rot_to_quat(R, qe);
+    double te[3];
+    for (int r = 0; r < 3; r++) te[r] = V[3 * r] * u[3] + V[3 * r + 1] * u[4] + V[3 * r + 2] * u[5];
+    normalize_q(qe);
+    double rt[3];
+    quat_rotate(qe, T + 4, rt);
+    double q[4];
+    q[3] = qe[3] * T[3] - qe[0] * T[0] - qe[1] * T[1] - qe[2] * T[2];
+    q[0] = qe[3] * T[0] + qe[0] * T[3] + qe[1] * T[2] - qe[2] * T[1];
+    q[1] = qe[3] * T[1] + qe[1] * T[3] + qe[2] * T[0] - qe[0] * T[2];
+    q[2] = qe[3] * T[2] + qe[2] * T[3] + qe[0] * T[1] - qe[1] * T[0];
+    normalize_q(q);
+    O[0] = q[0]; O[1] = q[1]; O[2] = q[2]; O[3] = q[3];
+    O[4] = te[0] + rt[0]; O[5] = te[1] + rt[1]; O[6] = te[2] + rt[2];
+}
+
+// ================================================================================== fused per-trial point kernels
+// A trial is k_point_sys -> k_schur_blk -> the factorization (+ its pose epilogue) -> k_point_trial -> k_ctl_end. The
+// point kernels give one wave PW consecutive points and the slots of their edges (pe_idx, edge order within a point):
+// lanes take slots for the per-edge work and lanes < PW take points for the per-point sums, handing over through LDS
+// inside the wave, where the separate kernels of before (linearize, sys, schur_prep / backsub_update, trial
+// linearize) each paid a launch and its dependent global round trips.
+constexpr int PW = 8;   // points per wave (a window's points have <= 8 observations: one 64-slot chunk)
+
+// S's pose part at an iteration start: H_pp, b_p of Hessian pose block h — k_sys's sums (lanes strided over the pose's
+// edge list in edge order, the same products, the same fixed-order wave reduction) on Jacobian terms recomputed from
+// the state by the same linearisation (bit-identical to the records the point waves of the same launch write)
+__device__ __forceinline__ void pose_sys_wave(const Prob& d, int h, const double* pose, const double* pts) {
+    const int lane = threadIdx.x;
+    double acc[27];
+#pragma unroll
+    for (int k = 0; k < 27; k++) acc[k] = 0.0;
+    const int qs0 = d.qe_off[h], qs1 = d.qe_off[h + 1];
+    for (int base = qs0 + lane; base < qs1; base += 64 * SYS_PF) {
+        int qi[SYS_PF];
+#pragma unroll
+        for (int u = 0; u < SYS_PF; u++) qi[u] = base + 64 * u < qs1 ? d.qe_idx[base + 64 * u] : -1;
+#pragma unroll
+        for (int u = 0; u < SYS_PF; u++) {
+            if (qi[u] < 0) break;
+            const int e = qi[u], ipose = d.edge_pose[e];
+            double j[21], hr[18];
+            linearize_edge_at(d, pose + 7 * (size_t)ipose, pts + 3 * (size_t)d.edge_point[e], ipose, e, true, false, j,
+                              hr);
+            double B0[6], B1[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) { B0[k] = j[6 + k]; B1[k] = j[12 + k]; }
+            const double wo = j[20], o0 = j[18], o1 = j[19];
+            int q = 0;
+#pragma unroll
+            for (int a = 0; a < 6; a++)
+#pragma unroll
+                for (int c = a; c < 6; c++) acc[q++] += B0[a] * wo * B0[c] + B1[a] * wo * B1[c];
+#pragma unroll
+            for (int a = 0; a < 6; a++) acc[21 + a] += B0[a] * o0 + B1[a] * o1;
+        }
+    }
+    double tot[7];
+    {
+        double v28[28];
+#pragma unroll
+        for (int k = 0; k < 27; k++) v28[k] = acc[k];
+        v28[27] = 0.0;
+        wave_sum_scatter4<7>(v28, tot);
+    }
+    const int g = lane >> 4, il = lane & 15;
+    double val = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) val = (il == i) ? tot[i] : val;
+    const int q = 7 * g + il;
+    if (il < 7 && q < 27) {
+        if (q < 21) {
+            int a = 0, r = q;
+            while (r >= 6 - a) { r -= 6 - a; a++; }
+            const int c = a + r;
+            double* H = d.Hpp + 36 * (size_t)h;
+            H[6 * a + c] = val;
+            H[6 * c + a] = val;
+        } else {
+            d.b[6 * (size_t)h + (q - 21)] = val;
+        }
+    }
+}
+
+// D = H_ll + lambda I and its inverse as point_dinv computes it, from H in registers
+__device__ __forceinline__ void dinv_of(const double H[9], double lambda, double o[9]) {
+    double m[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) m[k] = H[k] + ((k % 4 == 0) ? lambda : 0.0);
+    const double c00 = m[4] * m[8] - m[5] * m[7], c10 = m[7] * m[2] - m[8] * m[1], c20 = m[1] * m[5] - m[2] * m[4];
+    const double det = c00 * m[0] + (c10 * m[3] + c20 * m[6]);
+    const double inv = 1.0 / det;
+    o[0] = c00 * inv; o[1] = c10 * inv; o[2] = c20 * inv;
+    o[3] = (m[5] * m[6] - m[3] * m[8]) * inv; o[4] = (m[8] * m[0] - m[6] * m[2]) * inv;
+    o[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
+    o[6] = (m[3] * m[7] - m[4] * m[6]) * inv; o[7] = (m[6] * m[1] - m[7] * m[0]) * inv;
+    o[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
+}
+
+// grid (ceil(L / PW) + Np, Q) x 64, the start of every trial:
+//  point waves — at an iteration start (need_lin, unless the setup pass already built iteration 0's system) the slots'
+//    edges linearised (H_pl records, errors) and the points' H_ll, b_l summed in edge order from the slots' terms
+//    (k_sys's sums); every trial D^-1 = (H_ll + lambda I)^-1 per point and, per slot, W = H_pl D^-1 and the
+//    coefficients H_pl D^-1 b_l (k_schur_prep's products);
+//  pose waves — at an iteration start H_pp, b_p (pose_sys_wave).
+__global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
-    const LM& lm = *d.lm;
-    if (lm.status || lm.done) return;
-    const int i = blockIdx.x * UPD_T + threadIdx.x;
-    const double* pose = d.pose[lm.cur];
-    const double* pts = d.pt[lm.cur];
-    double* pose_out = d.pose[1 - lm.cur];
-    double* pt_out = d.pt[1 - lm.cur];
-    if (i < d.L) {
+    const LMHead hd = lm_head(d.lm);
+    if (hd.status || hd.done) return;
+    const bool lin = hd.need_lin && !hd.sys_ready;
+    const int nbp = (d.L + PW - 1) / PW;
+    const double* pose = d.pose[hd.cur];
+    const double* pts = d.pt[hd.cur];
+    if ((int)blockIdx.x >= nbp) {
+        const int h = blockIdx.x - nbp;
+        if (lin && h < d.Np) pose_sys_wave(d, h, pose, pts);
+        return;
+    }
+    const int lane = threadIdx.x;
+    const double lambda = trial_lambda(hd);
+    const int h0 = blockIdx.x * PW, h1 = min(d.L, h0 + PW);
+    const int s0 = d.pe_off[h0], s1 = d.pe_off[h1];
+    const bool one = s1 - s0 <= 64;   // one slot chunk: the slots' H_pl stay in registers for the W products
+    __shared__ double cs[64 * 12];    // per slot: its H_ll (9) and b_l (3) terms
+    __shared__ double pdv[PW * 12];   // per point: D^-1 (9), D^-1 b_l (3)
+    const int hl = h0 + lane;
+    const bool plane = lane < PW && hl < h1;
+    const int ps0 = plane ? d.pe_off[hl] : 0, ps1 = plane ? d.pe_off[hl + 1] : 0;
+    double H[9], bl[3], hr[18];
+#pragma unroll
+    for (int k = 0; k < 9; k++) H[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) bl[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 18; k++) hr[k] = 0.0;
+    if (lin) {
+        for (int c0 = s0; c0 < s1; c0 += 64) {
+            const int s = c0 + lane;
+            if (s < s1) {
+                const int e = d.pe_idx[s];
+                double jr[21];
+                linearize_edge(d, pose, pts, e, true, jr, hr);
+                double* HP = d.hpl + 18 * (size_t)e;
+#pragma unroll
+                for (int k = 0; k < 18; k++) HP[k] = hr[k];
+                const double wo = jr[20];
+                double* c = cs + 12 * lane;
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    c[9 + a] = jr[a] * jr[18] + jr[3 + a] * jr[19];
+#pragma unroll
+                    for (int cc = 0; cc < 3; cc++) c[3 * a + cc] = jr[a] * wo * jr[cc] + jr[3 + a] * wo * jr[3 + cc];
+                }
+            }
+            __syncthreads();
+            if (plane) {
+                const int a0 = max(ps0, c0), a1 = min(ps1, c0 + 64);
+                for (int q = a0; q < a1; q++) {
+                    const double* c = cs + 12 * (q - c0);
+#pragma unroll
+                    for (int k = 0; k < 9; k++) H[k] += c[k];
+#pragma unroll
+                    for (int a = 0; a < 3; a++) bl[a] += c[9 + a];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (plane) {
+        double* Hg = d.Hll + 9 * (size_t)hl;
+        double* bg = d.b + 6 * (size_t)d.Np + 3 * (size_t)hl;
+        if (lin) {
+#pragma unroll
+            for (int k = 0; k < 9; k++) Hg[k] = H[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) bg[k] = bl[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 9; k++) H[k] = Hg[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) bl[k] = bg[k];
+        }
+        double Di[9];
+        dinv_of(H, lambda, Di);
+        double* Dg = d.Dinv + 9 * (size_t)hl;
+        double* pv = pdv + 12 * lane;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            Dg[k] = Di[k];
+            pv[k] = Di[k];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) pv[9 + i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
+    }
+    __syncthreads();
+    for (int c0 = s0; c0 < s1; c0 += 64) {
+        const int s = c0 + lane;
+        if (s >= s1) continue;
+        const int e = d.pe_idx[s];
+        const int4 em = d.emeta[e];
+        double o[18], cf[6];
+#pragma unroll
+        for (int k = 0; k < 18; k++) o[k] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) cf[k] = 0.0;
+        if (em.y >= 0) {
+            double B[18];
+            if (lin && one) {
+#pragma unroll
+                for (int k = 0; k < 18; k++) B[k] = hr[k];
+            } else if (lin) {   // several chunks: the H_pl record again by the same linearisation (not a reload of a
+                double jr[21];  // line another wave of this launch may have cached before it was written)
+                linearize_edge_at(d, pose + 7 * (size_t)d.edge_pose[e], pts + 3 * (size_t)em.x, d.edge_pose[e], e, true,
+                                  false, jr, B);
+            } else {
+                const double* HP = d.hpl + 18 * (size_t)e;
+#pragma unroll
+                for (int k = 0; k < 18; k++) B[k] = HP[k];
+            }
+            const double* Di = pdv + 12 * (em.x - h0);
+            const double* db = Di + 9;
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+#pragma unroll
+                for (int j = 0; j < 3; j++)
+                    o[3 * i + j] = B[3 * i] * Di[j] + B[3 * i + 1] * Di[3 + j] + B[3 * i + 2] * Di[6 + j];
+                cf[i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
+            }
+        }
+        double* W = d.bdinv + 18 * (size_t)e;
+        double* C = d.coef + 6 * (size_t)e;
+#pragma unroll
+        for (int k = 0; k < 18; k++) W[k] = o[k];
+#pragma unroll
+        for (int k = 0; k < 6; k++) C[k] = cf[k];
+    }
+}
+
+// grid (ceil(L / PW), Q) x 64, after the factorization and its pose epilogue (the trial poses): per point (lanes < PW)
+// the back-substitution x_l = D^-1 (b_l - H_pl^T x_p) in edge order (k_backsub_update's; skipped after a failed
+// factorization, which leaves the old x), the trial point X + x_l and its computeScale terms x_l (lambda x_l + b_l);
+// per slot the trial error of its edge at the trial pose and point (k_linearize's trial pass), summed per wave into
+// the chi2 partial of the trial
+__global__ __launch_bounds__(64) void k_point_trial(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    const LMHead hd = lm_head(d.lm);
+    if (hd.status || hd.done) return;
+    const int nbp = (d.L + PW - 1) / PW;
+    if ((int)blockIdx.x >= nbp) return;
+    const int lane = threadIdx.x;
+    const double lambda = trial_lambda(hd);
+    const double* pts = d.pt[hd.cur];
+    double* pt_out = d.pt[1 - hd.cur];
+    const double* pose_out = d.pose[1 - hd.cur];
+    const int h0 = blockIdx.x * PW, h1 = min(d.L, h0 + PW);
+    __shared__ double xn[PW * 3];
+    double sc = 0.0;
+    const int i = h0 + lane;
+    if (lane < PW && i < h1) {
         double* xl = d.x + 6 * (size_t)d.Np + 3 * (size_t)i;
-        if (!lm.fail) {
+        const double* bgl = d.b + 6 * (size_t)d.Np + 3 * (size_t)i;
+        double xv[3];
+        if (!hd.fail) {
             double cl[3];
-            for (int k = 0; k < 3; k++) cl[k] = d.b[6 * (size_t)d.Np + 3 * (size_t)i + k];
+            for (int k = 0; k < 3; k++) cl[k] = bgl[k];
             const int s1 = d.pe_off[i + 1];
             for (int sb = d.pe_off[i]; sb < s1; sb += PT_PF) {
-                int hps[PT_PF], pis[PT_PF];   // the point's slots loaded together, then its records in edge order
+                int hps[PT_PF], pis[PT_PF];
 #pragma unroll
                 for (int u = 0; u < PT_PF; u++) {
                     hps[u] = sb + u < s1 ? d.slot_hp[sb + u] : -2;
@@ -2030,55 +2502,108 @@ __global__ __launch_bounds__(UPD_T) void k_backsub_update(const Prob* __restrict
                 }
             }
             const double* Di = d.Dinv + 9 * (size_t)i;
-            for (int k = 0; k < 3; k++) xl[k] = Di[3 * k] * cl[0] + Di[3 * k + 1] * cl[1] + Di[3 * k + 2] * cl[2];
+            for (int k = 0; k < 3; k++) xv[k] = Di[3 * k] * cl[0] + Di[3 * k + 1] * cl[1] + Di[3 * k + 2] * cl[2];
+            for (int k = 0; k < 3; k++) xl[k] = xv[k];
+        } else {
+            for (int k = 0; k < 3; k++) xv[k] = xl[k];
         }
-        for (int k = 0; k < 3; k++) pt_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + xl[k];
+        for (int k = 0; k < 3; k++) {
+            const double X = pts[3 * (size_t)i + k] + xv[k];
+            pt_out[3 * (size_t)i + k] = X;
+            xn[3 * lane + k] = X;
+            sc += xv[k] * (lambda * xv[k] + bgl[k]);
+        }
     }
-    if (i < d.P) {
-        const double* T = pose + 7 * (size_t)i;
+    __syncthreads();
+    double r = 0.0;
+    const int s0 = d.pe_off[h0], s1 = d.pe_off[h1];
+    for (int c0 = s0; c0 < s1; c0 += 64) {
+        const int s = c0 + lane;
+        if (s < s1) {
+            const int e = d.pe_idx[s];
+            const int ipose = d.edge_pose[e];
+            double jr[21], hr[18];
+            r += linearize_edge_at(d, pose_out + 7 * (size_t)ipose, xn + 3 * (d.edge_point[e] - h0), ipose, e, false, true,
+                                   jr, hr);
+        }
+    }
+    r = wave_sum_d(r);
+    sc = wave_sum_d(sc);
+    if (lane == 0) {
+        d.part[blockIdx.x] = r;
+        d.part_s[blockIdx.x] = sc;
+    }
+}
+
+// The factorization's epilogue: the trial poses (k_backsub_update's pose part: T <- exp(x_p) T for optimised poses,
+// fixed poses copied) and computeScale's pose terms x_p (lambda x_p + b_p) into lm.scale_p (fixed-order block sum),
+// by the whole workgroup; xp: the solution's pose part (LDS after a solve; d.x — the previous trial's — after a failed
+// factorization, as the reference's update applies the old x)
+template <int T>
+__device__ __forceinline__ void pose_epilogue(const Prob& d, LM& lm, int cur, const double* xp, double lambda) {
+    __shared__ double red[T / 64];
+    const int t = threadIdx.x;
+    const double* pose = d.pose[cur];
+    double* pose_out = d.pose[1 - cur];
+    for (int i = t; i < d.P; i += T) {
+        const double* Tp = pose + 7 * (size_t)i;
         double* O = pose_out + 7 * (size_t)i;
         const int h = d.pose_h[i];
         if (h < 0) {
-            for (int k = 0; k < 7; k++) O[k] = T[k];
+            for (int k = 0; k < 7; k++) O[k] = Tp[k];
         } else {
-            const double* u = d.x + 6 * (size_t)h;
-            const double w0 = u[0], w1 = u[1], w2 = u[2];
-            const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
-            const double Om[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
-            double Om2[9];
-            for (int r = 0; r < 3; r++)
-                for (int c = 0; c < 3; c++)
-                    Om2[3 * r + c] = Om[3 * r] * Om[c] + Om[3 * r + 1] * Om[3 + c] + Om[3 * r + 2] * Om[6 + c];
-            double R[9], V[9];
-            if (theta < 0.00001) {
-                for (int k = 0; k < 9; k++) { R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + Om2[k]; V[k] = R[k]; }
-            } else {
-                const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-                const double c = (theta - sin(theta)) / (theta * theta * theta);
-                for (int k = 0; k < 9; k++) {
-                    const double I = (k % 4 == 0) ? 1.0 : 0.0;
-                    R[k] = I + a * Om[k] + b * Om2[k];
-                    V[k] = I + b * Om[k] + c * Om2[k];
-                }
-            }
-            double qe[4];
-            rot_to_quat(R, qe);
-            double te[3];
-            for (int r = 0; r < 3; r++) te[r] = V[3 * r] * u[3] + V[3 * r + 1] * u[4] + V[3 * r + 2] * u[5];
-            normalize_q(qe);
-            // exp * T
-            double rt[3];
-            quat_rotate(qe, T + 4, rt);
-            double q[4];
-            q[3] = qe[3] * T[3] - qe[0] * T[0] - qe[1] * T[1] - qe[2] * T[2];
-            q[0] = qe[3] * T[0] + qe[0] * T[3] + qe[1] * T[2] - qe[2] * T[1];
-            q[1] = qe[3] * T[1] + qe[1] * T[3] + qe[2] * T[0] - qe[0] * T[2];
-            q[2] = qe[3] * T[2] + qe[2] * T[3] + qe[0] * T[1] - qe[1] * T[0];
-            normalize_q(q);
-            O[0] = q[0]; O[1] = q[1]; O[2] = q[2]; O[3] = q[3];
-            O[4] = te[0] + rt[0]; O[5] = te[1] + rt[1]; O[6] = te[2] + rt[2];
+            double u[6];
+            for (int k = 0; k < 6; k++) u[k] = xp[6 * h + k];
+            se3_exp_mul(u, Tp, O);
         }
     }
+    double acc = 0.0;
+    for (int j = t; j < 6 * d.Np; j += T) acc += xp[j] * (lambda * xp[j] + d.b[j]);
+    acc = wave_sum_d(acc);
+    if ((t & 63) == 0) red[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) {
+        double sum = 0.0;
+        for (int w = 0; w < T / 64; w++) sum += red[w];
+        lm.scale_p = sum;
+    }
+}
+
+// grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
+// largest pool + y of the batch), then the pose epilogue
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_tiles(const Prob* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    const LMHead hd = lm_head(d.lm);
+    if (hd.status || hd.done || !hd.tiles_lds) return;
+    LM& lm = *d.lm;
+    if (d.Np == 0) {
+        if (threadIdx.x == 0) lm.fail = 0;
+    } else {
+        ldlt_tiles(d, lds_dyn, sh, hd);
+    }
+    __syncthreads();
+    pose_epilogue<LDLT_THREADS>(d, lm, hd.cur, d.x, trial_lambda(hd));
+}
+
+// grid (Q) x LDLT_THREADS: the others, factored in place in HBM (the panel workspace in LDS when use_lds), then the
+// pose epilogue
+template <bool use_lds>
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    const LMHead hd = lm_head(d.lm);
+    if (hd.status || hd.done || hd.tiles_lds) return;
+    LM& lm = *d.lm;
+    if (d.Np == 0) {
+        if (threadIdx.x == 0) lm.fail = 0;
+    } else {
+        ldlt_global<use_lds>(d, lds_dyn, sh);
+    }
+    __syncthreads();
+    pose_epilogue<LDLT_THREADS>(d, lm, hd.cur, d.x, trial_lambda(hd));
 }
 
 // grid (Q) x 256: end of a trial — levenberg.cpp:108-158 (rho, accept / reject, lambda), then the iteration-end
@@ -2089,27 +2614,33 @@ __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs)
     constexpr int T = RED;
     __shared__ double s[RED];
     const Prob& d = probs[blockIdx.x];
+    const LMHead hd = lm_head(d.lm);
+    if (hd.status || hd.done) return;
     LM& lm = *d.lm;
-    if (lm.status || lm.done) return;
-    // an iteration's first trial: the iteration-start state first (the chi2 of the linearised state on the first
-    // iteration, else the accepted trial's, bit for bit the same kernels on the same state; lambda_0)
-    const bool begin = lm.need_lin != 0;
-    const double lambda = trial_lambda(lm);
-    const double chi0 = (begin && lm.its == 0) ? chi_of_parts<T>(d, d.part0, s) : 0.0;
-    double tempChi = chi_of_parts<T>(d, d.part, s);
-    // computeScale: sum_j x_j (lambda x_j + b_j) over the full x (levenberg.cpp:187-194)
-    double acc[RED / T];
-    const int nbl = max(1, (d.E + EW - 1) / EW);
+    // an iteration's first trial: the iteration-start state first (the chi2 of the linearised state: on the first
+    // iteration the initial chi2 of the same state, else the accepted trial's; lambda_0)
+    const bool begin = hd.need_lin != 0;
+    const double lambda = trial_lambda(hd);
+    // the trial's chi2 and computeScale (levenberg.cpp:187-194: sum_j x_j (lambda x_j + b_j) over the full x) from
+    // k_point_trial's per-wave partials (fixed order: strided over RED virtual threads, then a tree) and the
+    // factorization epilogue's pose part
+    const int nbp = (d.L + PW - 1) / PW;
+    double acc[RED / T], acs[RED / T];
 #pragma unroll
     for (int v = 0; v < RED / T; v++) {
         acc[v] = 0.0;
-        for (int j = threadIdx.x + T * v; j < nbl; j += RED) acc[v] += d.part_s[j];
+        acs[v] = 0.0;
+        for (int j = threadIdx.x + T * v; j < nbp; j += RED) {
+            acc[v] += d.part[j];
+            acs[v] += d.part_s[j];
+        }
     }
-    const double scale0 = block_sum<T>(acc, s);
+    double tempChi = block_sum<T>(acc, s);
+    const double scale0 = block_sum<T>(acs, s) + lm.scale_p;
     if (threadIdx.x != 0) return;
     if (begin) {
-        if (lm.its == 0) {
-            lm.currentChi = chi0;
+        if (hd.its == 0) {
+            lm.currentChi = lm.initialChi;
             lm.ni = 2.0;
             lm.nBad = 0;
         } else {
@@ -2118,9 +2649,8 @@ __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs)
         lm.iniChi = lm.currentChi;
         lm.qmax = 0;
         lm.need_lin = 0;
-        lm.maxdiag = 0ull;   // k_sys gathers the next iteration's max
     }
-    if (lm.fail) tempChi = DBL_MAX;
+    if (hd.fail) tempChi = DBL_MAX;
     double rho = lm.currentChi - tempChi;
     const double scale = scale0 + 1e-3;
     rho /= scale;
@@ -2149,7 +2679,10 @@ __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs)
         if (lm.nBad >= 3) term = true;
     }
     if (term || lm.its >= lm.iterations) lm.done = 1;
-    else lm.need_lin = 1;
+    else {
+        lm.need_lin = 1;
+        lm.sys_ready = 0;   // the next iteration linearises at the accepted state
+    }
 }
 
 // grid (ceil(E/256), Q): isDepthPositive of the final estimate
@@ -2214,9 +2747,10 @@ size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
            al(4 * (size_t)E) + al(16 * (size_t)E) +
            al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) + al(4 * ((size_t)Np * Np + 1)) +
            al((size_t)(npad / 16) * (npad / 16)) + al(2 * (size_t)(npad / 16) * (npad / 16)) +
-           al(2 * (size_t)(npad / 16) * (npad / 16 + 1)) +
+           al(2 * (size_t)(npad / 16) * (npad / 16 + 1)) + 2 * al(40 * (size_t)std::max(npad / 16, 1)) +
+           al(2 * (size_t)std::max(npad / 16, 1)) + al(8 * 256 * (size_t)(npad / 16) * (npad / 16 + 1) / 2) +
            2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
-           2 * al(8 * (size_t)((E + 63) / 64 + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
+           3 * al(8 * (size_t)(std::max((E + 63) / 64, (L + mam::lba::PW - 1) / mam::lba::PW) + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
            al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
            al(8 * (size_t)npad * npad) + al(8 * nx) + al(8 * (size_t)npad) +
            al(8 * mam::lba::ldlt_ws_doubles(npad)) + al((size_t)E);
@@ -2240,15 +2774,20 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.tmask = cv.take<uint8_t>((size_t)d.nt * d.nt);
     d.tslot = cv.take<int16_t>((size_t)d.nt * d.nt);
     d.tlist = cv.take<int16_t>((size_t)d.nt * (d.nt + 1));
+    d.clist_g = cv.take<int8_t>((size_t)std::max(d.nt, 1) * 40);
+    d.rlist_g = cv.take<int8_t>((size_t)std::max(d.nt, 1) * 40);
+    d.ccnt_g = cv.take<uint8_t>(2 * (size_t)std::max(d.nt, 1));
+    d.pool = cv.take<double>((size_t)d.nt * (d.nt + 1) / 2 * 256);
     d.pose[0] = cv.take<double>(7 * (size_t)d.P);
     d.pose[1] = cv.take<double>(7 * (size_t)d.P);
     d.pt[0] = cv.take<double>(3 * (size_t)d.L);
     d.pt[1] = cv.take<double>(3 * (size_t)d.L);
     d.err = cv.take<double>(2 * (size_t)d.E);
     d.jac = cv.take<double>(21 * (size_t)d.E);
-    d.part = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
-    d.part0 = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
-    d.part_s = cv.take<double>((size_t)(d.E + 63) / 64 + 1);
+    const size_t np = (size_t)std::max((d.E + 63) / 64, (d.L + mam::lba::PW - 1) / mam::lba::PW) + 1;
+    d.part = cv.take<double>(np);
+    d.part0 = cv.take<double>(np);
+    d.part_s = cv.take<double>(np);
     d.hpl = cv.take<double>(18 * (size_t)d.E);
     d.bdinv = cv.take<double>(18 * (size_t)d.E);
     d.coef = cv.take<double>(6 * (size_t)d.E);
@@ -2419,14 +2958,17 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
         MAM_HIP(hipMemcpyAsync(c->probs.p, c->lm_host.p, sizeof(Prob) * Q, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_blk_fill, gB, dim3(64), 0, s, P);
-        hipLaunchKernelGGL(k_linearize, gE64, dim3(EW), 0, s, P, 2);
+        // iteration 0's linearisation and system at the initial state (lambda_0 needs its max |diag(H)|), the initial
+        // chi2; the first trial's k_point_sys then starts from this system
+        const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
+        hipLaunchKernelGGL(k_linearize, gE64, dim3(EW), 0, s, P);
+        hipLaunchKernelGGL(k_sys, gSys, dim3(64), 0, s, P);
         hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
     }
-    const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
-    const dim3 gPrep((std::max(maxE, maxL) + EW - 1) / EW > 0 ? (std::max(maxE, maxL) + EW - 1) / EW : 1, Q);
+    const int nbp = std::max((maxL + PW - 1) / PW, 1);
+    const dim3 gPts(nbp + maxNp, Q), gTri(nbp, Q);
     const dim3 gBlk(maxNp * (maxNp + 1) / 2 + maxNp > 0 ? maxNp * (maxNp + 1) / 2 + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
-    const dim3 gUpd((maxPL + UPD_T - 1) / UPD_T > 0 ? (maxPL + UPD_T - 1) / UPD_T : 1, Q);
     // The batch runs as G interleaved groups on G streams: one group's latency-bound factorization (one workgroup
     // per problem) overlaps the other groups' throughput kernels. Every kernel indexes its problems from the Prob
     // pointer it is given, so a group is the sub-array P + first with Q_g problems. MAM_LBA_SPLIT=<G> overrides
@@ -2456,16 +2998,14 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         const int q0 = g * Q / G, q1 = (g + 1) * Q / G, Qg = q1 - q0;
         const Prob* Pg = P + q0;
         hipStream_t st = sg[g];
-        const dim3 gE64g(gE64.x, Qg), gSysg(gSys.x, Qg), gPrepg(gPrep.x, Qg), gBlkg(gBlk.x, Qg), gUpdg(gUpd.x, Qg);
+        const dim3 gPtsg(gPts.x, Qg), gTrig(gTri.x, Qg), gBlkg(gBlk.x, Qg);
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
-            hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 0);
-            hipLaunchKernelGGL(k_sys, gSysg, dim3(64), 0, st, Pg);
+            hipLaunchKernelGGL(k_point_sys, gPtsg, dim3(64), 0, st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 1);
-            hipLaunchKernelGGL(k_schur_prep, gPrepg, dim3(64), 0, st, Pg);
             hipLaunchKernelGGL(k_schur_blk, gBlkg, dim3(64), 0, st, Pg);
         }
         {
@@ -2480,8 +3020,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
-            hipLaunchKernelGGL(k_backsub_update, gUpdg, dim3(UPD_T), 0, st, Pg);
-            hipLaunchKernelGGL(k_linearize, gE64g, dim3(EW), 0, st, Pg, 1);
+            hipLaunchKernelGGL(k_point_trial, gTrig, dim3(64), 0, st, Pg);
             hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
     };
@@ -2539,8 +3078,8 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         unsigned long long h[8];
         MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::lba::g_lprof), sizeof(h)));
         const double w = (double)std::max(1ull, h[7]);
-        fprintf(stderr, "ldlt cycles per WG: init %.0f B %.0f C1 %.0f C2 %.0f solve %.0f diag(w0) %.0f; WGs %llu\n",
-                h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7]);
+        fprintf(stderr, "ldlt cycles per WG: init %.0f B %.0f C1 %.0f C2 %.0f solve %.0f diag(w0) %.0f pull %.0f; WGs %llu\n",
+                h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[6] / w, h[7]);
     }
 #endif
     return MAM_OK;
