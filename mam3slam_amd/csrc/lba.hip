@@ -1351,6 +1351,23 @@ struct TileQueue {
 };
 
 
+#ifdef MAM_LDLT_TRACE
+// per-column timestamps of window 0 of the last k_ldlt_tiles launch (dataflow form): [kc][0..5] = after the critical
+// flag wait, after the pulled updates, after the panel loads, after the pivot steps, after the flag set, backward
+// step done
+__device__ long long g_ltrace[40][6];
+#define LTRACE(k, dep)                                                                          \
+    do {                                                                                        \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(dep) : "memory");                   \
+        const long long tn_ = clock64();                                                        \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_ltrace[kc][k] = tn_;                   \
+    } while (0)
+#else
+#define LTRACE(k, dep) \
+    do {               \
+    } while (0)
+#endif
+
 #ifdef MAM_LDLT_PROFILE
 // cycles per phase summed over workgroups (thread 0 after each barrier): init, B, C1, C2, solve, diag (wave 0), -, WGs
 __device__ unsigned long long g_lprof[8];
@@ -1647,17 +1664,19 @@ __device__ __forceinline__ void tile_update_multi(double* TL, const int* sc, con
             yv[k] = yj[k];
         }
     }
+    // the negation on the shared B operand: (-a) b and a (-b) are the same product, bit for bit, and the A operands
+    // load straight into registers (no per-tile wait for a negation); an absent tile (sa < 0, uniform) loads a valid
+    // tile, so every load issues unconditionally and one wait covers them all
 #pragma unroll
-    for (int q = 0; q < 4; q++) bv[q] = Lb[tsw(col, 4 * q + rq)] * dkp[4 * q + rq];
+    for (int q = 0; q < 4; q++) bv[q] = -(Lb[tsw(col, 4 * q + rq)] * dkp[4 * q + rq]);
 #pragma unroll
     for (int u = 0; u < N; u++) {
-        if (sa[u] < 0) continue;   // uniform: no tile u
-        const double* C = TL + (size_t)sc[u] * 256;
-        const double* La = TL + (size_t)sa[u] * 256;
+        const double* C = TL + (size_t)(sa[u] >= 0 ? sc[u] : sb) * 256;
+        const double* La = TL + (size_t)(sa[u] >= 0 ? sa[u] : sb) * 256;
 #pragma unroll
         for (int r = 0; r < 4; r++) acc[u][r] = C[tsw(rq + 4 * r, col)];
 #pragma unroll
-        for (int q = 0; q < 4; q++) av[u][q] = -La[tsw(col, 4 * q + rq)];
+        for (int q = 0; q < 4; q++) av[u][q] = La[tsw(col, 4 * q + rq)];
     }
 #pragma unroll
     for (int q = 0; q < 4; q++)
@@ -1847,9 +1866,11 @@ __device__ __forceinline__ void flow_factor_column(double* TL, const int16_t* sl
 #ifdef MAM_LDLT_PROFILE
         tp0 = clock64();   // after the last wait: the column's critical pull
 #endif
+        LTRACE(0, j);
         // y_kc -= L(kc, j) y_j (the panel-row forward update column j's tall panel did in the right-looking form)
         // rides on the batched tile update
         tile_update_multi<5>(TL, sc, sa, sb, dkj, lane, yj, &yd);
+        LTRACE(1, yd);
     }
     // the tall panel: the diagonal tile and the (<= 4) panel tiles, lane (g, il)
     const int r = g == 0 ? rows[0] : g == 1 ? rows[1] : g == 2 ? rows[2] : rows[3];
@@ -1863,19 +1884,22 @@ __device__ __forceinline__ void flow_factor_column(double* TL, const int16_t* sl
         pr[c] = r >= 0 ? Tp[tsw(il, c)] : 0.0;
     }
     double yp = 0.0, dmine = 1.0;
+    LTRACE(2, dr[15]);
 #ifdef MAM_LDLT_PROFILE
     long long tp1 = clock64();
     if (lane == 0) atomicAdd(&g_lprof[6], (unsigned long long)(tp1 - tp0));   // the critical pull + the panel loads
 #endif
     Tall16<0>::run(dr, pr, yd, yp, dmine, il);
+    LTRACE(3, dmine);
 #ifdef MAM_LDLT_PROFILE
     long long tp2 = clock64();
     if (lane == 0) atomicAdd(&g_lprof[5], (unsigned long long)(tp2 - tp1));   // the tall panel's pivot steps
 #endif
+    // the whole row, unpredicated: c < il holds L, c == il the pivot (dr[il] is never updated at its own step), the
+    // entries above the diagonal are overwritten by the L^-T pass below before anything reads them
     if (g == 0) {
 #pragma unroll
-        for (int c = 0; c < NB; c++)
-            if (c <= il) Td[tsw(il, c)] = c < il ? dr[c] : dmine;
+        for (int c = 0; c < NB; c++) Td[tsw(il, c)] = dr[c];
         sh.dkall[kc][il] = dmine;
         Y[kb + il] = yd;
         if (dmine == 0.0) sh.fail = 1;
@@ -1885,6 +1909,7 @@ __device__ __forceinline__ void flow_factor_column(double* TL, const int16_t* sl
         for (int c = 0; c < NB; c++) Tp[tsw(il, c)] = pr[c];
     }
     lds_flag_set(&sh.cflag[kc]);
+    LTRACE(4, kc);
 #ifdef MAM_LDLT_PROFILE
     if (lane == 0) atomicAdd(&g_lprof[2], (unsigned long long)(clock64() - tp2));   // stores + flag
 #endif
@@ -1936,6 +1961,7 @@ __device__ __forceinline__ void flow_back_column(const double* TL, const int16_t
     w += w1;
     if (lane < NB) Y[kb + lane] = w;
     lds_flag_set(&sh.bflag[kc]);
+    LTRACE(5, w);
 }
 
 __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShared& sh, const LMHead& hd) {
@@ -3073,6 +3099,17 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         max_trials = std::max(max_trials, lh[q].trials);
     }
     if (!was_stopped) c->trials_ema = 0.75 * c->trials_ema + 0.25 * std::max(1, max_trials);
+#ifdef MAM_LDLT_TRACE
+    {
+        long long tr[40][6];
+        MAM_HIP(hipMemcpyFromSymbol(tr, HIP_SYMBOL(mam::lba::g_ltrace), sizeof(tr)));
+        const int nt0 = hp[0].nt;
+        const long long t0 = tr[0][2];
+        for (int k = 0; k < nt0 && k < 40; k++)
+            fprintf(stderr, "ltrace col %2d: wait %7lld pull %7lld load %7lld panel %7lld flag %7lld back %7lld\n", k,
+                    tr[k][0] - t0, tr[k][1] - t0, tr[k][2] - t0, tr[k][3] - t0, tr[k][4] - t0, tr[k][5] - t0);
+    }
+#endif
 #ifdef MAM_LDLT_PROFILE
     {
         unsigned long long h[8];
