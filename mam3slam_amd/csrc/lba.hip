@@ -1413,6 +1413,7 @@ struct LdltShared {
     double dkall[40][NB];
     int cflag[40];
     int bflag[40];
+    int tcnt[40];                // dataflow tasks: the column's tile tasks done
     int maxc;
 };
 
@@ -1813,12 +1814,8 @@ __device__ __forceinline__ void tall_panel(double* TL, const int16_t* slot, int 
 }
 
 // ---- dataflow form for banded tile patterns (every column has at most 4 non-zero tiles below its diagonal tile, so one
-// tall-panel item per column): no workgroup barriers inside the factorization. Block column kc belongs to wave
-// kc % NW; the owner pulls every update its tiles receive — for each column j < kc with tile (kc, j) non-zero, in
-// ascending j: T(r, kc) -= L(r, j) D_j L(kc, j)^T for its non-zero rows r, and y_kc -= L(kc, j) y_j — waiting for
-// column j's LDS flag only when it gets there, so the updates from older columns run while the column before is still
-// being factored; then its tall panel (without the push of the panel rows' y: they pull theirs), the diagonal tile's
-// L^-T for the backward solve, and its flag. The backward solve runs the same way in reverse (column kc pulls
+// tall-panel item per column): no workgroup barriers inside the factorization, the waves synchronise through LDS flags
+// (the tasks: see flow_tile_task). The backward solve runs as one owner wave per column in reverse (column kc pulls
 // L(r, kc)^T x_r from its rows r once their flags are set). Every tile and every y entry sees the same updates in the
 // same order with the same arithmetic as in the right-looking schedule of ldlt_tiles.
 __device__ __forceinline__ int lds_flag_load(const int* f) {
@@ -1831,12 +1828,47 @@ __device__ __forceinline__ void lds_flag_set(int* f) {
     __hip_atomic_store(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// column kc of the dataflow factorization (its owner wave)
-__device__ __forceinline__ void flow_factor_column(double* TL, const int16_t* slot, int nt, int kc, double* Y,
-                                                   LdltShared& sh, int lane) {
+// The dataflow factorization as tasks: per block column kc, tile task t = 0 .. ncl pulls every update one tile of the
+// column receives (t = 0 the diagonal tile, which also pulls y_kc; t = 1 + a the panel tile of row clist[kc][a]) — for
+// each column j < kc with L(r, j) non-zero, in ascending j, T(r, kc) -= L(r, j) D_j L(kc, j)^T, waiting for column j's
+// flag when it gets there — and counts itself done in tcnt[kc]; the panel task (t = FLOW_TPC - 1) waits for the count,
+// factors the tall panel and sets the column's flag. Task (kc, t) runs on wave (FLOW_TPC kc + t) % NW: a column's
+// tasks are on distinct waves, so once column kc - 1's flag is set the <= 5 tiles of column kc take their last update
+// in parallel (4 f64 MFMAs each, 64 cycles apiece) instead of one wave's 16 in turn, and the next column's tile tasks
+// are never on the wave factoring this column's panel. Every wave walks the columns in ascending order with at most
+// one task per column (dependencies only on earlier columns, or on the same column's tile tasks: no wait cycle).
+constexpr int FLOW_TPC = 6;
+
+__device__ __forceinline__ void flow_tile_task(double* TL, const int16_t* slot, int nt, int kc, int t, double* Y,
+                                               LdltShared& sh, int lane) {
+    const int il = lane & 15, kb = NB * kc;
+    const int nrl = __builtin_amdgcn_readfirstlane(sh.rcount[kc]);
+    const int r = t == 0 ? kc : __builtin_amdgcn_readfirstlane(sh.clist[kc * 40 + t - 1]);
+    const int sc = __builtin_amdgcn_readfirstlane(slot[r * nt + kc]);
+    double yd = t == 0 ? Y[kb + il] : 0.0;
+    for (int q = 0; q < nrl; q++) {
+        const int j = __builtin_amdgcn_readfirstlane(sh.rlist[kc * 40 + q]);
+        const int sb = __builtin_amdgcn_readfirstlane(slot[kc * nt + j]);
+        const int sa = t == 0 ? sb : __builtin_amdgcn_readfirstlane(slot[r * nt + j]);
+        if (sa < 0) continue;   // uniform: L(r, j) is zero
+        lds_flag_wait(&sh.cflag[j]);
+        // y_kc -= L(kc, j) y_j rides on the diagonal tile's update
+        if (t == 0)
+            tile_update_multi<1>(TL, &sc, &sa, sb, sh.dkall[j], lane, Y + NB * j, &yd);
+        else
+            tile_update_multi<1>(TL, &sc, &sa, sb, sh.dkall[j], lane);
+    }
+    if (t == 0) {
+        if (lane < NB) Y[kb + lane] = yd;
+        LTRACE(0, yd);
+    }
+    if (lane == 0) __hip_atomic_fetch_add(&sh.tcnt[kc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot, int nt, int kc, double* Y,
+                                                LdltShared& sh, int lane) {
     const int g = lane >> 4, il = lane & 15, kb = NB * kc;
-    // the column's structure (LDS, the same in every lane) as scalars: uniform loops and branches
-    const int ncl = __builtin_amdgcn_readfirstlane(sh.ccount[kc]), nrl = __builtin_amdgcn_readfirstlane(sh.rcount[kc]);
+    const int ncl = __builtin_amdgcn_readfirstlane(sh.ccount[kc]);
     const int sd = __builtin_amdgcn_readfirstlane(slot[kc * nt + kc]);
     int rows[4], rsl[4];
 #pragma unroll
@@ -1844,34 +1876,12 @@ __device__ __forceinline__ void flow_factor_column(double* TL, const int16_t* sl
         rows[a] = a < ncl ? __builtin_amdgcn_readfirstlane(sh.clist[kc * 40 + a]) : -1;
         rsl[a] = a < ncl ? __builtin_amdgcn_readfirstlane(slot[rows[a] * nt + kc]) : -1;
     }
+    while (__hip_atomic_load(&sh.tcnt[kc], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= ncl)
+        __builtin_amdgcn_s_sleep(1);
 #ifdef MAM_LDLT_PROFILE
     long long tp0 = clock64();
 #endif
-    double yd = Y[kb + il];
-    for (int q = 0; q < nrl; q++) {
-        const int j = __builtin_amdgcn_readfirstlane(sh.rlist[kc * 40 + q]);
-        const int sb = __builtin_amdgcn_readfirstlane(slot[kc * nt + j]);
-        // the diagonal tile and the panel tiles (r, kc) whose L(r, j) is non-zero (sa < 0: none), in row order
-        int sc[5], sa[5];
-        sc[0] = sd;
-        sa[0] = sb;
-#pragma unroll
-        for (int a = 0; a < 4; a++) {
-            sc[1 + a] = rsl[a];
-            sa[1 + a] = a < ncl ? __builtin_amdgcn_readfirstlane(slot[rows[a] * nt + j]) : -1;
-        }
-        const double* dkj = sh.dkall[j];
-        const double* yj = Y + NB * j;
-        lds_flag_wait(&sh.cflag[j]);
-#ifdef MAM_LDLT_PROFILE
-        tp0 = clock64();   // after the last wait: the column's critical pull
-#endif
-        LTRACE(0, j);
-        // y_kc -= L(kc, j) y_j (the panel-row forward update column j's tall panel did in the right-looking form)
-        // rides on the batched tile update
-        tile_update_multi<5>(TL, sc, sa, sb, dkj, lane, yj, &yd);
-        LTRACE(1, yd);
-    }
+    LTRACE(1, kc);
     // the tall panel: the diagonal tile and the (<= 4) panel tiles, lane (g, il)
     const int r = g == 0 ? rows[0] : g == 1 ? rows[1] : g == 2 ? rows[2] : rows[3];
     const int rs = g == 0 ? rsl[0] : g == 1 ? rsl[1] : g == 2 ? rsl[2] : rsl[3];
@@ -1883,11 +1893,11 @@ __device__ __forceinline__ void flow_factor_column(double* TL, const int16_t* sl
         dr[c] = Td[tsw(il, c)];
         pr[c] = r >= 0 ? Tp[tsw(il, c)] : 0.0;
     }
-    double yp = 0.0, dmine = 1.0;
+    double yd = Y[kb + il], yp = 0.0, dmine = 1.0;
     LTRACE(2, dr[15]);
 #ifdef MAM_LDLT_PROFILE
     long long tp1 = clock64();
-    if (lane == 0) atomicAdd(&g_lprof[6], (unsigned long long)(tp1 - tp0));   // the critical pull + the panel loads
+    if (lane == 0) atomicAdd(&g_lprof[6], (unsigned long long)(tp1 - tp0));   // the panel loads
 #endif
     Tall16<0>::run(dr, pr, yd, yp, dmine, il);
     LTRACE(3, dmine);
@@ -2033,6 +2043,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             sh.ccount[t] = cv;
             sh.cflag[t] = 0;
             sh.bflag[t] = 0;
+            sh.tcnt[t] = 0;
         } else if (t < 2 * nt) {
             sh.rcount[t - nt] = cv;
         }
@@ -2046,7 +2057,14 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
 #define MAM_LDLT_FLOW 1
 #endif
     if (MAM_LDLT_FLOW && sh.maxc <= 4 && nt <= 40) {   // uniform: every column one tall-panel item
-        for (int kc = wid; kc < nt; kc += NW) flow_factor_column(TL, slot, nt, kc, Y, sh, lane);
+        static_assert(NW >= FLOW_TPC, "a column's tasks need distinct waves");
+        for (int kc = 0; kc < nt; kc++) {
+            const int tk = (wid - FLOW_TPC * kc % NW + NW) % NW;   // this wave's task in column kc
+            if (tk == FLOW_TPC - 1)
+                flow_panel_task(TL, slot, nt, kc, Y, sh, lane);
+            else if (tk <= __builtin_amdgcn_readfirstlane(sh.ccount[kc]))
+                flow_tile_task(TL, slot, nt, kc, tk, Y, sh, lane);
+        }
         __syncthreads();
         LPROF(1);
         const int fl = sh.fail;
