@@ -48,7 +48,11 @@ CONFIGS = {
     "c2": dict(width=1280, height=720, nfeatures=2000, lba=True),
     # BASELINE.json configs[3]: the testMultiAgentSystem agents (test/settingsForTest_00.yaml: KannalaBrandt8, 700
     # features) at 640x480, two agents in total (both on one GPU at --gpus 1, one per GPU at --gpus 2)
-    "c3": dict(width=640, height=480, nfeatures=700, lba=True, camera="kb8", agents=2),
+    # pool_frames: the two streams' keyframes over 16 steps are 32 distinct views (synth.frame_pose at the fisheye's
+    # focal length: 0.53 deg of parallax per frame), so CreateNewMapPoints' neighbours beyond the nearest two pass
+    # KannalaBrandt8's parallax test (cos < 0.9998, ~1.15 deg: KannalaBrandt8.cpp:316)
+    "c3": dict(width=640, height=480, nfeatures=700, lba=True, camera="kb8", agents=2, pool_frames=32, frame_stride=1,
+               coherent_map=True),
     # BASELINE.json configs[4]: 8 synthetic mono agents at 1280x720 / 2000 features, shared-map local BA, one agent
     # per GPU at --gpus 8 (all 8 on one GPU at --gpus 1); neighbouring agents' LBA windows overlap (keyframes and
     # MapPoints of the merged map), so the exchange resolves cross-GPU write conflicts in GPU order
@@ -186,13 +190,24 @@ class TrackingLeg:
         self.cap = cap
         cam = scene.kannala_brandt8(W, H) if cfg.get("camera") == "kb8" else scene.pinhole(W, H)
         self.cam = cam
+        # a pool of P = ceil(pool_frames / B) frame sets: step s tracks set s mod P, so the keyframes a stream inserts over P
+        # steps are different views (CreateNewMapPoints' neighbours then have parallax); set p, stream i renders frame
+        # (p B + i) x frame_stride of the agent's sequence. P = 1: the same B frames every step.
+        P, fs = max(1, -(-int(cfg.get("pool_frames", 1)) // B)), max(1, int(cfg.get("frame_stride", 1)))
+        self.P, self.p = P, 0
+        nfr = P * B
+        fidx = [g * fs for g in range(nfr)]
         # frames rendered through the camera they are tracked with (the KannalaBrandt8 agents see the scene through the
         # fisheye: synth.make_frame_camera; the Pinhole frames are make_frame's crops, the same images)
+        # (the fisheye's views at the canvas scale of its own focal length: the texture as dense in its image centre as
+        # in a Pinhole frame of make_frame, not minified ~2.3x into a mass of FAST corners)
+        fscene = float(cam.fx) if cam.is_kb8 else 500.0
         if cam.is_kb8:
-            self.frames = np.stack([synth.make_frame_camera(W, H, cam, agent=rank, frame=i) for i in range(B)])
+            frames = np.stack([synth.make_frame_camera(W, H, cam, agent=rank, frame=k, f=fscene) for k in fidx])
         else:
-            self.frames = np.stack([synth.make_frame(W, H, agent=rank, frame=i) for i in range(B)])
-        self.d_img = torch.from_numpy(self.frames).to(dev)
+            frames = np.stack([synth.make_frame(W, H, agent=rank, frame=k) for k in fidx])
+        self.d_img_pool = torch.from_numpy(frames).to(dev)
+        self.d_img = self.d_img_pool[:B].clone() if P > 1 else self.d_img_pool
         self.d_kps = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)
         self.d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
         self.d_cnt = torch.zeros((B, 2), dtype=torch.int32, device=dev)
@@ -202,53 +217,79 @@ class TrackingLeg:
         for l in range(lanes):
             self.lanes.append({"lo": l * BL, "ext": self.ext if l == 0 else ORBextractor(NF, 1.2, 8, 20, 7, device=di),
                                "stream": self.tstream if l == 0 else torch.cuda.Stream(dev)})
-        with torch.cuda.stream(self.tstream):
-            self._fork()
-            self._extract()
-            self._join()
-        torch.cuda.synchronize(dev)
-        kps_h = self.d_kps.cpu().numpy().view(KP_DTYPE).reshape(B, cap)
-        desc_h = self.d_desc.cpu().numpy()
-        cnt_h = self.d_cnt.cpu().numpy()
-        self.kps_h, self.cnt_h = kps_h, cnt_h
+        # every set's keypoints (the scene's MapPoints are placed on them)
+        kps_l, desc_l, cnt_l = [], [], []
+        for p in range(P):
+            with torch.cuda.stream(self.tstream):
+                if P > 1:
+                    self.d_img.copy_(self.d_img_pool[p * B:(p + 1) * B])
+                self._fork()
+                self._extract()
+                self._join()
+            torch.cuda.synchronize(dev)
+            kps_l.append(self.d_kps.clone())
+            desc_l.append(self.d_desc.clone())
+            cnt_l.append(self.d_cnt.clone())
+        self.d_kps_pool, self.d_desc_pool, self.d_cnt_pool = torch.cat(kps_l), torch.cat(desc_l), torch.cat(cnt_l)
+        if P > 1:
+            self.d_img.copy_(self.d_img_pool[:B])
+        kps_h = self.d_kps_pool.cpu().numpy().view(KP_DTYPE).reshape(nfr, cap)
+        desc_h = self.d_desc_pool.cpu().numpy()
+        cnt_h = self.d_cnt_pool.cpu().numpy()
         lasts, mpls, poses, poses_init = [], [], [], []
         F0 = None
-        for f in range(B):
+        for f in range(nfr):
             rng = np.random.default_rng(1000 * rank + f)
             F = scene.make_frame_data(kps_h[f, :cnt_h[f, 0]], desc_h[f, :cnt_h[f, 0]], W, H)
             # the pose of the camera that rendered the frame (synth.frame_pose: the canvas as a plane in front of a
             # translating, rolling camera), so keyframes' poses and image content agree (SearchForTriangulation's
             # epipolar tests between keyframes pass for real correspondences, KannalaBrandt8 included)
-            F.pose = synth.frame_pose(W, H, f)
+            F.pose = synth.frame_pose(W, H, fidx[f], f=fscene)
             F0 = F0 or F
             # the last frame's and the local map's MapPoints re-project onto the frame's keypoints under that pose:
             # 45 % of the keypoints each (together ~70 % of the frame tracked, as ORB-SLAM's monocular tracking keeps
             # a few hundred map points per 1000 features; the rest is what CreateNewMapPoints triangulates)
-            lasts.append(scene.motion_last_frame(F, cam, rng, frac=0.45))
-            mpls.append(scene.local_world_mappoints(F, cam, rng, frac=0.45))
+            # (coherent_map: the MapPoints on the scene regions the map covers, the same in every view)
+            cm = cfg.get("coherent_map", False)
+            lasts.append(scene.motion_last_frame(F, cam, rng, frac=0.45,
+                                                 sel=scene.coherent_selection(F, cam, 0.45, 1) if cm else None))
+            mpls.append(scene.local_world_mappoints(F, cam, rng, frac=0.45,
+                                                    sel=scene.coherent_selection(F, cam, 0.45, 2) if cm else None))
             poses.append(F.pose)
             # the motion model's guess mVelocity * LastFrame.GetPose() (Tracking.cc:2796): the true pose, 0.3 deg /
             # 2 cm off
             poses_init.append(scene.perturb_pose(F.pose, rng, rot=0.005, trans=0.02))
-        self.F0, self.lasts, self.mpls, self.poses, self.poses_init = F0, lasts, mpls, poses, poses_init
+        self.F0 = F0
+        # host copies of every set; frames / kps_h / cnt_h / desc_h / lasts / mpls / poses / poses_init: the set the
+        # device buffers hold (the last step's)
+        self.pool = dict(frames=frames, kps_h=kps_h, cnt_h=cnt_h, desc_h=desc_h, lasts=lasts, mpls=mpls, poses=poses,
+                         poses_init=poses_init)
+        self._set_views()
         Ls, Ms = max(len(x) for x in lasts), max(len(x) for x in mpls)
         self.Ls, self.Ms = Ls, Ms
-        last = np.zeros((B, Ls), LAST_ENTRY_DTYPE)
-        mpw = np.zeros((B, Ms), LOCAL_MP_DTYPE)
-        tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
-        for f in range(B):
+        last = np.zeros((nfr, Ls), LAST_ENTRY_DTYPE)
+        mpw = np.zeros((nfr, Ms), LOCAL_MP_DTYPE)
+        tcw = np.zeros(nfr, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
+        for f in range(nfr):
             last[f, :len(lasts[f])] = lasts[f]
             mpw[f, :len(mpls[f])] = mpls[f]
             tcw[f]["q"], tcw[f]["t"] = poses_init[f]
         self.tcw_bytes = tcw.dtype.itemsize
-        self.d_last = torch.from_numpy(last.view(np.uint8).reshape(B, -1).copy()).to(dev)
-        self.d_mpw = torch.from_numpy(mpw.view(np.uint8).reshape(B, -1).copy()).to(dev)
+        self.d_last_pool = torch.from_numpy(last.view(np.uint8).reshape(nfr, -1).copy()).to(dev)
+        self.d_mpw_pool = torch.from_numpy(mpw.view(np.uint8).reshape(nfr, -1).copy()).to(dev)
+        self.d_tcw_init_pool = torch.from_numpy(tcw.view(np.uint8).reshape(nfr, -1).copy()).to(dev)
+        self.d_nlast_pool = torch.tensor([len(x) for x in lasts], dtype=torch.int32, device=dev)
+        self.d_nmps_pool = torch.tensor([len(x) for x in mpls], dtype=torch.int32, device=dev)
+
+        def work(t):   # the step's buffer: set 0's slice (advance copies the next set in), the pool itself when P = 1
+            return t[:B].clone() if P > 1 else t
+
+        self.d_last, self.d_mpw = work(self.d_last_pool), work(self.d_mpw_pool)
         self.d_mps = torch.zeros((B, Ms * MP_TRACK_DTYPE.itemsize), dtype=torch.uint8, device=dev)
         # the motion model's guess (input of the step, never written) and the frame's pose as Tracking refines it
-        self.d_tcw_init = torch.from_numpy(tcw.view(np.uint8).copy()).to(dev)
+        self.d_tcw_init = work(self.d_tcw_init_pool).view(-1)
         self.d_tcw = self.d_tcw_init.clone()
-        self.d_nlast = torch.tensor([len(x) for x in lasts], dtype=torch.int32, device=dev)
-        self.d_nmps = torch.tensor([len(x) for x in mpls], dtype=torch.int32, device=dev)
+        self.d_nlast, self.d_nmps = work(self.d_nlast_pool), work(self.d_nmps_pool)
         self.d_ntm = torch.zeros(B, dtype=torch.int32, device=dev)
         self.d_out1 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
         self.d_out2 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
@@ -278,6 +319,30 @@ class TrackingLeg:
             if ln["po"].max_edges() < cap:
                 raise RuntimeError(f"PoseOptimization holds {ln['po'].max_edges()} edges per frame, frames have {cap}")
         self.graph = None
+
+    def _set_views(self):
+        B, p = self.B, self.p
+        for k, v in self.pool.items():
+            setattr(self, k, v[p * B:(p + 1) * B])
+
+    def advance(self):
+        """Move to the next frame set (P > 1): its images, last-frame and local-map MapPoints, motion-model guesses
+        copied into the step's buffers on the tracking stream — the new frames of the step arriving."""
+        import torch
+
+        if self.P == 1:
+            return
+        self.p = (self.p + 1) % self.P
+        with torch.cuda.stream(self.tstream):
+            self._copy_set(self.p)
+        self._set_views()
+
+    def _copy_set(self, p):
+        sl = slice(p * self.B, (p + 1) * self.B)
+        for w, src in ((self.d_img, self.d_img_pool), (self.d_last, self.d_last_pool), (self.d_mpw, self.d_mpw_pool),
+                       (self.d_tcw_init.view(self.B, -1), self.d_tcw_init_pool), (self.d_nlast, self.d_nlast_pool),
+                       (self.d_nmps, self.d_nmps_pool)):
+            w.copy_(src[sl])
 
     def _fork(self):
         for ln in self.lanes[1:]:
@@ -354,13 +419,30 @@ class TrackingLeg:
     def capture(self):
         import torch
 
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=self.tstream):
-            self.launch()
+        if self.P == 1:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=self.tstream):
+                self.launch()
+            return
+        # one graph per frame set: its frames' copy-in + the step
+        self.graphs = []
+        for p in range(self.P):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.tstream, pool=self.graphs[0].pool() if self.graphs else None):
+                self._copy_set(p)
+                self.launch()
+            self.graphs.append(g)
+        self.graph = self.graphs
 
     def step(self):
         import torch
 
+        if self.graph is not None and self.P > 1:
+            self.p = (self.p + 1) % self.P
+            self._set_views()
+            self.graphs[self.p].replay()
+            return
+        self.advance()
         if self.graph is not None:
             self.graph.replay()
         else:

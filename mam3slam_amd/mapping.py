@@ -255,11 +255,11 @@ class NewMapPointsLeg:
         self._FramesDev, self._TriBatch = FramesDev, TriBatch
         # initial ring: the first R frames, BoW on the device, no MapPoints yet
         with torch.cuda.stream(tr.tstream):
-            fr = torch.arange(R, device=device) % tr.B
-            self.keys.copy_(tr.d_kps[fr])
-            self.desc.copy_(tr.d_desc[fr])
-            self.cnt.copy_(tr.d_cnt[fr])
-            self.tcw.copy_(tr.d_tcw.view(tr.B, -1)[fr])
+            fr = torch.arange(R, device=device) % (tr.P * tr.B)   # the pool's frames in order, at their guessed poses
+            self.keys.copy_(tr.d_kps_pool[fr])
+            self.desc.copy_(tr.d_desc_pool[fr])
+            self.cnt.copy_(tr.d_cnt_pool[fr])
+            self.tcw.copy_(tr.d_tcw_init_pool.view(tr.P * tr.B, -1)[fr])
             self.fmp.copy_(self.fmp_frames[fr])
             self.voc.transform_batch_device(R, self.desc.data_ptr(), S, self.cnt.data_ptr(), 4, self.word.data_ptr(),
                                             self.weight.data_ptr(), self.nid.data_ptr(), stream=tr.tstream.cuda_stream)
@@ -286,7 +286,7 @@ class NewMapPointsLeg:
             self.desc[sl] = tr.d_desc[fr]
             self.cnt[sl] = tr.d_cnt[fr]
             self.tcw[sl] = tr.d_tcw.view(tr.B, -1)[fr]
-            self.fmp[sl] = self.fmp_frames[fr]
+            self.fmp[sl] = self.fmp_frames[fr + tr.p * tr.B]   # the frames of the pool set just tracked
             # GetMapPoint(i) != NULL: the keypoints Tracking matched (motion model or local map)
             self.has_mp[sl] = ((tr.d_out1[fr] >= 0) | (tr.d_out2[fr] >= 0)).to(torch.uint8)
             self.ready[head].record(tr.tstream)
@@ -352,12 +352,15 @@ class NewMapPointsLeg:
 
         tr, S = self.tr, self.S
         sf = tr.F0.scale_factors.astype(np.float64)
-        fmp = np.zeros((tr.B, S), FUSE_MP_DTYPE)
-        desc_h = tr.d_desc.cpu().numpy()
-        for f in range(tr.B):
-            n = int(tr.cnt_h[f, 0])
-            k = tr.kps_h[f, :n]
-            q, t = tr.poses[f]
+        # every frame of the tracking leg's frame pool (P sets of B: tr.pool)
+        pool = tr.pool
+        nfr = len(pool["poses"])
+        fmp = np.zeros((nfr, S), FUSE_MP_DTYPE)
+        desc_h = pool["desc_h"]
+        for f in range(nfr):
+            n = int(pool["cnt_h"][f, 0])
+            k = pool["kps_h"][f, :n]
+            q, t = pool["poses"][f]
             R = quat_to_rot(q).astype(np.float64)
             Ow = -R.T @ t.astype(np.float64)
             ray_c = np.concatenate([tr.cam.unproject_np(k["x"], k["y"]), np.ones((n, 1))], 1)
@@ -373,7 +376,7 @@ class NewMapPointsLeg:
             m["min_distance"] = (m["max_distance"] / np.float32(sf[-1])).astype(np.float32)
             m["valid"] = 1
             m["desc"] = desc_h[f, :n]
-        self.fmp_frames = torch.from_numpy(fmp.view(np.uint8).reshape(tr.B, -1)).to(self.dev)
+        self.fmp_frames = torch.from_numpy(fmp.view(np.uint8).reshape(nfr, -1)).to(self.dev)
         self.fmp = torch.zeros((self.R, S * FUSE_MP_DTYPE.itemsize), dtype=torch.uint8, device=self.dev)
         self.cnt_col = torch.zeros(self.R, dtype=torch.int32, device=self.dev)
         W, NN, NBK = self.W, self.NN, self.NB_BACK

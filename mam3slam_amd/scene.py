@@ -84,7 +84,7 @@ def local_mappoints(F: FrameData, rng: np.random.Generator, frac=0.8, dup_frac=0
 
 
 def local_world_mappoints(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.8, dup_frac=0.15,
-                          n_random=60, kflip=14, seen_frac=0.05):
+                          n_random=60, kflip=14, seen_frac=0.05, sel=None):
     """Local-map MapPoints in world coordinates around frame F (F.pose = Tcw): Tracking::mvpLocalMapPoints as
     SearchLocalPoints receives them (LOCAL_MP_DTYPE). Points back-project F's keypoints to depths 1.5-40 m, so
     Frame::isInFrustum re-projects them near their keypoints; their normals point from the camera centre with a
@@ -97,7 +97,8 @@ def local_world_mappoints(F: FrameData, cam: Pinhole, rng: np.random.Generator, 
     R = quat_to_rot(q).astype(np.float64)
     Ow = camera_center(F.pose).astype(np.float64)
     n = len(F.keys)
-    sel = rng.choice(n, size=int(n * frac), replace=False)
+    if sel is None:   # the keypoints the local map's points project near (coherent_selection: scene-consistent)
+        sel = rng.choice(n, size=int(n * frac), replace=False)
     m = len(sel)
     k = F.keys[sel]
     z = rng.uniform(1.5, 40.0, m)
@@ -181,14 +182,41 @@ def perturb_pose(pose, rng, rot=0.005, trans=0.02):
     return q, t
 
 
-def motion_last_frame(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.75, n_out=80, kflip=12):
-    """LastFrame entries whose MapPoints re-project near F's keypoints under F.pose (Tcw)."""
+def coherent_selection(F: FrameData, cam: Camera, frac: float, salt: int, cell: float = 0.25) -> np.ndarray:
+    """Indices of F's keypoints whose scene point — the keypoint's ray on the canvas plane (synth.PLANE_DEPTH, world
+    coordinates under F.pose) — lies in a "mapped" cell of the plane (cell x cell world units, ~13 px of a 640-wide
+    view): a hash of the cell below `frac`. The same scene regions are mapped in every view, so a keyframe's keypoints
+    without a MapPoint are mostly unmapped in its neighbours too (as in a real map; an independent draw per frame would
+    leave only frac^2 of the correspondences free in both keyframes of a CreateNewMapPoints pair)."""
+    from . import synth
+    from .match import quat_to_rot
+
+    q, t = F.pose
+    R = quat_to_rot(q).astype(np.float64)
+    Ow = -R.T @ t.astype(np.float64)
+    n = len(F.keys)
+    ray_c = np.concatenate([cam.unproject_np(F.keys["x"], F.keys["y"]), np.ones((n, 1))], 1)
+    ray_w = ray_c @ R   # R^T d
+    X = Ow[None, :] + ((synth.PLANE_DEPTH - Ow[2]) / ray_w[:, 2])[:, None] * ray_w
+    ix = np.floor(X[:, 0] / cell).astype(np.int64).astype(np.uint64)
+    iy = np.floor(X[:, 1] / cell).astype(np.int64).astype(np.uint64)
+    z = ix * np.uint64(0x9E3779B97F4A7C15) ^ iy * np.uint64(0xC2B2AE3D27D4EB4F) ^ np.uint64(salt) * np.uint64(0x165667B1)
+    z = (z ^ (z >> np.uint64(31))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = z ^ (z >> np.uint64(29))
+    return np.nonzero((z >> np.uint64(40)).astype(np.float64) / float(1 << 24) < frac)[0]
+
+
+def motion_last_frame(F: FrameData, cam: Pinhole, rng: np.random.Generator, frac=0.75, n_out=80, kflip=12,
+                      sel=None):
+    """LastFrame entries whose MapPoints re-project near F's keypoints under F.pose (Tcw); sel: the keypoints that
+    get one (default: a random `frac` of them)."""
     from .match import quat_to_rot
 
     q, t = F.pose
     R = quat_to_rot(q)
     n = len(F.keys)
-    sel = rng.choice(n, size=int(n * frac), replace=False)
+    if sel is None:
+        sel = rng.choice(n, size=int(n * frac), replace=False)
     m = len(sel)
     k = F.keys[sel]
     z = rng.uniform(2.0, 12.0, m)

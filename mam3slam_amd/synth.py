@@ -107,15 +107,34 @@ def frame_pose(w: int, h: int, frame: int, f: float = 500.0, depth: float = PLAN
     return q.astype(np.float32), np.array([txy[0], txy[1], 0.0], np.float32)
 
 
+_RAYS = {}
+
+
+def _camera_rays(w: int, h: int, cam, ss: int):
+    """(x / z, y / z) of the ss x ss sub-pixel sample points of every pixel (pose-independent: cached per camera)."""
+    key = (w, h, ss, tuple(cam.params().tolist()))
+    if key not in _RAYS:
+        rays = []
+        for sy in range(ss):
+            for sx in range(ss):
+                yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+                r = cam.unproject_np(xx + (sx + 0.5) / ss - 0.5, yy + (sy + 0.5) / ss - 0.5)
+                rays.append((r[..., 0].copy(), r[..., 1].copy()))
+        _RAYS[key] = rays
+    return _RAYS[key]
+
+
 def make_frame_camera(w: int, h: int, cam, agent: int = 0, frame: int = 0, f: float = 500.0,
-                      depth: float = PLANE_DEPTH, motion: bool = True) -> np.ndarray:
+                      depth: float = PLANE_DEPTH, motion: bool = True, ss: int = 3) -> np.ndarray:
     """make_frame's scene seen through camera `cam` (a match.KannalaBrandt8 — the testMultiAgentSystem agents' fisheye —
-    or a Pinhole) from the same pose, frame_pose(w, h, frame): every pixel's ray (cam.unproject_np) meets the canvas
+    or a Pinhole) from the same pose, frame_pose(w, h, frame): every sample ray (cam.unproject_np) meets the canvas
     plane z = depth (the camera rolls about z and translates in x / y, so the plane is at camera depth `depth` too),
-    where the canvas is sampled bilinearly (mirrored beyond its border). Keyframes of these frames see the scene
-    through the camera they are tracked with, so SearchForTriangulation's camera-specific epipolar test
-    (KannalaBrandt8::epipolarConstrain: two-view triangulation + reprojection) passes for true correspondences. The
-    u8 quantisation and sensor noise are make_frame's."""
+    where the canvas is sampled bilinearly (mirrored beyond its border); a pixel is the mean of ss x ss samples (the
+    fisheye sees the canvas minified ~2.3x: point samples would alias, and a keypoint's descriptor would change with
+    its sub-pixel phase from view to view). Keyframes of these frames see the scene through the camera they are
+    tracked with, so SearchForTriangulation's camera-specific epipolar test (KannalaBrandt8::epipolarConstrain:
+    two-view triangulation + reprojection) passes for true correspondences. The u8 quantisation and sensor noise are
+    make_frame's."""
     from scipy.ndimage import map_coordinates
 
     canvas_seed = frame_seed(agent, 0)
@@ -123,16 +142,16 @@ def make_frame_camera(w: int, h: int, cam, agent: int = 0, frame: int = 0, f: fl
     ch, cw = h + 2 * margin, w + 2 * margin + 4 * 256
     canvas = make_canvas(ch, cw, canvas_seed)
     q, t = frame_pose(w, h, frame, f, depth, motion)
-    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
-    ray = cam.unproject_np(xx, yy)                              # (x / z, y / z) in the camera
-    xc, yc = ray[..., 0] * depth, ray[..., 1] * depth
     a = -2.0 * np.arctan2(float(q[2]), float(q[3]))             # roll of frame_pose's quaternion (about z by -a)
     ca, sa = np.cos(a), np.sin(a)
-    dx, dy = xc - float(t[0]), yc - float(t[1])                 # R^T (Xc - t), R = [[ca, sa], [-sa, ca]]
-    xw, yw = ca * dx - sa * dy, sa * dx + ca * dy
-    px = xw * f / depth + margin + (w - 1) / 2.0                # canvas pixel of the world point (frame_pose's model)
-    py = yw * f / depth + margin + (h - 1) / 2.0
-    out = map_coordinates(canvas, [py, px], order=1, mode="mirror")
+    acc = np.zeros((h, w), np.float64)
+    for rx, ry in _camera_rays(w, h, cam, ss):
+        dx, dy = rx * depth - float(t[0]), ry * depth - float(t[1])   # R^T (Xc - t), R = [[ca, sa], [-sa, ca]]
+        xw, yw = ca * dx - sa * dy, sa * dx + ca * dy
+        px = xw * f / depth + margin + (w - 1) / 2.0            # canvas pixel of the world point (frame_pose's model)
+        py = yw * f / depth + margin + (h - 1) / 2.0
+        acc += map_coordinates(canvas, [py, px], order=1, mode="mirror")
+    out = (acc / (ss * ss)).astype(np.float32)
     rng = np.random.default_rng(frame_seed(agent, frame) ^ 0x5A5A)
     out = out + rng.normal(0.0, 1.5, size=out.shape).astype(np.float32)
     return np.ascontiguousarray(np.clip(np.rint(out), 0, 255).astype(np.uint8))
