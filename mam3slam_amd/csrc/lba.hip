@@ -1355,12 +1355,14 @@ struct TileQueue {
 // per-column timestamps of window 0 of the last k_ldlt_tiles launch (dataflow form): [kc][0..5] = after the critical
 // flag wait, after the pulled updates, after the panel loads, after the pivot steps, after the flag set, backward
 // step done
-__device__ long long g_ltrace[40][6];
+__device__ long long g_ltrace[40][8];
+// (timestamps kept in LDS — sh.ltr — and copied out once at the end: a global store per point would put its own
+// vmcnt wait into the next point's interval)
 #define LTRACE(k, dep)                                                                          \
     do {                                                                                        \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(dep) : "memory");                   \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(dep) : "memory");                            \
         const long long tn_ = clock64();                                                        \
-        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_ltrace[kc][k] = tn_;                   \
+        if ((threadIdx.x & 63) == 0) sh.ltr[kc][k] = tn_;                                       \
     } while (0)
 #else
 #define LTRACE(k, dep) \
@@ -1414,6 +1416,9 @@ struct LdltShared {
     int cflag[40];
     int bflag[40];
     int tcnt[40];                // dataflow tasks: the column's tile tasks done
+#ifdef MAM_LDLT_TRACE
+    long long ltr[40][8];
+#endif
     int maxc;
 };
 
@@ -1817,7 +1822,8 @@ __device__ __forceinline__ void tall_panel(double* TL, const int16_t* slot, int 
 // tall-panel item per column): no workgroup barriers inside the factorization, the waves synchronise through LDS flags
 // (the tasks: see flow_tile_task). The backward solve runs as one owner wave per column in reverse (column kc pulls
 // L(r, kc)^T x_r from its rows r once their flags are set). Every tile and every y entry sees the same updates in the
-// same order with the same arithmetic as in the right-looking schedule of ldlt_tiles.
+// same order as in the right-looking schedule of ldlt_tiles (each update's inner sums split into two chains: the
+// rounding differs from that schedule's in the last bits).
 __device__ __forceinline__ int lds_flag_load(const int* f) {
     return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -1839,6 +1845,52 @@ __device__ __forceinline__ void lds_flag_set(int* f) {
 // one task per column (dependencies only on earlier columns, or on the same column's tile tasks: no wait cycle).
 constexpr int FLOW_TPC = 6;
 
+// C(sc) -= L(sa) D_j L(sb)^T for one tile (a tile task's pulled update), with WITH_Y also y_kc -= L(kc, j) y_j (lane
+// il's row; L(kc, j) = L(sb)): every LDS operand loaded before any use (one wait instead of one per MFMA step), the four
+// MFMAs as two independent chains of two summed at the end, the y dot product as two chains of eight
+template <bool WITH_Y>
+__device__ __forceinline__ void tile_update1(double* TL, int sc, int sa, int sb, const double* dkp, int lane,
+                                             const double* yj, double& yd) {
+    const int col = lane & 15, rq = lane >> 4;
+    double* C = TL + (size_t)sc * 256;
+    const double* La = TL + (size_t)sa * 256;
+    const double* Lb = TL + (size_t)sb * 256;
+    double a[4], b[4], dk[4], lv[NB], yv[NB];
+    dbl4 acc, acc1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        a[q] = La[tsw(col, 4 * q + rq)];
+        b[q] = Lb[tsw(col, 4 * q + rq)];
+        dk[q] = dkp[4 * q + rq];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) acc[r] = C[tsw(rq + 4 * r, col)];
+    if constexpr (WITH_Y) {
+#pragma unroll
+        for (int k = 0; k < NB; k++) {
+            lv[k] = Lb[tsw(col, k)];
+            yv[k] = yj[k];
+        }
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int r = 0; r < 4; r++) acc1[r] = 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], -(b[0] * dk[0]), acc, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[2], -(b[2] * dk[2]), acc1, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], -(b[1] * dk[1]), acc, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[3], -(b[3] * dk[3]), acc1, 0, 0, 0);
+    if constexpr (WITH_Y) {
+        double v0 = yd, v1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < NB / 2; k++) v0 = fma(-lv[k], yv[k], v0);
+#pragma unroll
+        for (int k = NB / 2; k < NB; k++) v1 = fma(-lv[k], yv[k], v1);
+        yd = v0 + v1;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) C[tsw(rq + 4 * r, col)] = acc[r] + acc1[r];
+}
+
 __device__ __forceinline__ void flow_tile_task(double* TL, const int16_t* slot, int nt, int kc, int t, double* Y,
                                                LdltShared& sh, int lane) {
     const int il = lane & 15, kb = NB * kc;
@@ -1852,11 +1904,12 @@ __device__ __forceinline__ void flow_tile_task(double* TL, const int16_t* slot, 
         const int sa = t == 0 ? sb : __builtin_amdgcn_readfirstlane(slot[r * nt + j]);
         if (sa < 0) continue;   // uniform: L(r, j) is zero
         lds_flag_wait(&sh.cflag[j]);
+        if (t == 0) LTRACE(6, j);
         // y_kc -= L(kc, j) y_j rides on the diagonal tile's update
         if (t == 0)
-            tile_update_multi<1>(TL, &sc, &sa, sb, sh.dkall[j], lane, Y + NB * j, &yd);
+            tile_update1<true>(TL, sc, sa, sb, sh.dkall[j], lane, Y + NB * j, yd);
         else
-            tile_update_multi<1>(TL, &sc, &sa, sb, sh.dkall[j], lane);
+            tile_update1<false>(TL, sc, sa, sb, sh.dkall[j], lane, nullptr, yd);
     }
     if (t == 0) {
         if (lane < NB) Y[kb + lane] = yd;
@@ -1888,11 +1941,15 @@ __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot,
     double* Td = TL + (size_t)sd * 256;
     double* Tp = TL + (size_t)(r >= 0 ? rs : sd) * 256;
     double dr[NB], pr[NB];
+    // (r is per 16-lane group: every lane loads — an absent panel tile reads the diagonal tile — and selects, no
+    // exec-masked load per column)
 #pragma unroll
     for (int c = 0; c < NB; c++) {
         dr[c] = Td[tsw(il, c)];
-        pr[c] = r >= 0 ? Tp[tsw(il, c)] : 0.0;
+        pr[c] = Tp[tsw(il, c)];
     }
+#pragma unroll
+    for (int c = 0; c < NB; c++) pr[c] = r >= 0 ? pr[c] : 0.0;
     double yd = Y[kb + il], yp = 0.0, dmine = 1.0;
     LTRACE(2, dr[15]);
 #ifdef MAM_LDLT_PROFILE
@@ -1977,7 +2034,7 @@ __device__ __forceinline__ void flow_back_column(const double* TL, const int16_t
 __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShared& sh, const LMHead& hd) {
     LM& lm = *d.lm;
     const int n = 6 * d.Np, N = d.npad, nt = d.nt, T = hd.ntiles;
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int t = threadIdx.x, lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);   // uniform: scalar task branches
     constexpr int NW = LDLT_THREADS / 64;
 #ifdef MAM_LDLT_PROFILE
     long long lp0 = clock64();
@@ -2074,6 +2131,10 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             for (int kc = wid + (nt - 1 - wid) / NW * NW; kc >= 0; kc -= NW) flow_back_column(TL, slot, nt, kc, Y, sh, lane);
         __syncthreads();
         for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+#ifdef MAM_LDLT_TRACE
+        if (blockIdx.x == 0)
+            for (int i = t; i < nt * 8; i += LDLT_THREADS) g_ltrace[i / 8][i % 8] = sh.ltr[i / 8][i % 8];
+#endif
         LPROF(4);
 #ifdef MAM_LDLT_PROFILE
         if (t == 0) atomicAdd(&g_lprof[7], 1ull);
@@ -3119,13 +3180,14 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     if (!was_stopped) c->trials_ema = 0.75 * c->trials_ema + 0.25 * std::max(1, max_trials);
 #ifdef MAM_LDLT_TRACE
     {
-        long long tr[40][6];
+        long long tr[40][8];
         MAM_HIP(hipMemcpyFromSymbol(tr, HIP_SYMBOL(mam::lba::g_ltrace), sizeof(tr)));
         const int nt0 = hp[0].nt;
         const long long t0 = tr[0][2];
         for (int k = 0; k < nt0 && k < 40; k++)
-            fprintf(stderr, "ltrace col %2d: wait %7lld pull %7lld load %7lld panel %7lld flag %7lld back %7lld\n", k,
-                    tr[k][0] - t0, tr[k][1] - t0, tr[k][2] - t0, tr[k][3] - t0, tr[k][4] - t0, tr[k][5] - t0);
+            fprintf(stderr, "ltrace col %2d: dwait %7lld ddone %7lld count %7lld load %7lld panel %7lld flag %7lld back %7lld\n",
+                    k, tr[k][6] - t0, tr[k][0] - t0, tr[k][1] - t0, tr[k][2] - t0, tr[k][3] - t0, tr[k][4] - t0,
+                    tr[k][5] - t0);
     }
 #endif
 #ifdef MAM_LDLT_PROFILE

@@ -12,7 +12,7 @@ for n in "$@"; do
   if [ "$n" = "--" ]; then tv=0; continue; fi
   if [ $tv = 1 ]; then
     MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_$n.so timeout -k 10 120 python scripts/lba_bench.py --world --solves 3 > $O/lt_$n.json 2> $O/lt_$n.err || { tail -5 $O/lt_$n.err; exit 1; }
-    echo "== $n"; grep ltrace $O/lt_$n.err | tail -19 | awk 'NR%3==1'
+    echo "== $n"; grep ltrace $O/lt_$n.err | tail -19
   else
     bash scripts/gpu_lba_variants.sh $n || exit 1
   fi
