@@ -894,20 +894,43 @@ def main():
         return [a.elapsed_time(b) for a, b in lba_ev]
 
     step_no = [0]
+    # LocalMapping runs beside Tracking as in the reference (its own thread and stream, fed through a queue: the
+    # keyframe queue LocalMapping::InsertKeyFrame fills): one run in progress and one waiting at most, so Tracking
+    # blocks only when LocalMapping falls two runs behind. (Joining each run before the next tracking step would chain
+    # search(i-1) -> LBA(i) -> tracking(i+1) and make the step the sum of the legs.)
+    import queue
+
+    runs = queue.Queue(maxsize=1)
     worker = [None]
+    failure = []
+
+    def mapping_loop():
+        while True:
+            item = runs.get()
+            try:
+                if item is None:
+                    return
+                if not failure:
+                    mapping_worker(*item)
+            except BaseException as e:   # re-raised by finish_mapping on the main thread
+                failure.append(e)
+            finally:
+                runs.task_done()
 
     def finish_mapping():
         if worker[0] is not None:
-            worker[0].join()
-            worker[0] = None
+            runs.join()
+        if failure:
+            raise failure[0]
 
     def step():
-        # LocalMapping runs beside Tracking as in the reference (its own thread and stream): a mapping run started
-        # at one step may overlap the following tracking steps and is joined when the next one starts
         if mapping is not None and step_no[0] % map_every == 0:
-            finish_mapping()
-            worker[0] = threading.Thread(target=mapping_worker, args=(step_no[0] // map_every, newmp.take()))
-            worker[0].start()
+            if worker[0] is None:
+                worker[0] = threading.Thread(target=mapping_loop, daemon=True)
+                worker[0].start()
+            if failure:
+                raise failure[0]
+            runs.put((step_no[0] // map_every, newmp.take()))
         tr.step()
         if mapping is not None and (step_no[0] + 1) % map_every == 0:
             newmp.ingest(step_no[0])
@@ -1158,7 +1181,7 @@ def main():
                 except Exception:
                     mfma = None
             out["roofline_lba"] = {
-                "bound": "mfma", "kernel": "k_ldlt_tiles", "unit": "TFLOP/s", "achieved": ach,
+                "bound": "mfma", "kernel": "k_ldlt_any", "unit": "TFLOP/s", "achieved": ach,
                 "peak": FP64_PEAK_TFS, "frac": ach / FP64_PEAK_TFS if ach else None,
                 "frac_of_cus_used": ach / (FP64_PEAK_TFS * len(g0) / 256.0) if ach else None,
                 "flop_per_factorization": float(np.mean(fl_ldlt)), "windows_per_launch": len(g0),

@@ -120,6 +120,11 @@ struct Prob {
     int8_t* clist_g;
     int8_t* rlist_g;
     uint8_t* ccnt_g;
+    // the order of S's pose blocks (k_struct_tiles): pose block h at position perm[h] (rows 6 perm[h] ..), iperm the
+    // inverse; order_g: the block columns in the order the dataflow factorization takes them (by dependency level)
+    int16_t* perm;
+    int16_t* iperm;
+    int8_t* order_g;
     double* pool;                // [ntiles][256]: S's non-zero tiles in slot order, each 16 x 16 tile as the LDS
                                  // factorization holds it (tsw layout); written by k_schur_blk when lm.tiles_lds
     int nt;                      // npad / 16
@@ -842,7 +847,7 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
             double v = 0.0;
 #pragma unroll
             for (int k = 0; k < 6; k++) v = (k == lane) ? acc[k] : v;
-            d.bs[6 * (size_t)h + lane] = d.b[6 * (size_t)h + lane] - v;
+            d.bs[6 * (size_t)d.perm[h] + lane] = d.b[6 * (size_t)h + lane] - v;   // (position order)
         }
         return;
     }
@@ -852,12 +857,17 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
     tri_index(bt, &tr, &tc);
     const int i1 = d.Np - 1 - tr, i2 = i1 + tc;
     const int bx = i1 * d.Np + i2;   // the block's pair-list slot
+    // S(i1 row r, i2 col c) at the poses' positions, in the lower triangle
+    const int p1 = d.perm[i1], p2 = d.perm[i2];
+    auto store = [&](int r, int c, double v) {
+        if (p2 >= p1)
+            s_store(d, lm.tiles_lds != 0, 6 * p2 + c, 6 * p1 + r, v);
+        else
+            s_store(d, lm.tiles_lds != 0, 6 * p1 + r, 6 * p2 + c, v);
+    };
     if (i1 != i2 && !d.pairmask[(size_t)i1 * d.Np + i2]) {
         // no shared landmark: a zero block (the factorization's fill-in of the previous trial is overwritten)
-        if (lane < 36) {
-            const int r = lane / 6, c = lane % 6;
-            s_store(d, lm.tiles_lds != 0, 6 * i2 + c, 6 * i1 + r, 0.0);
-        }
+        if (lane < 36) store(lane / 6, lane % 6, 0.0);
         return;
     }
     const double lambda = trial_lambda(lm);
@@ -929,7 +939,7 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
         const int r = k / 6, c = k % 6;
         double out = -v;
         if (i1 == i2) out = (d.Hpp[36 * (size_t)i1 + k] + (r == c ? lambda : 0.0)) - v;
-        s_store(d, lm.tiles_lds != 0, 6 * i2 + c, 6 * i1 + r, out);   // the lower triangle, the one the factorization reads
+        store(r, c, out);   // the lower triangle, the one the factorization reads
     }
 }
 
@@ -947,6 +957,9 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
 // Then y /= D and the backward substitution L^T x = y, block by block, each thread updating its own y_i.
 // The workspace (panel + y) is LDS when it fits (use_lds), else the problem's global scratch.
 constexpr int NB = 16;
+#ifndef MAM_LBA_ORDER
+#define MAM_LBA_ORDER 1   // k_struct_tiles' two-chain pose order (0: the window's order)
+#endif
 constexpr int LDLT_TILES_NT_MAX = 40;   // ldlt_tiles' slot map in static LDS: nt <= 40 (npad <= 640)
 #ifndef MAM_LDLT_THREADS
 #define MAM_LDLT_THREADS 512
@@ -1002,16 +1015,6 @@ __global__ __launch_bounds__(SB) void k_blk_scan(const Prob* __restrict__ probs)
     }
     if (t == SB - 1) d.blk_off[n] = part[SB - 1];
 }
-// per problem: the S blocks' landmark pair total, and the LDS tile pool size when the factorization runs in LDS (the
-// host sizes the pair buffer and k_ldlt's dynamic LDS from them)
-__global__ void k_blk_total(const Prob* __restrict__ probs, int Q, int* __restrict__ out) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= Q) return;
-    const Prob& d = probs[q];
-    const LM& lm = *d.lm;
-    out[2 * q] = lm.status ? 0 : d.blk_off[d.Np * d.Np];
-    out[2 * q + 1] = (lm.status || !lm.tiles_lds) ? -1 : lm.ntiles;
-}
 // grid (Np * Np, Q) x 64: the pairs, compacted in edge order by ballot
 __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
@@ -1047,29 +1050,68 @@ __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs)
 __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ probs, int lds_bytes) {
     const Prob& d = probs[blockIdx.x];
     if (d.lm->status) return;
-    const int nt = d.nt, n = 6 * d.Np;
-    for (int q = threadIdx.x; q < nt * nt; q += SB) {
-        const int r = q / nt, c = q % nt;
-        uint8_t v = 0;
-        if (r == c) {
-            v = 1;
-        } else if (r > c) {
-            const int r0 = NB * r, r1 = min(NB * r + NB, n), c0 = NB * c, c1 = min(NB * c + NB, n);
-            if (r0 < r1 && c0 < c1) {
-                for (int i1 = c0 / 6; i1 <= (c1 - 1) / 6 && !v; i1++)
-                    for (int i2 = r0 / 6; i2 <= (r1 - 1) / 6 && !v; i2++)
-                        if (i1 == i2 || d.pairmask[(size_t)min(i1, i2) * d.Np + max(i1, i2)]) v = 1;
-            }
-        }
-        d.tmask[q] = v;
+    const int nt = d.nt, n = 6 * d.Np, Np = d.Np;
+    // The pose order. For a banded pose graph (bandwidth b: poses more than b apart in the window share no landmark),
+    // [0, m) | [m + s, Np) reversed | [m, m + s), s >= b: no S entry couples the two ends, so they factor as two
+    // independent dependency chains of about half the length and the separator follows (nested dissection, one
+    // level; Eigen's SimplicialLDLT orders with AMD for the same reason: linear_solver_eigen.h). m and m + (Np - m - s)
+    // are multiples of 8 poses (48 rows: three tiles), so no 16-row tile holds poses of two parts. Kept only when the
+    // reordered pattern (its fill included) still fits the LDS factorization; otherwise the window's own order.
+    __shared__ int bw, nnz;
+    if (threadIdx.x == 0) bw = 0;
+    __syncthreads();
+    for (int q = threadIdx.x; q < Np * Np; q += SB) {
+        const int i1 = q / Np, i2 = q % Np;
+        if (i2 > i1 && d.pairmask[q]) atomicMax(&bw, i2 - i1);
     }
     __syncthreads();
-    for (int c = 0; c + 1 < nt; c++) {
-        const int m = nt - 1 - c;
-        for (int q = threadIdx.x; q < m * m; q += SB) {
-            const int r1 = c + 1 + q / m, r2 = c + 1 + q % m;
-            if (r2 <= r1 && d.tmask[(size_t)r1 * nt + c] && d.tmask[(size_t)r2 * nt + c]) d.tmask[(size_t)r1 * nt + r2] = 1;
+    const int b = bw;
+    int sep = b;
+    while ((Np - sep) % 8) sep++;
+    const int m = (Np - sep) / 16 * 8, nb = Np - sep - m;
+    for (int attempt = MAM_LBA_ORDER && b > 0 && m >= 8 && nb >= 8 ? 0 : 1; attempt < 2; attempt++) {
+        for (int h = threadIdx.x; h < Np; h += SB) {
+            int p = h;
+            if (attempt == 0) p = h >= m + sep ? m + (Np - 1 - h) : h >= m ? h + nb : h;
+            d.perm[h] = (int16_t)p;
+            d.iperm[p] = (int16_t)h;
         }
+        if (threadIdx.x == 0) nnz = 0;
+        __syncthreads();
+        for (int q = threadIdx.x; q < nt * nt; q += SB) {
+            const int r = q / nt, c = q % nt;
+            uint8_t v = 0;
+            if (r == c) {
+                v = 1;
+            } else if (r > c) {
+                const int r0 = NB * r, r1 = min(NB * r + NB, n), c0 = NB * c, c1 = min(NB * c + NB, n);
+                if (r0 < r1 && c0 < c1) {
+                    for (int p1 = c0 / 6; p1 <= (c1 - 1) / 6 && !v; p1++)
+                        for (int p2 = r0 / 6; p2 <= (r1 - 1) / 6 && !v; p2++) {
+                            const int i1 = d.iperm[p1], i2 = d.iperm[p2];
+                            if (i1 == i2 || d.pairmask[(size_t)min(i1, i2) * Np + max(i1, i2)]) v = 1;
+                        }
+                }
+            }
+            d.tmask[q] = v;
+        }
+        __syncthreads();
+        for (int c = 0; c + 1 < nt; c++) {
+            const int mm = nt - 1 - c;
+            for (int q = threadIdx.x; q < mm * mm; q += SB) {
+                const int r1 = c + 1 + q / mm, r2 = c + 1 + q % mm;
+                if (r2 <= r1 && d.tmask[(size_t)r1 * nt + c] && d.tmask[(size_t)r2 * nt + c])
+                    d.tmask[(size_t)r1 * nt + r2] = 1;
+            }
+            __syncthreads();
+        }
+        int cnt = 0;
+        for (int q = threadIdx.x; q < nt * nt; q += SB) cnt += d.tmask[q];
+        atomicAdd(&nnz, cnt);
+        __syncthreads();
+        if (attempt == 0 && nt <= LDLT_TILES_NT_MAX &&
+            (size_t)nnz * 256 * sizeof(double) + (size_t)d.npad * sizeof(double) <= (size_t)lds_bytes)
+            break;   // uniform
         __syncthreads();
     }
     // the non-zero tiles' slots in ldlt_tiles' LDS pool (row-major order of (r, c), r >= c), their count, and whether
@@ -1130,6 +1172,32 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
             d.ccnt_g[k] = (uint8_t)nc;
             d.ccnt_g[nt + k] = (uint8_t)nr;
             atomicMax(&maxc, nc);
+        }
+        // the dataflow order: block columns by dependency level (1 + the deepest column they pull from), then index —
+        // with the split pose order the two ends' columns alternate (from LDS copies of the row lists: one thread
+        // walks them)
+        __shared__ int8_t rl_s[LDLT_TILES_NT_MAX * 40];
+        __shared__ uint8_t rc_s[LDLT_TILES_NT_MAX];
+        __shared__ int8_t lev[LDLT_TILES_NT_MAX];
+        for (int k = t; k < nt; k += SB) {
+            int nr = 0;
+            for (int c = 0; c < k; c++)
+                if (d.tmask[(size_t)k * nt + c]) rl_s[k * 40 + nr++] = (int8_t)c;
+            rc_s[k] = (uint8_t)nr;
+        }
+        __syncthreads();
+        if (t == 0) {
+            int maxl = 0;
+            for (int k = 0; k < nt; k++) {
+                int l = 0;
+                for (int q = 0; q < rc_s[k]; q++) l = max(l, lev[rl_s[k * 40 + q]] + 1);
+                lev[k] = (int8_t)l;
+                maxl = max(maxl, l);
+            }
+            int pos = 0;
+            for (int l = 0; l <= maxl; l++)
+                for (int k = 0; k < nt; k++)
+                    if (lev[k] == l) d.order_g[pos++] = (int8_t)k;
         }
         if (nt > 0)
             for (int q = t; q < nt * 256; q += SB) {
@@ -1362,7 +1430,7 @@ __device__ long long g_ltrace[40][8];
     do {                                                                                        \
         asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(dep) : "memory");                            \
         const long long tn_ = clock64();                                                        \
-        if ((threadIdx.x & 63) == 0) sh.ltr[kc][k] = tn_;                                       \
+        if ((threadIdx.x & 63) == 0) sh.ltr[kc][k] = (int)tn_;                                  \
     } while (0)
 #else
 #define LTRACE(k, dep) \
@@ -1398,26 +1466,34 @@ constexpr int C1_PF = MAM_LDLT_C1_PF;   // (C1) tiles per wave prefetched across
 constexpr int LDLT_TM_MAX = 40;         // the LDS path's tile-mask copy: nt <= 40 (npad <= 640)
 // The factorization's static LDS, shared by both forms of k_ldlt (ldlt_global, ldlt_tiles)
 struct LdltShared {
-    double Ld[NB * NB];          // ldlt_global: L11 row-major
+    // (the two forms' own fields share their LDS: a launch runs one form per problem. Every byte here is taken from
+    // the tile pool's budget.)
+    union {
+        struct {
+            double Ld[NB * NB];  // ldlt_global: L11 row-major
+            double invdk[NB];
+        };
+        struct {
+            // ldlt_tiles: per block column kc the rows r > kc of its non-zero tiles (ascending), per block row kc the
+            // columns c < kc of its non-zero tiles — the panel / trailing / backward loops walk only those
+            alignas(4) int8_t clist[40 * 40];
+            alignas(4) int8_t rlist[40 * 40];
+        };
+    };
     double dk[2][NB];
-    double invdk[NB];
     int fail;
     // ldlt_global<true>: the tile mask (uint8 [nt][nt]); ldlt_tiles: the tile slot map (int16 [nt][nt])
     int16_t map[LDLT_TM_MAX * LDLT_TM_MAX];
-    int16_t tl[2 * 96];          // ldlt_tiles: (r, c) of each pool slot
-    // ldlt_tiles: per block column kc the rows r > kc of its non-zero tiles (ascending), per block row kc the columns
-    // c < kc of its non-zero tiles — the panel / trailing / backward loops walk only those
-    alignas(4) int8_t clist[40 * 40];
-    alignas(4) int8_t rlist[40 * 40];
     uint8_t ccount[40];
     uint8_t rcount[40];
-    // ldlt_tiles' dataflow form: every column's D, the columns' factored / solved flags, the widest column's tile count
-    double dkall[40][NB];
+    // ldlt_tiles' dataflow form (a column's D: the diagonal of its factored diagonal tile): the columns' factored /
+    // solved flags, the widest column's tile count
     int cflag[40];
     int bflag[40];
     int tcnt[40];                // dataflow tasks: the column's tile tasks done
+    alignas(4) int8_t order[40]; // dataflow: the block columns in dependency-level order (k_struct_tiles)
 #ifdef MAM_LDLT_TRACE
-    long long ltr[40][8];
+    int ltr[40][8];   // (low 32 bits of the cycle counter)
 #endif
     int maxc;
 };
@@ -1611,7 +1687,7 @@ __device__ __forceinline__ void ldlt_global(const Prob& d, double* lds_ws, LdltS
         }
         __syncthreads();
     }
-    for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+    for (int i = t; i < n; i += LDLT_THREADS) d.x[6 * (size_t)d.iperm[i / 6] + i % 6] = Y[i];   // (pose order)
     LPROF(4);
 #ifdef MAM_LDLT_PROFILE
     if (t == 0) atomicAdd(&g_lprof[7], 1ull);
@@ -1782,6 +1858,36 @@ template <>
 struct Tall16<NB> {
     __device__ __forceinline__ static void run(double*, double*, double&, double&, double&, int) {}
 };
+// Tall16 with two panel rows per lane (tiles g and g + 4 of a column with up to 8 panel tiles); the panel rows' y is
+// not kept (the dataflow form's rows pull theirs)
+template <int J>
+struct Tall16x2 {
+    __device__ __forceinline__ static void run(double* dr, double* pr, double* pq, double& yd, double& dmine, int il) {
+        const double a = dr[J];
+        const double dj = bcast16_d(a, J);
+        if (il == J) dmine = dj;
+        const double inv0 = __builtin_amdgcn_rcp(dj);
+        const double e = fma(-dj, inv0, 1.0);
+        const double inv = fma(inv0, fma(e, e, e), inv0);
+        const double l = a * inv, lp = pr[J] * inv, lq = pq[J] * inv;
+        const double yj = bcast16_d(yd, J);
+        if constexpr (J + 1 < NB) dr[J + 1] = fma(-l, bcast16_d(a, J + 1), dr[J + 1]);
+        FnmacRow16<J, J + 2>::run(dr, a, l);
+        FnmacRow16<J, J + 1>::run(pr, a, lp);
+        FnmacRow16<J, J + 1>::run(pq, a, lq);
+        if (il > J) {
+            dr[J] = l;
+            yd = fma(-l, yj, yd);
+        }
+        pr[J] = lp;
+        pq[J] = lq;
+        Tall16x2<J + 1>::run(dr, pr, pq, yd, dmine, il);
+    }
+};
+template <>
+struct Tall16x2<NB> {
+    __device__ __forceinline__ static void run(double*, double*, double*, double&, double&, int) {}
+};
 
 // One tall-panel item of block column kc: the diagonal tile + the column's non-zero tiles clist[kc][4 q + g] (g = 0..3)
 // factored; the item-0 wave stores the diagonal tile (L below, D on it; the upper triangle is left to the inverse
@@ -1843,13 +1949,13 @@ __device__ __forceinline__ void lds_flag_set(int* f) {
 // in parallel (4 f64 MFMAs each, 64 cycles apiece) instead of one wave's 16 in turn, and the next column's tile tasks
 // are never on the wave factoring this column's panel. Every wave walks the columns in ascending order with at most
 // one task per column (dependencies only on earlier columns, or on the same column's tile tasks: no wait cycle).
-constexpr int FLOW_TPC = 6;
+constexpr int FLOW_TPC = 10;   // up to 9 tile tasks + the panel task per column (columns of up to 8 panel tiles)
 
 // C(sc) -= L(sa) D_j L(sb)^T for one tile (a tile task's pulled update), with WITH_Y also y_kc -= L(kc, j) y_j (lane
 // il's row; L(kc, j) = L(sb)): every LDS operand loaded before any use (one wait instead of one per MFMA step), the four
 // MFMAs as two independent chains of two summed at the end, the y dot product as two chains of eight
 template <bool WITH_Y>
-__device__ __forceinline__ void tile_update1(double* TL, int sc, int sa, int sb, const double* dkp, int lane,
+__device__ __forceinline__ void tile_update1(double* TL, int sc, int sa, int sb, const double* Dj, int lane,
                                              const double* yj, double& yd) {
     const int col = lane & 15, rq = lane >> 4;
     double* C = TL + (size_t)sc * 256;
@@ -1861,7 +1967,7 @@ __device__ __forceinline__ void tile_update1(double* TL, int sc, int sa, int sb,
     for (int q = 0; q < 4; q++) {
         a[q] = La[tsw(col, 4 * q + rq)];
         b[q] = Lb[tsw(col, 4 * q + rq)];
-        dk[q] = dkp[4 * q + rq];
+        dk[q] = Dj[NB * (4 * q + rq)];   // D_j(k) = the diagonal of column j's factored diagonal tile, tsw(k, k)
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) acc[r] = C[tsw(rq + 4 * r, col)];
@@ -1906,10 +2012,11 @@ __device__ __forceinline__ void flow_tile_task(double* TL, const int16_t* slot, 
         lds_flag_wait(&sh.cflag[j]);
         if (t == 0) LTRACE(6, j);
         // y_kc -= L(kc, j) y_j rides on the diagonal tile's update
+        const double* Dj = TL + (size_t)__builtin_amdgcn_readfirstlane(slot[j * nt + j]) * 256;
         if (t == 0)
-            tile_update1<true>(TL, sc, sa, sb, sh.dkall[j], lane, Y + NB * j, yd);
+            tile_update1<true>(TL, sc, sa, sb, Dj, lane, Y + NB * j, yd);
         else
-            tile_update1<false>(TL, sc, sa, sb, sh.dkall[j], lane, nullptr, yd);
+            tile_update1<false>(TL, sc, sa, sb, Dj, lane, nullptr, yd);
     }
     if (t == 0) {
         if (lane < NB) Y[kb + lane] = yd;
@@ -1923,9 +2030,9 @@ __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot,
     const int g = lane >> 4, il = lane & 15, kb = NB * kc;
     const int ncl = __builtin_amdgcn_readfirstlane(sh.ccount[kc]);
     const int sd = __builtin_amdgcn_readfirstlane(slot[kc * nt + kc]);
-    int rows[4], rsl[4];
+    int rows[8], rsl[8];
 #pragma unroll
-    for (int a = 0; a < 4; a++) {
+    for (int a = 0; a < 8; a++) {
         rows[a] = a < ncl ? __builtin_amdgcn_readfirstlane(sh.clist[kc * 40 + a]) : -1;
         rsl[a] = a < ncl ? __builtin_amdgcn_readfirstlane(slot[rows[a] * nt + kc]) : -1;
     }
@@ -1935,7 +2042,7 @@ __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot,
     long long tp0 = clock64();
 #endif
     LTRACE(1, kc);
-    // the tall panel: the diagonal tile and the (<= 4) panel tiles, lane (g, il)
+    // the tall panel: the diagonal tile and the panel tiles, lane (g, il) with row il of tiles g (and g + 4)
     const int r = g == 0 ? rows[0] : g == 1 ? rows[1] : g == 2 ? rows[2] : rows[3];
     const int rs = g == 0 ? rsl[0] : g == 1 ? rsl[1] : g == 2 ? rsl[2] : rsl[3];
     double* Td = TL + (size_t)sd * 256;
@@ -1951,12 +2058,28 @@ __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot,
 #pragma unroll
     for (int c = 0; c < NB; c++) pr[c] = r >= 0 ? pr[c] : 0.0;
     double yd = Y[kb + il], yp = 0.0, dmine = 1.0;
+    const bool two = ncl > 4;   // uniform
+    int r2 = -1;
+    double* Tq = Td;
+    double pq[NB];
+    if (two) {
+        r2 = g == 0 ? rows[4] : g == 1 ? rows[5] : g == 2 ? rows[6] : rows[7];
+        const int rs2 = g == 0 ? rsl[4] : g == 1 ? rsl[5] : g == 2 ? rsl[6] : rsl[7];
+        Tq = TL + (size_t)(r2 >= 0 ? rs2 : sd) * 256;
+#pragma unroll
+        for (int c = 0; c < NB; c++) pq[c] = Tq[tsw(il, c)];
+#pragma unroll
+        for (int c = 0; c < NB; c++) pq[c] = r2 >= 0 ? pq[c] : 0.0;
+    }
     LTRACE(2, dr[15]);
 #ifdef MAM_LDLT_PROFILE
     long long tp1 = clock64();
     if (lane == 0) atomicAdd(&g_lprof[6], (unsigned long long)(tp1 - tp0));   // the panel loads
 #endif
-    Tall16<0>::run(dr, pr, yd, yp, dmine, il);
+    if (two)
+        Tall16x2<0>::run(dr, pr, pq, yd, dmine, il);
+    else
+        Tall16<0>::run(dr, pr, yd, yp, dmine, il);
     LTRACE(3, dmine);
 #ifdef MAM_LDLT_PROFILE
     long long tp2 = clock64();
@@ -1967,13 +2090,16 @@ __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot,
     if (g == 0) {
 #pragma unroll
         for (int c = 0; c < NB; c++) Td[tsw(il, c)] = dr[c];
-        sh.dkall[kc][il] = dmine;
         Y[kb + il] = yd;
         if (dmine == 0.0) sh.fail = 1;
     }
     if (r >= 0) {
 #pragma unroll
         for (int c = 0; c < NB; c++) Tp[tsw(il, c)] = pr[c];
+    }
+    if (two && r2 >= 0) {
+#pragma unroll
+        for (int c = 0; c < NB; c++) Tq[tsw(il, c)] = pq[c];
     }
     lds_flag_set(&sh.cflag[kc]);
     LTRACE(4, kc);
@@ -2076,6 +2202,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             rw[u] = q < nw ? ((gu32*)d.rlist_g)[q] : 0u;
         }
         if (t < 2 * nt) cv = ((gu8*)d.ccnt_g)[t];
+        const int8_t ov = t < nt ? ((__attribute__((address_space(1))) const int8_t*)d.order_g)[t] : 0;
 #pragma unroll
         for (int u = 0; u < YPT; u++) {
             const int i = t + u * LDLT_THREADS;
@@ -2098,6 +2225,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         }
         if (t < nt) {
             sh.ccount[t] = cv;
+            sh.order[t] = ov;
             sh.cflag[t] = 0;
             sh.bflag[t] = 0;
             sh.tcnt[t] = 0;
@@ -2113,24 +2241,31 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
 #ifndef MAM_LDLT_FLOW
 #define MAM_LDLT_FLOW 1
 #endif
-    if (MAM_LDLT_FLOW && sh.maxc <= 4 && nt <= 40) {   // uniform: every column one tall-panel item
-        static_assert(NW >= FLOW_TPC, "a column's tasks need distinct waves");
-        for (int kc = 0; kc < nt; kc++) {
-            const int tk = (wid - FLOW_TPC * kc % NW + NW) % NW;   // this wave's task in column kc
-            if (tk == FLOW_TPC - 1)
-                flow_panel_task(TL, slot, nt, kc, Y, sh, lane);
-            else if (tk <= __builtin_amdgcn_readfirstlane(sh.ccount[kc]))
-                flow_tile_task(TL, slot, nt, kc, tk, Y, sh, lane);
+    if (MAM_LDLT_FLOW && sh.maxc <= 8 && nt <= 40) {   // uniform: every column one tall-panel item
+        // the columns in dependency-level order (k_struct_tiles: a topological order, so every wave walking it
+        // in turn waits only on tasks earlier in it), position sp's tasks on waves FLOW_TPC sp + t
+        for (int sp = 0; sp < nt; sp++) {
+            const int kc = __builtin_amdgcn_readfirstlane(sh.order[sp]);
+            const int ncl = __builtin_amdgcn_readfirstlane(sh.ccount[kc]);
+            // this wave's tasks of column kc in task order (tile tasks before the panel task: a wave holding both
+            // finishes its tile task first)
+            for (int tk = (wid - FLOW_TPC * sp % NW + NW) % NW; tk < FLOW_TPC; tk += NW) {
+                if (tk == FLOW_TPC - 1)
+                    flow_panel_task(TL, slot, nt, kc, Y, sh, lane);
+                else if (tk <= ncl)
+                    flow_tile_task(TL, slot, nt, kc, tk, Y, sh, lane);
+            }
         }
         __syncthreads();
         LPROF(1);
         const int fl = sh.fail;
         if (t == 0) lm.fail = fl;
         if (fl) return;   // uniform
-        if (wid < nt)   // the wave's columns, descending
-            for (int kc = wid + (nt - 1 - wid) / NW * NW; kc >= 0; kc -= NW) flow_back_column(TL, slot, nt, kc, Y, sh, lane);
+        // the backward steps in the reverse order (column kc waits for the rows below it: later in the order)
+        for (int sp = nt - 1; sp >= 0; sp--)
+            if (sp % NW == wid) flow_back_column(TL, slot, nt, __builtin_amdgcn_readfirstlane(sh.order[sp]), Y, sh, lane);
         __syncthreads();
-        for (int i = t; i < n; i += LDLT_THREADS) d.x[i] = Y[i];
+        for (int i = t; i < n; i += LDLT_THREADS) d.x[6 * (size_t)d.iperm[i / 6] + i % 6] = Y[i];   // (pose order)
 #ifdef MAM_LDLT_TRACE
         if (blockIdx.x == 0)
             for (int i = t; i < nt * 8; i += LDLT_THREADS) g_ltrace[i / 8][i % 8] = sh.ltr[i / 8][i % 8];
@@ -2256,7 +2391,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
             if (c >= 0) Y[yi] = sy;
         }
     }
-    for (int i = lane; i < n; i += 64) d.x[i] = Y[i];
+    for (int i = lane; i < n; i += 64) d.x[6 * (size_t)d.iperm[i / 6] + i % 6] = Y[i];   // (pose order)
     LPROF(4);
 #ifdef MAM_LDLT_PROFILE
     if (t == 0) atomicAdd(&g_lprof[7], 1ull);
@@ -2674,36 +2809,20 @@ __device__ __forceinline__ void pose_epilogue(const Prob& d, LM& lm, int cur, co
     }
 }
 
-// grid (Q) x LDLT_THREADS: S x = bs of the problems whose tile pool fits in LDS (lm.tiles_lds; dynamic LDS >= the
-// largest pool + y of the batch), then the pose epilogue
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_tiles(const Prob* __restrict__ probs) {
-    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-    __shared__ LdltShared sh;
-    const Prob& d = probs[blockIdx.x];
-    const LMHead hd = lm_head(d.lm);
-    if (hd.status || hd.done || !hd.tiles_lds) return;
-    LM& lm = *d.lm;
-    if (d.Np == 0) {
-        if (threadIdx.x == 0) lm.fail = 0;
-    } else {
-        ldlt_tiles(d, lds_dyn, sh, hd);
-    }
-    __syncthreads();
-    pose_epilogue<LDLT_THREADS>(d, lm, hd.cur, d.x, trial_lambda(hd));
-}
-
-// grid (Q) x LDLT_THREADS: the others, factored in place in HBM (the panel workspace in LDS when use_lds), then the
-// pose epilogue
+// grid (Q) x LDLT_THREADS: either form per problem (k_struct_tiles' choice, read on the device), so the host launches
+// one factorization per trial without reading the choice back; dynamic LDS: the larger of the two forms' needs
 template <bool use_lds>
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt(const Prob* __restrict__ probs) {
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restrict__ probs) {
     extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
     __shared__ LdltShared sh;
     const Prob& d = probs[blockIdx.x];
     const LMHead hd = lm_head(d.lm);
-    if (hd.status || hd.done || hd.tiles_lds) return;
+    if (hd.status || hd.done) return;
     LM& lm = *d.lm;
     if (d.Np == 0) {
         if (threadIdx.x == 0) lm.fail = 0;
+    } else if (hd.tiles_lds) {
+        ldlt_tiles(d, lds_dyn, sh, hd);
     } else {
         ldlt_global<use_lds>(d, lds_dyn, sh);
     }
@@ -2818,11 +2937,8 @@ struct mam_lba_ctx {
     mam::StageTimer timer{4};
     DevBuf<uint8_t> arena;        // per-problem structure, state and scratch of the current batch
     DevBuf<uint8_t> io;           // host API: inputs + outputs of the one problem
-    DevBuf<Prob> probs;
-    DevBuf<LM> lms;
+    DevBuf<uint8_t> hdr;          // Prob[Q] | LM[Q] | Outs[Q] of the current batch
     DevBuf<int2> blk_pairs;       // the S blocks' landmark pairs of the current batch
-    DevBuf<int> blk_tot;
-    mam::PinnedBuf blk_tot_host;
     static constexpr int kMaxGroups = 4;
     hipStream_t gstream[kMaxGroups - 1] = {};   // groups 1.. of a split batch (created on first use, caller's priority)
     hipEvent_t ev_start = nullptr, ev_done[kMaxGroups - 1] = {};
@@ -2853,7 +2969,8 @@ size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
            al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) + al(4 * ((size_t)Np * Np + 1)) +
            al((size_t)(npad / 16) * (npad / 16)) + al(2 * (size_t)(npad / 16) * (npad / 16)) +
            al(2 * (size_t)(npad / 16) * (npad / 16 + 1)) + 2 * al(40 * (size_t)std::max(npad / 16, 1)) +
-           al(2 * (size_t)std::max(npad / 16, 1)) + al(8 * 256 * (size_t)(npad / 16) * (npad / 16 + 1) / 2) +
+           al(2 * (size_t)std::max(npad / 16, 1)) + 2 * al(2 * (size_t)std::max(Np, 1)) + al(40) +
+           al(8 * 256 * (size_t)(npad / 16) * (npad / 16 + 1) / 2) +
            2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
            3 * al(8 * (size_t)(std::max((E + 63) / 64, (L + mam::lba::PW - 1) / mam::lba::PW) + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
            al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
@@ -2882,6 +2999,9 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.clist_g = cv.take<int8_t>((size_t)std::max(d.nt, 1) * 40);
     d.rlist_g = cv.take<int8_t>((size_t)std::max(d.nt, 1) * 40);
     d.ccnt_g = cv.take<uint8_t>(2 * (size_t)std::max(d.nt, 1));
+    d.perm = cv.take<int16_t>((size_t)std::max(d.Np, 1));
+    d.iperm = cv.take<int16_t>((size_t)std::max(d.Np, 1));
+    d.order_g = cv.take<int8_t>(40);
     d.pool = cv.take<double>((size_t)d.nt * (d.nt + 1) / 2 * 256);
     d.pose[0] = cv.take<double>(7 * (size_t)d.P);
     d.pose[1] = cv.take<double>(7 * (size_t)d.P);
@@ -2954,11 +3074,6 @@ __global__ __launch_bounds__(256) void k_finish(const Prob* __restrict__ probs, 
 
 namespace {
 
-DevBuf<Outs>& outs_buf() {
-    static thread_local DevBuf<Outs> b;
-    return b;
-}
-
 // The shared driver: Q problems whose inputs (id-ordered) are already in device memory, described by hp[q] (input
 // pointers, dimensions, delta, iterations in lm0[q]). Builds the structure on the device, runs the LM slots, writes
 // the outputs and fills the host-side scalars of res[q] (iterations, trials, chi2s, status).
@@ -2981,8 +3096,6 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         maxLb = std::max(maxLb, (d.L + 255) / 256 + d.Np);
         max_lds = std::max(max_lds, ldlt_lds_bytes(d.npad));
     }
-    size_t tiles_dyn = 0;                        // k_ldlt_tiles' dynamic LDS (set once the structure is known)
-    bool any_tiles = false, any_global = false;  // problems factored in LDS / in HBM
     if (max_lds > c->ldlt_lds_budget) lds_ok = false;
     if (ldlt_pad(6 * maxNp) / NB > LDLT_TM_MAX) lds_ok = false;   // the LDS path keeps the tile mask in LDS too
     // size bounds before any allocation: the dense pose x landmark edge table (Np L int32) and S (npad^2 f64) of one
@@ -3005,23 +3118,39 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
             return MAM_ERR_CAPACITY;
         }
     }
+    // the S blocks' landmark pairs: at most (edges of the optimised poses) x (optimised poses observing the landmark)
+    // per block column, so E Np per problem bounds them (sized up front: no read-back of the counts before the fill)
+    std::vector<size_t> pair_cap(Q);
+    size_t npairs = 0;
+    for (int q = 0; q < Q; q++) {
+        pair_cap[q] = (size_t)hp[q].E * (size_t)std::max(hp[q].Np, 1);
+        npairs += pair_cap[q];
+    }
     if (int rc = c->arena.alloc(bytes + kAlign)) return rc;
-    if (int rc = c->probs.alloc(Q)) return rc;
-    if (int rc = c->lms.alloc(Q)) return rc;
-    if (int rc = outs_buf().alloc(Q)) return rc;
+    if (int rc = c->blk_pairs.alloc(std::max<size_t>(npairs, 1))) return rc;
+    // one device block and one pinned block of the same layout: Prob[Q] | LM[Q] | Outs[Q], one upload
+    const size_t pb = al(sizeof(Prob) * Q), lb = al(sizeof(LM) * Q), ob = al(sizeof(Outs) * Q);
+    if (int rc = c->hdr.alloc(pb + lb + ob)) return rc;
+    if (int rc = c->lm_host.alloc(pb + lb + ob)) return rc;
+    Prob* const P = reinterpret_cast<Prob*>(c->hdr.p);
+    LM* const lms_d = reinterpret_cast<LM*>(c->hdr.p + pb);
+    Outs* const outs_d = reinterpret_cast<Outs*>(c->hdr.p + pb + lb);
     Carver cv{c->arena.p};
     for (auto& d : hp) carve_scratch(cv, d);
-    for (int q = 0; q < Q; q++) hp[q].lm = c->lms.p + q;
-    // one pinned block: Prob[Q] | LM[Q] | Outs[Q]
-    const size_t pb = al(sizeof(Prob) * Q), lb = al(sizeof(LM) * Q), ob = al(sizeof(Outs) * Q);
-    if (int rc = c->lm_host.alloc(pb + lb + ob)) return rc;
+    size_t base = 0;
+    for (int q = 0; q < Q; q++) {
+        hp[q].lm = lms_d + q;
+        hp[q].blk_pair = c->blk_pairs.p + base;
+        base += pair_cap[q];
+    }
     std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
     std::memcpy(c->lm_host.p + pb, lm0.data(), sizeof(LM) * Q);
     std::memcpy(c->lm_host.p + pb + lb, outs.data(), sizeof(Outs) * Q);
-    MAM_HIP(hipMemcpyAsync(c->probs.p, c->lm_host.p, sizeof(Prob) * Q, hipMemcpyHostToDevice, s));
-    MAM_HIP(hipMemcpyAsync(c->lms.p, c->lm_host.p + pb, sizeof(LM) * Q, hipMemcpyHostToDevice, s));
-    MAM_HIP(hipMemcpyAsync(outs_buf().p, c->lm_host.p + pb + lb, sizeof(Outs) * Q, hipMemcpyHostToDevice, s));
-    const Prob* P = c->probs.p;
+    MAM_HIP(hipMemcpyAsync(c->hdr.p, c->lm_host.p, pb + lb + ob, hipMemcpyHostToDevice, s));
+    // the factorization's dynamic LDS: the tile pool budget (k_struct_tiles keeps a problem's pool + y within it) and
+    // the HBM form's panel workspace, the larger
+    size_t ldlt_dyn = c->ldlt_lds_budget;
+    if (lds_ok) ldlt_dyn = std::max(ldlt_dyn, max_lds);
     const dim3 gE((maxE + 255) / 256 > 0 ? (maxE + 255) / 256 : 1, Q);
     const dim3 gE64((maxE + EW - 1) / EW > 0 ? (maxE + EW - 1) / EW : 1, Q);
     {
@@ -3032,36 +3161,10 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_struct_scatter, gE, dim3(256), 0, s, P);
         hipLaunchKernelGGL(k_struct_sort, dim3(std::max(maxLb, 1), Q), dim3(256), 0, s, P);
         hipLaunchKernelGGL(k_struct_tiles, dim3(Q), dim3(SB), 0, s, P, (int)c->ldlt_lds_budget);
-        // the S blocks' landmark pairs: counts, offsets, one read-back of the totals to size the pair buffer
+        // the S blocks' landmark pairs: counts, offsets, the pairs
         const dim3 gB(std::max(maxNp * maxNp, 1), Q);
         hipLaunchKernelGGL(k_blk_count, gB, dim3(64), 0, s, P);
         hipLaunchKernelGGL(k_blk_scan, dim3(1, Q), dim3(SB), 0, s, P);
-        if (int rc = c->blk_tot.alloc(2 * Q)) return rc;
-        if (int rc = c->blk_tot_host.alloc(2 * sizeof(int) * (size_t)Q)) return rc;
-        hipLaunchKernelGGL(k_blk_total, dim3((Q + 255) / 256), dim3(256), 0, s, P, Q, c->blk_tot.p);
-        MAM_HIP(hipGetLastError());
-        MAM_HIP(hipMemcpyAsync(c->blk_tot_host.p, c->blk_tot.p, 2 * sizeof(int) * (size_t)Q, hipMemcpyDeviceToHost,
-                               s));
-        MAM_HIP(hipStreamSynchronize(s));
-        const int* tot = reinterpret_cast<const int*>(c->blk_tot_host.p);
-        size_t npairs = 0;
-        for (int q = 0; q < Q; q++) npairs += (size_t)std::max(tot[2 * q], 0);
-        if (int rc = c->blk_pairs.alloc(std::max<size_t>(npairs, 1))) return rc;
-        size_t base = 0;
-        for (int q = 0; q < Q; q++) {
-            hp[q].blk_pair = c->blk_pairs.p + base;
-            base += (size_t)std::max(tot[2 * q], 0);
-            // k_ldlt_tiles' dynamic LDS: the batch's largest tile pool + y; the others go to k_ldlt
-            if (tot[2 * q + 1] >= 0) {
-                tiles_dyn = std::max(tiles_dyn, (size_t)tot[2 * q + 1] * 256 * sizeof(double) +
-                                                    (size_t)hp[q].npad * sizeof(double));
-                any_tiles = true;
-            } else {
-                any_global = true;
-            }
-        }
-        std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
-        MAM_HIP(hipMemcpyAsync(c->probs.p, c->lm_host.p, sizeof(Prob) * Q, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_blk_fill, gB, dim3(64), 0, s, P);
         // iteration 0's linearisation and system at the initial state (lambda_0 needs its max |diag(H)|), the initial
         // chi2; the first trial's k_point_sys then starts from this system
@@ -3115,13 +3218,10 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 2);
-            if (any_tiles) hipLaunchKernelGGL(k_ldlt_tiles, dim3(Qg), dim3(LDLT_THREADS), tiles_dyn, st, Pg);
-            if (any_global) {
-                if (lds_ok)
-                    hipLaunchKernelGGL(k_ldlt<true>, dim3(Qg), dim3(LDLT_THREADS), max_lds, st, Pg);
-                else
-                    hipLaunchKernelGGL(k_ldlt<false>, dim3(Qg), dim3(LDLT_THREADS), 0, st, Pg);
-            }
+            if (lds_ok)
+                hipLaunchKernelGGL(k_ldlt_any<true>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg);
+            else
+                hipLaunchKernelGGL(k_ldlt_any<false>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
@@ -3141,33 +3241,41 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     };
     auto stopped = [&]() { return stop_flag && *stop_flag; };
     // Every slot is one Levenberg trial of every unfinished problem, so a solve needs at most iterations x 10 slots;
-    // the host reads the states back once per chunk (the first chunk sized by the trials recent solves took).
+    // the host reads the states back once per chunk (the first chunk sized by the trials recent solves took). Each
+    // chunk ends with k_finish (the outputs of the current state: rewritten by the next chunk's if there is one), so
+    // a solve that ends within its first chunk costs one host round trip.
     int max_slots = 0;
     for (auto& l : lm0) max_slots = std::max(max_slots, 10 * std::max(l.iterations, 0));
     int chunk = std::max(1, (int)std::lround(c->trials_ema));   // nearest: a ceil of 9.02 enqueued a 10th slot
     int enq = 0;
     LM* lh = reinterpret_cast<LM*>(c->lm_host.p + pb);
     bool was_stopped = false;
+    const dim3 gFin(std::max({(maxE + 255) / 256, (maxPL + 255) / 256, 1}), Q);
+    auto finish_and_read = [&]() -> int {
+        if (int rc = join()) return rc;
+        hipLaunchKernelGGL(mam::lba::k_finish, gFin, dim3(256), 0, s, P, outs_d);
+        MAM_HIP(hipGetLastError());
+        MAM_HIP(hipMemcpyAsync(lh, lms_d, sizeof(LM) * Q, hipMemcpyDeviceToHost, s));
+        MAM_HIP(hipStreamSynchronize(s));
+        return MAM_OK;
+    };
+    bool read = false;   // lh (and the outputs) hold the state after the last enqueued slot
     while (enq < max_slots) {
         if (stopped()) { was_stopped = true; break; }
         const int k = std::min(chunk, max_slots - enq);
         for (int i = 0; i < k; i++) slot();
         enq += k;
         MAM_HIP(hipGetLastError());
-        if (int rc = join()) return rc;
-        MAM_HIP(hipMemcpyAsync(lh, c->lms.p, sizeof(LM) * Q, hipMemcpyDeviceToHost, s));
-        MAM_HIP(hipStreamSynchronize(s));
+        if (int rc = finish_and_read()) return rc;
+        read = true;
         bool all = true;
         for (int q = 0; q < Q; q++) all = all && (lh[q].done || lh[q].status);
         if (all) break;
+        read = false;   // more slots follow
         chunk = 2;
     }
-    if (int rc = join()) return rc;
-    hipLaunchKernelGGL(mam::lba::k_finish, dim3(std::max({(maxE + 255) / 256, (maxPL + 255) / 256, 1}), Q), dim3(256),
-                       0, s, P, outs_buf().p);
-    MAM_HIP(hipGetLastError());
-    MAM_HIP(hipMemcpyAsync(lh, c->lms.p, sizeof(LM) * Q, hipMemcpyDeviceToHost, s));
-    MAM_HIP(hipStreamSynchronize(s));
+    if (!read)
+        if (int rc = finish_and_read()) return rc;
     int max_trials = 0;
     for (int q = 0; q < Q; q++) {
         res[q].iterations = lh[q].its;
@@ -3251,14 +3359,14 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
     c->ldlt_lds_budget = 0;
     hipFuncAttributes fa{};
     size_t stat = 8192;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&mam::lba::k_ldlt_tiles)) == hipSuccess)
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&mam::lba::k_ldlt_any<true>)) == hipSuccess)
         stat = (fa.sharedSizeBytes + 255) / 256 * 256 + 256;
     else
         (void)hipGetLastError();
     for (size_t budget : {(size_t)160 * 1024 - stat, (size_t)64 * 1024 - stat}) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_tiles),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_any<true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess &&
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt<true>),
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_any<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess) {
             c->ldlt_lds_budget = budget;
             break;
