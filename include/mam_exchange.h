@@ -81,6 +81,37 @@ int mam_exchange_pack_sources(int n_windows, const mam_map_window* windows, cons
 int mam_exchange_apply_compact(const void* gathered, int n_agents, int kf_cap, int mp_cap, float* kf_table,
                                int64_t kf_rows, float* mp_table, int64_t mp_rows, int32_t* status, void* stream);
 
+/* ---- Device-side helpers of the harness around the path (bench.py / mam3slam_amd/mapping.py; no reference
+ * counterpart): keyframes entering the LocalMapping queue and the synthetic map's new state, without host-side
+ * tensor work inside the timed step. */
+
+/* One table of a row copy: row r of the destination (dst + r * dst_stride) gets row src_row_offset + s of the source,
+ * row_bytes bytes (DEVICE pointers; strides and sizes in bytes). */
+typedef struct mam_row_table {
+    const void* src;
+    void* dst;
+    int64_t row_bytes;
+    int64_t src_stride;
+    int64_t dst_stride;
+    int64_t src_row_offset;
+} mam_row_table;
+
+/* Copy n <= 64 rows (src_rows[i] -> dst_rows[i], HOST arrays passed by value) of n_tables <= 8 tables in one launch;
+ * with flags != NULL also flags[dst_rows[i] * flags_stride + j] = (flag_a[src_rows[i] * flag_stride + j] >= 0 ||
+ * flag_b[...] >= 0) for j < flag_cols (a keyframe's "has a MapPoint" flags from Tracking's match lists).
+ * Asynchronous. */
+int mam_copy_rows(int n_tables, const mam_row_table* tables, int n, const int32_t* src_rows, const int32_t* dst_rows,
+                  const int32_t* flag_a, const int32_t* flag_b, int64_t flag_stride, int flag_cols, uint8_t* flags,
+                  int64_t flags_stride, void* stream);
+
+/* The synthetic map's new keyframes at a perturbed state, deterministic in seed: KeyFrame rows kf_idx[i] (DEVICE
+ * int64) get q += N(0, sigma_q) per component, renormalised, w >= 0, and t += N(0, sigma_t); MapPoint rows mp_idx[i]
+ * get xyz += N(0, sigma_x) (counter-based normals). Rows outside the tables set *status to MAM_ERR_ARG.
+ * Asynchronous. */
+int mam_map_perturb(float* kf_table, int64_t kf_rows, const int64_t* kf_idx, int n_kf, float* mp_table,
+                    int64_t mp_rows, const int64_t* mp_idx, int n_mp, uint64_t seed, float sigma_q, float sigma_t,
+                    float sigma_x, int32_t* status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

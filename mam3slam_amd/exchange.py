@@ -24,6 +24,10 @@ _SIGS = {
                                             C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "mam_exchange_apply_compact": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64,
                                              C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),
+    "mam_copy_rows": (C.c_int, [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                C.c_int, C.c_void_p, C.c_int64, C.c_void_p]),
+    "mam_map_perturb": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_int,
+                                  C.c_uint64, C.c_float, C.c_float, C.c_float, C.c_void_p, C.c_void_p]),
 }
 
 # compact blocks (include/mam_exchange.h): header | KeyFrame records | MapPoint records
@@ -61,6 +65,39 @@ class MapWindow(C.Structure):
                 ("point_xyz", C.c_void_p)]
 
 
+class RowTable(C.Structure):
+    """mam_row_table: one table of a mam_copy_rows launch (device pointers, byte strides)."""
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("row_bytes", C.c_int64), ("src_stride", C.c_int64),
+                ("dst_stride", C.c_int64), ("src_row_offset", C.c_int64)]
+
+
+def copy_rows(tables, src_rows, dst_rows, flags=None, stream: int = 0):
+    """mam_copy_rows: rows src_rows[i] -> dst_rows[i] of every table [(src_ptr, dst_ptr, row_bytes, src_stride,
+    dst_stride, src_row_offset)] in one launch (<= 8 tables, <= 64 rows); flags = (flag_a_ptr, flag_b_ptr,
+    flag_stride_bytes, cols, flags_ptr, flags_stride_bytes) also sets flags[dst][j] = a[src][j] >= 0 or b[src][j] >= 0."""
+    L = _bind()
+    tb = (RowTable * max(1, len(tables)))(*[RowTable(*t) for t in tables])
+    n = len(src_rows)
+    sr = (C.c_int32 * max(1, n))(*[int(x) for x in src_rows])
+    dr = (C.c_int32 * max(1, n))(*[int(x) for x in dst_rows])
+    fa = fb = fl = None
+    fs = fc = fls = 0
+    if flags is not None:
+        fa, fb, fs, fc, fl, fls = flags
+        fs //= 4   # int32 elements
+    check(L.mam_copy_rows(len(tables), tb, n, sr, dr, C.c_void_p(fa), C.c_void_p(fb), int(fs), int(fc), C.c_void_p(fl),
+                          int(fls), C.c_void_p(stream)), "mam_copy_rows")
+
+
+def map_perturb(d_kf_table: int, kf_rows: int, d_kf_idx: int, n_kf: int, d_mp_table: int, mp_rows: int, d_mp_idx: int,
+                n_mp: int, seed: int, sigma_q: float, sigma_t: float, sigma_x: float, d_status: int, stream: int = 0):
+    """mam_map_perturb: the synthetic map's new keyframes / MapPoints at a perturbed state (deterministic in seed)."""
+    check(_bind().mam_map_perturb(C.c_void_p(d_kf_table), int(kf_rows), C.c_void_p(d_kf_idx), int(n_kf),
+                                  C.c_void_p(d_mp_table), int(mp_rows), C.c_void_p(d_mp_idx), int(n_mp),
+                                  int(seed) & 0xFFFFFFFFFFFFFFFF, float(sigma_q), float(sigma_t), float(sigma_x),
+                                  C.c_void_p(d_status), C.c_void_p(stream)), "mam_map_perturb")
+
+
 def _bind():
     L = lib()
     for name, (res, args) in _SIGS.items():
@@ -88,7 +125,8 @@ def _all_gather(recv, send, world, group):
     import torch.distributed as dist
 
     if world == 1:
-        recv.copy_(send)
+        if recv.data_ptr() != send.data_ptr():
+            recv.copy_(send)
     elif dist.get_backend(group) == "gloo":
         if send.is_cuda:
             torch.cuda.current_stream(send.device).synchronize()
@@ -117,7 +155,9 @@ class CompactExchange:
         self.rank = dist.get_rank(group) if self.world > 1 else 0
         self.block_bytes = compact_block_bytes(self.kf_cap, self.mp_cap)
         self.send = torch.zeros(self.block_bytes, dtype=torch.uint8, device=device)
-        self.recv = torch.zeros(self.world * self.block_bytes, dtype=torch.uint8, device=device)
+        # one rank: the gathered blocks are its own block (no copy)
+        self.recv = self.send if self.world == 1 else torch.zeros(self.world * self.block_bytes, dtype=torch.uint8,
+                                                                   device=device)
         self._L = _bind()
         self._pack_stream = None
         self.gather_ms = []   # host wall of each all-gather (collective on torch's current stream, synchronised)

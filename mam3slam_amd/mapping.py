@@ -129,18 +129,14 @@ class LocalMappingLeg:
 
     def new_keyframes(self, step: int):
         """Enter every window's new keyframe and its new MapPoints at a perturbed state (deterministic in step)."""
-        import torch
+        # one HIP launch (mam_map_perturb): q + N(0, 0.004) renormalised with w >= 0, t + N(0, 0.012), new MapPoints +
+        # N(0, 0.017), counter-based normals seeded by (step, rank)
+        from .exchange import map_perturb
 
-        g = torch.Generator(device=self.dev)
-        g.manual_seed(1_000_003 * (step + 1) + 7919 * self.rank)
-        nk = self.new_kf
-        dq = torch.randn((len(nk), 4), generator=g, device=self.dev) * 0.004
-        q = self.kf_table[nk, :4] + dq
-        q = q / q.norm(dim=1, keepdim=True)
-        q = torch.where(q[:, 3:4] < 0, -q, q)
-        self.kf_table[nk, :4] = q
-        self.kf_table[nk, 4:7] += torch.randn((len(nk), 3), generator=g, device=self.dev) * 0.012
-        self.mp_table[self.new_mp, :3] += torch.randn((len(self.new_mp), 3), generator=g, device=self.dev) * 0.017
+        map_perturb(self.kf_table.data_ptr(), self.world.n_kf, self.new_kf.data_ptr(), len(self.new_kf),
+                    self.mp_table.data_ptr(), self.world.n_mp, self.new_mp.data_ptr(), len(self.new_mp),
+                    1_000_003 * (step + 1) + 7919 * self.rank, 0.004, 0.012, 0.017, self.status.data_ptr(),
+                    stream=self.stream.cuda_stream)
 
     def run(self, step: int, new_keyframes: bool = True):
         """One LocalMapping step: the solves are synchronous (mam_lba_solve_batch_device returns with the Levenberg
@@ -261,6 +257,7 @@ class NewMapPointsLeg:
             self.cnt.copy_(tr.d_cnt_pool[fr])
             self.tcw.copy_(tr.d_tcw_init_pool.view(tr.P * tr.B, -1)[fr])
             self.fmp.copy_(self.fmp_frames[fr])
+            self.cnt_col.copy_(self.cnt[:, 0])
             self.voc.transform_batch_device(R, self.desc.data_ptr(), S, self.cnt.data_ptr(), 4, self.word.data_ptr(),
                                             self.weight.data_ptr(), self.nid.data_ptr(), stream=tr.tstream.cuda_stream)
             for ev in self.ready.values():
@@ -270,27 +267,34 @@ class NewMapPointsLeg:
     def ingest(self, step: int):
         """Copy step `step`'s new keyframes (frames f = step mod K + i K) into the ring at the next head; on the
         tracking stream after the tracking step. Their BoW is computed by the next `run`."""
-        import torch
-
         tr, W, R = self.tr, self.W, self.R
         K = max(1, tr.B // W)
         head = (self.head + W) % R   # the run at self.head was launched right after its ingest
-        fr = (torch.arange(W, device=self.dev) * K + step % K) % tr.B
-        sl = slice(head, head + W)
+        fr = [(i * K + step % K) % tr.B for i in range(W)]
         # the latest search that read these slots is the one two heads back (R >= 2 W + NN): it must be done
         prev = self.done[(head - 2 * W) % R]
-        with torch.cuda.stream(tr.tstream):
-            if prev is not None:
-                tr.tstream.wait_event(prev)
-            self.keys[sl] = tr.d_kps[fr]
-            self.desc[sl] = tr.d_desc[fr]
-            self.cnt[sl] = tr.d_cnt[fr]
-            self.tcw[sl] = tr.d_tcw.view(tr.B, -1)[fr]
-            self.fmp[sl] = self.fmp_frames[fr + tr.p * tr.B]   # the frames of the pool set just tracked
-            # GetMapPoint(i) != NULL: the keypoints Tracking matched (motion model or local map)
-            self.has_mp[sl] = ((tr.d_out1[fr] >= 0) | (tr.d_out2[fr] >= 0)).to(torch.uint8)
-            self.ready[head].record(tr.tstream)
+        if prev is not None:
+            tr.tstream.wait_event(prev)
+        # one launch (mam_copy_rows): keypoints, descriptors, counts, pose, MapPoints of the frames (the pool set just
+        # tracked), and GetMapPoint(i) != NULL — the keypoints Tracking matched (motion model or local map)
+        self._ingest_rows(tr, fr, list(range(head, head + W)), tr.p * tr.B, tr.tstream.cuda_stream)
+        self.ready[head].record(tr.tstream)
         self.pending = head
+
+    def _ingest_rows(self, tr, fr, slots, fmp_offset, stream, flags=True):
+        from .exchange import copy_rows
+
+        S = self.S
+        tables = [(tr.d_kps.data_ptr(), self.keys.data_ptr(), S * 28, S * 28, S * 28, 0),
+                  (tr.d_desc.data_ptr(), self.desc.data_ptr(), S * 32, S * 32, S * 32, 0),
+                  (tr.d_cnt.data_ptr(), self.cnt.data_ptr(), 8, 8, 8, 0),
+                  (tr.d_cnt.data_ptr(), self.cnt_col.data_ptr(), 4, 8, 4, 0),
+                  (tr.d_tcw.data_ptr(), self.tcw.data_ptr(), tr.tcw_bytes, tr.tcw_bytes, tr.tcw_bytes, 0),
+                  (self.fmp_frames.data_ptr(), self.fmp.data_ptr(), self.fmp.shape[1], self.fmp_frames.shape[1],
+                   self.fmp.shape[1], fmp_offset)]
+        fl = (tr.d_out1.data_ptr(), tr.d_out2.data_ptr(), 4 * tr.cap, S, self.has_mp.data_ptr(), S) if flags else None
+        for i in range(0, len(fr), 64):
+            copy_rows(tables, fr[i:i + 64], slots[i:i + 64], fl, stream=stream)
 
     def take(self):
         """The ring head of the keyframes ingested since the last take (None if none): the next run's work. Called
@@ -425,9 +429,7 @@ class NewMapPointsLeg:
         tcw = self.tcw.data_ptr()
         import torch
 
-        with torch.cuda.stream(stream):
-            self.cnt_col.copy_(self.cnt[:, 0])   # MapPoints of list m (ring slot m): the slot's keypoints
-        m = self.matcher
+        m = self.matcher   # (cnt_col: MapPoints of list m = ring slot m's keypoints, kept by the ingest)
         m.fuse_items_batch_device(self.tr.F0, fr, tcw, self.tr.cam, len(fwd_frame), fwd_frame.data_ptr(),
                                   fwd_mp.data_ptr(), self.fmp.data_ptr(), self.S, self.cnt_col.data_ptr(), 3.0,
                                   self.fwd_idx.data_ptr(), self.fwd_dist.data_ptr(), self.fwd_n.data_ptr(), stream=s)

@@ -242,3 +242,54 @@ def test_compact_pack_apply_kernels(gpu_lib):
     assert any(_norm_orders_differ(q) for r in data[0][0] for q in r[0])
     kf_s, mp_s = _sequential(data[0][0] + data[1][0], data[0][1] + data[1][1], mp_base, 128, 1000)
     assert np.array_equal(kf.cpu().numpy(), kf_s) and np.array_equal(mpt.cpu().numpy(), mp_s)
+
+
+@pytest.mark.gpu
+def test_copy_rows_and_perturb_kernels(gpu_lib):
+    """mam_copy_rows (the ring ingest's one launch) against torch row indexing, incl. an offset source table, a
+    4-byte column of a strided table and the flags; mam_map_perturb: unit quaternions with w >= 0, only the listed
+    rows changed, deterministic in the seed."""
+    import torch
+
+    from mam3slam_amd.exchange import copy_rows, map_perturb
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(3)
+    A = torch.randint(0, 256, (10, 100), dtype=torch.uint8, generator=g).to(dev)
+    B = torch.zeros((7, 100), dtype=torch.uint8, device=dev)
+    cnt = torch.randint(0, 1000, (10, 2), dtype=torch.int32, generator=g).to(dev)
+    col = torch.zeros(7, dtype=torch.int32, device=dev)
+    F = torch.randint(0, 256, (20, 48), dtype=torch.uint8, generator=g).to(dev)
+    G = torch.zeros((7, 48), dtype=torch.uint8, device=dev)
+    o1 = torch.randint(-1, 3, (10, 30), dtype=torch.int32, generator=g).to(dev)
+    o2 = torch.randint(-1, 3, (10, 30), dtype=torch.int32, generator=g).to(dev)
+    fl = torch.zeros((7, 30), dtype=torch.uint8, device=dev)
+    src, dst = [4, 0, 9], [6, 2, 3]
+    copy_rows([(A.data_ptr(), B.data_ptr(), 100, 100, 100, 0), (cnt.data_ptr(), col.data_ptr(), 4, 8, 4, 0),
+               (F.data_ptr(), G.data_ptr(), 48, 48, 48, 10)], src, dst,
+              (o1.data_ptr(), o2.data_ptr(), 4 * 30, 30, fl.data_ptr(), 30))
+    torch.cuda.synchronize()
+    for s_, d_ in zip(src, dst):
+        assert torch.equal(B[d_], A[s_]) and int(col[d_]) == int(cnt[s_, 0]) and torch.equal(G[d_], F[10 + s_])
+        assert torch.equal(fl[d_], ((o1[s_] >= 0) | (o2[s_] >= 0)).to(torch.uint8))
+    for r in set(range(7)) - set(dst):
+        assert int(B[r].sum()) == 0 and int(fl[r].sum()) == 0
+    kf = torch.zeros((5, 8), dtype=torch.float32, device=dev)
+    kf[:, 3] = 1.0
+    mp = torch.zeros((9, 4), dtype=torch.float32, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    ki, mi = torch.tensor([1, 3], device=dev), torch.tensor([0, 5, 8], device=dev)
+    outs = []
+    for _ in range(2):
+        k2, m2 = kf.clone(), mp.clone()
+        map_perturb(k2.data_ptr(), 5, ki.data_ptr(), 2, m2.data_ptr(), 9, mi.data_ptr(), 3, 1234, 0.004, 0.012, 0.017,
+                    st.data_ptr())
+        torch.cuda.synchronize()
+        outs.append((k2, m2))
+    assert int(st) == 0
+    k2, m2 = outs[0]
+    assert torch.equal(k2, outs[1][0]) and torch.equal(m2, outs[1][1])
+    q = k2[ki, :4]
+    assert torch.allclose(q.norm(dim=1), torch.ones(2, device=dev), atol=1e-6) and bool((q[:, 3] >= 0).all())
+    assert bool((k2[[0, 2, 4]] == kf[[0, 2, 4]]).all()) and bool((m2[[1, 2, 3, 4, 6, 7]] == 0).all())
+    assert float(m2[mi, :3].abs().max()) > 0 and float(m2[mi, :3].abs().max()) < 0.2
