@@ -54,8 +54,9 @@ def _u8p(a):
     return a.ctypes.data_as(C.POINTER(C.c_uint8))
 
 
-def extract(img: np.ndarray, p: OrbParams | None = None, lap=(0, 1000)):
-    """ORBextractor::operator() on the oracle. Returns (keypoints structured array, desc (N,32) u8, mono)."""
+def extract(img: np.ndarray, p: OrbParams | None = None, lap=(0, 1000), simd: bool = False):
+    """ORBextractor::operator() on the oracle. Returns (keypoints structured array, desc (N,32) u8, mono). simd: with
+    the AVX2 resize / blur / FAST (oracle/orb_simd.cpp; the same outputs)."""
     p = p or params()
     img = np.ascontiguousarray(img, dtype=np.uint8)
     h, w = img.shape
@@ -64,8 +65,9 @@ def extract(img: np.ndarray, p: OrbParams | None = None, lap=(0, 1000)):
     desc = np.zeros((cap, 32), np.uint8)
     n = C.c_int(0)
     mono = C.c_int(0)
-    rc = lib().oracle_orb_extract(C.byref(p), _u8p(img), w, h, C.c_size_t(w), int(lap[0]), int(lap[1]),
-                                  kps.ctypes.data_as(C.c_void_p), _u8p(desc), cap, C.byref(n), C.byref(mono))
+    fn = lib().oracle_orb_extract_simd if simd else lib().oracle_orb_extract
+    rc = fn(C.byref(p), _u8p(img), w, h, C.c_size_t(w), int(lap[0]), int(lap[1]), kps.ctypes.data_as(C.c_void_p),
+            _u8p(desc), cap, C.byref(n), C.byref(mono))
     if rc != 0:
         raise RuntimeError(f"oracle_orb_extract rc={rc}")
     return kps[:n.value].copy(), desc[:n.value].copy(), mono.value
@@ -101,28 +103,30 @@ def pyramid(img: np.ndarray, p: OrbParams | None = None):
     return levels
 
 
-def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+def resize_linear(src: np.ndarray, dw: int, dh: int, simd: bool = False) -> np.ndarray:
     src = np.ascontiguousarray(src, dtype=np.uint8)
     sh, sw = src.shape
     dst = np.zeros((dh, dw), np.uint8)
-    lib().oracle_resize_linear(_u8p(src), sw, sh, C.c_size_t(sw), _u8p(dst), dw, dh)
+    fn = lib().oracle_resize_linear_simd if simd else lib().oracle_resize_linear
+    fn(_u8p(src), sw, sh, C.c_size_t(sw), _u8p(dst), dw, dh)
     return dst
 
 
-def fast(roi: np.ndarray, threshold: int) -> np.ndarray:
+def fast(roi: np.ndarray, threshold: int, simd: bool = False) -> np.ndarray:
     roi = np.ascontiguousarray(roi, dtype=np.uint8)
     rows, cols = roi.shape
     cap = rows * cols
     out = np.zeros(max(cap, 1), np.uint32)
-    n = lib().oracle_fast(_u8p(roi), cols, rows, C.c_size_t(cols), threshold, out.ctypes.data_as(C.c_void_p), cap)
+    fn = lib().oracle_fast_simd if simd else lib().oracle_fast
+    n = fn(_u8p(roi), cols, rows, C.c_size_t(cols), threshold, out.ctypes.data_as(C.c_void_p), cap)
     return out[:n].copy()
 
 
-def gaussian7(src: np.ndarray) -> np.ndarray:
+def gaussian7(src: np.ndarray, simd: bool = False) -> np.ndarray:
     src = np.ascontiguousarray(src, dtype=np.uint8)
     h, w = src.shape
     dst = np.zeros_like(src)
-    lib().oracle_gaussian7(_u8p(src), w, h, _u8p(dst))
+    (lib().oracle_gaussian7_simd if simd else lib().oracle_gaussian7)(_u8p(src), w, h, _u8p(dst))
     return dst
 
 

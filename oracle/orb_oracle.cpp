@@ -26,6 +26,16 @@
 #include <utility>
 #include <vector>
 
+// the AVX2 restatements of resize / blur / FAST (orb_simd.cpp): the second CPU-baseline column
+namespace oracle_simd {
+struct Kp {
+    float x, y, response;
+};
+void resize_vline(const int* r0, const int* r1, int b0, int b1, int xvec, int dw, uint8_t* D);
+void gaussian7(const uint8_t* src, int w, int h, size_t sstride, uint8_t* dst, size_t dstride);
+void fast16(const uint8_t* img, int cols, int rows, size_t step, int threshold, std::vector<Kp>& keypoints);
+}  // namespace oracle_simd
+
 namespace {
 
 // ---------------------------------------------------------------- OpenCV scalar helpers (App. A.5)
@@ -104,6 +114,9 @@ Tables makeTables(const mam_orb_params* p) {
 // OpenCV imgproc/resize.cpp: coefficient tables (hal::resize), HResizeLinear (exact int), VResizeLinear
 // with VResizeLinearVec_32s8u (SSE baseline: 16-lane loop, then 8-lane loop while x < w-8) and the
 // FixedPtCast<int,uchar,22> scalar tail.
+// the extractor's image primitives: the scalar restatement, or (g_simd: oracle_orb_extract_simd) the AVX2 one
+thread_local bool g_simd = false;
+
 void resizeLinear(const uint8_t* src, int sw, int sh, size_t sstride, uint8_t* dst, int dw, int dh, size_t dstride) {
     const int ONE = 2048;
     double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
@@ -156,6 +169,10 @@ void resizeLinear(const uint8_t* src, int sw, int sh, size_t sstride, uint8_t* d
         hresize(src + (size_t)clip(sy0 + 1) * sstride, r1.data());
         int b0 = ibeta[dy * 2], b1 = ibeta[dy * 2 + 1];
         uint8_t* D = dst + (size_t)dy * dstride;
+        if (g_simd) {
+            oracle_simd::resize_vline(r0.data(), r1.data(), b0, b1, xvec, dw, D);
+            continue;
+        }
         for (int x = 0; x < dw; x++) {
             if (x < xvec) {
                 int16_t h0 = sat16(r0[x] >> 4), h1 = sat16(r1[x] >> 4);
@@ -215,6 +232,17 @@ int cornerScore16(const uint8_t* ptr, const int pixel[], int threshold) {
 }
 
 void fast16(const uint8_t* img, int cols, int rows, size_t step, int threshold, std::vector<KeyPoint>& keypoints) {
+    if (g_simd) {
+        std::vector<oracle_simd::Kp> v;
+        oracle_simd::fast16(img, cols, rows, step, threshold, v);
+        keypoints.clear();
+        for (const auto& c : v) {
+            KeyPoint kp;
+            kp.x = c.x; kp.y = c.y; kp.size = 7.f; kp.angle = -1; kp.response = c.response;
+            keypoints.push_back(kp);
+        }
+        return;
+    }
     const int K = 8, N = 16 + K + 1;
     int i, j, k, pixel[25];
     makeOffsets(pixel, (int)step);
@@ -311,6 +339,10 @@ inline int refl101(int p, int n) {
 }
 
 void gaussian7(const uint8_t* src, int w, int h, size_t sstride, uint8_t* dst, size_t dstride) {
+    if (g_simd) {
+        oracle_simd::gaussian7(src, w, h, sstride, dst, dstride);
+        return;
+    }
     std::vector<uint32_t> hb((size_t)w * h);
     for (int y = 0; y < h; y++)
         for (int x = 0; x < w; x++) {
@@ -885,6 +917,32 @@ int oracle_orb_extract(const mam_orb_params* p, const uint8_t* img, int w, int h
     }
     *mono_out = monoIndex;
     return MAM_OK;
+}
+
+// the same with the AVX2 image primitives (byte-identical outputs)
+int oracle_orb_extract_simd(const mam_orb_params* p, const uint8_t* img, int w, int h, size_t stride, int lap0,
+                            int lap1, mam_keypoint* kps, uint8_t* desc, int capacity, int* n_out, int* mono_out) {
+    g_simd = true;
+    const int rc = oracle_orb_extract(p, img, w, h, stride, lap0, lap1, kps, desc, capacity, n_out, mono_out);
+    g_simd = false;
+    return rc;
+}
+void oracle_resize_linear_simd(const uint8_t* src, int sw, int sh, size_t sstride, uint8_t* dst, int dw, int dh) {
+    g_simd = true;
+    resizeLinear(src, sw, sh, sstride, dst, dw, dh, dw);
+    g_simd = false;
+}
+void oracle_gaussian7_simd(const uint8_t* src, int w, int h, uint8_t* dst) {
+    oracle_simd::gaussian7(src, w, h, w, dst, w);
+}
+int oracle_fast_simd(const uint8_t* roi, int cols, int rows, size_t stride, int threshold, uint32_t* out, int cap) {
+    g_simd = true;
+    std::vector<KeyPoint> kps;
+    fast16(roi, cols, rows, stride, threshold, kps);
+    g_simd = false;
+    int n = (int)kps.size();
+    for (int i = 0; i < n && i < cap; i++) out[i] = packKp(kps[i]);
+    return n;
 }
 
 }  // extern "C"

@@ -63,6 +63,15 @@ def test_oracle_reproduces_orb_golden(oracle):
         assert np.array_equal(d, z[f"desc{i}"]) and m == int(z[f"mono{i}"]), i
 
 
+def test_oracle_simd_reproduces_orb_golden(oracle):
+    """The CPU baseline's AVX2 column (oracle/orb_simd.cpp: resize, blur, FAST) gives the golden bytes too."""
+    z = _load("orb.npz")
+    for i in range(3):
+        k, d, m = oracle.extract(z[f"img{i}"], oracle.params(int(z[f"nfeat{i}"])), simd=True)
+        assert np.array_equal(k.view(np.uint8).reshape(-1, 28), z[f"kps{i}"]), i
+        assert np.array_equal(d, z[f"desc{i}"]) and m == int(z[f"mono{i}"]), i
+
+
 def test_oracle_reproduces_match_golden(oracle):
     from mam3slam_amd import scene
 

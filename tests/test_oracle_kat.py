@@ -497,3 +497,26 @@ def test_pinhole_kf_triangulation_oracle_equals_f12_entry(oracle):
     n1, o1 = oracle.search_for_triangulation_kf(KF1, KF2, pin, pin, True, False)
     n2, o2 = oracle.search_for_triangulation(KF1, KF2, F12, ep, True, False)
     assert n1 == n2 and np.array_equal(o1, o2) and n1 > 50
+
+
+def test_simd_primitives_equal_scalar(oracle):
+    """oracle/orb_simd.cpp (AVX2 resize vertical pass, 7x7 fixed-point blur, FAST 9/16 with the run-length counters)
+    byte- / keypoint-identical to the scalar restatement on random and synthetic images, odd sizes and borders
+    included; the whole extractor on synthetic frames of the bench shapes."""
+    from mam3slam_amd import synth
+
+    rng = np.random.default_rng(5)
+    imgs = [rng.integers(0, 256, (h, w), dtype=np.uint8) for h, w in ((7, 7), (9, 40), (37, 53), (120, 161))]
+    imgs += [synth.make_frame(640, 480, agent=3, frame=1), synth.make_frame(333, 251, agent=4, frame=2)]
+    for im in imgs:
+        h, w = im.shape
+        for dw, dh in ((round(w / 1.2), round(h / 1.2)), (max(1, w // 2), max(1, h // 2)), (w + 13, h + 5)):
+            assert np.array_equal(oracle.resize_linear(im, dw, dh, simd=True), oracle.resize_linear(im, dw, dh))
+        assert np.array_equal(oracle.gaussian7(im, simd=True), oracle.gaussian7(im))
+        for th in (7, 20, 0, 60):
+            assert np.array_equal(oracle.fast(im, th, simd=True), oracle.fast(im, th)), (im.shape, th)
+    for (w, h, nf) in ((640, 480, 1000), (1280, 720, 2000)):
+        img = synth.make_frame(w, h, agent=1, frame=2)
+        k1, d1, m1 = oracle.extract(img, oracle.params(nf))
+        k2, d2, m2 = oracle.extract(img, oracle.params(nf), simd=True)
+        assert np.array_equal(k1.view(np.uint8), k2.view(np.uint8)) and np.array_equal(d1, d2) and m1 == m2
