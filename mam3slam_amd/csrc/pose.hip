@@ -419,28 +419,16 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
     double lambda = 0.0, ni = 2.0;
     int nBad = 0, its = 0;
     bool ok = true;
-    // Each trial pass is a full buildSystem at the trial pose (errors, robust chi2 AND the quadratic form): when the
-    // trial is accepted, the next iteration's linearisation at that pose is the one just computed (the same errors,
-    // weights and sums), so an iteration costs one edge pass instead of two. Two LDS buffers: red = the system at T,
-    // spec = the last trial's.
-    double* red = scr + NW * (NRED + 1) + 8;   // H upper, b, chi (LDS)
-    double* spec = red + NRED + 1;
-    bool have = false;                        // red already holds the system at T (the accepted trial's)
     for (int it = 0; it < 10 && ok; it++) {
+        double* red = scr + NW * (NRED + 1) + 8;   // H upper, b, chi (LDS)
 #ifdef MAM_POSE_PROFILE
         long long tp = clock64();
 #endif
-        double currentChi;
-        if (have) {
-            currentChi = red[NRED];
-        } else {
-            currentChi = build_system<KB8>(E, T, c, robust, delta, scr, red);
-#ifdef MAM_POSE_PROFILE
-            if (threadIdx.x == 0) atomicAdd(&g_pprof[6], 1ull);
-#endif
-        }
-        have = false;
+        double currentChi = build_system<KB8>(E, T, c, robust, delta, scr, red);
         PPROF(0, tp);
+#ifdef MAM_POSE_PROFILE
+        if (threadIdx.x == 0) atomicAdd(&g_pprof[6], 1ull);
+#endif
         const double iniChi = currentChi;
         if (it == 0) {
             double md = 0.0;
@@ -489,7 +477,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
                 se3::exp_mul(x, T, Tn);
                 PPROF(2, tp);
             }
-            double tempChi = build_system<KB8>(E, Tn, c, robust, delta, scr, spec);
+            double tempChi = active_chi<KB8>(E, Tn, c, robust, delta, scr);
             PPROF(3, tp);
 #ifdef MAM_POSE_PROFILE
             if (threadIdx.x == 0) atomicAdd(&g_pprof[5], 1ull);
@@ -507,10 +495,6 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
                 ni = 2;
                 currentChi = tempChi;
                 for (int k = 0; k < 7; k++) T[k] = Tn[k];
-                double* tmp = red;   // the trial's system is the system at the new T
-                red = spec;
-                spec = tmp;
-                have = true;
             } else {
                 lambda *= ni;
                 ni *= 2;
@@ -534,7 +518,7 @@ template <bool KB8>
 __global__ __launch_bounds__(Cfg<KB8>::PT) void k_pose_opt(Args a) {
     constexpr int PT = Cfg<KB8>::PT, NW = Cfg<KB8>::NW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ double scr[NW * (NRED + 1) + 8 + 2 * (NRED + 1)];   // wave partials | chi sum | 2 x (H, b, chi sums)
+    __shared__ double scr[NW * (NRED + 1) + 8 + NRED + 1];   // wave partials | chi sum | H, b, chi sums
     __shared__ int s_nbad;
     const int f = blockIdx.x, t = threadIdx.x;
     const int n = a.n_edges[f];
