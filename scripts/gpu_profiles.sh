@@ -17,7 +17,7 @@ RND=${1:?round}
 PART=${2:?part}
 mkdir -p $O
 cd $R
-export GPU_MAX_HW_QUEUES=16
+# (the box default GPU_MAX_HW_QUEUES, as the driver runs bench.py)
 case $PART in
 lba)
   timeout -k 10 300 python scripts/lba_bench.py --world --batch 32 --oracle > $O/lba_bench.json 2> $O/lba_bench.err || { tail -5 $O/lba_bench.err; exit 1; }

@@ -176,3 +176,47 @@ def test_lba_arena_reuse(solver, oracle):
         assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials)
         assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
         assert _rel(rg.pose_t, ro.pose_t) <= 1e-4
+
+
+@pytest.mark.parametrize("n_opt", [200])
+def test_lba_map_scale(solver, oracle, n_opt):
+    """Map scale (the welding / global BA the reference runs over hundreds of keyframes — its own run
+    reaches 478, output/KF_traj.txt): a 200-keyframe graph of the shared synthetic map (all its keyframes optimised
+    but the map's first) solved by the same device LM — S is 1200 x 1200, beyond the LDS tile pool (40 tile columns),
+    so the factorization takes the HBM form — against the oracle on the same graph; the time is printed."""
+    import time
+
+    from mam3slam_amd import world as W
+
+    wd = W.make_world(n_kf=n_opt + 60, seed=21)
+    prob = W.window(wd, 0, n_opt=n_opt)[0]
+    assert int((np.asarray(prob.pose_fixed) == 0).sum()) >= n_opt - 1
+    solver.solve(prob)   # warm (allocations)
+    t0 = time.perf_counter()
+    rg = solver.solve(prob)
+    ms = (time.perf_counter() - t0) * 1e3
+    ro = oracle.lba_solve(prob)
+    print(f"\nmap-scale LBA: {n_opt} KF, {len(prob.point_id)} MP, {len(prob.edge_point)} edges: {ms:.1f} ms on the GPU, "
+          f"{rg.iterations} iterations / {rg.lm_trials} trials")
+    assert rg.status == 0 and ro.status == 0
+    assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials)
+    assert abs(rg.final_chi2 - ro.final_chi2) <= 1e-6 * ro.final_chi2 and ro.final_chi2 < ro.initial_chi2
+    assert _rel(rg.pose_t, ro.pose_t) <= 1e-4 and _rel(rg.pose_q, ro.pose_q) <= 1e-4
+    assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
+
+
+def test_lba_map_scale_478(solver):
+    """The reference run's map size (478 keyframes, output/KF_traj.txt) on the device alone (S 2868 x 2868; the
+    oracle's dense factorization would take minutes on one core): solved without a capacity error, chi2 reduced."""
+    import time
+
+    from mam3slam_amd import world as W
+
+    wd = W.make_world(n_kf=540, seed=22)
+    prob = W.window(wd, 0, n_opt=478)[0]
+    t0 = time.perf_counter()
+    rg = solver.solve(prob)
+    ms = (time.perf_counter() - t0) * 1e3
+    print(f"\nmap-scale LBA: 478 KF, {len(prob.point_id)} MP, {len(prob.edge_point)} edges: {ms:.1f} ms on the GPU, "
+          f"{rg.iterations} iterations / {rg.lm_trials} trials")
+    assert rg.status == 0 and rg.final_chi2 < rg.initial_chi2
