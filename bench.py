@@ -56,7 +56,9 @@ CONFIGS = {
     # BASELINE.json configs[4]: 8 synthetic mono agents at 1280x720 / 2000 features, shared-map local BA, one agent
     # per GPU at --gpus 8 (all 8 on one GPU at --gpus 1); neighbouring agents' LBA windows overlap (keyframes and
     # MapPoints of the merged map), so the exchange resolves cross-GPU write conflicts in GPU order
-    "c4": dict(width=1280, height=720, nfeatures=2000, lba=True, agents=8),
+    # (pool_frames: 9 sets of the 8 agents' frames — coprime with the keyframe cadence, so the keyframes the ring
+    # holds are 72 different views: no identical keyframes in CreateNewMapPoints' neighbourhoods)
+    "c4": dict(width=1280, height=720, nfeatures=2000, lba=True, agents=8, pool_frames=72),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFS = 78.6    # MI355X FP64 vector / matrix (spec)
@@ -896,11 +898,13 @@ def main():
         # LocalBundleAdjustment windows after them and the queued pack / all-gather / apply of their write-backs: the
         # run's span on the LocalMapping stream, from events recorded around it (the exchange tail included)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t_m = time.perf_counter()
         e0.record(mapping.stream)
         newmp.wait(mapping.stream, head)
         mapping.run(step_idx)
         e1.record(mapping.stream)
         lba_ev.append((e0, e1))
+        host_s["mapping_run"] += time.perf_counter() - t_m
 
     def lba_ms():
         torch.cuda.synchronize(dev)
@@ -936,7 +940,10 @@ def main():
         if failure:
             raise failure[0]
 
+    host_s = {"queue_wait": 0.0, "tracking_launch": 0.0, "keyframe_ingest_launch": 0.0, "mapping_run": 0.0}
+
     def step():
+        t_a = time.perf_counter()
         if mapping is not None and step_no[0] % map_every == 0:
             if worker[0] is None:
                 worker[0] = threading.Thread(target=mapping_loop, daemon=True)
@@ -944,10 +951,16 @@ def main():
             if failure:
                 raise failure[0]
             runs.put((step_no[0] // map_every, newmp.take()))
+        t_b = time.perf_counter()
         tr.step()
+        t_c = time.perf_counter()
         if mapping is not None and (step_no[0] + 1) % map_every == 0:
             newmp.ingest(step_no[0])
             newmp.launch(newmp.pending)
+        t_d = time.perf_counter()
+        host_s["queue_wait"] += t_b - t_a
+        host_s["tracking_launch"] += t_c - t_b
+        host_s["keyframe_ingest_launch"] += t_d - t_c
         step_no[0] += 1
 
     for _ in range(args.warmup):
@@ -978,6 +991,8 @@ def main():
         newmp.voc.set_profiling(on)
 
     lba_ev.clear()
+    for k in host_s:
+        host_s[k] = 0.0
     if mapping is not None and args.profile_timed:
         set_profiling(True)
     if world > 1:
@@ -991,6 +1006,9 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # host time per timed step by phase (the main thread: queue wait, the tracking graph launch, the keyframe ingest +
+    # search launch; the LocalMapping thread: its run) — where a host-bound step would show
+    host_ms = {k: v * 1e3 / args.steps for k, v in host_s.items()}
     lba_stage = None
     tri_stage = None
     if mapping is not None and not args.profile_timed:
@@ -1145,6 +1163,7 @@ def main():
             out["ingest"] = ingest
         if overlap is not None:
             out["overlap"] = overlap
+        out["host_ms_per_step"] = host_ms
         if mapping is not None:
             its = [s[0] for s in mapping.stats]
             trials = [s[1] for s in mapping.stats]
