@@ -993,6 +993,8 @@ def main():
     lba_ev.clear()
     for k in host_s:
         host_s[k] = 0.0
+    if mapping is not None:
+        mapping.host_s = {}
     if mapping is not None and args.profile_timed:
         set_profiling(True)
     if world > 1:
@@ -1009,6 +1011,8 @@ def main():
     # host time per timed step by phase (the main thread: queue wait, the tracking graph launch, the keyframe ingest +
     # search launch; the LocalMapping thread: its run) — where a host-bound step would show
     host_ms = {k: v * 1e3 / args.steps for k, v in host_s.items()}
+    if mapping is not None:
+        host_ms.update({"mapping_" + k: v * 1e3 / args.steps for k, v in mapping.host_s.items()})
     lba_stage = None
     tri_stage = None
     if mapping is not None and not args.profile_timed:

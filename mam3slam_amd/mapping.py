@@ -122,6 +122,7 @@ class LocalMappingLeg:
         self.new_mp_win = torch.from_numpy(np.concatenate([np.full(len(h), w) for w, h in enumerate(homes)])).to(device)
         self.stats = None
         self.windows_solved = 0
+        self.host_s = {}
 
     @property
     def edges(self):
@@ -142,17 +143,22 @@ class LocalMappingLeg:
         """One LocalMapping step: the solves are synchronous (mam_lba_solve_batch_device returns with the Levenberg
         state read back), the pack / all-gather / apply are queued: on return the map tables are final for work
         ordered after self.stream (a consumer on another stream waits on it)."""
+        import time
+
         import torch
 
         with torch.cuda.stream(self.stream):
+            t0 = time.perf_counter()
             s = self.stream.cuda_stream
             if new_keyframes:
                 self.new_keyframes(step)
             self.exch.read_windows(self.kf_table.data_ptr(), self.world.n_kf, self.mp_table.data_ptr(), self.world.n_mp,
                                    self.mp_base, self.d_read.data_ptr(), self.W, self.max_rows,
                                    self.status.data_ptr(), stream=s)
+            t1 = time.perf_counter()
             check = self.solver._L.mam_lba_solve_batch_device(self.solver._ctx, self.W, C.byref(self.c_probs),
                                                                C.byref(self.c_res), C.c_void_p(s))
+            t2 = time.perf_counter()
             if check != 0:
                 raise RuntimeError(f"mam_lba_solve_batch_device: {check}")
             self.stats = [(int(r.iterations), int(r.lm_trials), int(r.status)) for r in self.c_res]
@@ -162,6 +168,11 @@ class LocalMappingLeg:
             self.exch.gather(timed=self.time_gather)
             self.exch.apply(self.kf_table.data_ptr(), self.world.n_kf, self.mp_table.data_ptr(), self.world.n_mp,
                             self.status.data_ptr(), stream=s)
+            t3 = time.perf_counter()
+        # host wall per phase (the solve returns after its last read-back: it includes the GPU time of everything
+        # queued before it on the stream — the keyframe searches it waits for)
+        for k, v in (("launch", t1 - t0), ("solve", t2 - t1), ("exchange", t3 - t2)):
+            self.host_s[k] = self.host_s.get(k, 0.0) + v
         return self.stats
 
     def window_inputs(self, w: int):
