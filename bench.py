@@ -1208,7 +1208,8 @@ def main():
             ms_solve, n_solve = lba_stage["solve"]
             tr_mean = float(np.mean(trials[:len(g0)]))
             ach = args.steps * tr_mean * sum(fl_ldlt) / (ms_solve * 1e-3) / 1e12 if ms_solve else None
-            mpath = os.path.join(ROOT, "profiles", "r03", "lba_mfma_f64.json")
+            mrel = "profiles/r04/lba_mfma_f64.json"
+            mpath = os.path.join(ROOT, mrel)
             mfma = None
             if os.path.exists(mpath):
                 try:
@@ -1222,10 +1223,12 @@ def main():
                 "frac_of_cus_used": ach / (FP64_PEAK_TFS * len(g0) / 256.0) if ach else None,
                 "flop_per_factorization": float(np.mean(fl_ldlt)), "windows_per_launch": len(g0),
                 "avg_launch_ms": ms_solve / max(n_solve, 1), "launches": n_solve,
-                "mfma_counters": mfma, "mfma_counters_file": "profiles/r03/lba_mfma_f64.json" if mfma else None,
-                "limiter": ("latency: one workgroup per window factors a 19-panel chain; per panel the diagonal "
-                            "tile's 16-step LDL^T + inverse runs on one wave (DPP-broadcast FP64 FMAs, ~6k cycles) "
-                            "between two barriers, the MFMA tile products beside it"),
+                "mfma_counters": mfma, "mfma_counters_file": mrel if mfma else None,
+                "limiter": ("latency: one workgroup per window factors the tile pattern as a dataflow of per-tile and "
+                            "per-panel tasks (two chains of 6-9 block columns + the separator's 3-4 under the split "
+                            "pose order); per column ~6.4k cycles: the critical tile update (4 FP64 MFMAs + operand "
+                            "loads) ~1.5k, the tall panel's 16 dependent pivot steps ~2.3k, stores + flag ~1.2k "
+                            "(scripts/gpu_ldlt_trace.sh)"),
                 "note": "algorithmic = tile-skipping LDL^T + solves (ldlt_tile_flops); frac_of_cus_used prices "
                         "against the FP64 MFMA peak of the CUs the launch's workgroups occupy (one per window)"}
         if newmp is not None:
