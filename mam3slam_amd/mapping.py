@@ -132,12 +132,15 @@ class LocalMappingLeg:
         """Enter every window's new keyframe and its new MapPoints at a perturbed state (deterministic in step)."""
         # one HIP launch (mam_map_perturb): q + N(0, 0.004) renormalised with w >= 0, t + N(0, 0.012), new MapPoints +
         # N(0, 0.017), counter-based normals seeded by (step, rank)
+        import torch
+
         from .exchange import map_perturb
 
+        # on torch's current stream (run() makes it self.stream): ordered with the caller's tensor reads
         map_perturb(self.kf_table.data_ptr(), self.world.n_kf, self.new_kf.data_ptr(), len(self.new_kf),
                     self.mp_table.data_ptr(), self.world.n_mp, self.new_mp.data_ptr(), len(self.new_mp),
                     1_000_003 * (step + 1) + 7919 * self.rank, 0.004, 0.012, 0.017, self.status.data_ptr(),
-                    stream=self.stream.cuda_stream)
+                    stream=torch.cuda.current_stream(self.dev).cuda_stream)
 
     def run(self, step: int, new_keyframes: bool = True):
         """One LocalMapping step: the solves are synchronous (mam_lba_solve_batch_device returns with the Levenberg
