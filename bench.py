@@ -570,6 +570,44 @@ def ingest_section(tr, reps=5):
             "d2h_bytes_per_step": int(bo), "h2d_GBs": bi / (m_in * 1e-3) / 1e9, "d2h_GBs": bo / (m_out * 1e-3) / 1e9}
 
 
+def ring_lba_section(newmp, check=True):
+    """LocalBundleAdjustment over the keyframes this run's Tracking inserted (mapping.RingLBA): the last keyframe
+    run's windows — each new keyframe with its 30 ring neighbours (20 optimised, 10 fixed), its keypoints' MapPoints
+    and their observations from the run's forward Fuse matches — assembled on the device and solved by the batch
+    device API; with check, window 0 against the oracle on the same graph. Outside the timed region: the timed
+    LocalMapping leg solves the shared synthetic map's windows, whose write-backs the exchange carries."""
+    import torch
+
+    from mam3slam_amd.mapping import RingLBA
+
+    rl = RingLBA(newmp)
+    torch.cuda.synchronize()
+    rl.assemble(newmp.stream)
+    rl.solve(newmp.stream)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        rl.assemble(newmp.stream)
+        rl.solve(newmp.stream)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    prob = rl.window(0)
+    act = prob.edge_active.reshape(-1, rl.NV)
+    _, _, _, its, trials, st, ic, fc = rl.result(0)
+    res = {"windows": newmp.W, "poses": rl.NV, "optimised_poses": rl.NV - rl.n_fixed,
+           "points_observed": int((act.sum(1) > 0).sum()), "observations": int(act.sum()),
+           "ms_per_batch": ms, "iterations": its, "trials": trials, "status": st, "chi2": [ic, fc]}
+    if check:
+        from oracle import oracle_py
+
+        ro = oracle_py.lba_solve(prob)
+        q, t, x = rl.result(0)[:3]
+        rel = float(np.abs(x - ro.point_xyz).max() / max(np.abs(ro.point_xyz).max(), 1e-12))
+        res["oracle_same_control_flow"] = (its, trials) == (ro.iterations, ro.lm_trials)
+        res["oracle_max_point_rel_diff"] = rel
+    return res
+
+
 def parity_section(tr, mapping, newmp=None):
     """In-run parity against the oracle, stage by stage on each stage's own inputs from the timed region: one frame's
     extraction; its TrackWithMotionModel (motion search, PoseOptimization, outlier discard) and TrackLocalMap
@@ -1074,6 +1112,7 @@ def main():
 
         sin_info = fuse_bench.run(args.config, reps=max(args.steps, 5), device=dev.index or 0,
                                   oracle=not args.no_cpu_baseline and rank == 0)
+    ring = ring_lba_section(newmp) if newmp is not None and rank == 0 else None
     parity = parity_section(tr, mapping, newmp) if rank == 0 else None
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
@@ -1168,6 +1207,11 @@ def main():
         if overlap is not None:
             out["overlap"] = overlap
         out["host_ms_per_step"] = host_ms
+        if ring is not None:
+            out["ring_lba"] = ring
+            if parity is not None:
+                parity["ring_lba_same_control_flow"] = ring.get("oracle_same_control_flow")
+                parity["ring_lba_max_point_rel_diff"] = ring.get("oracle_max_point_rel_diff")
         if mapping is not None:
             its = [s[0] for s in mapping.stats]
             trials = [s[1] for s in mapping.stats]
@@ -1263,7 +1307,7 @@ def main():
             out["parity"] = parity
             # every exactness flag must hold and every float difference stay inside the north star's 1e-4
             bad = [k for k, v in parity.items() if isinstance(v, bool) and not v]
-            bad += [k for k in ("lba_max_point_rel_diff", "pose_optimization_max_rel_diff")
+            bad += [k for k in ("lba_max_point_rel_diff", "pose_optimization_max_rel_diff", "ring_lba_max_point_rel_diff")
                     if parity.get(k) is not None and not parity[k] <= 1e-4]
             out["parity_ok"] = not bad
             if bad:

@@ -112,6 +112,32 @@ int mam_map_perturb(float* kf_table, int64_t kf_rows, const int64_t* kf_idx, int
                     int64_t mp_rows, const int64_t* mp_idx, int n_mp, uint64_t seed, float sigma_q, float sigma_t,
                     float sigma_x, int32_t* status, void* stream);
 
+/* ---- LocalBundleAdjustment windows from the keyframes Tracking inserted (Optimizer.cc:1118-1331 on the device
+ * keyframe ring of the harness): window w = keyframe pairs[w nn][0] (pose 0, optimised) and its nn neighbours
+ * pairs[w nn + k][1] (poses 1 .. nn, nearest first; the last n_fixed of them fixed), its MapPoints = its keypoints'
+ * scene points (mps[kf][p], p < its keypoint count), and per MapPoint the observations: its own keypoint and the
+ * neighbours' keypoints match[(w nn + k) S + p] (Fuse's forward matches: the keypoint of neighbour k the MapPoint
+ * projects onto, -1 none). Fixed problem shape: S points x (nn + 1) edge slots per point, edge e = p (nn + 1) + v on
+ * pose v, inactive (edge_active 0) where there is no observation and for every edge of a MapPoint with fewer than two
+ * observations (a 3-DoF point needs two views); obs = the keypoint (x, y), inv_sigma2 = inv_level_sigma2[octave].
+ * Estimates: the keyframes' tracked Tcw and the MapPoints' positions, float cast to double. DEVICE arrays throughout
+ * (outs: a device array of n_windows descriptors); inv_level_sigma2: host, nlevels <= 8. Asynchronous. */
+typedef struct mam_ring_window {
+    double* pose_q;                      /* [nn + 1][4] */
+    double* pose_t;                      /* [nn + 1][3] */
+    uint8_t* pose_fixed;                 /* [nn + 1] */
+    double* point_xyz;                   /* [S][3] */
+    int32_t* edge_point;                 /* [S (nn + 1)] */
+    int32_t* edge_pose;
+    double* edge_obs;                    /* [S (nn + 1)][2] */
+    double* edge_inv_sigma2;
+    uint8_t* edge_active;
+} mam_ring_window;
+
+int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn, int n_fixed, const void* keys, const int32_t* cnt,
+                         const void* tcw, const void* mps, int S, const int32_t* match, const float* inv_level_sigma2,
+                         int nlevels, const mam_ring_window* outs, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

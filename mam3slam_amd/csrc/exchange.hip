@@ -208,7 +208,101 @@ __global__ __launch_bounds__(256) void k_perturb(float* __restrict__ kf, int64_t
     }
 }
 
+// ---- LBA windows from the keyframe ring: grid (ceil(S / 64), n_windows) x 64, one thread per MapPoint (its nn + 1
+// edge slots, the poses by the first threads of each window)
+struct RingArgs {
+    const int32_t* pairs;
+    int nn, n_fixed, S, nlevels;
+    const mam_keypoint* keys;
+    const int32_t* cnt;
+    const float* tcw;    // [R][7]: q xyzw, t
+    const float* mps;    // [R][S][20] (mam_fuse_mp: pos first)
+    const int32_t* match;
+    float inv_s2[8];
+    const mam_ring_window* outs;
+};
+
+__global__ __launch_bounds__(64) void k_ring_windows(const RingArgs a) {
+    const int w = blockIdx.y, p = blockIdx.x * 64 + threadIdx.x;
+    const mam_ring_window& o = a.outs[w];
+    const int NV = a.nn + 1;
+    const int j = a.pairs[2 * (w * a.nn)];
+    if (p < NV) {
+        const int slot = p == 0 ? j : a.pairs[2 * (w * a.nn + p - 1) + 1];
+        const float* T = a.tcw + 7 * (size_t)slot;
+        for (int k = 0; k < 4; k++) o.pose_q[4 * p + k] = (double)T[k];
+        for (int k = 0; k < 3; k++) o.pose_t[3 * p + k] = (double)T[4 + k];
+        o.pose_fixed[p] = p >= NV - a.n_fixed ? 1 : 0;
+    }
+    if (p >= a.S) return;
+    const int n = min(max(a.cnt[2 * j], 0), a.S);
+    const bool valid = p < n;
+    const float* M = a.mps + ((size_t)j * a.S + p) * 20;
+    for (int k = 0; k < 3; k++) o.point_xyz[3 * (size_t)p + k] = valid ? (double)M[k] : 0.0;
+    // the observations: count first (a MapPoint seen by fewer than two keyframes is left out), then the slots
+    int nobs = valid ? 1 : 0;
+    if (valid)
+        for (int k = 0; k < a.nn; k++) {
+            const int nb = a.pairs[2 * (w * a.nn + k) + 1];
+            const int idx = a.match[(size_t)(w * a.nn + k) * a.S + p];
+            nobs += (idx >= 0 && idx < min(a.cnt[2 * nb], a.S)) ? 1 : 0;
+        }
+    const bool keep = nobs >= 2;
+    for (int v = 0; v < NV; v++) {
+        const size_t e = (size_t)p * NV + v;
+        int slot = j, idx = p;
+        if (v > 0) {
+            slot = a.pairs[2 * (w * a.nn + v - 1) + 1];
+            idx = valid ? a.match[(size_t)(w * a.nn + v - 1) * a.S + p] : -1;
+            if (idx >= min(a.cnt[2 * slot], a.S)) idx = -1;
+        } else if (!valid) {
+            idx = -1;
+        }
+        const bool act = keep && idx >= 0;
+        o.edge_point[e] = p;
+        o.edge_pose[e] = v;
+        o.edge_active[e] = act ? 1 : 0;
+        if (act) {
+            const mam_keypoint& kp = a.keys[(size_t)slot * a.S + idx];
+            o.edge_obs[2 * e] = (double)kp.x;
+            o.edge_obs[2 * e + 1] = (double)kp.y;
+            o.edge_inv_sigma2[e] = (double)a.inv_s2[min(max(kp.octave, 0), a.nlevels - 1)];
+        } else {
+            o.edge_obs[2 * e] = 0.0;
+            o.edge_obs[2 * e + 1] = 0.0;
+            o.edge_inv_sigma2[e] = 1.0;
+        }
+    }
+}
+
 }  // namespace mam
+
+extern "C" int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn, int n_fixed, const void* keys,
+                                    const int32_t* cnt, const void* tcw, const void* mps, int S, const int32_t* match,
+                                    const float* inv_level_sigma2, int nlevels, const mam_ring_window* outs,
+                                    void* stream) {
+    if (n_windows < 0 || nn < 1 || n_fixed < 0 || n_fixed > nn || S < 1 || nlevels < 1 || nlevels > 8 || !pairs ||
+        !keys || !cnt || !tcw || !mps || !match || !inv_level_sigma2 || (n_windows > 0 && !outs))
+        return MAM_ERR_ARG;
+    if (n_windows == 0) return MAM_OK;
+    mam::RingArgs a{};
+    a.pairs = pairs;
+    a.nn = nn;
+    a.n_fixed = n_fixed;
+    a.S = S;
+    a.nlevels = nlevels;
+    a.keys = reinterpret_cast<const mam_keypoint*>(keys);
+    a.cnt = cnt;
+    a.tcw = reinterpret_cast<const float*>(tcw);
+    a.mps = reinterpret_cast<const float*>(mps);
+    a.match = match;
+    for (int l = 0; l < nlevels; l++) a.inv_s2[l] = inv_level_sigma2[l];
+    a.outs = outs;
+    const int np = std::max(S, nn + 1);
+    hipLaunchKernelGGL(mam::k_ring_windows, dim3((np + 63) / 64, n_windows), dim3(64), 0, (hipStream_t)stream, a);
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
 
 extern "C" int mam_copy_rows(int n_tables, const mam_row_table* tables, int n, const int32_t* src_rows,
                              const int32_t* dst_rows, const int32_t* flag_a, const int32_t* flag_b, int64_t flag_stride,

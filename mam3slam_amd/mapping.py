@@ -513,3 +513,102 @@ class NewMapPointsLeg:
             F.pose = (t[:4].copy(), t[4:7].copy())
             out.append(F)
         return out
+
+
+class RingWindow(C.Structure):
+    """mam_ring_window: one assembled window's device arrays."""
+    _fields_ = [("pose_q", C.c_void_p), ("pose_t", C.c_void_p), ("pose_fixed", C.c_void_p), ("point_xyz", C.c_void_p),
+                ("edge_point", C.c_void_p), ("edge_pose", C.c_void_p), ("edge_obs", C.c_void_p),
+                ("edge_inv_sigma2", C.c_void_p), ("edge_active", C.c_void_p)]
+
+
+class RingLBA:
+    """LocalBundleAdjustment over the keyframes Tracking inserted (Optimizer.cc:1118-1331 on the NewMapPointsLeg ring):
+    per new keyframe of the last run, the window of the keyframe and its NN neighbours (the nearest NN - n_fixed
+    optimised, the rest fixed), its keypoints' MapPoints and their observations by the neighbours from the run's
+    forward Fuse matches (mam_ring_lba_windows, on the leg's stream right after the run), solved with the batch device
+    API (mam_lba_solve_batch_device). Fixed problem shape: S MapPoint slots x (NN + 1) edge slots, unobserved slots
+    inactive."""
+
+    def __init__(self, nm, n_fixed: int = 10, iterations: int = 10, solver=None):
+        import torch
+
+        from .lba import HUBER_MONO
+
+        self.nm, self.dev = nm, nm.dev
+        W, NN, S = nm.W, nm.NN, nm.S
+        self.NV, self.n_fixed = NN + 1, int(n_fixed)
+        NV, E = self.NV, S * (NN + 1)
+        z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=self.dev)  # noqa: E731
+        self.bufs = []
+        wins = (RingWindow * W)()
+        self.c_probs = (_Problem * W)()
+        self.c_res = (_Result * W)()
+        cam = nm.tr.cam
+        self.cams = torch.from_numpy(np.ascontiguousarray(cam.params(), np.float32)[None]).to(self.dev)
+        for w in range(W):
+            b = dict(pose_q=z((NV, 4), torch.float64), pose_t=z((NV, 3), torch.float64), pose_fixed=z(NV, torch.uint8),
+                     point_xyz=z((S, 3), torch.float64), edge_point=z(E, torch.int32), edge_pose=z(E, torch.int32),
+                     edge_obs=z((E, 2), torch.float64), edge_inv_sigma2=z(E, torch.float64),
+                     edge_active=z(E, torch.uint8), out_q=z((NV, 4), torch.float64), out_t=z((NV, 3), torch.float64),
+                     out_xyz=z((S, 3), torch.float64), out_chi2=z(E, torch.float64), out_depth=z(E, torch.uint8))
+            self.bufs.append(b)
+            for f in RingWindow._fields_:
+                setattr(wins[w], f[0], b[f[0]].data_ptr())
+            P = self.c_probs[w]
+            P.n_poses, P.n_points, P.n_edges, P.n_cams = NV, S, E, 1
+            P.pose_id = P.point_id = P.pose_cam = None
+            P.pose_fixed, P.pose_q, P.pose_t = b["pose_fixed"].data_ptr(), b["pose_q"].data_ptr(), b["pose_t"].data_ptr()
+            P.point_xyz = b["point_xyz"].data_ptr()
+            P.edge_point, P.edge_pose = b["edge_point"].data_ptr(), b["edge_pose"].data_ptr()
+            P.edge_obs, P.edge_inv_sigma2 = b["edge_obs"].data_ptr(), b["edge_inv_sigma2"].data_ptr()
+            P.edge_active, P.cams = b["edge_active"].data_ptr(), self.cams.data_ptr()
+            P.huber_delta, P.iterations = HUBER_MONO, int(iterations)
+            P.cam_model = 1 if cam.is_kb8 else 0
+            P.n_opt_poses = NV - self.n_fixed
+            R = self.c_res[w]
+            R.pose_q, R.pose_t, R.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
+            R.edge_chi2, R.edge_depth_ok = b["out_chi2"].data_ptr(), b["out_depth"].data_ptr()
+        self.d_wins = torch.from_numpy(np.frombuffer(bytes(wins), np.uint8).copy()).to(self.dev)
+        s2 = np.asarray(nm.tr.F0.level_sigma2, np.float32)
+        self.inv_s2 = (C.c_float * len(s2))(*[float(np.float32(1.0) / x) for x in s2])
+        self.nlevels = len(s2)
+        self.solver = solver or LBASolver(device=self.dev.index or 0)
+        self.stats = None
+
+    def assemble(self, stream):
+        """The windows of the keyframes of the leg's last run (after its search_in_neighbors on `stream`)."""
+        from ._lib import check
+        from .exchange import _bind
+
+        nm = self.nm
+        check(_bind().mam_ring_lba_windows(nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.n_fixed, nm.keys.data_ptr(), nm.cnt.data_ptr(),
+                 nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2, self.nlevels,
+                 self.d_wins.data_ptr(), stream.cuda_stream), "mam_ring_lba_windows")
+
+    def solve(self, stream):
+        rc = self.solver._L.mam_lba_solve_batch_device(self.solver._ctx, self.nm.W, C.byref(self.c_probs),
+                                                       C.byref(self.c_res), C.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"mam_lba_solve_batch_device: {rc}")
+        self.stats = [(int(r.iterations), int(r.lm_trials), int(r.status)) for r in self.c_res]
+        return self.stats
+
+    def window(self, w: int):
+        """Host LBAProblem of window w as assembled (ids = array order)."""
+        from .lba import HUBER_MONO, LBAProblem
+
+        b = {k: v.cpu().numpy() for k, v in self.bufs[w].items()}
+        S = self.nm.S
+        return LBAProblem(pose_id=np.arange(self.NV, dtype=np.int64), pose_fixed=b["pose_fixed"], pose_q=b["pose_q"],
+                          pose_t=b["pose_t"], point_id=np.arange(S, dtype=np.int64) + self.NV,
+                          point_xyz=b["point_xyz"], edge_point=b["edge_point"], edge_pose=b["edge_pose"],
+                          edge_obs=b["edge_obs"], edge_inv_sigma2=b["edge_inv_sigma2"],
+                          cams=self.cams.cpu().numpy(), huber_delta=HUBER_MONO, iterations=int(self.c_probs[w].iterations),
+                          edge_active=b["edge_active"], cam_model=int(self.c_probs[w].cam_model)).contiguous()
+
+    def result(self, w: int):
+        b = self.bufs[w]
+        r = self.c_res[w]
+        return (b["out_q"].cpu().numpy(), b["out_t"].cpu().numpy(), b["out_xyz"].cpu().numpy(), int(r.iterations),
+                int(r.lm_trials), int(r.status), float(r.initial_chi2), float(r.final_chi2))
