@@ -329,17 +329,20 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
 #pragma unroll
         for (int i = k + 1; i < 6; i++)
             if (fabs(m[7 * i]) > bv) { bv = fabs(m[7 * i]); big = i; }
+        // the pivot is the same in every lane (the matrix is): a scalar branch takes the one exchange needed instead
+        // of predicated swaps over every candidate
+        big = __builtin_amdgcn_readfirstlane(big);
         tr[k] = big;
 #pragma unroll
         for (int b = k + 1; b < 6; b++) {
-            const bool c = big == b;
+            if (big != b) continue;
 #pragma unroll
-            for (int j = 0; j < k; j++) cswap(c, m[6 * k + j], m[6 * b + j]);
+            for (int j = 0; j < k; j++) cswap(true, m[6 * k + j], m[6 * b + j]);
 #pragma unroll
-            for (int i = b + 1; i < 6; i++) cswap(c, m[6 * i + k], m[6 * i + b]);
-            cswap(c, m[7 * k], m[7 * b]);
+            for (int i = b + 1; i < 6; i++) cswap(true, m[6 * i + k], m[6 * i + b]);
+            cswap(true, m[7 * k], m[7 * b]);
 #pragma unroll
-            for (int i = k + 1; i < b; i++) cswap(c, m[6 * i + k], m[6 * b + i]);
+            for (int i = k + 1; i < b; i++) cswap(true, m[6 * i + k], m[6 * b + i]);
         }
         if (k > 0) {
             double temp[6];
@@ -379,7 +382,8 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
 #pragma unroll
     for (int k = 0; k < 6; k++)
 #pragma unroll
-        for (int i = k + 1; i < 6; i++) cswap(tr[k] == i, d[k], d[i]);
+        for (int i = k + 1; i < 6; i++)
+            if (tr[k] == i) cswap(true, d[k], d[i]);
 #pragma unroll
     for (int k = 0; k < 6; k++)
 #pragma unroll
@@ -394,7 +398,8 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
 #pragma unroll
     for (int k = 5; k >= 0; k--)
 #pragma unroll
-        for (int i = k + 1; i < 6; i++) cswap(tr[k] == i, d[k], d[i]);
+        for (int i = k + 1; i < 6; i++)
+            if (tr[k] == i) cswap(true, d[k], d[i]);
 #pragma unroll
     for (int j = 0; j < 6; j++) x[j] = d[j];
     return sign == 1 || sign == 0;
