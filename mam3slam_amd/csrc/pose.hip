@@ -45,6 +45,22 @@ struct Cfg {
 };
 constexpr int NRED = 27;       // 21 upper entries of H + 6 of b
 
+#ifdef MAM_POSE_PROFILE
+// phase cycles (thread 0 of every workgroup): 0 build pass + sums, 1 LDL^T solve, 2 exp * T, 3 trial pass + sum,
+// 4 LM control, 5 trials, 6 build passes
+__device__ unsigned long long g_pprof[16];
+#define PPROF(k, t0)                                                                    \
+    do {                                                                                \
+        const long long tn_ = clock64();                                               \
+        if (threadIdx.x == 0) atomicAdd(&g_pprof[k], (unsigned long long)(tn_ - (t0))); \
+        (t0) = tn_;                                                                     \
+    } while (0)
+#else
+#define PPROF(k, t0) \
+    do {             \
+    } while (0)
+#endif
+
 struct Args {
     int nframes;
     const mam_pose* tcw;
@@ -89,8 +105,38 @@ __device__ __forceinline__ double lane63(double v) {
 // 4 Q wave sums at once, reduce-scatter style: the xor-32 and xor-16 steps exchange only the half of the values the
 // lane keeps, then xor 8 .. 1 on the Q left; lane group g = lane >> 4 ends with sums [g Q, g Q + Q) (fixed pattern:
 // the bits do not depend on timing) — 7 Q shuffles instead of a full reduction per value
+// a(l) + a(l ^ 32) on lanes 0-31, b(l ^ 32) + b(l) on lanes 32-63: one v_permlane32_swap per dword (gfx950), no LDS
+__device__ __forceinline__ double swap32_sum(double a, double b) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+// the same across rows of 16: a on even rows, b on odd rows
+__device__ __forceinline__ double swap16_sum(double a, double b) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+
 template <int Q>
 __device__ __forceinline__ void wave_sum_scatter4(const double (&v)[4 * Q], double (&out)[Q]) {
+#ifndef MAM_POSE_SHFL
+    // lanes swap through v_permlane{32,16}_swap, then a symmetric DPP butterfly inside each row (every lane of the row
+    // ends with the same bits: each step adds the same two partials in either order)
+    double h[2 * Q];
+#pragma unroll
+    for (int i = 0; i < 2 * Q; i++) h[i] = swap32_sum(v[i], v[2 * Q + i]);
+#pragma unroll
+    for (int i = 0; i < Q; i++) out[i] = swap16_sum(h[i], h[Q + i]);
+#pragma unroll
+    for (int i = 0; i < Q; i++) out[i] += dpp_d<0xb1>(out[i]);    // quad_perm [1,0,3,2]
+#pragma unroll
+    for (int i = 0; i < Q; i++) out[i] += dpp_d<0x4e>(out[i]);    // quad_perm [2,3,0,1]
+#pragma unroll
+    for (int i = 0; i < Q; i++) out[i] += dpp_d<0x141>(out[i]);   // row_half_mirror
+#pragma unroll
+    for (int i = 0; i < Q; i++) out[i] += dpp_d<0x140>(out[i]);   // row_mirror
+#else
     const int lane = threadIdx.x & 63;
     const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0;
     double h[2 * Q];
@@ -110,6 +156,7 @@ __device__ __forceinline__ void wave_sum_scatter4(const double (&v)[4 * Q], doub
     for (int o = 8; o > 0; o >>= 1)
 #pragma unroll
         for (int i = 0; i < Q; i++) out[i] += __shfl_xor(out[i], o, 64);
+#endif
 }
 
 // Block sum of N per-thread values into out[0..N) (LDS; waves summed in order 0..NW-1, a fixed pattern inside a
@@ -117,6 +164,9 @@ __device__ __forceinline__ void wave_sum_scatter4(const double (&v)[4 * Q], doub
 template <int N, int NW>
 __device__ __forceinline__ void block_sum(const double (&v)[N], double* scr, double* out) {
     const int w = threadIdx.x >> 6;
+#ifdef MAM_POSE_PROFILE
+    long long tq = clock64();
+#endif
     if constexpr (N % 4 == 0 && N >= 8) {
         constexpr int Q = N / 4;
         double tot[Q];
@@ -126,6 +176,7 @@ __device__ __forceinline__ void block_sum(const double (&v)[N], double* scr, dou
 #pragma unroll
         for (int i = 0; i < Q; i++) val = il == i ? tot[i] : val;
         if (il < Q) scr[w * N + Q * (lane >> 4) + il] = val;
+        PPROF(8, tq);
     } else {
 #pragma unroll
         for (int k = 0; k < N; k++) {
@@ -134,6 +185,7 @@ __device__ __forceinline__ void block_sum(const double (&v)[N], double* scr, dou
         }
     }
     __syncthreads();
+    if (N > 1) PPROF(9, tq);
     if (threadIdx.x < N) {
         double s = scr[threadIdx.x];
 #pragma unroll
@@ -141,6 +193,7 @@ __device__ __forceinline__ void block_sum(const double (&v)[N], double* scr, dou
         out[threadIdx.x] = s;
     }
     __syncthreads();
+    if (N > 1) PPROF(10, tq);
 }
 
 struct Edges {
@@ -161,8 +214,9 @@ __device__ __forceinline__ double edge_error(const Edges& E, int i, const double
     if (KB8) {
         cam::project_d(c, Xc, &u, &v);   // KannalaBrandt8::project(Vector3d)
     } else {
-        u = (double)c.fx * Xc[0] / Xc[2] + (double)c.cx;
-        v = (double)c.fy * Xc[1] / Xc[2] + (double)c.cy;
+        const double iz = 1.0 / Xc[2];   // one division, two products (within an ulp of fx * x / z)
+        u = (double)c.fx * Xc[0] * iz + (double)c.cx;
+        v = (double)c.fy * Xc[1] * iz + (double)c.cy;
     }
     const double e0 = (double)E.ox[i] - u, e1 = (double)E.oy[i] - v;
     *e0o = e0;
@@ -176,21 +230,6 @@ __device__ __forceinline__ void rho_of(double chi, bool robust, double delta, do
     else { *r0 = chi; *r1 = 1.0; }
 }
 
-#ifdef MAM_POSE_PROFILE
-// phase cycles (thread 0 of every workgroup): 0 build pass + sums, 1 LDL^T solve, 2 exp * T, 3 trial pass + sum,
-// 4 LM control, 5 trials, 6 build passes
-__device__ unsigned long long g_pprof[8];
-#define PPROF(k, t0)                                                                    \
-    do {                                                                                \
-        const long long tn_ = clock64();                                               \
-        if (threadIdx.x == 0) atomicAdd(&g_pprof[k], (unsigned long long)(tn_ - (t0))); \
-        (t0) = tn_;                                                                     \
-    } while (0)
-#else
-#define PPROF(k, t0) \
-    do {             \
-    } while (0)
-#endif
 
 // computeActiveErrors at T (errors stored) + activeRobustChi2
 template <bool KB8>
@@ -235,12 +274,17 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
         se3::map_point(T, Xw, Xc);
         const double x = Xc[0], y = Xc[1], z = Xc[2];
         constexpr bool kb8 = KB8;
-        double u, v;
+        double u, v, iz = 0.0, fxz = 0.0, fyz = 0.0;
         if (kb8) {
             cam::project_d(c, Xc, &u, &v);
         } else {
-            u = (double)c.fx * x / z + (double)c.cx;
-            v = (double)c.fy * y / z + (double)c.cy;
+            // Pinhole with one reciprocal of z for the projection and the Jacobian (six divisions before; the
+            // products are within an ulp of the quotients, inside the 1e-4 pose parity)
+            iz = 1.0 / z;
+            fxz = (double)c.fx * x * iz;
+            fyz = (double)c.fy * y * iz;
+            u = fxz + (double)c.cx;
+            v = fyz + (double)c.cy;
         }
         const double e0 = (double)E.ox[i] - u, e1 = (double)E.oy[i] - v;
         E.err[2 * i] = e0;
@@ -258,8 +302,8 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
             for (int k = 0; k < 6; k++) J[k] = -J[k];
         } else {
             const double fx = c.fx, fy = c.fy;
-            J[0] = -(fx / z); J[1] = -0.0; J[2] = -(-fx * x / (z * z));
-            J[3] = -0.0; J[4] = -(fy / z); J[5] = -(-fy * y / (z * z));
+            J[0] = -(fx * iz); J[1] = -0.0; J[2] = fxz * iz;
+            J[3] = -0.0; J[4] = -(fy * iz); J[5] = fyz * iz;
         }
         double A[12];
         if (kb8) {
@@ -284,13 +328,24 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
         double wA[12];   // A * wo once per entry: (A[a] * wo) * A[b] is the same product as before
 #pragma unroll
         for (int k = 0; k < 12; k++) wA[k] = A[k] * wo;
+        // H and b as FMA chains; Pinhole's structural zeros (A[4], A[9]) skipped (the loops unroll, so the tests fold)
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; a++)
 #pragma unroll
-            for (int b = a; b < 6; b++) acc[q++] += wA[a] * A[b] + wA[6 + a] * A[6 + b];
+            for (int b = a; b < 6; b++) {
+                double h = acc[q];
+                if (kb8 || (a != 3 && b != 3)) h = fma(wA[6 + a], A[6 + b], h);
+                if (kb8 || (a != 4 && b != 4)) h = fma(wA[a], A[b], h);
+                acc[q++] = h;
+            }
 #pragma unroll
-        for (int a = 0; a < 6; a++) acc[21 + a] += A[a] * o0 + A[6 + a] * o1;
+        for (int a = 0; a < 6; a++) {
+            double g = acc[21 + a];
+            if (kb8 || a != 3) g = fma(A[6 + a], o1, g);
+            if (kb8 || a != 4) g = fma(A[a], o0, g);
+            acc[21 + a] = g;
+        }
     }
     PPROF(7, tb);   // the edge loop alone (thread 0's view)
     block_sum<NRED + 1, NW>(acc, scr, red);
@@ -298,9 +353,11 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
 }
 
 // Eigen 3.4.0 LDLT<MatrixXd, Lower> compute + solve of (H + lambda I) x = b, 6x6, diagonal pivoting; returns
-// isPositive(). Same operation order as the oracle (oracle/pose_oracle.cpp eigen_ldlt_solve). Fully unrolled: the
-// pivot row/column exchanges are predicated swaps over the candidate indices, so the matrix stays in registers
-// (a runtime-indexed private array would live in scratch memory).
+// isPositive(). Eigen's left-looking order (oracle/pose_oracle.cpp eigen_ldlt_solve) with the dot products as FMA chains
+// and one reciprocal per pivot (within a few ulp of the oracle's quotients; the 1e-4 pose parity). Fully unrolled, the
+// matrix in registers (a runtime-indexed private array would live in scratch memory); the pivot is the same in every
+// lane, so its row / column exchange — and the right-hand side's — is one scalar branch, and the sign bookkeeping is
+// branch-free.
 __device__ __forceinline__ void cswap(bool c, double& a, double& b) {
     const double ta = a, tb = b;
     a = c ? tb : ta;
@@ -318,19 +375,19 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
 #pragma unroll
         for (int j = 0; j < 6; j++) m[7 * j] += lambda;
     }
+    double d[6];   // the right-hand side, exchanged with the rows as they pivot (Transpositions * b)
+#pragma unroll
+    for (int j = 0; j < 6; j++) d[j] = red[21 + j];
     int tr[6];
-    int sign = 0;   // 0 zero, 1 positive semidef, 2 negative semidef, 3 indefinite
-    bool done = false;
+    double rd[6];
+    bool neg = false;   // a negative pivot: Eigen's sign ends NegativeSemiDef or Indefinite
 #pragma unroll
     for (int k = 0; k < 6; k++) {
-        if (done) continue;
         int big = k;
         double bv = fabs(m[7 * k]);
 #pragma unroll
         for (int i = k + 1; i < 6; i++)
             if (fabs(m[7 * i]) > bv) { bv = fabs(m[7 * i]); big = i; }
-        // the pivot is the same in every lane (the matrix is): a scalar branch takes the one exchange needed instead
-        // of predicated swaps over every candidate
         big = __builtin_amdgcn_readfirstlane(big);
         tr[k] = big;
 #pragma unroll
@@ -343,6 +400,7 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
             cswap(true, m[7 * k], m[7 * b]);
 #pragma unroll
             for (int i = k + 1; i < b; i++) cswap(true, m[6 * i + k], m[6 * b + i]);
+            cswap(true, d[k], d[b]);
         }
         if (k > 0) {
             double temp[6];
@@ -350,59 +408,52 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
             for (int j = 0; j < k; j++) temp[j] = m[7 * j] * m[6 * k + j];
             double s = 0.0;
 #pragma unroll
-            for (int j = 0; j < k; j++) s += m[6 * k + j] * temp[j];
+            for (int j = 0; j < k; j++) s = fma(m[6 * k + j], temp[j], s);
             m[7 * k] -= s;
 #pragma unroll
             for (int i = k + 1; i < 6; i++) {
                 double t = 0.0;
 #pragma unroll
-                for (int j = 0; j < k; j++) t += m[6 * i + j] * temp[j];
+                for (int j = 0; j < k; j++) t = fma(m[6 * i + j], temp[j], t);
                 m[6 * i + k] -= t;
             }
         }
         const double akk = m[7 * k];
         const bool valid = fabs(akk) > 0.0;
-        if (k == 0 && !valid) {   // the whole diagonal is zero
-            sign = 0;
+        if (k == 0 && !valid) {
+            // the whole diagonal is zero: ZeroSign, identity transpositions, and the solve's tolerance gives x = 0
 #pragma unroll
-            for (int j = 0; j < 6; j++) tr[j] = j;
-            done = true;
-            continue;
+            for (int j = 0; j < 6; j++) x[j] = 0.0;
+            return true;
         }
-        if (valid)
+        const double rk = 1.0 / akk;
+        rd[k] = rk;
+        const double rs = valid ? rk : 1.0;   // a zero pivot leaves its column as it is
 #pragma unroll
-            for (int i = k + 1; i < 6; i++) m[6 * i + k] /= akk;
-        if (sign == 1) { if (akk < 0) sign = 3; }
-        else if (sign == 2) { if (akk > 0) sign = 3; }
-        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+        for (int i = k + 1; i < 6; i++) m[6 * i + k] *= rs;
+        neg = neg || akk < 0.0;
     }
-    double d[6];
-#pragma unroll
-    for (int j = 0; j < 6; j++) d[j] = red[21 + j];
 #pragma unroll
     for (int k = 0; k < 6; k++)
 #pragma unroll
-        for (int i = k + 1; i < 6; i++)
-            if (tr[k] == i) cswap(true, d[k], d[i]);
-#pragma unroll
-    for (int k = 0; k < 6; k++)
-#pragma unroll
-        for (int i = k + 1; i < 6; i++) d[i] -= m[6 * i + k] * d[k];
+        for (int i = k + 1; i < 6; i++) d[i] = fma(-m[6 * i + k], d[k], d[i]);
     const double tol = 2.2250738585072014e-308;   // numeric_limits<double>::min()
 #pragma unroll
-    for (int i = 0; i < 6; i++) d[i] = fabs(m[7 * i]) > tol ? d[i] / m[7 * i] : 0.0;
+    for (int i = 0; i < 6; i++) d[i] = fabs(m[7 * i]) > tol ? d[i] * rd[i] : 0.0;
 #pragma unroll
     for (int k = 5; k >= 0; k--)
 #pragma unroll
-        for (int i = 0; i < k; i++) d[i] -= m[6 * k + i] * d[k];
+        for (int i = 0; i < k; i++) d[i] = fma(-m[6 * k + i], d[k], d[i]);
 #pragma unroll
     for (int k = 5; k >= 0; k--)
 #pragma unroll
-        for (int i = k + 1; i < 6; i++)
-            if (tr[k] == i) cswap(true, d[k], d[i]);
+        for (int b = k + 1; b < 6; b++) {
+            if (tr[k] != b) continue;
+            cswap(true, d[k], d[b]);
+        }
 #pragma unroll
     for (int j = 0; j < 6; j++) x[j] = d[j];
-    return sign == 1 || sign == 0;
+    return !neg;
 }
 
 
@@ -459,8 +510,13 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
                 // issue slots), x / Tn / the verdict broadcast through LDS
                 __shared__ double s_step[14];
                 if (threadIdx.x < 64) {
+#ifdef MAM_POSE_PROFILE
+                    long long tl = clock64();
+#endif
                     ok2 = ldlt6(red, lambda, x);
-                    se3::exp_mul(x, T, Tn);
+                    PPROF(11, tl);
+                    se3::exp_mul<true>(x, T, Tn);
+                    PPROF(12, tl);
                     if (threadIdx.x == 0) {
 #pragma unroll
                         for (int k = 0; k < 6; k++) s_step[k] = x[k];
@@ -479,7 +535,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
             } else {
                 ok2 = ldlt6(red, lambda, x);
                 PPROF(1, tp);
-                se3::exp_mul(x, T, Tn);
+                se3::exp_mul<true>(x, T, Tn);
                 PPROF(2, tp);
             }
             double tempChi = active_chi<KB8>(E, Tn, c, robust, delta, scr);
@@ -794,8 +850,12 @@ int mam_pose_optimization_batch_device(mam_pose_ctx* c, int nframes, const mam_p
 #ifdef MAM_POSE_PROFILE
     {
         MAM_HIP(hipStreamSynchronize(s));
-        unsigned long long h[8];
+        unsigned long long h[16];
         MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::pose::g_pprof), sizeof(h)));
+        fprintf(stderr, "pose reduce: scatter %.0f barrier1 %.0f sum+barrier2 %.0f /pass; ldlt6 %.0f exp %.0f /trial\n",
+                h[8] / (double)std::max(1ull, h[6]), h[9] / (double)std::max(1ull, h[6]),
+                h[10] / (double)std::max(1ull, h[6]), h[11] / (double)std::max(1ull, h[5]),
+                h[12] / (double)std::max(1ull, h[5]));
         const double nb = (double)std::max(1ull, h[6]), nt = (double)std::max(1ull, h[5]);
         fprintf(stderr, "pose cycles (cumulative): build %.0f/pass (edge loop %.0f) ldlt %.0f exp %.0f trial %.0f/trial "
                         "control %.0f; builds %llu trials %llu\n", h[0] / nb, h[7] / nb, h[1] / nt, h[2] / nt, h[3] / nt,
