@@ -43,16 +43,27 @@ struct Cfg {
     static constexpr int PT = KB8 ? MAM_POSE_THREADS_KB8 : MAM_POSE_THREADS;
     static constexpr int NW = PT / 64;
 };
+#ifndef MAM_POSE_BUILD_UNROLL
+#define MAM_POSE_BUILD_UNROLL 2
+#endif
+#ifndef MAM_POSE_CHI_UNROLL
+#define MAM_POSE_CHI_UNROLL 2
+#endif
+#define MAM_POSE_PRAGMA_(x) _Pragma(#x)
+#define MAM_POSE_PRAGMA(x) MAM_POSE_PRAGMA_(x)
 constexpr int NRED = 27;       // 21 upper entries of H + 6 of b
 
 #ifdef MAM_POSE_PROFILE
 // phase cycles (thread 0 of every workgroup): 0 build pass + sums, 1 LDL^T solve, 2 exp * T, 3 trial pass + sum,
 // 4 LM control, 5 trials, 6 build passes
 __device__ unsigned long long g_pprof[16];
+// thread 0 accumulates in LDS (a global atomic per probe would put its memory latency into the next barrier) and
+// flushes once at the end of the workgroup
+__shared__ unsigned long long s_pprof[16];
 #define PPROF(k, t0)                                                                    \
     do {                                                                                \
         const long long tn_ = clock64();                                               \
-        if (threadIdx.x == 0) atomicAdd(&g_pprof[k], (unsigned long long)(tn_ - (t0))); \
+        if (threadIdx.x == 0) s_pprof[k] += (unsigned long long)(tn_ - (t0));           \
         (t0) = tn_;                                                                     \
     } while (0)
 #else
@@ -84,6 +95,16 @@ __device__ __forceinline__ double dpp_d(double v) {
     const int lo = __double2loint(v), hi = __double2hiint(v);
     return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false),
                             __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false));
+}
+
+// 1 / a as v_rcp_f64 + two Newton steps (the fdiv lowering without its range scaling: |a| stays far inside the
+// normal range here); within an ulp of the quotient, half the dependent instructions
+__device__ __forceinline__ double rcp_nr(double a) {
+    double r = __builtin_amdgcn_rcp(a);
+    double e = fma(-a, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-a, r, 1.0);
+    return fma(r, e, r);
 }
 
 // Wave sum with a fixed DPP pattern (quad perms, row shifts, row broadcasts); the total lands in lane 63.
@@ -214,7 +235,7 @@ __device__ __forceinline__ double edge_error(const Edges& E, int i, const double
     if (KB8) {
         cam::project_d(c, Xc, &u, &v);   // KannalaBrandt8::project(Vector3d)
     } else {
-        const double iz = 1.0 / Xc[2];   // one division, two products (within an ulp of fx * x / z)
+        const double iz = rcp_nr(Xc[2]);   // one reciprocal, two products (within an ulp of fx * x / z)
         u = (double)c.fx * Xc[0] * iz + (double)c.cx;
         v = (double)c.fy * Xc[1] * iz + (double)c.cy;
     }
@@ -237,7 +258,7 @@ __device__ double active_chi(const Edges& E, const double T[7], const mam_camera
                              double* scr) {
     constexpr int PT = Cfg<KB8>::PT, NW = Cfg<KB8>::NW;
     double acc[1] = {0.0};
-#pragma unroll 2
+    MAM_POSE_PRAGMA(unroll MAM_POSE_CHI_UNROLL)
     for (int i = threadIdx.x; i < E.n; i += PT) {
         if (E.level[i]) continue;
         double e0, e1;
@@ -266,7 +287,7 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
 #endif
     // two edges per iteration: their dependency chains (map, divisions, robust weight, Jacobian, sums) interleave —
     // one wave per SIMD has nothing else to hide the FP64 latency with
-#pragma unroll 2
+    MAM_POSE_PRAGMA(unroll MAM_POSE_BUILD_UNROLL)
     for (int i = threadIdx.x; i < E.n; i += PT) {
         if (E.level[i]) continue;
         const double Xw[3] = {(double)E.X[i], (double)E.Y[i], (double)E.Z[i]};
@@ -280,7 +301,7 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
         } else {
             // Pinhole with one reciprocal of z for the projection and the Jacobian (six divisions before; the
             // products are within an ulp of the quotients, inside the 1e-4 pose parity)
-            iz = 1.0 / z;
+            iz = rcp_nr(z);
             fxz = (double)c.fx * x * iz;
             fyz = (double)c.fy * y * iz;
             u = fxz + (double)c.cx;
@@ -352,56 +373,30 @@ __device__ double build_system(const Edges& E, const double T[7], const mam_came
     return red[NRED];
 }
 
-// Eigen 3.4.0 LDLT<MatrixXd, Lower> compute + solve of (H + lambda I) x = b, 6x6, diagonal pivoting; returns
-// isPositive(). Eigen's left-looking order (oracle/pose_oracle.cpp eigen_ldlt_solve) with the dot products as FMA chains
-// and one reciprocal per pivot (within a few ulp of the oracle's quotients; the 1e-4 pose parity). Fully unrolled, the
-// matrix in registers (a runtime-indexed private array would live in scratch memory); the pivot is the same in every
-// lane, so its row / column exchange — and the right-hand side's — is one scalar branch, and the sign bookkeeping is
-// branch-free.
-__device__ __forceinline__ void cswap(bool c, double& a, double& b) {
-    const double ta = a, tb = b;
-    a = c ? tb : ta;
-    b = c ? ta : tb;
-}
-
+// (H + lambda I) x = b, 6x6: Eigen 3.4.0 LDLT<MatrixXd, Lower>'s left-looking LDL^T and solve
+// (oracle/pose_oracle.cpp eigen_ldlt_solve) without its diagonal pivoting, returning isPositive() (no negative
+// pivot). H = J^T W J is positive semi-definite (Huber weights are positive) and lambda > 0, so the unpivoted LDL^T is
+// as stable as the pivoted one; only the rounding differs (within the 1e-4 pose parity). Pivoting cost three times the
+// instructions of the factorization itself in row / column exchanges and the inverse permutation (a runtime-indexed
+// private array would live in scratch memory). Dot products as FMA chains, one reciprocal per pivot.
 __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
-    double m[36];
+    double m[36];   // lower triangle used
     {
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; a++)
 #pragma unroll
-            for (int b = a; b < 6; b++) { m[6 * a + b] = red[q]; m[6 * b + a] = red[q]; q++; }
+            for (int b = a; b < 6; b++) m[6 * b + a] = red[q++];
 #pragma unroll
         for (int j = 0; j < 6; j++) m[7 * j] += lambda;
     }
-    double d[6];   // the right-hand side, exchanged with the rows as they pivot (Transpositions * b)
+    double d[6];
 #pragma unroll
     for (int j = 0; j < 6; j++) d[j] = red[21 + j];
-    int tr[6];
     double rd[6];
     bool neg = false;   // a negative pivot: Eigen's sign ends NegativeSemiDef or Indefinite
 #pragma unroll
     for (int k = 0; k < 6; k++) {
-        int big = k;
-        double bv = fabs(m[7 * k]);
-#pragma unroll
-        for (int i = k + 1; i < 6; i++)
-            if (fabs(m[7 * i]) > bv) { bv = fabs(m[7 * i]); big = i; }
-        big = __builtin_amdgcn_readfirstlane(big);
-        tr[k] = big;
-#pragma unroll
-        for (int b = k + 1; b < 6; b++) {
-            if (big != b) continue;
-#pragma unroll
-            for (int j = 0; j < k; j++) cswap(true, m[6 * k + j], m[6 * b + j]);
-#pragma unroll
-            for (int i = b + 1; i < 6; i++) cswap(true, m[6 * i + k], m[6 * i + b]);
-            cswap(true, m[7 * k], m[7 * b]);
-#pragma unroll
-            for (int i = k + 1; i < b; i++) cswap(true, m[6 * i + k], m[6 * b + i]);
-            cswap(true, d[k], d[b]);
-        }
         if (k > 0) {
             double temp[6];
 #pragma unroll
@@ -419,16 +414,9 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
             }
         }
         const double akk = m[7 * k];
-        const bool valid = fabs(akk) > 0.0;
-        if (k == 0 && !valid) {
-            // the whole diagonal is zero: ZeroSign, identity transpositions, and the solve's tolerance gives x = 0
-#pragma unroll
-            for (int j = 0; j < 6; j++) x[j] = 0.0;
-            return true;
-        }
-        const double rk = 1.0 / akk;
+        const double rk = rcp_nr(akk);
         rd[k] = rk;
-        const double rs = valid ? rk : 1.0;   // a zero pivot leaves its column as it is
+        const double rs = fabs(akk) > 0.0 ? rk : 1.0;   // a zero pivot leaves its column as it is
 #pragma unroll
         for (int i = k + 1; i < 6; i++) m[6 * i + k] *= rs;
         neg = neg || akk < 0.0;
@@ -444,13 +432,6 @@ __device__ bool ldlt6(const double* red, double lambda, double x[6]) {
     for (int k = 5; k >= 0; k--)
 #pragma unroll
         for (int i = 0; i < k; i++) d[i] = fma(-m[6 * k + i], d[k], d[i]);
-#pragma unroll
-    for (int k = 5; k >= 0; k--)
-#pragma unroll
-        for (int b = k + 1; b < 6; b++) {
-            if (tr[k] != b) continue;
-            cswap(true, d[k], d[b]);
-        }
 #pragma unroll
     for (int j = 0; j < 6; j++) x[j] = d[j];
     return !neg;
@@ -483,7 +464,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
         double currentChi = build_system<KB8>(E, T, c, robust, delta, scr, red);
         PPROF(0, tp);
 #ifdef MAM_POSE_PROFILE
-        if (threadIdx.x == 0) atomicAdd(&g_pprof[6], 1ull);
+        if (threadIdx.x == 0) s_pprof[6] += 1ull;
 #endif
         const double iniChi = currentChi;
         if (it == 0) {
@@ -541,7 +522,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
             double tempChi = active_chi<KB8>(E, Tn, c, robust, delta, scr);
             PPROF(3, tp);
 #ifdef MAM_POSE_PROFILE
-            if (threadIdx.x == 0) atomicAdd(&g_pprof[5], 1ull);
+            if (threadIdx.x == 0) s_pprof[5] += 1ull;
 #endif
             if (!ok2) tempChi = 1.7976931348623157e308;
             rho = currentChi - tempChi;
@@ -588,6 +569,9 @@ __global__ __launch_bounds__(Cfg<KB8>::PT) void k_pose_opt(Args a) {
         if (t == 0) { R->n_inliers = MAM_ERR_CAPACITY; R->rounds = 0; R->iterations = 0; R->lm_trials = 0; }
         return;
     }
+#ifdef MAM_POSE_PROFILE
+    if (t < 16) s_pprof[t] = 0;
+#endif
     uint8_t* p = smem;
     Edges E;
     E.err = reinterpret_cast<double*>(p);      p += a16((size_t)a.cap * 16);
@@ -648,6 +632,10 @@ __global__ __launch_bounds__(Cfg<KB8>::PT) void k_pose_opt(Args a) {
         }
     }
     for (int i = t; i < n; i += PT) out[i] = E.level[i];
+#ifdef MAM_POSE_PROFILE
+    __syncthreads();
+    if (t < 16) atomicAdd(&g_pprof[t], s_pprof[t]);
+#endif
     if (t == 0) {
         R->q[0] = T[0]; R->q[1] = T[1]; R->q[2] = T[2]; R->q[3] = T[3];
         R->t[0] = T[4]; R->t[1] = T[5]; R->t[2] = T[6];

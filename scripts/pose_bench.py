@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--oracle", action="store_true")
+    ap.add_argument("--no-single", action="store_true", help="batch launches only (counter passes: one shape)")
     args = ap.parse_args()
     import torch
 
@@ -69,30 +70,34 @@ def main():
 
     for _ in range(3):
         run(B)
-        run(1)
+        if not args.no_single:
+            run(1)
     torch.cuda.synchronize()
     P.set_profiling(True)
     for _ in range(args.reps):
         run(B)
     torch.cuda.synchronize()
     ms_b = P.stage_times()["pose"][0] / args.reps
-    P.set_profiling(True)
-    for _ in range(args.reps):
-        run(1)
-    torch.cuda.synchronize()
-    ms_1 = P.stage_times()["pose"][0] / args.reps
-    P.set_profiling(False)
-    lat = []
-    for _ in range(args.reps):
-        t0 = time.perf_counter()
-        run(1)
-        st.synchronize()
-        lat.append((time.perf_counter() - t0) * 1e3)
+    ms_1, lat = None, None
+    if not args.no_single:
+        P.set_profiling(True)
+        for _ in range(args.reps):
+            run(1)
+        torch.cuda.synchronize()
+        ms_1 = P.stage_times()["pose"][0] / args.reps
+        P.set_profiling(False)
+        lat = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            run(1)
+            st.synchronize()
+            lat.append((time.perf_counter() - t0) * 1e3)
     res = t_r.cpu().numpy().view(pose.POSE_RESULT_DTYPE).reshape(B)
     out = {"config": args.config, "batch": B, "edges_per_frame": float(np.mean([len(e) for e in edges_l])),
            "ms_per_batch_launch": ms_b, "frames_per_s": B / (ms_b * 1e-3), "ms_b1_launch": ms_1,
-           "ms_b1_wall": float(np.median(lat)), "iterations_per_frame": float(res["iterations"].mean()),
+           "ms_b1_wall": float(np.median(lat)) if lat else None, "iterations_per_frame": float(res["iterations"].mean()),
            "lm_trials_per_frame": float(res["lm_trials"].mean())}
+    out["roofline"] = roofline(out["edges_per_frame"], out["iterations_per_frame"], out["lm_trials_per_frame"], B, ms_b)
     if args.oracle:
         from oracle import oracle_py
 
@@ -109,8 +114,46 @@ def main():
     print(json.dumps(out), flush=True)
 
 
-if __name__ == "__main__":
-    main()
+
+# algorithmic FP64 flops per active edge (Pinhole; a division or square root counts as one flop):
+#   linearisation pass (build_system): T.map(Xw) 33, projection 7, error 2, chi 5, Huber 4, Jacobian 4, J*SE3deriv 10,
+#     robust weights 5, weighted rows 10, H (21 entries of two products) 60, b 20, chi sum 1  -> 161
+#   trial pass (active_chi at the candidate pose): map 33, projection 7, error 2, chi 5, Huber 4, sum 1  -> 52
+FLOP_BUILD_EDGE, FLOP_TRIAL_EDGE = 161, 52
+FP64_VALU_PEAK_TFS = 78.6   # MI355X vector FP64 (MI355X_MICROARCH.md); PoseOptimization is VALU FP64, not MFMA
+PMC_FILE = "profiles/r04/pose_pmc_c2.json"
+
+
+def roofline(edges, iterations, trials, frames, ms_launch) -> dict:
+    """FP64 VALU roofline of one k_pose_opt launch: algorithmic flops = frames x edges x (iterations x 161 + trials x
+    52) (every edge counted active: the outlier rounds deactivate a few per cent, so an upper bound) / launch time,
+    against the vector FP64 peak of the whole chip and of the CUs the launch occupies (one workgroup per frame)."""
+    fl = frames * edges * (iterations * FLOP_BUILD_EDGE + trials * FLOP_TRIAL_EDGE)
+    ach = fl / (ms_launch * 1e-3) / 1e12
+    r = {"bound": "fp64_valu", "kernel": "k_pose_opt", "unit": "TFLOP/s", "achieved": ach, "peak": FP64_VALU_PEAK_TFS,
+         "frac": ach / FP64_VALU_PEAK_TFS, "frac_of_cus_used": ach / (FP64_VALU_PEAK_TFS * min(frames, 256) / 256.0),
+         "flop_per_launch": fl, "avg_launch_ms": ms_launch,
+         "limiter": "latency: one workgroup (8 waves) per frame; per LM iteration a linearisation pass over the "
+                    "edges + a 28-value block reduction, per trial the serial 6x6 LDL^T + SE3 exp on wave 0 and a "
+                    "chi2 pass + reduction (scripts/gpu_pose_pmc.sh for the VALU counters)"}
+    path = os.path.join(ROOT, PMC_FILE)
+    if os.path.exists(path):
+        try:
+            pj = json.load(open(path))
+            e = next((v for k, v in pj.items() if "k_pose_opt" in k), None)
+            if e:
+                r["pmc"] = {k: e[k] for k in ("valu_busy", "SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64",
+                                              "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                                              "SQ_INSTS_VALU_TRANS_F64", "us_mean") if k in e}
+                r["pmc_file"] = PMC_FILE
+                f64 = sum(e.get(f"SQ_INSTS_VALU_{c}_F64", 0.0) for c in ("ADD", "MUL", "FMA", "TRANS"))
+                if f64 and e.get("us_mean"):
+                    # wave-instructions x 4 cycles (wave64 on a 16-lane FP64 unit) over the chip's SIMD-cycles
+                    r["pmc"]["fp64_pipe_busy"] = f64 * 4 / (1024 * e["us_mean"] * 1e-6 * 2.4e9)
+                    r["pmc"]["valu_pipe_busy"] = e.get("SQ_INSTS_VALU", 0.0) * 4 / (1024 * e["us_mean"] * 1e-6 * 2.4e9)
+        except Exception:
+            pass
+    return r
 
 
 def section(tr, reps=20, oracle=True) -> dict:
@@ -173,6 +216,8 @@ def section(tr, reps=20, oracle=True) -> dict:
             "iterations_per_frame": float(res["iterations"].mean()),
             "lm_trials_per_frame": float(res["lm_trials"].mean()),
             "inliers_per_frame": float(res["n_inliers"].mean())}
+    info["roofline"] = roofline(info["edges_per_frame"], info["iterations_per_frame"], info["lm_trials_per_frame"],
+                                B, ms_b)
     if oracle:
         from oracle import oracle_py
 
@@ -183,3 +228,7 @@ def section(tr, reps=20, oracle=True) -> dict:
         info["cpu_ms_per_frame"] = (time.perf_counter() - t0) * 1e3 / n
         info["cpu_sample"] = f"{n} frames, oracle C++ restatement, 1 thread"
     return info
+
+
+if __name__ == "__main__":
+    main()
