@@ -268,6 +268,75 @@ __device__ __forceinline__ double edge_error(const Edges& E, int i, const Rt& T,
     return e0 * (w * e0) + e1 * (w * e1);
 }
 
+// O = SE3Quat::exp(u) * T (VertexSE3Expmap::oplusImpl, types/se3quat.h) for the LM step, on its serial critical path:
+// the rotation's quaternion straight from the half angle, (sin(θ/2) / θ · ω, cos(θ/2)) — what Quaterniond(R(ω))
+// gives up to rounding, also in g2o's θ < 1e-5 branch, whose I + Ω + Ω² agrees with the rotation to O(θ⁴) after the
+// normalisation — and V's Rodrigues coefficients (1 - cos θ) / θ², (θ - sin θ) / θ³ as their Taylor series below
+// θ = 0.25 (truncation below 1e-18; one sincos pair above), V = I + Ω + Ω² below θ = 1e-5 as g2o has it.
+__device__ __forceinline__ void exp_mul_step(const double u[6], const double T[7], double O[7]) {
+    const double w0 = u[0], w1 = u[1], w2 = u[2];
+    const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
+    const double th = sqrt(th2);
+    double sh, ch, b, c;   // sin(θ/2) / θ, cos(θ/2), (1 - cos θ) / θ², (θ - sin θ) / θ³
+    if (th < 0.25) {
+        const double x = 0.25 * th2;   // (θ/2)²
+        double s = fma(x, 1.0 / 6227020800.0, -1.0 / 39916800.0);
+        s = fma(x, s, 1.0 / 362880.0);
+        s = fma(x, s, -1.0 / 5040.0);
+        s = fma(x, s, 1.0 / 120.0);
+        s = fma(x, s, -1.0 / 6.0);
+        s = fma(x, s, 1.0);
+        sh = 0.5 * s;
+        double k = fma(x, 1.0 / 479001600.0, -1.0 / 3628800.0);
+        k = fma(x, k, 1.0 / 40320.0);
+        k = fma(x, k, -1.0 / 720.0);
+        k = fma(x, k, 1.0 / 24.0);
+        k = fma(x, k, -0.5);
+        ch = fma(x, k, 1.0);
+        double bb = fma(th2, -1.0 / 20922789888000.0, 1.0 / 87178291200.0);
+        bb = fma(th2, bb, -1.0 / 479001600.0);
+        bb = fma(th2, bb, 1.0 / 3628800.0);
+        bb = fma(th2, bb, -1.0 / 40320.0);
+        bb = fma(th2, bb, 1.0 / 720.0);
+        bb = fma(th2, bb, -1.0 / 24.0);
+        b = fma(th2, bb, 0.5);
+        double cc = fma(th2, -1.0 / 355687428096000.0, 1.0 / 1307674368000.0);
+        cc = fma(th2, cc, -1.0 / 6227020800.0);
+        cc = fma(th2, cc, 1.0 / 39916800.0);
+        cc = fma(th2, cc, -1.0 / 362880.0);
+        cc = fma(th2, cc, 1.0 / 5040.0);
+        cc = fma(th2, cc, -1.0 / 120.0);
+        c = fma(th2, cc, 1.0 / 6.0);
+    } else {
+        double sn, cs, s2, c2;
+        sincos(th, &sn, &cs);
+        sincos(0.5 * th, &s2, &c2);
+        const double it = 1.0 / th;
+        sh = s2 * it;
+        ch = c2;
+        b = (1 - cs) * (it * it);
+        c = (th - sn) * (it * it * it);
+    }
+    if (th < 0.00001) { b = 1.0; c = 1.0; }   // g2o's small-angle V = I + Ω + Ω²
+    const double qe[4] = {sh * w0, sh * w1, sh * w2, ch};
+    // V u_t = u_t + b (ω × u_t) + c (ω × (ω × u_t))
+    const double t0 = u[3], t1 = u[4], t2 = u[5];
+    const double x0 = w1 * t2 - w2 * t1, x1 = w2 * t0 - w0 * t2, x2 = w0 * t1 - w1 * t0;
+    const double y0 = w1 * x2 - w2 * x1, y1 = w2 * x0 - w0 * x2, y2 = w0 * x1 - w1 * x0;
+    const double te[3] = {fma(c, y0, fma(b, x0, t0)), fma(c, y1, fma(b, x1, t1)), fma(c, y2, fma(b, x2, t2))};
+    double rt[3];
+    se3::quat_rotate(qe, T + 4, rt);
+    double q[4];
+    q[3] = qe[3] * T[3] - qe[0] * T[0] - qe[1] * T[1] - qe[2] * T[2];
+    q[0] = qe[3] * T[0] + qe[0] * T[3] + qe[1] * T[2] - qe[2] * T[1];
+    q[1] = qe[3] * T[1] + qe[1] * T[3] + qe[2] * T[0] - qe[0] * T[2];
+    q[2] = qe[3] * T[2] + qe[2] * T[3] + qe[0] * T[1] - qe[1] * T[0];
+    if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+    const double r = rcp_nr(sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]));
+    O[0] = q[0] * r; O[1] = q[1] * r; O[2] = q[2] * r; O[3] = q[3] * r;
+    O[4] = te[0] + rt[0]; O[5] = te[1] + rt[1]; O[6] = te[2] + rt[2];
+}
+
 // RobustKernelHuber::robustify (core/robust_kernel_impl.cpp:76-91) with sqrt(e) and delta / sqrt(e) from one
 // v_rsq_f64 + two Newton steps (within a few ulp of the sqrt and the quotient; the 1e-4 pose parity)
 __device__ __forceinline__ void rho_of(double chi, bool robust, double delta, double* r0, double* r1) {
@@ -531,7 +600,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
 #endif
                     ok2 = ldlt6(red, lambda, x);
                     PPROF(11, tl);
-                    se3::exp_mul<true>(x, T, Tn);
+                    exp_mul_step(x, T, Tn);
                     PPROF(12, tl);
                     if (threadIdx.x == 0) {
 #pragma unroll
@@ -551,7 +620,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
             } else {
                 ok2 = ldlt6(red, lambda, x);
                 PPROF(1, tp);
-                se3::exp_mul<true>(x, T, Tn);
+                exp_mul_step(x, T, Tn);
                 PPROF(2, tp);
             }
             double tempChi = active_chi<KB8>(E, Tn, c, robust, delta, scr);

@@ -68,22 +68,13 @@ __device__ __forceinline__ void rot_to_quat(const double m[9], double q[4]) {
     }
 }
 
-template <bool RCP = false>
 __device__ __forceinline__ void normalize_q(double q[4]) {
     if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
     const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    if (RCP) {
-        const double r = 1.0 / n;
-        q[0] *= r; q[1] *= r; q[2] *= r; q[3] *= r;
-    } else {
-        q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
-    }
+    q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
 }
 
-// O = exp(u) * T (VertexSE3Expmap::oplusImpl: SE3Quat::exp(update) * estimate()). RCP: the divisions as reciprocal
-// products and sin / cos from one sincos, within a few ulp of the quotient form — PoseOptimization's serial LM step,
-// where it is on the critical path of every trial and the 1e-4 pose parity leaves the room
-template <bool RCP = false>
+// O = exp(u) * T (VertexSE3Expmap::oplusImpl: SE3Quat::exp(update) * estimate())
 __device__ __forceinline__ void exp_mul(const double u[6], const double T[7], double O[7]) {
     const double w0 = u[0], w1 = u[1], w2 = u[2];
     const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
@@ -95,19 +86,8 @@ __device__ __forceinline__ void exp_mul(const double u[6], const double T[7], do
     if (theta < 0.00001) {
         for (int k = 0; k < 9; k++) { R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + Om2[k]; V[k] = R[k]; }
     } else {
-        double a, b, c;
-        if (RCP) {
-            double sn, cs;
-            sincos(theta, &sn, &cs);
-            const double it = 1.0 / theta, it2 = it * it;
-            a = sn * it;
-            b = (1 - cs) * it2;
-            c = (theta - sn) * (it2 * it);
-        } else {
-            a = sin(theta) / theta;
-            b = (1 - cos(theta)) / (theta * theta);
-            c = (theta - sin(theta)) / (theta * theta * theta);
-        }
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+        const double c = (theta - sin(theta)) / (theta * theta * theta);
         for (int k = 0; k < 9; k++) {
             const double I = (k % 4 == 0) ? 1.0 : 0.0;
             R[k] = I + a * Om[k] + b * Om2[k];
@@ -118,7 +98,7 @@ __device__ __forceinline__ void exp_mul(const double u[6], const double T[7], do
     rot_to_quat(R, qe);
     double te[3];
     for (int r = 0; r < 3; r++) te[r] = V[3 * r] * u[3] + V[3 * r + 1] * u[4] + V[3 * r + 2] * u[5];
-    normalize_q<RCP>(qe);
+    normalize_q(qe);
     double rt[3];
     quat_rotate(qe, T + 4, rt);
     double q[4];
@@ -126,7 +106,7 @@ __device__ __forceinline__ void exp_mul(const double u[6], const double T[7], do
     q[0] = qe[3] * T[0] + qe[0] * T[3] + qe[1] * T[2] - qe[2] * T[1];
     q[1] = qe[3] * T[1] + qe[1] * T[3] + qe[2] * T[0] - qe[0] * T[2];
     q[2] = qe[3] * T[2] + qe[2] * T[3] + qe[0] * T[1] - qe[1] * T[0];
-    normalize_q<RCP>(q);
+    normalize_q(q);
     O[0] = q[0]; O[1] = q[1]; O[2] = q[2]; O[3] = q[3];
     O[4] = te[0] + rt[0]; O[5] = te[1] + rt[1]; O[6] = te[2] + rt[2];
 }
