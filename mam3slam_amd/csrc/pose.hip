@@ -278,7 +278,8 @@ __device__ __forceinline__ void exp_mul_step(const double u[6], const double T[7
     const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
     const double th = sqrt(th2);
     double sh, ch, b, c;   // sin(θ/2) / θ, cos(θ/2), (1 - cos θ) / θ², (θ - sin θ) / θ³
-    if (th < 0.25) {
+    // θ is the same in every lane: a scalar branch, so the sincos path is not if-converted into the series path
+    if (__builtin_amdgcn_readfirstlane(th < 0.25 ? 1 : 0)) {
         const double x = 0.25 * th2;   // (θ/2)²
         double s = fma(x, 1.0 / 6227020800.0, -1.0 / 39916800.0);
         s = fma(x, s, 1.0 / 362880.0);
@@ -308,14 +309,17 @@ __device__ __forceinline__ void exp_mul_step(const double u[6], const double T[7
         cc = fma(th2, cc, -1.0 / 120.0);
         c = fma(th2, cc, 1.0 / 6.0);
     } else {
+        // an opaque copy of θ: the sincos pair cannot be speculated above the branch onto the common path
+        double thv = th;
+        asm volatile("" : "+v"(thv));
         double sn, cs, s2, c2;
-        sincos(th, &sn, &cs);
-        sincos(0.5 * th, &s2, &c2);
-        const double it = 1.0 / th;
+        sincos(thv, &sn, &cs);
+        sincos(0.5 * thv, &s2, &c2);
+        const double it = 1.0 / thv;
         sh = s2 * it;
         ch = c2;
         b = (1 - cs) * (it * it);
-        c = (th - sn) * (it * it * it);
+        c = (thv - sn) * (it * it * it);
     }
     if (th < 0.00001) { b = 1.0; c = 1.0; }   // g2o's small-angle V = I + Ω + Ω²
     const double qe[4] = {sh * w0, sh * w1, sh * w2, ch};
