@@ -51,6 +51,7 @@ SIGNATURES = {
     "mam_orb_stage_times": (C.c_int, [_vp, _vp, _vp]),
     "mam_orb_debug_candidates": (C.c_int, [_vp, _i32, _i32, _vp, _i32]),
     "mam_orb_debug_blurred": (C.c_int, [_vp, _i32, _i32, _vp]),
+    "mam_orb_debug_set_option": (C.c_int, [_vp, _i32, _i32]),
 }
 
 

@@ -3119,15 +3119,21 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
     }
     // the S blocks' landmark pairs: at most (edges of the optimised poses) x (optimised poses observing the landmark)
-    // per block column, so E Np per problem bounds them (sized up front: no read-back of the counts before the fill)
+    // per block column, so E Np per problem bounds them. Below kPairBoundBytes the buffer is sized by that bound up
+    // front (no read-back of the counts before the fill); above it (map-scale graphs, where E Np overestimates the
+    // sum over landmarks of their observers squared by orders of magnitude) the exact counts are read back after
+    // k_blk_scan and the buffer sized by them
+    constexpr size_t kPairBoundBytes = (size_t)256 << 20;
     std::vector<size_t> pair_cap(Q);
     size_t npairs = 0;
     for (int q = 0; q < Q; q++) {
         pair_cap[q] = (size_t)hp[q].E * (size_t)std::max(hp[q].Np, 1);
         npairs += pair_cap[q];
     }
+    const bool exact_pairs = npairs * sizeof(int2) > kPairBoundBytes;
     if (int rc = c->arena.alloc(bytes + kAlign)) return rc;
-    if (int rc = c->blk_pairs.alloc(std::max<size_t>(npairs, 1))) return rc;
+    if (!exact_pairs)
+        if (int rc = c->blk_pairs.alloc(std::max<size_t>(npairs, 1))) return rc;
     // one device block and one pinned block of the same layout: Prob[Q] | LM[Q] | Outs[Q], one upload
     const size_t pb = al(sizeof(Prob) * Q), lb = al(sizeof(LM) * Q), ob = al(sizeof(Outs) * Q);
     if (int rc = c->hdr.alloc(pb + lb + ob)) return rc;
@@ -3140,7 +3146,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     size_t base = 0;
     for (int q = 0; q < Q; q++) {
         hp[q].lm = lms_d + q;
-        hp[q].blk_pair = c->blk_pairs.p + base;
+        hp[q].blk_pair = exact_pairs ? nullptr : c->blk_pairs.p + base;
         base += pair_cap[q];
     }
     std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
@@ -3165,6 +3171,27 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         const dim3 gB(std::max(maxNp * maxNp, 1), Q);
         hipLaunchKernelGGL(k_blk_count, gB, dim3(64), 0, s, P);
         hipLaunchKernelGGL(k_blk_scan, dim3(1, Q), dim3(SB), 0, s, P);
+        if (exact_pairs) {
+            // the totals at blk_off[Np * Np] (a problem whose structure failed keeps status != 0 and fills nothing)
+            std::vector<int32_t> tot(Q, 0);
+            for (int q = 0; q < Q; q++)
+                MAM_HIP(hipMemcpyAsync(&tot[q], hp[q].blk_off + (size_t)hp[q].Np * hp[q].Np, sizeof(int32_t),
+                                       hipMemcpyDeviceToHost, s));
+            MAM_HIP(hipStreamSynchronize(s));
+            size_t n_exact = 0;
+            std::vector<size_t> off(Q);
+            for (int q = 0; q < Q; q++) {
+                off[q] = n_exact;
+                n_exact += (size_t)std::min<size_t>((size_t)std::max(tot[q], 0), pair_cap[q]);
+            }
+            if (int rc = c->blk_pairs.alloc(std::max<size_t>(n_exact, 1))) return rc;
+            std::vector<int2*> ptr(Q);
+            for (int q = 0; q < Q; q++) {
+                ptr[q] = c->blk_pairs.p + off[q];
+                MAM_HIP(hipMemcpyAsync(&P[q].blk_pair, &ptr[q], sizeof(int2*), hipMemcpyHostToDevice, s));
+            }
+            MAM_HIP(hipStreamSynchronize(s));
+        }
         hipLaunchKernelGGL(k_blk_fill, gB, dim3(64), 0, s, P);
         // iteration 0's linearisation and system at the initial state (lambda_0 needs its max |diag(H)|), the initial
         // chi2; the first trial's k_point_sys then starts from this system

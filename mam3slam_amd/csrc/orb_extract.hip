@@ -20,6 +20,7 @@
 #include "orb_common.hpp"
 #include "runtime.hpp"
 #include "orb_kernels.hip"
+#include "distribute.hpp"
 
 namespace {
 
@@ -61,11 +62,22 @@ struct mam_orb_ctx {
     DevBuf<uint8_t> d_pyr, d_blur, d_input;
     DevBuf<uint32_t> d_cand, d_keys, d_okey, d_orank;
     DevBuf<uint16_t> d_knode;
+    DevBuf<uint32_t> d_knode32;   // k_distribute2's node words of keys beyond its register capacity
     DevBuf<int> d_cellcnt, d_lvlcnt;
     DevBuf<mam_keypoint> d_kps;
     DevBuf<uint8_t> d_desc;
     DevBuf<int32_t> d_counts;
+    // mam_orb_extract's staging: the frame and one [counts | keypoints | descriptors] block, pinned on the host and
+    // contiguous on the device, so a call is one upload, the pipeline, one download and one synchronisation
+    mam::PinnedBuf h_in, h_out;
+    DevBuf<uint8_t> d_out;
     size_t fast_lds = 0, dist_lds = 0;
+    size_t dist2_lds[3] = {0, 0, 0};   // k_distribute2 LDS bytes for 256 / 512 / 1024 threads
+    int dist_nt = -1;                  // DistributeOctTree width override (mam_orb_debug_set_option), -1 = auto
+    int fork = -1;                     // latency-mode stream fork override (mam_orb_debug_set_option), -1 = auto
+    // latency mode's side streams and their fork / join events (run_pipeline)
+    hipStream_t side[2] = {nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_side[2] = {nullptr, nullptr};
     int dist_kcap = 0;   // candidates per level k_distribute keeps in LDS (more: global scratch)
     int fast_cw = 0;   // k_fast_cells plane pitch instance
     // single-launch pyramid (k_pyr_bands): per band count, the band table and its LDS carve
@@ -366,10 +378,18 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         // candidate keys + node ids in LDS (6 B each) up to a 64 KB workgroup (two per CU)
         c->dist_kcap = (int)std::min<size_t>(16384, c->dist_lds < 60 * 1024 ? (64 * 1024 - c->dist_lds) / 6 : 0) & ~63;
         c->dist_lds += (size_t)c->dist_kcap * 6 + 32;
-        if (c->fast_lds > 160 * 1024 || c->dist_lds > 160 * 1024) {
+        for (int i = 0; i < 3; i++) c->dist2_lds[i] = mam::dist::lds_bytes(g.node_cap, maxcells, 256 << i);
+        if (g.node_cap > 16383) { g_last_error = "too many DistributeOctTree nodes (nfeatures too large)"; return MAM_ERR_ARG; }
+        if (c->fast_lds > 160 * 1024 || c->dist_lds > 160 * 1024 || c->dist2_lds[2] > 160 * 1024) {
             g_last_error = "LDS budget exceeded (nfeatures or cell size too large)";
             return MAM_ERR_ARG;
         }
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<256, 16>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[0]);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<512, 16>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[1]);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<1024, 8>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[2]);
         for (int nb = 8; nb <= 64; nb += 8)
             if (int rc = build_pyr_plan(c, nb)) return rc;
         if (pyr_forced_bands() > 0 && pyr_forced_bands() % 8)
@@ -392,6 +412,7 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
     if (int rc = c->d_cand.alloc(cand)) return rc;
     if (int rc = c->d_keys.alloc(cand)) return rc;
     if (int rc = c->d_knode.alloc(cand)) return rc;
+    if (int rc = c->d_knode32.alloc(cand)) return rc;
     if (int rc = c->d_cellcnt.alloc((size_t)Fcap * g.cells_per_frame)) return rc;
     if (int rc = c->d_lvlcnt.alloc((size_t)Fcap * L * 2)) return rc;
     if (int rc = c->d_okey.alloc((size_t)Fcap * g.kp_slots)) return rc;
@@ -498,16 +519,41 @@ mam_orb_ctx::PyrPlan* choose_pyr_plan(mam_orb_ctx* c, int F) {
     return nullptr;
 }
 
+// DistributeOctTree kernel: k_distribute2 with 1024 threads per (frame, level) for a few frames (latency: a level's
+// rounds are chains of barriers, more threads shorten the key passes), 256 for batches (occupancy). MAM_DIST_NT=0 the
+// round-3 k_distribute, 256 / 512 / 1024 force a width.
+int dist_threads(const mam_orb_ctx* c, int F) {
+    static const int forced = [] {
+        const char* e = getenv("MAM_DIST_NT");
+        return e ? atoi(e) : -1;
+    }();
+    const int v = c->dist_nt >= 0 ? c->dist_nt : forced;
+    if (v == 0 || v == 256 || v == 512 || v == 1024) return v;
+    return F <= 4 ? 1024 : 256;
+}
+
+// Latency mode (run_pipeline's three-stream dataflow) for up to 4 frames per call; MAM_ORB_FORK=0 / the context
+// option turn it off (one stream, stages in order).
+bool fork_enabled(const mam_orb_ctx* c, int F, int nt) {
+    static const int env = [] {
+        const char* e = getenv("MAM_ORB_FORK");
+        return e ? atoi(e) : -1;
+    }();
+    const int v = c->fork >= 0 ? c->fork : env;
+    if (v == 0 || nt == 0 || !c->side[0]) return false;
+    return F <= 4;
+}
+
 int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size_t fstride, int lap0, int lap1,
                  mam_keypoint* d_kps, uint8_t* d_desc, int capacity, int32_t* d_counts, hipStream_t s) {
     const mam::Geom& g = c->geom;
     const int L = g.nlevels;
     mam::LevelSrc src{d_in, stride, fstride, c->d_pyr.p};
-    {
-        StageScope sc(&c->timer, s, MAM_STAGE_PYRAMID);
+    auto launch_pyramid = [&](hipStream_t s) {
         if (mam_orb_ctx::PyrPlan* pp = choose_pyr_plan(c, F)) {
-            hipLaunchKernelGGL(mam::k_pyr_bands, dim3(pp->nb, F), dim3(256), pp->lds, s, c->d_geom.p, src, c->d_pyr.p,
-                               pp->bands.p, pp->buf1_off, pp->rc_off);
+            // a band's rows per level are few (c1: ~6-20): 1024 threads spread each level over ~1-3 rows per thread
+            hipLaunchKernelGGL(mam::k_pyr_bands<1024>, dim3(pp->nb, F), dim3(1024), pp->lds, s, c->d_geom.p, src,
+                               c->d_pyr.p, pp->bands.p, pp->buf1_off, pp->rc_off);
         } else {
             // k_pyr_flat reads whole source words: level 0 rows must be word-aligned and a multiple of 4 wide (the
             // last word of the frame's last row must not run past the caller's buffer)
@@ -530,32 +576,83 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
                 }
             }
         }
-    }
-    // (blur and FAST both keep the CUs' issue slots busy: running the blur on a second stream beside FAST + DistributeOctTree
-    // measured no gain, so the stages stay in order on one stream)
-    {
-        StageScope sc(&c->timer, s, MAM_STAGE_BLUR);
-        hipLaunchKernelGGL(mam::k_blur7, dim3((g.tiles_per_frame + mam::BLUR_TPB - 1) / mam::BLUR_TPB, F), dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p);
-    }
-    {
-        StageScope sc(&c->timer, s, MAM_STAGE_FAST);
-        const dim3 fg(g.cells_per_frame, F), fb(mam::FAST_THREADS);
+    };
+    auto launch_fast = [&](hipStream_t st, int cell_first, int ncells) {
+        const dim3 fg(ncells, F), fb(mam::FAST_THREADS);
         switch (c->fast_cw) {
-            case 24: hipLaunchKernelGGL(mam::k_fast_cells<24>, fg, fb, c->fast_lds, s, c->d_geom.p, c->d_cells.p, src,
-                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast); break;
-            case 32: hipLaunchKernelGGL(mam::k_fast_cells<32>, fg, fb, c->fast_lds, s, c->d_geom.p, c->d_cells.p, src,
-                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast); break;
-            case 40: hipLaunchKernelGGL(mam::k_fast_cells<40>, fg, fb, c->fast_lds, s, c->d_geom.p, c->d_cells.p, src,
-                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast); break;
-            default: hipLaunchKernelGGL(mam::k_fast_cells<48>, fg, fb, c->fast_lds, s, c->d_geom.p, c->d_cells.p, src,
-                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast); break;
+            case 24: hipLaunchKernelGGL(mam::k_fast_cells<24>, fg, fb, c->fast_lds, st, c->d_geom.p, c->d_cells.p, src,
+                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast, cell_first); break;
+            case 32: hipLaunchKernelGGL(mam::k_fast_cells<32>, fg, fb, c->fast_lds, st, c->d_geom.p, c->d_cells.p, src,
+                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast, cell_first); break;
+            case 40: hipLaunchKernelGGL(mam::k_fast_cells<40>, fg, fb, c->fast_lds, st, c->d_geom.p, c->d_cells.p, src,
+                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast, cell_first); break;
+            default: hipLaunchKernelGGL(mam::k_fast_cells<48>, fg, fb, c->fast_lds, st, c->d_geom.p, c->d_cells.p, src,
+                                        c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast, cell_first); break;
         }
-    }
-    {
-        StageScope sc(&c->timer, s, MAM_STAGE_DISTRIBUTE);
-        hipLaunchKernelGGL(mam::k_distribute, dim3(L, F), dim3(256), c->dist_lds, s, c->d_geom.p, c->d_cellcnt.p,
-                           c->d_cand.p, c->d_keys.p, c->d_knode.p, c->d_okey.p, c->d_orank.p, c->d_lvlcnt.p, lap0,
-                           lap1, c->dist_kcap);
+    };
+    const int nt = dist_threads(c, F);
+    auto launch_dist = [&](hipStream_t st, int l_first, int nl) {
+        if (nt == 0) {   // the round-3 kernel (all levels)
+            hipLaunchKernelGGL(mam::k_distribute, dim3(L, F), dim3(256), c->dist_lds, st, c->d_geom.p, c->d_cellcnt.p,
+                               c->d_cand.p, c->d_keys.p, c->d_knode.p, c->d_okey.p, c->d_orank.p, c->d_lvlcnt.p, lap0,
+                               lap1, c->dist_kcap);
+            return;
+        }
+        const int li = nt == 1024 ? 2 : nt == 512 ? 1 : 0;
+        const size_t lds = c->dist2_lds[li];
+#define MAM_DIST2_LAUNCH(NT_, KPT_)                                                                                   \
+    hipLaunchKernelGGL((mam::k_distribute2<NT_, KPT_>), dim3(nl, F), dim3(NT_), lds, st, c->d_geom.p, c->d_cellcnt.p, \
+                       c->d_cand.p, c->d_keys.p, c->d_knode32.p, c->d_okey.p, c->d_orank.p, c->d_lvlcnt.p, lap0, lap1,  \
+                       l_first)
+        if (nt == 1024) MAM_DIST2_LAUNCH(1024, 8);
+        else if (nt == 512) MAM_DIST2_LAUNCH(512, 16);
+        else MAM_DIST2_LAUNCH(256, 16);
+#undef MAM_DIST2_LAUNCH
+    };
+    if (fork_enabled(c, F, nt)) {
+        // latency mode (a few frames): the stages as a dataflow over three streams. Level 0's FAST cells and its
+        // DistributeOctTree need only the input frame, so they run beside the pyramid; the blur of every level runs
+        // beside FAST + DistributeOctTree of levels >= 1; the descriptors join both.
+        //   side A: FAST(level 0) -> DistributeOctTree(level 0)
+        //   s:      pyramid -> FAST(levels >= 1) -> DistributeOctTree(levels >= 1) -> [join A, B] -> describe
+        //   side B: [pyramid] -> blur (all levels)
+        MAM_HIP(hipEventRecord(c->ev_fork, s));
+        MAM_HIP(hipStreamWaitEvent(c->side[0], c->ev_fork, 0));
+        launch_fast(c->side[0], 0, g.L[0].ncells);
+        launch_dist(c->side[0], 0, 1);
+        MAM_HIP(hipEventRecord(c->ev_side[0], c->side[0]));
+        launch_pyramid(s);
+        MAM_HIP(hipEventRecord(c->ev_pyr, s));
+        MAM_HIP(hipStreamWaitEvent(c->side[1], c->ev_pyr, 0));
+        hipLaunchKernelGGL(mam::k_blur7, dim3((g.tiles_per_frame + mam::BLUR_TPB - 1) / mam::BLUR_TPB, F), dim3(256), 0,
+                           c->side[1], c->d_geom.p, src, c->d_blur.p);
+        MAM_HIP(hipEventRecord(c->ev_side[1], c->side[1]));
+        if (L > 1) {
+            launch_fast(s, g.L[1].cell_base, g.cells_per_frame - g.L[1].cell_base);
+            launch_dist(s, 1, L - 1);
+        }
+        MAM_HIP(hipStreamWaitEvent(s, c->ev_side[0], 0));
+        MAM_HIP(hipStreamWaitEvent(s, c->ev_side[1], 0));
+    } else {
+        {
+            StageScope sc(&c->timer, s, MAM_STAGE_PYRAMID);
+            launch_pyramid(s);
+        }
+        // (blur and FAST both keep the CUs' issue slots busy in a batch: running the blur on a second stream beside
+        // FAST + DistributeOctTree measured no gain there, so batches keep the stages in order on one stream)
+        {
+            StageScope sc(&c->timer, s, MAM_STAGE_BLUR);
+            hipLaunchKernelGGL(mam::k_blur7, dim3((g.tiles_per_frame + mam::BLUR_TPB - 1) / mam::BLUR_TPB, F), dim3(256),
+                               0, s, c->d_geom.p, src, c->d_blur.p);
+        }
+        {
+            StageScope sc(&c->timer, s, MAM_STAGE_FAST);
+            launch_fast(s, 0, g.cells_per_frame);
+        }
+        {
+            StageScope sc(&c->timer, s, MAM_STAGE_DISTRIBUTE);
+            launch_dist(s, 0, L);
+        }
     }
     {
         StageScope sc(&c->timer, s, MAM_STAGE_DESCRIBE);
@@ -609,6 +706,10 @@ int mam_orb_create(const mam_orb_params* params, int device, mam_orb_ctx** out) 
     c->device = device;
     build_tables(c);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pyr, hipEventDisableTiming);
+    for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->ev_side[i], hipEventDisableTiming);
     if (e != hipSuccess) {
         g_last_error = hipGetErrorString(e);
         delete c;
@@ -624,8 +725,14 @@ void mam_orb_destroy(mam_orb_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->d_geom.release(); c->d_cells.release(); c->d_tabs_i.release(); c->d_tabs_s.release();
     c->d_pyr.release(); c->d_blur.release(); c->d_input.release();
-    c->d_cand.release(); c->d_keys.release(); c->d_okey.release(); c->d_orank.release(); c->d_knode.release();
-    c->d_cellcnt.release(); c->d_lvlcnt.release(); c->d_kps.release(); c->d_desc.release(); c->d_counts.release();
+    c->d_cand.release(); c->d_keys.release(); c->d_okey.release(); c->d_orank.release(); c->d_knode.release(); c->d_knode32.release();
+    c->d_cellcnt.release(); c->d_lvlcnt.release(); c->d_kps.release(); c->d_desc.release(); c->d_counts.release(); c->d_out.release();
+    for (int i = 0; i < 2; i++) {
+        if (c->side[i]) { (void)hipStreamSynchronize(c->side[i]); (void)hipStreamDestroy(c->side[i]); }
+        if (c->ev_side[i]) (void)hipEventDestroy(c->ev_side[i]);
+    }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_pyr) (void)hipEventDestroy(c->ev_pyr);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -678,25 +785,34 @@ int mam_orb_extract(mam_orb_ctx* c, const uint8_t* img, int w, int h, size_t str
     MAM_DEVICE_SCOPE(c->device);
     if (int rc = ensure_geometry(c, w, h, 1)) return rc;
     const int kcap = c->geom.kp_slots;
-    if (int rc = c->d_input.alloc((size_t)w * h)) return rc;
-    if (int rc = c->d_kps.alloc(kcap)) return rc;
-    if (int rc = c->d_desc.alloc((size_t)kcap * 32)) return rc;
-    if (int rc = c->d_counts.alloc(2)) return rc;
-    MAM_HIP(hipMemcpy2DAsync(c->d_input.p, w, img, stride, w, h, hipMemcpyHostToDevice, c->stream));
-    if (int rc = run_pipeline(c, c->d_input.p, 1, w, (size_t)w * h, lap0, lap1, c->d_kps.p, c->d_desc.p, kcap,
-                              c->d_counts.p, c->stream))
+    // device / pinned block: counts (64 B) | kcap keypoints | kcap descriptors
+    const size_t kp_off = 64, desc_off = (kp_off + sizeof(mam_keypoint) * (size_t)kcap + 15) & ~(size_t)15;
+    const size_t out_bytes = desc_off + (size_t)kcap * 32;
+    const size_t in_bytes = (size_t)w * h;
+    if (int rc = c->d_input.alloc(in_bytes + 64)) return rc;   // k_pyr_flat may read up to 3 bytes past the frame
+    if (int rc = c->d_out.alloc(out_bytes)) return rc;
+    if (int rc = c->h_in.alloc(in_bytes)) return rc;
+    if (int rc = c->h_out.alloc(out_bytes)) return rc;
+    if (stride == (size_t)w) std::memcpy(c->h_in.p, img, in_bytes);
+    else
+        for (int y = 0; y < h; y++) std::memcpy(c->h_in.p + (size_t)y * w, img + (size_t)y * stride, w);
+    MAM_HIP(hipMemcpyAsync(c->d_input.p, c->h_in.p, in_bytes, hipMemcpyHostToDevice, c->stream));
+    int32_t* d_cnt = reinterpret_cast<int32_t*>(c->d_out.p);
+    mam_keypoint* d_kp = reinterpret_cast<mam_keypoint*>(c->d_out.p + kp_off);
+    uint8_t* d_ds = c->d_out.p + desc_off;
+    if (int rc = run_pipeline(c, c->d_input.p, 1, w, in_bytes, lap0, lap1, d_kp, d_ds, kcap, d_cnt, c->stream))
         return rc;
-    int32_t cnt[2];
-    MAM_HIP(hipMemcpyAsync(cnt, c->d_counts.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    MAM_HIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
     MAM_HIP(hipStreamSynchronize(c->stream));
+    int32_t cnt[2];
+    std::memcpy(cnt, c->h_out.p, sizeof(cnt));
     if (cnt[0] < 0) { g_last_error = "internal keypoint slot overflow"; return MAM_ERR_DEVICE; }
     *n_out = cnt[0];
     if (cnt[0] > capacity || (cnt[0] > 0 && (!kps || !desc))) return MAM_ERR_CAPACITY;
     *mono_out = cnt[1];
     if (cnt[0] > 0) {
-        MAM_HIP(hipMemcpyAsync(kps, c->d_kps.p, sizeof(mam_keypoint) * cnt[0], hipMemcpyDeviceToHost, c->stream));
-        MAM_HIP(hipMemcpyAsync(desc, c->d_desc.p, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost, c->stream));
-        MAM_HIP(hipStreamSynchronize(c->stream));
+        std::memcpy(kps, c->h_out.p + kp_off, sizeof(mam_keypoint) * (size_t)cnt[0]);
+        std::memcpy(desc, c->h_out.p + desc_off, (size_t)cnt[0] * 32);
     }
     return MAM_OK;
 }
@@ -747,6 +863,21 @@ int mam_orb_debug_candidates(mam_orb_ctx* c, int frame, int level, uint32_t* out
             n++;
         }
     return n;
+}
+
+int mam_orb_debug_set_option(mam_orb_ctx* c, int option, int value) {
+    if (!c) return MAM_ERR_ARG;
+    switch (option) {
+        case MAM_ORB_OPT_DISTRIBUTE_THREADS:
+            if (value != -1 && value != 0 && value != 256 && value != 512 && value != 1024) return MAM_ERR_ARG;
+            c->dist_nt = value;
+            return MAM_OK;
+        case MAM_ORB_OPT_FORK:
+            if (value < -1 || value > 1) return MAM_ERR_ARG;
+            c->fork = value;
+            return MAM_OK;
+        default: return MAM_ERR_ARG;
+    }
 }
 
 int mam_orb_set_profiling(mam_orb_ctx* c, int enable) {

@@ -308,14 +308,15 @@ __global__ __launch_bounds__(256) void k_pyr_down(const Geom* __restrict__ g, in
 // column coefficients stay in registers for the whole level.
 // One level of k_pyr_bands: rows [bl.x, bl.y) of level l from the LDS rows of level l-1 (first row r0, pitch sp);
 // rc = this level's row coefficients {yofs, ibeta0 | ibeta1 << 16} for rows bl.x.. (LDS).
+template <int NT>
 __device__ __forceinline__ void pyr_band_level(const LevelGeom& L, int sh, const uint8_t* src, int sp, int r0,
                                                int4 bl, const int2* rc, uint8_t* lds_dst, bool keep, uint8_t* gdst,
                                                int tid, const PyrQuad& pre) {
     const int dp = (L.w + 3) & ~3;
     const int nq = (L.w + 3) >> 2;
-    const int RG = max(1, 256 / nq);
+    const int RG = max(1, NT / nq);
     const int nrows = bl.y - bl.x;
-    for (int t = tid; t < nq * RG; t += 256) {
+    for (int t = tid; t < nq * RG; t += NT) {
         const int q = t % nq, rg = t / nq;
         PyrQuad c;
         if (t == tid) c = pre;
@@ -345,7 +346,8 @@ __device__ __forceinline__ void pyr_band_level(const LevelGeom& L, int sh, const
 // LDS: [even levels' rows (level 0 staged from the frame)] [odd levels' rows] [row coefficients of every level].
 // The prologue puts everything with a global-memory latency in flight at once (level-0 rows, all row coefficients);
 // each level's column coefficients are fetched into registers while the previous level computes.
-__global__ __launch_bounds__(256) void k_pyr_bands(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ pyr,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pyr_bands(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ pyr,
                                                    const int4* __restrict__ bands, int buf1_off, int rc_off) {
     extern __shared__ __attribute__((aligned(16))) uint8_t pbuf[];
     const int j = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, NL = g->nlevels;
@@ -361,24 +363,24 @@ __global__ __launch_bounds__(256) void k_pyr_bands(const Geom* __restrict__ g, L
             // 8 loads in flight per thread before the LDS stores (a load-store loop would wait out one global
             // latency per word)
             const int wpr = w0 >> 2, nw = nr * wpr;
-            for (int i0 = 0; i0 < nw; i0 += 8 * 256) {
+            for (int i0 = 0; i0 < nw; i0 += 8 * NT) {
                 uint32_t v[8];
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
-                    const int i = i0 + k * 256 + tid;
+                    const int i = i0 + k * NT + tid;
                     const int r = i / wpr, c = i - r * wpr;
                     v[k] = i < nw ? *reinterpret_cast<const uint32_t*>(in + (size_t)(b0.x + r) * s.in_stride + 4 * c)
                                   : 0u;
                 }
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
-                    const int i = i0 + k * 256 + tid;
+                    const int i = i0 + k * NT + tid;
                     const int r = i / wpr, c = i - r * wpr;
                     if (i < nw) *reinterpret_cast<uint32_t*>(pbuf + r * p0 + 4 * c) = v[k];
                 }
             }
         } else {
-            for (int i = tid; i < nr * w0; i += 256) {
+            for (int i = tid; i < nr * w0; i += NT) {
                 const int r = i / w0, c = i - r * w0;
                 pbuf[r * p0 + c] = in[(size_t)(b0.x + r) * s.in_stride + c];
             }
@@ -387,7 +389,7 @@ __global__ __launch_bounds__(256) void k_pyr_bands(const Geom* __restrict__ g, L
         for (int l = 1; l < NL; l++) {
             const LevelGeom& L = g->L[l];
             const int4 bl = B[l];
-            for (int r = tid; r < bl.y - bl.x; r += 256) {
+            for (int r = tid; r < bl.y - bl.x; r += NT) {
                 const int dy = bl.x + r;
                 rcoef[off + r] = make_int2(L.yofs[dy], (L.ibeta[2 * dy] & 0xFFFF) | ((int)L.ibeta[2 * dy + 1] << 16));
             }
@@ -404,7 +406,7 @@ __global__ __launch_bounds__(256) void k_pyr_bands(const Geom* __restrict__ g, L
         const PyrQuad cur = pre;
         if (l + 1 < NL) pyr_quad_setup(g->L[l + 1], 4 * (tid % ((g->L[l + 1].w + 3) >> 2)), 0, pre);
         const uint8_t* src = pbuf + ((l - 1) & 1 ? buf1_off : 0);
-        pyr_band_level(L, g->L[l - 1].h, src, (g->L[l - 1].w + 3) & ~3, B[l - 1].x, bl, rcoef + off,
+        pyr_band_level<NT>(L, g->L[l - 1].h, src, (g->L[l - 1].w + 3) & ~3, B[l - 1].x, bl, rcoef + off,
                        pbuf + (l & 1 ? buf1_off : 0), l + 1 < NL, pyr + L.pyr_off + (size_t)f * L.frame_bytes, tid,
                        cur);
         off += bl.y - bl.x;
@@ -507,7 +509,8 @@ template <int CW>
 __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restrict__ g,
                                                              const CellDesc* __restrict__ cells, LevelSrc s,
                                                              uint32_t* __restrict__ cand,
-                                                             int* __restrict__ cell_counts, int iniTh, int minTh) {
+                                                             int* __restrict__ cell_counts, int iniTh, int minTh,
+                                                             int cell_first) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int T = FAST_THREADS, NW = FAST_THREADS / 64;
 #ifndef MAM_FAST_XCD
@@ -521,6 +524,7 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
         f = logical / gridDim.x;
         cell_i = logical - f * gridDim.x;
     }
+    cell_i += cell_first;   // a launch over the cells [cell_first, cell_first + gridDim.x) of every frame
     const CellDesc c = cells[cell_i];
     const LevelGeom& L = g->L[c.level];
     const int tid = threadIdx.x, lane = lane_id(), w = wave_id();

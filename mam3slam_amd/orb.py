@@ -142,6 +142,14 @@ class ORBextractor:
         names = ["pyramid", "fast", "blur", "distribute", "describe"]
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
 
+    def set_distribute_threads(self, nt: int):
+        """DistributeOctTree kernel width (parity tests / A/B): 256, 512, 1024, 0 (round-3 kernel), -1 automatic."""
+        check(lib().mam_orb_debug_set_option(self._ctx, 1, int(nt)), "mam_orb_debug_set_option")
+
+    def set_fork(self, on: int):
+        """Latency-mode stream fork for up to 4 frames per call: 1 on, 0 off, -1 automatic."""
+        check(lib().mam_orb_debug_set_option(self._ctx, 2, int(on)), "mam_orb_debug_set_option")
+
     def debug_candidates(self, level: int, frame: int = 0) -> np.ndarray:
         n = check(lib().mam_orb_debug_candidates(self._ctx, frame, level, None, 0), "debug_candidates")
         out = np.zeros(max(n, 1), np.uint32)

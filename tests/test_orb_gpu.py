@@ -183,3 +183,79 @@ def test_batch_input_ends_at_last_row(gpu_lib, oracle):
     ko, do, _ = oracle.extract(imgs[F - 1], oracle.params(1000))
     n = int(d_cnt[F - 1, 0])
     assert n == len(ko) and np.array_equal(d_desc[F - 1, :n].cpu().numpy(), do)
+
+
+@pytest.mark.parametrize("nt", [0, 256, 512, 1024])
+def test_distribute_widths_bit_exact(gpu_lib, oracle, nt):
+    """Every DistributeOctTree kernel width (k_distribute2 at 256 / 512 / 1024 threads, the round-3 kernel) gives the
+    oracle's keypoints in the oracle's order, single frames and a 3-frame batch, on every extractor shape (incl. the
+    5x init extractor, whose final phase sorts more than 256 candidates)."""
+    import torch
+
+    from mam3slam_amd.orb import KP_DTYPE
+
+    for w, h, nfeat in CASES:
+        ext = _extractor(nfeat)
+        ext.set_distribute_threads(nt)
+        p = oracle.params(nfeat)
+        imgs = np.stack([synth.make_frame(w, h, agent=5, frame=i) for i in range(3)])
+        ref = [oracle.extract(imgs[i], p) for i in range(3)]
+        kg, dg, mg = ext(imgs[0])
+        _assert_kps_equal(kg, dg, mg, *ref[0], f"nt {nt} {w}x{h}/{nfeat} single")
+        cap = ext.max_keypoints()
+        d_img = torch.from_numpy(imgs).cuda()
+        d_kps = torch.zeros((3, cap * 28), dtype=torch.uint8, device="cuda")
+        d_desc = torch.zeros((3, cap, 32), dtype=torch.uint8, device="cuda")
+        d_cnt = torch.zeros((3, 2), dtype=torch.int32, device="cuda")
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        ext.extract_batch_device(d_img.data_ptr(), 3, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                                 d_cnt.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        cnt = d_cnt.cpu().numpy()
+        kps = d_kps.cpu().numpy().view(KP_DTYPE).reshape(3, cap)
+        desc = d_desc.cpu().numpy()
+        for i in range(3):
+            n = int(cnt[i, 0])
+            _assert_kps_equal(kps[i, :n], desc[i, :n], int(cnt[i, 1]), *ref[i], f"nt {nt} {w}x{h}/{nfeat} batch {i}")
+        ext.close()
+
+
+@pytest.mark.parametrize("fork", [0, 1])
+def test_latency_mode_fork_bit_exact(gpu_lib, oracle, fork):
+    """The latency mode's three-stream dataflow (level 0's FAST + DistributeOctTree beside the pyramid, the blur beside
+    the other levels) and the in-order single stream give the oracle's output: through the host API, and at B = 1 on a
+    device stream captured into a HIP graph (the fork / join events inside the capture) and replayed."""
+    import torch
+
+    from mam3slam_amd.orb import KP_DTYPE
+
+    for w, h, nfeat in CASES[:3]:
+        ext = _extractor(nfeat)
+        ext.set_fork(fork)
+        p = oracle.params(nfeat)
+        imgs = [synth.make_frame(w, h, agent=6, frame=i) for i in range(2)]
+        ref = [oracle.extract(im, p) for im in imgs]
+        for i in range(2):
+            kg, dg, mg = ext(imgs[i])
+            _assert_kps_equal(kg, dg, mg, *ref[i], f"fork {fork} {w}x{h}/{nfeat} host {i}")
+        cap = ext.max_keypoints()
+        d_img = torch.from_numpy(imgs[0]).cuda()
+        d_kps = torch.zeros(cap * 28, dtype=torch.uint8, device="cuda")
+        d_desc = torch.zeros((cap, 32), dtype=torch.uint8, device="cuda")
+        d_cnt = torch.zeros(2, dtype=torch.int32, device="cuda")
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            ext.extract_batch_device(d_img.data_ptr(), 1, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                                     d_cnt.data_ptr(), stream=st.cuda_stream)
+        for i in (1, 0):
+            d_img.copy_(torch.from_numpy(imgs[i]))
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            n = int(d_cnt[0])
+            kps = d_kps.cpu().numpy().view(KP_DTYPE)[:n]
+            _assert_kps_equal(kps, d_desc.cpu().numpy()[:n], int(d_cnt[1]), *ref[i], f"fork {fork} {w}x{h} graph {i}")
+        ext.close()

@@ -138,7 +138,7 @@ def test_motion_search_wider_window_retry(gpu_lib, oracle):
             nlast[f] = nl
             tcw[f, :4], tcw[f, 4:] = pose
         F.pose = pose
-        expect.append(oracle.track_motion_search(F, last, tr.cam, 15.0, True) + (last,))
+        expect.append(oracle.track_motion_search(F, last, tr.cam, 15.0, True) + (last, pose))
     assert [e[2] for e in expect] == [f % 2 == 0 for f in range(B)]
     assert expect[0][0] >= 20 and expect[6][0] < 20
     tr.d_tcw_init.copy_(torch.from_numpy(tcw.view(np.uint8).reshape(-1)).to(dev))
@@ -147,11 +147,23 @@ def test_motion_search_wider_window_retry(gpu_lib, oracle):
     torch.cuda.synchronize()
     nm1 = tr.d_nm1.cpu().numpy()
     pn = tr.d_pn.cpu().numpy()
+    pout = tr.d_pout.cpu().numpy()
+    out1, taken = tr.d_out1.cpu().numpy(), tr.d_taken.cpu().numpy()
     for f in range(B):
         n = int(cnt[f, 0])
-        no, oo, _, last = expect[f]
+        no, oo, _, last, pose = expect[f]
         assert int(nm1[f]) == no, (f, int(nm1[f]), no)
         # PoseOptimization call 1 received the final search's matches
         idx = np.nonzero(oo >= 0)[0]
         keys = scene.make_frame_data(kps[f, :n], desc[f, :n], tr.W, tr.H).keys
-        assert int(pn[0, f]) == len(make_edges(keys, tr.inv_s2, idx, last["pos"][oo[idx]])), f
+        e1 = make_edges(keys, tr.inv_s2, idx, last["pos"][oo[idx]])
+        assert int(pn[0, f]) == len(e1), f
+        _, ol1, _, _ = oracle.pose_optimization_edges(pose, tr.cam, e1)
+        assert np.array_equal(pout[0, f, :len(e1)], ol1), f
+        # index-exact: the retried frames' matches are the th-30 search's (no stale th-15 slot survives), after the
+        # outlier discard (Tracking.cc:2840-2857), and the taken bits are the final search's
+        o1 = oo.copy()
+        o1[idx[ol1 == 1]] = -1
+        assert np.array_equal(out1[f, :n], o1), f
+        tk = ((o1 >= 0) & (last["nobs"][np.maximum(o1, 0)] > 0)).astype(np.uint8)
+        assert np.array_equal(taken[f, :n], tk), f
