@@ -12,7 +12,7 @@
 //           (the next final-phase candidates)                                                       | barrier
 //   remap   every key to its node's new id (computed from the scan results, no per-key table)
 // The final phase's std::sort of (size, UL.x) with libstdc++'s tie behaviour is replayed by one wave
-// (stl_sort_wave) while the other waves run the count pass; the expansion cut (size >= N after an expansion) is a
+// (stl_sort_wave2) while the other waves run the count pass; the expansion cut (size >= N after an expansion) is a
 // wave-level scan over the sorted candidates. Retain-best keeps the first max response in candidate order (:758-776).
 #pragma once
 
@@ -75,11 +75,11 @@ __device__ __forceinline__ int quad2(uint2 r, uint32_t key) {
 }
 
 __host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~(size_t)15; }
-// sort scratch: the wave sort's stack + stopper positions for up to 8 elements per lane
+// sort scratch: the wave sort's stack, stopper positions and move buffer for up to 4 elements per lane
 #define MAM_DIST_SORT_E 4
 __host__ __device__ inline size_t lds_bytes(int NC, int max_cells, int NT) {
     size_t s = a16((size_t)(max_cells + 1) * 4) + a16((size_t)4 * (NT / 64) * 4) + 64 +
-               a16((size_t)MAM_SORT_WAVE_SCRATCH(MAM_DIST_SORT_E) * 4);
+               a16((size_t)MAM_SORT_WAVE2_SCRATCH(MAM_DIST_SORT_E) * 4);
     s += 2 * (a16((size_t)NC * 8) + a16((size_t)NC * 4) + a16((size_t)NC * 4) + a16((size_t)NC * 16));
     s += 3 * a16((size_t)NC * 4) + a16((size_t)NC * 8);
     return s;
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
     int* cellOff = (int*)take((size_t)(g->max_level_cells + 1) * 4);
     uint32_t* part = (uint32_t*)take((size_t)4 * (NT / 64) * 4);
     int* sh = (int*)take(64);
-    int* sortscr = (int*)take((size_t)MAM_SORT_WAVE_SCRATCH(MAM_DIST_SORT_E) * 4);
+    int* sortscr = (int*)take((size_t)MAM_SORT_WAVE2_SCRATCH(MAM_DIST_SORT_E) * 4);
     uint2* rect0 = (uint2*)take((size_t)NC * 8);
     uint32_t* cnt0 = (uint32_t*)take((size_t)NC * 4);
     int* xr0 = (int*)take((size_t)NC * 4);
@@ -254,9 +254,9 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                 __builtin_amdgcn_wave_barrier();
-                if (m <= 64) stl_sort_wave<1>(arr, m, sortscr);
-                else if (m <= 128) stl_sort_wave<2>(arr, m, sortscr);
-                else if (m <= 256) stl_sort_wave<4>(arr, m, sortscr);
+                if (m <= 64) stl_sort_wave2<1>(arr, m, sortscr);
+                else if (m <= 128) stl_sort_wave2<2>(arr, m, sortscr);
+                else if (m <= 256) stl_sort_wave2<4>(arr, m, sortscr);
                 else if (lane == 0) stl_sort(arr, arr + m);
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                 __builtin_amdgcn_wave_barrier();

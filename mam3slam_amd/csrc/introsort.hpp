@@ -13,6 +13,11 @@
 
 #include <stdint.h>
 
+#if !defined(__HIPCC__)
+#include <algorithm>
+#include <vector>
+#endif
+
 #if defined(__HIPCC__)
 #define MAM_HD __host__ __device__ __forceinline__
 #else
@@ -252,6 +257,42 @@ inline void stl_sort_model(SortEl* a, int n) {
     for (int i = 0; i < n; i++) a[i] = tmp[i];
 }
 
+// The same with the final insertion sort restated per leaf: the partitions leave [0, n) tiled by leaves (ranges of at
+// most 16 elements, or heap-sorted ranges), and every key of a leaf is <= every key of a later leaf (a partition puts
+// keys <= pivot left of the cut and keys >= pivot right of it). A stable sort of the whole array therefore equals the
+// leaves stable-sorted one by one in place: an element's final position is its leaf's start + its stable rank inside
+// the leaf (the device's final stage: at most 16 comparisons per element instead of n).
+#if !defined(__HIPCC__)
+inline void stl_sort_model_leaf(SortEl* a, int n) {
+    if (n == 0) return;
+    int sf[64], sl[64], sd[64], sp = 0;
+    std::vector<int> leaf_start;
+    sf[sp] = 0; sl[sp] = n; sd[sp] = sl_lg(n) * 2; ++sp;
+    while (sp > 0) {
+        --sp;
+        int f = sf[sp], l = sl[sp], d = sd[sp];
+        while (l - f > 16) {
+            if (d == 0) { sl_heap_sort(a + f, a + l); break; }
+            --d;
+            const int cut = sl_partition_model(a, f, l);
+            sf[sp] = cut; sl[sp] = l; sd[sp] = d; ++sp;
+            l = cut;
+        }
+        if (f < l) leaf_start.push_back(f);
+    }
+    std::sort(leaf_start.begin(), leaf_start.end());
+    std::vector<SortEl> tmp(a, a + n);
+    for (size_t j = 0; j < leaf_start.size(); j++) {
+        const int s0 = leaf_start[j], s1 = j + 1 < leaf_start.size() ? leaf_start[j + 1] : n;
+        for (int p = s0; p < s1; p++) {
+            int r = 0;
+            for (int q = s0; q < s1; q++) r += sl_less(tmp[q], tmp[p]) || (tmp[q].key == tmp[p].key && q < p);
+            a[s0 + r] = tmp[p];
+        }
+    }
+}
+#endif
+
 #if defined(__HIPCC__)
 // One full wave sorts arr[0, n) (n <= 64 * E, in LDS) exactly like stl_sort: E elements per lane in registers
 // (position e * 64 + lane), the stoppers of each partition found by ballot and paired through LDS by rank. Ranges
@@ -434,6 +475,229 @@ __device__ __forceinline__ void stl_sort_wave(SortEl* arr, int n, int* scratch) 
     for (int e = 0; e < E; e++) {
         if (e * 64 + lane < n) { arr[r[e]].key = key[e]; arr[r[e]].val = val[e]; }
     }
+}
+
+// stl_sort_wave's partitions with two LDS round trips each (both stopper pairings read at once, the elements moved by
+// an LDS scatter to their destinations instead of per-slot shuffles, the cut found by ballots) and the final insertion
+// sort per leaf (stl_sort_model_leaf): each element ranked against the at most 16 elements of its leaf. Same result.
+// scratch: LDS, >= MAM_SORT_WAVE2_SCRATCH(E) ints, private to this wave.
+#define MAM_SORT_WAVE2_SCRATCH(E) (3 * 24 + 4 * 64 * (E))
+template <int E>
+__device__ __forceinline__ void stl_sort_wave2(SortEl* arr, int n, int* scratch) {
+    const int lane = threadIdx.x & 63;
+    if (n <= 1) return;
+    int* const stack = scratch;
+    int* const Lpos = scratch + 72;
+    int* const Rpos = Lpos + 64 * E;
+    SortEl* const tmp = reinterpret_cast<SortEl*>(Rpos + 64 * E);
+    uint32_t key[E], val[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int p = e * 64 + lane;
+        key[e] = p < n ? arr[p].key : 0xFFFFFFFFu;
+        val[e] = p < n ? arr[p].val : 0u;
+    }
+    auto key_at = [&](int p) -> uint32_t {   // wave-uniform position
+        uint32_t r = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            if ((p >> 6) == e) r = (uint32_t)__builtin_amdgcn_readlane((int)key[e], p & 63);
+        return r;
+    };
+    auto val_at = [&](int p) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            if ((p >> 6) == e) r = (uint32_t)__builtin_amdgcn_readlane((int)val[e], p & 63);
+        return r;
+    };
+    // position of the first set bit of a wave-uniform (64 E)-bit mask (-1 if none)
+    auto first_bit = [&](const uint64_t* m) -> int {
+        int r = -1;
+#pragma unroll
+        for (int e = E - 1; e >= 0; e--)
+            if (m[e]) r = 64 * e + __ffsll((unsigned long long)m[e]) - 1;
+        return r;
+    };
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint64_t above = ~(below | (1ull << lane));
+    uint64_t leaf[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) leaf[e] = 0;
+    int sp = 0;
+    int cf = 0, cl = n, cd = sl_lg(n) * 2;
+    while (true) {
+        while (cl - cf > 16) {
+            if (cd == 0) {   // depth budget spent: lane 0 heap-sorts the range in LDS (stl_sort's operations)
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int p = e * 64 + lane;
+                    if (p < n) { arr[p].key = key[e]; arr[p].val = val[e]; }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) sl_heap_sort(arr + cf, arr + cl);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int p = e * 64 + lane;
+                    if (p < n) { key[e] = arr[p].key; val[e] = arr[p].val; }
+                }
+                break;
+            }
+            --cd;
+            // __move_median_to_first(first, first + 1, mid, last - 1)
+            const int mid = cf + (cl - cf) / 2;
+            const uint32_t ka = key_at(cf + 1), kb = key_at(mid), kc = key_at(cl - 1);
+            int sw;
+            if (ka < kb) sw = kb < kc ? mid : (ka < kc ? cl - 1 : cf + 1);
+            else sw = ka < kc ? cf + 1 : (kb < kc ? cl - 1 : mid);
+            const uint32_t kf = key_at(cf), vf = val_at(cf), ks = key_at(sw), vs = val_at(sw);
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int p = e * 64 + lane;
+                if (p == cf) { key[e] = ks; val[e] = vs; }
+                else if (p == sw) { key[e] = kf; val[e] = vf; }
+            }
+            const uint32_t pv = ks;
+            uint64_t mL[E], mR[E];
+            bool isL[E], isR[E];
+            int nl = 0, nr = 0;
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int p = e * 64 + lane;
+                const bool inr = p > cf && p < cl;
+                isL[e] = inr && !(key[e] < pv);                    // left scan stops here
+                isR[e] = (inr && !(pv < key[e])) || p == cf;       // right scan stops here (pivot = sentinel)
+                mL[e] = __ballot(isL[e]);
+                mR[e] = __ballot(isR[e]);
+                nl += __popcll(mL[e]);
+                nr += __popcll(mR[e]);
+            }
+            int rankL[E], rankR[E];
+            {
+                int lo = 0;
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    rankL[e] = lo + __popcll(mL[e] & below);        // k-th from the left
+                    lo += __popcll(mL[e]);
+                }
+                int hi = 0;
+#pragma unroll
+                for (int e = E - 1; e >= 0; e--) {
+                    rankR[e] = hi + __popcll(mR[e] & above);        // k-th from the right
+                    hi += __popcll(mR[e]);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                if (isL[e]) Lpos[rankL[e]] = e * 64 + lane;
+                if (isR[e]) Rpos[rankR[e]] = e * 64 + lane;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            // both pairings read at once: L_k's partner R_k, R_k's partner L_k; swap k happens iff L_k < R_k (monotone
+            // in k, so the swaps are k < K)
+            int dst[E];
+            int K = 0;
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int p = e * 64 + lane;
+                const int pl = (isL[e] && rankL[e] < nr) ? Rpos[rankL[e]] : -1;
+                const int pr = (isR[e] && rankR[e] < nl) ? Lpos[rankR[e]] : -1;
+                const bool swapL = pl > p;
+                K += __popcll(__ballot(swapL));
+                dst[e] = swapL ? pl : (pr >= 0 ? -2 - pr : p);   // R stoppers decided once K is known
+            }
+            uint64_t mK[E], mKR[E], mL0[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                if (dst[e] <= -2) dst[e] = rankR[e] < K ? -2 - dst[e] : e * 64 + lane;
+                mK[e] = __ballot(isL[e] && rankL[e] == K);          // L_K
+                mKR[e] = __ballot(isR[e] && rankR[e] == K - 1);     // R_{K-1}
+                mL0[e] = mL[e];
+            }
+            // returned cut: L_0 if no swap, else min(L_K, R_{K-1}) (L_K absent -> R_{K-1})
+            int cut;
+            if (K == 0) cut = first_bit(mL0);
+            else {
+                const int rk = first_bit(mKR);
+                const int lk = K < nl ? first_bit(mK) : -1;
+                cut = (lk >= 0 && lk < rk) ? lk : rk;
+            }
+            // move every element to its destination through LDS
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int p = e * 64 + lane;
+                if (p < n) { tmp[dst[e]].key = key[e]; tmp[dst[e]].val = val[e]; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int p = e * 64 + lane;
+                if (p < n) { key[e] = tmp[p].key; val[e] = tmp[p].val; }
+            }
+            if (lane == 0) { stack[3 * sp] = cut; stack[3 * sp + 1] = cl; stack[3 * sp + 2] = cd; }
+            ++sp;
+            cl = cut;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (cf < cl) {   // [cf, cl) is a leaf
+#pragma unroll
+            for (int e = 0; e < E; e++)
+                if ((cf >> 6) == e) leaf[e] |= 1ull << (cf & 63);
+        }
+        if (sp == 0) break;
+        --sp;
+        cf = stack[3 * sp];
+        cl = stack[3 * sp + 1];
+        cd = stack[3 * sp + 2];
+    }
+    // final insertion sort, per leaf: position = leaf start + stable rank inside the leaf
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int p = e * 64 + lane;
+        if (p < n) { tmp[p].key = key[e]; tmp[p].val = val[e]; }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int dpos[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int p = e * 64 + lane;
+        dpos[e] = -1;
+        if (p < n) {
+            int s0 = 0, s1 = n;   // leaf [s0, s1) holding p: last leaf start <= p, first leaf start > p
+#pragma unroll
+            for (int e2 = 0; e2 < E; e2++) {
+                uint64_t m = leaf[e2];
+                const int o = p - 64 * e2;
+                if (o < 0) m = 0;
+                else if (o < 63) m &= (2ull << o) - 1ull;
+                if (m) s0 = 64 * e2 + 63 - __clzll((long long)m);
+            }
+#pragma unroll
+            for (int e2 = E - 1; e2 >= 0; e2--) {
+                uint64_t m = leaf[e2];
+                const int o = p - 64 * e2;
+                if (o >= 63) m = 0;
+                else if (o >= 0) m &= ~((2ull << o) - 1ull);
+                if (m) s1 = 64 * e2 + __ffsll((unsigned long long)m) - 1;
+            }
+            int r = 0;
+            for (int q = s0; q < s1; q++) {
+                const uint32_t kq = tmp[q].key;
+                r += (kq < key[e]) || (kq == key[e] && q < p);
+            }
+            dpos[e] = s0 + r;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (dpos[e] >= 0) { arr[dpos[e]].key = key[e]; arr[dpos[e]].val = val[e]; }
 }
 #endif
 

@@ -1,0 +1,39 @@
+#!/bin/bash
+# One GPU session of several parts (PARTS="orb lat lone bench" by default): the ORB parity tests + the motion retry
+# test, the single-frame extraction latency and its kernel trace, the lone LocalBundleAdjustment trace, a c1 bench line.
+# Every step under its own time limit; the session stops at the first failure.
+set -u
+R=${GRAFT_REPO_ROOT:-/root/repo}
+O=$R/gpurun_out/sess
+mkdir -p $O
+export TMPDIR=/tmp
+for part in ${PARTS:-orb lat lone bench}; do
+  echo "=== $part"
+  case $part in
+    orb)
+      cd $R && timeout -k 10 700 python -u -m pytest ${TESTS:-tests/test_orb_gpu.py tests/test_track_gpu.py} -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+      st=$?; tail -12 $O/pytest.log; [ $st -eq 0 ] || exit $st ;;
+    lat)
+      cd /tmp && timeout -k 10 300 python3 -u $R/scripts/extract_latency.py --out $O/latency.json > $O/latency.log 2>&1 || { cat $O/latency.log; exit 1; }
+      cat $O/latency.log
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_lat -o run -- python3 -u $R/scripts/extract_latency.py --reps 50 --configs c1,c2 > $O/prof_lat.log 2>&1 || { tail -20 $O/prof_lat.log; exit 1; }
+      python3 - $O/prof_lat/run_kernel_stats.csv <<'PY'
+import csv, sys
+for x in list(csv.DictReader(open(sys.argv[1])))[:14]:
+    print(x["Name"][:58].ljust(58), x["Calls"].rjust(6), "%8.1f avg" % (float(x["AverageNs"]) / 1e3), "%8.1f min" % (float(x["MinNs"]) / 1e3), "%8.1f max" % (float(x["MaxNs"]) / 1e3))
+PY
+      ;;
+    lone)
+      cd /tmp && timeout -k 10 300 python3 $R/scripts/lba_bench.py --world --solves 10 > $O/lone_bench.json 2> $O/lone_bench.err || { tail -20 $O/lone_bench.err; exit 1; }
+      head -c 600 $O/lone_bench.json; echo
+      timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $O/prof_lone -o run -- python3 $R/scripts/lba_bench.py --world --solves 6 > $O/prof_lone.log 2>&1 || { tail -20 $O/prof_lone.log; exit 1; }
+      python3 $R/scripts/lone_trace.py $O/prof_lone/run_kernel_trace.csv --skip 2 | tee $O/lone_trace.txt | tail -30 ;;
+    bench)
+      cd $R && timeout -k 10 600 python3 bench.py --config ${BENCH_CONFIG:-c1} ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+      python3 -c "
+import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1])
+print('value', d['value'], 'ms/step', d['ms_per_step'], 'parity_ok', d.get('parity_ok'))
+print('latency', d.get('latency')); print('north_star', {k: v for k, v in (d.get('north_star') or {}).items() if k != 'note'})
+print('stage', d.get('stage_ms_per_step'))" ;;
+  esac
+done

@@ -25,9 +25,10 @@ int main() {
                       [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
                           return a.first < b.first;
                       });
-            std::vector<mam::SortEl> par(emu);
+            std::vector<mam::SortEl> par(emu), leaf(emu);
             mam::stl_sort(emu.data(), emu.data() + n);
             mam::stl_sort_model(par.data(), n);   // data-parallel formulation (device wave sort)
+            mam::stl_sort_model_leaf(leaf.data(), n);   // ... with the per-leaf final stage (stl_sort_wave2)
             for (int i = 0; i < n; i++) {
                 if (ref[i].first != emu[i].key || ref[i].second != emu[i].val) {
                     printf("MISMATCH trial=%d n=%d i=%d\n", trial, n, i);
@@ -35,6 +36,10 @@ int main() {
                 }
                 if (ref[i].first != par[i].key || ref[i].second != par[i].val) {
                     printf("MODEL MISMATCH trial=%d n=%d i=%d\n", trial, n, i);
+                    return 1;
+                }
+                if (ref[i].first != leaf[i].key || ref[i].second != leaf[i].val) {
+                    printf("LEAF MODEL MISMATCH trial=%d n=%d i=%d\n", trial, n, i);
                     return 1;
                 }
             }
