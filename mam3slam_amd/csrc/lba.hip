@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <numeric>
 #include <string>
@@ -2937,6 +2938,8 @@ struct mam_lba_ctx {
     mam::StageTimer timer{4};
     DevBuf<uint8_t> arena;        // per-problem structure, state and scratch of the current batch
     DevBuf<uint8_t> io;           // host API: inputs + outputs of the one problem
+    hipStream_t up_stream = nullptr;   // host API: the observations' upload beside the structure build
+    hipEvent_t up_done = nullptr;
     DevBuf<uint8_t> hdr;          // Prob[Q] | LM[Q] | Outs[Q] of the current batch
     DevBuf<int2> blk_pairs;       // the S blocks' landmark pairs of the current batch
     static constexpr int kMaxGroups = 4;
@@ -3077,8 +3080,12 @@ namespace {
 // The shared driver: Q problems whose inputs (id-ordered) are already in device memory, described by hp[q] (input
 // pointers, dimensions, delta, iterations in lm0[q]). Builds the structure on the device, runs the LM slots, writes
 // the outputs and fills the host-side scalars of res[q] (iterations, trials, chi2s, status).
+// before_lin (may be empty): called once the structure build is enqueued, before the first linearisation; it may
+// enqueue work the linearisation needs (mam_lba_solve: the observations' upload, overlapped with the build) and
+// returns an event the stream then waits on (nullptr: none) or sets rc.
 int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const std::vector<Outs>& outs,
-              const volatile uint8_t* stop_flag, hipStream_t s, mam_lba_result* res) {
+              const volatile uint8_t* stop_flag, hipStream_t s, mam_lba_result* res,
+              const std::function<hipEvent_t(int*)>& before_lin = {}) {
     using namespace mam::lba;
     const int Q = (int)hp.size();
     if (Q == 0) return MAM_OK;
@@ -3196,6 +3203,12 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         // iteration 0's linearisation and system at the initial state (lambda_0 needs its max |diag(H)|), the initial
         // chi2; the first trial's k_point_sys then starts from this system
         const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
+        if (before_lin) {
+            int rc = MAM_OK;
+            const hipEvent_t ev = before_lin(&rc);
+            if (rc) return rc;
+            if (ev) MAM_HIP(hipStreamWaitEvent(s, ev, 0));
+        }
         hipLaunchKernelGGL(k_linearize, gE64, dim3(EW), 0, s, P);
         hipLaunchKernelGGL(k_sys, gSys, dim3(64), 0, s, P);
         hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
@@ -3390,7 +3403,10 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
         stat = (fa.sharedSizeBytes + 255) / 256 * 256 + 256;
     else
         (void)hipGetLastError();
-    for (size_t budget : {(size_t)160 * 1024 - stat, (size_t)64 * 1024 - stat}) {
+    // MAM_LBA_LDS_KB=<k> caps the budget (experiments: a factorization that leaves room on its CU for other work)
+    size_t cap_kb = 160;
+    if (const char* lk = std::getenv("MAM_LBA_LDS_KB")) cap_kb = std::max<size_t>(16, std::min<size_t>(160, (size_t)atoi(lk)));
+    for (size_t budget : {cap_kb * 1024 - stat, (size_t)64 * 1024 - stat}) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_any<true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess &&
             hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_any<false>),
@@ -3429,6 +3445,11 @@ void mam_lba_destroy(mam_lba_ctx* c) {
     for (auto& e : c->ev_done)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    if (c->up_stream) {
+        (void)hipStreamSynchronize(c->up_stream);
+        (void)hipStreamDestroy(c->up_stream);
+    }
+    if (c->up_done) (void)hipEventDestroy(c->up_done);
     delete c;
 }
 
@@ -3490,10 +3511,10 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         T* d = dv.take<T>(count);
         return std::make_pair(d, reinterpret_cast<T*>(hb + (reinterpret_cast<uint8_t*>(d) - c->io.p)));
     };
+    // two upload parts: what the structure build reads (edges' vertices, poses, points), then the observations and
+    // their weights (read first by the linearisation), staged and copied while the GPU builds the structure
     auto [d_ep, h_ep] = put((int32_t*)nullptr, E);
     auto [d_eo, h_eo] = put((int32_t*)nullptr, E);
-    auto [d_obs, h_obs] = put((double*)nullptr, 2 * (size_t)E);
-    auto [d_w, h_w] = put((double*)nullptr, E);
     auto [d_act, h_act] = put((uint8_t*)nullptr, E);
     auto [d_cams, h_cams] = put((float*)nullptr, ncw);
     auto [d_pc, h_pc] = put((int32_t*)nullptr, P);
@@ -3501,6 +3522,9 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     auto [d_q, h_q] = put((double*)nullptr, 4 * (size_t)P);
     auto [d_t, h_t] = put((double*)nullptr, 3 * (size_t)P);
     auto [d_x, h_x] = put((double*)nullptr, 3 * (size_t)L);
+    const size_t upload_a = dv.off;
+    auto [d_obs, h_obs] = put((double*)nullptr, 2 * (size_t)E);
+    auto [d_w, h_w] = put((double*)nullptr, E);
     const size_t upload = dv.off;
     // staging: plain copies when the ids are already in Hessian order, permuted copies otherwise
     if (E) {
@@ -3508,8 +3532,6 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
         else for (int e = 0; e < E; e++) h_ep[e] = ipl[p->edge_point[e]];
         if (ident_po) std::memcpy(h_eo, p->edge_pose, sizeof(int32_t) * E);
         else for (int e = 0; e < E; e++) h_eo[e] = ipo[p->edge_pose[e]];
-        std::memcpy(h_obs, p->edge_obs, sizeof(double) * 2 * (size_t)E);
-        std::memcpy(h_w, p->edge_inv_sigma2, sizeof(double) * E);
         if (p->edge_active) std::memcpy(h_act, p->edge_active, E);
     }
     std::memcpy(h_cams, p->cams, sizeof(float) * ncw);
@@ -3531,7 +3553,34 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     o.chi2 = r->edge_chi2 ? dv.take<double>(E) : nullptr;
     o.depth = r->edge_depth_ok ? dv.take<uint8_t>(E) : nullptr;
     hipStream_t s = c->stream;
-    if (upload) MAM_HIP(hipMemcpyAsync(c->io.p, hb, upload, hipMemcpyHostToDevice, s));
+    if (upload_a) MAM_HIP(hipMemcpyAsync(c->io.p, hb, upload_a, hipMemcpyHostToDevice, s));
+    // part two, once the structure build is enqueued: host staging copy (overlapping the GPU's build), then its upload
+    // on the upload stream, which the linearisation waits for
+    double* const hobs = h_obs;   // (structured bindings cannot be captured in C++17)
+    double* const hw = h_w;
+    auto upload_b = [&, hobs, hw](int* rc) -> hipEvent_t {
+        if (E) {
+            std::memcpy(hobs, p->edge_obs, sizeof(double) * 2 * (size_t)E);
+            std::memcpy(hw, p->edge_inv_sigma2, sizeof(double) * E);
+        }
+        if (upload == upload_a) return nullptr;
+        if (!c->up_stream) {
+            if (hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&c->up_done, hipEventDisableTiming) != hipSuccess) {
+                mam::set_last_error("LBA upload stream");
+                *rc = MAM_ERR_DEVICE;
+                return nullptr;
+            }
+        }
+        if (hipMemcpyAsync(c->io.p + upload_a, hb + upload_a, upload - upload_a, hipMemcpyHostToDevice, c->up_stream) !=
+                hipSuccess ||
+            hipEventRecord(c->up_done, c->up_stream) != hipSuccess) {
+            mam::set_last_error("LBA observation upload");
+            *rc = MAM_ERR_DEVICE;
+            return nullptr;
+        }
+        return c->up_done;
+    };
     mam_lba_problem pd = *p;
     pd.edge_point = d_ep;
     pd.edge_pose = d_eo;
@@ -3550,7 +3599,7 @@ int mam_lba_solve(mam_lba_ctx* c, const mam_lba_problem* p, const volatile uint8
     std::memset(lm0.data(), 0, sizeof(LM));
     lm0[0].iterations = p->iterations;
     std::vector<Outs> outs{o};
-    if (int rc = run_batch(c, hp, lm0, outs, stop_flag, s, r)) return rc;
+    if (int rc = run_batch(c, hp, lm0, outs, stop_flag, s, r, upload_b)) return rc;
     // results back to the caller's order: one D2H copy of the output region into the pinned staging block (pageable
     // destinations were one staged, synchronous copy each)
     if (dv.off > upload) MAM_HIP(hipMemcpyAsync(hb + upload, c->io.p + upload, dv.off - upload, hipMemcpyDeviceToHost, s));

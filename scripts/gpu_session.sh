@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/sess
 mkdir -p $O
 export TMPDIR=/tmp
-for part in ${PARTS:-orb lat lone bench}; do
+for part in ${PARTS:-orb lat lone bench bench2}; do
   echo "=== $part"
   case $part in
     orb)
@@ -28,12 +28,13 @@ PY
       head -c 600 $O/lone_bench.json; echo
       timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $O/prof_lone -o run -- python3 $R/scripts/lba_bench.py --world --solves 6 > $O/prof_lone.log 2>&1 || { tail -20 $O/prof_lone.log; exit 1; }
       python3 $R/scripts/lone_trace.py $O/prof_lone/run_kernel_trace.csv --skip 2 | tee $O/lone_trace.txt | tail -30 ;;
-    bench)
-      cd $R && timeout -k 10 600 python3 bench.py --config ${BENCH_CONFIG:-c1} ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+    bench|bench2)
+      cfg=c1; [ $part = bench2 ] && cfg=c2
+      cd $R && timeout -k 10 600 python3 bench.py --config $cfg ${BENCH_ARGS:-} > $O/bench_$cfg.json 2> $O/bench_$cfg.err || { tail -20 $O/bench_$cfg.err; exit 1; }
       python3 -c "
-import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1])
+import json; d=json.loads(open('$O/bench_$cfg.json').read().strip().splitlines()[-1])
 print('value', d['value'], 'ms/step', d['ms_per_step'], 'parity_ok', d.get('parity_ok'))
 print('latency', d.get('latency')); print('north_star', {k: v for k, v in (d.get('north_star') or {}).items() if k != 'note'})
-print('stage', d.get('stage_ms_per_step'))" ;;
+print('stage', d.get('stage_ms_per_step')); print('overlap', d.get('overlap')); print('pose', (d.get('pose_optimization') or {}).get('ms_single_frame_launch'))" ;;
   esac
 done
