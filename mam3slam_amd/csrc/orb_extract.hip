@@ -80,6 +80,14 @@ struct mam_orb_ctx {
     hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_side[2] = {nullptr, nullptr};
     int dist_kcap = 0;   // candidates per level k_distribute keeps in LDS (more: global scratch)
     int fast_cw = 0;   // k_fast_cells plane pitch instance
+    // k_fast_chunks (cells of a row in chunks of up to FAST_G): chunk table, plane pitch instance, LDS, first chunk of
+    // each level
+    std::vector<mam::ChunkDesc> chunks;
+    DevBuf<mam::ChunkDesc> d_chunks;
+    int fastc_cw = 0;
+    size_t fastc_lds = 0;
+    int chunk_base[MAM_MAX_LEVELS + 1] = {};
+    int fast_chunks = -1;   // k_fast_chunks instead of k_fast_cells (mam_orb_debug_set_option), -1 = automatic
     // single-launch pyramid (k_pyr_bands): per band count, the band table and its LDS carve
     struct PyrPlan {
         int nb = 0;
@@ -366,6 +374,46 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
             if (cw >= mam::fast_min_cw(cmax)) { c->fast_cw = cw; break; }
         if (c->fast_cw == 0) { g_last_error = "FAST cell too wide"; return MAM_ERR_ARG; }
         c->fast_lds = mam::fast_lds_bytes(rmax, c->fast_cw);
+        // chunks: consecutive cells of one row (the cells table lists a row's cells in column order)
+        c->chunks.clear();
+        int chunk_cols = 0;
+        for (int l = 0; l < L; l++) {
+            c->chunk_base[l] = (int)c->chunks.size();
+            const mam::LevelGeom& lv = g.L[l];
+            for (int i0 = lv.cell_base; i0 < lv.cell_base + lv.ncells;) {
+                int i1 = i0 + 1;
+                while (i1 < lv.cell_base + lv.ncells && i1 - i0 < mam::FAST_G && c->cells[i1].ci == c->cells[i0].ci &&
+                       c->cells[i1].cj == c->cells[i1 - 1].cj + 1)
+                    i1++;
+                mam::ChunkDesc ch;
+                ch.level = l;
+                ch.cell0 = i0;
+                ch.ncell = i1 - i0;
+                ch.x0 = c->cells[i0].x0; ch.y0 = c->cells[i0].y0;
+                ch.x1 = c->cells[i1 - 1].x1; ch.y1 = c->cells[i0].y1;
+                ch.ci = c->cells[i0].ci; ch.cj0 = c->cells[i0].cj;
+                chunk_cols = std::max(chunk_cols, ch.x1 - ch.x0);
+                c->chunks.push_back(ch);
+                i0 = i1;
+            }
+        }
+        c->chunk_base[L] = (int)c->chunks.size();
+        c->fastc_cw = 0;
+        for (int cw : {64, 80, 96, 112, 128, 160})
+            if (cw >= mam::fast_min_cw(chunk_cols)) { c->fastc_cw = cw; break; }
+        c->fastc_lds = c->fastc_cw ? mam::fastc_lds_bytes(rmax, c->fastc_cw) : 0;
+        if (c->fastc_lds > 160 * 1024) c->fastc_cw = 0;   // (no chunk kernel for this geometry: k_fast_cells)
+        if (int rc = c->d_chunks.alloc(std::max<size_t>(c->chunks.size(), 1))) return rc;
+        if (!c->chunks.empty())
+            MAM_HIP(hipMemcpy(c->d_chunks.p, c->chunks.data(), c->chunks.size() * sizeof(mam::ChunkDesc),
+                              hipMemcpyHostToDevice));
+        for (const void* fn : {reinterpret_cast<const void*>(&mam::k_fast_chunks<64>),
+                               reinterpret_cast<const void*>(&mam::k_fast_chunks<80>),
+                               reinterpret_cast<const void*>(&mam::k_fast_chunks<96>),
+                               reinterpret_cast<const void*>(&mam::k_fast_chunks<112>),
+                               reinterpret_cast<const void*>(&mam::k_fast_chunks<128>),
+                               reinterpret_cast<const void*>(&mam::k_fast_chunks<160>)})
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         {
             const int max_pairs = std::max(rmax - 6, 0) * ((std::max(cmax - 6, 0) + 1) / 2);
             if ((max_pairs + mam::FAST_THREADS - 1) / mam::FAST_THREADS * (mam::FAST_THREADS / 64) >
@@ -532,6 +580,17 @@ int dist_threads(const mam_orb_ctx* c, int F) {
     return F <= 4 ? 1024 : 256;
 }
 
+// k_fast_chunks for every launch (MAM_FAST_CHUNKS=1 / the context option; default off until measured), when the
+// geometry has a chunk plane pitch
+bool fast_chunks_enabled(const mam_orb_ctx* c) {
+    static const int env = [] {
+        const char* e = getenv("MAM_FAST_CHUNKS");
+        return e ? atoi(e) : -1;
+    }();
+    const int v = c->fast_chunks >= 0 ? c->fast_chunks : env;
+    return v == 1 && c->fastc_cw > 0;
+}
+
 // Latency mode (run_pipeline's three-stream dataflow) for up to 4 frames per call; MAM_ORB_FORK=0 / the context
 // option turn it off (one stream, stages in order).
 bool fork_enabled(const mam_orb_ctx* c, int F, int nt) {
@@ -590,6 +649,27 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
                                         c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast, cell_first); break;
         }
     };
+    const bool chunked = fast_chunks_enabled(c);
+    // FAST over the cells of levels [l0, l1)
+    auto launch_fast_levels = [&](hipStream_t st, int l0, int l1) {
+        if (chunked) {
+            const int c0 = c->chunk_base[l0], n = c->chunk_base[l1] - c0;
+            if (n <= 0) return;
+            const dim3 fg(n, F), fb(mam::FAST_THREADS);
+#define MAM_FASTC(CW_)                                                                                                \
+    case CW_: hipLaunchKernelGGL(mam::k_fast_chunks<CW_>, fg, fb, c->fastc_lds, st, c->d_geom.p, c->d_chunks.p,       \
+                                 c->d_cells.p, src, c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast,                 \
+                                 c->prm.min_th_fast, c0); break
+            switch (c->fastc_cw) {
+                MAM_FASTC(64); MAM_FASTC(80); MAM_FASTC(96); MAM_FASTC(112); MAM_FASTC(128); MAM_FASTC(160);
+                default: break;
+            }
+#undef MAM_FASTC
+            return;
+        }
+        const int cf = g.L[l0].cell_base, cl = l1 < L ? g.L[l1].cell_base : g.cells_per_frame;
+        launch_fast(st, cf, cl - cf);
+    };
     const int nt = dist_threads(c, F);
     auto launch_dist = [&](hipStream_t st, int l_first, int nl) {
         if (nt == 0) {   // the round-3 kernel (all levels)
@@ -618,7 +698,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
         //   side B: [pyramid] -> blur (all levels)
         MAM_HIP(hipEventRecord(c->ev_fork, s));
         MAM_HIP(hipStreamWaitEvent(c->side[0], c->ev_fork, 0));
-        launch_fast(c->side[0], 0, g.L[0].ncells);
+        launch_fast_levels(c->side[0], 0, 1);
         launch_dist(c->side[0], 0, 1);
         MAM_HIP(hipEventRecord(c->ev_side[0], c->side[0]));
         launch_pyramid(s);
@@ -628,7 +708,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
                            c->side[1], c->d_geom.p, src, c->d_blur.p);
         MAM_HIP(hipEventRecord(c->ev_side[1], c->side[1]));
         if (L > 1) {
-            launch_fast(s, g.L[1].cell_base, g.cells_per_frame - g.L[1].cell_base);
+            launch_fast_levels(s, 1, L);
             launch_dist(s, 1, L - 1);
         }
         MAM_HIP(hipStreamWaitEvent(s, c->ev_side[0], 0));
@@ -647,7 +727,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
         }
         {
             StageScope sc(&c->timer, s, MAM_STAGE_FAST);
-            launch_fast(s, 0, g.cells_per_frame);
+            launch_fast_levels(s, 0, L);
         }
         {
             StageScope sc(&c->timer, s, MAM_STAGE_DISTRIBUTE);
@@ -723,7 +803,7 @@ void mam_orb_destroy(mam_orb_ctx* c) {
     if (!c) return;
     ::mam::DeviceScope mam_dev_scope_(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    c->d_geom.release(); c->d_cells.release(); c->d_tabs_i.release(); c->d_tabs_s.release();
+    c->d_geom.release(); c->d_cells.release(); c->d_chunks.release(); c->d_tabs_i.release(); c->d_tabs_s.release();
     c->d_pyr.release(); c->d_blur.release(); c->d_input.release();
     c->d_cand.release(); c->d_keys.release(); c->d_okey.release(); c->d_orank.release(); c->d_knode.release(); c->d_knode32.release();
     c->d_cellcnt.release(); c->d_lvlcnt.release(); c->d_kps.release(); c->d_desc.release(); c->d_counts.release(); c->d_out.release();
@@ -871,6 +951,10 @@ int mam_orb_debug_set_option(mam_orb_ctx* c, int option, int value) {
         case MAM_ORB_OPT_DISTRIBUTE_THREADS:
             if (value != -1 && value != 0 && value != 256 && value != 512 && value != 1024) return MAM_ERR_ARG;
             c->dist_nt = value;
+            return MAM_OK;
+        case MAM_ORB_OPT_FAST_CHUNKS:
+            if (value < -1 || value > 1) return MAM_ERR_ARG;
+            c->fast_chunks = value;
             return MAM_OK;
         case MAM_ORB_OPT_FORK:
             if (value < -1 || value > 1) return MAM_ERR_ARG;

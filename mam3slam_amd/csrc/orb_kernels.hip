@@ -700,6 +700,236 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
     if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = use_hi ? tot_hi : tot_lo;
 }
 
+// ---- FAST over chunks of a cell row (the band formulation): one workgroup per (frame, chunk of up to FAST_G
+// consecutive cells of one cell row). The cells of a row share their ROI rows and their detection columns tile the
+// row, so the chunk stages its ROI once (the cells' 6-pixel overlaps read once), computes the strength of every
+// pixel once, then per cell: NMS with the neighbours outside the cell's detection area as 0 (cv::FAST on the cell
+// ROI scores nothing outside it), the iniThFAST / minThFAST choice from the cell's counts and the cell's candidates
+// in row-major order into its own slots — exactly k_fast_cells' outputs.
+constexpr int FAST_G = 4;
+struct ChunkDesc {
+    int level;
+    int cell0, ncell;   // first cell (index into the frame's cell table) and cells in the chunk (<= FAST_G)
+    int x0, y0, x1, y1; // ROI: the first cell's x0 .. the last cell's x1, the row's y0 .. y1
+    int ci, cj0;        // cell row, column of the first cell
+};
+__host__ __device__ inline size_t fastc_off_s(int rmax, int cw) { return fast_align16((size_t)rmax * 2 * cw * 4); }
+__host__ __device__ inline size_t fastc_off_pk(int rmax, int cw) {
+    return fastc_off_s(rmax, cw) + fast_align16((size_t)(rmax - 4) * cw * 4);
+}
+__host__ __device__ inline int fastc_max_entries(int rmax, int cw) {
+    const int np = (rmax - 6) * (cw - 2);
+    return (np + FAST_THREADS - 1) / FAST_THREADS * (FAST_THREADS / 64) * FAST_G;
+}
+__host__ __device__ inline size_t fastc_off_cnt(int rmax, int cw) {
+    return fastc_off_pk(rmax, cw) + fast_align16((size_t)(rmax - 6) * cw * 2);
+}
+__host__ __device__ inline size_t fastc_lds_bytes(int rmax, int cw) {
+    return fastc_off_cnt(rmax, cw) + (size_t)fastc_max_entries(rmax, cw) * 4;
+}
+
+template <int CW>
+__global__ __launch_bounds__(FAST_THREADS) void k_fast_chunks(const Geom* __restrict__ g,
+                                                              const ChunkDesc* __restrict__ chunks,
+                                                              const CellDesc* __restrict__ cells, LevelSrc s,
+                                                              uint32_t* __restrict__ cand,
+                                                              int* __restrict__ cell_counts, int iniTh, int minTh,
+                                                              int chunk_first) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int T = FAST_THREADS, NW = FAST_THREADS / 64;
+    int ch_i = blockIdx.x, f = blockIdx.y;
+    {
+        const int logical = xcd_logical(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+        f = logical / gridDim.x;
+        ch_i = logical - f * gridDim.x;
+    }
+    const ChunkDesc c = chunks[chunk_first + ch_i];
+    const LevelGeom& L = g->L[c.level];
+    const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+    int pitch;
+    const uint8_t* lev = level_ptr(g, s, f, c.level, &pitch);
+    const int rows = c.y1 - c.y0, cols = c.x1 - c.x0;
+    const int bh = rows - 6, bw = cols - 6;
+    const int pw = bw > 0 ? (bw + 1) >> 1 : 0;
+    const int np = bh > 0 ? bh * pw : 0;
+    const int wc = L.wCell, G = c.ncell;
+    constexpr int SC = CW;
+    half2_t* hp = reinterpret_cast<half2_t*>(smem);
+    const int rmax = g->roi_max_rows;
+    half2_t* Sh = reinterpret_cast<half2_t*>(smem + fastc_off_s(rmax, CW));
+    uint16_t* pkm = reinterpret_cast<uint16_t*>(smem + fastc_off_pk(rmax, CW));
+    int* cnt = reinterpret_cast<int*>(smem + fastc_off_cnt(rmax, CW));
+    const half2_t z = {(_Float16)0, (_Float16)0};
+    // (a) stage the chunk ROI as f16 pixel pairs (k_fast_cells' staging)
+    {
+        const int qc = (cols + 3) >> 2, nq = rows * qc;
+        const int dq = T / qc, dr = T - dq * qc;
+        int r = tid / qc, q = tid - r * qc;
+        const uint8_t* src = lev + (size_t)c.y0 * pitch + c.x0;
+#pragma unroll 2
+        for (int i = tid; i < nq; i += T) {
+            const uint8_t* pr = src + (size_t)r * pitch + 4 * q;
+            uint32_t w4;
+            __builtin_memcpy(&w4, pr, 4);
+            const uint32_t b4x = (uint32_t)pr[4] | 0x64646400u;
+            constexpr uint32_t K64 = 0x64646464u;
+            uint32_t* dE = reinterpret_cast<uint32_t*>(hp + r * 2 * CW + 2 * q);
+            uint32_t* dO = dE + CW;
+            dE[0] = __builtin_amdgcn_perm(K64, w4, 0x04010400u);
+            dO[0] = __builtin_amdgcn_perm(K64, w4, 0x04020401u);
+            dE[1] = __builtin_amdgcn_perm(K64, w4, 0x04030402u);
+            dO[1] = __builtin_amdgcn_perm(b4x, w4, 0x05040503u);
+            r += dq;
+            q += dr;
+            if (q >= qc) { q -= qc; r++; }
+        }
+        if (np > 0) {
+            for (int i = tid; i < SC; i += T) { Sh[i] = z; Sh[(bh + 1) * SC + i] = z; }
+            for (int i = tid; i < bh; i += T) { Sh[(i + 1) * SC] = z; Sh[(i + 1) * SC + pw + 1] = z; }
+        }
+    }
+    __syncthreads();
+    const int pwm = max(pw, 1);
+    const int dq = T / pwm, dr = T - dq * pwm;
+    const int r_start = tid / pwm, p_start = tid - r_start * pwm;
+    // (b) strength of every inner pair of the chunk, once
+    {
+        int r = r_start, pc = p_start;
+        for (int i = tid; i < np; i += T) {
+            half2_t S2 = fast_strength_h2<CW>(hp, r + 3, pc);
+            S2 = __builtin_elementwise_maximum(S2, z);
+            if (2 * pc + 1 >= bw) S2.y = (_Float16)0;
+            Sh[(r + 1) * SC + pc + 1] = S2;
+            r += dq;
+            pc += dr;
+            if (pc >= pw) { pc -= pw; r++; }
+        }
+    }
+    __syncthreads();
+    const int tlo = max(iniTh, 1), thi = max(minTh, 1);
+    const int iters = (np + T - 1) / T;
+    // the cell (within the chunk) of inner column ic, and whether ic is its cell's first / last detection column
+    auto cell_of = [&](int ic) { return min(ic / wc, G - 1); };
+    // (c) NMS peaks with the neighbours of other cells masked; per (iteration, wave, cell) counts at both thresholds
+    {
+        int r = r_start, pc = p_start;
+        for (int j = 0; j < iters; j++) {
+            const int i = j * T + tid;
+            int pk0 = 0, pk1 = 0, k0 = 0, k1 = 0;
+            if (i < np) {
+                const half2_t* q = Sh + (r + 1) * SC + pc + 1;
+                const int ic0 = 2 * pc, ic1 = 2 * pc + 1;
+                k0 = cell_of(ic0);
+                k1 = cell_of(ic1);
+                // neighbour columns of pixel ic0: ic0 - 1 (pair pc - 1's .y) and ic1 (this pair's .y); of ic1: ic0
+                // (this .x) and ic1 + 1 (pair pc + 1's .x). A neighbour in another cell reads as 0.
+                const bool l0 = ic0 > 0 && cell_of(ic0 - 1) == k0, r0 = k1 == k0;
+                const bool l1 = k0 == k1, r1 = ic1 + 1 < bw && cell_of(ic1 + 1) == k1;
+                const half2_t UL = q[-SC - 1], U = q[-SC], UR = q[-SC + 1];
+                const half2_t ML = q[-1], M = q[0], MR = q[1];
+                const half2_t DL = q[SC - 1], D = q[SC], DR = q[SC + 1];
+                const _Float16 zf = (_Float16)0;
+                // pixel 0: columns ic0 - 1 (UL.y, ML.y, DL.y), ic0 (U.x, D.x), ic1 (U.y, M.y, D.y)
+                const _Float16 a0 = l0 ? __builtin_elementwise_maximum(UL.y, __builtin_elementwise_maximum(ML.y, DL.y)) : zf;
+                const _Float16 b0 = __builtin_elementwise_maximum(U.x, D.x);
+                const _Float16 c0 = r0 ? __builtin_elementwise_maximum(U.y, __builtin_elementwise_maximum(M.y, D.y)) : zf;
+                const _Float16 m0 = __builtin_elementwise_maximum(a0, __builtin_elementwise_maximum(b0, c0));
+                // pixel 1: columns ic0 (U.x, M.x, D.x), ic1 (U.y, D.y), ic1 + 1 (UR.x, MR.x, DR.x)
+                const _Float16 a1 = l1 ? __builtin_elementwise_maximum(U.x, __builtin_elementwise_maximum(M.x, D.x)) : zf;
+                const _Float16 b1 = __builtin_elementwise_maximum(U.y, D.y);
+                const _Float16 c1 = r1 ? __builtin_elementwise_maximum(UR.x, __builtin_elementwise_maximum(MR.x, DR.x)) : zf;
+                const _Float16 m1 = __builtin_elementwise_maximum(a1, __builtin_elementwise_maximum(b1, c1));
+                pk0 = (M.x > m0 && M.x >= (_Float16)2) ? (int)M.x : 0;
+                pk1 = (M.y > m1 && M.y >= (_Float16)2) ? (int)M.y : 0;
+                pkm[i] = (uint16_t)(pk0 | (pk1 << 8));
+                r += dq;
+                pc += dr;
+                if (pc >= pw) { pc -= pw; r++; }
+            }
+            for (int k = 0; k < G; k++) {
+                const int chi = __popcll(__ballot(k0 == k && pk0 > tlo)) + __popcll(__ballot(k1 == k && pk1 > tlo));
+                const int clo = __popcll(__ballot(k0 == k && pk0 > thi)) + __popcll(__ballot(k1 == k && pk1 > thi));
+                if (lane == 0) cnt[(j * NW + w) * FAST_G + k] = (chi << 16) | clo;
+            }
+        }
+    }
+    __syncthreads();
+    // (d) per cell: totals, the threshold, this wave's first-entry bases
+    int tot[FAST_G], base[FAST_G];
+    const int nent = iters * NW;
+#pragma unroll
+    for (int k = 0; k < FAST_G; k++) { tot[k] = 0; base[k] = 0; }
+    for (int e = 0; e < nent; e++) {
+#pragma unroll
+        for (int k = 0; k < FAST_G; k++) {
+            const int v = k < G ? cnt[e * FAST_G + k] : 0;
+            if (e == w) base[k] = tot[k];
+            tot[k] += v;
+        }
+    }
+    bool use_hi[FAST_G];
+#pragma unroll
+    for (int k = 0; k < FAST_G; k++) use_hi[k] = (tot[k] >> 16) > 0;
+    // (e) ordered emit per cell: in the chunk's row-major pair order each cell's pixels keep their row-major order
+    {
+        int r = r_start, pc = p_start;
+        const uint64_t below = (1ull << lane) - 1ull;
+        const int xbase = 3 + c.cj0 * wc;
+        for (int j = 0; j < iters; j++) {
+            if (j > 0) {
+                for (int e = (j - 1) * NW + w; e < j * NW + w; e++)
+#pragma unroll
+                    for (int k = 0; k < FAST_G; k++) base[k] += k < G ? cnt[e * FAST_G + k] : 0;
+            }
+            const int i = j * T + tid;
+            int pk0 = 0, pk1 = 0, k0 = 0, k1 = 0;
+            if (i < np) {
+                const int v = pkm[i];
+                pk0 = v & 0xFF;
+                pk1 = v >> 8;
+                k0 = cell_of(2 * pc);
+                k1 = cell_of(2 * pc + 1);
+            }
+            int th0 = thi, th1 = thi, b0 = 0, b1 = 0;
+#pragma unroll
+            for (int k = 0; k < FAST_G; k++) {
+                const int th = use_hi[k] ? tlo : thi;
+                const int bk = use_hi[k] ? base[k] >> 16 : base[k] & 0xFFFF;
+                if (k == k0) { th0 = th; b0 = bk; }
+                if (k == k1) { th1 = th; b1 = bk; }
+            }
+            const bool f0 = i < np && pk0 > th0, f1 = i < np && pk1 > th1;
+            int pos0 = b0, pos1 = b1 + ((f0 && k0 == k1) ? 1 : 0);
+#pragma unroll
+            for (int k = 0; k < FAST_G; k++) {
+                const uint64_t m0 = __ballot(f0 && k0 == k), m1 = __ballot(f1 && k1 == k);
+                const int before = __popcll(m0 & below) + __popcll(m1 & below);
+                if (k == k0) pos0 += before;
+                if (k == k1) pos1 += before;
+            }
+            if (i < np) {
+                const uint32_t x = (uint32_t)(xbase + 2 * pc);
+                const uint32_t y = (uint32_t)(r + 3 + c.ci * L.hCell);
+                if (f0) {
+                    uint32_t* out = cand + (size_t)f * g->cand_per_frame + L.cand_base + (size_t)cells[c.cell0 + k0].slot * L.cellcap;
+                    out[pos0] = x | (y << 12) | ((uint32_t)(pk0 - 1) << 24);
+                }
+                if (f1) {
+                    uint32_t* out = cand + (size_t)f * g->cand_per_frame + L.cand_base + (size_t)cells[c.cell0 + k1].slot * L.cellcap;
+                    out[pos1] = (x + 1) | (y << 12) | ((uint32_t)(pk1 - 1) << 24);
+                }
+                r += dq;
+                pc += dr;
+                if (pc >= pw) { pc -= pw; r++; }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < FAST_G; k++)
+        if (tid == k && k < G)
+            cell_counts[(size_t)f * g->cells_per_frame + c.cell0 + k] = use_hi[k] ? tot[k] >> 16 : tot[k] & 0xFFFF;
+}
+
 // ------------------------------------------------------------------------------------------------ blur
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 u16_pair(uint32_t hi, uint32_t lo, uint32_t sel) {

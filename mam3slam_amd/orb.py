@@ -150,6 +150,10 @@ class ORBextractor:
         """Latency-mode stream fork for up to 4 frames per call: 1 on, 0 off, -1 automatic."""
         check(lib().mam_orb_debug_set_option(self._ctx, 2, int(on)), "mam_orb_debug_set_option")
 
+    def set_fast_chunks(self, on: int):
+        """FAST over chunks of a cell row (k_fast_chunks) instead of one workgroup per cell: 1 on, 0 off, -1 auto."""
+        check(lib().mam_orb_debug_set_option(self._ctx, 3, int(on)), "mam_orb_debug_set_option")
+
     def debug_candidates(self, level: int, frame: int = 0) -> np.ndarray:
         n = check(lib().mam_orb_debug_candidates(self._ctx, frame, level, None, 0), "debug_candidates")
         out = np.zeros(max(n, 1), np.uint32)

@@ -259,3 +259,29 @@ def test_latency_mode_fork_bit_exact(gpu_lib, oracle, fork):
             kps = d_kps.cpu().numpy().view(KP_DTYPE)[:n]
             _assert_kps_equal(kps, d_desc.cpu().numpy()[:n], int(d_cnt[1]), *ref[i], f"fork {fork} {w}x{h} graph {i}")
         ext.close()
+
+
+@pytest.mark.parametrize("w,h,nfeat", CASES[:3])
+def test_fast_chunks_bit_exact(gpu_lib, oracle, w, h, nfeat):
+    """k_fast_chunks (FAST over chunks of up to 4 cells of a cell row: one staging and one strength map per chunk, NMS
+    with the other cells' pixels masked, per-cell threshold choice and ordered emit) gives the oracle's per-level
+    candidates and the end-to-end output, single frames (latency mode) and a batch."""
+    ext = _extractor(nfeat)
+    ext.set_fast_chunks(1)
+    p = oracle.params(nfeat)
+    for fr in range(2):
+        img = synth.make_frame(w, h, agent=7, frame=fr)
+        kg, dg, mg = ext(img)
+        ko, do, mo = oracle.extract(img, p)
+        _assert_kps_equal(kg, dg, mg, ko, do, mo, f"chunks {w}x{h}/{nfeat} frame {fr}")
+        for l in range(8):
+            cand_o, _ = oracle.level_stage(img, l, p)
+            cand_g = ext.debug_candidates(l)
+            assert len(cand_g) == len(cand_o), f"level {l}: {len(cand_g)} candidates vs oracle {len(cand_o)}"
+            d = _first_diff(cand_g, cand_o)
+            assert d is None, f"level {l} candidate {d}: gpu={oracle.unpack(cand_g[d])} oracle={oracle.unpack(cand_o[d])}"
+    ext.set_fork(0)   # one stream, every level in one launch
+    img = synth.make_frame(w, h, agent=7, frame=5)
+    kg, dg, mg = ext(img)
+    _assert_kps_equal(kg, dg, mg, *oracle.extract(img, p), f"chunks {w}x{h}/{nfeat} no fork")
+    ext.close()
