@@ -87,6 +87,25 @@ __host__ __device__ inline size_t lds_bytes(int NC, int max_cells, int NT) {
 
 }  // namespace dist
 
+#ifdef MAM_DIST2_PROFILE
+// per level: cycles by phase summed over launches (thread 0's clock after each phase), iteration counts, launches
+// [0] init [1] phase-1 count [2] final sort + count [3] cut scan [4] kept scan [5] table write [6] remap
+// [7] retain + output [8] final iterations [9] phase-1 rounds [10] sum of m [11] launches
+__device__ unsigned long long g_d2prof[8][12];
+#define D2P(k)                                                                                         \
+    do {                                                                                               \
+        if (tid == 0) {                                                                                \
+            const long long tn_ = clock64();                                                           \
+            atomicAdd(&g_d2prof[l & 7][k], (unsigned long long)(tn_ - d2t));                           \
+            d2t = tn_;                                                                                 \
+        }                                                                                              \
+    } while (0)
+#define D2C(k, v) do { if (tid == 0) atomicAdd(&g_d2prof[l & 7][k], (unsigned long long)(v)); } while (0)
+#else
+#define D2P(k) do {} while (0)
+#define D2C(k, v) do {} while (0)
+#endif
+
 // grid (levels, frames) x NT; levels l_first + blockIdx.x. ovf_key / ovf_node: per frame cand_per_frame u32 each
 // (keys beyond NT * KPT of a level). lvl_counts[f][l] = {kept keypoints, lapping ones} or {-1, 0} on overflow.
 template <int NT, int KPT>
@@ -120,6 +139,10 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
     SortEl* arr = (SortEl*)take((size_t)NC * 8);        // sort array; then the retain-best maxima
     int flip = 0;
     int* lc = lvl_counts + ((size_t)f * g->nlevels + l) * 2;
+#ifdef MAM_DIST2_PROFILE
+    long long d2t = clock64();
+    D2C(11, 1);
+#endif
 
     // ---- 0. this level's candidates in reference order (cells row-major, FAST order inside): cell offsets
     const int* cc = cell_counts + (size_t)f * g->cells_per_frame + L.cell_base;
@@ -211,6 +234,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
     }
     __syncthreads();
     for_keys([&](uint32_t, uint32_t& nd, int) { nd = nb[nd]; });
+    D2P(0);
 
     // ---- 2. rounds
     int cur = 0, m = 0;
@@ -264,6 +288,9 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
             }
             count_pass();
             __syncthreads();
+            D2P(2);
+            D2C(8, 1);
+            D2C(10, m);
             // expansion cut: after expanding ranks 0..r the list has S + sum (e - 1) nodes; stop at the first r where
             // that reaches N (:746-747). Wave 0 scans the ranks: creation / big-child bases, the cut, and marks the
             // candidates past the cut as not expanded.
@@ -303,12 +330,15 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
                 if (lane == 0) { sh[0] = (int)C; sh[1] = (int)M; }
             }
             __syncthreads();
+            D2P(3);
             C = (uint32_t)sh[0];
             M = (uint32_t)sh[1];
         } else {
             // ---- phase-1 round (:605-677): every node with > 1 keys divides
             count_pass();
             __syncthreads();
+            D2P(1);
+            D2C(9, 1);
         }
         // kept nodes' ranks (and in phase 1 the creation / big-child bases) over the list in order
         uint32_t K = 0;
@@ -339,6 +369,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
             if (!final_phase) { C = c1 & 0xFFFF; M = c1 >> 16; }
             K = c2;
         }
+        D2P(4);
         const int Snew = (int)(C + K);
         const bool fin = Snew >= N || Snew == S;
         const bool next_final = !fin && (final_phase || Snew + 3 * (int)M > N);
@@ -372,6 +403,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
             }
         }
         __syncthreads();
+        D2P(5);
         for_keys([&](uint32_t, uint32_t& nd, int) {
             const int p = nd & 0xFFFF;
             if (XR[p] >= 0) {
@@ -383,6 +415,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
                 nd = C + nb[p];
             }
         });
+        D2P(6);
         S = Snew;
         m = (int)M;
         cur ^= 1;
@@ -435,6 +468,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
         st_carry += t1;
     }
     if (tid == 0) { lc[0] = S; lc[1] = (int)st_carry; }
+    D2P(7);
 }
 
 }  // namespace mam

@@ -23,6 +23,16 @@ for x in list(csv.DictReader(open(sys.argv[1])))[:14]:
     print(x["Name"][:58].ljust(58), x["Calls"].rjust(6), "%8.1f avg" % (float(x["AverageNs"]) / 1e3), "%8.1f min" % (float(x["MinNs"]) / 1e3), "%8.1f max" % (float(x["MaxNs"]) / 1e3))
 PY
       ;;
+    sweep)
+      # single-frame extraction under implementation switches (env), c1 and c2, and the DistributeOctTree phase profile
+      cd /tmp
+      for v in "MAM_ORB_FORK=0" "MAM_PYR_BANDS=0" "MAM_PYR_BANDS=16" "MAM_PYR_BANDS=32" "MAM_ORB_FORK=0 MAM_PYR_BANDS=0" "MAM_FAST_CHUNKS=1" ${SWEEP_EXTRA:-}; do
+        echo "-- $v"; env $v timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 100 --configs c1,c2 2>&1 | grep '^c'
+      done
+      if [ -f $R/variants/libmam_gpu_d2prof.so ]; then
+        MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_d2prof.so timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 100 --configs c1,c2 > $O/d2prof.log 2>&1
+        grep "d2prof" $O/d2prof.log | awk '!seen[$2 $3 $4]++' | head -24
+      fi ;;
     lone)
       cd /tmp && timeout -k 10 300 python3 $R/scripts/lba_bench.py --world --solves 10 > $O/lone_bench.json 2> $O/lone_bench.err || { tail -20 $O/lone_bench.err; exit 1; }
       head -c 600 $O/lone_bench.json; echo
