@@ -118,7 +118,8 @@ int mam_orb_debug_blurred(mam_orb_ctx* ctx, int frame, int level, uint8_t* out);
  * MAM_ORB_OPT_DISTRIBUTE_THREADS: DistributeOctTree workgroup width, 256 / 512 / 1024 (k_distribute2), 0 (the
  * round-3 kernel) or -1 (automatic: 1024 for up to 4 frames per call, else 256).
  * MAM_ORB_OPT_FORK: latency mode for up to 4 frames per call (level 0's FAST + DistributeOctTree beside the pyramid,
- * the blur beside the other levels' FAST, on the context's side streams), 1 on / 0 off / -1 automatic (on).
+ * the blur beside the other levels' FAST, on the context's side streams), 1 on / 0 off / -1 automatic (off: the
+ * cross-stream waits cost more than the overlap gains on MI355X).
  * MAM_ORB_OPT_FAST_CHUNKS: FAST over chunks of up to 4 cells of a cell row (k_fast_chunks) instead of one workgroup per
  * cell (k_fast_cells): 1 on / 0 off / -1 automatic. */
 enum { MAM_ORB_OPT_DISTRIBUTE_THREADS = 1, MAM_ORB_OPT_FORK = 2, MAM_ORB_OPT_FAST_CHUNKS = 3 };

@@ -91,7 +91,7 @@ __host__ __device__ inline size_t lds_bytes(int NC, int max_cells, int NT) {
 // per level: cycles by phase summed over launches (thread 0's clock after each phase), iteration counts, launches
 // [0] init [1] phase-1 count [2] final sort + count [3] cut scan [4] kept scan [5] table write [6] remap
 // [7] retain + output [8] final iterations [9] phase-1 rounds [10] sum of m [11] launches
-__device__ unsigned long long g_d2prof[8][12];
+__device__ unsigned long long g_d2prof[8][13];   // [12]: wave 0's sort alone
 #define D2P(k)                                                                                         \
     do {                                                                                               \
         if (tid == 0) {                                                                                \
@@ -278,12 +278,18 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+#ifdef MAM_DIST2_PROFILE
+                const long long ts0 = clock64();
+#endif
                 if (m <= 64) stl_sort_wave2<1>(arr, m, sortscr);
                 else if (m <= 128) stl_sort_wave2<2>(arr, m, sortscr);
                 else if (m <= 256) stl_sort_wave2<4>(arr, m, sortscr);
                 else if (lane == 0) stl_sort(arr, arr + m);
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+#ifdef MAM_DIST2_PROFILE
+                if (lane == 0) atomicAdd(&g_d2prof[l & 7][12], (unsigned long long)(clock64() - ts0));
+#endif
                 for (int i = lane; i < m; i += 64) srt[m - 1 - i] = arr[i].val;   // expansion rank: largest first
             }
             count_pass();

@@ -33,6 +33,23 @@ PY
         MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_d2prof.so timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 100 --configs c1,c2 > $O/d2prof.log 2>&1
         grep "d2prof" $O/d2prof.log | awk '!seen[$2 $3 $4]++' | head -24
       fi ;;
+    sweep2)
+      # DistributeOctTree phase profile per workgroup width; batch stage times with / without the FAST chunks
+      cd /tmp
+      for nt in 256 512 1024; do
+        echo "-- MAM_DIST_NT=$nt"
+        MAM_DIST_NT=$nt MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_d2prof.so timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 60 --configs c1,c2 > $O/d2prof_$nt.log 2>&1
+        grep "^c" $O/d2prof_$nt.log; grep "d2prof" $O/d2prof_$nt.log | awk '!seen[$2 $3 $4]++' | grep -E " l0:| l1:| l7:"
+      done
+      cd $R
+      for v in "MAM_FAST_CHUNKS=0" "MAM_FAST_CHUNKS=1"; do
+        for cfg in c1 c2; do
+          env $v timeout -k 10 300 python3 bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline --no-latency --no-pose --no-sin --no-overlap > $O/sw2_$cfg.json 2> $O/sw2_$cfg.err || { tail -5 $O/sw2_$cfg.err; exit 1; }
+          python3 -c "
+import json; d=json.loads(open('$O/sw2_$cfg.json').read().strip().splitlines()[-1])
+print('$v $cfg', 'value %.0f' % d['value'], {k: round(v, 3) for k, v in d['stage_ms_per_step'].items() if k in ('fast', 'distribute', 'pyramid')}, d['roofline']['avg_launch_ms'])"
+        done
+      done ;;
     lone)
       cd /tmp && timeout -k 10 300 python3 $R/scripts/lba_bench.py --world --solves 10 > $O/lone_bench.json 2> $O/lone_bench.err || { tail -20 $O/lone_bench.err; exit 1; }
       head -c 600 $O/lone_bench.json; echo
