@@ -5,15 +5,16 @@
 // index k = j * NT + tid; beyond NT * KPT in global scratch), each with its current node id and the quadrant it went
 // to in the last count pass. The node list lives in LDS as two ping-pong tables in LIST ORDER (node id == position).
 // A quadtree round (ORBextractor.cc:605-677) or a final-phase expansion (:680-748) is:
-//   count   every key of an expanded node adds itself to its child quadrant (LDS atomics)        | barrier
 //   scan    over the list: children per expanded node (creation bases), kept nodes (their rank) | 1 barrier inside
 //   write   the new table: children of the expanded nodes in reverse creation order (push_front), then the kept
 //           nodes in order — exactly the std::list the reference leaves — and the >1-key children in creation order
 //           (the next final-phase candidates)                                                       | barrier
-//   remap   every key to its node's new id (computed from the scan results, no per-key table)
+//   pass    every key to its node's new id (computed from the scan results, no per-key table) and at once its count
+//           in the next round: the child quadrant of its node if that node expands (LDS atomics, aggregated per wave
+//           by ballot)                                                                               | barrier
 // The final phase's std::sort of (size, UL.x) with libstdc++'s tie behaviour is replayed by one wave
-// (stl_sort_wave2) while the other waves run the count pass; the expansion cut (size >= N after an expansion) is a
-// wave-level scan over the sorted candidates. Retain-best keeps the first max response in candidate order (:758-776).
+// (stl_sort_wave2) during the pass; the expansion cut (size >= N after an expansion) is a wave-level scan over the
+// sorted candidates. Retain-best keeps the first max response in candidate order (:758-776).
 #pragma once
 
 namespace mam {
@@ -74,6 +75,24 @@ __device__ __forceinline__ int quad2(uint2 r, uint32_t key) {
     return (right ? 1 : 0) | (bottom ? 2 : 0);
 }
 
+// cnt[t] += 1 for every active lane with t >= 0: lanes of the wave with the same target are counted by ballot and
+// added by one leader (the early rounds send whole waves to the same few nodes: per-lane LDS atomics on one address
+// serialise), up to AGG distinct targets per call; lanes left after that add one by one
+template <int AGG>
+__device__ __forceinline__ void agg_add(uint32_t* cnt, int t) {
+#pragma unroll
+    for (int it = 0; it < AGG; it++) {
+        const uint64_t act = __ballot(t >= 0);
+        if (!act) return;
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const int lt = __builtin_amdgcn_readlane(t, leader);
+        const uint64_t mm = __ballot(t == lt);
+        if ((int)(threadIdx.x & 63) == leader) atomicAdd(cnt + lt, (uint32_t)__popcll(mm));
+        if (t == lt) t = -1;
+    }
+    if (t >= 0) atomicAdd(cnt + t, 1u);
+}
+
 __host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~(size_t)15; }
 // sort scratch: the wave sort's stack, stopper positions and move buffer for up to 4 elements per lane
 #define MAM_DIST_SORT_E 4
@@ -89,8 +108,8 @@ __host__ __device__ inline size_t lds_bytes(int NC, int max_cells, int NT) {
 
 #ifdef MAM_DIST2_PROFILE
 // per level: cycles by phase summed over launches (thread 0's clock after each phase), iteration counts, launches
-// [0] init [1] phase-1 count [2] final sort + count [3] cut scan [4] kept scan [5] table write [6] remap
-// [7] retain + output [8] final iterations [9] phase-1 rounds [10] sum of m [11] launches
+// [0] init (+ the first count) [3] cut scan [4] kept scan [5] table write [6] the pass (remap + next count, wave 0's
+// sort) [7] retain + output [8] final iterations [9] phase-1 rounds [10] sum of m [11] launches [12] wave 0's sort
 __device__ unsigned long long g_d2prof[8][13];   // [12]: wave 0's sort alone
 #define D2P(k)                                                                                         \
     do {                                                                                               \
@@ -209,7 +228,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
     for_keys([&](uint32_t key, uint32_t& nd, int) {
         const int i = (int)((float)(key & 0xFFF) / L.hX);   // vpIniNodes[kp.pt.x / hX]
         nd = (uint32_t)i;
-        atomicAdd(&cnt1[i], 1u);
+        dist::agg_add<4>(cnt1, i);
     });
     __syncthreads();
     int S = 0;
@@ -233,7 +252,20 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
         S = (int)kc;
     }
     __syncthreads();
-    for_keys([&](uint32_t, uint32_t& nd, int) { nd = nb[nd]; });
+    // the keys to their compacted initial nodes, and the first round's count (every node with > 1 keys divides)
+    for_keys([&](uint32_t key, uint32_t& nd, int) {
+        const int p = (int)nb[nd];
+        int t = -1;
+        if (xr0[p] >= 0) {
+            const int q = dist::quad2(rect0[p], key);
+            t = 4 * p + q;
+            nd = (uint32_t)p | ((uint32_t)q << 16);
+        } else {
+            nd = (uint32_t)p;
+        }
+        dist::agg_add<8>(reinterpret_cast<uint32_t*>(chc0), t);
+    });
+    __syncthreads();
     D2P(0);
 
     // ---- 2. rounds
@@ -255,46 +287,10 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
         int* const XRn = b ? xr0 : xr1;
         uint4* const CHn = b ? chc0 : chc1;
         if (final_phase && m == 0) break;
-        // count: keys of the nodes that expand (phase 1: every node with > 1 keys; final phase: the candidates)
-        auto count_pass = [&]() {
-            for_keys([&](uint32_t key, uint32_t& nd, int) {
-                const int p = nd & 0xFFFF;
-                if (XR[p] >= 0) {
-                    const int q = dist::quad2(R[p], key);
-                    atomicAdd(reinterpret_cast<uint32_t*>(&CH[p]) + q, 1u);
-                    nd = (uint32_t)p | ((uint32_t)q << 16);
-                }
-            });
-        };
         uint32_t C = 0, M = 0;
         if (final_phase) {
-            // ---- final phase (ORBextractor.cc:680-748): wave 0 sorts last round's > 1-key children by (size, UL.x)
-            // as libstdc++'s introsort orders them (ties included) while the other waves count
-            if (wid == 0) {
-                for (int i = lane; i < m; i += 64) {
-                    const int p = (int)candl[i];
-                    arr[i].key = (CN[p] << 12) | (R[p].x & 0xFFFFu);
-                    arr[i].val = (uint32_t)p;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-#ifdef MAM_DIST2_PROFILE
-                const long long ts0 = clock64();
-#endif
-                if (m <= 64) stl_sort_wave2<1>(arr, m, sortscr);
-                else if (m <= 128) stl_sort_wave2<2>(arr, m, sortscr);
-                else if (m <= 256) stl_sort_wave2<4>(arr, m, sortscr);
-                else if (lane == 0) stl_sort(arr, arr + m);
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-#ifdef MAM_DIST2_PROFILE
-                if (lane == 0) atomicAdd(&g_d2prof[l & 7][12], (unsigned long long)(clock64() - ts0));
-#endif
-                for (int i = lane; i < m; i += 64) srt[m - 1 - i] = arr[i].val;   // expansion rank: largest first
-            }
-            count_pass();
-            __syncthreads();
-            D2P(2);
+            // ---- final phase (ORBextractor.cc:680-748): the candidates (last round's > 1-key children) were sorted
+            // by wave 0 and counted by every key in the pass that ended the previous round
             D2C(8, 1);
             D2C(10, m);
             // expansion cut: after expanding ranks 0..r the list has S + sum (e - 1) nodes; stop at the first r where
@@ -340,10 +336,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
             C = (uint32_t)sh[0];
             M = (uint32_t)sh[1];
         } else {
-            // ---- phase-1 round (:605-677): every node with > 1 keys divides
-            count_pass();
-            __syncthreads();
-            D2P(1);
+            // ---- phase-1 round (:605-677): every node with > 1 keys divides (counted in the previous pass)
             D2C(9, 1);
         }
         // kept nodes' ranks (and in phase 1 the creation / big-child bases) over the list in order
@@ -410,17 +403,56 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
         }
         __syncthreads();
         D2P(5);
-        for_keys([&](uint32_t, uint32_t& nd, int) {
+        // the pass between rounds: every key to its node's new id (from the scan results), and — unless the list is
+        // final — straight away its count in the next round (the new table's expanding nodes); in the final phase
+        // wave 0 first sorts the next round's candidates by (size, UL.x) as libstdc++'s introsort orders them (ties
+        // included) while the other waves run the pass
+        const bool count_next = !fin;
+        if (count_next && next_final && wid == 0) {
+            const int mn = (int)M;
+            for (int i = lane; i < mn; i += 64) {
+                const int p = (int)candl[i];
+                arr[i].key = (CNn[p] << 12) | (Rn[p].x & 0xFFFFu);
+                arr[i].val = (uint32_t)p;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#ifdef MAM_DIST2_PROFILE
+            const long long ts0 = clock64();
+#endif
+            if (mn <= 64) stl_sort_wave2<1>(arr, mn, sortscr);
+            else if (mn <= 128) stl_sort_wave2<2>(arr, mn, sortscr);
+            else if (mn <= 256) stl_sort_wave2<4>(arr, mn, sortscr);
+            else if (lane == 0) stl_sort(arr, arr + mn);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#ifdef MAM_DIST2_PROFILE
+            if (lane == 0) atomicAdd(&g_d2prof[l & 7][12], (unsigned long long)(clock64() - ts0));
+#endif
+            for (int i = lane; i < mn; i += 64) srt[mn - 1 - i] = arr[i].val;   // expansion rank: largest first
+        }
+        for_keys([&](uint32_t key, uint32_t& nd, int) {
             const int p = nd & 0xFFFF;
+            int np;
             if (XR[p] >= 0) {
                 const int q = nd >> 16;
                 const uint4 c4 = CH[p];
                 const int j = (q > 0 && c4.x > 0) + (q > 1 && c4.y > 0) + (q > 2 && c4.z > 0);
-                nd = (uint32_t)((int)C - 1 - ((int)(nb[p] & 0xFFFF) + j));
+                np = (int)C - 1 - ((int)(nb[p] & 0xFFFF) + j);
             } else {
-                nd = C + nb[p];
+                np = (int)C + (int)nb[p];
             }
+            int t = -1;
+            if (count_next && XRn[np] >= 0) {
+                const int q = dist::quad2(Rn[np], key);
+                t = 4 * np + q;
+                nd = (uint32_t)np | ((uint32_t)q << 16);
+            } else {
+                nd = (uint32_t)np;
+            }
+            if (count_next) dist::agg_add<8>(reinterpret_cast<uint32_t*>(CHn), t);
         });
+        if (count_next) __syncthreads();
         D2P(6);
         S = Snew;
         m = (int)M;

@@ -752,8 +752,8 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
             MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::g_d2prof), sizeof(h)));
             for (int l = 0; l < 8; l++) {
                 const double n = h[l][11] ? (double)h[l][11] : 1.0;
-                fprintf(stderr, "d2prof W%d L%d l%d: init %.0f p1count %.0f fsort+count %.0f cut %.0f kept %.0f write %.0f "
-                        "remap %.0f out %.0f | final its %.2f p1 rounds %.2f mean m %.1f | sort %.0f\n", g.L[0].w,
+                fprintf(stderr, "d2prof W%d L%d l%d: init %.0f - %.0f - %.0f cut %.0f kept %.0f write %.0f "
+                        "pass %.0f out %.0f | final its %.2f p1 rounds %.2f mean m %.1f | sort %.0f\n", g.L[0].w,
                         c->prm.nfeatures, l, h[l][0] / n, h[l][1] / n, h[l][2] / n, h[l][3] / n, h[l][4] / n, h[l][5] / n,
                         h[l][6] / n, h[l][7] / n, h[l][8] / n, h[l][9] / n, h[l][8] ? (double)h[l][10] / h[l][8] : 0.0,
                         h[l][12] / n);
