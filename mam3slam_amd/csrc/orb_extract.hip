@@ -743,6 +743,22 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
                            c->prm.fp_policy);
     }
     MAM_HIP(hipGetLastError());
+#ifdef MAM_PYR_PROFILE
+    {
+        static int callsp = 0;
+        if (++callsp % 50 == 0) {
+            unsigned long long h[10];
+            MAM_HIP(hipStreamSynchronize(s));
+            MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::g_pyrprof), sizeof(h)));
+            const double n = h[9] ? (double)h[9] : 1.0;
+            fprintf(stderr, "pyrprof W%d F%d bands/launch %.1f: prologue %.0f", g.L[0].w, F, n / 50.0, h[0] / n);
+            for (int l = 1; l < 9; l++) fprintf(stderr, " l%d %.0f", l, h[l] / n);
+            fprintf(stderr, "\n");
+            unsigned long long zero[10] = {};
+            MAM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(mam::g_pyrprof), zero, sizeof(zero)));
+        }
+    }
+#endif
 #ifdef MAM_DIST2_PROFILE
     {
         static int calls2 = 0;

@@ -343,6 +343,22 @@ __device__ __forceinline__ void pyr_band_level(const LevelGeom& L, int sh, const
     }
 }
 
+#ifdef MAM_PYR_PROFILE
+// cycles per phase summed over workgroups (thread 0): [0] prologue (level-0 rows + row coefficients staged), [l] level
+// l, [9] workgroups
+__device__ unsigned long long g_pyrprof[10];
+#define PYRP(k)                                                                        \
+    do {                                                                               \
+        if (tid == 0) {                                                                \
+            const long long tn_ = clock64();                                           \
+            atomicAdd(&g_pyrprof[k], (unsigned long long)(tn_ - pt0));                 \
+            pt0 = tn_;                                                                 \
+        }                                                                              \
+    } while (0)
+#else
+#define PYRP(k) do {} while (0)
+#endif
+
 // LDS: [even levels' rows (level 0 staged from the frame)] [odd levels' rows] [row coefficients of every level].
 // The prologue puts everything with a global-memory latency in flight at once (level-0 rows, all row coefficients);
 // each level's column coefficients are fetched into registers while the previous level computes.
@@ -353,6 +369,10 @@ __global__ __launch_bounds__(NT) void k_pyr_bands(const Geom* __restrict__ g, Le
     const int j = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, NL = g->nlevels;
     const int4* B = bands + (size_t)j * NL;
     int2* rcoef = reinterpret_cast<int2*>(pbuf + rc_off);
+#ifdef MAM_PYR_PROFILE
+    long long pt0 = clock64();
+    if (tid == 0) atomicAdd(&g_pyrprof[9], 1ull);
+#endif
     // ---- prologue: level-0 rows [B[0].x, B[0].y) and the row coefficients of every level
     {
         const int4 b0 = B[0];
@@ -399,6 +419,7 @@ __global__ __launch_bounds__(NT) void k_pyr_bands(const Geom* __restrict__ g, Le
     PyrQuad pre;
     pyr_quad_setup(g->L[1], 4 * (tid % ((g->L[1].w + 3) >> 2)), 0, pre);
     __syncthreads();
+    PYRP(0);
     int off = 0;
     for (int l = 1; l < NL; l++) {
         const LevelGeom& L = g->L[l];
@@ -411,6 +432,7 @@ __global__ __launch_bounds__(NT) void k_pyr_bands(const Geom* __restrict__ g, Le
                        cur);
         off += bl.y - bl.x;
         __syncthreads();
+        PYRP(l);
     }
 }
 

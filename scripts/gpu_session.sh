@@ -33,6 +33,14 @@ PY
         MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_d2prof.so timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 100 --configs c1,c2 > $O/d2prof.log 2>&1
         grep "d2prof" $O/d2prof.log | awk '!seen[$2 $3 $4]++' | head -24
       fi ;;
+    pyr)
+      # single-launch pyramid phase profile (cycles per workgroup) per band count, c1 and c2
+      cd /tmp
+      for nb in ${PYR_BANDS:-8 16 32 64}; do
+        echo "-- MAM_PYR_BANDS=$nb"
+        MAM_PYR_BANDS=$nb MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_pyrprof.so timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 60 --configs c1,c2 > $O/pyrprof_$nb.log 2>&1 || { tail -5 $O/pyrprof_$nb.log; exit 1; }
+        grep "^c" $O/pyrprof_$nb.log; grep "pyrprof" $O/pyrprof_$nb.log | awk '!seen[$2 $3]++'
+      done ;;
     sweep2)
       # DistributeOctTree phase profile per workgroup width; batch stage times with / without the FAST chunks
       cd /tmp
