@@ -1052,18 +1052,37 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
     const Prob& d = probs[blockIdx.x];
     if (d.lm->status) return;
     const int nt = d.nt, n = 6 * d.Np, Np = d.Np;
+    const int t = threadIdx.x, lane = t & 63;
+    // Windows of up to 64 tiles and 128 poses (every window the LDS factorization takes) work on LDS copies of the
+    // pair mask and the tile mask, and run the symbolic factorization and the dependency levels in one wave on 64-bit
+    // tile rows (lane r: row r of L's tile pattern) — the global-memory form below walks the same steps with a barrier
+    // per block column.
+    const bool small = nt <= 64 && Np <= 128;
+    __shared__ uint8_t pm_s[128 * 128];
+    __shared__ uint8_t tm_s[64 * 64];
+    __shared__ int16_t ip_s[128];
+    __shared__ int bw, nnz;
+    const uint8_t* pm = small ? pm_s : d.pairmask;
+    uint8_t* tm = small ? tm_s : d.tmask;
+    const int16_t* ip = small ? ip_s : d.iperm;
+    if (t == 0) bw = 0;
+    if (small)
+        for (int q = t; q < Np * Np; q += SB) pm_s[q] = d.pairmask[q];
+    __syncthreads();
     // The pose order. For a banded pose graph (bandwidth b: poses more than b apart in the window share no landmark),
     // [0, m) | [m + s, Np) reversed | [m, m + s), s >= b: no S entry couples the two ends, so they factor as two
     // independent dependency chains of about half the length and the separator follows (nested dissection, one
     // level; Eigen's SimplicialLDLT orders with AMD for the same reason: linear_solver_eigen.h). m and m + (Np - m - s)
     // are multiples of 8 poses (48 rows: three tiles), so no 16-row tile holds poses of two parts. Kept only when the
     // reordered pattern (its fill included) still fits the LDS factorization; otherwise the window's own order.
-    __shared__ int bw, nnz;
-    if (threadIdx.x == 0) bw = 0;
-    __syncthreads();
-    for (int q = threadIdx.x; q < Np * Np; q += SB) {
-        const int i1 = q / Np, i2 = q % Np;
-        if (i2 > i1 && d.pairmask[q]) atomicMax(&bw, i2 - i1);
+    {
+        int lb = 0;
+        for (int q = t; q < Np * Np; q += SB) {
+            const int i1 = q / Np, i2 = q % Np;
+            if (i2 > i1 && pm[q]) lb = max(lb, i2 - i1);
+        }
+        for (int o = 32; o > 0; o >>= 1) lb = max(lb, __shfl_xor(lb, o, 64));
+        if (lane == 0 && lb > 0) atomicMax(&bw, lb);
     }
     __syncthreads();
     const int b = bw;
@@ -1071,15 +1090,16 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
     while ((Np - sep) % 8) sep++;
     const int m = (Np - sep) / 16 * 8, nb = Np - sep - m;
     for (int attempt = MAM_LBA_ORDER && b > 0 && m >= 8 && nb >= 8 ? 0 : 1; attempt < 2; attempt++) {
-        for (int h = threadIdx.x; h < Np; h += SB) {
+        for (int h = t; h < Np; h += SB) {
             int p = h;
             if (attempt == 0) p = h >= m + sep ? m + (Np - 1 - h) : h >= m ? h + nb : h;
             d.perm[h] = (int16_t)p;
             d.iperm[p] = (int16_t)h;
+            if (small) ip_s[p] = (int16_t)h;
         }
-        if (threadIdx.x == 0) nnz = 0;
+        if (t == 0) nnz = 0;
         __syncthreads();
-        for (int q = threadIdx.x; q < nt * nt; q += SB) {
+        for (int q = t; q < nt * nt; q += SB) {
             const int r = q / nt, c = q % nt;
             uint8_t v = 0;
             if (r == c) {
@@ -1089,42 +1109,66 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
                 if (r0 < r1 && c0 < c1) {
                     for (int p1 = c0 / 6; p1 <= (c1 - 1) / 6 && !v; p1++)
                         for (int p2 = r0 / 6; p2 <= (r1 - 1) / 6 && !v; p2++) {
-                            const int i1 = d.iperm[p1], i2 = d.iperm[p2];
-                            if (i1 == i2 || d.pairmask[(size_t)min(i1, i2) * Np + max(i1, i2)]) v = 1;
+                            const int i1 = ip[p1], i2 = ip[p2];
+                            if (i1 == i2 || pm[(size_t)min(i1, i2) * Np + max(i1, i2)]) v = 1;
                         }
                 }
             }
-            d.tmask[q] = v;
+            tm[q] = v;
         }
         __syncthreads();
-        for (int c = 0; c + 1 < nt; c++) {
-            const int mm = nt - 1 - c;
-            for (int q = threadIdx.x; q < mm * mm; q += SB) {
-                const int r1 = c + 1 + q / mm, r2 = c + 1 + q % mm;
-                if (r2 <= r1 && d.tmask[(size_t)r1 * nt + c] && d.tmask[(size_t)r2 * nt + c])
-                    d.tmask[(size_t)r1 * nt + r2] = 1;
+        if (small) {
+            // the right-looking symbolic LDL^T at tile granularity: column c's pattern is final once the columns before
+            // it are done; every row r1 > c holding tile (r1, c) fills (r1, r2) for the rows c < r2 <= r1 of column c
+            if (t < 64) {
+                uint64_t R = 0;
+                if (lane < nt)
+                    for (int c = 0; c <= lane; c++) R |= (uint64_t)(tm_s[lane * nt + c] != 0) << c;
+                for (int c = 0; c + 1 < nt; c++) {
+                    const uint64_t col = __ballot(((R >> c) & 1) != 0);
+                    if (lane > c && ((R >> c) & 1)) {
+                        const uint64_t upto = lane >= 63 ? ~0ull : ((2ull << lane) - 1);
+                        R |= col & upto & ~((2ull << c) - 1);
+                    }
+                }
+                int cnt = 0;
+                if (lane < nt) {
+                    for (int c = 0; c < nt; c++) tm_s[lane * nt + c] = (uint8_t)((R >> c) & 1);
+                    cnt = __popcll(R);
+                }
+                for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                if (lane == 0) nnz = cnt;
             }
-            __syncthreads();
+        } else {
+            for (int c = 0; c + 1 < nt; c++) {
+                const int mm = nt - 1 - c;
+                for (int q = t; q < mm * mm; q += SB) {
+                    const int r1 = c + 1 + q / mm, r2 = c + 1 + q % mm;
+                    if (r2 <= r1 && tm[(size_t)r1 * nt + c] && tm[(size_t)r2 * nt + c]) tm[(size_t)r1 * nt + r2] = 1;
+                }
+                __syncthreads();
+            }
+            int cnt = 0;
+            for (int q = t; q < nt * nt; q += SB) cnt += tm[q];
+            atomicAdd(&nnz, cnt);
         }
-        int cnt = 0;
-        for (int q = threadIdx.x; q < nt * nt; q += SB) cnt += d.tmask[q];
-        atomicAdd(&nnz, cnt);
         __syncthreads();
         if (attempt == 0 && nt <= LDLT_TILES_NT_MAX &&
             (size_t)nnz * 256 * sizeof(double) + (size_t)d.npad * sizeof(double) <= (size_t)lds_bytes)
             break;   // uniform
         __syncthreads();
     }
+    if (small)
+        for (int q = t; q < nt * nt; q += SB) d.tmask[q] = tm_s[q];
     // the non-zero tiles' slots in ldlt_tiles' LDS pool (row-major order of (r, c), r >= c), their count, and whether
     // the pool and y fit the factorization's dynamic LDS (lds_bytes)
     __shared__ int wsum[SB / 64];
     __shared__ int carry;
-    const int t = threadIdx.x;
     if (t == 0) carry = 0;
     __syncthreads();
     for (int c0 = 0; c0 < nt * nt; c0 += SB) {
         const int q = c0 + t;
-        const int f = (q < nt * nt && d.tmask[q]) ? 1 : 0;
+        const int f = (q < nt * nt && tm[q]) ? 1 : 0;
         int v = f;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1167,38 +1211,30 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
         for (int k = t; k < nt; k += SB) {
             int nc = 0, nr = 0;
             for (int r = k + 1; r < nt; r++)
-                if (d.tmask[(size_t)r * nt + k]) d.clist_g[k * 40 + nc++] = (int8_t)r;
+                if (tm[(size_t)r * nt + k]) d.clist_g[k * 40 + nc++] = (int8_t)r;
             for (int c = 0; c < k; c++)
-                if (d.tmask[(size_t)k * nt + c]) d.rlist_g[k * 40 + nr++] = (int8_t)c;
+                if (tm[(size_t)k * nt + c]) d.rlist_g[k * 40 + nr++] = (int8_t)c;
             d.ccnt_g[k] = (uint8_t)nc;
             d.ccnt_g[nt + k] = (uint8_t)nr;
             atomicMax(&maxc, nc);
         }
         // the dataflow order: block columns by dependency level (1 + the deepest column they pull from), then index —
-        // with the split pose order the two ends' columns alternate (from LDS copies of the row lists: one thread
-        // walks them)
-        __shared__ int8_t rl_s[LDLT_TILES_NT_MAX * 40];
-        __shared__ uint8_t rc_s[LDLT_TILES_NT_MAX];
-        __shared__ int8_t lev[LDLT_TILES_NT_MAX];
-        for (int k = t; k < nt; k += SB) {
-            int nr = 0;
-            for (int c = 0; c < k; c++)
-                if (d.tmask[(size_t)k * nt + c]) rl_s[k * 40 + nr++] = (int8_t)c;
-            rc_s[k] = (uint8_t)nr;
-        }
-        __syncthreads();
-        if (t == 0) {
-            int maxl = 0;
-            for (int k = 0; k < nt; k++) {
-                int l = 0;
-                for (int q = 0; q < rc_s[k]; q++) l = max(l, lev[rl_s[k * 40 + q]] + 1);
-                lev[k] = (int8_t)l;
-                maxl = max(maxl, l);
+        // with the split pose order the two ends' columns alternate. One wave, lane k: column k's parents (the
+        // columns c < k of row k's non-zero tiles) as a bit row; level l = the columns whose parents all have levels
+        // < l (Kahn's layering: the longest dependency path), positions by a prefix count within the level.
+        if (t < 64) {
+            uint64_t P = 0;
+            if (lane < nt)
+                for (int c = 0; c < lane; c++) P |= (uint64_t)(tm[(size_t)lane * nt + c] != 0) << c;
+            const uint64_t all = nt >= 64 ? ~0ull : ((1ull << nt) - 1);
+            uint64_t done = 0;
+            int base = 0;
+            for (int l = 0; done != all && l < 64; l++) {
+                const uint64_t ready = __ballot(lane < nt && !((done >> lane) & 1) && (P & ~done) == 0);
+                if ((ready >> lane) & 1) d.order_g[base + __popcll(ready & ((1ull << lane) - 1))] = (int8_t)lane;
+                base += __popcll(ready);
+                done |= ready;
             }
-            int pos = 0;
-            for (int l = 0; l <= maxl; l++)
-                for (int k = 0; k < nt; k++)
-                    if (lev[k] == l) d.order_g[pos++] = (int8_t)k;
         }
         if (nt > 0)
             for (int q = t; q < nt * 256; q += SB) {

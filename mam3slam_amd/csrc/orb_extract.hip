@@ -92,7 +92,7 @@ struct mam_orb_ctx {
     struct PyrPlan {
         int nb = 0;
         size_t lds = 0;
-        int buf1_off = 0, rc_off = 0;
+        int buf1_off = 0, rc_off = 0, qc_off = 0, qtot = 0;   // LDS carve: level rows, row / column coefficients
         DevBuf<int4> bands;
     };
     std::vector<std::vector<int>> h_yofs;       // resize row tables per level (host copy, l >= 1)
@@ -511,7 +511,11 @@ int build_pyr_plan(mam_orb_ctx* c, int nb) {
     plan->nb = nb;
     plan->buf1_off = (int)((buf[0] + 15) & ~(size_t)15);
     plan->rc_off = (int)((plan->buf1_off + buf[1] + 15) & ~(size_t)15);
-    plan->lds = plan->rc_off + rows_max * 8 + 16;   // +16: pyr_quad's 12-byte window may run past the last row
+    // +16: pyr_quad's 12-byte window may run past the last row
+    plan->qc_off = (int)((plan->rc_off + rows_max * 8 + 16 + 15) & ~(size_t)15);
+    plan->qtot = 0;
+    for (int l = 1; l < L; l++) plan->qtot += (g.L[l].w + 3) / 4;
+    plan->lds = plan->qc_off + (size_t)plan->qtot * 20;
     if (plan->lds > 160 * 1024) return MAM_OK;
     if (int rc = plan->bands.alloc(tab.size())) return rc;
     MAM_HIP(hipMemcpy(plan->bands.p, tab.data(), tab.size() * sizeof(int4), hipMemcpyHostToDevice));
@@ -612,7 +616,7 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
         if (mam_orb_ctx::PyrPlan* pp = choose_pyr_plan(c, F)) {
             // a band's rows per level are few (c1: ~6-20): 1024 threads spread each level over ~1-3 rows per thread
             hipLaunchKernelGGL(mam::k_pyr_bands<1024>, dim3(pp->nb, F), dim3(1024), pp->lds, s, c->d_geom.p, src,
-                               c->d_pyr.p, pp->bands.p, pp->buf1_off, pp->rc_off);
+                               c->d_pyr.p, pp->bands.p, pp->buf1_off, pp->rc_off, pp->qc_off, pp->qtot);
         } else {
             // k_pyr_flat reads whole source words: level 0 rows must be word-aligned and a multiple of 4 wide (the
             // last word of the frame's last row must not run past the caller's buffer)

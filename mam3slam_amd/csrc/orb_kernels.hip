@@ -306,37 +306,57 @@ __global__ __launch_bounds__(256) void k_pyr_down(const Geom* __restrict__ g, in
 // launches (and their per-launch latency, ~10 us each at one frame) become one. Arithmetic identical to
 // k_pyr_down (pyr_quad). Thread t works on quad column q = t % nq for rows t / nq, t / nq + RG, ... so its
 // column coefficients stay in registers for the whole level.
-// One level of k_pyr_bands: rows [bl.x, bl.y) of level l from the LDS rows of level l-1 (first row r0, pitch sp);
-// rc = this level's row coefficients {yofs, ibeta0 | ibeta1 << 16} for rows bl.x.. (LDS).
+
+// A level's parameters for k_pyr_bands, staged once in LDS (the level loop reads no global memory but its stores)
+struct PyrLvl {
+    int w, h, pitch, sh;      // level size and pitch, the source level's height
+    int sp, r0, qbase, rcoff;  // source LDS pitch and first row, the level's quads in the column table, row coefs
+    int4 bl;                   // the band's rows of this level (needed [x, y), owned [z, w))
+    uint8_t* gdst;             // the level in the pyramid buffer (this frame)
+};
+
+// One level of k_pyr_bands: rows [bl.x, bl.y) of level l from the LDS rows of level l-1 (first row P.r0, pitch
+// P.sp); rc = this level's row coefficients {yofs, ibeta0 | ibeta1 << 16} for rows bl.x.. (LDS), qa / qb its quads'
+// packed column coefficients (LevelGeom.qcoef: word 0..3 of the first uint4, word 0 of the second).
 template <int NT>
-__device__ __forceinline__ void pyr_band_level(const LevelGeom& L, int sh, const uint8_t* src, int sp, int r0,
-                                               int4 bl, const int2* rc, uint8_t* lds_dst, bool keep, uint8_t* gdst,
-                                               int tid, const PyrQuad& pre) {
-    const int dp = (L.w + 3) & ~3;
-    const int nq = (L.w + 3) >> 2;
+__device__ __forceinline__ void pyr_band_level(const PyrLvl& P, const uint8_t* src, const int2* rc, const uint4* qa,
+                                               const uint32_t* qb, uint8_t* lds_dst, bool keep, int tid) {
+    const int dp = (P.w + 3) & ~3;
+    const int nq = (P.w + 3) >> 2;
     const int RG = max(1, NT / nq);
+    const int4 bl = P.bl;
     const int nrows = bl.y - bl.x;
     for (int t = tid; t < nq * RG; t += NT) {
         const int q = t % nq, rg = t / nq;
         PyrQuad c;
-        if (t == tid) c = pre;
-        else pyr_quad_setup(L, 4 * q, 0, c);
+        {
+            const uint4 c0 = qa[q];
+            const uint32_t pa[4] = {c0.y, c0.z, c0.w, qb[q]};
+            c.base = (int)(c0.x & 0xFFFu);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                c.o[i] = (int)((c0.x >> (12 + 4 * i)) & 0xFu);
+                c.vec[i] = ((c0.x >> (28 + i)) & 1u) != 0;
+                c.a0[i] = (int)(pa[i] & 0xFFFFu);
+                c.a1[i] = (int)(pa[i] >> 16);
+            }
+        }
 #pragma unroll 2
         for (int r = rg; r < nrows; r += RG) {
             const int dy = bl.x + r;
             const int2 yc = rc[r];
             const int sy = yc.x;
-            const int ry0 = sy >= 0 ? (sy < sh ? sy : sh - 1) : 0;
-            const int ry1 = sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0;
-            const uint32_t packed = pyr_quad(src + (ry0 - r0) * sp, src + (ry1 - r0) * sp, c,
+            const int ry0 = sy >= 0 ? (sy < P.sh ? sy : P.sh - 1) : 0;
+            const int ry1 = sy + 1 >= 0 ? (sy + 1 < P.sh ? sy + 1 : P.sh - 1) : 0;
+            const uint32_t packed = pyr_quad(src + (ry0 - P.r0) * P.sp, src + (ry1 - P.r0) * P.sp, c,
                                              (int)(short)(yc.y & 0xFFFF), yc.y >> 16);
             if (keep) *reinterpret_cast<uint32_t*>(lds_dst + r * dp + 4 * q) = packed;
             if (dy >= bl.z && dy < bl.w) {
-                uint8_t* o = gdst + (size_t)dy * L.pitch + 4 * q;
-                if (4 * q + 4 <= L.w) {
+                uint8_t* o = P.gdst + (size_t)dy * P.pitch + 4 * q;
+                if (4 * q + 4 <= P.w) {
                     *reinterpret_cast<uint32_t*>(o) = packed;
                 } else {
-                    for (int i = 0; i < 4 && 4 * q + i < L.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+                    for (int i = 0; i < 4 && 4 * q + i < P.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
                 }
             }
         }
@@ -344,8 +364,8 @@ __device__ __forceinline__ void pyr_band_level(const LevelGeom& L, int sh, const
 }
 
 #ifdef MAM_PYR_PROFILE
-// cycles per phase summed over workgroups (thread 0): [0] prologue (level-0 rows + row coefficients staged), [l] level
-// l, [9] workgroups
+// cycles per phase summed over workgroups (thread 0): [0] prologue (level-0 rows + row / column coefficients staged),
+// [l] level l, [9] workgroups
 __device__ unsigned long long g_pyrprof[10];
 #define PYRP(k)                                                                        \
     do {                                                                               \
@@ -359,29 +379,58 @@ __device__ unsigned long long g_pyrprof[10];
 #define PYRP(k) do {} while (0)
 #endif
 
-// LDS: [even levels' rows (level 0 staged from the frame)] [odd levels' rows] [row coefficients of every level].
-// The prologue puts everything with a global-memory latency in flight at once (level-0 rows, all row coefficients);
-// each level's column coefficients are fetched into registers while the previous level computes.
+// LDS: [even levels' rows (level 0 staged from the frame)] [odd levels' rows] [row coefficients of every level]
+// [column coefficients of every level: qtot uint4, then qtot words]. The prologue puts everything with a global-memory
+// latency in flight at once (level-0 rows, all row and column coefficients, the levels' parameters); the level loop
+// then reads LDS only — each level is its compute and one barrier (a global load per level, the coefficient prefetch
+// of the round-4 form, measured ~3-5 us per level at one frame: the chain of levels paid it seven times).
 template <int NT>
 __global__ __launch_bounds__(NT) void k_pyr_bands(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ pyr,
-                                                   const int4* __restrict__ bands, int buf1_off, int rc_off) {
+                                                   const int4* __restrict__ bands, int buf1_off, int rc_off,
+                                                   int qc_off, int qtot) {
     extern __shared__ __attribute__((aligned(16))) uint8_t pbuf[];
+    __shared__ PyrLvl lv[MAM_MAX_LEVELS];
     const int j = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, NL = g->nlevels;
     const int4* B = bands + (size_t)j * NL;
     int2* rcoef = reinterpret_cast<int2*>(pbuf + rc_off);
+    uint4* qa = reinterpret_cast<uint4*>(pbuf + qc_off);
+    uint32_t* qb = reinterpret_cast<uint32_t*>(pbuf + qc_off + (size_t)qtot * 16);
 #ifdef MAM_PYR_PROFILE
     long long pt0 = clock64();
     if (tid == 0) atomicAdd(&g_pyrprof[9], 1ull);
 #endif
-    // ---- prologue: level-0 rows [B[0].x, B[0].y) and the row coefficients of every level
+    // ---- prologue
+    if (tid < NL) {
+        // the levels' parameters (each thread sums the row / quad offsets of the levels below its own)
+        const int l = tid;
+        const LevelGeom& L = g->L[l];
+        PyrLvl P;
+        P.w = L.w;
+        P.h = L.h;
+        P.pitch = L.pitch;
+        P.bl = B[l];
+        P.gdst = pyr + L.pyr_off + (size_t)f * L.frame_bytes;
+        P.sh = l > 0 ? g->L[l - 1].h : 0;
+        P.sp = l > 0 ? ((g->L[l - 1].w + 3) & ~3) : 0;
+        P.r0 = l > 0 ? B[l - 1].x : 0;
+        int qb0 = 0, rc0 = 0;
+        for (int k = 1; k < l; k++) {
+            qb0 += (g->L[k].w + 3) >> 2;
+            const int4 bk = B[k];
+            rc0 += bk.y - bk.x;
+        }
+        P.qbase = qb0;
+        P.rcoff = rc0;
+        lv[l] = P;
+    }
     {
+        // level-0 rows [B[0].x, B[0].y), the band's row coefficients of every level, the column coefficients of every
+        // level: loads first (8 per thread in flight), then the LDS stores
         const int4 b0 = B[0];
         const int w0 = g->L[0].w, p0 = (w0 + 3) & ~3;
         const uint8_t* in = s.in0 + (size_t)f * s.in_fstride;
         const int nr = b0.y - b0.x;
         if (((s.in_stride | (size_t)in | (size_t)w0) & 3) == 0) {
-            // 8 loads in flight per thread before the LDS stores (a load-store loop would wait out one global
-            // latency per word)
             const int wpr = w0 >> 2, nw = nr * wpr;
             for (int i0 = 0; i0 < nw; i0 += 8 * NT) {
                 uint32_t v[8];
@@ -405,32 +454,28 @@ __global__ __launch_bounds__(NT) void k_pyr_bands(const Geom* __restrict__ g, Le
                 pbuf[r * p0 + c] = in[(size_t)(b0.x + r) * s.in_stride + c];
             }
         }
+        const uint4* qg = g->L[1].qcoef;   // the levels' tables are contiguous from level 1 on
+        for (int i = tid; i < qtot; i += NT) {
+            const uint4 a = qg[2 * i];
+            const uint32_t bw = qg[2 * i + 1].x;
+            qa[i] = a;
+            qb[i] = bw;
+        }
         int off = 0;
         for (int l = 1; l < NL; l++) {
-            const LevelGeom& L = g->L[l];
             const int4 bl = B[l];
-            for (int r = tid; r < bl.y - bl.x; r += NT) {
-                const int dy = bl.x + r;
-                rcoef[off + r] = make_int2(L.yofs[dy], (L.ibeta[2 * dy] & 0xFFFF) | ((int)L.ibeta[2 * dy + 1] << 16));
-            }
+            const int2* rg = g->L[l].rcoef;
+            for (int r = tid; r < bl.y - bl.x; r += NT) rcoef[off + r] = rg[bl.x + r];
             off += bl.y - bl.x;
         }
     }
-    PyrQuad pre;
-    pyr_quad_setup(g->L[1], 4 * (tid % ((g->L[1].w + 3) >> 2)), 0, pre);
     __syncthreads();
     PYRP(0);
-    int off = 0;
     for (int l = 1; l < NL; l++) {
-        const LevelGeom& L = g->L[l];
-        const int4 bl = B[l];
-        const PyrQuad cur = pre;
-        if (l + 1 < NL) pyr_quad_setup(g->L[l + 1], 4 * (tid % ((g->L[l + 1].w + 3) >> 2)), 0, pre);
+        const PyrLvl& P = lv[l];
         const uint8_t* src = pbuf + ((l - 1) & 1 ? buf1_off : 0);
-        pyr_band_level<NT>(L, g->L[l - 1].h, src, (g->L[l - 1].w + 3) & ~3, B[l - 1].x, bl, rcoef + off,
-                       pbuf + (l & 1 ? buf1_off : 0), l + 1 < NL, pyr + L.pyr_off + (size_t)f * L.frame_bytes, tid,
-                       cur);
-        off += bl.y - bl.x;
+        pyr_band_level<NT>(P, src, rcoef + P.rcoff, qa + P.qbase, qb + P.qbase, pbuf + (l & 1 ? buf1_off : 0),
+                           l + 1 < NL, tid);
         __syncthreads();
         PYRP(l);
     }
