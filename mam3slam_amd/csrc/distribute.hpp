@@ -78,6 +78,9 @@ __device__ __forceinline__ int quad2(uint2 r, uint32_t key) {
 // cnt[t] += 1 for every active lane with t >= 0: lanes of the wave with the same target are counted by ballot and
 // added by one leader (the early rounds send whole waves to the same few nodes: per-lane LDS atomics on one address
 // serialise), up to AGG distinct targets per call; lanes left after that add one by one
+#ifndef MAM_DIST_AGG
+#define MAM_DIST_AGG 8   // distinct targets aggregated per wave in the count passes (0: plain LDS atomics)
+#endif
 template <int AGG>
 __device__ __forceinline__ void agg_add(uint32_t* cnt, int t) {
 #pragma unroll
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
     for_keys([&](uint32_t key, uint32_t& nd, int) {
         const int i = (int)((float)(key & 0xFFF) / L.hX);   // vpIniNodes[kp.pt.x / hX]
         nd = (uint32_t)i;
-        dist::agg_add<4>(cnt1, i);
+        dist::agg_add<(MAM_DIST_AGG < 4 ? MAM_DIST_AGG : 4)>(cnt1, i);
     });
     __syncthreads();
     int S = 0;
@@ -263,7 +266,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
         } else {
             nd = (uint32_t)p;
         }
-        dist::agg_add<8>(reinterpret_cast<uint32_t*>(chc0), t);
+        dist::agg_add<MAM_DIST_AGG>(reinterpret_cast<uint32_t*>(chc0), t);
     });
     __syncthreads();
     D2P(0);
@@ -450,7 +453,7 @@ __global__ __launch_bounds__(NT) void k_distribute2(const Geom* __restrict__ g, 
             } else {
                 nd = (uint32_t)np;
             }
-            if (count_next) dist::agg_add<8>(reinterpret_cast<uint32_t*>(CHn), t);
+            if (count_next) dist::agg_add<MAM_DIST_AGG>(reinterpret_cast<uint32_t*>(CHn), t);
         });
         if (count_next) __syncthreads();
         D2P(6);

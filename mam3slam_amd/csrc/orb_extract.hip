@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -913,17 +914,35 @@ int mam_orb_extract(mam_orb_ctx* c, const uint8_t* img, int w, int h, size_t str
     if (int rc = c->d_out.alloc(out_bytes)) return rc;
     if (int rc = c->h_in.alloc(in_bytes)) return rc;
     if (int rc = c->h_out.alloc(out_bytes)) return rc;
+    // MAM_ORB_HOST_PROFILE=1: the call's host phases (microseconds, averaged over 200 calls) on stderr
+    static const bool hprof = [] {
+        const char* e = getenv("MAM_ORB_HOST_PROFILE");
+        return e && atoi(e) == 1;
+    }();
+    using hclock = std::chrono::steady_clock;
+    hclock::time_point ht[7];
+    if (hprof) ht[0] = hclock::now();
     if (stride == (size_t)w) std::memcpy(c->h_in.p, img, in_bytes);
     else
         for (int y = 0; y < h; y++) std::memcpy(c->h_in.p + (size_t)y * w, img + (size_t)y * stride, w);
+    if (hprof) ht[1] = hclock::now();
     MAM_HIP(hipMemcpyAsync(c->d_input.p, c->h_in.p, in_bytes, hipMemcpyHostToDevice, c->stream));
+    if (hprof) ht[2] = hclock::now();
     int32_t* d_cnt = reinterpret_cast<int32_t*>(c->d_out.p);
     mam_keypoint* d_kp = reinterpret_cast<mam_keypoint*>(c->d_out.p + kp_off);
     uint8_t* d_ds = c->d_out.p + desc_off;
     if (int rc = run_pipeline(c, c->d_input.p, 1, w, in_bytes, lap0, lap1, d_kp, d_ds, kcap, d_cnt, c->stream))
         return rc;
+    if (hprof) ht[3] = hclock::now();
     MAM_HIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    if (hprof) ht[4] = hclock::now();
     MAM_HIP(hipStreamSynchronize(c->stream));
+    if (hprof) ht[5] = hclock::now();
+    struct HostProf {
+        double acc[6] = {};
+        int n = 0;
+    };
+    static HostProf hp;
     int32_t cnt[2];
     std::memcpy(cnt, c->h_out.p, sizeof(cnt));
     if (cnt[0] < 0) { g_last_error = "internal keypoint slot overflow"; return MAM_ERR_DEVICE; }
@@ -933,6 +952,16 @@ int mam_orb_extract(mam_orb_ctx* c, const uint8_t* img, int w, int h, size_t str
     if (cnt[0] > 0) {
         std::memcpy(kps, c->h_out.p + kp_off, sizeof(mam_keypoint) * (size_t)cnt[0]);
         std::memcpy(desc, c->h_out.p + desc_off, (size_t)cnt[0] * 32);
+    }
+    if (hprof) {
+        ht[6] = hclock::now();
+        for (int k = 0; k < 6; k++) hp.acc[k] += std::chrono::duration<double, std::micro>(ht[k + 1] - ht[k]).count();
+        if (++hp.n == 200) {
+            fprintf(stderr, "orb host %dx%d: memcpy-in %.1f h2d-enqueue %.1f pipeline-enqueue %.1f d2h-enqueue %.1f "
+                    "sync-wait %.1f copy-out %.1f us (out %zu B)\n", w, h, hp.acc[0] / 200, hp.acc[1] / 200,
+                    hp.acc[2] / 200, hp.acc[3] / 200, hp.acc[4] / 200, hp.acc[5] / 200, out_bytes);
+            hp = HostProf{};
+        }
     }
     return MAM_OK;
 }
