@@ -121,8 +121,10 @@ int mam_orb_debug_blurred(mam_orb_ctx* ctx, int frame, int level, uint8_t* out);
  * the blur beside the other levels' FAST, on the context's side streams), 1 on / 0 off / -1 automatic (off: the
  * cross-stream waits cost more than the overlap gains on MI355X).
  * MAM_ORB_OPT_FAST_CHUNKS: FAST over chunks of up to 4 cells of a cell row (k_fast_chunks) instead of one workgroup per
- * cell (k_fast_cells): 1 on / 0 off / -1 automatic. */
-enum { MAM_ORB_OPT_DISTRIBUTE_THREADS = 1, MAM_ORB_OPT_FORK = 2, MAM_ORB_OPT_FAST_CHUNKS = 3 };
+ * cell (k_fast_cells): 1 on / 0 off / -1 automatic.
+ * MAM_ORB_OPT_FAST_BLUR: FAST and the blur in one launch (k_fast_blur) instead of two: 1 on / 0 off / -1 automatic
+ * (on for up to 4 frames per call). */
+enum { MAM_ORB_OPT_DISTRIBUTE_THREADS = 1, MAM_ORB_OPT_FORK = 2, MAM_ORB_OPT_FAST_CHUNKS = 3, MAM_ORB_OPT_FAST_BLUR = 4 };
 int mam_orb_debug_set_option(mam_orb_ctx* ctx, int option, int value);
 
 /* Last HIP error string for MAM_ERR_DEVICE. */

@@ -79,7 +79,7 @@ __device__ __forceinline__ int quad2(uint2 r, uint32_t key) {
 // added by one leader (the early rounds send whole waves to the same few nodes: per-lane LDS atomics on one address
 // serialise), up to AGG distinct targets per call; lanes left after that add one by one
 #ifndef MAM_DIST_AGG
-#define MAM_DIST_AGG 8   // distinct targets aggregated per wave in the count passes (0: plain LDS atomics)
+#define MAM_DIST_AGG 1   // distinct targets aggregated per wave in the count passes (0: plain LDS atomics; 1 measured best: 2 / 8 cost more issue than the conflicts they save)
 #endif
 template <int AGG>
 __device__ __forceinline__ void agg_add(uint32_t* cnt, int t) {

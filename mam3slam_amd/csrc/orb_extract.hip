@@ -89,6 +89,7 @@ struct mam_orb_ctx {
     size_t fastc_lds = 0;
     int chunk_base[MAM_MAX_LEVELS + 1] = {};
     int fast_chunks = -1;   // k_fast_chunks instead of k_fast_cells (mam_orb_debug_set_option), -1 = automatic
+    int fast_blur = -1;     // FAST + blur in one launch (k_fast_blur; mam_orb_debug_set_option), -1 = automatic
     // single-launch pyramid (k_pyr_bands): per band count, the band table and its LDS carve
     struct PyrPlan {
         int nb = 0;
@@ -408,7 +409,11 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         if (!c->chunks.empty())
             MAM_HIP(hipMemcpy(c->d_chunks.p, c->chunks.data(), c->chunks.size() * sizeof(mam::ChunkDesc),
                               hipMemcpyHostToDevice));
-        for (const void* fn : {reinterpret_cast<const void*>(&mam::k_fast_chunks<64>),
+        for (const void* fn : {reinterpret_cast<const void*>(&mam::k_fast_blur<24>),
+                               reinterpret_cast<const void*>(&mam::k_fast_blur<32>),
+                               reinterpret_cast<const void*>(&mam::k_fast_blur<40>),
+                               reinterpret_cast<const void*>(&mam::k_fast_blur<48>),
+                               reinterpret_cast<const void*>(&mam::k_fast_chunks<64>),
                                reinterpret_cast<const void*>(&mam::k_fast_chunks<80>),
                                reinterpret_cast<const void*>(&mam::k_fast_chunks<96>),
                                reinterpret_cast<const void*>(&mam::k_fast_chunks<112>),
@@ -596,6 +601,18 @@ bool fast_chunks_enabled(const mam_orb_ctx* c) {
     return v == 1 && c->fastc_cw > 0;
 }
 
+// FAST + blur in one launch (k_fast_blur) for up to 4 frames per call (latency: one dependent launch less);
+// MAM_FAST_BLUR=0 / 1 or the context option override
+bool fast_blur_enabled(const mam_orb_ctx* c, int F) {
+    static const int env = [] {
+        const char* e = getenv("MAM_FAST_BLUR");
+        return e ? atoi(e) : -1;
+    }();
+    const int v = c->fast_blur >= 0 ? c->fast_blur : env;
+    if (v == 0 || v == 1) return v == 1;
+    return F <= 4;
+}
+
 // Latency mode (run_pipeline's three-stream dataflow) for up to 4 frames per call; MAM_ORB_FORK=0 / the context
 // option turn it off (one stream, stages in order).
 bool fork_enabled(const mam_orb_ctx* c, int F, int nt) {
@@ -723,16 +740,35 @@ int run_pipeline(mam_orb_ctx* c, const uint8_t* d_in, int F, size_t stride, size
             StageScope sc(&c->timer, s, MAM_STAGE_PYRAMID);
             launch_pyramid(s);
         }
-        // (blur and FAST both keep the CUs' issue slots busy in a batch: running the blur on a second stream beside
-        // FAST + DistributeOctTree measured no gain there, so batches keep the stages in order on one stream)
-        {
-            StageScope sc(&c->timer, s, MAM_STAGE_BLUR);
-            hipLaunchKernelGGL(mam::k_blur7, dim3((g.tiles_per_frame + mam::BLUR_TPB - 1) / mam::BLUR_TPB, F), dim3(256),
-                               0, s, c->d_geom.p, src, c->d_blur.p);
-        }
-        {
+        if (!chunked && fast_blur_enabled(c, F)) {
+            // one launch: every cell's FAST and the blur tile groups (the blur's time counts in the FAST stage)
             StageScope sc(&c->timer, s, MAM_STAGE_FAST);
-            launch_fast_levels(s, 0, L);
+            const int ng = (g.tiles_per_frame + mam::BLUR_TPB - 1) / mam::BLUR_TPB;
+            const dim3 fg(g.cells_per_frame + ng, F), fb(mam::FAST_THREADS);
+            const size_t lds = std::max(c->fast_lds, mam::BLUR_LDS_BYTES);
+#define MAM_FASTB(CW_)                                                                                                \
+    case CW_: hipLaunchKernelGGL(mam::k_fast_blur<CW_>, fg, fb, lds, s, c->d_geom.p, c->d_cells.p, src, c->d_cand.p,   \
+                                 c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast, 0, g.cells_per_frame,         \
+                                 c->d_blur.p); break
+            switch (c->fast_cw) {
+                MAM_FASTB(24); MAM_FASTB(32); MAM_FASTB(40);
+                default: hipLaunchKernelGGL(mam::k_fast_blur<48>, fg, fb, lds, s, c->d_geom.p, c->d_cells.p, src,
+                                            c->d_cand.p, c->d_cellcnt.p, c->prm.ini_th_fast, c->prm.min_th_fast, 0,
+                                            g.cells_per_frame, c->d_blur.p); break;
+            }
+#undef MAM_FASTB
+        } else {
+            // (blur and FAST both keep the CUs' issue slots busy in a batch: running the blur on a second stream
+            // beside FAST + DistributeOctTree measured no gain there, so batches keep the stages in order)
+            {
+                StageScope sc(&c->timer, s, MAM_STAGE_BLUR);
+                hipLaunchKernelGGL(mam::k_blur7, dim3((g.tiles_per_frame + mam::BLUR_TPB - 1) / mam::BLUR_TPB, F),
+                                   dim3(256), 0, s, c->d_geom.p, src, c->d_blur.p);
+            }
+            {
+                StageScope sc(&c->timer, s, MAM_STAGE_FAST);
+                launch_fast_levels(s, 0, L);
+            }
         }
         {
             StageScope sc(&c->timer, s, MAM_STAGE_DISTRIBUTE);
@@ -928,13 +964,25 @@ int mam_orb_extract(mam_orb_ctx* c, const uint8_t* img, int w, int h, size_t str
     if (hprof) ht[1] = hclock::now();
     MAM_HIP(hipMemcpyAsync(c->d_input.p, c->h_in.p, in_bytes, hipMemcpyHostToDevice, c->stream));
     if (hprof) ht[2] = hclock::now();
-    int32_t* d_cnt = reinterpret_cast<int32_t*>(c->d_out.p);
-    mam_keypoint* d_kp = reinterpret_cast<mam_keypoint*>(c->d_out.p + kp_off);
-    uint8_t* d_ds = c->d_out.p + desc_off;
+    // the descriptor kernel writes the counts, keypoints and descriptors straight into the pinned host block (its
+    // device mapping): no device-to-host copy launch after it (MAM_ORB_ZERO_COPY_OUT=0: the copy)
+    static const bool zc_out = [] {
+        const char* e = getenv("MAM_ORB_ZERO_COPY_OUT");
+        return !(e && atoi(e) == 0);
+    }();
+    uint8_t* outp = c->d_out.p;
+    if (zc_out) {
+        void* dp = nullptr;
+        MAM_HIP(hipHostGetDevicePointer(&dp, c->h_out.p, 0));
+        outp = static_cast<uint8_t*>(dp);
+    }
+    int32_t* d_cnt = reinterpret_cast<int32_t*>(outp);
+    mam_keypoint* d_kp = reinterpret_cast<mam_keypoint*>(outp + kp_off);
+    uint8_t* d_ds = outp + desc_off;
     if (int rc = run_pipeline(c, c->d_input.p, 1, w, in_bytes, lap0, lap1, d_kp, d_ds, kcap, d_cnt, c->stream))
         return rc;
     if (hprof) ht[3] = hclock::now();
-    MAM_HIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    if (!zc_out) MAM_HIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
     if (hprof) ht[4] = hclock::now();
     MAM_HIP(hipStreamSynchronize(c->stream));
     if (hprof) ht[5] = hclock::now();
@@ -1028,6 +1076,10 @@ int mam_orb_debug_set_option(mam_orb_ctx* c, int option, int value) {
         case MAM_ORB_OPT_FORK:
             if (value < -1 || value > 1) return MAM_ERR_ARG;
             c->fork = value;
+            return MAM_OK;
+        case MAM_ORB_OPT_FAST_BLUR:
+            if (value < -1 || value > 1) return MAM_ERR_ARG;
+            c->fast_blur = value;
             return MAM_OK;
         default: return MAM_ERR_ARG;
     }

@@ -572,26 +572,13 @@ __device__ __forceinline__ half2_t fast_strength_h2(const half2_t* hp, int r, in
 // (e) corners written in row-major order (pair order = pixel order) at ballot prefix positions.
 // Issue/latency-bound per workgroup (PMC: VALU busy ~11 %, a third of the wave cycles waiting, a third issue-stalled;
 // the circle test is ~a quarter of the time, staging without global loads is no faster): DESIGN.md §3 / §6.
+// One cell (cell_i of frame f) by one workgroup; smem: fast_lds_bytes() of dynamic LDS
 template <int CW>
-__global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restrict__ g,
-                                                             const CellDesc* __restrict__ cells, LevelSrc s,
-                                                             uint32_t* __restrict__ cand,
-                                                             int* __restrict__ cell_counts, int iniTh, int minTh,
-                                                             int cell_first) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+__device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
+                                               const LevelSrc& s, uint32_t* __restrict__ cand,
+                                               int* __restrict__ cell_counts, int iniTh, int minTh, int cell_i, int f,
+                                               uint8_t* smem) {
     constexpr int T = FAST_THREADS, NW = FAST_THREADS / 64;
-#ifndef MAM_FAST_XCD
-#define MAM_FAST_XCD 1
-#endif
-    // XCD-aware order (as k_blur7): each XCD works a contiguous range of (frame, cell) ids, so the ROI rows adjacent
-    // cells share (6-pixel overlaps, 128-byte lines spanning ~4 cells) are fetched into one L2 instead of up to four
-    int cell_i = blockIdx.x, f = blockIdx.y;
-    if (MAM_FAST_XCD) {
-        const int logical = xcd_logical(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-        f = logical / gridDim.x;
-        cell_i = logical - f * gridDim.x;
-    }
-    cell_i += cell_first;   // a launch over the cells [cell_first, cell_first + gridDim.x) of every frame
     const CellDesc c = cells[cell_i];
     const LevelGeom& L = g->L[c.level];
     const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
@@ -765,6 +752,28 @@ __global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restr
         }
     }
     if (tid == 0) cell_counts[(size_t)f * g->cells_per_frame + cell_i] = use_hi ? tot_hi : tot_lo;
+}
+
+#ifndef MAM_FAST_XCD
+#define MAM_FAST_XCD 1
+#endif
+template <int CW>
+__global__ __launch_bounds__(FAST_THREADS) void k_fast_cells(const Geom* __restrict__ g,
+                                                             const CellDesc* __restrict__ cells, LevelSrc s,
+                                                             uint32_t* __restrict__ cand,
+                                                             int* __restrict__ cell_counts, int iniTh, int minTh,
+                                                             int cell_first) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // XCD-aware order (as k_blur7): each XCD works a contiguous range of (frame, cell) ids, so the ROI rows adjacent
+    // cells share (6-pixel overlaps, 128-byte lines spanning ~4 cells) are fetched into one L2 instead of up to four
+    int cell_i = blockIdx.x, f = blockIdx.y;
+    if (MAM_FAST_XCD) {
+        const int logical = xcd_logical(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+        f = logical / gridDim.x;
+        cell_i = logical - f * gridDim.x;
+    }
+    cell_i += cell_first;   // a launch over the cells [cell_first, cell_first + gridDim.x) of every frame
+    fast_cell_body<CW>(g, cells, s, cand, cell_counts, iniTh, minTh, cell_i, f, smem);
 }
 
 // ---- FAST over chunks of a cell row (the band formulation): one workgroup per (frame, chunk of up to FAST_G
@@ -1082,25 +1091,13 @@ __device__ __forceinline__ void blur_fetch(const BlurTile& t, int tid, uint32_t 
 // Workgroup = BLUR_TPB consecutive tiles of one frame (possibly of different levels), software-pipelined: the next
 // tile's words are loaded into registers while this tile's horizontal and vertical passes run, so the load latency
 // of a tile is hidden behind the previous one's arithmetic.
-__global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ blur) {
-    __shared__ __attribute__((aligned(16))) uint8_t tin[BLUR_IN_H][BLUR_IN_W];
-    __shared__ __attribute__((aligned(16))) uint16_t th_[BLUR_IN_H][BLUR_TILE_W];
-#ifndef MAM_BLUR_XCD
-#define MAM_BLUR_XCD 1
-#endif
-    // XCD-aware order: the hardware deals linear block ids round-robin over the 8 XCDs; remap them (bijectively, any
-    // grid size) so each XCD works a contiguous range of (frame, tile) ids, putting vertically adjacent tiles, whose
-    // staged halo rows overlap, on the same L2
-    const int nlin = gridDim.x * gridDim.y;
-    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
-    int logical = lin;
-    if (MAM_BLUR_XCD) {
-        const int q = nlin >> 3, rem = nlin & 7, x = lin & 7, k = lin >> 3;
-        logical = x < rem ? x * (q + 1) + k : rem * (q + 1) + (x - rem) * q + k;
-    }
-    const int f = logical / gridDim.x;
+constexpr size_t BLUR_LDS_BYTES = ((size_t)BLUR_IN_H * BLUR_IN_W + 15) / 16 * 16 + (size_t)BLUR_IN_H * BLUR_TILE_W * 2;
+// Tile group `grp` (BLUR_TPB consecutive tiles) of frame f; tin / th_: the staged bytes and the horizontal sums (LDS)
+__device__ __forceinline__ void blur_group_body(const Geom* __restrict__ g, const LevelSrc& s,
+                                                uint8_t* __restrict__ blur, int f, int grp,
+                                                uint8_t (*tin)[BLUR_IN_W], uint16_t (*th_)[BLUR_TILE_W]) {
     const int tid = threadIdx.x;
-    const int tile0 = (logical - f * gridDim.x) * BLUR_TPB;
+    const int tile0 = grp * BLUR_TPB;
     const int ntiles = min(BLUR_TPB, g->tiles_per_frame - tile0);
     uint32_t v[BLUR_NIT];
     BlurTile t = blur_tile(g, s, f, tile0);
@@ -1180,6 +1177,47 @@ __global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, Level
                     for (int c = 0; c < 4 && x + c < w; c++) o[c] = (uint8_t)(packed >> (8 * c));
             }
         }
+    }
+}
+
+#ifndef MAM_BLUR_XCD
+#define MAM_BLUR_XCD 1
+#endif
+// XCD-aware order: the hardware deals linear block ids round-robin over the 8 XCDs; remap them (bijectively, any grid
+// size) so each XCD works a contiguous range of (frame, tile) ids, putting vertically adjacent tiles, whose staged halo
+// rows overlap, on the same L2
+__device__ __forceinline__ int blur_xcd_logical(int lin, int nlin) {
+    if (!MAM_BLUR_XCD) return lin;
+    const int q = nlin >> 3, rem = nlin & 7, x = lin & 7, k = lin >> 3;
+    return x < rem ? x * (q + 1) + k : rem * (q + 1) + (x - rem) * q + k;
+}
+__global__ __launch_bounds__(256) void k_blur7(const Geom* __restrict__ g, LevelSrc s, uint8_t* __restrict__ blur) {
+    __shared__ __attribute__((aligned(16))) uint8_t tin[BLUR_IN_H][BLUR_IN_W];
+    __shared__ __attribute__((aligned(16))) uint16_t th_[BLUR_IN_H][BLUR_TILE_W];
+    const int logical = blur_xcd_logical(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int f = logical / gridDim.x;
+    blur_group_body(g, s, blur, f, logical - f * gridDim.x, tin, th_);
+}
+
+// Latency mode (a few frames): FAST over cells [cell_first, cell_first + ncells) and the blur of every level in ONE
+// launch — blocks [0, ncells) of a frame row take a cell, blocks [ncells, ncells + ngroups) a blur tile group. Both
+// stages read only the pyramid, so the blur runs beside FAST instead of in its own launch (one dependent launch less
+// on the extraction's critical path). Dynamic LDS: max(fast_lds_bytes, BLUR_LDS_BYTES).
+template <int CW>
+__global__ __launch_bounds__(FAST_THREADS) void k_fast_blur(const Geom* __restrict__ g,
+                                                            const CellDesc* __restrict__ cells, LevelSrc s,
+                                                            uint32_t* __restrict__ cand, int* __restrict__ cell_counts,
+                                                            int iniTh, int minTh, int cell_first, int ncells,
+                                                            uint8_t* __restrict__ blur) {
+    static_assert(FAST_THREADS == 256, "the blur tile group takes 256 threads");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int f = blockIdx.y;
+    if ((int)blockIdx.x < ncells) {
+        fast_cell_body<CW>(g, cells, s, cand, cell_counts, iniTh, minTh, cell_first + (int)blockIdx.x, f, smem);
+    } else {
+        blur_group_body(g, s, blur, f, (int)blockIdx.x - ncells, reinterpret_cast<uint8_t (*)[BLUR_IN_W]>(smem),
+                        reinterpret_cast<uint16_t (*)[BLUR_TILE_W]>(
+                            smem + ((size_t)BLUR_IN_H * BLUR_IN_W + 15) / 16 * 16));
     }
 }
 

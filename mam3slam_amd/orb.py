@@ -154,6 +154,10 @@ class ORBextractor:
         """FAST over chunks of a cell row (k_fast_chunks) instead of one workgroup per cell: 1 on, 0 off, -1 auto."""
         check(lib().mam_orb_debug_set_option(self._ctx, 3, int(on)), "mam_orb_debug_set_option")
 
+    def set_fast_blur(self, on: int):
+        """FAST and the blur in one launch (k_fast_blur) instead of two: 1 on, 0 off, -1 automatic (few frames)."""
+        check(lib().mam_orb_debug_set_option(self._ctx, 4, int(on)), "mam_orb_debug_set_option")
+
     def debug_candidates(self, level: int, frame: int = 0) -> np.ndarray:
         n = check(lib().mam_orb_debug_candidates(self._ctx, frame, level, None, 0), "debug_candidates")
         out = np.zeros(max(n, 1), np.uint32)

@@ -49,8 +49,14 @@ PY
         MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_$v.so timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 100 --configs c1,c2 > $O/agg_$v.log 2>&1 || { tail -5 $O/agg_$v.log; exit 1; }
         grep "^c" $O/agg_$v.log; grep "d2prof" $O/agg_$v.log | awk '!seen[$2 $3 $4]++' | grep -E " l0:| l7:"
       done
-      MAM_ORB_HOST_PROFILE=1 timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 400 --configs c1,c2 > $O/hostprof.log 2>&1 || { tail -5 $O/hostprof.log; exit 1; }
-      grep -E "^c|orb host" $O/hostprof.log | awk '!seen[$1 $2 $3]++' ;;
+      ;;
+    hostprof)
+      cd /tmp
+      for v in ${HOSTPROF_ENVS:-MAM_ORB_ZERO_COPY_OUT=1}; do
+        echo "-- $v"
+        env $v MAM_ORB_HOST_PROFILE=1 timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 400 --configs c1,c2 > $O/hostprof.log 2>&1 || { tail -5 $O/hostprof.log; exit 1; }
+        grep -E "^c|orb host" $O/hostprof.log | awk '!seen[$1 $2 $3]++'
+      done ;;
     sweep2)
       # DistributeOctTree phase profile per workgroup width; batch stage times with / without the FAST chunks
       cd /tmp

@@ -285,3 +285,41 @@ def test_fast_chunks_bit_exact(gpu_lib, oracle, w, h, nfeat):
     kg, dg, mg = ext(img)
     _assert_kps_equal(kg, dg, mg, *oracle.extract(img, p), f"chunks {w}x{h}/{nfeat} no fork")
     ext.close()
+
+
+@pytest.mark.parametrize("fb", [0, 1])
+def test_fast_blur_launch_bit_exact(gpu_lib, oracle, fb):
+    """FAST and the blur in one launch (k_fast_blur, the latency-mode default) or in two (k_blur7 + k_fast_cells):
+    the oracle's keypoints, descriptors and blurred levels either way, single frames through the host API and a
+    device batch of 3 frames."""
+    import torch
+
+    from mam3slam_amd.orb import KP_DTYPE
+
+    for w, h, nfeat in CASES[:3]:
+        ext = _extractor(nfeat)
+        ext.set_fast_blur(fb)
+        p = oracle.params(nfeat)
+        imgs = np.stack([synth.make_frame(w, h, agent=8, frame=i) for i in range(3)])
+        for i in range(2):
+            kg, dg, mg = ext(imgs[i])
+            _assert_kps_equal(kg, dg, mg, *oracle.extract(imgs[i], p), f"fast_blur {fb} {w}x{h}/{nfeat} frame {i}")
+        levels = oracle.pyramid(imgs[1], p)
+        for l in (0, 3, 7):
+            d = _first_diff(ext.debug_blurred(l), oracle.gaussian7(levels[l]))
+            assert d is None, f"fast_blur {fb} {w}x{h} blurred level {l} pixel {d}"
+        F = 3
+        cap = ext.max_keypoints()
+        d_img = torch.from_numpy(imgs).cuda()
+        d_kps = torch.zeros((F, cap * 28), dtype=torch.uint8, device="cuda")
+        d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device="cuda")
+        d_cnt = torch.zeros((F, 2), dtype=torch.int32, device="cuda")
+        ext.extract_batch_device(d_img.data_ptr(), F, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                                 d_cnt.data_ptr())
+        torch.cuda.synchronize()
+        for i in range(F):
+            n = int(d_cnt[i, 0])
+            kps = d_kps[i].cpu().numpy().view(KP_DTYPE)[:n]
+            _assert_kps_equal(kps, d_desc[i].cpu().numpy()[:n], int(d_cnt[i, 1]), *oracle.extract(imgs[i], p),
+                              f"fast_blur {fb} {w}x{h}/{nfeat} batch {i}")
+        ext.close()
