@@ -57,6 +57,13 @@ PY
         env $v MAM_ORB_HOST_PROFILE=1 timeout -k 10 120 python3 -u $R/scripts/extract_latency.py --reps 400 --configs c1,c2 > $O/hostprof.log 2>&1 || { tail -5 $O/hostprof.log; exit 1; }
         grep -E "^c|orb host" $O/hostprof.log | awk '!seen[$1 $2 $3]++'
       done ;;
+    ldlt)
+      # the dataflow LDL^T of the lone window: per-column timestamps (MAM_LDLT_TRACE) and cycles per phase
+      cd /tmp
+      MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_ltrace.so timeout -k 10 120 python3 $R/scripts/lba_bench.py --world --solves 3 > $O/lt.json 2> $O/lt.err || { tail -5 $O/lt.err; exit 1; }
+      grep ltrace $O/lt.err | tail -${LT_COLS:-24}
+      MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_lprof.so timeout -k 10 120 python3 $R/scripts/lba_bench.py --world --solves 3 > $O/lp.json 2> $O/lp.err || { tail -5 $O/lp.err; exit 1; }
+      grep "ldlt cycles" $O/lp.err | tail -2 ;;
     sweep2)
       # DistributeOctTree phase profile per workgroup width; batch stage times with / without the FAST chunks
       cd /tmp
