@@ -142,7 +142,8 @@ struct Prob {
     double* bdinv;               // [E][18] H_pl D^-1
     double* coef;                // [E][6]  H_pl D^-1 b_l
     // system
-    double* Hpp;                 // [Np][36]
+    double* Hpp;                 // [POSE_SPLIT][Np][36]: H_pp in partial sums (their fixed-order sum is the block)
+    double* bp;                  // [POSE_SPLIT][Np][6]: b_p likewise (k_schur_blk sums them into b's pose part)
     double* Hll;                 // [L][9]
     double* b;                   // [6Np + 3L]
     double* Dinv;                // [L][9]
@@ -631,6 +632,13 @@ __global__ __launch_bounds__(EW) void k_linearize(const Prob* __restrict__ probs
 #endif
 constexpr int SYS_PF = MAM_SYS_PF;   // edge indices per lane prefetched per pass (a pose: ~480 edges)
 constexpr int PT_PF = 8;             // a point's edge indices prefetched per pass (a window's points: <= 8 edges)
+// A pose's H_pp / b_p sums at an iteration start over POSE_SPLIT waves (slot chunks of 64 interleaved), each writing
+// its partial sums; the consumers add the partials in part order. One wave per pose walked ~480 edges in 8 strides
+// of dependent loads: the longest wave of k_point_sys.
+#ifndef MAM_POSE_SPLIT
+#define MAM_POSE_SPLIT 4
+#endif
+constexpr int POSE_SPLIT = MAM_POSE_SPLIT;
 __device__ double sys_body(const Prob& d) {
     const int nb_pts = (d.L + 63) / 64;
     if ((int)blockIdx.x < nb_pts) {
@@ -706,14 +714,19 @@ __device__ double sys_body(const Prob& d) {
             int a = 0, r = q;
             while (r >= 6 - a) { r -= 6 - a; a++; }
             const int c = a + r;
-            double* H = d.Hpp + 36 * (size_t)h;
+            double* H = d.Hpp + 36 * (size_t)h;   // partial 0 holds the sum, the others zeros
             H[6 * a + c] = val;
             H[6 * c + a] = val;
             if (c == a) m = fabs(val);
         } else {
             d.b[6 * (size_t)h + (q - 21)] = val;
+            d.bp[6 * (size_t)h + (q - 21)] = val;
         }
     }
+    // partials 1.. of this pose (layout [part][Np][36] / [part][Np][6]) are zeros
+    for (int k = lane; k < 36 * (POSE_SPLIT - 1); k += 64)
+        d.Hpp[36 * ((size_t)(1 + k / 36) * d.Np + h) + k % 36] = 0.0;
+    for (int k = lane; k < 6 * (POSE_SPLIT - 1); k += 64) d.bp[6 * ((size_t)(1 + k / 6) * d.Np + h) + k % 6] = 0.0;
     return m;
 }
 
@@ -811,18 +824,21 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
     *tc = q - r * (r + 1) / 2;
 }
 
-// grid (Np (Np + 1) / 2 + Np, Q) x 64: one wave per block (i1 <= i2) of S (the triangle only: the upper half's
-// workgroups would exit at once, half of the dispatches) over its landmark pairs
-// (k_blk_fill), lanes strided over the pairs + a fixed-order wave sum; then one wave per pose for b_s. Only the lower
+// grid (Np (Np + 1) / 2 + Np, Q) x SCHUR_T: one workgroup per block (i1 <= i2) of S (the triangle only: the upper
+// half's workgroups would exit at once, half of the dispatches) over its landmark pairs (k_blk_fill): the waves take
+// interleaved 64-pair chunks (a diagonal block has all ~480 of its pose's edges: one wave walked them in ~8 dependent
+// strides), lanes strided over the pairs, a fixed-order wave sum, then the waves' partial sums added in wave order;
+// then one workgroup per pose for b_s (and b's pose part: the sum of the POSE_SPLIT partials). Only the lower
 // triangle of S is written (the one the factorization reads).
-#ifndef MAM_SCHUR_WAVES
-#define MAM_SCHUR_WAVES 3   // resident waves per SIMD the register budget is sized for
-#endif
 #ifndef MAM_SCHUR_PF
 #define MAM_SCHUR_PF 2
 #endif
-constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per pass (2 / 4 / 8: the same time)
-__global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* __restrict__ probs) {
+constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per pass
+#ifndef MAM_SCHUR_T
+#define MAM_SCHUR_T 256
+#endif
+constexpr int SCHUR_T = MAM_SCHUR_T, SCHUR_NW = SCHUR_T / 64;
+__global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ probs) {
     // XCD-aware: each XCD takes a contiguous range of (problem, block row) ids, so the W / H_pl records of the
     // landmarks its rows share stay in its L2
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
@@ -831,13 +847,14 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
     const Prob& d = probs[logical / gridDim.x];
     const LM& lm = *d.lm;
     if (lm.status || lm.done) return;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int ntri = d.Np * (d.Np + 1) / 2;
+    __shared__ double red[SCHUR_NW][36];
     if (bt >= ntri) {
         const int h = bt - ntri;
         if (h >= d.Np) return;
         double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        for (int s = d.qe_off[h] + lane; s < d.qe_off[h + 1]; s += 64) {
+        for (int s = d.qe_off[h] + threadIdx.x; s < d.qe_off[h + 1]; s += SCHUR_T) {
             const double* c = d.coef + 6 * (size_t)d.qe_idx[s];
 #pragma unroll
             for (int k = 0; k < 6; k++) acc[k] += c[k];
@@ -848,7 +865,18 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
             double v = 0.0;
 #pragma unroll
             for (int k = 0; k < 6; k++) v = (k == lane) ? acc[k] : v;
-            d.bs[6 * (size_t)d.perm[h] + lane] = d.b[6 * (size_t)h + lane] - v;   // (position order)
+            red[wid][lane] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < 6) {
+            const int k = threadIdx.x;
+            double v = 0.0, bsum = 0.0;
+#pragma unroll
+            for (int w = 0; w < SCHUR_NW; w++) v += red[w][k];
+#pragma unroll
+            for (int p = 0; p < POSE_SPLIT; p++) bsum += d.bp[6 * ((size_t)p * d.Np + h) + k];
+            d.b[6 * (size_t)h + k] = bsum;
+            d.bs[6 * (size_t)d.perm[h] + k] = bsum - v;   // (position order)
         }
         return;
     }
@@ -868,32 +896,27 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
     };
     if (i1 != i2 && !d.pairmask[(size_t)i1 * d.Np + i2]) {
         // no shared landmark: a zero block (the factorization's fill-in of the previous trial is overwritten)
-        if (lane < 36) store(lane / 6, lane % 6, 0.0);
+        if (threadIdx.x < 36) store(threadIdx.x / 6, threadIdx.x % 6, 0.0);
         return;
     }
     const double lambda = trial_lambda(lm);
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
-#ifndef MAM_SCHUR_HALVES
-#define MAM_SCHUR_HALVES 1
-#endif
     const int k1 = d.blk_off[bx + 1];
-    for (int kb = d.blk_off[bx] + lane; kb < k1; kb += 64 * SCHUR_PF) {
+    for (int kb = d.blk_off[bx] + 64 * wid + lane; kb < k1; kb += SCHUR_T * SCHUR_PF) {
         // the lane's pair records of up to SCHUR_PF strides loaded together (one round trip, not one per pair)
         int2 prs[SCHUR_PF];
 #pragma unroll
-        for (int u = 0; u < SCHUR_PF; u++) prs[u] = kb + 64 * u < k1 ? d.blk_pair[kb + 64 * u] : make_int2(-1, -1);
+        for (int u = 0; u < SCHUR_PF; u++) prs[u] = kb + SCHUR_T * u < k1 ? d.blk_pair[kb + SCHUR_T * u] : make_int2(-1, -1);
 #pragma unroll
         for (int u = 0; u < SCHUR_PF; u++) {
             if (prs[u].x < 0) break;
             const int2 pr = prs[u];
             const double* W = d.bdinv + 18 * (size_t)pr.x;
             const double* B = d.hpl + 18 * (size_t)pr.y;
-#if MAM_SCHUR_HALVES
-            // rows of W and of H_pl three at a time (9 doubles each): 152 instead of 166 VGPRs, no spill (batch of 32
-            // windows 6.11 vs 6.27 ms; capped at 128 for 4 waves per SIMD it spills and is 11 % slower); the same products
-            // summed in the same order per accumulator
+            // rows of W and of H_pl three at a time (9 doubles each): no spill at 152 VGPRs; the same products summed
+            // in the same order per accumulator
 #pragma unroll
             for (int hr = 0; hr < 2; hr++) {
                 double w[9];
@@ -912,24 +935,9 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
                                 w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
                 }
             }
-#else
-            double w[18], b[18];   // 144-byte records, 16-byte aligned: nine 16-byte loads each (staging the records
-                                   // cooperatively through LDS measured slower: 18 KB per wave halves the resident waves)
-#pragma unroll
-            for (int q = 0; q < 9; q++) {
-                const double2 wv = reinterpret_cast<const double2*>(W)[q], bv = reinterpret_cast<const double2*>(B)[q];
-                w[2 * q] = wv.x; w[2 * q + 1] = wv.y;
-                b[2 * q] = bv.x; b[2 * q + 1] = bv.y;
-            }
-#pragma unroll
-            for (int r = 0; r < 6; r++)
-#pragma unroll
-                for (int c = 0; c < 6; c++)
-                    acc[6 * r + c] += w[3 * r] * b[3 * c] + w[3 * r + 1] * b[3 * c + 1] + w[3 * r + 2] * b[3 * c + 2];
-#endif
         }
     }
-    // the 36 sums reduce-scattered: lane group g holds sums [9 g, 9 g + 9)
+    // the 36 sums reduce-scattered per wave: lane group g holds sums [9 g, 9 g + 9); the waves' sums in wave order
     double tot[9];
     wave_sum_scatter4<9>(acc, tot);
     const int il = lane & 15, k = 9 * (lane >> 4) + il;
@@ -937,9 +945,21 @@ __global__ __launch_bounds__(64, MAM_SCHUR_WAVES) void k_schur_blk(const Prob* _
         double v = 0.0;
 #pragma unroll
         for (int i = 0; i < 9; i++) v = (il == i) ? tot[i] : v;
-        const int r = k / 6, c = k % 6;
+        red[wid][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 36) {
+        const int q = threadIdx.x, r = q / 6, c = q % 6;
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < SCHUR_NW; w++) v += red[w][q];
         double out = -v;
-        if (i1 == i2) out = (d.Hpp[36 * (size_t)i1 + k] + (r == c ? lambda : 0.0)) - v;
+        if (i1 == i2) {
+            double hs = 0.0;
+#pragma unroll
+            for (int p = 0; p < POSE_SPLIT; p++) hs += d.Hpp[36 * ((size_t)p * d.Np + i1) + q];
+            out = (hs + (r == c ? lambda : 0.0)) - v;
+        }
         store(r, c, out);   // the lower triangle, the one the factorization reads
     }
 }
@@ -2520,16 +2540,18 @@ constexpr int PW = 8;   // points per wave (a window's points have <= 8 observat
 // S's pose part at an iteration start: H_pp, b_p of Hessian pose block h — k_sys's sums (lanes strided over the pose's
 // edge list in edge order, the same products, the same fixed-order wave reduction) on Jacobian terms recomputed from
 // the state by the same linearisation (bit-identical to the records the point waves of the same launch write)
-__device__ __forceinline__ void pose_sys_wave(const Prob& d, int h, const double* pose, const double* pts) {
+__device__ __forceinline__ void pose_sys_wave(const Prob& d, int h, int part, const double* pose, const double* pts) {
     const int lane = threadIdx.x;
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
+    // this partial's slots: chunks part, part + POSE_SPLIT, ... of 64 of the pose's edge list
     const int qs0 = d.qe_off[h], qs1 = d.qe_off[h + 1];
-    for (int base = qs0 + lane; base < qs1; base += 64 * SYS_PF) {
+    for (int base = qs0 + 64 * part + lane; base < qs1; base += 64 * POSE_SPLIT * SYS_PF) {
         int qi[SYS_PF];
 #pragma unroll
-        for (int u = 0; u < SYS_PF; u++) qi[u] = base + 64 * u < qs1 ? d.qe_idx[base + 64 * u] : -1;
+        for (int u = 0; u < SYS_PF; u++)
+            qi[u] = base + 64 * POSE_SPLIT * u < qs1 ? d.qe_idx[base + 64 * POSE_SPLIT * u] : -1;
 #pragma unroll
         for (int u = 0; u < SYS_PF; u++) {
             if (qi[u] < 0) break;
@@ -2568,11 +2590,11 @@ __device__ __forceinline__ void pose_sys_wave(const Prob& d, int h, const double
             int a = 0, r = q;
             while (r >= 6 - a) { r -= 6 - a; a++; }
             const int c = a + r;
-            double* H = d.Hpp + 36 * (size_t)h;
+            double* H = d.Hpp + 36 * ((size_t)part * d.Np + h);
             H[6 * a + c] = val;
             H[6 * c + a] = val;
         } else {
-            d.b[6 * (size_t)h + (q - 21)] = val;
+            d.bp[6 * ((size_t)part * d.Np + h) + (q - 21)] = val;
         }
     }
 }
@@ -2592,12 +2614,12 @@ __device__ __forceinline__ void dinv_of(const double H[9], double lambda, double
     o[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
 }
 
-// grid (ceil(L / PW) + Np, Q) x 64, the start of every trial:
+// grid (ceil(L / PW) + Np POSE_SPLIT, Q) x 64, the start of every trial:
 //  point waves — at an iteration start (need_lin, unless the setup pass already built iteration 0's system) the slots'
 //    edges linearised (H_pl records, errors) and the points' H_ll, b_l summed in edge order from the slots' terms
 //    (k_sys's sums); every trial D^-1 = (H_ll + lambda I)^-1 per point and, per slot, W = H_pl D^-1 and the
 //    coefficients H_pl D^-1 b_l (k_schur_prep's products);
-//  pose waves — at an iteration start H_pp, b_p (pose_sys_wave).
+//  pose waves — at an iteration start H_pp, b_p in POSE_SPLIT partial sums per pose (pose_sys_wave).
 __global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     const LMHead hd = lm_head(d.lm);
@@ -2607,8 +2629,8 @@ __global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs
     const double* pose = d.pose[hd.cur];
     const double* pts = d.pt[hd.cur];
     if ((int)blockIdx.x >= nbp) {
-        const int h = blockIdx.x - nbp;
-        if (lin && h < d.Np) pose_sys_wave(d, h, pose, pts);
+        const int h = (blockIdx.x - nbp) / POSE_SPLIT, part = (blockIdx.x - nbp) % POSE_SPLIT;
+        if (lin && h < d.Np) pose_sys_wave(d, h, part, pose, pts);
         return;
     }
     const int lane = threadIdx.x;
@@ -3055,7 +3077,8 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.hpl = cv.take<double>(18 * (size_t)d.E);
     d.bdinv = cv.take<double>(18 * (size_t)d.E);
     d.coef = cv.take<double>(6 * (size_t)d.E);
-    d.Hpp = cv.take<double>(36 * (size_t)d.Np);
+    d.Hpp = cv.take<double>(36 * (size_t)mam::lba::POSE_SPLIT * d.Np);
+    d.bp = cv.take<double>(6 * (size_t)mam::lba::POSE_SPLIT * d.Np);
     d.Hll = cv.take<double>(9 * (size_t)d.L);
     d.b = cv.take<double>(nx);
     d.Dinv = cv.take<double>(9 * (size_t)d.L);
@@ -3250,7 +3273,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
     }
     const int nbp = std::max((maxL + PW - 1) / PW, 1);
-    const dim3 gPts(nbp + maxNp, Q), gTri(nbp, Q);
+    const dim3 gPts(nbp + maxNp * POSE_SPLIT, Q), gTri(nbp, Q);
     const dim3 gBlk(maxNp * (maxNp + 1) / 2 + maxNp > 0 ? maxNp * (maxNp + 1) / 2 + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
     // The batch runs as G interleaved groups on G streams: one group's latency-bound factorization (one workgroup
@@ -3290,7 +3313,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 1);
-            hipLaunchKernelGGL(k_schur_blk, gBlkg, dim3(64), 0, st, Pg);
+            hipLaunchKernelGGL(k_schur_blk, gBlkg, dim3(SCHUR_T), 0, st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 2);
