@@ -2650,11 +2650,14 @@ __global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs
     for (int k = 0; k < 3; k++) bl[k] = 0.0;
 #pragma unroll
     for (int k = 0; k < 18; k++) hr[k] = 0.0;
+    // one chunk: the lane's slot edge loaded once, up front
+    const int e1 = (one && s0 + lane < s1) ? d.pe_idx[s0 + lane] : 0;
+
     if (lin) {
         for (int c0 = s0; c0 < s1; c0 += 64) {
             const int s = c0 + lane;
             if (s < s1) {
-                const int e = d.pe_idx[s];
+                const int e = one ? e1 : d.pe_idx[s];
                 double jr[21];
                 linearize_edge(d, pose, pts, e, true, jr, hr);
                 double* HP = d.hpl + 18 * (size_t)e;
@@ -2713,7 +2716,7 @@ __global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs
     for (int c0 = s0; c0 < s1; c0 += 64) {
         const int s = c0 + lane;
         if (s >= s1) continue;
-        const int e = d.pe_idx[s];
+        const int e = one ? e1 : d.pe_idx[s];
         const int4 em = d.emeta[e];
         double o[18], cf[6];
 #pragma unroll

@@ -64,6 +64,16 @@ PY
       grep ltrace $O/lt.err | tail -${LT_COLS:-24}
       MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_lprof.so timeout -k 10 120 python3 $R/scripts/lba_bench.py --world --solves 3 > $O/lp.json 2> $O/lp.err || { tail -5 $O/lp.err; exit 1; }
       grep "ldlt cycles" $O/lp.err | tail -2 ;;
+    lbavar)
+      # lone-window solve per library variant (LBA_VARIANTS: variants/libmam_gpu_<name>.so; "main" = the in-tree build)
+      cd /tmp
+      for v in ${LBA_VARIANTS:-main}; do
+        lib=$R/variants/libmam_gpu_$v.so; [ $v = main ] && lib=$R/mam3slam_amd/libmam_gpu.so
+        MAM3SLAM_GPU_LIB=$lib timeout -k 10 120 python3 $R/scripts/lba_bench.py --world --solves 12 > $O/lbavar_$v.json 2> $O/lbavar_$v.err || { tail -5 $O/lbavar_$v.err; exit 1; }
+        python3 -c "
+import json; d=json.loads(open('$O/lbavar_$v.json').read())
+print('$v', 'median %.4f min %.4f' % (d['ms_per_solve_median'], d['ms_per_solve_min']), {k: round(v, 4) for k, v in d['stage_ms_per_solve'].items()})"
+      done ;;
     sweep2)
       # DistributeOctTree phase profile per workgroup width; batch stage times with / without the FAST chunks
       cd /tmp
