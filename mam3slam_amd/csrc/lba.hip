@@ -25,6 +25,8 @@
 // same launches.
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -498,14 +500,49 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
         if (h >= d.L) return;
         int32_t* s = d.pe_idx + d.pe_off[h];
         const int n = d.pe_off[h + 1] - d.pe_off[h];
+        // per slot / per edge metadata the per-trial kernels read with one load instead of a chain of dependent ones
+        constexpr int NR = 8;   // a window's points: <= 8 observations, their pose blocks kept in registers
+        if (n <= NR) {
+            // the list sorted in registers (an unrolled exchange network; edge ids are distinct), and each dependent
+            // lookup issued for the whole list at once: three memory round trips instead of a few per element
+            int v[NR], ep[NR], hv[NR];
+#pragma unroll
+            for (int a = 0; a < NR; a++) v[a] = a < n ? s[a] : INT_MAX;
+#pragma unroll
+            for (int i = 0; i < NR - 1; i++)
+#pragma unroll
+                for (int j = 0; j < NR - 1 - i; j++) {
+                    const int lo = min(v[j], v[j + 1]), hi = max(v[j], v[j + 1]);
+                    v[j] = lo;
+                    v[j + 1] = hi;
+                }
+#pragma unroll
+            for (int a = 0; a < NR; a++) ep[a] = a < n ? d.edge_pose[v[a]] : 0;
+#pragma unroll
+            for (int a = 0; a < NR; a++) hv[a] = a < n ? d.pose_h[ep[a]] : -1;
+#pragma unroll
+            for (int a = 0; a < NR; a++)
+                if (a < n) {
+                    s[a] = v[a];
+                    d.slot_hp[d.pe_off[h] + a] = hv[a];
+                    d.emeta[v[a]] = make_int4(h, hv[a], a == 0 ? 1 : 0, 0);
+                }
+            // the S blocks this landmark contributes to (g2o's BlockSolver keeps only these, block_solver.hpp:181-224)
+#pragma unroll
+            for (int a = 0; a < NR; a++)
+#pragma unroll
+                for (int b = a + 1; b < NR; b++) {
+                    const int ha = hv[a], hb = hv[b];
+                    if (ha >= 0 && hb >= 0 && hb != ha) d.pairmask[(size_t)min(ha, hb) * d.Np + max(ha, hb)] = 1;
+                }
+            return;
+        }
         for (int k = 1; k < n; k++) {
             const int v = s[k];
             int m = k - 1;
             while (m >= 0 && s[m] > v) { s[m + 1] = s[m]; m--; }
             s[m + 1] = v;
         }
-        // per slot / per edge metadata the per-trial kernels read with one load instead of a chain of dependent ones
-        constexpr int NR = 8;   // a window's points: <= 8 observations, their pose blocks kept in registers
         int hpv[NR];
 #pragma unroll
         for (int a = 0; a < NR; a++) hpv[a] = -1;
@@ -835,7 +872,7 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
 #endif
 constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per pass
 #ifndef MAM_SCHUR_T
-#define MAM_SCHUR_T 256
+#define MAM_SCHUR_T 128   // lone window: 64 / 128 / 256 threads 23.0 / 21.9 / 24.5 us per launch
 #endif
 constexpr int SCHUR_T = MAM_SCHUR_T, SCHUR_NW = SCHUR_T / 64;
 __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ probs) {
@@ -886,25 +923,40 @@ __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ 
     tri_index(bt, &tr, &tc);
     const int i1 = d.Np - 1 - tr, i2 = i1 + tc;
     const int bx = i1 * d.Np + i2;   // the block's pair-list slot
-    // S(i1 row r, i2 col c) at the poses' positions, in the lower triangle
+    // everything that depends only on the block index loaded at once (positions, pair mask, pair range, the diagonal
+    // block's H_pp partials), then this thread's S entry's tile slot: two memory round trips before the pair records
+    // instead of a chain of five
     const int p1 = d.perm[i1], p2 = d.perm[i2];
-    auto store = [&](int r, int c, double v) {
-        if (p2 >= p1)
-            s_store(d, lm.tiles_lds != 0, 6 * p2 + c, 6 * p1 + r, v);
-        else
-            s_store(d, lm.tiles_lds != 0, 6 * p1 + r, 6 * p2 + c, v);
+    const bool nz = i1 == i2 || d.pairmask[(size_t)i1 * d.Np + i2];
+    const int k0 = d.blk_off[bx], k1 = d.blk_off[bx + 1];
+    const bool pool = lm.tiles_lds != 0;
+    const int q36 = threadIdx.x < 36 ? threadIdx.x : 0;
+    double hs = 0.0;
+    if (i1 == i2 && threadIdx.x < 36) {
+#pragma unroll
+        for (int p = 0; p < POSE_SPLIT; p++) hs += d.Hpp[36 * ((size_t)p * d.Np + i1) + q36];
+    }
+    // S(i1 row r, i2 col c) at the poses' positions, in the lower triangle
+    const int r36 = q36 / 6, c36 = q36 % 6;
+    const int srow = p2 >= p1 ? 6 * p2 + c36 : 6 * p1 + r36, scol = p2 >= p1 ? 6 * p1 + r36 : 6 * p2 + c36;
+    const int sslot = (pool && threadIdx.x < 36) ? d.tslot[(size_t)(srow >> 4) * d.nt + (scol >> 4)] : -1;
+    auto store = [&](double v) {
+        if (pool) {
+            if (sslot >= 0) d.pool[(size_t)sslot * 256 + tsw(srow & 15, scol & 15)] = v;
+        } else {
+            d.S[(size_t)srow * d.npad + scol] = v;
+        }
     };
-    if (i1 != i2 && !d.pairmask[(size_t)i1 * d.Np + i2]) {
+    if (!nz) {
         // no shared landmark: a zero block (the factorization's fill-in of the previous trial is overwritten)
-        if (threadIdx.x < 36) store(threadIdx.x / 6, threadIdx.x % 6, 0.0);
+        if (threadIdx.x < 36) store(0.0);
         return;
     }
     const double lambda = trial_lambda(lm);
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
-    const int k1 = d.blk_off[bx + 1];
-    for (int kb = d.blk_off[bx] + 64 * wid + lane; kb < k1; kb += SCHUR_T * SCHUR_PF) {
+    for (int kb = k0 + 64 * wid + lane; kb < k1; kb += SCHUR_T * SCHUR_PF) {
         // the lane's pair records of up to SCHUR_PF strides loaded together (one round trip, not one per pair)
         int2 prs[SCHUR_PF];
 #pragma unroll
@@ -949,18 +1001,12 @@ __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ 
     }
     __syncthreads();
     if (threadIdx.x < 36) {
-        const int q = threadIdx.x, r = q / 6, c = q % 6;
         double v = 0.0;
 #pragma unroll
-        for (int w = 0; w < SCHUR_NW; w++) v += red[w][q];
+        for (int w = 0; w < SCHUR_NW; w++) v += red[w][q36];
         double out = -v;
-        if (i1 == i2) {
-            double hs = 0.0;
-#pragma unroll
-            for (int p = 0; p < POSE_SPLIT; p++) hs += d.Hpp[36 * ((size_t)p * d.Np + i1) + q];
-            out = (hs + (r == c ? lambda : 0.0)) - v;
-        }
-        store(r, c, out);   // the lower triangle, the one the factorization reads
+        if (i1 == i2) out = (hs + (r36 == c36 ? lambda : 0.0)) - v;
+        store(out);   // the lower triangle, the one the factorization reads
     }
 }
 
@@ -995,6 +1041,31 @@ __host__ __device__ inline int ldlt_pad(int n) { return (n + NB - 1) / NB * NB; 
 __device__ __forceinline__ bool blk_nonzero(const Prob& d, int i1, int i2) {
     return i2 >= i1 && (i1 == i2 || d.pairmask[(size_t)i1 * d.Np + i2]);
 }
+// The pose-i1 edges of the landmarks pose i2's edges qe_idx[s0 + 64 u] observe (eidx_at for BLK_PF strides of the
+// lane at once: each dependent lookup issued for the whole batch, five memory round trips per batch instead of per
+// stride); ea[u] = -1 where there is none or past the list
+constexpr int BLK_PF = 8;
+__device__ __forceinline__ void blk_batch(const Prob& d, const int32_t* ei1, int i1, int s0, int end, int (&ec)[BLK_PF],
+                                          int (&ea)[BLK_PF]) {
+    int ip[BLK_PF], ep2[BLK_PF], eo[BLK_PF];
+#pragma unroll
+    for (int u = 0; u < BLK_PF; u++) ec[u] = s0 + 64 * u < end ? d.qe_idx[s0 + 64 * u] : -1;
+#pragma unroll
+    for (int u = 0; u < BLK_PF; u++) ip[u] = ec[u] >= 0 ? d.edge_point[ec[u]] : 0;
+#pragma unroll
+    for (int u = 0; u < BLK_PF; u++) {
+        const int e = ec[u] >= 0 ? ei1[ip[u]] : -1;
+        ea[u] = (unsigned)e < (unsigned)d.E ? e : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < BLK_PF; u++) {
+        ep2[u] = ea[u] >= 0 ? d.edge_point[ea[u]] : -1;
+        eo[u] = ea[u] >= 0 ? d.edge_pose[ea[u]] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < BLK_PF; u++)
+        if (ea[u] >= 0 && !(ep2[u] == ip[u] && d.pose_h[eo[u]] == i1)) ea[u] = -1;
+}
 // grid (Np * Np, Q) x 64: pairs per block
 __global__ __launch_bounds__(64) void k_blk_count(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
@@ -1005,7 +1076,13 @@ __global__ __launch_bounds__(64) void k_blk_count(const Prob* __restrict__ probs
     int n = 0;
     if (blk_nonzero(d, i1, i2)) {
         const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
-        for (int s = d.qe_off[i2] + lane; s < d.qe_off[i2 + 1]; s += 64) n += eidx_at(d, ei1, i1, d.edge_point[d.qe_idx[s]]) >= 0;
+        const int end = d.qe_off[i2 + 1];
+        for (int s0 = d.qe_off[i2] + lane; s0 < end; s0 += 64 * BLK_PF) {
+            int ec[BLK_PF], ea[BLK_PF];
+            blk_batch(d, ei1, i1, s0, end, ec, ea);
+#pragma unroll
+            for (int u = 0; u < BLK_PF; u++) n += ea[u] >= 0;
+        }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
     }
@@ -1047,17 +1124,17 @@ __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs)
     const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
     int base = d.blk_off[bx];
     const int end = d.qe_off[i2 + 1];
-    for (int s0 = d.qe_off[i2]; s0 < end; s0 += 64) {
-        const int s = s0 + lane;
-        int ec = -1, ea = -1;
-        if (s < end) {
-            ec = d.qe_idx[s];
-            ea = eidx_at(d, ei1, i1, d.edge_point[ec]);
+    // (every lane runs the batches of the longest lane: the ballots need the whole wave)
+    for (int c0 = d.qe_off[i2]; c0 < end; c0 += 64 * BLK_PF) {
+        int ec[BLK_PF], ea[BLK_PF];
+        blk_batch(d, ei1, i1, c0 + lane, end, ec, ea);
+#pragma unroll
+        for (int u = 0; u < BLK_PF; u++) {   // the 64-slot chunks in list order
+            const bool hit = ea[u] >= 0;
+            const uint64_t m = __ballot(hit);
+            if (hit) d.blk_pair[base + __popcll(m & ((1ull << lane) - 1ull))] = make_int2(ea[u], ec[u]);
+            base += __popcll(m);
         }
-        const bool hit = ea >= 0;
-        const uint64_t m = __ballot(hit);
-        if (hit) d.blk_pair[base + __popcll(m & ((1ull << lane) - 1ull))] = make_int2(ea, ec);
-        base += __popcll(m);
     }
 }
 
@@ -1184,6 +1261,7 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
     // the pool and y fit the factorization's dynamic LDS (lds_bytes)
     __shared__ int wsum[SB / 64];
     __shared__ int carry;
+    __shared__ int16_t sl_last[64];   // the last tile row's slots (the padding loop below reads them from LDS)
     if (t == 0) carry = 0;
     __syncthreads();
     for (int c0 = 0; c0 < nt * nt; c0 += SB) {
@@ -1209,6 +1287,7 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
                 d.tlist[2 * sl] = (int16_t)(q / nt);
                 d.tlist[2 * sl + 1] = (int16_t)(q % nt);
             }
+            if (q / nt == nt - 1 && q % nt < 64) sl_last[q % nt] = f ? (int16_t)sl : (int16_t)-1;
         }
         __syncthreads();
         if (t == 0) carry += tot;
@@ -1261,7 +1340,7 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
                 const int c = q >> 8, e = q & 255;
                 const int j = e >> 4, i = (e & 15) ^ j;   // tsw(i, j) = j * 16 + (i ^ j)
                 const int gi = NB * (nt - 1) + i, gj = NB * c + j;
-                const int sl = d.tslot[(size_t)(nt - 1) * nt + c];
+                const int sl = sl_last[c];   // (nt <= LDLT_TILES_NT_MAX < 64)
                 if (gi >= n && sl >= 0) d.pool[(size_t)sl * 256 + e] = gi == gj ? 1.0 : 0.0;
             }
     }
