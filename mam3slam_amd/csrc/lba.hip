@@ -1870,7 +1870,8 @@ __device__ __forceinline__ void tile_update(double* TL, int sc, int sa, int sb, 
 // panel's panel-row forward update, its operands loaded with the tiles'.
 template <int N>
 __device__ __forceinline__ void tile_update_multi(double* TL, const int* sc, const int* sa, int sb, const double* dkp,
-                                                  int lane, const double* yj = nullptr, double* yd = nullptr) {
+                                                  int lane, const double* yj = nullptr, double* yd = nullptr,
+                                                  int dstride = 1) {
     const int col = lane & 15, rq = lane >> 4;
     const double* Lb = TL + (size_t)sb * 256;
     double bv[4], av[N][4], lv[NB], yv[NB];
@@ -1886,7 +1887,7 @@ __device__ __forceinline__ void tile_update_multi(double* TL, const int* sc, con
     // load straight into registers (no per-tile wait for a negation); an absent tile (sa < 0, uniform) loads a valid
     // tile, so every load issues unconditionally and one wait covers them all
 #pragma unroll
-    for (int q = 0; q < 4; q++) bv[q] = -(Lb[tsw(col, 4 * q + rq)] * dkp[4 * q + rq]);
+    for (int q = 0; q < 4; q++) bv[q] = -(Lb[tsw(col, 4 * q + rq)] * dkp[dstride * (4 * q + rq)]);
 #pragma unroll
     for (int u = 0; u < N; u++) {
         const double* C = TL + (size_t)(sa[u] >= 0 ? sc[u] : sb) * 256;
@@ -2085,6 +2086,9 @@ __device__ __forceinline__ void lds_flag_set(int* f) {
 // in parallel (4 f64 MFMAs each, 64 cycles apiece) instead of one wave's 16 in turn, and the next column's tile tasks
 // are never on the wave factoring this column's panel. Every wave walks the columns in ascending order with at most
 // one task per column (dependencies only on earlier columns, or on the same column's tile tasks: no wait cycle).
+#ifndef MAM_LDLT_LAST
+#define MAM_LDLT_LAST 0   // 1: the panel task applies its column's last update (flow_last_update)
+#endif
 constexpr int FLOW_TPC = 10;   // up to 9 tile tasks + the panel task per column (columns of up to 8 panel tiles)
 
 // C(sc) -= L(sa) D_j L(sb)^T for one tile (a tile task's pulled update), with WITH_Y also y_kc -= L(kc, j) y_j (lane
@@ -2140,7 +2144,9 @@ __device__ __forceinline__ void flow_tile_task(double* TL, const int16_t* slot, 
     const int r = t == 0 ? kc : __builtin_amdgcn_readfirstlane(sh.clist[kc * 40 + t - 1]);
     const int sc = __builtin_amdgcn_readfirstlane(slot[r * nt + kc]);
     double yd = t == 0 ? Y[kb + il] : 0.0;
-    for (int q = 0; q < nrl; q++) {
+    // (MAM_LDLT_LAST: every update but the last column's, rlist's last entry — the panel task applies that one itself,
+    // to all of the column's tiles at once, straight before its pivot steps)
+    for (int q = 0; q + MAM_LDLT_LAST < nrl; q++) {
         const int j = __builtin_amdgcn_readfirstlane(sh.rlist[kc * 40 + q]);
         const int sb = __builtin_amdgcn_readfirstlane(slot[kc * nt + j]);
         const int sa = t == 0 ? sb : __builtin_amdgcn_readfirstlane(slot[r * nt + j]);
@@ -2161,6 +2167,45 @@ __device__ __forceinline__ void flow_tile_task(double* TL, const int16_t* slot, 
     if (lane == 0) __hip_atomic_fetch_add(&sh.tcnt[kc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The panel task's update of column kc's tiles (the diagonal tile and its ncl panel tiles) by column jm: T(r, kc) -=
+// L(r, jm) D_jm L(kc, jm)^T where L(r, jm) is non-zero, and y_kc -= L(kc, jm) y_jm (lane il's row). Not inlined: its
+// operands would otherwise stay live across the tall panel's registers and spill.
+__device__ __attribute__((noinline)) void flow_last_update(double* TL, const int16_t* slot, int nt, int kc, int jm,
+                                                           int ncl, double* Y, LdltShared& sh, int lane) {
+    const int il = lane & 15, kb = NB * kc;
+    const int sb = __builtin_amdgcn_readfirstlane(slot[kc * nt + jm]);
+    const int sd = __builtin_amdgcn_readfirstlane(slot[kc * nt + kc]);
+    // D_jm: the diagonal of column jm's factored diagonal tile (D(k) at tsw(k, k) = NB k)
+    const double* Dj = TL + (size_t)__builtin_amdgcn_readfirstlane(slot[jm * nt + jm]) * 256;
+    for (int a0 = -1; a0 < ncl; a0 += 4) {   // groups of up to 4 tiles (the diagonal tile first)
+        int scs[4], sas[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int a = a0 + u;
+            if (a < 0) {
+                scs[u] = sd;
+                sas[u] = sb;
+            } else if (a < ncl) {
+                const int r = __builtin_amdgcn_readfirstlane(sh.clist[kc * 40 + a]);
+                scs[u] = __builtin_amdgcn_readfirstlane(slot[r * nt + kc]);
+                sas[u] = __builtin_amdgcn_readfirstlane(slot[r * nt + jm]);
+            } else {
+                scs[u] = sd;
+                sas[u] = -1;
+            }
+        }
+        tile_update_multi<4>(TL, scs, sas, sb, Dj, lane, nullptr, nullptr, NB);
+    }
+    // y_kc -= L(kc, jm) y_jm (two chains of eight, as the tile tasks' y updates)
+    const double* Lb = TL + (size_t)sb * 256;
+    double v0 = Y[kb + il], v1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB / 2; k++) v0 = fma(-Lb[tsw(il, k)], Y[NB * jm + k], v0);
+#pragma unroll
+    for (int k = NB / 2; k < NB; k++) v1 = fma(-Lb[tsw(il, k)], Y[NB * jm + k], v1);
+    if (lane < NB) Y[kb + lane] = v0 + v1;
+}
+
 __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot, int nt, int kc, double* Y,
                                                 LdltShared& sh, int lane) {
     const int g = lane >> 4, il = lane & 15, kb = NB * kc;
@@ -2174,6 +2219,19 @@ __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot,
     }
     while (__hip_atomic_load(&sh.tcnt[kc], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= ncl)
         __builtin_amdgcn_s_sleep(1);
+    // the column's last update (from column jm, rlist's last: the latest to finish) on every tile of the column in
+    // one wave (flow_last_update) instead of a tile task per tile handing over through the task count: on the critical
+    // path a column was a flag wait, a tile task, a count wait and this task's loads; now a flag wait and this update
+    const int nrl = __builtin_amdgcn_readfirstlane(sh.rcount[kc]);
+    if (MAM_LDLT_LAST && nrl > 0) {
+        const int jm = __builtin_amdgcn_readfirstlane(sh.rlist[kc * 40 + nrl - 1]);
+        lds_flag_wait(&sh.cflag[jm]);
+        LTRACE(6, jm);
+        flow_last_update(TL, slot, nt, kc, jm, ncl, Y, sh, lane);
+        // the updated tiles and y_kc (written by other lanes of this wave) before the row loads below
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
 #ifdef MAM_LDLT_PROFILE
     long long tp0 = clock64();
 #endif
@@ -2853,6 +2911,19 @@ __global__ __launch_bounds__(64) void k_point_trial(const Prob* __restrict__ pro
     const double* pose_out = d.pose[1 - hd.cur];
     const int h0 = blockIdx.x * PW, h1 = min(d.L, h0 + PW);
     __shared__ double xn[PW * 3];
+    // the trial-error pass's slot edge, its pose and that pose's trial value loaded before the back-substitution (one
+    // 64-slot chunk, a window's points): their round trips overlap it instead of following the barrier
+    const int s0 = d.pe_off[h0], s1 = d.pe_off[h1];
+    const bool one = s1 - s0 <= 64;
+    int e_pf = 0, ip_pf = 0, pt_pf = h0;
+    double T_pf[7];
+    if (one && s0 + lane < s1) {
+        e_pf = d.pe_idx[s0 + lane];
+        ip_pf = d.edge_pose[e_pf];
+        pt_pf = d.edge_point[e_pf];
+#pragma unroll
+        for (int k = 0; k < 7; k++) T_pf[k] = pose_out[7 * (size_t)ip_pf + k];
+    }
     double sc = 0.0;
     const int i = h0 + lane;
     if (lane < PW && i < h1) {
@@ -2897,15 +2968,21 @@ __global__ __launch_bounds__(64) void k_point_trial(const Prob* __restrict__ pro
     }
     __syncthreads();
     double r = 0.0;
-    const int s0 = d.pe_off[h0], s1 = d.pe_off[h1];
-    for (int c0 = s0; c0 < s1; c0 += 64) {
-        const int s = c0 + lane;
-        if (s < s1) {
-            const int e = d.pe_idx[s];
-            const int ipose = d.edge_pose[e];
+    if (one) {
+        if (s0 + lane < s1) {
             double jr[21], hr[18];
-            r += linearize_edge_at(d, pose_out + 7 * (size_t)ipose, xn + 3 * (d.edge_point[e] - h0), ipose, e, false, true,
-                                   jr, hr);
+            r = linearize_edge_at(d, T_pf, xn + 3 * (pt_pf - h0), ip_pf, e_pf, false, true, jr, hr);
+        }
+    } else {
+        for (int c0 = s0; c0 < s1; c0 += 64) {
+            const int s = c0 + lane;
+            if (s < s1) {
+                const int e = d.pe_idx[s];
+                const int ipose = d.edge_pose[e];
+                double jr[21], hr[18];
+                r += linearize_edge_at(d, pose_out + 7 * (size_t)ipose, xn + 3 * (d.edge_point[e] - h0), ipose, e, false,
+                                       true, jr, hr);
+            }
         }
     }
     r = wave_sum_d(r);
