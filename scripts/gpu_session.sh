@@ -60,10 +60,11 @@ PY
     ldlt)
       # the dataflow LDL^T of the lone window: per-column timestamps (MAM_LDLT_TRACE) and cycles per phase
       cd /tmp
-      MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_ltrace.so timeout -k 10 120 python3 $R/scripts/lba_bench.py --world --solves 3 > $O/lt.json 2> $O/lt.err || { tail -5 $O/lt.err; exit 1; }
-      grep ltrace $O/lt.err | tail -${LT_COLS:-24}
-      MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_lprof.so timeout -k 10 120 python3 $R/scripts/lba_bench.py --world --solves 3 > $O/lp.json 2> $O/lp.err || { tail -5 $O/lp.err; exit 1; }
-      grep "ldlt cycles" $O/lp.err | tail -2 ;;
+      for v in ${LT_VARIANTS:-ltrace}; do
+        echo "-- $v"
+        MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_$v.so timeout -k 10 120 python3 $R/scripts/lba_bench.py --world --solves 3 > $O/lt_$v.json 2> $O/lt_$v.err || { tail -5 $O/lt_$v.err; exit 1; }
+        grep -E "ltrace|ldlt cycles" $O/lt_$v.err | tail -${LT_COLS:-20}
+      done ;;
     lbavar)
       # lone-window solve per library variant (LBA_VARIANTS: variants/libmam_gpu_<name>.so; "main" = the in-tree build)
       cd /tmp
