@@ -1321,6 +1321,7 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
         // with the split pose order the two ends' columns alternate. One wave, lane k: column k's parents (the
         // columns c < k of row k's non-zero tiles) as a bit row; level l = the columns whose parents all have levels
         // < l (Kahn's layering: the longest dependency path), positions by a prefix count within the level.
+        __shared__ int8_t ord_s[64], jm_s[64];
         if (t < 64) {
             uint64_t P = 0;
             if (lane < nt)
@@ -1330,9 +1331,39 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
             int base = 0;
             for (int l = 0; done != all && l < 64; l++) {
                 const uint64_t ready = __ballot(lane < nt && !((done >> lane) & 1) && (P & ~done) == 0);
-                if ((ready >> lane) & 1) d.order_g[base + __popcll(ready & ((1ull << lane) - 1))] = (int8_t)lane;
+                if ((ready >> lane) & 1) {
+                    const int pos = base + __popcll(ready & ((1ull << lane) - 1));
+                    d.order_g[pos] = (int8_t)lane;
+                    ord_s[pos] = (int8_t)lane;
+                }
                 base += __popcll(ready);
                 done |= ready;
+            }
+            // the column's last parent (its latest update: rlist's last entry), -1 for a chain's first column
+            jm_s[lane] = (int8_t)(P ? 63 - __clzll((long long)P) : -1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            // the dataflow's wave per column (order_g[40 + kc]): a chain's columns on one wave (its diagonal tile
+            // task and panel task follow the previous column's panel task there: no cross-wave hand-off on the chain),
+            // chains on disjoint halves of the waves (helper tile tasks on the next three waves of the half), a
+            // column inheriting a parent's wave another column took already moves to the other half
+            if (lane == 0) {
+                uint64_t taken = 0;
+                int nchain = 0;
+                int8_t mwv[64];
+                for (int sp = 0; sp < nt; sp++) {
+                    const int kc = ord_s[sp], jm = jm_s[kc];
+                    int mw;
+                    if (jm < 0) {
+                        mw = (4 * nchain++) % (LDLT_THREADS / 64);
+                    } else {
+                        mw = mwv[jm];
+                        if ((taken >> jm) & 1) mw = (mw + 4) % (LDLT_THREADS / 64);
+                        taken |= 1ull << jm;
+                    }
+                    mwv[kc] = (int8_t)mw;
+                    d.order_g[40 + kc] = (int8_t)mw;
+                }
             }
         }
         if (nt > 0)
@@ -1628,6 +1659,7 @@ struct LdltShared {
     int bflag[40];
     int tcnt[40];                // dataflow tasks: the column's tile tasks done
     alignas(4) int8_t order[40]; // dataflow: the block columns in dependency-level order (k_struct_tiles)
+    alignas(4) int8_t mainw[40]; // dataflow: each column's wave (its diagonal tile task and panel task; k_struct_tiles)
 #ifdef MAM_LDLT_TRACE
     int ltr[40][8];   // (low 32 bits of the cycle counter)
 #endif
@@ -2089,7 +2121,11 @@ __device__ __forceinline__ void lds_flag_set(int* f) {
 #ifndef MAM_LDLT_LAST
 #define MAM_LDLT_LAST 0   // 1: the panel task applies its column's last update (flow_last_update)
 #endif
-constexpr int FLOW_TPC = 10;   // up to 9 tile tasks + the panel task per column (columns of up to 8 panel tiles)
+#ifndef MAM_LDLT_CHAINWAVE
+#define MAM_LDLT_CHAINWAVE 0   // 1: chain-aligned task-to-wave map (k_struct_tiles' order_g[40 + kc]); 0: round robin
+#endif
+static_assert(!MAM_LDLT_CHAINWAVE || LDLT_THREADS == 512, "the chain-aligned wave map assumes two halves of 4 waves");
+[[maybe_unused]] constexpr int FLOW_TPC = 10;   // up to 9 tile tasks + the panel task per column (columns of up to 8 panel tiles)
 
 // C(sc) -= L(sa) D_j L(sb)^T for one tile (a tile task's pulled update), with WITH_Y also y_kc -= L(kc, j) y_j (lane
 // il's row; L(kc, j) = L(sb)): every LDS operand loaded before any use (one wait instead of one per MFMA step), the four
@@ -2397,6 +2433,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         }
         if (t < 2 * nt) cv = ((gu8*)d.ccnt_g)[t];
         const int8_t ov = t < nt ? ((__attribute__((address_space(1))) const int8_t*)d.order_g)[t] : 0;
+        const int8_t mv = t < nt ? ((__attribute__((address_space(1))) const int8_t*)d.order_g)[40 + t] : 0;
 #pragma unroll
         for (int u = 0; u < YPT; u++) {
             const int i = t + u * LDLT_THREADS;
@@ -2420,6 +2457,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         if (t < nt) {
             sh.ccount[t] = cv;
             sh.order[t] = ov;
+            sh.mainw[t] = mv;
             sh.cflag[t] = 0;
             sh.bflag[t] = 0;
             sh.tcnt[t] = 0;
@@ -2441,6 +2479,15 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         for (int sp = 0; sp < nt; sp++) {
             const int kc = __builtin_amdgcn_readfirstlane(sh.order[sp]);
             const int ncl = __builtin_amdgcn_readfirstlane(sh.ccount[kc]);
+#if MAM_LDLT_CHAINWAVE
+            // the column's wave runs its diagonal tile task and then its panel task; the panel tiles' tasks go to the
+            // next three waves of its half (k_struct_tiles' chain-aligned wave map)
+            const int mw = __builtin_amdgcn_readfirstlane(sh.mainw[kc]);
+            if (wid == mw) flow_tile_task(TL, slot, nt, kc, 0, Y, sh, lane);
+            for (int tk = 1; tk <= ncl; tk++)
+                if (wid == (mw & ~3) + ((mw & 3) + 1 + (tk - 1) % 3) % 4) flow_tile_task(TL, slot, nt, kc, tk, Y, sh, lane);
+            if (wid == mw) flow_panel_task(TL, slot, nt, kc, Y, sh, lane);
+#else
             // this wave's tasks of column kc in task order (tile tasks before the panel task: a wave holding both
             // finishes its tile task first)
             for (int tk = (wid - FLOW_TPC * sp % NW + NW) % NW; tk < FLOW_TPC; tk += NW) {
@@ -2449,6 +2496,7 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
                 else if (tk <= ncl)
                     flow_tile_task(TL, slot, nt, kc, tk, Y, sh, lane);
             }
+#endif
         }
         __syncthreads();
         LPROF(1);
@@ -3221,7 +3269,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.ccnt_g = cv.take<uint8_t>(2 * (size_t)std::max(d.nt, 1));
     d.perm = cv.take<int16_t>((size_t)std::max(d.Np, 1));
     d.iperm = cv.take<int16_t>((size_t)std::max(d.Np, 1));
-    d.order_g = cv.take<int8_t>(40);
+    d.order_g = cv.take<int8_t>(80);   // [0, 40) the columns in dataflow order, [40, 80) each column's wave
     d.pool = cv.take<double>((size_t)d.nt * (d.nt + 1) / 2 * 256);
     d.pose[0] = cv.take<double>(7 * (size_t)d.P);
     d.pose[1] = cv.take<double>(7 * (size_t)d.P);
