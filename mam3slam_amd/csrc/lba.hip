@@ -819,6 +819,8 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
         lm.fail = 0;
         lm.need_lin = 1;
         lm.sys_ready = 1;   // the setup's k_linearize + k_sys built iteration 0's system
+        lm.pad0 = 0;        // no trial pending its control step
+        lm.pad1 = 0;        // k_point_sys<true>'s workgroup count
         lm.done = (d.Np + d.L == 0 || lm.iterations <= 0) ? 1 : 0;
     }
 }
@@ -1321,7 +1323,6 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
         // with the split pose order the two ends' columns alternate. One wave, lane k: column k's parents (the
         // columns c < k of row k's non-zero tiles) as a bit row; level l = the columns whose parents all have levels
         // < l (Kahn's layering: the longest dependency path), positions by a prefix count within the level.
-        __shared__ int8_t ord_s[64], jm_s[64];
         if (t < 64) {
             uint64_t P = 0;
             if (lane < nt)
@@ -1331,39 +1332,9 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
             int base = 0;
             for (int l = 0; done != all && l < 64; l++) {
                 const uint64_t ready = __ballot(lane < nt && !((done >> lane) & 1) && (P & ~done) == 0);
-                if ((ready >> lane) & 1) {
-                    const int pos = base + __popcll(ready & ((1ull << lane) - 1));
-                    d.order_g[pos] = (int8_t)lane;
-                    ord_s[pos] = (int8_t)lane;
-                }
+                if ((ready >> lane) & 1) d.order_g[base + __popcll(ready & ((1ull << lane) - 1))] = (int8_t)lane;
                 base += __popcll(ready);
                 done |= ready;
-            }
-            // the column's last parent (its latest update: rlist's last entry), -1 for a chain's first column
-            jm_s[lane] = (int8_t)(P ? 63 - __clzll((long long)P) : -1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            // the dataflow's wave per column (order_g[40 + kc]): a chain's columns on one wave (its diagonal tile
-            // task and panel task follow the previous column's panel task there: no cross-wave hand-off on the chain),
-            // chains on disjoint halves of the waves (helper tile tasks on the next three waves of the half), a
-            // column inheriting a parent's wave another column took already moves to the other half
-            if (lane == 0) {
-                uint64_t taken = 0;
-                int nchain = 0;
-                int8_t mwv[64];
-                for (int sp = 0; sp < nt; sp++) {
-                    const int kc = ord_s[sp], jm = jm_s[kc];
-                    int mw;
-                    if (jm < 0) {
-                        mw = (4 * nchain++) % (LDLT_THREADS / 64);
-                    } else {
-                        mw = mwv[jm];
-                        if ((taken >> jm) & 1) mw = (mw + 4) % (LDLT_THREADS / 64);
-                        taken |= 1ull << jm;
-                    }
-                    mwv[kc] = (int8_t)mw;
-                    d.order_g[40 + kc] = (int8_t)mw;
-                }
             }
         }
         if (nt > 0)
@@ -1659,7 +1630,6 @@ struct LdltShared {
     int bflag[40];
     int tcnt[40];                // dataflow tasks: the column's tile tasks done
     alignas(4) int8_t order[40]; // dataflow: the block columns in dependency-level order (k_struct_tiles)
-    alignas(4) int8_t mainw[40]; // dataflow: each column's wave (its diagonal tile task and panel task; k_struct_tiles)
 #ifdef MAM_LDLT_TRACE
     int ltr[40][8];   // (low 32 bits of the cycle counter)
 #endif
@@ -2118,14 +2088,7 @@ __device__ __forceinline__ void lds_flag_set(int* f) {
 // in parallel (4 f64 MFMAs each, 64 cycles apiece) instead of one wave's 16 in turn, and the next column's tile tasks
 // are never on the wave factoring this column's panel. Every wave walks the columns in ascending order with at most
 // one task per column (dependencies only on earlier columns, or on the same column's tile tasks: no wait cycle).
-#ifndef MAM_LDLT_LAST
-#define MAM_LDLT_LAST 0   // 1: the panel task applies its column's last update (flow_last_update)
-#endif
-#ifndef MAM_LDLT_CHAINWAVE
-#define MAM_LDLT_CHAINWAVE 0   // 1: chain-aligned task-to-wave map (k_struct_tiles' order_g[40 + kc]); 0: round robin
-#endif
-static_assert(!MAM_LDLT_CHAINWAVE || LDLT_THREADS == 512, "the chain-aligned wave map assumes two halves of 4 waves");
-[[maybe_unused]] constexpr int FLOW_TPC = 10;   // up to 9 tile tasks + the panel task per column (columns of up to 8 panel tiles)
+constexpr int FLOW_TPC = 10;   // up to 9 tile tasks + the panel task per column (columns of up to 8 panel tiles)
 
 // C(sc) -= L(sa) D_j L(sb)^T for one tile (a tile task's pulled update), with WITH_Y also y_kc -= L(kc, j) y_j (lane
 // il's row; L(kc, j) = L(sb)): every LDS operand loaded before any use (one wait instead of one per MFMA step), the four
@@ -2180,9 +2143,7 @@ __device__ __forceinline__ void flow_tile_task(double* TL, const int16_t* slot, 
     const int r = t == 0 ? kc : __builtin_amdgcn_readfirstlane(sh.clist[kc * 40 + t - 1]);
     const int sc = __builtin_amdgcn_readfirstlane(slot[r * nt + kc]);
     double yd = t == 0 ? Y[kb + il] : 0.0;
-    // (MAM_LDLT_LAST: every update but the last column's, rlist's last entry — the panel task applies that one itself,
-    // to all of the column's tiles at once, straight before its pivot steps)
-    for (int q = 0; q + MAM_LDLT_LAST < nrl; q++) {
+    for (int q = 0; q < nrl; q++) {
         const int j = __builtin_amdgcn_readfirstlane(sh.rlist[kc * 40 + q]);
         const int sb = __builtin_amdgcn_readfirstlane(slot[kc * nt + j]);
         const int sa = t == 0 ? sb : __builtin_amdgcn_readfirstlane(slot[r * nt + j]);
@@ -2203,45 +2164,6 @@ __device__ __forceinline__ void flow_tile_task(double* TL, const int16_t* slot, 
     if (lane == 0) __hip_atomic_fetch_add(&sh.tcnt[kc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// The panel task's update of column kc's tiles (the diagonal tile and its ncl panel tiles) by column jm: T(r, kc) -=
-// L(r, jm) D_jm L(kc, jm)^T where L(r, jm) is non-zero, and y_kc -= L(kc, jm) y_jm (lane il's row). Not inlined: its
-// operands would otherwise stay live across the tall panel's registers and spill.
-__device__ __attribute__((noinline)) void flow_last_update(double* TL, const int16_t* slot, int nt, int kc, int jm,
-                                                           int ncl, double* Y, LdltShared& sh, int lane) {
-    const int il = lane & 15, kb = NB * kc;
-    const int sb = __builtin_amdgcn_readfirstlane(slot[kc * nt + jm]);
-    const int sd = __builtin_amdgcn_readfirstlane(slot[kc * nt + kc]);
-    // D_jm: the diagonal of column jm's factored diagonal tile (D(k) at tsw(k, k) = NB k)
-    const double* Dj = TL + (size_t)__builtin_amdgcn_readfirstlane(slot[jm * nt + jm]) * 256;
-    for (int a0 = -1; a0 < ncl; a0 += 4) {   // groups of up to 4 tiles (the diagonal tile first)
-        int scs[4], sas[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int a = a0 + u;
-            if (a < 0) {
-                scs[u] = sd;
-                sas[u] = sb;
-            } else if (a < ncl) {
-                const int r = __builtin_amdgcn_readfirstlane(sh.clist[kc * 40 + a]);
-                scs[u] = __builtin_amdgcn_readfirstlane(slot[r * nt + kc]);
-                sas[u] = __builtin_amdgcn_readfirstlane(slot[r * nt + jm]);
-            } else {
-                scs[u] = sd;
-                sas[u] = -1;
-            }
-        }
-        tile_update_multi<4>(TL, scs, sas, sb, Dj, lane, nullptr, nullptr, NB);
-    }
-    // y_kc -= L(kc, jm) y_jm (two chains of eight, as the tile tasks' y updates)
-    const double* Lb = TL + (size_t)sb * 256;
-    double v0 = Y[kb + il], v1 = 0.0;
-#pragma unroll
-    for (int k = 0; k < NB / 2; k++) v0 = fma(-Lb[tsw(il, k)], Y[NB * jm + k], v0);
-#pragma unroll
-    for (int k = NB / 2; k < NB; k++) v1 = fma(-Lb[tsw(il, k)], Y[NB * jm + k], v1);
-    if (lane < NB) Y[kb + lane] = v0 + v1;
-}
-
 __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot, int nt, int kc, double* Y,
                                                 LdltShared& sh, int lane) {
     const int g = lane >> 4, il = lane & 15, kb = NB * kc;
@@ -2255,19 +2177,6 @@ __device__ __forceinline__ void flow_panel_task(double* TL, const int16_t* slot,
     }
     while (__hip_atomic_load(&sh.tcnt[kc], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= ncl)
         __builtin_amdgcn_s_sleep(1);
-    // the column's last update (from column jm, rlist's last: the latest to finish) on every tile of the column in
-    // one wave (flow_last_update) instead of a tile task per tile handing over through the task count: on the critical
-    // path a column was a flag wait, a tile task, a count wait and this task's loads; now a flag wait and this update
-    const int nrl = __builtin_amdgcn_readfirstlane(sh.rcount[kc]);
-    if (MAM_LDLT_LAST && nrl > 0) {
-        const int jm = __builtin_amdgcn_readfirstlane(sh.rlist[kc * 40 + nrl - 1]);
-        lds_flag_wait(&sh.cflag[jm]);
-        LTRACE(6, jm);
-        flow_last_update(TL, slot, nt, kc, jm, ncl, Y, sh, lane);
-        // the updated tiles and y_kc (written by other lanes of this wave) before the row loads below
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
 #ifdef MAM_LDLT_PROFILE
     long long tp0 = clock64();
 #endif
@@ -2433,7 +2342,6 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         }
         if (t < 2 * nt) cv = ((gu8*)d.ccnt_g)[t];
         const int8_t ov = t < nt ? ((__attribute__((address_space(1))) const int8_t*)d.order_g)[t] : 0;
-        const int8_t mv = t < nt ? ((__attribute__((address_space(1))) const int8_t*)d.order_g)[40 + t] : 0;
 #pragma unroll
         for (int u = 0; u < YPT; u++) {
             const int i = t + u * LDLT_THREADS;
@@ -2457,7 +2365,6 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         if (t < nt) {
             sh.ccount[t] = cv;
             sh.order[t] = ov;
-            sh.mainw[t] = mv;
             sh.cflag[t] = 0;
             sh.bflag[t] = 0;
             sh.tcnt[t] = 0;
@@ -2479,15 +2386,6 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
         for (int sp = 0; sp < nt; sp++) {
             const int kc = __builtin_amdgcn_readfirstlane(sh.order[sp]);
             const int ncl = __builtin_amdgcn_readfirstlane(sh.ccount[kc]);
-#if MAM_LDLT_CHAINWAVE
-            // the column's wave runs its diagonal tile task and then its panel task; the panel tiles' tasks go to the
-            // next three waves of its half (k_struct_tiles' chain-aligned wave map)
-            const int mw = __builtin_amdgcn_readfirstlane(sh.mainw[kc]);
-            if (wid == mw) flow_tile_task(TL, slot, nt, kc, 0, Y, sh, lane);
-            for (int tk = 1; tk <= ncl; tk++)
-                if (wid == (mw & ~3) + ((mw & 3) + 1 + (tk - 1) % 3) % 4) flow_tile_task(TL, slot, nt, kc, tk, Y, sh, lane);
-            if (wid == mw) flow_panel_task(TL, slot, nt, kc, Y, sh, lane);
-#else
             // this wave's tasks of column kc in task order (tile tasks before the panel task: a wave holding both
             // finishes its tile task first)
             for (int tk = (wid - FLOW_TPC * sp % NW + NW) % NW; tk < FLOW_TPC; tk += NW) {
@@ -2496,7 +2394,6 @@ __device__ __forceinline__ void ldlt_tiles(const Prob& d, double* lds, LdltShare
                 else if (tk <= ncl)
                     flow_tile_task(TL, slot, nt, kc, tk, Y, sh, lane);
             }
-#endif
         }
         __syncthreads();
         LPROF(1);
@@ -2805,9 +2702,7 @@ __device__ __forceinline__ void dinv_of(const double H[9], double lambda, double
 //    (k_sys's sums); every trial D^-1 = (H_ll + lambda I)^-1 per point and, per slot, W = H_pl D^-1 and the
 //    coefficients H_pl D^-1 b_l (k_schur_prep's products);
 //  pose waves — at an iteration start H_pp, b_p in POSE_SPLIT partial sums per pose (pose_sys_wave).
-__global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs) {
-    const Prob& d = probs[blockIdx.y];
-    const LMHead hd = lm_head(d.lm);
+__device__ __forceinline__ void point_sys_body(const Prob& d, const LMHead& hd) {
     if (hd.status || hd.done) return;
     const bool lin = hd.need_lin && !hd.sys_ready;
     const int nbp = (d.L + PW - 1) / PW;
@@ -2938,6 +2833,113 @@ __global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs
         for (int k = 0; k < 18; k++) W[k] = o[k];
 #pragma unroll
         for (int k = 0; k < 6; k++) C[k] = cf[k];
+    }
+}
+
+// the trial's chi2 and computeScale (levenberg.cpp:187-194: sum_j x_j (lambda x_j + b_j) over the full x) from
+// k_point_trial's per-wave partials (fixed order: strided over RED virtual threads, then a tree; the same bits for any
+// T) and the factorization epilogue's pose part
+template <int T>
+__device__ void trial_sums(const Prob& d, double* s, double* tempChi, double* scale0) {
+    const int nbp = (d.L + PW - 1) / PW;
+    double acc[RED / T], acs[RED / T];
+#pragma unroll
+    for (int v = 0; v < RED / T; v++) {
+        acc[v] = 0.0;
+        acs[v] = 0.0;
+        for (int j = threadIdx.x + T * v; j < nbp; j += RED) {
+            acc[v] += d.part[j];
+            acs[v] += d.part_s[j];
+        }
+    }
+    *tempChi = block_sum<T>(acc, s);
+    *scale0 = block_sum<T>(acs, s) + d.lm->scale_p;
+}
+
+// The end of a trial (thread 0): levenberg.cpp:108-158 (rho, accept / reject, lambda), then the iteration-end tests of
+// levenberg.cpp:159-168 and sparse_optimizer.cpp:381-409, on the state lm (hd: its head as the trial left it)
+__device__ void ctl_step(LM& lm, const LMHead& hd, double tempChi, double scale0) {
+    const bool begin = hd.need_lin != 0;
+    const double lambda = trial_lambda(hd);
+    if (begin) {
+        if (hd.its == 0) {
+            lm.currentChi = lm.initialChi;
+            lm.ni = 2.0;
+            lm.nBad = 0;
+        } else {
+            lm.currentChi = lm.acceptedChi;
+        }
+        lm.iniChi = lm.currentChi;
+        lm.qmax = 0;
+        lm.need_lin = 0;
+    }
+    if (hd.fail) tempChi = DBL_MAX;
+    double rho = lm.currentChi - tempChi;
+    const double scale = scale0 + 1e-3;
+    rho /= scale;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow((2 * rho - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        const double scaleFactor = fmax(1. / 3., alpha);
+        lm.lambda = lambda * scaleFactor;
+        lm.ni = 2;
+        lm.currentChi = tempChi;
+        lm.acceptedChi = tempChi;
+        lm.cur = 1 - lm.cur;   // accept: discardTop
+    } else {
+        lm.lambda = lambda * lm.ni;   // reject: pop
+        lm.ni *= 2;
+    }
+    lm.qmax++;
+    lm.trials++;
+    if (rho < 0 && lm.qmax < 10) return;   // another trial of this iteration
+    lm.its++;
+    bool term = false;
+    if (lm.qmax == 10 || rho == 0) term = true;
+    else {
+        if ((lm.iniChi - lm.currentChi) * 1e3 < lm.iniChi) lm.nBad++;
+        else lm.nBad = 0;
+        if (lm.nBad >= 3) term = true;
+    }
+    if (term || lm.its >= lm.iterations) lm.done = 1;
+    else {
+        lm.need_lin = 1;
+        lm.sys_ready = 0;   // the next iteration linearises at the accepted state
+    }
+}
+
+// FOLD (a single window): the previous trial's control step first (lm.pad0 set: ctl_step, computed by every
+// workgroup from the same partials — the same bits — and written back by the last workgroup to finish, once every
+// workgroup has read the state it started from), instead of a k_ctl_end launch between the trials.
+template <bool FOLD>
+__global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs) {
+    const Prob& d = probs[blockIdx.y];
+    LMHead hd = lm_head(d.lm);
+    __shared__ LM lml;
+    bool counted = false;
+    if constexpr (FOLD) {
+        if (!hd.status && !hd.done && hd.pad0) {   // uniform
+            __shared__ double s[RED];
+            double tempChi, scale0;
+            trial_sums<64>(d, s, &tempChi, &scale0);
+            if (threadIdx.x == 0) {
+                lml = *d.lm;
+                ctl_step(lml, hd, tempChi, scale0);
+                lml.pad0 = 0;
+            }
+            __syncthreads();
+            __builtin_memcpy(&hd, &lml, sizeof(hd));
+            counted = true;
+        }
+    }
+    point_sys_body(d, hd);
+    if (FOLD && counted) {
+        __syncthreads();
+        if (threadIdx.x == 0 &&
+            atomicAdd(&d.lm->pad1, 1) == (int)(gridDim.x * gridDim.y) - 1) {   // the last workgroup (one window)
+            lml.pad1 = 0;
+            *d.lm = lml;
+        }
     }
 }
 
@@ -3085,6 +3087,7 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restric
     const LMHead hd = lm_head(d.lm);
     if (hd.status || hd.done) return;
     LM& lm = *d.lm;
+    if (threadIdx.x == 0) lm.pad0 = 1;   // a trial pending its control step (k_ctl_end, or the next k_point_sys)
     if (d.Np == 0) {
         if (threadIdx.x == 0) lm.fail = 0;
     } else if (hd.tiles_lds) {
@@ -3100,79 +3103,23 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restric
 // tests of levenberg.cpp:159-168 and sparse_optimizer.cpp:381-409. (Run instead by the last workgroup of the trial's
 // k_linearize, the kernel boundary replaced by a release / acquire per workgroup, the batch of 32 took 5.6 -> 9.5 ms:
 // every workgroup's agent-scope release writes its L2 back.)
+// grid (Q) x 256: end of a trial — ctl_step on the trial's chi2 and computeScale. (Run instead by the last workgroup of
+// the trial's k_linearize, the kernel boundary replaced by a release / acquire per workgroup, the batch of 32 took
+// 5.6 -> 9.5 ms: every workgroup's agent-scope release writes its L2 back.) Only with a trial pending (lm.pad0, set by
+// the factorization): a single window folds this step into the next trial's k_point_sys and runs it here once, before
+// the chunk's k_finish.
 __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs) {
     constexpr int T = RED;
     __shared__ double s[RED];
     const Prob& d = probs[blockIdx.x];
     const LMHead hd = lm_head(d.lm);
-    if (hd.status || hd.done) return;
+    if (hd.status || hd.done || !hd.pad0) return;
     LM& lm = *d.lm;
-    // an iteration's first trial: the iteration-start state first (the chi2 of the linearised state: on the first
-    // iteration the initial chi2 of the same state, else the accepted trial's; lambda_0)
-    const bool begin = hd.need_lin != 0;
-    const double lambda = trial_lambda(hd);
-    // the trial's chi2 and computeScale (levenberg.cpp:187-194: sum_j x_j (lambda x_j + b_j) over the full x) from
-    // k_point_trial's per-wave partials (fixed order: strided over RED virtual threads, then a tree) and the
-    // factorization epilogue's pose part
-    const int nbp = (d.L + PW - 1) / PW;
-    double acc[RED / T], acs[RED / T];
-#pragma unroll
-    for (int v = 0; v < RED / T; v++) {
-        acc[v] = 0.0;
-        acs[v] = 0.0;
-        for (int j = threadIdx.x + T * v; j < nbp; j += RED) {
-            acc[v] += d.part[j];
-            acs[v] += d.part_s[j];
-        }
-    }
-    double tempChi = block_sum<T>(acc, s);
-    const double scale0 = block_sum<T>(acs, s) + lm.scale_p;
+    double tempChi, scale0;
+    trial_sums<T>(d, s, &tempChi, &scale0);
     if (threadIdx.x != 0) return;
-    if (begin) {
-        if (hd.its == 0) {
-            lm.currentChi = lm.initialChi;
-            lm.ni = 2.0;
-            lm.nBad = 0;
-        } else {
-            lm.currentChi = lm.acceptedChi;
-        }
-        lm.iniChi = lm.currentChi;
-        lm.qmax = 0;
-        lm.need_lin = 0;
-    }
-    if (hd.fail) tempChi = DBL_MAX;
-    double rho = lm.currentChi - tempChi;
-    const double scale = scale0 + 1e-3;
-    rho /= scale;
-    if (rho > 0 && isfinite(tempChi)) {
-        double alpha = 1. - pow((2 * rho - 1), 3);
-        alpha = fmin(alpha, 2. / 3.);
-        const double scaleFactor = fmax(1. / 3., alpha);
-        lm.lambda = lambda * scaleFactor;
-        lm.ni = 2;
-        lm.currentChi = tempChi;
-        lm.acceptedChi = tempChi;
-        lm.cur = 1 - lm.cur;   // accept: discardTop
-    } else {
-        lm.lambda = lambda * lm.ni;   // reject: pop
-        lm.ni *= 2;
-    }
-    lm.qmax++;
-    lm.trials++;
-    if (rho < 0 && lm.qmax < 10) return;   // another trial of this iteration
-    lm.its++;
-    bool term = false;
-    if (lm.qmax == 10 || rho == 0) term = true;
-    else {
-        if ((lm.iniChi - lm.currentChi) * 1e3 < lm.iniChi) lm.nBad++;
-        else lm.nBad = 0;
-        if (lm.nBad >= 3) term = true;
-    }
-    if (term || lm.its >= lm.iterations) lm.done = 1;
-    else {
-        lm.need_lin = 1;
-        lm.sys_ready = 0;   // the next iteration linearises at the accepted state
-    }
+    ctl_step(lm, hd, tempChi, scale0);
+    lm.pad0 = 0;
 }
 
 // grid (ceil(E/256), Q): isDepthPositive of the final estimate
@@ -3269,7 +3216,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.ccnt_g = cv.take<uint8_t>(2 * (size_t)std::max(d.nt, 1));
     d.perm = cv.take<int16_t>((size_t)std::max(d.Np, 1));
     d.iperm = cv.take<int16_t>((size_t)std::max(d.Np, 1));
-    d.order_g = cv.take<int8_t>(80);   // [0, 40) the columns in dataflow order, [40, 80) each column's wave
+    d.order_g = cv.take<int8_t>(40);
     d.pool = cv.take<double>((size_t)d.nt * (d.nt + 1) / 2 * 256);
     d.pose[0] = cv.take<double>(7 * (size_t)d.P);
     d.pose[1] = cv.take<double>(7 * (size_t)d.P);
@@ -3508,6 +3455,13 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         MAM_HIP(hipEventRecord(c->ev_start, s));   // the structure build precedes every group
         for (int g = 1; g < G; g++) MAM_HIP(hipStreamWaitEvent(sg[g], c->ev_start, 0));
     }
+    // a single window: every trial's control step folded into the next trial's k_point_sys (MAM_LBA_FOLD=0: the
+    // k_ctl_end launch per trial)
+    static const bool fold_env = [] {
+        const char* e = std::getenv("MAM_LBA_FOLD");
+        return !(e && std::atoi(e) == 0);
+    }();
+    const bool fold = fold_env && Q == 1 && G == 1;
     auto slot_g = [&](int g) {
         const int q0 = g * Q / G, q1 = (g + 1) * Q / G, Qg = q1 - q0;
         const Prob* Pg = P + q0;
@@ -3516,7 +3470,8 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
-            hipLaunchKernelGGL(k_point_sys, gPtsg, dim3(64), 0, st, Pg);
+            if (fold) hipLaunchKernelGGL(k_point_sys<true>, gPtsg, dim3(64), 0, st, Pg);
+            else hipLaunchKernelGGL(k_point_sys<false>, gPtsg, dim3(64), 0, st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 1);
@@ -3532,12 +3487,13 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         {
             mam::StageTimer::Scope sc(tm, st, 3);
             hipLaunchKernelGGL(k_point_trial, gTrig, dim3(64), 0, st, Pg);
-            hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
+            if (!fold) hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
     };
     auto slot = [&]() {
         for (int g = 0; g < G; g++) slot_g(g);
     };
+    (void)fold;
     auto join = [&]() -> int {   // the other groups' work before anything the first stream does next
         for (int g = 1; g < G; g++) {
             MAM_HIP(hipEventRecord(c->ev_done[g - 1], sg[g]));
@@ -3559,6 +3515,8 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     const dim3 gFin(std::max({(maxE + 255) / 256, (maxPL + 255) / 256, 1}), Q);
     auto finish_and_read = [&]() -> int {
         if (int rc = join()) return rc;
+        // the last trial's control step (pending when the trials folded it into the next k_point_sys)
+        if (fold) hipLaunchKernelGGL(mam::lba::k_ctl_end, dim3(Q), dim3(mam::lba::RED), 0, s, P);
         hipLaunchKernelGGL(mam::lba::k_finish, gFin, dim3(256), 0, s, P, outs_d);
         MAM_HIP(hipGetLastError());
         MAM_HIP(hipMemcpyAsync(lh, lms_d, sizeof(LM) * Q, hipMemcpyDeviceToHost, s));
