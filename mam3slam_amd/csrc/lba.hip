@@ -819,8 +819,6 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
         lm.fail = 0;
         lm.need_lin = 1;
         lm.sys_ready = 1;   // the setup's k_linearize + k_sys built iteration 0's system
-        lm.pad0 = 0;        // no trial pending its control step
-        lm.pad1 = 0;        // k_point_sys<true>'s workgroup count
         lm.done = (d.Np + d.L == 0 || lm.iterations <= 0) ? 1 : 0;
     }
 }
@@ -2908,39 +2906,9 @@ __device__ void ctl_step(LM& lm, const LMHead& hd, double tempChi, double scale0
     }
 }
 
-// FOLD (a single window): the previous trial's control step first (lm.pad0 set: ctl_step, computed by every
-// workgroup from the same partials — the same bits — and written back by the last workgroup to finish, once every
-// workgroup has read the state it started from), instead of a k_ctl_end launch between the trials.
-template <bool FOLD>
 __global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
-    LMHead hd = lm_head(d.lm);
-    __shared__ LM lml;
-    bool counted = false;
-    if constexpr (FOLD) {
-        if (!hd.status && !hd.done && hd.pad0) {   // uniform
-            __shared__ double s[RED];
-            double tempChi, scale0;
-            trial_sums<64>(d, s, &tempChi, &scale0);
-            if (threadIdx.x == 0) {
-                lml = *d.lm;
-                ctl_step(lml, hd, tempChi, scale0);
-                lml.pad0 = 0;
-            }
-            __syncthreads();
-            __builtin_memcpy(&hd, &lml, sizeof(hd));
-            counted = true;
-        }
-    }
-    point_sys_body(d, hd);
-    if (FOLD && counted) {
-        __syncthreads();
-        if (threadIdx.x == 0 &&
-            atomicAdd(&d.lm->pad1, 1) == (int)(gridDim.x * gridDim.y) - 1) {   // the last workgroup (one window)
-            lml.pad1 = 0;
-            *d.lm = lml;
-        }
-    }
+    point_sys_body(d, lm_head(d.lm));
 }
 
 // grid (ceil(L / PW), Q) x 64, after the factorization and its pose epilogue (the trial poses): per point (lanes < PW)
@@ -3087,7 +3055,6 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restric
     const LMHead hd = lm_head(d.lm);
     if (hd.status || hd.done) return;
     LM& lm = *d.lm;
-    if (threadIdx.x == 0) lm.pad0 = 1;   // a trial pending its control step (k_ctl_end, or the next k_point_sys)
     if (d.Np == 0) {
         if (threadIdx.x == 0) lm.fail = 0;
     } else if (hd.tiles_lds) {
@@ -3105,21 +3072,19 @@ __global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restric
 // every workgroup's agent-scope release writes its L2 back.)
 // grid (Q) x 256: end of a trial — ctl_step on the trial's chi2 and computeScale. (Run instead by the last workgroup of
 // the trial's k_linearize, the kernel boundary replaced by a release / acquire per workgroup, the batch of 32 took
-// 5.6 -> 9.5 ms: every workgroup's agent-scope release writes its L2 back.) Only with a trial pending (lm.pad0, set by
-// the factorization): a single window folds this step into the next trial's k_point_sys and runs it here once, before
-// the chunk's k_finish.
+// 5.6 -> 9.5 ms: every workgroup's agent-scope release writes its L2 back. Folded into the next trial's k_point_sys
+// for a single window — every workgroup computing it from the same partials, the last one writing the state back —
+// the lone window took 1.278 -> 1.318 ms: k_point_sys grew 7.6 us, more than the launch it saved.)
 __global__ __launch_bounds__(RED) void k_ctl_end(const Prob* __restrict__ probs) {
     constexpr int T = RED;
     __shared__ double s[RED];
     const Prob& d = probs[blockIdx.x];
     const LMHead hd = lm_head(d.lm);
-    if (hd.status || hd.done || !hd.pad0) return;
-    LM& lm = *d.lm;
+    if (hd.status || hd.done) return;
     double tempChi, scale0;
     trial_sums<T>(d, s, &tempChi, &scale0);
     if (threadIdx.x != 0) return;
-    ctl_step(lm, hd, tempChi, scale0);
-    lm.pad0 = 0;
+    ctl_step(*d.lm, hd, tempChi, scale0);
 }
 
 // grid (ceil(E/256), Q): isDepthPositive of the final estimate
@@ -3455,13 +3420,6 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         MAM_HIP(hipEventRecord(c->ev_start, s));   // the structure build precedes every group
         for (int g = 1; g < G; g++) MAM_HIP(hipStreamWaitEvent(sg[g], c->ev_start, 0));
     }
-    // a single window: every trial's control step folded into the next trial's k_point_sys (MAM_LBA_FOLD=0: the
-    // k_ctl_end launch per trial)
-    static const bool fold_env = [] {
-        const char* e = std::getenv("MAM_LBA_FOLD");
-        return !(e && std::atoi(e) == 0);
-    }();
-    const bool fold = fold_env && Q == 1 && G == 1;
     auto slot_g = [&](int g) {
         const int q0 = g * Q / G, q1 = (g + 1) * Q / G, Qg = q1 - q0;
         const Prob* Pg = P + q0;
@@ -3470,8 +3428,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
-            if (fold) hipLaunchKernelGGL(k_point_sys<true>, gPtsg, dim3(64), 0, st, Pg);
-            else hipLaunchKernelGGL(k_point_sys<false>, gPtsg, dim3(64), 0, st, Pg);
+            hipLaunchKernelGGL(k_point_sys, gPtsg, dim3(64), 0, st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 1);
@@ -3487,13 +3444,12 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         {
             mam::StageTimer::Scope sc(tm, st, 3);
             hipLaunchKernelGGL(k_point_trial, gTrig, dim3(64), 0, st, Pg);
-            if (!fold) hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
+            hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
     };
     auto slot = [&]() {
         for (int g = 0; g < G; g++) slot_g(g);
     };
-    (void)fold;
     auto join = [&]() -> int {   // the other groups' work before anything the first stream does next
         for (int g = 1; g < G; g++) {
             MAM_HIP(hipEventRecord(c->ev_done[g - 1], sg[g]));
@@ -3515,8 +3471,6 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     const dim3 gFin(std::max({(maxE + 255) / 256, (maxPL + 255) / 256, 1}), Q);
     auto finish_and_read = [&]() -> int {
         if (int rc = join()) return rc;
-        // the last trial's control step (pending when the trials folded it into the next k_point_sys)
-        if (fold) hipLaunchKernelGGL(mam::lba::k_ctl_end, dim3(Q), dim3(mam::lba::RED), 0, s, P);
         hipLaunchKernelGGL(mam::lba::k_finish, gFin, dim3(256), 0, s, P, outs_d);
         MAM_HIP(hipGetLastError());
         MAM_HIP(hipMemcpyAsync(lh, lms_d, sizeof(LM) * Q, hipMemcpyDeviceToHost, s));
