@@ -597,9 +597,10 @@ def ingest_section(tr, reps=5):
 
 def ring_lba_section(newmp, check=True):
     """LocalBundleAdjustment over the keyframes this run's Tracking inserted (mapping.RingLBA): the last keyframe
-    run's windows — each new keyframe with its 30 ring neighbours (20 optimised, 10 fixed), its keypoints' MapPoints
-    and their observations from the run's forward Fuse matches — assembled on the device and solved by the batch
-    device API; with check, window 0 against the oracle on the same graph. Outside the timed region: the timed
+    run's windows by the reference's window rule — each new keyframe with its covisible ring neighbours optimised and
+    the other neighbours observing its MapPoints fixed, its keypoints' MapPoints and their observations from the run's
+    forward Fuse matches, compacted — assembled on the device and solved by the batch device API; with check, window 0
+    against the oracle on the same graph. Outside the timed region: the timed
     LocalMapping leg solves the shared synthetic map's windows, whose write-backs the exchange carries."""
     import torch
 
@@ -617,11 +618,13 @@ def ring_lba_section(newmp, check=True):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / reps
     prob = rl.window(0)
-    act = prob.edge_active.reshape(-1, rl.NV)
     _, _, _, its, trials, st, ic, fc = rl.result(0)
-    res = {"windows": newmp.W, "poses": rl.NV, "optimised_poses": rl.NV - rl.n_fixed,
-           "points_observed": int((act.sum(1) > 0).sum()), "observations": int(act.sum()),
-           "ms_per_batch": ms, "iterations": its, "trials": trials, "status": st, "chi2": [ic, fc]}
+    sz = rl.sizes   # per window: poses, points, edges, optimised poses (the compacted covisibility windows)
+    res = {"windows": newmp.W, "rule": rl.rule, "covisibility_threshold": rl.COVIS_TH,
+           "poses_mean": float(sz[:, 0].mean()), "optimised_poses_mean": float(sz[:, 3].mean()),
+           "points_mean": float(sz[:, 1].mean()), "observations_mean": float(sz[:, 2].mean()),
+           "ms_per_batch": ms, "iterations": its, "trials": trials, "status": st, "chi2": [ic, fc],
+           "trials_all": [t for _, t, _ in rl.stats]}
     if check:
         from oracle import oracle_py
 

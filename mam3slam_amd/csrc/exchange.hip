@@ -275,6 +275,141 @@ __global__ __launch_bounds__(64) void k_ring_windows(const RingArgs a) {
     }
 }
 
+// ---- LBA windows by the reference's window rule, compacted: grid (n_windows) x 256, one workgroup per window.
+// Optimizer::LocalBundleAdjustment (Optimizer.cc:1118-1186): the local keyframes are the new keyframe and its
+// covisible keyframes (GetVectorCovisibleKeyFrames: the connections KeyFrame::UpdateConnections keeps, weight = shared
+// MapPoints >= 15, or the heaviest one when none reaches it, KeyFrame.cc:312-380), the local MapPoints those the new
+// keyframe observes (the ring's MapPoints are the new keyframe's; a point seen by fewer than two keyframes is left
+// out, as the fixed-shape form did), the fixed keyframes every other keyframe observing a local MapPoint. Poses: the
+// new keyframe, its covisible keyframes in neighbour order, then the fixed ones; points in keypoint order; edges
+// point-major (the new keyframe's observation first, then the neighbours' in neighbour order) — only real
+// observations, no inactive slots. counts[w] = {poses, points, edges, optimised poses}; pose_slot[w][i] the ring slot
+// of pose i, point_src[w][i] the keypoint (MapPoint row of the new keyframe) of point i.
+constexpr int RINGC_T = 256;
+__device__ __forceinline__ int ringc_excl_scan(int v, int* wsum, int& total) {
+    // block exclusive scan of RINGC_T values (wave inclusive scans by shuffle, then the wave totals)
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(x, o, 64);
+        if (lane >= o) x += u;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int pre = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < RINGC_T / 64; w++) {
+        const int t = wsum[w];
+        if (w < wid) pre += t;
+        total += t;
+    }
+    __syncthreads();
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(RINGC_T) void k_ring_windows_covis(const RingArgs a, int covis_th, int32_t* counts,
+                                                                int32_t* pose_slot, int32_t* point_src) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t obsm[];   // [S]: bit k = observed by neighbour k
+    __shared__ int wt[32], vpose[33], wsum[RINGC_T / 64], carry[2], hdr[4];
+    const int w = blockIdx.x, t = threadIdx.x, nn = a.nn, S = a.S;
+    const mam_ring_window& o = a.outs[w];
+    const int j = a.pairs[2 * (w * nn)];
+    const int n = min(max(a.cnt[2 * j], 0), S);
+    if (t < 32) wt[t] = 0;
+    __syncthreads();
+    // observation masks and the covisibility weights (shared MapPoints per neighbour)
+    for (int p0 = 0; p0 < S; p0 += RINGC_T) {   // (uniform trip count: the ballots need every lane)
+        const int p = p0 + t;
+        uint32_t m = 0;
+        if (p < n)
+            for (int k = 0; k < nn; k++) {
+                const int nb = a.pairs[2 * (w * nn + k) + 1];
+                const int idx = a.match[(size_t)(w * nn + k) * S + p];
+                if (idx >= 0 && idx < min(a.cnt[2 * nb], S)) m |= 1u << k;
+            }
+        if (p < S) obsm[p] = m;
+        for (int k = 0; k < nn; k++) {
+            const int c = __popcll(__ballot((m >> k) & 1u));
+            if ((t & 63) == 0 && c) atomicAdd(&wt[k], c);
+        }
+    }
+    __syncthreads();
+    // the window's keyframes (thread 0: 30 neighbours)
+    if (t == 0) {
+        int best = -1, bw = 0, nloc = 0;
+        for (int k = 0; k < nn; k++) {
+            if (wt[k] >= covis_th) nloc++;
+            if (wt[k] > bw) { bw = wt[k]; best = k; }
+        }
+        int np = 1;
+        vpose[0] = 0;
+        for (int k = 0; k < nn; k++) {
+            const bool loc = nloc > 0 ? wt[k] >= covis_th : k == best;
+            vpose[1 + k] = loc ? np++ : -1;
+        }
+        const int nopt = np;
+        for (int k = 0; k < nn; k++)
+            if (vpose[1 + k] < 0 && wt[k] > 0) vpose[1 + k] = np++;
+        hdr[0] = np;
+        hdr[1] = nopt;
+    }
+    __syncthreads();
+    const int np = hdr[0], nopt = hdr[1];
+    if (t <= nn) {
+        const int v = t, pi = vpose[v];
+        if (pi >= 0) {
+            const int slot = v == 0 ? j : a.pairs[2 * (w * nn + v - 1) + 1];
+            const float* T = a.tcw + 7 * (size_t)slot;
+            for (int k = 0; k < 4; k++) o.pose_q[4 * pi + k] = (double)T[k];
+            for (int k = 0; k < 3; k++) o.pose_t[3 * pi + k] = (double)T[4 + k];
+            o.pose_fixed[pi] = pi >= nopt ? 1 : 0;
+            pose_slot[(size_t)w * (nn + 1) + pi] = slot;
+        }
+    }
+    // points (kept: observed by the new keyframe and at least one neighbour) and their edges, compacted in order
+    if (t == 0) { carry[0] = 0; carry[1] = 0; }
+    __syncthreads();
+    for (int p0 = 0; p0 < S; p0 += RINGC_T) {
+        const int p = p0 + t;
+        const uint32_t m = p < S ? obsm[p] : 0u;
+        const bool keep = m != 0;
+        const int ne = keep ? 1 + __popc(m) : 0;
+        int tp, te;
+        const int pi = ringc_excl_scan(keep ? 1 : 0, wsum, tp) + carry[0];
+        const int e0 = ringc_excl_scan(ne, wsum, te) + carry[1];
+        if (keep) {
+            const float* M = a.mps + ((size_t)j * S + p) * 20;
+            for (int k = 0; k < 3; k++) o.point_xyz[3 * (size_t)pi + k] = (double)M[k];
+            point_src[(size_t)w * S + pi] = p;
+            int e = e0;
+            for (int v = 0; v <= nn; v++) {
+                if (v > 0 && !((m >> (v - 1)) & 1u)) continue;
+                const int slot = v == 0 ? j : a.pairs[2 * (w * nn + v - 1) + 1];
+                const int idx = v == 0 ? p : a.match[(size_t)(w * nn + v - 1) * S + p];
+                const mam_keypoint& kp = a.keys[(size_t)slot * S + idx];
+                o.edge_point[e] = pi;
+                o.edge_pose[e] = vpose[v];
+                o.edge_obs[2 * (size_t)e] = (double)kp.x;
+                o.edge_obs[2 * (size_t)e + 1] = (double)kp.y;
+                o.edge_inv_sigma2[e] = (double)a.inv_s2[min(max(kp.octave, 0), a.nlevels - 1)];
+                if (o.edge_active) o.edge_active[e] = 1;
+                e++;
+            }
+        }
+        __syncthreads();
+        if (t == 0) { carry[0] += tp; carry[1] += te; }
+        __syncthreads();
+    }
+    if (t == 0) {
+        counts[4 * w] = np;
+        counts[4 * w + 1] = carry[0];
+        counts[4 * w + 2] = carry[1];
+        counts[4 * w + 3] = nopt;
+    }
+}
+
 }  // namespace mam
 
 extern "C" int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn, int n_fixed, const void* keys,
@@ -300,6 +435,35 @@ extern "C" int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn,
     a.outs = outs;
     const int np = std::max(S, nn + 1);
     hipLaunchKernelGGL(mam::k_ring_windows, dim3((np + 63) / 64, n_windows), dim3(64), 0, (hipStream_t)stream, a);
+    MAM_HIP(hipGetLastError());
+    return MAM_OK;
+}
+
+extern "C" int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, int nn, int covis_th, const void* keys,
+                                          const int32_t* cnt, const void* tcw, const void* mps, int S,
+                                          const int32_t* match, const float* inv_level_sigma2, int nlevels,
+                                          const mam_ring_window* outs, int32_t* counts, int32_t* pose_slot,
+                                          int32_t* point_src, void* stream) {
+    if (n_windows < 0 || nn < 1 || nn > 31 || S < 1 || nlevels < 1 || nlevels > 8 || !pairs || !keys || !cnt || !tcw ||
+        !mps || !match || !inv_level_sigma2 || (n_windows > 0 && (!outs || !counts || !pose_slot || !point_src)))
+        return MAM_ERR_ARG;
+    if ((size_t)S * 4 > 64 * 1024) return MAM_ERR_CAPACITY;
+    if (n_windows == 0) return MAM_OK;
+    mam::RingArgs a{};
+    a.pairs = pairs;
+    a.nn = nn;
+    a.n_fixed = 0;
+    a.S = S;
+    a.nlevels = nlevels;
+    a.keys = reinterpret_cast<const mam_keypoint*>(keys);
+    a.cnt = cnt;
+    a.tcw = reinterpret_cast<const float*>(tcw);
+    a.mps = reinterpret_cast<const float*>(mps);
+    a.match = match;
+    for (int l = 0; l < nlevels; l++) a.inv_s2[l] = inv_level_sigma2[l];
+    a.outs = outs;
+    hipLaunchKernelGGL(mam::k_ring_windows_covis, dim3(n_windows), dim3(mam::RINGC_T), (size_t)S * 4,
+                       (hipStream_t)stream, a, covis_th, counts, pose_slot, point_src);
     MAM_HIP(hipGetLastError());
     return MAM_OK;
 }

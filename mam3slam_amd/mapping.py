@@ -524,18 +524,25 @@ class RingWindow(C.Structure):
 
 class RingLBA:
     """LocalBundleAdjustment over the keyframes Tracking inserted (Optimizer.cc:1118-1331 on the NewMapPointsLeg ring):
-    per new keyframe of the last run, the window of the keyframe and its NN neighbours (the nearest NN - n_fixed
-    optimised, the rest fixed), its keypoints' MapPoints and their observations by the neighbours from the run's
-    forward Fuse matches (mam_ring_lba_windows, on the leg's stream right after the run), solved with the batch device
-    API (mam_lba_solve_batch_device). Fixed problem shape: S MapPoint slots x (NN + 1) edge slots, unobserved slots
-    inactive."""
+    per new keyframe of the last run, its window solved with the batch device API (mam_lba_solve_batch_device).
 
-    def __init__(self, nm, n_fixed: int = 10, iterations: int = 10, solver=None):
+    rule "covisibility" (the reference's window rule, mam_ring_lba_windows_covis): the new keyframe and its covisible
+    ring neighbours (weight = its MapPoints a neighbour observes, from the run's forward Fuse matches: >= 15 as
+    KeyFrame::UpdateConnections keeps them, the heaviest when none reaches it) optimised, every other neighbour
+    observing one of its MapPoints fixed; the problem compacted to the real observations (sizes read back once per
+    batch). rule "sequence" (mam_ring_lba_windows): the NN neighbours nearest in sequence, the last n_fixed of them
+    fixed, a fixed S x (NN + 1) edge-slot shape with unobserved slots inactive."""
+
+    COVIS_TH = 15
+
+    def __init__(self, nm, n_fixed: int = 10, iterations: int = 10, solver=None, rule: str = "covisibility"):
         import torch
 
         from .lba import HUBER_MONO
 
-        self.nm, self.dev = nm, nm.dev
+        if rule not in ("covisibility", "sequence"):
+            raise ValueError(rule)
+        self.nm, self.dev, self.rule = nm, nm.dev, rule
         W, NN, S = nm.W, nm.NN, nm.S
         self.NV, self.n_fixed = NN + 1, int(n_fixed)
         NV, E = self.NV, S * (NN + 1)
@@ -562,7 +569,8 @@ class RingLBA:
             P.point_xyz = b["point_xyz"].data_ptr()
             P.edge_point, P.edge_pose = b["edge_point"].data_ptr(), b["edge_pose"].data_ptr()
             P.edge_obs, P.edge_inv_sigma2 = b["edge_obs"].data_ptr(), b["edge_inv_sigma2"].data_ptr()
-            P.edge_active, P.cams = b["edge_active"].data_ptr(), self.cams.data_ptr()
+            P.edge_active = b["edge_active"].data_ptr() if rule == "sequence" else None
+            P.cams = self.cams.data_ptr()
             P.huber_delta, P.iterations = HUBER_MONO, int(iterations)
             P.cam_model = 1 if cam.is_kb8 else 0
             P.n_opt_poses = NV - self.n_fixed
@@ -570,6 +578,13 @@ class RingLBA:
             R.pose_q, R.pose_t, R.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
             R.edge_chi2, R.edge_depth_ok = b["out_chi2"].data_ptr(), b["out_depth"].data_ptr()
         self.d_wins = torch.from_numpy(np.frombuffer(bytes(wins), np.uint8).copy()).to(self.dev)
+        # covisibility windows: per window {poses, points, edges, optimised poses}, the ring slot of each pose, the new
+        # keyframe's keypoint of each point (device), and the sizes' pinned host copy
+        self.counts = z((W, 4), torch.int32)
+        self.pose_slot = z((W, NV), torch.int32)
+        self.point_src = z((W, S), torch.int32)
+        self.counts_h = torch.zeros((W, 4), dtype=torch.int32).pin_memory()
+        self.sizes = None
         s2 = np.asarray(nm.tr.F0.level_sigma2, np.float32)
         self.inv_s2 = (C.c_float * len(s2))(*[float(np.float32(1.0) / x) for x in s2])
         self.nlevels = len(s2)
@@ -582,11 +597,29 @@ class RingLBA:
         from .exchange import _bind
 
         nm = self.nm
-        check(_bind().mam_ring_lba_windows(nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.n_fixed, nm.keys.data_ptr(), nm.cnt.data_ptr(),
-                 nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2, self.nlevels,
-                 self.d_wins.data_ptr(), stream.cuda_stream), "mam_ring_lba_windows")
+        if self.rule == "covisibility":
+            check(_bind().mam_ring_lba_windows_covis(
+                nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.COVIS_TH, nm.keys.data_ptr(), nm.cnt.data_ptr(),
+                nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2, self.nlevels,
+                self.d_wins.data_ptr(), self.counts.data_ptr(), self.pose_slot.data_ptr(), self.point_src.data_ptr(),
+                stream.cuda_stream), "mam_ring_lba_windows_covis")
+        else:
+            check(_bind().mam_ring_lba_windows(nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.n_fixed, nm.keys.data_ptr(), nm.cnt.data_ptr(),
+                     nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2, self.nlevels,
+                     self.d_wins.data_ptr(), stream.cuda_stream), "mam_ring_lba_windows")
 
     def solve(self, stream):
+        if self.rule == "covisibility":
+            # the compacted sizes: one small read-back (the problem descriptors are host structs)
+            import torch
+
+            with torch.cuda.stream(stream):
+                self.counts_h.copy_(self.counts, non_blocking=True)
+            stream.synchronize()
+            self.sizes = self.counts_h.numpy().copy()
+            for w in range(self.nm.W):
+                P = self.c_probs[w]
+                P.n_poses, P.n_points, P.n_edges, P.n_opt_poses = (int(v) for v in self.sizes[w])
         rc = self.solver._L.mam_lba_solve_batch_device(self.solver._ctx, self.nm.W, C.byref(self.c_probs),
                                                        C.byref(self.c_res), C.c_void_p(stream.cuda_stream))
         if rc != 0:
@@ -594,21 +627,27 @@ class RingLBA:
         self.stats = [(int(r.iterations), int(r.lm_trials), int(r.status)) for r in self.c_res]
         return self.stats
 
+    def _size(self, w: int):
+        P = self.c_probs[w]
+        return int(P.n_poses), int(P.n_points), int(P.n_edges)
+
     def window(self, w: int):
-        """Host LBAProblem of window w as assembled (ids = array order)."""
+        """Host LBAProblem of window w as assembled (ids = array order; the compacted prefix of the buffers)."""
         from .lba import HUBER_MONO, LBAProblem
 
         b = {k: v.cpu().numpy() for k, v in self.bufs[w].items()}
-        S = self.nm.S
-        return LBAProblem(pose_id=np.arange(self.NV, dtype=np.int64), pose_fixed=b["pose_fixed"], pose_q=b["pose_q"],
-                          pose_t=b["pose_t"], point_id=np.arange(S, dtype=np.int64) + self.NV,
-                          point_xyz=b["point_xyz"], edge_point=b["edge_point"], edge_pose=b["edge_pose"],
-                          edge_obs=b["edge_obs"], edge_inv_sigma2=b["edge_inv_sigma2"],
+        P, L, E = self._size(w)
+        act = b["edge_active"][:E] if self.rule == "sequence" else None
+        return LBAProblem(pose_id=np.arange(P, dtype=np.int64), pose_fixed=b["pose_fixed"][:P], pose_q=b["pose_q"][:P],
+                          pose_t=b["pose_t"][:P], point_id=np.arange(L, dtype=np.int64) + P,
+                          point_xyz=b["point_xyz"][:L], edge_point=b["edge_point"][:E], edge_pose=b["edge_pose"][:E],
+                          edge_obs=b["edge_obs"][:E], edge_inv_sigma2=b["edge_inv_sigma2"][:E],
                           cams=self.cams.cpu().numpy(), huber_delta=HUBER_MONO, iterations=int(self.c_probs[w].iterations),
-                          edge_active=b["edge_active"], cam_model=int(self.c_probs[w].cam_model)).contiguous()
+                          edge_active=act, cam_model=int(self.c_probs[w].cam_model)).contiguous()
 
     def result(self, w: int):
         b = self.bufs[w]
         r = self.c_res[w]
-        return (b["out_q"].cpu().numpy(), b["out_t"].cpu().numpy(), b["out_xyz"].cpu().numpy(), int(r.iterations),
-                int(r.lm_trials), int(r.status), float(r.initial_chi2), float(r.final_chi2))
+        P, L, _ = self._size(w)
+        return (b["out_q"].cpu().numpy()[:P], b["out_t"].cpu().numpy()[:P], b["out_xyz"].cpu().numpy()[:L],
+                int(r.iterations), int(r.lm_trials), int(r.status), float(r.initial_chi2), float(r.final_chi2))

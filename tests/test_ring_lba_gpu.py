@@ -15,6 +15,99 @@ def _rel(a, b):
     return float((num / den).max()) if len(a) else 0.0
 
 
+def _ring(cfg, B, W):
+    import torch
+
+    import bench
+    from mam3slam_amd.mapping import NewMapPointsLeg
+
+    dev = torch.device("cuda", 0)
+    tr = bench.TrackingLeg(dict(bench.CONFIGS[cfg]), B, 1, 0, dev)
+    nm = NewMapPointsLeg(tr, W, dev)
+    for step in range(nm.R // nm.W + 2):   # the ring past one turn: every neighbour a tracked keyframe
+        tr.step()
+        nm.ingest(step)
+        nm.launch(nm.pending)
+    return tr, nm
+
+
+@pytest.mark.parametrize("cfg,B,W", [("c1", 16, 2), ("c3", 2, 2)])
+def test_ring_windows_covisibility_rule(gpu_lib, oracle, cfg, B, W):
+    """The reference's window rule (Optimizer.cc:1118-1186) on the ring, compacted: local keyframes = the new keyframe
+    + the neighbours sharing >= 15 of its MapPoints (the heaviest when none does), fixed = the other neighbours that
+    observe one, points = its MapPoints seen by >= 2 keyframes, edges = their real observations — every array, the
+    sizes and the slot / keypoint maps byte-exact against a host restatement from the ring buffers; the solve against
+    the oracle on the assembled graph (identical Levenberg control flow, 1e-4)."""
+    import torch
+
+    from mam3slam_amd.mapping import RingLBA
+    from mam3slam_amd.match import FUSE_MP_DTYPE
+    from mam3slam_amd.orb import KP_DTYPE
+
+    tr, nm = _ring(cfg, B, W)
+    rl = RingLBA(nm)
+    rl.assemble(nm.stream)
+    rl.solve(nm.stream)
+    torch.cuda.synchronize()
+    S, NN = nm.S, nm.NN
+    keys = nm.keys.cpu().numpy().view(KP_DTYPE).reshape(nm.R, S)
+    cnt = nm.cnt.cpu().numpy()[:, 0]
+    tcw = nm.tcw.cpu().numpy().view(np.float32).reshape(nm.R, 7)
+    mps = nm.fmp.cpu().numpy().view(FUSE_MP_DTYPE).reshape(nm.R, S)
+    match = nm.fwd_idx.cpu().numpy()
+    pairs = nm.pairs[nm.head].cpu().numpy()
+    inv_s2 = (np.float32(1.0) / np.asarray(tr.F0.level_sigma2, np.float32)).astype(np.float32)
+    pose_slot, point_src = rl.pose_slot.cpu().numpy(), rl.point_src.cpu().numpy()
+    n_local_total = 0
+    for w in range(W):
+        j = int(pairs[w * NN, 0])
+        nbs = [int(pairs[w * NN + k, 1]) for k in range(NN)]
+        n = min(int(cnt[j]), S)
+        mask = np.zeros((n, NN), bool)
+        for k in range(NN):
+            idx = match[w * NN + k, :n]
+            mask[:, k] = (idx >= 0) & (idx < min(int(cnt[nbs[k]]), S))
+        wt = mask.sum(0)
+        loc = wt >= RingLBA.COVIS_TH
+        if not loc.any() and wt.max() > 0:
+            loc[int(np.argmax(wt))] = True
+        fix = (wt > 0) & ~loc
+        views = [0] + [1 + k for k in range(NN) if loc[k]] + [1 + k for k in range(NN) if fix[k]]
+        vpose = {v: i for i, v in enumerate(views)}
+        slots = [j if v == 0 else nbs[v - 1] for v in views]
+        nopt = 1 + int(loc.sum())
+        n_local_total += nopt
+        kept = [p for p in range(n) if mask[p].any()]
+        ep, eo, obs, w2 = [], [], [], []
+        for i, p in enumerate(kept):
+            for v in [0] + [1 + k for k in range(NN) if mask[p, k]]:
+                slot = j if v == 0 else nbs[v - 1]
+                kp = keys[slot, p if v == 0 else int(match[w * NN + v - 1, p])]
+                ep.append(i)
+                eo.append(vpose[v])
+                obs.append((kp["x"], kp["y"]))
+                w2.append(inv_s2[kp["octave"]])
+        assert tuple(rl.sizes[w]) == (len(views), len(kept), len(ep), nopt)
+        assert np.array_equal(pose_slot[w, :len(views)], slots)
+        assert np.array_equal(point_src[w, :len(kept)], kept)
+        prob = rl.window(w)
+        assert np.array_equal(prob.pose_q, tcw[slots, :4].astype(np.float64))
+        assert np.array_equal(prob.pose_t, tcw[slots, 4:7].astype(np.float64))
+        assert np.array_equal(prob.pose_fixed, (np.arange(len(views)) >= nopt).astype(np.uint8))
+        assert np.array_equal(prob.point_xyz, mps[j, kept]["pos"].astype(np.float64))
+        assert np.array_equal(prob.edge_point, ep) and np.array_equal(prob.edge_pose, eo)
+        assert np.array_equal(prob.edge_obs, np.array(obs, np.float64).reshape(-1, 2))
+        assert np.array_equal(prob.edge_inv_sigma2, np.array(w2, np.float64))
+        assert len(ep) > 3 * len(kept), (len(ep), len(kept))   # a multi-view graph
+        q, t, x, its, trials, st, ic, fc = rl.result(w)
+        ro = oracle.lba_solve(prob)
+        assert st == 0 and ro.status == 0
+        assert (its, trials) == (ro.iterations, ro.lm_trials), (w, its, trials, ro.iterations, ro.lm_trials)
+        assert abs(fc - ro.final_chi2) <= 1e-6 * ro.final_chi2 and fc < ic
+        assert _rel(t, ro.pose_t) <= 1e-4 and _rel(q, ro.pose_q) <= 1e-4 and _rel(x, ro.point_xyz) <= 1e-4
+    assert n_local_total > 2 * W   # covisible neighbours were found (not only the keyframe itself)
+
+
 @pytest.mark.parametrize("cfg,B,W", [("c1", 16, 2), ("c3", 2, 2)])
 def test_ring_windows_match_oracle(gpu_lib, oracle, cfg, B, W):
     import torch
@@ -31,7 +124,7 @@ def test_ring_windows_match_oracle(gpu_lib, oracle, cfg, B, W):
         tr.step()
         nm.ingest(step)
         nm.launch(nm.pending)
-    rl = RingLBA(nm)
+    rl = RingLBA(nm, rule="sequence")
     rl.assemble(nm.stream)
     rl.solve(nm.stream)
     torch.cuda.synchronize()
