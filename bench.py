@@ -894,6 +894,9 @@ def main():
     ap.add_argument("--no-pose", action="store_true", help="skip the PoseOptimization section")
     ap.add_argument("--no-sin", action="store_true", help="skip the SearchInNeighbors section")
     ap.add_argument("--no-overlap", action="store_true", help="skip timing each leg alone")
+    ap.add_argument("--lm-windows", default="ring", choices=("ring", "world"),
+                    help="the timed LocalMapping leg's LBA windows: ring = the keyframes the step tracked (RingMappingLeg, "
+                         "the reference's window rule), world = the synthetic shared map's windows (LocalMappingLeg)")
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--profile-timed", action="store_true",
                     help="record LocalMapping's stage events inside the timed region (default: a second pass)")
@@ -950,11 +953,14 @@ def main():
     tr = TrackingLeg(cfg, B, NL, rank, dev)
     mapping = newmp = None
     if cfg["lba"]:
-        from mam3slam_amd.mapping import LocalMappingLeg, NewMapPointsLeg
+        from mam3slam_amd.mapping import LocalMappingLeg, NewMapPointsLeg, RingMappingLeg
 
-        mapping = LocalMappingLeg(max(1, B // K), rank, world, dev, camera=tr.cam if cfg.get("camera") else None,
-                                  width=tr.W, height=tr.H)
         newmp = NewMapPointsLeg(tr, max(1, B // K), dev)
+        if args.lm_windows == "ring":
+            mapping = RingMappingLeg(newmp, rank, world, dev)
+        else:
+            mapping = LocalMappingLeg(max(1, B // K), rank, world, dev, camera=tr.cam if cfg.get("camera") else None,
+                                      width=tr.W, height=tr.H)
 
     lba_ev = []   # (start, end) events of each LocalMapping run on its stream
 
@@ -967,7 +973,7 @@ def main():
         t_m = time.perf_counter()
         e0.record(mapping.stream)
         newmp.wait(mapping.stream, head)
-        mapping.run(step_idx)
+        mapping.run(step_idx, head=head)
         e1.record(mapping.stream)
         lba_ev.append((e0, e1))
         host_s["mapping_run"] += time.perf_counter() - t_m
@@ -1195,10 +1201,20 @@ def main():
             workload += (f" + a keyframe every {K} frames per stream: {mapping.W} new keyframes per "
                          f"{'step' if map_every == 1 else f'{map_every} steps'}, each with "
                          f"ComputeBoW + 30 SearchForTriangulation (CreateNewMapPoints) + SearchInNeighbors (Fuse both ways + "
-                         f"ComputeDistinctiveDescriptors) and a LocalBundleAdjustment window "
-                         f"(50 KF + fixed, ~{int(np.mean([len(p.point_id) for p in mapping.probs]))} MapPoints) "
-                         f"over the shared map, batched, concurrent with tracking; write-backs exchanged and "
-                         f"applied to the map the next windows read")
+                         f"ComputeDistinctiveDescriptors) and ")
+            if args.lm_windows == "ring":
+                sz = mapping.rl.sizes
+                workload += (f"a LocalBundleAdjustment window of the keyframe by the reference's window rule over "
+                             f"the keyframes the step tracked (covisible: ~{float(np.mean(sz[:, 3])):.1f} optimised "
+                             f"KF + {float(np.mean(sz[:, 0] - sz[:, 3])):.1f} fixed, ~{int(np.mean(sz[:, 1]))} "
+                             f"MapPoints, ~{int(np.mean(sz[:, 2]))} observations), batched, concurrent with "
+                             f"tracking; write-backs exchanged (all-gather) and applied to the shared map every GPU "
+                             f"holds")
+            else:
+                workload += (f"a LocalBundleAdjustment window (50 KF + fixed, "
+                             f"~{int(np.mean([len(p.point_id) for p in mapping.probs]))} MapPoints) of the synthetic "
+                             f"shared map, batched, concurrent with tracking; write-backs exchanged and applied to "
+                             f"the map the next windows read")
         out = {
             "metric": "tracked frames/sec (ORB extract+match+localBA) at 1/2/4/8 GPUs vs CPU ref",
             "value": frames_total / T,

@@ -139,12 +139,14 @@ int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn, int n_fixe
                          int nlevels, const mam_ring_window* outs, void* stream);
 
 /* The same windows by the reference's window rule (Optimizer.cc:1118-1186), compacted: local keyframes = the new
- * keyframe + its covisible ring neighbours (weight = shared MapPoints >= covis_th, KeyFrame::UpdateConnections' 15;
- * the heaviest when none reaches it), fixed = every other neighbour observing one of its MapPoints; points = the new
- * keyframe's MapPoints seen by >= 2 keyframes; edges = their real observations only (edge_active, when given, all 1).
- * Per window: counts[4 w ..] = {poses, points, edges, optimised poses} (the optimised poses first), pose_slot[w (nn + 1)
- * + i] = ring slot of pose i, point_src[w S + i] = the new keyframe's keypoint of point i. nn <= 31. */
-int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, int nn, int covis_th, const void* keys,
+ * keyframe + its covisible ring neighbours by weight (weight = shared MapPoints >= covis_th, KeyFrame::UpdateConnections'
+ * 15; the heaviest when none reaches it), fixed = every other neighbour observing one of its MapPoints — and when that
+ * leaves none fixed (where the reference skips the LBA, Optimizer.cc:1179-1183), the n_fixed least covisible local
+ * ones; points = the new keyframe's MapPoints seen by >= 2 keyframes; edges = their real observations only
+ * (edge_active, when given, all 1). Per window: counts[4 w ..] = {poses, points, edges, optimised poses} (the
+ * optimised poses first), pose_slot[w (nn + 1) + i] = ring slot of pose i, point_src[w S + i] = the new keyframe's
+ * keypoint of point i. nn <= 31. */
+int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, int nn, int covis_th, int n_fixed, const void* keys,
                                const int32_t* cnt, const void* tcw, const void* mps, int S, const int32_t* match,
                                const float* inv_level_sigma2, int nlevels, const mam_ring_window* outs, int32_t* counts,
                                int32_t* pose_slot, int32_t* point_src, void* stream);

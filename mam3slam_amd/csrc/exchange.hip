@@ -281,7 +281,7 @@ __global__ __launch_bounds__(64) void k_ring_windows(const RingArgs a) {
 // MapPoints >= 15, or the heaviest one when none reaches it, KeyFrame.cc:312-380), the local MapPoints those the new
 // keyframe observes (the ring's MapPoints are the new keyframe's; a point seen by fewer than two keyframes is left
 // out, as the fixed-shape form did), the fixed keyframes every other keyframe observing a local MapPoint. Poses: the
-// new keyframe, its covisible keyframes in neighbour order, then the fixed ones; points in keypoint order; edges
+// new keyframe, its covisible keyframes by weight, then the fixed ones; points in keypoint order; edges
 // point-major (the new keyframe's observation first, then the neighbours' in neighbour order) — only real
 // observations, no inactive slots. counts[w] = {poses, points, edges, optimised poses}; pose_slot[w][i] the ring slot
 // of pose i, point_src[w][i] the keypoint (MapPoint row of the new keyframe) of point i.
@@ -309,8 +309,9 @@ __device__ __forceinline__ int ringc_excl_scan(int v, int* wsum, int& total) {
     return pre + x - v;
 }
 
-__global__ __launch_bounds__(RINGC_T) void k_ring_windows_covis(const RingArgs a, int covis_th, int32_t* counts,
-                                                                int32_t* pose_slot, int32_t* point_src) {
+__global__ __launch_bounds__(RINGC_T) void k_ring_windows_covis(const RingArgs a, int covis_th, int n_fixed,
+                                                                int32_t* counts, int32_t* pose_slot,
+                                                                int32_t* point_src) {
     extern __shared__ __attribute__((aligned(16))) uint32_t obsm[];   // [S]: bit k = observed by neighbour k
     __shared__ int wt[32], vpose[33], wsum[RINGC_T / 64], carry[2], hdr[4];
     const int w = blockIdx.x, t = threadIdx.x, nn = a.nn, S = a.S;
@@ -336,24 +337,29 @@ __global__ __launch_bounds__(RINGC_T) void k_ring_windows_covis(const RingArgs a
         }
     }
     __syncthreads();
-    // the window's keyframes (thread 0: 30 neighbours)
+    // the window's keyframes (thread 0, <= 31 neighbours): the neighbours by covisibility weight, heaviest first (ties
+    // by neighbour order: GetVectorCovisibleKeyFrames' order), the covisible ones (>= covis_th, or the heaviest when none
+    // reaches it) local, the other observers fixed; with no fixed keyframe left the reference skips the LBA
+    // (Optimizer.cc:1179-1183) — here the n_fixed least covisible local ones are fixed instead, the gauge anchor the
+    // fixed cameras are
     if (t == 0) {
-        int best = -1, bw = 0, nloc = 0;
+        int ord[32];
+        int no = 0;
         for (int k = 0; k < nn; k++) {
-            if (wt[k] >= covis_th) nloc++;
-            if (wt[k] > bw) { bw = wt[k]; best = k; }
+            if (wt[k] <= 0) continue;
+            int i = no++;
+            while (i > 0 && wt[ord[i - 1]] < wt[k]) { ord[i] = ord[i - 1]; i--; }
+            ord[i] = k;
         }
-        int np = 1;
+        int nloc = 0;
+        while (nloc < no && wt[ord[nloc]] >= covis_th) nloc++;
+        if (nloc == 0 && no > 0) nloc = 1;
+        if (nloc == no) nloc = max(no - n_fixed, min(no, 1));
+        for (int k = 0; k <= nn; k++) vpose[k] = -1;
         vpose[0] = 0;
-        for (int k = 0; k < nn; k++) {
-            const bool loc = nloc > 0 ? wt[k] >= covis_th : k == best;
-            vpose[1 + k] = loc ? np++ : -1;
-        }
-        const int nopt = np;
-        for (int k = 0; k < nn; k++)
-            if (vpose[1 + k] < 0 && wt[k] > 0) vpose[1 + k] = np++;
-        hdr[0] = np;
-        hdr[1] = nopt;
+        for (int i = 0; i < no; i++) vpose[1 + ord[i]] = 1 + i;
+        hdr[0] = 1 + no;
+        hdr[1] = 1 + nloc;
     }
     __syncthreads();
     const int np = hdr[0], nopt = hdr[1];
@@ -439,12 +445,14 @@ extern "C" int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn,
     return MAM_OK;
 }
 
-extern "C" int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, int nn, int covis_th, const void* keys,
+extern "C" int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, int nn, int covis_th, int n_fixed,
+                                          const void* keys,
                                           const int32_t* cnt, const void* tcw, const void* mps, int S,
                                           const int32_t* match, const float* inv_level_sigma2, int nlevels,
                                           const mam_ring_window* outs, int32_t* counts, int32_t* pose_slot,
                                           int32_t* point_src, void* stream) {
-    if (n_windows < 0 || nn < 1 || nn > 31 || S < 1 || nlevels < 1 || nlevels > 8 || !pairs || !keys || !cnt || !tcw ||
+    if (n_windows < 0 || nn < 1 || nn > 31 || n_fixed < 0 || S < 1 || nlevels < 1 || nlevels > 8 || !pairs || !keys ||
+        !cnt || !tcw ||
         !mps || !match || !inv_level_sigma2 || (n_windows > 0 && (!outs || !counts || !pose_slot || !point_src)))
         return MAM_ERR_ARG;
     if ((size_t)S * 4 > 64 * 1024) return MAM_ERR_CAPACITY;
@@ -463,7 +471,7 @@ extern "C" int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, i
     for (int l = 0; l < nlevels; l++) a.inv_s2[l] = inv_level_sigma2[l];
     a.outs = outs;
     hipLaunchKernelGGL(mam::k_ring_windows_covis, dim3(n_windows), dim3(mam::RINGC_T), (size_t)S * 4,
-                       (hipStream_t)stream, a, covis_th, counts, pose_slot, point_src);
+                       (hipStream_t)stream, a, covis_th, n_fixed, counts, pose_slot, point_src);
     MAM_HIP(hipGetLastError());
     return MAM_OK;
 }

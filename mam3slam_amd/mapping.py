@@ -142,8 +142,8 @@ class LocalMappingLeg:
                     1_000_003 * (step + 1) + 7919 * self.rank, 0.004, 0.012, 0.017, self.status.data_ptr(),
                     stream=torch.cuda.current_stream(self.dev).cuda_stream)
 
-    def run(self, step: int, new_keyframes: bool = True):
-        """One LocalMapping step: the solves are synchronous (mam_lba_solve_batch_device returns with the Levenberg
+    def run(self, step: int, head=None, new_keyframes: bool = True):
+        """One LocalMapping step (head: unused, the ring leg's argument): the solves are synchronous (mam_lba_solve_batch_device returns with the Levenberg
         state read back), the pack / all-gather / apply are queued: on return the map tables are final for work
         ordered after self.stream (a consumer on another stream waits on it)."""
         import time
@@ -277,6 +277,7 @@ class NewMapPointsLeg:
             for ev in self.ready.values():
                 ev.record(tr.tstream)
         self.pending = None
+        self.ring = None   # a RingMappingLeg assembling each run's LocalBundleAdjustment windows
 
     def ingest(self, step: int):
         """Copy step `step`'s new keyframes (frames f = step mod K + i K) into the ring at the next head; on the
@@ -353,6 +354,8 @@ class NewMapPointsLeg:
         self.matcher.search_for_triangulation_batch_device(self.tr.F0, self.tr.cam, b, self.out.data_ptr(),
                                                            self.nmatch.data_ptr(), False, stream=s)
         self.search_in_neighbors(stream, h)
+        if self.ring is not None:   # the LocalBundleAdjustment windows of these keyframes (RingMappingLeg)
+            self.ring.assemble(stream, h)
 
     # ------------------------------------------------------------------------------------------ SearchInNeighbors
     NB_BACK = 4   # neighbours whose MapPoints form a keyframe's fuse candidates
@@ -527,15 +530,18 @@ class RingLBA:
     per new keyframe of the last run, its window solved with the batch device API (mam_lba_solve_batch_device).
 
     rule "covisibility" (the reference's window rule, mam_ring_lba_windows_covis): the new keyframe and its covisible
-    ring neighbours (weight = its MapPoints a neighbour observes, from the run's forward Fuse matches: >= 15 as
-    KeyFrame::UpdateConnections keeps them, the heaviest when none reaches it) optimised, every other neighbour
+    ring neighbours by weight (weight = its MapPoints a neighbour observes, from the run's forward Fuse matches: >= 15
+    as KeyFrame::UpdateConnections keeps them, the heaviest when none reaches it) optimised, every other neighbour
     observing one of its MapPoints fixed; the problem compacted to the real observations (sizes read back once per
-    batch). rule "sequence" (mam_ring_lba_windows): the NN neighbours nearest in sequence, the last n_fixed of them
+    batch). The ring's searched neighbours are the new keyframe's 30 nearest in its sequence, all of them covisible in
+    the synthetic scene, so the reference's rule would leave no fixed keyframe (it then skips the LBA,
+    Optimizer.cc:1179-1183): the n_fixed least covisible neighbours are fixed instead, as the gauge anchor. rule "sequence" (mam_ring_lba_windows): the NN neighbours nearest in sequence, the last n_fixed of them
     fixed, a fixed S x (NN + 1) edge-slot shape with unobserved slots inactive."""
 
     COVIS_TH = 15
 
-    def __init__(self, nm, n_fixed: int = 10, iterations: int = 10, solver=None, rule: str = "covisibility"):
+    def __init__(self, nm, n_fixed: int = 10, iterations: int = 10, solver=None, rule: str = "covisibility",
+                 sets: int = 1):
         import torch
 
         from .lba import HUBER_MONO
@@ -547,85 +553,122 @@ class RingLBA:
         self.NV, self.n_fixed = NN + 1, int(n_fixed)
         NV, E = self.NV, S * (NN + 1)
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=self.dev)  # noqa: E731
-        self.bufs = []
-        wins = (RingWindow * W)()
-        self.c_probs = (_Problem * W)()
-        self.c_res = (_Result * W)()
         cam = nm.tr.cam
         self.cams = torch.from_numpy(np.ascontiguousarray(cam.params(), np.float32)[None]).to(self.dev)
-        for w in range(W):
-            b = dict(pose_q=z((NV, 4), torch.float64), pose_t=z((NV, 3), torch.float64), pose_fixed=z(NV, torch.uint8),
-                     point_xyz=z((S, 3), torch.float64), edge_point=z(E, torch.int32), edge_pose=z(E, torch.int32),
-                     edge_obs=z((E, 2), torch.float64), edge_inv_sigma2=z(E, torch.float64),
-                     edge_active=z(E, torch.uint8), out_q=z((NV, 4), torch.float64), out_t=z((NV, 3), torch.float64),
-                     out_xyz=z((S, 3), torch.float64), out_chi2=z(E, torch.float64), out_depth=z(E, torch.uint8))
-            self.bufs.append(b)
-            for f in RingWindow._fields_:
-                setattr(wins[w], f[0], b[f[0]].data_ptr())
-            P = self.c_probs[w]
-            P.n_poses, P.n_points, P.n_edges, P.n_cams = NV, S, E, 1
-            P.pose_id = P.point_id = P.pose_cam = None
-            P.pose_fixed, P.pose_q, P.pose_t = b["pose_fixed"].data_ptr(), b["pose_q"].data_ptr(), b["pose_t"].data_ptr()
-            P.point_xyz = b["point_xyz"].data_ptr()
-            P.edge_point, P.edge_pose = b["edge_point"].data_ptr(), b["edge_pose"].data_ptr()
-            P.edge_obs, P.edge_inv_sigma2 = b["edge_obs"].data_ptr(), b["edge_inv_sigma2"].data_ptr()
-            P.edge_active = b["edge_active"].data_ptr() if rule == "sequence" else None
-            P.cams = self.cams.data_ptr()
-            P.huber_delta, P.iterations = HUBER_MONO, int(iterations)
-            P.cam_model = 1 if cam.is_kb8 else 0
-            P.n_opt_poses = NV - self.n_fixed
-            R = self.c_res[w]
-            R.pose_q, R.pose_t, R.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
-            R.edge_chi2, R.edge_depth_ok = b["out_chi2"].data_ptr(), b["out_depth"].data_ptr()
-        self.d_wins = torch.from_numpy(np.frombuffer(bytes(wins), np.uint8).copy()).to(self.dev)
-        # covisibility windows: per window {poses, points, edges, optimised poses}, the ring slot of each pose, the new
-        # keyframe's keypoint of each point (device), and the sizes' pinned host copy
-        self.counts = z((W, 4), torch.int32)
-        self.pose_slot = z((W, NV), torch.int32)
-        self.point_src = z((W, S), torch.int32)
-        self.counts_h = torch.zeros((W, 4), dtype=torch.int32).pin_memory()
-        self.sizes = None
+        # `sets` buffer sets (a window batch each: a set assembled while an earlier one is solved)
+        self.sets = []
+        for _ in range(max(1, int(sets))):
+            bufs = []
+            wins = (RingWindow * W)()
+            c_probs = (_Problem * W)()
+            c_res = (_Result * W)()
+            for w in range(W):
+                b = dict(pose_q=z((NV, 4), torch.float64), pose_t=z((NV, 3), torch.float64),
+                         pose_fixed=z(NV, torch.uint8), point_xyz=z((S, 3), torch.float64),
+                         edge_point=z(E, torch.int32), edge_pose=z(E, torch.int32), edge_obs=z((E, 2), torch.float64),
+                         edge_inv_sigma2=z(E, torch.float64), edge_active=z(E, torch.uint8),
+                         out_q=z((NV, 4), torch.float64), out_t=z((NV, 3), torch.float64),
+                         out_xyz=z((S, 3), torch.float64), out_chi2=z(E, torch.float64), out_depth=z(E, torch.uint8))
+                bufs.append(b)
+                for f in RingWindow._fields_:
+                    setattr(wins[w], f[0], b[f[0]].data_ptr())
+                P = c_probs[w]
+                P.n_poses, P.n_points, P.n_edges, P.n_cams = NV, S, E, 1
+                P.pose_id = P.point_id = P.pose_cam = None
+                P.pose_fixed, P.pose_q, P.pose_t = b["pose_fixed"].data_ptr(), b["pose_q"].data_ptr(), b["pose_t"].data_ptr()
+                P.point_xyz = b["point_xyz"].data_ptr()
+                P.edge_point, P.edge_pose = b["edge_point"].data_ptr(), b["edge_pose"].data_ptr()
+                P.edge_obs, P.edge_inv_sigma2 = b["edge_obs"].data_ptr(), b["edge_inv_sigma2"].data_ptr()
+                P.edge_active = b["edge_active"].data_ptr() if rule == "sequence" else None
+                P.cams = self.cams.data_ptr()
+                P.huber_delta, P.iterations = HUBER_MONO, int(iterations)
+                P.cam_model = 1 if cam.is_kb8 else 0
+                P.n_opt_poses = NV - self.n_fixed
+                R = c_res[w]
+                R.pose_q, R.pose_t, R.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
+                R.edge_chi2, R.edge_depth_ok = b["out_chi2"].data_ptr(), b["out_depth"].data_ptr()
+            st = dict(bufs=bufs, c_probs=c_probs, c_res=c_res,
+                      d_wins=torch.from_numpy(np.frombuffer(bytes(wins), np.uint8).copy()).to(self.dev),
+                      # covisibility windows: per window {poses, points, edges, optimised poses}, the ring slot of
+                      # each pose, the new keyframe's keypoint of each point (device), and the host copy of the first two
+                      counts=z((W, 4), torch.int32), pose_slot=z((W, NV), torch.int32), point_src=z((W, S), torch.int32),
+                      meta_h=torch.zeros((W, 4 + NV), dtype=torch.int32).pin_memory(), sizes=None, slots=None,
+                      stats=None)
+            self.sets.append(st)
+        self.cur = 0   # the set window() / result() / stats describe: the last solved
         s2 = np.asarray(nm.tr.F0.level_sigma2, np.float32)
         self.inv_s2 = (C.c_float * len(s2))(*[float(np.float32(1.0) / x) for x in s2])
         self.nlevels = len(s2)
         self.solver = solver or LBASolver(device=self.dev.index or 0)
-        self.stats = None
 
-    def assemble(self, stream):
+    # the last solved set's views (what ring_lba_section and the tests read)
+    @property
+    def bufs(self):
+        return self.sets[self.cur]["bufs"]
+
+    @property
+    def c_probs(self):
+        return self.sets[self.cur]["c_probs"]
+
+    @property
+    def c_res(self):
+        return self.sets[self.cur]["c_res"]
+
+    @property
+    def sizes(self):
+        return self.sets[self.cur]["sizes"]
+
+    @property
+    def stats(self):
+        return self.sets[self.cur]["stats"]
+
+    @property
+    def pose_slot(self):
+        return self.sets[self.cur]["pose_slot"]
+
+    @property
+    def point_src(self):
+        return self.sets[self.cur]["point_src"]
+
+    def assemble(self, stream, set_index: int = 0):
         """The windows of the keyframes of the leg's last run (after its search_in_neighbors on `stream`)."""
         from ._lib import check
         from .exchange import _bind
 
-        nm = self.nm
+        nm, st = self.nm, self.sets[set_index]
         if self.rule == "covisibility":
             check(_bind().mam_ring_lba_windows_covis(
-                nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.COVIS_TH, nm.keys.data_ptr(), nm.cnt.data_ptr(),
-                nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2, self.nlevels,
-                self.d_wins.data_ptr(), self.counts.data_ptr(), self.pose_slot.data_ptr(), self.point_src.data_ptr(),
-                stream.cuda_stream), "mam_ring_lba_windows_covis")
+                nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.COVIS_TH, self.n_fixed, nm.keys.data_ptr(),
+                nm.cnt.data_ptr(), nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2,
+                self.nlevels, st["d_wins"].data_ptr(), st["counts"].data_ptr(), st["pose_slot"].data_ptr(),
+                st["point_src"].data_ptr(), stream.cuda_stream), "mam_ring_lba_windows_covis")
         else:
             check(_bind().mam_ring_lba_windows(nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.n_fixed, nm.keys.data_ptr(), nm.cnt.data_ptr(),
                      nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2, self.nlevels,
-                     self.d_wins.data_ptr(), stream.cuda_stream), "mam_ring_lba_windows")
+                     st["d_wins"].data_ptr(), stream.cuda_stream), "mam_ring_lba_windows")
 
-    def solve(self, stream):
+    def solve(self, stream, set_index: int = 0):
+        import torch
+
+        st = self.sets[set_index]
         if self.rule == "covisibility":
-            # the compacted sizes: one small read-back (the problem descriptors are host structs)
-            import torch
-
+            # the compacted sizes and the pose slots: one small read-back (the problem descriptors are host structs)
             with torch.cuda.stream(stream):
-                self.counts_h.copy_(self.counts, non_blocking=True)
+                st["meta_h"][:, :4].copy_(st["counts"], non_blocking=True)
+                st["meta_h"][:, 4:].copy_(st["pose_slot"], non_blocking=True)
             stream.synchronize()
-            self.sizes = self.counts_h.numpy().copy()
+            meta = st["meta_h"].numpy()
+            st["sizes"], st["slots"] = meta[:, :4].copy(), meta[:, 4:].copy()
             for w in range(self.nm.W):
-                P = self.c_probs[w]
-                P.n_poses, P.n_points, P.n_edges, P.n_opt_poses = (int(v) for v in self.sizes[w])
-        rc = self.solver._L.mam_lba_solve_batch_device(self.solver._ctx, self.nm.W, C.byref(self.c_probs),
-                                                       C.byref(self.c_res), C.c_void_p(stream.cuda_stream))
+                P = st["c_probs"][w]
+                P.n_poses, P.n_points, P.n_edges, P.n_opt_poses = (int(v) for v in st["sizes"][w])
+        rc = self.solver._L.mam_lba_solve_batch_device(self.solver._ctx, self.nm.W, C.byref(st["c_probs"]),
+                                                       C.byref(st["c_res"]), C.c_void_p(stream.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"mam_lba_solve_batch_device: {rc}")
-        self.stats = [(int(r.iterations), int(r.lm_trials), int(r.status)) for r in self.c_res]
-        return self.stats
+        st["stats"] = [(int(r.iterations), int(r.lm_trials), int(r.status)) for r in st["c_res"]]
+        self.cur = set_index
+        return st["stats"]
 
     def _size(self, w: int):
         P = self.c_probs[w]
@@ -651,3 +694,145 @@ class RingLBA:
         P, L, _ = self._size(w)
         return (b["out_q"].cpu().numpy()[:P], b["out_t"].cpu().numpy()[:P], b["out_xyz"].cpu().numpy()[:L],
                 int(r.iterations), int(r.lm_trials), int(r.status), float(r.initial_chi2), float(r.final_chi2))
+
+
+class RingMappingLeg:
+    """The LocalMapping leg over the keyframes Tracking inserted: per step, the LocalBundleAdjustment windows of the
+    keyframes whose searches the NewMapPointsLeg ran (RingLBA, the reference's window rule, assembled on the
+    NewMapPointsLeg's stream right after those searches, one buffer set per ring head), solved together
+    (mam_lba_solve_batch_device), and their write-back (Optimizer.cc:1463-1497) exchanged: every optimised KeyFrame
+    once (the last window optimising it) and every window's MapPoints as 32-byte / 16-byte records
+    (mam_exchange_pack_sources), one all-gather across GPUs, applied in rank order to the shared map every GPU holds
+    (rows: rank x ring slot for KeyFrames, (rank x ring slot) x S + keypoint for MapPoints).
+
+    The interface of LocalMappingLeg (bench.py reads the same fields)."""
+
+    def __init__(self, nm, rank: int, world_size: int, device, iterations: int = 10, stream=None):
+        import torch
+        import torch.distributed as dist
+
+        from .exchange import CompactExchange, MapWindow
+
+        self.nm, self.dev = nm, device
+        self.W, self.rank, self.world_size = nm.W, rank, world_size
+        self.nheads = nm.R // nm.W
+        self.rl = RingLBA(nm, iterations=iterations, sets=self.nheads)
+        nm.ring = self   # the NewMapPointsLeg assembles each run's windows right after its searches
+        self.solver = self.rl.solver
+        self.stream = stream if stream is not None else torch.cuda.Stream(device, priority=-1)
+        self.status = torch.zeros(1, dtype=torch.int32, device=device)
+        NV, S, R = self.rl.NV, nm.S, nm.R
+        # the shared map every GPU holds: KeyFrame rows [q xyzw, t, valid], MapPoint rows [xyz, bad]
+        self.kf_rows, self.mp_rows = world_size * R, world_size * R * S
+        self.kf_table = torch.zeros((self.kf_rows, 8), dtype=torch.float32, device=device)
+        self.mp_table = torch.zeros((self.mp_rows, 4), dtype=torch.float32, device=device)
+        kf_cap, mp_cap = self.W * NV, self.W * S   # the same on every rank (same W, NN, S)
+        self.exch = CompactExchange(kf_cap, mp_cap, device=device)
+        # per buffer set: the windows' global vertex ids (device, computed per step) and the pack descriptors
+        self.pose_gid = [torch.zeros((self.W, NV), dtype=torch.int64, device=device) for _ in range(self.nheads)]
+        self.point_gid = [torch.zeros((self.W, S), dtype=torch.int64, device=device) for _ in range(self.nheads)]
+        self.d_pack = []
+        for k, st in enumerate(self.rl.sets):
+            pk = (MapWindow * self.W)()
+            for w in range(self.W):
+                b = st["bufs"][w]
+                d = pk[w]
+                d.n_poses, d.n_points = NV, S
+                d.pose_id, d.pose_fixed = self.pose_gid[k][w].data_ptr(), b["pose_fixed"].data_ptr()
+                d.point_id, d.point_bad = self.point_gid[k][w].data_ptr(), None
+                d.pose_q, d.pose_t, d.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
+            self.d_pack.append(torch.from_numpy(np.frombuffer(bytes(pk), np.uint8).copy()).to(device))
+        self.src_h = torch.zeros(2 * (kf_cap + mp_cap), dtype=torch.int32).pin_memory()
+        self.src_d = torch.zeros(2 * (kf_cap + mp_cap), dtype=torch.int32, device=device)
+        self.n_kf_upd = self.n_mp_upd = 0
+        self.time_gather = False
+        self.stats = None
+        self.windows_solved = 0
+        self.host_s = {}
+        self.last = None   # the buffer set of the last solve
+        self._probs = None
+        if world_size > 1 and dist.is_available() and dist.is_initialized():
+            dist.barrier()
+
+    def assemble(self, stream, head):
+        self.rl.assemble(stream, head // self.W)
+
+    def run(self, step: int, head=None):
+        """One LocalMapping step: the windows of the keyframes at `head` (their searches and assembly ordered before
+        this on the caller's wait), solved synchronously, then the pack / all-gather / apply queued on self.stream."""
+        import time
+
+        import torch
+
+        if head is None:
+            if self.last is None:   # no keyframe run yet: nothing to solve
+                self.stats = [(0, 0, 0)] * self.W
+                return self.stats
+            head = self.last * self.W
+        k = head // self.W
+        with torch.cuda.stream(self.stream):
+            t0 = time.perf_counter()
+            s = self.stream.cuda_stream
+            t1 = time.perf_counter()
+            self.stats = self.rl.solve(self.stream, k)
+            t2 = time.perf_counter()
+            self.windows_solved += self.W
+            self.last = k
+            self._probs = None
+            st = self.rl.sets[k]
+            sizes, slots = st["sizes"], st["slots"]
+            R, S = self.nm.R, self.nm.S
+            base = self.rank * R
+            # global ids: KeyFrame row = rank R + ring slot; MapPoint row = (rank R + the new keyframe's slot) S + keypoint
+            self.pose_gid[k].copy_(st["pose_slot"].to(torch.int64) + base)
+            self.point_gid[k].copy_((st["pose_slot"][:, :1].to(torch.int64) + base) * S + st["point_src"].to(torch.int64))
+            # the write-back sources: every optimised KeyFrame once (from the last window optimising it), every
+            # window's MapPoints (a keyframe's own: no two windows share one)
+            kf = {}
+            for w in range(self.W):
+                for i in range(int(sizes[w, 3])):
+                    kf[base + int(slots[w, i])] = (w, i)
+            kf_src = np.array([kf[g] for g in sorted(kf)], np.int32).reshape(-1, 2)
+            mp_src = np.concatenate([np.stack([np.full(int(sizes[w, 1]), w), np.arange(int(sizes[w, 1]))], 1)
+                                     for w in range(self.W)]).astype(np.int32)
+            self.n_kf_upd, self.n_mp_upd = len(kf_src), len(mp_src)
+            nk = 2 * len(kf_src)
+            src = self.src_h.numpy()
+            src[:nk] = kf_src.reshape(-1)
+            src[nk:nk + 2 * len(mp_src)] = mp_src.reshape(-1)
+            n_all = nk + 2 * len(mp_src)
+            self.src_d[:n_all].copy_(self.src_h[:n_all], non_blocking=True)
+            self.exch.pack(self.d_pack[k].data_ptr(), self.W, self.src_d.data_ptr(), len(kf_src),
+                           self.src_d.data_ptr() + 4 * nk, len(mp_src), 0, stream=s)
+            self.exch.gather(timed=self.time_gather)
+            self.exch.apply(self.kf_table.data_ptr(), self.kf_rows, self.mp_table.data_ptr(), self.mp_rows,
+                            self.status.data_ptr(), stream=s)
+            t3 = time.perf_counter()
+        for key, v in (("launch", t1 - t0), ("solve", t2 - t1), ("exchange", t3 - t2)):
+            self.host_s[key] = self.host_s.get(key, 0.0) + v
+        return self.stats
+
+    @property
+    def probs(self):
+        """Host LBAProblems of the last solved windows (built on first use after a solve)."""
+        if self._probs is None:
+            self._probs = [self.rl.window(w) for w in range(self.W)]
+        return self._probs
+
+    @property
+    def edges(self):
+        return [int(v) for v in self.rl.sizes[:, 2]]
+
+    def window_inputs(self, w: int):
+        return self.rl.window(w)
+
+    def window_result(self, w: int):
+        from .lba import LBAResult
+
+        P, L, E = self.rl._size(w)
+        b = self.rl.bufs[w]
+        r = self.rl.c_res[w]
+        it, tr, st = self.stats[w]
+        return LBAResult(b["out_q"].cpu().numpy()[:P], b["out_t"].cpu().numpy()[:P], b["out_xyz"].cpu().numpy()[:L],
+                         b["out_chi2"].cpu().numpy()[:E], b["out_depth"].cpu().numpy()[:E], it, tr,
+                         float(r.initial_chi2), float(r.final_chi2), st)

@@ -34,8 +34,9 @@ def _ring(cfg, B, W):
 @pytest.mark.parametrize("cfg,B,W", [("c1", 16, 2), ("c3", 2, 2)])
 def test_ring_windows_covisibility_rule(gpu_lib, oracle, cfg, B, W):
     """The reference's window rule (Optimizer.cc:1118-1186) on the ring, compacted: local keyframes = the new keyframe
-    + the neighbours sharing >= 15 of its MapPoints (the heaviest when none does), fixed = the other neighbours that
-    observe one, points = its MapPoints seen by >= 2 keyframes, edges = their real observations — every array, the
+    + the neighbours sharing >= 15 of its MapPoints by weight (the heaviest when none does), fixed = the other
+    neighbours that observe one (the n_fixed least covisible when that leaves none fixed), points = its MapPoints seen
+    by >= 2 keyframes, edges = their real observations — every array, the
     sizes and the slot / keypoint maps byte-exact against a host restatement from the ring buffers; the solve against
     the oracle on the assembled graph (identical Levenberg control flow, 1e-4)."""
     import torch
@@ -68,14 +69,16 @@ def test_ring_windows_covisibility_rule(gpu_lib, oracle, cfg, B, W):
             idx = match[w * NN + k, :n]
             mask[:, k] = (idx >= 0) & (idx < min(int(cnt[nbs[k]]), S))
         wt = mask.sum(0)
-        loc = wt >= RingLBA.COVIS_TH
-        if not loc.any() and wt.max() > 0:
-            loc[int(np.argmax(wt))] = True
-        fix = (wt > 0) & ~loc
-        views = [0] + [1 + k for k in range(NN) if loc[k]] + [1 + k for k in range(NN) if fix[k]]
+        order = sorted((k for k in range(NN) if wt[k] > 0), key=lambda k: (-wt[k], k))   # covisibility order
+        nloc = sum(1 for k in order if wt[k] >= RingLBA.COVIS_TH)
+        if nloc == 0 and order:
+            nloc = 1
+        if nloc == len(order):   # no fixed observer: the least covisible n_fixed are the gauge anchor
+            nloc = max(len(order) - rl.n_fixed, min(len(order), 1))
+        views = [0] + [1 + k for k in order]
         vpose = {v: i for i, v in enumerate(views)}
         slots = [j if v == 0 else nbs[v - 1] for v in views]
-        nopt = 1 + int(loc.sum())
+        nopt = 1 + nloc
         n_local_total += nopt
         kept = [p for p in range(n) if mask[p].any()]
         ep, eo, obs, w2 = [], [], [], []
@@ -106,6 +109,7 @@ def test_ring_windows_covisibility_rule(gpu_lib, oracle, cfg, B, W):
         assert abs(fc - ro.final_chi2) <= 1e-6 * ro.final_chi2 and fc < ic
         assert _rel(t, ro.pose_t) <= 1e-4 and _rel(q, ro.pose_q) <= 1e-4 and _rel(x, ro.point_xyz) <= 1e-4
     assert n_local_total > 2 * W   # covisible neighbours were found (not only the keyframe itself)
+    assert all(int(v[0]) > int(v[3]) for v in rl.sizes)   # every window has fixed keyframes
 
 
 @pytest.mark.parametrize("cfg,B,W", [("c1", 16, 2), ("c3", 2, 2)])
