@@ -662,13 +662,37 @@ class RingLBA:
             for w in range(self.nm.W):
                 P = st["c_probs"][w]
                 P.n_poses, P.n_points, P.n_edges, P.n_opt_poses = (int(v) for v in st["sizes"][w])
-        rc = self.solver._L.mam_lba_solve_batch_device(self.solver._ctx, self.nm.W, C.byref(st["c_probs"]),
-                                                       C.byref(st["c_res"]), C.c_void_p(stream.cuda_stream))
-        if rc != 0:
-            raise RuntimeError(f"mam_lba_solve_batch_device: {rc}")
-        st["stats"] = [(int(r.iterations), int(r.lm_trials), int(r.status)) for r in st["c_res"]]
+            # a window with no local MapPoint observed twice, or no fixed keyframe, is not solved — the reference's
+            # LocalBundleAdjustment returns there (Optimizer.cc:1179-1183); its sizes are zeroed
+            sz = st["sizes"]
+            valid = [w for w in range(self.nm.W) if sz[w, 1] > 0 and sz[w, 2] > 0 and sz[w, 0] > sz[w, 3]]
+            for w in range(self.nm.W):
+                if w not in valid:
+                    sz[w] = 0
+                    P = st["c_probs"][w]
+                    P.n_poses = P.n_points = P.n_edges = P.n_opt_poses = 0
+        else:
+            valid = list(range(self.nm.W))
+        st["valid"] = valid
+        stats = [(0, 0, 0)] * self.nm.W
+        if valid:
+            if len(valid) == self.nm.W:
+                probs, res = st["c_probs"], st["c_res"]
+            else:
+                probs = (_Problem * len(valid))(*[st["c_probs"][w] for w in valid])
+                res = (_Result * len(valid))(*[st["c_res"][w] for w in valid])
+            rc = self.solver._L.mam_lba_solve_batch_device(self.solver._ctx, len(valid), C.byref(probs),
+                                                           C.byref(res), C.c_void_p(stream.cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"mam_lba_solve_batch_device: {rc}")
+            for i, w in enumerate(valid):
+                if res is not st["c_res"]:
+                    st["c_res"][w] = res[i]
+                r = st["c_res"][w]
+                stats[w] = (int(r.iterations), int(r.lm_trials), int(r.status))
+        st["stats"] = stats
         self.cur = set_index
-        return st["stats"]
+        return stats
 
     def _size(self, w: int):
         P = self.c_probs[w]
