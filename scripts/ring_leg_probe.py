@@ -18,6 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--steps", type=int, default=6)
+ap.add_argument("--n-fixed", type=int, default=10)
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 cfg = dict(bench.CONFIGS[a.config])
@@ -25,6 +26,7 @@ tr = bench.TrackingLeg(cfg, a.batch, 4, 0, dev)
 W = max(1, a.batch // 8)
 nm = NewMapPointsLeg(tr, W, dev)
 leg = RingMappingLeg(nm, 0, 1, dev)
+leg.rl.n_fixed = a.n_fixed
 print("legs", "W", W, "R", nm.R, "S", nm.S, "sets", leg.nheads, flush=True)
 prev = None
 for step in range(a.steps):
@@ -52,7 +54,17 @@ for step in range(a.steps):
         if bad:
             sys.exit(2)
         t0 = time.perf_counter()
-        leg.run(step, head=prev)
+        try:
+            leg.run(step, head=prev)
+        except RuntimeError as e:
+            import ctypes as C
+
+            from mam3slam_amd._lib import lib
+
+            L = lib()
+            L.mam_last_error.restype = C.c_char_p
+            print("FAILED", e, "last error:", L.mam_last_error(), flush=True)
+            raise
         torch.cuda.synchronize()
         print(f"  solved {time.perf_counter() - t0:.4f} s stats {leg.stats[:3]} status {int(leg.status.item())}"
               f" records kf {leg.n_kf_upd} mp {leg.n_mp_upd}", flush=True)
