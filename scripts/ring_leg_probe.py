@@ -19,6 +19,7 @@ ap.add_argument("--config", default="c2")
 ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--steps", type=int, default=6)
 ap.add_argument("--n-fixed", type=int, default=10)
+ap.add_argument("--dump", default=None, help="write the first assembled windows (npz) and stop before solving")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 cfg = dict(bench.CONFIGS[a.config])
@@ -53,6 +54,18 @@ for step in range(a.steps):
               f" E {cnt[:, 2].min()}-{cnt[:, 2].max()} opt {cnt[:, 3].min()}-{cnt[:, 3].max()} bad {bad[:4]}", flush=True)
         if bad:
             sys.exit(2)
+        if a.dump:
+            leg.rl.cur = prev // W
+            arrs = {}
+            for w in range(4):
+                pr = leg.rl.window(w)
+                for f in ("pose_fixed", "pose_q", "pose_t", "point_xyz", "edge_point", "edge_pose", "edge_obs",
+                          "edge_inv_sigma2", "cams"):
+                    arrs[f"w{w}_{f}"] = np.asarray(getattr(pr, f))
+                arrs[f"w{w}_meta"] = np.array([pr.huber_delta, pr.iterations, pr.cam_model], np.float64)
+            np.savez(a.dump, **arrs)
+            print("dumped", a.dump, flush=True)
+            sys.exit(0)
         t0 = time.perf_counter()
         try:
             leg.run(step, head=prev)
