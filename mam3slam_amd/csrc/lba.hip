@@ -3135,28 +3135,11 @@ struct Carver {
     size_t off = 0;
     template <typename T>
     T* take(size_t n) {
-        T* p = reinterpret_cast<T*>(base + off);
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;   // (base null: a dry run counting bytes)
         off += al(n * sizeof(T));
         return p;
     }
 };
-
-// Arena bytes of one problem's structure, state and scratch (the inputs and outputs live elsewhere)
-size_t scratch_bytes(int P, int L, int E, int Np, int npad) {
-    const size_t nx = 6 * (size_t)Np + 3 * (size_t)L;
-    return al(4 * (size_t)P) + al(4 * (size_t)Np) + al(4 * (size_t)(L + 1)) + al(4 * (size_t)E) +
-           al(4 * (size_t)E) + al(16 * (size_t)E) +
-           al(4 * (size_t)(Np + 1)) + al(4 * (size_t)E) + al(4 * (size_t)(L + Np)) + al(4 * (size_t)Np * L) + al((size_t)Np * Np) + al(4 * ((size_t)Np * Np + 1)) +
-           al((size_t)(npad / 16) * (npad / 16)) + al(2 * (size_t)(npad / 16) * (npad / 16)) +
-           al(2 * (size_t)(npad / 16) * (npad / 16 + 1)) + 2 * al(40 * (size_t)std::max(npad / 16, 1)) +
-           al(2 * (size_t)std::max(npad / 16, 1)) + 2 * al(2 * (size_t)std::max(Np, 1)) + al(40) +
-           al(8 * 256 * (size_t)(npad / 16) * (npad / 16 + 1) / 2) +
-           2 * al(8 * 7 * (size_t)P) + 2 * al(8 * 3 * (size_t)L) + al(8 * 2 * (size_t)E) + al(8 * 21 * (size_t)E) +
-           3 * al(8 * (size_t)(std::max((E + 63) / 64, (L + mam::lba::PW - 1) / mam::lba::PW) + 1)) + 2 * al(8 * 18 * (size_t)E) + al(8 * 6 * (size_t)E) +
-           al(8 * 36 * (size_t)Np) + al(8 * 9 * (size_t)L) + al(8 * nx) + al(8 * 9 * (size_t)L) +
-           al(8 * (size_t)npad * npad) + al(8 * nx) + al(8 * (size_t)npad) +
-           al(8 * mam::lba::ldlt_ws_doubles(npad)) + al((size_t)E);
-}
 
 void carve_scratch(Carver& cv, Prob& d) {
     const size_t nx = 6 * (size_t)d.Np + 3 * (size_t)d.L;
@@ -3206,6 +3189,16 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.bs = cv.take<double>(d.npad);
     d.ws = cv.take<double>(mam::lba::ldlt_ws_doubles(d.npad));
     d.depth = cv.take<uint8_t>(d.E);
+}
+
+// Arena bytes of one problem's structure, state and scratch (the inputs and outputs live elsewhere): a dry run of
+// carve_scratch, so the size and the carve cannot drift apart (a hand-kept formula once missed the pose sums'
+// POSE_SPLIT partials and a batch's problems overran into their neighbours' structure)
+size_t scratch_bytes(const Prob& d0) {
+    Prob d = d0;
+    Carver cv{nullptr};
+    carve_scratch(cv, d);
+    return cv.off;
 }
 
 // Output pointers of a batch problem (device memory); chi2 / depth may be NULL
@@ -3273,7 +3266,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     bool lds_ok = true;
     for (auto& d : hp) {
         d.npad = ldlt_pad(6 * d.Np);
-        bytes += scratch_bytes(d.P, d.L, d.E, d.Np, d.npad);
+        bytes += scratch_bytes(d);
         maxE = std::max(maxE, d.E);
         maxL = std::max(maxL, d.L);
         maxP = std::max(maxP, d.P);

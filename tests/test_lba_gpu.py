@@ -143,6 +143,28 @@ def test_lba_batch_device(solver, oracle):
         assert np.array_equal(B.result(i).point_xyz, first[i].point_xyz)
 
 
+def test_lba_batch_same_shape(solver, oracle):
+    """Problems of one shape in one device batch (the ring's covisibility windows: 21 optimised + 10 fixed poses, dense
+    covisibility): every problem's arena scratch is its own. Regression: a hand-kept size formula that lagged the carve
+    (the pose sums' POSE_SPLIT partials) let problem q's pose sums overrun problem q + 1's structure."""
+    import torch
+
+    from mam3slam_amd.lba import DeviceBatch, id_ordered
+
+    probs = [synthetic_problem(n_opt=21, n_fixed=10, n_points=1500, obs_per_point=12, seed=40 + i, init_kf_local=False)
+             for i in range(4)]
+    B = DeviceBatch(probs, torch.device("cuda", 0))
+    stats = solver.solve_batch_device(B)
+    for i, p in enumerate(probs):
+        ro = oracle.lba_solve(id_ordered(p)[0])
+        rg = B.result(i)
+        assert stats[i]["status"] == 0 and ro.status == 0
+        assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials), i
+        assert abs(rg.final_chi2 - ro.final_chi2) <= 1e-6 * ro.final_chi2
+        assert _rel(rg.pose_t, ro.pose_t) <= 1e-4 and _rel(rg.pose_q, ro.pose_q) <= 1e-4
+        assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
+
+
 def test_lba_size_bound(solver):
     """A problem whose dense pose x landmark table would exceed 4 GiB (1100 optimised poses x 1M points) is refused
     with MAM_ERR_CAPACITY and a message naming the sizes, before any scratch allocation."""
