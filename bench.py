@@ -174,7 +174,7 @@ class TrackingLeg:
     """B frames resident in HBM, split into lanes (sub-batches with their own contexts and HIP stream, captured
     together into one HIP graph) so one lane's latency-bound stages overlap another's compute."""
 
-    def __init__(self, cfg, B, lanes, rank, dev):
+    def __init__(self, cfg, B, lanes, rank, dev, new_stream=None):
         import torch
 
         from mam3slam_amd import ORBextractor, scene, synth
@@ -214,11 +214,13 @@ class TrackingLeg:
         self.d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
         self.d_cnt = torch.zeros((B, 2), dtype=torch.int32, device=dev)
         # one explicit stream orders extraction -> motion search -> frustum -> local search
-        self.tstream = torch.cuda.Stream(dev)
+        # (new_stream: the streams' factory — CU-masked streams under --cu-split)
+        new_stream = new_stream or (lambda: torch.cuda.Stream(dev))
+        self.tstream = new_stream()
         self.lanes = []
         for l in range(lanes):
             self.lanes.append({"lo": l * BL, "ext": self.ext if l == 0 else ORBextractor(NF, 1.2, 8, 20, 7, device=di),
-                               "stream": self.tstream if l == 0 else torch.cuda.Stream(dev)})
+                               "stream": self.tstream if l == 0 else new_stream()})
         # every set's keypoints (the scene's MapPoints are placed on them)
         kps_l, desc_l, cnt_l = [], [], []
         for p in range(P):
@@ -898,6 +900,9 @@ def main():
                     help="the timed LocalMapping leg's LBA windows: ring = the keyframes the step tracked (RingMappingLeg, "
                          "the reference's window rule), world = the synthetic shared map's windows (LocalMappingLeg)")
     ap.add_argument("--lanes", type=int, default=4)
+    ap.add_argument("--cu-split", type=int, default=0, choices=(0, 2, 4, 6),
+                    help="LocalMapping's LBA on eighths/8 of every XCD's CUs, Tracking and the keyframe searches on the "
+                         "rest (CU-masked streams; 0: every stream on every CU)")
     ap.add_argument("--profile-timed", action="store_true",
                     help="record LocalMapping's stage events inside the timed region (default: a second pass)")
     ap.add_argument("--launch-check", action="store_true",
@@ -950,14 +955,25 @@ def main():
         raise SystemExit(f"--batch {B} is not a multiple of --lanes {NL}")
     # keyframe cadence: B/K new keyframes (LBA windows) per step; with fewer streams than K, one every K/B steps
     map_every = max(1, K // B)
-    tr = TrackingLeg(cfg, B, NL, rank, dev)
+    tr_stream = lm_stream = lm_mask = None
+    if args.cu_split and cfg["lba"]:
+        from mam3slam_amd import streams
+
+        ncu = streams.cu_count(dev.index or 0)
+        lm_mask = streams.cu_mask(ncu, args.cu_split)
+        tr_mask = streams.cu_mask(ncu, args.cu_split, complement=True)
+        tr_stream = lambda: streams.masked_stream(dev, tr_mask)  # noqa: E731
+        lm_stream = streams.masked_stream(dev, lm_mask)
+    tr = TrackingLeg(cfg, B, NL, rank, dev, new_stream=tr_stream)
     mapping = newmp = None
     if cfg["lba"]:
         from mam3slam_amd.mapping import LocalMappingLeg, NewMapPointsLeg, RingMappingLeg
 
-        newmp = NewMapPointsLeg(tr, max(1, B // K), dev)
+        newmp = NewMapPointsLeg(tr, max(1, B // K), dev, stream=tr_stream() if tr_stream else None)
         if args.lm_windows == "ring":
-            mapping = RingMappingLeg(newmp, rank, world, dev)
+            mapping = RingMappingLeg(newmp, rank, world, dev, stream=lm_stream)
+            if lm_mask is not None:
+                mapping.solver.set_cu_mask(lm_mask)
         else:
             mapping = LocalMappingLeg(max(1, B // K), rank, world, dev, camera=tr.cam if cfg.get("camera") else None,
                                       width=tr.W, height=tr.H)

@@ -98,6 +98,9 @@ int mam_lba_solve_batch_device(mam_lba_ctx* ctx, int n_problems, const mam_lba_p
                                mam_lba_result* results, void* stream);
 
 int mam_lba_set_profiling(mam_lba_ctx* ctx, int enable);
+/* CU mask (n_words 32-bit words, include/mam_stream.h) of the streams a batch solve splits its problem groups onto
+ * besides the caller's stream (which the caller creates with the same mask); n_words 0: every CU. */
+int mam_lba_set_cu_mask(mam_lba_ctx* ctx, int n_words, const uint32_t* mask);
 /* [0] structure + linearize + blocks, [1] Schur, [2] dense solve, [3] back-substitution + update + chi2 */
 int mam_lba_stage_times(mam_lba_ctx* ctx, double* ms_out, int64_t* launches_out);
 

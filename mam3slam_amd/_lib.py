@@ -61,8 +61,9 @@ def _match_sigs():
     from .match import _SIGS
     from .pose import _SIGS as pose_sigs
     from .bow import _SIGS as bow_sigs
+    from .streams import _SIGS as stream_sigs
 
-    return {**_SIGS, **lba_sigs, **ex_sigs, **pose_sigs, **bow_sigs}
+    return {**_SIGS, **lba_sigs, **ex_sigs, **pose_sigs, **bow_sigs, **stream_sigs}
 
 
 def lib() -> C.CDLL:

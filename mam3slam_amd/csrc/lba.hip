@@ -113,6 +113,7 @@ struct Prob {
     int32_t* cnt;                // [L + Np] counters / cursors of the device structure build
     int32_t* eidx;               // [Np][L] edge of (pose block, point), never cleared: read through eidx_at
     uint8_t* pairmask;           // [Np][Np] (i1 < i2): the two poses share a landmark (S block non-zero)
+    unsigned long long* pm_rows; // [64] (Np <= 64): pairmask row i1 as bits i2 (k_struct_sort; k_struct_tiles expands)
     int32_t* blk_off;            // [Np * Np + 1] start of block (i1, i2)'s landmark pairs in blk_pair (i1 <= i2)
     int2* blk_pair;              // (edge of pose i1, edge of pose i2) per shared landmark, i2's edge order
     uint8_t* tmask;              // [nt][nt] (r >= c): 16x16 tile (r, c) of L is structurally non-zero (S + fill)
@@ -374,6 +375,7 @@ __global__ __launch_bounds__(SB) void k_struct_init(const Prob* __restrict__ pro
     }
     for (int i = g0; i < d.L + d.Np; i += gstride) d.cnt[i] = 0;
     for (size_t i = g0; i < (size_t)d.Np * d.Np; i += gstride) d.pairmask[i] = 0;
+    if (g0 < 64) d.pm_rows[g0] = 0ull;
     const size_t n6 = 6 * (size_t)d.Np;
     for (size_t i = g0; i < ((size_t)d.npad - n6) * d.npad; i += gstride) d.S[n6 * d.npad + i] = 0.0;
     for (int i = g0; i < d.P; i += gstride) {
@@ -488,90 +490,116 @@ __global__ __launch_bounds__(256) void k_struct_scatter(const Prob* __restrict__
     if (h >= 0) d.qe_idx[d.qe_off[h] + hist[h] + r] = e;
 }
 
-// grid (ceil(L/256) + Np, Q) x 256: restore edge order inside every list — per point an insertion sort by one thread
-// (a handful of observations), per pose a rank sort of its segment staged in LDS (chunks of 4096 when longer: a
-// bitonic-free merge is not needed because every chunk's ranks are counted over the whole segment)
+// one point's edge list (n <= NR) sorted in registers (an unrolled exchange network; edge ids are distinct) with each
+// dependent lookup issued for the whole list at once: three memory round trips instead of a few per element. The S
+// blocks the landmark contributes to (g2o's BlockSolver keeps only these, block_solver.hpp:181-224) go to the LDS bit
+// rows (rows != null: windows of <= 64 optimised poses) or straight to the byte pair mask.
+template <int NR>
+__device__ __forceinline__ void point_list_regs(const Prob& d, int h, int32_t* s, int n, unsigned long long* rows) {
+    int v[NR], ep[NR], hv[NR];
+#pragma unroll
+    for (int a = 0; a < NR; a++) v[a] = a < n ? s[a] : INT_MAX;
+#pragma unroll
+    for (int i = 0; i < NR - 1; i++)
+#pragma unroll
+        for (int j = 0; j < NR - 1 - i; j++) {
+            const int lo = min(v[j], v[j + 1]), hi = max(v[j], v[j + 1]);
+            v[j] = lo;
+            v[j + 1] = hi;
+        }
+#pragma unroll
+    for (int a = 0; a < NR; a++) ep[a] = a < n ? d.edge_pose[v[a]] : 0;
+#pragma unroll
+    for (int a = 0; a < NR; a++) hv[a] = a < n ? d.pose_h[ep[a]] : -1;
+#pragma unroll
+    for (int a = 0; a < NR; a++)
+        if (a < n) {
+            s[a] = v[a];
+            d.slot_hp[d.pe_off[h] + a] = hv[a];
+            d.emeta[v[a]] = make_int4(h, hv[a], a == 0 ? 1 : 0, 0);
+        }
+    if (rows) {
+        unsigned long long m = 0;
+#pragma unroll
+        for (int a = 0; a < NR; a++) m |= hv[a] >= 0 ? 1ull << hv[a] : 0ull;
+        // row ha gets the poses above it (the upper triangle, as the byte mask holds it)
+#pragma unroll
+        for (int a = 0; a < NR; a++)
+            if (hv[a] >= 0) {
+                const unsigned long long up = m & ~((2ull << hv[a]) - 1ull);
+                if (up) atomicOr(&rows[hv[a]], up);
+            }
+        return;
+    }
+#pragma unroll
+    for (int a = 0; a < NR; a++)
+#pragma unroll
+        for (int b = a + 1; b < NR; b++) {
+            const int ha = hv[a], hb = hv[b];
+            if (ha >= 0 && hb >= 0 && hb != ha) d.pairmask[(size_t)min(ha, hb) * d.Np + max(ha, hb)] = 1;
+        }
+}
+
+// grid (ceil(L/256) + Np, Q) x 256: restore edge order inside every list — per point its list sorted in registers (up
+// to 32 observations; longer lists by one thread in place), per pose a bitonic sort of its segment staged in LDS
+// (segments of up to 4096 edges; longer ones, global BA, by odd-even transposition in place). Windows of <= 64
+// optimised poses collect the pair mask as LDS bit rows per workgroup (one device atomic per row present instead of a
+// byte store per observation pair: ~2.7M stores per batch of 32 ring windows), k_struct_tiles expands them.
 __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     if (d.lm->status) return;
     const int nb_pts = (d.L + 255) / 256;
     if ((int)blockIdx.x < nb_pts) {
+        __shared__ unsigned long long rows_s[64];
+        const bool bits = d.Np <= 64;   // uniform
+        if (bits && threadIdx.x < 64) rows_s[threadIdx.x] = 0ull;
+        __syncthreads();
+        unsigned long long* rows = bits ? rows_s : nullptr;
         const int h = blockIdx.x * 256 + threadIdx.x;
-        if (h >= d.L) return;
-        int32_t* s = d.pe_idx + d.pe_off[h];
-        const int n = d.pe_off[h + 1] - d.pe_off[h];
-        // per slot / per edge metadata the per-trial kernels read with one load instead of a chain of dependent ones
-        constexpr int NR = 8;   // a window's points: <= 8 observations, their pose blocks kept in registers
-        if (n <= NR) {
-            // the list sorted in registers (an unrolled exchange network; edge ids are distinct), and each dependent
-            // lookup issued for the whole list at once: three memory round trips instead of a few per element
-            int v[NR], ep[NR], hv[NR];
-#pragma unroll
-            for (int a = 0; a < NR; a++) v[a] = a < n ? s[a] : INT_MAX;
-#pragma unroll
-            for (int i = 0; i < NR - 1; i++)
-#pragma unroll
-                for (int j = 0; j < NR - 1 - i; j++) {
-                    const int lo = min(v[j], v[j + 1]), hi = max(v[j], v[j + 1]);
-                    v[j] = lo;
-                    v[j + 1] = hi;
+        if (h < d.L) {
+            int32_t* s = d.pe_idx + d.pe_off[h];
+            const int n = d.pe_off[h + 1] - d.pe_off[h];
+            if (n <= 8) {
+                point_list_regs<8>(d, h, s, n, rows);
+            } else if (n <= 32) {
+                point_list_regs<32>(d, h, s, n, rows);
+            } else {
+                for (int k = 1; k < n; k++) {
+                    const int v = s[k];
+                    int m = k - 1;
+                    while (m >= 0 && s[m] > v) { s[m + 1] = s[m]; m--; }
+                    s[m + 1] = v;
                 }
-#pragma unroll
-            for (int a = 0; a < NR; a++) ep[a] = a < n ? d.edge_pose[v[a]] : 0;
-#pragma unroll
-            for (int a = 0; a < NR; a++) hv[a] = a < n ? d.pose_h[ep[a]] : -1;
-#pragma unroll
-            for (int a = 0; a < NR; a++)
-                if (a < n) {
-                    s[a] = v[a];
-                    d.slot_hp[d.pe_off[h] + a] = hv[a];
-                    d.emeta[v[a]] = make_int4(h, hv[a], a == 0 ? 1 : 0, 0);
+                unsigned long long msk = 0;
+                for (int a = 0; a < n; a++) {
+                    const int e = s[a];
+                    const int hp = d.pose_h[d.edge_pose[e]];
+                    d.slot_hp[d.pe_off[h] + a] = hp;
+                    d.emeta[e] = make_int4(h, hp, a == 0 ? 1 : 0, 0);
+                    if (bits && hp >= 0) msk |= 1ull << hp;
                 }
-            // the S blocks this landmark contributes to (g2o's BlockSolver keeps only these, block_solver.hpp:181-224)
-#pragma unroll
-            for (int a = 0; a < NR; a++)
-#pragma unroll
-                for (int b = a + 1; b < NR; b++) {
-                    const int ha = hv[a], hb = hv[b];
-                    if (ha >= 0 && hb >= 0 && hb != ha) d.pairmask[(size_t)min(ha, hb) * d.Np + max(ha, hb)] = 1;
+                if (bits) {
+                    for (int a = 0; a < n; a++) {
+                        const int ha = d.slot_hp[d.pe_off[h] + a];
+                        if (ha < 0) continue;
+                        const unsigned long long up = msk & ~((2ull << ha) - 1ull);
+                        if (up) atomicOr(&rows_s[ha], up);
+                    }
+                } else {
+                    for (int a = 0; a < n; a++) {
+                        const int ha = d.pose_h[d.edge_pose[s[a]]];
+                        if (ha < 0) continue;
+                        for (int b = a + 1; b < n; b++) {
+                            const int hb = d.pose_h[d.edge_pose[s[b]]];
+                            if (hb >= 0 && hb != ha) d.pairmask[(size_t)min(ha, hb) * d.Np + max(ha, hb)] = 1;
+                        }
+                    }
                 }
-            return;
-        }
-        for (int k = 1; k < n; k++) {
-            const int v = s[k];
-            int m = k - 1;
-            while (m >= 0 && s[m] > v) { s[m + 1] = s[m]; m--; }
-            s[m + 1] = v;
-        }
-        int hpv[NR];
-#pragma unroll
-        for (int a = 0; a < NR; a++) hpv[a] = -1;
-        for (int a = 0; a < n; a++) {
-            const int e = s[a];
-            const int hp = d.pose_h[d.edge_pose[e]];
-            d.slot_hp[d.pe_off[h] + a] = hp;
-            d.emeta[e] = make_int4(h, hp, a == 0 ? 1 : 0, 0);
-#pragma unroll
-            for (int k = 0; k < NR; k++) hpv[k] = k == a ? hp : hpv[k];
-        }
-        // the S blocks this landmark contributes to (g2o's BlockSolver keeps only these, block_solver.hpp:181-224)
-        if (n <= NR) {   // from the registers (the general loop reloads through the stores it may alias)
-#pragma unroll
-            for (int a = 0; a < NR; a++)
-#pragma unroll
-                for (int b = a + 1; b < NR; b++) {
-                    const int ha = hpv[a], hb = hpv[b];
-                    if (ha >= 0 && hb >= 0 && hb != ha) d.pairmask[(size_t)min(ha, hb) * d.Np + max(ha, hb)] = 1;
-                }
-            return;
-        }
-        for (int a = 0; a < n; a++) {
-            const int ha = d.pose_h[d.edge_pose[s[a]]];
-            if (ha < 0) continue;
-            for (int b = a + 1; b < n; b++) {
-                const int hb = d.pose_h[d.edge_pose[s[b]]];
-                if (hb >= 0 && hb != ha) d.pairmask[(size_t)min(ha, hb) * d.Np + max(ha, hb)] = 1;
             }
+        }
+        if (bits) {   // uniform
+            __syncthreads();
+            if (threadIdx.x < d.Np && rows_s[threadIdx.x]) atomicOr(&d.pm_rows[threadIdx.x], rows_s[threadIdx.x]);
         }
         return;
     }
@@ -582,14 +610,26 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
     int32_t* s = d.qe_idx + d.qe_off[h];
     const int n = d.qe_off[h + 1] - d.qe_off[h];
     if (n <= CH) {
-        for (int i = threadIdx.x; i < n; i += 256) seg[i] = s[i];
+        // a bitonic sort of the segment padded to a power of two with INT_MAX (a rank count over the segment was
+        // O(n^2): ~270 us per batch of 32 ring windows, ~1.7k edges per pose)
+        int np2 = 1;
+        while (np2 < n) np2 <<= 1;
+        for (int i = threadIdx.x; i < np2; i += 256) seg[i] = i < n ? s[i] : INT_MAX;
         __syncthreads();
-        for (int i = threadIdx.x; i < n; i += 256) {
-            const int v = seg[i];
-            int r = 0;
-            for (int j = 0; j < n; j++) r += seg[j] < v;   // edge ids are distinct
-            s[r] = v;
-        }
+        for (int k = 2; k <= np2; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int t = threadIdx.x; t < (np2 >> 1); t += 256) {
+                    const int i = 2 * t - (t & (j - 1)), l = i + j;   // pair (i, l = i + j), i with bit j clear
+                    const int a = seg[i], b = seg[l];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        seg[i] = b;
+                        seg[l] = a;
+                    }
+                }
+                __syncthreads();
+            }
+        for (int i = threadIdx.x; i < n; i += 256) s[i] = seg[i];
     } else {
         // long segments (global BA): odd-even transposition in place, n rounds
         for (int round = 0; round < n; round++) {
@@ -1163,8 +1203,18 @@ __global__ __launch_bounds__(SB) void k_struct_tiles(const Prob* __restrict__ pr
     uint8_t* tm = small ? tm_s : d.tmask;
     const int16_t* ip = small ? ip_s : d.iperm;
     if (t == 0) bw = 0;
-    if (small)
+    if (Np <= 64) {
+        // k_struct_sort's bit rows expanded into the byte mask (the LDS copy here, the global one for k_blk_* and
+        // k_schur_blk)
+        for (int q = t; q < Np * Np; q += SB) {
+            const int i1 = q / Np, i2 = q % Np;
+            const uint8_t v = (uint8_t)((d.pm_rows[i1] >> i2) & 1ull);
+            pm_s[q] = v;
+            d.pairmask[q] = v;
+        }
+    } else if (small) {
         for (int q = t; q < Np * Np; q += SB) pm_s[q] = d.pairmask[q];
+    }
     __syncthreads();
     // The pose order. For a banded pose graph (bandwidth b: poses more than b apart in the window share no landmark),
     // [0, m) | [m + s, Np) reversed | [m, m + s), s >= b: no S entry couples the two ends, so they factor as two
@@ -3122,6 +3172,7 @@ struct mam_lba_ctx {
     static constexpr int kMaxGroups = 4;
     hipStream_t gstream[kMaxGroups - 1] = {};   // groups 1.. of a split batch (created on first use, caller's priority)
     hipEvent_t ev_start = nullptr, ev_done[kMaxGroups - 1] = {};
+    std::vector<uint32_t> cu_mask;   // the group streams' CU mask (mam_lba_set_cu_mask; empty: every CU)
     double trials_ema = 8.0;      // slots enqueued before the first read-back (tracks the trials solves take)
 };
 
@@ -3154,6 +3205,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.cnt = cv.take<int32_t>(d.L + d.Np);
     d.eidx = cv.take<int32_t>((size_t)d.Np * d.L);
     d.pairmask = cv.take<uint8_t>((size_t)d.Np * d.Np);
+    d.pm_rows = cv.take<unsigned long long>(64);
     d.blk_off = cv.take<int32_t>((size_t)d.Np * d.Np + 1);
     d.nt = d.npad / mam::lba::NB;
     d.tmask = cv.take<uint8_t>((size_t)d.nt * d.nt);
@@ -3401,7 +3453,10 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         if (hipStreamGetPriority(s, &prio) != hipSuccess) prio = 0;
         if (!c->ev_start) MAM_HIP(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
         for (int g = 1; g < G; g++) {
-            if (!c->gstream[g - 1]) {
+            if (!c->gstream[g - 1] && !c->cu_mask.empty()) {
+                MAM_HIP(hipExtStreamCreateWithCUMask(&c->gstream[g - 1], (uint32_t)c->cu_mask.size(), c->cu_mask.data()));
+                MAM_HIP(hipEventCreateWithFlags(&c->ev_done[g - 1], hipEventDisableTiming));
+            } else if (!c->gstream[g - 1]) {
                 if (hipStreamCreateWithPriority(&c->gstream[g - 1], hipStreamNonBlocking, prio) != hipSuccess) {
                     (void)hipGetLastError();
                     MAM_HIP(hipStreamCreateWithFlags(&c->gstream[g - 1], hipStreamNonBlocking));
@@ -3622,6 +3677,25 @@ void mam_lba_destroy(mam_lba_ctx* c) {
     }
     if (c->up_done) (void)hipEventDestroy(c->up_done);
     delete c;
+}
+
+int mam_lba_set_cu_mask(mam_lba_ctx* c, int n_words, const uint32_t* mask) {
+    if (!c || n_words < 0 || (n_words > 0 && !mask)) return MAM_ERR_ARG;
+    MAM_DEVICE_SCOPE(c->device);
+    // the group streams are re-created on the new mask at the next split batch
+    for (int g = 0; g < mam_lba_ctx::kMaxGroups - 1; g++) {
+        if (c->gstream[g]) {
+            MAM_HIP(hipStreamSynchronize(c->gstream[g]));
+            MAM_HIP(hipStreamDestroy(c->gstream[g]));
+            c->gstream[g] = nullptr;
+        }
+        if (c->ev_done[g]) {
+            MAM_HIP(hipEventDestroy(c->ev_done[g]));
+            c->ev_done[g] = nullptr;
+        }
+    }
+    c->cu_mask.assign(mask, mask + n_words);
+    return MAM_OK;
 }
 
 int mam_lba_set_profiling(mam_lba_ctx* c, int enable) {

@@ -42,6 +42,7 @@ _SIGS = {
     "mam_lba_solve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mam_lba_solve_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mam_lba_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "mam_lba_set_cu_mask": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     "mam_lba_stage_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
 }
 
@@ -168,6 +169,13 @@ class LBASolver:
         batch.stats = [dict(iterations=int(r.iterations), lm_trials=int(r.lm_trials), initial_chi2=float(r.initial_chi2),
                             final_chi2=float(r.final_chi2), status=int(r.status)) for r in batch.c_res]
         return batch.stats
+
+    def set_cu_mask(self, mask):
+        """The CU mask (uint32 words; None: every CU) of the streams a split batch solve adds (mam_lba_set_cu_mask)."""
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint32)
+        check(self._L.mam_lba_set_cu_mask(self._ctx, 0 if m is None else len(m), None if m is None else m.ctypes.data),
+              "lba_set_cu_mask")
+        self._cu_mask = m
 
     def set_profiling(self, enable: bool):
         check(self._L.mam_lba_set_profiling(self._ctx, 1 if enable else 0), "lba_set_profiling")

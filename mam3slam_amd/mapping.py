@@ -214,7 +214,7 @@ class NewMapPointsLeg:
 
     NN = 30
 
-    def __init__(self, tr, n_new: int, device, seed: int = 0):
+    def __init__(self, tr, n_new: int, device, seed: int = 0, stream=None):
         import torch
 
         from . import bow
@@ -241,7 +241,7 @@ class NewMapPointsLeg:
         self.ready = {h: torch.cuda.Event() for h in range(0, self.R, self.W)}
         # completion of the search run at each head (None until one was issued there)
         self.done = {h: None for h in range(0, self.R, self.W)}
-        self.stream = torch.cuda.Stream(device, priority=-1)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device, priority=-1)
         # pairs for each head position. With at least NN + 1 keyframes per ingest (c2: 32), new keyframe i (frame
         # i K + s of the agent's sequence) searches the NN keyframes of the same ingest nearest to it in the sequence
         # (frames i' K + s, |i - i'| smallest, earlier first on a tie): the covisible keyframes

@@ -38,10 +38,13 @@ def main():
     ap.add_argument("npz")
     ap.add_argument("--mode", choices=("single", "batch", "oracle"), default="single")
     ap.add_argument("--windows", type=int, default=0, help="how many windows (0: all)")
+    ap.add_argument("--repeat", type=int, default=1, help="the windows repeated this many times in the batch")
+    ap.add_argument("--solves", type=int, default=1, help="batch solves (timed after the first)")
     a = ap.parse_args()
     probs = load(a.npz)
     if a.windows:
         probs = probs[:a.windows]
+    probs = probs * a.repeat
     for i, p in enumerate(probs):
         print(f"window {i}: P {len(p.pose_id)} opt {int((p.pose_fixed == 0).sum())} L {len(p.point_id)} "
               f"E {len(p.edge_point)}", flush=True)
@@ -71,7 +74,15 @@ def main():
         B = DeviceBatch(probs, torch.device("cuda", 0))
         st = s.solve_batch_device(B)
         torch.cuda.synchronize()
-        for i in range(len(probs)):
+        ts = []
+        for _ in range(a.solves - 1):
+            t0 = time.perf_counter()
+            s.solve_batch_device(B)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        if ts:
+            print(f"batch of {len(probs)}: ms per solve median {np.median(ts):.3f} min {min(ts):.3f}", flush=True)
+        for i in range(min(len(probs), 4)):
             r = B.result(i)
             print(f"batch {i}: {st[i]} chi2 {r.initial_chi2:.6g} -> {r.final_chi2:.6g}", flush=True)
 
