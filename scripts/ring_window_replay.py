@@ -66,8 +66,14 @@ def main():
     if a.mode == "single":
         for i, p in enumerate(probs):
             r = s.solve(p)
+            ts = []
+            for _ in range(a.solves - 1):
+                t0 = time.perf_counter()
+                s.solve(p)
+                ts.append((time.perf_counter() - t0) * 1e3)
+            med = f" ms per solve median {np.median(ts):.3f} min {min(ts):.3f}" if ts else ""
             print(f"single {i}: status {r.status} its {r.iterations} trials {r.lm_trials} chi2 {r.initial_chi2:.6g} -> "
-                  f"{r.final_chi2:.6g}", flush=True)
+                  f"{r.final_chi2:.6g}{med}", flush=True)
     else:
         from mam3slam_amd.lba import DeviceBatch
 
