@@ -184,9 +184,11 @@ def section(tr, reps=20, oracle=True) -> dict:
     t_e = torch.from_numpy(E.view(np.uint8).reshape(B, -1)).to(dev)
     t_n = torch.tensor([len(e) for e in edges_l], dtype=torch.int32, device=dev)
     tcw = np.zeros(B, dtype=np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,))]))
-    rng = np.random.default_rng(7)
     for f in range(B):
-        tcw[f]["q"], tcw[f]["t"] = scene.small_pose(rng)   # the motion model's guess around the frame's pose
+        # the motion model's guess the step itself starts from (TrackingLeg.poses_init: the frame's pose 0.3 deg / 2 cm
+        # off). (Rounds 3-4 started this section from a small pose around the identity instead, far from the frames'
+        # poses: 26 iterations / 45 LM trials a frame, not the step's workload.)
+        tcw[f]["q"], tcw[f]["t"] = tr.poses_init[f]
     t_p = torch.from_numpy(tcw.view(np.uint8)).to(dev)
     t_o = torch.zeros((B, S), dtype=torch.uint8, device=dev)
     t_r = torch.zeros((B, pose.POSE_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
