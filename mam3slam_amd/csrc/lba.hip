@@ -499,14 +499,19 @@ __device__ __forceinline__ void point_list_regs(const Prob& d, int h, int32_t* s
     int v[NR], ep[NR], hv[NR];
 #pragma unroll
     for (int a = 0; a < NR; a++) v[a] = a < n ? s[a] : INT_MAX;
+    // (a list already in edge order — a window's edges listed point-major — skips the network)
+    bool sorted = true;
 #pragma unroll
-    for (int i = 0; i < NR - 1; i++)
+    for (int a = 0; a + 1 < NR; a++) sorted = sorted && (a + 1 >= n || v[a] < v[a + 1]);
+    if (!sorted)
 #pragma unroll
-        for (int j = 0; j < NR - 1 - i; j++) {
-            const int lo = min(v[j], v[j + 1]), hi = max(v[j], v[j + 1]);
-            v[j] = lo;
-            v[j + 1] = hi;
-        }
+        for (int i = 0; i < NR - 1; i++)
+#pragma unroll
+            for (int j = 0; j < NR - 1 - i; j++) {
+                const int lo = min(v[j], v[j + 1]), hi = max(v[j], v[j + 1]);
+                v[j] = lo;
+                v[j + 1] = hi;
+            }
 #pragma unroll
     for (int a = 0; a < NR; a++) ep[a] = a < n ? d.edge_pose[v[a]] : 0;
 #pragma unroll
@@ -742,7 +747,10 @@ __device__ double sys_body(const Prob& d) {
         for (int k = 0; k < 3; k++) d.b[6 * (size_t)d.Np + 3 * (size_t)h + k] = bl[k];
         return fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
     }
-    const int h = blockIdx.x - nb_pts, lane = threadIdx.x;
+    // POSE_SPLIT waves per pose, as the trials' pose_sys_wave: partial `part` sums the chunks part, part + POSE_SPLIT,
+    // ... of 64 of the pose's edge list (a new keyframe's pose sees every MapPoint of its window: ~1.7k edges were 27
+    // dependent strides of one wave); max |diag(H_pp)| over the summed partials in k_ctl_init
+    const int hb = blockIdx.x - nb_pts, h = hb / POSE_SPLIT, part = hb % POSE_SPLIT, lane = threadIdx.x;
     if (h >= d.Np) return 0.0;
     double acc[27];
 #pragma unroll
@@ -750,10 +758,11 @@ __device__ double sys_body(const Prob& d) {
     // the lane's edge indices of up to SYS_PF strides loaded together first (one memory round trip where there was
     // one per edge before its record's loads); the records then summed in the same order as before
     const int qs0 = d.qe_off[h], qs1 = d.qe_off[h + 1];
-    for (int base = qs0 + lane; base < qs1; base += 64 * SYS_PF) {
+    for (int base = qs0 + 64 * part + lane; base < qs1; base += 64 * POSE_SPLIT * SYS_PF) {
         int qi[SYS_PF];
 #pragma unroll
-        for (int u = 0; u < SYS_PF; u++) qi[u] = base + 64 * u < qs1 ? d.qe_idx[base + 64 * u] : -1;
+        for (int u = 0; u < SYS_PF; u++)
+            qi[u] = base + 64 * POSE_SPLIT * u < qs1 ? d.qe_idx[base + 64 * POSE_SPLIT * u] : -1;
 #pragma unroll
         for (int u = 0; u < SYS_PF; u++) {
             if (qi[u] < 0) break;
@@ -785,26 +794,19 @@ __device__ double sys_body(const Prob& d) {
 #pragma unroll
     for (int i = 0; i < 7; i++) val = (il == i) ? tot[i] : val;
     const int q = 7 * g + il;   // this lane's sum (upper-triangle order of H, then b)
-    double m = 0.0;
     if (il < 7 && q < 27) {
         if (q < 21) {
             int a = 0, r = q;
             while (r >= 6 - a) { r -= 6 - a; a++; }
             const int c = a + r;
-            double* H = d.Hpp + 36 * (size_t)h;   // partial 0 holds the sum, the others zeros
+            double* H = d.Hpp + 36 * ((size_t)part * d.Np + h);
             H[6 * a + c] = val;
             H[6 * c + a] = val;
-            if (c == a) m = fabs(val);
         } else {
-            d.b[6 * (size_t)h + (q - 21)] = val;
-            d.bp[6 * (size_t)h + (q - 21)] = val;
+            d.bp[6 * ((size_t)part * d.Np + h) + (q - 21)] = val;   // (b's pose part: k_schur_blk sums the partials)
         }
     }
-    // partials 1.. of this pose (layout [part][Np][36] / [part][Np][6]) are zeros
-    for (int k = lane; k < 36 * (POSE_SPLIT - 1); k += 64)
-        d.Hpp[36 * ((size_t)(1 + k / 36) * d.Np + h) + k % 36] = 0.0;
-    for (int k = lane; k < 6 * (POSE_SPLIT - 1); k += 64) d.bp[6 * ((size_t)(1 + k / 6) * d.Np + h) + k % 6] = 0.0;
-    return m;
+    return 0.0;
 }
 
 // Fixed-order sums over RED = 256 virtual threads (strided per-thread sums, then a tree), run by T real threads
@@ -849,7 +851,24 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
     LM& lm = *d.lm;
     if (lm.status) return;
     const double chi = chi_of_parts<RED>(d, d.part0, s);
+    // max |diag(H_pp)| over the poses' summed POSE_SPLIT partials (k_sys' pose waves write partials; its point waves
+    // already put max |diag(H_ll)| into lm.maxdiag), in k_schur_blk's summation order
+    double pm = 0.0;
+    for (int q = threadIdx.x; q < 6 * d.Np; q += RED) {
+        const int h = q / 6, k = q % 6;
+        double v = 0.0;
+#pragma unroll
+        for (int p = 0; p < POSE_SPLIT; p++) v += d.Hpp[36 * ((size_t)p * d.Np + h) + 7 * k];
+        pm = fmax(pm, fabs(v));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pm = fmax(pm, __shfl_xor(pm, o));
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = pm;
+    __syncthreads();
     if (threadIdx.x == 0) {
+        for (int w = 0; w < RED / 64; w++) pm = fmax(pm, s[w]);
+        const double md = fmax(__longlong_as_double((long long)lm.maxdiag), pm);
+        lm.maxdiag = (unsigned long long)__double_as_longlong(md);
         lm.initialChi = chi;
         lm.acceptedChi = chi;
         lm.currentChi = chi;
@@ -864,7 +883,8 @@ __global__ __launch_bounds__(RED) void k_ctl_init(const Prob* __restrict__ probs
 }
 
 
-// grid (ceil(L/64) + Np, Q) x 64: the system (sys_body) and max |diag(H)| (one device atomic per wave)
+// grid (ceil(L/64) + Np POSE_SPLIT, Q) x 64: the system (sys_body) and the points' max |diag(H_ll)| (one device atomic
+// per wave; the poses' in k_ctl_init)
 // (the setup pass: iteration 0's system; lambda_0 = 1e-5 max |diag(H)| is the only max the Levenberg loop reads)
 __global__ __launch_bounds__(64) void k_sys(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
@@ -3425,7 +3445,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_blk_fill, gB, dim3(64), 0, s, P);
         // iteration 0's linearisation and system at the initial state (lambda_0 needs its max |diag(H)|), the initial
         // chi2; the first trial's k_point_sys then starts from this system
-        const dim3 gSys((maxL + 63) / 64 + maxNp > 0 ? (maxL + 63) / 64 + maxNp : 1, Q);
+        const dim3 gSys((maxL + 63) / 64 + maxNp * POSE_SPLIT > 0 ? (maxL + 63) / 64 + maxNp * POSE_SPLIT : 1, Q);
         if (before_lin) {
             int rc = MAM_OK;
             const hipEvent_t ev = before_lin(&rc);
