@@ -899,7 +899,10 @@ def main():
     ap.add_argument("--lm-windows", default="ring", choices=("ring", "world"),
                     help="the timed LocalMapping leg's LBA windows: ring = the keyframes the step tracked (RingMappingLeg, "
                          "the reference's window rule), world = the synthetic shared map's windows (LocalMappingLeg)")
-    ap.add_argument("--lanes", type=int, default=4)
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="tracking sub-batches (own contexts and stream, one graph); default 4, or 2 with LocalMapping "
+                         "beside Tracking (c2: 23.9k vs 22.9k frames/s at 2 / 4 lanes, same box: fewer concurrent "
+                         "tracking launches leave the LBA's latency-bound kernels more of the chip)")
     ap.add_argument("--cu-split", type=int, default=0, choices=(0, 2, 4, 6),
                     help="LocalMapping's LBA on eighths/8 of every XCD's CUs, Tracking and the keyframe searches on the "
                          "rest (CU-masked streams; 0: every stream on every CU)")
@@ -950,7 +953,8 @@ def main():
     cfg = CONFIGS[args.config]
     agents_total = cfg.get("agents")
     B = args.batch if args.batch is not None else (max(1, agents_total // world) if agents_total else 256)
-    NL, K = min(max(1, args.lanes), B), max(1, args.kf_every)
+    lanes = args.lanes if args.lanes is not None else (2 if cfg["lba"] else 4)
+    NL, K = min(max(1, lanes), B), max(1, args.kf_every)
     if B % NL:
         raise SystemExit(f"--batch {B} is not a multiple of --lanes {NL}")
     # keyframe cadence: B/K new keyframes (LBA windows) per step; with fewer streams than K, one every K/B steps
