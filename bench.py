@@ -1195,6 +1195,13 @@ def main():
         try:
             tj = json.load(open(tpath))
             traffic, traffic_raw = tj.get(dom), tj.get("raw", {}).get(dom)
+            # the passes' launch shape (gpu_fast_pmc.sh: --lanes 1 --batch 64) scaled to this run's launches of
+            # tr.BL frames (the stage's bytes are per frame)
+            fl = float(tj.get("frames_per_launch", 64))
+            if traffic is not None:
+                traffic *= tr.BL / fl
+            if traffic_raw is not None:
+                traffic_raw *= tr.BL / fl
             pmc_counters = {k: tj.get(k, {}).get(dom) for k in ("valu_busy", "wave_frac_wait", "wave_frac_issue_stall")}
         except Exception:
             traffic = traffic_raw = None

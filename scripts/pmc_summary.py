@@ -51,6 +51,7 @@ def write_traffic(out, path):
     t = {"_note": "HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (separate rocprofv3 passes, KB): stage values "
                   "apply the gfx950 x2 FETCH_SIZE correction of MI355X_MICROARCH.md (exact for wide coalesced reads, "
                   "an upper bound for narrower loads); 'raw' holds the uncorrected lower bound",
+         "frames_per_launch": 64,   # scripts/gpu_fast_pmc.sh: --lanes 1 --batch 64 (bench.py scales to its launches)
          "raw": {}, "valu_busy": {}, "wave_frac_wait": {}, "wave_frac_issue_stall": {}}
     for stage, kern in STAGES.items():
         for name, e in out.items():
