@@ -1323,7 +1323,11 @@ def main():
             ms_solve, n_solve = lba_stage["solve"]
             tr_mean = float(np.mean(trials[:len(g0)]))
             ach = args.steps * tr_mean * sum(fl_ldlt) / (ms_solve * 1e-3) / 1e12 if ms_solve else None
-            mrel = "profiles/r04/lba_mfma_f64.json"
+            # the FP64-MFMA counter pass over the windows this leg solves (ring: profiles/r05's 32 ring windows;
+            # the synthetic world's windows: the round-4 pass over its batch of 32)
+            mrel = ("profiles/r05/lba_mfma_f64_ring.json" if args.lm_windows == "ring"
+                    and os.path.exists(os.path.join(ROOT, "profiles/r05/lba_mfma_f64_ring.json"))
+                    else "profiles/r04/lba_mfma_f64.json")
             mpath = os.path.join(ROOT, mrel)
             mfma = None
             if os.path.exists(mpath):

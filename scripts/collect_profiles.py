@@ -74,6 +74,8 @@ def main():
     cp(f"{rnd}lba_trace/run_kernel_stats.csv", os.path.join(P, "kernel_stats_lba_batch32.csv"))
     cp(f"{rnd}lba.json", os.path.join(P, "lba_pmc_batch32.json"))
     mfma(f"pmc_{rnd}lba", os.path.join(P, "lba_mfma_f64.json"))
+    cp(f"{rnd}lba_ring/run_kernel_stats.csv", os.path.join(P, "kernel_stats_lba_ring32.csv"))
+    mfma(f"pmc_{rnd}lba_ring", os.path.join(P, "lba_mfma_f64_ring.json"))
 
 
 if __name__ == "__main__":
