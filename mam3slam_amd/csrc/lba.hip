@@ -931,6 +931,9 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
 #define MAM_SCHUR_PF 2
 #endif
 constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per pass
+#ifndef MAM_SCHUR_FULL
+#define MAM_SCHUR_FULL 0   // a pair's two records loaded whole before its products (variant)
+#endif
 #ifndef MAM_SCHUR_T
 #define MAM_SCHUR_T 128   // lone window: 64 / 128 / 256 threads 23.0 / 21.9 / 24.5 us per launch
 #endif
@@ -1027,6 +1030,22 @@ __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ 
             const int2 pr = prs[u];
             const double* W = d.bdinv + 18 * (size_t)pr.x;
             const double* B = d.hpl + 18 * (size_t)pr.y;
+#if MAM_SCHUR_FULL
+            // both records loaded at once (9 16-byte loads each in flight together), then the products
+            double wf[18], bf[18];
+#pragma unroll
+            for (int q = 0; q < 9; q++) {
+                const double2 a = reinterpret_cast<const double2*>(W)[q], c = reinterpret_cast<const double2*>(B)[q];
+                wf[2 * q] = a.x; wf[2 * q + 1] = a.y;
+                bf[2 * q] = c.x; bf[2 * q + 1] = c.y;
+            }
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int c = 0; c < 6; c++)
+                    acc[6 * r + c] += wf[3 * r] * bf[3 * c] + wf[3 * r + 1] * bf[3 * c + 1] + wf[3 * r + 2] * bf[3 * c + 2];
+            continue;
+#endif
             // rows of W and of H_pl three at a time (9 doubles each): no spill at 152 VGPRs; the same products summed
             // in the same order per accumulator
 #pragma unroll
