@@ -932,7 +932,7 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
 #endif
 constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per pass
 #ifndef MAM_SCHUR_FULL
-#define MAM_SCHUR_FULL 0   // a pair's two records loaded whole before its products (variant)
+#define MAM_SCHUR_FULL 1   // a pair's two records loaded whole before its products (lone ring window 1.30 -> 1.26 ms; 0: in halves)
 #endif
 #ifndef MAM_SCHUR_T
 #define MAM_SCHUR_T 128   // lone window: 64 / 128 / 256 threads 23.0 / 21.9 / 24.5 us per launch
