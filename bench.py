@@ -602,30 +602,38 @@ def ring_lba_section(newmp, check=True):
     run's windows by the reference's window rule — each new keyframe with its covisible ring neighbours optimised and
     the other neighbours observing its MapPoints fixed, its keypoints' MapPoints and their observations from the run's
     forward Fuse matches, compacted — assembled on the device and solved by the batch device API; with check, window 0
-    against the oracle on the same graph. Outside the timed region: the timed
-    LocalMapping leg solves the shared synthetic map's windows, whose write-backs the exchange carries."""
+    against the oracle on the same graph. Standalone, after the timed region (whose LocalMapping leg solves the same
+    kind of windows beside Tracking): the assembly and the batch solve (incl. its size read-back) timed apart."""
     import torch
 
     from mam3slam_amd.mapping import RingLBA
 
     rl = RingLBA(newmp)
     torch.cuda.synchronize()
-    rl.assemble(newmp.stream)
-    rl.solve(newmp.stream)
-    reps = 3
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    for _ in range(3):   # warm (the solver context's arena, its trials-per-solve estimate for the read-back chunk)
         rl.assemble(newmp.stream)
         rl.solve(newmp.stream)
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / reps
+    reps, ms_asm, ms_solve = 5, 0.0, 0.0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rl.assemble(newmp.stream)
+        newmp.stream.synchronize()
+        t1 = time.perf_counter()
+        rl.solve(newmp.stream)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ms_asm += (t1 - t0) * 1e3 / reps
+        ms_solve += (t2 - t1) * 1e3 / reps
+    ms = ms_asm + ms_solve
     prob = rl.window(0)
     _, _, _, its, trials, st, ic, fc = rl.result(0)
     sz = rl.sizes   # per window: poses, points, edges, optimised poses (the compacted covisibility windows)
     res = {"windows": newmp.W, "rule": rl.rule, "covisibility_threshold": rl.COVIS_TH,
            "poses_mean": float(sz[:, 0].mean()), "optimised_poses_mean": float(sz[:, 3].mean()),
            "points_mean": float(sz[:, 1].mean()), "observations_mean": float(sz[:, 2].mean()),
-           "ms_per_batch": ms, "iterations": its, "trials": trials, "status": st, "chi2": [ic, fc],
+           "ms_per_batch": ms, "ms_assemble": ms_asm, "ms_solve": ms_solve, "iterations": its, "trials": trials,
+           "status": st, "chi2": [ic, fc],
            "trials_all": [t for _, t, _ in rl.stats]}
     if check:
         from oracle import oracle_py

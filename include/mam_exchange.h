@@ -145,7 +145,8 @@ int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn, int n_fixe
  * ones; points = the new keyframe's MapPoints seen by >= 2 keyframes; edges = their real observations only
  * (edge_active, when given, all 1). Per window: counts[4 w ..] = {poses, points, edges, optimised poses} (the
  * optimised poses first), pose_slot[w (nn + 1) + i] = ring slot of pose i, point_src[w S + i] = the new keyframe's
- * keypoint of point i. nn <= 31. */
+ * keypoint of point i. A neighbour keypoint claimed by several of the keyframe's MapPoints keeps the first claimant's
+ * observation only (the reference's Fuse merges such MapPoints, ORBmatcher.cc:1014-1122). nn <= 31, S * 8 <= 64 KiB. */
 int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, int nn, int covis_th, int n_fixed, const void* keys,
                                const int32_t* cnt, const void* tcw, const void* mps, int S, const int32_t* match,
                                const float* inv_level_sigma2, int nlevels, const mam_ring_window* outs, int32_t* counts,

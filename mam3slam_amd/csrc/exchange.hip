@@ -315,14 +315,13 @@ __global__ __launch_bounds__(RINGC_T) void k_ring_windows_covis(const RingArgs a
     extern __shared__ __attribute__((aligned(16))) uint32_t obsm[];   // [S]: bit k = observed by neighbour k
     __shared__ int wt[32], vpose[33], wsum[RINGC_T / 64], carry[2], hdr[4];
     const int w = blockIdx.x, t = threadIdx.x, nn = a.nn, S = a.S;
+    int* claim = reinterpret_cast<int*>(obsm + S);                    // [S]: a neighbour keypoint's first claimant
     const mam_ring_window& o = a.outs[w];
     const int j = a.pairs[2 * (w * nn)];
     const int n = min(max(a.cnt[2 * j], 0), S);
     if (t < 32) wt[t] = 0;
-    __syncthreads();
-    // observation masks and the covisibility weights (shared MapPoints per neighbour)
-    for (int p0 = 0; p0 < S; p0 += RINGC_T) {   // (uniform trip count: the ballots need every lane)
-        const int p = p0 + t;
+    // observation masks: the forward Fuse matches of the new keyframe's MapPoints in each neighbour
+    for (int p = t; p < S; p += RINGC_T) {
         uint32_t m = 0;
         if (p < n)
             for (int k = 0; k < nn; k++) {
@@ -330,7 +329,26 @@ __global__ __launch_bounds__(RINGC_T) void k_ring_windows_covis(const RingArgs a
                 const int idx = a.match[(size_t)(w * nn + k) * S + p];
                 if (idx >= 0 && idx < min(a.cnt[2 * nb], S)) m |= 1u << k;
             }
-        if (p < S) obsm[p] = m;
+        obsm[p] = m;
+    }
+    // one MapPoint per neighbour keypoint: when two of the keyframe's MapPoints claim the same keypoint of a
+    // neighbour, the reference's Fuse merges them (ORBmatcher.cc:1014-1122: the second finds the keypoint taken and
+    // Replace()s one by the other); here the first claimant (lowest MapPoint index) keeps the observation and the later
+    // claims are dropped
+    for (int k = 0; k < nn; k++) {
+        for (int q = t; q < S; q += RINGC_T) claim[q] = INT_MAX;
+        __syncthreads();
+        for (int p = t; p < n; p += RINGC_T)
+            if ((obsm[p] >> k) & 1u) atomicMin(&claim[a.match[(size_t)(w * nn + k) * S + p]], p);
+        __syncthreads();
+        for (int p = t; p < n; p += RINGC_T)
+            if (((obsm[p] >> k) & 1u) && claim[a.match[(size_t)(w * nn + k) * S + p]] != p) obsm[p] &= ~(1u << k);
+        __syncthreads();
+    }
+    // the covisibility weights (shared MapPoints per neighbour)
+    for (int p0 = 0; p0 < S; p0 += RINGC_T) {   // (uniform trip count: the ballots need every lane)
+        const int p = p0 + t;
+        const uint32_t m = p < S ? obsm[p] : 0u;
         for (int k = 0; k < nn; k++) {
             const int c = __popcll(__ballot((m >> k) & 1u));
             if ((t & 63) == 0 && c) atomicAdd(&wt[k], c);
@@ -455,7 +473,7 @@ extern "C" int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, i
         !cnt || !tcw ||
         !mps || !match || !inv_level_sigma2 || (n_windows > 0 && (!outs || !counts || !pose_slot || !point_src)))
         return MAM_ERR_ARG;
-    if ((size_t)S * 4 > 64 * 1024) return MAM_ERR_CAPACITY;
+    if ((size_t)S * 8 > 64 * 1024) return MAM_ERR_CAPACITY;
     if (n_windows == 0) return MAM_OK;
     mam::RingArgs a{};
     a.pairs = pairs;
@@ -470,7 +488,7 @@ extern "C" int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, i
     a.match = match;
     for (int l = 0; l < nlevels; l++) a.inv_s2[l] = inv_level_sigma2[l];
     a.outs = outs;
-    hipLaunchKernelGGL(mam::k_ring_windows_covis, dim3(n_windows), dim3(mam::RINGC_T), (size_t)S * 4,
+    hipLaunchKernelGGL(mam::k_ring_windows_covis, dim3(n_windows), dim3(mam::RINGC_T), (size_t)S * 8,
                        (hipStream_t)stream, a, covis_th, n_fixed, counts, pose_slot, point_src);
     MAM_HIP(hipGetLastError());
     return MAM_OK;

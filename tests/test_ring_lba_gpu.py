@@ -36,7 +36,8 @@ def test_ring_windows_covisibility_rule(gpu_lib, oracle, cfg, B, W):
     """The reference's window rule (Optimizer.cc:1118-1186) on the ring, compacted: local keyframes = the new keyframe
     + the neighbours sharing >= 15 of its MapPoints by weight (the heaviest when none does), fixed = the other
     neighbours that observe one (the n_fixed least covisible when that leaves none fixed), points = its MapPoints seen
-    by >= 2 keyframes, edges = their real observations — every array, the
+    by >= 2 keyframes, edges = their real observations, a neighbour keypoint claimed by several MapPoints kept by the
+    first — every array, the
     sizes and the slot / keypoint maps byte-exact against a host restatement from the ring buffers; the solve against
     the oracle on the assembled graph (identical Levenberg control flow, 1e-4)."""
     import torch
@@ -68,6 +69,13 @@ def test_ring_windows_covisibility_rule(gpu_lib, oracle, cfg, B, W):
         for k in range(NN):
             idx = match[w * NN + k, :n]
             mask[:, k] = (idx >= 0) & (idx < min(int(cnt[nbs[k]]), S))
+            # one MapPoint per neighbour keypoint: the first claimant keeps it (Fuse merges the others)
+            seen = set()
+            for p in range(n):
+                if mask[p, k]:
+                    if int(idx[p]) in seen:
+                        mask[p, k] = False
+                    seen.add(int(idx[p]))
         wt = mask.sum(0)
         order = sorted((k for k in range(NN) if wt[k] > 0), key=lambda k: (-wt[k], k))   # covisibility order
         nloc = sum(1 for k in order if wt[k] >= RingLBA.COVIS_TH)
