@@ -546,8 +546,9 @@ __device__ __forceinline__ void point_list_regs(const Prob& d, int h, int32_t* s
 }
 
 // grid (ceil(L/256) + Np, Q) x 256: restore edge order inside every list — per point its list sorted in registers (up
-// to 32 observations; longer lists by one thread in place), per pose a bitonic sort of its segment staged in LDS
-// (segments of up to 4096 edges; longer ones, global BA, by odd-even transposition in place). Windows of <= 64
+// to 32 observations; longer lists by one thread in place), per pose its segment ranked through a bitmap of the
+// problem's edge ids (segments of up to 4096 edges in problems of up to 262144; else a bitonic sort in LDS, and
+// longer segments, global BA, by odd-even transposition in place). Windows of <= 64
 // optimised poses collect the pair mask as LDS bit rows per workgroup (one device atomic per row present instead of a
 // byte store per observation pair: ~2.7M stores per batch of 32 ring windows), k_struct_tiles expands them.
 __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ probs) {
@@ -614,7 +615,49 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
     __shared__ int32_t seg[CH];
     int32_t* s = d.qe_idx + d.qe_off[h];
     const int n = d.qe_off[h + 1] - d.qe_off[h];
-    if (n <= CH) {
+    constexpr int BMW = 8192;   // bitmap words: problems of <= 262144 edges
+    if (n <= CH && d.E <= 32 * BMW) {
+        // the segment's edge ids (distinct, in [0, E)) as a bitmap over the problem's edges; an id's rank = the set
+        // bits before it: the per-thread word-range popcounts scanned once, then each id's rank from its own range.
+        // Five barriers (the bitonic network's 66 stages of ~1.2k cycles each took ~37 us for a 1.7k-edge pose).
+        __shared__ uint32_t bm[BMW];
+        __shared__ int tpre[256], wsum2[4];
+        const int t = threadIdx.x, nw = (d.E + 31) >> 5, per = (nw + 255) >> 8;
+        for (int i = t; i < nw; i += 256) bm[i] = 0u;
+        int ev[CH / 256];
+#pragma unroll
+        for (int u = 0; u < CH / 256; u++) ev[u] = t + 256 * u < n ? s[t + 256 * u] : -1;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < CH / 256; u++)
+            if (ev[u] >= 0) atomicOr(&bm[ev[u] >> 5], 1u << (ev[u] & 31));
+        __syncthreads();
+        const int w0 = t * per, w1 = min(nw, w0 + per);
+        int c = 0;
+        for (int w = w0; w < w1; w++) c += __popc(bm[w]);
+        int x = c;   // block exclusive scan of the per-thread counts
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if ((t & 63) >= o) x += y;
+        }
+        if ((t & 63) == 63) wsum2[t >> 6] = x;
+        __syncthreads();
+        int pre = x - c;
+        for (int wv = 0; wv < (t >> 6); wv++) pre += wsum2[wv];
+        tpre[t] = pre;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < CH / 256; u++) {
+            const int e = ev[u];
+            if (e < 0) continue;
+            const int w = e >> 5, own = w / per;
+            int r = tpre[own];
+            for (int q = own * per; q < w; q++) r += __popc(bm[q]);
+            r += __popc(bm[w] & ((1u << (e & 31)) - 1u));
+            s[r] = e;
+        }
+    } else if (n <= CH) {
         // a bitonic sort of the segment padded to a power of two with INT_MAX (a rank count over the segment was
         // O(n^2): ~270 us per batch of 32 ring windows, ~1.7k edges per pose)
         int np2 = 1;
