@@ -114,7 +114,9 @@ struct Prob {
     int32_t* eidx;               // [Np][L] edge of (pose block, point), never cleared: read through eidx_at
     uint8_t* pairmask;           // [Np][Np] (i1 < i2): the two poses share a landmark (S block non-zero)
     unsigned long long* pm_rows; // [64] (Np <= 64): pairmask row i1 as bits i2 (k_struct_sort; k_struct_tiles expands)
-    int32_t* blk_off;            // [Np * Np + 1] start of block (i1, i2)'s landmark pairs in blk_pair (i1 <= i2)
+    int32_t* blk_off;            // [Np * Np + 1] start of block (i1, i2)'s landmark pairs in blk_pair (i1 <= i2); with
+                                 // pair_fixed: the block's pair count, its pairs at the fixed offset i1 E + qe_off[i2]
+    int pair_fixed;              // the pair buffer at its E Np bound: blocks at fixed offsets (no count / scan pass)
     int2* blk_pair;              // (edge of pose i1, edge of pose i2) per shared landmark, i2's edge order
     uint8_t* tmask;              // [nt][nt] (r >= c): 16x16 tile (r, c) of L is structurally non-zero (S + fill)
     int16_t* tslot;              // [nt][nt]: the tile's slot in the LDS tile pool (ldlt_tiles), -1 structurally zero
@@ -1034,7 +1036,8 @@ __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ 
     // instead of a chain of five
     const int p1 = d.perm[i1], p2 = d.perm[i2];
     const bool nz = i1 == i2 || d.pairmask[(size_t)i1 * d.Np + i2];
-    const int k0 = d.blk_off[bx], k1 = d.blk_off[bx + 1];
+    const int k0 = d.pair_fixed ? i1 * d.E + d.qe_off[i2] : d.blk_off[bx];
+    const int k1 = d.pair_fixed ? k0 + d.blk_off[bx] : d.blk_off[bx + 1];
     const bool pool = lm.tiles_lds != 0;
     const int q36 = threadIdx.x < 36 ? threadIdx.x : 0;
     double hs = 0.0;
@@ -1242,9 +1245,15 @@ __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs)
     const int bx = blockIdx.x;
     if (bx >= d.Np * d.Np) return;
     const int i1 = bx / d.Np, i2 = bx % d.Np, lane = threadIdx.x;
-    if (!blk_nonzero(d, i1, i2)) return;
+    if (!blk_nonzero(d, i1, i2)) {
+        if (d.pair_fixed && lane == 0) d.blk_off[bx] = 0;
+        return;
+    }
     const int32_t* ei1 = d.eidx + (size_t)i1 * d.L;
-    int base = d.blk_off[bx];
+    // pair_fixed: the block's pairs at i1 E + qe_off[i2] (at most pose i2's edge count: the E Np buffer holds every
+    // block without a count pass), its count left in blk_off[bx]
+    const int base0 = d.pair_fixed ? i1 * d.E + d.qe_off[i2] : d.blk_off[bx];
+    int base = base0;
     const int end = d.qe_off[i2 + 1];
     // (every lane runs the batches of the longest lane: the ballots need the whole wave)
     for (int c0 = d.qe_off[i2]; c0 < end; c0 += 64 * BLK_PF) {
@@ -1258,6 +1267,7 @@ __global__ __launch_bounds__(64) void k_blk_fill(const Prob* __restrict__ probs)
             base += __popcll(m);
         }
     }
+    if (d.pair_fixed && lane == 0) d.blk_off[bx] = base - base0;
 }
 
 // grid (Q) x SB, after k_struct_sort: the 16x16 tile pattern of L. A tile of S is non-zero when it holds a pose
@@ -3459,6 +3469,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     for (int q = 0; q < Q; q++) {
         hp[q].lm = lms_d + q;
         hp[q].blk_pair = exact_pairs ? nullptr : c->blk_pairs.p + base;
+        hp[q].pair_fixed = exact_pairs ? 0 : 1;
         base += pair_cap[q];
     }
     std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
@@ -3481,8 +3492,10 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_struct_tiles, dim3(Q), dim3(SB), 0, s, P, (int)c->ldlt_lds_budget);
         // the S blocks' landmark pairs: counts, offsets, the pairs
         const dim3 gB(std::max(maxNp * maxNp, 1), Q);
-        hipLaunchKernelGGL(k_blk_count, gB, dim3(64), 0, s, P);
-        hipLaunchKernelGGL(k_blk_scan, dim3(1, Q), dim3(SB), 0, s, P);
+        if (exact_pairs) {   // (else the blocks sit at fixed offsets of the E Np buffer: k_blk_fill counts them)
+            hipLaunchKernelGGL(k_blk_count, gB, dim3(64), 0, s, P);
+            hipLaunchKernelGGL(k_blk_scan, dim3(1, Q), dim3(SB), 0, s, P);
+        }
         if (exact_pairs) {
             // the totals at blk_off[Np * Np] (a problem whose structure failed keeps status != 0 and fills nothing)
             std::vector<int32_t> tot(Q, 0);
