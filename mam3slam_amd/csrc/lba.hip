@@ -3086,11 +3086,49 @@ __global__ __launch_bounds__(64) void k_point_trial(const Prob* __restrict__ pro
     }
     double sc = 0.0;
     const int i = h0 + lane;
+    // one slot chunk: every slot's H_pl^T x_p term by its own lane (one round of loads for the chunk instead of a
+    // dependent walk over the point's slots by the point's lane), summed per point in slot order from LDS
+    __shared__ double cst[64 * 3];
+    if (one && !hd.fail) {
+        double c[3] = {0.0, 0.0, 0.0};
+        if (s0 + lane < s1) {
+            const int hp = d.slot_hp[s0 + lane];
+            if (hp >= 0) {
+                const double* B = d.hpl + 18 * (size_t)e_pf;
+                const double* xp = d.x + 6 * (size_t)hp;
+                double bv[18], xv6[6];
+#pragma unroll
+                for (int k = 0; k < 18; k++) bv[k] = B[k];
+#pragma unroll
+                for (int k = 0; k < 6; k++) xv6[k] = xp[k];
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    double v = bv[j] * xv6[0];
+#pragma unroll
+                    for (int k = 1; k < 6; k++) v += bv[3 * k + j] * xv6[k];
+                    c[j] = v;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) cst[3 * lane + j] = c[j];
+        __syncthreads();
+    }
     if (lane < PW && i < h1) {
         double* xl = d.x + 6 * (size_t)d.Np + 3 * (size_t)i;
         const double* bgl = d.b + 6 * (size_t)d.Np + 3 * (size_t)i;
         double xv[3];
-        if (!hd.fail) {
+        if (!hd.fail && one) {
+            double cl[3];
+            for (int k = 0; k < 3; k++) cl[k] = bgl[k];
+            const int sa = d.pe_off[i], sz = d.pe_off[i + 1];
+            for (int sb = sa; sb < sz; sb++)
+#pragma unroll
+                for (int j = 0; j < 3; j++) cl[j] -= cst[3 * (sb - s0) + j];
+            const double* Di = d.Dinv + 9 * (size_t)i;
+            for (int k = 0; k < 3; k++) xv[k] = Di[3 * k] * cl[0] + Di[3 * k + 1] * cl[1] + Di[3 * k + 2] * cl[2];
+            for (int k = 0; k < 3; k++) xl[k] = xv[k];
+        } else if (!hd.fail) {
             double cl[3];
             for (int k = 0; k < 3; k++) cl[k] = bgl[k];
             const int s1 = d.pe_off[i + 1];
