@@ -117,6 +117,7 @@ struct Prob {
     int32_t* blk_off;            // [Np * Np + 1] start of block (i1, i2)'s landmark pairs in blk_pair (i1 <= i2); with
                                  // pair_fixed: the block's pair count, its pairs at the fixed offset i1 E + qe_off[i2]
     int pair_fixed;              // the pair buffer at its E Np bound: blocks at fixed offsets (no count / scan pass)
+    int pw;                      // points per k_point_sys / k_point_trial workgroup of this batch (PW or PW_SMALL)
     int2* blk_pair;              // (edge of pose i1, edge of pose i2) per shared landmark, i2's edge order
     uint8_t* tmask;              // [nt][nt] (r >= c): 16x16 tile (r, c) of L is structurally non-zero (S + fill)
     int16_t* tslot;              // [nt][nt]: the tile's slot in the LDS tile pool (ldlt_tiles), -1 structurally zero
@@ -2757,7 +2758,16 @@ __device__ __forceinline__ void se3_exp_mul(const double u[6], const double* T, 
 // lanes take slots for the per-edge work and lanes < PW take points for the per-point sums, handing over through LDS
 // inside the wave, where the separate kernels of before (linearize, sys, schur_prep / backsub_update, trial
 // linearize) each paid a launch and its dependent global round trips.
-constexpr int PW = 8;   // points per wave (a window's points have <= 8 observations: one 64-slot chunk)
+#ifndef MAM_PW
+#define MAM_PW 8
+#endif
+constexpr int PW = MAM_PW;   // points per wave (a window's points have <= 8 observations: one 64-slot chunk)
+#ifndef MAM_PW_SMALL
+#define MAM_PW_SMALL 2
+#endif
+// lone windows of many observations per point: 2 points per wave (4x the point workgroups of its few trial kernels,
+// each with a quarter of the dependent work; run_batch's choice)
+constexpr int PW_SMALL = MAM_PW_SMALL;
 
 // S's pose part at an iteration start: H_pp, b_p of Hessian pose block h — k_sys's sums (lanes strided over the pose's
 // edge list in edge order, the same products, the same fixed-order wave reduction) on Jacobian terms recomputed from
@@ -2842,10 +2852,11 @@ __device__ __forceinline__ void dinv_of(const double H[9], double lambda, double
 //    (k_sys's sums); every trial D^-1 = (H_ll + lambda I)^-1 per point and, per slot, W = H_pl D^-1 and the
 //    coefficients H_pl D^-1 b_l (k_schur_prep's products);
 //  pose waves — at an iteration start H_pp, b_p in POSE_SPLIT partial sums per pose (pose_sys_wave).
+template <int PWT>
 __device__ __forceinline__ void point_sys_body(const Prob& d, const LMHead& hd) {
     if (hd.status || hd.done) return;
     const bool lin = hd.need_lin && !hd.sys_ready;
-    const int nbp = (d.L + PW - 1) / PW;
+    const int nbp = (d.L + PWT - 1) / PWT;
     const double* pose = d.pose[hd.cur];
     const double* pts = d.pt[hd.cur];
     if ((int)blockIdx.x >= nbp) {
@@ -2855,13 +2866,13 @@ __device__ __forceinline__ void point_sys_body(const Prob& d, const LMHead& hd) 
     }
     const int lane = threadIdx.x;
     const double lambda = trial_lambda(hd);
-    const int h0 = blockIdx.x * PW, h1 = min(d.L, h0 + PW);
+    const int h0 = blockIdx.x * PWT, h1 = min(d.L, h0 + PWT);
     const int s0 = d.pe_off[h0], s1 = d.pe_off[h1];
     const bool one = s1 - s0 <= 64;   // one slot chunk: the slots' H_pl stay in registers for the W products
     __shared__ double cs[64 * 12];    // per slot: its H_ll (9) and b_l (3) terms
-    __shared__ double pdv[PW * 12];   // per point: D^-1 (9), D^-1 b_l (3)
+    __shared__ double pdv[PWT * 12];   // per point: D^-1 (9), D^-1 b_l (3)
     const int hl = h0 + lane;
-    const bool plane = lane < PW && hl < h1;
+    const bool plane = lane < PWT && hl < h1;
     const int ps0 = plane ? d.pe_off[hl] : 0, ps1 = plane ? d.pe_off[hl + 1] : 0;
     double H[9], bl[3], hr[18];
 #pragma unroll
@@ -2981,7 +2992,7 @@ __device__ __forceinline__ void point_sys_body(const Prob& d, const LMHead& hd) 
 // T) and the factorization epilogue's pose part
 template <int T>
 __device__ void trial_sums(const Prob& d, double* s, double* tempChi, double* scale0) {
-    const int nbp = (d.L + PW - 1) / PW;
+    const int nbp = (d.L + d.pw - 1) / d.pw;   // k_point_trial's workgroups (d.pw points each)
     double acc[RED / T], acs[RED / T];
 #pragma unroll
     for (int v = 0; v < RED / T; v++) {
@@ -3048,9 +3059,10 @@ __device__ void ctl_step(LM& lm, const LMHead& hd, double tempChi, double scale0
     }
 }
 
+template <int PWT>
 __global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
-    point_sys_body(d, lm_head(d.lm));
+    point_sys_body<PWT>(d, lm_head(d.lm));
 }
 
 // grid (ceil(L / PW), Q) x 64, after the factorization and its pose epilogue (the trial poses): per point (lanes < PW)
@@ -3058,19 +3070,20 @@ __global__ __launch_bounds__(64) void k_point_sys(const Prob* __restrict__ probs
 // factorization, which leaves the old x), the trial point X + x_l and its computeScale terms x_l (lambda x_l + b_l);
 // per slot the trial error of its edge at the trial pose and point (k_linearize's trial pass), summed per wave into
 // the chi2 partial of the trial
+template <int PWT>
 __global__ __launch_bounds__(64) void k_point_trial(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     const LMHead hd = lm_head(d.lm);
     if (hd.status || hd.done) return;
-    const int nbp = (d.L + PW - 1) / PW;
+    const int nbp = (d.L + PWT - 1) / PWT;
     if ((int)blockIdx.x >= nbp) return;
     const int lane = threadIdx.x;
     const double lambda = trial_lambda(hd);
     const double* pts = d.pt[hd.cur];
     double* pt_out = d.pt[1 - hd.cur];
     const double* pose_out = d.pose[1 - hd.cur];
-    const int h0 = blockIdx.x * PW, h1 = min(d.L, h0 + PW);
-    __shared__ double xn[PW * 3];
+    const int h0 = blockIdx.x * PWT, h1 = min(d.L, h0 + PWT);
+    __shared__ double xn[PWT * 3];
     // the trial-error pass's slot edge, its pose and that pose's trial value loaded before the back-substitution (one
     // 64-slot chunk, a window's points): their round trips overlap it instead of following the barrier
     const int s0 = d.pe_off[h0], s1 = d.pe_off[h1];
@@ -3114,7 +3127,7 @@ __global__ __launch_bounds__(64) void k_point_trial(const Prob* __restrict__ pro
         for (int j = 0; j < 3; j++) cst[3 * lane + j] = c[j];
         __syncthreads();
     }
-    if (lane < PW && i < h1) {
+    if (lane < PWT && i < h1) {
         double* xl = d.x + 6 * (size_t)d.Np + 3 * (size_t)i;
         const double* bgl = d.b + 6 * (size_t)d.Np + 3 * (size_t)i;
         double xv[3];
@@ -3354,7 +3367,8 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.pt[1] = cv.take<double>(3 * (size_t)d.L);
     d.err = cv.take<double>(2 * (size_t)d.E);
     d.jac = cv.take<double>(21 * (size_t)d.E);
-    const size_t np = (size_t)std::max((d.E + 63) / 64, (d.L + mam::lba::PW - 1) / mam::lba::PW) + 1;
+    const int pwm = std::min(mam::lba::PW, mam::lba::PW_SMALL);
+    const size_t np = (size_t)std::max((d.E + 63) / 64, (d.L + pwm - 1) / pwm) + 1;
     d.part = cv.take<double>(np);
     d.part0 = cv.take<double>(np);
     d.part_s = cv.take<double>(np);
@@ -3504,10 +3518,20 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     Carver cv{c->arena.p};
     for (auto& d : hp) carve_scratch(cv, d);
     size_t base = 0;
+    // points per k_point_sys / k_point_trial workgroup: PW_SMALL for a lone window whose points have many observations
+    // (a covisibility ring window, ~12 a point: 1.23 -> 1.11 ms), PW otherwise (a window of ~8 observations a point
+    // fills PW = 8 points' 64 slots exactly: 1.23 ms, 1.28 at PW_SMALL; batches are throughput-bound: PW)
+    size_t sumE = 0, sumL = 0;
+    for (int q = 0; q < Q; q++) {
+        sumE += (size_t)hp[q].E;
+        sumL += (size_t)hp[q].L;
+    }
+    const int pw_batch = (Q <= 2 && sumL > 0 && (double)sumE > 10.0 * (double)sumL) ? PW_SMALL : PW;
     for (int q = 0; q < Q; q++) {
         hp[q].lm = lms_d + q;
         hp[q].blk_pair = exact_pairs ? nullptr : c->blk_pairs.p + base;
         hp[q].pair_fixed = exact_pairs ? 0 : 1;
+        hp[q].pw = pw_batch;   // (the launches below take the same)
         base += pair_cap[q];
     }
     std::memcpy(c->lm_host.p, hp.data(), sizeof(Prob) * Q);
@@ -3569,7 +3593,8 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipLaunchKernelGGL(k_sys, gSys, dim3(64), 0, s, P);
         hipLaunchKernelGGL(k_ctl_init, dim3(Q), dim3(RED), 0, s, P);
     }
-    const int nbp = std::max((maxL + PW - 1) / PW, 1);
+    const int pw = pw_batch;
+    const int nbp = std::max((maxL + pw - 1) / pw, 1);
     const dim3 gPts(nbp + maxNp * POSE_SPLIT, Q), gTri(nbp, Q);
     const dim3 gBlk(maxNp * (maxNp + 1) / 2 + maxNp > 0 ? maxNp * (maxNp + 1) / 2 + maxNp : 1, Q);
     const int maxPL = std::max(maxP, maxL);
@@ -3609,7 +3634,10 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
-            hipLaunchKernelGGL(k_point_sys, gPtsg, dim3(64), 0, st, Pg);
+            if (pw == PW_SMALL)
+                hipLaunchKernelGGL(k_point_sys<PW_SMALL>, gPtsg, dim3(64), 0, st, Pg);
+            else
+                hipLaunchKernelGGL(k_point_sys<PW>, gPtsg, dim3(64), 0, st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 1);
@@ -3624,7 +3652,10 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
-            hipLaunchKernelGGL(k_point_trial, gTrig, dim3(64), 0, st, Pg);
+            if (pw == PW_SMALL)
+                hipLaunchKernelGGL(k_point_trial<PW_SMALL>, gTrig, dim3(64), 0, st, Pg);
+            else
+                hipLaunchKernelGGL(k_point_trial<PW>, gTrig, dim3(64), 0, st, Pg);
             hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
     };
