@@ -1404,8 +1404,9 @@ def main():
             if lat is not None:
                 # the north star's per-frame figure: ORBextractor (the host-API call a Frame constructor makes, B = 1)
                 # + a lone LocalBundleAdjustment window every K frames, GPU vs the oracle on the same inputs. With a
-                # LocalMapping leg the window is one of its timed-region windows; without one (c1) the same-shape
-                # 50-keyframe window of the synthetic map at this config's camera, its oracle time and parity here
+                # LocalMapping leg the window is one of its timed-region windows; without one (c1) a 50-keyframe window
+                # of the synthetic map (BASELINE configs[2]'s LBA shape) at this config's camera, its oracle time and
+                # parity here
                 from mam3slam_amd.lba import LBASolver
 
                 win_note = "the same timed-region window"
@@ -1422,7 +1423,8 @@ def main():
                     ro = oracle_py.lba_solve(prob)
                     lba_cpu = (time.perf_counter() - t1) * 1e3
                     win_note = (f"a 50-keyframe window of the synthetic map ({len(prob.pose_id)} KF incl. fixed, "
-                                f"{len(prob.point_id)} MapPoints, {len(prob.edge_point)} edges; c2's window shape) "
+                                f"{len(prob.point_id)} MapPoints, {len(prob.edge_point)} edges; the 50-KF LBA shape of BASELINE "
+                                f"configs[2]) "
                                 f"at this config's camera")
                 sol = LBASolver(device=dev.index or 0)
                 rg = sol.solve(prob)
