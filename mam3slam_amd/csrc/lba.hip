@@ -2768,6 +2768,8 @@ constexpr int PW = MAM_PW;   // points per wave (a window's points have <= 8 obs
 // lone windows of many observations per point: 2 points per wave (4x the point workgroups of its few trial kernels,
 // each with a quarter of the dependent work; run_batch's choice)
 constexpr int PW_SMALL = MAM_PW_SMALL;
+static_assert((PW == 2 || PW == 4 || PW == 8) && (PW_SMALL == 2 || PW_SMALL == 4 || PW_SMALL == 8),
+              "the point kernels are instantiated for 2, 4 and 8 points per workgroup");
 
 // S's pose part at an iteration start: H_pp, b_p of Hessian pose block h — k_sys's sums (lanes strided over the pose's
 // edge list in edge order, the same products, the same fixed-order wave reduction) on Jacobian terms recomputed from
@@ -3367,7 +3369,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.pt[1] = cv.take<double>(3 * (size_t)d.L);
     d.err = cv.take<double>(2 * (size_t)d.E);
     d.jac = cv.take<double>(21 * (size_t)d.E);
-    const int pwm = std::min(mam::lba::PW, mam::lba::PW_SMALL);
+    const int pwm = 2;   // (the fewest points per workgroup any launch takes)
     const size_t np = (size_t)std::max((d.E + 63) / 64, (d.L + pwm - 1) / pwm) + 1;
     d.part = cv.take<double>(np);
     d.part0 = cv.take<double>(np);
@@ -3526,7 +3528,11 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         sumE += (size_t)hp[q].E;
         sumL += (size_t)hp[q].L;
     }
-    const int pw_batch = (Q <= 2 && sumL > 0 && (double)sumE > 10.0 * (double)sumL) ? PW_SMALL : PW;
+    int pw_batch = (Q <= 2 && sumL > 0 && (double)sumE > 10.0 * (double)sumL) ? PW_SMALL : PW;
+    if (const char* e = std::getenv("MAM_LBA_PW")) {   // experiments: force 2, 4 or 8 points per workgroup
+        const int v = std::atoi(e);
+        if (v == 2 || v == 4 || v == 8) pw_batch = v;
+    }
     for (int q = 0; q < Q; q++) {
         hp[q].lm = lms_d + q;
         hp[q].blk_pair = exact_pairs ? nullptr : c->blk_pairs.p + base;
@@ -3634,10 +3640,12 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
-            if (pw == PW_SMALL)
-                hipLaunchKernelGGL(k_point_sys<PW_SMALL>, gPtsg, dim3(64), 0, st, Pg);
+            if (pw == 2)
+                hipLaunchKernelGGL(k_point_sys<2>, gPtsg, dim3(64), 0, st, Pg);
+            else if (pw == 4)
+                hipLaunchKernelGGL(k_point_sys<4>, gPtsg, dim3(64), 0, st, Pg);
             else
-                hipLaunchKernelGGL(k_point_sys<PW>, gPtsg, dim3(64), 0, st, Pg);
+                hipLaunchKernelGGL(k_point_sys<8>, gPtsg, dim3(64), 0, st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 1);
@@ -3652,10 +3660,12 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
-            if (pw == PW_SMALL)
-                hipLaunchKernelGGL(k_point_trial<PW_SMALL>, gTrig, dim3(64), 0, st, Pg);
+            if (pw == 2)
+                hipLaunchKernelGGL(k_point_trial<2>, gTrig, dim3(64), 0, st, Pg);
+            else if (pw == 4)
+                hipLaunchKernelGGL(k_point_trial<4>, gTrig, dim3(64), 0, st, Pg);
             else
-                hipLaunchKernelGGL(k_point_trial<PW>, gTrig, dim3(64), 0, st, Pg);
+                hipLaunchKernelGGL(k_point_trial<8>, gTrig, dim3(64), 0, st, Pg);
             hipLaunchKernelGGL(k_ctl_end, dim3(Qg), dim3(RED), 0, st, Pg);
         }
     };
