@@ -165,6 +165,20 @@ def test_lba_batch_same_shape(solver, oracle):
         assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
 
 
+@pytest.mark.parametrize("pw", ["2", "4", "8"])
+def test_lba_points_per_workgroup(solver, oracle, pw, monkeypatch):
+    """The point kernels at 2 / 4 / 8 points per workgroup (a lone window of many observations a point takes 2, batches
+    8; MAM_LBA_PW forces one): the same Levenberg control flow and solution as the oracle at each."""
+    monkeypatch.setenv("MAM_LBA_PW", pw)
+    prob = synthetic_problem(n_opt=21, n_fixed=10, n_points=1200, obs_per_point=14, seed=31, init_kf_local=False)
+    rg, ro = solver.solve(prob), oracle.lba_solve(prob)
+    assert rg.status == 0 and ro.status == 0
+    assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials)
+    assert abs(rg.final_chi2 - ro.final_chi2) <= 1e-6 * ro.final_chi2
+    assert _rel(rg.pose_t, ro.pose_t) <= 1e-4 and _rel(rg.pose_q, ro.pose_q) <= 1e-4
+    assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
+
+
 def test_lba_size_bound(solver):
     """A problem whose dense pose x landmark table would exceed 4 GiB (1100 optimised poses x 1M points) is refused
     with MAM_ERR_CAPACITY and a message naming the sizes, before any scratch allocation."""
