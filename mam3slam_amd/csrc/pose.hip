@@ -46,6 +46,10 @@ struct Cfg {
 #ifndef MAM_POSE_BUILD_UNROLL
 #define MAM_POSE_BUILD_UNROLL 2
 #endif
+// 1: every wave runs the serial LM step itself (no wave-0 solve + LDS broadcast); an experiment switch
+#ifndef MAM_POSE_STEP_ALL_WAVES
+#define MAM_POSE_STEP_ALL_WAVES 0
+#endif
 #ifndef MAM_POSE_CHI_UNROLL
 #define MAM_POSE_CHI_UNROLL 2
 #endif
@@ -594,7 +598,7 @@ __device__ int optimize(const Edges& E, double T[7], const mam_camera& c, bool r
             PPROF(4, tp);   // LM control since the last pass
             bool ok2;
             double Tn[7];
-            if constexpr (NW > 4) {
+            if constexpr (NW > 4 && !MAM_POSE_STEP_ALL_WAVES) {
                 // more waves than SIMDs: the serial step on wave 0 only (redundant copies would share its SIMD's
                 // issue slots), x / Tn / the verdict broadcast through LDS
                 __shared__ double s_step[14];
