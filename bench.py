@@ -45,7 +45,10 @@ CONFIGS = {
     # BASELINE.json configs[1]: single-agent mono 640x480, 1000 features, 8 levels, extract + match
     "c1": dict(width=640, height=480, nfeatures=1000, lba=False),
     # BASELINE.json configs[2]: 1280x720, 2000 features + LocalBundleAdjustment (50 KF / ~3000 MapPoints windows)
-    "c2": dict(width=1280, height=720, nfeatures=2000, lba=True),
+    # path: 16 px of travel and 0.25 deg of roll per frame over a 4096-px wider scene — keyframes 8 frames apart are
+    # 128 px apart, so a keyframe shares MapPoints with the ~50 keyframes around it and not with the far ones (the
+    # covisibility graph LocalBundleAdjustment's window rule needs: local and fixed keyframes)
+    "c2": dict(width=1280, height=720, nfeatures=2000, lba=True, path=(16.0, 0.25, 4096)),
     # BASELINE.json configs[3]: the testMultiAgentSystem agents (test/settingsForTest_00.yaml: KannalaBrandt8, 700
     # features) at 640x480, two agents in total (both on one GPU at --gpus 1, one per GPU at --gpus 2)
     # pool_frames: the two streams' keyframes over 16 steps are 32 distinct views (synth.frame_pose at the fisheye's
@@ -204,10 +207,12 @@ class TrackingLeg:
         # (the fisheye's views at the canvas scale of its own focal length: the texture as dense in its image centre as
         # in a Pinhole frame of make_frame, not minified ~2.3x into a mass of FAST corners)
         fscene = float(cam.fx) if cam.is_kb8 else 500.0
+        path = cfg.get("path")   # the camera path over the scene (synth.DEFAULT_MOTION unless the config sets one)
         if cam.is_kb8:
-            frames = np.stack([synth.make_frame_camera(W, H, cam, agent=rank, frame=k, f=fscene) for k in fidx])
+            frames = np.stack([synth.make_frame_camera(W, H, cam, agent=rank, frame=k, f=fscene, path=path)
+                               for k in fidx])
         else:
-            frames = np.stack([synth.make_frame(W, H, agent=rank, frame=k) for k in fidx])
+            frames = np.stack([synth.make_frame(W, H, agent=rank, frame=k, path=path) for k in fidx])
         self.d_img_pool = torch.from_numpy(frames).to(dev)
         self.d_img = self.d_img_pool[:B].clone() if P > 1 else self.d_img_pool
         self.d_kps = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)
@@ -248,7 +253,7 @@ class TrackingLeg:
             # the pose of the camera that rendered the frame (synth.frame_pose: the canvas as a plane in front of a
             # translating, rolling camera), so keyframes' poses and image content agree (SearchForTriangulation's
             # epipolar tests between keyframes pass for real correspondences, KannalaBrandt8 included)
-            F.pose = synth.frame_pose(W, H, fidx[f], f=fscene)
+            F.pose = synth.frame_pose(W, H, fidx[f], f=fscene, path=path)
             F0 = F0 or F
             # the last frame's and the local map's MapPoints re-project onto the frame's keypoints under that pose:
             # 45 % of the keypoints each (together ~70 % of the frame tracked, as ORB-SLAM's monocular tracking keeps
@@ -598,12 +603,12 @@ def ingest_section(tr, reps=5):
 
 
 def ring_lba_section(newmp, check=True):
-    """LocalBundleAdjustment over the keyframes this run's Tracking inserted (mapping.RingLBA): the last keyframe
-    run's windows by the reference's window rule — each new keyframe with its covisible ring neighbours optimised and
-    the other neighbours observing its MapPoints fixed, its keypoints' MapPoints and their observations from the run's
-    forward Fuse matches, compacted — assembled on the device and solved by the batch device API; with check, window 0
-    against the oracle on the same graph. Standalone, after the timed region (whose LocalMapping leg solves the same
-    kind of windows beside Tracking): the assembly and the batch solve (incl. its size read-back) timed apart."""
+    """LocalBundleAdjustment of the last LocalMapping run's keyframes (mapping.RingLBA over the device map): each new
+    keyframe's window by the reference's rule — local = the keyframe + its covisible keyframes, local MapPoints = every
+    MapPoint of every local keyframe, fixed = their other observers — assembled on the device and solved by the batch
+    device API, standalone after the timed region (whose LocalMapping leg assembles and solves the same windows beside
+    Tracking; no write-back here), assembly and solve (incl. its size read-back) timed apart; with check, the first
+    solved window against the oracle on the same graph."""
     import torch
 
     from mam3slam_amd.mapping import RingLBA
@@ -626,21 +631,24 @@ def ring_lba_section(newmp, check=True):
         ms_asm += (t1 - t0) * 1e3 / reps
         ms_solve += (t2 - t1) * 1e3 / reps
     ms = ms_asm + ms_solve
-    prob = rl.window(0)
-    _, _, _, its, trials, st, ic, fc = rl.result(0)
-    sz = rl.sizes   # per window: poses, points, edges, optimised poses (the compacted covisibility windows)
-    res = {"windows": newmp.W, "rule": rl.rule, "covisibility_threshold": rl.COVIS_TH,
+    v = rl.valid
+    sz = rl.sizes[v] if v else np.zeros((1, 4))   # per solved window: poses, points, edges, optimised poses
+    res = {"windows": newmp.W, "windows_solved": len(v), "rule": "covisibility (device map)",
+           "covisibility_threshold": rl.COVIS_TH,
            "poses_mean": float(sz[:, 0].mean()), "optimised_poses_mean": float(sz[:, 3].mean()),
            "points_mean": float(sz[:, 1].mean()), "observations_mean": float(sz[:, 2].mean()),
-           "ms_per_batch": ms, "ms_assemble": ms_asm, "ms_solve": ms_solve, "iterations": its, "trials": trials,
-           "status": st, "chi2": [ic, fc],
+           "ms_per_batch": ms, "ms_assemble": ms_asm, "ms_solve": ms_solve,
            "trials_all": [t for _, t, _ in rl.stats]}
-    if check:
+    if check and v:
         from oracle import oracle_py
 
+        w = v[0]
+        prob = rl.window(w)
+        _, _, _, its, trials, st, ic, fc = rl.result(w)
         ro = oracle_py.lba_solve(prob)
-        q, t, x = rl.result(0)[:3]
+        q, t, x = rl.result(w)[:3]
         rel = float(np.abs(x - ro.point_xyz).max() / max(np.abs(ro.point_xyz).max(), 1e-12))
+        res.update({"iterations": its, "trials": trials, "status": st, "chi2": [ic, fc]})
         res["oracle_same_control_flow"] = (its, trials) == (ro.iterations, ro.lm_trials)
         res["oracle_max_point_rel_diff"] = rel
     return res
@@ -731,7 +739,7 @@ def parity_section(tr, mapping, newmp=None):
         out["fuse_index_exact"] = bool(ok)
         out["fuse_items"] = {"forward_fused": fused[0], "backward_fused": fused[1]}
     if mapping is not None:
-        w = 0
+        w = mapping.first_valid() if hasattr(mapping, "first_valid") else 0
         prob = mapping.window_inputs(w)
         rg = mapping.window_result(w)
         t0 = time.perf_counter()
@@ -854,11 +862,10 @@ def cpu_baseline(tr, cfg, lba_window_ms, K, seconds=10.0, newmp=None):
             t2 = time.perf_counter()
             oracle_py.fuse(KF, mps, tr.cam, 3.0)
             sin_ms += (time.perf_counter() - t2) * 1e3
-        off = newmp.upd_off.cpu().numpy()
-        n1 = newmp.upd_n // newmp.W
-        descs = newmp.upd_desc[:int(off[n1])].cpu().numpy()
+        # ComputeDistinctiveDescriptors of the keyframe's MapPoints (their observations' descriptors from the map)
+        off, descs = newmp.distinctive_inputs(newmp.head)
         t2 = time.perf_counter()
-        oracle_py.distinctive_descriptors(off[:n1 + 1], descs)
+        oracle_py.distinctive_descriptors(off, descs)
         sin_ms += (time.perf_counter() - t2) * 1e3
         per_frame_ms += (tri_ms + bow_ms + sin_ms) / K
     ext_ms, ext_scalar_ms = ext_s * 1e3 / n, ext_scalar_s * 1e3 / n
@@ -992,16 +999,20 @@ def main():
 
     lba_ev = []   # (start, end) events of each LocalMapping run on its stream
 
-    def mapping_worker(step_idx, head):
-        # LocalMapping per new keyframe: ComputeBoW + CreateNewMapPoints' 30 SearchForTriangulation (the keyframes the
-        # previous tracking steps inserted; started on the leg's stream when they were ingested), then the
-        # LocalBundleAdjustment windows after them and the queued pack / all-gather / apply of their write-backs: the
-        # run's span on the LocalMapping stream, from events recorded around it (the exchange tail included)
+    def mapping_worker(step_idx, item):
+        # one LocalMapping run (LocalMapping::Run for the keyframes one step inserted), serial on LocalMapping's
+        # stream: the keyframes into the ring, ComputeBoW, MapPointCulling, CreateNewMapPoints, SearchInNeighbors and
+        # their map edits (NewMapPointsLeg.process), then the LocalBundleAdjustment windows, their solve and
+        # write-back and the exchange of the write-back (RingMappingLeg.run; the world leg: its synthetic map's
+        # windows) — the run's span on the stream from events recorded around it (the exchange tail included)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t_m = time.perf_counter()
         e0.record(mapping.stream)
-        newmp.wait(mapping.stream, head)
-        mapping.run(step_idx, head=head)
+        if args.lm_windows == "ring":
+            mapping.run(step_idx, item)
+        else:
+            newmp.process(mapping.stream, item)
+            mapping.run(step_idx)
         e1.record(mapping.stream)
         lba_ev.append((e0, e1))
         host_s["mapping_run"] += time.perf_counter() - t_m
@@ -1044,23 +1055,25 @@ def main():
 
     def step():
         t_a = time.perf_counter()
-        if mapping is not None and step_no[0] % map_every == 0:
+        tr.step()
+        t_b = time.perf_counter()
+        t_c = t_b
+        if mapping is not None and (step_no[0] + 1) % map_every == 0:
+            # the step's new keyframes into a staging set (tracking stream), then the run queued for LocalMapping's
+            # thread: put blocks while one run is in progress and one waits (Tracking blocks when LocalMapping falls
+            # two runs behind)
+            item = newmp.ingest(step_no[0])
             if worker[0] is None:
                 worker[0] = threading.Thread(target=mapping_loop, daemon=True)
                 worker[0].start()
             if failure:
                 raise failure[0]
-            runs.put((step_no[0] // map_every, newmp.take()))
-        t_b = time.perf_counter()
-        tr.step()
-        t_c = time.perf_counter()
-        if mapping is not None and (step_no[0] + 1) % map_every == 0:
-            newmp.ingest(step_no[0])
-            newmp.launch(newmp.pending)
+            t_c = time.perf_counter()
+            runs.put((step_no[0] // map_every, item))
         t_d = time.perf_counter()
-        host_s["queue_wait"] += t_b - t_a
-        host_s["tracking_launch"] += t_c - t_b
-        host_s["keyframe_ingest_launch"] += t_d - t_c
+        host_s["tracking_launch"] += t_b - t_a
+        host_s["keyframe_ingest_launch"] += t_c - t_b
+        host_s["queue_wait"] += t_d - t_c
         step_no[0] += 1
 
     for _ in range(args.warmup):
@@ -1083,9 +1096,10 @@ def main():
         raise RuntimeError(f"device error codes in outputs: {nm1.min()} {nm2.min()} {cnt[:, 0].min()}")
 
     def set_profiling(on):
-        # LocalMapping's per-stage HIP events (8 event records per LM trial on the LBA stream, 2 per search batch)
-        # and the all-gather's wall time
+        # LocalMapping's per-stage HIP events (8 event records per LM trial on the LBA stream, 2 per search batch,
+        # the map edits') and the all-gather's wall time
         mapping.time_gather = on
+        newmp.profile = on
         mapping.solver.set_profiling(on)
         newmp.matcher.set_profiling(on)
         newmp.voc.set_profiling(on)
@@ -1152,8 +1166,12 @@ def main():
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
-        for i in range(args.steps):
-            mapping.run(10_000 + i)
+        for i in range(args.steps):   # the last run's keyframes again (re-inserted: the same LocalMapping work)
+            if args.lm_windows == "ring":
+                mapping.run(10_000 + i)
+            else:
+                newmp.process(mapping.stream, newmp.last_item)
+                mapping.run(10_000 + i)
         torch.cuda.synchronize(dev)
         lm_only = (time.perf_counter() - t1) * 1e3 / args.steps
         overlap = {"combined_ms_per_step": el * 1e3 / args.steps, "tracking_only_ms_per_step": tr_only,
@@ -1238,13 +1256,16 @@ def main():
                          f"ComputeBoW + 30 SearchForTriangulation (CreateNewMapPoints) + SearchInNeighbors (Fuse both ways + "
                          f"ComputeDistinctiveDescriptors) and ")
             if args.lm_windows == "ring":
-                sz = mapping.rl.sizes
-                workload += (f"a LocalBundleAdjustment window of the keyframe by the reference's window rule over "
-                             f"the keyframes the step tracked (covisible: ~{float(np.mean(sz[:, 3])):.1f} optimised "
-                             f"KF + {float(np.mean(sz[:, 0] - sz[:, 3])):.1f} fixed, ~{int(np.mean(sz[:, 1]))} "
-                             f"MapPoints, ~{int(np.mean(sz[:, 2]))} observations), batched, concurrent with "
-                             f"tracking; write-backs exchanged (all-gather) and applied to the shared map every GPU "
-                             f"holds")
+                sz = mapping.rl.sizes[mapping.rl.valid]
+                workload += (f"MapPoint creation, Fuse's Replace / AddObservation and the MapPoints' descriptor / "
+                             f"normal / depth update on the device map the ring's keyframes share, and a "
+                             f"LocalBundleAdjustment window of the keyframe by the reference's window rule over that "
+                             f"map (local = the keyframe + its covisible keyframes, ~{float(np.mean(sz[:, 3])):.1f} "
+                             f"optimised KF; every MapPoint of every local keyframe, ~{int(np.mean(sz[:, 1]))}; "
+                             f"fixed = their other observers, {float(np.mean(sz[:, 0] - sz[:, 3])):.1f} KF; "
+                             f"~{int(np.mean(sz[:, 2]))} observations), batched, its write-back (outlier erase, poses, "
+                             f"positions, normals / depth ranges) applied to the map, concurrent with tracking; "
+                             f"write-backs exchanged (all-gather) and applied to the replica every GPU holds")
             else:
                 workload += (f"a LocalBundleAdjustment window (50 KF + fixed, "
                              f"~{int(np.mean([len(p.point_id) for p in mapping.probs]))} MapPoints) of the synthetic "
@@ -1292,15 +1313,22 @@ def main():
                 parity["ring_lba_same_control_flow"] = ring.get("oracle_same_control_flow")
                 parity["ring_lba_max_point_rel_diff"] = ring.get("oracle_max_point_rel_diff")
         if mapping is not None:
-            its = [s[0] for s in mapping.stats]
-            trials = [s[1] for s in mapping.stats]
-            E = float(np.mean(mapping.edges))
-            L = float(np.mean([len(p.point_id) for p in mapping.probs]))
-            Np = float(np.mean([int((p.pose_fixed == 0).sum()) for p in mapping.probs]))
+            # the last run's solved windows (a window without fixed keyframes is not solved: Optimizer.cc:1182-1185)
+            vw = list(mapping.rl.valid) if args.lm_windows == "ring" else list(range(mapping.W))
+            probs_v = [mapping.probs[w] for w in vw]
+            its = [mapping.stats[w][0] for w in vw]
+            trials = [mapping.stats[w][1] for w in vw]
+            E = float(np.mean([mapping.edges[w] for w in vw]))
+            L = float(np.mean([len(p.point_id) for p in probs_v]))
+            Np = float(np.mean([int((p.pose_fixed == 0).sum()) for p in probs_v]))
             fl = lba_flops(E, L, Np, E / L, float(np.mean(trials)), float(np.mean(its)))
             spans = lba_ms()
             solve_ms = float(np.mean(spans)) if spans else None
-            out["lba"] = {"windows_per_step": mapping.W, "ms_per_step_span": solve_ms,
+            if args.lm_windows == "ring":
+                nkr, nmr, xst = mapping.exchange_counts()
+            else:
+                nkr, nmr, xst = mapping.n_kf_upd, mapping.n_mp_upd, 0
+            out["lba"] = {"windows_per_step": mapping.W, "windows_solved_last_run": len(vw), "ms_per_step_span": solve_ms,
                           "ms_per_window_span": solve_ms / mapping.W if solve_ms else None,
                           "span_note": "LocalMapping run per step on its stream (events around it: the keyframe "
                                        "searches it waits on, the LBA windows, the pack / all-gather / apply of "
@@ -1308,25 +1336,27 @@ def main():
                           "iterations_mean": float(np.mean(its)), "trials_mean": float(np.mean(trials)),
                           "edges_per_window": E, "points_per_window": L, "opt_keyframes": Np,
                           "algorithmic_gflop_per_window": fl / 1e9,
-                          "achieved_fp64_tflops": (fl * mapping.W) / (solve_ms * 1e-3) / 1e12 if solve_ms else None,
+                          "achieved_fp64_tflops": (fl * len(vw)) / (solve_ms * 1e-3) / 1e12 if solve_ms else None,
                           "fp64_peak_tflops": FP64_PEAK_TFS,
                           "stage_ms_total": {k: v[0] for k, v in lba_stage.items()},
                           "stage_launches": {k: v[1] for k, v in lba_stage.items()},
                           "exchange_bytes_per_step": int(mapping.exch.send.numel() * world),
                           "exchange": {"bytes_per_rank_block": int(mapping.exch.block_bytes),
-                                       "keyframe_records": mapping.n_kf_upd, "mappoint_records": mapping.n_mp_upd,
+                                       "keyframe_records": nkr, "mappoint_records": nmr, "status": xst,
                                        "bytes_per_window": mapping.exch.block_bytes / mapping.W,
                                        "allgather_ms_median": float(np.median(mapping.exch.gather_ms))
                                        if mapping.exch.gather_ms else None,
                                        "note": "one fixed-size all_gather_into_tensor per step of each GPU's "
-                                               "deduplicated write-back (32-B KeyFrame, 16-B MapPoint records); "
+                                               "deduplicated write-back (32-B KeyFrame records; MapPoint records: "
+                                               "48 B with normal and depth range on the device map, 16 B on the "
+                                               "world leg); "
                                                "gather time = host wall around the collective with the stream "
                                                "synchronised, from the untimed profiling pass"}}
             # the LocalBundleAdjustment's roofline: its dominant kernel, the tile LDL^T (one workgroup per window,
             # FP64 MFMA), from the profiled pass's solve-stage events (the first stream group's launches: windows
             # [0, Q / G) of the batch) and the tile structure of those windows
-            G = 2 if mapping.W >= 4 else 1
-            g0 = mapping.probs[:mapping.W // G]
+            G = 2 if len(vw) >= 4 else 1
+            g0 = probs_v[:len(vw) // G]
             fl_ldlt = [ldlt_tile_flops(p) for p in g0]
             ms_solve, n_solve = lba_stage["solve"]
             tr_mean = float(np.mean(trials[:len(g0)]))
@@ -1371,15 +1401,19 @@ def main():
                 "fused_per_forward_fuse": float(newmp.fwd_n.float().mean().item()),
                 "fused_per_backward_fuse": float(newmp.bwd_n.float().mean().item()),
                 "candidate_pairs_per_search": tri_b["candidate_pairs"] / newmp.npairs,
+                "map_edits_ms_last_profiled_run": newmp.profiled_map_ms(),
+                "map": newmp.map.stats(),
                 "algorithmic_bytes_per_step_triangulation": tri_b["bytes"],
                 "achieved_GBs_triangulation": tri_b["bytes"] / (tri_ms * 1e-3) / 1e9 if tri_ms > 0 else None,
-                "note": "ComputeBoW (levelsup 4, synthetic k=10 L=6 vocabulary) + CreateNewMapPoints' "
-                        "SearchForTriangulation against the 30 nearest keyframes of the agent's sequence + "
-                        "SearchInNeighbors (Fuse into the 30, Fuse of 4 neighbours' MapPoints back, "
-                        "ComputeDistinctiveDescriptors), on their own stream as "
-                        "soon as the keyframes are ingested, before the LBA windows of the same keyframes (stage "
-                        "times on that stream, concurrent with tracking, from a second untimed pass of the same steps "
-                        "with the HIP events on; --profile-timed records them inside the timed region); algorithmic bytes per SURVEY §8(d): "
+                "note": "ComputeBoW (levelsup 4, synthetic k=10 L=6 vocabulary) + MapPointCulling + "
+                        "CreateNewMapPoints' SearchForTriangulation against the 30 nearest older keyframes of the "
+                        "agent's sequence and the MapPoints of its matches + SearchInNeighbors (Fuse into the 30, Fuse "
+                        "of 4 neighbours' MapPoints back, Replace / AddObservation, ComputeDistinctiveDescriptors + "
+                        "UpdateNormalAndDepth) on the device map, on LocalMapping's stream before the LBA windows of "
+                        "the same keyframes (stage times on that stream, concurrent with tracking, from a second "
+                        "untimed pass of the same steps with the HIP events on; --profile-timed records them inside "
+                        "the timed region; map: MapPoints alive, observations per MapPoint, MapPoints per keyframe); "
+                        "algorithmic bytes per SURVEY §8(d): "
                         "sum over shared BoW nodes of |f1| x |f2| x 32 B of descriptors + the two FeatureVectors' "
                         "keypoints, flags and keys (the last run's pairs)"}
         if pose_info is not None:
@@ -1412,7 +1446,7 @@ def main():
                 win_note = "the same timed-region window"
                 win_parity = None
                 if mapping is not None:
-                    prob = mapping.probs[0]
+                    prob = probs_v[0]
                 else:
                     from mam3slam_amd import world as WD
                     from oracle import oracle_py

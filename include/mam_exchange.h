@@ -112,45 +112,8 @@ int mam_map_perturb(float* kf_table, int64_t kf_rows, const int64_t* kf_idx, int
                     int64_t mp_rows, const int64_t* mp_idx, int n_mp, uint64_t seed, float sigma_q, float sigma_t,
                     float sigma_x, int32_t* status, void* stream);
 
-/* ---- LocalBundleAdjustment windows from the keyframes Tracking inserted (Optimizer.cc:1118-1331 on the device
- * keyframe ring of the harness): window w = keyframe pairs[w nn][0] (pose 0, optimised) and its nn neighbours
- * pairs[w nn + k][1] (poses 1 .. nn, nearest first; the last n_fixed of them fixed), its MapPoints = its keypoints'
- * scene points (mps[kf][p], p < its keypoint count), and per MapPoint the observations: its own keypoint and the
- * neighbours' keypoints match[(w nn + k) S + p] (Fuse's forward matches: the keypoint of neighbour k the MapPoint
- * projects onto, -1 none). Fixed problem shape: S points x (nn + 1) edge slots per point, edge e = p (nn + 1) + v on
- * pose v, inactive (edge_active 0) where there is no observation and for every edge of a MapPoint with fewer than two
- * observations (a 3-DoF point needs two views); obs = the keypoint (x, y), inv_sigma2 = inv_level_sigma2[octave].
- * Estimates: the keyframes' tracked Tcw and the MapPoints' positions, float cast to double. DEVICE arrays throughout
- * (outs: a device array of n_windows descriptors); inv_level_sigma2: host, nlevels <= 8. Asynchronous. */
-typedef struct mam_ring_window {
-    double* pose_q;                      /* [nn + 1][4] */
-    double* pose_t;                      /* [nn + 1][3] */
-    uint8_t* pose_fixed;                 /* [nn + 1] */
-    double* point_xyz;                   /* [S][3] */
-    int32_t* edge_point;                 /* [S (nn + 1)] */
-    int32_t* edge_pose;
-    double* edge_obs;                    /* [S (nn + 1)][2] */
-    double* edge_inv_sigma2;
-    uint8_t* edge_active;
-} mam_ring_window;
-
-int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn, int n_fixed, const void* keys, const int32_t* cnt,
-                         const void* tcw, const void* mps, int S, const int32_t* match, const float* inv_level_sigma2,
-                         int nlevels, const mam_ring_window* outs, void* stream);
-
-/* The same windows by the reference's window rule (Optimizer.cc:1118-1186), compacted: local keyframes = the new
- * keyframe + its covisible ring neighbours by weight (weight = shared MapPoints >= covis_th, KeyFrame::UpdateConnections'
- * 15; the heaviest when none reaches it), fixed = every other neighbour observing one of its MapPoints — and when that
- * leaves none fixed (where the reference skips the LBA, Optimizer.cc:1179-1183), the n_fixed least covisible local
- * ones; points = the new keyframe's MapPoints seen by >= 2 keyframes; edges = their real observations only
- * (edge_active, when given, all 1). Per window: counts[4 w ..] = {poses, points, edges, optimised poses} (the
- * optimised poses first), pose_slot[w (nn + 1) + i] = ring slot of pose i, point_src[w S + i] = the new keyframe's
- * keypoint of point i. A neighbour keypoint claimed by several of the keyframe's MapPoints keeps the first claimant's
- * observation only (the reference's Fuse merges such MapPoints, ORBmatcher.cc:1014-1122). nn <= 31, S * 8 <= 64 KiB. */
-int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, int nn, int covis_th, int n_fixed, const void* keys,
-                               const int32_t* cnt, const void* tcw, const void* mps, int S, const int32_t* match,
-                               const float* inv_level_sigma2, int nlevels, const mam_ring_window* outs, int32_t* counts,
-                               int32_t* pose_slot, int32_t* point_src, void* stream);
+/* The LocalBundleAdjustment windows of the keyframes Tracking inserted are built on the device map
+ * (include/mam_ringmap.h: mam_ringmap_windows, the reference's window rule over MapPoints shared by the keyframes). */
 
 #ifdef __cplusplus
 }

@@ -17,7 +17,7 @@ LIB = os.path.join(HERE, "libmam_gpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # Translation units linked into libmam_gpu.so (each includes its own kernels).
-SOURCES = ["orb_extract.hip", "match.hip", "lba.hip", "exchange.hip", "pose.hip", "bow.hip", "streams.hip"]
+SOURCES = ["orb_extract.hip", "match.hip", "lba.hip", "exchange.hip", "pose.hip", "bow.hip", "streams.hip", "ringmap.hip"]
 
 FLAGS = [
     "--offload-arch=gfx950",

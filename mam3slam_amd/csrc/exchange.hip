@@ -208,291 +208,7 @@ __global__ __launch_bounds__(256) void k_perturb(float* __restrict__ kf, int64_t
     }
 }
 
-// ---- LBA windows from the keyframe ring: grid (ceil(S / 64), n_windows) x 64, one thread per MapPoint (its nn + 1
-// edge slots, the poses by the first threads of each window)
-struct RingArgs {
-    const int32_t* pairs;
-    int nn, n_fixed, S, nlevels;
-    const mam_keypoint* keys;
-    const int32_t* cnt;
-    const float* tcw;    // [R][7]: q xyzw, t
-    const float* mps;    // [R][S][20] (mam_fuse_mp: pos first)
-    const int32_t* match;
-    float inv_s2[8];
-    const mam_ring_window* outs;
-};
-
-__global__ __launch_bounds__(64) void k_ring_windows(const RingArgs a) {
-    const int w = blockIdx.y, p = blockIdx.x * 64 + threadIdx.x;
-    const mam_ring_window& o = a.outs[w];
-    const int NV = a.nn + 1;
-    const int j = a.pairs[2 * (w * a.nn)];
-    if (p < NV) {
-        const int slot = p == 0 ? j : a.pairs[2 * (w * a.nn + p - 1) + 1];
-        const float* T = a.tcw + 7 * (size_t)slot;
-        for (int k = 0; k < 4; k++) o.pose_q[4 * p + k] = (double)T[k];
-        for (int k = 0; k < 3; k++) o.pose_t[3 * p + k] = (double)T[4 + k];
-        o.pose_fixed[p] = p >= NV - a.n_fixed ? 1 : 0;
-    }
-    if (p >= a.S) return;
-    const int n = min(max(a.cnt[2 * j], 0), a.S);
-    const bool valid = p < n;
-    const float* M = a.mps + ((size_t)j * a.S + p) * 20;
-    for (int k = 0; k < 3; k++) o.point_xyz[3 * (size_t)p + k] = valid ? (double)M[k] : 0.0;
-    // the observations: count first (a MapPoint seen by fewer than two keyframes is left out), then the slots
-    int nobs = valid ? 1 : 0;
-    if (valid)
-        for (int k = 0; k < a.nn; k++) {
-            const int nb = a.pairs[2 * (w * a.nn + k) + 1];
-            const int idx = a.match[(size_t)(w * a.nn + k) * a.S + p];
-            nobs += (idx >= 0 && idx < min(a.cnt[2 * nb], a.S)) ? 1 : 0;
-        }
-    const bool keep = nobs >= 2;
-    for (int v = 0; v < NV; v++) {
-        const size_t e = (size_t)p * NV + v;
-        int slot = j, idx = p;
-        if (v > 0) {
-            slot = a.pairs[2 * (w * a.nn + v - 1) + 1];
-            idx = valid ? a.match[(size_t)(w * a.nn + v - 1) * a.S + p] : -1;
-            if (idx >= min(a.cnt[2 * slot], a.S)) idx = -1;
-        } else if (!valid) {
-            idx = -1;
-        }
-        const bool act = keep && idx >= 0;
-        o.edge_point[e] = p;
-        o.edge_pose[e] = v;
-        o.edge_active[e] = act ? 1 : 0;
-        if (act) {
-            const mam_keypoint& kp = a.keys[(size_t)slot * a.S + idx];
-            o.edge_obs[2 * e] = (double)kp.x;
-            o.edge_obs[2 * e + 1] = (double)kp.y;
-            o.edge_inv_sigma2[e] = (double)a.inv_s2[min(max(kp.octave, 0), a.nlevels - 1)];
-        } else {
-            o.edge_obs[2 * e] = 0.0;
-            o.edge_obs[2 * e + 1] = 0.0;
-            o.edge_inv_sigma2[e] = 1.0;
-        }
-    }
-}
-
-// ---- LBA windows by the reference's window rule, compacted: grid (n_windows) x 256, one workgroup per window.
-// Optimizer::LocalBundleAdjustment (Optimizer.cc:1118-1186): the local keyframes are the new keyframe and its
-// covisible keyframes (GetVectorCovisibleKeyFrames: the connections KeyFrame::UpdateConnections keeps, weight = shared
-// MapPoints >= 15, or the heaviest one when none reaches it, KeyFrame.cc:312-380), the local MapPoints those the new
-// keyframe observes (the ring's MapPoints are the new keyframe's; a point seen by fewer than two keyframes is left
-// out, as the fixed-shape form did), the fixed keyframes every other keyframe observing a local MapPoint. Poses: the
-// new keyframe, its covisible keyframes by weight, then the fixed ones; points in keypoint order; edges
-// point-major (the new keyframe's observation first, then the neighbours' in neighbour order) — only real
-// observations, no inactive slots. counts[w] = {poses, points, edges, optimised poses}; pose_slot[w][i] the ring slot
-// of pose i, point_src[w][i] the keypoint (MapPoint row of the new keyframe) of point i.
-constexpr int RINGC_T = 256;
-__device__ __forceinline__ int ringc_excl_scan(int v, int* wsum, int& total) {
-    // block exclusive scan of RINGC_T values (wave inclusive scans by shuffle, then the wave totals)
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(x, o, 64);
-        if (lane >= o) x += u;
-    }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    int pre = 0;
-    total = 0;
-#pragma unroll
-    for (int w = 0; w < RINGC_T / 64; w++) {
-        const int t = wsum[w];
-        if (w < wid) pre += t;
-        total += t;
-    }
-    __syncthreads();
-    return pre + x - v;
-}
-
-__global__ __launch_bounds__(RINGC_T) void k_ring_windows_covis(const RingArgs a, int covis_th, int n_fixed,
-                                                                int32_t* counts, int32_t* pose_slot,
-                                                                int32_t* point_src) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t obsm[];   // [S]: bit k = observed by neighbour k
-    __shared__ int wt[32], vpose[33], wsum[RINGC_T / 64], carry[2], hdr[4];
-    const int w = blockIdx.x, t = threadIdx.x, nn = a.nn, S = a.S;
-    int* claim = reinterpret_cast<int*>(obsm + S);                    // [S]: a neighbour keypoint's first claimant
-    const mam_ring_window& o = a.outs[w];
-    const int j = a.pairs[2 * (w * nn)];
-    const int n = min(max(a.cnt[2 * j], 0), S);
-    if (t < 32) wt[t] = 0;
-    // observation masks: the forward Fuse matches of the new keyframe's MapPoints in each neighbour
-    for (int p = t; p < S; p += RINGC_T) {
-        uint32_t m = 0;
-        if (p < n)
-            for (int k = 0; k < nn; k++) {
-                const int nb = a.pairs[2 * (w * nn + k) + 1];
-                const int idx = a.match[(size_t)(w * nn + k) * S + p];
-                if (idx >= 0 && idx < min(a.cnt[2 * nb], S)) m |= 1u << k;
-            }
-        obsm[p] = m;
-    }
-    // one MapPoint per neighbour keypoint: when two of the keyframe's MapPoints claim the same keypoint of a
-    // neighbour, the reference's Fuse merges them (ORBmatcher.cc:1014-1122: the second finds the keypoint taken and
-    // Replace()s one by the other); here the first claimant (lowest MapPoint index) keeps the observation and the later
-    // claims are dropped
-    for (int k = 0; k < nn; k++) {
-        for (int q = t; q < S; q += RINGC_T) claim[q] = INT_MAX;
-        __syncthreads();
-        for (int p = t; p < n; p += RINGC_T)
-            if ((obsm[p] >> k) & 1u) atomicMin(&claim[a.match[(size_t)(w * nn + k) * S + p]], p);
-        __syncthreads();
-        for (int p = t; p < n; p += RINGC_T)
-            if (((obsm[p] >> k) & 1u) && claim[a.match[(size_t)(w * nn + k) * S + p]] != p) obsm[p] &= ~(1u << k);
-        __syncthreads();
-    }
-    // the covisibility weights (shared MapPoints per neighbour)
-    for (int p0 = 0; p0 < S; p0 += RINGC_T) {   // (uniform trip count: the ballots need every lane)
-        const int p = p0 + t;
-        const uint32_t m = p < S ? obsm[p] : 0u;
-        for (int k = 0; k < nn; k++) {
-            const int c = __popcll(__ballot((m >> k) & 1u));
-            if ((t & 63) == 0 && c) atomicAdd(&wt[k], c);
-        }
-    }
-    __syncthreads();
-    // the window's keyframes (thread 0, <= 31 neighbours): the neighbours by covisibility weight, heaviest first (ties
-    // by neighbour order: GetVectorCovisibleKeyFrames' order), the covisible ones (>= covis_th, or the heaviest when none
-    // reaches it) local, the other observers fixed; with no fixed keyframe left the reference skips the LBA
-    // (Optimizer.cc:1179-1183) — here the n_fixed least covisible local ones are fixed instead, the gauge anchor the
-    // fixed cameras are
-    if (t == 0) {
-        int ord[32];
-        int no = 0;
-        for (int k = 0; k < nn; k++) {
-            if (wt[k] <= 0) continue;
-            int i = no++;
-            while (i > 0 && wt[ord[i - 1]] < wt[k]) { ord[i] = ord[i - 1]; i--; }
-            ord[i] = k;
-        }
-        int nloc = 0;
-        while (nloc < no && wt[ord[nloc]] >= covis_th) nloc++;
-        if (nloc == 0 && no > 0) nloc = 1;
-        if (nloc == no) nloc = max(no - n_fixed, min(no, 1));
-        for (int k = 0; k <= nn; k++) vpose[k] = -1;
-        vpose[0] = 0;
-        for (int i = 0; i < no; i++) vpose[1 + ord[i]] = 1 + i;
-        hdr[0] = 1 + no;
-        hdr[1] = 1 + nloc;
-    }
-    __syncthreads();
-    const int np = hdr[0], nopt = hdr[1];
-    if (t <= nn) {
-        const int v = t, pi = vpose[v];
-        if (pi >= 0) {
-            const int slot = v == 0 ? j : a.pairs[2 * (w * nn + v - 1) + 1];
-            const float* T = a.tcw + 7 * (size_t)slot;
-            for (int k = 0; k < 4; k++) o.pose_q[4 * pi + k] = (double)T[k];
-            for (int k = 0; k < 3; k++) o.pose_t[3 * pi + k] = (double)T[4 + k];
-            o.pose_fixed[pi] = pi >= nopt ? 1 : 0;
-            pose_slot[(size_t)w * (nn + 1) + pi] = slot;
-        }
-    }
-    // points (kept: observed by the new keyframe and at least one neighbour) and their edges, compacted in order
-    if (t == 0) { carry[0] = 0; carry[1] = 0; }
-    __syncthreads();
-    for (int p0 = 0; p0 < S; p0 += RINGC_T) {
-        const int p = p0 + t;
-        const uint32_t m = p < S ? obsm[p] : 0u;
-        const bool keep = m != 0;
-        const int ne = keep ? 1 + __popc(m) : 0;
-        int tp, te;
-        const int pi = ringc_excl_scan(keep ? 1 : 0, wsum, tp) + carry[0];
-        const int e0 = ringc_excl_scan(ne, wsum, te) + carry[1];
-        if (keep) {
-            const float* M = a.mps + ((size_t)j * S + p) * 20;
-            for (int k = 0; k < 3; k++) o.point_xyz[3 * (size_t)pi + k] = (double)M[k];
-            point_src[(size_t)w * S + pi] = p;
-            int e = e0;
-            for (int v = 0; v <= nn; v++) {
-                if (v > 0 && !((m >> (v - 1)) & 1u)) continue;
-                const int slot = v == 0 ? j : a.pairs[2 * (w * nn + v - 1) + 1];
-                const int idx = v == 0 ? p : a.match[(size_t)(w * nn + v - 1) * S + p];
-                const mam_keypoint& kp = a.keys[(size_t)slot * S + idx];
-                o.edge_point[e] = pi;
-                o.edge_pose[e] = vpose[v];
-                o.edge_obs[2 * (size_t)e] = (double)kp.x;
-                o.edge_obs[2 * (size_t)e + 1] = (double)kp.y;
-                o.edge_inv_sigma2[e] = (double)a.inv_s2[min(max(kp.octave, 0), a.nlevels - 1)];
-                if (o.edge_active) o.edge_active[e] = 1;
-                e++;
-            }
-        }
-        __syncthreads();
-        if (t == 0) { carry[0] += tp; carry[1] += te; }
-        __syncthreads();
-    }
-    if (t == 0) {
-        counts[4 * w] = np;
-        counts[4 * w + 1] = carry[0];
-        counts[4 * w + 2] = carry[1];
-        counts[4 * w + 3] = nopt;
-    }
-}
-
 }  // namespace mam
-
-extern "C" int mam_ring_lba_windows(int n_windows, const int32_t* pairs, int nn, int n_fixed, const void* keys,
-                                    const int32_t* cnt, const void* tcw, const void* mps, int S, const int32_t* match,
-                                    const float* inv_level_sigma2, int nlevels, const mam_ring_window* outs,
-                                    void* stream) {
-    if (n_windows < 0 || nn < 1 || n_fixed < 0 || n_fixed > nn || S < 1 || nlevels < 1 || nlevels > 8 || !pairs ||
-        !keys || !cnt || !tcw || !mps || !match || !inv_level_sigma2 || (n_windows > 0 && !outs))
-        return MAM_ERR_ARG;
-    if (n_windows == 0) return MAM_OK;
-    mam::RingArgs a{};
-    a.pairs = pairs;
-    a.nn = nn;
-    a.n_fixed = n_fixed;
-    a.S = S;
-    a.nlevels = nlevels;
-    a.keys = reinterpret_cast<const mam_keypoint*>(keys);
-    a.cnt = cnt;
-    a.tcw = reinterpret_cast<const float*>(tcw);
-    a.mps = reinterpret_cast<const float*>(mps);
-    a.match = match;
-    for (int l = 0; l < nlevels; l++) a.inv_s2[l] = inv_level_sigma2[l];
-    a.outs = outs;
-    const int np = std::max(S, nn + 1);
-    hipLaunchKernelGGL(mam::k_ring_windows, dim3((np + 63) / 64, n_windows), dim3(64), 0, (hipStream_t)stream, a);
-    MAM_HIP(hipGetLastError());
-    return MAM_OK;
-}
-
-extern "C" int mam_ring_lba_windows_covis(int n_windows, const int32_t* pairs, int nn, int covis_th, int n_fixed,
-                                          const void* keys,
-                                          const int32_t* cnt, const void* tcw, const void* mps, int S,
-                                          const int32_t* match, const float* inv_level_sigma2, int nlevels,
-                                          const mam_ring_window* outs, int32_t* counts, int32_t* pose_slot,
-                                          int32_t* point_src, void* stream) {
-    if (n_windows < 0 || nn < 1 || nn > 31 || n_fixed < 0 || S < 1 || nlevels < 1 || nlevels > 8 || !pairs || !keys ||
-        !cnt || !tcw ||
-        !mps || !match || !inv_level_sigma2 || (n_windows > 0 && (!outs || !counts || !pose_slot || !point_src)))
-        return MAM_ERR_ARG;
-    if ((size_t)S * 8 > 64 * 1024) return MAM_ERR_CAPACITY;
-    if (n_windows == 0) return MAM_OK;
-    mam::RingArgs a{};
-    a.pairs = pairs;
-    a.nn = nn;
-    a.n_fixed = 0;
-    a.S = S;
-    a.nlevels = nlevels;
-    a.keys = reinterpret_cast<const mam_keypoint*>(keys);
-    a.cnt = cnt;
-    a.tcw = reinterpret_cast<const float*>(tcw);
-    a.mps = reinterpret_cast<const float*>(mps);
-    a.match = match;
-    for (int l = 0; l < nlevels; l++) a.inv_s2[l] = inv_level_sigma2[l];
-    a.outs = outs;
-    hipLaunchKernelGGL(mam::k_ring_windows_covis, dim3(n_windows), dim3(mam::RINGC_T), (size_t)S * 8,
-                       (hipStream_t)stream, a, covis_th, n_fixed, counts, pose_slot, point_src);
-    MAM_HIP(hipGetLastError());
-    return MAM_OK;
-}
 
 extern "C" int mam_copy_rows(int n_tables, const mam_row_table* tables, int n, const int32_t* src_rows,
                              const int32_t* dst_rows, const int32_t* flag_a, const int32_t* flag_b, int64_t flag_stride,

@@ -28,12 +28,6 @@ _SIGS = {
                                 C.c_int, C.c_void_p, C.c_int64, C.c_void_p]),
     "mam_map_perturb": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_int,
                                   C.c_uint64, C.c_float, C.c_float, C.c_float, C.c_void_p, C.c_void_p]),
-    "mam_ring_lba_windows": (C.c_int, [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                                       C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
-    "mam_ring_lba_windows_covis": (C.c_int, [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                                             C.c_void_p,
-                                             C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
-                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
 }
 
 # compact blocks (include/mam_exchange.h): header | KeyFrame records | MapPoint records

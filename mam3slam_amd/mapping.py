@@ -197,73 +197,90 @@ class LocalMappingLeg:
 
 
 class NewMapPointsLeg:
-    """LocalMapping::ProcessNewKeyFrame's ComputeBoW and CreateNewMapPoints' SearchForTriangulation against the new
-    keyframe's 30 neighbours (LocalMapping.cc:504-582, nn = 30 for monocular; ORBmatcher(0.6, false): no rotation
-    check), for the W keyframes the agents on this GPU insert per step, on the device.
+    """LocalMapping's keyframe work on the device, for the W keyframes the agents on this GPU insert per LocalMapping
+    run (LocalMapping::Run, LocalMapping.cc:95-172, one run = the step's W new keyframes): ProcessNewKeyFrame's
+    ComputeBoW (DBoW2 transform, synthetic k=10 L=6 vocabulary — ORBvoc.txt is a missing blob), MapPointCulling,
+    CreateNewMapPoints (SearchForTriangulation against the keyframe's NN = 30 neighbours, LocalMapping.cc:504-582,
+    ORBmatcher(0.6, false), and the MapPoints of its matches) and SearchInNeighbors (Fuse of the keyframe's MapPoints
+    into its neighbours, Fuse of its NB_BACK nearest neighbours' MapPoints into it, and the Replace / AddObservation
+    side effects, ComputeDistinctiveDescriptors + UpdateNormalAndDepth of its MapPoints, LocalMapping.cc:830-939) —
+    the searches on the matcher kernels, the map edits on the device map (ringmap.RingMap, include/mam_ringmap.h).
 
-    The keyframes live in a ring of R slots in HBM (keypoints, descriptors, MapPoint flags, pose, BoW node + weight at
-    levelsup 4): `ingest` copies the step's new keyframes out of the tracking buffers (on the tracking stream, after
-    the step that tracked them: the reference's Tracking -> LocalMapping hand-off); `run` computes their BoW (DBoW2
-    transform, synthetic k=10 L=6 vocabulary — ORBvoc.txt is a missing blob) and searches each against its 30
-    neighbours (the synthetic map has no covisibility graph: the keyframes nearest in the agent's frame sequence stand
-    in for the best covisible ones; the keyframes' poses are those of the camera that rendered them,
-    synth.frame_pose, refined by Tracking's PoseOptimization); then SearchInNeighbors (LocalMapping.cc:830-939):
-    Fuse of the keyframe's MapPoints into its 30 neighbours, Fuse of the neighbours' fuse candidates into the keyframe
-    and ComputeDistinctiveDescriptors of its MapPoints (`search_in_neighbors`). The triangulation and MapPoint creation that follow the search (LocalMapping.cc:590-828) are
-    outside the hot path; the map's new MapPoints enter through LocalMappingLeg.new_keyframes."""
+    The keyframes live in a ring of R slots in HBM (keypoints, descriptors, pose, BoW node + weight, and per keypoint
+    the scene point a new MapPoint made there gets: `fmp`, the stand-in for the triangulated position); the map's
+    MapPoints are shared across the slots (RingMap: mp_of / okp / records). `ingest` copies a step's new keyframes out
+    of the tracking buffers into a staging set (on the tracking stream, after the step that tracked them: the
+    reference's Tracking -> LocalMapping hand-off); `process` (on LocalMapping's stream) moves them into the next W
+    ring slots — the keyframes there leave the map (KeyFrame::SetBadFlag) — and runs the keyframe work. A new
+    keyframe's neighbours (GetBestCovisibilityKeyFrames(30) for a camera moving through one scene) are the NN older
+    ring keyframes nearest to it along the agent's frame sequence (same view last; ties: the more recent first);
+    the W keyframes of one run see the map as the run started (they are processed together, as concurrent agents'
+    LocalMapping threads would)."""
 
     NN = 30
+    NB_BACK = 4   # the neighbours whose MapPoints are the backward Fuse's candidates
+    NSTAGE = 3
 
     def __init__(self, tr, n_new: int, device, seed: int = 0, stream=None):
         import torch
 
         from . import bow
-        from .match import FramesDev, ORBmatcher, TriBatch
+        from .match import FUSE_MP_DTYPE, FramesDev, ORBmatcher, TriBatch
+        from .ringmap import RingMap
 
         self.dev, self.tr, self.W = device, tr, int(n_new)
-        # new slots + at least NN older ones + one spare group (the next ingest writes while a search may run),
-        # a multiple of W
+        # the new slots + at least NN older ones + one spare group, a multiple of W
         self.R = self.W * (2 + -(-self.NN // self.W))
         R, S = self.R, tr.cap
         self.S = S
-        self.keys = torch.zeros((R, S * 28), dtype=torch.uint8, device=device)
-        self.desc = torch.zeros((R, S, 32), dtype=torch.uint8, device=device)
-        self.cnt = torch.zeros((R, 2), dtype=torch.int32, device=device)
-        self.has_mp = torch.zeros((R, S), dtype=torch.uint8, device=device)
-        self.tcw = torch.zeros((R, tr.tcw_bytes), dtype=torch.uint8, device=device)
-        self.nid = torch.zeros((R, S), dtype=torch.int32, device=device)
-        self.weight = torch.zeros((R, S), dtype=torch.float64, device=device)
-        self.word = torch.zeros((R, S), dtype=torch.int32, device=device)
+        z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=device)  # noqa: E731
+        self.keys = z((R, S * 28), torch.uint8)
+        self.desc = z((R, S, 32), torch.uint8)
+        self.cnt = z((R, 2), torch.int32)
+        self.has_mp = z((R, S), torch.uint8)
+        self.tcw = z((R, tr.tcw_bytes), torch.uint8)
+        self.nid = z((R, S), torch.int32)
+        self.weight = z((R, S), torch.float64)
+        self.word = z((R, S), torch.int32)
+        self.cnt_col = z(R, torch.int32)
+        self.fmp = z((R, S * FUSE_MP_DTYPE.itemsize), torch.uint8)
+        # staging sets: a step's keyframes between the ingest and the run that moves them into the ring
+        W = self.W
+        self.stage = [dict(keys=z((W, S * 28), torch.uint8), desc=z((W, S, 32), torch.uint8), cnt=z((W, 2), torch.int32),
+                           tcw=z((W, tr.tcw_bytes), torch.uint8), fmp=z((W, S * FUSE_MP_DTYPE.itemsize), torch.uint8),
+                           ready=torch.cuda.Event(), used=None)
+                      for _ in range(self.NSTAGE)]
         self.voc = bow.ORBVocabulary(bow.synthetic_vocabulary(10, 6, np.random.default_rng(seed), early_leaf=0.02),
                                      device=device.index or 0)
         self.matcher = ORBmatcher(0.6, False, device=device.index or 0)
-        self.head = 0
-        self.ready = {h: torch.cuda.Event() for h in range(0, self.R, self.W)}
-        # completion of the search run at each head (None until one was issued there)
-        self.done = {h: None for h in range(0, self.R, self.W)}
         self.stream = stream if stream is not None else torch.cuda.Stream(device, priority=-1)
-        # pairs for each head position. With at least NN + 1 keyframes per ingest (c2: 32), new keyframe i (frame
-        # i K + s of the agent's sequence) searches the NN keyframes of the same ingest nearest to it in the sequence
-        # (frames i' K + s, |i - i'| smallest, earlier first on a tie): the covisible keyframes
-        # GetBestCovisibilityKeyFrames(30) returns for a camera moving through one scene. With fewer, slot j = head + i
-        # searches the NN slots inserted before it.
-        self.pairs = {}
-        for head in range(0, R, self.W):
-            p = []
-            for i in range(self.W):
-                j = (head + i) % R
-                if self.W > self.NN:
-                    near = sorted((x for x in range(self.W) if x != i), key=lambda x: (abs(x - i), x))[:self.NN]
-                    p += [(j, (head + x) % R) for x in near]
-                else:
-                    p += [(j, (j - k) % R) for k in range(1, self.NN + 1)]
-            self.pairs[head] = torch.tensor(np.array(p, np.int32), device=device)
-        self.npairs = self.W * self.NN
-        self.out = torch.zeros((self.npairs, S), dtype=torch.int32, device=device)
-        self.nmatch = torch.zeros(self.npairs, dtype=torch.int32, device=device)
-        self._init_search_in_neighbors(seed)
+        self.npairs = W * self.NN
+        NB = min(self.NB_BACK, self.NN)
+        self.NB = NB
+        self.out = z((self.npairs, S), torch.int32)
+        self.nmatch = z(self.npairs, torch.int32)
+        self.fwd_idx = z((self.npairs, S), torch.int32)
+        self.fwd_dist = z((self.npairs, S), torch.int32)
+        self.fwd_n = z(self.npairs, torch.int32)
+        self.bwd_idx = z((W * NB, S), torch.int32)
+        self.bwd_dist = z((W * NB, S), torch.int32)
+        self.bwd_n = z(W * NB, torch.int32)
+        # per run: pairs [W NN][2], fuse items (fwd frame, fwd list [W NN], bwd frame, bwd list [W NB]) in one buffer
+        self.n_items = 2 * self.npairs + 2 * self.npairs + 2 * W * NB
+        self.items_h = torch.zeros(self.n_items, dtype=torch.int32).pin_memory()
+        self.items_d = z(self.n_items, torch.int32)
+        o = 2 * self.npairs
+        self.pairs_d = self.items_d[:o].view(self.npairs, 2)
+        self.fwd_frame, self.fwd_list = self.items_d[o:o + self.npairs], self.items_d[o + self.npairs:o + 2 * self.npairs]
+        o += 2 * self.npairs
+        self.bwd_frame, self.bwd_list = self.items_d[o:o + W * NB], self.items_d[o + W * NB:o + 2 * W * NB]
+        self._items_ev = None
+        self._init_scene_points()
         self._FramesDev, self._TriBatch = FramesDev, TriBatch
-        # initial ring: the first R frames, BoW on the device, no MapPoints yet
+        # trajectory position (pool frame index) and insertion order of each slot: the neighbour rule's inputs
+        self.slot_pos = np.zeros(R, np.int64)
+        self.slot_age = np.arange(R, dtype=np.int64) - R
+        # initial ring: the first R frames of the pool, BoW on the device, no MapPoint yet
         with torch.cuda.stream(tr.tstream):
             fr = torch.arange(R, device=device) % (tr.P * tr.B)   # the pool's frames in order, at their guessed poses
             self.keys.copy_(tr.d_kps_pool[fr])
@@ -274,98 +291,25 @@ class NewMapPointsLeg:
             self.cnt_col.copy_(self.cnt[:, 0])
             self.voc.transform_batch_device(R, self.desc.data_ptr(), S, self.cnt.data_ptr(), 4, self.word.data_ptr(),
                                             self.weight.data_ptr(), self.nid.data_ptr(), stream=tr.tstream.cuda_stream)
-            for ev in self.ready.values():
-                ev.record(tr.tstream)
-        self.pending = None
-        self.ring = None   # a RingMappingLeg assembling each run's LocalBundleAdjustment windows
+        torch.cuda.synchronize(device)
+        self.slot_pos[:] = np.arange(R) % (tr.P * tr.B)
+        self.map = RingMap(R, S, tr.F0.scale_factors, tr.F0.level_sigma2, self.keys, self.desc, self.cnt, self.tcw,
+                           self.fmp, self.has_mp, device)
+        self.next_head = 0
+        self.ingests = 0
+        self.runs = 0
+        self.head = 0          # the head of the last processed run
+        self.pending = None    # the last ingest's item (tests / launch)
+        self.last_item = None  # the last processed item
+        self.map_ms = []       # per profiled run: the map edits' GPU time (HIP events on the run's stream)
+        self.profile = False
 
-    def ingest(self, step: int):
-        """Copy step `step`'s new keyframes (frames f = step mod K + i K) into the ring at the next head; on the
-        tracking stream after the tracking step. Their BoW is computed by the next `run`."""
-        tr, W, R = self.tr, self.W, self.R
-        K = max(1, tr.B // W)
-        head = (self.head + W) % R   # the run at self.head was launched right after its ingest
-        fr = [(i * K + step % K) % tr.B for i in range(W)]
-        # the latest search that read these slots is the one two heads back (R >= 2 W + NN): it must be done
-        prev = self.done[(head - 2 * W) % R]
-        if prev is not None:
-            tr.tstream.wait_event(prev)
-        # one launch (mam_copy_rows): keypoints, descriptors, counts, pose, MapPoints of the frames (the pool set just
-        # tracked), and GetMapPoint(i) != NULL — the keypoints Tracking matched (motion model or local map)
-        self._ingest_rows(tr, fr, list(range(head, head + W)), tr.p * tr.B, tr.tstream.cuda_stream)
-        self.ready[head].record(tr.tstream)
-        self.pending = head
-
-    def _ingest_rows(self, tr, fr, slots, fmp_offset, stream, flags=True):
-        from .exchange import copy_rows
-
-        S = self.S
-        tables = [(tr.d_kps.data_ptr(), self.keys.data_ptr(), S * 28, S * 28, S * 28, 0),
-                  (tr.d_desc.data_ptr(), self.desc.data_ptr(), S * 32, S * 32, S * 32, 0),
-                  (tr.d_cnt.data_ptr(), self.cnt.data_ptr(), 8, 8, 8, 0),
-                  (tr.d_cnt.data_ptr(), self.cnt_col.data_ptr(), 4, 8, 4, 0),
-                  (tr.d_tcw.data_ptr(), self.tcw.data_ptr(), tr.tcw_bytes, tr.tcw_bytes, tr.tcw_bytes, 0),
-                  (self.fmp_frames.data_ptr(), self.fmp.data_ptr(), self.fmp.shape[1], self.fmp_frames.shape[1],
-                   self.fmp.shape[1], fmp_offset)]
-        fl = (tr.d_out1.data_ptr(), tr.d_out2.data_ptr(), 4 * tr.cap, S, self.has_mp.data_ptr(), S) if flags else None
-        for i in range(0, len(fr), 64):
-            copy_rows(tables, fr[i:i + 64], slots[i:i + 64], fl, stream=stream)
-
-    def take(self):
-        """The ring head of the keyframes ingested since the last take (None if none): the next run's work. Called
-        by the thread that starts the run, so a run never sees a later ingest."""
-        h, self.pending = self.pending, None
-        return h
-
-    def launch(self, head):
-        """Start the run of the keyframes ingested at `head` on this leg's own stream as soon as they are ingested (a
-        search of one step's keyframes overlaps the LocalBundleAdjustment of the previous step's: different agents'
-        keyframes, as with the reference's per-agent LocalMapping threads); `wait(stream, head)` orders a consumer of
-        the same keyframes after it."""
-        import torch
-
-        self.run(self.stream, head)
-        ev = torch.cuda.Event()
-        ev.record(self.stream)
-        self.done[head] = ev
-
-    def wait(self, stream, head):
-        if head is not None and self.done[head] is not None:
-            stream.wait_event(self.done[head])
-
-    def run(self, stream, head):
-        """ComputeBoW of the new keyframes at `head` + their W x 30 SearchForTriangulation, asynchronous on
-        `stream`."""
-        if head is None:
-            return
-        stream.wait_event(self.ready[head])
-        self.head = head
-        W, S, h = self.W, self.S, self.head
-        s = stream.cuda_stream
-        self.voc.transform_batch_device(W, self.desc[h].data_ptr(), S, self.cnt[h].data_ptr(), 4,
-                                        self.word[h].data_ptr(), self.weight[h].data_ptr(), self.nid[h].data_ptr(),
-                                        stream=s)
-        b = self._TriBatch()
-        b.kfs = self._FramesDev(self.R, S, self.keys.data_ptr(), self.desc.data_ptr(), self.cnt.data_ptr(), None, None, 0)
-        b.has_mp, b.nid, b.weight = self.has_mp.data_ptr(), self.nid.data_ptr(), self.weight.data_ptr()
-        b.tcw = self.tcw.data_ptr()
-        pairs = self.pairs[h]
-        b.npairs, b.pairs = int(pairs.shape[0]), pairs.data_ptr()
-        self.matcher.search_for_triangulation_batch_device(self.tr.F0, self.tr.cam, b, self.out.data_ptr(),
-                                                           self.nmatch.data_ptr(), False, stream=s)
-        self.search_in_neighbors(stream, h)
-        if self.ring is not None:   # the LocalBundleAdjustment windows of these keyframes (RingMappingLeg)
-            self.ring.assemble(stream, h)
-
-    # ------------------------------------------------------------------------------------------ SearchInNeighbors
-    NB_BACK = 4   # neighbours whose MapPoints form a keyframe's fuse candidates
-
-    def _init_search_in_neighbors(self, seed):
-        """MapPoints of every tracked frame (the ring copies them with the keyframe) and the update's observation
-        descriptors. A keyframe's MapPoints: its keypoints on the scene plane (synth.PLANE_DEPTH, world coordinates
-        under the pose of the camera that rendered the frame), as MapPoint::UpdateNormalAndDepth leaves them
-        (MapPoint.cc:426-494: normal = viewing direction, mfMaxDistance = distance x scale factor of the keypoint's
-        level, mfMinDistance = mfMaxDistance / scale factor of the last level), descriptor = the keypoint's."""
+    # ------------------------------------------------------------------------------------------ scene points
+    def _init_scene_points(self):
+        """Per pool frame and keypoint, the MapPoint a triangulation there makes (the stand-in for
+        GeometricTools::Triangulate, LocalMapping.cc:701): the keypoint's ray on the scene plane (synth.PLANE_DEPTH,
+        world coordinates under the pose of the camera that rendered the frame), normal = viewing direction, depth
+        range as UpdateNormalAndDepth leaves it for one view, descriptor = the keypoint's."""
         import torch
 
         from . import synth
@@ -373,7 +317,6 @@ class NewMapPointsLeg:
 
         tr, S = self.tr, self.S
         sf = tr.F0.scale_factors.astype(np.float64)
-        # every frame of the tracking leg's frame pool (P sets of B: tr.pool)
         pool = tr.pool
         nfr = len(pool["poses"])
         fmp = np.zeros((nfr, S), FUSE_MP_DTYPE)
@@ -398,81 +341,209 @@ class NewMapPointsLeg:
             m["valid"] = 1
             m["desc"] = desc_h[f, :n]
         self.fmp_frames = torch.from_numpy(fmp.view(np.uint8).reshape(nfr, -1)).to(self.dev)
-        self.fmp = torch.zeros((self.R, S * FUSE_MP_DTYPE.itemsize), dtype=torch.uint8, device=self.dev)
-        self.cnt_col = torch.zeros(self.R, dtype=torch.int32, device=self.dev)
-        W, NN, NBK = self.W, self.NN, self.NB_BACK
-        # items per ring head: forward (slot's MapPoints -> each of its NN neighbours), backward (the NB_BACK nearest
-        # neighbours' MapPoints -> the slot)
-        self.sin_items = {}
-        for head, pr in self.pairs.items():
-            pr = pr.cpu().numpy()
-            fwd_frame, fwd_mp = pr[:, 1], pr[:, 0]
-            bwd_frame = np.repeat(pr[::NN, 0], NBK)
-            bwd_mp = pr.reshape(W, NN, 2)[:, :NBK, 1].reshape(-1)
-            self.sin_items[head] = tuple(torch.tensor(np.ascontiguousarray(a, np.int32), device=self.dev)
-                                         for a in (fwd_frame, fwd_mp, bwd_frame, bwd_mp))
-        nf, nb = W * NN, W * NBK
-        self.fwd_idx = torch.zeros((nf, S), dtype=torch.int32, device=self.dev)
-        self.fwd_dist = torch.zeros((nf, S), dtype=torch.int32, device=self.dev)
-        self.fwd_n = torch.zeros(nf, dtype=torch.int32, device=self.dev)
-        self.bwd_idx = torch.zeros((nb, S), dtype=torch.int32, device=self.dev)
-        self.bwd_dist = torch.zeros((nb, S), dtype=torch.int32, device=self.dev)
-        self.bwd_n = torch.zeros(nb, dtype=torch.int32, device=self.dev)
-        # update: the W keyframes' MapPoints, 2..12 observations each, the observing keypoints' descriptors (the
-        # keyframe's with up to 20 flipped bits: views of the point from other keyframes)
-        from .scene import flip_bits
 
-        rng = np.random.default_rng(seed + 11)
-        n_upd = int(sum(int(tr.cnt_h[f % tr.B, 0]) for f in range(W)))
-        sizes = rng.integers(2, 13, n_upd)
-        off = np.zeros(n_upd + 1, np.int32)
-        off[1:] = np.cumsum(sizes)
-        base = np.concatenate([desc_h[f % tr.B, :int(tr.cnt_h[f % tr.B, 0])] for f in range(W)])
-        descs = flip_bits(np.repeat(base, sizes, 0), rng, 20)
-        self.upd_n = n_upd
-        self.upd_off = torch.from_numpy(off).to(self.dev)
-        self.upd_desc = torch.from_numpy(descs).to(self.dev)
-        self.upd_best = torch.zeros(n_upd, dtype=torch.int32, device=self.dev)
+    # ------------------------------------------------------------------------------------------ ingest
+    def ingest(self, step: int):
+        """Copy step `step`'s new keyframes (frames f = step mod K + i K of the tracking batch) into a staging set, on
+        the tracking stream after the step that tracked them; returns the run item (head, staging set, the frames'
+        pool indices), also kept as self.pending."""
+        from .exchange import copy_rows
 
-    def search_in_neighbors(self, stream, head):
-        """SearchInNeighbors of the keyframes at `head` (after their CreateNewMapPoints searches, on `stream`):
-        forward Fuse of each keyframe's MapPoints into its NN neighbours, backward Fuse of its NB_BACK nearest
-        neighbours' MapPoints (the fuse candidates) into it, ComputeDistinctiveDescriptors of the keyframes' MapPoints
-        (UpdateNormalAndDepth and the map updates Fuse implies are host-side bookkeeping, not searched)."""
-        fwd_frame, fwd_mp, bwd_frame, bwd_mp = self.sin_items[head]
+        tr, W = self.tr, self.W
+        K = max(1, tr.B // W)
+        fr = [(i * K + step % K) % tr.B for i in range(W)]
+        k = self.ingests % self.NSTAGE
+        st = self.stage[k]
+        if st["used"] is not None:   # the run that read this set last has moved it into the ring
+            tr.tstream.wait_event(st["used"])
+        S = self.S
+        tables = [(tr.d_kps.data_ptr(), st["keys"].data_ptr(), S * 28, S * 28, S * 28, 0),
+                  (tr.d_desc.data_ptr(), st["desc"].data_ptr(), S * 32, S * 32, S * 32, 0),
+                  (tr.d_cnt.data_ptr(), st["cnt"].data_ptr(), 8, 8, 8, 0),
+                  (tr.d_tcw.data_ptr(), st["tcw"].data_ptr(), tr.tcw_bytes, tr.tcw_bytes, tr.tcw_bytes, 0),
+                  (self.fmp_frames.data_ptr(), st["fmp"].data_ptr(), self.fmp.shape[1], self.fmp_frames.shape[1],
+                   self.fmp.shape[1], tr.p * tr.B)]
+        for i in range(0, W, 64):
+            copy_rows(tables, fr[i:i + 64], list(range(i, min(W, i + 64))), stream=tr.tstream.cuda_stream)
+        st["ready"].record(tr.tstream)
+        item = (self.next_head, k, [tr.p * tr.B + f for f in fr])
+        self.next_head = (self.next_head + W) % self.R
+        self.ingests += 1
+        self.pending = item
+        return item
+
+    def take(self):
+        h, self.pending = self.pending, None
+        return h
+
+    def launch(self, item):
+        """process() on this leg's own stream (tests; the bench's LocalMapping thread calls process on its stream)."""
+        if item is not None:
+            self.process(self.stream, item)
+
+    def wait(self, stream, item):
+        pass
+
+    def _pairs(self, head: int, pos_new):
+        """Each new keyframe's NN neighbours: the older ring slots nearest along the frame sequence (a keyframe of
+        the same view last), the more recently inserted first on a tie, then the lower slot."""
+        R, W, NN = self.R, self.W, self.NN
+        new = set(range(head, head + W))
+        older = np.array([s for s in range(R) if s not in new])
+        pairs = np.zeros((W, NN, 2), np.int32)
+        for w in range(W):
+            d = np.abs(self.slot_pos[older] - pos_new[w])
+            key = np.lexsort((older, -self.slot_age[older], d, d == 0))
+            nb = older[key[:NN]]
+            pairs[w, :, 0] = head + w
+            pairs[w, :, 1] = nb
+        return pairs.reshape(-1, 2)
+
+    def process(self, stream, item, run: int | None = None, hook=None):
+        """LocalMapping's keyframe work for the keyframes of `item`, asynchronous on `stream` (a torch stream): the
+        keyframes into ring slots [head, head + W) (the previous ones leave the map), ComputeBoW, MapPointCulling,
+        CreateNewMapPoints, SearchInNeighbors. hook(phase) (tests): called after each phase's launches ("insert",
+        "evict", "search", "create", "fuse_search", "fuse_apply", "refresh")."""
+        import torch
+
+        if item is None:
+            return
+        head, k, frames = item
+        self.last_item = item
+        W, S, R = self.W, self.S, self.R
+        run = self.runs if run is None else run
+        self.runs += 1
+        st = self.stage[k]
+        s = stream.cuda_stream
+        stream.wait_event(st["ready"])
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if self.profile else None
+        with torch.cuda.stream(stream):
+            # the keyframes into the ring (InsertKeyFrame), the staging set free again
+            sl = slice(head, head + W)
+            self.keys[sl].copy_(st["keys"])
+            self.desc[sl].copy_(st["desc"])
+            self.cnt[sl].copy_(st["cnt"])
+            self.tcw[sl].copy_(st["tcw"])
+            self.fmp[sl].copy_(st["fmp"])
+            self.cnt_col[sl].copy_(st["cnt"][:, 0])
+            if st["used"] is None:
+                st["used"] = torch.cuda.Event()
+            st["used"].record(stream)
+            pos = np.asarray(frames, np.int64)
+            pairs = self._pairs(head, pos)
+            self.slot_pos[sl] = pos
+            self.slot_age[sl] = self.ingests + np.arange(W)
+            NN, NB = self.NN, self.NB
+            items = np.concatenate([pairs.reshape(-1), pairs[:, 1], pairs[:, 0],
+                                    np.repeat(pairs[::NN, 0], NB), pairs.reshape(W, NN, 2)[:, :NB, 1].reshape(-1)])
+            if self._items_ev is not None:   # the previous run's copy out of the pinned buffer has finished
+                self._items_ev.synchronize()
+            self.items_h.numpy()[:] = items
+            self.items_d.copy_(self.items_h, non_blocking=True)
+            self._items_ev = torch.cuda.Event()
+            self._items_ev.record(stream)
+            self.head = head
+            self.run_index = run
+            if hook:
+                hook("insert")
+            if ev:
+                ev[0].record(stream)
+            # KeyFrame::SetBadFlag of the slots' previous keyframes + MapPointCulling
+            self.map.evict(head, W, run, s)
+            self.map.flags(s)
+            if hook:
+                hook("evict")
+            if ev:
+                ev[1].record(stream)
+            self.voc.transform_batch_device(W, self.desc[head].data_ptr(), S, self.cnt[head].data_ptr(), 4,
+                                            self.word[head].data_ptr(), self.weight[head].data_ptr(),
+                                            self.nid[head].data_ptr(), stream=s)
+            b = self._TriBatch()
+            b.kfs = self._FramesDev(R, S, self.keys.data_ptr(), self.desc.data_ptr(), self.cnt.data_ptr(), None, None, 0)
+            b.has_mp, b.nid, b.weight = self.has_mp.data_ptr(), self.nid.data_ptr(), self.weight.data_ptr()
+            b.tcw = self.tcw.data_ptr()
+            b.npairs, b.pairs = self.npairs, self.pairs_d.data_ptr()
+            self.matcher.search_for_triangulation_batch_device(self.tr.F0, self.tr.cam, b, self.out.data_ptr(),
+                                                               self.nmatch.data_ptr(), False, stream=s)
+            if hook:
+                hook("search")
+            if ev:
+                ev[2].record(stream)
+            self.map.create(head, W, self.pairs_d.data_ptr(), NN, self.out.data_ptr(), run, s)
+            self.map.gather(s)
+            if hook:
+                hook("create")
+            if ev:
+                ev[3].record(stream)
+            self.search_in_neighbors(stream)
+            if hook:
+                hook("fuse_search")
+            if ev:
+                ev[4].record(stream)
+            self.map.fuse_apply(head, W, self.pairs_d.data_ptr(), NN, NB, self.fwd_idx.data_ptr(),
+                                self.bwd_idx.data_ptr(), s)
+            if hook:
+                hook("fuse_apply")
+            self.map.refresh(head, W, s)
+            if hook:
+                hook("refresh")
+            if ev:
+                ev[5].record(stream)
+                self._ev = ev
+
+    def profiled_map_ms(self):
+        """GPU ms of the last profiled run's map edits (evict + flags, create + gather, fuse apply + refresh; HIP
+        events on the run's stream), None when the run was not profiled."""
+        ev = getattr(self, "_ev", None)
+        if not ev:
+            return None
+        ev[-1].synchronize()
+        return ev[0].elapsed_time(ev[1]) + ev[2].elapsed_time(ev[3]) + ev[4].elapsed_time(ev[5])
+
+    # ------------------------------------------------------------------------------------------ SearchInNeighbors
+    def search_in_neighbors(self, stream):
+        """SearchInNeighbors' searches of the run's keyframes (after their CreateNewMapPoints MapPoints): forward Fuse
+        of each keyframe's MapPoints into its NN neighbours, backward Fuse of its NB nearest neighbours' MapPoints
+        into it — the MapPoint lists gathered from the map (KeyFrame::GetMapPointMatches, valid 0 where a keypoint has
+        none). The side effects follow in RingMap.fuse_apply."""
         s = stream.cuda_stream
         fr = self._FramesDev(self.R, self.S, self.keys.data_ptr(), self.desc.data_ptr(), self.cnt.data_ptr(), None,
                              None, 0)
         tcw = self.tcw.data_ptr()
-        import torch
-
-        m = self.matcher   # (cnt_col: MapPoints of list m = ring slot m's keypoints, kept by the ingest)
-        m.fuse_items_batch_device(self.tr.F0, fr, tcw, self.tr.cam, len(fwd_frame), fwd_frame.data_ptr(),
-                                  fwd_mp.data_ptr(), self.fmp.data_ptr(), self.S, self.cnt_col.data_ptr(), 3.0,
+        lists = self.map.lists.data_ptr()
+        m = self.matcher   # (cnt_col: list m's length = ring slot m's keypoints)
+        m.fuse_items_batch_device(self.tr.F0, fr, tcw, self.tr.cam, self.npairs, self.fwd_frame.data_ptr(),
+                                  self.fwd_list.data_ptr(), lists, self.S, self.cnt_col.data_ptr(), 3.0,
                                   self.fwd_idx.data_ptr(), self.fwd_dist.data_ptr(), self.fwd_n.data_ptr(), stream=s)
-        m.fuse_items_batch_device(self.tr.F0, fr, tcw, self.tr.cam, len(bwd_frame), bwd_frame.data_ptr(),
-                                  bwd_mp.data_ptr(), self.fmp.data_ptr(), self.S, self.cnt_col.data_ptr(), 3.0,
+        m.fuse_items_batch_device(self.tr.F0, fr, tcw, self.tr.cam, self.W * self.NB, self.bwd_frame.data_ptr(),
+                                  self.bwd_list.data_ptr(), lists, self.S, self.cnt_col.data_ptr(), 3.0,
                                   self.bwd_idx.data_ptr(), self.bwd_dist.data_ptr(), self.bwd_n.data_ptr(), stream=s)
-        m.distinctive_batch_device(self.upd_n, self.upd_off.data_ptr(), self.upd_desc.data_ptr(),
-                                   self.upd_best.data_ptr(), stream=s)
 
-    def fuse_inputs(self, backward: bool, b: int):
-        """Host (KeyFrame FrameData with pose, MapPoints) of forward / backward Fuse item b of the last run."""
-        from .match import FUSE_MP_DTYPE, FrameData
+    # ------------------------------------------------------------------------------------------ host views
+    def _frame(self, slot: int, with_bow: bool = False):
+        from .match import FrameData
         from .orb import KP_DTYPE
 
-        fwd_frame, fwd_mp, bwd_frame, bwd_mp = self.sin_items[self.head]
-        slot = int((bwd_frame if backward else fwd_frame)[b].item())
-        ms = int((bwd_mp if backward else fwd_mp)[b].item())
         n = int(self.cnt[slot, 0].item())
         keys = self.keys[slot].cpu().numpy().view(KP_DTYPE)[:n]
-        KF = FrameData(keys=keys, desc=self.desc[slot, :n].cpu().numpy(), width=self.tr.W, height=self.tr.H,
-                       scale_factors=self.tr.F0.scale_factors, level_sigma2=self.tr.F0.level_sigma2)
+        F = FrameData(keys=keys, desc=self.desc[slot, :n].cpu().numpy(), width=self.tr.W, height=self.tr.H,
+                      scale_factors=self.tr.F0.scale_factors, level_sigma2=self.tr.F0.level_sigma2)
         t = self.tcw[slot].cpu().numpy().view(np.float32)
-        KF.pose = (t[:4].copy(), t[4:7].copy())
+        F.pose = (t[:4].copy(), t[4:7].copy())
+        return F
+
+    def fuse_inputs(self, backward: bool, b: int, lists=None):
+        """Host (KeyFrame FrameData with pose, MapPoint list) of forward / backward Fuse item b of the last run (the
+        lists as the run gathered them, or `lists` [R S] FUSE_MP_DTYPE)."""
+        from .match import FUSE_MP_DTYPE
+
+        slot = int((self.bwd_frame if backward else self.fwd_frame)[b].item())
+        ms = int((self.bwd_list if backward else self.fwd_list)[b].item())
+        KF = self._frame(slot)
         nm = int(self.cnt[ms, 0].item())
-        mps = self.fmp[ms].cpu().numpy().view(FUSE_MP_DTYPE)[:nm]
-        return KF, mps
+        if lists is None:
+            lists = self.map.lists.cpu().numpy().view(FUSE_MP_DTYPE).reshape(self.R, self.S)
+        return KF, lists[ms, :nm].copy()
 
     def algorithmic_bytes(self):
         """SURVEY §8(d) bytes of the last run's searches: per pair, sum over the BoW nodes both FeatureVectors hold of
@@ -488,229 +559,176 @@ class NewMapPointsLeg:
             u, c = np.unique(v, return_counts=True)
             per_slot.append(dict(zip(u.tolist(), c.tolist())))
         cand, fv = 0, 0
-        for a, b in self.pairs[self.head].cpu().numpy():
+        for a, b in self.pairs_d.cpu().numpy():
             A, B = per_slot[a], per_slot[b]
             cand += sum(c * B[u] for u, c in A.items() if u in B)
             fv += sum(A.values()) + sum(B.values())
         return {"candidate_pairs": int(cand), "bytes": int(cand * 32 + fv * (8 + 1 + 28 + 32))}
 
-    def pair_inputs(self, q: int):
-        """Host FrameData of pair q of the last run (keys, desc, has_mp, FeatureVector from the device BoW, pose)."""
-        from .match import FrameData
-        from .orb import KP_DTYPE
-
+    def pair_inputs(self, q: int, has_mp=None):
+        """Host FrameData of pair q of the last run (keys, desc, has_mp — the map's flags the search read, or
+        `has_mp` [R][S] — FeatureVector from the device BoW, pose)."""
+        if has_mp is None:
+            has_mp = self.has_mp.cpu().numpy()
         out = []
-        for slot in self.pairs[self.head][q].cpu().numpy():
-            n = int(self.cnt[slot, 0].item())
-            keys = self.keys[slot].cpu().numpy().view(KP_DTYPE)[:n]
-            F = FrameData(keys=keys, desc=self.desc[slot, :n].cpu().numpy(), width=self.tr.W, height=self.tr.H,
-                          scale_factors=self.tr.F0.scale_factors, level_sigma2=self.tr.F0.level_sigma2)
-            F.has_mp = self.has_mp[slot, :n].cpu().numpy()
+        for slot in self.pairs_d[q].cpu().numpy():
+            F = self._frame(int(slot))
+            n = len(F.keys)
+            F.has_mp = has_mp[slot, :n].copy()
             nid, w = self.nid[slot, :n].cpu().numpy(), self.weight[slot, :n].cpu().numpy()
             fv = {}
             for i in range(n):
                 if w[i] > 0:
                     fv.setdefault(int(np.uint32(nid[i])), []).append(i)
             F.featvec = dict(sorted(fv.items()))
-            t = self.tcw[slot].cpu().numpy().view(np.float32)
-            F.pose = (t[:4].copy(), t[4:7].copy())
             out.append(F)
         return out
 
-
-class RingWindow(C.Structure):
-    """mam_ring_window: one assembled window's device arrays."""
-    _fields_ = [("pose_q", C.c_void_p), ("pose_t", C.c_void_p), ("pose_fixed", C.c_void_p), ("point_xyz", C.c_void_p),
-                ("edge_point", C.c_void_p), ("edge_pose", C.c_void_p), ("edge_obs", C.c_void_p),
-                ("edge_inv_sigma2", C.c_void_p), ("edge_active", C.c_void_p)]
+    def distinctive_inputs(self, slot: int):
+        """(offsets, descriptors) of the MapPoints keyframe `slot` observes — their observations' descriptors in slot
+        order — ComputeDistinctiveDescriptors' inputs for the oracle (host; synchronises)."""
+        R, S = self.R, self.S
+        mp_of = self.map.mp_of.cpu().numpy().reshape(R, S)
+        okp = self.map.okp.cpu().numpy()
+        desc = self.desc.cpu().numpy()
+        off, ds = [0], []
+        for m in mp_of[slot][mp_of[slot] >= 0]:
+            for s in np.nonzero(okp[m] >= 0)[0]:
+                ds.append(desc[s, okp[m, s]])
+            off.append(len(ds))
+        return np.array(off, np.int32), (np.stack(ds) if ds else np.zeros((0, 32), np.uint8))
 
 
 class RingLBA:
-    """LocalBundleAdjustment over the keyframes Tracking inserted (Optimizer.cc:1118-1331 on the NewMapPointsLeg ring):
-    per new keyframe of the last run, its window solved with the batch device API (mam_lba_solve_batch_device).
-
-    rule "covisibility" (the reference's window rule, mam_ring_lba_windows_covis): the new keyframe and its covisible
-    ring neighbours by weight (weight = its MapPoints a neighbour observes, from the run's forward Fuse matches: >= 15
-    as KeyFrame::UpdateConnections keeps them, the heaviest when none reaches it) optimised, every other neighbour
-    observing one of its MapPoints fixed; the problem compacted to the real observations (sizes read back once per
-    batch). The ring's searched neighbours are the new keyframe's 30 nearest in its sequence, all of them covisible in
-    the synthetic scene, so the reference's rule would leave no fixed keyframe (it then skips the LBA,
-    Optimizer.cc:1179-1183): the n_fixed least covisible neighbours are fixed instead, as the gauge anchor. rule "sequence" (mam_ring_lba_windows): the NN neighbours nearest in sequence, the last n_fixed of them
-    fixed, a fixed S x (NN + 1) edge-slot shape with unobserved slots inactive."""
+    """LocalBundleAdjustment of each new keyframe of the last LocalMapping run (Optimizer.cc:1118-1497 on the device
+    map, ringmap.RingMap): its window by the reference's rule (mam_ringmap_windows: local = the keyframe + its
+    covisible keyframes by weight, local MapPoints = every MapPoint of every local keyframe, fixed = their other
+    observers; windows with no fixed keyframe are not solved, as the reference aborts), the W windows solved as one
+    batch (mam_lba_solve_batch_device; the sizes read back once per batch), and their write-back (mam_ringmap_writeback:
+    outlier erase, SetPose, SetWorldPos + UpdateNormalAndDepth)."""
 
     COVIS_TH = 15
 
-    def __init__(self, nm, n_fixed: int = 10, iterations: int = 10, solver=None, rule: str = "covisibility",
-                 sets: int = 1):
+    def __init__(self, nm, iterations: int = 10, solver=None, pcap: int = 16384, ecap: int = 262144):
         import torch
 
         from .lba import HUBER_MONO
+        from .ringmap import RingMapResult, RingMapWindow
 
-        if rule not in ("covisibility", "sequence"):
-            raise ValueError(rule)
-        self.nm, self.dev, self.rule = nm, nm.dev, rule
-        W, NN, S = nm.W, nm.NN, nm.S
-        self.NV, self.n_fixed = NN + 1, int(n_fixed)
-        NV, E = self.NV, S * (NN + 1)
+        self.nm, self.dev = nm, nm.dev
+        W, R = nm.W, nm.R
+        self.pcap, self.ecap = int(pcap), int(ecap)
+        P, E = self.pcap, self.ecap
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=self.dev)  # noqa: E731
         cam = nm.tr.cam
         self.cams = torch.from_numpy(np.ascontiguousarray(cam.params(), np.float32)[None]).to(self.dev)
-        # `sets` buffer sets (a window batch each: a set assembled while an earlier one is solved)
-        self.sets = []
-        for _ in range(max(1, int(sets))):
-            bufs = []
-            wins = (RingWindow * W)()
-            c_probs = (_Problem * W)()
-            c_res = (_Result * W)()
-            for w in range(W):
-                b = dict(pose_q=z((NV, 4), torch.float64), pose_t=z((NV, 3), torch.float64),
-                         pose_fixed=z(NV, torch.uint8), point_xyz=z((S, 3), torch.float64),
-                         edge_point=z(E, torch.int32), edge_pose=z(E, torch.int32), edge_obs=z((E, 2), torch.float64),
-                         edge_inv_sigma2=z(E, torch.float64), edge_active=z(E, torch.uint8),
-                         out_q=z((NV, 4), torch.float64), out_t=z((NV, 3), torch.float64),
-                         out_xyz=z((S, 3), torch.float64), out_chi2=z(E, torch.float64), out_depth=z(E, torch.uint8))
-                bufs.append(b)
-                for f in RingWindow._fields_:
-                    setattr(wins[w], f[0], b[f[0]].data_ptr())
-                P = c_probs[w]
-                P.n_poses, P.n_points, P.n_edges, P.n_cams = NV, S, E, 1
-                P.pose_id = P.point_id = P.pose_cam = None
-                P.pose_fixed, P.pose_q, P.pose_t = b["pose_fixed"].data_ptr(), b["pose_q"].data_ptr(), b["pose_t"].data_ptr()
-                P.point_xyz = b["point_xyz"].data_ptr()
-                P.edge_point, P.edge_pose = b["edge_point"].data_ptr(), b["edge_pose"].data_ptr()
-                P.edge_obs, P.edge_inv_sigma2 = b["edge_obs"].data_ptr(), b["edge_inv_sigma2"].data_ptr()
-                P.edge_active = b["edge_active"].data_ptr() if rule == "sequence" else None
-                P.cams = self.cams.data_ptr()
-                P.huber_delta, P.iterations = HUBER_MONO, int(iterations)
-                P.cam_model = 1 if cam.is_kb8 else 0
-                P.n_opt_poses = NV - self.n_fixed
-                R = c_res[w]
-                R.pose_q, R.pose_t, R.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
-                R.edge_chi2, R.edge_depth_ok = b["out_chi2"].data_ptr(), b["out_depth"].data_ptr()
-            st = dict(bufs=bufs, c_probs=c_probs, c_res=c_res,
-                      d_wins=torch.from_numpy(np.frombuffer(bytes(wins), np.uint8).copy()).to(self.dev),
-                      # covisibility windows: per window {poses, points, edges, optimised poses}, the ring slot of
-                      # each pose, the new keyframe's keypoint of each point (device), and the host copy of the first two
-                      counts=z((W, 4), torch.int32), pose_slot=z((W, NV), torch.int32), point_src=z((W, S), torch.int32),
-                      meta_h=torch.zeros((W, 4 + NV), dtype=torch.int32).pin_memory(), sizes=None, slots=None,
-                      stats=None)
-            self.sets.append(st)
-        self.cur = 0   # the set window() / result() / stats describe: the last solved
-        s2 = np.asarray(nm.tr.F0.level_sigma2, np.float32)
-        self.inv_s2 = (C.c_float * len(s2))(*[float(np.float32(1.0) / x) for x in s2])
-        self.nlevels = len(s2)
+        self.bufs = []
+        wins = (RingMapWindow * W)()
+        ress = (RingMapResult * W)()
+        self.c_probs = (_Problem * W)()
+        self.c_res = (_Result * W)()
+        for w in range(W):
+            b = dict(pose_q=z((R, 4), torch.float64), pose_t=z((R, 3), torch.float64), pose_fixed=z(R, torch.uint8),
+                     point_xyz=z((P, 3), torch.float64), edge_point=z(E, torch.int32), edge_pose=z(E, torch.int32),
+                     edge_obs=z((E, 2), torch.float64), edge_inv_sigma2=z(E, torch.float64),
+                     out_q=z((R, 4), torch.float64), out_t=z((R, 3), torch.float64), out_xyz=z((P, 3), torch.float64),
+                     out_chi2=z(E, torch.float64), out_depth=z(E, torch.uint8))
+            self.bufs.append(b)
+            for f in RingMapWindow._fields_:
+                setattr(wins[w], f[0], b[f[0]].data_ptr())
+            r = ress[w]
+            r.pose_q, r.pose_t, r.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
+            r.edge_chi2, r.edge_depth_ok = b["out_chi2"].data_ptr(), b["out_depth"].data_ptr()
+            Pb = self.c_probs[w]
+            Pb.pose_id = Pb.point_id = Pb.pose_cam = None
+            Pb.pose_fixed, Pb.pose_q, Pb.pose_t = b["pose_fixed"].data_ptr(), b["pose_q"].data_ptr(), b["pose_t"].data_ptr()
+            Pb.point_xyz = b["point_xyz"].data_ptr()
+            Pb.edge_point, Pb.edge_pose = b["edge_point"].data_ptr(), b["edge_pose"].data_ptr()
+            Pb.edge_obs, Pb.edge_inv_sigma2 = b["edge_obs"].data_ptr(), b["edge_inv_sigma2"].data_ptr()
+            Pb.edge_active = None
+            Pb.n_cams, Pb.cams = 1, self.cams.data_ptr()
+            Pb.huber_delta, Pb.iterations = HUBER_MONO, int(iterations)
+            Pb.cam_model = 1 if cam.is_kb8 else 0
+            Rs = self.c_res[w]
+            Rs.pose_q, Rs.pose_t, Rs.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
+            Rs.edge_chi2, Rs.edge_depth_ok = b["out_chi2"].data_ptr(), b["out_depth"].data_ptr()
+        self.d_wins = torch.from_numpy(np.frombuffer(bytes(wins), np.uint8).copy()).to(self.dev)
+        self.d_res = torch.from_numpy(np.frombuffer(bytes(ress), np.uint8).copy()).to(self.dev)
+        self.counts = z((W, 4), torch.int32)
+        self.pose_slot = z((W, R), torch.int32)
+        self.point_id = z((W, P), torch.int32)
+        self.meta_h = torch.zeros((W, 4 + R), dtype=torch.int32).pin_memory()
+        self.sizes = np.zeros((W, 4), np.int64)
+        self.slots = np.zeros((W, R), np.int64)
+        self.valid = []
+        self.stats = [(0, 0, 0)] * W
         self.solver = solver or LBASolver(device=self.dev.index or 0)
 
-    # the last solved set's views (what ring_lba_section and the tests read)
-    @property
-    def bufs(self):
-        return self.sets[self.cur]["bufs"]
+    def assemble(self, stream):
+        """The windows of the run's keyframes (after its map edits on `stream`)."""
+        nm = self.nm
+        nm.map.windows(nm.head, nm.W, self.COVIS_TH, self.d_wins.data_ptr(), self.pcap, self.ecap,
+                       self.counts.data_ptr(), self.pose_slot.data_ptr(), self.point_id.data_ptr(), stream.cuda_stream)
 
-    @property
-    def c_probs(self):
-        return self.sets[self.cur]["c_probs"]
-
-    @property
-    def c_res(self):
-        return self.sets[self.cur]["c_res"]
-
-    @property
-    def sizes(self):
-        return self.sets[self.cur]["sizes"]
-
-    @property
-    def stats(self):
-        return self.sets[self.cur]["stats"]
-
-    @property
-    def pose_slot(self):
-        return self.sets[self.cur]["pose_slot"]
-
-    @property
-    def point_src(self):
-        return self.sets[self.cur]["point_src"]
-
-    def assemble(self, stream, set_index: int = 0):
-        """The windows of the keyframes of the leg's last run (after its search_in_neighbors on `stream`)."""
-        from ._lib import check
-        from .exchange import _bind
-
-        nm, st = self.nm, self.sets[set_index]
-        if self.rule == "covisibility":
-            check(_bind().mam_ring_lba_windows_covis(
-                nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.COVIS_TH, self.n_fixed, nm.keys.data_ptr(),
-                nm.cnt.data_ptr(), nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2,
-                self.nlevels, st["d_wins"].data_ptr(), st["counts"].data_ptr(), st["pose_slot"].data_ptr(),
-                st["point_src"].data_ptr(), stream.cuda_stream), "mam_ring_lba_windows_covis")
-        else:
-            check(_bind().mam_ring_lba_windows(nm.W, nm.pairs[nm.head].data_ptr(), nm.NN, self.n_fixed, nm.keys.data_ptr(), nm.cnt.data_ptr(),
-                     nm.tcw.data_ptr(), nm.fmp.data_ptr(), nm.S, nm.fwd_idx.data_ptr(), self.inv_s2, self.nlevels,
-                     st["d_wins"].data_ptr(), stream.cuda_stream), "mam_ring_lba_windows")
-
-    def solve(self, stream, set_index: int = 0):
+    def solve(self, stream):
         import torch
 
-        st = self.sets[set_index]
-        if self.rule == "covisibility":
-            # the compacted sizes and the pose slots: one small read-back (the problem descriptors are host structs)
-            with torch.cuda.stream(stream):
-                st["meta_h"][:, :4].copy_(st["counts"], non_blocking=True)
-                st["meta_h"][:, 4:].copy_(st["pose_slot"], non_blocking=True)
-            stream.synchronize()
-            meta = st["meta_h"].numpy()
-            st["sizes"], st["slots"] = meta[:, :4].copy(), meta[:, 4:].copy()
-            for w in range(self.nm.W):
-                P = st["c_probs"][w]
-                P.n_poses, P.n_points, P.n_edges, P.n_opt_poses = (int(v) for v in st["sizes"][w])
-            # a window with no local MapPoint observed twice, or no fixed keyframe, is not solved — the reference's
-            # LocalBundleAdjustment returns there (Optimizer.cc:1179-1183); its sizes are zeroed
-            sz = st["sizes"]
-            valid = [w for w in range(self.nm.W) if sz[w, 1] > 0 and sz[w, 2] > 0 and sz[w, 0] > sz[w, 3]]
-            for w in range(self.nm.W):
-                if w not in valid:
-                    sz[w] = 0
-                    P = st["c_probs"][w]
-                    P.n_poses = P.n_points = P.n_edges = P.n_opt_poses = 0
-        else:
-            valid = list(range(self.nm.W))
-        st["valid"] = valid
-        stats = [(0, 0, 0)] * self.nm.W
+        W = self.nm.W
+        with torch.cuda.stream(stream):
+            self.meta_h[:, :4].copy_(self.counts, non_blocking=True)
+            self.meta_h[:, 4:].copy_(self.pose_slot, non_blocking=True)
+        stream.synchronize()
+        meta = self.meta_h.numpy()
+        self.sizes, self.slots = meta[:, :4].astype(np.int64), meta[:, 4:].astype(np.int64)
+        if (self.sizes < 0).any():
+            w = int(np.nonzero((self.sizes < 0).any(1))[0][0])
+            raise RuntimeError(f"ring LBA window {w} exceeds the buffers (points <= {self.pcap}, edges <= {self.ecap})")
+        for w in range(W):
+            P = self.c_probs[w]
+            P.n_poses, P.n_points, P.n_edges, P.n_opt_poses = (int(v) for v in self.sizes[w])
+        # windows the reference would not solve (no fixed keyframe, no MapPoint) come back empty
+        valid = [w for w in range(W) if self.sizes[w, 2] > 0]
+        self.valid = valid
+        stats = [(0, 0, 0)] * W
         if valid:
-            if len(valid) == self.nm.W:
-                probs, res = st["c_probs"], st["c_res"]
+            if len(valid) == W:
+                probs, res = self.c_probs, self.c_res
             else:
-                probs = (_Problem * len(valid))(*[st["c_probs"][w] for w in valid])
-                res = (_Result * len(valid))(*[st["c_res"][w] for w in valid])
+                probs = (_Problem * len(valid))(*[self.c_probs[w] for w in valid])
+                res = (_Result * len(valid))(*[self.c_res[w] for w in valid])
             rc = self.solver._L.mam_lba_solve_batch_device(self.solver._ctx, len(valid), C.byref(probs),
                                                            C.byref(res), C.c_void_p(stream.cuda_stream))
             if rc != 0:
                 raise RuntimeError(f"mam_lba_solve_batch_device: {rc}")
             for i, w in enumerate(valid):
-                if res is not st["c_res"]:
-                    st["c_res"][w] = res[i]
-                r = st["c_res"][w]
+                if res is not self.c_res:
+                    self.c_res[w] = res[i]
+                r = self.c_res[w]
                 stats[w] = (int(r.iterations), int(r.lm_trials), int(r.status))
-        st["stats"] = stats
-        self.cur = set_index
+        self.stats = stats
         return stats
 
+    def writeback(self, stream):
+        nm = self.nm
+        nm.map.writeback(nm.W, self.d_wins.data_ptr(), self.d_res.data_ptr(), self.counts.data_ptr(),
+                         self.pose_slot.data_ptr(), self.point_id.data_ptr(), self.pcap, self.ecap, stream.cuda_stream)
+
     def _size(self, w: int):
-        P = self.c_probs[w]
-        return int(P.n_poses), int(P.n_points), int(P.n_edges)
+        return int(self.sizes[w, 0]), int(self.sizes[w, 1]), int(self.sizes[w, 2])
 
     def window(self, w: int):
-        """Host LBAProblem of window w as assembled (ids = array order; the compacted prefix of the buffers)."""
+        """Host LBAProblem of window w as assembled (ids = array order)."""
         from .lba import HUBER_MONO, LBAProblem
 
-        b = {k: v.cpu().numpy() for k, v in self.bufs[w].items()}
         P, L, E = self._size(w)
-        act = b["edge_active"][:E] if self.rule == "sequence" else None
+        b = {k: v.cpu().numpy() for k, v in self.bufs[w].items() if not k.startswith("out")}
         return LBAProblem(pose_id=np.arange(P, dtype=np.int64), pose_fixed=b["pose_fixed"][:P], pose_q=b["pose_q"][:P],
                           pose_t=b["pose_t"][:P], point_id=np.arange(L, dtype=np.int64) + P,
                           point_xyz=b["point_xyz"][:L], edge_point=b["edge_point"][:E], edge_pose=b["edge_pose"][:E],
                           edge_obs=b["edge_obs"][:E], edge_inv_sigma2=b["edge_inv_sigma2"][:E],
-                          cams=self.cams.cpu().numpy(), huber_delta=HUBER_MONO, iterations=int(self.c_probs[w].iterations),
-                          edge_active=act, cam_model=int(self.c_probs[w].cam_model)).contiguous()
+                          cams=self.cams.cpu().numpy(), huber_delta=HUBER_MONO,
+                          iterations=int(self.c_probs[w].iterations), edge_active=None,
+                          cam_model=int(self.c_probs[w].cam_model)).contiguous()
 
     def result(self, w: int):
         b = self.bufs[w]
@@ -721,124 +739,89 @@ class RingLBA:
 
 
 class RingMappingLeg:
-    """The LocalMapping leg over the keyframes Tracking inserted: per step, the LocalBundleAdjustment windows of the
-    keyframes whose searches the NewMapPointsLeg ran (RingLBA, the reference's window rule, assembled on the
-    NewMapPointsLeg's stream right after those searches, one buffer set per ring head), solved together
-    (mam_lba_solve_batch_device), and their write-back (Optimizer.cc:1463-1497) exchanged: every optimised KeyFrame
-    once (the last window optimising it) and every window's MapPoints as 32-byte / 16-byte records
-    (mam_exchange_pack_sources), one all-gather across GPUs, applied in rank order to the shared map every GPU holds
-    (rows: rank x ring slot for KeyFrames, (rank x ring slot) x S + keypoint for MapPoints).
+    """The LocalMapping leg over the keyframes Tracking inserted: per run, the LocalBundleAdjustment windows of the
+    keyframes the NewMapPointsLeg just processed (RingLBA: the reference's window rule over the device map), solved
+    together, their write-back applied to the map (outlier erase, poses, positions, normals / depth ranges), and the
+    write-back exchanged: packed as records (every changed KeyFrame and MapPoint, 32 / 48 bytes:
+    mam_ringmap_pack), all-gathered across GPUs (RCCL over xGMI), applied in rank order to the replica of every
+    GPU's map each GPU holds (rows: rank x ring slot for KeyFrames, (rank x R + home slot) x S + keypoint for
+    MapPoints).
 
     The interface of LocalMappingLeg (bench.py reads the same fields)."""
 
-    def __init__(self, nm, rank: int, world_size: int, device, iterations: int = 10, stream=None):
+    def __init__(self, nm, rank: int, world_size: int, device, iterations: int = 10, stream=None,
+                 mp_cap: int | None = None, pcap: int = 16384, ecap: int = 262144):
         import torch
         import torch.distributed as dist
 
-        from .exchange import CompactExchange, MapWindow
+        from .ringmap import RingMapExchange
 
         self.nm, self.dev = nm, device
         self.W, self.rank, self.world_size = nm.W, rank, world_size
-        self.nheads = nm.R // nm.W
-        self.rl = RingLBA(nm, iterations=iterations, sets=self.nheads)
-        nm.ring = self   # the NewMapPointsLeg assembles each run's windows right after its searches
+        self.rl = RingLBA(nm, iterations=iterations, pcap=pcap, ecap=ecap)
         self.solver = self.rl.solver
         self.stream = stream if stream is not None else torch.cuda.Stream(device, priority=-1)
         self.status = torch.zeros(1, dtype=torch.int32, device=device)
-        NV, S, R = self.rl.NV, nm.S, nm.R
-        # the shared map every GPU holds: KeyFrame rows [q xyzw, t, valid], MapPoint rows [xyz, bad]
+        R, S = nm.R, nm.S
         self.kf_rows, self.mp_rows = world_size * R, world_size * R * S
         self.kf_table = torch.zeros((self.kf_rows, 8), dtype=torch.float32, device=device)
-        self.mp_table = torch.zeros((self.mp_rows, 4), dtype=torch.float32, device=device)
-        kf_cap, mp_cap = self.W * NV, self.W * S   # the same on every rank (same W, NN, S)
-        self.exch = CompactExchange(kf_cap, mp_cap, device=device)
-        # per buffer set: the windows' global vertex ids (device, computed per step) and the pack descriptors
-        self.pose_gid = [torch.zeros((self.W, NV), dtype=torch.int64, device=device) for _ in range(self.nheads)]
-        self.point_gid = [torch.zeros((self.W, S), dtype=torch.int64, device=device) for _ in range(self.nheads)]
-        self.d_pack = []
-        for k, st in enumerate(self.rl.sets):
-            pk = (MapWindow * self.W)()
-            for w in range(self.W):
-                b = st["bufs"][w]
-                d = pk[w]
-                d.n_poses, d.n_points = NV, S
-                d.pose_id, d.pose_fixed = self.pose_gid[k][w].data_ptr(), b["pose_fixed"].data_ptr()
-                d.point_id, d.point_bad = self.point_gid[k][w].data_ptr(), None
-                d.pose_q, d.pose_t, d.point_xyz = b["out_q"].data_ptr(), b["out_t"].data_ptr(), b["out_xyz"].data_ptr()
-            self.d_pack.append(torch.from_numpy(np.frombuffer(bytes(pk), np.uint8).copy()).to(device))
-        self.src_h = torch.zeros(2 * (kf_cap + mp_cap), dtype=torch.int32).pin_memory()
-        self.src_d = torch.zeros(2 * (kf_cap + mp_cap), dtype=torch.int32, device=device)
-        self.n_kf_upd = self.n_mp_upd = 0
+        self.mp_table = torch.zeros((self.mp_rows, 12), dtype=torch.float32, device=device)
+        self.exch = RingMapExchange(R, mp_cap if mp_cap is not None else R * S // 2, device)
         self.time_gather = False
         self.stats = None
         self.windows_solved = 0
         self.host_s = {}
-        self.last = None   # the buffer set of the last solve
+        self.last = None
         self._probs = None
+        self.n_kf_upd = self.n_mp_upd = 0
         if world_size > 1 and dist.is_available() and dist.is_initialized():
             dist.barrier()
 
-    def assemble(self, stream, head):
-        self.rl.assemble(stream, head // self.W)
-
-    def run(self, step: int, head=None):
-        """One LocalMapping step: the windows of the keyframes at `head` (their searches and assembly ordered before
-        this on the caller's wait), solved synchronously, then the pack / all-gather / apply queued on self.stream."""
+    def run(self, step: int, item=None):
+        """One LocalMapping run: the keyframe work of `item` (NewMapPointsLeg.process), the windows, the solve (host
+        synchronous: the sizes and the Levenberg state are read back), the write-back, and the exchange queued on
+        self.stream. item None: the last item again (the same keyframes re-inserted)."""
         import time
 
         import torch
 
-        if head is None:
-            if self.last is None:   # no keyframe run yet: nothing to solve
+        if item is None:
+            item = self.last
+            if item is None:
                 self.stats = [(0, 0, 0)] * self.W
                 return self.stats
-            head = self.last * self.W
-        k = head // self.W
-        with torch.cuda.stream(self.stream):
-            t0 = time.perf_counter()
-            s = self.stream.cuda_stream
-            t1 = time.perf_counter()
-            self.stats = self.rl.solve(self.stream, k)
-            t2 = time.perf_counter()
-            self.windows_solved += self.W
-            self.last = k
-            self._probs = None
-            st = self.rl.sets[k]
-            sizes, slots = st["sizes"], st["slots"]
-            R, S = self.nm.R, self.nm.S
-            base = self.rank * R
-            # global ids: KeyFrame row = rank R + ring slot; MapPoint row = (rank R + the new keyframe's slot) S + keypoint
-            self.pose_gid[k].copy_(st["pose_slot"].to(torch.int64) + base)
-            self.point_gid[k].copy_((st["pose_slot"][:, :1].to(torch.int64) + base) * S + st["point_src"].to(torch.int64))
-            # the write-back sources: every optimised KeyFrame once (from the last window optimising it), every
-            # window's MapPoints (a keyframe's own: no two windows share one)
-            kf = {}
-            for w in range(self.W):
-                for i in range(int(sizes[w, 3])):
-                    kf[base + int(slots[w, i])] = (w, i)
-            kf_src = np.array([kf[g] for g in sorted(kf)], np.int32).reshape(-1, 2)
-            mp_src = np.concatenate([np.stack([np.full(int(sizes[w, 1]), w), np.arange(int(sizes[w, 1]))], 1)
-                                     for w in range(self.W)]).astype(np.int32)
-            self.n_kf_upd, self.n_mp_upd = len(kf_src), len(mp_src)
-            nk = 2 * len(kf_src)
-            src = self.src_h.numpy()
-            src[:nk] = kf_src.reshape(-1)
-            src[nk:nk + 2 * len(mp_src)] = mp_src.reshape(-1)
-            n_all = nk + 2 * len(mp_src)
-            self.src_d[:n_all].copy_(self.src_h[:n_all], non_blocking=True)
-            self.exch.pack(self.d_pack[k].data_ptr(), self.W, self.src_d.data_ptr(), len(kf_src),
-                           self.src_d.data_ptr() + 4 * nk, len(mp_src), 0, stream=s)
-            self.exch.gather(timed=self.time_gather)
+        self.last = item
+        nm, st = self.nm, self.stream
+        t0 = time.perf_counter()
+        nm.process(st, item)
+        self.rl.assemble(st)
+        t1 = time.perf_counter()
+        self.stats = self.rl.solve(st)
+        t2 = time.perf_counter()
+        self.windows_solved += len(self.rl.valid)
+        self._probs = None
+        with torch.cuda.stream(st):
+            self.rl.writeback(st)
+            R, S = nm.R, nm.S
+            nm.map.pack(self.rank * R, self.rank * R * S, self.rank, self.exch.send.data_ptr(), self.exch.kf_cap,
+                        self.exch.mp_cap, st.cuda_stream)
+            self.exch.gather(st, timed=self.time_gather)
             self.exch.apply(self.kf_table.data_ptr(), self.kf_rows, self.mp_table.data_ptr(), self.mp_rows,
-                            self.status.data_ptr(), stream=s)
-            t3 = time.perf_counter()
+                            self.status.data_ptr(), st.cuda_stream)
+        t3 = time.perf_counter()
         for key, v in (("launch", t1 - t0), ("solve", t2 - t1), ("exchange", t3 - t2)):
             self.host_s[key] = self.host_s.get(key, 0.0) + v
         return self.stats
 
+    def exchange_counts(self):
+        """(KeyFrame records, MapPoint records, status) of the last packed block (synchronises)."""
+        h = self.exch.header()
+        self.n_kf_upd, self.n_mp_upd = int(h["n_kf"]), int(h["n_mp"])
+        return self.n_kf_upd, self.n_mp_upd, int(h["status"])
+
     @property
     def probs(self):
-        """Host LBAProblems of the last solved windows (built on first use after a solve)."""
+        """Host LBAProblems of the last solved windows (built on first use after a solve; empty windows included)."""
         if self._probs is None:
             self._probs = [self.rl.window(w) for w in range(self.W)]
         return self._probs
@@ -846,6 +829,11 @@ class RingMappingLeg:
     @property
     def edges(self):
         return [int(v) for v in self.rl.sizes[:, 2]]
+
+    def first_valid(self):
+        if not self.rl.valid:
+            raise RuntimeError("no LocalBundleAdjustment window was solved in the last run")
+        return self.rl.valid[0]
 
     def window_inputs(self, w: int):
         return self.rl.window(w)

@@ -62,14 +62,25 @@ def make_canvas(h: int, w: int, seed: int, n_rects: int | None = None) -> np.nda
     return img
 
 
-def make_frame(w: int, h: int, agent: int = 0, frame: int = 0, motion: bool = True) -> np.ndarray:
-    """u8 h x w frame; consecutive `frame` indices of one agent view one moving scene."""
+# The camera path: `px` canvas pixels of translation and `deg` degrees of roll per frame index, over a canvas `extent`
+# pixels wider than the view (frames up to extent / px). The default is the survey's 2 px / 0.2 deg per frame; a
+# longer path (BASELINE configs[2]'s LocalMapping: keyframes far enough apart that the farther ones no longer share
+# MapPoints, as a camera moving through a scene leaves them) uses a wider canvas.
+DEFAULT_MOTION = (2.0, 0.2, 4 * 256)
+
+
+def make_frame(w: int, h: int, agent: int = 0, frame: int = 0, motion: bool = True, path=None) -> np.ndarray:
+    """u8 h x w frame; consecutive `frame` indices of one agent view one moving scene (path = (px, deg, extent) per
+    frame, default DEFAULT_MOTION)."""
+    px, deg, extent = path or DEFAULT_MOTION
     canvas_seed = frame_seed(agent, 0)
     margin = 64
-    ch, cw = h + 2 * margin, w + 2 * margin + 4 * 256
+    ch, cw = h + 2 * margin, w + 2 * margin + int(extent)
     canvas = make_canvas(ch, cw, canvas_seed)
-    tx = 2.0 * frame if motion else 0.0
-    ang = 0.2 * frame if motion else 0.0
+    tx = px * frame if motion else 0.0
+    ang = deg * frame if motion else 0.0
+    if int(tx) > int(extent):
+        raise ValueError(f"frame {frame} leaves the canvas (path {path})")
     if ang != 0.0:
         from scipy.ndimage import rotate
 
@@ -94,13 +105,16 @@ def make_frame(w: int, h: int, agent: int = 0, frame: int = 0, motion: bool = Tr
 PLANE_DEPTH = 5.0
 
 
-def frame_pose(w: int, h: int, frame: int, f: float = 500.0, depth: float = PLANE_DEPTH, motion: bool = True):
-    """Tcw (q xyzw float32, t float32) of the camera that rendered make_frame(w, h, agent, frame) (any agent)."""
+def frame_pose(w: int, h: int, frame: int, f: float = 500.0, depth: float = PLANE_DEPTH, motion: bool = True,
+               path=None):
+    """Tcw (q xyzw float32, t float32) of the camera that rendered make_frame(w, h, agent, frame, path=path) (any
+    agent)."""
+    px, deg, _ = path or DEFAULT_MOTION
     k = frame if motion else 0
-    a = np.deg2rad(0.2 * k)
+    a = np.deg2rad(deg * k)
     ca, sa = np.cos(a), np.sin(a)
     R2 = np.array([[ca, sa], [-sa, ca]])
-    d = np.array([-float(int(2.0 * k)), 0.0])   # o_0 - o_k
+    d = np.array([-float(int(px * k)), 0.0])   # o_0 - o_k
     txy = depth / f * (R2 @ d + np.array([(w - 1) / 2.0 - w / 2.0, (h - 1) / 2.0 - h / 2.0]))
     # R = [[R2, 0], [0, 1]]: quaternion of a rotation about z by angle -a (R2 is that rotation in x-right, y-down axes)
     q = np.array([0.0, 0.0, np.sin(-a / 2.0), np.cos(-a / 2.0)])
@@ -125,7 +139,7 @@ def _camera_rays(w: int, h: int, cam, ss: int):
 
 
 def make_frame_camera(w: int, h: int, cam, agent: int = 0, frame: int = 0, f: float = 500.0,
-                      depth: float = PLANE_DEPTH, motion: bool = True, ss: int = 3) -> np.ndarray:
+                      depth: float = PLANE_DEPTH, motion: bool = True, ss: int = 3, path=None) -> np.ndarray:
     """make_frame's scene seen through camera `cam` (a match.KannalaBrandt8 — the testMultiAgentSystem agents' fisheye —
     or a Pinhole) from the same pose, frame_pose(w, h, frame): every sample ray (cam.unproject_np) meets the canvas
     plane z = depth (the camera rolls about z and translates in x / y, so the plane is at camera depth `depth` too),
@@ -139,9 +153,9 @@ def make_frame_camera(w: int, h: int, cam, agent: int = 0, frame: int = 0, f: fl
 
     canvas_seed = frame_seed(agent, 0)
     margin = 64
-    ch, cw = h + 2 * margin, w + 2 * margin + 4 * 256
+    ch, cw = h + 2 * margin, w + 2 * margin + int((path or DEFAULT_MOTION)[2])
     canvas = make_canvas(ch, cw, canvas_seed)
-    q, t = frame_pose(w, h, frame, f, depth, motion)
+    q, t = frame_pose(w, h, frame, f, depth, motion, path=path)
     a = -2.0 * np.arctan2(float(q[2]), float(q[3]))             # roll of frame_pose's quaternion (about z by -a)
     ca, sa = np.cos(a), np.sin(a)
     acc = np.zeros((h, w), np.float64)

@@ -27,8 +27,8 @@ lba)
   timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -f csv -d $O/pmc_${RND}lba -o run -- python3 $R/scripts/lba_bench.py --world --batch 32 --solves 3 > $O/pmc_${RND}lba.log 2>&1 || { tail -5 $O/pmc_${RND}lba.log; exit 1; }
   # the timed leg's windows: 32 ring windows (the dumped covisibility windows x 8, scripts/ring_window_replay.py)
   # under a kernel trace and the FP64-MFMA pass bench.py's roofline_lba reads; the windows are dumped first when absent
-  # (scripts/ring_leg_probe.py --dump, a GPU run; scratch/ is git-ignored)
-  [ -f $R/scratch/ring_windows.npz ] || timeout -k 10 300 python3 $R/scripts/ring_leg_probe.py --dump $R/scratch/ring_windows.npz > $O/ring_dump.log 2>&1 || { tail -5 $O/ring_dump.log; exit 1; }
+  # (scripts/ringmap_probe.py --dump: the device map's windows, a GPU run; scratch/ is git-ignored)
+  [ -f $R/scratch/ring_windows.npz ] || timeout -k 10 300 python3 $R/scripts/ringmap_probe.py --runs 8 --dump $R/scratch/ring_windows.npz > $O/ring_dump.log 2>&1 || { tail -5 $O/ring_dump.log; exit 1; }
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/${RND}lba_ring -o run -- python3 $R/scripts/ring_window_replay.py $R/scratch/ring_windows.npz --mode batch --repeat 8 --solves 6 > $O/${RND}lba_ring.log 2>&1 || { tail -5 $O/${RND}lba_ring.log; exit 1; }
   timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -f csv -d $O/pmc_${RND}lba_ring -o run -- python3 $R/scripts/ring_window_replay.py $R/scratch/ring_windows.npz --mode batch --repeat 8 --solves 3 > $O/pmc_${RND}lba_ring.log 2>&1 || { tail -5 $O/pmc_${RND}lba_ring.log; exit 1; }
   ;;
