@@ -45,10 +45,10 @@ CONFIGS = {
     # BASELINE.json configs[1]: single-agent mono 640x480, 1000 features, 8 levels, extract + match
     "c1": dict(width=640, height=480, nfeatures=1000, lba=False),
     # BASELINE.json configs[2]: 1280x720, 2000 features + LocalBundleAdjustment (50 KF / ~3000 MapPoints windows)
-    # path: 16 px of travel and 0.25 deg of roll per frame over a 4096-px wider scene — keyframes 8 frames apart are
-    # 128 px apart, so a keyframe shares MapPoints with the ~50 keyframes around it and not with the far ones (the
-    # covisibility graph LocalBundleAdjustment's window rule needs: local and fixed keyframes)
-    "c2": dict(width=1280, height=720, nfeatures=2000, lba=True, path=(16.0, 0.25, 4096)),
+    # path: 13 px of travel and 0.25 deg of roll per frame over a 4096-px wider scene — keyframes 8 frames apart are
+    # 104 px apart, so a keyframe shares >= 15 MapPoints with the ~50 keyframes around it and fewer with the farther
+    # ones (the covisibility graph LocalBundleAdjustment's window rule needs: local and fixed keyframes)
+    "c2": dict(width=1280, height=720, nfeatures=2000, lba=True, path=(13.0, 0.25, 4096)),
     # BASELINE.json configs[3]: the testMultiAgentSystem agents (test/settingsForTest_00.yaml: KannalaBrandt8, 700
     # features) at 640x480, two agents in total (both on one GPU at --gpus 1, one per GPU at --gpus 2)
     # pool_frames: the two streams' keyframes over 16 steps are 32 distinct views (synth.frame_pose at the fisheye's

@@ -62,8 +62,9 @@ def _match_sigs():
     from .pose import _SIGS as pose_sigs
     from .bow import _SIGS as bow_sigs
     from .streams import _SIGS as stream_sigs
+    from .ringmap import _SIGS as ringmap_sigs
 
-    return {**_SIGS, **lba_sigs, **ex_sigs, **pose_sigs, **bow_sigs, **stream_sigs}
+    return {**_SIGS, **lba_sigs, **ex_sigs, **pose_sigs, **bow_sigs, **stream_sigs, **ringmap_sigs}
 
 
 def lib() -> C.CDLL:

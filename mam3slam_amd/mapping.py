@@ -244,6 +244,7 @@ class NewMapPointsLeg:
         self.word = z((R, S), torch.int32)
         self.cnt_col = z(R, torch.int32)
         self.fmp = z((R, S * FUSE_MP_DTYPE.itemsize), torch.uint8)
+        self.tcw_search = z((R, tr.tcw_bytes), torch.uint8)   # the poses the last run's searches read
         # staging sets: a step's keyframes between the ingest and the run that moves them into the ring
         W = self.W
         self.stage = [dict(keys=z((W, S * 28), torch.uint8), desc=z((W, S, 32), torch.uint8), cnt=z((W, 2), torch.int32),
@@ -455,6 +456,7 @@ class NewMapPointsLeg:
                 hook("evict")
             if ev:
                 ev[1].record(stream)
+            self.tcw_search.copy_(self.tcw)   # (the parity checks' view: the write-back moves the poses later)
             self.voc.transform_batch_device(W, self.desc[head].data_ptr(), S, self.cnt[head].data_ptr(), 4,
                                             self.word[head].data_ptr(), self.weight[head].data_ptr(),
                                             self.nid[head].data_ptr(), stream=s)
@@ -520,7 +522,7 @@ class NewMapPointsLeg:
                                   self.bwd_idx.data_ptr(), self.bwd_dist.data_ptr(), self.bwd_n.data_ptr(), stream=s)
 
     # ------------------------------------------------------------------------------------------ host views
-    def _frame(self, slot: int, with_bow: bool = False):
+    def _frame(self, slot: int, search_pose: bool = False):
         from .match import FrameData
         from .orb import KP_DTYPE
 
@@ -528,7 +530,7 @@ class NewMapPointsLeg:
         keys = self.keys[slot].cpu().numpy().view(KP_DTYPE)[:n]
         F = FrameData(keys=keys, desc=self.desc[slot, :n].cpu().numpy(), width=self.tr.W, height=self.tr.H,
                       scale_factors=self.tr.F0.scale_factors, level_sigma2=self.tr.F0.level_sigma2)
-        t = self.tcw[slot].cpu().numpy().view(np.float32)
+        t = (self.tcw_search if search_pose else self.tcw)[slot].cpu().numpy().view(np.float32)
         F.pose = (t[:4].copy(), t[4:7].copy())
         return F
 
@@ -539,7 +541,7 @@ class NewMapPointsLeg:
 
         slot = int((self.bwd_frame if backward else self.fwd_frame)[b].item())
         ms = int((self.bwd_list if backward else self.fwd_list)[b].item())
-        KF = self._frame(slot)
+        KF = self._frame(slot, search_pose=True)
         nm = int(self.cnt[ms, 0].item())
         if lists is None:
             lists = self.map.lists.cpu().numpy().view(FUSE_MP_DTYPE).reshape(self.R, self.S)
@@ -572,7 +574,7 @@ class NewMapPointsLeg:
             has_mp = self.has_mp.cpu().numpy()
         out = []
         for slot in self.pairs_d[q].cpu().numpy():
-            F = self._frame(int(slot))
+            F = self._frame(int(slot), search_pose=True)
             n = len(F.keys)
             F.has_mp = has_mp[slot, :n].copy()
             nid, w = self.nid[slot, :n].cpu().numpy(), self.weight[slot, :n].cpu().numpy()
@@ -586,7 +588,7 @@ class NewMapPointsLeg:
 
     def distinctive_inputs(self, slot: int):
         """(offsets, descriptors) of the MapPoints keyframe `slot` observes — their observations' descriptors in slot
-        order — ComputeDistinctiveDescriptors' inputs for the oracle (host; synchronises)."""
+        order — ComputeDistinctiveDescriptors' inputs on the host (the CPU baseline; synchronises)."""
         R, S = self.R, self.S
         mp_of = self.map.mp_of.cpu().numpy().reshape(R, S)
         okp = self.map.okp.cpu().numpy()
