@@ -54,14 +54,16 @@ CONFIGS = {
     # pool_frames: the two streams' keyframes over 16 steps are 32 distinct views (synth.frame_pose at the fisheye's
     # focal length: 0.53 deg of parallax per frame), so CreateNewMapPoints' neighbours beyond the nearest two pass
     # KannalaBrandt8's parallax test (cos < 0.9998, ~1.15 deg: KannalaBrandt8.cpp:316)
+    # (path: 24 px / 0.25 deg per frame, as c2's: keyframes far enough apart that the ring holds covisible and fixed
+    # ones)
     "c3": dict(width=640, height=480, nfeatures=700, lba=True, camera="kb8", agents=2, pool_frames=32, frame_stride=1,
-               coherent_map=True),
+               coherent_map=True, path=(24.0, 0.25, 1024)),
     # BASELINE.json configs[4]: 8 synthetic mono agents at 1280x720 / 2000 features, shared-map local BA, one agent
     # per GPU at --gpus 8 (all 8 on one GPU at --gpus 1); neighbouring agents' LBA windows overlap (keyframes and
     # MapPoints of the merged map), so the exchange resolves cross-GPU write conflicts in GPU order
     # (pool_frames: 9 sets of the 8 agents' frames — coprime with the keyframe cadence, so the keyframes the ring
     # holds are 72 different views: no identical keyframes in CreateNewMapPoints' neighbourhoods)
-    "c4": dict(width=1280, height=720, nfeatures=2000, lba=True, agents=8, pool_frames=72),
+    "c4": dict(width=1280, height=720, nfeatures=2000, lba=True, agents=8, pool_frames=72, path=(40.0, 0.25, 2944)),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFS = 78.6    # MI355X FP64 vector / matrix (spec)
@@ -738,7 +740,11 @@ def parity_section(tr, mapping, newmp=None):
             fused.append(int(nf))
         out["fuse_index_exact"] = bool(ok)
         out["fuse_items"] = {"forward_fused": fused[0], "backward_fused": fused[1]}
-    if mapping is not None:
+    solved = mapping is not None and (not hasattr(mapping, "rl") or len(mapping.rl.valid) > 0)
+    if mapping is not None and not solved:
+        # no window of the last run had a fixed keyframe (the reference aborts those LBAs): nothing to compare
+        out["lba_window"] = None
+    if solved:
         w = mapping.first_valid() if hasattr(mapping, "first_valid") else 0
         prob = mapping.window_inputs(w)
         rg = mapping.window_result(w)
@@ -1312,9 +1318,15 @@ def main():
             if parity is not None:
                 parity["ring_lba_same_control_flow"] = ring.get("oracle_same_control_flow")
                 parity["ring_lba_max_point_rel_diff"] = ring.get("oracle_max_point_rel_diff")
+        vw = []
         if mapping is not None:
             # the last run's solved windows (a window without fixed keyframes is not solved: Optimizer.cc:1182-1185)
             vw = list(mapping.rl.valid) if args.lm_windows == "ring" else list(range(mapping.W))
+        if mapping is not None and not vw:
+            out["lba"] = {"windows_per_step": mapping.W, "windows_solved_last_run": 0,
+                          "note": "no window of the last LocalMapping run had a fixed keyframe (the reference aborts "
+                                  "those LocalBundleAdjustments, Optimizer.cc:1182-1185)"}
+        if mapping is not None and vw:
             probs_v = [mapping.probs[w] for w in vw]
             its = [mapping.stats[w][0] for w in vw]
             trials = [mapping.stats[w][1] for w in vw]
@@ -1435,7 +1447,7 @@ def main():
             out["cpu_baseline"]["ms_per_frame"] = 1e3 / out["cpu_baseline"]["value"]
             if lat is not None:
                 out["speedup_latency_b1"] = out["cpu_baseline"]["tracking_ms_per_frame"] / lat["device_graph_ms"]
-            if lat is not None:
+            if lat is not None and (mapping is None or vw):
                 # the north star's per-frame figure: ORBextractor (the host-API call a Frame constructor makes, B = 1)
                 # + a lone LocalBundleAdjustment window every K frames, GPU vs the oracle on the same inputs. With a
                 # LocalMapping leg the window is one of its timed-region windows; without one (c1) a 50-keyframe window

@@ -74,6 +74,7 @@ struct mam_orb_ctx {
     DevBuf<uint8_t> d_out;
     size_t fast_lds = 0, dist_lds = 0;
     size_t dist2_lds[3] = {0, 0, 0};   // k_distribute2 LDS bytes for 256 / 512 / 1024 threads
+    bool dist2_ok[3] = {false, false, false};   // the width's LDS fits a CU
     int dist_nt = -1;                  // DistributeOctTree width override (mam_orb_debug_set_option), -1 = auto
     int fork = -1;                     // latency-mode stream fork override (mam_orb_debug_set_option), -1 = auto
     // latency mode's side streams and their fork / join events (run_pipeline)
@@ -434,16 +435,22 @@ int ensure_geometry(mam_orb_ctx* c, int W, int H, int F) {
         c->dist_lds += (size_t)c->dist_kcap * 6 + 32;
         for (int i = 0; i < 3; i++) c->dist2_lds[i] = mam::dist::lds_bytes(g.node_cap, maxcells, 256 << i);
         if (g.node_cap > 16383) { g_last_error = "too many DistributeOctTree nodes (nfeatures too large)"; return MAM_ERR_ARG; }
-        if (c->fast_lds > 160 * 1024 || c->dist_lds > 160 * 1024 || c->dist2_lds[2] > 160 * 1024) {
+        // the round-3 k_distribute (~60 B a node) is the fallback every geometry must fit; each k_distribute2 width
+        // (~84 B a node at 1024 threads) runs only where its LDS fits (dist_threads falls back to the next narrower)
+        if (c->fast_lds > 160 * 1024 || c->dist_lds > 160 * 1024) {
             g_last_error = "LDS budget exceeded (nfeatures or cell size too large)";
             return MAM_ERR_ARG;
         }
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<256, 16>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[0]);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<512, 16>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[1]);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<1024, 8>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[2]);
+        for (int i = 0; i < 3; i++) c->dist2_ok[i] = c->dist2_lds[i] <= 160 * 1024;
+        if (c->dist2_ok[0])
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<256, 16>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[0]);
+        if (c->dist2_ok[1])
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<512, 16>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[1]);
+        if (c->dist2_ok[2])
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::k_distribute2<1024, 8>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->dist2_lds[2]);
         for (int nb = 8; nb <= 64; nb += 8)
             if (int rc = build_pyr_plan(c, nb)) return rc;
         if (pyr_forced_bands() > 0 && pyr_forced_bands() % 8)
@@ -585,9 +592,12 @@ int dist_threads(const mam_orb_ctx* c, int F) {
         const char* e = getenv("MAM_DIST_NT");
         return e ? atoi(e) : -1;
     }();
-    const int v = c->dist_nt >= 0 ? c->dist_nt : forced;
-    if (v == 0 || v == 256 || v == 512 || v == 1024) return v;
-    return F <= 4 ? 1024 : 256;
+    int v = c->dist_nt >= 0 ? c->dist_nt : forced;
+    if (!(v == 0 || v == 256 || v == 512 || v == 1024)) v = F <= 4 ? 1024 : 256;
+    // a width whose LDS does not fit this geometry (large extractors, e.g. Tracking.cc:606's 5x init extractor at
+    // 1800-2500 features): the next narrower one, down to the round-3 kernel
+    while (v > 0 && !c->dist2_ok[v == 1024 ? 2 : v == 512 ? 1 : 0]) v = v == 256 ? 0 : v / 2;
+    return v;
 }
 
 // k_fast_chunks for every launch (MAM_FAST_CHUNKS=1 / the context option; default off until measured), when the

@@ -9,4 +9,4 @@ mkdir -p $R/variants
 C=$R/mam3slam_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
   -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -Werror=return-type "$@" \
-  -o $R/variants/libmam_gpu_$N.so $C/orb_extract.hip $C/${MATCH_SRC:-match.hip} $C/lba.hip $C/exchange.hip $C/pose.hip $C/bow.hip $C/streams.hip
+  -o $R/variants/libmam_gpu_$N.so $C/orb_extract.hip $C/${MATCH_SRC:-match.hip} $C/lba.hip $C/exchange.hip $C/pose.hip $C/bow.hip $C/streams.hip $C/ringmap.hip

@@ -94,7 +94,7 @@ def main():
                       "edge_inv_sigma2", "cams"):
                 z[f"w{i}_{f}"] = getattr(p, f)
             z[f"w{i}_meta"] = np.array([p.huber_delta, p.iterations, p.cam_model], np.float64)
-        np.savez(a.dump, **z)
+        np.savez_compressed(a.dump, **z)
 
 
 if __name__ == "__main__":

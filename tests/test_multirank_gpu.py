@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("cfg,ranks,extra", [("c3", 2, []), ("c2", 2, ["--batch", "32"]), ("c4", 4, [])])
+@pytest.mark.parametrize("cfg,ranks,extra", [("c3", 2, []), ("c2", 2, ["--batch", "128"]), ("c4", 4, [])])
 def test_bench_ranks_one_gpu(cfg, ranks, extra):
     """c4: four of BASELINE configs[4]'s 8 agents' GPUs as four ranks (two agents each), neighbouring ranks' LBA
     windows overlapping (cross-rank write conflicts resolved in rank order)."""

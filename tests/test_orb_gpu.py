@@ -323,3 +323,17 @@ def test_fast_blur_launch_bit_exact(gpu_lib, oracle, fb):
             _assert_kps_equal(kps, d_desc[i].cpu().numpy()[:n], int(d_cnt[i, 1]), *oracle.extract(imgs[i], p),
                               f"fast_blur {fb} {w}x{h}/{nfeat} batch {i}")
         ext.close()
+
+
+def test_large_extractor_distribute_fallback(gpu_lib, oracle):
+    """A 10000-feature extractor at 1280x720 (Tracking.cc:606's 5x init extractor for 2000 features): level 0's
+    DistributeOctTree needs more LDS than the 1024-thread k_distribute2 has, so the narrower width (or the round-3
+    kernel) runs instead of the geometry being refused — bit-exact against the oracle, single frame and batch."""
+    from mam3slam_amd import ORBextractor
+
+    ext = ORBextractor(10000, 1.2, 8, 20, 7)
+    img = synth.make_frame(1280, 720, agent=9, frame=4)
+    kg, dg, mg = ext(img)
+    ko, do, mo = oracle.extract(img, oracle.params(10000))
+    _assert_kps_equal(kg, dg, mg, ko, do, mo, "10000 features")
+    assert len(kg) > 5000
