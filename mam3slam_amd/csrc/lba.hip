@@ -967,6 +967,45 @@ __device__ __forceinline__ void tri_index(int q, int* tr, int* tc) {
     *tc = q - r * (r + 1) / 2;
 }
 
+// A short block's sum with one lane per entry of the 6x6 block (lanes 0..35 of one wave), each summing its entry over
+// the block's landmark pairs in landmark order (g2o's order, block_solver.hpp:372-439): no reduction; 64 pair records
+// fetched per coalesced load and broadcast by shuffles, 4 pairs' rows in flight per lane
+__device__ __forceinline__ double schur_lane_sum(const Prob& d, int k0, int k1, int lane, bool act, int r36, int c36) {
+    double acc = 0.0;
+    const double* Wb = d.bdinv + 3 * r36;
+    const double* Hb = d.hpl + 3 * c36;
+    for (int kb = k0; kb < k1; kb += 64) {
+        const int2 mine = kb + lane < k1 ? d.blk_pair[kb + lane] : make_int2(0, 0);
+        const int n = min(64, k1 - kb);
+        int j = 0;
+        for (; j + 4 <= n; j += 4) {
+            double w[4][3], b[4][3];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int px = __shfl(mine.x, j + u, 64), py = __shfl(mine.y, j + u, 64);
+                if (act) {
+#pragma unroll
+                    for (int q = 0; q < 3; q++) {
+                        w[u][q] = Wb[18 * (size_t)px + q];
+                        b[u][q] = Hb[18 * (size_t)py + q];
+                    }
+                }
+            }
+            if (act) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) acc += w[u][0] * b[u][0] + w[u][1] * b[u][1] + w[u][2] * b[u][2];
+            }
+        }
+        for (; j < n; j++) {
+            const int px = __shfl(mine.x, j, 64), py = __shfl(mine.y, j, 64);
+            if (act)
+                acc += Wb[18 * (size_t)px] * Hb[18 * (size_t)py] + Wb[18 * (size_t)px + 1] * Hb[18 * (size_t)py + 1] +
+                       Wb[18 * (size_t)px + 2] * Hb[18 * (size_t)py + 2];
+        }
+    }
+    return acc;
+}
+
 // grid (Np (Np + 1) / 2 + Np, Q) x SCHUR_T: one workgroup per block (i1 <= i2) of S (the triangle only: the upper
 // half's workgroups would exit at once, half of the dispatches) over its landmark pairs (k_blk_fill): the waves take
 // interleaved 64-pair chunks (a diagonal block has all ~480 of its pose's edges: one wave walked them in ~8 dependent
@@ -982,6 +1021,9 @@ constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per
 #endif
 #ifndef MAM_SCHUR_T
 #define MAM_SCHUR_T 128   // lone window: 64 / 128 / 256 threads 23.0 / 21.9 / 24.5 us per launch
+#endif
+#ifndef MAM_SCHUR_LANE_MAX
+#define MAM_SCHUR_LANE_MAX 192   // blocks of at most this many landmark pairs: one wave, a lane per entry (0: never)
 #endif
 constexpr int SCHUR_T = MAM_SCHUR_T, SCHUR_NW = SCHUR_T / 64;
 __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ probs) {
@@ -1063,6 +1105,17 @@ __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ 
         return;
     }
     const double lambda = trial_lambda(lm);
+    if (k1 - k0 <= MAM_SCHUR_LANE_MAX) {
+        // a short block (most off-diagonal ones): the per-lane 36-entry sums would be mostly reduction
+        if (wid != 0) return;
+        const double v = schur_lane_sum(d, k0, k1, lane, threadIdx.x < 36, r36, c36);
+        if (threadIdx.x < 36) {
+            double out = -v;
+            if (i1 == i2) out = (hs + (r36 == c36 ? lambda : 0.0)) - v;
+            store(out);
+        }
+        return;
+    }
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
@@ -3240,15 +3293,332 @@ __device__ __forceinline__ void pose_epilogue(const Prob& d, LM& lm, int cur, co
     }
 }
 
-// grid (Q) x LDLT_THREADS: either form per problem (k_struct_tiles' choice, read on the device), so the host launches
-// one factorization per trial without reading the choice back; dynamic LDS: the larger of the two forms' needs
-template <bool use_lds>
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restrict__ probs) {
+// ---- the factorization with S's tiles in registers: the form for a dense reduced system (a covisibility window whose
+// local keyframes all share MapPoints: every tile of L non-zero, more than the LDS pool holds). The lower-triangle
+// tiles (i, j) are numbered by block column from the last and dealt round-robin over the 8 waves (tile q to wave q mod
+// 8, register slot q / 8: REG_RT slots of four doubles a lane, the MFMA accumulator layout), the next ones in the LDS
+// the launch has left over, the rest (the first columns) in place in S. Blocked
+// right-looking LDL^T as ldlt_global computes it, with no global memory round trip inside the loop: per block column
+// k (a) the owners stage the diagonal tile and the panel tiles in LDS, (b) wave 0 factors the diagonal tile and
+// solves y_k, (c) every thread one panel row (L21 = A21 L11^-T D^-1, y2 -= L21 y1), (d) the owners take their L
+// tiles back and update their trailing tiles by f64 MFMA (operands from the staged panel). Then y /= D and the
+// backward substitution by block rows: wave 0 solves the diagonal block, each tile of the row subtracts L^T y_k from
+// its column's y block (one tile per y block per step: no two writers).
+// REG_T threads, REG_RT tiles a wave (at 256 threads a wave may hold 512 registers, but the compiler keeps ~2 registers
+// per tile element: 24 tiles a wave at 256 threads, 16 at 512, the same 128 tiles a workgroup without spills)
+#ifndef MAM_LBA_REG_T
+#define MAM_LBA_REG_T 512
+#endif
+#ifndef MAM_LBA_REG_RT
+#define MAM_LBA_REG_RT 16
+#endif
+constexpr int REG_T = MAM_LBA_REG_T, REG_RT = MAM_LBA_REG_RT;
+__host__ __device__ inline size_t ldlt_reg_lds_bytes(int nt) {
+    const int ntri = nt * (nt + 1) / 2, N = 16 * nt;
+    return ((size_t)16 * (N - 16) + 2 * (size_t)N + 256) * sizeof(double) + 2 * (size_t)ntri + 16;
+}
+
+#ifdef MAM_REG_PROFILE
+// cycles per phase summed over workgroups (thread 0 after each barrier): init, (a) staging, (b) diagonal tile,
+// (c) panel rows, (d) updates, backward solve, -, WGs
+__device__ unsigned long long g_rprof[8];
+#define RPROF(k)                                                                     \
+    do {                                                                             \
+        if (t == 0) {                                                                \
+            const long long tn = clock64();                                          \
+            atomicAdd(&g_rprof[k], (unsigned long long)(tn - rp0));                  \
+            rp0 = tn;                                                                \
+        }                                                                            \
+    } while (0)
+#else
+#define RPROF(k) \
+    do {         \
+    } while (0)
+#endif
+
+__device__ __forceinline__ void ldlt_reg(const Prob& d, double* lds, size_t lds_bytes, LdltShared& sh) {
+#ifdef MAM_REG_PROFILE
+    long long rp0 = clock64();
+    if (threadIdx.x == 0) atomicAdd(&g_rprof[7], 1ull);
+#endif
+    LM& lm = *d.lm;
+    constexpr int T = REG_T, NW = T / 64;
+    const int nt = d.nt, N = d.npad, n = 6 * d.Np;
+    const int ntri = nt * (nt + 1) / 2, nreg = NW * REG_RT;
+    const int over = ntri > nreg ? ntri - nreg : 0;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int col = lane & 15, rq = lane >> 4;
+    const int mmax = N - 16;
+    double* PT = lds;                        // the staged panel, transposed: L(16 (k + 1) + r, 16 k + c) at c * m + r
+    double* Y = PT + (size_t)16 * mmax;
+    double* Dd = Y + N;                      // D
+    double* DB = Dd + N;                     // the diagonal tile: column-major (forward), row-major L (backward)
+    int8_t* ti = reinterpret_cast<int8_t*>(DB + 256);
+    int8_t* tj = ti + ntri;
+    uint8_t* tm = reinterpret_cast<uint8_t*>(sh.map);   // the tile mask of L (S + fill)
+    gdouble* A = (gdouble*)d.S;
+    // overflow tile q: LDS slot q - nreg while they last (after the tables), else in place in S
+    double* OT = reinterpret_cast<double*>(((uintptr_t)(tj + ntri) + 15) & ~(uintptr_t)15);
+    const size_t used = (size_t)((char*)OT - (char*)lds);
+    const int nlds = lds_bytes > used ? (int)((lds_bytes - used) / (256 * sizeof(double))) : 0;
+    auto at = [&](int q, int r, int c) -> double* {
+        return q - nreg < nlds ? OT + (size_t)(q - nreg) * 256 + r * 16 + c
+                               : (double*)(A + (size_t)(16 * ti[q] + r) * N + 16 * tj[q] + c);
+    };
+    // tile order: by block column from the last (updated at every step) to the first (read once as a panel), so the
+    // registers hold the most-updated tiles and the ones in S are a few first columns', touched at a step or two
+    for (int q = t; q < ntri; q += T) {
+        int r, c;
+        tri_index(q, &r, &c);   // r = columns from the end - 1, c = rows below the diagonal
+        ti[q] = (int8_t)(nt - 1 - r + c);
+        tj[q] = (int8_t)(nt - 1 - r);
+    }
+    for (int q = t; q < nt * nt; q += T) tm[q] = d.tmask[q];
+    for (int i = t; i < N; i += T) Y[i] = i < n ? d.bs[i] : 0.0;
+    if (t == 0) sh.fail = 0;
+    __syncthreads();
+    // S's lower triangle; the padding rows / columns an identity block (as ldlt_global sets it), a diagonal tile's
+    // upper triangle zero
+    auto s_at = [&](int row, int cc) -> double {
+        if (cc > row) return 0.0;
+        if (row >= n || cc >= n) return row == cc ? 1.0 : 0.0;
+        return A[(size_t)row * N + cc];
+    };
+    // (the overflow tiles' elements are read and rewritten by the same thread)
+    dbl4 R[REG_RT];
+#pragma unroll
+    for (int u = 0; u < REG_RT; u++) {
+        const int q = u * NW + wid;
+        R[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+        if (q < ntri) {
+            const int i = ti[q], j = tj[q];
+            if (tm[i * nt + j]) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) R[u][r] = s_at(16 * i + rq + 4 * r, 16 * j + col);
+            }
+        }
+    }
+    for (int x = t; x < over * 256; x += T) {
+        const int q = nreg + x / 256, e = x % 256, i = ti[q], j = tj[q];
+        const double v = tm[i * nt + j] ? s_at(16 * i + e / 16, 16 * j + e % 16) : 0.0;
+        *at(q, e / 16, e % 16) = v;
+    }
+    __syncthreads();
+    RPROF(0);
+    for (int k = 0; k < nt; k++) {
+        const int m = 16 * (nt - k - 1);
+        // (a) the diagonal tile -> DB, the column's panel tiles -> PT
+#pragma unroll
+        for (int u = 0; u < REG_RT; u++) {
+            const int q = u * NW + wid;
+            if (q >= ntri) continue;
+            const int i = ti[q], j = tj[q];
+            if (j != k) continue;
+            if (i == k) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) DB[col * 16 + rq + 4 * r] = R[u][r];
+            } else if (tm[i * nt + k]) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) PT[col * m + 16 * (i - k - 1) + rq + 4 * r] = R[u][r];
+            }
+        }
+        for (int x = t; x < over * 256; x += T) {
+            const int q = nreg + x / 256;
+            if (tj[q] != k) continue;
+            const int i = ti[q], e = x % 256;
+            if (i == k) DB[(e % 16) * 16 + e / 16] = *at(q, e / 16, e % 16);
+            else if (tm[i * nt + k]) PT[(e % 16) * m + 16 * (i - k - 1) + e / 16] = *at(q, e / 16, e % 16);
+        }
+        __syncthreads();
+        RPROF(1);
+        // (b) wave 0: LDL^T of the diagonal tile, the forward block solve of y_k
+        if (wid == 0) {
+            double row[NB];
+#pragma unroll
+            for (int c = 0; c < NB; c++) row[c] = lane < NB ? DB[c * 16 + lane] : 0.0;
+            const double dmine = diag16_factor(row, lane);
+            const double yv = diag16_forward(row, lane < NB ? Y[16 * k + lane] : 0.0, lane);
+            if (lane < NB) {
+#pragma unroll
+                for (int c = 0; c < NB; c++) sh.Ld[lane * NB + c] = row[c];
+                sh.dk[0][lane] = dmine;
+                sh.invdk[lane] = dmine != 0.0 ? 1.0 / dmine : 0.0;
+                Dd[16 * k + lane] = dmine;
+                Y[16 * k + lane] = yv;
+                if (dmine == 0.0) sh.fail = 1;
+            }
+        }
+        __syncthreads();
+        RPROF(2);
+        // (c) the panel rows in place: L21 = A21 L11^-T D^-1, y2 -= L21 y1
+        for (int r = t; r < m; r += T) {
+            const int i = 16 * (k + 1) + r;
+            if (!tm[(i >> 4) * nt + k]) continue;
+            asm volatile("" ::: "memory");
+            double w[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j++) w[j] = PT[j * m + r];
+#pragma unroll
+            for (int j = 1; j < NB; j++) {
+#pragma unroll
+                for (int kk = 0; kk < j; kk++) w[j] = fma(-w[kk], sh.Ld[j * NB + kk], w[j]);
+            }
+            double yi = Y[i];
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const double lij = w[j] * sh.invdk[j];
+                PT[j * m + r] = lij;
+                yi = fma(-lij, Y[16 * k + j], yi);
+            }
+            Y[i] = yi;
+        }
+        __syncthreads();
+        RPROF(3);
+        // (d) the column's L back into its tiles; the trailing tiles -= L(i, k) D L(j, k)^T
+#pragma unroll
+        for (int u = 0; u < REG_RT; u++) {
+            const int q = u * NW + wid;
+            if (q >= ntri) continue;
+            const int i = ti[q], j = tj[q];
+            if (j == k) {
+                if (i == k) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) R[u][r] = sh.Ld[(rq + 4 * r) * NB + col];
+                } else if (tm[i * nt + k]) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) R[u][r] = PT[col * m + 16 * (i - k - 1) + rq + 4 * r];
+                }
+            } else if (j > k && tm[i * nt + j] && tm[i * nt + k] && tm[j * nt + k]) {
+                const int bi = 16 * (i - k - 1), bj = 16 * (j - k - 1);
+#pragma unroll
+                for (int k0 = 0; k0 < NB; k0 += 4) {
+                    const int kk = k0 + rq;
+                    const double av = -PT[kk * m + bi + col];
+                    const double bv = PT[kk * m + bj + col] * sh.dk[0][kk];
+                    R[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, R[u], 0, 0, 0);
+                }
+            }
+        }
+        for (int q = nreg + wid; q < ntri; q += NW) {
+            const int i = ti[q], j = tj[q];
+            if (j == k) {
+                if (i == k) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) *at(q, rq + 4 * r, col) = sh.Ld[(rq + 4 * r) * NB + col];
+                } else if (tm[i * nt + k]) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) *at(q, rq + 4 * r, col) = PT[col * m + 16 * (i - k - 1) + rq + 4 * r];
+                }
+            } else if (j > k && tm[i * nt + j] && tm[i * nt + k] && tm[j * nt + k]) {
+                const int bi = 16 * (i - k - 1), bj = 16 * (j - k - 1);
+                dbl4 c4;
+#pragma unroll
+                for (int r = 0; r < 4; r++) c4[r] = *at(q, rq + 4 * r, col);
+#pragma unroll
+                for (int k0 = 0; k0 < NB; k0 += 4) {
+                    const int kk = k0 + rq;
+                    const double av = -PT[kk * m + bi + col];
+                    const double bv = PT[kk * m + bj + col] * sh.dk[0][kk];
+                    c4 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c4, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) *at(q, rq + 4 * r, col) = c4[r];
+            }
+        }
+        __syncthreads();
+        RPROF(4);
+    }
+    if (t == 0) lm.fail = sh.fail;
+    if (sh.fail) return;   // uniform (LDS flag after the last barrier)
+    for (int i = t; i < N; i += T) Y[i] /= Dd[i];
+    __syncthreads();
+    // backward substitution L^T x = y by block rows, the last first
+    for (int k = nt - 1; k >= 0; k--) {
+        const int qd = (nt - k) * (nt - k - 1) / 2;   // the diagonal tile (row-major L into DB)
+        if (qd < nreg) {
+            if (qd % NW == wid) {
+#pragma unroll
+                for (int u = 0; u < REG_RT; u++)
+                    if (u * NW + wid == qd) {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) DB[(rq + 4 * r) * 16 + col] = R[u][r];
+                    }
+            }
+        } else {
+            for (int x = t; x < 256; x += T) DB[x] = *at(qd, x / 16, x % 16);
+        }
+        __syncthreads();
+        if (wid == 0) {
+            double cl[NB];   // lane c: L(kb + j, kb + c)
+#pragma unroll
+            for (int j = 0; j < NB; j++) cl[j] = lane < NB ? DB[j * 16 + lane] : 0.0;
+            double v = lane < NB ? Y[16 * k + lane] : 0.0;
+#pragma unroll
+            for (int j = NB - 1; j >= 0; j--) {
+                const double xj = bcast16_d(v, j);
+                if (lane < j) v = fma(-cl[j], xj, v);
+            }
+            if (lane < NB) Y[16 * k + lane] = v;
+        }
+        __syncthreads();
+        // y_j -= L(k, j)^T y_k for the row's non-zero tiles j < k
+        const double y0 = Y[16 * k + rq], y1 = Y[16 * k + rq + 4], y2 = Y[16 * k + rq + 8], y3 = Y[16 * k + rq + 12];
+#pragma unroll
+        for (int u = 0; u < REG_RT; u++) {
+            const int q = u * NW + wid;
+            if (q >= ntri) continue;
+            const int i = ti[q], j = tj[q];
+            if (i != k || j >= k || !tm[i * nt + j]) continue;
+            double p = R[u][0] * y0;
+            p = fma(R[u][1], y1, p);
+            p = fma(R[u][2], y2, p);
+            p = fma(R[u][3], y3, p);
+            p += __shfl_xor(p, 16, 64);
+            p += __shfl_xor(p, 32, 64);
+            if (rq == 0) Y[16 * j + col] -= p;
+        }
+        for (int q = nreg + wid; q < ntri; q += NW) {
+            const int i = ti[q], j = tj[q];
+            if (i != k || j >= k || !tm[i * nt + j]) continue;
+            double p = *at(q, rq, col) * y0;
+            p = fma(*at(q, rq + 4, col), y1, p);
+            p = fma(*at(q, rq + 8, col), y2, p);
+            p = fma(*at(q, rq + 12, col), y3, p);
+            p += __shfl_xor(p, 16, 64);
+            p += __shfl_xor(p, 32, 64);
+            if (rq == 0) Y[16 * j + col] -= p;
+        }
+        __syncthreads();
+    }
+    for (int i = t; i < n; i += T) d.x[6 * (size_t)d.iperm[i / 6] + i % 6] = Y[i];   // (pose order)
+    RPROF(5);
+}
+
+// grid (Q) x LDLT_THREADS: the register form for the problems it takes (dense, nt <= reg_nt_max; k_ldlt_any leaves
+// them alone), then the trial poses
+__global__ __launch_bounds__(REG_T) void k_ldlt_reg(const Prob* __restrict__ probs, int reg_nt_max,
+                                                           size_t lds_bytes) {
     extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
     __shared__ LdltShared sh;
     const Prob& d = probs[blockIdx.x];
     const LMHead hd = lm_head(d.lm);
     if (hd.status || hd.done) return;
+    if (d.Np == 0 || hd.tiles_lds || d.nt > reg_nt_max) return;
+    ldlt_reg(d, lds_dyn, lds_bytes, sh);
+    __syncthreads();
+    pose_epilogue<REG_T>(d, *d.lm, hd.cur, d.x, trial_lambda(hd));
+}
+
+// grid (Q) x LDLT_THREADS: either form per problem (k_struct_tiles' choice, read on the device), so the host launches
+// one factorization per trial without reading the choice back; dynamic LDS: the larger of the two forms' needs
+template <bool use_lds>
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restrict__ probs, int reg_nt_max) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const Prob& d = probs[blockIdx.x];
+    const LMHead hd = lm_head(d.lm);
+    if (hd.status || hd.done) return;
+    if (d.Np > 0 && !hd.tiles_lds && d.nt <= reg_nt_max) return;   // k_ldlt_reg's
     LM& lm = *d.lm;
     if (d.Np == 0) {
         if (threadIdx.x == 0) lm.fail = 0;
@@ -3548,6 +3918,36 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     // the HBM form's panel workspace, the larger
     size_t ldlt_dyn = c->ldlt_lds_budget;
     if (lds_ok) ldlt_dyn = std::max(ldlt_dyn, max_lds);
+    // the register form (k_ldlt_reg) for the problems whose nt it holds in registers + the LDS budget, unless they
+    // fit the LDS tile pool (decided on the device), with MAM_LBA_REG=1; otherwise every problem goes to k_ldlt_any
+    // (while the tiles neither registers nor the LDS left over hold — read-modify-written in S — number at most
+    // MAM_LBA_REG_GLOBAL, default 64)
+    int reg_nt_max = 0, reg_nt_used = 0;
+    auto reg_over_lds = [](int nt) {   // tiles past the registers, and the LDS they take (+ the 16-B alignment)
+        const int over = std::max(0, nt * (nt + 1) / 2 - (REG_T / 64) * REG_RT);
+        return std::make_pair(over, (size_t)over * 256 * sizeof(double) + 16);
+    };
+    {
+        const char* rv = std::getenv("MAM_LBA_REG");
+        const char* gv = std::getenv("MAM_LBA_REG_GLOBAL");
+        const int gmax = gv ? std::atoi(gv) : 64;
+        if (rv && rv[0] == '1')   // (off by default until it beats the HBM form: DESIGN §6)
+            while (reg_nt_max < LDLT_TM_MAX) {
+                const int nt = reg_nt_max + 1;
+                const size_t base = ldlt_reg_lds_bytes(nt);
+                if (base + 16 > c->ldlt_lds_budget) break;
+                const auto ov = reg_over_lds(nt);
+                const int fit = (int)((c->ldlt_lds_budget - base - 16) / (256 * sizeof(double)));
+                if (ov.first - fit > gmax) break;
+                reg_nt_max = nt;
+            }
+        for (auto& d : hp)
+            if (d.Np > 0 && d.npad / NB <= reg_nt_max) reg_nt_used = std::max(reg_nt_used, d.npad / NB);
+        if (reg_nt_used == 0) reg_nt_max = 0;
+    }
+    const size_t reg_dyn = reg_nt_used ? std::min(c->ldlt_lds_budget, ldlt_reg_lds_bytes(reg_nt_used) +
+                                                                          reg_over_lds(reg_nt_used).second)
+                                       : 0;
     const dim3 gE((maxE + 255) / 256 > 0 ? (maxE + 255) / 256 : 1, Q);
     const dim3 gE64((maxE + EW - 1) / EW > 0 ? (maxE + EW - 1) / EW : 1, Q);
     {
@@ -3654,9 +4054,12 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         {
             mam::StageTimer::Scope sc(tm, st, 2);
             if (lds_ok)
-                hipLaunchKernelGGL(k_ldlt_any<true>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg);
+                hipLaunchKernelGGL(k_ldlt_any<true>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg, reg_nt_max);
             else
-                hipLaunchKernelGGL(k_ldlt_any<false>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg);
+                hipLaunchKernelGGL(k_ldlt_any<false>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg, reg_nt_max);
+            if (reg_nt_max)
+                hipLaunchKernelGGL(k_ldlt_reg, dim3(Qg), dim3(REG_T), reg_dyn, st, Pg, reg_nt_max,
+                                   reg_dyn);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 3);
@@ -3747,6 +4150,22 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
                 h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[6] / w, h[7]);
     }
 #endif
+#ifdef MAM_REG_PROFILE
+    {
+        MAM_HIP(hipStreamSynchronize(s));
+        unsigned long long h[8];
+        MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::lba::g_rprof), sizeof(h)));
+        const double w = (double)std::max(1ull, h[7]);
+        int hist[64] = {0};
+        for (auto& d : hp)
+            if (d.Np > 0) hist[std::min(63, d.npad / NB)]++;
+        for (int i = 0; i < 64; i++)
+            if (hist[i]) fprintf(stderr, "nt %d: %d problems\n", i, hist[i]);
+        fprintf(stderr, "reg ldlt cycles per WG: init %.0f stage %.0f diag %.0f panel %.0f update %.0f backward %.0f; "
+                        "WGs %llu reg_nt_max %d\n", h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7],
+                reg_nt_max);
+    }
+#endif
     return MAM_OK;
 }
 
@@ -3810,6 +4229,8 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_any<true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess &&
             hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_any<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_reg),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess) {
             c->ldlt_lds_budget = budget;
             break;

@@ -18,6 +18,16 @@ for part in ${PARTS:-probe3 probe4 dense tests}; do
     probe2)
       timeout -k 10 400 python3 -u scripts/ringmap_probe.py --config c2 --runs 10 --check > $O/probe_c2.log 2>&1 || { tail -5 $O/probe_c2.log; exit 1; }
       grep '"run": [6-9]' $O/probe_c2.log | cut -c1-330; grep same_control $O/probe_c2.log ;;
+    dump)
+      mkdir -p variants
+      timeout -k 10 400 python3 -u scripts/ringmap_probe.py --config c2 --runs 8 --check --dump variants/ring_windows.npz > $O/probe_dump.log 2>&1 || { tail -5 $O/probe_dump.log; exit 1; }
+      grep same_control $O/probe_dump.log | cut -c1-400; cp variants/ring_windows.npz $O/ ;;
+    regab)
+      for reg in 1 0; do
+        echo "-- MAM_LBA_REG=$reg"
+        MAM_LBA_REG=$reg timeout -k 10 180 python3 -u scripts/ring_window_replay.py variants/ring_windows.npz --mode batch --solves 6 > $O/regab_$reg.log 2>&1 || { tail -5 $O/regab_$reg.log; exit 1; }
+        grep -v "^window" $O/regab_$reg.log
+      done ;;
     dense)
       LV="${LV:-main t1024 b8}" SPLITS="${SPLITS:-1 2 4}" bash scripts/gpu_lba_dense.sh || exit 1 ;;
     tests)

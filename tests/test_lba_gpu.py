@@ -165,6 +165,34 @@ def test_lba_batch_same_shape(solver, oracle):
         assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
 
 
+def test_lba_dense_register_form(solver, oracle, monkeypatch):
+    """Dense reduced systems past the LDS tile pool (every pose pair shares landmarks): the register form of the
+    factorization (k_ldlt_reg, MAM_LBA_REG=1) holds 128 tiles in registers, the next ones in LDS and the rest in place in S; nt 15
+    (all in registers), 19 (registers + LDS), 21 (+ 54 tiles in S). Batched and alone, the oracle's control flow and
+    solution."""
+    import torch
+
+    from mam3slam_amd.lba import DeviceBatch, id_ordered
+
+    monkeypatch.setenv("MAM_LBA_REG", "1")
+    probs = [synthetic_problem(n_opt=n, n_fixed=8, n_points=1200, obs_per_point=14, seed=60 + n, init_kf_local=False)
+             for n in (40, 50, 56)]
+    B = DeviceBatch(probs, torch.device("cuda", 0))
+    stats = solver.solve_batch_device(B)
+    for i, p in enumerate(probs):
+        ro = oracle.lba_solve(id_ordered(p)[0])
+        for rg, st in ((B.result(i), stats[i]["status"]), (None, None)):
+            if rg is None:
+                rg = solver.solve(p)
+                ro = oracle.lba_solve(p)
+                st = rg.status
+            assert st == 0 and ro.status == 0
+            assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials), i
+            assert abs(rg.final_chi2 - ro.final_chi2) <= 1e-6 * ro.final_chi2
+            assert _rel(rg.pose_t, ro.pose_t) <= 1e-4 and _rel(rg.pose_q, ro.pose_q) <= 1e-4
+            assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
+
+
 @pytest.mark.parametrize("pw", ["2", "4", "8"])
 def test_lba_points_per_workgroup(solver, oracle, pw, monkeypatch):
     """The point kernels at 2 / 4 / 8 points per workgroup (a lone window of many observations a point takes 2, batches
