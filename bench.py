@@ -1389,9 +1389,9 @@ def main():
             ach = args.steps * tr_mean * sum(fl_ldlt) / (ms_solve * 1e-3) / 1e12 if ms_solve else None
             # the FP64-MFMA counter pass over the windows this leg solves (ring: profiles/r05's 32 ring windows;
             # the synthetic world's windows: the round-4 pass over its batch of 32)
-            mrel = ("profiles/r05/lba_mfma_f64_ring.json" if args.lm_windows == "ring"
-                    and os.path.exists(os.path.join(ROOT, "profiles/r05/lba_mfma_f64_ring.json"))
-                    else "profiles/r04/lba_mfma_f64.json")
+            mrel = next((f"profiles/{r}/{f}" for r in ("r06", "r05", "r04")
+                         for f in (("lba_mfma_f64_ring.json",) if args.lm_windows == "ring" else ("lba_mfma_f64.json",))
+                         if os.path.exists(os.path.join(ROOT, f"profiles/{r}/{f}"))), "profiles/r04/lba_mfma_f64.json")
             mpath = os.path.join(ROOT, mrel)
             mfma = None
             if os.path.exists(mpath):

@@ -86,6 +86,10 @@ __device__ __forceinline__ LMHead lm_head(const LM* lm) {
     return h;
 }
 
+// the column-chain factorization's per-problem ints: [0] claim counter, [1] the launch's base, [2] failure, [8 + k]
+// column k's flag (k < 40)
+constexpr int MW_INTS = 48;
+
 struct Prob {
     int P, L, E, Np, npad, n_cams, cam_model;
     double delta;                // Huber delta; <= 0: no robust kernel
@@ -156,7 +160,8 @@ struct Prob {
     double* S;                   // [npad][npad]
     double* x;                   // [6Np + 3L]
     double* bs;                  // [npad]
-    double* ws;                  // LDL^T workspace when it does not fit in LDS
+    double* ws;                  // LDL^T workspace when it does not fit in LDS (the column-chain form: y, D)
+    int32_t* mw;                 // the column-chain form's claim counter, launch base, failure, column flags (MW_INTS)
     uint8_t* depth;              // [E] isDepthPositive of the final state
     LM* lm;
 };
@@ -377,6 +382,7 @@ __global__ __launch_bounds__(SB) void k_struct_init(const Prob* __restrict__ pro
         }
     }
     for (int i = g0; i < d.L + d.Np; i += gstride) d.cnt[i] = 0;
+    if (g0 < MW_INTS) d.mw[g0] = 0;
     for (size_t i = g0; i < (size_t)d.Np * d.Np; i += gstride) d.pairmask[i] = 0;
     if (g0 < 64) d.pm_rows[g0] = 0ull;
     const size_t n6 = 6 * (size_t)d.Np;
@@ -1023,7 +1029,8 @@ constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per
 #define MAM_SCHUR_T 128   // lone window: 64 / 128 / 256 threads 23.0 / 21.9 / 24.5 us per launch
 #endif
 #ifndef MAM_SCHUR_LANE_MAX
-#define MAM_SCHUR_LANE_MAX 192   // blocks of at most this many landmark pairs: one wave, a lane per entry (0: never)
+#define MAM_SCHUR_LANE_MAX 0   // blocks of at most this many landmark pairs: one wave, a lane per entry (0: never;
+                               // 192 measured slower: ring batch 472 -> 603 us, world window 0.20 -> 0.32 ms per solve)
 #endif
 constexpr int SCHUR_T = MAM_SCHUR_T, SCHUR_NW = SCHUR_T / 64;
 __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ probs) {
@@ -3313,9 +3320,13 @@ __device__ __forceinline__ void pose_epilogue(const Prob& d, LM& lm, int cur, co
 #define MAM_LBA_REG_RT 16
 #endif
 constexpr int REG_T = MAM_LBA_REG_T, REG_RT = MAM_LBA_REG_RT;
+#ifndef MAM_REG_PANEL_MFMA
+#define MAM_REG_PANEL_MFMA 0   // the panel by L11^-T D^-1 and f64 MFMA (spills at REG_RT 16; 0: per-row forward
+                               // substitution)
+#endif
 __host__ __device__ inline size_t ldlt_reg_lds_bytes(int nt) {
     const int ntri = nt * (nt + 1) / 2, N = 16 * nt;
-    return ((size_t)16 * (N - 16) + 2 * (size_t)N + 256) * sizeof(double) + 2 * (size_t)ntri + 16;
+    return ((size_t)16 * (N - 16) + 2 * (size_t)N + 512) * sizeof(double) + 2 * (size_t)ntri + 16;
 }
 
 #ifdef MAM_REG_PROFILE
@@ -3353,7 +3364,8 @@ __device__ __forceinline__ void ldlt_reg(const Prob& d, double* lds, size_t lds_
     double* Y = PT + (size_t)16 * mmax;
     double* Dd = Y + N;                      // D
     double* DB = Dd + N;                     // the diagonal tile: column-major (forward), row-major L (backward)
-    int8_t* ti = reinterpret_cast<int8_t*>(DB + 256);
+    double* MB = DB + 256;                   // L11^-T D^-1 (row kk, column j at kk * 16 + j): the panel's right factor
+    int8_t* ti = reinterpret_cast<int8_t*>(MB + 256);
     int8_t* tj = ti + ntri;
     uint8_t* tm = reinterpret_cast<uint8_t*>(sh.map);   // the tile mask of L (S + fill)
     gdouble* A = (gdouble*)d.S;
@@ -3422,10 +3434,10 @@ __device__ __forceinline__ void ldlt_reg(const Prob& d, double* lds, size_t lds_
                 for (int r = 0; r < 4; r++) PT[col * m + 16 * (i - k - 1) + rq + 4 * r] = R[u][r];
             }
         }
-        for (int x = t; x < over * 256; x += T) {
-            const int q = nreg + x / 256;
-            if (tj[q] != k) continue;
-            const int i = ti[q], e = x % 256;
+        // column k's tiles are q in [c0, c0 + nt - k) (diagonal first), its overflow ones the part past nreg
+        const int c0 = (nt - k) * (nt - k - 1) / 2, oq0 = max(c0, nreg), oq1 = c0 + nt - k;
+        for (int x = t; x < (oq1 - oq0) * 256; x += T) {
+            const int q = oq0 + x / 256, i = k + (q - c0), e = x % 256;
             if (i == k) DB[(e % 16) * 16 + e / 16] = *at(q, e / 16, e % 16);
             else if (tm[i * nt + k]) PT[(e % 16) * m + 16 * (i - k - 1) + e / 16] = *at(q, e / 16, e % 16);
         }
@@ -3447,9 +3459,61 @@ __device__ __forceinline__ void ldlt_reg(const Prob& d, double* lds, size_t lds_
                 Y[16 * k + lane] = yv;
                 if (dmine == 0.0) sh.fail = 1;
             }
+#if MAM_REG_PANEL_MFMA
+            // L11^-1 by 16 forward solves of unit vectors (independent chains, interleaved), then MB = L11^-T D^-1
+            // (two halves of 8 columns: the tiles' registers leave room for 8 chains)
+            const double invd = dmine != 0.0 ? 1.0 / dmine : 0.0;
+#pragma unroll
+            for (int h = 0; h < NB; h += 8) {
+                double xc[8];
+#pragma unroll
+                for (int c = 0; c < 8; c++) xc[c] = lane == h + c ? 1.0 : 0.0;
+#pragma unroll
+                for (int j = 0; j < NB; j++) {
+#pragma unroll
+                    for (int c = 0; c < 8; c++) {
+                        if (h + c > j) continue;   // X(j, c) = 0 for j < c: nothing to subtract
+                        const double xj = bcast16_d(xc[c], j);
+                        if (lane > j) xc[c] = fma(-row[j], xj, xc[c]);
+                    }
+                }
+                if (lane < NB) {
+#pragma unroll
+                    for (int c = 0; c < 8; c++) MB[(h + c) * 16 + lane] = xc[c] * invd;   // M(c, lane) = Linv(lane, c) / d
+                }
+            }
+#endif
         }
         __syncthreads();
         RPROF(2);
+#if MAM_REG_PANEL_MFMA
+        // (c) the panel L21 = A21 M by f64 MFMA, one 16-row tile per wave in place (a wave reads and writes only its
+        // tile's rows); y2 -= L21 y1 in (d)
+        for (int rt = wid; rt < m / 16; rt += NW) {
+            if (!tm[(k + 1 + rt) * nt + k]) continue;
+            dbl4 c4 = dbl4{0.0, 0.0, 0.0, 0.0};
+            double av[4], bv[4];
+#pragma unroll
+            for (int k0 = 0; k0 < NB; k0 += 4) {
+                av[k0 / 4] = PT[(k0 + rq) * m + 16 * rt + col];
+                bv[k0 / 4] = MB[(k0 + rq) * 16 + col];
+            }
+#pragma unroll
+            for (int k0 = 0; k0 < 4; k0++) c4 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[k0], bv[k0], c4, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; r++) PT[col * m + 16 * rt + rq + 4 * r] = c4[r];
+        }
+        __syncthreads();
+        RPROF(3);
+        for (int r = t; r < m; r += T) {
+            const int i = 16 * (k + 1) + r;
+            if (!tm[(i >> 4) * nt + k]) continue;
+            double yi = Y[i];
+#pragma unroll
+            for (int j = 0; j < NB; j++) yi = fma(-PT[j * m + r], Y[16 * k + j], yi);
+            Y[i] = yi;
+        }
+#else
         // (c) the panel rows in place: L21 = A21 L11^-T D^-1, y2 -= L21 y1
         for (int r = t; r < m; r += T) {
             const int i = 16 * (k + 1) + r;
@@ -3474,6 +3538,7 @@ __device__ __forceinline__ void ldlt_reg(const Prob& d, double* lds, size_t lds_
         }
         __syncthreads();
         RPROF(3);
+#endif
         // (d) the column's L back into its tiles; the trailing tiles -= L(i, k) D L(j, k)^T
 #pragma unroll
         for (int u = 0; u < REG_RT; u++) {
@@ -3499,7 +3564,7 @@ __device__ __forceinline__ void ldlt_reg(const Prob& d, double* lds, size_t lds_
                 }
             }
         }
-        for (int q = nreg + wid; q < ntri; q += NW) {
+        for (int q = nreg + wid; q < c0 + nt - k; q += NW) {   // (columns < k are final)
             const int i = ti[q], j = tj[q];
             if (j == k) {
                 if (i == k) {
@@ -3577,9 +3642,9 @@ __device__ __forceinline__ void ldlt_reg(const Prob& d, double* lds, size_t lds_
             p += __shfl_xor(p, 32, 64);
             if (rq == 0) Y[16 * j + col] -= p;
         }
-        for (int q = nreg + wid; q < ntri; q += NW) {
-            const int i = ti[q], j = tj[q];
-            if (i != k || j >= k || !tm[i * nt + j]) continue;
+        for (int j = wid; j < k; j += NW) {   // row k's tiles (k, j): q = (nt - j)(nt - j - 1) / 2 + k - j
+            const int q = (nt - j) * (nt - j - 1) / 2 + k - j;
+            if (q < nreg || !tm[k * nt + j]) continue;
             double p = *at(q, rq, col) * y0;
             p = fma(*at(q, rq + 4, col), y1, p);
             p = fma(*at(q, rq + 8, col), y2, p);
@@ -3609,16 +3674,358 @@ __global__ __launch_bounds__(REG_T) void k_ldlt_reg(const Prob* __restrict__ pro
     pose_epilogue<REG_T>(d, *d.lm, hd.cur, d.x, trial_lambda(hd));
 }
 
+// ---- the dense factorization over several workgroups per problem (the column-chain form): a dense reduced system
+// (the covisibility windows of a map where every local keyframe shares MapPoints with every other: ~300-380 unknowns,
+// no zero tile) is ~10-18 MFLOP, too much dependent work for the one CU of the single-workgroup forms (~425 us a
+// launch of 16 such windows). Here MW_G workgroups per problem claim block columns in order from a per-problem counter
+// and each runs its column's whole left-looking chain: the column's tiles in registers (wave w: row blocks j + w,
+// j + w + 8, ...), then for every k < j with L(j, k) != 0: wait for column k's flag, L(i, k) D_k L(j, k)^T off its tiles
+// by f64 MFMA (the same products in the same k order as the right-looking forms) and y_j -= L(j, k) y_k; then its own
+// panel: the diagonal tile's LDL^T on wave 0, L21 = A21 L11^-T D^-1 one row a thread, L(:, j), D_j and the solved y_j
+// stored, the flag raised. The workgroup that finishes the last column does the backward substitution (row by row,
+// the next row's tiles loaded before the diagonal solve) and the trial poses. Deadlock-free without co-residency:
+// a column waits only for smaller columns, claimed earlier by running workgroups (one resident workgroup alone runs
+// every column in turn). Cross-workgroup data (L, D, y, flags) moves by agent-scope relaxed atomics (sc1 loads /
+// stores, coherent across XCDs) and an s_waitcnt before the flag — no L2 write-back / invalidate per step (an
+// agent-scope release writes the whole L2 back: DESIGN §6). Flags carry the launch's tag (base + 1; base advances by
+// the claims a launch makes), so nothing is reset between launches.
+#ifndef MAM_LBA_MW_G
+#define MAM_LBA_MW_G 8   // workgroups per dense problem
+#endif
+#ifndef MAM_LBA_MW_T
+#define MAM_LBA_MW_T 256   // threads: one wave per SIMD, 512 registers a wave (the column's tiles + the panel rows)
+#endif
+constexpr int MW_G = MAM_LBA_MW_G, MW_NT_MAX = 40, MW_T = MAM_LBA_MW_T;
+__host__ __device__ inline size_t ldlt_mw_lds_bytes(int npad) {
+    return ((size_t)16 * (npad > 16 ? npad - 16 : 0) + 256 + 256 + 48) * sizeof(double);
+}
+// (global address space: flat accesses would also count in lgkmcnt)
+typedef __attribute__((address_space(1))) int gint;
+__device__ __forceinline__ double ld_c(const double* p) {
+    return __hip_atomic_load((gdouble*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_c(double* p, double v) {
+    __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_ci(const int* p) {
+    return __hip_atomic_load((gint*)const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_ci(int* p, int v) {
+    __hip_atomic_store((gint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The published data (L, D, y: written once a launch, by sc1 stores, before the flag) is read after the flag with
+// plain loads from L2 once the CU's L1 is invalidated (MAM_MW_SC1_LOADS=1: agent-coherent loads instead). A line of a
+// published column is never in any L2 before its final value (only its owner reads the column's earlier values, and
+// the owner's sc1 stores update its own XCD's copy), so an L2 hit is current; the L1 may hold the owner's earlier
+// reads when it shares the CU, hence the invalidate.
+#ifndef MAM_MW_SC1_LOADS
+#define MAM_MW_SC1_LOADS 0
+#endif
+__device__ __forceinline__ double ld_pub(const double* p) {
+#if MAM_MW_SC1_LOADS
+    return ld_c(p);
+#else
+    return *(const gdouble*)p;
+#endif
+}
+__device__ __forceinline__ void inv_l1() {
+#if !MAM_MW_SC1_LOADS
+    asm volatile("buffer_inv sc0" ::: "memory");
+#endif
+}
+// thread 0 waits for column k's flag (bounded: a wait that never ends marks the factorization failed instead of hanging)
+__device__ __forceinline__ void mw_wait(int* mw, int k, int tag) {
+    int it = 0;
+    while (ld_ci(&mw[8 + k]) != tag) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > (1 << 20)) {
+            st_ci(&mw[2], 2);
+            break;
+        }
+    }
+}
+
+// returns true in the workgroup that finished the factorization and wrote d.x (it runs the pose epilogue)
+#ifdef MAM_MW_PROFILE
+// cycles summed over workgroups (thread 0): flag waits, the k steps' loads + updates, the panel, the publish, the
+// backward pass; [6] columns, [7] k steps
+__device__ unsigned long long g_mwprof[8];
+#define MWPROF(k)                                                                    \
+    do {                                                                             \
+        if (t == 0) {                                                                \
+            const long long tn = clock64();                                          \
+            atomicAdd(&g_mwprof[k], (unsigned long long)(tn - mp0));                 \
+            mp0 = tn;                                                                \
+        }                                                                            \
+    } while (0)
+#else
+#define MWPROF(k) \
+    do {          \
+    } while (0)
+#endif
+template <int T>
+__device__ bool ldlt_mw(const Prob& d, double* lds, LdltShared& sh) {
+#ifdef MAM_MW_PROFILE
+    long long mp0 = clock64();
+#endif
+    constexpr int NW = T / 64, RT = (MW_NT_MAX + NW - 1) / NW;   // tiles a wave holds
+    const int nt = d.nt, N = d.npad, n = 6 * d.Np;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6, col = lane & 15, rq = lane >> 4;
+    int* mw = d.mw;
+    double* S = d.S;
+    double* Yg = d.ws;
+    double* Dg = d.ws + N;
+    double* PT = lds;                         // the panel, transposed (c * m + r); the backward pass's z
+    double* DB = PT + (size_t)16 * (N - 16);  // the diagonal tile, column-major
+    double* LJ = DB + 256;                    // L(j, k), row-major
+    double* DK = LJ + 256;                    // D_k, then D_j
+    double* YK = DK + 16;                     // y_k
+    double* YJ = YK + 16;                     // the column's y block
+    uint8_t* tm = reinterpret_cast<uint8_t*>(sh.map);
+    __shared__ int s_col;
+    for (int q = t; q < nt * nt; q += T) tm[q] = ((const __attribute__((address_space(1))) uint8_t*)d.tmask)[q];
+    const int base = ld_ci(&mw[1]), tag = base + 1;
+    auto s_at = [&](int row, int cc) -> double {
+        if (cc > row) return 0.0;
+        if (row >= n || cc >= n) return row == cc ? 1.0 : 0.0;
+        return S[(size_t)row * N + cc];
+    };
+    bool last = false;
+    for (;;) {
+        __syncthreads();
+        if (t == 0) s_col = atomicAdd(&mw[0], 1) - base;
+        __syncthreads();
+        const int j = s_col;
+        if (j >= nt) {
+            if (t == 0 && j == nt + MW_G - 1) st_ci(&mw[1], base + nt + MW_G);   // every workgroup has read base
+            break;
+        }
+        // the column's tiles (S as k_schur_blk wrote it: padding identity, the diagonal tile's upper triangle zero)
+        dbl4 R[RT];
+#pragma unroll
+        for (int u = 0; u < RT; u++) {
+            const int i = j + wid + NW * u;
+            R[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+            if (i < nt && tm[i * nt + j]) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) R[u][r] = s_at(16 * i + rq + 4 * r, 16 * j + col);
+            }
+        }
+        if (t < 16) YJ[t] = 16 * j + t < n ? d.bs[16 * j + t] : 0.0;
+        for (int k = 0; k < j; k++) {
+            if (!tm[j * nt + k]) continue;
+            __syncthreads();   // (the previous step's LJ / YK reads)
+            MWPROF(1);
+            if (t == 0) mw_wait(mw, k, tag);
+            __syncthreads();
+            inv_l1();
+            MWPROF(0);
+#ifdef MAM_MW_PROFILE
+            if (t == 0) atomicAdd(&g_mwprof[7], 1ull);
+#endif
+            // L(j, k), D_k, y_k and the wave's A operands L(i, k) requested together: one memory round trip
+            static_assert(T == 256, "one L(j, k) element a thread");
+            const double ljv = ld_pub(&S[(size_t)(16 * j + t / 16) * N + 16 * k + t % 16]);
+            double dkv = 0.0, ykv = 0.0;
+            if (t < 16) {
+                dkv = ld_pub(&Dg[16 * k + t]);
+                ykv = ld_pub(&Yg[16 * k + t]);
+            }
+            double av[RT][4];
+#pragma unroll
+            for (int u = 0; u < RT; u++) {
+                const int i = j + wid + NW * u;
+                const bool on = i < nt && tm[i * nt + k];
+#pragma unroll
+                for (int q4 = 0; q4 < 4; q4++)
+                    av[u][q4] = on ? -ld_pub(&S[(size_t)(16 * i + col) * N + 16 * k + 4 * q4 + rq]) : 0.0;
+            }
+            LJ[t] = ljv;
+            if (t < 16) {
+                DK[t] = dkv;
+                YK[t] = ykv;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RT; u++) {
+                const int i = j + wid + NW * u;
+                if (i >= nt || !tm[i * nt + k]) continue;
+#pragma unroll
+                for (int q4 = 0; q4 < 4; q4++) {
+                    const int kk = 4 * q4 + rq;
+                    R[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u][q4], LJ[col * 16 + kk] * DK[kk], R[u], 0, 0, 0);
+                }
+            }
+            if (t < 16) {
+                double v = YJ[t];
+#pragma unroll
+                for (int c = 0; c < NB; c++) v = fma(-LJ[t * 16 + c], YK[c], v);
+                YJ[t] = v;
+            }
+        }
+        __syncthreads();
+        MWPROF(1);
+#ifdef MAM_MW_PROFILE
+        if (t == 0) atomicAdd(&g_mwprof[6], 1ull);
+#endif
+        // the column's panel: stage, factor the diagonal tile, the panel rows
+        const int m = 16 * (nt - j - 1);
+#pragma unroll
+        for (int u = 0; u < RT; u++) {
+            const int i = j + wid + NW * u;
+            if (i >= nt) continue;
+            if (i == j) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) DB[col * 16 + rq + 4 * r] = R[u][r];
+            } else if (tm[i * nt + j]) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) PT[col * m + 16 * (i - j - 1) + rq + 4 * r] = R[u][r];
+            }
+        }
+        __syncthreads();
+        if (wid == 0) {
+            double row[NB];
+#pragma unroll
+            for (int c = 0; c < NB; c++) row[c] = lane < NB ? DB[c * 16 + lane] : 0.0;
+            const double dmine = diag16_factor(row, lane);
+            const double yv = diag16_forward(row, lane < NB ? YJ[lane] : 0.0, lane);
+            if (lane < NB) {
+#pragma unroll
+                for (int c = 0; c < NB; c++) sh.Ld[lane * NB + c] = row[c];
+                sh.invdk[lane] = dmine != 0.0 ? 1.0 / dmine : 0.0;
+                DK[lane] = dmine;
+                YJ[lane] = yv;
+                if (dmine == 0.0) st_ci(&mw[2], 1);
+            }
+        }
+        __syncthreads();
+        for (int r = t; r < m; r += T) {
+            if (!tm[(j + 1 + r / 16) * nt + j]) continue;
+            asm volatile("" ::: "memory");   // (keeps the 120 L11 reads in the loop: hoisted they take 240 VGPRs)
+            double w[NB];
+#pragma unroll
+            for (int c = 0; c < NB; c++) w[c] = PT[c * m + r];
+            // right-looking: once w[kk] is final its updates are independent (each w[c] still takes them in kk order:
+            // the same operations as the row's dot products, 16 dependent steps instead of 120)
+#pragma unroll
+            for (int kk = 0; kk < NB - 1; kk++) {
+#pragma unroll
+                for (int c = kk + 1; c < NB; c++) w[c] = fma(-w[kk], sh.Ld[c * NB + kk], w[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < NB; c++) PT[c * m + r] = w[c] * sh.invdk[c];
+        }
+        __syncthreads();
+        MWPROF(2);
+        // publish L(:, j) (the diagonal tile's unit lower part; D_j apart), D_j, y_j; then the flag
+        for (int x = t; x < 256; x += T) {
+            const int r = x / 16, c = x % 16;
+            if (c < r) st_c(&S[(size_t)(16 * j + r) * N + 16 * j + c], sh.Ld[r * NB + c]);
+        }
+        for (int x = t; x < m * 16; x += T) {
+            const int r = x / 16, c = x % 16;
+            if (tm[(j + 1 + r / 16) * nt + j]) st_c(&S[(size_t)(16 * (j + 1) + r) * N + 16 * j + c], PT[c * m + r]);
+        }
+        if (t < 16) {
+            st_c(&Dg[16 * j + t], DK[t]);
+            st_c(&Yg[16 * j + t], YJ[t]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) st_ci(&mw[8 + j], tag);
+        MWPROF(3);
+        if (j == nt - 1) last = true;
+    }
+    if (!last) return false;
+    // the backward substitution L^T x = D^-1 y, by block rows from the last (every column's flag first: the last
+    // column's chain skipped the columns whose L(nt - 1, k) is zero)
+    if (t == 0)
+        for (int k = 0; k < nt; k++) mw_wait(mw, k, tag);
+    __syncthreads();
+    inv_l1();
+    LM& lm = *d.lm;
+    const int fl = ld_ci(&mw[2]);
+    if (t == 0) lm.fail = fl != 0;
+    if (fl) return true;
+    double* Z = PT;
+    for (int i = t; i < N; i += T) Z[i] = ld_pub(&Yg[i]) / ld_pub(&Dg[i]);
+    __syncthreads();
+    for (int k = nt - 1; k >= 0; k--) {
+        // row k's tiles (k, i), i < k, loaded first (their latency under the diagonal solve)
+        dbl4 Q[RT];
+#pragma unroll
+        for (int u = 0; u < RT; u++) {
+            const int i = wid + NW * u;
+            Q[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+            if (i < k && tm[k * nt + i]) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) Q[u][r] = ld_pub(&S[(size_t)(16 * k + rq + 4 * r) * N + 16 * i + col]);
+            }
+        }
+        if (wid == 0) {
+            double cl[NB];   // lane c: L(kb + jj, kb + c)
+#pragma unroll
+            for (int jj = 0; jj < NB; jj++)
+                cl[jj] = (lane < NB && jj > lane) ? ld_pub(&S[(size_t)(16 * k + jj) * N + 16 * k + lane]) : 0.0;
+            double v = lane < NB ? Z[16 * k + lane] : 0.0;
+#pragma unroll
+            for (int jj = NB - 1; jj >= 0; jj--) {
+                const double xj = bcast16_d(v, jj);
+                if (lane < jj) v = fma(-cl[jj], xj, v);
+            }
+            if (lane < NB) Z[16 * k + lane] = v;
+        }
+        __syncthreads();
+        const double y0 = Z[16 * k + rq], y1 = Z[16 * k + rq + 4], y2 = Z[16 * k + rq + 8], y3 = Z[16 * k + rq + 12];
+#pragma unroll
+        for (int u = 0; u < RT; u++) {
+            const int i = wid + NW * u;
+            if (i >= k || !tm[k * nt + i]) continue;
+            double p = Q[u][0] * y0;
+            p = fma(Q[u][1], y1, p);
+            p = fma(Q[u][2], y2, p);
+            p = fma(Q[u][3], y3, p);
+            p += __shfl_xor(p, 16, 64);
+            p += __shfl_xor(p, 32, 64);
+            if (rq == 0) Z[16 * i + col] -= p;
+        }
+        __syncthreads();
+    }
+    for (int i = t; i < n; i += T) d.x[6 * (size_t)d.iperm[i / 6] + i % 6] = Z[i];   // (pose order)
+    MWPROF(4);
+    return true;
+}
+
 // grid (Q) x LDLT_THREADS: either form per problem (k_struct_tiles' choice, read on the device), so the host launches
 // one factorization per trial without reading the choice back; dynamic LDS: the larger of the two forms' needs
+__device__ __forceinline__ bool mw_takes(const Prob& d, const LMHead& hd) {
+    return d.Np > 0 && !hd.tiles_lds && d.nt <= MW_NT_MAX;
+}
+// grid (MW_G x Q rounded up to 8) x MW_T: the column-chain form's workgroups, a problem's MW_G on one XCD (block b on
+// XCD b mod 8), for the dense problems it takes (k_ldlt_any, launched before with mw_on, leaves them alone)
+__global__ __launch_bounds__(MW_T) void k_ldlt_mw(const Prob* __restrict__ probs, int Q) {
+    extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+    __shared__ LdltShared sh;
+    const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8, p = (idx / MW_G) * 8 + xcd;
+    if (p >= Q) return;
+    const Prob& d = probs[p];
+    const LMHead hd = lm_head(d.lm);
+    if (hd.status || hd.done || !mw_takes(d, hd)) return;
+    if (ldlt_mw<MW_T>(d, lds_dyn, sh)) {
+        __syncthreads();
+        pose_epilogue<MW_T>(d, *d.lm, hd.cur, d.x, trial_lambda(hd));
+    }
+}
+
 template <bool use_lds>
-__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restrict__ probs, int reg_nt_max) {
+__global__ __launch_bounds__(LDLT_THREADS) void k_ldlt_any(const Prob* __restrict__ probs, int reg_nt_max, int mw_on) {
     extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
     __shared__ LdltShared sh;
     const Prob& d = probs[blockIdx.x];
     const LMHead hd = lm_head(d.lm);
     if (hd.status || hd.done) return;
     if (d.Np > 0 && !hd.tiles_lds && d.nt <= reg_nt_max) return;   // k_ldlt_reg's
+    if (mw_on && mw_takes(d, hd)) return;                          // k_ldlt_mw's
     LM& lm = *d.lm;
     if (d.Np == 0) {
         if (threadIdx.x == 0) lm.fail = 0;
@@ -3756,6 +4163,7 @@ void carve_scratch(Carver& cv, Prob& d) {
     d.x = cv.take<double>(nx);
     d.bs = cv.take<double>(d.npad);
     d.ws = cv.take<double>(mam::lba::ldlt_ws_doubles(d.npad));
+    d.mw = cv.take<int32_t>(mam::lba::MW_INTS);
     d.depth = cv.take<uint8_t>(d.E);
 }
 
@@ -3948,6 +4356,26 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     const size_t reg_dyn = reg_nt_used ? std::min(c->ldlt_lds_budget, ldlt_reg_lds_bytes(reg_nt_used) +
                                                                           reg_over_lds(reg_nt_used).second)
                                        : 0;
+    // the column-chain form (ldlt_mw) for the problems whose every tile would not fit the LDS tile pool (the device
+    // decides per problem: a sparse pattern still goes to the pool); MAM_LBA_MW=0 leaves them to the HBM form
+    // (batches only: a lone window's chain of column handoffs is slower than one workgroup's HBM form, 2.94 against
+    // 2.77 ms for a c2 ring window; MAM_LBA_MW=2 takes lone problems too)
+    bool mw_on = false;
+    size_t mw_dyn = 0;
+    {
+        const char* mv = std::getenv("MAM_LBA_MW");
+        int cand = 0;
+        if (!(mv && mv[0] == '0') && reg_nt_max == 0)
+            for (auto& d : hp) {
+                const int nt = d.npad / NB;
+                if (d.Np > 0 && nt <= MW_NT_MAX &&
+                    (size_t)nt * (nt + 1) / 2 * 256 * sizeof(double) + (size_t)d.npad * sizeof(double) > c->ldlt_lds_budget) {
+                    cand++;
+                    mw_dyn = std::max(mw_dyn, ldlt_mw_lds_bytes(d.npad));
+                }
+            }
+        mw_on = cand >= ((mv && mv[0] == '2') ? 1 : 2);
+    }
     const dim3 gE((maxE + 255) / 256 > 0 ? (maxE + 255) / 256 : 1, Q);
     const dim3 gE64((maxE + EW - 1) / EW > 0 ? (maxE + EW - 1) / EW : 1, Q);
     {
@@ -4037,6 +4465,8 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         const Prob* Pg = P + q0;
         hipStream_t st = sg[g];
         const dim3 gPtsg(gPts.x, Qg), gTrig(gTri.x, Qg), gBlkg(gBlk.x, Qg);
+        // the column-chain form's workgroups when a problem may be dense past the LDS tile pool (decided on the device)
+        const int mwb = mw_on ? MW_G * ((Qg + 7) / 8 * 8) : 0;
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
@@ -4054,9 +4484,12 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         {
             mam::StageTimer::Scope sc(tm, st, 2);
             if (lds_ok)
-                hipLaunchKernelGGL(k_ldlt_any<true>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg, reg_nt_max);
+                hipLaunchKernelGGL(k_ldlt_any<true>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg, reg_nt_max,
+                                   (int)mw_on);
             else
-                hipLaunchKernelGGL(k_ldlt_any<false>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg, reg_nt_max);
+                hipLaunchKernelGGL(k_ldlt_any<false>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg, reg_nt_max,
+                                   (int)mw_on);
+            if (mw_on) hipLaunchKernelGGL(k_ldlt_mw, dim3(mwb), dim3(MW_T), mw_dyn, st, Pg, Qg);
             if (reg_nt_max)
                 hipLaunchKernelGGL(k_ldlt_reg, dim3(Qg), dim3(REG_T), reg_dyn, st, Pg, reg_nt_max,
                                    reg_dyn);
@@ -4150,6 +4583,18 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
                 h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[6] / w, h[7]);
     }
 #endif
+#ifdef MAM_MW_PROFILE
+    {
+        MAM_HIP(hipStreamSynchronize(s));
+        unsigned long long h[8];
+        MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::lba::g_mwprof), sizeof(h)));
+        fprintf(stderr, "mw cycles (sum over workgroups): wait %.3g steps %.3g panel %.3g publish %.3g backward %.3g; "
+                        "columns %llu k steps %llu; per step: wait %.0f update %.0f; per column: panel %.0f publish %.0f\n",
+                (double)h[0], (double)h[1], (double)h[2], (double)h[3], (double)h[4], h[6], h[7],
+                h[0] / (double)std::max(1ull, h[7]), h[1] / (double)std::max(1ull, h[7]),
+                h[2] / (double)std::max(1ull, h[6]), h[3] / (double)std::max(1ull, h[6]));
+    }
+#endif
 #ifdef MAM_REG_PROFILE
     {
         MAM_HIP(hipStreamSynchronize(s));
@@ -4231,6 +4676,8 @@ int mam_lba_create(int device, mam_lba_ctx** out) {
             hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_any<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess &&
             hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_reg),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&mam::lba::k_ldlt_mw),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) == hipSuccess) {
             c->ldlt_lds_budget = budget;
             break;

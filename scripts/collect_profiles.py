@@ -61,6 +61,8 @@ def main():
     os.makedirs(P, exist_ok=True)
     for c in ("c1", "c2", "c3", "c4"):
         cp(f"bench_{c}.json", os.path.join(P, f"bench_{c}.json"))
+    cp("bench_c2_world.json", os.path.join(P, "bench_c2_world.json"))
+    cp(f"{rnd}pose.json", os.path.join(P, "pose_pmc_c2.json"))
     for n in ("lba_bench", "tri_bench", "pose_c2", "fuse_c2", "bow_c2"):
         cp(f"{n}.json", os.path.join(P, f"{n}.json"))
     cp("pytest_gpu.log", os.path.join(P, "pytest_gpu.log"))

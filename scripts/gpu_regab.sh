@@ -11,6 +11,7 @@ for v in ${VARIANTS:-reg reg_g0 hbm}; do
   case $v in
     reg) E="MAM_LBA_REG=1" ;;
     hbm) E="" ;;
+    rprof) E="MAM_LBA_REG=1 MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_rprof.so" ;;
     *) E="MAM3SLAM_GPU_LIB=$R/variants/libmam_gpu_$v.so" ;;   # a library variant
   esac
   env $E timeout -k 10 180 python3 -u $R/scripts/ring_window_replay.py $R/variants/ring_windows.npz --mode batch --solves 6 > $O/$v.log 2>&1 || { tail -5 $O/$v.log; exit 1; }

@@ -125,7 +125,9 @@ def main():
 #   trial pass (active_chi at the candidate pose): map 33, projection 7, error 2, chi 5, Huber 4, sum 1  -> 52
 FLOP_BUILD_EDGE, FLOP_TRIAL_EDGE = 161, 52
 FP64_VALU_PEAK_TFS = 78.6   # MI355X vector FP64 (MI355X_MICROARCH.md); PoseOptimization is VALU FP64, not MFMA
-PMC_FILE = "profiles/r04/pose_pmc_c2.json"
+# the newest round's counter pass (scripts/gpu_pose_pmc.sh, copied by scripts/collect_profiles.py)
+PMC_FILE = next((f"profiles/{r}/pose_pmc_c2.json" for r in ("r06", "r05", "r04")
+                 if os.path.exists(os.path.join(ROOT, f"profiles/{r}/pose_pmc_c2.json"))), "profiles/r04/pose_pmc_c2.json")
 
 
 def roofline(edges, iterations, trials, frames, ms_launch) -> dict:

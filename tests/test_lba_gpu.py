@@ -165,6 +165,47 @@ def test_lba_batch_same_shape(solver, oracle):
         assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
 
 
+@pytest.mark.parametrize("alone", [False, True])
+def test_lba_dense_column_chain(solver, oracle, alone, monkeypatch):
+    """Dense reduced systems past the LDS tile pool go to the column-chain factorization (ldlt_mw: 8 workgroups per
+    problem claim block columns in order; cross-workgroup flags and panels through agent-coherent loads / stores):
+    nt 14, 19, 22, 24 batched (and alone with MAM_LBA_MW=2), the oracle's control flow and solution; a second batch solve reproduces the
+    first bit for bit (the flags' launch tags advance, nothing is reset)."""
+    import torch
+
+    from mam3slam_amd.lba import DeviceBatch, id_ordered
+
+    sizes = (36, 50, 58, 63) if not alone else (58,)
+    if alone:
+        monkeypatch.setenv("MAM_LBA_MW", "2")   # (batches only by default)
+    probs = [synthetic_problem(n_opt=n, n_fixed=8, n_points=1200, obs_per_point=14, seed=80 + n, init_kf_local=False)
+             for n in sizes]
+    if alone:
+        for p in probs:
+            rg, ro = solver.solve(p), oracle.lba_solve(p)
+            assert rg.status == 0 and ro.status == 0
+            assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials)
+            assert abs(rg.final_chi2 - ro.final_chi2) <= 1e-6 * ro.final_chi2
+            assert _rel(rg.pose_t, ro.pose_t) <= 1e-4 and _rel(rg.pose_q, ro.pose_q) <= 1e-4
+            assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
+        return
+    B = DeviceBatch(probs, torch.device("cuda", 0))
+    stats = solver.solve_batch_device(B)
+    first = []
+    for i, p in enumerate(probs):
+        ro = oracle.lba_solve(id_ordered(p)[0])
+        rg = B.result(i)
+        first.append(rg.point_xyz.copy())
+        assert stats[i]["status"] == 0 and ro.status == 0
+        assert (rg.iterations, rg.lm_trials) == (ro.iterations, ro.lm_trials), i
+        assert abs(rg.final_chi2 - ro.final_chi2) <= 1e-6 * ro.final_chi2
+        assert _rel(rg.pose_t, ro.pose_t) <= 1e-4 and _rel(rg.pose_q, ro.pose_q) <= 1e-4
+        assert _rel(rg.point_xyz, ro.point_xyz) <= 1e-4
+    solver.solve_batch_device(B)
+    for i in range(len(probs)):
+        assert np.array_equal(B.result(i).point_xyz, first[i])
+
+
 def test_lba_dense_register_form(solver, oracle, monkeypatch):
     """Dense reduced systems past the LDS tile pool (every pose pair shares landmarks): the register form of the
     factorization (k_ldlt_reg, MAM_LBA_REG=1) holds 128 tiles in registers, the next ones in LDS and the rest in place in S; nt 15
