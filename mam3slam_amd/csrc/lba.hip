@@ -1032,8 +1032,12 @@ constexpr int SCHUR_PF = MAM_SCHUR_PF;   // pair indices per lane prefetched per
 #define MAM_SCHUR_LANE_MAX 0   // blocks of at most this many landmark pairs: one wave, a lane per entry (0: never;
                                // 192 measured slower: ring batch 472 -> 603 us, world window 0.20 -> 0.32 ms per solve)
 #endif
-constexpr int SCHUR_T = MAM_SCHUR_T, SCHUR_NW = SCHUR_T / 64;
+#ifndef MAM_SCHUR_T_BATCH
+#define MAM_SCHUR_T_BATCH 64   // batches of >= 4 windows: 64 threads, records in halves (156 VGPRs: 3 waves a SIMD);
+#endif                         // ring batch of 32: 14.34 -> 13.43 (64 threads) -> 13.20 ms (+ halves)
+template <int SCHUR_T, bool FULL>
 __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ probs) {
+    constexpr int SCHUR_NW = SCHUR_T / 64;
     // XCD-aware: each XCD takes a contiguous range of (problem, block row) ids, so the W / H_pl records of the
     // landmarks its rows share stay in its L2
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1137,7 +1141,7 @@ __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ 
             const int2 pr = prs[u];
             const double* W = d.bdinv + 18 * (size_t)pr.x;
             const double* B = d.hpl + 18 * (size_t)pr.y;
-#if MAM_SCHUR_FULL
+            if constexpr (FULL) {
             // both records loaded at once (9 16-byte loads each in flight together), then the products
             double wf[18], bf[18];
 #pragma unroll
@@ -1152,7 +1156,7 @@ __global__ __launch_bounds__(SCHUR_T) void k_schur_blk(const Prob* __restrict__ 
                 for (int c = 0; c < 6; c++)
                     acc[6 * r + c] += wf[3 * r] * bf[3 * c] + wf[3 * r + 1] * bf[3 * c + 1] + wf[3 * r + 2] * bf[3 * c + 2];
             continue;
-#endif
+            }
             // rows of W and of H_pl three at a time (9 doubles each): no spill at 152 VGPRs; the same products summed
             // in the same order per accumulator
 #pragma unroll
@@ -3764,7 +3768,7 @@ __device__ unsigned long long g_mwprof[8];
     } while (0)
 #endif
 template <int T>
-__device__ bool ldlt_mw(const Prob& d, double* lds, LdltShared& sh) {
+__device__ bool ldlt_mw(const Prob& d, double* lds, LdltShared& sh, int G) {
 #ifdef MAM_MW_PROFILE
     long long mp0 = clock64();
 #endif
@@ -3797,7 +3801,7 @@ __device__ bool ldlt_mw(const Prob& d, double* lds, LdltShared& sh) {
         __syncthreads();
         const int j = s_col;
         if (j >= nt) {
-            if (t == 0 && j == nt + MW_G - 1) st_ci(&mw[1], base + nt + MW_G);   // every workgroup has read base
+            if (t == 0 && j == nt + G - 1) st_ci(&mw[1], base + nt + G);   // every workgroup has read base
             break;
         }
         // the column's tiles (S as k_schur_blk wrote it: padding identity, the diagonal tile's upper triangle zero)
@@ -4001,17 +4005,17 @@ __device__ bool ldlt_mw(const Prob& d, double* lds, LdltShared& sh) {
 __device__ __forceinline__ bool mw_takes(const Prob& d, const LMHead& hd) {
     return d.Np > 0 && !hd.tiles_lds && d.nt <= MW_NT_MAX;
 }
-// grid (MW_G x Q rounded up to 8) x MW_T: the column-chain form's workgroups, a problem's MW_G on one XCD (block b on
+// grid (G x Q rounded up to 8) x MW_T: the column-chain form's workgroups, a problem's G on one XCD (block b on
 // XCD b mod 8), for the dense problems it takes (k_ldlt_any, launched before with mw_on, leaves them alone)
-__global__ __launch_bounds__(MW_T) void k_ldlt_mw(const Prob* __restrict__ probs, int Q) {
+__global__ __launch_bounds__(MW_T) void k_ldlt_mw(const Prob* __restrict__ probs, int Q, int G) {
     extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
     __shared__ LdltShared sh;
-    const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8, p = (idx / MW_G) * 8 + xcd;
+    const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8, p = (idx / G) * 8 + xcd;
     if (p >= Q) return;
     const Prob& d = probs[p];
     const LMHead hd = lm_head(d.lm);
     if (hd.status || hd.done || !mw_takes(d, hd)) return;
-    if (ldlt_mw<MW_T>(d, lds_dyn, sh)) {
+    if (ldlt_mw<MW_T>(d, lds_dyn, sh, G)) {
         __syncthreads();
         pose_epilogue<MW_T>(d, *d.lm, hd.cur, d.x, trial_lambda(hd));
     }
@@ -4466,7 +4470,10 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         hipStream_t st = sg[g];
         const dim3 gPtsg(gPts.x, Qg), gTrig(gTri.x, Qg), gBlkg(gBlk.x, Qg);
         // the column-chain form's workgroups when a problem may be dense past the LDS tile pool (decided on the device)
-        const int mwb = mw_on ? MW_G * ((Qg + 7) / 8 * 8) : 0;
+        // (a lone problem: a workgroup per column, every column's chain at once)
+        int mwg = MW_G;
+        if (Qg == 1) mwg = std::max(MW_G, std::min(hp[q0].npad / NB, MW_NT_MAX));
+        const int mwb = mw_on ? mwg * ((Qg + 7) / 8 * 8) : 0;
         mam::StageTimer* tm = g == 0 ? &c->timer : nullptr;   // stage times: the first half's kernels
         {
             mam::StageTimer::Scope sc(tm, st, 0);
@@ -4479,7 +4486,12 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         }
         {
             mam::StageTimer::Scope sc(tm, st, 1);
-            hipLaunchKernelGGL(k_schur_blk, gBlkg, dim3(SCHUR_T), 0, st, Pg);
+            if (Qg >= 4)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_schur_blk<MAM_SCHUR_T_BATCH, false>), gBlkg, dim3(MAM_SCHUR_T_BATCH), 0,
+                                   st, Pg);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_schur_blk<MAM_SCHUR_T, (bool)MAM_SCHUR_FULL>), gBlkg, dim3(MAM_SCHUR_T), 0,
+                                   st, Pg);
         }
         {
             mam::StageTimer::Scope sc(tm, st, 2);
@@ -4489,7 +4501,7 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
             else
                 hipLaunchKernelGGL(k_ldlt_any<false>, dim3(Qg), dim3(LDLT_THREADS), ldlt_dyn, st, Pg, reg_nt_max,
                                    (int)mw_on);
-            if (mw_on) hipLaunchKernelGGL(k_ldlt_mw, dim3(mwb), dim3(MW_T), mw_dyn, st, Pg, Qg);
+            if (mw_on) hipLaunchKernelGGL(k_ldlt_mw, dim3(mwb), dim3(MW_T), mw_dyn, st, Pg, Qg, mwg);
             if (reg_nt_max)
                 hipLaunchKernelGGL(k_ldlt_reg, dim3(Qg), dim3(REG_T), reg_dyn, st, Pg, reg_nt_max,
                                    reg_dyn);
