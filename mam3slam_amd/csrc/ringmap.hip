@@ -546,6 +546,28 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int& total) {
     return pre + x - v;
 }
 
+// f(s, k) for every observation (slot s, keypoint k >= 0) of a MapPoint row, in slot order: 16-byte loads of eight
+// slots when the row is 16-byte aligned (R a multiple of 8: c2's R = 96), else one slot a load
+template <class F>
+__device__ __forceinline__ void for_obs(const int16_t* r, int R, F f) {
+    if ((R & 7) == 0) {
+        const uint4* r4 = reinterpret_cast<const uint4*>(r);
+        for (int q = 0; q < R / 8; q++) {
+            const uint4 v = r4[q];
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const int k0 = (int16_t)(wv[h] & 0xffffu), k1 = (int16_t)(wv[h] >> 16);
+                if (k0 >= 0) f(8 * q + 2 * h, k0);
+                if (k1 >= 0) f(8 * q + 2 * h + 1, k1);
+            }
+        }
+    } else {
+        for (int s = 0; s < R; s++)
+            if (r[s] >= 0) f(s, (int)r[s]);
+    }
+}
+
 struct WinArgs {
     int head, covis_th, pcap, ecap;
     const mam_ringmap_window* outs;
@@ -571,9 +593,9 @@ __global__ __launch_bounds__(WIN_T) void k_windows(const mam_ringmap M, const Wi
     for (int kp = t; kp < S; kp += WIN_T) {
         const int m = M.mp_of[j * S + kp];
         if (m < 0) continue;
-        const int16_t* r = okp_row(M, m);
-        for (int s = 0; s < R; s++)
-            if (s != j && r[s] >= 0) atomicAdd(wt + s, 1);
+        for_obs(okp_row(M, m), R, [&](int s, int) {
+            if (s != j) atomicAdd(wt + s, 1);
+        });
     }
     __syncthreads();
     if (t == 0) {   // GetVectorCovisibleKeyFrames: weight >= th, descending (ties: slot); none: the heaviest
@@ -603,38 +625,39 @@ __global__ __launch_bounds__(WIN_T) void k_windows(const mam_ringmap M, const Wi
     __syncthreads();
     const int nloc = hdr[0];
     // local MapPoints: every MapPoint of every local keyframe, in keyframe order then keypoint order, once
-    for (int li = 0; li < nloc; li++) {
-        const int s = order[li];
-        for (int k0 = 0; k0 < S; k0 += WIN_T) {
-            const int kp = k0 + t;
-            int m = -1;
-            if (kp < S) m = M.mp_of[s * S + kp];
-            bool nw = false;
-            if (m >= 0) {
-                const uint32_t bit = 1u << (m & 31);
-                nw = !(atomicOr(taken + (m >> 5), bit) & bit);
-            }
-            int tot;
-            const int pos = block_excl_scan(nw ? 1 : 0, wsum, tot) + hdr[1];
-            if (nw && pos < a.pcap) {
-                a.point_id[(size_t)w * a.pcap + pos] = m;
-                const mam_fuse_mp& rc = M.rec[m];
-                for (int c = 0; c < 3; c++) o.point_xyz[3 * (size_t)pos + c] = (double)rc.pos[c];
-            }
-            __syncthreads();
-            if (t == 0) hdr[1] += tot;
-            __syncthreads();
+    // (one keyframe chunk of WIN_T keypoints a pass; the next chunk's ids loaded before this one's scan)
+    const int nch = (S + WIN_T - 1) / WIN_T;
+    auto chunk_id = [&](int c) -> int {
+        const int kp = (c % nch) * WIN_T + t;
+        return (c < nloc * nch && kp < S) ? M.mp_of[order[c / nch] * S + kp] : -1;
+    };
+    int m_next = chunk_id(0), base = 0;   // (base: every thread's copy of the running count)
+    for (int c = 0; c < nloc * nch; c++) {
+        const int m = m_next;
+        m_next = chunk_id(c + 1);
+        bool nw = false;
+        if (m >= 0) {
+            const uint32_t bit = 1u << (m & 31);
+            nw = !(atomicOr(taken + (m >> 5), bit) & bit);
+        }
+        int tot;
+        const int pos = block_excl_scan(nw ? 1 : 0, wsum, tot) + base;   // (its barriers order the chunks' atomics)
+        base += tot;
+        if (nw && pos < a.pcap) {
+            a.point_id[(size_t)w * a.pcap + pos] = m;
+            const mam_fuse_mp& rc = M.rec[m];
+            for (int cc = 0; cc < 3; cc++) o.point_xyz[3 * (size_t)pos + cc] = (double)rc.pos[cc];
         }
     }
-    const int np_all = hdr[1];
+    const int np_all = base;
     const int npts = min(np_all, a.pcap);
     __threadfence_block();
     __syncthreads();
     // fixed keyframes: the other observers of local MapPoints, by first encounter (MapPoint order, then slot order)
     for (int p = t; p < npts; p += WIN_T) {
-        const int16_t* r = okp_row(M, a.point_id[(size_t)w * a.pcap + p]);
-        for (int s = 0; s < R; s++)
-            if (r[s] >= 0 && posei[s] < 0) atomicMin(first + s, p);
+        for_obs(okp_row(M, a.point_id[(size_t)w * a.pcap + p]), R, [&](int s, int) {
+            if (posei[s] < 0) atomicMin(first + s, p);
+        });
     }
     __syncthreads();
     if (t == 0) {
@@ -671,20 +694,20 @@ __global__ __launch_bounds__(WIN_T) void k_windows(const mam_ringmap M, const Wi
         a.pose_slot[(size_t)w * R + i] = s;
     }
     // edges: per MapPoint in order, its observations in slot order
+    int ebase = 0;   // (every thread's copy of the running edge count)
     for (int p0 = 0; p0 < npts; p0 += WIN_T) {
         const int p = p0 + t;
         int ne = 0;
         const int16_t* r = nullptr;
         if (p < npts) {
             r = okp_row(M, a.point_id[(size_t)w * a.pcap + p]);
-            for (int s = 0; s < R; s++) ne += r[s] >= 0;
+            for_obs(r, R, [&](int, int) { ne++; });
         }
         int tot;
-        int e = block_excl_scan(ne, wsum, tot) + hdr[4];
+        int e = block_excl_scan(ne, wsum, tot) + ebase;
+        ebase += tot;
         if (p < npts && e + ne <= a.ecap) {
-            for (int s = 0; s < R; s++) {
-                const int k = r[s];
-                if (k < 0) continue;
+            for_obs(r, R, [&](int s, int k) {
                 const mam_keypoint& kp = M.keys[(size_t)s * S + k];
                 o.edge_point[e] = p;
                 o.edge_pose[e] = posei[s];
@@ -692,17 +715,14 @@ __global__ __launch_bounds__(WIN_T) void k_windows(const mam_ringmap M, const Wi
                 o.edge_obs[2 * (size_t)e + 1] = (double)kp.y;
                 o.edge_inv_sigma2[e] = (double)M.inv_level_sigma2[min(max(kp.octave, 0), M.nlevels - 1)];
                 e++;
-            }
+            });
         }
-        __syncthreads();
-        if (t == 0) hdr[4] += tot;
-        __syncthreads();
     }
     if (t == 0) {
-        const bool over = hdr[4] > a.ecap;
+        const bool over = ebase > a.ecap;
         a.counts[4 * w] = over ? -1 : np;
         a.counts[4 * w + 1] = over ? -1 : npts;
-        a.counts[4 * w + 2] = over ? -1 : hdr[4];
+        a.counts[4 * w + 2] = over ? -1 : ebase;
         a.counts[4 * w + 3] = over ? -1 : nloc;
     }
 }
