@@ -1401,19 +1401,28 @@ def main():
                 except Exception:
                     mfma = None
             out["roofline_lba"] = {
-                "bound": "mfma", "kernel": "k_ldlt_any", "unit": "TFLOP/s", "achieved": ach,
+                "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
+                "kernel": ("k_ldlt_any + k_ldlt_mw" if args.lm_windows == "ring" else "k_ldlt_any"),
                 "peak": FP64_PEAK_TFS, "frac": ach / FP64_PEAK_TFS if ach else None,
-                "frac_of_cus_used": ach / (FP64_PEAK_TFS * len(g0) / 256.0) if ach else None,
+                "frac_of_cus_used": (ach / (FP64_PEAK_TFS * min(256, len(g0) * (8 if args.lm_windows == "ring" else 1)) / 256.0)
+                                     if ach else None),
                 "flop_per_factorization": float(np.mean(fl_ldlt)), "windows_per_launch": len(g0),
                 "avg_launch_ms": ms_solve / max(n_solve, 1), "launches": n_solve,
                 "mfma_counters": mfma, "mfma_counters_file": mrel if mfma else None,
-                "limiter": ("latency: one workgroup per window factors the tile pattern as a dataflow of per-tile and "
+                "limiter": ("latency: the device map's windows are dense (every optimised pose pair shares a MapPoint), so "
+                            "the solve stage is k_ldlt_mw's column chain — 8 workgroups a window, a panel workgroup "
+                            "factoring every 16-wide block column in turn (~10 us a column: the ready column's "
+                            "agent-coherent load, the last update, the diagonal tile's 16 pivot steps, the panel rows, "
+                            "the publish) while the others stream the earlier updates (DESIGN §3)"
+                            if args.lm_windows == "ring" else
+                            "latency: one workgroup per window factors the tile pattern as a dataflow of per-tile and "
                             "per-panel tasks (two chains of 6-9 block columns + the separator's 3-4 under the split "
                             "pose order); per column ~6.4k cycles: the critical tile update (4 FP64 MFMAs + operand "
                             "loads) ~1.5k, the tall panel's 16 dependent pivot steps ~2.3k, stores + flag ~1.2k "
                             "(scripts/gpu_ldlt_trace.sh)"),
                 "note": "algorithmic = tile-skipping LDL^T + solves (ldlt_tile_flops); frac_of_cus_used prices "
-                        "against the FP64 MFMA peak of the CUs the launch's workgroups occupy (one per window)"}
+                        "against the FP64 MFMA peak of the CUs the launch's workgroups occupy (one per window; eight "
+                        "per dense window of the ring leg)"}
             # the Schur stage (k_schur_blk: FP64 VALU products of each landmark's pose pairs), the same windows
             fl_schur = [schur_flops(p) for p in g0]
             ms_schur, n_schur = lba_stage["schur"]

@@ -4014,6 +4014,9 @@ __device__ bool ldlt_mw(const Prob& d, double* lds, LdltShared& sh, int G) {
 // itself (compare-and-swap on the counter), so one resident workgroup alone still runs every column: no co-residency
 // needed. Per column on the critical path: the ready column's load, one update, the diagonal tile, the panel rows,
 // the publish — ~half the chain form's handoff.
+#ifndef MAM_MW_DEFER
+#define MAM_MW_DEFER 0   // the panel flag raised after the next column's load and update (its stores drain meanwhile)
+#endif
 template <int T>
 __device__ bool ldlt_mw_la(const Prob& d, double* lds, LdltShared& sh, int G) {
     constexpr int NW = T / 64, RT = (MW_NT_MAX + NW - 1) / NW;
@@ -4105,7 +4108,7 @@ __device__ bool ldlt_mw_la(const Prob& d, double* lds, LdltShared& sh, int G) {
     };
     // one loop for both roles (a single site of the chain's updates keeps the register allocation in bounds)
     bool panel = false;
-    int jp = 0, mprev = 0;
+    int jp = 0, mprev = 0, pending = -1;   // (pending: a published panel whose flag waits for its stores, MAM_MW_DEFER)
     for (;;) {
         int j;
         bool own = true;
@@ -4189,7 +4192,15 @@ __device__ bool ldlt_mw_la(const Prob& d, double* lds, LdltShared& sh, int G) {
                     YJ[t] = v;
                 }
             }
+#if MAM_MW_DEFER
+            // the previous panel's flag, its stores drained under this column's load and update
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             __syncthreads();   // (the previous panel read before this one is staged over it)
+#if MAM_MW_DEFER
+            if (t == 0 && pending >= 0) st_ci(&mw[8 + pending], tag);
+            pending = -1;
+#endif
         }
         // the panel of column j: stage, the diagonal tile on wave 0, the rows, publish
         const int m = 16 * (nt - j - 1);
@@ -4251,11 +4262,20 @@ __device__ bool ldlt_mw_la(const Prob& d, double* lds, LdltShared& sh, int G) {
             st_c(&Dg[16 * j + t], DP[t]);
             st_c(&Yg[16 * j + t], YP[t]);
         }
+#if MAM_MW_DEFER
+        pending = j;
+#else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0) st_ci(&mw[8 + j], tag);
+#endif
         mprev = m;
         if (++jp == nt) break;
+    }
+    if (pending >= 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) st_ci(&mw[8 + pending], tag);
     }
     if (t == 0 && G == 1) st_ci(&mw[1], base + nt);   // (no helper made the last claim)
     // the backward substitution (every panel is this workgroup's own)
