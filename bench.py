@@ -1277,15 +1277,18 @@ def main():
                          f"ComputeDistinctiveDescriptors) and ")
             if args.lm_windows == "ring":
                 sz = mapping.rl.sizes[mapping.rl.valid]
+                # (a short run's windows may all lack a fixed keyframe: the reference skips those LBAs)
+                shape = (f"~{float(np.mean(sz[:, 3])):.1f} optimised KF; every MapPoint of every local keyframe, "
+                         f"~{int(np.mean(sz[:, 1]))}; fixed = their other observers, "
+                         f"{float(np.mean(sz[:, 0] - sz[:, 3])):.1f} KF; ~{int(np.mean(sz[:, 2]))} observations"
+                         if len(sz) else "no window of the last run had a fixed keyframe")
                 workload += (f"MapPoint creation, Fuse's Replace / AddObservation and the MapPoints' descriptor / "
                              f"normal / depth update on the device map the ring's keyframes share, and a "
                              f"LocalBundleAdjustment window of the keyframe by the reference's window rule over that "
-                             f"map (local = the keyframe + its covisible keyframes, ~{float(np.mean(sz[:, 3])):.1f} "
-                             f"optimised KF; every MapPoint of every local keyframe, ~{int(np.mean(sz[:, 1]))}; "
-                             f"fixed = their other observers, {float(np.mean(sz[:, 0] - sz[:, 3])):.1f} KF; "
-                             f"~{int(np.mean(sz[:, 2]))} observations), batched, its write-back (outlier erase, poses, "
-                             f"positions, normals / depth ranges) applied to the map, concurrent with tracking; "
-                             f"write-backs exchanged (all-gather) and applied to the replica every GPU holds")
+                             f"map (local = the keyframe + its covisible keyframes, {shape}), batched, its write-back "
+                             f"(outlier erase, poses, positions, normals / depth ranges) applied to the map, "
+                             f"concurrent with tracking; write-backs exchanged (all-gather) and applied to the "
+                             f"replica every GPU holds")
             else:
                 workload += (f"a LocalBundleAdjustment window (50 KF + fixed, "
                              f"~{int(np.mean([len(p.point_id) for p in mapping.probs]))} MapPoints) of the synthetic "

@@ -4015,7 +4015,7 @@ __device__ bool ldlt_mw(const Prob& d, double* lds, LdltShared& sh, int G) {
 // needed. Per column on the critical path: the ready column's load, one update, the diagonal tile, the panel rows,
 // the publish — ~half the chain form's handoff.
 #ifndef MAM_MW_DEFER
-#define MAM_MW_DEFER 0   // the panel flag raised after the next column's load and update (its stores drain meanwhile)
+#define MAM_MW_DEFER 1   // the panel flag raised after the next column's load and update (its stores drain meanwhile)
 #endif
 template <int T>
 __device__ bool ldlt_mw_la(const Prob& d, double* lds, LdltShared& sh, int G) {
@@ -4125,7 +4125,9 @@ __device__ bool ldlt_mw_la(const Prob& d, double* lds, LdltShared& sh, int G) {
         } else {
             j = jp;
             __syncthreads();
-            if (t == 0) s_col = atomicCAS(&mw[0], base + j, base + j + 1) == base + j ? 1 : 0;
+            // a ready column is a helper's (one load); else take it if nobody has claimed it
+            if (t == 0)
+                s_col = ld_ci(&mw[48 + j]) == tag ? 0 : (atomicCAS(&mw[0], base + j, base + j + 1) == base + j ? 1 : 0);
             __syncthreads();
             own = s_col != 0;
         }
