@@ -4620,7 +4620,9 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
     // front (no read-back of the counts before the fill); above it (map-scale graphs, where E Np overestimates the
     // sum over landmarks of their observers squared by orders of magnitude) the exact counts are read back after
     // k_blk_scan and the buffer sized by them
-    constexpr size_t kPairBoundBytes = (size_t)256 << 20;
+    // (2 GiB of 288: a batch of 32 dense c2 windows bounds at ~490 MB and takes the up-front form; at 256 MB it took
+    // the read-back form: 2 Q 4-byte copies and two host synchronisations a solve on LocalMapping's stream)
+    constexpr size_t kPairBoundBytes = (size_t)2 << 30;
     std::vector<size_t> pair_cap(Q);
     size_t npairs = 0;
     for (int q = 0; q < Q; q++) {

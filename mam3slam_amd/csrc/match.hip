@@ -1036,23 +1036,32 @@ struct TriBatchArgs {
     unsigned long long* skey;   // [nkf][skey_stride] (nid << 32 | idx) ascending, ~0 past the FeatureVector
     int skey_stride;            // power of two >= kp_stride
     int32_t* nfv;               // [nkf] features in the FeatureVector
+    unsigned long long* raw;    // [nkf][skey_stride] the unsorted keys skey was sorted from (the previous call's)
+    int32_t* raw_ok;            // [nkf] raw / skey / nfv of the slot hold a sort of this stride's keys
     cam::PairGeom* pg;          // [npairs]
     int32_t* out;               // [npairs][kp_stride]
     int32_t* out_n;             // [npairs]
 };
 
 // grid (nkf) x 1024: every keyframe's FeatureVector as one sorted key array (node id, then feature index: the order
-// the reference walks a FeatureVector, std::map by node + insertion order), bitonic sort in LDS
+// the reference walks a FeatureVector, std::map by node + insertion order), bitonic sort in LDS. A keyframe slot whose
+// keys equal, element for element, the keys of the slot's previous sort keeps that sort (a ring's older keyframes:
+// only the run's new keyframes change between LocalMapping runs).
 __global__ __launch_bounds__(1024) void k_tri_fv_sort(TriBatchArgs a) {
     extern __shared__ unsigned long long sk[];
     const int k = blockIdx.x, P = a.skey_stride;
     const int n = frame_n(a.kfs, k);
     const size_t base = (size_t)k * a.kfs.kp_stride;
+    const bool had = a.raw_ok[k] != 0;
+    int diff = had ? 0 : 1;
     for (int i = threadIdx.x; i < P; i += 1024) {
         unsigned long long v = ~0ull;
         if (i < n && a.weight[base + i] > 0.0) v = ((unsigned long long)a.nid[base + i] << 32) | (unsigned)i;
         sk[i] = v;
+        if (had && a.raw[(size_t)k * P + i] != v) diff = 1;
     }
+    if (!__syncthreads_or(diff)) return;   // the same keys: skey / nfv of the slot stand
+    for (int i = threadIdx.x; i < P; i += 1024) a.raw[(size_t)k * P + i] = sk[i];
     __syncthreads();
     for (int size = 2; size <= P; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -1079,6 +1088,7 @@ __global__ __launch_bounds__(1024) void k_tri_fv_sort(TriBatchArgs a) {
         int t = 0;
         for (int w = 0; w < 16; w++) t += red[w];
         a.nfv[k] = t;
+        a.raw_ok[k] = 1;
     }
 }
 
@@ -1626,8 +1636,9 @@ struct mam_match_ctx {
     // host-API staging
     DevBuf<uint8_t> stage;
     // batched triangulation scratch
-    DevBuf<unsigned long long> tri_skey;
-    DevBuf<int32_t> tri_nfv;
+    DevBuf<unsigned long long> tri_skey, tri_raw;
+    DevBuf<int32_t> tri_nfv, tri_ok;
+    int tri_P = 0, tri_nkf = 0;   // the stride / slot count tri_raw holds sorts of (else tri_ok is cleared)
     DevBuf<mam::cam::PairGeom> tri_pg;
 };
 
@@ -2165,8 +2176,14 @@ int mam_search_for_triangulation_batch_device(mam_match_ctx* c, const mam_frame_
     const int nkf = b->kfs.nframes, S = b->kfs.kp_stride;
     int P = 1;
     while (P < S) P <<= 1;
+    const bool keep = c->tri_raw.p && c->tri_P == P && c->tri_nkf == nkf && c->tri_skey.n >= (size_t)nkf * P;
     if (int rc = c->tri_skey.alloc((size_t)nkf * P)) return rc;
+    if (int rc = c->tri_raw.alloc((size_t)nkf * P)) return rc;
     if (int rc = c->tri_nfv.alloc(nkf)) return rc;
+    if (int rc = c->tri_ok.alloc(nkf)) return rc;
+    if (!keep) MAM_HIP(hipMemsetAsync(c->tri_ok.p, 0, sizeof(int32_t) * nkf, s));
+    c->tri_P = P;
+    c->tri_nkf = nkf;
     if (int rc = c->tri_pg.alloc(b->npairs)) return rc;
     mam::TriBatchArgs a{};
     a.g = *g;
@@ -2183,6 +2200,8 @@ int mam_search_for_triangulation_batch_device(mam_match_ctx* c, const mam_frame_
     a.skey = c->tri_skey.p;
     a.skey_stride = P;
     a.nfv = c->tri_nfv.p;
+    a.raw = c->tri_raw.p;
+    a.raw_ok = c->tri_ok.p;
     a.pg = c->tri_pg.p;
     a.out = out_match12;
     a.out_n = out_nmatches;
