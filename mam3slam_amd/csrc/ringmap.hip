@@ -409,14 +409,35 @@ __device__ __forceinline__ int desc_dist32(const uint8_t* a, const uint8_t* b) {
 
 // UpdateNormalAndDepth (MapPoint.cc:426-494) of MapPoint id: observations in slot order, the reference keyframe =
 // the home slot
+// f(s, k) for every observation (slot s, keypoint k >= 0) of a MapPoint row, in slot order: 16-byte loads of eight
+// slots when the row is 16-byte aligned (R a multiple of 8: c2's R = 96), else one slot a load
+template <class F>
+__device__ __forceinline__ void for_obs(const int16_t* r, int R, F f) {
+    if ((R & 7) == 0) {
+        const uint4* r4 = reinterpret_cast<const uint4*>(r);
+        for (int q = 0; q < R / 8; q++) {
+            const uint4 v = r4[q];
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const int k0 = (int16_t)(wv[h] & 0xffffu), k1 = (int16_t)(wv[h] >> 16);
+                if (k0 >= 0) f(8 * q + 2 * h, k0);
+                if (k1 >= 0) f(8 * q + 2 * h + 1, k1);
+            }
+        }
+    } else {
+        for (int s = 0; s < R; s++)
+            if (r[s] >= 0) f(s, (int)r[s]);
+    }
+}
+
 __device__ void normal_depth(const mam_ringmap& M, int id) {
     mam_fuse_mp& rec = M.rec[id];
     const int16_t* r = okp_row(M, id);
     const float P0 = rec.pos[0], P1 = rec.pos[1], P2 = rec.pos[2];
     float n0 = 0.0f, n1 = 0.0f, n2 = 0.0f;
     int n = 0;
-    for (int s = 0; s < M.R; s++) {
-        if (r[s] < 0) continue;
+    for_obs(r, M.R, [&](int s, int) {
         float ow[3];
         camera_center(M.tcw + 7 * (size_t)s, ow);
         const float a0 = P0 - ow[0], a1 = P1 - ow[1], a2 = P2 - ow[2];
@@ -425,7 +446,7 @@ __device__ void normal_depth(const mam_ringmap& M, int id) {
         n1 = n1 + a1 / nr;
         n2 = n2 + a2 / nr;
         n++;
-    }
+    });
     if (n == 0) return;
     const int hs = id / M.S, hk = id % M.S;
     float ow[3];
@@ -457,13 +478,14 @@ __global__ __launch_bounds__(RF_T) void k_refresh(const mam_ringmap M, uint8_t b
     for (int base = (blockIdx.x * (RF_T / 64) + wv) * 64; base < n_ids; base += nwaves * 64) {
         const int myid = base + lane;
         const bool want = myid < n_ids && (M.flag[myid] & bit) && M.rec[myid].valid;
+        // UpdateNormalAndDepth: every lane its own MapPoint (a record's normal / depth fields, nothing another reads)
+        if (want) normal_depth(M, myid);
+        if (!DESC) continue;
         uint64_t todo = __ballot(want);
         while (todo) {
             const int l = __ffsll((unsigned long long)todo) - 1;
             todo &= todo - 1;
             const int id = base + l;
-            if (lane == 0) normal_depth(M, id);
-            if (!DESC) continue;
             const int16_t* r = okp_row(M, id);
             // the observations in slot order: lane l holds slots l and l + 64
             const int k0 = lane < M.R ? r[lane] : -1, k1 = lane + 64 < M.R ? r[lane + 64] : -1;
@@ -544,28 +566,6 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int& total) {
     }
     __syncthreads();
     return pre + x - v;
-}
-
-// f(s, k) for every observation (slot s, keypoint k >= 0) of a MapPoint row, in slot order: 16-byte loads of eight
-// slots when the row is 16-byte aligned (R a multiple of 8: c2's R = 96), else one slot a load
-template <class F>
-__device__ __forceinline__ void for_obs(const int16_t* r, int R, F f) {
-    if ((R & 7) == 0) {
-        const uint4* r4 = reinterpret_cast<const uint4*>(r);
-        for (int q = 0; q < R / 8; q++) {
-            const uint4 v = r4[q];
-            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int h = 0; h < 4; h++) {
-                const int k0 = (int16_t)(wv[h] & 0xffffu), k1 = (int16_t)(wv[h] >> 16);
-                if (k0 >= 0) f(8 * q + 2 * h, k0);
-                if (k1 >= 0) f(8 * q + 2 * h + 1, k1);
-            }
-        }
-    } else {
-        for (int s = 0; s < R; s++)
-            if (r[s] >= 0) f(s, (int)r[s]);
-    }
 }
 
 struct WinArgs {
