@@ -532,17 +532,11 @@ __device__ __forceinline__ void point_list_regs(const Prob& d, int h, int32_t* s
             d.slot_hp[d.pe_off[h] + a] = hv[a];
             d.emeta[v[a]] = make_int4(h, hv[a], a == 0 ? 1 : 0, 0);
         }
-    if (rows) {
+    if (rows) {   // (bits mode: the point's pose mask; the workgroup folds the masks into the pair rows)
         unsigned long long m = 0;
 #pragma unroll
         for (int a = 0; a < NR; a++) m |= hv[a] >= 0 ? 1ull << hv[a] : 0ull;
-        // row ha gets the poses above it (the upper triangle, as the byte mask holds it)
-#pragma unroll
-        for (int a = 0; a < NR; a++)
-            if (hv[a] >= 0) {
-                const unsigned long long up = m & ~((2ull << hv[a]) - 1ull);
-                if (up) atomicOr(&rows[hv[a]], up);
-            }
+        *rows = m;
         return;
     }
 #pragma unroll
@@ -560,16 +554,36 @@ __device__ __forceinline__ void point_list_regs(const Prob& d, int h, int32_t* s
 // longer segments, global BA, by odd-even transposition in place). Windows of <= 64
 // optimised poses collect the pair mask as LDS bit rows per workgroup (one device atomic per row present instead of a
 // byte store per observation pair: ~2.7M stores per batch of 32 ring windows), k_struct_tiles expands them.
+#ifdef MAM_SORT_PROFILE
+// cycles (thread 0, whole workgroup) of k_struct_sort's point workgroups [0] / pose workgroups [1], their counts [2] [3]
+__device__ unsigned long long g_sortprof[4];
+struct SortProf {
+    long long t0 = clock64();
+    int part;
+    __device__ explicit SortProf(int p) : part(p) {}
+    __device__ ~SortProf() {
+        if (threadIdx.x == 0) {
+            atomicAdd(&g_sortprof[part], (unsigned long long)(clock64() - t0));
+            atomicAdd(&g_sortprof[2 + part], 1ull);
+        }
+    }
+};
+#endif
 __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ probs) {
     const Prob& d = probs[blockIdx.y];
     if (d.lm->status) return;
     const int nb_pts = (d.L + 255) / 256;
+#ifdef MAM_SORT_PROFILE
+    SortProf sp((int)blockIdx.x < nb_pts ? 0 : 1);
+#endif
     if ((int)blockIdx.x < nb_pts) {
-        __shared__ unsigned long long rows_s[64];
+        // bits mode (Np <= 64): each thread leaves its point's pose mask in pm_s; row r of the pair mask is then the
+        // OR over the masks holding r of their poses above r — one thread a row over the 256 masks (LDS broadcast
+        // reads) instead of an LDS atomic per (point, pose): ~1.8k atomics on ~50 addresses a workgroup, ~100 us
+        __shared__ unsigned long long pm_s[256];
         const bool bits = d.Np <= 64;   // uniform
-        if (bits && threadIdx.x < 64) rows_s[threadIdx.x] = 0ull;
-        __syncthreads();
-        unsigned long long* rows = bits ? rows_s : nullptr;
+        pm_s[threadIdx.x] = 0ull;
+        unsigned long long* rows = bits ? pm_s + threadIdx.x : nullptr;
         const int h = blockIdx.x * 256 + threadIdx.x;
         if (h < d.L) {
             int32_t* s = d.pe_idx + d.pe_off[h];
@@ -579,27 +593,44 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
             } else if (n <= 32) {
                 point_list_regs<32>(d, h, s, n, rows);
             } else {
-                for (int k = 1; k < n; k++) {
-                    const int v = s[k];
-                    int m = k - 1;
-                    while (m >= 0 && s[m] > v) { s[m + 1] = s[m]; m--; }
-                    s[m + 1] = v;
+                // a long list (a ring window's MapPoints reach ~56 observations): 16 loads in flight a round (one
+                // element a round trip took ~190 us for the window's longest lists); usually already in edge order,
+                // sorted in place otherwise
+                constexpr int CK = 16;
+                bool sorted = true;
+                for (int a0 = 0; a0 + 1 < n; a0 += CK) {
+                    int w[CK + 1];
+#pragma unroll
+                    for (int u = 0; u <= CK; u++) w[u] = a0 + u < n ? s[a0 + u] : INT_MAX;
+#pragma unroll
+                    for (int u = 0; u < CK; u++) sorted = sorted && (a0 + u + 1 >= n || w[u] < w[u + 1]);
                 }
+                if (!sorted)
+                    for (int k = 1; k < n; k++) {
+                        const int v = s[k];
+                        int m = k - 1;
+                        while (m >= 0 && s[m] > v) { s[m + 1] = s[m]; m--; }
+                        s[m + 1] = v;
+                    }
                 unsigned long long msk = 0;
-                for (int a = 0; a < n; a++) {
-                    const int e = s[a];
-                    const int hp = d.pose_h[d.edge_pose[e]];
-                    d.slot_hp[d.pe_off[h] + a] = hp;
-                    d.emeta[e] = make_int4(h, hp, a == 0 ? 1 : 0, 0);
-                    if (bits && hp >= 0) msk |= 1ull << hp;
+                for (int a0 = 0; a0 < n; a0 += CK) {   // (the edges' pose blocks and metadata)
+                    int ev[CK], pv[CK], hv2[CK];
+#pragma unroll
+                    for (int u = 0; u < CK; u++) ev[u] = a0 + u < n ? s[a0 + u] : 0;
+#pragma unroll
+                    for (int u = 0; u < CK; u++) pv[u] = a0 + u < n ? d.edge_pose[ev[u]] : 0;
+#pragma unroll
+                    for (int u = 0; u < CK; u++) hv2[u] = a0 + u < n ? d.pose_h[pv[u]] : -1;
+#pragma unroll
+                    for (int u = 0; u < CK; u++) {
+                        if (a0 + u >= n) continue;
+                        d.slot_hp[d.pe_off[h] + a0 + u] = hv2[u];
+                        d.emeta[ev[u]] = make_int4(h, hv2[u], a0 + u == 0 ? 1 : 0, 0);
+                        if (bits && hv2[u] >= 0) msk |= 1ull << hv2[u];
+                    }
                 }
                 if (bits) {
-                    for (int a = 0; a < n; a++) {
-                        const int ha = d.slot_hp[d.pe_off[h] + a];
-                        if (ha < 0) continue;
-                        const unsigned long long up = msk & ~((2ull << ha) - 1ull);
-                        if (up) atomicOr(&rows_s[ha], up);
-                    }
+                    *rows = msk;
                 } else {
                     for (int a = 0; a < n; a++) {
                         const int ha = d.pose_h[d.edge_pose[s[a]]];
@@ -614,7 +645,16 @@ __global__ __launch_bounds__(256) void k_struct_sort(const Prob* __restrict__ pr
         }
         if (bits) {   // uniform
             __syncthreads();
-            if (threadIdx.x < d.Np && rows_s[threadIdx.x]) atomicOr(&d.pm_rows[threadIdx.x], rows_s[threadIdx.x]);
+            const int r = threadIdx.x;
+            if (r < d.Np) {
+                const unsigned long long above = ~((2ull << r) - 1ull);
+                unsigned long long acc = 0ull;
+                for (int i = 0; i < 256; i++) {
+                    const unsigned long long m = pm_s[i];
+                    if ((m >> r) & 1ull) acc |= m & above;
+                }
+                if (acc) atomicOr(&d.pm_rows[r], acc);
+            }
         }
         return;
     }
@@ -4934,6 +4974,15 @@ int run_batch(mam_lba_ctx* c, std::vector<Prob>& hp, std::vector<LM>& lm0, const
         const double w = (double)std::max(1ull, h[7]);
         fprintf(stderr, "ldlt cycles per WG: init %.0f B %.0f C1 %.0f C2 %.0f solve %.0f diag(w0) %.0f pull %.0f; WGs %llu\n",
                 h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[6] / w, h[7]);
+    }
+#endif
+#ifdef MAM_SORT_PROFILE
+    {
+        MAM_HIP(hipStreamSynchronize(s));
+        unsigned long long h[4];
+        MAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(mam::lba::g_sortprof), sizeof(h)));
+        fprintf(stderr, "struct_sort cycles per workgroup: points %.0f (%llu) poses %.0f (%llu)\n",
+                h[0] / (double)std::max(1ull, h[2]), h[2], h[1] / (double)std::max(1ull, h[3]), h[3]);
     }
 #endif
 #ifdef MAM_MW_PROFILE
